@@ -1,0 +1,51 @@
+"""Build libdwhmc.so (gfx950) in-tree with hipcc.
+
+The shared library is the drop-in boundary (include/dwhmc.h); it links only the
+HIP runtime, no torch.  Called by __graft_entry__.build() and lazily by the
+ctypes binding when the .so is missing or older than its sources.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIB = os.path.join(PKG, "libdwhmc.so")
+SOURCES = [os.path.join(CSRC, "dwhmc_kernels.hip"), os.path.join(CSRC, "dwhmc_api.cpp")]
+DEPS = SOURCES + [os.path.join(CSRC, "dwhmc_internal.h"), os.path.join(CSRC, "pole_table.inc"),
+                  os.path.join(ROOT, "include", "dwhmc.h")]
+ARCH = os.environ.get("DWHMC_OFFLOAD_ARCH", "gfx950")
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc"):
+        if cand and os.path.exists(cand):
+            return cand
+    return "hipcc"
+
+
+def needs_build() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    return any(os.path.getmtime(p) > t for p in DEPS if os.path.exists(p))
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not needs_build():
+        return LIB
+    tmp = LIB + ".tmp"
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-Wall", "-Wno-unused-result", f"-I{os.path.join(ROOT, 'include')}", *SOURCES, "-o", tmp]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,179 @@
+"""FermionContext: a typed handle on one dwh_ctx (batched over chains).
+
+Array conventions on the Python side follow the reference's Julia indexing:
+per chain a bond field is (N, 2) with column 0 = +x, 1 = +y
+(src/Types.jl:106-111); batched fields are (nchains, N, 2).  They are
+converted to the ABI's column-major layout here and nowhere else.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, ptr
+
+
+def _to_abi(a: np.ndarray, nc: int, N: int) -> np.ndarray:
+    a = np.asarray(a, dtype=np.complex128)
+    if a.shape == (N, 2):
+        a = a[None]
+    if a.shape != (nc, N, 2):
+        raise ValueError(f"expected bond field of shape ({nc}, {N}, 2) or ({N}, 2), got {a.shape}")
+    return np.ascontiguousarray(np.transpose(a, (0, 2, 1)))
+
+
+def _from_abi(a: np.ndarray, nc: int, N: int) -> np.ndarray:
+    return np.ascontiguousarray(np.transpose(a.reshape(nc, 2, N), (0, 2, 1)))
+
+
+def table_to_abi(table: np.ndarray) -> np.ndarray:
+    """(N, 4) 1-based Int table -> Julia column-major N x 4 Int64 buffer."""
+    t = np.asarray(table)
+    if t.ndim != 2 or t.shape[1] != 4:
+        raise ValueError("neighbour table must be (N, 4)")
+    return np.ascontiguousarray(t.T, dtype=np.int64)
+
+
+class FermionContext:
+    """Device-resident fermionic action/force evaluator for nchains chains."""
+
+    def __init__(self, Lx, Ly, t, tp, mu, beta, J, nn_table, nnn_table, disorder,
+                 delta_cap: float = 2.0, device: int = 0):
+        self._lib = _lib.load()
+        dis = np.ascontiguousarray(np.atleast_2d(np.asarray(disorder, dtype=np.float64)))
+        self.N = int(Lx) * int(Ly)
+        if dis.shape[1] != self.N:
+            raise ValueError(f"disorder must have N={self.N} entries per chain")
+        self.nchains = dis.shape[0]
+        self.beta, self.J = float(beta), float(J)
+        h = C.c_void_p()
+        nn = table_to_abi(nn_table)
+        nnn = table_to_abi(nnn_table)
+        rc = self._lib.dwh_create_batched(C.byref(h), int(Lx), int(Ly), float(t), float(tp),
+                                          float(mu), float(beta), float(J), ptr(nn), ptr(nnn),
+                                          self.nchains, ptr(dis), float(delta_cap), int(device))
+        check(rc, None)
+        self._h = h
+        self.info = self._info()
+
+    # -- lifecycle -------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.dwh_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _c(self, rc):
+        check(rc, self._h)
+
+    def _info(self):
+        inf = _lib.dwh_info_t()
+        self._c(self._lib.dwh_info(self._h, C.byref(inf)))
+        return {k: getattr(inf, k) for k, _ in inf._fields_}
+
+    # -- hot path --------------------------------------------------------
+    def set_pairing(self, Delta):
+        a = _to_abi(Delta, self.nchains, self.N)
+        self._c(self._lib.dwh_update_pairing(self._h, ptr(a)))
+
+    def factorize(self):
+        self._c(self._lib.dwh_factorize(self._h))
+
+    def forces(self, Delta=None) -> np.ndarray:
+        d = None if Delta is None else _to_abi(Delta, self.nchains, self.N)
+        out = np.empty((self.nchains, 2, self.N), dtype=np.complex128)
+        self._c(self._lib.dwh_forces(self._h, ptr(d), ptr(out)))
+        return _from_abi(out, self.nchains, self.N)
+
+    def pairing(self) -> np.ndarray:
+        out = np.empty((self.nchains, 2, self.N), dtype=np.complex128)
+        self._c(self._lib.dwh_pairing(self._h, ptr(out)))
+        return _from_abi(out, self.nchains, self.N)
+
+    def fermion_energy(self) -> np.ndarray:
+        out = np.empty(self.nchains)
+        self._c(self._lib.dwh_fermion_energy(self._h, ptr(out)))
+        return out
+
+    def hole_trace(self) -> np.ndarray:
+        out = np.empty(self.nchains)
+        self._c(self._lib.dwh_hole_trace(self._h, ptr(out)))
+        return out
+
+    def total_energy(self, mass: float) -> np.ndarray:
+        out = np.empty(self.nchains)
+        self._c(self._lib.dwh_total_energy(self._h, float(mass), ptr(out)))
+        return out
+
+    def set_state(self, Delta=None, pi=None):
+        d = None if Delta is None else _to_abi(Delta, self.nchains, self.N)
+        p = None if pi is None else _to_abi(pi, self.nchains, self.N)
+        self._c(self._lib.dwh_set_state(self._h, ptr(d), ptr(p)))
+
+    def get_state(self):
+        d = np.empty((self.nchains, 2, self.N), dtype=np.complex128)
+        p = np.empty_like(d)
+        self._c(self._lib.dwh_get_state(self._h, ptr(d), ptr(p)))
+        return _from_abi(d, self.nchains, self.N), _from_abi(p, self.nchains, self.N)
+
+    def hmc_sweep(self, noise, uniform, Nt: int, dt: float, mass: float):
+        nz = _to_abi(noise, self.nchains, self.N)
+        u = np.ascontiguousarray(np.atleast_1d(np.asarray(uniform, dtype=np.float64)))
+        if u.shape != (self.nchains,):
+            raise ValueError("one uniform per chain")
+        acc = np.zeros(self.nchains, dtype=np.uint8)
+        dH = np.zeros(self.nchains)
+        self._c(self._lib.dwh_hmc_sweep(self._h, ptr(nz), ptr(u), int(Nt), float(dt), float(mass),
+                                        ptr(acc), ptr(dH)))
+        return acc.astype(bool), dH
+
+    # -- throughput path -------------------------------------------------
+    def load_draws(self, noise, uniform):
+        noise = np.asarray(noise, dtype=np.complex128)
+        ns = noise.shape[0]
+        nz = np.ascontiguousarray(np.transpose(noise.reshape(ns, self.nchains, self.N, 2), (0, 1, 3, 2)))
+        u = np.ascontiguousarray(np.asarray(uniform, dtype=np.float64).reshape(ns, self.nchains))
+        self._c(self._lib.dwh_load_draws(self._h, ns, ptr(nz), ptr(u)))
+
+    def run_sweeps(self, first: int, nsweeps: int, Nt: int, dt: float, mass: float):
+        self._c(self._lib.dwh_run_sweeps(self._h, int(first), int(nsweeps), int(Nt), float(dt),
+                                         float(mass)))
+
+    def sweep_results(self, first: int, nsweeps: int):
+        acc = np.zeros((nsweeps, self.nchains), dtype=np.uint8)
+        dH = np.zeros((nsweeps, self.nchains))
+        self._c(self._lib.dwh_sweep_results(self._h, int(first), int(nsweeps), ptr(acc), ptr(dH)))
+        return acc.astype(bool), dH
+
+    def synchronize(self):
+        self._c(self._lib.dwh_synchronize(self._h))
+
+    def stream(self) -> int:
+        s = C.c_void_p()
+        self._c(self._lib.dwh_stream(self._h, C.byref(s)))
+        return s.value or 0
+
+    # -- timing ----------------------------------------------------------
+    def timing_enable(self, on: bool = True):
+        self._c(self._lib.dwh_timing_enable(self._h, 1 if on else 0))
+
+    def timing_reset(self):
+        self._c(self._lib.dwh_timing_reset(self._h))
+
+    def timing_read(self, name: str):
+        ms = C.c_double()
+        n = C.c_int64()
+        w = C.c_double()
+        self._c(self._lib.dwh_timing_read(self._h, name.encode(), C.byref(ms), C.byref(n), C.byref(w)))
+        return ms.value, n.value, w.value
+
+
+def selftest_mfma(device: int = 0) -> int:
+    return int(_lib.load().dwh_selftest_mfma(int(device)))

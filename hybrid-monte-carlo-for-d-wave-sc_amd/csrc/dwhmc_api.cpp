@@ -1,0 +1,781 @@
+// C-ABI context of the MI355X fermionic action/force path (include/dwhmc.h).
+//
+// Host-side responsibilities, each restating a reference function:
+//   * static hopping block h from the neighbour tables with the reference's
+//     upper-triangle overwrite order        (src/Hamiltonian.jl:10-47)
+//   * pairing pattern D[r, c] <- Δ[src]/2 with the reference's overwrite order
+//                                            (src/Hamiltonian.jl:55-86)
+//   * pole selection from the compiled table for κ = β E'/2
+//   * the per-sweep launch sequence of hmc_sweep! (src/HMC.jl:71-144)
+// All arithmetic runs in the HIP kernels (dwhmc_kernels.hip); there is no CPU
+// fallback: a missing device is an error.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/dwhmc.h"
+#include "dwhmc_internal.h"
+#include "pole_table.inc"
+
+using dwh::Dims;
+using dwh::kGJ;
+using dwh::kHSlots;
+using dwh::kSlots;
+
+namespace {
+
+thread_local std::string g_create_error;
+
+enum TimerName { T_GJ_UPDATE = 0, T_GJ_PANEL, T_GJ_DIAG, T_ASSEMBLE, T_CONTRACT, T_STEP, T_COUNT };
+const char* kTimerNames[T_COUNT] = {"gj_update", "gj_panel", "gj_diag", "assemble", "contract", "step"};
+
+struct TimingRec {
+  int name;
+  hipEvent_t a, b;
+  double work;
+};
+
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+};
+
+}  // namespace
+
+struct dwh_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  Dims d{};
+  int64_t Lx = 0, Ly = 0;
+  double t = 0, tp = 0, mu = 0, beta = 0, J = 0, delta_cap = 2.0;
+  double kappa = 0, Ebound = 0, Cx = 0, err_tanh = 0, hmax = 0;
+  std::vector<double> y, cq;
+  int64_t device_bytes = 0;
+  bool factorized = false;
+  std::string err;
+
+  // device buffers
+  double2 *R = nullptr, *T = nullptr, *S = nullptr, *Cpanel = nullptr, *Pinv = nullptr;
+  double2 *G12nn = nullptr, *diagS = nullptr;
+  double *ldpart = nullptr, *ldstatic = nullptr, *d_y = nullptr, *d_c = nullptr;
+  int *Dcol = nullptr, *Dsrc = nullptr, *hcol = nullptr, *bond_ij = nullptr, *bond_ji = nullptr;
+  double* hval = nullptr;
+  double2 *Delta = nullptr, *Pi = nullptr, *Pair = nullptr, *F = nullptr, *DeltaB = nullptr,
+          *PairB = nullptr;
+  double *Ef = nullptr, *EfB = nullptr, *Trhh = nullptr, *TrhhB = nullptr, *Hold = nullptr,
+         *Hnew = nullptr;
+  int* flag = nullptr;
+  // draws / results: single-sweep scratch (s_*) and the throughput path
+  double2* s_noise = nullptr;
+  double* s_uniform = nullptr;
+  uint8_t* s_acc = nullptr;
+  double* s_dH = nullptr;
+  int64_t ndraws = 0;
+  double2* noise = nullptr;
+  double* uniform = nullptr;
+  uint8_t* acc = nullptr;
+  double* dH = nullptr;
+  std::vector<void*> allocations;
+
+  // timing
+  bool timing = false;
+  std::vector<TimingRec> recs;
+  std::vector<hipEvent_t> pool;
+  double t_ms[T_COUNT] = {0};
+  int64_t t_n[T_COUNT] = {0};
+  double t_work[T_COUNT] = {0};
+};
+
+namespace {
+
+int fail(dwh_ctx* ctx, int code, const std::string& msg) {
+  if (ctx) ctx->err = msg;
+  else g_create_error = msg;
+  return code;
+}
+
+#define HIPCHECK(ctx, x)                                                                  \
+  do {                                                                                    \
+    hipError_t e_ = (x);                                                                  \
+    if (e_ != hipSuccess)                                                                 \
+      return fail((ctx), DWH_ERR_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+template <typename T>
+int dalloc(dwh_ctx* ctx, T** p, size_t n) {
+  void* q = nullptr;
+  const size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
+  hipError_t e = hipMalloc(&q, bytes);
+  if (e != hipSuccess)
+    return fail(ctx, DWH_ERR_HIP, "hipMalloc(" + std::to_string(bytes) + " B): " + hipGetErrorString(e));
+  ctx->allocations.push_back(q);
+  ctx->device_bytes += (int64_t)bytes;
+  *p = static_cast<T*>(q);
+  return DWH_OK;
+}
+
+hipEvent_t take_event(dwh_ctx* ctx) {
+  if (!ctx->pool.empty()) {
+    hipEvent_t e = ctx->pool.back();
+    ctx->pool.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+struct Scope {
+  dwh_ctx* ctx;
+  int name;
+  double work;
+  hipEvent_t a{};
+  Scope(dwh_ctx* c, int n, double w) : ctx(c), name(n), work(w) {
+    if (ctx->timing) {
+      a = take_event(ctx);
+      (void)hipEventRecord(a, ctx->stream);
+    }
+  }
+  ~Scope() {
+    if (ctx->timing) {
+      hipEvent_t b = take_event(ctx);
+      (void)hipEventRecord(b, ctx->stream);
+      ctx->recs.push_back({name, a, b, work});
+    }
+  }
+};
+
+void drain_timing(dwh_ctx* ctx) {
+  if (ctx->recs.empty()) return;
+  (void)hipStreamSynchronize(ctx->stream);
+  for (auto& r : ctx->recs) {
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, r.a, r.b);
+    ctx->t_ms[r.name] += ms;
+    ctx->t_n[r.name] += 1;
+    ctx->t_work[r.name] += r.work;
+    ctx->pool.push_back(r.a);
+    ctx->pool.push_back(r.b);
+  }
+  ctx->recs.clear();
+}
+
+double tile_flops() { return 8.0 * kGJ * kGJ * kGJ; }
+
+// Blocked no-pivot Gauss-Jordan inversion of all nbatch matrices in M.
+void run_gj(dwh_ctx* ctx, double2* M) {
+  const Dims& d = ctx->d;
+  for (int k = 0; k < d.nb; ++k) {
+    {
+      Scope s(ctx, T_GJ_DIAG, d.nbatch * tile_flops());
+      dwh::launch_gj_diag(d, M, k, ctx->Pinv, ctx->ldpart, ctx->stream);
+    }
+    {
+      Scope s(ctx, T_GJ_PANEL, (double)d.nbatch * (d.nb - 1) * tile_flops());
+      dwh::launch_gj_panel(d, M, k, ctx->Pinv, ctx->Cpanel, ctx->stream);
+    }
+    if (d.nb > 1) {
+      Scope s(ctx, T_GJ_UPDATE, (double)d.nbatch * (d.nb - 1) * d.nb * tile_flops());
+      dwh::launch_gj_update(d, M, k, ctx->Cpanel, ctx->stream);
+    }
+  }
+}
+
+// assemble -> GJ -> contract -> P (and optional kick) -> E_f
+void factorize_enqueue(dwh_ctx* ctx, double kick) {
+  const Dims& d = ctx->d;
+  Scope step(ctx, T_STEP, (double)d.nbatch * 8.0 * (double)d.N * d.N * d.N);
+  {
+    Scope s(ctx, T_ASSEMBLE, (double)d.nbatch * 48.0 * d.N * (double)d.N);
+    dwh::launch_assemble(d, ctx->R, ctx->T, ctx->S, ctx->Dcol, ctx->Dsrc, ctx->Delta, ctx->hcol,
+                         ctx->hval, ctx->d_y, ctx->stream);
+  }
+  run_gj(ctx, ctx->S);
+  {
+    Scope s(ctx, T_CONTRACT, (double)d.nbatch * 32.0 * d.N * (double)d.N);
+    dwh::launch_contract(d, ctx->T, ctx->S, ctx->Dcol, ctx->G12nn, ctx->diagS, ctx->stream);
+  }
+  dwh::launch_pair_force(d, ctx->G12nn, ctx->bond_ij, ctx->bond_ji, ctx->d_c, ctx->Delta,
+                         ctx->Pair, ctx->F, ctx->Pi, kick, ctx->beta, ctx->J, ctx->stream);
+}
+
+void fermion_energy_enqueue(dwh_ctx* ctx) {
+  dwh::launch_fermion_energy(ctx->d, ctx->ldstatic, ctx->ldpart, ctx->diagS, ctx->d_c, ctx->Cx,
+                             ctx->beta, ctx->Ef, ctx->Trhh, ctx->stream);
+}
+
+// One hmc_sweep! body reading draws from device pointers (src/HMC.jl:71-144).
+void sweep_enqueue(dwh_ctx* ctx, const double2* noise, const double* uniform, uint8_t* acc,
+                   double* dH, int64_t Nt, double dt, double mass) {
+  const Dims& d = ctx->d;
+  hipStream_t s = ctx->stream;
+  dwh::launch_refresh(d, noise, ctx->Pi, std::sqrt(2.0 * mass), s);                  // :77
+  dwh::launch_total_energy(d, ctx->Delta, ctx->Pi, ctx->Ef, ctx->beta, ctx->J, mass,  // :80
+                           ctx->Hold, s);
+  dwh::launch_backup(d, ctx->Delta, ctx->Pair, ctx->Ef, ctx->Trhh, ctx->DeltaB, ctx->PairB,  // :84-86
+                     ctx->EfB, ctx->TrhhB, s);
+  dwh::launch_force_from_pair(d, ctx->Pair, ctx->Delta, ctx->F, ctx->Pi, 0.5 * dt, ctx->beta,  // :91-92
+                              ctx->J, s);
+  const double coef_field = dt / (2.0 * mass);                                        // :95
+  for (int64_t step = 1; step <= Nt; ++step) {                                        // :98
+    dwh::launch_drift(d, ctx->Delta, ctx->Pi, coef_field, ctx->delta_cap, ctx->flag, s);  // :101
+    // :105-107 update_H_BdG! + diagonalize + compute_forces!, then the kick of
+    // :111-113 (dt) fused with the final half kick of :118 on the last step
+    factorize_enqueue(ctx, step < Nt ? dt : 0.5 * dt);
+  }
+  if (Nt <= 0)
+    dwh::launch_force_from_pair(d, ctx->Pair, ctx->Delta, ctx->F, ctx->Pi, 0.5 * dt, ctx->beta,
+                                ctx->J, s);
+  else
+    fermion_energy_enqueue(ctx);
+  dwh::launch_total_energy(d, ctx->Delta, ctx->Pi, ctx->Ef, ctx->beta, ctx->J, mass,  // :122
+                           ctx->Hnew, s);
+  dwh::launch_metropolis(d, ctx->Hold, ctx->Hnew, uniform, acc, dH, s);               // :124-129
+  dwh::launch_restore(d, acc, ctx->DeltaB, ctx->PairB, ctx->EfB, ctx->TrhhB, ctx->Delta,  // :130-141
+                      ctx->Pair, ctx->Ef, ctx->Trhh, s);
+}
+
+int check_flag(dwh_ctx* ctx) {
+  int f = 0;
+  HIPCHECK(ctx, hipMemcpyAsync(&f, ctx->flag, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+  if (f) {
+    HIPCHECK(ctx, hipMemsetAsync(ctx->flag, 0, sizeof(int), ctx->stream));
+    char buf[256];
+    std::snprintf(buf, sizeof buf,
+                  "|Delta_ij| exceeded delta_cap=%g: the pole set was built for spectra within "
+                  "E'=%g; recreate the context with a larger delta_cap",
+                  ctx->delta_cap, ctx->Ebound);
+    return fail(ctx, DWH_ERR_SPECTRUM, buf);
+  }
+  return DWH_OK;
+}
+
+int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, double mu, double beta,
+                double J, const int64_t* nn, const int64_t* nnn, int64_t nchains,
+                const double* disorder, double delta_cap, int32_t device) {
+  if (!out) return fail(nullptr, DWH_ERR_ARG, "ctx pointer is NULL");
+  *out = nullptr;
+  if (Lx < 1 || Ly < 1) return fail(nullptr, DWH_ERR_ARG, "Lx, Ly must be >= 1");
+  if (!(beta > 0)) return fail(nullptr, DWH_ERR_ARG, "beta must be > 0");
+  if (J == 0 || !std::isfinite(J)) return fail(nullptr, DWH_ERR_ARG, "J must be finite and nonzero");
+  if (nchains < 1) return fail(nullptr, DWH_ERR_ARG, "nchains must be >= 1");
+  if (!nn || !nnn || !disorder) return fail(nullptr, DWH_ERR_ARG, "NULL table or disorder");
+  const int64_t N64 = Lx * Ly;
+  if (N64 > 9216) return fail(nullptr, DWH_ERR_ARG, "N = Lx*Ly > 9216 not supported (LDS row staging)");
+  const int N = (int)N64;
+  if (delta_cap <= 0) delta_cap = 2.0;
+  for (int64_t e = 0; e < 4 * N64; ++e)
+    if (nn[e] < 1 || nn[e] > N64 || nnn[e] < 1 || nnn[e] > N64)
+      return fail(nullptr, DWH_ERR_ARG, "neighbour table entry out of [1, N]");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1)
+    return fail(nullptr, DWH_ERR_HIP, "no HIP device available (the fermion path has no CPU fallback)");
+  if (device < 0 || device >= ndev) return fail(nullptr, DWH_ERR_ARG, "device index out of range");
+
+  auto NN = [&](int i, int dir) { return (int)(nn[(int64_t)dir * N + i] - 1); };
+  auto NNN = [&](int i, int dir) { return (int)(nnn[(int64_t)dir * N + i] - 1); };
+
+  // --- static h: reference upper-triangle loop with overwrite (Hamiltonian.jl:26-44)
+  std::map<std::pair<int, int>, double> up;
+  for (int i = 0; i < N; ++i) {
+    for (int dir = 0; dir < 4; ++dir) {
+      const int j = NN(i, dir);
+      if (j > i) up[{i, j}] = -t;
+    }
+    for (int dir = 0; dir < 4; ++dir) {
+      const int j = NNN(i, dir);
+      if (j > i) up[{i, j}] = -tp;
+    }
+  }
+  std::vector<std::vector<std::pair<int, double>>> hrow(N);
+  for (auto& kv : up) {
+    hrow[kv.first.first].push_back({kv.first.second, kv.second});
+    hrow[kv.first.second].push_back({kv.first.first, kv.second});
+  }
+  std::vector<int> hcol((size_t)N * kHSlots, -1);
+  std::vector<double> hval((size_t)nchains * N * kHSlots, 0.0);
+  double hmax = 0;
+  for (int i = 0; i < N; ++i) {
+    if ((int)hrow[i].size() + 1 > kHSlots)
+      return fail(nullptr, DWH_ERR_ARG, "more than 8 hopping partners per site");
+    hcol[(size_t)i * kHSlots] = i;
+    double off = 0;
+    for (size_t s = 0; s < hrow[i].size(); ++s) {
+      hcol[(size_t)i * kHSlots + 1 + s] = hrow[i][s].first;
+      off += std::fabs(hrow[i][s].second);
+    }
+    for (int64_t c = 0; c < nchains; ++c) {
+      const double w = disorder[c * N64 + i];
+      if (!std::isfinite(w)) return fail(nullptr, DWH_ERR_ARG, "non-finite disorder");
+      hval[((size_t)c * N + i) * kHSlots] = w - mu;  // Hamiltonian.jl:18-22
+      for (size_t s = 0; s < hrow[i].size(); ++s)
+        hval[((size_t)c * N + i) * kHSlots + 1 + s] = hrow[i][s].second;
+      hmax = std::max(hmax, std::fabs(w - mu) + off);
+    }
+  }
+  // --- pairing pattern with the reference overwrite order (Hamiltonian.jl:68-83)
+  std::map<std::pair<int, int>, int> dmap;
+  for (int i = 0; i < N; ++i)
+    for (int dir = 0; dir < 2; ++dir) {
+      const int j = NN(i, dir);
+      const int src = i + N * dir;
+      dmap[{i, j}] = src;
+      dmap[{j, i}] = src;
+    }
+  std::vector<int> Dcol((size_t)N * kSlots, -1), Dsrc((size_t)N * kSlots, -1);
+  std::vector<int> dcount(N, 0);
+  for (auto& kv : dmap) {
+    const int r = kv.first.first;
+    if (dcount[r] >= kSlots) return fail(nullptr, DWH_ERR_ARG, "more than 4 pairing partners per site");
+    Dcol[(size_t)r * kSlots + dcount[r]] = kv.first.second;
+    Dsrc[(size_t)r * kSlots + dcount[r]] = kv.second;
+    dcount[r]++;
+  }
+  for (auto& kv : dmap) {
+    auto it = dmap.find({kv.first.second, kv.first.first});
+    if (it == dmap.end() || it->second != kv.second)
+      return fail(nullptr, DWH_ERR_ARG, "pairing block not symmetric (unsupported table)");
+  }
+  auto slot_of = [&](int r, int c) {
+    for (int s = 0; s < kSlots; ++s)
+      if (Dcol[(size_t)r * kSlots + s] == c) return s;
+    return -1;
+  };
+  std::vector<int> bij(2 * (size_t)N), bji(2 * (size_t)N);
+  for (int dir = 0; dir < 2; ++dir)
+    for (int i = 0; i < N; ++i) {
+      const int j = NN(i, dir);
+      bij[(size_t)dir * N + i] = i * kSlots + slot_of(i, j);
+      bji[(size_t)dir * N + i] = j * kSlots + slot_of(j, i);
+    }
+
+  // --- pole selection: E' >= Gershgorin bound of H_BdG with |Δ| <= delta_cap
+  const double Eb = hmax + 2.0 * delta_cap;
+  const double kneed = 0.5 * beta * Eb;
+  int sel = -1;
+  for (int e = 0; e < kPoleTableSize; ++e)
+    if (kPoleEntries[e].kappa >= kneed * (1.0 - 1e-12)) {
+      sel = e;
+      break;
+    }
+  if (sel < 0) {
+    char buf[256];
+    std::snprintf(buf, sizeof buf, "beta*E_bound/2 = %g exceeds the pole table (max kappa %g)", kneed,
+                  kPoleEntries[kPoleTableSize - 1].kappa);
+    return fail(nullptr, DWH_ERR_TABLE, buf);
+  }
+  const PoleEntry& pe = kPoleEntries[sel];
+  const double kappa = pe.kappa;
+  const double Ep = 2.0 * kappa / beta;
+  std::vector<double> y(pe.m), cq(pe.m);
+  double suma = 0;
+  for (int q = 0; q < pe.m; ++q) {
+    y[q] = Ep * std::sqrt(kPoleT[pe.off + q]);
+    cq[q] = 0.5 * kPoleA[pe.off + q] * Ep;
+    suma += kPoleA[pe.off + q];
+  }
+
+  dwh_ctx* ctx = new dwh_ctx();
+  ctx->device = device;
+  ctx->Lx = Lx;
+  ctx->Ly = Ly;
+  ctx->t = t;
+  ctx->tp = tp;
+  ctx->mu = mu;
+  ctx->beta = beta;
+  ctx->J = J;
+  ctx->delta_cap = delta_cap;
+  ctx->kappa = kappa;
+  ctx->Ebound = Ep;
+  ctx->hmax = hmax;
+  ctx->err_tanh = pe.err_tanh;
+  ctx->Cx = pe.C_u - kappa * std::log(Ep) * suma;
+  ctx->y = y;
+  ctx->cq = cq;
+  Dims& d = ctx->d;
+  d.N = N;
+  d.Np = ((N + kGJ - 1) / kGJ) * kGJ;
+  d.nb = d.Np / kGJ;
+  d.nc = (int)nchains;
+  d.P = pe.m;
+  d.nbatch = d.nc * d.P;
+  d.mat = (int64_t)d.Np * d.Np;
+
+  auto bail = [&](int code) {
+    g_create_error = ctx->err;
+    dwh_destroy(ctx);
+    return code;
+  };
+  if (hipSetDevice(device) != hipSuccess) {
+    ctx->err = "hipSetDevice failed";
+    return bail(DWH_ERR_HIP);
+  }
+  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+    ctx->err = "hipStreamCreate failed";
+    return bail(DWH_ERR_HIP);
+  }
+  const size_t nmat = (size_t)d.nbatch * d.mat;
+  const size_t nbond = (size_t)d.nc * 2 * N;
+  int rc = DWH_OK;
+#define ALLOC(p, n) \
+  if ((rc = dalloc(ctx, &ctx->p, (n))) != DWH_OK) return bail(rc)
+  ALLOC(R, nmat);
+  ALLOC(T, nmat);
+  ALLOC(S, nmat);
+  ALLOC(Cpanel, (size_t)d.nbatch * d.Np * kGJ);
+  ALLOC(Pinv, (size_t)d.nbatch * kGJ * kGJ);
+  ALLOC(G12nn, (size_t)d.nbatch * N * kSlots);
+  ALLOC(diagS, (size_t)d.nbatch * N);
+  ALLOC(ldpart, (size_t)d.nbatch * d.nb);
+  ALLOC(ldstatic, (size_t)d.nbatch);
+  ALLOC(d_y, (size_t)d.P);
+  ALLOC(d_c, (size_t)d.P);
+  ALLOC(Dcol, Dcol.size());
+  ALLOC(Dsrc, Dsrc.size());
+  ALLOC(hcol, hcol.size());
+  ALLOC(hval, hval.size());
+  ALLOC(bond_ij, bij.size());
+  ALLOC(bond_ji, bji.size());
+  ALLOC(Delta, nbond);
+  ALLOC(Pi, nbond);
+  ALLOC(Pair, nbond);
+  ALLOC(F, nbond);
+  ALLOC(DeltaB, nbond);
+  ALLOC(PairB, nbond);
+  ALLOC(Ef, (size_t)d.nc);
+  ALLOC(EfB, (size_t)d.nc);
+  ALLOC(Trhh, (size_t)d.nc);
+  ALLOC(TrhhB, (size_t)d.nc);
+  ALLOC(Hold, (size_t)d.nc);
+  ALLOC(Hnew, (size_t)d.nc);
+  ALLOC(flag, 1);
+  ALLOC(s_noise, nbond);
+  ALLOC(s_uniform, (size_t)d.nc);
+  ALLOC(s_acc, (size_t)d.nc);
+  ALLOC(s_dH, (size_t)d.nc);
+#undef ALLOC
+  ctx->ndraws = 0;
+  hipStream_t s = ctx->stream;
+#define UP(dst, src, n)                                                                     \
+  if (hipMemcpyAsync(ctx->dst, (src), (n) * sizeof(*ctx->dst), hipMemcpyHostToDevice, s) != \
+      hipSuccess) {                                                                         \
+    ctx->err = "upload " #dst;                                                              \
+    return bail(DWH_ERR_HIP);                                                               \
+  }
+  UP(d_y, y.data(), y.size());
+  UP(d_c, cq.data(), cq.size());
+  UP(Dcol, Dcol.data(), Dcol.size());
+  UP(Dsrc, Dsrc.data(), Dsrc.size());
+  UP(hcol, hcol.data(), hcol.size());
+  UP(hval, hval.data(), hval.size());
+  UP(bond_ij, bij.data(), bij.size());
+  UP(bond_ji, bji.data(), bji.size());
+#undef UP
+  // zeroed cache, like initialize_cache (src/Types.jl:182-212): P = 0, E_f = 0
+  (void)hipMemsetAsync(ctx->Delta, 0, nbond * sizeof(double2), s);
+  (void)hipMemsetAsync(ctx->Pi, 0, nbond * sizeof(double2), s);
+  (void)hipMemsetAsync(ctx->Pair, 0, nbond * sizeof(double2), s);
+  (void)hipMemsetAsync(ctx->F, 0, nbond * sizeof(double2), s);
+  (void)hipMemsetAsync(ctx->Ef, 0, d.nc * sizeof(double), s);
+  (void)hipMemsetAsync(ctx->Trhh, 0, d.nc * sizeof(double), s);
+  (void)hipMemsetAsync(ctx->flag, 0, sizeof(int), s);
+  (void)hipMemsetAsync(ctx->diagS, 0, (size_t)d.nbatch * N * sizeof(double2), s);
+  // static R = (h - i y)^-1 and ln|det(h - i y)| for every (chain, pole)
+  dwh::launch_fill_hz(d, ctx->R, ctx->hcol, ctx->hval, ctx->d_y, s);
+  run_gj(ctx, ctx->R);
+  dwh::launch_sum_ld(d, ctx->ldpart, ctx->ldstatic, s);
+  if (hipStreamSynchronize(s) != hipSuccess || hipGetLastError() != hipSuccess) {
+    ctx->err = "static R initialisation failed on the device";
+    return bail(DWH_ERR_HIP);
+  }
+  *out = ctx;
+  return DWH_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dwh_create(dwh_ctx** ctx, int64_t Lx, int64_t Ly, double t, double tp, double mu, double beta,
+               double J, const int64_t* nn_table, const int64_t* nnn_table, const double* disorder,
+               int32_t device) {
+  return create_impl(ctx, Lx, Ly, t, tp, mu, beta, J, nn_table, nnn_table, 1, disorder, 2.0, device);
+}
+
+int dwh_create_batched(dwh_ctx** ctx, int64_t Lx, int64_t Ly, double t, double tp, double mu,
+                       double beta, double J, const int64_t* nn_table, const int64_t* nnn_table,
+                       int64_t nchains, const double* disorder, double delta_cap, int32_t device) {
+  return create_impl(ctx, Lx, Ly, t, tp, mu, beta, J, nn_table, nnn_table, nchains, disorder,
+                     delta_cap, device);
+}
+
+void dwh_destroy(dwh_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  for (auto& r : ctx->recs) {
+    (void)hipEventDestroy(r.a);
+    (void)hipEventDestroy(r.b);
+  }
+  for (auto e : ctx->pool) (void)hipEventDestroy(e);
+  for (void* p : ctx->allocations) (void)hipFree(p);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+const char* dwh_last_error(const dwh_ctx* ctx) {
+  return ctx ? ctx->err.c_str() : g_create_error.c_str();
+}
+
+int dwh_info(dwh_ctx* ctx, dwh_info_t* out) {
+  if (!ctx || !out) return DWH_ERR_ARG;
+  out->N = ctx->d.N;
+  out->Np = ctx->d.Np;
+  out->nchains = ctx->d.nc;
+  out->npoles = ctx->d.P;
+  out->kappa = ctx->kappa;
+  out->e_bound = ctx->Ebound;
+  out->err_tanh = ctx->err_tanh;
+  out->delta_cap = ctx->delta_cap;
+  out->device_bytes = ctx->device_bytes;
+  return DWH_OK;
+}
+
+int dwh_update_pairing(dwh_ctx* ctx, const dwh_c128* Delta) {
+  if (!ctx || !Delta) return fail(ctx, DWH_ERR_ARG, "NULL argument");
+  HIPCHECK(ctx, hipSetDevice(ctx->device));
+  HIPCHECK(ctx, hipMemcpyAsync(ctx->Delta, Delta, (size_t)ctx->d.nc * 2 * ctx->d.N * sizeof(double2),
+                               hipMemcpyHostToDevice, ctx->stream));
+  HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+  return DWH_OK;
+}
+
+int dwh_factorize(dwh_ctx* ctx) {
+  if (!ctx) return DWH_ERR_ARG;
+  HIPCHECK(ctx, hipSetDevice(ctx->device));
+  factorize_enqueue(ctx, 0.0);
+  fermion_energy_enqueue(ctx);
+  HIPCHECK(ctx, hipGetLastError());
+  HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->factorized = true;
+  drain_timing(ctx);
+  return DWH_OK;
+}
+
+int dwh_forces(dwh_ctx* ctx, const dwh_c128* Delta, dwh_c128* F_out) {
+  if (!ctx || !F_out) return fail(ctx, DWH_ERR_ARG, "NULL argument");
+  HIPCHECK(ctx, hipSetDevice(ctx->device));
+  const size_t nb = (size_t)ctx->d.nc * 2 * ctx->d.N * sizeof(double2);
+  if (Delta)
+    HIPCHECK(ctx, hipMemcpyAsync(ctx->DeltaB, Delta, nb, hipMemcpyHostToDevice, ctx->stream));
+  dwh::launch_force_from_pair(ctx->d, ctx->Pair, Delta ? ctx->DeltaB : ctx->Delta, ctx->F, ctx->Pi,
+                              0.0, ctx->beta, ctx->J, ctx->stream);
+  HIPCHECK(ctx, hipMemcpyAsync(F_out, ctx->F, nb, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+  return DWH_OK;
+}
+
+int dwh_pairing(dwh_ctx* ctx, dwh_c128* P_out) {
+  if (!ctx || !P_out) return fail(ctx, DWH_ERR_ARG, "NULL argument");
+  HIPCHECK(ctx, hipSetDevice(ctx->device));
+  HIPCHECK(ctx, hipMemcpyAsync(P_out, ctx->Pair, (size_t)ctx->d.nc * 2 * ctx->d.N * sizeof(double2),
+                               hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+  return DWH_OK;
+}
+
+int dwh_fermion_energy(dwh_ctx* ctx, double* Ef) {
+  if (!ctx || !Ef) return fail(ctx, DWH_ERR_ARG, "NULL argument");
+  HIPCHECK(ctx, hipSetDevice(ctx->device));
+  HIPCHECK(ctx, hipMemcpyAsync(Ef, ctx->Ef, ctx->d.nc * sizeof(double), hipMemcpyDeviceToHost,
+                               ctx->stream));
+  HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+  return DWH_OK;
+}
+
+int dwh_hole_trace(dwh_ctx* ctx, double* tr) {
+  if (!ctx || !tr) return fail(ctx, DWH_ERR_ARG, "NULL argument");
+  HIPCHECK(ctx, hipSetDevice(ctx->device));
+  HIPCHECK(ctx, hipMemcpyAsync(tr, ctx->Trhh, ctx->d.nc * sizeof(double), hipMemcpyDeviceToHost,
+                               ctx->stream));
+  HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+  return DWH_OK;
+}
+
+int dwh_total_energy(dwh_ctx* ctx, double mass, double* H) {
+  if (!ctx || !H) return fail(ctx, DWH_ERR_ARG, "NULL argument");
+  HIPCHECK(ctx, hipSetDevice(ctx->device));
+  dwh::launch_total_energy(ctx->d, ctx->Delta, ctx->Pi, ctx->Ef, ctx->beta, ctx->J, mass, ctx->Hnew,
+                           ctx->stream);
+  HIPCHECK(ctx, hipMemcpyAsync(H, ctx->Hnew, ctx->d.nc * sizeof(double), hipMemcpyDeviceToHost,
+                               ctx->stream));
+  HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+  return DWH_OK;
+}
+
+int dwh_set_state(dwh_ctx* ctx, const dwh_c128* Delta, const dwh_c128* pi) {
+  if (!ctx) return DWH_ERR_ARG;
+  HIPCHECK(ctx, hipSetDevice(ctx->device));
+  const size_t nb = (size_t)ctx->d.nc * 2 * ctx->d.N * sizeof(double2);
+  if (Delta) HIPCHECK(ctx, hipMemcpyAsync(ctx->Delta, Delta, nb, hipMemcpyHostToDevice, ctx->stream));
+  if (pi) HIPCHECK(ctx, hipMemcpyAsync(ctx->Pi, pi, nb, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+  return DWH_OK;
+}
+
+int dwh_get_state(dwh_ctx* ctx, dwh_c128* Delta, dwh_c128* pi) {
+  if (!ctx) return DWH_ERR_ARG;
+  HIPCHECK(ctx, hipSetDevice(ctx->device));
+  const size_t nb = (size_t)ctx->d.nc * 2 * ctx->d.N * sizeof(double2);
+  if (Delta) HIPCHECK(ctx, hipMemcpyAsync(Delta, ctx->Delta, nb, hipMemcpyDeviceToHost, ctx->stream));
+  if (pi) HIPCHECK(ctx, hipMemcpyAsync(pi, ctx->Pi, nb, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+  return DWH_OK;
+}
+
+int dwh_hmc_sweep(dwh_ctx* ctx, const dwh_c128* noise, const double* uniform, int64_t Nt, double dt,
+                  double mass, uint8_t* accepted, double* dH) {
+  if (!ctx || !noise || !uniform || !accepted || !dH) return fail(ctx, DWH_ERR_ARG, "NULL argument");
+  if (Nt < 0 || !(mass > 0) || !std::isfinite(dt)) return fail(ctx, DWH_ERR_ARG, "bad Nt/dt/mass");
+  HIPCHECK(ctx, hipSetDevice(ctx->device));
+  const Dims& d = ctx->d;
+  double2* nz = ctx->s_noise;
+  double* un = ctx->s_uniform;
+  uint8_t* ac = ctx->s_acc;
+  double* dh = ctx->s_dH;
+  HIPCHECK(ctx, hipMemcpyAsync(nz, noise, (size_t)d.nc * 2 * d.N * sizeof(double2),
+                               hipMemcpyHostToDevice, ctx->stream));
+  HIPCHECK(ctx, hipMemcpyAsync(un, uniform, d.nc * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+  sweep_enqueue(ctx, nz, un, ac, dh, Nt, dt, mass);
+  HIPCHECK(ctx, hipGetLastError());
+  HIPCHECK(ctx, hipMemcpyAsync(accepted, ac, d.nc, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHECK(ctx, hipMemcpyAsync(dH, dh, d.nc * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+  if (Nt > 0) ctx->factorized = true;
+  drain_timing(ctx);
+  return check_flag(ctx);
+}
+
+int dwh_load_draws(dwh_ctx* ctx, int64_t nsweeps, const dwh_c128* noise, const double* uniform) {
+  if (!ctx || nsweeps < 1 || !noise || !uniform) return fail(ctx, DWH_ERR_ARG, "bad argument");
+  HIPCHECK(ctx, hipSetDevice(ctx->device));
+  const Dims& d = ctx->d;
+  const size_t nbond = (size_t)d.nc * 2 * d.N;
+  if (nsweeps > ctx->ndraws) {
+    HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+    auto drop = [&](void* p) {
+      if (!p) return;
+      auto it = std::find(ctx->allocations.begin(), ctx->allocations.end(), p);
+      if (it != ctx->allocations.end()) ctx->allocations.erase(it);
+      (void)hipFree(p);
+    };
+    drop(ctx->noise);
+    drop(ctx->uniform);
+    drop(ctx->acc);
+    drop(ctx->dH);
+    int rc;
+    if ((rc = dalloc(ctx, &ctx->noise, nbond * nsweeps)) != DWH_OK) return rc;
+    if ((rc = dalloc(ctx, &ctx->uniform, (size_t)d.nc * nsweeps)) != DWH_OK) return rc;
+    if ((rc = dalloc(ctx, &ctx->acc, (size_t)d.nc * nsweeps)) != DWH_OK) return rc;
+    if ((rc = dalloc(ctx, &ctx->dH, (size_t)d.nc * nsweeps)) != DWH_OK) return rc;
+  }
+  ctx->ndraws = std::max<int64_t>(ctx->ndraws, nsweeps);
+  HIPCHECK(ctx, hipMemcpyAsync(ctx->noise, noise, nbond * nsweeps * sizeof(double2),
+                               hipMemcpyHostToDevice, ctx->stream));
+  HIPCHECK(ctx, hipMemcpyAsync(ctx->uniform, uniform, (size_t)d.nc * nsweeps * sizeof(double),
+                               hipMemcpyHostToDevice, ctx->stream));
+  HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+  return DWH_OK;
+}
+
+int dwh_run_sweeps(dwh_ctx* ctx, int64_t first, int64_t nsweeps, int64_t Nt, double dt, double mass) {
+  if (!ctx) return DWH_ERR_ARG;
+  if (first < 0 || nsweeps < 0 || first + nsweeps > ctx->ndraws)
+    return fail(ctx, DWH_ERR_ARG, "sweep range outside the loaded draws");
+  if (Nt < 0 || !(mass > 0)) return fail(ctx, DWH_ERR_ARG, "bad Nt/mass");
+  HIPCHECK(ctx, hipSetDevice(ctx->device));
+  const Dims& d = ctx->d;
+  const size_t nbond = (size_t)d.nc * 2 * d.N;
+  for (int64_t sw = first; sw < first + nsweeps; ++sw)
+    sweep_enqueue(ctx, ctx->noise + nbond * sw, ctx->uniform + (size_t)d.nc * sw,
+                  ctx->acc + (size_t)d.nc * sw, ctx->dH + (size_t)d.nc * sw, Nt, dt, mass);
+  HIPCHECK(ctx, hipGetLastError());
+  if (Nt > 0 && nsweeps > 0) ctx->factorized = true;
+  return DWH_OK;
+}
+
+int dwh_sweep_results(dwh_ctx* ctx, int64_t first, int64_t nsweeps, uint8_t* accepted, double* dH) {
+  if (!ctx) return DWH_ERR_ARG;
+  if (first < 0 || nsweeps < 0 || first + nsweeps > ctx->ndraws)
+    return fail(ctx, DWH_ERR_ARG, "sweep range outside the loaded draws");
+  HIPCHECK(ctx, hipSetDevice(ctx->device));
+  const size_t nc = ctx->d.nc;
+  if (accepted)
+    HIPCHECK(ctx, hipMemcpyAsync(accepted, ctx->acc + nc * first, nc * nsweeps, hipMemcpyDeviceToHost,
+                                 ctx->stream));
+  if (dH)
+    HIPCHECK(ctx, hipMemcpyAsync(dH, ctx->dH + nc * first, nc * nsweeps * sizeof(double),
+                                 hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+  return check_flag(ctx);
+}
+
+int dwh_synchronize(dwh_ctx* ctx) {
+  if (!ctx) return DWH_ERR_ARG;
+  HIPCHECK(ctx, hipSetDevice(ctx->device));
+  HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+  HIPCHECK(ctx, hipGetLastError());
+  drain_timing(ctx);
+  return DWH_OK;
+}
+
+int dwh_stream(dwh_ctx* ctx, void** stream) {
+  if (!ctx || !stream) return DWH_ERR_ARG;
+  *stream = (void*)ctx->stream;
+  return DWH_OK;
+}
+
+int dwh_timing_enable(dwh_ctx* ctx, int32_t enable) {
+  if (!ctx) return DWH_ERR_ARG;
+  drain_timing(ctx);
+  ctx->timing = enable != 0;
+  return DWH_OK;
+}
+
+int dwh_timing_read(dwh_ctx* ctx, const char* name, double* total_ms, int64_t* launches,
+                    double* work) {
+  if (!ctx || !name) return DWH_ERR_ARG;
+  drain_timing(ctx);
+  for (int i = 0; i < T_COUNT; ++i)
+    if (std::strcmp(name, kTimerNames[i]) == 0) {
+      if (total_ms) *total_ms = ctx->t_ms[i];
+      if (launches) *launches = ctx->t_n[i];
+      if (work) *work = ctx->t_work[i];
+      return DWH_OK;
+    }
+  return fail(ctx, DWH_ERR_ARG, std::string("unknown timer ") + name);
+}
+
+int dwh_timing_reset(dwh_ctx* ctx) {
+  if (!ctx) return DWH_ERR_ARG;
+  drain_timing(ctx);
+  for (int i = 0; i < T_COUNT; ++i) {
+    ctx->t_ms[i] = 0;
+    ctx->t_n[i] = 0;
+    ctx->t_work[i] = 0;
+  }
+  return DWH_OK;
+}
+
+int dwh_selftest_mfma(int32_t device) { return dwh::selftest_mfma_layout(device); }
+
+}  // extern "C"

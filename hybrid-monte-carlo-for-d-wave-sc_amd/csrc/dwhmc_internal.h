@@ -1,0 +1,72 @@
+// Internal launch interface between the C-ABI context (dwhmc_api.cpp) and the
+// gfx950 kernels (dwhmc_kernels.hip).  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dwh {
+
+constexpr int kGJ = 64;        // Gauss-Jordan block (rows/cols of one diagonal block)
+constexpr int kSlots = 4;      // pairing entries per BdG row (NN bonds)
+constexpr int kHSlots = 9;     // hopping entries per row (diag + 4 NN + 4 NNN)
+
+struct Dims {
+  int N;        // sites
+  int Np;       // padded to kGJ
+  int nb;       // Np / kGJ
+  int nc;       // chains
+  int P;        // poles per chain
+  int nbatch;   // nc * P
+  int64_t mat;  // elements per padded matrix (Np*Np)
+};
+
+// dense h - i y_q (padded with identity) for every (chain, pole): R init input
+void launch_fill_hz(const Dims& d, double2* M, const int* hcol, const double* hval,
+                    const double* ypole, hipStream_t s);
+// one Gauss-Jordan block step k on all nbatch matrices in M (in place, no pivoting)
+void launch_gj_diag(const Dims& d, double2* M, int k, double2* Pinv, double* ldpart,
+                    hipStream_t s);
+void launch_gj_panel(const Dims& d, double2* M, int k, const double2* Pinv, double2* Cpanel,
+                     hipStream_t s);
+void launch_gj_update(const Dims& d, double2* M, int k, const double2* Cpanel, hipStream_t s);
+// T = R D and S^T = -(h + i y) - (D† R D)^T for every (chain, pole)
+void launch_assemble(const Dims& d, const double2* R, double2* T, double2* S, const int* Dcol,
+                     const int* Dsrc, const double2* Delta, const int* hcol, const double* hval,
+                     const double* ypole, hipStream_t s);
+// G12 at the pairing pattern: G12nn[bi][i][s] = -(T S^{-1})[i, Dcol[i][s]]; diag of S^{-1}
+void launch_contract(const Dims& d, const double2* T, const double2* SinvT, const int* Dcol,
+                     double2* G12nn, double2* diagS, hipStream_t s);
+// P = Σ_q c_q (G12[i,j] + G12[j,i]); F = -β/2J (Δ - J P); π += kick·F
+void launch_pair_force(const Dims& d, const double2* G12nn, const int* bond_ij,
+                       const int* bond_ji, const double* cpole, const double2* Delta,
+                       double2* Pair, double2* F, double2* Pi, double kick, double beta,
+                       double J, hipStream_t s);
+// F from cached P, π += kick·F
+void launch_force_from_pair(const Dims& d, const double2* Pair, const double2* Delta,
+                            double2* F, double2* Pi, double kick, double beta, double J,
+                            hipStream_t s);
+// Δ += coef·π with the |Δ| guard
+void launch_drift(const Dims& d, double2* Delta, const double2* Pi, double coef, double cap,
+                  int* flag, hipStream_t s);
+// E_f and Tr ρ_hh from the pivots of the last factorisation
+void launch_fermion_energy(const Dims& d, const double* ldstatic, const double* ldpart,
+                           const double2* diagS, const double* cpole, double Cx, double beta,
+                           double* Ef, double* Trhh, hipStream_t s);
+// H = Σ|π|²/2m + β/2J Σ|Δ|² + E_f into Hout[c]
+void launch_total_energy(const Dims& d, const double2* Delta, const double2* Pi,
+                         const double* Ef, double beta, double J, double mass, double* Hout,
+                         hipStream_t s);
+void launch_refresh(const Dims& d, const double2* noise, double2* Pi, double scale, hipStream_t s);
+void launch_backup(const Dims& d, const double2* Delta, const double2* Pair, const double* Ef,
+                   const double* Trhh, double2* DeltaB, double2* PairB, double* EfB,
+                   double* TrhhB, hipStream_t s);
+void launch_metropolis(const Dims& d, const double* Hold, const double* Hnew,
+                       const double* uniform, uint8_t* accepted, double* dH, hipStream_t s);
+void launch_restore(const Dims& d, const uint8_t* accepted, const double2* DeltaB,
+                    const double2* PairB, const double* EfB, const double* TrhhB,
+                    double2* Delta, double2* Pair, double* Ef, double* Trhh, hipStream_t s);
+void launch_sum_ld(const Dims& d, const double* ldpart, double* ldsum, hipStream_t s);
+
+int selftest_mfma_layout(int device);
+
+}  // namespace dwh

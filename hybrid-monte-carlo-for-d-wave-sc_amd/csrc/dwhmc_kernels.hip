@@ -1,0 +1,722 @@
+// gfx950 (MI355X, CDNA4) kernels of the DwaveHMC.jl fermionic action/force path.
+//
+// Per leapfrog step (src/HMC.jl:98-114) and per imaginary-axis pole z = i y_q:
+//   S(z)    = -(h + z) - D† R(z) D          Schur complement of H_BdG - z over
+//                                            its static particle block, R = (h - z)^-1
+//   S^-1    : in-place blocked Gauss-Jordan, no pivoting (i·S has Hermitian part
+//             y·I > 0, so every pivot is bounded away from 0), trailing updates on
+//             v_mfma_f64_16x16x4_f64 tiles staged through LDS
+//   G12     = -R D S^-1   only at the 4N nearest-neighbour entries
+//   P_ij    = Σ_q c_q (G12[i,j] + G12[j,i])   (= -ρ_{i,j+N} - ρ_{j,i+N})
+//   F_ij    = -β/2J (Δ_ij - J P_ij)          (src/Observables.jl:14-62)
+//   E_f     = -2N C - β Σ_q c_q ln|det(H - i y_q)|  from the GJ pivots
+// See DESIGN.md §2-§3 for the derivation and the roofline of each kernel.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dwhmc_internal.h"
+
+namespace dwh {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ double2 cmul(double2 a, double2 b) {
+  return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+// a * conj(b)
+__device__ __forceinline__ double2 cmulc(double2 a, double2 b) {
+  return make_double2(a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y);
+}
+__device__ __forceinline__ double2 cadd(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ double2 csub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ double2 cinv(double2 a) {
+  const double s = 1.0 / (a.x * a.x + a.y * a.y);
+  return make_double2(a.x * s, -a.y * s);
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// dense M = h_c - i y_q, padded with identity (input of the R = (h - i y)^-1 GJ)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_fill_hz(double2* __restrict__ M, int64_t mat, int N,
+                                                 int Np, int P, const int* __restrict__ hcol,
+                                                 const double* __restrict__ hval,
+                                                 const double* __restrict__ ypole) {
+  const int a = blockIdx.x, bi = blockIdx.y;
+  const int c = bi / P, q = bi % P;
+  double2* row = M + (int64_t)bi * mat + (int64_t)a * Np;
+  __shared__ int hc[kHSlots];
+  __shared__ double hv[kHSlots];
+  if (threadIdx.x < kHSlots) {
+    hc[threadIdx.x] = (a < N) ? hcol[a * kHSlots + threadIdx.x] : -1;
+    hv[threadIdx.x] = (a < N) ? hval[((int64_t)c * N + a) * kHSlots + threadIdx.x] : 0.0;
+  }
+  __syncthreads();
+  const double y = ypole[q];
+  for (int b = threadIdx.x; b < Np; b += blockDim.x) {
+    double2 v = make_double2(0.0, 0.0);
+    if (a < N) {
+#pragma unroll
+      for (int s = 0; s < kHSlots; ++s)
+        if (hc[s] == b) v.x = hv[s];
+      if (b == a) v.y = -y;
+    } else if (b == a) {
+      v.x = 1.0;
+    }
+    row[b] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Gauss-Jordan, diagonal block: 64x64 complex in registers (16 per thread),
+// row/column p exchanged through double-buffered LDS — one barrier per pivot.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_gj_diag(double2* __restrict__ M, int64_t mat, int Np,
+                                                 int k, int nb, double2* __restrict__ Pinv,
+                                                 double* __restrict__ ldpart) {
+  const int bi = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int i = tid >> 2;       // row of this thread
+  const int seg = tid & 3;      // 16-column segment
+  const double2* A = M + (int64_t)bi * mat + (int64_t)(k * kGJ) * Np + k * kGJ;
+  double2 a[16];
+#pragma unroll
+  for (int jj = 0; jj < 16; ++jj) a[jj] = A[(int64_t)i * Np + seg * 16 + jj];
+  __shared__ double2 rowbuf[2][kGJ];
+  __shared__ double2 colbuf[2][kGJ];
+  double ld = 0.0;
+#pragma unroll 1
+  for (int pb = 0; pb < 4; ++pb) {
+#pragma unroll
+    for (int pp = 0; pp < 16; ++pp) {
+      const int p = pb * 16 + pp;
+      const int par = pp & 1;
+      if (i == p) {
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) rowbuf[par][seg * 16 + jj] = a[jj];
+      }
+      if (seg == pb) colbuf[par][i] = a[pp];
+      __syncthreads();
+      const double2 piv = rowbuf[par][p];
+      const double2 inv = cinv(piv);
+      if (tid == 0) ld += 0.5 * log(piv.x * piv.x + piv.y * piv.y);
+      if (i == p) {
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) {
+          if (seg == pb && jj == pp) a[jj] = inv;
+          else a[jj] = cmul(rowbuf[par][seg * 16 + jj], inv);
+        }
+      } else {
+        const double2 fi = cmul(colbuf[par][i], inv);
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) {
+          if (seg == pb && jj == pp) a[jj] = make_double2(-fi.x, -fi.y);
+          else a[jj] = csub(a[jj], cmul(fi, rowbuf[par][seg * 16 + jj]));
+        }
+      }
+    }
+  }
+  double2* Pout = Pinv + (int64_t)bi * kGJ * kGJ;
+#pragma unroll
+  for (int jj = 0; jj < 16; ++jj) Pout[i * kGJ + seg * 16 + jj] = a[jj];
+  if (tid == 0) ldpart[(int64_t)bi * nb + k] = ld;
+}
+
+// ---------------------------------------------------------------------------
+// 64x64x64 complex tile GEMM on f64 MFMA.
+//   C = A·B            (NEG = false, LOADC = false)
+//   C = C0 - A·B       (NEG = true,  LOADC = true; C0 = 0 when zeroC)
+// A: 64 rows x 64 k (lda), B: 64 k x 64 cols (ldb).  4 waves, each a 32x32
+// complex output = 2x2 blocks of 16x16; every complex MAC is 4 real MFMAs
+// (no 3M trick, rounding stays the plain complex product's).
+// v_mfma_f64_16x16x4_f64 layouts (gfx950): A lane l -> A[l&15][l>>4],
+// B lane l -> B[l>>4][l&15], C/D reg r -> C[(l>>4) + 4r][l&15].
+// ---------------------------------------------------------------------------
+template <bool NEG, bool LOADC>
+__device__ __forceinline__ void tile_cgemm(const double2* __restrict__ A, int lda,
+                                           const double2* __restrict__ B, int ldb,
+                                           double2* __restrict__ C, int ldc, bool zeroC,
+                                           double2 (*At)[kGJ], double2 (*Bs)[kGJ]) {
+  const int tid = threadIdx.x;
+  const int w = tid >> 6, l = tid & 63;
+  const int wr = (w >> 1) * 32, wc = (w & 1) * 32;
+  const int lr = l & 15, lk = l >> 4;
+  d4 acr[2][2], aci[2][2];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) {
+      if (LOADC && !zeroC) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const double2 v = C[(int64_t)(wr + mi * 16 + lk + 4 * r) * ldc + wc + ni * 16 + lr];
+          acr[mi][ni][r] = v.x;
+          aci[mi][ni][r] = v.y;
+        }
+      } else {
+        acr[mi][ni] = d4{0.0, 0.0, 0.0, 0.0};
+        aci[mi][ni] = d4{0.0, 0.0, 0.0, 0.0};
+      }
+    }
+
+#pragma unroll 1
+  for (int kc = 0; kc < kGJ; kc += 16) {
+    // stage A chunk transposed (At[k][row]) and B chunk (Bs[k][col])
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int kk = tid & 15, row = (tid >> 4) + 16 * s;
+      At[kk][row] = A[(int64_t)row * lda + kc + kk];
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int kk = tid >> 4, col = (tid & 15) * 4 + s;
+      Bs[kk][col] = B[(int64_t)(kc + kk) * ldb + col];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < 16; ks += 4) {
+      double ar[2], ai[2], nai[2], br[2], bim[2];
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi) {
+        const double2 v = At[ks + lk][wr + mi * 16 + lr];
+        ar[mi] = NEG ? -v.x : v.x;
+        ai[mi] = NEG ? -v.y : v.y;
+        nai[mi] = -ai[mi];
+      }
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) {
+        const double2 v = Bs[ks + lk][wc + ni * 16 + lr];
+        br[ni] = v.x;
+        bim[ni] = v.y;
+      }
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) {
+          acr[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[mi], br[ni], acr[mi][ni], 0, 0, 0);
+          aci[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[mi], bim[ni], aci[mi][ni], 0, 0, 0);
+        }
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) {
+          acr[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(nai[mi], bim[ni], acr[mi][ni], 0, 0, 0);
+          aci[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[mi], br[ni], aci[mi][ni], 0, 0, 0);
+        }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        C[(int64_t)(wr + mi * 16 + lk + 4 * r) * ldc + wc + ni * 16 + lr] =
+            make_double2(acr[mi][ni][r], aci[mi][ni][r]);
+}
+
+// Row panel X_kj = P S_kj (j != k), S_kk = P; column panel copy S_ik -> Cpanel (i != k).
+__global__ __launch_bounds__(256) void k_gj_panel(double2* __restrict__ M, int64_t mat, int Np,
+                                                  int nb, int k, const double2* __restrict__ Pinv,
+                                                  double2* __restrict__ Cpanel) {
+  __shared__ double2 At[16][kGJ];
+  __shared__ double2 Bs[16][kGJ];
+  const int bi = blockIdx.y, x = blockIdx.x;
+  double2* Mb = M + (int64_t)bi * mat;
+  const double2* Pb = Pinv + (int64_t)bi * kGJ * kGJ;
+  if (x < nb) {
+    const int j = x;
+    double2* Skj = Mb + (int64_t)(k * kGJ) * Np + j * kGJ;
+    if (j == k) {
+      for (int e = threadIdx.x; e < kGJ * kGJ; e += blockDim.x)
+        Skj[(int64_t)(e >> 6) * Np + (e & 63)] = Pb[e];
+    } else {
+      tile_cgemm<false, false>(Pb, kGJ, Skj, Np, Skj, Np, false, At, Bs);
+    }
+  } else {
+    const int i = x - nb;
+    if (i == k) return;
+    const double2* Sik = Mb + (int64_t)(i * kGJ) * Np + k * kGJ;
+    double2* dst = Cpanel + (int64_t)bi * Np * kGJ + (int64_t)i * kGJ * kGJ;
+    for (int e = threadIdx.x; e < kGJ * kGJ; e += blockDim.x)
+      dst[e] = Sik[(int64_t)(e >> 6) * Np + (e & 63)];
+  }
+}
+
+// Trailing update: S_IJ = [J != k] S_IJ - Cpanel_I X_kJ for I != k (X_kk = P).
+__global__ __launch_bounds__(256) void k_gj_update(double2* __restrict__ M, int64_t mat, int Np,
+                                                   int nb, int k,
+                                                   const double2* __restrict__ Cpanel) {
+  __shared__ double2 At[16][kGJ];
+  __shared__ double2 Bs[16][kGJ];
+  const int bi = blockIdx.y;
+  const int t = blockIdx.x;
+  const int Ii = t / nb, J = t - Ii * nb;
+  const int I = Ii < k ? Ii : Ii + 1;
+  double2* Mb = M + (int64_t)bi * mat;
+  const double2* Ci = Cpanel + (int64_t)bi * Np * kGJ + (int64_t)I * kGJ * kGJ;
+  tile_cgemm<true, true>(Ci, kGJ, Mb + (int64_t)(k * kGJ) * Np + J * kGJ, Np,
+                         Mb + (int64_t)(I * kGJ) * Np + J * kGJ, Np, J == k, At, Bs);
+}
+
+// ---------------------------------------------------------------------------
+// Assembly of T = R D and S^T for one row a (block) of one (chain, pole).
+//   TT[a,k]  = Σ_{l ∈ Dcol(a)} D[a,l] R[l,k]               (rows of R, coalesced)
+//   S^T[a,b] = -(h[a,b] + i y δ_ab) - Σ_{k ∈ Dcol(b)} TT[a,k] conj(D[b,k])
+//   T[a,b]   = Σ_{l ∈ Dcol(b)} R[a,l] D[b,l]
+// D[r, Dcol[r][s]] = Δ[Dsrc[r][s]] / 2 (reference overwrite order, host-built).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_assemble(const double2* __restrict__ R,
+                                                  double2* __restrict__ T,
+                                                  double2* __restrict__ S, int64_t mat, int N,
+                                                  int Np, int P, const int* __restrict__ Dcol,
+                                                  const int* __restrict__ Dsrc,
+                                                  const double2* __restrict__ Delta,
+                                                  const int* __restrict__ hcol,
+                                                  const double* __restrict__ hval,
+                                                  const double* __restrict__ ypole) {
+  extern __shared__ double2 smem[];
+  double2* TTrow = smem;
+  double2* Rrow = smem + Np;
+  const int a = blockIdx.x, bi = blockIdx.y;
+  const int c = bi / P, q = bi % P;
+  double2* Srow = S + (int64_t)bi * mat + (int64_t)a * Np;
+  if (a >= N) {  // padding rows: identity
+    for (int b = threadIdx.x; b < Np; b += blockDim.x)
+      Srow[b] = make_double2(b == a ? 1.0 : 0.0, 0.0);
+    return;
+  }
+  const double2* Rb = R + (int64_t)bi * mat;
+  const double2* Dc = Delta + (int64_t)c * 2 * N;
+  int lcol[kSlots];
+  double2 dval[kSlots];
+#pragma unroll
+  for (int s = 0; s < kSlots; ++s) {
+    lcol[s] = Dcol[a * kSlots + s];
+    const int src = Dsrc[a * kSlots + s];
+    const double2 d = src >= 0 ? Dc[src] : make_double2(0.0, 0.0);
+    dval[s] = make_double2(0.5 * d.x, 0.5 * d.y);
+  }
+  __shared__ int hc[kHSlots];
+  __shared__ double hv[kHSlots];
+  if (threadIdx.x < kHSlots) {
+    hc[threadIdx.x] = hcol[a * kHSlots + threadIdx.x];
+    hv[threadIdx.x] = hval[((int64_t)c * N + a) * kHSlots + threadIdx.x];
+  }
+  for (int kk = threadIdx.x; kk < N; kk += blockDim.x) {
+    double2 tt = make_double2(0.0, 0.0);
+#pragma unroll
+    for (int s = 0; s < kSlots; ++s)
+      if (lcol[s] >= 0) tt = cadd(tt, cmul(dval[s], Rb[(int64_t)lcol[s] * Np + kk]));
+    TTrow[kk] = tt;
+    Rrow[kk] = Rb[(int64_t)a * Np + kk];
+  }
+  __syncthreads();
+  const double y = ypole[q];
+  double2* Trow = T + (int64_t)bi * mat + (int64_t)a * Np;
+  for (int b = threadIdx.x; b < Np; b += blockDim.x) {
+    double2 st = make_double2(0.0, 0.0), tv = make_double2(0.0, 0.0);
+    if (b < N) {
+#pragma unroll
+      for (int s = 0; s < kSlots; ++s) {
+        const int kcol = Dcol[b * kSlots + s];
+        if (kcol >= 0) {
+          const int src = Dsrc[b * kSlots + s];
+          const double2 d0 = Dc[src];
+          const double2 db = make_double2(0.5 * d0.x, 0.5 * d0.y);
+          st = cadd(st, cmulc(TTrow[kcol], db));
+          tv = cadd(tv, cmul(Rrow[kcol], db));
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < kHSlots; ++s)
+        if (hc[s] == b) st.x += hv[s];
+      if (b == a) st.y += y;
+    }
+    Srow[b] = make_double2(-st.x, -st.y);
+    Trow[b] = tv;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Contraction: G12[i, j] = -Σ_k T[i,k] S^-1[k,j] = -Σ_k T[i,k] SinvT[j,k]
+// for the ≤4 pairing columns j of row i; plus diag(S^-1) for Tr ρ_hh.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_contract(const double2* __restrict__ T,
+                                                  const double2* __restrict__ SinvT, int64_t mat,
+                                                  int N, int Np, const int* __restrict__ Dcol,
+                                                  double2* __restrict__ G12nn,
+                                                  double2* __restrict__ diagS) {
+  const int i = blockIdx.x, bi = blockIdx.y;
+  const double2* Trow = T + (int64_t)bi * mat + (int64_t)i * Np;
+  const double2* Sb = SinvT + (int64_t)bi * mat;
+  int js[kSlots];
+#pragma unroll
+  for (int s = 0; s < kSlots; ++s) js[s] = Dcol[i * kSlots + s];
+  double acc[2 * kSlots];
+#pragma unroll
+  for (int s = 0; s < 2 * kSlots; ++s) acc[s] = 0.0;
+  for (int kk = threadIdx.x; kk < N; kk += blockDim.x) {
+    const double2 t = Trow[kk];
+#pragma unroll
+    for (int s = 0; s < kSlots; ++s) {
+      if (js[s] >= 0) {
+        const double2 v = Sb[(int64_t)js[s] * Np + kk];
+        acc[2 * s] += t.x * v.x - t.y * v.y;
+        acc[2 * s + 1] += t.x * v.y + t.y * v.x;
+      }
+    }
+  }
+  __shared__ double red[4][2 * kSlots];
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+#pragma unroll
+  for (int s = 0; s < 2 * kSlots; ++s) {
+    const double v = wave_sum(acc[s]);
+    if (l == 0) red[w][s] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 * kSlots) {
+    const int s = threadIdx.x;
+    const double v = red[0][s] + red[1][s] + red[2][s] + red[3][s];
+    double* out = reinterpret_cast<double*>(G12nn + ((int64_t)bi * N + i) * kSlots);
+    out[s] = js[s >> 1] >= 0 ? -v : 0.0;
+  }
+  if (threadIdx.x == 0) diagS[(int64_t)bi * N + i] = Sb[(int64_t)i * Np + i];
+}
+
+// ---------------------------------------------------------------------------
+// Bond-level kernels (O(N)).  Bond b = i + N*dir, chain c: offset c*2N + b.
+// ---------------------------------------------------------------------------
+__global__ void k_pair_force(const double2* __restrict__ G12nn, const int* __restrict__ bond_ij,
+                             const int* __restrict__ bond_ji, const double* __restrict__ cpole,
+                             int N, int P, const double2* __restrict__ Delta,
+                             double2* __restrict__ Pair, double2* __restrict__ F,
+                             double2* __restrict__ Pi, double kick, double beta, double J) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = blockIdx.y;
+  if (b >= 2 * N) return;
+  const int ij = bond_ij[b], ji = bond_ji[b];
+  double2 Pv = make_double2(0.0, 0.0);
+  for (int q = 0; q < P; ++q) {
+    const double2* G = G12nn + (int64_t)(c * P + q) * N * kSlots;
+    const double2 g1 = G[ij], g2 = G[ji];
+    const double cq = cpole[q];
+    Pv.x += cq * (g1.x + g2.x);
+    Pv.y += cq * (g1.y + g2.y);
+  }
+  const int64_t o = (int64_t)c * 2 * N + b;
+  Pair[o] = Pv;
+  const double2 d = Delta[o];
+  const double f = -beta / (2.0 * J);
+  const double2 Fv = make_double2(f * (d.x - J * Pv.x), f * (d.y - J * Pv.y));
+  F[o] = Fv;
+  if (kick != 0.0) {
+    double2 p = Pi[o];
+    p.x += kick * Fv.x;
+    p.y += kick * Fv.y;
+    Pi[o] = p;
+  }
+}
+
+__global__ void k_force_from_pair(const double2* __restrict__ Pair, const double2* __restrict__ Delta,
+                                  double2* __restrict__ F, double2* __restrict__ Pi, int N,
+                                  double kick, double beta, double J) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = blockIdx.y;
+  if (b >= 2 * N) return;
+  const int64_t o = (int64_t)c * 2 * N + b;
+  const double2 Pv = Pair[o], d = Delta[o];
+  const double f = -beta / (2.0 * J);
+  const double2 Fv = make_double2(f * (d.x - J * Pv.x), f * (d.y - J * Pv.y));
+  F[o] = Fv;
+  if (kick != 0.0) {
+    double2 p = Pi[o];
+    p.x += kick * Fv.x;
+    p.y += kick * Fv.y;
+    Pi[o] = p;
+  }
+}
+
+__global__ void k_drift(double2* __restrict__ Delta, const double2* __restrict__ Pi, int N,
+                        double coef, double cap2, int* __restrict__ flag) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = blockIdx.y;
+  if (b >= 2 * N) return;
+  const int64_t o = (int64_t)c * 2 * N + b;
+  double2 d = Delta[o];
+  const double2 p = Pi[o];
+  d.x += coef * p.x;
+  d.y += coef * p.y;
+  Delta[o] = d;
+  if (d.x * d.x + d.y * d.y > cap2) atomicOr(flag, 1);
+}
+
+__global__ __launch_bounds__(256) void k_fermion_energy(const double* __restrict__ ldstatic,
+                                                        const double* __restrict__ ldpart,
+                                                        const double2* __restrict__ diagS,
+                                                        const double* __restrict__ cpole, int N,
+                                                        int nb, int P, double Cx, double beta,
+                                                        double* __restrict__ Ef,
+                                                        double* __restrict__ Trhh) {
+  const int c = blockIdx.x;
+  __shared__ double red[4];
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  double ef_acc = 0.0, tr_acc = 0.0;
+  for (int q = 0; q < P; ++q) {
+    const int bi = c * P + q;
+    double ld = 0.0, tr = 0.0;
+    for (int k = threadIdx.x; k < nb; k += blockDim.x) ld += ldpart[(int64_t)bi * nb + k];
+    for (int i = threadIdx.x; i < N; i += blockDim.x) tr += diagS[(int64_t)bi * N + i].x;
+    ld = wave_sum(ld);
+    if (l == 0) red[w] = ld;
+    __syncthreads();
+    ld = red[0] + red[1] + red[2] + red[3];
+    __syncthreads();
+    tr = wave_sum(tr);
+    if (l == 0) red[w] = tr;
+    __syncthreads();
+    tr = red[0] + red[1] + red[2] + red[3];
+    __syncthreads();
+    ef_acc += cpole[q] * (ldstatic[bi] + ld);
+    tr_acc += cpole[q] * tr;
+  }
+  if (threadIdx.x == 0) {
+    Ef[c] = -2.0 * N * Cx - beta * ef_acc;
+    Trhh[c] = 0.5 * N - tr_acc;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_total_energy(const double2* __restrict__ Delta,
+                                                      const double2* __restrict__ Pi,
+                                                      const double* __restrict__ Ef, int N,
+                                                      double beta, double J, double mass,
+                                                      double* __restrict__ Hout) {
+  const int c = blockIdx.x;
+  __shared__ double red[2][4];
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  double sd = 0.0, sp = 0.0;
+  for (int b = threadIdx.x; b < 2 * N; b += blockDim.x) {
+    const double2 d = Delta[(int64_t)c * 2 * N + b];
+    const double2 p = Pi[(int64_t)c * 2 * N + b];
+    sd += d.x * d.x + d.y * d.y;
+    sp += p.x * p.x + p.y * p.y;
+  }
+  sd = wave_sum(sd);
+  sp = wave_sum(sp);
+  if (l == 0) {
+    red[0][w] = sd;
+    red[1][w] = sp;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double SD = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    const double SP = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+    Hout[c] = (1.0 / (2.0 * mass)) * SP + (beta / (2.0 * J)) * SD + Ef[c];
+  }
+}
+
+__global__ void k_refresh(const double2* __restrict__ noise, double2* __restrict__ Pi, int n,
+                          double scale) {
+  const int o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= n) return;
+  const double2 z = noise[o];
+  Pi[o] = make_double2(z.x * scale, z.y * scale);
+}
+
+__global__ void k_backup(const double2* __restrict__ Delta, const double2* __restrict__ Pair,
+                         const double* __restrict__ Ef, const double* __restrict__ Trhh,
+                         double2* __restrict__ DeltaB, double2* __restrict__ PairB,
+                         double* __restrict__ EfB, double* __restrict__ TrhhB, int n, int nc) {
+  const int o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o < n) {
+    DeltaB[o] = Delta[o];
+    PairB[o] = Pair[o];
+  }
+  if (o < nc) {
+    EfB[o] = Ef[o];
+    TrhhB[o] = Trhh[o];
+  }
+}
+
+__global__ void k_metropolis(const double* __restrict__ Hold, const double* __restrict__ Hnew,
+                             const double* __restrict__ uniform, uint8_t* __restrict__ accepted,
+                             double* __restrict__ dH, int nc) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nc) return;
+  const double d = Hnew[c] - Hold[c];
+  // src/HMC.jl:128 — accept if ΔH < 0 || rand() < exp(-ΔH)
+  const bool acc = (d < 0.0) || (uniform[c] < exp(-d));
+  accepted[c] = acc ? 1 : 0;
+  dH[c] = d;
+}
+
+__global__ void k_restore(const uint8_t* __restrict__ accepted, const double2* __restrict__ DeltaB,
+                          const double2* __restrict__ PairB, const double* __restrict__ EfB,
+                          const double* __restrict__ TrhhB, double2* __restrict__ Delta,
+                          double2* __restrict__ Pair, double* __restrict__ Ef,
+                          double* __restrict__ Trhh, int N) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = blockIdx.y;
+  if (accepted[c]) return;
+  if (b < 2 * N) {
+    const int64_t o = (int64_t)c * 2 * N + b;
+    Delta[o] = DeltaB[o];
+    Pair[o] = PairB[o];
+  }
+  if (b == 0) {
+    Ef[c] = EfB[c];
+    Trhh[c] = TrhhB[c];
+  }
+}
+
+__global__ void k_sum_ld(const double* __restrict__ ldpart, double* __restrict__ ldsum, int nb,
+                         int nbatch) {
+  const int bi = blockIdx.x * blockDim.x + threadIdx.x;
+  if (bi >= nbatch) return;
+  double s = 0.0;
+  for (int k = 0; k < nb; ++k) s += ldpart[(int64_t)bi * nb + k];
+  ldsum[bi] = s;
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+static inline dim3 bonds_grid(const Dims& d) { return dim3((2 * d.N + 255) / 256, d.nc); }
+
+void launch_fill_hz(const Dims& d, double2* M, const int* hcol, const double* hval,
+                    const double* ypole, hipStream_t s) {
+  hipLaunchKernelGGL(k_fill_hz, dim3(d.Np, d.nbatch), dim3(256), 0, s, M, d.mat, d.N, d.Np, d.P,
+                     hcol, hval, ypole);
+}
+void launch_gj_diag(const Dims& d, double2* M, int k, double2* Pinv, double* ldpart,
+                    hipStream_t s) {
+  hipLaunchKernelGGL(k_gj_diag, dim3(d.nbatch), dim3(256), 0, s, M, d.mat, d.Np, k, d.nb, Pinv,
+                     ldpart);
+}
+void launch_gj_panel(const Dims& d, double2* M, int k, const double2* Pinv, double2* Cpanel,
+                     hipStream_t s) {
+  hipLaunchKernelGGL(k_gj_panel, dim3(2 * d.nb, d.nbatch), dim3(256), 0, s, M, d.mat, d.Np, d.nb,
+                     k, Pinv, Cpanel);
+}
+void launch_gj_update(const Dims& d, double2* M, int k, const double2* Cpanel, hipStream_t s) {
+  if (d.nb < 2) return;
+  hipLaunchKernelGGL(k_gj_update, dim3((d.nb - 1) * d.nb, d.nbatch), dim3(256), 0, s, M, d.mat,
+                     d.Np, d.nb, k, Cpanel);
+}
+void launch_assemble(const Dims& d, const double2* R, double2* T, double2* S, const int* Dcol,
+                     const int* Dsrc, const double2* Delta, const int* hcol, const double* hval,
+                     const double* ypole, hipStream_t s) {
+  const size_t shm = 2 * (size_t)d.Np * sizeof(double2);
+  hipLaunchKernelGGL(k_assemble, dim3(d.Np, d.nbatch), dim3(256), shm, s, R, T, S, d.mat, d.N,
+                     d.Np, d.P, Dcol, Dsrc, Delta, hcol, hval, ypole);
+}
+void launch_contract(const Dims& d, const double2* T, const double2* SinvT, const int* Dcol,
+                     double2* G12nn, double2* diagS, hipStream_t s) {
+  hipLaunchKernelGGL(k_contract, dim3(d.N, d.nbatch), dim3(256), 0, s, T, SinvT, d.mat, d.N, d.Np,
+                     Dcol, G12nn, diagS);
+}
+void launch_pair_force(const Dims& d, const double2* G12nn, const int* bond_ij,
+                       const int* bond_ji, const double* cpole, const double2* Delta,
+                       double2* Pair, double2* F, double2* Pi, double kick, double beta,
+                       double J, hipStream_t s) {
+  hipLaunchKernelGGL(k_pair_force, bonds_grid(d), dim3(256), 0, s, G12nn, bond_ij, bond_ji, cpole,
+                     d.N, d.P, Delta, Pair, F, Pi, kick, beta, J);
+}
+void launch_force_from_pair(const Dims& d, const double2* Pair, const double2* Delta,
+                            double2* F, double2* Pi, double kick, double beta, double J,
+                            hipStream_t s) {
+  hipLaunchKernelGGL(k_force_from_pair, bonds_grid(d), dim3(256), 0, s, Pair, Delta, F, Pi, d.N,
+                     kick, beta, J);
+}
+void launch_drift(const Dims& d, double2* Delta, const double2* Pi, double coef, double cap,
+                  int* flag, hipStream_t s) {
+  hipLaunchKernelGGL(k_drift, bonds_grid(d), dim3(256), 0, s, Delta, Pi, d.N, coef, cap * cap,
+                     flag);
+}
+void launch_fermion_energy(const Dims& d, const double* ldstatic, const double* ldpart,
+                           const double2* diagS, const double* cpole, double Cx, double beta,
+                           double* Ef, double* Trhh, hipStream_t s) {
+  hipLaunchKernelGGL(k_fermion_energy, dim3(d.nc), dim3(256), 0, s, ldstatic, ldpart, diagS, cpole,
+                     d.N, d.nb, d.P, Cx, beta, Ef, Trhh);
+}
+void launch_total_energy(const Dims& d, const double2* Delta, const double2* Pi,
+                         const double* Ef, double beta, double J, double mass, double* Hout,
+                         hipStream_t s) {
+  hipLaunchKernelGGL(k_total_energy, dim3(d.nc), dim3(256), 0, s, Delta, Pi, Ef, d.N, beta, J,
+                     mass, Hout);
+}
+void launch_refresh(const Dims& d, const double2* noise, double2* Pi, double scale, hipStream_t s) {
+  const int n = 2 * d.N * d.nc;
+  hipLaunchKernelGGL(k_refresh, dim3((n + 255) / 256), dim3(256), 0, s, noise, Pi, n, scale);
+}
+void launch_backup(const Dims& d, const double2* Delta, const double2* Pair, const double* Ef,
+                   const double* Trhh, double2* DeltaB, double2* PairB, double* EfB,
+                   double* TrhhB, hipStream_t s) {
+  const int n = 2 * d.N * d.nc;
+  const int m = n > d.nc ? n : d.nc;
+  hipLaunchKernelGGL(k_backup, dim3((m + 255) / 256), dim3(256), 0, s, Delta, Pair, Ef, Trhh,
+                     DeltaB, PairB, EfB, TrhhB, n, d.nc);
+}
+void launch_metropolis(const Dims& d, const double* Hold, const double* Hnew,
+                       const double* uniform, uint8_t* accepted, double* dH, hipStream_t s) {
+  hipLaunchKernelGGL(k_metropolis, dim3((d.nc + 63) / 64), dim3(64), 0, s, Hold, Hnew, uniform,
+                     accepted, dH, d.nc);
+}
+void launch_restore(const Dims& d, const uint8_t* accepted, const double2* DeltaB,
+                    const double2* PairB, const double* EfB, const double* TrhhB,
+                    double2* Delta, double2* Pair, double* Ef, double* Trhh, hipStream_t s) {
+  hipLaunchKernelGGL(k_restore, bonds_grid(d), dim3(256), 0, s, accepted, DeltaB, PairB, EfB,
+                     TrhhB, Delta, Pair, Ef, Trhh, d.N);
+}
+void launch_sum_ld(const Dims& d, const double* ldpart, double* ldsum, hipStream_t s) {
+  hipLaunchKernelGGL(k_sum_ld, dim3((d.nbatch + 63) / 64), dim3(64), 0, s, ldpart, ldsum, d.nb,
+                     d.nbatch);
+}
+
+// ---------------------------------------------------------------------------
+// MFMA f64 layout self-test (A = asymmetric integers, B asymmetric): exact.
+// ---------------------------------------------------------------------------
+__global__ void k_mfma_layout(const double* A, const double* B, double* D) {
+  const int l = threadIdx.x;
+  d4 acc = {0.0, 0.0, 0.0, 0.0};
+  acc = __builtin_amdgcn_mfma_f64_16x16x4f64(A[(l & 15) * 4 + (l >> 4)], B[(l >> 4) * 16 + (l & 15)],
+                                            acc, 0, 0, 0);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) D[((l >> 4) + 4 * r) * 16 + (l & 15)] = acc[r];
+}
+
+int selftest_mfma_layout(int device) {
+  if (hipSetDevice(device) != hipSuccess) return -2;
+  double hA[64], hB[64], hD[256];
+  for (int i = 0; i < 16; ++i)
+    for (int k = 0; k < 4; ++k) hA[i * 4 + k] = (double)(i * 7 + k * 3 + 1);
+  for (int k = 0; k < 4; ++k)
+    for (int j = 0; j < 16; ++j) hB[k * 16 + j] = (double)(k * 11 - j * 2 + 5);
+  double *dA, *dB, *dD;
+  if (hipMalloc(&dA, sizeof hA) != hipSuccess) return -2;
+  if (hipMalloc(&dB, sizeof hB) != hipSuccess) return -2;
+  if (hipMalloc(&dD, sizeof hD) != hipSuccess) return -2;
+  (void)hipMemcpy(dA, hA, sizeof hA, hipMemcpyHostToDevice);
+  (void)hipMemcpy(dB, hB, sizeof hB, hipMemcpyHostToDevice);
+  hipLaunchKernelGGL(k_mfma_layout, dim3(1), dim3(64), 0, 0, dA, dB, dD);
+  (void)hipMemcpy(hD, dD, sizeof hD, hipMemcpyDeviceToHost);
+  (void)hipFree(dA);
+  (void)hipFree(dB);
+  (void)hipFree(dD);
+  int bad = 0;
+  for (int i = 0; i < 16; ++i)
+    for (int j = 0; j < 16; ++j) {
+      double r = 0;
+      for (int k = 0; k < 4; ++k) r += hA[i * 4 + k] * hB[k * 16 + j];
+      if (r != hD[i * 16 + j]) ++bad;
+    }
+  return bad;
+}
+
+}  // namespace dwh

@@ -1,0 +1,137 @@
+/*
+ * dwhmc.h — C ABI of the MI355X-native fermionic action/force path of
+ * DwaveHMC.jl (YinkaiYu/Hybrid-Monte-Carlo-for-d-wave-SC).
+ *
+ * The reference is pure Julia with no FFI; each entry point below replaces a
+ * Julia function of the hot path (file:line of the reference in brackets) and
+ * is what a Julia `ccall`, a C++ host or Python `ctypes` binds (see
+ * INTEGRATION.md).  Conventions:
+ *   - every array is borrowed for the duration of the call only;
+ *   - complex numbers are interleaved fp64 pairs (Julia ComplexF64,
+ *     numpy complex128, C99 double _Complex);
+ *   - per-chain bond arrays (Δ, π, F, P) are Julia's column-major N×2 layout:
+ *     element (i, dir) at offset i + N*dir, dir 0 = +x, dir 1 = +y
+ *     (src/Types.jl:106-111); chain c starts at offset c*2N;
+ *   - neighbour tables are Julia's column-major N×4 Int64 matrices, 1-based
+ *     (src/Types.jl:53-80);
+ *   - functions return DWH_OK (0) or a negative DWH_ERR_* code; the message is
+ *     in dwh_last_error(ctx) (dwh_last_error(NULL) after a failed create);
+ *   - a context is bound to one HIP device and one stream and is not
+ *     thread-safe (one context per host thread).
+ */
+#ifndef DWHMC_H
+#define DWHMC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct { double re, im; } dwh_c128;
+typedef struct dwh_ctx dwh_ctx;
+
+enum {
+  DWH_OK = 0,
+  DWH_ERR_ARG = -1,       /* bad argument (Julia: ArgumentError / DimensionMismatch) */
+  DWH_ERR_HIP = -2,       /* HIP runtime failure (no device, OOM, launch failure) */
+  DWH_ERR_STATE = -3,     /* call out of order */
+  DWH_ERR_SPECTRUM = -4,  /* |Δ| left the guarded range the pole set was built for */
+  DWH_ERR_TABLE = -5      /* β·E_bound outside the compiled pole table */
+};
+
+typedef struct {
+  int64_t N;          /* sites Lx*Ly */
+  int64_t Np;         /* N padded to the 64-row GJ block */
+  int64_t nchains;
+  int64_t npoles;     /* imaginary-axis pole pairs = no-pivot LUs per chain per step */
+  double kappa;       /* β·E'/2 of the pole table entry in use */
+  double e_bound;     /* E' : spectral bound the poles are valid on */
+  double err_tanh;    /* sup |tanh - rational| of the table entry */
+  double delta_cap;   /* guard on max|Δ_ij| */
+  int64_t device_bytes;
+} dwh_info_t;
+
+/* ModelParameters + initialize_cache + init_static_H!
+ * [src/Types.jl:49-91, src/Types.jl:182-212, src/Hamiltonian.jl:10-47].
+ * One chain, delta_cap = 2.0.  disorder: length N (state.disorder_pot). */
+int dwh_create(dwh_ctx** ctx, int64_t Lx, int64_t Ly, double t, double tp, double mu,
+               double beta, double J, const int64_t* nn_table, const int64_t* nnn_table,
+               const double* disorder, int32_t device);
+
+/* Batched form: nchains independent Markov chains / disorder realisations on one
+ * device (disorder: nchains*N).  delta_cap <= 0 selects the default 2.0. */
+int dwh_create_batched(dwh_ctx** ctx, int64_t Lx, int64_t Ly, double t, double tp, double mu,
+                       double beta, double J, const int64_t* nn_table, const int64_t* nnn_table,
+                       int64_t nchains, const double* disorder, double delta_cap, int32_t device);
+
+void dwh_destroy(dwh_ctx* ctx);
+const char* dwh_last_error(const dwh_ctx* ctx);
+int dwh_info(dwh_ctx* ctx, dwh_info_t* out);
+
+/* update_H_BdG! [src/Hamiltonian.jl:55-86]: set Δ (nchains*2N) on the device. */
+int dwh_update_pairing(dwh_ctx* ctx, const dwh_c128* Delta);
+
+/* diagonalize_H_BdG! replacement [src/Hamiltonian.jl:96-114]: pole-expanded
+ * no-pivot LU of H_BdG(Δ) - i y_q for all poles; caches the pairing
+ * amplitudes P_ij and the fermion energy E_f for the current Δ. */
+int dwh_factorize(dwh_ctx* ctx);
+
+/* compute_forces! [src/Observables.jl:14-62]: F = -β/2J (Δ - J P) with the
+ * cached P.  Delta may be NULL (use the device Δ).  F_out: nchains*2N. */
+int dwh_forces(dwh_ctx* ctx, const dwh_c128* Delta, dwh_c128* F_out);
+
+/* P_ij = -ρ_{i,j+N} - ρ_{j,i+N} of the last factorisation [src/Observables.jl:37-53]. */
+int dwh_pairing(dwh_ctx* ctx, dwh_c128* P_out);
+
+/* Fermion part of compute_total_energy [src/HMC.jl:21-27], per chain. */
+int dwh_fermion_energy(dwh_ctx* ctx, double* Ef);
+
+/* Tr ρ_hh per chain (hole-block trace of the density matrix); with
+ * Tr ρ_pp + Tr ρ_hh = N this gives hole_conc = 2 Tr ρ_hh / N - 1
+ * [src/Observables.jl:120-145]. */
+int dwh_hole_trace(dwh_ctx* ctx, double* tr_hh);
+
+/* compute_total_energy [src/HMC.jl:12-41] for the device Δ, π and cached E_f. */
+int dwh_total_energy(dwh_ctx* ctx, double mass, double* H);
+
+/* Device state access (Δ, π: nchains*2N; either pointer may be NULL). */
+int dwh_set_state(dwh_ctx* ctx, const dwh_c128* Delta, const dwh_c128* pi);
+int dwh_get_state(dwh_ctx* ctx, dwh_c128* Delta, dwh_c128* pi);
+
+/* hmc_sweep! [src/HMC.jl:71-144] with the RNG draws injected (the reference
+ * is unseeded): noise = randn!(ComplexF64) draws (Var Re = Var Im = 1/2),
+ * nchains*2N; uniform = the rand() of the Metropolis test, nchains.
+ * Outputs accepted[nchains] (0/1) and dH[nchains]. */
+int dwh_hmc_sweep(dwh_ctx* ctx, const dwh_c128* noise, const double* uniform, int64_t Nt,
+                  double dt, double mass, uint8_t* accepted, double* dH);
+
+/* Throughput path: upload the draws of nsweeps sweeps once (noise:
+ * nsweeps*nchains*2N, uniform: nsweeps*nchains), then enqueue sweeps that
+ * read them from HBM without host round trips. */
+int dwh_load_draws(dwh_ctx* ctx, int64_t nsweeps, const dwh_c128* noise, const double* uniform);
+int dwh_run_sweeps(dwh_ctx* ctx, int64_t first_sweep, int64_t nsweeps, int64_t Nt, double dt,
+                   double mass);
+int dwh_sweep_results(dwh_ctx* ctx, int64_t first_sweep, int64_t nsweeps, uint8_t* accepted,
+                      double* dH);
+int dwh_synchronize(dwh_ctx* ctx);
+
+/* hipStream_t the context launches on (for events / interop). */
+int dwh_stream(dwh_ctx* ctx, void** stream);
+
+/* Kernel timing with HIP events on the context stream (bench/profiling). */
+int dwh_timing_enable(dwh_ctx* ctx, int32_t enable);
+/* name: "gj_update", "gj_panel", "gj_diag", "assemble", "contract", "step";
+ * returns total milliseconds, launches and algorithmic flops (or bytes) per
+ * launch summed over launches. */
+int dwh_timing_read(dwh_ctx* ctx, const char* name, double* total_ms, int64_t* launches,
+                    double* work);
+int dwh_timing_reset(dwh_ctx* ctx);
+
+/* Self-test of the f64 MFMA fragment layout (A = I, asymmetric B); 0 = pass. */
+int dwh_selftest_mfma(int32_t device);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DWHMC_H */

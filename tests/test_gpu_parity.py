@@ -1,0 +1,219 @@
+"""GPU parity: the HIP path through the C ABI vs the CPU oracle.
+
+Tolerances (fp64; the pole set approximates tanh to <= 2e-14 on the spectrum):
+  * forces          ‖F_gpu - F_ref‖∞ ≤ 1e-10 (1 + ‖F_ref‖∞)
+  * pairing P_ij    ‖P_gpu - P_ref‖∞ ≤ 1e-11
+  * E_f             |ΔE_f| ≤ 1e-11 |E_f|
+  * hole density    |Δ hole_conc| ≤ 1e-11
+  * HMC sweep       |ΔdH| ≤ 1e-8 (1 + |dH|), Δ after the sweep ≤ 1e-10, accept flag equal
+The oracle restates the reference with LAPACK zheevr (oracle/dwhmc_oracle.py).
+"""
+import math
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+T, TP, MU, J = 1.0, -0.35, -1.08, 0.8
+
+
+def make_case(O, Lx, Ly, beta, seed, W=1.0, nimp=0.05, amp=0.3, mu=MU, tp=TP, Jc=J):
+    p = O.ModelParameters(Lx, Ly, T, tp, mu, W, nimp, beta, Jc, 1.0)
+    rng = np.random.default_rng(seed)
+    st = O.initialize_state(p, rng)
+    N = p.N
+    dwave = np.stack([np.ones(N), -np.ones(N)], axis=1) * amp
+    Delta = st.Delta + dwave * (1 + 0.3 * rng.standard_normal((N, 1))) * np.exp(1j * 0.2 * rng.standard_normal((N, 1)))
+    return p, st.disorder_pot, Delta
+
+
+def device_ctx(dwhmc, p, disorder, **kw):
+    return dwhmc.FermionContext(p.Lx, p.Ly, p.t, p.tp, p.mu, p.beta, p.J, p.nn_table, p.nnn_table,
+                                disorder, **kw)
+
+
+def test_mfma_f64_layout(dwhmc):
+    assert dwhmc.selftest_mfma(0) == 0
+
+
+@pytest.mark.parametrize("Lx,Ly,beta", [(4, 4, 4.0), (6, 6, 8.0), (5, 7, 16.0), (8, 8, 16.0),
+                                        (16, 16, 8.0), (16, 8, 16.0), (3, 3, 4.0), (2, 2, 4.0),
+                                        (2, 5, 8.0)])
+def test_factorize_matches_oracle(dwhmc, oracle, Lx, Ly, beta):
+    O = oracle
+    p, dis, Delta = make_case(O, Lx, Ly, beta, seed=Lx * 100 + Ly)
+    cache, F_ref, Ef_ref = O.evaluate(p, dis, Delta)
+    P_ref, _ = O.pairing_P(cache.U, cache.E_n, p)
+    ctx = device_ctx(dwhmc, p, dis)
+    ctx.set_pairing(Delta)
+    ctx.factorize()
+    P = ctx.pairing()[0]
+    F = ctx.forces()[0]
+    Ef = ctx.fermion_energy()[0]
+    assert np.max(np.abs(P - P_ref)) <= 1e-11, np.max(np.abs(P - P_ref))
+    assert np.max(np.abs(F - F_ref)) <= 1e-10 * (1 + np.max(np.abs(F_ref)))
+    assert abs(Ef - Ef_ref) <= 1e-11 * abs(Ef_ref), (Ef, Ef_ref)
+    # hole density from Tr ρ_hh (src/Observables.jl:120-145)
+    hole_ref = O.measure_observables(cache, p, Delta)["hole_conc"]
+    hole = 2.0 * ctx.hole_trace()[0] / p.N - 1.0
+    assert abs(hole - hole_ref) <= 1e-11, (hole, hole_ref)
+    ctx.close()
+
+
+def test_full_size_L32_beta16(dwhmc, oracle):
+    """BASELINE config C3 size (N = 1024, n = 2048) against the eigen oracle."""
+    O = oracle
+    p, dis, Delta = make_case(O, 32, 32, 16.0, seed=3232)
+    cache, F_ref, Ef_ref = O.evaluate(p, dis, Delta)
+    ctx = device_ctx(dwhmc, p, dis)
+    ctx.set_pairing(Delta)
+    ctx.factorize()
+    F = ctx.forces()[0]
+    Ef = ctx.fermion_energy()[0]
+    assert np.max(np.abs(F - F_ref)) <= 1e-10 * (1 + np.max(np.abs(F_ref)))
+    assert abs(Ef - Ef_ref) <= 1e-11 * abs(Ef_ref)
+    ctx.close()
+
+
+def test_batched_chains_independent(dwhmc, oracle):
+    O = oracle
+    cases = [make_case(O, 6, 6, 8.0, seed=s) for s in (1, 2, 3)]
+    p = cases[0][0]
+    dis = np.stack([c[1] for c in cases])
+    Delta = np.stack([c[2] for c in cases])
+    ctx = device_ctx(dwhmc, p, dis)
+    ctx.set_pairing(Delta)
+    ctx.factorize()
+    F = ctx.forces()
+    Ef = ctx.fermion_energy()
+    for c, (pc, dc, Dc) in enumerate(cases):
+        _, F_ref, Ef_ref = O.evaluate(pc, dc, Dc)
+        assert np.max(np.abs(F[c] - F_ref)) <= 1e-10 * (1 + np.max(np.abs(F_ref)))
+        assert abs(Ef[c] - Ef_ref) <= 1e-11 * abs(Ef_ref)
+    ctx.close()
+
+
+def test_clean_dwave_closed_form_on_device(dwhmc, oracle):
+    """I5 / scripts/benchmark_clean.jl:15-43 directly on the HIP path."""
+    O = oracle
+    L, beta, D0 = 8, 16.0, 0.25
+    p = O.ModelParameters(L, L, T, TP, MU, 0.0, 0.0, beta, J, 1.0)
+    Delta = np.stack([np.full(p.N, D0), np.full(p.N, -D0)], axis=1).astype(np.complex128)
+    _, Px, Fx, Ef = O.clean_dwave_closed_form(D0, L, L, T, TP, MU, beta, J)
+    ctx = device_ctx(dwhmc, p, np.zeros(p.N))
+    ctx.set_pairing(Delta)
+    ctx.factorize()
+    P = ctx.pairing()[0]
+    F = ctx.forces()[0]
+    assert np.max(np.abs(P[:, 0] - Px)) <= 1e-11
+    assert np.max(np.abs(P[:, 1] + Px)) <= 1e-11
+    assert np.max(np.abs(F[:, 0] - Fx)) <= 1e-10
+    assert abs(ctx.fermion_energy()[0] - Ef) <= 1e-11 * abs(Ef)
+    ctx.close()
+
+
+def _oracle_after_sweeps(O, p, dis, Delta0, draws, Nt, dt, factorize_first=True):
+    cache = O.initialize_cache(p)
+    O.init_static_H(cache, p, dis)
+    st = O.SimulationState(dis, Delta0.copy(), np.zeros_like(Delta0))
+    O.update_H_BdG(cache, p, st.Delta)
+    if factorize_first:
+        O.diagonalize_H_BdG(cache, p)
+    out = []
+    for noise, u in draws:
+        acc, dH = O.hmc_sweep(cache, p, st, Nt, dt, noise, u)
+        out.append((acc, dH, st.Delta.copy(), st.pi.copy()))
+    return out
+
+
+@pytest.mark.parametrize("factorize_first", [True, False])
+def test_hmc_sweep_matches_oracle(dwhmc, oracle, factorize_first):
+    """hmc_sweep! (src/HMC.jl:71-144) with injected draws; factorize_first=False
+    reproduces the zeroed-cache first sweep of scripts/benchmark_clean.jl:82-88."""
+    O = oracle
+    p, dis, Delta0 = make_case(O, 6, 6, 8.0, seed=77, amp=0.1)
+    Nt = 6
+    dt = O.calc_optimal_dt(p.beta, p.J, p.mass, Nt)
+    rng = np.random.default_rng(5)
+    draws = [((rng.standard_normal((p.N, 2)) + 1j * rng.standard_normal((p.N, 2))) * math.sqrt(0.5),
+              float(rng.random())) for _ in range(4)]
+    ref = _oracle_after_sweeps(O, p, dis, Delta0, draws, Nt, dt, factorize_first)
+    ctx = device_ctx(dwhmc, p, dis)
+    ctx.set_pairing(Delta0)
+    if factorize_first:
+        ctx.factorize()
+    for (noise, u), (acc_r, dH_r, D_r, pi_r) in zip(draws, ref):
+        acc, dH = ctx.hmc_sweep(noise, np.array([u]), Nt, dt, p.mass)
+        D, pi = ctx.get_state()
+        assert abs(dH[0] - dH_r) <= 1e-8 * (1 + abs(dH_r)), (dH[0], dH_r)
+        assert bool(acc[0]) == acc_r
+        assert np.max(np.abs(D[0] - D_r)) <= 1e-10
+        assert np.max(np.abs(pi[0] - pi_r)) <= 1e-9
+    ctx.close()
+
+
+def test_throughput_path_equals_single_sweeps(dwhmc, oracle):
+    O = oracle
+    p, dis, Delta0 = make_case(O, 8, 8, 8.0, seed=9, amp=0.1)
+    Nt, ns = 4, 3
+    dt = O.calc_optimal_dt(p.beta, p.J, p.mass, Nt)
+    rng = np.random.default_rng(11)
+    noise = (rng.standard_normal((ns, 2, p.N, 2)) + 1j * rng.standard_normal((ns, 2, p.N, 2))) * math.sqrt(0.5)
+    uni = rng.random((ns, 2))
+    dis2 = np.stack([dis, dis[::-1].copy()])
+    D2 = np.stack([Delta0, Delta0[::-1].copy()])
+    a = device_ctx(dwhmc, p, dis2)
+    a.set_pairing(D2)
+    a.factorize()
+    res_single = [a.hmc_sweep(noise[s], uni[s], Nt, dt, p.mass) for s in range(ns)]
+    Da, _ = a.get_state()
+    b = device_ctx(dwhmc, p, dis2)
+    b.set_pairing(D2)
+    b.factorize()
+    b.load_draws(noise, uni)
+    b.run_sweeps(0, ns, Nt, dt, p.mass)
+    acc, dH = b.sweep_results(0, ns)
+    Db, _ = b.get_state()
+    for s in range(ns):
+        assert np.array_equal(acc[s], res_single[s][0])
+        assert np.array_equal(dH[s], res_single[s][1])
+    assert np.array_equal(Da, Db)
+    a.close()
+    b.close()
+
+
+def test_spectrum_guard_trips(dwhmc, oracle):
+    O = oracle
+    p, dis, Delta0 = make_case(O, 4, 4, 4.0, seed=1, amp=0.9)
+    ctx = device_ctx(dwhmc, p, dis, delta_cap=0.5)
+    ctx.set_pairing(Delta0)
+    ctx.factorize()
+    noise = np.zeros((p.N, 2), dtype=np.complex128)
+    with pytest.raises(dwhmc.SpectrumGuardError):
+        ctx.hmc_sweep(noise, np.array([0.5]), 2, 0.05, 1.0)
+    ctx.close()
+
+
+def test_host_mirror_api_roundtrip(dwhmc, oracle):
+    """The reference-named API (init_static_H ... hmc_sweep) drives the device."""
+    O = oracle
+    m = dwhmc
+    p = m.ModelParameters(6, 6, T, TP, MU, 1.0, 0.05, 8.0, J, 1.0)
+    st = m.initialize_state(p, np.random.default_rng(4))
+    cache = m.initialize_cache(p)
+    m.init_static_H(cache, p, st)
+    m.update_H_BdG(cache, p, st)
+    m.diagonalize_H_BdG(cache, p)
+    m.compute_forces(cache, p, st)
+    po = O.ModelParameters(6, 6, T, TP, MU, 1.0, 0.05, 8.0, J, 1.0)
+    oc, F_ref, Ef_ref = O.evaluate(po, st.disorder_pot, st.Delta)
+    assert np.max(np.abs(cache.forces - F_ref)) <= 1e-10 * (1 + np.max(np.abs(F_ref)))
+    obs = m.measure_observables(cache, p, st)
+    obs_ref = O.measure_observables(oc, po, st.Delta)
+    for k in O.OBS_FIELDS:
+        a, b = getattr(obs, k), obs_ref[k]
+        assert abs(a - b) <= 1e-10 * (1 + abs(b)), (k, a, b)
+    acc, dH = m.hmc_sweep(cache, p, st, Nt=4, dt=m.calc_optimal_dt(p.beta, p.J, p.mass, 4),
+                          rng=np.random.default_rng(0))
+    assert np.isfinite(dH)

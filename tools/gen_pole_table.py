@@ -1,0 +1,258 @@
+#!/usr/bin/env python3
+"""Offline generator of the imaginary-axis pole tables used by the HIP path.
+
+What the table approximates
+---------------------------
+The reference needs f(H) = (1 + e^{βH})^{-1} (src/Observables.jl:24-51) and
+E_f = -Σ_n ln(1 + e^{-βE_n}) (src/HMC.jl:21-27).  With x = E' u (E' an upper
+bound of the BdG spectrum) and κ = βE'/2:
+
+    tanh(κu) ≈ Σ_q a_q · u / (u² + t_q),     u ∈ [-1, 1],  t_q > 0,  a_q > 0
+    ln 2cosh(κu) ≈ C_u + (κ/2) Σ_q a_q ln(u² + t_q)
+
+i.e. a real, odd rational approximant whose poles ±i√t_q lie on the imaginary
+axis.  Each pole pair costs ONE complex no-pivot LU per leapfrog step on the
+GPU (H - i y_q and H + i y_q = (H - i y_q)† share it), see DESIGN.md §2.
+
+How it is built
+---------------
+tanh(κ√s)/√s is a Markov (Stieltjes) function of s = u²:
+    τ(s) = Σ_{k≥1} (2/κ) / (s + ((2k-1)π/2κ)²).
+A multipoint Padé approximant of a Markov function interpolating at 2m real
+nodes s_j ∈ [0,1] is the m-point Gauss quadrature of the modified measure
+dμ(t)/Π_j(t+s_j) — so its poles are guaranteed real-negative in s (purely
+imaginary in u) with positive residues.  The Gauss rule is computed with
+mpmath (Lanczos with full re-orthogonalisation); the Matsubara tail k > K is
+folded in by an exact Gauss rule on its Hurwitz-zeta moments.  The 2m nodes
+are then moved Remez-style (equalising the local error maxima in the
+log(s + a) variable) until sup|error| stops improving.
+
+Run: python tools/gen_pole_table.py  (≈10–30 min on 8 cores); writes
+hybrid-monte-carlo-for-d-wave-sc_amd/csrc/pole_table.inc and
+tests/golden/pole_table.json.  Tests re-verify every entry on a dense grid.
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+import sys
+import time
+from multiprocessing import Pool
+
+import mpmath as mp
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EPS_TANH = 2.0e-14        # sup |tanh(κu) - r(u)| target on [-1, 1]
+KAPPA_EXPONENTS = range(0, 45)   # κ = 2^(j/4), 1 .. 2048
+DPS = 40
+
+
+def _gauss_from_moments(M, n):
+    H = mp.matrix(n + 1, n + 1)
+    for i in range(n + 1):
+        for j in range(n + 1):
+            H[i, j] = M[i + j]
+    R = mp.cholesky(H).T
+    a, b = [], []
+    for j in range(n):
+        aj = R[j, j + 1] / R[j, j] - (R[j - 1, j] / R[j - 1, j - 1] if j > 0 else 0)
+        a.append(aj)
+        if j < n - 1:
+            b.append(R[j + 1, j + 1] / R[j, j])
+    Jm = mp.matrix(n, n)
+    for i in range(n):
+        Jm[i, i] = a[i]
+        if i < n - 1:
+            Jm[i, i + 1] = Jm[i + 1, i] = b[i]
+    E, V = mp.eigsy(Jm)
+    return [E[i] for i in range(n)], [M[0] * V[0, i] ** 2 for i in range(n)]
+
+
+def _hurwitz(s, a):
+    """ζ(s, a) through the polygamma function (mpmath's zeta(s, a) loses
+    ~50 digits for a ~ 1e3 at s ~ 40; psi stays accurate)."""
+    return (-1) ** s * mp.psi(s - 1, a) / mp.factorial(s - 1)
+
+
+def matsubara_measure(kappa, ntail=10):
+    """Atoms (t_k, μ_k) of τ's Stieltjes measure; tail k > K folded into ntail
+    Gauss atoms of ρ = Σ_{k>K} (w/t_k) δ(1/t_k) (moments via Hurwitz zeta)."""
+    kap = mp.mpf(kappa)
+    w = 2 / kap
+    K = int(max(40, math.ceil(kappa)))
+    t = [((2 * k - 1) * mp.pi / (2 * kap)) ** 2 for k in range(1, K + 1)]
+    mu = [w] * K
+    tK = t[-1]
+    with mp.workdps(3 * DPS):
+        # moments of ρ in the scaled variable x' = tK / t ∈ (0, 1]
+        M = [w * tK ** p * (2 * kap / mp.pi) ** (2 * p + 2) * mp.mpf(2) ** (-2 * p - 2)
+             * _hurwitz(2 * p + 2, K + mp.mpf(1) / 2) for p in range(2 * ntail + 1)]
+        x, rho = _gauss_from_moments(M, ntail)
+    for xi, ri in zip(x, rho):
+        ti = tK / xi
+        t.append(ti)
+        mu.append(ri * ti)
+    return t, mu
+
+
+def multipoint_pade(t, mu, m, nodes_s):
+    s = [mp.mpf(float(x)) for x in nodes_s]
+    K = len(t)
+    nu = []
+    for tk, mk in zip(t, mu):
+        om = mp.mpf(1)
+        for sj in s:
+            om *= (tk + sj)
+        nu.append(mk / om)
+    tot = mp.fsum(nu)
+    Q = [[mp.sqrt(x / tot) for x in nu]]
+    alpha, beta = [], []
+    for j in range(m):
+        v = [t[i] * Q[-1][i] for i in range(K)]
+        alpha.append(mp.fsum(v[i] * Q[-1][i] for i in range(K)))
+        for _ in range(2):
+            for qq in Q:
+                c = mp.fsum(v[i] * qq[i] for i in range(K))
+                v = [v[i] - c * qq[i] for i in range(K)]
+        b = mp.sqrt(mp.fsum(x * x for x in v))
+        if j < m - 1:
+            beta.append(b)
+            Q.append([x / b for x in v])
+    Jm = mp.matrix(m, m)
+    for i in range(m):
+        Jm[i, i] = alpha[i]
+        if i < m - 1:
+            Jm[i, i + 1] = Jm[i + 1, i] = beta[i]
+    E, V = mp.eigsy(Jm)
+    tq, a = [], []
+    for i in range(m):
+        om = mp.mpf(1)
+        for sj in s:
+            om *= (E[i] + sj)
+        tq.append(E[i])
+        a.append(tot * V[0, i] ** 2 * om)
+    order = sorted(range(m), key=lambda i: tq[i])
+    return (np.array([float(tq[i]) for i in order]),
+            np.array([float(a[i]) for i in order]))
+
+
+def ugrid(kappa, n):
+    return np.unique(np.concatenate([np.linspace(0.0, 1.0, n),
+                                     np.geomspace(1e-5 / kappa, 1.0, n)]))
+
+
+def tanh_error(kappa, tq, a, u):
+    return np.sum(a[None, :] * u[:, None] / (u[:, None] ** 2 + tq[None, :]), axis=1) - np.tanh(kappa * u)
+
+
+def phi_fit(kappa, tq, a, u):
+    """C_u and sup error of ln 2cosh(κu) ≈ C_u + (κ/2) Σ a ln(u² + t)."""
+    phi = np.logaddexp(kappa * u, -kappa * u)
+    apx = 0.5 * kappa * np.sum(a[None, :] * np.log(u[:, None] ** 2 + tq[None, :]), axis=1)
+    d = phi - apx
+    return 0.5 * (d.max() + d.min()), 0.5 * (d.max() - d.min())
+
+
+def optimise(kappa, m, t, mu, iters=40):
+    a0 = (math.pi / (2 * kappa)) ** 2
+    lo, hi = math.log(a0), math.log(1 + a0)
+    L = np.full(2 * m + 1, (hi - lo) / (2 * m + 1))
+    u = ugrid(kappa, 20001)
+    best = (np.inf, None)
+    stall = 0
+    for _ in range(iters):
+        s = np.exp(lo + np.cumsum(L)[:-1]) - a0
+        tq, a = multipoint_pade(t, mu, m, s)
+        e = tanh_error(kappa, tq, a, u)
+        sup = float(np.max(np.abs(e)))
+        if sup < 0.97 * best[0]:
+            stall = 0
+        else:
+            stall += 1
+        if sup < best[0]:
+            best = (sup, (tq, a))
+        if stall >= 6:
+            break
+        edges = np.concatenate([[0.0], np.sqrt(np.maximum(s, 0.0)), [1.0]])
+        E = np.array([np.max(np.abs(e[(u >= edges[i]) & (u <= edges[i + 1])]), initial=0.0) + 1e-300
+                      for i in range(2 * m + 1)])
+        g = math.exp(float(np.mean(np.log(E))))
+        L = L * (E / g) ** (-0.08)
+        L *= (hi - lo) / L.sum()
+    return best
+
+
+def entry(j):
+    mp.mp.dps = DPS
+    kappa = 2.0 ** (j / 4.0)
+    t, mu = matsubara_measure(kappa)
+    m = max(2, int(math.floor(2.0 + 2.35 * math.log(kappa + 1.0))))
+    tried = {}
+    while True:
+        sup, (tq, a) = optimise(kappa, m, t, mu)
+        tried[m] = (sup, tq, a)
+        if sup <= EPS_TANH:
+            if m - 1 >= 1 and (m - 1) not in tried:
+                m -= 1
+                continue
+            break
+        if (m + 1) in tried:
+            m += 1
+            break
+        m += 1
+    sup, tq, a = tried[m]
+    uf = ugrid(kappa, 400001)
+    err = float(np.max(np.abs(tanh_error(kappa, tq, a, uf))))
+    C_u, phierr = phi_fit(kappa, tq, a, uf)
+    return dict(j=j, kappa=kappa, m=int(m), t=[float(x) for x in tq], a=[float(x) for x in a],
+                C_u=float(C_u), err_tanh=err, err_phi=float(phierr))
+
+
+def write_outputs(entries):
+    entries = sorted(entries, key=lambda e: e["kappa"])
+    jpath = os.path.join(ROOT, "tests", "golden", "pole_table.json")
+    with open(jpath, "w") as f:
+        json.dump(dict(eps_tanh=EPS_TANH, generator="tools/gen_pole_table.py", entries=entries), f, indent=1)
+    cpath = os.path.join(ROOT, "hybrid-monte-carlo-for-d-wave-sc_amd", "csrc", "pole_table.inc")
+    with open(cpath, "w") as f:
+        f.write("// GENERATED by tools/gen_pole_table.py — do not edit.\n")
+        f.write("// tanh(k u) ~ sum_q a_q u/(u^2+t_q) on [-1,1];  ln2cosh(k u) ~ C_u + k/2 sum_q a_q ln(u^2+t_q)\n")
+        f.write(f"static const int kPoleTableSize = {len(entries)};\n")
+        f.write("struct PoleEntry { double kappa; int m; double C_u; double err_tanh; double err_phi; int off; };\n")
+        off = 0
+        f.write("static const PoleEntry kPoleEntries[] = {\n")
+        for e in entries:
+            f.write(f"  {{{e['kappa']!r}, {e['m']}, {e['C_u']!r}, {e['err_tanh']!r}, {e['err_phi']!r}, {off}}},\n")
+            off += e["m"]
+        f.write("};\n")
+        f.write(f"static const double kPoleT[{off}] = {{\n")
+        for e in entries:
+            f.write("  " + ", ".join(repr(x) for x in e["t"]) + ",\n")
+        f.write("};\n")
+        f.write(f"static const double kPoleA[{off}] = {{\n")
+        for e in entries:
+            f.write("  " + ", ".join(repr(x) for x in e["a"]) + ",\n")
+        f.write("};\n")
+    return jpath, cpath
+
+
+def main():
+    js = list(KAPPA_EXPONENTS)
+    if len(sys.argv) > 1:
+        js = [int(x) for x in sys.argv[1].split(",")]
+    t0 = time.time()
+    procs = int(os.environ.get("GEN_PROCS", "7"))
+    out = []
+    with Pool(procs) as pool:
+        # largest κ first so the slow ones start early
+        for e in pool.imap_unordered(entry, sorted(js, reverse=True)):
+            out.append(e)
+            print(f"kappa={e['kappa']:9.3f} m={e['m']:2d} err_tanh={e['err_tanh']:.2e} "
+                  f"err_phi={e['err_phi']:.2e}  [{time.time()-t0:.0f}s]", flush=True)
+    print(write_outputs(out))
+
+
+if __name__ == "__main__":
+    main()
