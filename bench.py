@@ -1,0 +1,215 @@
+#!/usr/bin/env python3
+"""Headline benchmark: fp64 leapfrog steps/s of DwaveHMC.jl's hot path
+(BASELINE.json metric) on MI355X, one process per GPU.
+
+A bench "step" is ONE leapfrog step of hmc_sweep! (src/HMC.jl:98-114) for
+every chain the rank owns: drift, pairing update, pole-expanded no-pivot LU of
+H_BdG(Δ) - i y_q for all poles, force contraction, kick.  The timed region
+runs steps/Nt complete sweeps (momentum refresh, H_old, backup, initial force,
+Nt leapfrog steps, H_new, Metropolis, restore), so Metropolis and energies
+are inside the timed work.  Workload (BASELINE configs[2] / C3): L=32
+(N=1024, BdG n=2048), β=16, one chain per GPU; t=1, t'=-0.35, μ=-1.08, W=1,
+n_imp=0.05, J=0.8, m=1, Nt=10, dt = calc_optimal_dt (src/Simulation.jl:11-14);
+synthetic disorder/Δ₀/momenta from seed 1000+replica.  N>1: independent
+disorder replicas per rank (weak scaling), no collective in the data path;
+torch.distributed (RCCL) only for the barrier, the max-time reduction and the
+observable gather.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--L 32] [--beta 16]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "fp64 leapfrog steps/sec at L=32, 1→8 MI355X; % fp64 MFMA roofline"
+PEAK_F64_TFLOPS = 78.6        # MI355X dense fp64 matrix peak (= fp64 vector peak on CDNA4)
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50, help="leapfrog steps timed (multiple of --Nt)")
+    ap.add_argument("--warmup", type=int, default=10, help="untimed leapfrog steps (multiple of --Nt)")
+    ap.add_argument("--L", type=int, default=32)
+    ap.add_argument("--beta", type=float, default=16.0)
+    ap.add_argument("--chains", type=int, default=1, help="chains per GPU")
+    ap.add_argument("--Nt", type=int, default=10)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-steps", type=int, default=0, help="oracle leapfrog steps for the CPU leg (0 = auto)")
+    ap.add_argument("--no-timing", action="store_true", help="disable per-kernel HIP events")
+    return ap.parse_args()
+
+
+def synthetic(p, O, replica, nchains, Nt, nsweeps):
+    """Disorder, Δ₀ and the sweep draws for `nchains` chains of one replica."""
+    dis, D0 = [], []
+    for c in range(nchains):
+        rng = np.random.default_rng(1000 + replica * nchains + c)
+        st = O.initialize_state(p, rng)            # src/Types.jl:118-134
+        dis.append(st.disorder_pot)
+        D0.append(st.Delta)
+    rng = np.random.default_rng(7_000_000 + replica)
+    shape = (nsweeps, nchains, p.N, 2)
+    noise = (rng.standard_normal(shape) + 1j * rng.standard_normal(shape)) * math.sqrt(0.5)
+    uni = rng.random((nsweeps, nchains))
+    return np.stack(dis), np.stack(D0), noise, uni
+
+
+def cpu_baseline(O, p, Delta0, disorder, steps):
+    """Oracle (numpy/scipy zheevr restatement) leapfrog steps on the host."""
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max([i.get("num_threads", 1) for i in threadpool_info()
+                       if i.get("internal_api") in ("openblas", "mkl", "blis")] or [1])
+    except Exception:
+        threads = os.cpu_count() or 1
+    cache = O.initialize_cache(p)
+    O.init_static_H(cache, p, disorder)
+    Delta = Delta0.copy()
+    pi = np.zeros_like(Delta)
+    O.update_H_BdG(cache, p, Delta)
+    O.diagonalize_H_BdG(cache, p)
+    O.compute_forces(cache, p, Delta)
+    dt = O.calc_optimal_dt(p.beta, p.J, p.mass, 10)
+    t0 = time.perf_counter()
+    for _ in range(steps):                          # src/HMC.jl:101-113
+        Delta += dt / (2 * p.mass) * pi
+        O.update_H_BdG(cache, p, Delta)
+        O.diagonalize_H_BdG(cache, p)
+        O.compute_forces(cache, p, Delta)
+        pi += dt * cache.forces
+    el = time.perf_counter() - t0
+    return steps / el, threads, el
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.steps % a.Nt or a.warmup % a.Nt:
+        raise SystemExit("--steps and --warmup must be multiples of --Nt")
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import dwhmc_loader
+    from oracle import dwhmc_oracle as O   # synthetic-input generation + CPU leg only
+    m = dwhmc_loader.load_package()
+    m.load_library(build_if_missing=False)
+
+    p = O.ModelParameters(a.L, a.L, 1.0, -0.35, -1.08, 1.0, 0.05, a.beta, 0.8, 1.0)
+    n_warm, n_time = a.warmup // a.Nt, a.steps // a.Nt
+    dis, D0, noise, uni = synthetic(p, O, rank, a.chains, a.Nt, n_warm + n_time)
+    dt = m.calc_optimal_dt(p.beta, p.J, p.mass, a.Nt)
+    ctx = m.FermionContext(p.Lx, p.Ly, p.t, p.tp, p.mu, p.beta, p.J, p.nn_table, p.nnn_table, dis,
+                           device=local)
+    ctx.set_pairing(D0)
+    ctx.factorize()                                 # src/Simulation.jl:84-86
+    ctx.load_draws(noise, uni)                      # inputs resident in HBM before timing
+    if n_warm:
+        ctx.run_sweeps(0, n_warm, a.Nt, dt, p.mass)
+    ctx.synchronize()
+    if not a.no_timing:
+        ctx.timing_enable(True)
+        ctx.timing_reset()
+
+    if dist is not None:
+        dist.barrier()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    ctx.run_sweeps(n_warm, n_time, a.Nt, dt, p.mass)
+    ctx.synchronize()
+    el = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([el], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+        dist.barrier()
+
+    acc, dH = ctx.sweep_results(n_warm, n_time)
+    info = ctx.info
+    kern = {}
+    if not a.no_timing:
+        for name in ("gj_update", "gj_panel", "gj_diag", "assemble", "contract", "step"):
+            ms, n, w = ctx.timing_read(name)
+            kern[name] = (ms, n, w)
+        ctx.timing_enable(False)
+    # observables gather over RCCL (the only collective): acceptance and <dH>
+    obs = np.array([acc.mean(), dH.mean(), float(np.mean(np.exp(-dH)))], dtype=np.float64)
+    if dist is not None:
+        import torch
+        t = torch.tensor(obs, device=f"cuda:{local}")
+        gl = [torch.zeros_like(t) for _ in range(world)] if rank == 0 else None
+        dist.gather(t, gl, dst=0)
+        if rank == 0:
+            obs = torch.stack(gl).mean(0).cpu().numpy()
+
+    if rank == 0:
+        leap = a.steps * a.chains * world
+        value = leap / el
+        ms_per_step = 1000.0 * el / a.steps
+        N, P = info["N"], info["npoles"]
+        rec = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "leapfrog steps/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {"workload": f"L={a.L} beta={a.beta:g} single-chain HMC (BASELINE configs[2], C3)"
+                       if a.chains == 1 else f"L={a.L} beta={a.beta:g} {a.chains} chains/GPU",
+                       "L": a.L, "N": N, "bdg_dim": 2 * N, "beta": a.beta, "chains_per_gpu": a.chains,
+                       "Nt": a.Nt, "dt": dt, "poles": P, "kappa": info["kappa"],
+                       "parallelism": f"replicas x{world}" if world > 1 else "single GPU"},
+            "acceptance": float(obs[0]), "mean_dH": float(obs[1]), "mean_exp_minus_dH": float(obs[2]),
+            "ref_equiv_tflops": leap * (40.0 / 3.0) * (2 * N) ** 3 / el / 1e12,
+            "alg_tflops": leap * P * 8.0 * N ** 3 / el / 1e12,
+        }
+        if kern:
+            ms, n, w = kern["gj_update"]
+            ach = w / n / (ms / n * 1e-3) / 1e12 if n and ms > 0 else None
+            rec["roofline"] = {"bound": "mfma", "kernel": "k_gj_update", "achieved": ach,
+                               "peak": PEAK_F64_TFLOPS, "unit": "TFLOP/s",
+                               "frac": ach / PEAK_F64_TFLOPS if ach else None, "traffic": None,
+                               "avg_launch_us": 1000.0 * ms / n if n else None,
+                               "flops_per_launch": w / n if n else None}
+            rec["kernels_ms_per_step"] = {k: v[0] / a.steps for k, v in kern.items()}
+            rec["kernels_tflops"] = {k: (v[2] / (v[0] * 1e-3) / 1e12 if v[0] > 0 else None)
+                                     for k, v in kern.items() if k.startswith("gj") or k == "step"}
+        if not a.no_cpu_baseline and world == 1:
+            steps_cpu = a.cpu_steps or (3 if a.L >= 32 else 20)
+            v, threads, el_cpu = cpu_baseline(O, p, D0[0], dis[0], steps_cpu)
+            rec["cpu_baseline"] = {"value": v, "unit": "leapfrog steps/s", "cores": threads,
+                                   "kind": "port",
+                                   "sample": f"{steps_cpu} leapfrog steps at L={a.L}, beta={a.beta:g} "
+                                             f"(numpy/scipy zheevr restatement, {el_cpu:.1f} s)"}
+        print(json.dumps(rec), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

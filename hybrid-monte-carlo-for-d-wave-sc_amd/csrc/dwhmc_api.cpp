@@ -354,8 +354,10 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
   for (int dir = 0; dir < 2; ++dir)
     for (int i = 0; i < N; ++i) {
       const int j = NN(i, dir);
-      bij[(size_t)dir * N + i] = i * kSlots + slot_of(i, j);
-      bji[(size_t)dir * N + i] = j * kSlots + slot_of(j, i);
+      const int sij = slot_of(i, j), sji = slot_of(j, i);
+      if (sij < 0 || sji < 0) return fail(nullptr, DWH_ERR_ARG, "bond missing from the pairing pattern");
+      bij[(size_t)dir * N + i] = i * kSlots + sij;
+      bji[(size_t)dir * N + i] = j * kSlots + sji;
     }
 
   // --- pole selection: E' >= Gershgorin bound of H_BdG with |Δ| <= delta_cap
