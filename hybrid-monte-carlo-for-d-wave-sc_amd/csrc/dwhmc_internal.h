@@ -28,7 +28,10 @@ void launch_gj_diag(const Dims& d, double2* M, int k, double2* Pinv, double* ldp
                     hipStream_t s);
 void launch_gj_panel(const Dims& d, double2* M, int k, const double2* Pinv, double2* Cpanel,
                      hipStream_t s);
-void launch_gj_update(const Dims& d, double2* M, int k, const double2* Cpanel, hipStream_t s);
+// mode 0: all tiles I != k; 1: block row/col k+1 (lookahead edge); 2: the rest
+int gj_update_tiles(const Dims& d, int mode);
+void launch_gj_update(const Dims& d, double2* M, int k, int mode, const double2* Cpanel,
+                      hipStream_t s);
 // T = R D and S^T = -(h + i y) - (D† R D)^T for every (chain, pole)
 void launch_assemble(const Dims& d, const double2* R, double2* T, double2* S, const int* Dcol,
                      const int* Dsrc, const double2* Delta, const int* hcol, const double* hval,

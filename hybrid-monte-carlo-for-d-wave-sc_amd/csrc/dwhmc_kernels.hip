@@ -73,58 +73,64 @@ __global__ __launch_bounds__(256) void k_fill_hz(double2* __restrict__ M, int64_
 }
 
 // ---------------------------------------------------------------------------
-// Gauss-Jordan, diagonal block: 64x64 complex in registers (16 per thread),
+// Gauss-Jordan, diagonal block: 64x64 complex in registers of 1024 threads
+// (row i = tid/16, 4 columns each; 4 waves per SIMD hide the LDS/rcp latency),
 // row/column p exchanged through double-buffered LDS — one barrier per pivot.
+// ln|pivot| is summed after the loop from the stored |pivot|².
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_gj_diag(double2* __restrict__ M, int64_t mat, int Np,
-                                                 int k, int nb, double2* __restrict__ Pinv,
-                                                 double* __restrict__ ldpart) {
+__global__ __launch_bounds__(1024) void k_gj_diag(double2* __restrict__ M, int64_t mat, int Np,
+                                                  int k, int nb, double2* __restrict__ Pinv,
+                                                  double* __restrict__ ldpart) {
   const int bi = blockIdx.x;
   const int tid = threadIdx.x;
-  const int i = tid >> 2;       // row of this thread
-  const int seg = tid & 3;      // 16-column segment
+  const int i = tid >> 4;       // row of this thread
+  const int seg = tid & 15;     // 4-column segment
   const double2* A = M + (int64_t)bi * mat + (int64_t)(k * kGJ) * Np + k * kGJ;
-  double2 a[16];
+  double2 a[4];
 #pragma unroll
-  for (int jj = 0; jj < 16; ++jj) a[jj] = A[(int64_t)i * Np + seg * 16 + jj];
+  for (int jj = 0; jj < 4; ++jj) a[jj] = A[(int64_t)i * Np + seg * 4 + jj];
   __shared__ double2 rowbuf[2][kGJ];
   __shared__ double2 colbuf[2][kGJ];
-  double ld = 0.0;
+  __shared__ double pmag[kGJ];
 #pragma unroll 1
-  for (int pb = 0; pb < 4; ++pb) {
+  for (int pb = 0; pb < 16; ++pb) {
 #pragma unroll
-    for (int pp = 0; pp < 16; ++pp) {
-      const int p = pb * 16 + pp;
+    for (int pp = 0; pp < 4; ++pp) {
+      const int p = pb * 4 + pp;
       const int par = pp & 1;
       if (i == p) {
 #pragma unroll
-        for (int jj = 0; jj < 16; ++jj) rowbuf[par][seg * 16 + jj] = a[jj];
+        for (int jj = 0; jj < 4; ++jj) rowbuf[par][seg * 4 + jj] = a[jj];
       }
       if (seg == pb) colbuf[par][i] = a[pp];
       __syncthreads();
       const double2 piv = rowbuf[par][p];
       const double2 inv = cinv(piv);
-      if (tid == 0) ld += 0.5 * log(piv.x * piv.x + piv.y * piv.y);
+      if (tid == 0) pmag[p] = piv.x * piv.x + piv.y * piv.y;
       if (i == p) {
 #pragma unroll
-        for (int jj = 0; jj < 16; ++jj) {
+        for (int jj = 0; jj < 4; ++jj) {
           if (seg == pb && jj == pp) a[jj] = inv;
-          else a[jj] = cmul(rowbuf[par][seg * 16 + jj], inv);
+          else a[jj] = cmul(rowbuf[par][seg * 4 + jj], inv);
         }
       } else {
         const double2 fi = cmul(colbuf[par][i], inv);
 #pragma unroll
-        for (int jj = 0; jj < 16; ++jj) {
+        for (int jj = 0; jj < 4; ++jj) {
           if (seg == pb && jj == pp) a[jj] = make_double2(-fi.x, -fi.y);
-          else a[jj] = csub(a[jj], cmul(fi, rowbuf[par][seg * 16 + jj]));
+          else a[jj] = csub(a[jj], cmul(fi, rowbuf[par][seg * 4 + jj]));
         }
       }
     }
   }
   double2* Pout = Pinv + (int64_t)bi * kGJ * kGJ;
 #pragma unroll
-  for (int jj = 0; jj < 16; ++jj) Pout[i * kGJ + seg * 16 + jj] = a[jj];
-  if (tid == 0) ldpart[(int64_t)bi * nb + k] = ld;
+  for (int jj = 0; jj < 4; ++jj) Pout[i * kGJ + seg * 4 + jj] = a[jj];
+  __syncthreads();
+  if (tid < 64) {
+    const double v = wave_sum(0.5 * log(pmag[tid]));
+    if (tid == 0) ldpart[(int64_t)bi * nb + k] = v;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -250,15 +256,34 @@ __global__ __launch_bounds__(256) void k_gj_panel(double2* __restrict__ M, int64
 }
 
 // Trailing update: S_IJ = [J != k] S_IJ - Cpanel_I X_kJ for I != k (X_kk = P).
+// mode 0: every tile I != k; mode 1 ("edge", lookahead): the tiles of block
+// row k+1 and block column k+1; mode 2 ("rest"): all other tiles.
 __global__ __launch_bounds__(256) void k_gj_update(double2* __restrict__ M, int64_t mat, int Np,
-                                                   int nb, int k,
+                                                   int nb, int k, int mode,
                                                    const double2* __restrict__ Cpanel) {
   __shared__ double2 At[16][kGJ];
   __shared__ double2 Bs[16][kGJ];
   const int bi = blockIdx.y;
   const int t = blockIdx.x;
-  const int Ii = t / nb, J = t - Ii * nb;
-  const int I = Ii < k ? Ii : Ii + 1;
+  int I, J;
+  if (mode == 0) {
+    const int Ii = t / nb;
+    J = t - Ii * nb;
+    I = Ii < k ? Ii : Ii + 1;
+  } else if (mode == 1) {
+    if (t < nb) {
+      I = k + 1;
+      J = t;
+    } else {
+      const int u = t - nb;
+      I = u < k ? u : u + 2;
+      J = k + 1;
+    }
+  } else {
+    const int Ii = t / (nb - 1), Jj = t - Ii * (nb - 1);
+    I = Ii < k ? Ii : Ii + 2;
+    J = Jj < k + 1 ? Jj : Jj + 1;
+  }
   double2* Mb = M + (int64_t)bi * mat;
   const double2* Ci = Cpanel + (int64_t)bi * Np * kGJ + (int64_t)I * kGJ * kGJ;
   tile_cgemm<true, true>(Ci, kGJ, Mb + (int64_t)(k * kGJ) * Np + J * kGJ, Np,
@@ -596,7 +621,7 @@ void launch_fill_hz(const Dims& d, double2* M, const int* hcol, const double* hv
 }
 void launch_gj_diag(const Dims& d, double2* M, int k, double2* Pinv, double* ldpart,
                     hipStream_t s) {
-  hipLaunchKernelGGL(k_gj_diag, dim3(d.nbatch), dim3(256), 0, s, M, d.mat, d.Np, k, d.nb, Pinv,
+  hipLaunchKernelGGL(k_gj_diag, dim3(d.nbatch), dim3(1024), 0, s, M, d.mat, d.Np, k, d.nb, Pinv,
                      ldpart);
 }
 void launch_gj_panel(const Dims& d, double2* M, int k, const double2* Pinv, double2* Cpanel,
@@ -604,10 +629,18 @@ void launch_gj_panel(const Dims& d, double2* M, int k, const double2* Pinv, doub
   hipLaunchKernelGGL(k_gj_panel, dim3(2 * d.nb, d.nbatch), dim3(256), 0, s, M, d.mat, d.Np, d.nb,
                      k, Pinv, Cpanel);
 }
-void launch_gj_update(const Dims& d, double2* M, int k, const double2* Cpanel, hipStream_t s) {
-  if (d.nb < 2) return;
-  hipLaunchKernelGGL(k_gj_update, dim3((d.nb - 1) * d.nb, d.nbatch), dim3(256), 0, s, M, d.mat,
-                     d.Np, d.nb, k, Cpanel);
+int gj_update_tiles(const Dims& d, int mode) {
+  if (d.nb < 2) return 0;
+  if (mode == 0) return (d.nb - 1) * d.nb;
+  if (mode == 1) return 2 * d.nb - 2;
+  return (d.nb - 2) * (d.nb - 1);
+}
+void launch_gj_update(const Dims& d, double2* M, int k, int mode, const double2* Cpanel,
+                      hipStream_t s) {
+  const int tiles = gj_update_tiles(d, mode);
+  if (tiles <= 0) return;
+  hipLaunchKernelGGL(k_gj_update, dim3(tiles, d.nbatch), dim3(256), 0, s, M, d.mat, d.Np, d.nb, k,
+                     mode, Cpanel);
 }
 void launch_assemble(const Dims& d, const double2* R, double2* T, double2* S, const int* Dcol,
                      const int* Dsrc, const double2* Delta, const int* hcol, const double* hval,

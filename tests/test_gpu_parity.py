@@ -217,3 +217,24 @@ def test_host_mirror_api_roundtrip(dwhmc, oracle):
     acc, dH = m.hmc_sweep(cache, p, st, Nt=4, dt=m.calc_optimal_dt(p.beta, p.J, p.mass, 4),
                           rng=np.random.default_rng(0))
     assert np.isfinite(dH)
+
+
+@pytest.mark.parametrize("L", [4, 8])
+def test_golden_fixture_on_device(dwhmc, L):
+    """Committed oracle vectors (tests/golden/oracle_L*.npz, tools/make_golden.py)."""
+    import os
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", f"oracle_L{L}.npz"), allow_pickle=False)
+    beta = float(g["beta"])
+    ctx = dwhmc.FermionContext(L, L, T, TP, MU, beta, J, g["nn"], g["nnn"], g["disorder"])
+    ctx.set_pairing(g["Delta"])
+    ctx.factorize()
+    F = ctx.forces()[0]
+    assert np.max(np.abs(F - g["F"])) <= 1e-10 * (1 + np.max(np.abs(g["F"])))
+    assert abs(ctx.fermion_energy()[0] - float(g["Ef"])) <= 1e-11 * abs(float(g["Ef"]))
+    acc, dH = ctx.hmc_sweep(g["sweep_noise"], np.array([float(g["sweep_uniform"])]), int(g["sweep_Nt"]),
+                            float(g["sweep_dt"]), 1.0)
+    assert abs(dH[0] - float(g["sweep_dH"])) <= 1e-8 * (1 + abs(float(g["sweep_dH"])))
+    assert bool(acc[0]) == bool(g["sweep_accepted"])
+    D, pi = ctx.get_state()
+    assert np.max(np.abs(D[0] - g["sweep_Delta"])) <= 1e-10
+    ctx.close()

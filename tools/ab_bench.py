@@ -1,0 +1,82 @@
+#!/usr/bin/env python3
+"""Interleaved in-process A/B of context variants (env knobs read at create):
+python tools/ab_bench.py --L 32 --beta 16 --variants "LA=0" "LA=1,SC=0" "LA=1,SC=32"
+LA -> DWHMC_LOOKAHEAD, SC -> DWHMC_SIDE_CUS.  Prints ms per leapfrog step
+(median / min over rounds) and the per-kernel event totals of the last round."""
+import argparse
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--L", type=int, default=32)
+    ap.add_argument("--beta", type=float, default=16.0)
+    ap.add_argument("--chains", type=int, default=1)
+    ap.add_argument("--Nt", type=int, default=10)
+    ap.add_argument("--sweeps", type=int, default=3)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--variants", nargs="+", default=["LA=1"])
+    a = ap.parse_args()
+    import dwhmc_loader
+    from oracle import dwhmc_oracle as O
+    m = dwhmc_loader.load_package()
+    p = O.ModelParameters(a.L, a.L, 1.0, -0.35, -1.08, 1.0, 0.05, a.beta, 0.8, 1.0)
+    dis, D0 = [], []
+    for c in range(a.chains):
+        st = O.initialize_state(p, np.random.default_rng(1000 + c))
+        dis.append(st.disorder_pot)
+        D0.append(st.Delta)
+    rng = np.random.default_rng(7)
+    shape = (a.sweeps, a.chains, p.N, 2)
+    noise = (rng.standard_normal(shape) + 1j * rng.standard_normal(shape)) * math.sqrt(0.5)
+    uni = rng.random((a.sweeps, a.chains))
+    dt = m.calc_optimal_dt(p.beta, p.J, p.mass, a.Nt)
+    ctxs = {}
+    for v in a.variants:
+        kv = dict(x.split("=") for x in v.split(",") if x)
+        os.environ["DWHMC_LOOKAHEAD"] = kv.get("LA", "1")
+        os.environ["DWHMC_SIDE_CUS"] = kv.get("SC", "32")
+        ctx = m.FermionContext(p.Lx, p.Ly, p.t, p.tp, p.mu, p.beta, p.J, p.nn_table, p.nnn_table,
+                               np.stack(dis))
+        ctx.set_pairing(np.stack(D0))
+        ctx.factorize()
+        ctx.load_draws(noise, uni)
+        ctxs[v] = ctx
+    res = {v: [] for v in a.variants}
+    for r in range(a.rounds + 1):
+        for v, ctx in ctxs.items():
+            ctx.set_pairing(np.stack(D0))
+            ctx.factorize()
+            ctx.synchronize()
+            t0 = time.perf_counter()
+            ctx.run_sweeps(0, a.sweeps, a.Nt, dt, p.mass)
+            ctx.synchronize()
+            el = time.perf_counter() - t0
+            if r > 0:
+                res[v].append(1000 * el / (a.sweeps * a.Nt))
+    print(f"L={a.L} beta={a.beta} chains={a.chains} poles={next(iter(ctxs.values())).info['npoles']}")
+    for v, ctx in ctxs.items():
+        ctx.timing_enable(True)
+        ctx.timing_reset()
+        ctx.run_sweeps(0, 1, a.Nt, dt, p.mass)
+        ctx.synchronize()
+        kt = {k: ctx.timing_read(k) for k in ("gj_update", "gj_panel", "gj_diag", "assemble", "contract", "step")}
+        ctx.timing_enable(False)
+        x = np.array(res[v])
+        upd = kt["gj_update"]
+        print(f"{v:24s} ms/step median {np.median(x):.3f} min {x.min():.3f}  steps/s {1000*a.chains/np.median(x):.1f}  "
+              f"gj_update {upd[2]/upd[0]/1e9:.1f} TF  " +
+              " ".join(f"{k}={val[0]/a.Nt:.3f}ms/{val[1]//a.Nt}" for k, val in kt.items()), flush=True)
+        ctx.close()
+
+
+if __name__ == "__main__":
+    main()
