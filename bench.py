@@ -146,7 +146,7 @@ def main():
     info = ctx.info
     kern = {}
     if not a.no_timing:
-        for name in ("gj_update", "gj_panel", "gj_diag", "assemble", "contract", "step"):
+        for name in ("gj_update", "gj_pivot", "assemble", "contract", "step"):
             ms, n, w = ctx.timing_read(name)
             kern[name] = (ms, n, w)
         ctx.timing_enable(False)

@@ -34,8 +34,8 @@ namespace {
 
 thread_local std::string g_create_error;
 
-enum TimerName { T_GJ_UPDATE = 0, T_GJ_PANEL, T_GJ_DIAG, T_ASSEMBLE, T_CONTRACT, T_STEP, T_COUNT };
-const char* kTimerNames[T_COUNT] = {"gj_update", "gj_panel", "gj_diag", "assemble", "contract", "step"};
+enum TimerName { T_GJ_UPDATE = 0, T_GJ_PIVOT, T_ASSEMBLE, T_CONTRACT, T_STEP, T_COUNT };
+const char* kTimerNames[T_COUNT] = {"gj_update", "gj_pivot", "assemble", "contract", "step"};
 
 struct TimingRec {
   int name;
@@ -53,11 +53,7 @@ struct DevBuf {
 
 struct dwh_ctx {
   int device = 0;
-  hipStream_t stream = nullptr;   // main stream: every launch except the lookahead
-  hipStream_t side = nullptr;     // high-priority stream: GJ diag+panel of step k+1
-  hipEvent_t ev_edge = nullptr, ev_panel = nullptr;
-  bool lookahead = true;
-  int side_cus = 0, total_cus = 0;
+  hipStream_t stream = nullptr;
   Dims d{};
   int64_t Lx = 0, Ly = 0;
   double t = 0, tp = 0, mu = 0, beta = 0, J = 0, delta_cap = 2.0;
@@ -144,8 +140,7 @@ struct Scope {
   double work;
   hipStream_t st;
   hipEvent_t a{};
-  Scope(dwh_ctx* c, int n, double w, hipStream_t s = nullptr)
-      : ctx(c), name(n), work(w), st(s ? s : c->stream) {
+  Scope(dwh_ctx* c, int n, double w) : ctx(c), name(n), work(w), st(c->stream) {
     if (ctx->timing) {
       a = take_event(ctx);
       (void)hipEventRecord(a, st);
@@ -163,7 +158,6 @@ struct Scope {
 void drain_timing(dwh_ctx* ctx) {
   if (ctx->recs.empty()) return;
   (void)hipStreamSynchronize(ctx->stream);
-  (void)hipStreamSynchronize(ctx->side);
   for (auto& r : ctx->recs) {
     float ms = 0.f;
     (void)hipEventElapsedTime(&ms, r.a, r.b);
@@ -178,52 +172,19 @@ void drain_timing(dwh_ctx* ctx) {
 
 double tile_flops() { return 8.0 * kGJ * kGJ * kGJ; }
 
-double2* pinv_buf(dwh_ctx* ctx, int k) { return ctx->Pinv + (size_t)(k & 1) * ctx->d.nbatch * kGJ * kGJ; }
-double2* cpanel_buf(dwh_ctx* ctx, int k) {
-  return ctx->Cpanel + (size_t)(k & 1) * ctx->d.nbatch * ctx->d.Np * kGJ;
-}
-
-void gj_diag_panel(dwh_ctx* ctx, double2* M, int k, hipStream_t st) {
-  const Dims& d = ctx->d;
-  {
-    Scope s(ctx, T_GJ_DIAG, d.nbatch * tile_flops(), st);
-    dwh::launch_gj_diag(d, M, k, pinv_buf(ctx, k), ctx->ldpart, st);
-  }
-  Scope s(ctx, T_GJ_PANEL, (double)d.nbatch * (d.nb - 1) * tile_flops(), st);
-  dwh::launch_gj_panel(d, M, k, pinv_buf(ctx, k), cpanel_buf(ctx, k), st);
-}
-
-void gj_update(dwh_ctx* ctx, double2* M, int k, int mode) {
-  const Dims& d = ctx->d;
-  Scope s(ctx, T_GJ_UPDATE, (double)d.nbatch * dwh::gj_update_tiles(d, mode) * tile_flops());
-  dwh::launch_gj_update(d, M, k, mode, cpanel_buf(ctx, k), ctx->stream);
-}
-
-// Blocked no-pivot Gauss-Jordan inversion of all nbatch matrices in M, with
-// one-step lookahead: after the edge tiles (block row/col k+1) of update k,
-// diag+panel of step k+1 run on the side stream while the rest of update k
-// runs on the main stream.  Pinv/Cpanel are double-buffered by k parity.
+// Blocked no-pivot Gauss-Jordan inversion of all nbatch matrices in M:
+// per block step a pivot launch (S_kk^-1, row panel, column copy) and a
+// trailing-update launch.
 void run_gj(dwh_ctx* ctx, double2* M) {
   const Dims& d = ctx->d;
-  if (!ctx->lookahead) {
-    for (int k = 0; k < d.nb; ++k) {
-      gj_diag_panel(ctx, M, k, ctx->stream);
-      gj_update(ctx, M, k, 0);
-    }
-    return;
-  }
-  gj_diag_panel(ctx, M, 0, ctx->stream);
   for (int k = 0; k < d.nb; ++k) {
-    if (k + 1 < d.nb) {
-      gj_update(ctx, M, k, 1);
-      (void)hipEventRecord(ctx->ev_edge, ctx->stream);
-      (void)hipStreamWaitEvent(ctx->side, ctx->ev_edge, 0);
-      gj_diag_panel(ctx, M, k + 1, ctx->side);
-      (void)hipEventRecord(ctx->ev_panel, ctx->side);
-      gj_update(ctx, M, k, 2);
-      (void)hipStreamWaitEvent(ctx->stream, ctx->ev_panel, 0);
-    } else {
-      gj_update(ctx, M, k, 0);
+    {
+      Scope s(ctx, T_GJ_PIVOT, (double)d.nbatch * d.nb * tile_flops());
+      dwh::launch_gj_pivot(d, M, k, ctx->Pinv, ctx->Cpanel, ctx->ldpart, ctx->stream);
+    }
+    if (d.nb > 1) {
+      Scope s(ctx, T_GJ_UPDATE, (double)d.nbatch * dwh::gj_update_tiles(d) * tile_flops());
+      dwh::launch_gj_update(d, M, k, ctx->Cpanel, ctx->Pinv, ctx->stream);
     }
   }
 }
@@ -460,44 +421,8 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     ctx->err = "hipSetDevice failed";
     return bail(DWH_ERR_HIP);
   }
-  // Streams.  With lookahead the GJ diag+panel of step k+1 run on `side`
-  // while the trailing update of step k runs on `stream`; the two streams get
-  // disjoint CU masks (the update's blocks would otherwise occupy every SIMD
-  // and starve the 1024-thread diag block).  DWHMC_LOOKAHEAD=0 disables it,
-  // DWHMC_SIDE_CUS sets the CUs reserved for the side stream.
-  hipDeviceProp_t prop;
-  if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
-    ctx->err = "hipGetDeviceProperties failed";
-    return bail(DWH_ERR_HIP);
-  }
-  ctx->total_cus = prop.multiProcessorCount;
-  const char* la = std::getenv("DWHMC_LOOKAHEAD");
-  ctx->lookahead = !(la && la[0] == '0');
-  const char* sc = std::getenv("DWHMC_SIDE_CUS");
-  ctx->side_cus = sc ? std::atoi(sc) : 32;
-  if (!ctx->lookahead || d.nb < 3) ctx->side_cus = 0;
-  if (ctx->side_cus < 0 || ctx->side_cus >= ctx->total_cus / 2) ctx->side_cus = 0;
-  hipError_t e1, e2;
-  if (ctx->side_cus > 0) {
-    const int nw = (ctx->total_cus + 31) / 32;
-    std::vector<uint32_t> mmain(nw, 0), mside(nw, 0);
-    const int stride = ctx->total_cus / ctx->side_cus;
-    for (int cu = 0; cu < ctx->total_cus; ++cu) {
-      const bool side = (cu % stride == 0) && (cu / stride < ctx->side_cus);
-      (side ? mside : mmain)[cu / 32] |= 1u << (cu % 32);
-    }
-    e1 = hipExtStreamCreateWithCUMask(&ctx->stream, nw, mmain.data());
-    e2 = hipExtStreamCreateWithCUMask(&ctx->side, nw, mside.data());
-  } else {
-    int prio_lo = 0, prio_hi = 0;
-    (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-    e1 = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
-    e2 = hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, prio_hi);
-  }
-  if (e1 != hipSuccess || e2 != hipSuccess ||
-      hipEventCreateWithFlags(&ctx->ev_edge, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&ctx->ev_panel, hipEventDisableTiming) != hipSuccess) {
-    ctx->err = "hipStream/hipEvent create failed";
+  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+    ctx->err = "hipStreamCreate failed";
     return bail(DWH_ERR_HIP);
   }
   const size_t nmat = (size_t)d.nbatch * d.mat;
@@ -508,8 +433,8 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
   ALLOC(R, nmat);
   ALLOC(T, nmat);
   ALLOC(S, nmat);
-  ALLOC(Cpanel, 2 * (size_t)d.nbatch * d.Np * kGJ);
-  ALLOC(Pinv, 2 * (size_t)d.nbatch * kGJ * kGJ);
+  ALLOC(Cpanel, (size_t)d.nbatch * d.Np * kGJ);
+  ALLOC(Pinv, (size_t)d.nbatch * kGJ * kGJ);
   ALLOC(G12nn, (size_t)d.nbatch * N * kSlots);
   ALLOC(diagS, (size_t)d.nbatch * N);
   ALLOC(ldpart, (size_t)d.nbatch * d.nb);
@@ -604,11 +529,7 @@ void dwh_destroy(dwh_ctx* ctx) {
     (void)hipEventDestroy(r.b);
   }
   for (auto e : ctx->pool) (void)hipEventDestroy(e);
-  if (ctx->side) (void)hipStreamSynchronize(ctx->side);
   for (void* p : ctx->allocations) (void)hipFree(p);
-  if (ctx->ev_edge) (void)hipEventDestroy(ctx->ev_edge);
-  if (ctx->ev_panel) (void)hipEventDestroy(ctx->ev_panel);
-  if (ctx->side) (void)hipStreamDestroy(ctx->side);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }

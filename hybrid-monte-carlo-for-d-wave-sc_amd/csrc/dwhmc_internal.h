@@ -23,14 +23,12 @@ struct Dims {
 // dense h - i y_q (padded with identity) for every (chain, pole): R init input
 void launch_fill_hz(const Dims& d, double2* M, const int* hcol, const double* hval,
                     const double* ypole, hipStream_t s);
-// one Gauss-Jordan block step k on all nbatch matrices in M (in place, no pivoting)
-void launch_gj_diag(const Dims& d, double2* M, int k, double2* Pinv, double* ldpart,
-                    hipStream_t s);
-void launch_gj_panel(const Dims& d, double2* M, int k, const double2* Pinv, double2* Cpanel,
-                     hipStream_t s);
-// mode 0: all tiles I != k; 1: block row/col k+1 (lookahead edge); 2: the rest
-int gj_update_tiles(const Dims& d, int mode);
-void launch_gj_update(const Dims& d, double2* M, int k, int mode, const double2* Cpanel,
+// Gauss-Jordan block step k on all nbatch matrices in M (in place, no pivoting):
+// pivot (invert S_kk in every block, row panel, column copy), then update.
+void launch_gj_pivot(const Dims& d, double2* M, int k, double2* Pbuf, double2* Cpanel,
+                     double* ldpart, hipStream_t s);
+int gj_update_tiles(const Dims& d);
+void launch_gj_update(const Dims& d, double2* M, int k, const double2* Cpanel, const double2* Pbuf,
                       hipStream_t s);
 // T = R D and S^T = -(h + i y) - (D† R D)^T for every (chain, pole)
 void launch_assemble(const Dims& d, const double2* R, double2* T, double2* S, const int* Dcol,

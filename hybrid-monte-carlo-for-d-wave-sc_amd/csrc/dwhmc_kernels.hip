@@ -73,67 +73,6 @@ __global__ __launch_bounds__(256) void k_fill_hz(double2* __restrict__ M, int64_
 }
 
 // ---------------------------------------------------------------------------
-// Gauss-Jordan, diagonal block: 64x64 complex in registers of 1024 threads
-// (row i = tid/16, 4 columns each; 4 waves per SIMD hide the LDS/rcp latency),
-// row/column p exchanged through double-buffered LDS — one barrier per pivot.
-// ln|pivot| is summed after the loop from the stored |pivot|².
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void k_gj_diag(double2* __restrict__ M, int64_t mat, int Np,
-                                                  int k, int nb, double2* __restrict__ Pinv,
-                                                  double* __restrict__ ldpart) {
-  const int bi = blockIdx.x;
-  const int tid = threadIdx.x;
-  const int i = tid >> 4;       // row of this thread
-  const int seg = tid & 15;     // 4-column segment
-  const double2* A = M + (int64_t)bi * mat + (int64_t)(k * kGJ) * Np + k * kGJ;
-  double2 a[4];
-#pragma unroll
-  for (int jj = 0; jj < 4; ++jj) a[jj] = A[(int64_t)i * Np + seg * 4 + jj];
-  __shared__ double2 rowbuf[2][kGJ];
-  __shared__ double2 colbuf[2][kGJ];
-  __shared__ double pmag[kGJ];
-#pragma unroll 1
-  for (int pb = 0; pb < 16; ++pb) {
-#pragma unroll
-    for (int pp = 0; pp < 4; ++pp) {
-      const int p = pb * 4 + pp;
-      const int par = pp & 1;
-      if (i == p) {
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) rowbuf[par][seg * 4 + jj] = a[jj];
-      }
-      if (seg == pb) colbuf[par][i] = a[pp];
-      __syncthreads();
-      const double2 piv = rowbuf[par][p];
-      const double2 inv = cinv(piv);
-      if (tid == 0) pmag[p] = piv.x * piv.x + piv.y * piv.y;
-      if (i == p) {
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          if (seg == pb && jj == pp) a[jj] = inv;
-          else a[jj] = cmul(rowbuf[par][seg * 4 + jj], inv);
-        }
-      } else {
-        const double2 fi = cmul(colbuf[par][i], inv);
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          if (seg == pb && jj == pp) a[jj] = make_double2(-fi.x, -fi.y);
-          else a[jj] = csub(a[jj], cmul(fi, rowbuf[par][seg * 4 + jj]));
-        }
-      }
-    }
-  }
-  double2* Pout = Pinv + (int64_t)bi * kGJ * kGJ;
-#pragma unroll
-  for (int jj = 0; jj < 4; ++jj) Pout[i * kGJ + seg * 4 + jj] = a[jj];
-  __syncthreads();
-  if (tid < 64) {
-    const double v = wave_sum(0.5 * log(pmag[tid]));
-    if (tid == 0) ldpart[(int64_t)bi * nb + k] = v;
-  }
-}
-
-// ---------------------------------------------------------------------------
 // 64x64x64 complex tile GEMM on f64 MFMA.
 //   C = A·B            (NEG = false, LOADC = false)
 //   C = C0 - A·B       (NEG = true,  LOADC = true; C0 = 0 when zeroC)
@@ -227,67 +166,216 @@ __device__ __forceinline__ void tile_cgemm(const double2* __restrict__ A, int ld
             make_double2(acr[mi][ni][r], aci[mi][ni][r]);
 }
 
-// Row panel X_kj = P S_kj (j != k), S_kk = P; column panel copy S_ik -> Cpanel (i != k).
-__global__ __launch_bounds__(256) void k_gj_panel(double2* __restrict__ M, int64_t mat, int Np,
-                                                  int nb, int k, const double2* __restrict__ Pinv,
-                                                  double2* __restrict__ Cpanel) {
-  __shared__ double2 At[16][kGJ];
-  __shared__ double2 Bs[16][kGJ];
-  const int bi = blockIdx.y, x = blockIdx.x;
-  double2* Mb = M + (int64_t)bi * mat;
-  const double2* Pb = Pinv + (int64_t)bi * kGJ * kGJ;
-  if (x < nb) {
-    const int j = x;
-    double2* Skj = Mb + (int64_t)(k * kGJ) * Np + j * kGJ;
-    if (j == k) {
-      for (int e = threadIdx.x; e < kGJ * kGJ; e += blockDim.x)
-        Skj[(int64_t)(e >> 6) * Np + (e & 63)] = Pb[e];
-    } else {
-      tile_cgemm<false, false>(Pb, kGJ, Skj, Np, Skj, Np, false, At, Bs);
+// ---------------------------------------------------------------------------
+// Pivot step k of the blocked Gauss-Jordan (one launch per step, grid nb x nbatch):
+// every block inverts the 64x64 pivot block S_kk in LDS (4 sub-steps of 16:
+// a wave-local 16x16 inversion through lane shuffles, then MFMA rank-16
+// updates), then block j != k forms its row-panel tile X_kj = S_kk^-1 S_kj in
+// place and copies the column-panel tile S_jk to Cpanel; block k stores
+// S_kk^-1 to Pbuf and the pivots' ln|u_pp|.  The redundant inversions cost
+// latency only (all blocks run concurrently) and remove the serial diag launch.
+// ---------------------------------------------------------------------------
+
+// 16x16 complex block in one wave: lane l holds row l>>2, columns (l&3)*4..+3.
+__device__ __forceinline__ void wave_inv16(double2 (&a)[4], double* pm, int pbase) {
+  const int l = threadIdx.x & 63;
+  const int r = l >> 2, cq = l & 3;
+#pragma unroll
+  for (int p = 0; p < 16; ++p) {
+    const int ps = p >> 2, pe = p & 3;
+    double2 piv, colp, rowp[4];
+    piv.x = __shfl(a[pe].x, p * 4 + ps, 64);
+    piv.y = __shfl(a[pe].y, p * 4 + ps, 64);
+    colp.x = __shfl(a[pe].x, r * 4 + ps, 64);
+    colp.y = __shfl(a[pe].y, r * 4 + ps, 64);
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      rowp[jj].x = __shfl(a[jj].x, p * 4 + cq, 64);
+      rowp[jj].y = __shfl(a[jj].y, p * 4 + cq, 64);
     }
-  } else {
-    const int i = x - nb;
-    if (i == k) return;
-    const double2* Sik = Mb + (int64_t)(i * kGJ) * Np + k * kGJ;
-    double2* dst = Cpanel + (int64_t)bi * Np * kGJ + (int64_t)i * kGJ * kGJ;
-    for (int e = threadIdx.x; e < kGJ * kGJ; e += blockDim.x)
-      dst[e] = Sik[(int64_t)(e >> 6) * Np + (e & 63)];
+    const double2 inv = cinv(piv);
+    if (pm != nullptr && l == 0) pm[pbase + p] = piv.x * piv.x + piv.y * piv.y;
+    if (r == p) {
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) a[jj] = (cq * 4 + jj == p) ? inv : cmul(rowp[jj], inv);
+    } else {
+      const double2 fi = cmul(colp, inv);
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+        a[jj] = (cq * 4 + jj == p) ? make_double2(-fi.x, -fi.y) : csub(a[jj], cmul(fi, rowp[jj]));
+    }
   }
 }
 
-// Trailing update: S_IJ = [J != k] S_IJ - Cpanel_I X_kJ for I != k (X_kk = P).
-// mode 0: every tile I != k; mode 1 ("edge", lookahead): the tiles of block
-// row k+1 and block column k+1; mode 2 ("rest"): all other tiles.
+// acc(16x16, C layout) += sgn * Aop(16 x 16, k) * Bop(16 x 16), complex, 4 MFMA per k-step.
+// Aop(m, k) = A[(m) * lda + k], Bop(k, n) = B[k * ldb + n]  (LDS pointers)
+template <bool NEG>
+__device__ __forceinline__ void mma16_lds(d4& acr, d4& aci, const double2* A, int lda,
+                                          const double2* B, int ldb) {
+  const int l = threadIdx.x & 63;
+  const int lr = l & 15, lk = l >> 4;
+#pragma unroll
+  for (int ks = 0; ks < 16; ks += 4) {
+    const double2 av = A[lr * lda + ks + lk];
+    const double2 bv = B[(ks + lk) * ldb + lr];
+    const double ar = NEG ? -av.x : av.x, ai = NEG ? -av.y : av.y;
+    acr = __builtin_amdgcn_mfma_f64_16x16x4f64(ar, bv.x, acr, 0, 0, 0);
+    aci = __builtin_amdgcn_mfma_f64_16x16x4f64(ar, bv.y, aci, 0, 0, 0);
+    acr = __builtin_amdgcn_mfma_f64_16x16x4f64(-ai, bv.y, acr, 0, 0, 0);
+    aci = __builtin_amdgcn_mfma_f64_16x16x4f64(ai, bv.x, aci, 0, 0, 0);
+  }
+}
+
+constexpr int kLdA = kGJ + 1;   // padded LDS row stride of the pivot block
+
+__global__ __launch_bounds__(256) void k_gj_pivot(double2* __restrict__ M, int64_t mat, int Np,
+                                                  int nb, int k, double2* __restrict__ Pbuf,
+                                                  double2* __restrict__ Cpanel,
+                                                  double* __restrict__ ldpart) {
+  __shared__ double2 A[kGJ * kLdA];        // the pivot block, inverted in place
+  __shared__ double2 Xs[16 * kGJ];         // row sub-panel of the current sub-step
+  __shared__ double2 Cs[kGJ * 16];         // column sub-panel copy
+  __shared__ double2 Dw[4][16 * 16];       // per-wave copy of the 16x16 sub-block inverse
+  __shared__ double2 Bs[16][kGJ];          // staging of S_kj for the panel product
+  __shared__ double pm[kGJ];
+  const int j = blockIdx.x, bi = blockIdx.y;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int lr = l & 15, lk = l >> 4;
+  double2* Mb = M + (int64_t)bi * mat;
+  const double2* Skk = Mb + (int64_t)(k * kGJ) * Np + k * kGJ;
+  for (int e = tid; e < kGJ * kGJ; e += 256) A[(e >> 6) * kLdA + (e & 63)] = Skk[(int64_t)(e >> 6) * Np + (e & 63)];
+  __syncthreads();
+
+#pragma unroll 1
+  for (int kb = 0; kb < 4; ++kb) {
+    const int o = kb * 16;
+    // (a) every wave inverts the 16x16 diagonal sub-block (redundantly)
+    double2 dv[4];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) dv[jj] = A[(o + (l >> 2)) * kLdA + o + (l & 3) * 4 + jj];
+    wave_inv16(dv, w == 0 ? pm : nullptr, o);
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) Dw[w][(l >> 2) * 16 + (l & 3) * 4 + jj] = dv[jj];
+    // column sub-panel copy (old values)
+    for (int e = tid; e < kGJ * 16; e += 256) Cs[e] = A[(e >> 4) * kLdA + o + (e & 15)];
+    // (b) X[:, block w] = Dinv * A[kb rows, block w]  (block kb: X = Dinv)
+    {
+      d4 xr = {0, 0, 0, 0}, xi = {0, 0, 0, 0};
+      if (w == kb) {
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const double2 v = Dw[w][(lk + 4 * rr) * 16 + lr];
+          xr[rr] = v.x;
+          xi[rr] = v.y;
+        }
+      } else {
+        mma16_lds<false>(xr, xi, Dw[w], 16, A + o * kLdA + w * 16, kLdA);
+      }
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) Xs[(lk + 4 * rr) * kGJ + w * 16 + lr] = make_double2(xr[rr], xi[rr]);
+    }
+    __syncthreads();
+    // (c) rows kb <- X; other rows: A[ib, jb] = [jb != kb] A[ib, jb] - C[ib] X[jb]
+    for (int e = tid; e < 16 * kGJ; e += 256) A[(o + (e >> 6)) * kLdA + (e & 63)] = Xs[e];
+#pragma unroll
+    for (int tt = 0; tt < 3; ++tt) {
+      const int t = w + 4 * tt;
+      const int ibx = t >> 2;
+      const int ib = ibx < kb ? ibx : ibx + 1;
+      const int jb = t & 3;
+      d4 cr, ci;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const double2 v = (jb == kb) ? make_double2(0.0, 0.0)
+                                     : A[(ib * 16 + lk + 4 * rr) * kLdA + jb * 16 + lr];
+        cr[rr] = v.x;
+        ci[rr] = v.y;
+      }
+      mma16_lds<true>(cr, ci, Cs + ib * 16 * 16, 16, Xs + jb * 16, kGJ);
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) A[(ib * 16 + lk + 4 * rr) * kLdA + jb * 16 + lr] = make_double2(cr[rr], ci[rr]);
+    }
+    __syncthreads();
+  }
+
+  if (j == k) {
+    double2* Pb = Pbuf + (int64_t)bi * kGJ * kGJ;
+    for (int e = tid; e < kGJ * kGJ; e += 256) Pb[e] = A[(e >> 6) * kLdA + (e & 63)];
+    if (nb == 1) {
+      double2* Sk = Mb + (int64_t)(k * kGJ) * Np + k * kGJ;
+      for (int e = tid; e < kGJ * kGJ; e += 256) Sk[(int64_t)(e >> 6) * Np + (e & 63)] = A[(e >> 6) * kLdA + (e & 63)];
+    }
+    if (tid < 64) {
+      const double v = wave_sum(0.5 * log(pm[tid]));
+      if (tid == 0) ldpart[(int64_t)bi * nb + k] = v;
+    }
+    return;
+  }
+  // column-panel copy S_jk -> Cpanel[j]
+  {
+    const double2* Sjk = Mb + (int64_t)(j * kGJ) * Np + k * kGJ;
+    double2* dst = Cpanel + (int64_t)bi * Np * kGJ + (int64_t)j * kGJ * kGJ;
+    for (int e = tid; e < kGJ * kGJ; e += 256) dst[e] = Sjk[(int64_t)(e >> 6) * Np + (e & 63)];
+  }
+  // row-panel tile X_kj = A * S_kj (in place): 4 waves x (32x32) outputs
+  double2* Skj = Mb + (int64_t)(k * kGJ) * Np + j * kGJ;
+  const int wr = (w >> 1) * 32, wc = (w & 1) * 32;
+  d4 acr[2][2], aci[2][2];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) {
+      acr[mi][ni] = d4{0.0, 0.0, 0.0, 0.0};
+      aci[mi][ni] = d4{0.0, 0.0, 0.0, 0.0};
+    }
+#pragma unroll 1
+  for (int kc = 0; kc < kGJ; kc += 16) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int kk = tid >> 4, col = (tid & 15) * 4 + s;
+      Bs[kk][col] = Skj[(int64_t)(kc + kk) * Np + col];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+        mma16_lds<false>(acr[mi][ni], aci[mi][ni], A + (wr + mi * 16) * kLdA + kc, kLdA,
+                         &Bs[0][wc + ni * 16], kGJ);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        Skj[(int64_t)(wr + mi * 16 + lk + 4 * r) * Np + wc + ni * 16 + lr] =
+            make_double2(acr[mi][ni][r], aci[mi][ni][r]);
+}
+
+// Trailing update: S_IJ = [J != k] S_IJ - Cpanel_I X_kJ for every tile I != k,
+// X_kJ = S_kJ (row panel, already scaled) and X_kk = Pbuf; the block with the
+// smallest I at J = k also stores Pbuf into S_kk (nobody reads S_kk here).
 __global__ __launch_bounds__(256) void k_gj_update(double2* __restrict__ M, int64_t mat, int Np,
-                                                   int nb, int k, int mode,
-                                                   const double2* __restrict__ Cpanel) {
+                                                   int nb, int k, const double2* __restrict__ Cpanel,
+                                                   const double2* __restrict__ Pbuf) {
   __shared__ double2 At[16][kGJ];
   __shared__ double2 Bs[16][kGJ];
   const int bi = blockIdx.y;
   const int t = blockIdx.x;
-  int I, J;
-  if (mode == 0) {
-    const int Ii = t / nb;
-    J = t - Ii * nb;
-    I = Ii < k ? Ii : Ii + 1;
-  } else if (mode == 1) {
-    if (t < nb) {
-      I = k + 1;
-      J = t;
-    } else {
-      const int u = t - nb;
-      I = u < k ? u : u + 2;
-      J = k + 1;
-    }
-  } else {
-    const int Ii = t / (nb - 1), Jj = t - Ii * (nb - 1);
-    I = Ii < k ? Ii : Ii + 2;
-    J = Jj < k + 1 ? Jj : Jj + 1;
-  }
+  const int Ii = t / nb, J = t - Ii * nb;
+  const int I = Ii < k ? Ii : Ii + 1;
   double2* Mb = M + (int64_t)bi * mat;
   const double2* Ci = Cpanel + (int64_t)bi * Np * kGJ + (int64_t)I * kGJ * kGJ;
-  tile_cgemm<true, true>(Ci, kGJ, Mb + (int64_t)(k * kGJ) * Np + J * kGJ, Np,
-                         Mb + (int64_t)(I * kGJ) * Np + J * kGJ, Np, J == k, At, Bs);
+  const double2* Pb = Pbuf + (int64_t)bi * kGJ * kGJ;
+  const bool jk = (J == k);
+  tile_cgemm<true, true>(Ci, kGJ, jk ? Pb : Mb + (int64_t)(k * kGJ) * Np + J * kGJ, jk ? kGJ : Np,
+                         Mb + (int64_t)(I * kGJ) * Np + J * kGJ, Np, jk, At, Bs);
+  if (jk && Ii == 0) {
+    double2* Sk = Mb + (int64_t)(k * kGJ) * Np + k * kGJ;
+    for (int e = threadIdx.x; e < kGJ * kGJ; e += blockDim.x) Sk[(int64_t)(e >> 6) * Np + (e & 63)] = Pb[e];
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -619,28 +707,18 @@ void launch_fill_hz(const Dims& d, double2* M, const int* hcol, const double* hv
   hipLaunchKernelGGL(k_fill_hz, dim3(d.Np, d.nbatch), dim3(256), 0, s, M, d.mat, d.N, d.Np, d.P,
                      hcol, hval, ypole);
 }
-void launch_gj_diag(const Dims& d, double2* M, int k, double2* Pinv, double* ldpart,
-                    hipStream_t s) {
-  hipLaunchKernelGGL(k_gj_diag, dim3(d.nbatch), dim3(1024), 0, s, M, d.mat, d.Np, k, d.nb, Pinv,
-                     ldpart);
+void launch_gj_pivot(const Dims& d, double2* M, int k, double2* Pbuf, double2* Cpanel,
+                     double* ldpart, hipStream_t s) {
+  hipLaunchKernelGGL(k_gj_pivot, dim3(d.nb, d.nbatch), dim3(256), 0, s, M, d.mat, d.Np, d.nb, k,
+                     Pbuf, Cpanel, ldpart);
 }
-void launch_gj_panel(const Dims& d, double2* M, int k, const double2* Pinv, double2* Cpanel,
-                     hipStream_t s) {
-  hipLaunchKernelGGL(k_gj_panel, dim3(2 * d.nb, d.nbatch), dim3(256), 0, s, M, d.mat, d.Np, d.nb,
-                     k, Pinv, Cpanel);
-}
-int gj_update_tiles(const Dims& d, int mode) {
-  if (d.nb < 2) return 0;
-  if (mode == 0) return (d.nb - 1) * d.nb;
-  if (mode == 1) return 2 * d.nb - 2;
-  return (d.nb - 2) * (d.nb - 1);
-}
-void launch_gj_update(const Dims& d, double2* M, int k, int mode, const double2* Cpanel,
+int gj_update_tiles(const Dims& d) { return d.nb < 2 ? 0 : (d.nb - 1) * d.nb; }
+void launch_gj_update(const Dims& d, double2* M, int k, const double2* Cpanel, const double2* Pbuf,
                       hipStream_t s) {
-  const int tiles = gj_update_tiles(d, mode);
+  const int tiles = gj_update_tiles(d);
   if (tiles <= 0) return;
   hipLaunchKernelGGL(k_gj_update, dim3(tiles, d.nbatch), dim3(256), 0, s, M, d.mat, d.Np, d.nb, k,
-                     mode, Cpanel);
+                     Cpanel, Pbuf);
 }
 void launch_assemble(const Dims& d, const double2* R, double2* T, double2* S, const int* Dcol,
                      const int* Dsrc, const double2* Delta, const int* hcol, const double* hval,

@@ -121,7 +121,7 @@ int dwh_stream(dwh_ctx* ctx, void** stream);
 
 /* Kernel timing with HIP events on the context stream (bench/profiling). */
 int dwh_timing_enable(dwh_ctx* ctx, int32_t enable);
-/* name: "gj_update", "gj_panel", "gj_diag", "assemble", "contract", "step";
+/* name: "gj_update", "gj_pivot", "assemble", "contract", "step";
  * returns total milliseconds, launches and algorithmic flops (or bytes) per
  * launch summed over launches. */
 int dwh_timing_read(dwh_ctx* ctx, const char* name, double* total_ms, int64_t* launches,

@@ -68,7 +68,7 @@ def main():
         ctx.timing_reset()
         ctx.run_sweeps(0, 1, a.Nt, dt, p.mass)
         ctx.synchronize()
-        kt = {k: ctx.timing_read(k) for k in ("gj_update", "gj_panel", "gj_diag", "assemble", "contract", "step")}
+        kt = {k: ctx.timing_read(k) for k in ("gj_update", "gj_pivot", "assemble", "contract", "step")}
         ctx.timing_enable(False)
         x = np.array(res[v])
         upd = kt["gj_update"]
