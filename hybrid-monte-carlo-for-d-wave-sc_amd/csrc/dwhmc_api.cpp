@@ -411,6 +411,7 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
   d.P = pe.m;
   d.nbatch = d.nc * d.P;
   d.mat = (int64_t)d.Np * d.Np;
+  if (const char* uv = std::getenv("DWHMC_UPDATE")) d.update_variant = std::atoi(uv) == 1 ? 1 : 2;
 
   auto bail = [&](int code) {
     g_create_error = ctx->err;

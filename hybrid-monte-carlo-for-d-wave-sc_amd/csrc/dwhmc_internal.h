@@ -18,6 +18,7 @@ struct Dims {
   int P;        // poles per chain
   int nbatch;   // nc * P
   int64_t mat;  // elements per padded matrix (Np*Np)
+  int update_variant = 2;  // trailing-update kernel: 1 LDS-staged, 2 register-direct (DWHMC_UPDATE)
 };
 
 // dense h - i y_q (padded with identity) for every (chain, pole): R init input

@@ -14,6 +14,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
+
 #include "dwhmc_internal.h"
 
 namespace dwh {
@@ -32,6 +34,14 @@ __device__ __forceinline__ double2 csub(double2 a, double2 b) { return make_doub
 __device__ __forceinline__ double2 cinv(double2 a) {
   const double s = 1.0 / (a.x * a.x + a.y * a.y);
   return make_double2(a.x * s, -a.y * s);
+}
+
+// Bijective XCD-aware remap of a 1D grid (cdna_hip_programming.md §5): blocks
+// b and b+8 share an XCD, so item ranges [x*q, (x+1)*q) are given to one XCD
+// and neighbouring rows of one matrix share that XCD's L2.  Speed only.
+__device__ __forceinline__ int xcd_remap(int orig, int total) {
+  const int q = total / 8, r = total % 8, xcd = orig % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
 }
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -228,14 +238,31 @@ __device__ __forceinline__ void mma16_lds(d4& acr, d4& aci, const double2* A, in
 
 constexpr int kLdA = kGJ + 1;   // padded LDS row stride of the pivot block
 
+// Diagnostic build only (-DDWH_STAMPS, tools/micro/pivot_stamps.hip): per-block
+// s_memtime stamps of the pivot kernel's phases; never compiled into the library.
+#ifdef DWH_STAMPS
+__device__ unsigned long long g_stamps[4096][8];
+#define DWH_STAMP(i)                                                          \
+  do {                                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                        \
+    if (threadIdx.x == 0)                                                     \
+      g_stamps[blockIdx.y * gridDim.x + blockIdx.x][i] = __builtin_amdgcn_s_memtime(); \
+    __builtin_amdgcn_sched_barrier(0);                                        \
+  } while (0)
+#else
+#define DWH_STAMP(i) \
+  do {               \
+  } while (0)
+#endif
+
 __global__ __launch_bounds__(256) void k_gj_pivot(double2* __restrict__ M, int64_t mat, int Np,
                                                   int nb, int k, double2* __restrict__ Pbuf,
                                                   double2* __restrict__ Cpanel,
                                                   double* __restrict__ ldpart) {
   __shared__ double2 A[kGJ * kLdA];        // the pivot block, inverted in place
   __shared__ double2 Xs[16 * kGJ];         // row sub-panel of the current sub-step
-  __shared__ double2 Cs[kGJ * 16];         // column sub-panel copy
-  __shared__ double2 Dw[4][16 * 16];       // per-wave copy of the 16x16 sub-block inverse
+  __shared__ double2 Cs[kGJ * 17];         // column sub-panel copy (row stride 17: no bank conflicts)
+  __shared__ double2 Dw[4][16 * 17];       // per-wave copy of the 16x16 sub-block inverse
   __shared__ double2 Bs[16][kGJ];          // staging of S_kj for the panel product
   __shared__ double pm[kGJ];
   const int j = blockIdx.x, bi = blockIdx.y;
@@ -243,8 +270,10 @@ __global__ __launch_bounds__(256) void k_gj_pivot(double2* __restrict__ M, int64
   const int lr = l & 15, lk = l >> 4;
   double2* Mb = M + (int64_t)bi * mat;
   const double2* Skk = Mb + (int64_t)(k * kGJ) * Np + k * kGJ;
+  DWH_STAMP(0);
   for (int e = tid; e < kGJ * kGJ; e += 256) A[(e >> 6) * kLdA + (e & 63)] = Skk[(int64_t)(e >> 6) * Np + (e & 63)];
   __syncthreads();
+  DWH_STAMP(1);
 
 #pragma unroll 1
   for (int kb = 0; kb < 4; ++kb) {
@@ -254,27 +283,29 @@ __global__ __launch_bounds__(256) void k_gj_pivot(double2* __restrict__ M, int64
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) dv[jj] = A[(o + (l >> 2)) * kLdA + o + (l & 3) * 4 + jj];
     wave_inv16(dv, w == 0 ? pm : nullptr, o);
+    if (kb == 0) DWH_STAMP(2);
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) Dw[w][(l >> 2) * 16 + (l & 3) * 4 + jj] = dv[jj];
+    for (int jj = 0; jj < 4; ++jj) Dw[w][(l >> 2) * 17 + (l & 3) * 4 + jj] = dv[jj];
     // column sub-panel copy (old values)
-    for (int e = tid; e < kGJ * 16; e += 256) Cs[e] = A[(e >> 4) * kLdA + o + (e & 15)];
+    for (int e = tid; e < kGJ * 16; e += 256) Cs[(e >> 4) * 17 + (e & 15)] = A[(e >> 4) * kLdA + o + (e & 15)];
     // (b) X[:, block w] = Dinv * A[kb rows, block w]  (block kb: X = Dinv)
     {
       d4 xr = {0, 0, 0, 0}, xi = {0, 0, 0, 0};
       if (w == kb) {
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
-          const double2 v = Dw[w][(lk + 4 * rr) * 16 + lr];
+          const double2 v = Dw[w][(lk + 4 * rr) * 17 + lr];
           xr[rr] = v.x;
           xi[rr] = v.y;
         }
       } else {
-        mma16_lds<false>(xr, xi, Dw[w], 16, A + o * kLdA + w * 16, kLdA);
+        mma16_lds<false>(xr, xi, Dw[w], 17, A + o * kLdA + w * 16, kLdA);
       }
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) Xs[(lk + 4 * rr) * kGJ + w * 16 + lr] = make_double2(xr[rr], xi[rr]);
     }
     __syncthreads();
+    if (kb == 0) DWH_STAMP(3);
     // (c) rows kb <- X; other rows: A[ib, jb] = [jb != kb] A[ib, jb] - C[ib] X[jb]
     for (int e = tid; e < 16 * kGJ; e += 256) A[(o + (e >> 6)) * kLdA + (e & 63)] = Xs[e];
 #pragma unroll
@@ -291,12 +322,14 @@ __global__ __launch_bounds__(256) void k_gj_pivot(double2* __restrict__ M, int64
         cr[rr] = v.x;
         ci[rr] = v.y;
       }
-      mma16_lds<true>(cr, ci, Cs + ib * 16 * 16, 16, Xs + jb * 16, kGJ);
+      mma16_lds<true>(cr, ci, Cs + ib * 16 * 17, 17, Xs + jb * 16, kGJ);
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) A[(ib * 16 + lk + 4 * rr) * kLdA + jb * 16 + lr] = make_double2(cr[rr], ci[rr]);
     }
     __syncthreads();
+    if (kb == 0) DWH_STAMP(4);
   }
+  DWH_STAMP(5);
 
   if (j == k) {
     double2* Pb = Pbuf + (int64_t)bi * kGJ * kGJ;
@@ -317,6 +350,7 @@ __global__ __launch_bounds__(256) void k_gj_pivot(double2* __restrict__ M, int64
     double2* dst = Cpanel + (int64_t)bi * Np * kGJ + (int64_t)j * kGJ * kGJ;
     for (int e = tid; e < kGJ * kGJ; e += 256) dst[e] = Sjk[(int64_t)(e >> 6) * Np + (e & 63)];
   }
+  DWH_STAMP(6);
   // row-panel tile X_kj = A * S_kj (in place): 4 waves x (32x32) outputs
   double2* Skj = Mb + (int64_t)(k * kGJ) * Np + j * kGJ;
   const int wr = (w >> 1) * 32, wc = (w & 1) * 32;
@@ -352,6 +386,7 @@ __global__ __launch_bounds__(256) void k_gj_pivot(double2* __restrict__ M, int64
       for (int r = 0; r < 4; ++r)
         Skj[(int64_t)(wr + mi * 16 + lk + 4 * r) * Np + wc + ni * 16 + lr] =
             make_double2(acr[mi][ni][r], aci[mi][ni][r]);
+  DWH_STAMP(7);
 }
 
 // Trailing update: S_IJ = [J != k] S_IJ - Cpanel_I X_kJ for every tile I != k,
@@ -378,6 +413,100 @@ __global__ __launch_bounds__(256) void k_gj_update(double2* __restrict__ M, int6
   }
 }
 
+// Trailing update, variant 2: no LDS and no barriers.  Each wave owns a
+// 32x32 complex sub-tile and loads its MFMA fragments straight from L2 into
+// registers with a two-deep software prefetch (one k-step = 16 MFMAs = 1024
+// issue cycles, enough to cover an L2 hit).  1D grid with an XCD-aware remap:
+// consecutive work items (same batch matrix, i.e. the same A/B panels) land on
+// one XCD so the panels stay in that XCD's 4 MB L2 (placement is speed only).
+__global__ __launch_bounds__(256) void k_gj_update2(double2* __restrict__ M, int64_t mat, int Np,
+                                                    int nb, int k, int total,
+                                                    const double2* __restrict__ Cpanel,
+                                                    const double2* __restrict__ Pbuf) {
+  const int tiles = (nb - 1) * nb;
+  const int item = xcd_remap(blockIdx.x, total);
+  const int bi = item / tiles, t = item - bi * tiles;
+  const int Ii = t / nb, J = t - Ii * nb;
+  const int I = Ii < k ? Ii : Ii + 1;
+  const bool jk = (J == k);
+  double2* Mb = M + (int64_t)bi * mat;
+  const double2* A = Cpanel + (int64_t)bi * Np * kGJ + (int64_t)I * kGJ * kGJ;       // [64][64]
+  const double2* B = jk ? Pbuf + (int64_t)bi * kGJ * kGJ : Mb + (int64_t)(k * kGJ) * Np + J * kGJ;
+  const int ldb = jk ? kGJ : Np;
+  double2* C = Mb + (int64_t)(I * kGJ) * Np + J * kGJ;
+  const int tid = threadIdx.x;
+  const int w = tid >> 6, l = tid & 63;
+  const int wr = (w >> 1) * 32, wc = (w & 1) * 32;
+  const int lr = l & 15, lk = l >> 4;
+  const double2* Ap0 = A + (wr + lr) * kGJ + lk;
+  const double2* Ap1 = Ap0 + 16 * kGJ;
+  const double2* Bp0 = B + (int64_t)lk * ldb + wc + lr;
+  const double2* Bp1 = Bp0 + 16;
+  // prefetch k-steps 0 and 1
+  double2 a0[2], a1[2], b0[2], b1[2];
+  a0[0] = Ap0[0]; a1[0] = Ap1[0]; b0[0] = Bp0[0]; b1[0] = Bp1[0];
+  a0[1] = Ap0[4]; a1[1] = Ap1[4]; b0[1] = Bp0[(int64_t)4 * ldb]; b1[1] = Bp1[(int64_t)4 * ldb];
+  d4 acr[2][2], aci[2][2];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) {
+      if (!jk) {
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const double2 v = C[(int64_t)(wr + mi * 16 + lk + 4 * rr) * Np + wc + ni * 16 + lr];
+          acr[mi][ni][rr] = v.x;
+          aci[mi][ni][rr] = v.y;
+        }
+      } else {
+        acr[mi][ni] = d4{0.0, 0.0, 0.0, 0.0};
+        aci[mi][ni] = d4{0.0, 0.0, 0.0, 0.0};
+      }
+    }
+#pragma unroll
+  for (int ks = 0; ks < 16; ++ks) {
+    const int cur = ks & 1;
+    const double2 av[2] = {a0[cur], a1[cur]};
+    const double2 bv[2] = {b0[cur], b1[cur]};
+    if (ks + 2 < 16) {
+      const int kn = (ks + 2) * 4;
+      a0[cur] = Ap0[kn];
+      a1[cur] = Ap1[kn];
+      b0[cur] = Bp0[(int64_t)kn * ldb];
+      b1[cur] = Bp1[(int64_t)kn * ldb];
+    }
+    // C -= A B  ->  feed -A
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) {
+        acr[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av[mi].x, bv[ni].x, acr[mi][ni], 0, 0, 0);
+        aci[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av[mi].x, bv[ni].y, aci[mi][ni], 0, 0, 0);
+      }
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) {
+        acr[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[mi].y, bv[ni].y, acr[mi][ni], 0, 0, 0);
+        aci[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av[mi].y, bv[ni].x, aci[mi][ni], 0, 0, 0);
+      }
+  }
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+        C[(int64_t)(wr + mi * 16 + lk + 4 * rr) * Np + wc + ni * 16 + lr] =
+            make_double2(acr[mi][ni][rr], aci[mi][ni][rr]);
+  if (jk && Ii == 0) {
+    __syncthreads();
+    const double2* Pb = Pbuf + (int64_t)bi * kGJ * kGJ;
+    double2* Sk = Mb + (int64_t)(k * kGJ) * Np + k * kGJ;
+    for (int e = tid; e < kGJ * kGJ; e += blockDim.x) Sk[(int64_t)(e >> 6) * Np + (e & 63)] = Pb[e];
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Assembly of T = R D and S^T for one row a (block) of one (chain, pole).
 //   TT[a,k]  = Σ_{l ∈ Dcol(a)} D[a,l] R[l,k]               (rows of R, coalesced)
@@ -397,7 +526,8 @@ __global__ __launch_bounds__(256) void k_assemble(const double2* __restrict__ R,
   extern __shared__ double2 smem[];
   double2* TTrow = smem;
   double2* Rrow = smem + Np;
-  const int a = blockIdx.x, bi = blockIdx.y;
+  const int item = xcd_remap(blockIdx.x, gridDim.x);
+  const int bi = item / Np, a = item - bi * Np;
   const int c = bi / P, q = bi % P;
   double2* Srow = S + (int64_t)bi * mat + (int64_t)a * Np;
   if (a >= N) {  // padding rows: identity
@@ -466,7 +596,8 @@ __global__ __launch_bounds__(256) void k_contract(const double2* __restrict__ T,
                                                   int N, int Np, const int* __restrict__ Dcol,
                                                   double2* __restrict__ G12nn,
                                                   double2* __restrict__ diagS) {
-  const int i = blockIdx.x, bi = blockIdx.y;
+  const int item = xcd_remap(blockIdx.x, gridDim.x);
+  const int bi = item / N, i = item - bi * N;
   const double2* Trow = T + (int64_t)bi * mat + (int64_t)i * Np;
   const double2* Sb = SinvT + (int64_t)bi * mat;
   int js[kSlots];
@@ -717,19 +848,25 @@ void launch_gj_update(const Dims& d, double2* M, int k, const double2* Cpanel, c
                       hipStream_t s) {
   const int tiles = gj_update_tiles(d);
   if (tiles <= 0) return;
-  hipLaunchKernelGGL(k_gj_update, dim3(tiles, d.nbatch), dim3(256), 0, s, M, d.mat, d.Np, d.nb, k,
-                     Cpanel, Pbuf);
+  if (d.update_variant == 1) {
+    hipLaunchKernelGGL(k_gj_update, dim3(tiles, d.nbatch), dim3(256), 0, s, M, d.mat, d.Np, d.nb, k,
+                       Cpanel, Pbuf);
+  } else {
+    const int total = tiles * d.nbatch;
+    hipLaunchKernelGGL(k_gj_update2, dim3(total), dim3(256), 0, s, M, d.mat, d.Np, d.nb, k, total,
+                       Cpanel, Pbuf);
+  }
 }
 void launch_assemble(const Dims& d, const double2* R, double2* T, double2* S, const int* Dcol,
                      const int* Dsrc, const double2* Delta, const int* hcol, const double* hval,
                      const double* ypole, hipStream_t s) {
   const size_t shm = 2 * (size_t)d.Np * sizeof(double2);
-  hipLaunchKernelGGL(k_assemble, dim3(d.Np, d.nbatch), dim3(256), shm, s, R, T, S, d.mat, d.N,
+  hipLaunchKernelGGL(k_assemble, dim3(d.Np * d.nbatch), dim3(256), shm, s, R, T, S, d.mat, d.N,
                      d.Np, d.P, Dcol, Dsrc, Delta, hcol, hval, ypole);
 }
 void launch_contract(const Dims& d, const double2* T, const double2* SinvT, const int* Dcol,
                      double2* G12nn, double2* diagS, hipStream_t s) {
-  hipLaunchKernelGGL(k_contract, dim3(d.N, d.nbatch), dim3(256), 0, s, T, SinvT, d.mat, d.N, d.Np,
+  hipLaunchKernelGGL(k_contract, dim3(d.N * d.nbatch), dim3(256), 0, s, T, SinvT, d.mat, d.N, d.Np,
                      Dcol, G12nn, diagS);
 }
 void launch_pair_force(const Dims& d, const double2* G12nn, const int* bond_ij,

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Interleaved in-process A/B of context variants (env knobs read at create):
 python tools/ab_bench.py --L 32 --beta 16 --variants "LA=0" "LA=1,SC=0" "LA=1,SC=32"
-LA -> DWHMC_LOOKAHEAD, SC -> DWHMC_SIDE_CUS.  Prints ms per leapfrog step
+UPD -> DWHMC_UPDATE (trailing-update kernel variant).  Prints ms per leapfrog step
 (median / min over rounds) and the per-kernel event totals of the last round."""
 import argparse
 import math
@@ -44,6 +44,7 @@ def main():
         kv = dict(x.split("=") for x in v.split(",") if x)
         os.environ["DWHMC_LOOKAHEAD"] = kv.get("LA", "1")
         os.environ["DWHMC_SIDE_CUS"] = kv.get("SC", "32")
+        os.environ["DWHMC_UPDATE"] = kv.get("UPD", "2")
         ctx = m.FermionContext(p.Lx, p.Ly, p.t, p.tp, p.mu, p.beta, p.J, p.nn_table, p.nnn_table,
                                np.stack(dis))
         ctx.set_pairing(np.stack(D0))
