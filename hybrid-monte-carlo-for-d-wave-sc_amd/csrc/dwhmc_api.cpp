@@ -53,7 +53,10 @@ struct DevBuf {
 
 struct dwh_ctx {
   int device = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;   // main stream
+  hipStream_t side = nullptr;     // high-priority stream: GJ pivot of step k+1 (lookahead)
+  hipEvent_t ev_edge = nullptr, ev_pivot = nullptr;
+  bool lookahead = true;
   Dims d{};
   int64_t Lx = 0, Ly = 0;
   double t = 0, tp = 0, mu = 0, beta = 0, J = 0, delta_cap = 2.0;
@@ -140,7 +143,8 @@ struct Scope {
   double work;
   hipStream_t st;
   hipEvent_t a{};
-  Scope(dwh_ctx* c, int n, double w) : ctx(c), name(n), work(w), st(c->stream) {
+  Scope(dwh_ctx* c, int n, double w, hipStream_t s = nullptr)
+      : ctx(c), name(n), work(w), st(s ? s : c->stream) {
     if (ctx->timing) {
       a = take_event(ctx);
       (void)hipEventRecord(a, st);
@@ -158,6 +162,7 @@ struct Scope {
 void drain_timing(dwh_ctx* ctx) {
   if (ctx->recs.empty()) return;
   (void)hipStreamSynchronize(ctx->stream);
+  (void)hipStreamSynchronize(ctx->side);
   for (auto& r : ctx->recs) {
     float ms = 0.f;
     (void)hipEventElapsedTime(&ms, r.a, r.b);
@@ -172,19 +177,41 @@ void drain_timing(dwh_ctx* ctx) {
 
 double tile_flops() { return 8.0 * kGJ * kGJ * kGJ; }
 
-// Blocked no-pivot Gauss-Jordan inversion of all nbatch matrices in M:
-// per block step a pivot launch (S_kk^-1, row panel, column copy) and a
-// trailing-update launch.
+void gj_pivot(dwh_ctx* ctx, double2* M, int k, hipStream_t st) {
+  const Dims& d = ctx->d;
+  Scope s(ctx, T_GJ_PIVOT, (double)d.nbatch * d.nb * tile_flops(), st);
+  dwh::launch_gj_pivot(d, M, k, ctx->Pinv, ctx->Cpanel, ctx->ldpart, st);
+}
+
+void gj_update(dwh_ctx* ctx, double2* M, int k, int mode) {
+  const Dims& d = ctx->d;
+  Scope s(ctx, T_GJ_UPDATE, (double)d.nbatch * dwh::gj_update_tiles(d, mode) * tile_flops());
+  dwh::launch_gj_update(d, M, k, mode, ctx->Cpanel, ctx->Pinv, ctx->stream);
+}
+
+// Blocked no-pivot Gauss-Jordan inversion of all nbatch matrices in M.  Per
+// block step k: a pivot launch (S_kk^-1 in every block, row panel) and a
+// trailing update.  Lookahead: the update's edge tiles (block row/col k+1)
+// run first; the pivot of step k+1 then runs on the high-priority side stream
+// while the rest of update k runs on the main stream (the pivot kernel uses
+// LDS, the update registers, so their blocks can share a CU).  Pbuf and the
+// column panel are double-buffered by step parity.  Opt-in: DWHMC_LOOKAHEAD=1.
 void run_gj(dwh_ctx* ctx, double2* M) {
   const Dims& d = ctx->d;
+  gj_pivot(ctx, M, 0, ctx->stream);
   for (int k = 0; k < d.nb; ++k) {
-    {
-      Scope s(ctx, T_GJ_PIVOT, (double)d.nbatch * d.nb * tile_flops());
-      dwh::launch_gj_pivot(d, M, k, ctx->Pinv, ctx->Cpanel, ctx->ldpart, ctx->stream);
-    }
-    if (d.nb > 1) {
-      Scope s(ctx, T_GJ_UPDATE, (double)d.nbatch * dwh::gj_update_tiles(d) * tile_flops());
-      dwh::launch_gj_update(d, M, k, ctx->Cpanel, ctx->Pinv, ctx->stream);
+    if (d.nb < 2) break;
+    if (ctx->lookahead && k + 1 < d.nb) {
+      gj_update(ctx, M, k, 1);
+      (void)hipEventRecord(ctx->ev_edge, ctx->stream);
+      (void)hipStreamWaitEvent(ctx->side, ctx->ev_edge, 0);
+      gj_pivot(ctx, M, k + 1, ctx->side);
+      (void)hipEventRecord(ctx->ev_pivot, ctx->side);
+      gj_update(ctx, M, k, 2);
+      (void)hipStreamWaitEvent(ctx->stream, ctx->ev_pivot, 0);
+    } else {
+      gj_update(ctx, M, k, 0);
+      if (k + 1 < d.nb) gj_pivot(ctx, M, k + 1, ctx->stream);
     }
   }
 }
@@ -411,7 +438,6 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
   d.P = pe.m;
   d.nbatch = d.nc * d.P;
   d.mat = (int64_t)d.Np * d.Np;
-  if (const char* uv = std::getenv("DWHMC_UPDATE")) d.update_variant = std::atoi(uv) == 1 ? 1 : 2;
 
   auto bail = [&](int code) {
     g_create_error = ctx->err;
@@ -422,8 +448,17 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     ctx->err = "hipSetDevice failed";
     return bail(DWH_ERR_HIP);
   }
-  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
-    ctx->err = "hipStreamCreate failed";
+  // lookahead is opt-in: measured slower on MI355X because the pivot blocks
+  // (LDS + ~190 VGPR/wave) find no SIMD room next to 3 update waves and queue
+  const char* la = std::getenv("DWHMC_LOOKAHEAD");
+  ctx->lookahead = (la && la[0] == '1');
+  int prio_lo = 0, prio_hi = 0;
+  (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_edge, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_pivot, hipEventDisableTiming) != hipSuccess) {
+    ctx->err = "hipStream/hipEvent create failed";
     return bail(DWH_ERR_HIP);
   }
   const size_t nmat = (size_t)d.nbatch * d.mat;
@@ -434,8 +469,8 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
   ALLOC(R, nmat);
   ALLOC(T, nmat);
   ALLOC(S, nmat);
-  ALLOC(Cpanel, (size_t)d.nbatch * d.Np * kGJ);
-  ALLOC(Pinv, (size_t)d.nbatch * kGJ * kGJ);
+  ALLOC(Cpanel, 2 * (size_t)d.nbatch * d.Np * kGJ);
+  ALLOC(Pinv, 2 * (size_t)d.nbatch * kGJ * kGJ);
   ALLOC(G12nn, (size_t)d.nbatch * N * kSlots);
   ALLOC(diagS, (size_t)d.nbatch * N);
   ALLOC(ldpart, (size_t)d.nbatch * d.nb);
@@ -530,7 +565,11 @@ void dwh_destroy(dwh_ctx* ctx) {
     (void)hipEventDestroy(r.b);
   }
   for (auto e : ctx->pool) (void)hipEventDestroy(e);
+  if (ctx->side) (void)hipStreamSynchronize(ctx->side);
   for (void* p : ctx->allocations) (void)hipFree(p);
+  if (ctx->ev_edge) (void)hipEventDestroy(ctx->ev_edge);
+  if (ctx->ev_pivot) (void)hipEventDestroy(ctx->ev_pivot);
+  if (ctx->side) (void)hipStreamDestroy(ctx->side);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }

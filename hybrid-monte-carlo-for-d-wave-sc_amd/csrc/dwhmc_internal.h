@@ -18,19 +18,22 @@ struct Dims {
   int P;        // poles per chain
   int nbatch;   // nc * P
   int64_t mat;  // elements per padded matrix (Np*Np)
-  int update_variant = 2;  // trailing-update kernel: 1 LDS-staged, 2 register-direct (DWHMC_UPDATE)
 };
 
 // dense h - i y_q (padded with identity) for every (chain, pole): R init input
 void launch_fill_hz(const Dims& d, double2* M, const int* hcol, const double* hval,
                     const double* ypole, hipStream_t s);
 // Gauss-Jordan block step k on all nbatch matrices in M (in place, no pivoting):
-// pivot (invert S_kk in every block, row panel, column copy), then update.
+// pivot (invert S_kk in every block, row panel), then update.  Cpanel holds two
+// parity buffers of nbatch x Np x 64: step k reads buffer k&1 and the update
+// of step k fills buffer (k+1)&1 (the next column panel).
 void launch_gj_pivot(const Dims& d, double2* M, int k, double2* Pbuf, double2* Cpanel,
                      double* ldpart, hipStream_t s);
-int gj_update_tiles(const Dims& d);
-void launch_gj_update(const Dims& d, double2* M, int k, const double2* Cpanel, const double2* Pbuf,
-                      hipStream_t s);
+// mode 0: every tile I != k; 1: lookahead edge (block row/col k+1); 2: the rest.
+// Pbuf holds two parity buffers of nbatch x 64 x 64 (step k uses k&1).
+int gj_update_tiles(const Dims& d, int mode);
+void launch_gj_update(const Dims& d, double2* M, int k, int mode, double2* Cpanel,
+                      const double2* Pbuf, hipStream_t s);
 // T = R D and S^T = -(h + i y) - (D† R D)^T for every (chain, pole)
 void launch_assemble(const Dims& d, const double2* R, double2* T, double2* S, const int* Dcol,
                      const int* Dsrc, const double2* Delta, const int* hcol, const double* hval,

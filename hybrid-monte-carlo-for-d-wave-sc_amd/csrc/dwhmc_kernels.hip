@@ -35,6 +35,18 @@ __device__ __forceinline__ double2 cinv(double2 a) {
   const double s = 1.0 / (a.x * a.x + a.y * a.y);
   return make_double2(a.x * s, -a.y * s);
 }
+// 1/a with v_rcp_f64 + two Newton steps (error ~1 ulp; the IEEE division
+// sequence has ~3x the latency and sits on the pivot dependency chain).
+__device__ __forceinline__ double rcp_nr(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  r = fma(r, fma(-d, r, 1.0), r);
+  r = fma(r, fma(-d, r, 1.0), r);
+  return r;
+}
+__device__ __forceinline__ double2 cinv_fast(double2 a) {
+  const double s = rcp_nr(fma(a.x, a.x, a.y * a.y));
+  return make_double2(a.x * s, -a.y * s);
+}
 
 // Bijective XCD-aware remap of a 1D grid (cdna_hip_programming.md §5): blocks
 // b and b+8 share an XCD, so item ranges [x*q, (x+1)*q) are given to one XCD
@@ -83,100 +95,6 @@ __global__ __launch_bounds__(256) void k_fill_hz(double2* __restrict__ M, int64_
 }
 
 // ---------------------------------------------------------------------------
-// 64x64x64 complex tile GEMM on f64 MFMA.
-//   C = A·B            (NEG = false, LOADC = false)
-//   C = C0 - A·B       (NEG = true,  LOADC = true; C0 = 0 when zeroC)
-// A: 64 rows x 64 k (lda), B: 64 k x 64 cols (ldb).  4 waves, each a 32x32
-// complex output = 2x2 blocks of 16x16; every complex MAC is 4 real MFMAs
-// (no 3M trick, rounding stays the plain complex product's).
-// v_mfma_f64_16x16x4_f64 layouts (gfx950): A lane l -> A[l&15][l>>4],
-// B lane l -> B[l>>4][l&15], C/D reg r -> C[(l>>4) + 4r][l&15].
-// ---------------------------------------------------------------------------
-template <bool NEG, bool LOADC>
-__device__ __forceinline__ void tile_cgemm(const double2* __restrict__ A, int lda,
-                                           const double2* __restrict__ B, int ldb,
-                                           double2* __restrict__ C, int ldc, bool zeroC,
-                                           double2 (*At)[kGJ], double2 (*Bs)[kGJ]) {
-  const int tid = threadIdx.x;
-  const int w = tid >> 6, l = tid & 63;
-  const int wr = (w >> 1) * 32, wc = (w & 1) * 32;
-  const int lr = l & 15, lk = l >> 4;
-  d4 acr[2][2], aci[2][2];
-#pragma unroll
-  for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < 2; ++ni) {
-      if (LOADC && !zeroC) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const double2 v = C[(int64_t)(wr + mi * 16 + lk + 4 * r) * ldc + wc + ni * 16 + lr];
-          acr[mi][ni][r] = v.x;
-          aci[mi][ni][r] = v.y;
-        }
-      } else {
-        acr[mi][ni] = d4{0.0, 0.0, 0.0, 0.0};
-        aci[mi][ni] = d4{0.0, 0.0, 0.0, 0.0};
-      }
-    }
-
-#pragma unroll 1
-  for (int kc = 0; kc < kGJ; kc += 16) {
-    // stage A chunk transposed (At[k][row]) and B chunk (Bs[k][col])
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int kk = tid & 15, row = (tid >> 4) + 16 * s;
-      At[kk][row] = A[(int64_t)row * lda + kc + kk];
-    }
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int kk = tid >> 4, col = (tid & 15) * 4 + s;
-      Bs[kk][col] = B[(int64_t)(kc + kk) * ldb + col];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int ks = 0; ks < 16; ks += 4) {
-      double ar[2], ai[2], nai[2], br[2], bim[2];
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi) {
-        const double2 v = At[ks + lk][wr + mi * 16 + lr];
-        ar[mi] = NEG ? -v.x : v.x;
-        ai[mi] = NEG ? -v.y : v.y;
-        nai[mi] = -ai[mi];
-      }
-#pragma unroll
-      for (int ni = 0; ni < 2; ++ni) {
-        const double2 v = Bs[ks + lk][wc + ni * 16 + lr];
-        br[ni] = v.x;
-        bim[ni] = v.y;
-      }
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni) {
-          acr[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[mi], br[ni], acr[mi][ni], 0, 0, 0);
-          aci[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[mi], bim[ni], aci[mi][ni], 0, 0, 0);
-        }
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni) {
-          acr[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(nai[mi], bim[ni], acr[mi][ni], 0, 0, 0);
-          aci[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[mi], br[ni], aci[mi][ni], 0, 0, 0);
-        }
-    }
-    __syncthreads();
-  }
-#pragma unroll
-  for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        C[(int64_t)(wr + mi * 16 + lk + 4 * r) * ldc + wc + ni * 16 + lr] =
-            make_double2(acr[mi][ni][r], aci[mi][ni][r]);
-}
-
-// ---------------------------------------------------------------------------
 // Pivot step k of the blocked Gauss-Jordan (one launch per step, grid nb x nbatch):
 // every block inverts the 64x64 pivot block S_kk in LDS (4 sub-steps of 16:
 // a wave-local 16x16 inversion through lane shuffles, then MFMA rank-16
@@ -187,33 +105,47 @@ __device__ __forceinline__ void tile_cgemm(const double2* __restrict__ A, int ld
 // ---------------------------------------------------------------------------
 
 // 16x16 complex block in one wave: lane l holds row l>>2, columns (l&3)*4..+3.
-__device__ __forceinline__ void wave_inv16(double2 (&a)[4], double* pm, int pbase) {
+// Row p and column p are exchanged through a per-wave LDS scratch (xb: 16
+// row + 16 column entries) between wavefront-scope fences; the update is
+// branch-free (selects instead of a divergent row-p path).  pm receives
+// |pivot|^2 (lane 0) when non-null.
+__device__ __forceinline__ void wave_inv16(double2 (&a)[4], double2* xb, double* pm, int pbase) {
   const int l = threadIdx.x & 63;
   const int r = l >> 2, cq = l & 3;
 #pragma unroll
   for (int p = 0; p < 16; ++p) {
     const int ps = p >> 2, pe = p & 3;
-    double2 piv, colp, rowp[4];
-    piv.x = __shfl(a[pe].x, p * 4 + ps, 64);
-    piv.y = __shfl(a[pe].y, p * 4 + ps, 64);
-    colp.x = __shfl(a[pe].x, r * 4 + ps, 64);
-    colp.y = __shfl(a[pe].y, r * 4 + ps, 64);
+    const bool prow = (r == p);
+    if (prow) {
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) xb[cq * 4 + jj] = a[jj];
+    }
+    if (cq == ps) xb[16 + r] = a[pe];
+    // cross-lane hand-off: the fences are compiler ordering points (a plain
+    // predicated store/load pair may legally be reordered for other lanes)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const double2 piv = xb[p];
+    const double2 colp = xb[16 + r];
+    double2 rowp[4];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) rowp[jj] = xb[cq * 4 + jj];
+    const double2 inv = cinv_fast(piv);
+    if (pm != nullptr && l == 0) pm[pbase + p] = piv.x * piv.x + piv.y * piv.y;
+    // row p: a <- rowp * inv ; other rows: a <- a - (colp*inv) * rowp
+    const double2 fi = cmul(colp, inv);
+    const double2 g = prow ? make_double2(-inv.x, -inv.y) : fi;
+    const double2 pc = prow ? inv : make_double2(-fi.x, -fi.y);   // new value in column p
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
-      rowp[jj].x = __shfl(a[jj].x, p * 4 + cq, 64);
-      rowp[jj].y = __shfl(a[jj].y, p * 4 + cq, 64);
+      const double2 base = prow ? make_double2(0.0, 0.0) : a[jj];
+      const double2 v = csub(base, cmul(g, rowp[jj]));
+      a[jj] = (cq * 4 + jj == p) ? pc : v;
     }
-    const double2 inv = cinv(piv);
-    if (pm != nullptr && l == 0) pm[pbase + p] = piv.x * piv.x + piv.y * piv.y;
-    if (r == p) {
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) a[jj] = (cq * 4 + jj == p) ? inv : cmul(rowp[jj], inv);
-    } else {
-      const double2 fi = cmul(colp, inv);
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj)
-        a[jj] = (cq * 4 + jj == p) ? make_double2(-fi.x, -fi.y) : csub(a[jj], cmul(fi, rowp[jj]));
-    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
 }
 
@@ -264,6 +196,7 @@ __global__ __launch_bounds__(256) void k_gj_pivot(double2* __restrict__ M, int64
   __shared__ double2 Cs[kGJ * 17];         // column sub-panel copy (row stride 17: no bank conflicts)
   __shared__ double2 Dw[4][16 * 17];       // per-wave copy of the 16x16 sub-block inverse
   __shared__ double2 Bs[16][kGJ];          // staging of S_kj for the panel product
+  __shared__ double2 xbw[4][32];           // per-wave row/column exchange of wave_inv16
   __shared__ double pm[kGJ];
   const int j = blockIdx.x, bi = blockIdx.y;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
@@ -271,7 +204,19 @@ __global__ __launch_bounds__(256) void k_gj_pivot(double2* __restrict__ M, int64
   double2* Mb = M + (int64_t)bi * mat;
   const double2* Skk = Mb + (int64_t)(k * kGJ) * Np + k * kGJ;
   DWH_STAMP(0);
-  for (int e = tid; e < kGJ * kGJ; e += 256) A[(e >> 6) * kLdA + (e & 63)] = Skk[(int64_t)(e >> 6) * Np + (e & 63)];
+  {
+    double2 v[16];   // all 16 loads in flight before the LDS stores
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int e = tid + 256 * u;
+      v[u] = Skk[(int64_t)(e >> 6) * Np + (e & 63)];
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int e = tid + 256 * u;
+      A[(e >> 6) * kLdA + (e & 63)] = v[u];
+    }
+  }
   __syncthreads();
   DWH_STAMP(1);
 
@@ -282,7 +227,7 @@ __global__ __launch_bounds__(256) void k_gj_pivot(double2* __restrict__ M, int64
     double2 dv[4];
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) dv[jj] = A[(o + (l >> 2)) * kLdA + o + (l & 3) * 4 + jj];
-    wave_inv16(dv, w == 0 ? pm : nullptr, o);
+    wave_inv16(dv, xbw[w], w == 0 ? pm : nullptr, o);
     if (kb == 0) DWH_STAMP(2);
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) Dw[w][(l >> 2) * 17 + (l & 3) * 4 + jj] = dv[jj];
@@ -332,7 +277,7 @@ __global__ __launch_bounds__(256) void k_gj_pivot(double2* __restrict__ M, int64
   DWH_STAMP(5);
 
   if (j == k) {
-    double2* Pb = Pbuf + (int64_t)bi * kGJ * kGJ;
+    double2* Pb = Pbuf + (size_t)(k & 1) * gridDim.y * kGJ * kGJ + (int64_t)bi * kGJ * kGJ;
     for (int e = tid; e < kGJ * kGJ; e += 256) Pb[e] = A[(e >> 6) * kLdA + (e & 63)];
     if (nb == 1) {
       double2* Sk = Mb + (int64_t)(k * kGJ) * Np + k * kGJ;
@@ -344,11 +289,21 @@ __global__ __launch_bounds__(256) void k_gj_pivot(double2* __restrict__ M, int64
     }
     return;
   }
-  // column-panel copy S_jk -> Cpanel[j]
-  {
+  // column-panel copy S_jk -> Cpanel(k)[j]: only at k == 0; for k > 0 the
+  // update of step k-1 wrote it (tiles J = k) and the row-panel tile of the
+  // previous pivot wrote block j = k-1 (below).
+  double2* CpK = Cpanel + (size_t)(k & 1) * gridDim.y * Np * kGJ + (int64_t)bi * Np * kGJ;
+  if (k == 0) {
     const double2* Sjk = Mb + (int64_t)(j * kGJ) * Np + k * kGJ;
-    double2* dst = Cpanel + (int64_t)bi * Np * kGJ + (int64_t)j * kGJ * kGJ;
-    for (int e = tid; e < kGJ * kGJ; e += 256) dst[e] = Sjk[(int64_t)(e >> 6) * Np + (e & 63)];
+    double2* dst = CpK + (int64_t)j * kGJ * kGJ;
+    double2 v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int e = tid + 256 * u;
+      v[u] = Sjk[(int64_t)(e >> 6) * Np + (e & 63)];
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) dst[tid + 256 * u] = v[u];
   }
   DWH_STAMP(6);
   // row-panel tile X_kj = A * S_kj (in place): 4 waves x (32x32) outputs
@@ -365,10 +320,7 @@ __global__ __launch_bounds__(256) void k_gj_pivot(double2* __restrict__ M, int64
 #pragma unroll 1
   for (int kc = 0; kc < kGJ; kc += 16) {
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int kk = tid >> 4, col = (tid & 15) * 4 + s;
-      Bs[kk][col] = Skj[(int64_t)(kc + kk) * Np + col];
-    }
+    for (int s4 = 0; s4 < 4; ++s4) Bs[tid >> 4][(tid & 15) * 4 + s4] = Skj[(int64_t)(kc + (tid >> 4)) * Np + (tid & 15) * 4 + s4];
     __syncthreads();
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi)
@@ -378,60 +330,69 @@ __global__ __launch_bounds__(256) void k_gj_pivot(double2* __restrict__ M, int64
                          &Bs[0][wc + ni * 16], kGJ);
     __syncthreads();
   }
+  // X_{k,k+1} is also column block k+1's entry for row block k: next step's Cpanel
+  double2* CpN = (j == k + 1) ? Cpanel + (size_t)((k + 1) & 1) * gridDim.y * Np * kGJ +
+                                    (int64_t)bi * Np * kGJ + (int64_t)k * kGJ * kGJ
+                              : nullptr;
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
     for (int ni = 0; ni < 2; ++ni)
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        Skj[(int64_t)(wr + mi * 16 + lk + 4 * r) * Np + wc + ni * 16 + lr] =
-            make_double2(acr[mi][ni][r], aci[mi][ni][r]);
+      for (int r = 0; r < 4; ++r) {
+        const int row = wr + mi * 16 + lk + 4 * r, col = wc + ni * 16 + lr;
+        const double2 v = make_double2(acr[mi][ni][r], aci[mi][ni][r]);
+        Skj[(int64_t)row * Np + col] = v;
+        if (CpN) CpN[row * kGJ + col] = v;
+      }
   DWH_STAMP(7);
 }
 
-// Trailing update: S_IJ = [J != k] S_IJ - Cpanel_I X_kJ for every tile I != k,
-// X_kJ = S_kJ (row panel, already scaled) and X_kk = Pbuf; the block with the
-// smallest I at J = k also stores Pbuf into S_kk (nobody reads S_kk here).
-__global__ __launch_bounds__(256) void k_gj_update(double2* __restrict__ M, int64_t mat, int Np,
-                                                   int nb, int k, const double2* __restrict__ Cpanel,
-                                                   const double2* __restrict__ Pbuf) {
-  __shared__ double2 At[16][kGJ];
-  __shared__ double2 Bs[16][kGJ];
-  const int bi = blockIdx.y;
-  const int t = blockIdx.x;
-  const int Ii = t / nb, J = t - Ii * nb;
-  const int I = Ii < k ? Ii : Ii + 1;
-  double2* Mb = M + (int64_t)bi * mat;
-  const double2* Ci = Cpanel + (int64_t)bi * Np * kGJ + (int64_t)I * kGJ * kGJ;
-  const double2* Pb = Pbuf + (int64_t)bi * kGJ * kGJ;
-  const bool jk = (J == k);
-  tile_cgemm<true, true>(Ci, kGJ, jk ? Pb : Mb + (int64_t)(k * kGJ) * Np + J * kGJ, jk ? kGJ : Np,
-                         Mb + (int64_t)(I * kGJ) * Np + J * kGJ, Np, jk, At, Bs);
-  if (jk && Ii == 0) {
-    double2* Sk = Mb + (int64_t)(k * kGJ) * Np + k * kGJ;
-    for (int e = threadIdx.x; e < kGJ * kGJ; e += blockDim.x) Sk[(int64_t)(e >> 6) * Np + (e & 63)] = Pb[e];
-  }
-}
-
-// Trailing update, variant 2: no LDS and no barriers.  Each wave owns a
+// Trailing update S_IJ = [J != k] S_IJ - Cpanel_I X_kJ for every tile I != k
+// (X_kJ = S_kJ, the scaled row panel; X_kk = Pbuf).  No LDS and no barriers.  Each wave owns a
 // 32x32 complex sub-tile and loads its MFMA fragments straight from L2 into
 // registers with a two-deep software prefetch (one k-step = 16 MFMAs = 1024
 // issue cycles, enough to cover an L2 hit).  1D grid with an XCD-aware remap:
 // consecutive work items (same batch matrix, i.e. the same A/B panels) land on
 // one XCD so the panels stay in that XCD's 4 MB L2 (placement is speed only).
-__global__ __launch_bounds__(256) void k_gj_update2(double2* __restrict__ M, int64_t mat, int Np,
-                                                    int nb, int k, int total,
-                                                    const double2* __restrict__ Cpanel,
+__global__ __launch_bounds__(256) void k_gj_update(double2* __restrict__ M, int64_t mat, int Np,
+                                                    int nb, int k, int mode, int nbatch, int total,
+                                                    double2* __restrict__ Cpanel,
                                                     const double2* __restrict__ Pbuf) {
-  const int tiles = (nb - 1) * nb;
+  // tiles of one matrix in this launch: mode 0 all (I != k); mode 1 the
+  // lookahead edge (block row k+1 and block column k+1); mode 2 the rest
+  const int tiles = mode == 0 ? (nb - 1) * nb : mode == 1 ? 2 * nb - 2 : (nb - 2) * (nb - 1);
   const int item = xcd_remap(blockIdx.x, total);
   const int bi = item / tiles, t = item - bi * tiles;
-  const int Ii = t / nb, J = t - Ii * nb;
-  const int I = Ii < k ? Ii : Ii + 1;
+  int I, J;
+  if (mode == 0) {
+    const int Ii = t / nb;
+    J = t - Ii * nb;
+    I = Ii < k ? Ii : Ii + 1;
+  } else if (mode == 1) {
+    if (t < nb) {
+      I = k + 1;
+      J = t;
+    } else {
+      const int u = t - nb;
+      I = u < k ? u : u + 2;
+      J = k + 1;
+    }
+  } else {
+    const int Ii = t / (nb - 1), Jj = t - Ii * (nb - 1);
+    I = Ii < k ? Ii : Ii + 2;
+    J = Jj < k + 1 ? Jj : Jj + 1;
+  }
+  const int Ii = (I == (k == 0 ? 1 : 0)) ? 0 : 1;   // 0 marks the block that stores S_kk = P
   const bool jk = (J == k);
   double2* Mb = M + (int64_t)bi * mat;
-  const double2* A = Cpanel + (int64_t)bi * Np * kGJ + (int64_t)I * kGJ * kGJ;       // [64][64]
-  const double2* B = jk ? Pbuf + (int64_t)bi * kGJ * kGJ : Mb + (int64_t)(k * kGJ) * Np + J * kGJ;
+  const size_t cstride = (size_t)nbatch * Np * kGJ;
+  const double2* A = Cpanel + (size_t)(k & 1) * cstride + (int64_t)bi * Np * kGJ + (int64_t)I * kGJ * kGJ;
+  double2* Cnext = (J == k + 1) ? Cpanel + (size_t)((k + 1) & 1) * cstride + (int64_t)bi * Np * kGJ +
+                                      (int64_t)I * kGJ * kGJ
+                                : nullptr;
+  const double2* Pb = Pbuf + (size_t)(k & 1) * nbatch * kGJ * kGJ + (int64_t)bi * kGJ * kGJ;
+  const double2* B = jk ? Pb : Mb + (int64_t)(k * kGJ) * Np + J * kGJ;
   const int ldb = jk ? kGJ : Np;
   double2* C = Mb + (int64_t)(I * kGJ) * Np + J * kGJ;
   const int tid = threadIdx.x;
@@ -496,12 +457,14 @@ __global__ __launch_bounds__(256) void k_gj_update2(double2* __restrict__ M, int
 #pragma unroll
     for (int ni = 0; ni < 2; ++ni)
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr)
-        C[(int64_t)(wr + mi * 16 + lk + 4 * rr) * Np + wc + ni * 16 + lr] =
-            make_double2(acr[mi][ni][rr], aci[mi][ni][rr]);
+      for (int rr = 0; rr < 4; ++rr) {
+        const int row = wr + mi * 16 + lk + 4 * rr, col = wc + ni * 16 + lr;
+        const double2 v = make_double2(acr[mi][ni][rr], aci[mi][ni][rr]);
+        C[(int64_t)row * Np + col] = v;
+        if (Cnext) Cnext[row * kGJ + col] = v;   // column panel of step k+1
+      }
   if (jk && Ii == 0) {
     __syncthreads();
-    const double2* Pb = Pbuf + (int64_t)bi * kGJ * kGJ;
     double2* Sk = Mb + (int64_t)(k * kGJ) * Np + k * kGJ;
     for (int e = tid; e < kGJ * kGJ; e += blockDim.x) Sk[(int64_t)(e >> 6) * Np + (e & 63)] = Pb[e];
   }
@@ -843,19 +806,19 @@ void launch_gj_pivot(const Dims& d, double2* M, int k, double2* Pbuf, double2* C
   hipLaunchKernelGGL(k_gj_pivot, dim3(d.nb, d.nbatch), dim3(256), 0, s, M, d.mat, d.Np, d.nb, k,
                      Pbuf, Cpanel, ldpart);
 }
-int gj_update_tiles(const Dims& d) { return d.nb < 2 ? 0 : (d.nb - 1) * d.nb; }
-void launch_gj_update(const Dims& d, double2* M, int k, const double2* Cpanel, const double2* Pbuf,
-                      hipStream_t s) {
-  const int tiles = gj_update_tiles(d);
+int gj_update_tiles(const Dims& d, int mode) {
+  if (d.nb < 2) return 0;
+  if (mode == 0) return (d.nb - 1) * d.nb;
+  if (mode == 1) return 2 * d.nb - 2;
+  return (d.nb - 2) * (d.nb - 1);
+}
+void launch_gj_update(const Dims& d, double2* M, int k, int mode, double2* Cpanel,
+                      const double2* Pbuf, hipStream_t s) {
+  const int tiles = gj_update_tiles(d, mode);
   if (tiles <= 0) return;
-  if (d.update_variant == 1) {
-    hipLaunchKernelGGL(k_gj_update, dim3(tiles, d.nbatch), dim3(256), 0, s, M, d.mat, d.Np, d.nb, k,
-                       Cpanel, Pbuf);
-  } else {
-    const int total = tiles * d.nbatch;
-    hipLaunchKernelGGL(k_gj_update2, dim3(total), dim3(256), 0, s, M, d.mat, d.Np, d.nb, k, total,
-                       Cpanel, Pbuf);
-  }
+  const int total = tiles * d.nbatch;
+  hipLaunchKernelGGL(k_gj_update, dim3(total), dim3(256), 0, s, M, d.mat, d.Np, d.nb, k, mode,
+                     d.nbatch, total, Cpanel, Pbuf);
 }
 void launch_assemble(const Dims& d, const double2* R, double2* T, double2* S, const int* Dcol,
                      const int* Dsrc, const double2* Delta, const int* hcol, const double* hval,

@@ -19,15 +19,15 @@ int main(int argc, char** argv) {
       for (int j = 0; j < d.Np; ++j)
         h[(size_t)b * d.mat + (size_t)i * d.Np + j] = make_double2(0.05 * U(g), (i == j ? -3.0 : 0.0) + 0.05 * U(g));
   double2 *M, *P, *C; double* ld;
-  hipMalloc(&M, h.size() * 16); hipMalloc(&P, (size_t)nbatch * 4096 * 16);
-  hipMalloc(&C, (size_t)nbatch * d.Np * 64 * 16); hipMalloc(&ld, nbatch * d.nb * 8);
+  hipMalloc(&M, h.size() * 16); hipMalloc(&P, 2 * (size_t)nbatch * 4096 * 16);
+  hipMalloc(&C, 2 * (size_t)nbatch * d.Np * 64 * 16); hipMalloc(&ld, nbatch * d.nb * 8);
   hipMemcpy(M, h.data(), h.size() * 16, hipMemcpyHostToDevice);
   hipEvent_t e0, e1, e2; hipEventCreate(&e0); hipEventCreate(&e1); hipEventCreate(&e2);
   for (int rep = 0; rep < 3; ++rep) {
     hipEventRecord(e0);
     launch_gj_pivot(d, M, 0, P, C, ld, 0);
     hipEventRecord(e1);
-    launch_gj_update(d, M, 0, C, P, 0);
+    launch_gj_update(d, M, 0, 0, C, P, 0);
     hipEventRecord(e2);
     hipEventSynchronize(e2);
     float t1, t2; hipEventElapsedTime(&t1, e0, e1); hipEventElapsedTime(&t2, e1, e2);
