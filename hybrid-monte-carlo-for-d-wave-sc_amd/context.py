@@ -161,8 +161,17 @@ class FermionContext:
         return s.value or 0
 
     # -- timing ----------------------------------------------------------
-    def timing_enable(self, on: bool = True):
-        self._c(self._lib.dwh_timing_enable(self._h, 1 if on else 0))
+    TIMERS = ("gj_update", "gj_pivot", "assemble", "contract", "step")
+
+    def timing_enable(self, on=True):
+        """on: True (all timers), False, or an iterable of timer names."""
+        if on is True:
+            mask = -1
+        elif not on:
+            mask = 0
+        else:
+            mask = sum(1 << self.TIMERS.index(n) for n in on)
+        self._c(self._lib.dwh_timing_enable(self._h, mask))
 
     def timing_reset(self):
         self._c(self._lib.dwh_timing_reset(self._h))

@@ -90,7 +90,7 @@ struct dwh_ctx {
   std::vector<void*> allocations;
 
   // timing
-  bool timing = false;
+  int timing = 0;   // bitmask over TimerName (bit i = kTimerNames[i])
   std::vector<TimingRec> recs;
   std::vector<hipEvent_t> pool;
   double t_ms[T_COUNT] = {0};
@@ -143,15 +143,16 @@ struct Scope {
   double work;
   hipStream_t st;
   hipEvent_t a{};
+  bool on;
   Scope(dwh_ctx* c, int n, double w, hipStream_t s = nullptr)
-      : ctx(c), name(n), work(w), st(s ? s : c->stream) {
-    if (ctx->timing) {
+      : ctx(c), name(n), work(w), st(s ? s : c->stream), on(((c->timing >> n) & 1) != 0) {
+    if (on) {
       a = take_event(ctx);
       (void)hipEventRecord(a, st);
     }
   }
   ~Scope() {
-    if (ctx->timing) {
+    if (on) {
       hipEvent_t b = take_event(ctx);
       (void)hipEventRecord(b, st);
       ctx->recs.push_back({name, a, b, work});
@@ -789,7 +790,7 @@ int dwh_stream(dwh_ctx* ctx, void** stream) {
 int dwh_timing_enable(dwh_ctx* ctx, int32_t enable) {
   if (!ctx) return DWH_ERR_ARG;
   drain_timing(ctx);
-  ctx->timing = enable != 0;
+  ctx->timing = enable;
   return DWH_OK;
 }
 

@@ -119,7 +119,10 @@ int dwh_synchronize(dwh_ctx* ctx);
 /* hipStream_t the context launches on (for events / interop). */
 int dwh_stream(dwh_ctx* ctx, void** stream);
 
-/* Kernel timing with HIP events on the context stream (bench/profiling). */
+/* Kernel timing with HIP events on the stream each kernel runs on
+ * (bench/profiling).  enable is a bitmask over the timer names below
+ * (bit 0 "gj_update", bit 1 "gj_pivot", bit 2 "assemble", bit 3 "contract",
+ * bit 4 "step"); 0 disables, -1 times everything. */
 int dwh_timing_enable(dwh_ctx* ctx, int32_t enable);
 /* name: "gj_update", "gj_pivot", "assemble", "contract", "step";
  * returns total milliseconds, launches and algorithmic flops (or bytes) per
