@@ -53,10 +53,7 @@ struct DevBuf {
 
 struct dwh_ctx {
   int device = 0;
-  hipStream_t stream = nullptr;   // main stream
-  hipStream_t side = nullptr;     // high-priority stream: GJ pivot of step k+1 (lookahead)
-  hipEvent_t ev_edge = nullptr, ev_pivot = nullptr;
-  bool lookahead = true;
+  hipStream_t stream = nullptr;
   Dims d{};
   int64_t Lx = 0, Ly = 0;
   double t = 0, tp = 0, mu = 0, beta = 0, J = 0, delta_cap = 2.0;
@@ -67,7 +64,10 @@ struct dwh_ctx {
   std::string err;
 
   // device buffers
-  double2 *R = nullptr, *T = nullptr, *S = nullptr, *Cpanel = nullptr, *Pinv = nullptr;
+  double2 *R = nullptr, *T = nullptr, *S = nullptr;
+  // Gauss-Jordan panels: column panels CpA[2] (parity), CpB; row panels XR1/XR2; pivots Pb1/Pb2
+  double2 *CpA0 = nullptr, *CpA1 = nullptr, *CpB = nullptr, *XR1 = nullptr, *XR2 = nullptr,
+          *Pb1 = nullptr, *Pb2 = nullptr;
   double2 *G12nn = nullptr, *diagS = nullptr;
   double *ldpart = nullptr, *ldstatic = nullptr, *d_y = nullptr, *d_c = nullptr;
   int *Dcol = nullptr, *Dsrc = nullptr, *hcol = nullptr, *bond_ij = nullptr, *bond_ji = nullptr;
@@ -91,6 +91,7 @@ struct dwh_ctx {
 
   // timing
   int timing = 0;   // bitmask over TimerName (bit i = kTimerNames[i])
+  bool gj_pair = true;   // DWHMC_GJ_PAIR=0: one rank-64 update per pivot step (A/B knob)
   std::vector<TimingRec> recs;
   std::vector<hipEvent_t> pool;
   double t_ms[T_COUNT] = {0};
@@ -144,8 +145,8 @@ struct Scope {
   hipStream_t st;
   hipEvent_t a{};
   bool on;
-  Scope(dwh_ctx* c, int n, double w, hipStream_t s = nullptr)
-      : ctx(c), name(n), work(w), st(s ? s : c->stream), on(((c->timing >> n) & 1) != 0) {
+  Scope(dwh_ctx* c, int n, double w)
+      : ctx(c), name(n), work(w), st(c->stream), on(((c->timing >> n) & 1) != 0) {
     if (on) {
       a = take_event(ctx);
       (void)hipEventRecord(a, st);
@@ -163,7 +164,6 @@ struct Scope {
 void drain_timing(dwh_ctx* ctx) {
   if (ctx->recs.empty()) return;
   (void)hipStreamSynchronize(ctx->stream);
-  (void)hipStreamSynchronize(ctx->side);
   for (auto& r : ctx->recs) {
     float ms = 0.f;
     (void)hipEventElapsedTime(&ms, r.a, r.b);
@@ -178,41 +178,65 @@ void drain_timing(dwh_ctx* ctx) {
 
 double tile_flops() { return 8.0 * kGJ * kGJ * kGJ; }
 
-void gj_pivot(dwh_ctx* ctx, double2* M, int k, hipStream_t st) {
+void gj_pivot(dwh_ctx* ctx, double2* M, int k, double2* Pout, double2* XR, double2* colcopy,
+              double2* nextcol) {
   const Dims& d = ctx->d;
-  Scope s(ctx, T_GJ_PIVOT, (double)d.nbatch * d.nb * tile_flops(), st);
-  dwh::launch_gj_pivot(d, M, k, ctx->Pinv, ctx->Cpanel, ctx->ldpart, st);
+  Scope s(ctx, T_GJ_PIVOT, (double)d.nbatch * d.nb * tile_flops());
+  dwh::launch_gj_pivot(d, M, k, Pout, XR, colcopy, nextcol, ctx->ldpart, ctx->stream);
 }
 
-void gj_update(dwh_ctx* ctx, double2* M, int k, int mode) {
-  const Dims& d = ctx->d;
-  Scope s(ctx, T_GJ_UPDATE, (double)d.nbatch * dwh::gj_update_tiles(d, mode) * tile_flops());
-  dwh::launch_gj_update(d, M, k, mode, ctx->Cpanel, ctx->Pinv, ctx->stream);
+// complex K=64 terms of one update launch (per matrix), for the flop count
+double gj_update_terms(const Dims& d, int mode) {
+  const int nb = d.nb;
+  if (nb < 2) return 0;
+  if (mode == 0) return (double)(nb - 1) * nb;
+  if (mode == 1) return 2.0 * nb - 2;
+  return nb + (double)(nb - 2) * (1 + 2.0 * (nb - 1));
 }
 
-// Blocked no-pivot Gauss-Jordan inversion of all nbatch matrices in M.  Per
-// block step k: a pivot launch (S_kk^-1 in every block, row panel) and a
-// trailing update.  Lookahead: the update's edge tiles (block row/col k+1)
-// run first; the pivot of step k+1 then runs on the high-priority side stream
-// while the rest of update k runs on the main stream (the pivot kernel uses
-// LDS, the update registers, so their blocks can share a CU).  Pbuf and the
-// column panel are double-buffered by step parity.  Opt-in: DWHMC_LOOKAHEAD=1.
+void gj_update(dwh_ctx* ctx, double2* M, int k, int mode, const dwh::GJPanelPtrs& p) {
+  const Dims& d = ctx->d;
+  Scope s(ctx, T_GJ_UPDATE, (double)d.nbatch * gj_update_terms(d, mode) * tile_flops());
+  dwh::launch_gj_update(d, M, k, mode, p, ctx->stream);
+}
+
+// Blocked no-pivot Gauss-Jordan inversion of all nbatch matrices in M, two
+// 64-wide block steps at a time: pivot k, edge update (block row k+1 and the
+// next column panel), pivot k+1, then ONE rank-128 update of the remaining
+// tiles — every matrix tile is streamed through HBM once per two pivot steps.
+// An odd last step uses the single rank-64 update.
 void run_gj(dwh_ctx* ctx, double2* M) {
   const Dims& d = ctx->d;
-  gj_pivot(ctx, M, 0, ctx->stream);
-  for (int k = 0; k < d.nb; ++k) {
-    if (d.nb < 2) break;
-    if (ctx->lookahead && k + 1 < d.nb) {
-      gj_update(ctx, M, k, 1);
-      (void)hipEventRecord(ctx->ev_edge, ctx->stream);
-      (void)hipStreamWaitEvent(ctx->side, ctx->ev_edge, 0);
-      gj_pivot(ctx, M, k + 1, ctx->side);
-      (void)hipEventRecord(ctx->ev_pivot, ctx->side);
-      gj_update(ctx, M, k, 2);
-      (void)hipStreamWaitEvent(ctx->stream, ctx->ev_pivot, 0);
+  double2* CpA[2] = {ctx->CpA0, ctx->CpA1};
+  if (d.nb == 1) {
+    gj_pivot(ctx, M, 0, ctx->Pb1, ctx->XR1, nullptr, nullptr);
+    return;
+  }
+  int cur = 0;
+  for (int k = 0; k < d.nb;) {
+    double2* colcopy = (k == 0) ? CpA[cur] : nullptr;
+    if (!ctx->gj_pair) {
+      double2* nxt = k + 1 < d.nb ? CpA[cur ^ 1] : nullptr;
+      gj_pivot(ctx, M, k, ctx->Pb1, ctx->XR1, colcopy, nxt);
+      dwh::GJPanelPtrs sg{CpA[cur], nullptr, ctx->XR1, nullptr, ctx->Pb1, nullptr, nullptr, nxt};
+      gj_update(ctx, M, k, 0, sg);
+      cur ^= 1;
+      k += 1;
+    } else if (k + 1 < d.nb) {
+      gj_pivot(ctx, M, k, ctx->Pb1, ctx->XR1, colcopy, nullptr);
+      dwh::GJPanelPtrs e{CpA[cur], nullptr, ctx->XR1, nullptr, ctx->Pb1, nullptr, ctx->CpB, nullptr};
+      gj_update(ctx, M, k, 1, e);
+      gj_pivot(ctx, M, k + 1, ctx->Pb2, ctx->XR2, nullptr, CpA[cur ^ 1]);
+      dwh::GJPanelPtrs c{CpA[cur], ctx->CpB, ctx->XR1, ctx->XR2, ctx->Pb1, ctx->Pb2, nullptr,
+                         k + 2 < d.nb ? CpA[cur ^ 1] : nullptr};
+      gj_update(ctx, M, k, 2, c);
+      cur ^= 1;
+      k += 2;
     } else {
-      gj_update(ctx, M, k, 0);
-      if (k + 1 < d.nb) gj_pivot(ctx, M, k + 1, ctx->stream);
+      gj_pivot(ctx, M, k, ctx->Pb1, ctx->XR1, colcopy, nullptr);
+      dwh::GJPanelPtrs sg{CpA[cur], nullptr, ctx->XR1, nullptr, ctx->Pb1, nullptr, nullptr, nullptr};
+      gj_update(ctx, M, k, 0, sg);
+      k += 1;
     }
   }
 }
@@ -424,6 +448,7 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
   ctx->beta = beta;
   ctx->J = J;
   ctx->delta_cap = delta_cap;
+  if (const char* e = std::getenv("DWHMC_GJ_PAIR")) ctx->gj_pair = std::atoi(e) != 0;
   ctx->kappa = kappa;
   ctx->Ebound = Ep;
   ctx->hmax = hmax;
@@ -449,17 +474,8 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     ctx->err = "hipSetDevice failed";
     return bail(DWH_ERR_HIP);
   }
-  // lookahead is opt-in: measured slower on MI355X because the pivot blocks
-  // (LDS + ~190 VGPR/wave) find no SIMD room next to 3 update waves and queue
-  const char* la = std::getenv("DWHMC_LOOKAHEAD");
-  ctx->lookahead = (la && la[0] == '1');
-  int prio_lo = 0, prio_hi = 0;
-  (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, prio_hi) != hipSuccess ||
-      hipEventCreateWithFlags(&ctx->ev_edge, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&ctx->ev_pivot, hipEventDisableTiming) != hipSuccess) {
-    ctx->err = "hipStream/hipEvent create failed";
+  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+    ctx->err = "hipStreamCreate failed";
     return bail(DWH_ERR_HIP);
   }
   const size_t nmat = (size_t)d.nbatch * d.mat;
@@ -470,8 +486,14 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
   ALLOC(R, nmat);
   ALLOC(T, nmat);
   ALLOC(S, nmat);
-  ALLOC(Cpanel, 2 * (size_t)d.nbatch * d.Np * kGJ);
-  ALLOC(Pinv, 2 * (size_t)d.nbatch * kGJ * kGJ);
+  const size_t npanel = (size_t)d.nbatch * d.Np * kGJ;
+  ALLOC(CpA0, npanel);
+  ALLOC(CpA1, npanel);
+  ALLOC(CpB, npanel);
+  ALLOC(XR1, npanel);
+  ALLOC(XR2, npanel);
+  ALLOC(Pb1, (size_t)d.nbatch * kGJ * kGJ);
+  ALLOC(Pb2, (size_t)d.nbatch * kGJ * kGJ);
   ALLOC(G12nn, (size_t)d.nbatch * N * kSlots);
   ALLOC(diagS, (size_t)d.nbatch * N);
   ALLOC(ldpart, (size_t)d.nbatch * d.nb);
@@ -566,11 +588,7 @@ void dwh_destroy(dwh_ctx* ctx) {
     (void)hipEventDestroy(r.b);
   }
   for (auto e : ctx->pool) (void)hipEventDestroy(e);
-  if (ctx->side) (void)hipStreamSynchronize(ctx->side);
   for (void* p : ctx->allocations) (void)hipFree(p);
-  if (ctx->ev_edge) (void)hipEventDestroy(ctx->ev_edge);
-  if (ctx->ev_pivot) (void)hipEventDestroy(ctx->ev_pivot);
-  if (ctx->side) (void)hipStreamDestroy(ctx->side);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }

@@ -23,17 +23,21 @@ struct Dims {
 // dense h - i y_q (padded with identity) for every (chain, pole): R init input
 void launch_fill_hz(const Dims& d, double2* M, const int* hcol, const double* hval,
                     const double* ypole, hipStream_t s);
-// Gauss-Jordan block step k on all nbatch matrices in M (in place, no pivoting):
-// pivot (invert S_kk in every block, row panel), then update.  Cpanel holds two
-// parity buffers of nbatch x Np x 64: step k reads buffer k&1 and the update
-// of step k fills buffer (k+1)&1 (the next column panel).
-void launch_gj_pivot(const Dims& d, double2* M, int k, double2* Pbuf, double2* Cpanel,
-                     double* ldpart, hipStream_t s);
-// mode 0: every tile I != k; 1: lookahead edge (block row/col k+1); 2: the rest.
-// Pbuf holds two parity buffers of nbatch x 64 x 64 (step k uses k&1).
+// Blocked Gauss-Jordan (no pivoting) on all nbatch matrices in M, in pairs of
+// 64-wide block steps (see k_gj_update in dwhmc_kernels.hip for the modes).
+// pivot: every block inverts S_kk; block j writes X_kj = S_kk^-1 S_kj in place
+// and to XRout; block k writes S_kk^-1 to Pout; colcopy (nullable) receives the
+// column panel of block column k; nextcol (nullable) receives X_{k,k+1} as row
+// block k of the next column panel.
+void launch_gj_pivot(const Dims& d, double2* M, int k, double2* Pout, double2* XRout,
+                     double2* colcopy, double2* nextcol, double* ldpart, hipStream_t s);
+struct GJPanelPtrs {
+  const double2 *CpA, *CpB, *XR1, *XR2, *Pb1, *Pb2;
+  double2 *CpBw, *CpN;
+};
 int gj_update_tiles(const Dims& d, int mode);
-void launch_gj_update(const Dims& d, double2* M, int k, int mode, double2* Cpanel,
-                      const double2* Pbuf, hipStream_t s);
+void launch_gj_update(const Dims& d, double2* M, int k, int mode, const GJPanelPtrs& p,
+                      hipStream_t s);
 // T = R D and S^T = -(h + i y) - (D† R D)^T for every (chain, pole)
 void launch_assemble(const Dims& d, const double2* R, double2* T, double2* S, const int* Dcol,
                      const int* Dsrc, const double2* Delta, const int* hcol, const double* hval,

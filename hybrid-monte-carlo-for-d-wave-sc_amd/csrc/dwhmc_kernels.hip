@@ -99,7 +99,7 @@ __global__ __launch_bounds__(256) void k_fill_hz(double2* __restrict__ M, int64_
 // every block inverts the 64x64 pivot block S_kk in LDS (4 sub-steps of 16:
 // a wave-local 16x16 inversion through lane shuffles, then MFMA rank-16
 // updates), then block j != k forms its row-panel tile X_kj = S_kk^-1 S_kj in
-// place and copies the column-panel tile S_jk to Cpanel; block k stores
+// place (and into the row-panel buffer); block k stores
 // S_kk^-1 to Pbuf and the pivots' ln|u_pp|.  The redundant inversions cost
 // latency only (all blocks run concurrently) and remove the serial diag launch.
 // ---------------------------------------------------------------------------
@@ -188,8 +188,10 @@ __device__ unsigned long long g_stamps[4096][8];
 #endif
 
 __global__ __launch_bounds__(256) void k_gj_pivot(double2* __restrict__ M, int64_t mat, int Np,
-                                                  int nb, int k, double2* __restrict__ Pbuf,
-                                                  double2* __restrict__ Cpanel,
+                                                  int nb, int k, double2* __restrict__ Pout,
+                                                  double2* __restrict__ XRout,
+                                                  double2* __restrict__ colcopy,
+                                                  double2* __restrict__ nextcol,
                                                   double* __restrict__ ldpart) {
   __shared__ double2 A[kGJ * kLdA];        // the pivot block, inverted in place
   __shared__ double2 Xs[16 * kGJ];         // row sub-panel of the current sub-step
@@ -277,7 +279,7 @@ __global__ __launch_bounds__(256) void k_gj_pivot(double2* __restrict__ M, int64
   DWH_STAMP(5);
 
   if (j == k) {
-    double2* Pb = Pbuf + (size_t)(k & 1) * gridDim.y * kGJ * kGJ + (int64_t)bi * kGJ * kGJ;
+    double2* Pb = Pout + (int64_t)bi * kGJ * kGJ;
     for (int e = tid; e < kGJ * kGJ; e += 256) Pb[e] = A[(e >> 6) * kLdA + (e & 63)];
     if (nb == 1) {
       double2* Sk = Mb + (int64_t)(k * kGJ) * Np + k * kGJ;
@@ -289,13 +291,11 @@ __global__ __launch_bounds__(256) void k_gj_pivot(double2* __restrict__ M, int64
     }
     return;
   }
-  // column-panel copy S_jk -> Cpanel(k)[j]: only at k == 0; for k > 0 the
-  // update of step k-1 wrote it (tiles J = k) and the row-panel tile of the
-  // previous pivot wrote block j = k-1 (below).
-  double2* CpK = Cpanel + (size_t)(k & 1) * gridDim.y * Np * kGJ + (int64_t)bi * Np * kGJ;
-  if (k == 0) {
+  // column-panel copy S_jk -> colcopy[j] (first step only; later steps get
+  // their column panel from the previous update)
+  if (colcopy != nullptr) {
     const double2* Sjk = Mb + (int64_t)(j * kGJ) * Np + k * kGJ;
-    double2* dst = CpK + (int64_t)j * kGJ * kGJ;
+    double2* dst = colcopy + (int64_t)bi * Np * kGJ + (int64_t)j * kGJ * kGJ;
     double2 v[16];
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
@@ -330,10 +330,11 @@ __global__ __launch_bounds__(256) void k_gj_pivot(double2* __restrict__ M, int64
                          &Bs[0][wc + ni * 16], kGJ);
     __syncthreads();
   }
-  // X_{k,k+1} is also column block k+1's entry for row block k: next step's Cpanel
-  double2* CpN = (j == k + 1) ? Cpanel + (size_t)((k + 1) & 1) * gridDim.y * Np * kGJ +
-                                    (int64_t)bi * Np * kGJ + (int64_t)k * kGJ * kGJ
-                              : nullptr;
+  // X_{k,k+1} is also row block k of the next column panel (nextcol)
+  double2* CpN = (j == k + 1 && nextcol != nullptr)
+                     ? nextcol + (int64_t)bi * Np * kGJ + (int64_t)k * kGJ * kGJ
+                     : nullptr;
+  double2* XRt = XRout ? XRout + (int64_t)bi * kGJ * Np + j * kGJ : nullptr;
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
@@ -343,100 +344,42 @@ __global__ __launch_bounds__(256) void k_gj_pivot(double2* __restrict__ M, int64
         const int row = wr + mi * 16 + lk + 4 * r, col = wc + ni * 16 + lr;
         const double2 v = make_double2(acr[mi][ni][r], aci[mi][ni][r]);
         Skj[(int64_t)row * Np + col] = v;
+        if (XRt) XRt[(int64_t)row * Np + col] = v;
         if (CpN) CpN[row * kGJ + col] = v;
       }
   DWH_STAMP(7);
 }
 
-// Trailing update S_IJ = [J != k] S_IJ - Cpanel_I X_kJ for every tile I != k
-// (X_kJ = S_kJ, the scaled row panel; X_kk = Pbuf).  No LDS and no barriers.  Each wave owns a
-// 32x32 complex sub-tile and loads its MFMA fragments straight from L2 into
-// registers with a two-deep software prefetch (one k-step = 16 MFMAs = 1024
-// issue cycles, enough to cover an L2 hit).  1D grid with an XCD-aware remap:
-// consecutive work items (same batch matrix, i.e. the same A/B panels) land on
-// one XCD so the panels stay in that XCD's 4 MB L2 (placement is speed only).
-__global__ __launch_bounds__(256) void k_gj_update(double2* __restrict__ M, int64_t mat, int Np,
-                                                    int nb, int k, int mode, int nbatch, int total,
-                                                    double2* __restrict__ Cpanel,
-                                                    const double2* __restrict__ Pbuf) {
-  // tiles of one matrix in this launch: mode 0 all (I != k); mode 1 the
-  // lookahead edge (block row k+1 and block column k+1); mode 2 the rest
-  const int tiles = mode == 0 ? (nb - 1) * nb : mode == 1 ? 2 * nb - 2 : (nb - 2) * (nb - 1);
-  const int item = xcd_remap(blockIdx.x, total);
-  const int bi = item / tiles, t = item - bi * tiles;
-  int I, J;
-  if (mode == 0) {
-    const int Ii = t / nb;
-    J = t - Ii * nb;
-    I = Ii < k ? Ii : Ii + 1;
-  } else if (mode == 1) {
-    if (t < nb) {
-      I = k + 1;
-      J = t;
-    } else {
-      const int u = t - nb;
-      I = u < k ? u : u + 2;
-      J = k + 1;
-    }
-  } else {
-    const int Ii = t / (nb - 1), Jj = t - Ii * (nb - 1);
-    I = Ii < k ? Ii : Ii + 2;
-    J = Jj < k + 1 ? Jj : Jj + 1;
-  }
-  const int Ii = (I == (k == 0 ? 1 : 0)) ? 0 : 1;   // 0 marks the block that stores S_kk = P
-  const bool jk = (J == k);
-  double2* Mb = M + (int64_t)bi * mat;
-  const size_t cstride = (size_t)nbatch * Np * kGJ;
-  const double2* A = Cpanel + (size_t)(k & 1) * cstride + (int64_t)bi * Np * kGJ + (int64_t)I * kGJ * kGJ;
-  double2* Cnext = (J == k + 1) ? Cpanel + (size_t)((k + 1) & 1) * cstride + (int64_t)bi * Np * kGJ +
-                                      (int64_t)I * kGJ * kGJ
-                                : nullptr;
-  const double2* Pb = Pbuf + (size_t)(k & 1) * nbatch * kGJ * kGJ + (int64_t)bi * kGJ * kGJ;
-  const double2* B = jk ? Pb : Mb + (int64_t)(k * kGJ) * Np + J * kGJ;
-  const int ldb = jk ? kGJ : Np;
-  double2* C = Mb + (int64_t)(I * kGJ) * Np + J * kGJ;
-  const int tid = threadIdx.x;
-  const int w = tid >> 6, l = tid & 63;
-  const int wr = (w >> 1) * 32, wc = (w & 1) * 32;
-  const int lr = l & 15, lk = l >> 4;
-  const double2* Ap0 = A + (wr + lr) * kGJ + lk;
-  const double2* Ap1 = Ap0 + 16 * kGJ;
-  const double2* Bp0 = B + (int64_t)lk * ldb + wc + lr;
-  const double2* Bp1 = Bp0 + 16;
-  // prefetch k-steps 0 and 1
-  double2 a0[2], a1[2], b0[2], b1[2];
-  a0[0] = Ap0[0]; a1[0] = Ap1[0]; b0[0] = Bp0[0]; b1[0] = Bp1[0];
-  a0[1] = Ap0[4]; a1[1] = Ap1[4]; b0[1] = Bp0[(int64_t)4 * ldb]; b1[1] = Bp1[(int64_t)4 * ldb];
-  d4 acr[2][2], aci[2][2];
+// One wave's 32x32 share of  acc -= sum_h A_h B_h  (NT terms, K = 64 each).
+// Per-lane fragment pointers; fully unrolled with a two-deep register
+// prefetch that runs across the term boundary.
+struct GemmTerm {
+  const double2* a;   // &A[wr + lr][lk]
+  const double2* b;   // &B[lk][wc + lr]
+  int lda, ldb;
+};
+
+template <int NT>
+__device__ __forceinline__ void tile_nt_gemm(d4 (&acr)[2][2], d4 (&aci)[2][2], const GemmTerm& t0,
+                                             const GemmTerm& t1) {
+  constexpr int NS = 16 * NT;
+  double2 fa[2][2], fb[2][2];
+  auto load = [&](int s, double2 (&a)[2], double2 (&b)[2]) {
+    const GemmTerm& t = (s >= 16) ? t1 : t0;
+    const int kk = (s & 15) * 4;
+    a[0] = t.a[kk];
+    a[1] = t.a[(int64_t)16 * t.lda + kk];
+    b[0] = t.b[(int64_t)kk * t.ldb];
+    b[1] = t.b[(int64_t)kk * t.ldb + 16];
+  };
+  load(0, fa[0], fb[0]);
+  load(1, fa[1], fb[1]);
 #pragma unroll
-  for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < 2; ++ni) {
-      if (!jk) {
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          const double2 v = C[(int64_t)(wr + mi * 16 + lk + 4 * rr) * Np + wc + ni * 16 + lr];
-          acr[mi][ni][rr] = v.x;
-          aci[mi][ni][rr] = v.y;
-        }
-      } else {
-        acr[mi][ni] = d4{0.0, 0.0, 0.0, 0.0};
-        aci[mi][ni] = d4{0.0, 0.0, 0.0, 0.0};
-      }
-    }
-#pragma unroll
-  for (int ks = 0; ks < 16; ++ks) {
-    const int cur = ks & 1;
-    const double2 av[2] = {a0[cur], a1[cur]};
-    const double2 bv[2] = {b0[cur], b1[cur]};
-    if (ks + 2 < 16) {
-      const int kn = (ks + 2) * 4;
-      a0[cur] = Ap0[kn];
-      a1[cur] = Ap1[kn];
-      b0[cur] = Bp0[(int64_t)kn * ldb];
-      b1[cur] = Bp1[(int64_t)kn * ldb];
-    }
-    // C -= A B  ->  feed -A
+  for (int s = 0; s < NS; ++s) {
+    const int c = s & 1;
+    const double2 av[2] = {fa[c][0], fa[c][1]};
+    const double2 bv[2] = {fb[c][0], fb[c][1]};
+    if (s + 2 < NS) load(s + 2, fa[c], fb[c]);
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
@@ -452,6 +395,130 @@ __global__ __launch_bounds__(256) void k_gj_update(double2* __restrict__ M, int6
         aci[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av[mi].y, bv[ni].x, aci[mi][ni], 0, 0, 0);
       }
   }
+}
+
+// Trailing updates of the blocked Gauss-Jordan, one 64x64 tile per block:
+//   out = init - sum_h A_h * B_h   (h = 1 or 2 terms of K = 64 each)
+// Each wave owns a 32x32 sub-tile; MFMA fragments come straight from L2 into
+// registers with a two-deep prefetch (no LDS, no barriers).  1D grid with an
+// XCD-aware remap so one matrix's panels stay in one XCD's L2.
+//
+// Panels (per batch item): CpA = column panel of block column k (rows I != k),
+// CpB = column k+1 after the edge update, XR1/XR2 = row panels of pivots k /
+// k+1 (64 x Np, ld Np), Pb1/Pb2 = the pivot inverses.  Modes:
+//  0 SINGLE  (step k):       I != k:  out = [J!=k]S_IJ - CpA_I*(J==k ? Pb1 : XR1_J)
+//  1 EDGE    (pair k,k+1):   row k+1: S_{k+1,J} = [J!=k]S_{k+1,J} - CpA_{k+1}*(J==k ? Pb1 : XR1_J)
+//                            col k+1: CpB_I = S_{I,k+1} - CpA_I*XR1_{k+1}   (I != k, k+1)
+//  2 COMBINED (pair k,k+1):  rank-128 remainder of both steps, I != k+1:
+//     I == k : out = init_k - XR1_{k+1} * (J==k+1 ? Pb2 : XR2_J),
+//              init_k = J==k ? Pb1 : J==k+1 ? 0 : XR1_J
+//     I != k : out = [J!=k,k+1]S_IJ - CpA_I*(J==k ? Pb1 : J==k+1 ? 0 : XR1_J)
+//                                   - CpB_I*(J==k+1 ? Pb2 : XR2_J)
+// In modes 0/2 tiles of block column `ncol` (k+1 resp. k+2) are also written
+// to CpN, the next column panel; mode 0 stores S_kk = Pb1 and mode 2 stores
+// S_{k+1,k+1} = Pb2 from one designated tile.
+struct GJPanels {
+  const double2 *CpA, *CpB, *XR1, *XR2, *Pb1, *Pb2;
+  double2 *CpBw, *CpN;
+};
+
+template <int mode>
+__global__ __launch_bounds__(256) void k_gj_update(double2* __restrict__ M, int64_t mat, int Np,
+                                                   int nb, int k, int total, GJPanels pn) {
+  const int tiles = mode == 1 ? 2 * nb - 2 : (nb - 1) * nb;
+  const int item = xcd_remap(blockIdx.x, total);
+  const int bi = item / tiles, t = item - bi * tiles;
+  int I, J;
+  if (mode == 1) {
+    if (t < nb) {
+      I = k + 1;
+      J = t;
+    } else {
+      const int u = t - nb;
+      I = u < k ? u : u + 2;
+      J = k + 1;
+    }
+  } else {
+    const int skip = mode == 0 ? k : k + 1;
+    const int Ii = t / nb;
+    J = t - Ii * nb;
+    I = Ii < skip ? Ii : Ii + 1;
+  }
+  double2* Mb = M + (int64_t)bi * mat;
+  const int64_t pnl = (int64_t)bi * Np * kGJ;     // column panel / row panel batch offset
+  const int64_t pvb = (int64_t)bi * kGJ * kGJ;
+  auto colp = [&](const double2* base, int row) { return base + pnl + (int64_t)row * kGJ * kGJ; };
+  auto rowp = [&](const double2* base, int col) { return base + pnl + col * kGJ; };
+  // terms: A (64 x 64, lda), B (64 x 64, ldb); init source
+  const double2 *A0 = nullptr, *B0 = nullptr, *A1 = nullptr, *B1 = nullptr, *Cin = nullptr;
+  int lda0 = kGJ, ldb0 = Np, lda1 = kGJ, ldb1 = Np, ldc_in = Np;
+  double2* out = Mb + (int64_t)(I * kGJ) * Np + J * kGJ;
+  int ldo = Np;
+  double2* out2 = nullptr;
+  if (mode == 0) {
+    A0 = colp(pn.CpA, I);
+    if (J == k) { B0 = pn.Pb1 + pvb; ldb0 = kGJ; } else { B0 = rowp(pn.XR1, J); }
+    if (J != k) Cin = out;
+    if (J == k + 1 && pn.CpN) out2 = const_cast<double2*>(colp(pn.CpN, I));
+  } else if (mode == 1) {
+    A0 = colp(pn.CpA, I);
+    if (J == k) { B0 = pn.Pb1 + pvb; ldb0 = kGJ; } else { B0 = rowp(pn.XR1, J); }
+    if (I == k + 1) {
+      if (J != k) Cin = out;
+    } else {            // column k+1: result goes to CpB only
+      Cin = out;
+      out = const_cast<double2*>(colp(pn.CpBw, I));
+      ldo = kGJ;
+    }
+  } else {
+    if (I == k) {
+      A1 = rowp(pn.XR1, k + 1); lda1 = Np;
+      if (J == k + 1) { B1 = pn.Pb2 + pvb; ldb1 = kGJ; } else { B1 = rowp(pn.XR2, J); }
+      if (J == k) { Cin = pn.Pb1 + pvb; ldc_in = kGJ; }
+      else if (J != k + 1) { Cin = rowp(pn.XR1, J); }
+    } else {
+      if (J != k + 1) {
+        A0 = colp(pn.CpA, I);
+        if (J == k) { B0 = pn.Pb1 + pvb; ldb0 = kGJ; } else { B0 = rowp(pn.XR1, J); }
+      }
+      A1 = colp(pn.CpB, I);
+      if (J == k + 1) { B1 = pn.Pb2 + pvb; ldb1 = kGJ; } else { B1 = rowp(pn.XR2, J); }
+      if (J != k && J != k + 1) Cin = out;
+    }
+    if (J == k + 2 && pn.CpN) out2 = const_cast<double2*>(colp(pn.CpN, I));
+  }
+  if (A0 == nullptr) {   // single term in slot 1 -> move to slot 0
+    A0 = A1; B0 = B1; lda0 = lda1; ldb0 = ldb1;
+    A1 = nullptr;
+  }
+  const int tid = threadIdx.x;
+  const int w = tid >> 6, l = tid & 63;
+  const int wr = (w >> 1) * 32, wc = (w & 1) * 32;
+  const int lr = l & 15, lk = l >> 4;
+  d4 acr[2][2], aci[2][2];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) {
+      if (Cin != nullptr) {
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const double2 v = Cin[(int64_t)(wr + mi * 16 + lk + 4 * rr) * ldc_in + wc + ni * 16 + lr];
+          acr[mi][ni][rr] = v.x;
+          aci[mi][ni][rr] = v.y;
+        }
+      } else {
+        acr[mi][ni] = d4{0.0, 0.0, 0.0, 0.0};
+        aci[mi][ni] = d4{0.0, 0.0, 0.0, 0.0};
+      }
+    }
+  const GemmTerm t0{A0 + (int64_t)(wr + lr) * lda0 + lk, B0 + (int64_t)lk * ldb0 + wc + lr, lda0, ldb0};
+  if (A1 != nullptr) {
+    const GemmTerm t1{A1 + (int64_t)(wr + lr) * lda1 + lk, B1 + (int64_t)lk * ldb1 + wc + lr, lda1, ldb1};
+    tile_nt_gemm<2>(acr, aci, t0, t1);
+  } else {
+    tile_nt_gemm<1>(acr, aci, t0, t0);
+  }
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
@@ -460,12 +527,15 @@ __global__ __launch_bounds__(256) void k_gj_update(double2* __restrict__ M, int6
       for (int rr = 0; rr < 4; ++rr) {
         const int row = wr + mi * 16 + lk + 4 * rr, col = wc + ni * 16 + lr;
         const double2 v = make_double2(acr[mi][ni][rr], aci[mi][ni][rr]);
-        C[(int64_t)row * Np + col] = v;
-        if (Cnext) Cnext[row * kGJ + col] = v;   // column panel of step k+1
+        out[(int64_t)row * ldo + col] = v;
+        if (out2) out2[row * kGJ + col] = v;
       }
-  if (jk && Ii == 0) {
-    __syncthreads();
-    double2* Sk = Mb + (int64_t)(k * kGJ) * Np + k * kGJ;
+  // designated tile stores the pivot inverse into the diagonal block
+  const int dI = mode == 0 ? (k == 0 ? 1 : 0) : (k == 0 ? 0 : 0);
+  const int pk = mode == 0 ? k : k + 1;
+  if (mode != 1 && I == dI && J == pk) {
+    const double2* Pb = (mode == 0 ? pn.Pb1 : pn.Pb2) + pvb;
+    double2* Sk = Mb + (int64_t)(pk * kGJ) * Np + pk * kGJ;
     for (int e = tid; e < kGJ * kGJ; e += blockDim.x) Sk[(int64_t)(e >> 6) * Np + (e & 63)] = Pb[e];
   }
 }
@@ -801,24 +871,26 @@ void launch_fill_hz(const Dims& d, double2* M, const int* hcol, const double* hv
   hipLaunchKernelGGL(k_fill_hz, dim3(d.Np, d.nbatch), dim3(256), 0, s, M, d.mat, d.N, d.Np, d.P,
                      hcol, hval, ypole);
 }
-void launch_gj_pivot(const Dims& d, double2* M, int k, double2* Pbuf, double2* Cpanel,
-                     double* ldpart, hipStream_t s) {
+void launch_gj_pivot(const Dims& d, double2* M, int k, double2* Pout, double2* XRout,
+                     double2* colcopy, double2* nextcol, double* ldpart, hipStream_t s) {
   hipLaunchKernelGGL(k_gj_pivot, dim3(d.nb, d.nbatch), dim3(256), 0, s, M, d.mat, d.Np, d.nb, k,
-                     Pbuf, Cpanel, ldpart);
+                     Pout, XRout, colcopy, nextcol, ldpart);
 }
 int gj_update_tiles(const Dims& d, int mode) {
   if (d.nb < 2) return 0;
-  if (mode == 0) return (d.nb - 1) * d.nb;
-  if (mode == 1) return 2 * d.nb - 2;
-  return (d.nb - 2) * (d.nb - 1);
+  return mode == 1 ? 2 * d.nb - 2 : (d.nb - 1) * d.nb;
 }
-void launch_gj_update(const Dims& d, double2* M, int k, int mode, double2* Cpanel,
-                      const double2* Pbuf, hipStream_t s) {
+void launch_gj_update(const Dims& d, double2* M, int k, int mode, const GJPanelPtrs& p,
+                      hipStream_t s) {
   const int tiles = gj_update_tiles(d, mode);
   if (tiles <= 0) return;
   const int total = tiles * d.nbatch;
-  hipLaunchKernelGGL(k_gj_update, dim3(total), dim3(256), 0, s, M, d.mat, d.Np, d.nb, k, mode,
-                     d.nbatch, total, Cpanel, Pbuf);
+  GJPanels pn{p.CpA, p.CpB, p.XR1, p.XR2, p.Pb1, p.Pb2, p.CpBw, p.CpN};
+  switch (mode) {
+    case 0: hipLaunchKernelGGL(k_gj_update<0>, dim3(total), dim3(256), 0, s, M, d.mat, d.Np, d.nb, k, total, pn); break;
+    case 1: hipLaunchKernelGGL(k_gj_update<1>, dim3(total), dim3(256), 0, s, M, d.mat, d.Np, d.nb, k, total, pn); break;
+    default: hipLaunchKernelGGL(k_gj_update<2>, dim3(total), dim3(256), 0, s, M, d.mat, d.Np, d.nb, k, total, pn); break;
+  }
 }
 void launch_assemble(const Dims& d, const double2* R, double2* T, double2* S, const int* Dcol,
                      const int* Dsrc, const double2* Delta, const int* hcol, const double* hval,

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Interleaved in-process A/B of context variants (env knobs read at create):
-python tools/ab_bench.py --L 32 --beta 16 --variants "LA=0" "LA=1,SC=0" "LA=1,SC=32"
-UPD -> DWHMC_UPDATE (trailing-update kernel variant).  Prints ms per leapfrog step
+python tools/ab_bench.py --L 32 --beta 16 --variants "PAIR=1" "PAIR=0"
+PAIR -> DWHMC_GJ_PAIR (paired rank-128 Gauss-Jordan updates or one rank-64
+update per pivot step).  Prints ms per leapfrog step
 (median / min over rounds) and the per-kernel event totals of the last round."""
 import argparse
 import math
@@ -23,7 +24,7 @@ def main():
     ap.add_argument("--Nt", type=int, default=10)
     ap.add_argument("--sweeps", type=int, default=3)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--variants", nargs="+", default=["LA=1"])
+    ap.add_argument("--variants", nargs="+", default=["PAIR=1", "PAIR=0"])
     a = ap.parse_args()
     import dwhmc_loader
     from oracle import dwhmc_oracle as O
@@ -42,9 +43,7 @@ def main():
     ctxs = {}
     for v in a.variants:
         kv = dict(x.split("=") for x in v.split(",") if x)
-        os.environ["DWHMC_LOOKAHEAD"] = kv.get("LA", "1")
-        os.environ["DWHMC_SIDE_CUS"] = kv.get("SC", "32")
-        os.environ["DWHMC_UPDATE"] = kv.get("UPD", "2")
+        os.environ["DWHMC_GJ_PAIR"] = kv.get("PAIR", "1")
         ctx = m.FermionContext(p.Lx, p.Ly, p.t, p.tp, p.mu, p.beta, p.J, p.nn_table, p.nnn_table,
                                np.stack(dis))
         ctx.set_pairing(np.stack(D0))

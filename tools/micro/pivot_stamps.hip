@@ -25,9 +25,9 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1, e2; hipEventCreate(&e0); hipEventCreate(&e1); hipEventCreate(&e2);
   for (int rep = 0; rep < 3; ++rep) {
     hipEventRecord(e0);
-    launch_gj_pivot(d, M, 0, P, C, ld, 0);
+    launch_gj_pivot(d, M, 0, P, C, C, nullptr, ld, 0);
     hipEventRecord(e1);
-    launch_gj_update(d, M, 0, 0, C, P, 0);
+    { GJPanelPtrs pp{C, nullptr, C, nullptr, P, nullptr, nullptr, nullptr}; launch_gj_update(d, M, 0, 0, pp, 0); }
     hipEventRecord(e2);
     hipEventSynchronize(e2);
     float t1, t2; hipEventElapsedTime(&t1, e0, e1); hipEventElapsedTime(&t2, e1, e2);
