@@ -87,17 +87,31 @@ def load(build_if_missing: bool = True) -> C.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    if build_if_missing and _build.needs_build():
-        _build.build()
-    if not os.path.exists(_build.LIB):
-        raise DwhError(DWH_ERR_HIP, f"{_build.LIB} missing: run __graft_entry__.build()")
-    lib = C.CDLL(_build.LIB)
-    for name, (res, args) in SIGNATURES.items():
-        fn = getattr(lib, name)
-        fn.restype = res
-        fn.argtypes = args
-    _lib = lib
-    return lib
+    path = os.environ.get("DWHMC_LIB")   # A/B builds of kernel variants (tools/)
+    if path is None:
+        if build_if_missing and _build.needs_build():
+            _build.build()
+        path = _build.LIB
+    if not os.path.exists(path):
+        raise DwhError(DWH_ERR_HIP, f"{path} missing: run __graft_entry__.build()")
+    _lib = load_path(path)
+    return _lib
+
+
+_variants: dict = {}
+
+
+def load_path(path: str) -> C.CDLL:
+    """Load a specific build of the library (A/B variants in tools/)."""
+    path = os.path.abspath(path)
+    if path not in _variants:
+        lib = C.CDLL(path)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _variants[path] = lib
+    return _variants[path]
 
 
 def lib_path() -> str:

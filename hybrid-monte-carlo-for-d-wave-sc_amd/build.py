@@ -34,18 +34,27 @@ def needs_build() -> bool:
     return any(os.path.getmtime(p) > t for p in DEPS if os.path.exists(p))
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not needs_build():
+def build(force: bool = False, verbose: bool = False, out: str = LIB, defines=()) -> str:
+    """defines: extra -D flags for A/B builds of kernel variants (tools/ab_bench.py
+    loads such a build through DWHMC_LIB); the default build uses none."""
+    if not force and out == LIB and not needs_build():
         return LIB
-    tmp = LIB + ".tmp"
+    tmp = out + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-result", f"-I{os.path.join(ROOT, 'include')}", *SOURCES, "-o", tmp]
+           "-Wall", "-Wno-unused-result", f"-I{os.path.join(ROOT, 'include')}",
+           *[f"-D{d}" for d in defines], *SOURCES, "-o", tmp]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, out)
+    return out
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--out", default=LIB)
+    ap.add_argument("-D", dest="defines", action="append", default=[])
+    a = ap.parse_args()
+    print(build(force=a.force or a.out != LIB, verbose=True, out=a.out, defines=a.defines))

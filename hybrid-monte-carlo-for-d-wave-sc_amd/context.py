@@ -40,8 +40,8 @@ class FermionContext:
     """Device-resident fermionic action/force evaluator for nchains chains."""
 
     def __init__(self, Lx, Ly, t, tp, mu, beta, J, nn_table, nnn_table, disorder,
-                 delta_cap: float = 2.0, device: int = 0):
-        self._lib = _lib.load()
+                 delta_cap: float = 2.0, device: int = 0, lib_path: str | None = None):
+        self._lib = _lib.load() if lib_path is None else _lib.load_path(lib_path)
         dis = np.ascontiguousarray(np.atleast_2d(np.asarray(disorder, dtype=np.float64)))
         self.N = int(Lx) * int(Ly)
         if dis.shape[1] != self.N:

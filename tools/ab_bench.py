@@ -2,7 +2,9 @@
 """Interleaved in-process A/B of context variants (env knobs read at create):
 python tools/ab_bench.py --L 32 --beta 16 --variants "PAIR=1" "PAIR=0"
 PAIR -> DWHMC_GJ_PAIR (paired rank-128 Gauss-Jordan updates or one rank-64
-update per pivot step).  Prints ms per leapfrog step
+update per pivot step); LIB=path loads another build of the library
+(hybrid-monte-carlo-for-d-wave-sc_amd/build.py --out build/var/x.so -D ...) so
+kernel variants are compared in one process.  Prints ms per leapfrog step
 (median / min over rounds) and the per-kernel event totals of the last round."""
 import argparse
 import math
@@ -45,7 +47,7 @@ def main():
         kv = dict(x.split("=") for x in v.split(",") if x)
         os.environ["DWHMC_GJ_PAIR"] = kv.get("PAIR", "1")
         ctx = m.FermionContext(p.Lx, p.Ly, p.t, p.tp, p.mu, p.beta, p.J, p.nn_table, p.nnn_table,
-                               np.stack(dis))
+                               np.stack(dis), lib_path=kv.get("LIB"))
         ctx.set_pairing(np.stack(D0))
         ctx.factorize()
         ctx.load_draws(noise, uni)
