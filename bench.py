@@ -33,6 +33,27 @@ sys.path.insert(0, ROOT)
 
 METRIC = "fp64 leapfrog steps/sec at L=32, 1→8 MI355X; % fp64 MFMA roofline"
 PEAK_F64_TFLOPS = 78.6        # MI355X dense fp64 matrix peak (= fp64 vector peak on CDNA4)
+PEAK_HBM_GBS = 8000.0         # MI355X HBM3E peak (MI355X_MICROARCH.md)
+TRAFFIC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_pmc_traffic.json")
+
+
+def measured_traffic(kernel, L, beta, chains):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
+    (tools/pmc_summary.py: FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md
+    gfx950 correction) for this exact workload, else None.  PMC counters cannot
+    be read inside the timed run, so they come from their own profiled runs."""
+    try:
+        with open(TRAFFIC_FILE) as f:
+            rec = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    w = rec.get("workload", {})
+    if (w.get("L"), w.get("beta"), w.get("chains")) != (L, beta, chains):
+        return None, None
+    k = rec.get("kernels", {}).get(kernel)
+    if not k:
+        return None, None
+    return k["hbm_bytes_per_launch"], "profiles/" + os.path.basename(TRAFFIC_FILE)
 PEAK_HBM_GBS = 8000.0
 
 
@@ -125,7 +146,8 @@ def main():
         ctx.run_sweeps(0, n_warm, a.Nt, dt, p.mass)
     ctx.synchronize()
     if not a.no_timing:
-        ctx.timing_enable(["gj_update"])   # events only around the dominant kernel
+        # events only around the dominant kernel (and the once-per-factorize assembly)
+        ctx.timing_enable(["gj_update", "assemble"])
         ctx.timing_reset()
 
     if dist is not None:
@@ -147,6 +169,7 @@ def main():
     kern = {}
     if not a.no_timing:
         kern["gj_update"] = ctx.timing_read("gj_update")
+        kern["assemble"] = ctx.timing_read("assemble")
         ctx.timing_enable(False)
     # observables gather over RCCL (the only collective): acceptance and <dH>
     obs = np.array([acc.mean(), dH.mean(), float(np.mean(np.exp(-dH)))], dtype=np.float64)
@@ -188,12 +211,21 @@ def main():
         if kern:
             ms, n, w = kern["gj_update"]
             ach = w / n / (ms / n * 1e-3) / 1e12 if n and ms > 0 else None
-            rec["roofline"] = {"bound": "mfma", "kernel": "k_gj_update", "achieved": ach,
+            kname = "k_gj_update<2>" if info["N"] % 128 == 0 else "k_gj_update<2>+<0>"
+            traffic, tsrc = measured_traffic(kname, a.L, a.beta, a.chains)
+            rec["roofline"] = {"bound": "mfma", "kernel": kname, "achieved": ach,
                                "peak": PEAK_F64_TFLOPS, "unit": "TFLOP/s",
-                               "frac": ach / PEAK_F64_TFLOPS if ach else None, "traffic": None,
+                               "frac": ach / PEAK_F64_TFLOPS if ach else None, "traffic": traffic,
+                               "traffic_unit": "bytes/launch", "traffic_source": tsrc,
                                "avg_launch_us": 1000.0 * ms / n if n else None,
                                "flops_per_launch": w / n if n else None}
             rec["gj_update_ms_per_step"] = ms / a.steps
+            ms, n, w = kern["assemble"]
+            if n and ms > 0:
+                gbs = w / n / (ms / n * 1e-3) / 1e9
+                rec["assembly"] = {"bound": "hbm", "kernel": "k_assemble", "achieved": gbs,
+                                   "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS,
+                                   "bytes_per_launch": w / n, "avg_launch_us": 1000.0 * ms / n}
         if not a.no_cpu_baseline and world == 1:
             steps_cpu = a.cpu_steps or (3 if a.L >= 32 else 20)
             v, threads, el_cpu = cpu_baseline(O, p, D0[0], dis[0], steps_cpu)

@@ -161,7 +161,7 @@ class FermionContext:
         return s.value or 0
 
     # -- timing ----------------------------------------------------------
-    TIMERS = ("gj_update", "gj_pivot", "assemble", "contract", "step")
+    TIMERS = ("gj_update", "gj_pivot", "assemble", "contract", "step", "gj_edge")
 
     def timing_enable(self, on=True):
         """on: True (all timers), False, or an iterable of timer names."""

@@ -34,8 +34,8 @@ namespace {
 
 thread_local std::string g_create_error;
 
-enum TimerName { T_GJ_UPDATE = 0, T_GJ_PIVOT, T_ASSEMBLE, T_CONTRACT, T_STEP, T_COUNT };
-const char* kTimerNames[T_COUNT] = {"gj_update", "gj_pivot", "assemble", "contract", "step"};
+enum TimerName { T_GJ_UPDATE = 0, T_GJ_PIVOT, T_ASSEMBLE, T_CONTRACT, T_STEP, T_GJ_EDGE, T_COUNT };
+const char* kTimerNames[T_COUNT] = {"gj_update", "gj_pivot", "assemble", "contract", "step", "gj_edge"};
 
 struct TimingRec {
   int name;
@@ -64,7 +64,8 @@ struct dwh_ctx {
   std::string err;
 
   // device buffers
-  double2 *R = nullptr, *T = nullptr, *S = nullptr;
+  double2 *R = nullptr, *S = nullptr;
+  double2* Dv = nullptr;   // pairing values of D per chain (nc x N x kSlots)
   // Gauss-Jordan panels: column panels CpA[2] (parity), CpB; row panels XR1/XR2; pivots Pb1/Pb2
   double2 *CpA0 = nullptr, *CpA1 = nullptr, *CpB = nullptr, *XR1 = nullptr, *XR2 = nullptr,
           *Pb1 = nullptr, *Pb2 = nullptr;
@@ -196,7 +197,8 @@ double gj_update_terms(const Dims& d, int mode) {
 
 void gj_update(dwh_ctx* ctx, double2* M, int k, int mode, const dwh::GJPanelPtrs& p) {
   const Dims& d = ctx->d;
-  Scope s(ctx, T_GJ_UPDATE, (double)d.nbatch * gj_update_terms(d, mode) * tile_flops());
+  Scope s(ctx, mode == 1 ? T_GJ_EDGE : T_GJ_UPDATE,
+          (double)d.nbatch * gj_update_terms(d, mode) * tile_flops());
   dwh::launch_gj_update(d, M, k, mode, p, ctx->stream);
 }
 
@@ -245,15 +247,18 @@ void run_gj(dwh_ctx* ctx, double2* M) {
 void factorize_enqueue(dwh_ctx* ctx, double kick) {
   const Dims& d = ctx->d;
   Scope step(ctx, T_STEP, (double)d.nbatch * 8.0 * (double)d.N * d.N * d.N);
+  dwh::launch_dvals(d, ctx->Dsrc, ctx->Delta, ctx->Dv, ctx->stream);
   {
-    Scope s(ctx, T_ASSEMBLE, (double)d.nbatch * 48.0 * d.N * (double)d.N);
-    dwh::launch_assemble(d, ctx->R, ctx->T, ctx->S, ctx->Dcol, ctx->Dsrc, ctx->Delta, ctx->hcol,
-                         ctx->hval, ctx->d_y, ctx->stream);
+    // algorithmic bytes: read R once, write S^T
+    Scope s(ctx, T_ASSEMBLE, (double)d.nbatch * 32.0 * d.N * (double)d.N);
+    dwh::launch_assemble(d, ctx->R, ctx->S, ctx->Dcol, ctx->Dv, ctx->hcol, ctx->hval, ctx->d_y,
+                         ctx->stream);
   }
   run_gj(ctx, ctx->S);
   {
     Scope s(ctx, T_CONTRACT, (double)d.nbatch * 32.0 * d.N * (double)d.N);
-    dwh::launch_contract(d, ctx->T, ctx->S, ctx->Dcol, ctx->G12nn, ctx->diagS, ctx->stream);
+    dwh::launch_contract(d, ctx->R, ctx->S, ctx->Dcol, ctx->Dv, ctx->G12nn, ctx->diagS,
+                         ctx->stream);
   }
   dwh::launch_pair_force(d, ctx->G12nn, ctx->bond_ij, ctx->bond_ji, ctx->d_c, ctx->Delta,
                          ctx->Pair, ctx->F, ctx->Pi, kick, ctx->beta, ctx->J, ctx->stream);
@@ -484,8 +489,8 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
 #define ALLOC(p, n) \
   if ((rc = dalloc(ctx, &ctx->p, (n))) != DWH_OK) return bail(rc)
   ALLOC(R, nmat);
-  ALLOC(T, nmat);
   ALLOC(S, nmat);
+  ALLOC(Dv, (size_t)d.nc * N * kSlots);
   const size_t npanel = (size_t)d.nbatch * d.Np * kGJ;
   ALLOC(CpA0, npanel);
   ALLOC(CpA1, npanel);

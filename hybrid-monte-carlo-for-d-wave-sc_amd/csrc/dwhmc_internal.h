@@ -38,13 +38,16 @@ struct GJPanelPtrs {
 int gj_update_tiles(const Dims& d, int mode);
 void launch_gj_update(const Dims& d, double2* M, int k, int mode, const GJPanelPtrs& p,
                       hipStream_t s);
-// T = R D and S^T = -(h + i y) - (D† R D)^T for every (chain, pole)
-void launch_assemble(const Dims& d, const double2* R, double2* T, double2* S, const int* Dcol,
-                     const int* Dsrc, const double2* Delta, const int* hcol, const double* hval,
-                     const double* ypole, hipStream_t s);
-// G12 at the pairing pattern: G12nn[bi][i][s] = -(T S^{-1})[i, Dcol[i][s]]; diag of S^{-1}
-void launch_contract(const Dims& d, const double2* T, const double2* SinvT, const int* Dcol,
-                     double2* G12nn, double2* diagS, hipStream_t s);
+// Dv[c][r][s] = Δ_c[Dsrc[r][s]] / 2: the pairing values of D for every chain
+void launch_dvals(const Dims& d, const int* Dsrc, const double2* Delta, double2* Dv,
+                  hipStream_t s);
+// S^T = -(h + i y) - (D† R D)^T for every (chain, pole)
+void launch_assemble(const Dims& d, const double2* R, double2* S, const int* Dcol,
+                     const double2* Dv, const int* hcol, const double* hval, const double* ypole,
+                     hipStream_t s);
+// G12 at the pairing pattern: G12nn[bi][i][s] = -(R D S^{-1})[i, Dcol[i][s]]; diag of S^{-1}
+void launch_contract(const Dims& d, const double2* R, const double2* SinvT, const int* Dcol,
+                     const double2* Dv, double2* G12nn, double2* diagS, hipStream_t s);
 // P = Σ_q c_q (G12[i,j] + G12[j,i]); F = -β/2J (Δ - J P); π += kick·F
 void launch_pair_force(const Dims& d, const double2* G12nn, const int* bond_ij,
                        const int* bond_ji, const double* cpole, const double2* Delta,

@@ -541,24 +541,37 @@ __global__ __launch_bounds__(256) void k_gj_update(double2* __restrict__ M, int6
 }
 
 // ---------------------------------------------------------------------------
-// Assembly of T = R D and S^T for one row a (block) of one (chain, pole).
+// Pairing values of D for every chain, slot-major so that lanes indexed by
+// row load contiguously: Dv[c][s][r] = Δ_c[Dsrc[r][s]] / 2 (the reference's
+// overwrite order is resolved on the host into Dsrc).
+// ---------------------------------------------------------------------------
+__global__ void k_dvals(const int* __restrict__ Dsrc, const double2* __restrict__ Delta,
+                        double2* __restrict__ Dv, int N) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = blockIdx.y;
+  if (e >= N * kSlots) return;
+  const int src = Dsrc[e];
+  const double2 d = src >= 0 ? Delta[(int64_t)c * 2 * N + src] : make_double2(0.0, 0.0);
+  const int r = e / kSlots, sl = e - r * kSlots;
+  Dv[(int64_t)c * N * kSlots + (int64_t)sl * N + r] = make_double2(0.5 * d.x, 0.5 * d.y);
+}
+
+// ---------------------------------------------------------------------------
+// Assembly of S^T for one row a of one (chain, pole):
 //   TT[a,k]  = Σ_{l ∈ Dcol(a)} D[a,l] R[l,k]               (rows of R, coalesced)
 //   S^T[a,b] = -(h[a,b] + i y δ_ab) - Σ_{k ∈ Dcol(b)} TT[a,k] conj(D[b,k])
-//   T[a,b]   = Σ_{l ∈ Dcol(b)} R[a,l] D[b,l]
-// D[r, Dcol[r][s]] = Δ[Dsrc[r][s]] / 2 (reference overwrite order, host-built).
+// T = R D is not stored: k_contract rebuilds its rows from rows of R.
 // ---------------------------------------------------------------------------
+static_assert(kSlots == 4, "k_assemble / k_contract load the pairing pattern as int4");
 __global__ __launch_bounds__(256) void k_assemble(const double2* __restrict__ R,
-                                                  double2* __restrict__ T,
                                                   double2* __restrict__ S, int64_t mat, int N,
                                                   int Np, int P, const int* __restrict__ Dcol,
-                                                  const int* __restrict__ Dsrc,
-                                                  const double2* __restrict__ Delta,
+                                                  const double2* __restrict__ Dv,
                                                   const int* __restrict__ hcol,
                                                   const double* __restrict__ hval,
                                                   const double* __restrict__ ypole) {
   extern __shared__ double2 smem[];
   double2* TTrow = smem;
-  double2* Rrow = smem + Np;
   const int item = xcd_remap(blockIdx.x, gridDim.x);
   const int bi = item / Np, a = item - bi * Np;
   const int c = bi / P, q = bi % P;
@@ -569,15 +582,13 @@ __global__ __launch_bounds__(256) void k_assemble(const double2* __restrict__ R,
     return;
   }
   const double2* Rb = R + (int64_t)bi * mat;
-  const double2* Dc = Delta + (int64_t)c * 2 * N;
+  const double2* Dvc = Dv + (int64_t)c * N * kSlots;
   int lcol[kSlots];
   double2 dval[kSlots];
 #pragma unroll
   for (int s = 0; s < kSlots; ++s) {
     lcol[s] = Dcol[a * kSlots + s];
-    const int src = Dsrc[a * kSlots + s];
-    const double2 d = src >= 0 ? Dc[src] : make_double2(0.0, 0.0);
-    dval[s] = make_double2(0.5 * d.x, 0.5 * d.y);
+    dval[s] = Dvc[s * N + a];
   }
   __shared__ int hc[kHSlots];
   __shared__ double hv[kHSlots];
@@ -591,56 +602,73 @@ __global__ __launch_bounds__(256) void k_assemble(const double2* __restrict__ R,
     for (int s = 0; s < kSlots; ++s)
       if (lcol[s] >= 0) tt = cadd(tt, cmul(dval[s], Rb[(int64_t)lcol[s] * Np + kk]));
     TTrow[kk] = tt;
-    Rrow[kk] = Rb[(int64_t)a * Np + kk];
   }
   __syncthreads();
   const double y = ypole[q];
-  double2* Trow = T + (int64_t)bi * mat + (int64_t)a * Np;
   for (int b = threadIdx.x; b < Np; b += blockDim.x) {
-    double2 st = make_double2(0.0, 0.0), tv = make_double2(0.0, 0.0);
+    double2 st = make_double2(0.0, 0.0);
     if (b < N) {
+      const int4 kc4 = *reinterpret_cast<const int4*>(Dcol + b * kSlots);
+      const int kc[4] = {kc4.x, kc4.y, kc4.z, kc4.w};
 #pragma unroll
-      for (int s = 0; s < kSlots; ++s) {
-        const int kcol = Dcol[b * kSlots + s];
-        if (kcol >= 0) {
-          const int src = Dsrc[b * kSlots + s];
-          const double2 d0 = Dc[src];
-          const double2 db = make_double2(0.5 * d0.x, 0.5 * d0.y);
-          st = cadd(st, cmulc(TTrow[kcol], db));
-          tv = cadd(tv, cmul(Rrow[kcol], db));
-        }
-      }
+      for (int s = 0; s < kSlots; ++s)
+        if (kc[s] >= 0) st = cadd(st, cmulc(TTrow[kc[s]], Dvc[s * N + b]));
 #pragma unroll
       for (int s = 0; s < kHSlots; ++s)
         if (hc[s] == b) st.x += hv[s];
       if (b == a) st.y += y;
     }
     Srow[b] = make_double2(-st.x, -st.y);
-    Trow[b] = tv;
   }
 }
 
 // ---------------------------------------------------------------------------
 // Contraction: G12[i, j] = -Σ_k T[i,k] S^-1[k,j] = -Σ_k T[i,k] SinvT[j,k]
 // for the ≤4 pairing columns j of row i; plus diag(S^-1) for Tr ρ_hh.
+// T[i,k] = Σ_{l ∈ Dcol(k)} R[i,l] D[k,l] is rebuilt on the fly from row i of R
+// (staged in LDS), so T never goes through HBM.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_contract(const double2* __restrict__ T,
-                                                  const double2* __restrict__ SinvT, int64_t mat,
-                                                  int N, int Np, const int* __restrict__ Dcol,
-                                                  double2* __restrict__ G12nn,
-                                                  double2* __restrict__ diagS) {
+template <int NT, bool TWO_PASS>
+__global__ __launch_bounds__(NT) void k_contract(const double2* __restrict__ R,
+                                                 const double2* __restrict__ SinvT, int64_t mat,
+                                                 int N, int Np, int P, const int* __restrict__ Dcol,
+                                                 const double2* __restrict__ Dv,
+                                                 double2* __restrict__ G12nn,
+                                                 double2* __restrict__ diagS) {
+  constexpr int NW = NT / 64;
+  extern __shared__ double2 smem[];
+  double2* Rrow = smem;
+  double2* Trow = smem + Np;   // TWO_PASS only
   const int item = xcd_remap(blockIdx.x, gridDim.x);
   const int bi = item / N, i = item - bi * N;
-  const double2* Trow = T + (int64_t)bi * mat + (int64_t)i * Np;
+  const int c = bi / P;
+  const double2* Ri = R + (int64_t)bi * mat + (int64_t)i * Np;
   const double2* Sb = SinvT + (int64_t)bi * mat;
+  const double2* Dvc = Dv + (int64_t)c * N * kSlots;
+  for (int kk = threadIdx.x; kk < N; kk += NT) Rrow[kk] = Ri[kk];
   int js[kSlots];
 #pragma unroll
   for (int s = 0; s < kSlots; ++s) js[s] = Dcol[i * kSlots + s];
+  __syncthreads();
+  auto trow = [&](int kk) {
+    const int4 lc = *reinterpret_cast<const int4*>(Dcol + kk * kSlots);
+    const int ls[4] = {lc.x, lc.y, lc.z, lc.w};
+    double2 t = make_double2(0.0, 0.0);
+#pragma unroll
+    for (int s = 0; s < kSlots; ++s)
+      if (ls[s] >= 0) t = cadd(t, cmul(Rrow[ls[s]], Dvc[s * N + kk]));
+    return t;
+  };
+  if (TWO_PASS) {
+    for (int kk = threadIdx.x; kk < N; kk += NT) Trow[kk] = trow(kk);
+    __syncthreads();
+  }
   double acc[2 * kSlots];
 #pragma unroll
   for (int s = 0; s < 2 * kSlots; ++s) acc[s] = 0.0;
-  for (int kk = threadIdx.x; kk < N; kk += blockDim.x) {
-    const double2 t = Trow[kk];
+#pragma unroll 4
+  for (int kk = threadIdx.x; kk < N; kk += NT) {
+    const double2 t = TWO_PASS ? Trow[kk] : trow(kk);
 #pragma unroll
     for (int s = 0; s < kSlots; ++s) {
       if (js[s] >= 0) {
@@ -650,7 +678,7 @@ __global__ __launch_bounds__(256) void k_contract(const double2* __restrict__ T,
       }
     }
   }
-  __shared__ double red[4][2 * kSlots];
+  __shared__ double red[NW][2 * kSlots];
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
 #pragma unroll
   for (int s = 0; s < 2 * kSlots; ++s) {
@@ -660,7 +688,9 @@ __global__ __launch_bounds__(256) void k_contract(const double2* __restrict__ T,
   __syncthreads();
   if (threadIdx.x < 2 * kSlots) {
     const int s = threadIdx.x;
-    const double v = red[0][s] + red[1][s] + red[2][s] + red[3][s];
+    double v = 0.0;
+#pragma unroll
+    for (int ww = 0; ww < NW; ++ww) v += red[ww][s];
     double* out = reinterpret_cast<double*>(G12nn + ((int64_t)bi * N + i) * kSlots);
     out[s] = js[s >> 1] >= 0 ? -v : 0.0;
   }
@@ -892,17 +922,33 @@ void launch_gj_update(const Dims& d, double2* M, int k, int mode, const GJPanelP
     default: hipLaunchKernelGGL(k_gj_update<2>, dim3(total), dim3(256), 0, s, M, d.mat, d.Np, d.nb, k, total, pn); break;
   }
 }
-void launch_assemble(const Dims& d, const double2* R, double2* T, double2* S, const int* Dcol,
-                     const int* Dsrc, const double2* Delta, const int* hcol, const double* hval,
-                     const double* ypole, hipStream_t s) {
-  const size_t shm = 2 * (size_t)d.Np * sizeof(double2);
-  hipLaunchKernelGGL(k_assemble, dim3(d.Np * d.nbatch), dim3(256), shm, s, R, T, S, d.mat, d.N,
-                     d.Np, d.P, Dcol, Dsrc, Delta, hcol, hval, ypole);
+void launch_dvals(const Dims& d, const int* Dsrc, const double2* Delta, double2* Dv,
+                  hipStream_t s) {
+  hipLaunchKernelGGL(k_dvals, dim3((d.N * kSlots + 255) / 256, d.nc), dim3(256), 0, s, Dsrc, Delta,
+                     Dv, d.N);
 }
-void launch_contract(const Dims& d, const double2* T, const double2* SinvT, const int* Dcol,
-                     double2* G12nn, double2* diagS, hipStream_t s) {
-  hipLaunchKernelGGL(k_contract, dim3(d.N * d.nbatch), dim3(256), 0, s, T, SinvT, d.mat, d.N, d.Np,
-                     Dcol, G12nn, diagS);
+void launch_assemble(const Dims& d, const double2* R, double2* S, const int* Dcol,
+                     const double2* Dv, const int* hcol, const double* hval, const double* ypole,
+                     hipStream_t s) {
+  const size_t shm = (size_t)d.Np * sizeof(double2);
+#ifndef DWH_ASSEMBLE_NT
+#define DWH_ASSEMBLE_NT 256
+#endif
+  hipLaunchKernelGGL(k_assemble, dim3(d.Np * d.nbatch), dim3(DWH_ASSEMBLE_NT), shm, s, R, S, d.mat,
+                     d.N, d.Np, d.P, Dcol, Dv, hcol, hval, ypole);
+}
+void launch_contract(const Dims& d, const double2* R, const double2* SinvT, const int* Dcol,
+                     const double2* Dv, double2* G12nn, double2* diagS, hipStream_t s) {
+#ifndef DWH_CONTRACT_NT
+#define DWH_CONTRACT_NT 256
+#endif
+#ifndef DWH_CONTRACT_2P
+#define DWH_CONTRACT_2P false
+#endif
+  const size_t shm = (DWH_CONTRACT_2P ? 2 : 1) * (size_t)d.Np * sizeof(double2);
+  hipLaunchKernelGGL((k_contract<DWH_CONTRACT_NT, DWH_CONTRACT_2P>), dim3(d.N * d.nbatch),
+                     dim3(DWH_CONTRACT_NT), shm, s, R, SinvT, d.mat, d.N, d.Np, d.P, Dcol, Dv, G12nn,
+                     diagS);
 }
 void launch_pair_force(const Dims& d, const double2* G12nn, const int* bond_ij,
                        const int* bond_ji, const double* cpole, const double2* Delta,
