@@ -422,8 +422,11 @@ struct GJPanels {
   double2 *CpBw, *CpN;
 };
 
+#ifndef DWH_UPD_OCC
+#define DWH_UPD_OCC 1
+#endif
 template <int mode>
-__global__ __launch_bounds__(256) void k_gj_update(double2* __restrict__ M, int64_t mat, int Np,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DWH_UPD_OCC))) void k_gj_update(double2* __restrict__ M, int64_t mat, int Np,
                                                    int nb, int k, int total, GJPanels pn) {
   const int tiles = mode == 1 ? 2 * nb - 2 : (nb - 1) * nb;
   const int item = xcd_remap(blockIdx.x, total);
