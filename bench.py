@@ -54,7 +54,15 @@ def measured_traffic(kernel, L, beta, chains):
     if not k:
         return None, None
     return k["hbm_bytes_per_launch"], "profiles/" + os.path.basename(TRAFFIC_FILE)
-PEAK_HBM_GBS = 8000.0
+
+
+# BASELINE.json configs; the headline line is C3.
+PRESETS = {
+    "C2": dict(L=16, beta=8.0, chains=1, label="L=16 beta=8 single-chain HMC (BASELINE configs[1], C2)"),
+    "C3": dict(L=32, beta=16.0, chains=1, label="L=32 beta=16 single-chain HMC (BASELINE configs[2], C3)"),
+    "C4": dict(L=32, beta=16.0, chains=1, label="L=32 beta=16 one disorder replica per GPU (BASELINE configs[3], C4)"),
+    "C5": dict(L=48, beta=32.0, chains=4, label="L=48 beta=32 4 chains/GPU batched (BASELINE configs[4], C5)"),
+}
 
 
 def parse():
@@ -62,9 +70,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50, help="leapfrog steps timed (multiple of --Nt)")
     ap.add_argument("--warmup", type=int, default=10, help="untimed leapfrog steps (multiple of --Nt)")
-    ap.add_argument("--L", type=int, default=32)
-    ap.add_argument("--beta", type=float, default=16.0)
-    ap.add_argument("--chains", type=int, default=1, help="chains per GPU")
+    ap.add_argument("--config", choices=sorted(PRESETS), default=None,
+                    help="BASELINE config preset (default: C3, or C4 when launched on >1 GPU)")
+    ap.add_argument("--L", type=int, default=None)
+    ap.add_argument("--beta", type=float, default=None)
+    ap.add_argument("--chains", type=int, default=None, help="chains per GPU")
     ap.add_argument("--Nt", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=0, help="oracle leapfrog steps for the CPU leg (0 = auto)")
@@ -119,6 +129,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    preset = PRESETS[a.config or ("C4" if world > 1 else "C3")]
+    custom = any(getattr(a, k) not in (None, preset[k]) for k in ("L", "beta", "chains"))
+    for k in ("L", "beta", "chains"):
+        if getattr(a, k) is None:
+            setattr(a, k, preset[k])
+    workload = (f"L={a.L} beta={a.beta:g} {a.chains} chain(s)/GPU (custom)" if custom else preset["label"])
     if a.steps % a.Nt or a.warmup % a.Nt:
         raise SystemExit("--steps and --warmup must be multiples of --Nt")
     dist = None
@@ -199,8 +215,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic",
-            "config": {"workload": f"L={a.L} beta={a.beta:g} single-chain HMC (BASELINE configs[2], C3)"
-                       if a.chains == 1 else f"L={a.L} beta={a.beta:g} {a.chains} chains/GPU",
+            "config": {"workload": workload,
                        "L": a.L, "N": N, "bdg_dim": 2 * N, "beta": a.beta, "chains_per_gpu": a.chains,
                        "Nt": a.Nt, "dt": dt, "poles": P, "kappa": info["kappa"],
                        "parallelism": f"replicas x{world}" if world > 1 else "single GPU"},
@@ -211,7 +226,8 @@ def main():
         if kern:
             ms, n, w = kern["gj_update"]
             ach = w / n / (ms / n * 1e-3) / 1e12 if n and ms > 0 else None
-            kname = "k_gj_update<2>" if info["N"] % 128 == 0 else "k_gj_update<2>+<0>"
+            nb = -(-info["N"] // 64)                 # GJ block steps; odd nb ends with one rank-64 step
+            kname = "k_gj_update<2>" if nb % 2 == 0 else "k_gj_update<2>+<0>"
             traffic, tsrc = measured_traffic(kname, a.L, a.beta, a.chains)
             rec["roofline"] = {"bound": "mfma", "kernel": kname, "achieved": ach,
                                "peak": PEAK_F64_TFLOPS, "unit": "TFLOP/s",
@@ -227,7 +243,7 @@ def main():
                                    "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS,
                                    "bytes_per_launch": w / n, "avg_launch_us": 1000.0 * ms / n}
         if not a.no_cpu_baseline and world == 1:
-            steps_cpu = a.cpu_steps or (3 if a.L >= 32 else 20)
+            steps_cpu = a.cpu_steps or (1 if a.L >= 48 else 3 if a.L >= 32 else 20)
             v, threads, el_cpu = cpu_baseline(O, p, D0[0], dis[0], steps_cpu)
             rec["cpu_baseline"] = {"value": v, "unit": "leapfrog steps/s", "cores": threads,
                                    "kind": "port",

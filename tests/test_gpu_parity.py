@@ -76,6 +76,25 @@ def test_full_size_L32_beta16(dwhmc, oracle):
     ctx.close()
 
 
+def test_full_size_L48_beta32_batched(dwhmc, oracle):
+    """BASELINE config C5 size (N = 2304, n = 4608, β = 32), two batched
+    chains with different disorder, against the eigen oracle."""
+    O = oracle
+    cases = [make_case(O, 48, 48, 32.0, seed=s) for s in (4848, 4849)]
+    p = cases[0][0]
+    ctx = device_ctx(dwhmc, p, np.stack([c[1] for c in cases]))
+    assert ctx.info["npoles"] >= 15
+    ctx.set_pairing(np.stack([c[2] for c in cases]))
+    ctx.factorize()
+    F = ctx.forces()
+    Ef = ctx.fermion_energy()
+    for c, (pc, dc, Dc) in enumerate(cases):
+        _, F_ref, Ef_ref = O.evaluate(pc, dc, Dc)
+        assert np.max(np.abs(F[c] - F_ref)) <= 1e-10 * (1 + np.max(np.abs(F_ref)))
+        assert abs(Ef[c] - Ef_ref) <= 1e-11 * abs(Ef_ref)
+    ctx.close()
+
+
 def test_batched_chains_independent(dwhmc, oracle):
     O = oracle
     cases = [make_case(O, 6, 6, 8.0, seed=s) for s in (1, 2, 3)]
