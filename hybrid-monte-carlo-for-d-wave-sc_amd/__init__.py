@@ -5,6 +5,7 @@ Layout:
   _lib.py    ctypes binding of the ABI
   context.py FermionContext: batched device handle
   hmc.py     the reference's hot-path API (ModelParameters ... hmc_sweep)
+  simulation.py run_simulation (src/Simulation.jl): adaptive Nt, log, observables.csv
   replicas.py one-process-per-GPU replica driver (RCCL only gathers observables)
 
 The directory name is not a Python identifier; import it through
@@ -15,6 +16,7 @@ from .hmc import (ComputeCache, ModelParameters, ObservablesResult, SimulationSt
                   initialize_cache, initialize_state, measure_observables, neighbour_tables,
                   refresh_momentum, standard_complex_normal, update_H_BdG)
 from .context import FermionContext, selftest_mfma
+from .simulation import AdaptiveNt, SimulationResult, run_simulation
 from ._lib import DwhError, SpectrumGuardError, lib_path, load as load_library
 
 __all__ = [
@@ -22,5 +24,6 @@ __all__ = [
     "compute_forces", "compute_total_energy", "diagonalize_H_BdG", "hmc_sweep", "init_static_H",
     "initialize_cache", "initialize_state", "measure_observables", "neighbour_tables",
     "refresh_momentum", "standard_complex_normal", "update_H_BdG", "FermionContext", "selftest_mfma",
-    "DwhError", "SpectrumGuardError", "lib_path", "load_library",
+    "DwhError", "SpectrumGuardError", "lib_path", "load_library", "AdaptiveNt", "SimulationResult",
+    "run_simulation",
 ]

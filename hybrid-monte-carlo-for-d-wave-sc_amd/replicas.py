@@ -120,11 +120,4 @@ def write_observables_csv(path: str, records: np.ndarray):
                         (r, s + 1, int(x[0]), x[1], *x[2:]))
 
 
-def main():
-    """python -m torch.distributed.run --nproc-per-node N replicas.py via
-    tools/run_replicas.py (kept as a function for import-time safety)."""
-    raise SystemExit("use tools/run_replicas.py")
-
-
-if __name__ == "__main__":
-    main()
+# Launcher: tools/run_replicas.py (python -m torch.distributed.run ... tools/run_replicas.py)

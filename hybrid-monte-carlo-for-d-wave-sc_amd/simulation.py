@@ -1,0 +1,152 @@
+"""run_simulation: the reference's driver (src/Simulation.jl:34-236) over the
+MI355X hot path.
+
+Same phases, adaptive-Nt rule, log lines and observables.csv format as the
+reference; every sweep's fermionic work runs on the GPU through the C ABI
+(hmc.py -> FermionContext), and the lightweight measurements come from the
+factorisation outputs (P_ij, E_f, Tr ρ_hh; hmc.measure_observables).
+
+Not reproduced (out of the hot-path scope): the heavy
+transport/spectra measurement (`measure_transport_and_spectra`,
+src/Observables.jl:225-526, needs eigenvectors) — transport.csv gets its
+header only and the log says so — and the JLD2 spectra bins (no JLD2 writer in
+this image).  The reference's RNG is global and unseeded; here the caller
+passes `rng` (draw order per sweep: randn(ComplexF64, N, 2), then rand()).
+"""
+from __future__ import annotations
+
+import math
+import os
+import time
+from dataclasses import dataclass, field
+from datetime import datetime
+
+import numpy as np
+
+from . import hmc as H
+
+OBS_HEADER = ("Sweep,Accepted,dH,Energy,Delta_Amp,Delta_Loc,Delta_Glob,S_Delta,Hole_p,Delta_Diff,"
+              "Delta_Pair,Delta_LocalPair")
+TRANSPORT_HEADER = "Sweep,Superfluid_Stiffness,DC_Conductivity"
+
+
+def obs_csv_line(sweep: int, acc: bool, dH: float, obs: H.ObservablesResult) -> str:
+    """One observables.csv row, src/Simulation.jl:161-166 formats."""
+    return "%d,%d,%.5e,%.6f,%.6f,%.6f,%.6f,%.6f,%.6f,%.6f,%.6f,%.6f\n" % (
+        sweep, int(acc), dH, obs.total_energy, obs.Delta_amp, obs.Delta_local, obs.Delta_global,
+        obs.S_Delta, obs.hole_conc, obs.Delta_diff, obs.Delta_pair, obs.Delta_localpair)
+
+
+@dataclass
+class AdaptiveNt:
+    """Thermalisation step-count controller, src/Simulation.jl:103-129: every
+    `window` sweeps, acceptance < 0.60 -> Nt += 2; > 0.95 and Nt > 4 -> Nt -= 1."""
+    Nt: int
+    window: int = 5
+    recent: int = 0
+
+    def record(self, i: int, accepted: bool):
+        """Sweep i (1-based) finished.  Returns None between windows, else
+        (rate, old_Nt, new_Nt)."""
+        if accepted:
+            self.recent += 1
+        if i % self.window != 0:
+            return None
+        rate = self.recent / self.window
+        self.recent = 0
+        old = self.Nt
+        if rate < 0.60:
+            self.Nt += 2
+        elif rate > 0.95 and self.Nt > 4:
+            self.Nt -= 1
+        return rate, old, self.Nt
+
+
+@dataclass
+class SimulationResult:
+    Nt_final: int
+    therm_acceptance: float
+    meas_acceptance: float
+    records: list = field(default_factory=list)   # (sweep, accepted, dH, ObservablesResult)
+
+
+def run_simulation(p: H.ModelParameters, out_dir: str, *, n_therm: int = 100, n_measure: int = 500,
+                   Nt_therm_init: int = 10, Nt_measure: int = 5, measure_transport_freq: int = 1,
+                   bin_size: int = 5, verbose: bool = True, rng: np.random.Generator | None = None,
+                   device: int = 0, delta_cap: float = 2.0, state: H.SimulationState | None = None,
+                   cache: H.ComputeCache | None = None) -> SimulationResult:
+    """src/Simulation.jl:34-236.  Files in out_dir: simulation.log (appended),
+    observables.csv, transport.csv (header only)."""
+    rng = rng if rng is not None else np.random.default_rng()
+    os.makedirs(out_dir, exist_ok=True)
+    f_log = open(os.path.join(out_dir, "simulation.log"), "a")
+    f_obs = open(os.path.join(out_dir, "observables.csv"), "w")
+    f_trans = open(os.path.join(out_dir, "transport.csv"), "w")
+
+    def tee(msg: str):
+        line = f"[{datetime.now().strftime('%Y-%m-%d %H:%M:%S')}] {msg}"
+        print(line, file=f_log, flush=True)
+        if verbose:
+            print(line, flush=True)
+
+    try:
+        f_obs.write(OBS_HEADER + "\n")
+        f_trans.write(TRANSPORT_HEADER + "\n")
+        tee("Starting Simulation...")
+        tee(f"System: {p.Lx}x{p.Ly}, β={p.beta}, n_imp={p.n_imp}, J={p.J}")
+        tee(f"Config: Therm={n_therm}, Sweep={n_measure}, TransFreq={measure_transport_freq}, "
+            f"BinSize={bin_size}")
+        tee("Transport/spectra measurements need eigenvectors: not on the GPU path, "
+            "transport.csv holds the header only")
+
+        tee("Initializing State...")
+        if state is None:
+            state = H.initialize_state(p, rng)
+        if cache is None:
+            cache = H.initialize_cache(p, device=device, delta_cap=delta_cap)
+        H.init_static_H(cache, p, state)
+        H.update_H_BdG(cache, p, state)
+        H.diagonalize_H_BdG(cache, p)
+
+        ctl = AdaptiveNt(Nt_therm_init)
+        dt = H.calc_optimal_dt(p.beta, p.J, p.mass, ctl.Nt)
+        tee("--- Thermalization Start ---")
+        tee(f"Init: Nt={ctl.Nt}, dt={round(dt, 5)}")
+        t0 = time.time()
+        acc_therm = 0
+        for i in range(1, n_therm + 1):
+            acc, _ = H.hmc_sweep(cache, p, state, Nt=ctl.Nt, dt=dt, rng=rng)
+            acc_therm += int(acc)
+            r = ctl.record(i, acc)
+            if r is None:
+                continue
+            rate, old, new = r
+            if new != old:
+                dt = H.calc_optimal_dt(p.beta, p.J, p.mass, new)
+                tee("Therm %d/%d. Rate=%.2f. Adjust Nt: %d -> %d, dt: %.4f" % (i, n_therm, rate, old, new, dt))
+            elif i % 20 == 0:
+                tee("Therm %d/%d. Rate=%.2f. Nt=%d (Stable)" % (i, n_therm, rate, new))
+        tee(f"Thermalization Done. Time: {round(time.time() - t0, 2)}s")
+
+        dt_meas = H.calc_optimal_dt(p.beta, p.J, p.mass, Nt_measure)
+        tee("--- Measurement Start ---")
+        tee(f"Settings: Nt={Nt_measure}, dt={round(dt_meas, 5)}")
+        t1 = time.time()
+        acc_total = 0
+        res = SimulationResult(ctl.Nt, acc_therm / max(n_therm, 1), 0.0)
+        for i in range(1, n_measure + 1):
+            acc, dH = H.hmc_sweep(cache, p, state, Nt=Nt_measure, dt=dt_meas, rng=rng)
+            acc_total += int(acc)
+            obs = H.measure_observables(cache, p, state)
+            f_obs.write(obs_csv_line(i, acc, dH, obs))
+            f_obs.flush()
+            res.records.append((i, acc, dH, obs))
+            if i % 10 == 0:
+                tee("Meas %d/%d. Acc=%.2f. E=%.4f" % (i, n_measure, acc_total / i, obs.total_energy))
+        res.meas_acceptance = acc_total / max(n_measure, 1)
+        tee(f"Measurement Done. Total Time: {round(time.time() - t1, 2)}s")
+        return res
+    finally:
+        f_log.close()
+        f_obs.close()
+        f_trans.close()

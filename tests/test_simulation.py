@@ -1,0 +1,88 @@
+"""run_simulation (src/Simulation.jl:34-236) over the hot path.
+
+CPU: the driver logic — adaptive Nt rule, log lines, observables.csv format —
+with the oracle behind the FermionContext API (tests/oracle_context.py).
+GPU: the same driver on the HIP path against the oracle-backed run with the
+same seed; per-sweep records agree within the sweep tolerances of
+test_gpu_parity.py (|ΔdH| ≤ 1e-8 (1 + |dH|), observables ≤ 1e-9 abs)."""
+import importlib
+import os
+
+import numpy as np
+import pytest
+
+from oracle_context import OracleContext
+
+
+@pytest.fixture(scope="module")
+def sim(dwhmc):
+    return importlib.import_module(dwhmc.__name__ + ".simulation")
+
+
+@pytest.fixture(scope="module")
+def hmc_mod(dwhmc):
+    return importlib.import_module(dwhmc.__name__ + ".hmc")
+
+
+def test_adaptive_nt_rule(sim):
+    """src/Simulation.jl:109-129: windows of 5; <0.60 -> +2; >0.95 and Nt>4 -> -1."""
+    ctl = sim.AdaptiveNt(10)
+    seq = [True, True, False, False, False,      # 0.4 -> 12
+           True, True, True, True, False,        # 0.8 -> stable
+           True, True, True, True, True]         # 1.0 -> 11
+    out = [ctl.record(i + 1, a) for i, a in enumerate(seq)]
+    assert [o for o in out if o is not None] == [(0.4, 10, 12), (0.8, 12, 12), (1.0, 12, 11)]
+    ctl = sim.AdaptiveNt(4)
+    for i in range(1, 6):
+        r = ctl.record(i, True)
+    assert r == (1.0, 4, 4)                      # Nt > 4 required to shrink
+
+
+def test_obs_csv_line_format(sim, dwhmc):
+    obs = dwhmc.ObservablesResult(-1.25, 0.1, 0.2, 0.3, 0.09, -0.05, 0.5, 0.25, 0.125)
+    assert sim.obs_csv_line(7, True, 1.5e-3, obs) == (
+        "7,1,1.50000e-03,-1.250000,0.100000,0.200000,0.300000,0.090000,-0.050000,0.500000,0.250000,0.125000\n")
+
+
+def _run(sim, hmc_mod, dwhmc, out_dir, ctx_cls, seed=11, **kw):
+    p = dwhmc.ModelParameters(4, 4, 1.0, -0.35, -1.08, 1.0, 0.25, 8.0, 0.8, 1.0)
+    saved = hmc_mod.FermionContext
+    if ctx_cls is not None:
+        hmc_mod.FermionContext = ctx_cls
+    try:
+        return sim.run_simulation(p, str(out_dir), rng=np.random.default_rng(seed), verbose=False, **kw)
+    finally:
+        hmc_mod.FermionContext = saved
+
+
+def test_run_simulation_driver_on_oracle(sim, hmc_mod, dwhmc, tmp_path):
+    res = _run(sim, hmc_mod, dwhmc, tmp_path, OracleContext, n_therm=10, n_measure=10,
+               Nt_therm_init=2, Nt_measure=3)
+    log = (tmp_path / "simulation.log").read_text()
+    for s in ("Starting Simulation...", "System: 4x4, β=8.0", "--- Thermalization Start ---",
+              "Init: Nt=2", "Thermalization Done.", "--- Measurement Start ---", "Settings: Nt=3",
+              "Meas 10/10.", "Measurement Done."):
+        assert s in log, s
+    rows = (tmp_path / "observables.csv").read_text().splitlines()
+    assert rows[0] == sim.OBS_HEADER and len(rows) == 11
+    assert (tmp_path / "transport.csv").read_text().splitlines() == [sim.TRANSPORT_HEADER]
+    for k, (i, acc, dH, obs) in enumerate(res.records):
+        assert rows[k + 1] == sim.obs_csv_line(i, acc, dH, obs).rstrip("\n")
+        assert np.isfinite(obs.total_energy) and -1.0 <= obs.hole_conc <= 1.0
+    # the adaptive rule saw the thermalisation acceptances
+    assert res.Nt_final >= 2
+
+
+@pytest.mark.gpu
+def test_run_simulation_device_matches_oracle(sim, hmc_mod, dwhmc, tmp_path):
+    kw = dict(n_therm=10, n_measure=10, Nt_therm_init=4, Nt_measure=5)
+    ref = _run(sim, hmc_mod, dwhmc, tmp_path / "ref", OracleContext, seed=5, **kw)
+    dev = _run(sim, hmc_mod, dwhmc, tmp_path / "dev", None, seed=5, **kw)
+    assert dev.Nt_final == ref.Nt_final
+    assert len(dev.records) == len(ref.records) == 10
+    for (i, a1, dh1, o1), (j, a2, dh2, o2) in zip(dev.records, ref.records):
+        assert i == j and a1 == a2
+        assert abs(dh1 - dh2) <= 1e-8 * (1 + abs(dh2)), (i, dh1, dh2)
+        for f in ("total_energy", "Delta_amp", "Delta_local", "Delta_global", "S_Delta", "hole_conc",
+                  "Delta_diff", "Delta_pair", "Delta_localpair"):
+            assert abs(getattr(o1, f) - getattr(o2, f)) <= 1e-9, (i, f, getattr(o1, f), getattr(o2, f))
