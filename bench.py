@@ -79,6 +79,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=0, help="oracle leapfrog steps for the CPU leg (0 = auto)")
     ap.add_argument("--no-timing", action="store_true", help="disable per-kernel HIP events")
+    ap.add_argument("--algo", choices=["auto", "dense", "cr"], default="auto",
+                    help="factorisation (include/dwhmc.h DWH_ALGO_*); auto = cyclic reduction when 2L <= 96")
     return ap.parse_args()
 
 
@@ -154,7 +156,10 @@ def main():
     dis, D0, noise, uni = synthetic(p, O, rank, a.chains, a.Nt, n_warm + n_time)
     dt = m.calc_optimal_dt(p.beta, p.J, p.mass, a.Nt)
     ctx = m.FermionContext(p.Lx, p.Ly, p.t, p.tp, p.mu, p.beta, p.J, p.nn_table, p.nnn_table, dis,
-                           device=local)
+                           device=local, algo=a.algo)
+    cr = ctx.info["algo"] == 1
+    # dominant kernel: block products (cr) / rank-128 GJ update (dense)
+    dom = "cr_gemm" if cr else "gj_update"
     ctx.set_pairing(D0)
     ctx.factorize()                                 # src/Simulation.jl:84-86
     ctx.load_draws(noise, uni)                      # inputs resident in HBM before timing
@@ -163,7 +168,7 @@ def main():
     ctx.synchronize()
     if not a.no_timing:
         # events only around the dominant kernel (and the once-per-factorize assembly)
-        ctx.timing_enable(["gj_update", "assemble"])
+        ctx.timing_enable([dom, "assemble"] + (["cr_inv"] if cr else []))
         ctx.timing_reset()
 
     if dist is not None:
@@ -184,8 +189,8 @@ def main():
     info = ctx.info
     kern = {}
     if not a.no_timing:
-        kern["gj_update"] = ctx.timing_read("gj_update")
-        kern["assemble"] = ctx.timing_read("assemble")
+        for k in [dom, "assemble"] + (["cr_inv"] if cr else []):
+            kern[k] = ctx.timing_read(k)
         ctx.timing_enable(False)
     # observables gather over RCCL (the only collective): acceptance and <dH>
     obs = np.array([acc.mean(), dH.mean(), float(np.mean(np.exp(-dH)))], dtype=np.float64)
@@ -220,14 +225,27 @@ def main():
                        "Nt": a.Nt, "dt": dt, "poles": P, "kappa": info["kappa"],
                        "parallelism": f"replicas x{world}" if world > 1 else "single GPU"},
             "acceptance": float(obs[0]), "mean_dH": float(obs[1]), "mean_exp_minus_dH": float(obs[2]),
+            "algorithm": "block cyclic reduction" if cr else "dense Schur complement + Gauss-Jordan",
             "ref_equiv_tflops": leap * (40.0 / 3.0) * (2 * N) ** 3 / el / 1e12,
-            "alg_tflops": leap * P * 8.0 * N ** 3 / el / 1e12,
+            "dense_equiv_tflops": leap * P * 8.0 * N ** 3 / el / 1e12,
         }
+        if not cr:
+            rec["alg_tflops"] = rec["dense_equiv_tflops"]
         if kern:
-            ms, n, w = kern["gj_update"]
+            ms, n, w = kern[dom]
             ach = w / n / (ms / n * 1e-3) / 1e12 if n and ms > 0 else None
-            nb = -(-info["N"] // 64)                 # GJ block steps; odd nb ends with one rank-64 step
-            kname = "k_gj_update<2>" if nb % 2 == 0 else "k_gj_update<2>+<0>"
+            if cr:
+                kname = f"k_cr_gemm<{info['block']}>"
+                msi, ni, wi = kern["cr_inv"]
+                # the CR path's own algorithmic flops: block products + block inversions
+                rec["alg_tflops"] = (w + wi) * world / el / 1e12
+                rec["cr_inv"] = {"bound": "latency", "kernel": f"k_cr_inv<{info['block'] // 16}>",
+                                 "achieved_tflops": wi / (msi * 1e-3) / 1e12 if msi > 0 else None,
+                                 "avg_launch_us": 1000.0 * msi / ni if ni else None,
+                                 "ms_per_step": msi / a.steps}
+            else:
+                nb = -(-info["N"] // 64)                 # GJ block steps; odd nb ends with one rank-64 step
+                kname = "k_gj_update<2>" if nb % 2 == 0 else "k_gj_update<2>+<0>"
             traffic, tsrc = measured_traffic(kname, a.L, a.beta, a.chains)
             rec["roofline"] = {"bound": "mfma", "kernel": kname, "achieved": ach,
                                "peak": PEAK_F64_TFLOPS, "unit": "TFLOP/s",
@@ -235,11 +253,12 @@ def main():
                                "traffic_unit": "bytes/launch", "traffic_source": tsrc,
                                "avg_launch_us": 1000.0 * ms / n if n else None,
                                "flops_per_launch": w / n if n else None}
-            rec["gj_update_ms_per_step"] = ms / a.steps
+            rec[f"{dom}_ms_per_step"] = ms / a.steps
             ms, n, w = kern["assemble"]
             if n and ms > 0:
                 gbs = w / n / (ms / n * 1e-3) / 1e9
-                rec["assembly"] = {"bound": "hbm", "kernel": "k_assemble", "achieved": gbs,
+                rec["assembly"] = {"bound": "hbm", "kernel": "k_cr_fill" if cr else "k_assemble",
+                                   "achieved": gbs,
                                    "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS,
                                    "bytes_per_launch": w / n, "avg_launch_us": 1000.0 * ms / n}
         if not a.no_cpu_baseline and world == 1:

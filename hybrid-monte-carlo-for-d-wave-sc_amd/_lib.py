@@ -41,7 +41,8 @@ class c128(C.Structure):
 class dwh_info_t(C.Structure):
     _fields_ = [("N", C.c_int64), ("Np", C.c_int64), ("nchains", C.c_int64), ("npoles", C.c_int64),
                 ("kappa", C.c_double), ("e_bound", C.c_double), ("err_tanh", C.c_double),
-                ("delta_cap", C.c_double), ("device_bytes", C.c_int64)]
+                ("delta_cap", C.c_double), ("device_bytes", C.c_int64), ("algo", C.c_int64),
+                ("block", C.c_int64)]
 
 
 _P = C.c_void_p
@@ -55,6 +56,8 @@ SIGNATURES = {
     "dwh_create": (C.c_int, [C.POINTER(_P), _I64, _I64, _D, _D, _D, _D, _D, _P, _P, _P, _I32]),
     "dwh_create_batched": (C.c_int, [C.POINTER(_P), _I64, _I64, _D, _D, _D, _D, _D, _P, _P, _I64, _P,
                                      _D, _I32]),
+    "dwh_create_ex": (C.c_int, [C.POINTER(_P), _I64, _I64, _D, _D, _D, _D, _D, _P, _P, _I64, _P,
+                                _D, _I32, _I32]),
     "dwh_destroy": (None, [_P]),
     "dwh_last_error": (C.c_char_p, [_P]),
     "dwh_info": (C.c_int, [_P, C.POINTER(dwh_info_t)]),

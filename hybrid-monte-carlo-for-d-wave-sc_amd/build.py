@@ -14,8 +14,10 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libdwhmc.so")
-SOURCES = [os.path.join(CSRC, "dwhmc_kernels.hip"), os.path.join(CSRC, "dwhmc_api.cpp")]
-DEPS = SOURCES + [os.path.join(CSRC, "dwhmc_internal.h"), os.path.join(CSRC, "pole_table.inc"),
+SOURCES = [os.path.join(CSRC, "dwhmc_kernels.hip"), os.path.join(CSRC, "dwhmc_cr.hip"),
+           os.path.join(CSRC, "dwhmc_api.cpp")]
+DEPS = SOURCES + [os.path.join(CSRC, "dwhmc_internal.h"), os.path.join(CSRC, "dwhmc_device.h"),
+                  os.path.join(CSRC, "pole_table.inc"),
                   os.path.join(ROOT, "include", "dwhmc.h")]
 ARCH = os.environ.get("DWHMC_OFFLOAD_ARCH", "gfx950")
 

@@ -36,11 +36,17 @@ def table_to_abi(table: np.ndarray) -> np.ndarray:
     return np.ascontiguousarray(t.T, dtype=np.int64)
 
 
+# factorisation algorithm (include/dwhmc.h DWH_ALGO_*): "auto" = env DWHMC_ALGO,
+# else block cyclic reduction when 2 Lx <= 96
+ALGOS = {"auto": -1, "dense": 0, "cr": 1}
+
+
 class FermionContext:
     """Device-resident fermionic action/force evaluator for nchains chains."""
 
     def __init__(self, Lx, Ly, t, tp, mu, beta, J, nn_table, nnn_table, disorder,
-                 delta_cap: float = 2.0, device: int = 0, lib_path: str | None = None):
+                 delta_cap: float = 2.0, device: int = 0, lib_path: str | None = None,
+                 algo: str = "auto"):
         self._lib = _lib.load() if lib_path is None else _lib.load_path(lib_path)
         dis = np.ascontiguousarray(np.atleast_2d(np.asarray(disorder, dtype=np.float64)))
         self.N = int(Lx) * int(Ly)
@@ -51,9 +57,12 @@ class FermionContext:
         h = C.c_void_p()
         nn = table_to_abi(nn_table)
         nnn = table_to_abi(nnn_table)
-        rc = self._lib.dwh_create_batched(C.byref(h), int(Lx), int(Ly), float(t), float(tp),
-                                          float(mu), float(beta), float(J), ptr(nn), ptr(nnn),
-                                          self.nchains, ptr(dis), float(delta_cap), int(device))
+        if algo not in ALGOS:
+            raise ValueError(f"algo must be one of {sorted(ALGOS)}")
+        rc = self._lib.dwh_create_ex(C.byref(h), int(Lx), int(Ly), float(t), float(tp),
+                                     float(mu), float(beta), float(J), ptr(nn), ptr(nnn),
+                                     self.nchains, ptr(dis), float(delta_cap), ALGOS[algo],
+                                     int(device))
         check(rc, None)
         self._h = h
         self.info = self._info()
@@ -161,7 +170,7 @@ class FermionContext:
         return s.value or 0
 
     # -- timing ----------------------------------------------------------
-    TIMERS = ("gj_update", "gj_pivot", "assemble", "contract", "step", "gj_edge")
+    TIMERS = ("gj_update", "gj_pivot", "assemble", "contract", "step", "gj_edge", "cr_gemm", "cr_inv")
 
     def timing_enable(self, on=True):
         """on: True (all timers), False, or an iterable of timer names."""

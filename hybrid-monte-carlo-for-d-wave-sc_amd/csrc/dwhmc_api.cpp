@@ -34,8 +34,225 @@ namespace {
 
 thread_local std::string g_create_error;
 
-enum TimerName { T_GJ_UPDATE = 0, T_GJ_PIVOT, T_ASSEMBLE, T_CONTRACT, T_STEP, T_GJ_EDGE, T_COUNT };
-const char* kTimerNames[T_COUNT] = {"gj_update", "gj_pivot", "assemble", "contract", "step", "gj_edge"};
+enum TimerName {
+  T_GJ_UPDATE = 0, T_GJ_PIVOT, T_ASSEMBLE, T_CONTRACT, T_STEP, T_GJ_EDGE, T_CR_GEMM, T_CR_INV, T_COUNT
+};
+const char* kTimerNames[T_COUNT] = {"gj_update", "gj_pivot", "assemble", "contract",
+                                    "step",      "gj_edge",  "cr_gemm",  "cr_inv"};
+
+enum Algo { ALGO_DENSE = 0, ALGO_CR = 1 };
+
+// One stage of the cyclic-reduction plan: a batch of block inversions or a
+// task list of block products (all batch items at once).
+struct CrStage {
+  int kind;      // 0 inversion, 1 products
+  int first, n;  // range in CrPlan::inv_blk / CrPlan::tasks
+  double sg;     // products: sign of the sum
+  int terms;     // products: total K = BP terms over the tasks
+};
+
+struct CrPlan {
+  int nblk = 0;
+  std::vector<CrStage> stages;
+  std::vector<dwh::CrTask> tasks;
+  std::vector<int> inv_blk, inv_slot;
+  std::vector<int64_t> goff, doff;
+};
+
+// Block cyclic reduction of the periodic block-tridiagonal H_BdG - i y (blocks
+// = lattice rows) into stages; restates tools/cr_model.py (checked there
+// against dense inverses for Ly = 1 .. 16, odd and even).  Pool blocks:
+// level-0 D[y] = y, U[y] = Ly + y, L[y] = 2 Ly + y (filled by k_cr_fill).
+// Forward level (m blocks, eliminate odd e < m - m%2, keep even k):
+//   inv D_e;  V1 = -U_a D_e^-1, V2 = -L_e D_e^-1, W1 = -D_e^-1 L_a, W2 = -D_e^-1 U_e
+//   D'_k = D_k + V1(k+1) L_k + V2(k-1) U_(k-1);  U'_k = V1(k+1) U_(k+1);  L'_k = V2(k+1) L_k
+//   (m = 2 folds the self-couplings of the 1-block chain into D': 4 terms)
+// Backward (G of the next level known at its kept blocks and adjacent pairs):
+//   G_ea = W1 G_aa + W2 G_ca,  G_ec = W1 G_ac + W2 G_cc,
+//   G_ae = G_aa V1 + G_ac V2,  G_ce = G_ca V1 + G_cc V2,  G_ee = D_e^-1 + W1 G_ae + W2 G_ce.
+CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol) {
+  CrPlan pl;
+  int nblk = 3 * Ly;
+  auto nb = [&]() { return nblk++; };
+  struct Level {
+    int m;
+    std::vector<int> D, U, L, E, K;
+    std::vector<int> V1, V2, W1, W2;   // indexed by position e
+    std::vector<char> elim;
+  };
+  auto add_inv = [&](const std::vector<int>& blocks, int& slot) {
+    CrStage st{0, (int)pl.inv_blk.size(), (int)blocks.size(), 0.0, 0};
+    for (int b : blocks) {
+      pl.inv_blk.push_back(b);
+      pl.inv_slot.push_back(slot++);
+    }
+    pl.stages.push_back(st);
+  };
+  struct Term { int a, b; };
+  std::vector<dwh::CrTask> cur_tasks;
+  auto task = [&](int out, int cin, std::initializer_list<Term> terms) {
+    dwh::CrTask t{};
+    t.out = out;
+    t.cin = cin;
+    t.nt = 0;
+    for (const Term& x : terms) {
+      t.a[t.nt] = x.a;
+      t.b[t.nt] = x.b;
+      t.nt++;
+    }
+    cur_tasks.push_back(t);
+  };
+  auto flush = [&](double sg) {
+    if (cur_tasks.empty()) return;
+    CrStage st{1, (int)pl.tasks.size(), (int)cur_tasks.size(), sg, 0};
+    for (auto& t : cur_tasks) {
+      st.terms += t.nt;
+      pl.tasks.push_back(t);
+    }
+    pl.stages.push_back(st);
+    cur_tasks.clear();
+  };
+
+  Level cur;
+  cur.m = Ly;
+  for (int y = 0; y < Ly; ++y) {
+    cur.D.push_back(y);
+    cur.U.push_back(Ly + y);
+    cur.L.push_back(2 * Ly + y);
+  }
+  std::vector<Level> levels;
+  int slot = 0;
+  while (cur.m > 1) {
+    const int m = cur.m;
+    cur.elim.assign(m, 0);
+    cur.E.clear();
+    cur.K.clear();
+    for (int e = 1; e < m - (m % 2); e += 2) {
+      cur.E.push_back(e);
+      cur.elim[e] = 1;
+    }
+    for (int k = 0; k < m; k += 2) cur.K.push_back(k);
+    cur.V1.assign(m, -1);
+    cur.V2.assign(m, -1);
+    cur.W1.assign(m, -1);
+    cur.W2.assign(m, -1);
+    std::vector<int> inv;
+    for (int e : cur.E) inv.push_back(cur.D[e]);
+    add_inv(inv, slot);
+    for (int e : cur.E) {
+      const int a = e - 1;
+      cur.V1[e] = nb();
+      task(cur.V1[e], -1, {{cur.U[a], cur.D[e]}});
+      cur.V2[e] = nb();
+      task(cur.V2[e], -1, {{cur.L[e], cur.D[e]}});
+      cur.W1[e] = nb();
+      task(cur.W1[e], -1, {{cur.D[e], cur.L[a]}});
+      cur.W2[e] = nb();
+      task(cur.W2[e], -1, {{cur.D[e], cur.U[e]}});
+    }
+    flush(-1.0);
+    Level nxt;
+    nxt.m = (int)cur.K.size();
+    for (int k : cur.K) {
+      if (m == 2) {
+        const int e = 1, Dn = nb();
+        task(Dn, cur.D[0], {{cur.V1[e], cur.L[0]}, {cur.V2[e], cur.U[1]}, {cur.V1[e], cur.U[1]},
+                            {cur.V2[e], cur.L[0]}});
+        nxt.D.push_back(Dn);
+        nxt.U.push_back(-1);
+        nxt.L.push_back(-1);
+        continue;
+      }
+      const int er = k + 1, el = (k - 1 + m) % m;
+      const bool hr = er < m && cur.elim[er], hl = cur.elim[el];
+      const int Dn = nb();
+      if (hr && hl)
+        task(Dn, cur.D[k], {{cur.V1[er], cur.L[k]}, {cur.V2[el], cur.U[el]}});
+      else if (hr)
+        task(Dn, cur.D[k], {{cur.V1[er], cur.L[k]}});
+      else
+        task(Dn, cur.D[k], {{cur.V2[el], cur.U[el]}});
+      nxt.D.push_back(Dn);
+      if (hr) {
+        const int Un = nb(), Ln = nb();
+        task(Un, -1, {{cur.V1[er], cur.U[er]}});
+        task(Ln, -1, {{cur.V2[er], cur.L[k]}});
+        nxt.U.push_back(Un);
+        nxt.L.push_back(Ln);
+      } else {   // odd m: the kept pair (m-1, 0) keeps its direct coupling
+        nxt.U.push_back(cur.U[k]);
+        nxt.L.push_back(cur.L[k]);
+      }
+    }
+    flush(1.0);
+    levels.push_back(cur);
+    cur = nxt;
+  }
+  add_inv({cur.D[0]}, slot);
+  std::vector<int> GD{cur.D[0]}, GU{cur.D[0]}, GL{cur.D[0]};
+  for (int li = (int)levels.size() - 1; li >= 0; --li) {
+    const Level& lv = levels[li];
+    const int m = lv.m, mn = (int)lv.K.size();
+    std::vector<int> gd(m, -1), gu(m, -1), gl(m, -1);
+    for (int kk = 0; kk < mn; ++kk) {
+      const int k = lv.K[kk];
+      gd[k] = GD[kk];
+      if (!(k + 1 < m && lv.elim[k + 1])) {
+        gu[k] = GU[kk];
+        gl[k] = GL[kk];
+      }
+    }
+    std::vector<int> Gae(m, -1), Gce(m, -1);
+    for (int e : lv.E) {
+      const int a = e - 1, c = (e + 1) % m;
+      const int ia = a / 2, ic = (c / 2) % mn;
+      const int Gaa = GD[ia], Gcc = GD[ic];
+      const int Gac = mn == 1 ? GD[0] : GU[ia];
+      const int Gca = mn == 1 ? GD[0] : GL[ia];
+      const int gea = nb(), gec = nb(), gae = nb(), gce = nb();
+      task(gea, -1, {{lv.W1[e], Gaa}, {lv.W2[e], Gca}});
+      task(gec, -1, {{lv.W1[e], Gac}, {lv.W2[e], Gcc}});
+      task(gae, -1, {{Gaa, lv.V1[e]}, {Gac, lv.V2[e]}});
+      task(gce, -1, {{Gca, lv.V1[e]}, {Gcc, lv.V2[e]}});
+      gu[a] = gae;
+      gl[a] = gea;
+      gu[e] = gec;
+      gl[e] = gce;
+      Gae[e] = gae;
+      Gce[e] = gce;
+    }
+    flush(1.0);
+    for (int e : lv.E) {
+      task(lv.D[e], lv.D[e], {{lv.W1[e], Gae[e]}, {lv.W2[e], Gce[e]}});
+      gd[e] = lv.D[e];
+    }
+    flush(1.0);
+    GD = gd;
+    GU = gu;
+    GL = gl;
+  }
+  // gather offsets of the level-0 G blocks
+  const int N = Lx * Ly;
+  const int64_t BB = (int64_t)BP * BP;
+  pl.goff.assign((size_t)N * kSlots, -1);
+  pl.doff.assign(N, 0);
+  for (int i = 0; i < N; ++i) {
+    const int x = i % Lx, y = i / Lx;
+    for (int s = 0; s < kSlots; ++s) {
+      const int j = Dcol[(size_t)i * kSlots + s];
+      if (j < 0) continue;
+      const int xj = j % Lx, yj = j / Lx;
+      int blk;
+      if (Ly == 1 || yj == y) blk = GD[y];
+      else if (yj == (y + 1) % Ly) blk = GU[y];
+      else blk = GL[(y - 1 + Ly) % Ly];
+      pl.goff[(size_t)i * kSlots + s] = blk * BB + (int64_t)x * BP + (Lx + xj);
+    }
+    pl.doff[i] = GD[y] * BB + (int64_t)(Lx + x) * BP + (Lx + x);
+  }
+  pl.nblk = nblk;
+  return pl;
+}
 
 struct TimingRec {
   int name;
@@ -89,6 +306,15 @@ struct dwh_ctx {
   uint8_t* acc = nullptr;
   double* dH = nullptr;
   std::vector<void*> allocations;
+
+  // block cyclic-reduction path (algo == ALGO_CR)
+  int algo = ALGO_DENSE;
+  dwh::CrDims cr{};
+  CrPlan plan;
+  double2* bpool = nullptr;   // CR block pool (nbatch x nblk blocks)
+  dwh::CrTask* d_tasks = nullptr;
+  int *d_inv_blk = nullptr, *d_inv_slot = nullptr;
+  int64_t *d_goff = nullptr, *d_doff = nullptr;
 
   // timing
   int timing = 0;   // bitmask over TimerName (bit i = kTimerNames[i])
@@ -243,11 +469,42 @@ void run_gj(dwh_ctx* ctx, double2* M) {
   }
 }
 
+// level-0 blocks -> CR stages -> gather of the selected G entries
+void cr_enqueue(dwh_ctx* ctx) {
+  const dwh::CrDims& c = ctx->cr;
+  const double bp3 = 8.0 * c.BP * (double)c.BP * c.BP * c.nbatch;
+  {
+    // bytes written: the 3 Ly level-0 blocks of every batch item
+    Scope s(ctx, T_ASSEMBLE, 3.0 * c.Ly * 16.0 * c.BP * (double)c.BP * c.nbatch);
+    dwh::launch_cr_fill(c, ctx->bpool, ctx->hcol, ctx->hval, ctx->Dcol, ctx->Dv, ctx->d_y, ctx->stream);
+  }
+  for (const CrStage& st : ctx->plan.stages) {
+    if (st.kind == 0) {
+      Scope s(ctx, T_CR_INV, st.n * bp3);
+      dwh::launch_cr_inv(c, ctx->bpool, ctx->d_inv_blk + st.first, ctx->d_inv_slot + st.first, st.n,
+                         ctx->ldpart, ctx->stream);
+    } else {
+      Scope s(ctx, T_CR_GEMM, st.terms * bp3);
+      dwh::launch_cr_gemm(c, ctx->bpool, ctx->d_tasks + st.first, st.n, st.sg, ctx->stream);
+    }
+  }
+  {
+    Scope s(ctx, T_CONTRACT, 16.0 * (kSlots + 1) * (double)c.N * c.nbatch);
+    dwh::launch_cr_gather(c, ctx->bpool, ctx->d_goff, ctx->d_doff, ctx->G12nn, ctx->diagS, ctx->stream);
+  }
+}
+
 // assemble -> GJ -> contract -> P (and optional kick) -> E_f
 void factorize_enqueue(dwh_ctx* ctx, double kick) {
   const Dims& d = ctx->d;
   Scope step(ctx, T_STEP, (double)d.nbatch * 8.0 * (double)d.N * d.N * d.N);
   dwh::launch_dvals(d, ctx->Dsrc, ctx->Delta, ctx->Dv, ctx->stream);
+  if (ctx->algo == ALGO_CR) {
+    cr_enqueue(ctx);
+    dwh::launch_pair_force(d, ctx->G12nn, ctx->bond_ij, ctx->bond_ji, ctx->d_c, ctx->Delta,
+                           ctx->Pair, ctx->F, ctx->Pi, kick, ctx->beta, ctx->J, ctx->stream);
+    return;
+  }
   {
     // algorithmic bytes: read R once, write S^T
     Scope s(ctx, T_ASSEMBLE, (double)d.nbatch * 32.0 * d.N * (double)d.N);
@@ -318,7 +575,7 @@ int check_flag(dwh_ctx* ctx) {
 
 int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, double mu, double beta,
                 double J, const int64_t* nn, const int64_t* nnn, int64_t nchains,
-                const double* disorder, double delta_cap, int32_t device) {
+                const double* disorder, double delta_cap, int32_t algo_req, int32_t device) {
   if (!out) return fail(nullptr, DWH_ERR_ARG, "ctx pointer is NULL");
   *out = nullptr;
   if (Lx < 1 || Ly < 1) return fail(nullptr, DWH_ERR_ARG, "Lx, Ly must be >= 1");
@@ -469,6 +726,43 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
   d.P = pe.m;
   d.nbatch = d.nc * d.P;
   d.mat = (int64_t)d.Np * d.Np;
+  d.nld = d.nb;
+  // algorithm: explicit request, else DWHMC_ALGO = dense | cr | auto (default:
+  // cr when the lattice-row block 2 Lx fits a supported padded size)
+  {
+    const int BP = (int)((2 * Lx + 31) / 32 * 32);
+    std::string want = "auto";
+    if (algo_req == DWH_ALGO_DENSE) want = "dense";
+    else if (algo_req == DWH_ALGO_CR) want = "cr";
+    else if (const char* e = std::getenv("DWHMC_ALGO")) want = e;
+    if (want != "auto" && want != "dense" && want != "cr") {
+      ctx->err = "DWHMC_ALGO must be auto, dense or cr";
+      g_create_error = ctx->err;
+      delete ctx;
+      return DWH_ERR_ARG;
+    }
+    const bool ok = dwh::cr_supported_bp(BP);
+    if (want == "cr" && !ok) {
+      ctx->err = "DWHMC_ALGO=cr needs 2*Lx <= 96";
+      g_create_error = ctx->err;
+      delete ctx;
+      return DWH_ERR_ARG;
+    }
+    ctx->algo = (want == "dense" || !ok) ? ALGO_DENSE : ALGO_CR;
+    if (ctx->algo == ALGO_CR) {
+      ctx->plan = build_cr_plan((int)Lx, (int)Ly, BP, Dcol);
+      dwh::CrDims& c = ctx->cr;
+      c.Lx = (int)Lx;
+      c.Ly = (int)Ly;
+      c.N = N;
+      c.BP = BP;
+      c.P = d.P;
+      c.nbatch = d.nbatch;
+      c.nblk = ctx->plan.nblk;
+      c.item = (int64_t)c.nblk * BP * BP;
+      d.nld = (int)Ly;
+    }
+  }
 
   auto bail = [&](int code) {
     g_create_error = ctx->err;
@@ -488,20 +782,30 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
   int rc = DWH_OK;
 #define ALLOC(p, n) \
   if ((rc = dalloc(ctx, &ctx->p, (n))) != DWH_OK) return bail(rc)
-  ALLOC(R, nmat);
-  ALLOC(S, nmat);
+  if (ctx->algo == ALGO_DENSE) {
+    ALLOC(R, nmat);
+    ALLOC(S, nmat);
+    const size_t npanel = (size_t)d.nbatch * d.Np * kGJ;
+    ALLOC(CpA0, npanel);
+    ALLOC(CpA1, npanel);
+    ALLOC(CpB, npanel);
+    ALLOC(XR1, npanel);
+    ALLOC(XR2, npanel);
+    ALLOC(Pb1, (size_t)d.nbatch * kGJ * kGJ);
+    ALLOC(Pb2, (size_t)d.nbatch * kGJ * kGJ);
+  } else {
+    const CrPlan& pl = ctx->plan;
+    ALLOC(bpool, (size_t)d.nbatch * ctx->cr.item);
+    ALLOC(d_tasks, pl.tasks.size());
+    ALLOC(d_inv_blk, pl.inv_blk.size());
+    ALLOC(d_inv_slot, pl.inv_slot.size());
+    ALLOC(d_goff, pl.goff.size());
+    ALLOC(d_doff, pl.doff.size());
+  }
   ALLOC(Dv, (size_t)d.nc * N * kSlots);
-  const size_t npanel = (size_t)d.nbatch * d.Np * kGJ;
-  ALLOC(CpA0, npanel);
-  ALLOC(CpA1, npanel);
-  ALLOC(CpB, npanel);
-  ALLOC(XR1, npanel);
-  ALLOC(XR2, npanel);
-  ALLOC(Pb1, (size_t)d.nbatch * kGJ * kGJ);
-  ALLOC(Pb2, (size_t)d.nbatch * kGJ * kGJ);
   ALLOC(G12nn, (size_t)d.nbatch * N * kSlots);
   ALLOC(diagS, (size_t)d.nbatch * N);
-  ALLOC(ldpart, (size_t)d.nbatch * d.nb);
+  ALLOC(ldpart, (size_t)d.nbatch * d.nld);
   ALLOC(ldstatic, (size_t)d.nbatch);
   ALLOC(d_y, (size_t)d.P);
   ALLOC(d_c, (size_t)d.P);
@@ -545,6 +849,14 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
   UP(hval, hval.data(), hval.size());
   UP(bond_ij, bij.data(), bij.size());
   UP(bond_ji, bji.data(), bji.size());
+  if (ctx->algo == ALGO_CR) {
+    const CrPlan& pl = ctx->plan;
+    UP(d_tasks, pl.tasks.data(), pl.tasks.size());
+    UP(d_inv_blk, pl.inv_blk.data(), pl.inv_blk.size());
+    UP(d_inv_slot, pl.inv_slot.data(), pl.inv_slot.size());
+    UP(d_goff, pl.goff.data(), pl.goff.size());
+    UP(d_doff, pl.doff.data(), pl.doff.size());
+  }
 #undef UP
   // zeroed cache, like initialize_cache (src/Types.jl:182-212): P = 0, E_f = 0
   (void)hipMemsetAsync(ctx->Delta, 0, nbond * sizeof(double2), s);
@@ -555,10 +867,15 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
   (void)hipMemsetAsync(ctx->Trhh, 0, d.nc * sizeof(double), s);
   (void)hipMemsetAsync(ctx->flag, 0, sizeof(int), s);
   (void)hipMemsetAsync(ctx->diagS, 0, (size_t)d.nbatch * N * sizeof(double2), s);
-  // static R = (h - i y)^-1 and ln|det(h - i y)| for every (chain, pole)
-  dwh::launch_fill_hz(d, ctx->R, ctx->hcol, ctx->hval, ctx->d_y, s);
-  run_gj(ctx, ctx->R);
-  dwh::launch_sum_ld(d, ctx->ldpart, ctx->ldstatic, s);
+  if (ctx->algo == ALGO_DENSE) {
+    // static R = (h - i y)^-1 and ln|det(h - i y)| for every (chain, pole)
+    dwh::launch_fill_hz(d, ctx->R, ctx->hcol, ctx->hval, ctx->d_y, s);
+    run_gj(ctx, ctx->R);
+    dwh::launch_sum_ld(d, ctx->ldpart, ctx->ldstatic, s);
+  } else {
+    // the CR path factorises the whole BdG matrix: no static part
+    (void)hipMemsetAsync(ctx->ldstatic, 0, d.nbatch * sizeof(double), s);
+  }
   if (hipStreamSynchronize(s) != hipSuccess || hipGetLastError() != hipSuccess) {
     ctx->err = "static R initialisation failed on the device";
     return bail(DWH_ERR_HIP);
@@ -574,14 +891,24 @@ extern "C" {
 int dwh_create(dwh_ctx** ctx, int64_t Lx, int64_t Ly, double t, double tp, double mu, double beta,
                double J, const int64_t* nn_table, const int64_t* nnn_table, const double* disorder,
                int32_t device) {
-  return create_impl(ctx, Lx, Ly, t, tp, mu, beta, J, nn_table, nnn_table, 1, disorder, 2.0, device);
+  return create_impl(ctx, Lx, Ly, t, tp, mu, beta, J, nn_table, nnn_table, 1, disorder, 2.0,
+                     DWH_ALGO_AUTO, device);
 }
 
 int dwh_create_batched(dwh_ctx** ctx, int64_t Lx, int64_t Ly, double t, double tp, double mu,
                        double beta, double J, const int64_t* nn_table, const int64_t* nnn_table,
                        int64_t nchains, const double* disorder, double delta_cap, int32_t device) {
   return create_impl(ctx, Lx, Ly, t, tp, mu, beta, J, nn_table, nnn_table, nchains, disorder,
-                     delta_cap, device);
+                     delta_cap, DWH_ALGO_AUTO, device);
+}
+
+int dwh_create_ex(dwh_ctx** ctx, int64_t Lx, int64_t Ly, double t, double tp, double mu, double beta,
+                  double J, const int64_t* nn_table, const int64_t* nnn_table, int64_t nchains,
+                  const double* disorder, double delta_cap, int32_t algo, int32_t device) {
+  if (algo != DWH_ALGO_AUTO && algo != DWH_ALGO_DENSE && algo != DWH_ALGO_CR)
+    return fail(nullptr, DWH_ERR_ARG, "algo must be DWH_ALGO_AUTO, DWH_ALGO_DENSE or DWH_ALGO_CR");
+  return create_impl(ctx, Lx, Ly, t, tp, mu, beta, J, nn_table, nnn_table, nchains, disorder,
+                     delta_cap, algo, device);
 }
 
 void dwh_destroy(dwh_ctx* ctx) {
@@ -613,6 +940,8 @@ int dwh_info(dwh_ctx* ctx, dwh_info_t* out) {
   out->err_tanh = ctx->err_tanh;
   out->delta_cap = ctx->delta_cap;
   out->device_bytes = ctx->device_bytes;
+  out->algo = ctx->algo;
+  out->block = ctx->algo == ALGO_CR ? ctx->cr.BP : kGJ;
   return DWH_OK;
 }
 

@@ -1,0 +1,117 @@
+// Device helpers shared by the dense Gauss-Jordan (dwhmc_kernels.hip) and the
+// block cyclic-reduction (dwhmc_cr.hip) kernels: complex arithmetic, the
+// XCD-aware grid remap, wave reductions, the wave-local 16x16 complex
+// inversion and the LDS-operand complex MFMA step (v_mfma_f64_16x16x4_f64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dwh {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ double2 cmul(double2 a, double2 b) {
+  return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+// a * conj(b)
+__device__ __forceinline__ double2 cmulc(double2 a, double2 b) {
+  return make_double2(a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y);
+}
+__device__ __forceinline__ double2 cadd(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ double2 csub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ double2 cinv(double2 a) {
+  const double s = 1.0 / (a.x * a.x + a.y * a.y);
+  return make_double2(a.x * s, -a.y * s);
+}
+// 1/a with v_rcp_f64 + two Newton steps (error ~1 ulp; the IEEE division
+// sequence has ~3x the latency and sits on the pivot dependency chain).
+__device__ __forceinline__ double rcp_nr(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  r = fma(r, fma(-d, r, 1.0), r);
+  r = fma(r, fma(-d, r, 1.0), r);
+  return r;
+}
+__device__ __forceinline__ double2 cinv_fast(double2 a) {
+  const double s = rcp_nr(fma(a.x, a.x, a.y * a.y));
+  return make_double2(a.x * s, -a.y * s);
+}
+
+// Bijective XCD-aware remap of a 1D grid (cdna_hip_programming.md §5): blocks
+// b and b+8 share an XCD, so item ranges [x*q, (x+1)*q) are given to one XCD
+// and neighbouring rows of one matrix share that XCD's L2.  Speed only.
+__device__ __forceinline__ int xcd_remap(int orig, int total) {
+  const int q = total / 8, r = total % 8, xcd = orig % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// 16x16 complex block in one wave: lane l holds row l>>2, columns (l&3)*4..+3.
+// Row p and column p are exchanged through a per-wave LDS scratch (xb: 16
+// row + 16 column entries) between wavefront-scope fences; the update is
+// branch-free (selects instead of a divergent row-p path).  pm receives
+// |pivot|^2 (lane 0) when non-null.
+__device__ __forceinline__ void wave_inv16(double2 (&a)[4], double2* xb, double* pm, int pbase) {
+  const int l = threadIdx.x & 63;
+  const int r = l >> 2, cq = l & 3;
+#pragma unroll
+  for (int p = 0; p < 16; ++p) {
+    const int ps = p >> 2, pe = p & 3;
+    const bool prow = (r == p);
+    if (prow) {
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) xb[cq * 4 + jj] = a[jj];
+    }
+    if (cq == ps) xb[16 + r] = a[pe];
+    // cross-lane hand-off: the fences are compiler ordering points (a plain
+    // predicated store/load pair may legally be reordered for other lanes)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const double2 piv = xb[p];
+    const double2 colp = xb[16 + r];
+    double2 rowp[4];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) rowp[jj] = xb[cq * 4 + jj];
+    const double2 inv = cinv_fast(piv);
+    if (pm != nullptr && l == 0) pm[pbase + p] = piv.x * piv.x + piv.y * piv.y;
+    // row p: a <- rowp * inv ; other rows: a <- a - (colp*inv) * rowp
+    const double2 fi = cmul(colp, inv);
+    const double2 g = prow ? make_double2(-inv.x, -inv.y) : fi;
+    const double2 pc = prow ? inv : make_double2(-fi.x, -fi.y);   // new value in column p
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const double2 base = prow ? make_double2(0.0, 0.0) : a[jj];
+      const double2 v = csub(base, cmul(g, rowp[jj]));
+      a[jj] = (cq * 4 + jj == p) ? pc : v;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
+// acc(16x16, C layout) += sgn * Aop(16 x 16, k) * Bop(16 x 16), complex, 4 MFMA per k-step.
+// Aop(m, k) = A[(m) * lda + k], Bop(k, n) = B[k * ldb + n]  (LDS pointers)
+template <bool NEG>
+__device__ __forceinline__ void mma16_lds(d4& acr, d4& aci, const double2* A, int lda,
+                                          const double2* B, int ldb) {
+  const int l = threadIdx.x & 63;
+  const int lr = l & 15, lk = l >> 4;
+#pragma unroll
+  for (int ks = 0; ks < 16; ks += 4) {
+    const double2 av = A[lr * lda + ks + lk];
+    const double2 bv = B[(ks + lk) * ldb + lr];
+    const double ar = NEG ? -av.x : av.x, ai = NEG ? -av.y : av.y;
+    acr = __builtin_amdgcn_mfma_f64_16x16x4f64(ar, bv.x, acr, 0, 0, 0);
+    aci = __builtin_amdgcn_mfma_f64_16x16x4f64(ar, bv.y, aci, 0, 0, 0);
+    acr = __builtin_amdgcn_mfma_f64_16x16x4f64(-ai, bv.y, acr, 0, 0, 0);
+    aci = __builtin_amdgcn_mfma_f64_16x16x4f64(ai, bv.x, aci, 0, 0, 0);
+  }
+}
+
+}  // namespace dwh

@@ -18,7 +18,29 @@ struct Dims {
   int P;        // poles per chain
   int nbatch;   // nc * P
   int64_t mat;  // elements per padded matrix (Np*Np)
+  int nld;      // ln|det| partials per batch item (dense: nb pivot blocks; cr: Ly block inversions)
 };
+
+// Block cyclic-reduction path (dwhmc_cr.hip): every batch item owns a pool of
+// nblk BP x BP blocks (level-0 D/U/L, Schur complements, products, G blocks).
+struct CrDims {
+  int Lx, Ly, N, BP, P, nbatch, nblk;
+  int64_t item;   // elements per batch item pool (nblk * BP * BP)
+};
+// out = [cin] + sg * sum_{h<nt} A_h B_h over pool block indices (cin = -1: zero)
+struct CrTask {
+  int out, cin, nt, pad;
+  int a[4], b[4];
+};
+bool cr_supported_bp(int BP);
+void launch_cr_fill(const CrDims& c, double2* pool, const int* hcol, const double* hval,
+                    const int* Dcol, const double2* Dv, const double* ypole, hipStream_t s);
+void launch_cr_inv(const CrDims& c, double2* pool, const int* blk, const int* slot, int n,
+                   double* ldpart, hipStream_t s);
+void launch_cr_gemm(const CrDims& c, double2* pool, const CrTask* tasks, int ntasks, double sg,
+                    hipStream_t s);
+void launch_cr_gather(const CrDims& c, const double2* pool, const int64_t* goff,
+                      const int64_t* doff, double2* G12nn, double2* diagS, hipStream_t s);
 
 // dense h - i y_q (padded with identity) for every (chain, pole): R init input
 void launch_fill_hz(const Dims& d, double2* M, const int* hcol, const double* hval,

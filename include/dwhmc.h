@@ -50,6 +50,8 @@ typedef struct {
   double err_tanh;    /* sup |tanh - rational| of the table entry */
   double delta_cap;   /* guard on max|Δ_ij| */
   int64_t device_bytes;
+  int64_t algo;       /* 0 = dense Schur-complement Gauss-Jordan, 1 = block cyclic reduction */
+  int64_t block;      /* dense: GJ block (64); cr: padded lattice-row block BP >= 2 Lx */
 } dwh_info_t;
 
 /* ModelParameters + initialize_cache + init_static_H!
@@ -64,6 +66,21 @@ int dwh_create(dwh_ctx** ctx, int64_t Lx, int64_t Ly, double t, double tp, doubl
 int dwh_create_batched(dwh_ctx** ctx, int64_t Lx, int64_t Ly, double t, double tp, double mu,
                        double beta, double J, const int64_t* nn_table, const int64_t* nnn_table,
                        int64_t nchains, const double* disorder, double delta_cap, int32_t device);
+
+/* Factorisation algorithm of a context:
+ *   DWH_ALGO_DENSE  Schur complement over the static particle block + blocked
+ *                   Gauss-Jordan of the dense N x N complement per pole;
+ *   DWH_ALGO_CR     block cyclic reduction of the block-tridiagonal (lattice-row
+ *                   blocks, periodic) BdG matrix per pole; needs 2 Lx <= 96;
+ *   DWH_ALGO_AUTO   DWHMC_ALGO from the environment (dense | cr | auto), else CR
+ *                   when supported.  Both give the same results to fp64 rounding. */
+enum { DWH_ALGO_AUTO = -1, DWH_ALGO_DENSE = 0, DWH_ALGO_CR = 1 };
+
+/* dwh_create_batched with an explicit algorithm. */
+int dwh_create_ex(dwh_ctx** ctx, int64_t Lx, int64_t Ly, double t, double tp, double mu,
+                  double beta, double J, const int64_t* nn_table, const int64_t* nnn_table,
+                  int64_t nchains, const double* disorder, double delta_cap, int32_t algo,
+                  int32_t device);
 
 void dwh_destroy(dwh_ctx* ctx);
 const char* dwh_last_error(const dwh_ctx* ctx);
@@ -122,11 +139,13 @@ int dwh_stream(dwh_ctx* ctx, void** stream);
 /* Kernel timing with HIP events on the stream each kernel runs on
  * (bench/profiling).  enable is a bitmask over the timer names below
  * (bit 0 "gj_update", bit 1 "gj_pivot", bit 2 "assemble", bit 3 "contract",
- * bit 4 "step", bit 5 "gj_edge"); 0 disables, -1 times everything. */
+ * bit 4 "step", bit 5 "gj_edge", bit 6 "cr_gemm", bit 7 "cr_inv"); 0 disables, -1 times
+ * everything. */
 int dwh_timing_enable(dwh_ctx* ctx, int32_t enable);
 /* name: "gj_update" (rank-128 paired / rank-64 trailing updates),
  * "gj_edge" (edge update between the two pivots of a pair), "gj_pivot",
- * "assemble", "contract", "step"; returns total milliseconds, launches and the
+ * "cr_gemm" (cyclic-reduction block products), "cr_inv" (its block
+ * inversions), "assemble", "contract", "step"; returns total milliseconds, launches and the
  * algorithmic work summed over launches (fp64 flops; HBM bytes for
  * "assemble"). */
 int dwh_timing_read(dwh_ctx* ctx, const char* name, double* total_ms, int64_t* launches,

@@ -28,9 +28,18 @@ def make_case(O, Lx, Ly, beta, seed, W=1.0, nimp=0.05, amp=0.3, mu=MU, tp=TP, Jc
     return p, st.disorder_pot, Delta
 
 
-def device_ctx(dwhmc, p, disorder, **kw):
-    return dwhmc.FermionContext(p.Lx, p.Ly, p.t, p.tp, p.mu, p.beta, p.J, p.nn_table, p.nnn_table,
-                                disorder, **kw)
+@pytest.fixture(params=["cr", "dense"])
+def algo(request):
+    """Both factorisations (include/dwhmc.h DWH_ALGO_*) must meet the same bar."""
+    return request.param
+
+
+def device_ctx(dwhmc, p, disorder, algo="auto", **kw):
+    ctx = dwhmc.FermionContext(p.Lx, p.Ly, p.t, p.tp, p.mu, p.beta, p.J, p.nn_table, p.nnn_table,
+                               disorder, algo=algo, **kw)
+    if algo != "auto":
+        assert ctx.info["algo"] == {"dense": 0, "cr": 1}[algo]
+    return ctx
 
 
 def test_mfma_f64_layout(dwhmc):
@@ -40,12 +49,12 @@ def test_mfma_f64_layout(dwhmc):
 @pytest.mark.parametrize("Lx,Ly,beta", [(4, 4, 4.0), (6, 6, 8.0), (5, 7, 16.0), (8, 8, 16.0),
                                         (16, 16, 8.0), (16, 8, 16.0), (3, 3, 4.0), (2, 2, 4.0),
                                         (2, 5, 8.0)])
-def test_factorize_matches_oracle(dwhmc, oracle, Lx, Ly, beta):
+def test_factorize_matches_oracle(dwhmc, oracle, Lx, Ly, beta, algo):
     O = oracle
     p, dis, Delta = make_case(O, Lx, Ly, beta, seed=Lx * 100 + Ly)
     cache, F_ref, Ef_ref = O.evaluate(p, dis, Delta)
     P_ref, _ = O.pairing_P(cache.U, cache.E_n, p)
-    ctx = device_ctx(dwhmc, p, dis)
+    ctx = device_ctx(dwhmc, p, dis, algo)
     ctx.set_pairing(Delta)
     ctx.factorize()
     P = ctx.pairing()[0]
@@ -61,12 +70,12 @@ def test_factorize_matches_oracle(dwhmc, oracle, Lx, Ly, beta):
     ctx.close()
 
 
-def test_full_size_L32_beta16(dwhmc, oracle):
+def test_full_size_L32_beta16(dwhmc, oracle, algo):
     """BASELINE config C3 size (N = 1024, n = 2048) against the eigen oracle."""
     O = oracle
     p, dis, Delta = make_case(O, 32, 32, 16.0, seed=3232)
     cache, F_ref, Ef_ref = O.evaluate(p, dis, Delta)
-    ctx = device_ctx(dwhmc, p, dis)
+    ctx = device_ctx(dwhmc, p, dis, algo)
     ctx.set_pairing(Delta)
     ctx.factorize()
     F = ctx.forces()[0]
@@ -76,13 +85,13 @@ def test_full_size_L32_beta16(dwhmc, oracle):
     ctx.close()
 
 
-def test_full_size_L48_beta32_batched(dwhmc, oracle):
+def test_full_size_L48_beta32_batched(dwhmc, oracle, algo):
     """BASELINE config C5 size (N = 2304, n = 4608, β = 32), two batched
     chains with different disorder, against the eigen oracle."""
     O = oracle
     cases = [make_case(O, 48, 48, 32.0, seed=s) for s in (4848, 4849)]
     p = cases[0][0]
-    ctx = device_ctx(dwhmc, p, np.stack([c[1] for c in cases]))
+    ctx = device_ctx(dwhmc, p, np.stack([c[1] for c in cases]), algo)
     assert ctx.info["npoles"] >= 15
     ctx.set_pairing(np.stack([c[2] for c in cases]))
     ctx.factorize()
@@ -95,13 +104,13 @@ def test_full_size_L48_beta32_batched(dwhmc, oracle):
     ctx.close()
 
 
-def test_batched_chains_independent(dwhmc, oracle):
+def test_batched_chains_independent(dwhmc, oracle, algo):
     O = oracle
     cases = [make_case(O, 6, 6, 8.0, seed=s) for s in (1, 2, 3)]
     p = cases[0][0]
     dis = np.stack([c[1] for c in cases])
     Delta = np.stack([c[2] for c in cases])
-    ctx = device_ctx(dwhmc, p, dis)
+    ctx = device_ctx(dwhmc, p, dis, algo)
     ctx.set_pairing(Delta)
     ctx.factorize()
     F = ctx.forces()
@@ -113,14 +122,14 @@ def test_batched_chains_independent(dwhmc, oracle):
     ctx.close()
 
 
-def test_clean_dwave_closed_form_on_device(dwhmc, oracle):
+def test_clean_dwave_closed_form_on_device(dwhmc, oracle, algo):
     """I5 / scripts/benchmark_clean.jl:15-43 directly on the HIP path."""
     O = oracle
     L, beta, D0 = 8, 16.0, 0.25
     p = O.ModelParameters(L, L, T, TP, MU, 0.0, 0.0, beta, J, 1.0)
     Delta = np.stack([np.full(p.N, D0), np.full(p.N, -D0)], axis=1).astype(np.complex128)
     _, Px, Fx, Ef = O.clean_dwave_closed_form(D0, L, L, T, TP, MU, beta, J)
-    ctx = device_ctx(dwhmc, p, np.zeros(p.N))
+    ctx = device_ctx(dwhmc, p, np.zeros(p.N), algo)
     ctx.set_pairing(Delta)
     ctx.factorize()
     P = ctx.pairing()[0]
@@ -147,7 +156,7 @@ def _oracle_after_sweeps(O, p, dis, Delta0, draws, Nt, dt, factorize_first=True)
 
 
 @pytest.mark.parametrize("factorize_first", [True, False])
-def test_hmc_sweep_matches_oracle(dwhmc, oracle, factorize_first):
+def test_hmc_sweep_matches_oracle(dwhmc, oracle, factorize_first, algo):
     """hmc_sweep! (src/HMC.jl:71-144) with injected draws; factorize_first=False
     reproduces the zeroed-cache first sweep of scripts/benchmark_clean.jl:82-88."""
     O = oracle
@@ -158,7 +167,7 @@ def test_hmc_sweep_matches_oracle(dwhmc, oracle, factorize_first):
     draws = [((rng.standard_normal((p.N, 2)) + 1j * rng.standard_normal((p.N, 2))) * math.sqrt(0.5),
               float(rng.random())) for _ in range(4)]
     ref = _oracle_after_sweeps(O, p, dis, Delta0, draws, Nt, dt, factorize_first)
-    ctx = device_ctx(dwhmc, p, dis)
+    ctx = device_ctx(dwhmc, p, dis, algo)
     ctx.set_pairing(Delta0)
     if factorize_first:
         ctx.factorize()
@@ -172,7 +181,7 @@ def test_hmc_sweep_matches_oracle(dwhmc, oracle, factorize_first):
     ctx.close()
 
 
-def test_throughput_path_equals_single_sweeps(dwhmc, oracle):
+def test_throughput_path_equals_single_sweeps(dwhmc, oracle, algo):
     O = oracle
     p, dis, Delta0 = make_case(O, 8, 8, 8.0, seed=9, amp=0.1)
     Nt, ns = 4, 3
@@ -182,12 +191,12 @@ def test_throughput_path_equals_single_sweeps(dwhmc, oracle):
     uni = rng.random((ns, 2))
     dis2 = np.stack([dis, dis[::-1].copy()])
     D2 = np.stack([Delta0, Delta0[::-1].copy()])
-    a = device_ctx(dwhmc, p, dis2)
+    a = device_ctx(dwhmc, p, dis2, algo)
     a.set_pairing(D2)
     a.factorize()
     res_single = [a.hmc_sweep(noise[s], uni[s], Nt, dt, p.mass) for s in range(ns)]
     Da, _ = a.get_state()
-    b = device_ctx(dwhmc, p, dis2)
+    b = device_ctx(dwhmc, p, dis2, algo)
     b.set_pairing(D2)
     b.factorize()
     b.load_draws(noise, uni)
@@ -202,10 +211,10 @@ def test_throughput_path_equals_single_sweeps(dwhmc, oracle):
     b.close()
 
 
-def test_spectrum_guard_trips(dwhmc, oracle):
+def test_spectrum_guard_trips(dwhmc, oracle, algo):
     O = oracle
     p, dis, Delta0 = make_case(O, 4, 4, 4.0, seed=1, amp=0.9)
-    ctx = device_ctx(dwhmc, p, dis, delta_cap=0.5)
+    ctx = device_ctx(dwhmc, p, dis, algo, delta_cap=0.5)
     ctx.set_pairing(Delta0)
     ctx.factorize()
     noise = np.zeros((p.N, 2), dtype=np.complex128)
@@ -239,12 +248,12 @@ def test_host_mirror_api_roundtrip(dwhmc, oracle):
 
 
 @pytest.mark.parametrize("L", [4, 8])
-def test_golden_fixture_on_device(dwhmc, L):
+def test_golden_fixture_on_device(dwhmc, L, algo):
     """Committed oracle vectors (tests/golden/oracle_L*.npz, tools/make_golden.py)."""
     import os
     g = np.load(os.path.join(os.path.dirname(__file__), "golden", f"oracle_L{L}.npz"), allow_pickle=False)
     beta = float(g["beta"])
-    ctx = dwhmc.FermionContext(L, L, T, TP, MU, beta, J, g["nn"], g["nnn"], g["disorder"])
+    ctx = dwhmc.FermionContext(L, L, T, TP, MU, beta, J, g["nn"], g["nnn"], g["disorder"], algo=algo)
     ctx.set_pairing(g["Delta"])
     ctx.factorize()
     F = ctx.forces()[0]
@@ -256,4 +265,36 @@ def test_golden_fixture_on_device(dwhmc, L):
     assert bool(acc[0]) == bool(g["sweep_accepted"])
     D, pi = ctx.get_state()
     assert np.max(np.abs(D[0] - g["sweep_Delta"])) <= 1e-10
+    ctx.close()
+
+
+def test_cr_block_limit(dwhmc, oracle):
+    """DWH_ALGO_CR needs the padded lattice-row block 2 Lx <= 96; auto falls back to dense."""
+    O = oracle
+    p, dis, _ = make_case(O, 49, 2, 4.0, seed=1)
+    with pytest.raises(ValueError):
+        device_ctx(dwhmc, p, dis, "cr")
+    ctx = device_ctx(dwhmc, p, dis)
+    assert ctx.info["algo"] == 0
+    ctx.close()
+
+
+@pytest.mark.parametrize("Lx,Ly", [(4, 1), (6, 2), (5, 3), (3, 9), (7, 6), (48, 5), (16, 13)])
+def test_cr_ragged_chains(dwhmc, oracle, Lx, Ly):
+    """Cyclic-reduction chains of every shape: Ly = 1 (one block), 2 (single
+    off-diagonal block), odd lengths at every level, padded blocks (2 Lx not a
+    multiple of 32), against the eigen oracle."""
+    O = oracle
+    p, dis, Delta = make_case(O, Lx, Ly, 8.0, seed=Lx * 31 + Ly)
+    cache, F_ref, Ef_ref = O.evaluate(p, dis, Delta)
+    P_ref, _ = O.pairing_P(cache.U, cache.E_n, p)
+    ctx = device_ctx(dwhmc, p, dis, "cr")
+    ctx.set_pairing(Delta)
+    ctx.factorize()
+    assert np.max(np.abs(ctx.pairing()[0] - P_ref)) <= 1e-11
+    assert np.max(np.abs(ctx.forces()[0] - F_ref)) <= 1e-10 * (1 + np.max(np.abs(F_ref)))
+    Ef = ctx.fermion_energy()[0]
+    assert abs(Ef - Ef_ref) <= 1e-11 * abs(Ef_ref), (Ef, Ef_ref)
+    hole_ref = O.measure_observables(cache, p, Delta)["hole_conc"]
+    assert abs(2.0 * ctx.hole_trace()[0] / p.N - 1.0 - hole_ref) <= 1e-11
     ctx.close()
