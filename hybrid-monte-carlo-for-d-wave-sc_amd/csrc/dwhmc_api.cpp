@@ -45,10 +45,11 @@ enum Algo { ALGO_DENSE = 0, ALGO_CR = 1 };
 // One stage of the cyclic-reduction plan: a batch of block inversions or a
 // task list of block products (all batch items at once).
 struct CrStage {
-  int kind;      // 0 inversion, 1 products
-  int first, n;  // range in CrPlan::inv_blk / CrPlan::tasks
-  double sg;     // products: sign of the sum
-  int terms;     // products: total K = BP terms over the tasks
+  int kind;        // 0 inversion, 1 products
+  int first, n;    // range in CrPlan::inv_blk / CrPlan::tasks
+  double sg;       // products: sign of the sum
+  double flops;    // products: algorithmic fp64 flops per batch item (restricted ranges)
+  int maxt32, maxt16;
 };
 
 struct CrPlan {
@@ -57,6 +58,8 @@ struct CrPlan {
   std::vector<dwh::CrTask> tasks;
   std::vector<int> inv_blk, inv_slot;
   std::vector<int64_t> goff, doff;
+  std::vector<int> fill_all, fill_step;      // level-0 blocks written at create / every step
+  std::vector<int64_t> off_ph, off_hp;       // pairing entries outside fill_step (-1: none)
 };
 
 // Block cyclic reduction of the periodic block-tridiagonal H_BdG - i y (blocks
@@ -81,7 +84,7 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol) {
     std::vector<char> elim;
   };
   auto add_inv = [&](const std::vector<int>& blocks, int& slot) {
-    CrStage st{0, (int)pl.inv_blk.size(), (int)blocks.size(), 0.0, 0};
+    CrStage st{0, (int)pl.inv_blk.size(), (int)blocks.size(), 0.0, 0.0, 0, 0};
     for (int b : blocks) {
       pl.inv_blk.push_back(b);
       pl.inv_slot.push_back(slot++);
@@ -90,10 +93,16 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol) {
   };
   struct Term { int a, b; };
   std::vector<dwh::CrTask> cur_tasks;
+  // output window of the next tasks (full block unless restricted)
+  int w_r0 = 0, w_r1 = BP, w_c0 = 0, w_c1 = BP;
   auto task = [&](int out, int cin, std::initializer_list<Term> terms) {
     dwh::CrTask t{};
     t.out = out;
     t.cin = cin;
+    t.r0 = w_r0;
+    t.r1 = w_r1;
+    t.c0 = w_c0;
+    t.c1 = w_c1;
     t.nt = 0;
     for (const Term& x : terms) {
       t.a[t.nt] = x.a;
@@ -104,9 +113,11 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol) {
   };
   auto flush = [&](double sg) {
     if (cur_tasks.empty()) return;
-    CrStage st{1, (int)pl.tasks.size(), (int)cur_tasks.size(), sg, 0};
+    CrStage st{1, (int)pl.tasks.size(), (int)cur_tasks.size(), sg, 0.0, 0, 0};
     for (auto& t : cur_tasks) {
-      st.terms += t.nt;
+      st.flops += 8.0 * t.nt * BP * (double)(t.r1 - t.r0) * (t.c1 - t.c0);
+      st.maxt32 = std::max(st.maxt32, dwh::cr_task_tiles(t, 32));
+      st.maxt16 = std::max(st.maxt16, dwh::cr_task_tiles(t, 16));
       pl.tasks.push_back(t);
     }
     pl.stages.push_back(st);
@@ -202,6 +213,12 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol) {
         gl[k] = GL[kk];
       }
     }
+    // Level 0 is the last backward level: only the entries the force and
+    // Tr rho_hh read are formed there -- the particle-hole quadrant of G_ea,
+    // G_ec (cross-row bonds) and the hole columns of G_ae, G_ce, G_ee (G_ee:
+    // in-row bonds and the hole diagonal; G_ae, G_ce: also its operands).
+    const bool sel = (li == 0);
+    const int P0 = 0, P1 = sel ? Lx : BP, H0 = sel ? Lx : 0, H1 = sel ? 2 * Lx : BP;
     std::vector<int> Gae(m, -1), Gce(m, -1);
     for (int e : lv.E) {
       const int a = e - 1, c = (e + 1) % m;
@@ -210,8 +227,10 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol) {
       const int Gac = mn == 1 ? GD[0] : GU[ia];
       const int Gca = mn == 1 ? GD[0] : GL[ia];
       const int gea = nb(), gec = nb(), gae = nb(), gce = nb();
+      w_r0 = P0; w_r1 = P1; w_c0 = H0; w_c1 = H1;
       task(gea, -1, {{lv.W1[e], Gaa}, {lv.W2[e], Gca}});
       task(gec, -1, {{lv.W1[e], Gac}, {lv.W2[e], Gcc}});
+      w_r0 = 0; w_r1 = BP;
       task(gae, -1, {{Gaa, lv.V1[e]}, {Gac, lv.V2[e]}});
       task(gce, -1, {{Gca, lv.V1[e]}, {Gcc, lv.V2[e]}});
       gu[a] = gae;
@@ -227,6 +246,8 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol) {
       gd[e] = lv.D[e];
     }
     flush(1.0);
+    w_c0 = 0;
+    w_c1 = BP;
     GD = gd;
     GU = gu;
     GL = gl;
@@ -250,6 +271,34 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol) {
     }
     pl.doff[i] = GD[y] * BB + (int64_t)(Lx + x) * BP + (Lx + x);
   }
+  // level-0 fill lists and pairing scatter offsets: CR overwrites only the
+  // level-0 eliminated D blocks (in-place inversion, then G_ee)
+  std::vector<char> rewrite(3 * Ly, 0);
+  if (!levels.empty())
+    for (int e : levels[0].E) rewrite[levels[0].D[e]] = 1;
+  else
+    rewrite[0] = 1;   // Ly == 1: the single block is inverted in place
+  for (int b = 0; b < 3 * Ly; ++b) {
+    pl.fill_all.push_back(b);
+    if (rewrite[b]) pl.fill_step.push_back(b);
+  }
+  pl.off_ph.assign((size_t)N * kSlots, -1);
+  pl.off_hp.assign((size_t)N * kSlots, -1);
+  auto blk_of = [&](int yr, int yc) {
+    if (yc == yr) return yr;                              // D[yr]
+    if (Ly >= 2 && yc == (yr + 1) % Ly) return Ly + yr;   // U[yr]
+    return 2 * Ly + yc;                                   // L[yc] = A[yc+1, yc]
+  };
+  for (int i = 0; i < N; ++i)
+    for (int s = 0; s < kSlots; ++s) {
+      const int j = Dcol[(size_t)i * kSlots + s];
+      if (j < 0) continue;
+      const int yi = i / Lx, xi = i % Lx, yj = j / Lx, xj = j % Lx;
+      const int b = blk_of(yi, yj);
+      if (rewrite[b]) continue;
+      pl.off_ph[(size_t)i * kSlots + s] = b * BB + (int64_t)xi * BP + (Lx + xj);
+      pl.off_hp[(size_t)i * kSlots + s] = b * BB + (int64_t)(Lx + xi) * BP + xj;
+    }
   pl.nblk = nblk;
   return pl;
 }
@@ -314,7 +363,8 @@ struct dwh_ctx {
   double2* bpool = nullptr;   // CR block pool (nbatch x nblk blocks)
   dwh::CrTask* d_tasks = nullptr;
   int *d_inv_blk = nullptr, *d_inv_slot = nullptr;
-  int64_t *d_goff = nullptr, *d_doff = nullptr;
+  int64_t *d_goff = nullptr, *d_doff = nullptr, *d_off_ph = nullptr, *d_off_hp = nullptr;
+  int *d_fill_all = nullptr, *d_fill_step = nullptr;
 
   // timing
   int timing = 0;   // bitmask over TimerName (bit i = kTimerNames[i])
@@ -361,7 +411,9 @@ hipEvent_t take_event(dwh_ctx* ctx) {
     return e;
   }
   hipEvent_t e;
-  (void)hipEventCreate(&e);
+  // no system-scope fence per record: the timers bracket device kernels only,
+  // and the fence's L2 writeback would perturb the kernels being timed
+  (void)hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
   return e;
 }
 
@@ -475,8 +527,11 @@ void cr_enqueue(dwh_ctx* ctx) {
   const double bp3 = 8.0 * c.BP * (double)c.BP * c.BP * c.nbatch;
   {
     // bytes written: the 3 Ly level-0 blocks of every batch item
-    Scope s(ctx, T_ASSEMBLE, 3.0 * c.Ly * 16.0 * c.BP * (double)c.BP * c.nbatch);
-    dwh::launch_cr_fill(c, ctx->bpool, ctx->hcol, ctx->hval, ctx->Dcol, ctx->Dv, ctx->d_y, ctx->stream);
+    const CrPlan& pl = ctx->plan;
+    Scope s(ctx, T_ASSEMBLE, (double)pl.fill_step.size() * 16.0 * c.BP * (double)c.BP * c.nbatch);
+    dwh::launch_cr_fill(c, ctx->bpool, ctx->d_fill_step, (int)pl.fill_step.size(), ctx->hcol, ctx->hval,
+                        ctx->Dcol, ctx->Dv, ctx->d_y, ctx->stream);
+    dwh::launch_cr_pair_scatter(c, ctx->bpool, ctx->d_off_ph, ctx->d_off_hp, ctx->Dv, ctx->stream);
   }
   for (const CrStage& st : ctx->plan.stages) {
     if (st.kind == 0) {
@@ -484,8 +539,9 @@ void cr_enqueue(dwh_ctx* ctx) {
       dwh::launch_cr_inv(c, ctx->bpool, ctx->d_inv_blk + st.first, ctx->d_inv_slot + st.first, st.n,
                          ctx->ldpart, ctx->stream);
     } else {
-      Scope s(ctx, T_CR_GEMM, st.terms * bp3);
-      dwh::launch_cr_gemm(c, ctx->bpool, ctx->d_tasks + st.first, st.n, st.sg, ctx->stream);
+      Scope s(ctx, T_CR_GEMM, st.flops * c.nbatch);
+      dwh::launch_cr_gemm(c, ctx->bpool, ctx->d_tasks + st.first, st.n, st.maxt32, st.maxt16, st.sg,
+                          ctx->stream);
     }
   }
   {
@@ -801,6 +857,10 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     ALLOC(d_inv_slot, pl.inv_slot.size());
     ALLOC(d_goff, pl.goff.size());
     ALLOC(d_doff, pl.doff.size());
+    ALLOC(d_off_ph, pl.off_ph.size());
+    ALLOC(d_off_hp, pl.off_hp.size());
+    ALLOC(d_fill_all, pl.fill_all.size());
+    ALLOC(d_fill_step, pl.fill_step.size());
   }
   ALLOC(Dv, (size_t)d.nc * N * kSlots);
   ALLOC(G12nn, (size_t)d.nbatch * N * kSlots);
@@ -856,6 +916,10 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     UP(d_inv_slot, pl.inv_slot.data(), pl.inv_slot.size());
     UP(d_goff, pl.goff.data(), pl.goff.size());
     UP(d_doff, pl.doff.data(), pl.doff.size());
+    UP(d_off_ph, pl.off_ph.data(), pl.off_ph.size());
+    UP(d_off_hp, pl.off_hp.data(), pl.off_hp.size());
+    UP(d_fill_all, pl.fill_all.data(), pl.fill_all.size());
+    UP(d_fill_step, pl.fill_step.data(), pl.fill_step.size());
   }
 #undef UP
   // zeroed cache, like initialize_cache (src/Types.jl:182-212): P = 0, E_f = 0
@@ -873,8 +937,12 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     run_gj(ctx, ctx->R);
     dwh::launch_sum_ld(d, ctx->ldpart, ctx->ldstatic, s);
   } else {
-    // the CR path factorises the whole BdG matrix: no static part
+    // the CR path factorises the whole BdG matrix: no static part; every
+    // level-0 block written once (pairing entries 0 until the first factorize)
     (void)hipMemsetAsync(ctx->ldstatic, 0, d.nbatch * sizeof(double), s);
+    (void)hipMemsetAsync(ctx->Dv, 0, (size_t)d.nc * N * kSlots * sizeof(double2), s);
+    dwh::launch_cr_fill(ctx->cr, ctx->bpool, ctx->d_fill_all, (int)ctx->plan.fill_all.size(), ctx->hcol,
+                        ctx->hval, ctx->Dcol, ctx->Dv, ctx->d_y, s);
   }
   if (hipStreamSynchronize(s) != hipSuccess || hipGetLastError() != hipSuccess) {
     ctx->err = "static R initialisation failed on the device";

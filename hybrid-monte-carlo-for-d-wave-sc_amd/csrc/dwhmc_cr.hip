@@ -16,20 +16,44 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
+
 #include "dwhmc_device.h"
 #include "dwhmc_internal.h"
 
 namespace dwh {
 
+// Diagnostic build only (-DCR_STAMPS, tools/micro/cr_inv_stamps.hip): per-block
+// s_memtime stamps of k_cr_inv's phases; never compiled into the library.
+#ifdef CR_STAMPS
+__device__ unsigned long long g_cr_stamps[1024][16];
+#define CR_STAMP(i)                                                                  \
+  do {                                                                               \
+    __builtin_amdgcn_sched_barrier(0);                                               \
+    if (threadIdx.x == 0)                                                            \
+      g_cr_stamps[blockIdx.y * gridDim.x + blockIdx.x][i] = __builtin_amdgcn_s_memtime(); \
+    __builtin_amdgcn_sched_barrier(0);                                               \
+  } while (0)
+#else
+#define CR_STAMP(i) \
+  do {              \
+  } while (0)
+#endif
+
 // ---------------------------------------------------------------------------
 // Level-0 blocks D[y] (pool block y), U[y] = A[y, y+1] (Ly + y), L[y] =
 // A[y+1, y] (2 Ly + y) of A = H_BdG - i y_q for every (chain, pole); one wave
-// per block row, lanes over columns (coalesced row writes).  Ly == 2: the
-// single off-diagonal block lives in U (L = 0); Ly == 1: everything in D.
-// Padding rows/columns (b <= r < BP) are the identity in D, zero elsewhere.
+// per block row, lanes over columns (coalesced row writes), over the blocks of
+// `list` (level-0 block ids).  Ly == 2: the single off-diagonal block lives in
+// U (L = 0); Ly == 1: everything in D.  Padding rows/columns (b <= r < BP) are
+// the identity in D, zero elsewhere.  All blocks are written once at context
+// creation; per factorisation only the blocks CR overwrites (the level-0
+// eliminated D blocks) are rewritten and k_cr_pair_scatter refreshes the
+// pairing entries of the others.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_cr_fill(double2* __restrict__ pool, int64_t item, int Lx,
                                                  int Ly, int BP, int P, int nrows,
+                                                 const int* __restrict__ list,
                                                  const int* __restrict__ hcol,
                                                  const double* __restrict__ hval,
                                                  const int* __restrict__ Dcol,
@@ -40,9 +64,8 @@ __global__ __launch_bounds__(256) void k_cr_fill(double2* __restrict__ pool, int
   if (row >= nrows) return;
   const int bi = blockIdx.y, c = bi / P, q = bi - c * P;
   const int N = Lx * Ly, b = 2 * Lx;
-  const int t = row / (Ly * BP);              // 0 D, 1 U, 2 L
-  const int rem = row - t * Ly * BP;
-  const int y = rem / BP, r = rem - y * BP;
+  const int lb = list[row / BP], r = row - (row / BP) * BP;
+  const int t = lb / Ly, y = lb - t * Ly;     // t: 0 D, 1 U, 2 L
   double2* out = pool + (int64_t)bi * item + ((int64_t)(t * Ly + y) * BP + r) * BP;
   const bool zero = (t == 1 && Ly < 2) || (t == 2 && Ly < 3);
   const int yr = (t == 2) ? (y + 1) % Ly : y;
@@ -86,6 +109,24 @@ __global__ __launch_bounds__(256) void k_cr_fill(double2* __restrict__ pool, int
   }
 }
 
+// Pairing entries Δ/2 (particle row, hole column) and conj (hole row, particle
+// column) into the level-0 blocks CR does not overwrite (offsets from the
+// planner; -1 = entry lies in a rewritten block or the slot is empty).
+__global__ void k_cr_pair_scatter(double2* __restrict__ pool, int64_t item, int N, int P,
+                                  const int64_t* __restrict__ off_ph,
+                                  const int64_t* __restrict__ off_hp,
+                                  const double2* __restrict__ Dv) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int bi = blockIdx.y, c = bi / P;
+  if (e >= N * kSlots) return;
+  const int i = e / kSlots, sl = e - i * kSlots;
+  const double2 v = Dv[(int64_t)c * N * kSlots + (int64_t)sl * N + i];
+  double2* base = pool + (int64_t)bi * item;
+  const int64_t o1 = off_ph[e], o2 = off_hp[e];
+  if (o1 >= 0) base[o1] = v;
+  if (o2 >= 0) base[o2] = make_double2(v.x, -v.y);
+}
+
 // ---------------------------------------------------------------------------
 // In-place no-pivot Gauss-Jordan inversion of BP x BP blocks (BP = 16 NT),
 // register resident: the 2x2 wave grid owns NT/2 x NT/2 MFMA tiles each (C
@@ -107,14 +148,14 @@ __global__ __launch_bounds__(256) void k_cr_inv(double2* __restrict__ pool, int6
   __shared__ double2 Cp[BP * 17];
   __shared__ double2 Dw[4][16 * 17];
   __shared__ double2 Xw[4][16 * XS];
-  __shared__ double2 xbw[4][32];
-  __shared__ double pm[BP];
   const int bi = blockIdx.y, li = blockIdx.x;
+  double ld = 0.0;   // Σ ln|pivots| (identical in every wave)
   double2* M = pool + (int64_t)bi * item + (int64_t)blk[li] * BP * BP;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const int lr = l & 15, lk = l >> 4;
   const int I0 = (w >> 1) * TH, J0 = (w & 1) * TH;
   d4 ar[TH][TH], ai[TH][TH];
+  CR_STAMP(0);
 #pragma unroll
   for (int ti = 0; ti < TH; ++ti)
 #pragma unroll
@@ -125,6 +166,7 @@ __global__ __launch_bounds__(256) void k_cr_inv(double2* __restrict__ pool, int6
         ar[ti][tj][rr] = v.x;
         ai[ti][tj][rr] = v.y;
       }
+  CR_STAMP(1);
 #pragma unroll 1
   for (int kb = 0; kb < NT; ++kb) {
     // (1) publish block row kb and block column kb
@@ -147,13 +189,15 @@ __global__ __launch_bounds__(256) void k_cr_inv(double2* __restrict__ pool, int6
             Cp[((I0 + ti) * 16 + lk + 4 * rr) * 17 + lr] = make_double2(ar[ti][tj][rr], ai[ti][tj][rr]);
       }
     __syncthreads();
-    // (2) every wave inverts the pivot tile
+    if (kb == 0) CR_STAMP(2);
+    // (2) every wave inverts the pivot tile in registers (lane: row l&15, cols 4(l>>4)..)
     double2 dv[4];
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) dv[jj] = Rp[(l >> 2) * RS + kb * 16 + (l & 3) * 4 + jj];
-    wave_inv16(dv, xbw[w], w == 0 ? pm : nullptr, kb * 16);
+    for (int jj = 0; jj < 4; ++jj) dv[jj] = Rp[(l & 15) * RS + kb * 16 + (l >> 4) * 4 + jj];
+    ld += 0.5 * log(wave_inv16_dpp(dv));
+    if (kb == 0) CR_STAMP(3);
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) Dw[w][(l >> 2) * 17 + (l & 3) * 4 + jj] = dv[jj];
+    for (int jj = 0; jj < 4; ++jj) Dw[w][(l & 15) * 17 + (l >> 4) * 4 + jj] = dv[jj];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -177,6 +221,7 @@ __global__ __launch_bounds__(256) void k_cr_inv(double2* __restrict__ pool, int6
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (kb == 0) CR_STAMP(4);
     // (4) tile updates
 #pragma unroll
     for (int ti = 0; ti < TH; ++ti)
@@ -198,7 +243,9 @@ __global__ __launch_bounds__(256) void k_cr_inv(double2* __restrict__ pool, int6
         }
       }
     __syncthreads();
+    if (kb == 0) CR_STAMP(5);
   }
+  CR_STAMP(6);
 #pragma unroll
   for (int ti = 0; ti < TH; ++ti)
 #pragma unroll
@@ -207,38 +254,25 @@ __global__ __launch_bounds__(256) void k_cr_inv(double2* __restrict__ pool, int6
       for (int rr = 0; rr < 4; ++rr)
         M[(int64_t)((I0 + ti) * 16 + lk + 4 * rr) * BP + (J0 + tj) * 16 + lr] =
             make_double2(ar[ti][tj][rr], ai[ti][tj][rr]);
-  if (w == 0) {
-    double s = 0.0;
-    for (int p = l; p < BP; p += 64) s += 0.5 * log(pm[p]);
-    s = wave_sum(s);
-    if (l == 0) ldpart[(int64_t)bi * nslots + slot[li]] = s;
-  }
+  if (tid == 0) ldpart[(int64_t)bi * nslots + slot[li]] = ld;
+  CR_STAMP(7);
 }
 
 // ---------------------------------------------------------------------------
 // Batched block products: task t of batch item bi writes
 //   out = [cin] + sg Σ_{h < nt} A_h B_h      (BP x BP blocks of the item's pool)
-// One wave per 32x32 output tile, MFMA fragments straight from L2 with a
-// two-deep register prefetch, 1D grid with the XCD-aware remap so one item's
-// tasks share an XCD's L2.  out never aliases an operand (planner invariant);
-// out == cin is allowed.
+// One wave per TS x TS output tile (TS = 32: 2x2 MFMA tiles, operand reuse;
+// TS = 16: one MFMA tile with two interleaved accumulator chains, 4x the
+// waves for the small stages of the coarse levels, which are latency bound).
+// MFMA fragments come straight from L2 with a register prefetch; 1D grid with
+// the XCD-aware remap so one item's tasks share an XCD's L2.  out never
+// aliases an operand (planner invariant); out == cin is allowed.
 // ---------------------------------------------------------------------------
 template <int BP>
-__global__ __launch_bounds__(256) void k_cr_gemm(double2* __restrict__ pool, int64_t item,
-                                                 const CrTask* __restrict__ tasks, int ntasks,
-                                                 int total, double sg) {
-  constexpr int TW = BP / 32, TPT = TW * TW, KS = BP / 4;
+__device__ __forceinline__ void cr_tile32(double2* base, const CrTask* tk, int cin, int nt, int tr,
+                                          int tc, double sg) {
+  constexpr int KS = BP / 4;
   constexpr int64_t BB = (int64_t)BP * BP;
-  const int gw = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x) * 4 + (int)(threadIdx.x >> 6));
-  if (gw >= total) return;
-  const int per_item = ntasks * TPT;
-  const int bi = gw / per_item;
-  const int rmd = gw - bi * per_item;
-  const int tsk = rmd / TPT, tile = rmd - tsk * TPT;
-  const int tr = tile / TW, tc = tile - tr * TW;
-  const CrTask* tk = tasks + tsk;
-  const int cin = tk->cin, nt = tk->nt;
-  double2* base = pool + (int64_t)bi * item;
   const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
   d4 acr[2][2], aci[2][2];
 #pragma unroll
@@ -304,6 +338,78 @@ __global__ __launch_bounds__(256) void k_cr_gemm(double2* __restrict__ pool, int
         O[(int64_t)(mi * 16 + 4 * rr) * BP + ni * 16] = make_double2(acr[mi][ni][rr], aci[mi][ni][rr]);
 }
 
+template <int BP>
+__device__ __forceinline__ void cr_tile16(double2* base, const CrTask* tk, int cin, int nt, int tr,
+                                          int tc, double sg) {
+  constexpr int KS = BP / 4, PF = 4;
+  constexpr int64_t BB = (int64_t)BP * BP;
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  d4 acr[2], aci[2];
+  acr[1] = d4{0.0, 0.0, 0.0, 0.0};
+  aci[1] = d4{0.0, 0.0, 0.0, 0.0};
+  if (cin >= 0) {
+    const double2* C = base + cin * BB + (int64_t)(tr * 16 + lk) * BP + tc * 16 + lr;
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const double2 v = C[(int64_t)4 * rr * BP];
+      acr[0][rr] = v.x;
+      aci[0][rr] = v.y;
+    }
+  } else {
+    acr[0] = d4{0.0, 0.0, 0.0, 0.0};
+    aci[0] = d4{0.0, 0.0, 0.0, 0.0};
+  }
+#pragma unroll 1
+  for (int h = 0; h < nt; ++h) {
+    const double2* A = base + tk->a[h] * BB + (int64_t)(tr * 16 + lr) * BP + lk;
+    const double2* B = base + tk->b[h] * BB + (int64_t)lk * BP + tc * 16 + lr;
+    double2 fa[PF], fb[PF];
+#pragma unroll
+    for (int s = 0; s < PF; ++s) {
+      fa[s] = A[s * 4];
+      fb[s] = B[(int64_t)s * 4 * BP];
+    }
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int cs = s % PF, p = s & 1;
+      const double2 av = make_double2(sg * fa[cs].x, sg * fa[cs].y), bv = fb[cs];
+      if (s + PF < KS) {
+        fa[cs] = A[(s + PF) * 4];
+        fb[cs] = B[(int64_t)(s + PF) * 4 * BP];
+      }
+      acr[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.x, acr[p], 0, 0, 0);
+      aci[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.y, aci[p], 0, 0, 0);
+      acr[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av.y, bv.y, acr[p], 0, 0, 0);
+      aci[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, bv.x, aci[p], 0, 0, 0);
+    }
+  }
+  double2* O = base + tk->out * BB + (int64_t)(tr * 16 + lk) * BP + tc * 16 + lr;
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr)
+    O[(int64_t)4 * rr * BP] = make_double2(acr[0][rr] + acr[1][rr], aci[0][rr] + aci[1][rr]);
+}
+
+template <int BP, int TS>
+__global__ __launch_bounds__(256) void k_cr_gemm(double2* __restrict__ pool, int64_t item,
+                                                 const CrTask* __restrict__ tasks, int ntasks,
+                                                 int maxt, int total, double sg) {
+  const int gw = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x) * 4 + (int)(threadIdx.x >> 6));
+  if (gw >= total) return;
+  const int per_item = ntasks * maxt;
+  const int bi = gw / per_item;
+  const int rmd = gw - bi * per_item;
+  const int tsk = rmd / maxt, tile = rmd - tsk * maxt;
+  const CrTask* tk = tasks + tsk;
+  const int tr0 = tk->r0 / TS, tc0 = tk->c0 / TS;
+  const int ct = (tk->c1 + TS - 1) / TS - tc0;
+  const int rt = (tk->r1 + TS - 1) / TS - tr0;
+  if (tile >= rt * ct) return;   // restricted task: fewer tiles than the stage maximum
+  const int tr = tr0 + tile / ct, tc = tc0 + tile % ct;
+  double2* base = pool + (int64_t)bi * item;
+  if (TS == 32) cr_tile32<BP>(base, tk, tk->cin, tk->nt, tr, tc, sg);
+  else cr_tile16<BP>(base, tk, tk->cin, tk->nt, tr, tc, sg);
+}
+
 // ---------------------------------------------------------------------------
 // G12 at the pairing pattern and diag(G22) from the level-0 blocks of G
 // (element offsets precomputed by the planner; -1 = empty slot).
@@ -328,11 +434,19 @@ __global__ void k_cr_gather(const double2* __restrict__ pool, int64_t item, int 
 // ---------------------------------------------------------------------------
 bool cr_supported_bp(int BP) { return BP == 32 || BP == 64 || BP == 96; }
 
-void launch_cr_fill(const CrDims& c, double2* pool, const int* hcol, const double* hval,
-                    const int* Dcol, const double2* Dv, const double* ypole, hipStream_t s) {
-  const int nrows = 3 * c.Ly * c.BP;
+void launch_cr_fill(const CrDims& c, double2* pool, const int* list, int nlist, const int* hcol,
+                    const double* hval, const int* Dcol, const double2* Dv, const double* ypole,
+                    hipStream_t s) {
+  if (nlist <= 0) return;
+  const int nrows = nlist * c.BP;
   hipLaunchKernelGGL(k_cr_fill, dim3((nrows + 3) / 4, c.nbatch), dim3(256), 0, s, pool, c.item, c.Lx,
-                     c.Ly, c.BP, c.P, nrows, hcol, hval, Dcol, Dv, ypole);
+                     c.Ly, c.BP, c.P, nrows, list, hcol, hval, Dcol, Dv, ypole);
+}
+
+void launch_cr_pair_scatter(const CrDims& c, double2* pool, const int64_t* off_ph,
+                            const int64_t* off_hp, const double2* Dv, hipStream_t s) {
+  hipLaunchKernelGGL(k_cr_pair_scatter, dim3((c.N * kSlots + 255) / 256, c.nbatch), dim3(256), 0, s,
+                     pool, c.item, c.N, c.P, off_ph, off_hp, Dv);
 }
 
 void launch_cr_inv(const CrDims& c, double2* pool, const int* blk, const int* slot, int n,
@@ -346,17 +460,30 @@ void launch_cr_inv(const CrDims& c, double2* pool, const int* blk, const int* sl
   }
 }
 
-void launch_cr_gemm(const CrDims& c, double2* pool, const CrTask* tasks, int ntasks, double sg,
-                    hipStream_t s) {
+void launch_cr_gemm(const CrDims& c, double2* pool, const CrTask* tasks, int ntasks, int maxt32,
+                    int maxt16, double sg, hipStream_t s) {
   if (ntasks <= 0) return;
-  const int tpt = (c.BP / 32) * (c.BP / 32);
-  const int total = c.nbatch * ntasks * tpt;
-  const dim3 g((total + 3) / 4);
+  // latency-bound small stages (fewer than ~2 waves per SIMD at 32x32 tiles)
+  // run 16x16 wave tiles: 4x the waves, 4x shorter MFMA chains
+  static const int small = [] {
+    const char* e = std::getenv("DWHMC_CR_SMALL");
+    return e ? std::atoi(e) : 2048;
+  }();
+  const bool use16 = (int64_t)c.nbatch * ntasks * maxt32 < small;
+  const int maxt = use16 ? maxt16 : maxt32;
+  const int total = c.nbatch * ntasks * maxt;
+  const dim3 g((total + 3) / 4), b(256);
+#define CR_GEMM(BPV)                                                                             \
+  if (use16)                                                                                     \
+    hipLaunchKernelGGL((k_cr_gemm<BPV, 16>), g, b, 0, s, pool, c.item, tasks, ntasks, maxt, total, sg); \
+  else                                                                                           \
+    hipLaunchKernelGGL((k_cr_gemm<BPV, 32>), g, b, 0, s, pool, c.item, tasks, ntasks, maxt, total, sg);
   switch (c.BP) {
-    case 32: hipLaunchKernelGGL(k_cr_gemm<32>, g, dim3(256), 0, s, pool, c.item, tasks, ntasks, total, sg); break;
-    case 64: hipLaunchKernelGGL(k_cr_gemm<64>, g, dim3(256), 0, s, pool, c.item, tasks, ntasks, total, sg); break;
-    default: hipLaunchKernelGGL(k_cr_gemm<96>, g, dim3(256), 0, s, pool, c.item, tasks, ntasks, total, sg); break;
+    case 32: CR_GEMM(32) break;
+    case 64: CR_GEMM(64) break;
+    default: CR_GEMM(96) break;
   }
+#undef CR_GEMM
 }
 
 void launch_cr_gather(const CrDims& c, const double2* pool, const int64_t* goff,

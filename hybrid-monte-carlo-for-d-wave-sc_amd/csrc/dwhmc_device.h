@@ -6,6 +6,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <utility>
+
 namespace dwh {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
@@ -112,6 +114,84 @@ __device__ __forceinline__ void mma16_lds(d4& acr, d4& aci, const double2* A, in
     acr = __builtin_amdgcn_mfma_f64_16x16x4f64(-ai, bv.y, acr, 0, 0, 0);
     aci = __builtin_amdgcn_mfma_f64_16x16x4f64(ai, bv.x, aci, 0, 0, 0);
   }
+}
+
+// ---------------------------------------------------------------------------
+// Register-only 16x16 complex no-pivot Gauss-Jordan inversion in one wave.
+// Layout: lane l holds row r = l & 15, columns 4q .. 4q+3 with q = l >> 4.
+// Pivot p (compile time): row p reaches every lane of its 16-lane row through
+// DPP row_newbcast:p, column p reaches the other column quarters through
+// v_permlane16_swap / v_permlane32_swap, the pivot value through readlane.
+// No LDS, no barriers.  pprod accumulates Π |pivot|^2 (uniform in the wave).
+// ---------------------------------------------------------------------------
+template <int P>
+__device__ __forceinline__ double dpp_rowbcast(double x) {
+  // full row/bank masks + bound_ctrl: every lane is written, the old value is dead
+  return __builtin_amdgcn_update_dpp(x, x, 0x150 + P, 0xf, 0xf, true);
+}
+
+// value of quarter QS (lanes 16 QS .. 16 QS + 15) broadcast to all quarters, per row position
+template <int QS>
+__device__ __forceinline__ unsigned bcast_quarter_u32(unsigned u) {
+  const auto s16 = __builtin_amdgcn_permlane16_swap(u, u, false, false);   // [u0 u0 u2 u2], [u1 u1 u3 u3]
+  const unsigned y = (QS & 1) ? s16[1] : s16[0];
+  const auto s32 = __builtin_amdgcn_permlane32_swap(y, y, false, false);   // [y_lo y_lo], [y_hi y_hi]
+  return (QS & 2) ? s32[1] : s32[0];
+}
+template <int QS>
+__device__ __forceinline__ double bcast_quarter(double x) {
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, x);
+  const unsigned lo = bcast_quarter_u32<QS>((unsigned)b), hi = bcast_quarter_u32<QS>((unsigned)(b >> 32));
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ double readlane_f64(double x, int lane) {
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, x);
+  const unsigned lo = __builtin_amdgcn_readlane((unsigned)b, lane);
+  const unsigned hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), lane);
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+
+template <int P>
+__device__ __forceinline__ void inv16_step(double2 (&a)[4], double& pprod) {
+  constexpr int PS = P >> 2, PE = P & 3;
+  const int l = threadIdx.x & 63, r = l & 15, q = l >> 4;
+  double2 rowp[4];
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) rowp[jj] = make_double2(dpp_rowbcast<P>(a[jj].x), dpp_rowbcast<P>(a[jj].y));
+  const double2 colp = make_double2(bcast_quarter<PS>(a[PE].x), bcast_quarter<PS>(a[PE].y));
+  const double2 piv = make_double2(readlane_f64(colp.x, P), readlane_f64(colp.y, P));
+  const double m2 = fma(piv.x, piv.x, piv.y * piv.y);
+  const double s = rcp_nr(m2);
+  const double2 inv = make_double2(piv.x * s, -piv.y * s);
+  pprod *= m2;
+  // one update formula for every row: a <- a - f rowp with f = colp/piv, and
+  // f = 1 - 1/piv on the pivot row (a_p - (1 - 1/piv) a_p = a_p / piv)
+  const bool prow = (r == P);
+  const double2 fi = cmul(colp, inv);
+  const double2 f = prow ? make_double2(1.0 - inv.x, -inv.y) : fi;
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) {
+    const double2 x = rowp[jj];
+    double2 v;
+    v.x = fma(-f.x, x.x, fma(f.y, x.y, a[jj].x));
+    v.y = fma(-f.x, x.y, fma(-f.y, x.x, a[jj].y));
+    a[jj] = v;
+  }
+  // column p: 1/piv on the pivot row, -colp/piv elsewhere
+  if (q == PS) a[PE] = prow ? inv : make_double2(-fi.x, -fi.y);
+}
+
+template <int... Ps>
+__device__ __forceinline__ void inv16_all(double2 (&a)[4], double& pprod,
+                                          std::integer_sequence<int, Ps...>) {
+  (inv16_step<Ps>(a, pprod), ...);
+}
+
+// returns Π |pivot|^2 of the 16 pivots
+__device__ __forceinline__ double wave_inv16_dpp(double2 (&a)[4]) {
+  double pprod = 1.0;
+  inv16_all(a, pprod, std::make_integer_sequence<int, 16>{});
+  return pprod;
 }
 
 }  // namespace dwh

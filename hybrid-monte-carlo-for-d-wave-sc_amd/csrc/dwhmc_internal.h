@@ -27,18 +27,31 @@ struct CrDims {
   int Lx, Ly, N, BP, P, nbatch, nblk;
   int64_t item;   // elements per batch item pool (nblk * BP * BP)
 };
-// out = [cin] + sg * sum_{h<nt} A_h B_h over pool block indices (cin = -1: zero)
+// out = [cin] + sg * sum_{h<nt} A_h B_h over pool block indices (cin = -1: zero),
+// computed only on the output rows [r0, r1) x columns [c0, c1) (rounded out to
+// whole wave tiles; the rest of `out` is left untouched)
 struct CrTask {
   int out, cin, nt, pad;
   int a[4], b[4];
+  int r0, r1, c0, c1;
 };
+// wave tiles of a task at tile size ts
+inline int cr_task_tiles(const CrTask& t, int ts) {
+  return ((t.r1 + ts - 1) / ts - t.r0 / ts) * ((t.c1 + ts - 1) / ts - t.c0 / ts);
+}
 bool cr_supported_bp(int BP);
-void launch_cr_fill(const CrDims& c, double2* pool, const int* hcol, const double* hval,
-                    const int* Dcol, const double2* Dv, const double* ypole, hipStream_t s);
+// level-0 blocks of `list` (ids t*Ly + y, t = 0 D / 1 U / 2 L), fully rewritten
+void launch_cr_fill(const CrDims& c, double2* pool, const int* list, int nlist, const int* hcol,
+                    const double* hval, const int* Dcol, const double2* Dv, const double* ypole,
+                    hipStream_t s);
+// pairing entries of the level-0 blocks not in the per-step fill list
+void launch_cr_pair_scatter(const CrDims& c, double2* pool, const int64_t* off_ph,
+                            const int64_t* off_hp, const double2* Dv, hipStream_t s);
 void launch_cr_inv(const CrDims& c, double2* pool, const int* blk, const int* slot, int n,
                    double* ldpart, hipStream_t s);
-void launch_cr_gemm(const CrDims& c, double2* pool, const CrTask* tasks, int ntasks, double sg,
-                    hipStream_t s);
+// maxt32 / maxt16: the largest cr_task_tiles over the stage's tasks at ts = 32 / 16
+void launch_cr_gemm(const CrDims& c, double2* pool, const CrTask* tasks, int ntasks, int maxt32,
+                    int maxt16, double sg, hipStream_t s);
 void launch_cr_gather(const CrDims& c, const double2* pool, const int64_t* goff,
                       const int64_t* doff, double2* G12nn, double2* diagS, hipStream_t s);
 
