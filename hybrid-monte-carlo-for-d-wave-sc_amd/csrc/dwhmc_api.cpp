@@ -59,12 +59,14 @@ struct CrPlan {
   std::vector<int> inv_blk, inv_slot;
   std::vector<int64_t> goff, doff;
   std::vector<int> fill_all, fill_step;      // level-0 blocks written at create / every step
-  std::vector<int64_t> off_ph, off_hp;       // pairing entries outside fill_step (-1: none)
+  std::vector<int64_t> off_ph;               // pairing entries outside fill_step (-1: none)
 };
 
 // Block cyclic reduction of the periodic block-tridiagonal H_BdG - i y (blocks
-// = lattice rows) into stages; restates tools/cr_model.py (checked there
-// against dense inverses for Ly = 1 .. 16, odd and even).  Pool blocks:
+// = lattice rows) into stages; restates tools/cr_model.py
+// cr_selected_inverse_top (checked there against dense inverses for Ly = 1 ..
+// 24, odd and even).  Blocks are top halves (HP x BP); V, W are Q-form, every
+// other block M-form (the form of each right operand goes into CrTask::bq).  Pool blocks:
 // level-0 D[y] = y, U[y] = Ly + y, L[y] = 2 Ly + y (filled by k_cr_fill).
 // Forward level (m blocks, eliminate odd e < m - m%2, keep even k):
 //   inv D_e;  V1 = -U_a D_e^-1, V2 = -L_e D_e^-1, W1 = -D_e^-1 L_a, W2 = -D_e^-1 U_e
@@ -75,8 +77,17 @@ struct CrPlan {
 //   G_ae = G_aa V1 + G_ac V2,  G_ce = G_ca V1 + G_cc V2,  G_ee = D_e^-1 + W1 G_ae + W2 G_ce.
 CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol) {
   CrPlan pl;
+  const int HP = BP / 2;
   int nblk = 3 * Ly;
-  auto nb = [&]() { return nblk++; };
+  std::vector<char> qform(3 * Ly, 0);   // per pool block: Q-form (products V, W)
+  auto nb = [&]() {
+    qform.push_back(0);
+    return nblk++;
+  };
+  auto nbq = [&]() {
+    qform.push_back(1);
+    return nblk++;
+  };
   struct Level {
     int m;
     std::vector<int> D, U, L, E, K;
@@ -94,7 +105,7 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol) {
   struct Term { int a, b; };
   std::vector<dwh::CrTask> cur_tasks;
   // output window of the next tasks (full block unless restricted)
-  int w_r0 = 0, w_r1 = BP, w_c0 = 0, w_c1 = BP;
+  int w_r0 = 0, w_r1 = HP, w_c0 = 0, w_c1 = BP;
   auto task = [&](int out, int cin, std::initializer_list<Term> terms) {
     dwh::CrTask t{};
     t.out = out;
@@ -104,9 +115,11 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol) {
     t.c0 = w_c0;
     t.c1 = w_c1;
     t.nt = 0;
+    t.bq = 0;
     for (const Term& x : terms) {
       t.a[t.nt] = x.a;
       t.b[t.nt] = x.b;
+      if (qform[x.b]) t.bq |= 1 << t.nt;
       t.nt++;
     }
     cur_tasks.push_back(t);
@@ -152,13 +165,13 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol) {
     add_inv(inv, slot);
     for (int e : cur.E) {
       const int a = e - 1;
-      cur.V1[e] = nb();
+      cur.V1[e] = nbq();
       task(cur.V1[e], -1, {{cur.U[a], cur.D[e]}});
-      cur.V2[e] = nb();
+      cur.V2[e] = nbq();
       task(cur.V2[e], -1, {{cur.L[e], cur.D[e]}});
-      cur.W1[e] = nb();
+      cur.W1[e] = nbq();
       task(cur.W1[e], -1, {{cur.D[e], cur.L[a]}});
-      cur.W2[e] = nb();
+      cur.W2[e] = nbq();
       task(cur.W2[e], -1, {{cur.D[e], cur.U[e]}});
     }
     flush(-1.0);
@@ -213,12 +226,12 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol) {
         gl[k] = GL[kk];
       }
     }
-    // Level 0 is the last backward level: only the entries the force and
-    // Tr rho_hh read are formed there -- the particle-hole quadrant of G_ea,
-    // G_ec (cross-row bonds) and the hole columns of G_ae, G_ce, G_ee (G_ee:
-    // in-row bonds and the hole diagonal; G_ae, G_ce: also its operands).
+    // Level 0 is the last backward level: G_ea, G_ec (cross-row bonds, not
+    // operands of anything after them) are formed only on their pairing
+    // columns HP .. HP+Lx-1 there; G_ae, G_ce (right operands of G_ee) and
+    // G_ee (in-row bonds, hole diagonal) need their whole top half.
     const bool sel = (li == 0);
-    const int P0 = 0, P1 = sel ? Lx : BP, H0 = sel ? Lx : 0, H1 = sel ? 2 * Lx : BP;
+    const int H0 = sel ? HP : 0, H1 = sel ? HP + Lx : BP;
     std::vector<int> Gae(m, -1), Gce(m, -1);
     for (int e : lv.E) {
       const int a = e - 1, c = (e + 1) % m;
@@ -227,10 +240,12 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol) {
       const int Gac = mn == 1 ? GD[0] : GU[ia];
       const int Gca = mn == 1 ? GD[0] : GL[ia];
       const int gea = nb(), gec = nb(), gae = nb(), gce = nb();
-      w_r0 = P0; w_r1 = P1; w_c0 = H0; w_c1 = H1;
+      w_c0 = H0;
+      w_c1 = H1;
       task(gea, -1, {{lv.W1[e], Gaa}, {lv.W2[e], Gca}});
       task(gec, -1, {{lv.W1[e], Gac}, {lv.W2[e], Gcc}});
-      w_r0 = 0; w_r1 = BP;
+      w_c0 = 0;
+      w_c1 = BP;
       task(gae, -1, {{Gaa, lv.V1[e]}, {Gac, lv.V2[e]}});
       task(gce, -1, {{Gca, lv.V1[e]}, {Gcc, lv.V2[e]}});
       gu[a] = gae;
@@ -246,15 +261,13 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol) {
       gd[e] = lv.D[e];
     }
     flush(1.0);
-    w_c0 = 0;
-    w_c1 = BP;
     GD = gd;
     GU = gu;
     GL = gl;
   }
   // gather offsets of the level-0 G blocks
   const int N = Lx * Ly;
-  const int64_t BB = (int64_t)BP * BP;
+  const int64_t BB = (int64_t)HP * BP;
   pl.goff.assign((size_t)N * kSlots, -1);
   pl.doff.assign(N, 0);
   for (int i = 0; i < N; ++i) {
@@ -267,9 +280,9 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol) {
       if (Ly == 1 || yj == y) blk = GD[y];
       else if (yj == (y + 1) % Ly) blk = GU[y];
       else blk = GL[(y - 1 + Ly) % Ly];
-      pl.goff[(size_t)i * kSlots + s] = blk * BB + (int64_t)x * BP + (Lx + xj);
+      pl.goff[(size_t)i * kSlots + s] = blk * BB + (int64_t)x * BP + (HP + xj);
     }
-    pl.doff[i] = GD[y] * BB + (int64_t)(Lx + x) * BP + (Lx + x);
+    pl.doff[i] = GD[y] * BB + (int64_t)x * BP + x;   // G22[x, x] = -conj(A[x, x])
   }
   // level-0 fill lists and pairing scatter offsets: CR overwrites only the
   // level-0 eliminated D blocks (in-place inversion, then G_ee)
@@ -283,7 +296,6 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol) {
     if (rewrite[b]) pl.fill_step.push_back(b);
   }
   pl.off_ph.assign((size_t)N * kSlots, -1);
-  pl.off_hp.assign((size_t)N * kSlots, -1);
   auto blk_of = [&](int yr, int yc) {
     if (yc == yr) return yr;                              // D[yr]
     if (Ly >= 2 && yc == (yr + 1) % Ly) return Ly + yr;   // U[yr]
@@ -296,8 +308,7 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol) {
       const int yi = i / Lx, xi = i % Lx, yj = j / Lx, xj = j % Lx;
       const int b = blk_of(yi, yj);
       if (rewrite[b]) continue;
-      pl.off_ph[(size_t)i * kSlots + s] = b * BB + (int64_t)xi * BP + (Lx + xj);
-      pl.off_hp[(size_t)i * kSlots + s] = b * BB + (int64_t)(Lx + xi) * BP + xj;
+      pl.off_ph[(size_t)i * kSlots + s] = b * BB + (int64_t)xi * BP + (HP + xj);
     }
   pl.nblk = nblk;
   return pl;
@@ -363,7 +374,7 @@ struct dwh_ctx {
   double2* bpool = nullptr;   // CR block pool (nbatch x nblk blocks)
   dwh::CrTask* d_tasks = nullptr;
   int *d_inv_blk = nullptr, *d_inv_slot = nullptr;
-  int64_t *d_goff = nullptr, *d_doff = nullptr, *d_off_ph = nullptr, *d_off_hp = nullptr;
+  int64_t *d_goff = nullptr, *d_doff = nullptr, *d_off_ph = nullptr;
   int *d_fill_all = nullptr, *d_fill_step = nullptr;
 
   // timing
@@ -527,11 +538,11 @@ void cr_enqueue(dwh_ctx* ctx) {
   const double bp3 = 8.0 * c.BP * (double)c.BP * c.BP * c.nbatch;
   {
     // bytes written: the 3 Ly level-0 blocks of every batch item
+    // rewritten level-0 blocks (top halves) + pairing scatter, Δ/2 read directly
     const CrPlan& pl = ctx->plan;
-    Scope s(ctx, T_ASSEMBLE, (double)pl.fill_step.size() * 16.0 * c.BP * (double)c.BP * c.nbatch);
+    Scope s(ctx, T_ASSEMBLE, (double)pl.fill_step.size() * 8.0 * c.BP * (double)c.BP * c.nbatch);
     dwh::launch_cr_fill(c, ctx->bpool, ctx->d_fill_step, (int)pl.fill_step.size(), ctx->hcol, ctx->hval,
-                        ctx->Dcol, ctx->Dv, ctx->d_y, ctx->stream);
-    dwh::launch_cr_pair_scatter(c, ctx->bpool, ctx->d_off_ph, ctx->d_off_hp, ctx->Dv, ctx->stream);
+                        ctx->Dcol, ctx->Dsrc, ctx->Delta, ctx->d_y, ctx->d_off_ph, ctx->stream);
   }
   for (const CrStage& st : ctx->plan.stages) {
     if (st.kind == 0) {
@@ -544,23 +555,24 @@ void cr_enqueue(dwh_ctx* ctx) {
                           ctx->stream);
     }
   }
-  {
-    Scope s(ctx, T_CONTRACT, 16.0 * (kSlots + 1) * (double)c.N * c.nbatch);
-    dwh::launch_cr_gather(c, ctx->bpool, ctx->d_goff, ctx->d_doff, ctx->G12nn, ctx->diagS, ctx->stream);
-  }
 }
 
-// assemble -> GJ -> contract -> P (and optional kick) -> E_f
-void factorize_enqueue(dwh_ctx* ctx, double kick) {
+dwh::KickDrift kickdrift(dwh_ctx* ctx, double kick, double drift) {
+  return dwh::KickDrift{kick, drift, ctx->delta_cap, ctx->flag};
+}
+
+// assemble -> factorisation -> P -> F (+ kick / next drift); E_f separately
+void factorize_enqueue(dwh_ctx* ctx, const dwh::KickDrift& kd) {
   const Dims& d = ctx->d;
   Scope step(ctx, T_STEP, (double)d.nbatch * 8.0 * (double)d.N * d.N * d.N);
-  dwh::launch_dvals(d, ctx->Dsrc, ctx->Delta, ctx->Dv, ctx->stream);
   if (ctx->algo == ALGO_CR) {
     cr_enqueue(ctx);
-    dwh::launch_pair_force(d, ctx->G12nn, ctx->bond_ij, ctx->bond_ji, ctx->d_c, ctx->Delta,
-                           ctx->Pair, ctx->F, ctx->Pi, kick, ctx->beta, ctx->J, ctx->stream);
+    dwh::launch_cr_pair_force(ctx->cr, ctx->bpool, ctx->d_goff, ctx->bond_ij, ctx->bond_ji, ctx->d_c,
+                              ctx->Delta, ctx->Pair, ctx->F, ctx->Pi, kd, ctx->beta, ctx->J,
+                              ctx->stream);
     return;
   }
+  dwh::launch_dvals(d, ctx->Dsrc, ctx->Delta, ctx->Dv, ctx->stream);
   {
     // algorithmic bytes: read R once, write S^T
     Scope s(ctx, T_ASSEMBLE, (double)d.nbatch * 32.0 * d.N * (double)d.N);
@@ -574,12 +586,16 @@ void factorize_enqueue(dwh_ctx* ctx, double kick) {
                          ctx->stream);
   }
   dwh::launch_pair_force(d, ctx->G12nn, ctx->bond_ij, ctx->bond_ji, ctx->d_c, ctx->Delta,
-                         ctx->Pair, ctx->F, ctx->Pi, kick, ctx->beta, ctx->J, ctx->stream);
+                         ctx->Pair, ctx->F, ctx->Pi, kd, ctx->beta, ctx->J, ctx->stream);
 }
 
 void fermion_energy_enqueue(dwh_ctx* ctx) {
-  dwh::launch_fermion_energy(ctx->d, ctx->ldstatic, ctx->ldpart, ctx->diagS, ctx->d_c, ctx->Cx,
-                             ctx->beta, ctx->Ef, ctx->Trhh, ctx->stream);
+  if (ctx->algo == ALGO_CR)
+    dwh::launch_cr_fermion_energy(ctx->cr, ctx->bpool, ctx->d_doff, ctx->ldpart, ctx->d_c, ctx->Cx,
+                                  ctx->beta, ctx->Ef, ctx->Trhh, ctx->stream);
+  else
+    dwh::launch_fermion_energy(ctx->d, ctx->ldstatic, ctx->ldpart, ctx->diagS, ctx->d_c, ctx->Cx,
+                               ctx->beta, ctx->Ef, ctx->Trhh, ctx->stream);
 }
 
 // One hmc_sweep! body reading draws from device pointers (src/HMC.jl:71-144).
@@ -592,18 +608,19 @@ void sweep_enqueue(dwh_ctx* ctx, const double2* noise, const double* uniform, ui
                            ctx->Hold, s);
   dwh::launch_backup(d, ctx->Delta, ctx->Pair, ctx->Ef, ctx->Trhh, ctx->DeltaB, ctx->PairB,  // :84-86
                      ctx->EfB, ctx->TrhhB, s);
-  dwh::launch_force_from_pair(d, ctx->Pair, ctx->Delta, ctx->F, ctx->Pi, 0.5 * dt, ctx->beta,  // :91-92
-                              ctx->J, s);
   const double coef_field = dt / (2.0 * mass);                                        // :95
+  // :91-92 half kick, fused with step 1's drift (:101)
+  dwh::launch_force_from_pair(d, ctx->Pair, ctx->Delta, ctx->F, ctx->Pi,
+                              kickdrift(ctx, 0.5 * dt, Nt > 0 ? coef_field : 0.0), ctx->beta, ctx->J, s);
   for (int64_t step = 1; step <= Nt; ++step) {                                        // :98
-    dwh::launch_drift(d, ctx->Delta, ctx->Pi, coef_field, ctx->delta_cap, ctx->flag, s);  // :101
     // :105-107 update_H_BdG! + diagonalize + compute_forces!, then the kick of
-    // :111-113 (dt) fused with the final half kick of :118 on the last step
-    factorize_enqueue(ctx, step < Nt ? dt : 0.5 * dt);
+    // :111-113 (dt) and the next step's drift (:101), or the final half kick
+    // of :118 on the last step
+    factorize_enqueue(ctx, step < Nt ? kickdrift(ctx, dt, coef_field) : kickdrift(ctx, 0.5 * dt, 0.0));
   }
   if (Nt <= 0)
-    dwh::launch_force_from_pair(d, ctx->Pair, ctx->Delta, ctx->F, ctx->Pi, 0.5 * dt, ctx->beta,
-                                ctx->J, s);
+    dwh::launch_force_from_pair(d, ctx->Pair, ctx->Delta, ctx->F, ctx->Pi, kickdrift(ctx, 0.5 * dt, 0.0),
+                                ctx->beta, ctx->J, s);
   else
     fermion_energy_enqueue(ctx);
   dwh::launch_total_energy(d, ctx->Delta, ctx->Pi, ctx->Ef, ctx->beta, ctx->J, mass,  // :122
@@ -786,7 +803,7 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
   // algorithm: explicit request, else DWHMC_ALGO = dense | cr | auto (default:
   // cr when the lattice-row block 2 Lx fits a supported padded size)
   {
-    const int BP = (int)((2 * Lx + 31) / 32 * 32);
+    const int BP = (int)(2 * ((Lx + 15) / 16 * 16));   // top halves HP x BP, HP = Lx rounded to 16
     std::string want = "auto";
     if (algo_req == DWH_ALGO_DENSE) want = "dense";
     else if (algo_req == DWH_ALGO_CR) want = "cr";
@@ -815,7 +832,7 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
       c.P = d.P;
       c.nbatch = d.nbatch;
       c.nblk = ctx->plan.nblk;
-      c.item = (int64_t)c.nblk * BP * BP;
+      c.item = (int64_t)c.nblk * (BP / 2) * BP;
       d.nld = (int)Ly;
     }
   }
@@ -858,13 +875,14 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     ALLOC(d_goff, pl.goff.size());
     ALLOC(d_doff, pl.doff.size());
     ALLOC(d_off_ph, pl.off_ph.size());
-    ALLOC(d_off_hp, pl.off_hp.size());
     ALLOC(d_fill_all, pl.fill_all.size());
     ALLOC(d_fill_step, pl.fill_step.size());
   }
-  ALLOC(Dv, (size_t)d.nc * N * kSlots);
-  ALLOC(G12nn, (size_t)d.nbatch * N * kSlots);
-  ALLOC(diagS, (size_t)d.nbatch * N);
+  if (ctx->algo == ALGO_DENSE) {
+    ALLOC(Dv, (size_t)d.nc * N * kSlots);
+    ALLOC(G12nn, (size_t)d.nbatch * N * kSlots);
+    ALLOC(diagS, (size_t)d.nbatch * N);
+  }
   ALLOC(ldpart, (size_t)d.nbatch * d.nld);
   ALLOC(ldstatic, (size_t)d.nbatch);
   ALLOC(d_y, (size_t)d.P);
@@ -917,7 +935,6 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     UP(d_goff, pl.goff.data(), pl.goff.size());
     UP(d_doff, pl.doff.data(), pl.doff.size());
     UP(d_off_ph, pl.off_ph.data(), pl.off_ph.size());
-    UP(d_off_hp, pl.off_hp.data(), pl.off_hp.size());
     UP(d_fill_all, pl.fill_all.data(), pl.fill_all.size());
     UP(d_fill_step, pl.fill_step.data(), pl.fill_step.size());
   }
@@ -930,7 +947,7 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
   (void)hipMemsetAsync(ctx->Ef, 0, d.nc * sizeof(double), s);
   (void)hipMemsetAsync(ctx->Trhh, 0, d.nc * sizeof(double), s);
   (void)hipMemsetAsync(ctx->flag, 0, sizeof(int), s);
-  (void)hipMemsetAsync(ctx->diagS, 0, (size_t)d.nbatch * N * sizeof(double2), s);
+  if (ctx->diagS) (void)hipMemsetAsync(ctx->diagS, 0, (size_t)d.nbatch * N * sizeof(double2), s);
   if (ctx->algo == ALGO_DENSE) {
     // static R = (h - i y)^-1 and ln|det(h - i y)| for every (chain, pole)
     dwh::launch_fill_hz(d, ctx->R, ctx->hcol, ctx->hval, ctx->d_y, s);
@@ -940,9 +957,8 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     // the CR path factorises the whole BdG matrix: no static part; every
     // level-0 block written once (pairing entries 0 until the first factorize)
     (void)hipMemsetAsync(ctx->ldstatic, 0, d.nbatch * sizeof(double), s);
-    (void)hipMemsetAsync(ctx->Dv, 0, (size_t)d.nc * N * kSlots * sizeof(double2), s);
     dwh::launch_cr_fill(ctx->cr, ctx->bpool, ctx->d_fill_all, (int)ctx->plan.fill_all.size(), ctx->hcol,
-                        ctx->hval, ctx->Dcol, ctx->Dv, ctx->d_y, s);
+                        ctx->hval, ctx->Dcol, ctx->Dsrc, ctx->Delta, ctx->d_y, nullptr, s);
   }
   if (hipStreamSynchronize(s) != hipSuccess || hipGetLastError() != hipSuccess) {
     ctx->err = "static R initialisation failed on the device";
@@ -1025,7 +1041,7 @@ int dwh_update_pairing(dwh_ctx* ctx, const dwh_c128* Delta) {
 int dwh_factorize(dwh_ctx* ctx) {
   if (!ctx) return DWH_ERR_ARG;
   HIPCHECK(ctx, hipSetDevice(ctx->device));
-  factorize_enqueue(ctx, 0.0);
+  factorize_enqueue(ctx, kickdrift(ctx, 0.0, 0.0));
   fermion_energy_enqueue(ctx);
   HIPCHECK(ctx, hipGetLastError());
   HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
@@ -1041,7 +1057,7 @@ int dwh_forces(dwh_ctx* ctx, const dwh_c128* Delta, dwh_c128* F_out) {
   if (Delta)
     HIPCHECK(ctx, hipMemcpyAsync(ctx->DeltaB, Delta, nb, hipMemcpyHostToDevice, ctx->stream));
   dwh::launch_force_from_pair(ctx->d, ctx->Pair, Delta ? ctx->DeltaB : ctx->Delta, ctx->F, ctx->Pi,
-                              0.0, ctx->beta, ctx->J, ctx->stream);
+                              kickdrift(ctx, 0.0, 0.0), ctx->beta, ctx->J, ctx->stream);
   HIPCHECK(ctx, hipMemcpyAsync(F_out, ctx->F, nb, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
   return DWH_OK;

@@ -13,6 +13,16 @@
 // (dwhmc_api.cpp, mirrored by tools/cr_model.py) turns the recursion into
 // stages: block inversions (k_cr_inv) and task lists of block products
 // (k_cr_gemm), all batched over (chain, pole).
+//
+// Particle-hole symmetry (S H* S^-1 = -H, S = [[0, I], [-I, 0]] per site)
+// makes every CR block X either M-form [[A, B], [conj B, -conj A]] (H - i y,
+// inverses, G) or Q-form [[A, B], [-conj B, conj A]] (products of two
+// M-forms), with particle x at column x and hole x at column HP + x.  Blocks
+// are stored as their top half T = [A | B] (HP x BP, BP = 2 HP): half the
+// memory, and a product computes only the top half of its output with the
+// bottom rows of the right operand synthesised from its top half:
+//   Y[HP + i, j] = sgn * conj(T_Y[i, (j + HP) mod BP]),  sgn = -s_Y (j < HP), +s_Y (j >= HP)
+// (s = -1 M-form, +1 Q-form; tools/cr_model.py top_product).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -42,37 +52,57 @@ __device__ unsigned long long g_cr_stamps[1024][16];
 
 // ---------------------------------------------------------------------------
 // Level-0 blocks D[y] (pool block y), U[y] = A[y, y+1] (Ly + y), L[y] =
-// A[y+1, y] (2 Ly + y) of A = H_BdG - i y_q for every (chain, pole); one wave
-// per block row, lanes over columns (coalesced row writes), over the blocks of
-// `list` (level-0 block ids).  Ly == 2: the single off-diagonal block lives in
-// U (L = 0); Ly == 1: everything in D.  Padding rows/columns (b <= r < BP) are
-// the identity in D, zero elsewhere.  All blocks are written once at context
-// creation; per factorisation only the blocks CR overwrites (the level-0
-// eliminated D blocks) are rewritten and k_cr_pair_scatter refreshes the
-// pairing entries of the others.
+// A[y+1, y] (2 Ly + y) of A = H_BdG - i y_q for every (chain, pole), top
+// halves (particle rows): A part h - i y (columns 0..Lx-1), B part the pairing
+// Δ/2 (columns HP..HP+Lx-1).  One wave per block row, lanes over columns
+// (coalesced row writes), over the blocks of `list` (level-0 block ids).
+// Ly == 2: the single off-diagonal block lives in U (L = 0); Ly == 1:
+// everything in D.  Padded sites (Lx <= x < HP) are 1 on the diagonal of D
+// (hole -1 implied by the M-form), zero elsewhere.  All blocks are written
+// once at context creation; per factorisation only the blocks CR overwrites
+// (the level-0 eliminated D blocks) are rewritten and k_cr_pair_scatter
+// refreshes the pairing entries of the others.
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ double2 half_delta(const double2* __restrict__ Delta, const int* __restrict__ Dsrc,
+                                              int N, int c, int i, int s) {
+  const int src = Dsrc[i * kSlots + s];
+  if (src < 0) return make_double2(0.0, 0.0);
+  const double2 d = Delta[(int64_t)c * 2 * N + src];
+  return make_double2(0.5 * d.x, 0.5 * d.y);
+}
+
 __global__ __launch_bounds__(256) void k_cr_fill(double2* __restrict__ pool, int64_t item, int Lx,
-                                                 int Ly, int BP, int P, int nrows,
+                                                 int Ly, int BP, int P, int nrows, int fill_blocks,
                                                  const int* __restrict__ list,
                                                  const int* __restrict__ hcol,
                                                  const double* __restrict__ hval,
                                                  const int* __restrict__ Dcol,
-                                                 const double2* __restrict__ Dv,
-                                                 const double* __restrict__ ypole) {
+                                                 const int* __restrict__ Dsrc,
+                                                 const double2* __restrict__ Delta,
+                                                 const double* __restrict__ ypole,
+                                                 const int64_t* __restrict__ off_ph) {
+  const int bi = blockIdx.y, c = bi / P, q = bi - c * P;
+  const int N = Lx * Ly, HP = BP / 2;
+  if ((int)blockIdx.x >= fill_blocks) {
+    // pairing scatter Δ/2 (particle row, hole column) into the level-0 blocks
+    // CR does not overwrite (hole-row entries implied by the M-form)
+    const int e = ((int)blockIdx.x - fill_blocks) * blockDim.x + threadIdx.x;
+    if (e >= N * kSlots) return;
+    const int64_t o = off_ph[e];
+    if (o >= 0) pool[(int64_t)bi * item + o] = half_delta(Delta, Dsrc, N, c, e / kSlots, e % kSlots);
+    return;
+  }
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= nrows) return;
-  const int bi = blockIdx.y, c = bi / P, q = bi - c * P;
-  const int N = Lx * Ly, b = 2 * Lx;
-  const int lb = list[row / BP], r = row - (row / BP) * BP;
+  const int lb = list[row / HP], r = row - (row / HP) * HP;
   const int t = lb / Ly, y = lb - t * Ly;     // t: 0 D, 1 U, 2 L
-  double2* out = pool + (int64_t)bi * item + ((int64_t)(t * Ly + y) * BP + r) * BP;
+  double2* out = pool + (int64_t)bi * item + ((int64_t)(t * Ly + y) * HP + r) * BP;
   const bool zero = (t == 1 && Ly < 2) || (t == 2 && Ly < 3);
   const int yr = (t == 2) ? (y + 1) % Ly : y;
   const int yc = (t == 1) ? (y + 1) % Ly : y;
-  const bool rpad = r >= b;
-  const int pr = r >= Lx ? 1 : 0;
-  const int i = yr * Lx + (r - pr * Lx);
+  const bool rpad = r >= Lx;
+  const int i = yr * Lx + r;
   int hc[kHSlots], dc[kSlots];
   double hv[kHSlots];
   double2 dv[kSlots];
@@ -84,52 +114,36 @@ __global__ __launch_bounds__(256) void k_cr_fill(double2* __restrict__ pool, int
 #pragma unroll
   for (int s = 0; s < kSlots; ++s) {
     dc[s] = (!rpad && !zero) ? Dcol[i * kSlots + s] : -1;
-    dv[s] = (!rpad && !zero) ? Dv[(int64_t)c * N * kSlots + (int64_t)s * N + i] : make_double2(0.0, 0.0);
+    dv[s] = (!rpad && !zero) ? half_delta(Delta, Dsrc, N, c, i, s) : make_double2(0.0, 0.0);
   }
   const double yq = ypole[q];
   for (int cc = lane; cc < BP; cc += 64) {
     double2 v = make_double2(0.0, 0.0);
-    if (rpad || cc >= b) {
+    const int pc = cc >= HP ? 1 : 0, xc = cc - pc * HP;
+    if (rpad || xc >= Lx) {
       if (t == 0 && cc == r) v.x = 1.0;
     } else if (!zero) {
-      const int pc = cc >= Lx ? 1 : 0;
-      const int j = yc * Lx + (cc - pc * Lx);
-      if (pc == pr) {
+      const int j = yc * Lx + xc;
+      if (pc == 0) {          // particle-particle: h - i y
 #pragma unroll
         for (int s = 0; s < kHSlots; ++s)
-          if (hc[s] == j) v.x = pr ? -hv[s] : hv[s];
+          if (hc[s] == j) v.x = hv[s];
         if (i == j) v.y = -yq;
-      } else {
+      } else {                // particle-hole: Δ/2
 #pragma unroll
         for (int s = 0; s < kSlots; ++s)
-          if (dc[s] == j) v = pr ? make_double2(dv[s].x, -dv[s].y) : dv[s];
+          if (dc[s] == j) v = dv[s];
       }
     }
     out[cc] = v;
   }
 }
 
-// Pairing entries Δ/2 (particle row, hole column) and conj (hole row, particle
-// column) into the level-0 blocks CR does not overwrite (offsets from the
-// planner; -1 = entry lies in a rewritten block or the slot is empty).
-__global__ void k_cr_pair_scatter(double2* __restrict__ pool, int64_t item, int N, int P,
-                                  const int64_t* __restrict__ off_ph,
-                                  const int64_t* __restrict__ off_hp,
-                                  const double2* __restrict__ Dv) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  const int bi = blockIdx.y, c = bi / P;
-  if (e >= N * kSlots) return;
-  const int i = e / kSlots, sl = e - i * kSlots;
-  const double2 v = Dv[(int64_t)c * N * kSlots + (int64_t)sl * N + i];
-  double2* base = pool + (int64_t)bi * item;
-  const int64_t o1 = off_ph[e], o2 = off_hp[e];
-  if (o1 >= 0) base[o1] = v;
-  if (o2 >= 0) base[o2] = make_double2(v.x, -v.y);
-}
-
 // ---------------------------------------------------------------------------
-// In-place no-pivot Gauss-Jordan inversion of BP x BP blocks (BP = 16 NT),
-// register resident: the 2x2 wave grid owns NT/2 x NT/2 MFMA tiles each (C
+// In-place no-pivot Gauss-Jordan inversion of M-form BP x BP blocks (BP = 16
+// NT) stored as top halves: the bottom rows are synthesised on load
+// (conj B | -conj A), only the top half of the (M-form) inverse is stored.
+// Register resident: the 2x2 wave grid owns NT/2 x NT/2 MFMA tiles each (C
 // layout).  Per 16-wide sub-step kb: the owners publish block row kb and
 // block column kb to LDS, every wave inverts the 16x16 pivot tile (wave
 // local), forms X_J = P^-1 A_kJ for its own columns, then updates its tiles:
@@ -150,10 +164,11 @@ __global__ __launch_bounds__(256) void k_cr_inv(double2* __restrict__ pool, int6
   __shared__ double2 Xw[4][16 * XS];
   const int bi = blockIdx.y, li = blockIdx.x;
   double ld = 0.0;   // Σ ln|pivots| (identical in every wave)
-  double2* M = pool + (int64_t)bi * item + (int64_t)blk[li] * BP * BP;
+  constexpr int HP = BP / 2;
+  double2* M = pool + (int64_t)bi * item + (int64_t)blk[li] * HP * BP;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const int lr = l & 15, lk = l >> 4;
-  const int I0 = (w >> 1) * TH, J0 = (w & 1) * TH;
+  const int I0 = (w >> 1) * TH, J0 = (w & 1) * TH;   // wave row 0: top half, 1: bottom half
   d4 ar[TH][TH], ai[TH][TH];
   CR_STAMP(0);
 #pragma unroll
@@ -162,7 +177,14 @@ __global__ __launch_bounds__(256) void k_cr_inv(double2* __restrict__ pool, int6
     for (int tj = 0; tj < TH; ++tj)
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
-        const double2 v = M[(int64_t)((I0 + ti) * 16 + lk + 4 * rr) * BP + (J0 + tj) * 16 + lr];
+        const int row = (I0 + ti) * 16 + lk + 4 * rr, col = (J0 + tj) * 16 + lr;
+        double2 v;
+        if (row < HP) {
+          v = M[(int64_t)row * BP + col];
+        } else {   // M-form bottom half: [conj B | -conj A]
+          const double2 u = M[(int64_t)(row - HP) * BP + (col < HP ? col + HP : col - HP)];
+          v = col < HP ? make_double2(u.x, -u.y) : make_double2(-u.x, u.y);
+        }
         ar[ti][tj][rr] = v.x;
         ai[ti][tj][rr] = v.y;
       }
@@ -246,21 +268,26 @@ __global__ __launch_bounds__(256) void k_cr_inv(double2* __restrict__ pool, int6
     if (kb == 0) CR_STAMP(5);
   }
   CR_STAMP(6);
+  if (I0 == 0) {   // top half of the inverse
 #pragma unroll
-  for (int ti = 0; ti < TH; ++ti)
+    for (int ti = 0; ti < TH; ++ti)
 #pragma unroll
-    for (int tj = 0; tj < TH; ++tj)
+      for (int tj = 0; tj < TH; ++tj)
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr)
-        M[(int64_t)((I0 + ti) * 16 + lk + 4 * rr) * BP + (J0 + tj) * 16 + lr] =
-            make_double2(ar[ti][tj][rr], ai[ti][tj][rr]);
+        for (int rr = 0; rr < 4; ++rr)
+          M[(int64_t)((I0 + ti) * 16 + lk + 4 * rr) * BP + (J0 + tj) * 16 + lr] =
+              make_double2(ar[ti][tj][rr], ai[ti][tj][rr]);
+  }
   if (tid == 0) ldpart[(int64_t)bi * nslots + slot[li]] = ld;
   CR_STAMP(7);
 }
 
 // ---------------------------------------------------------------------------
-// Batched block products: task t of batch item bi writes
-//   out = [cin] + sg Σ_{h < nt} A_h B_h      (BP x BP blocks of the item's pool)
+// Batched block products on top halves: task t of batch item bi writes
+//   out = [cin] + sg Σ_{h < nt} A_h B_h      (top halves, HP x BP)
+// K runs over all BP rows of B_h: rows 0..HP-1 are stored, rows HP..BP-1 are
+// synthesised as sgn * conj(B_top[k - HP, (j + HP) mod BP]) with sgn from the
+// term's form bit (CrTask::bq) and the column half of the output tile.
 // One wave per TS x TS output tile (TS = 32: 2x2 MFMA tiles, operand reuse;
 // TS = 16: one MFMA tile with two interleaved accumulator chains, 4x the
 // waves for the small stages of the coarse levels, which are latency bound).
@@ -271,16 +298,17 @@ __global__ __launch_bounds__(256) void k_cr_inv(double2* __restrict__ pool, int6
 template <int BP>
 __device__ __forceinline__ void cr_tile32(double2* base, const CrTask* tk, int cin, int nt, int tr,
                                           int tc, double sg) {
-  constexpr int KS = BP / 4;
-  constexpr int64_t BB = (int64_t)BP * BP;
+  constexpr int HP = BP / 2, KS = BP / 4, KH = HP / 4;
+  constexpr int64_t BB = (int64_t)HP * BP;
   const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  const int c0 = tc * 32, crot = c0 < HP ? c0 + HP : c0 - HP;
   d4 acr[2][2], aci[2][2];
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
     for (int ni = 0; ni < 2; ++ni) {
       if (cin >= 0) {
-        const double2* C = base + cin * BB + (int64_t)(tr * 32 + mi * 16 + lk) * BP + tc * 32 + ni * 16 + lr;
+        const double2* C = base + cin * BB + (int64_t)(tr * 32 + mi * 16 + lk) * BP + c0 + ni * 16 + lr;
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
           const double2 v = C[(int64_t)4 * rr * BP];
@@ -295,13 +323,23 @@ __device__ __forceinline__ void cr_tile32(double2* base, const CrTask* tk, int c
 #pragma unroll 1
   for (int h = 0; h < nt; ++h) {
     const double2* A = base + tk->a[h] * BB + (int64_t)(tr * 32 + lr) * BP + lk;
-    const double2* B = base + tk->b[h] * BB + (int64_t)lk * BP + tc * 32 + lr;
+    const double2* Bt = base + tk->b[h] * BB + (int64_t)lk * BP + lr;
+    // synthesised rows: sgn * conj(.), sgn = -s (left column half) / +s (right), s = +1 Q, -1 M
+    const double sb = ((tk->bq >> h) & 1) ? 1.0 : -1.0;
+    const double sgn = c0 < HP ? -sb : sb;
     double2 fa[2][2], fb[2][2];
     auto load = [&](int s, double2 (&a)[2], double2 (&bb)[2]) {
       a[0] = A[s * 4];
       a[1] = A[(int64_t)16 * BP + s * 4];
-      bb[0] = B[(int64_t)s * 4 * BP];
-      bb[1] = B[(int64_t)s * 4 * BP + 16];
+      if (s < KH) {
+        bb[0] = Bt[(int64_t)s * 4 * BP + c0];
+        bb[1] = Bt[(int64_t)s * 4 * BP + c0 + 16];
+      } else {
+        const double2 u0 = Bt[(int64_t)(s - KH) * 4 * BP + crot];
+        const double2 u1 = Bt[(int64_t)(s - KH) * 4 * BP + crot + 16];
+        bb[0] = make_double2(sgn * u0.x, -sgn * u0.y);
+        bb[1] = make_double2(sgn * u1.x, -sgn * u1.y);
+      }
     };
     load(0, fa[0], fb[0]);
     load(1, fa[1], fb[1]);
@@ -328,7 +366,7 @@ __device__ __forceinline__ void cr_tile32(double2* base, const CrTask* tk, int c
         }
     }
   }
-  double2* O = base + tk->out * BB + (int64_t)(tr * 32 + lk) * BP + tc * 32 + lr;
+  double2* O = base + tk->out * BB + (int64_t)(tr * 32 + lk) * BP + c0 + lr;
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
@@ -341,14 +379,15 @@ __device__ __forceinline__ void cr_tile32(double2* base, const CrTask* tk, int c
 template <int BP>
 __device__ __forceinline__ void cr_tile16(double2* base, const CrTask* tk, int cin, int nt, int tr,
                                           int tc, double sg) {
-  constexpr int KS = BP / 4, PF = 4;
-  constexpr int64_t BB = (int64_t)BP * BP;
+  constexpr int HP = BP / 2, KS = BP / 4, KH = HP / 4, PF = 4;
+  constexpr int64_t BB = (int64_t)HP * BP;
   const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  const int c0 = tc * 16, crot = c0 < HP ? c0 + HP : c0 - HP;
   d4 acr[2], aci[2];
   acr[1] = d4{0.0, 0.0, 0.0, 0.0};
   aci[1] = d4{0.0, 0.0, 0.0, 0.0};
   if (cin >= 0) {
-    const double2* C = base + cin * BB + (int64_t)(tr * 16 + lk) * BP + tc * 16 + lr;
+    const double2* C = base + cin * BB + (int64_t)(tr * 16 + lk) * BP + c0 + lr;
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
       const double2 v = C[(int64_t)4 * rr * BP];
@@ -362,12 +401,19 @@ __device__ __forceinline__ void cr_tile16(double2* base, const CrTask* tk, int c
 #pragma unroll 1
   for (int h = 0; h < nt; ++h) {
     const double2* A = base + tk->a[h] * BB + (int64_t)(tr * 16 + lr) * BP + lk;
-    const double2* B = base + tk->b[h] * BB + (int64_t)lk * BP + tc * 16 + lr;
+    const double2* Bt = base + tk->b[h] * BB + (int64_t)lk * BP + lr;
+    const double sb = ((tk->bq >> h) & 1) ? 1.0 : -1.0;
+    const double sgn = c0 < HP ? -sb : sb;
+    auto bload = [&](int s) {
+      if (s < KH) return Bt[(int64_t)s * 4 * BP + c0];
+      const double2 u = Bt[(int64_t)(s - KH) * 4 * BP + crot];
+      return make_double2(sgn * u.x, -sgn * u.y);
+    };
     double2 fa[PF], fb[PF];
 #pragma unroll
     for (int s = 0; s < PF; ++s) {
       fa[s] = A[s * 4];
-      fb[s] = B[(int64_t)s * 4 * BP];
+      fb[s] = bload(s);
     }
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
@@ -375,7 +421,7 @@ __device__ __forceinline__ void cr_tile16(double2* base, const CrTask* tk, int c
       const double2 av = make_double2(sg * fa[cs].x, sg * fa[cs].y), bv = fb[cs];
       if (s + PF < KS) {
         fa[cs] = A[(s + PF) * 4];
-        fb[cs] = B[(int64_t)(s + PF) * 4 * BP];
+        fb[cs] = bload(s + PF);
       }
       acr[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.x, acr[p], 0, 0, 0);
       aci[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.y, aci[p], 0, 0, 0);
@@ -383,7 +429,7 @@ __device__ __forceinline__ void cr_tile16(double2* base, const CrTask* tk, int c
       aci[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, bv.x, aci[p], 0, 0, 0);
     }
   }
-  double2* O = base + tk->out * BB + (int64_t)(tr * 16 + lk) * BP + tc * 16 + lr;
+  double2* O = base + tk->out * BB + (int64_t)(tr * 16 + lk) * BP + c0 + lr;
 #pragma unroll
   for (int rr = 0; rr < 4; ++rr)
     O[(int64_t)4 * rr * BP] = make_double2(acr[0][rr] + acr[1][rr], aci[0][rr] + aci[1][rr]);
@@ -411,22 +457,73 @@ __global__ __launch_bounds__(256) void k_cr_gemm(double2* __restrict__ pool, int
 }
 
 // ---------------------------------------------------------------------------
-// G12 at the pairing pattern and diag(G22) from the level-0 blocks of G
-// (element offsets precomputed by the planner; -1 = empty slot).
+// Force from the level-0 G blocks: P_ij = Σ_q c_q (G12[i,j] + G12[j,i]) with
+// G12 read straight from the B parts of the pool (offsets goff per pairing
+// slot), F = -β/2J (Δ - J P) (src/Observables.jl:14-62), then the leapfrog
+// kick and the next step's drift (kick_drift).
 // ---------------------------------------------------------------------------
-__global__ void k_cr_gather(const double2* __restrict__ pool, int64_t item, int N,
-                            const int64_t* __restrict__ goff, const int64_t* __restrict__ doff,
-                            double2* __restrict__ G12nn, double2* __restrict__ diagS) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  const int bi = blockIdx.y;
-  if (i >= N) return;
-  const double2* base = pool + (int64_t)bi * item;
-#pragma unroll
-  for (int s = 0; s < kSlots; ++s) {
-    const int64_t o = goff[i * kSlots + s];
-    G12nn[((int64_t)bi * N + i) * kSlots + s] = o >= 0 ? base[o] : make_double2(0.0, 0.0);
+__global__ void k_cr_pair_force(const double2* __restrict__ pool, int64_t item,
+                                const int64_t* __restrict__ goff, const int* __restrict__ bond_ij,
+                                const int* __restrict__ bond_ji, const double* __restrict__ cpole,
+                                int N, int P, double2* __restrict__ Delta,
+                                double2* __restrict__ Pair, double2* __restrict__ F,
+                                double2* __restrict__ Pi, double kick, double drift, double cap2,
+                                int* __restrict__ flag, double beta, double J) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = blockIdx.y;
+  if (b >= 2 * N) return;
+  const int64_t o1 = goff[bond_ij[b]], o2 = goff[bond_ji[b]];
+  double2 Pv = make_double2(0.0, 0.0);
+  for (int q = 0; q < P; ++q) {
+    const double2* G = pool + (int64_t)(c * P + q) * item;
+    const double2 g1 = G[o1], g2 = G[o2];
+    const double cq = cpole[q];
+    Pv.x += cq * (g1.x + g2.x);
+    Pv.y += cq * (g1.y + g2.y);
   }
-  diagS[(int64_t)bi * N + i] = base[doff[i]];
+  const int64_t o = (int64_t)c * 2 * N + b;
+  Pair[o] = Pv;
+  const double2 d = Delta[o];
+  const double f = -beta / (2.0 * J);
+  const double2 Fv = make_double2(f * (d.x - J * Pv.x), f * (d.y - J * Pv.y));
+  F[o] = Fv;
+  kick_drift(Fv, o, Delta, Pi, kick, drift, cap2, flag);
+}
+
+// E_f = -2N C - β Σ_q c_q ln|det(H - i y_q)| (block pivots) and
+// Tr ρ_hh = N/2 - Σ_q c_q Re Tr G22 (G22[x,x] = -conj(A[x,x]) of the M-form
+// diagonal G blocks); one block per chain (src/HMC.jl:21-27, Observables.jl:120-145)
+__global__ __launch_bounds__(256) void k_cr_fermion_energy(const double2* __restrict__ pool,
+                                                           int64_t item,
+                                                           const int64_t* __restrict__ doff,
+                                                           const double* __restrict__ ldpart,
+                                                           const double* __restrict__ cpole, int N,
+                                                           int nld, int P, double Cx, double beta,
+                                                           double* __restrict__ Ef,
+                                                           double* __restrict__ Trhh) {
+  const int c = blockIdx.x;
+  __shared__ double red[2][4];
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  double ef = 0.0, tr = 0.0;
+  for (int q = 0; q < P; ++q) {
+    const int bi = c * P + q;
+    double ld = 0.0, t = 0.0;
+    for (int k = threadIdx.x; k < nld; k += blockDim.x) ld += ldpart[(int64_t)bi * nld + k];
+    for (int i = threadIdx.x; i < N; i += blockDim.x) t -= pool[(int64_t)bi * item + doff[i]].x;
+    ef += cpole[q] * ld;
+    tr += cpole[q] * t;
+  }
+  ef = wave_sum(ef);
+  tr = wave_sum(tr);
+  if (l == 0) {
+    red[0][w] = ef;
+    red[1][w] = tr;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    Ef[c] = -2.0 * N * Cx - beta * (red[0][0] + red[0][1] + red[0][2] + red[0][3]);
+    Trhh[c] = 0.5 * N - (red[1][0] + red[1][1] + red[1][2] + red[1][3]);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -435,18 +532,15 @@ __global__ void k_cr_gather(const double2* __restrict__ pool, int64_t item, int 
 bool cr_supported_bp(int BP) { return BP == 32 || BP == 64 || BP == 96; }
 
 void launch_cr_fill(const CrDims& c, double2* pool, const int* list, int nlist, const int* hcol,
-                    const double* hval, const int* Dcol, const double2* Dv, const double* ypole,
-                    hipStream_t s) {
-  if (nlist <= 0) return;
-  const int nrows = nlist * c.BP;
-  hipLaunchKernelGGL(k_cr_fill, dim3((nrows + 3) / 4, c.nbatch), dim3(256), 0, s, pool, c.item, c.Lx,
-                     c.Ly, c.BP, c.P, nrows, list, hcol, hval, Dcol, Dv, ypole);
-}
-
-void launch_cr_pair_scatter(const CrDims& c, double2* pool, const int64_t* off_ph,
-                            const int64_t* off_hp, const double2* Dv, hipStream_t s) {
-  hipLaunchKernelGGL(k_cr_pair_scatter, dim3((c.N * kSlots + 255) / 256, c.nbatch), dim3(256), 0, s,
-                     pool, c.item, c.N, c.P, off_ph, off_hp, Dv);
+                    const double* hval, const int* Dcol, const int* Dsrc, const double2* Delta,
+                    const double* ypole, const int64_t* off_ph, hipStream_t s) {
+  const int nrows = nlist * c.BP / 2;
+  const int fill_blocks = (nrows + 3) / 4;
+  const int scatter_blocks = off_ph ? (c.N * kSlots + 255) / 256 : 0;
+  if (fill_blocks + scatter_blocks == 0) return;
+  hipLaunchKernelGGL(k_cr_fill, dim3(fill_blocks + scatter_blocks, c.nbatch), dim3(256), 0, s, pool,
+                     c.item, c.Lx, c.Ly, c.BP, c.P, nrows, fill_blocks, list, hcol, hval, Dcol, Dsrc,
+                     Delta, ypole, off_ph);
 }
 
 void launch_cr_inv(const CrDims& c, double2* pool, const int* blk, const int* slot, int n,
@@ -467,9 +561,10 @@ void launch_cr_gemm(const CrDims& c, double2* pool, const CrTask* tasks, int nta
   // run 16x16 wave tiles: 4x the waves, 4x shorter MFMA chains
   static const int small = [] {
     const char* e = std::getenv("DWHMC_CR_SMALL");
-    return e ? std::atoi(e) : 2048;
+    return e ? std::atoi(e) : 1024;
   }();
-  const bool use16 = (int64_t)c.nbatch * ntasks * maxt32 < small;
+  // 32-wide tiles must not straddle the A | B column halves
+  const bool use16 = (c.BP / 2) % 32 != 0 || (int64_t)c.nbatch * ntasks * maxt32 < small;
   const int maxt = use16 ? maxt16 : maxt32;
   const int total = c.nbatch * ntasks * maxt;
   const dim3 g((total + 3) / 4), b(256);
@@ -486,10 +581,22 @@ void launch_cr_gemm(const CrDims& c, double2* pool, const CrTask* tasks, int nta
 #undef CR_GEMM
 }
 
-void launch_cr_gather(const CrDims& c, const double2* pool, const int64_t* goff,
-                      const int64_t* doff, double2* G12nn, double2* diagS, hipStream_t s) {
-  hipLaunchKernelGGL(k_cr_gather, dim3((c.N + 255) / 256, c.nbatch), dim3(256), 0, s, pool, c.item,
-                     c.N, goff, doff, G12nn, diagS);
+void launch_cr_pair_force(const CrDims& c, const double2* pool, const int64_t* goff,
+                          const int* bond_ij, const int* bond_ji, const double* cpole,
+                          double2* Delta, double2* Pair, double2* F, double2* Pi,
+                          const KickDrift& kd, double beta, double J, hipStream_t s) {
+  const int nc = c.nbatch / c.P;
+  hipLaunchKernelGGL(k_cr_pair_force, dim3((2 * c.N + 255) / 256, nc), dim3(256), 0, s, pool, c.item,
+                     goff, bond_ij, bond_ji, cpole, c.N, c.P, Delta, Pair, F, Pi, kd.kick, kd.drift,
+                     kd.cap * kd.cap, kd.flag, beta, J);
+}
+
+void launch_cr_fermion_energy(const CrDims& c, const double2* pool, const int64_t* doff,
+                              const double* ldpart, const double* cpole, double Cx, double beta,
+                              double* Ef, double* Trhh, hipStream_t s) {
+  const int nc = c.nbatch / c.P;
+  hipLaunchKernelGGL(k_cr_fermion_energy, dim3(nc), dim3(256), 0, s, pool, c.item, doff, ldpart,
+                     cpole, c.N, c.Ly, c.P, Cx, beta, Ef, Trhh);
 }
 
 }  // namespace dwh

@@ -116,6 +116,25 @@ __device__ __forceinline__ void mma16_lds(d4& acr, d4& aci, const double2* A, in
   }
 }
 
+// kick π += kick·F, then (drift != 0) the next leapfrog step's drift
+// Δ += drift·π with the |Δ| guard (src/HMC.jl:101 fused with :111-113)
+__device__ __forceinline__ void kick_drift(double2 Fv, int64_t o, double2* __restrict__ Delta,
+                                           double2* __restrict__ Pi, double kick, double drift,
+                                           double cap2, int* __restrict__ flag) {
+  if (kick == 0.0 && drift == 0.0) return;
+  double2 p = Pi[o];
+  p.x += kick * Fv.x;
+  p.y += kick * Fv.y;
+  Pi[o] = p;
+  if (drift != 0.0) {
+    double2 d = Delta[o];
+    d.x += drift * p.x;
+    d.y += drift * p.y;
+    Delta[o] = d;
+    if (d.x * d.x + d.y * d.y > cap2) atomicOr(flag, 1);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Register-only 16x16 complex no-pivot Gauss-Jordan inversion in one wave.
 // Layout: lane l holds row r = l & 15, columns 4q .. 4q+3 with q = l >> 4.

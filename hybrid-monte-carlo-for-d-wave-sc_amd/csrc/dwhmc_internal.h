@@ -21,17 +21,27 @@ struct Dims {
   int nld;      // ln|det| partials per batch item (dense: nb pivot blocks; cr: Ly block inversions)
 };
 
+// after the force: π += kick·F, then (drift != 0) Δ += drift·π with the
+// |Δ| <= cap guard setting *flag (the next leapfrog step's drift, fused)
+struct KickDrift {
+  double kick, drift, cap;
+  int* flag;
+};
+
 // Block cyclic-reduction path (dwhmc_cr.hip): every batch item owns a pool of
-// nblk BP x BP blocks (level-0 D/U/L, Schur complements, products, G blocks).
+// nblk blocks (level-0 D/U/L, Schur complements, products, G blocks), each the
+// top half (HP x BP, BP = 2 HP, HP = Lx rounded up to 16) of a BP x BP block
+// of particle-hole form (see dwhmc_cr.hip).
 struct CrDims {
   int Lx, Ly, N, BP, P, nbatch, nblk;
-  int64_t item;   // elements per batch item pool (nblk * BP * BP)
+  int64_t item;   // elements per batch item pool (nblk * HP * BP)
 };
 // out = [cin] + sg * sum_{h<nt} A_h B_h over pool block indices (cin = -1: zero),
 // computed only on the output rows [r0, r1) x columns [c0, c1) (rounded out to
-// whole wave tiles; the rest of `out` is left untouched)
+// whole wave tiles; the rest of `out` is left untouched); bit h of bq: B_h is
+// Q-form (else M-form)
 struct CrTask {
-  int out, cin, nt, pad;
+  int out, cin, nt, bq;
   int a[4], b[4];
   int r0, r1, c0, c1;
 };
@@ -40,20 +50,26 @@ inline int cr_task_tiles(const CrTask& t, int ts) {
   return ((t.r1 + ts - 1) / ts - t.r0 / ts) * ((t.c1 + ts - 1) / ts - t.c0 / ts);
 }
 bool cr_supported_bp(int BP);
-// level-0 blocks of `list` (ids t*Ly + y, t = 0 D / 1 U / 2 L), fully rewritten
+// level-0 blocks of `list` (ids t*Ly + y, t = 0 D / 1 U / 2 L) fully
+// rewritten, plus (off_ph != nullptr) the pairing entries Δ[Dsrc]/2 of the
+// level-0 blocks outside the list, in one launch
 void launch_cr_fill(const CrDims& c, double2* pool, const int* list, int nlist, const int* hcol,
-                    const double* hval, const int* Dcol, const double2* Dv, const double* ypole,
-                    hipStream_t s);
-// pairing entries of the level-0 blocks not in the per-step fill list
-void launch_cr_pair_scatter(const CrDims& c, double2* pool, const int64_t* off_ph,
-                            const int64_t* off_hp, const double2* Dv, hipStream_t s);
+                    const double* hval, const int* Dcol, const int* Dsrc, const double2* Delta,
+                    const double* ypole, const int64_t* off_ph, hipStream_t s);
+// P from the level-0 G blocks (pool offsets goff, pole weights), F, kick / drift
+void launch_cr_pair_force(const CrDims& c, const double2* pool, const int64_t* goff,
+                          const int* bond_ij, const int* bond_ji, const double* cpole,
+                          double2* Delta, double2* Pair, double2* F, double2* Pi,
+                          const KickDrift& kd, double beta, double J, hipStream_t s);
+// E_f and Tr ρ_hh from the CR block pivots and the G22 diagonal (pool offsets doff)
+void launch_cr_fermion_energy(const CrDims& c, const double2* pool, const int64_t* doff,
+                              const double* ldpart, const double* cpole, double Cx, double beta,
+                              double* Ef, double* Trhh, hipStream_t s);
 void launch_cr_inv(const CrDims& c, double2* pool, const int* blk, const int* slot, int n,
                    double* ldpart, hipStream_t s);
 // maxt32 / maxt16: the largest cr_task_tiles over the stage's tasks at ts = 32 / 16
 void launch_cr_gemm(const CrDims& c, double2* pool, const CrTask* tasks, int ntasks, int maxt32,
                     int maxt16, double sg, hipStream_t s);
-void launch_cr_gather(const CrDims& c, const double2* pool, const int64_t* goff,
-                      const int64_t* doff, double2* G12nn, double2* diagS, hipStream_t s);
 
 // dense h - i y_q (padded with identity) for every (chain, pole): R init input
 void launch_fill_hz(const Dims& d, double2* M, const int* hcol, const double* hval,
@@ -83,18 +99,14 @@ void launch_assemble(const Dims& d, const double2* R, double2* S, const int* Dco
 // G12 at the pairing pattern: G12nn[bi][i][s] = -(R D S^{-1})[i, Dcol[i][s]]; diag of S^{-1}
 void launch_contract(const Dims& d, const double2* R, const double2* SinvT, const int* Dcol,
                      const double2* Dv, double2* G12nn, double2* diagS, hipStream_t s);
-// P = Σ_q c_q (G12[i,j] + G12[j,i]); F = -β/2J (Δ - J P); π += kick·F
+// P = Σ_q c_q (G12[i,j] + G12[j,i]); F = -β/2J (Δ - J P); kick / drift
 void launch_pair_force(const Dims& d, const double2* G12nn, const int* bond_ij,
-                       const int* bond_ji, const double* cpole, const double2* Delta,
-                       double2* Pair, double2* F, double2* Pi, double kick, double beta,
-                       double J, hipStream_t s);
-// F from cached P, π += kick·F
-void launch_force_from_pair(const Dims& d, const double2* Pair, const double2* Delta,
-                            double2* F, double2* Pi, double kick, double beta, double J,
-                            hipStream_t s);
-// Δ += coef·π with the |Δ| guard
-void launch_drift(const Dims& d, double2* Delta, const double2* Pi, double coef, double cap,
-                  int* flag, hipStream_t s);
+                       const int* bond_ji, const double* cpole, double2* Delta, double2* Pair,
+                       double2* F, double2* Pi, const KickDrift& kd, double beta, double J,
+                       hipStream_t s);
+// F from cached P; kick / drift
+void launch_force_from_pair(const Dims& d, const double2* Pair, double2* Delta, double2* F,
+                            double2* Pi, const KickDrift& kd, double beta, double J, hipStream_t s);
 // E_f and Tr ρ_hh from the pivots of the last factorisation
 void launch_fermion_energy(const Dims& d, const double* ldstatic, const double* ldpart,
                            const double2* diagS, const double* cpole, double Cx, double beta,

@@ -600,9 +600,10 @@ __global__ __launch_bounds__(NT) void k_contract(const double2* __restrict__ R,
 // ---------------------------------------------------------------------------
 __global__ void k_pair_force(const double2* __restrict__ G12nn, const int* __restrict__ bond_ij,
                              const int* __restrict__ bond_ji, const double* __restrict__ cpole,
-                             int N, int P, const double2* __restrict__ Delta,
+                             int N, int P, double2* __restrict__ Delta,
                              double2* __restrict__ Pair, double2* __restrict__ F,
-                             double2* __restrict__ Pi, double kick, double beta, double J) {
+                             double2* __restrict__ Pi, double kick, double drift, double cap2,
+                             int* __restrict__ flag, double beta, double J) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   const int c = blockIdx.y;
   if (b >= 2 * N) return;
@@ -621,17 +622,13 @@ __global__ void k_pair_force(const double2* __restrict__ G12nn, const int* __res
   const double f = -beta / (2.0 * J);
   const double2 Fv = make_double2(f * (d.x - J * Pv.x), f * (d.y - J * Pv.y));
   F[o] = Fv;
-  if (kick != 0.0) {
-    double2 p = Pi[o];
-    p.x += kick * Fv.x;
-    p.y += kick * Fv.y;
-    Pi[o] = p;
-  }
+  kick_drift(Fv, o, Delta, Pi, kick, drift, cap2, flag);
 }
 
-__global__ void k_force_from_pair(const double2* __restrict__ Pair, const double2* __restrict__ Delta,
+__global__ void k_force_from_pair(const double2* __restrict__ Pair, double2* __restrict__ Delta,
                                   double2* __restrict__ F, double2* __restrict__ Pi, int N,
-                                  double kick, double beta, double J) {
+                                  double kick, double drift, double cap2, int* __restrict__ flag,
+                                  double beta, double J) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   const int c = blockIdx.y;
   if (b >= 2 * N) return;
@@ -640,26 +637,7 @@ __global__ void k_force_from_pair(const double2* __restrict__ Pair, const double
   const double f = -beta / (2.0 * J);
   const double2 Fv = make_double2(f * (d.x - J * Pv.x), f * (d.y - J * Pv.y));
   F[o] = Fv;
-  if (kick != 0.0) {
-    double2 p = Pi[o];
-    p.x += kick * Fv.x;
-    p.y += kick * Fv.y;
-    Pi[o] = p;
-  }
-}
-
-__global__ void k_drift(double2* __restrict__ Delta, const double2* __restrict__ Pi, int N,
-                        double coef, double cap2, int* __restrict__ flag) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  const int c = blockIdx.y;
-  if (b >= 2 * N) return;
-  const int64_t o = (int64_t)c * 2 * N + b;
-  double2 d = Delta[o];
-  const double2 p = Pi[o];
-  d.x += coef * p.x;
-  d.y += coef * p.y;
-  Delta[o] = d;
-  if (d.x * d.x + d.y * d.y > cap2) atomicOr(flag, 1);
+  kick_drift(Fv, o, Delta, Pi, kick, drift, cap2, flag);
 }
 
 __global__ __launch_bounds__(256) void k_fermion_energy(const double* __restrict__ ldstatic,
@@ -849,22 +827,17 @@ void launch_contract(const Dims& d, const double2* R, const double2* SinvT, cons
                      diagS);
 }
 void launch_pair_force(const Dims& d, const double2* G12nn, const int* bond_ij,
-                       const int* bond_ji, const double* cpole, const double2* Delta,
-                       double2* Pair, double2* F, double2* Pi, double kick, double beta,
-                       double J, hipStream_t s) {
+                       const int* bond_ji, const double* cpole, double2* Delta, double2* Pair,
+                       double2* F, double2* Pi, const KickDrift& kd, double beta, double J,
+                       hipStream_t s) {
   hipLaunchKernelGGL(k_pair_force, bonds_grid(d), dim3(256), 0, s, G12nn, bond_ij, bond_ji, cpole,
-                     d.N, d.P, Delta, Pair, F, Pi, kick, beta, J);
+                     d.N, d.P, Delta, Pair, F, Pi, kd.kick, kd.drift, kd.cap * kd.cap, kd.flag, beta,
+                     J);
 }
-void launch_force_from_pair(const Dims& d, const double2* Pair, const double2* Delta,
-                            double2* F, double2* Pi, double kick, double beta, double J,
-                            hipStream_t s) {
+void launch_force_from_pair(const Dims& d, const double2* Pair, double2* Delta, double2* F,
+                            double2* Pi, const KickDrift& kd, double beta, double J, hipStream_t s) {
   hipLaunchKernelGGL(k_force_from_pair, bonds_grid(d), dim3(256), 0, s, Pair, Delta, F, Pi, d.N,
-                     kick, beta, J);
-}
-void launch_drift(const Dims& d, double2* Delta, const double2* Pi, double coef, double cap,
-                  int* flag, hipStream_t s) {
-  hipLaunchKernelGGL(k_drift, bonds_grid(d), dim3(256), 0, s, Delta, Pi, d.N, coef, cap * cap,
-                     flag);
+                     kd.kick, kd.drift, kd.cap * kd.cap, kd.flag, beta, J);
 }
 void launch_fermion_energy(const Dims& d, const double* ldstatic, const double* ldpart,
                            const double2* diagS, const double* cpole, double Cx, double beta,

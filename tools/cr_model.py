@@ -143,3 +143,163 @@ if __name__ == "__main__":
     for Lx, Ly in [(4, 1), (4, 2), (3, 3), (4, 4), (6, 5), (4, 6), (2, 7), (5, 8), (3, 12), (4, 16), (2, 2), (8, 3)]:
         dl, e = check(Lx, Ly)
         print(f"Lx={Lx} Ly={Ly}: |d logdet|={dl:.2e} max|dG|={e:.2e}")
+
+
+# ---------------------------------------------------------------------------
+# Top-half ("quaternion") representation used by the device path.
+#
+# Particle-hole symmetry S H* S^-1 = -H (S = [[0, I], [-I, 0]] per site, SURVEY
+# I1) makes every block X of the CR (rows/cols = [particles | holes] of one
+# lattice row) one of two forms:
+#   M-form (s = -1): X = [[A, B], [ conj(B), -conj(A)]]   (H - i y, inverses, G)
+#   Q-form (s = +1): X = [[A, B], [-conj(B),  conj(A)]]   (products of two M-forms)
+# so only the top half T = [A | B] (n x 2n) is stored.  A product C = X Y has
+# form s_X * s_Y and top half  T_C = T_X Y_full  with the bottom rows of Y
+# synthesised from T_Y:  Y[n + i, j] = sgn_j * conj(T_Y[i, (j + n) mod 2n]),
+# sgn_j = -s_Y (j < n), +s_Y (j >= n).
+# ---------------------------------------------------------------------------
+def full_from_top(T, s):
+    n = T.shape[0]
+    A, B = T[:, :n], T[:, n:]
+    return np.block([[A, B], [-s * B.conj(), s * A.conj()]])
+
+
+def top_product(TX, TY, sY):
+    n = TX.shape[0]
+    Yb = np.empty_like(TY)
+    Yb[:, :n] = -sY * TY[:, n:].conj()
+    Yb[:, n:] = sY * TY[:, :n].conj()
+    return TX @ np.vstack([TY, Yb])
+
+
+def top_inverse_mform(T):
+    """Inverse of an M-form block from its top half by the 2x2 block formula:
+    Ainv = A^-1, F = A + B conj(Ainv B), P = F^-1, Q = P B conj(Ainv);
+    |det X| = |det A| |det F|.  Returns (top half [P | Q] (M-form), ln|det X|)."""
+    n = T.shape[0]
+    A, B = T[:, :n], T[:, n:]
+    Ainv = np.linalg.inv(A)
+    F = A + B @ (Ainv @ B).conj()
+    P = np.linalg.inv(F)
+    Q = P @ B @ Ainv.conj()
+    ld = np.linalg.slogdet(A)[1] + np.linalg.slogdet(F)[1]
+    return np.hstack([P, Q]), ld
+
+
+def check_top_half(n=5, seed=0, y=0.6):
+    rng = np.random.default_rng(seed)
+    def mform():
+        A = rng.standard_normal((n, n)) + 1j * rng.standard_normal((n, n))
+        A = 0.5 * (A + A.conj().T) - 1j * y * np.eye(n)          # h - i y, h Hermitian
+        B = rng.standard_normal((n, n)) + 1j * rng.standard_normal((n, n))
+        B = 0.5 * (B + B.T)                                      # pairing: symmetric
+        return np.hstack([A, B])
+    T1, T2 = mform(), mform()
+    X, Y = full_from_top(T1, -1), full_from_top(T2, -1)
+    err = 0.0
+    # the assembled H - i y is M-form
+    H = X
+    S = np.block([[np.zeros((n, n)), np.eye(n)], [-np.eye(n), np.zeros((n, n))]])
+    err = max(err, np.abs(S @ (H + 1j * y * np.eye(2 * n)).conj() @ np.linalg.inv(S) + (H + 1j * y * np.eye(2 * n))).max())
+    P = X @ Y                                                    # M M -> Q-form
+    err = max(err, np.abs(full_from_top(top_product(T1, T2, -1), +1) - P).max())
+    TP = top_product(T1, T2, -1)
+    R = P @ X                                                    # Q M -> M-form
+    err = max(err, np.abs(full_from_top(top_product(TP, T1, -1), -1) - R).max())
+    R2 = X @ P                                                   # M Q -> M-form
+    err = max(err, np.abs(full_from_top(top_product(T1, TP, +1), -1) - R2).max())
+    Ti, ld = top_inverse_mform(T1)
+    err = max(err, np.abs(full_from_top(Ti, -1) - np.linalg.inv(X)).max())
+    err = max(err, abs(ld - np.linalg.slogdet(X)[1]))
+    return err
+
+
+def cr_selected_inverse_top(Dg, U, L):
+    """cr_selected_inverse on top halves (n x 2n) with the form bookkeeping of
+    the device planner: D, U, L, inverses and G blocks are M-form; V, W are
+    Q-form.  Inputs/outputs are top halves of M-form blocks."""
+    M, Q = -1, +1
+    m = len(Dg)
+    mul = top_product
+    if m == 1:
+        Dfin = Dg[0] + U[0] + L[0]
+        G, ld = top_inverse_mform(Dfin)
+        return ld, [G], [G], [G]
+    E = list(range(1, m - (m % 2), 2))
+    K = [k for k in range(m) if k % 2 == 0]
+    ld = 0.0
+    Dinv, V1, V2, W1, W2 = {}, {}, {}, {}, {}
+    for e in E:
+        a = e - 1
+        Dinv[e], l_ = top_inverse_mform(Dg[e])
+        ld += l_
+        V1[e] = -mul(U[a], Dinv[e], M)
+        V2[e] = -mul(L[e], Dinv[e], M)
+        W1[e] = -mul(Dinv[e], L[a], M)
+        W2[e] = -mul(Dinv[e], U[e], M)
+    Dn, Un, Ln = [], [], []
+    for k in K:
+        if m == 2:
+            Dn.append(Dg[0] + mul(V1[1], L[0], M) + mul(V2[1], U[1], M) + mul(V1[1], U[1], M)
+                      + mul(V2[1], L[0], M))
+            Un.append(np.zeros_like(Dg[0]))
+            Ln.append(np.zeros_like(Dg[0]))
+            continue
+        d = Dg[k].copy()
+        if k + 1 in Dinv:
+            d += mul(V1[k + 1], L[k], M)
+        if (k - 1) % m in Dinv:
+            e = (k - 1) % m
+            d += mul(V2[e], U[e], M)
+        Dn.append(d)
+        if k + 1 in Dinv:
+            Un.append(mul(V1[k + 1], U[k + 1], M))
+            Ln.append(mul(V2[k + 1], L[k], M))
+        else:
+            Un.append(U[k])
+            Ln.append(L[k])
+    ld2, GDn, GUn, GLn = cr_selected_inverse_top(Dn, Un, Ln)
+    ld += ld2
+    mn = len(K)
+    GD, GU, GL = [None] * m, [None] * m, [None] * m
+    for kk, k in enumerate(K):
+        GD[k] = GDn[kk]
+        if k + 1 not in Dinv:
+            GU[k], GL[k] = GUn[kk], GLn[kk]
+    for e in E:
+        a, c = e - 1, (e + 1) % m
+        ia, ic = a // 2, (c // 2) % mn
+        Gaa, Gcc = GDn[ia], GDn[ic]
+        Gac, Gca = (GDn[0], GDn[0]) if mn == 1 else (GUn[ia], GLn[ia])
+        Gea = mul(W1[e], Gaa, M) + mul(W2[e], Gca, M)
+        Gec = mul(W1[e], Gac, M) + mul(W2[e], Gcc, M)
+        Gae = mul(Gaa, V1[e], Q) + mul(Gac, V2[e], Q)
+        Gce = mul(Gca, V1[e], Q) + mul(Gcc, V2[e], Q)
+        GD[e] = Dinv[e] + mul(W1[e], Gae, M) + mul(W2[e], Gce, M)
+        GU[a], GL[a], GU[e], GL[e] = Gae, Gea, Gec, Gce
+    return ld, GD, GU, GL
+
+
+def check_top_cr(Lx, Ly, seed=0, y=0.7):
+    """cr_selected_inverse_top against the full-block version on a BdG matrix."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
+    from oracle import dwhmc_oracle as O
+    p = O.ModelParameters(Lx, Ly, 1.0, -0.35, -1.08, 1.0, 0.1, 8.0, 0.8, 1.0)
+    rng = np.random.default_rng(seed)
+    st = O.initialize_state(p, rng)
+    Delta = st.Delta + 0.3 * (rng.standard_normal((p.N, 2)) + 1j * rng.standard_normal((p.N, 2)))
+    cache = O.initialize_cache(p)
+    O.init_static_H(cache, p, st.disorder_pot)
+    O.update_H_BdG(cache, p, Delta)
+    A = O.hermitian_from_upper(cache.H_base) - 1j * y * np.eye(2 * p.N)
+    Dg, U, L = blocks_from_dense(A, Lx, Ly)
+    ld, GD, GU, GL = cr_selected_inverse(Dg, U, L)
+    top = lambda X: [x[:Lx, :] for x in X]
+    ldt, GDt, GUt, GLt = cr_selected_inverse_top(top(Dg), top(U), top(L))
+    err = abs(ld - ldt)
+    for F, T in ((GD, GDt), (GU, GUt), (GL, GLt)):
+        for f, t in zip(F, T):
+            err = max(err, np.abs(f[:Lx, :] - t).max())
+    return err
