@@ -49,7 +49,8 @@ struct CrStage {
   int first, n;    // range in CrPlan::inv_blk / CrPlan::tasks
   double sg;       // products: sign of the sum
   double flops;    // products: algorithmic fp64 flops per batch item (restricted ranges)
-  int maxt32, maxt16;
+  int maxt32, maxt16, ntmax;
+  dwh::CrGemmCfg cfg;   // products: tile / K-split chosen once per context
 };
 
 struct CrPlan {
@@ -95,7 +96,7 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol) {
     std::vector<char> elim;
   };
   auto add_inv = [&](const std::vector<int>& blocks, int& slot) {
-    CrStage st{0, (int)pl.inv_blk.size(), (int)blocks.size(), 0.0, 0.0, 0, 0};
+    CrStage st{0, (int)pl.inv_blk.size(), (int)blocks.size(), 0.0, 0.0, 0, 0, 0, {16, 1}};
     for (int b : blocks) {
       pl.inv_blk.push_back(b);
       pl.inv_slot.push_back(slot++);
@@ -126,11 +127,12 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol) {
   };
   auto flush = [&](double sg) {
     if (cur_tasks.empty()) return;
-    CrStage st{1, (int)pl.tasks.size(), (int)cur_tasks.size(), sg, 0.0, 0, 0};
+    CrStage st{1, (int)pl.tasks.size(), (int)cur_tasks.size(), sg, 0.0, 0, 0, 0, {16, 1}};
     for (auto& t : cur_tasks) {
       st.flops += 8.0 * t.nt * BP * (double)(t.r1 - t.r0) * (t.c1 - t.c0);
       st.maxt32 = std::max(st.maxt32, dwh::cr_task_tiles(t, 32));
       st.maxt16 = std::max(st.maxt16, dwh::cr_task_tiles(t, 16));
+      st.ntmax = std::max(st.ntmax, t.nt);
       pl.tasks.push_back(t);
     }
     pl.stages.push_back(st);
@@ -551,8 +553,8 @@ void cr_enqueue(dwh_ctx* ctx) {
                          ctx->ldpart, ctx->stream);
     } else {
       Scope s(ctx, T_CR_GEMM, st.flops * c.nbatch);
-      dwh::launch_cr_gemm(c, ctx->bpool, ctx->d_tasks + st.first, st.n, st.maxt32, st.maxt16, st.sg,
-                          ctx->stream);
+      dwh::launch_cr_gemm(c, ctx->bpool, ctx->d_tasks + st.first, st.n, st.maxt32, st.maxt16, st.cfg,
+                          st.sg, ctx->stream);
     }
   }
 }
@@ -834,6 +836,19 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
       c.nblk = ctx->plan.nblk;
       c.item = (int64_t)c.nblk * (BP / 2) * BP;
       d.nld = (int)Ly;
+      for (CrStage& st : ctx->plan.stages)
+        if (st.kind == 1) st.cfg = dwh::cr_gemm_config(c, st.n, st.maxt32, st.maxt16, st.ntmax);
+      if (const char* e = std::getenv("DWHMC_CR_PLAN_DUMP"); e && *e == '1') {
+        int i = 0;
+        for (const CrStage& st : ctx->plan.stages) {
+          if (st.kind == 0)
+            std::fprintf(stderr, "cr stage %2d: inv   blocks=%d\n", i, st.n);
+          else
+            std::fprintf(stderr, "cr stage %2d: gemm  tasks=%d maxt32=%d maxt16=%d ntmax=%d flops/item=%.3g cfg=%d:%d\n",
+                         i, st.n, st.maxt32, st.maxt16, st.ntmax, st.flops, st.cfg.ts, st.cfg.ksplit);
+          ++i;
+        }
+      }
     }
   }
 

@@ -26,7 +26,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cmath>
 #include <cstdlib>
+#include <cstring>
 
 #include "dwhmc_device.h"
 #include "dwhmc_internal.h"
@@ -140,146 +142,164 @@ __global__ __launch_bounds__(256) void k_cr_fill(double2* __restrict__ pool, int
 }
 
 // ---------------------------------------------------------------------------
-// In-place no-pivot Gauss-Jordan inversion of M-form BP x BP blocks (BP = 16
-// NT) stored as top halves: the bottom rows are synthesised on load
+// In-place no-pivot block Gauss-Jordan inversion of M-form BP x BP blocks
+// (BP = 16 NT) stored as top halves: the bottom rows are synthesised on load
 // (conj B | -conj A), only the top half of the (M-form) inverse is stored.
-// Register resident: the 2x2 wave grid owns NT/2 x NT/2 MFMA tiles each (C
-// layout).  Per 16-wide sub-step kb: the owners publish block row kb and
-// block column kb to LDS, every wave inverts the 16x16 pivot tile (wave
-// local), forms X_J = P^-1 A_kJ for its own columns, then updates its tiles:
-//   A_IJ <- [J != kb] A_IJ - A_Ik X_J  (I != kb),   A_kJ <- X_J   (X_kb = P^-1).
+// NT waves; wave w keeps block column w (NT 16 x 16 MFMA tiles, C layout) in
+// registers.  Pivot step kb:
+//   wave kb   publishes its column (tile kb already holds P^-1 = A_kk^-1, the
+//             others the old A_Ik) to an LDS panel, then A_Ik <- -A_Ik P^-1;
+//   wave J    X_J = P^-1 A_kJ (its tile kb, used in place as the MFMA B
+//             operand: the C layout of row 4s + lk is the B layout of k-step s),
+//             A_kJ <- X_J, A_IJ <- A_IJ - A_Ik X_J;
+//   wave kb+1 (lookahead) updates tile kb+1 first and inverts it (the next
+//             pivot) before its other tiles, while the other waves update.
+// One barrier per pivot step (double-buffered panel).  16 x 16 pivot tiles are
+// inverted in registers (wave_inv16_dpp); complex MACs are 3 real MFMAs.
 // ln|det| (= Σ ln|pivots|) goes to ldpart[bi][slot].
 // ---------------------------------------------------------------------------
+// acc(16x16, C layout) += (NEG ? -1 : 1) * A(16 x 16, LDS row-major, stride 17) * B
+// with B given in the C layout (b_r, b_i: row 4 rr + lk, column lr).
+template <bool NEG>
+__device__ __forceinline__ void mma16_3m(d4& cr, d4& ci, const double2* A, const d4& br, const d4& bi) {
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  d4 t1 = cr, t2 = {0.0, 0.0, 0.0, 0.0}, t3 = cr + ci;
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const double2 av = A[lr * 17 + 4 * ks + lk];
+    const double a_r = NEG ? -av.x : av.x, a_i = NEG ? -av.y : av.y;
+    t1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a_r, br[ks], t1, 0, 0, 0);
+    t2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a_i, bi[ks], t2, 0, 0, 0);
+    t3 = __builtin_amdgcn_mfma_f64_16x16x4f64(a_r + a_i, br[ks] + bi[ks], t3, 0, 0, 0);
+  }
+  cr = t1 - t2;
+  ci = t3 - t1 - t2;
+}
+
 template <int NT>
-__global__ __launch_bounds__(256) void k_cr_inv(double2* __restrict__ pool, int64_t item,
-                                                const int* __restrict__ blk,
-                                                const int* __restrict__ slot,
-                                                double* __restrict__ ldpart, int nslots) {
-  constexpr int BP = 16 * NT, TH = NT / 2;
-  constexpr int RS = BP + 1;        // LDS row stride of the row panel
-  constexpr int XS = TH * 16 + 1;   // LDS row stride of a wave's X panel
-  __shared__ double2 Rp[16 * RS];
-  __shared__ double2 Cp[BP * 17];
-  __shared__ double2 Dw[4][16 * 17];
-  __shared__ double2 Xw[4][16 * XS];
+__global__ __launch_bounds__(64 * NT) void k_cr_inv(double2* __restrict__ pool, int64_t item,
+                                                    const int* __restrict__ blk,
+                                                    const int* __restrict__ slot,
+                                                    double* __restrict__ ldpart, int nslots) {
+  constexpr int BP = 16 * NT, HP = BP / 2, TSZ = 16 * 17;
+  __shared__ double2 pan[2][NT][TSZ];
+  __shared__ double2 scr[NT][TSZ];
+  __shared__ double ldw[NT];
   const int bi = blockIdx.y, li = blockIdx.x;
-  double ld = 0.0;   // Σ ln|pivots| (identical in every wave)
-  constexpr int HP = BP / 2;
   double2* M = pool + (int64_t)bi * item + (int64_t)blk[li] * HP * BP;
-  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
-  const int lr = l & 15, lk = l >> 4;
-  const int I0 = (w >> 1) * TH, J0 = (w & 1) * TH;   // wave row 0: top half, 1: bottom half
-  d4 ar[TH][TH], ai[TH][TH];
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  d4 ar[NT], ai[NT];
   CR_STAMP(0);
 #pragma unroll
-  for (int ti = 0; ti < TH; ++ti)
+  for (int I = 0; I < NT; ++I)
 #pragma unroll
-    for (int tj = 0; tj < TH; ++tj)
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int row = (I0 + ti) * 16 + lk + 4 * rr, col = (J0 + tj) * 16 + lr;
-        double2 v;
-        if (row < HP) {
-          v = M[(int64_t)row * BP + col];
-        } else {   // M-form bottom half: [conj B | -conj A]
-          const double2 u = M[(int64_t)(row - HP) * BP + (col < HP ? col + HP : col - HP)];
-          v = col < HP ? make_double2(u.x, -u.y) : make_double2(-u.x, u.y);
-        }
-        ar[ti][tj][rr] = v.x;
-        ai[ti][tj][rr] = v.y;
+    for (int rr = 0; rr < 4; ++rr) {
+      const int row = I * 16 + lk + 4 * rr, col = w * 16 + lr;
+      double2 v;
+      if (row < HP) {
+        v = M[(int64_t)row * BP + col];
+      } else {   // M-form bottom half: [conj B | -conj A]
+        const double2 u = M[(int64_t)(row - HP) * BP + (col < HP ? col + HP : col - HP)];
+        v = col < HP ? make_double2(u.x, -u.y) : make_double2(-u.x, u.y);
       }
+      ar[I][rr] = v.x;
+      ai[I][rr] = v.y;
+    }
   CR_STAMP(1);
-#pragma unroll 1
-  for (int kb = 0; kb < NT; ++kb) {
-    // (1) publish block row kb and block column kb
+  double ld = 0.0;
+  double2* S = scr[w];
+  // in-place inverse of a C-layout tile: transpose to the wave_inv16_dpp layout
+  // (lane: row l & 15, columns 4 (l >> 4) ..) through this wave's scratch
+  auto invert = [&](d4& tr, d4& ti) {
 #pragma unroll
-    for (int ti = 0; ti < TH; ++ti)
-      if (I0 + ti == kb) {
-#pragma unroll
-        for (int tj = 0; tj < TH; ++tj)
-#pragma unroll
-          for (int rr = 0; rr < 4; ++rr)
-            Rp[(lk + 4 * rr) * RS + (J0 + tj) * 16 + lr] = make_double2(ar[ti][tj][rr], ai[ti][tj][rr]);
-      }
-#pragma unroll
-    for (int tj = 0; tj < TH; ++tj)
-      if (J0 + tj == kb) {
-#pragma unroll
-        for (int ti = 0; ti < TH; ++ti)
-#pragma unroll
-          for (int rr = 0; rr < 4; ++rr)
-            Cp[((I0 + ti) * 16 + lk + 4 * rr) * 17 + lr] = make_double2(ar[ti][tj][rr], ai[ti][tj][rr]);
-      }
-    __syncthreads();
-    if (kb == 0) CR_STAMP(2);
-    // (2) every wave inverts the pivot tile in registers (lane: row l&15, cols 4(l>>4)..)
+    for (int rr = 0; rr < 4; ++rr) S[(lk + 4 * rr) * 17 + lr] = make_double2(tr[rr], ti[rr]);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     double2 dv[4];
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) dv[jj] = Rp[(l & 15) * RS + kb * 16 + (l >> 4) * 4 + jj];
+    for (int jj = 0; jj < 4; ++jj) dv[jj] = S[(l & 15) * 17 + (l >> 4) * 4 + jj];
     ld += 0.5 * log(wave_inv16_dpp(dv));
-    if (kb == 0) CR_STAMP(3);
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) Dw[w][(l & 15) * 17 + (l >> 4) * 4 + jj] = dv[jj];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // (3) X_J = P^-1 A_kJ for this wave's columns
 #pragma unroll
-    for (int tj = 0; tj < TH; ++tj) {
-      d4 xr = {0.0, 0.0, 0.0, 0.0}, xi = {0.0, 0.0, 0.0, 0.0};
-      if (J0 + tj == kb) {
+    for (int jj = 0; jj < 4; ++jj) S[(l & 15) * 17 + (l >> 4) * 4 + jj] = dv[jj];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          const double2 v = Dw[w][(lk + 4 * rr) * 17 + lr];
-          xr[rr] = v.x;
-          xi[rr] = v.y;
-        }
-      } else {
-        mma16_lds<false>(xr, xi, Dw[w], 17, Rp + (J0 + tj) * 16, RS);
-      }
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) Xw[w][(lk + 4 * rr) * XS + tj * 16 + lr] = make_double2(xr[rr], xi[rr]);
+    for (int rr = 0; rr < 4; ++rr) {
+      const double2 v = S[(lk + 4 * rr) * 17 + lr];
+      tr[rr] = v.x;
+      ti[rr] = v.y;
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (kb == 0) CR_STAMP(4);
-    // (4) tile updates
+  };
+  if (w == 0) invert(ar[0], ai[0]);
+  CR_STAMP(2);
+#pragma unroll 1
+  for (int kb = 0; kb < NT; ++kb) {
+    double2(*P)[TSZ] = pan[kb & 1];
+    if (w == kb) {
 #pragma unroll
-    for (int ti = 0; ti < TH; ++ti)
+      for (int I = 0; I < NT; ++I)
 #pragma unroll
-      for (int tj = 0; tj < TH; ++tj) {
-        if (I0 + ti == kb) {
+        for (int rr = 0; rr < 4; ++rr) P[I][(lk + 4 * rr) * 17 + lr] = make_double2(ar[I][rr], ai[I][rr]);
+    }
+    __syncthreads();
+    // this wave's tile kb (wave kb: P^-1; others: A_kJ)
+    d4 br = ar[0], bim = ai[0];
 #pragma unroll
-          for (int rr = 0; rr < 4; ++rr) {
-            const double2 v = Xw[w][(lk + 4 * rr) * XS + tj * 16 + lr];
-            ar[ti][tj][rr] = v.x;
-            ai[ti][tj][rr] = v.y;
-          }
-        } else {
-          if (J0 + tj == kb) {
-            ar[ti][tj] = d4{0.0, 0.0, 0.0, 0.0};
-            ai[ti][tj] = d4{0.0, 0.0, 0.0, 0.0};
-          }
-          mma16_lds<true>(ar[ti][tj], ai[ti][tj], Cp + (I0 + ti) * 16 * 17, 17, Xw[w] + tj * 16, XS);
+    for (int I = 1; I < NT; ++I)
+      if (I == kb) {
+        br = ar[I];
+        bim = ai[I];
+      }
+    if (w == kb) {
+#pragma unroll
+      for (int I = 0; I < NT; ++I)
+        if (I != kb) {
+          ar[I] = d4{0.0, 0.0, 0.0, 0.0};
+          ai[I] = d4{0.0, 0.0, 0.0, 0.0};
+          mma16_3m<true>(ar[I], ai[I], P[I], br, bim);
+        }
+    } else {
+      d4 xr = {0.0, 0.0, 0.0, 0.0}, xi = {0.0, 0.0, 0.0, 0.0};
+      mma16_3m<false>(xr, xi, P[kb], br, bim);
+      const bool look = (w == kb + 1);
+#pragma unroll
+      for (int I = 0; I < NT; ++I) {
+        if (I == kb) {
+          ar[I] = xr;
+          ai[I] = xi;
+        }
+        if (look && I == kb + 1) {
+          mma16_3m<true>(ar[I], ai[I], P[I], xr, xi);
+          invert(ar[I], ai[I]);
         }
       }
-    __syncthreads();
-    if (kb == 0) CR_STAMP(5);
+#pragma unroll
+      for (int I = 0; I < NT; ++I)
+        if (I != kb && !(look && I == kb + 1)) mma16_3m<true>(ar[I], ai[I], P[I], xr, xi);
+    }
+    if (kb == 0) CR_STAMP(3);
   }
-  CR_STAMP(6);
-  if (I0 == 0) {   // top half of the inverse
+  CR_STAMP(4);
+  // top half of the inverse: tile rows I < NT / 2
 #pragma unroll
-    for (int ti = 0; ti < TH; ++ti)
+  for (int I = 0; I < NT / 2; ++I)
 #pragma unroll
-      for (int tj = 0; tj < TH; ++tj)
+    for (int rr = 0; rr < 4; ++rr)
+      M[(int64_t)(I * 16 + lk + 4 * rr) * BP + w * 16 + lr] = make_double2(ar[I][rr], ai[I][rr]);
+  if (l == 0) ldw[w] = ld;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
 #pragma unroll
-        for (int rr = 0; rr < 4; ++rr)
-          M[(int64_t)((I0 + ti) * 16 + lk + 4 * rr) * BP + (J0 + tj) * 16 + lr] =
-              make_double2(ar[ti][tj][rr], ai[ti][tj][rr]);
+    for (int k = 0; k < NT; ++k) t += ldw[k];
+    ldpart[(int64_t)bi * nslots + slot[li]] = t;
   }
-  if (tid == 0) ldpart[(int64_t)bi * nslots + slot[li]] = ld;
-  CR_STAMP(7);
+  CR_STAMP(5);
 }
 
 // ---------------------------------------------------------------------------
@@ -288,172 +308,159 @@ __global__ __launch_bounds__(256) void k_cr_inv(double2* __restrict__ pool, int6
 // K runs over all BP rows of B_h: rows 0..HP-1 are stored, rows HP..BP-1 are
 // synthesised as sgn * conj(B_top[k - HP, (j + HP) mod BP]) with sgn from the
 // term's form bit (CrTask::bq) and the column half of the output tile.
-// One wave per TS x TS output tile (TS = 32: 2x2 MFMA tiles, operand reuse;
-// TS = 16: one MFMA tile with two interleaved accumulator chains, 4x the
-// waves for the small stages of the coarse levels, which are latency bound).
-// MFMA fragments come straight from L2 with a register prefetch; 1D grid with
-// the XCD-aware remap so one item's tasks share an XCD's L2.  out never
-// aliases an operand (planner invariant); out == cin is allowed.
+// Complex MACs use three real MFMAs (v_mfma_f64_16x16x4_f64):
+//   t1 += ar br,  t2 += ai bi,  t3 += (ar + ai)(br + bi);
+//   re = t1 - t2,  im = t3 - t1 - t2
+// Output tiles are TS x TS (TS = 16 MI).  KSPLIT waves of a workgroup share a
+// tile, each running 1/KSPLIT of every term's K range (short serial MFMA
+// chains for the latency-bound coarse stages); their partials are summed
+// through LDS.  KSPLIT = 1: four independent tiles per workgroup, no LDS, no
+// barriers.  MFMA fragments come straight from L2 with a register prefetch;
+// 1D grid with the XCD-aware remap so one item's tasks share an XCD's L2.
+// out never aliases an operand (planner invariant); out == cin is allowed.
 // ---------------------------------------------------------------------------
-template <int BP>
-__device__ __forceinline__ void cr_tile32(double2* base, const CrTask* tk, int cin, int nt, int tr,
-                                          int tc, double sg) {
-  constexpr int HP = BP / 2, KS = BP / 4, KH = HP / 4;
+template <int BP, int MI, int KSPLIT, int KQ>
+__device__ __forceinline__ void cr_tile_part(const double2* base, const CrTask* tk, int nt, int tr,
+                                             int tc, double sg, d4 (&t1)[MI][MI], d4 (&t2)[MI][MI],
+                                             d4 (&t3)[MI][MI]) {
+  constexpr int TS = 16 * MI, HP = BP / 2, KS = BP / 4, KH = HP / 4, KSS = KS / KSPLIT, S0 = KQ * KSS;
+  constexpr int PF = KSS < (MI == 1 ? 4 : 2) ? KSS : (MI == 1 ? 4 : 2);
   constexpr int64_t BB = (int64_t)HP * BP;
   const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
-  const int c0 = tc * 32, crot = c0 < HP ? c0 + HP : c0 - HP;
-  d4 acr[2][2], aci[2][2];
-#pragma unroll
-  for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < 2; ++ni) {
-      if (cin >= 0) {
-        const double2* C = base + cin * BB + (int64_t)(tr * 32 + mi * 16 + lk) * BP + c0 + ni * 16 + lr;
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          const double2 v = C[(int64_t)4 * rr * BP];
-          acr[mi][ni][rr] = v.x;
-          aci[mi][ni][rr] = v.y;
-        }
-      } else {
-        acr[mi][ni] = d4{0.0, 0.0, 0.0, 0.0};
-        aci[mi][ni] = d4{0.0, 0.0, 0.0, 0.0};
-      }
-    }
+  const int c0 = tc * TS, crot = c0 < HP ? c0 + HP : c0 - HP;
 #pragma unroll 1
   for (int h = 0; h < nt; ++h) {
-    const double2* A = base + tk->a[h] * BB + (int64_t)(tr * 32 + lr) * BP + lk;
+    const double2* A = base + tk->a[h] * BB + (int64_t)(tr * TS + lr) * BP + lk;
     const double2* Bt = base + tk->b[h] * BB + (int64_t)lk * BP + lr;
     // synthesised rows: sgn * conj(.), sgn = -s (left column half) / +s (right), s = +1 Q, -1 M
     const double sb = ((tk->bq >> h) & 1) ? 1.0 : -1.0;
     const double sgn = c0 < HP ? -sb : sb;
-    double2 fa[2][2], fb[2][2];
-    auto load = [&](int s, double2 (&a)[2], double2 (&bb)[2]) {
-      a[0] = A[s * 4];
-      a[1] = A[(int64_t)16 * BP + s * 4];
-      if (s < KH) {
-        bb[0] = Bt[(int64_t)s * 4 * BP + c0];
-        bb[1] = Bt[(int64_t)s * 4 * BP + c0 + 16];
-      } else {
-        const double2 u0 = Bt[(int64_t)(s - KH) * 4 * BP + crot];
-        const double2 u1 = Bt[(int64_t)(s - KH) * 4 * BP + crot + 16];
-        bb[0] = make_double2(sgn * u0.x, -sgn * u0.y);
-        bb[1] = make_double2(sgn * u1.x, -sgn * u1.y);
+    auto load = [&](int s, double2 (&a)[MI], double2 (&b)[MI]) {
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi) a[mi] = A[(int64_t)16 * mi * BP + s * 4];
+#pragma unroll
+      for (int ni = 0; ni < MI; ++ni) {
+        if (s < KH) {
+          b[ni] = Bt[(int64_t)s * 4 * BP + c0 + 16 * ni];
+        } else {
+          const double2 u = Bt[(int64_t)(s - KH) * 4 * BP + crot + 16 * ni];
+          b[ni] = make_double2(sgn * u.x, -sgn * u.y);
+        }
       }
     };
-    load(0, fa[0], fb[0]);
-    load(1, fa[1], fb[1]);
+    double2 fa[PF][MI], fb[PF][MI];
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const int cs = s & 1;
-      const double2 av[2] = {make_double2(sg * fa[cs][0].x, sg * fa[cs][0].y),
-                             make_double2(sg * fa[cs][1].x, sg * fa[cs][1].y)};
-      const double2 bv[2] = {fb[cs][0], fb[cs][1]};
-      if (s + 2 < KS) load(s + 2, fa[cs], fb[cs]);
+    for (int p = 0; p < PF; ++p) load(S0 + p, fa[p], fb[p]);
 #pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
+    for (int j = 0; j < KSS; ++j) {
+      const int cs = j % PF;
+      double ar[MI], ai[MI], as[MI], br[MI], bi[MI], bs[MI];
 #pragma unroll
-        for (int ni = 0; ni < 2; ++ni) {
-          acr[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[mi].x, bv[ni].x, acr[mi][ni], 0, 0, 0);
-          aci[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[mi].x, bv[ni].y, aci[mi][ni], 0, 0, 0);
-        }
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni) {
-          acr[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av[mi].y, bv[ni].y, acr[mi][ni], 0, 0, 0);
-          aci[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[mi].y, bv[ni].x, aci[mi][ni], 0, 0, 0);
-        }
-    }
-  }
-  double2* O = base + tk->out * BB + (int64_t)(tr * 32 + lk) * BP + c0 + lr;
-#pragma unroll
-  for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr)
-        O[(int64_t)(mi * 16 + 4 * rr) * BP + ni * 16] = make_double2(acr[mi][ni][rr], aci[mi][ni][rr]);
-}
-
-template <int BP>
-__device__ __forceinline__ void cr_tile16(double2* base, const CrTask* tk, int cin, int nt, int tr,
-                                          int tc, double sg) {
-  constexpr int HP = BP / 2, KS = BP / 4, KH = HP / 4, PF = 4;
-  constexpr int64_t BB = (int64_t)HP * BP;
-  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
-  const int c0 = tc * 16, crot = c0 < HP ? c0 + HP : c0 - HP;
-  d4 acr[2], aci[2];
-  acr[1] = d4{0.0, 0.0, 0.0, 0.0};
-  aci[1] = d4{0.0, 0.0, 0.0, 0.0};
-  if (cin >= 0) {
-    const double2* C = base + cin * BB + (int64_t)(tr * 16 + lk) * BP + c0 + lr;
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      const double2 v = C[(int64_t)4 * rr * BP];
-      acr[0][rr] = v.x;
-      aci[0][rr] = v.y;
-    }
-  } else {
-    acr[0] = d4{0.0, 0.0, 0.0, 0.0};
-    aci[0] = d4{0.0, 0.0, 0.0, 0.0};
-  }
-#pragma unroll 1
-  for (int h = 0; h < nt; ++h) {
-    const double2* A = base + tk->a[h] * BB + (int64_t)(tr * 16 + lr) * BP + lk;
-    const double2* Bt = base + tk->b[h] * BB + (int64_t)lk * BP + lr;
-    const double sb = ((tk->bq >> h) & 1) ? 1.0 : -1.0;
-    const double sgn = c0 < HP ? -sb : sb;
-    auto bload = [&](int s) {
-      if (s < KH) return Bt[(int64_t)s * 4 * BP + c0];
-      const double2 u = Bt[(int64_t)(s - KH) * 4 * BP + crot];
-      return make_double2(sgn * u.x, -sgn * u.y);
-    };
-    double2 fa[PF], fb[PF];
-#pragma unroll
-    for (int s = 0; s < PF; ++s) {
-      fa[s] = A[s * 4];
-      fb[s] = bload(s);
-    }
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const int cs = s % PF, p = s & 1;
-      const double2 av = make_double2(sg * fa[cs].x, sg * fa[cs].y), bv = fb[cs];
-      if (s + PF < KS) {
-        fa[cs] = A[(s + PF) * 4];
-        fb[cs] = bload(s + PF);
+      for (int mi = 0; mi < MI; ++mi) {
+        ar[mi] = sg * fa[cs][mi].x;
+        ai[mi] = sg * fa[cs][mi].y;
+        as[mi] = ar[mi] + ai[mi];
+        br[mi] = fb[cs][mi].x;
+        bi[mi] = fb[cs][mi].y;
+        bs[mi] = br[mi] + bi[mi];
       }
-      acr[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.x, acr[p], 0, 0, 0);
-      aci[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.y, aci[p], 0, 0, 0);
-      acr[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av.y, bv.y, acr[p], 0, 0, 0);
-      aci[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, bv.x, aci[p], 0, 0, 0);
+      if (j + PF < KSS) load(S0 + j + PF, fa[cs], fb[cs]);
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < MI; ++ni) {
+          t1[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[mi], br[ni], t1[mi][ni], 0, 0, 0);
+          t2[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[mi], bi[ni], t2[mi][ni], 0, 0, 0);
+          t3[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(as[mi], bs[ni], t3[mi][ni], 0, 0, 0);
+        }
     }
   }
-  double2* O = base + tk->out * BB + (int64_t)(tr * 16 + lk) * BP + c0 + lr;
-#pragma unroll
-  for (int rr = 0; rr < 4; ++rr)
-    O[(int64_t)4 * rr * BP] = make_double2(acr[0][rr] + acr[1][rr], aci[0][rr] + aci[1][rr]);
 }
 
-template <int BP, int TS>
-__global__ __launch_bounds__(256) void k_cr_gemm(double2* __restrict__ pool, int64_t item,
+template <int BP, int MI, int KSPLIT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_cr_gemm(double2* __restrict__ pool, int64_t item,
                                                  const CrTask* __restrict__ tasks, int ntasks,
                                                  int maxt, int total, double sg) {
-  const int gw = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x) * 4 + (int)(threadIdx.x >> 6));
-  if (gw >= total) return;
+  constexpr int TS = 16 * MI, TPW = 4 / KSPLIT, HP = BP / 2, NV = MI * MI * 4;
+  constexpr int64_t BB = (int64_t)HP * BP;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  const int kq = w % KSPLIT;
+  const int gt = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x) * TPW + w / KSPLIT);
   const int per_item = ntasks * maxt;
-  const int bi = gw / per_item;
-  const int rmd = gw - bi * per_item;
+  const int bi = gt / per_item;
+  const int rmd = gt - bi * per_item;
   const int tsk = rmd / maxt, tile = rmd - tsk * maxt;
-  const CrTask* tk = tasks + tsk;
+  bool valid = gt < total;
+  const CrTask* tk = tasks + (valid ? tsk : 0);
   const int tr0 = tk->r0 / TS, tc0 = tk->c0 / TS;
   const int ct = (tk->c1 + TS - 1) / TS - tc0;
   const int rt = (tk->r1 + TS - 1) / TS - tr0;
-  if (tile >= rt * ct) return;   // restricted task: fewer tiles than the stage maximum
-  const int tr = tr0 + tile / ct, tc = tc0 + tile % ct;
-  double2* base = pool + (int64_t)bi * item;
-  if (TS == 32) cr_tile32<BP>(base, tk, tk->cin, tk->nt, tr, tc, sg);
-  else cr_tile16<BP>(base, tk, tk->cin, tk->nt, tr, tc, sg);
+  valid = valid && tile < rt * ct;   // restricted task: fewer tiles than the stage maximum
+  const int tr = tr0 + (valid ? tile / ct : 0), tc = tc0 + (valid ? tile % ct : 0);
+  double2* base = pool + (int64_t)(valid ? bi : 0) * item;
+  d4 t1[MI][MI], t2[MI][MI], t3[MI][MI];
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < MI; ++ni) {
+      t1[mi][ni] = d4{0.0, 0.0, 0.0, 0.0};
+      t2[mi][ni] = d4{0.0, 0.0, 0.0, 0.0};
+      t3[mi][ni] = d4{0.0, 0.0, 0.0, 0.0};
+    }
+  if (valid) {
+    const int nt = tk->nt;
+    if (KSPLIT == 1 || kq == 0) cr_tile_part<BP, MI, KSPLIT, 0>(base, tk, nt, tr, tc, sg, t1, t2, t3);
+    if constexpr (KSPLIT >= 2) {
+      if (kq == 1) cr_tile_part<BP, MI, KSPLIT, 1>(base, tk, nt, tr, tc, sg, t1, t2, t3);
+    }
+    if constexpr (KSPLIT == 4) {
+      if (kq == 2) cr_tile_part<BP, MI, KSPLIT, 2>(base, tk, nt, tr, tc, sg, t1, t2, t3);
+      if (kq == 3) cr_tile_part<BP, MI, KSPLIT, 3>(base, tk, nt, tr, tc, sg, t1, t2, t3);
+    }
+  }
+  const int cin = tk->cin;
+  double2* O = base + tk->out * BB + (int64_t)(tr * TS + lk) * BP + tc * TS + lr;
+  const double2* C = cin >= 0 ? base + cin * BB + (int64_t)(tr * TS + lk) * BP + tc * TS + lr : nullptr;
+  auto put = [&](int v, double2 x) {
+    const int mi = v / (MI * 4), ni = (v / 4) % MI, rr = v % 4;
+    const int64_t o = (int64_t)(mi * 16 + 4 * rr) * BP + ni * 16;
+    if (C) {
+      const double2 c = C[o];
+      x.x += c.x;
+      x.y += c.y;
+    }
+    O[o] = x;
+  };
+  // complex partial of register slot v = (mi * MI + ni) * 4 + rr
+  auto partial = [&](int v) {
+    const int mi = v / (MI * 4), ni = (v / 4) % MI, rr = v % 4;
+    const double a = t1[mi][ni][rr], b = t2[mi][ni][rr], c = t3[mi][ni][rr];
+    return make_double2(a - b, c - a - b);
+  };
+  if constexpr (KSPLIT == 1) {
+    if (!valid) return;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) put(v, partial(v));
+  } else {
+    __shared__ double2 red[4][NV][64];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) red[w][v][l] = partial(v);
+    __syncthreads();
+    if (!valid) return;
+    const int g0 = w - kq;   // first wave of this tile's group
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      if (v % KSPLIT != kq) continue;
+      double2 x = red[g0][v][l];
+#pragma unroll
+      for (int k = 1; k < KSPLIT; ++k) {
+        const double2 y = red[g0 + k][v][l];
+        x.x += y.x;
+        x.y += y.y;
+      }
+      put(v, x);
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -548,36 +555,61 @@ void launch_cr_inv(const CrDims& c, double2* pool, const int* blk, const int* sl
   if (n <= 0) return;
   const dim3 g(n, c.nbatch);
   switch (c.BP) {
-    case 32: hipLaunchKernelGGL(k_cr_inv<2>, g, dim3(256), 0, s, pool, c.item, blk, slot, ldpart, c.Ly); break;
+    case 32: hipLaunchKernelGGL(k_cr_inv<2>, g, dim3(128), 0, s, pool, c.item, blk, slot, ldpart, c.Ly); break;
     case 64: hipLaunchKernelGGL(k_cr_inv<4>, g, dim3(256), 0, s, pool, c.item, blk, slot, ldpart, c.Ly); break;
-    default: hipLaunchKernelGGL(k_cr_inv<6>, g, dim3(256), 0, s, pool, c.item, blk, slot, ldpart, c.Ly); break;
+    default: hipLaunchKernelGGL(k_cr_inv<6>, g, dim3(384), 0, s, pool, c.item, blk, slot, ldpart, c.Ly); break;
   }
 }
 
-void launch_cr_gemm(const CrDims& c, double2* pool, const CrTask* tasks, int ntasks, int maxt32,
-                    int maxt16, double sg, hipStream_t s) {
-  if (ntasks <= 0) return;
-  // latency-bound small stages (fewer than ~2 waves per SIMD at 32x32 tiles)
-  // run 16x16 wave tiles: 4x the waves, 4x shorter MFMA chains
-  static const int small = [] {
-    const char* e = std::getenv("DWHMC_CR_SMALL");
-    return e ? std::atoi(e) : 1024;
+// Stage configuration (tile TS, K split).  16 x 16 tiles with a 4-way K
+// split measured fastest on every stage of the L=32 plan (tools/cr_cfg_sweep.sh,
+// profiles/r01_cr_gemm_config_sweep.txt): the stages are short and latency
+// bound, so short serial MFMA chains on many waves win over operand reuse.
+// DWHMC_CR_GEMM=TS:KSPLIT forces another configuration for every stage (A/B).
+CrGemmCfg cr_gemm_config(const CrDims& c, int ntasks, int maxt32, int maxt16, int ntmax) {
+  (void)ntasks;
+  (void)maxt32;
+  (void)maxt16;
+  (void)ntmax;
+  static const CrGemmCfg forced = [] {
+    CrGemmCfg f{0, 1};
+    if (const char* e = std::getenv("DWHMC_CR_GEMM")) {
+      f.ts = std::atoi(e);
+      if (const char* p = std::strchr(e, ':')) f.ksplit = std::atoi(p + 1);
+    }
+    if (f.ksplit != 1 && f.ksplit != 2 && f.ksplit != 4) f.ksplit = 1;
+    if (f.ts == 32 && f.ksplit == 4) f.ksplit = 2;
+    return f;
   }();
-  // 32-wide tiles must not straddle the A | B column halves
-  const bool use16 = (c.BP / 2) % 32 != 0 || (int64_t)c.nbatch * ntasks * maxt32 < small;
-  const int maxt = use16 ? maxt16 : maxt32;
+  const bool ts32_ok = (c.BP / 2) % 32 == 0;   // 32-wide tiles must not straddle A | B
+  if (forced.ts == 16 || (forced.ts == 32 && ts32_ok)) return forced;
+  return CrGemmCfg{16, 4};
+}
+
+void launch_cr_gemm(const CrDims& c, double2* pool, const CrTask* tasks, int ntasks, int maxt32,
+                    int maxt16, const CrGemmCfg& cfg, double sg, hipStream_t s) {
+  if (ntasks <= 0) return;
+  const int maxt = cfg.ts == 32 ? maxt32 : maxt16;
   const int total = c.nbatch * ntasks * maxt;
-  const dim3 g((total + 3) / 4), b(256);
-#define CR_GEMM(BPV)                                                                             \
-  if (use16)                                                                                     \
-    hipLaunchKernelGGL((k_cr_gemm<BPV, 16>), g, b, 0, s, pool, c.item, tasks, ntasks, maxt, total, sg); \
-  else                                                                                           \
-    hipLaunchKernelGGL((k_cr_gemm<BPV, 32>), g, b, 0, s, pool, c.item, tasks, ntasks, maxt, total, sg);
-  switch (c.BP) {
-    case 32: CR_GEMM(32) break;
-    case 64: CR_GEMM(64) break;
-    default: CR_GEMM(96) break;
+  const int tpw = 4 / cfg.ksplit;
+  const dim3 g((total + tpw - 1) / tpw), b(256);
+#define CR_GEMM(BPV, MIV, KSV) \
+  hipLaunchKernelGGL((k_cr_gemm<BPV, MIV, KSV>), g, b, 0, s, pool, c.item, tasks, ntasks, maxt, total, sg)
+#define CR_GEMM_BP(BPV)                        \
+  if (cfg.ts == 16) {                          \
+    if (cfg.ksplit == 4) CR_GEMM(BPV, 1, 4);   \
+    else if (cfg.ksplit == 2) CR_GEMM(BPV, 1, 2); \
+    else CR_GEMM(BPV, 1, 1);                   \
+  } else {                                     \
+    if (cfg.ksplit == 2) CR_GEMM(BPV, 2, 2);   \
+    else CR_GEMM(BPV, 2, 1);                   \
   }
+  switch (c.BP) {
+    case 32: CR_GEMM_BP(32) break;
+    case 64: CR_GEMM_BP(64) break;
+    default: CR_GEMM_BP(96) break;
+  }
+#undef CR_GEMM_BP
 #undef CR_GEMM
 }
 

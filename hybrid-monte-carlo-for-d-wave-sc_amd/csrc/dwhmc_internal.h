@@ -67,9 +67,16 @@ void launch_cr_fermion_energy(const CrDims& c, const double2* pool, const int64_
                               double* Ef, double* Trhh, hipStream_t s);
 void launch_cr_inv(const CrDims& c, double2* pool, const int* blk, const int* slot, int n,
                    double* ldpart, hipStream_t s);
-// maxt32 / maxt16: the largest cr_task_tiles over the stage's tasks at ts = 32 / 16
+// block-product stage configuration: output tile TS x TS (16 or 32) and the
+// number of waves splitting each tile's K range (1, 2, 4)
+struct CrGemmCfg {
+  int ts, ksplit;
+};
+// maxt32 / maxt16: the largest cr_task_tiles over the stage's tasks at ts = 32 / 16;
+// ntmax: the largest term count
+CrGemmCfg cr_gemm_config(const CrDims& c, int ntasks, int maxt32, int maxt16, int ntmax);
 void launch_cr_gemm(const CrDims& c, double2* pool, const CrTask* tasks, int ntasks, int maxt32,
-                    int maxt16, double sg, hipStream_t s);
+                    int maxt16, const CrGemmCfg& cfg, double sg, hipStream_t s);
 
 // dense h - i y_q (padded with identity) for every (chain, pole): R init input
 void launch_fill_hz(const Dims& d, double2* M, const int* hcol, const double* hval,

@@ -40,12 +40,12 @@ int main(int argc, char** argv) {
   static unsigned long long st[1024][16];
   hipMemcpyFromSymbol(st, HIP_SYMBOL(g_cr_stamps), sizeof st);
   const int nb = nblk * nbatch;
-  double acc[8] = {0};
+  double acc[6] = {0};
   for (int b = 0; b < nb; ++b)
-    for (int i = 1; i < 8; ++i) acc[i] += (double)(st[b][i] - st[b][i - 1]);
-  const char* nm[8] = {"", "load block", "publish+sync (kb0)", "inv16 (kb0)", "X panel (kb0)",
-                       "update+sync (kb0)", "kb1..", "store+ld"};
-  printf("mean s_memtime ticks per phase over %d blocks:\n", nb);
-  for (int i = 1; i < 8; ++i) printf("  %-20s %10.0f\n", nm[i], acc[i] / nb);
+    for (int i = 1; i < 6; ++i) acc[i] += (double)(st[b][i] - st[b][i - 1]);
+  const char* nm[6] = {"", "load block", "pivot 0 inverse", "step kb=0 (wave 0)", "steps kb=1..",
+                       "store+ld"};
+  printf("mean s_memtime ticks per phase over %d blocks (wave 0's view):\n", nb);
+  for (int i = 1; i < 6; ++i) printf("  %-20s %10.0f\n", nm[i], acc[i] / nb);
   return 0;
 }
