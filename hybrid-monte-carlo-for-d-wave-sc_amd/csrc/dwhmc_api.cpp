@@ -57,10 +57,11 @@ struct CrPlan {
   int nblk = 0;
   std::vector<CrStage> stages;
   std::vector<dwh::CrTask> tasks;
-  std::vector<int> inv_blk, inv_slot;
+  std::vector<int> inv_blk, inv_dst, inv_slot;   // inversion source / destination block, ln|det| slot
   std::vector<int64_t> goff, doff;
   std::vector<int> fill_all, fill_step;      // level-0 blocks written at create / every step
   std::vector<int64_t> off_ph;               // pairing entries outside fill_step (-1: none)
+  int n_ph = 0;                              // entries of off_ph >= 0
 };
 
 // Block cyclic reduction of the periodic block-tridiagonal H_BdG - i y (blocks
@@ -92,16 +93,25 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol) {
   struct Level {
     int m;
     std::vector<int> D, U, L, E, K;
+    std::vector<int> Dinv;             // block holding D_e^-1 (then G_ee), by position e
     std::vector<int> V1, V2, W1, W2;   // indexed by position e
     std::vector<char> elim;
   };
+  // Level-0 blocks are inverted out of place (they are never overwritten, so
+  // per step only their pairing entries change), coarser blocks in place.
+  // Returns the blocks that hold the inverses.
   auto add_inv = [&](const std::vector<int>& blocks, int& slot) {
     CrStage st{0, (int)pl.inv_blk.size(), (int)blocks.size(), 0.0, 0.0, 0, 0, 0, {16, 1}};
+    std::vector<int> dst;
     for (int b : blocks) {
+      const int d = b < 3 * Ly ? nb() : b;
       pl.inv_blk.push_back(b);
+      pl.inv_dst.push_back(d);
       pl.inv_slot.push_back(slot++);
+      dst.push_back(d);
     }
     pl.stages.push_back(st);
+    return dst;
   };
   struct Term { int a, b; };
   std::vector<dwh::CrTask> cur_tasks;
@@ -164,17 +174,19 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol) {
     cur.W2.assign(m, -1);
     std::vector<int> inv;
     for (int e : cur.E) inv.push_back(cur.D[e]);
-    add_inv(inv, slot);
+    const std::vector<int> dinv = add_inv(inv, slot);
+    cur.Dinv.assign(m, -1);
+    for (size_t i = 0; i < cur.E.size(); ++i) cur.Dinv[cur.E[i]] = dinv[i];
     for (int e : cur.E) {
       const int a = e - 1;
       cur.V1[e] = nbq();
-      task(cur.V1[e], -1, {{cur.U[a], cur.D[e]}});
+      task(cur.V1[e], -1, {{cur.U[a], cur.Dinv[e]}});
       cur.V2[e] = nbq();
-      task(cur.V2[e], -1, {{cur.L[e], cur.D[e]}});
+      task(cur.V2[e], -1, {{cur.L[e], cur.Dinv[e]}});
       cur.W1[e] = nbq();
-      task(cur.W1[e], -1, {{cur.D[e], cur.L[a]}});
+      task(cur.W1[e], -1, {{cur.Dinv[e], cur.L[a]}});
       cur.W2[e] = nbq();
-      task(cur.W2[e], -1, {{cur.D[e], cur.U[e]}});
+      task(cur.W2[e], -1, {{cur.Dinv[e], cur.U[e]}});
     }
     flush(-1.0);
     Level nxt;
@@ -214,8 +226,8 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol) {
     levels.push_back(cur);
     cur = nxt;
   }
-  add_inv({cur.D[0]}, slot);
-  std::vector<int> GD{cur.D[0]}, GU{cur.D[0]}, GL{cur.D[0]};
+  const int Dfin = add_inv({cur.D[0]}, slot)[0];
+  std::vector<int> GD{Dfin}, GU{Dfin}, GL{Dfin};
   for (int li = (int)levels.size() - 1; li >= 0; --li) {
     const Level& lv = levels[li];
     const int m = lv.m, mn = (int)lv.K.size();
@@ -259,8 +271,8 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol) {
     }
     flush(1.0);
     for (int e : lv.E) {
-      task(lv.D[e], lv.D[e], {{lv.W1[e], Gae[e]}, {lv.W2[e], Gce[e]}});
-      gd[e] = lv.D[e];
+      task(lv.Dinv[e], lv.Dinv[e], {{lv.W1[e], Gae[e]}, {lv.W2[e], Gce[e]}});
+      gd[e] = lv.Dinv[e];
     }
     flush(1.0);
     GD = gd;
@@ -286,13 +298,10 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol) {
     }
     pl.doff[i] = GD[y] * BB + (int64_t)x * BP + x;   // G22[x, x] = -conj(A[x, x])
   }
-  // level-0 fill lists and pairing scatter offsets: CR overwrites only the
-  // level-0 eliminated D blocks (in-place inversion, then G_ee)
+  // level-0 fill lists and pairing scatter offsets: CR never overwrites a
+  // level-0 block (their inverses are formed out of place), so per step only
+  // the pairing entries are scattered
   std::vector<char> rewrite(3 * Ly, 0);
-  if (!levels.empty())
-    for (int e : levels[0].E) rewrite[levels[0].D[e]] = 1;
-  else
-    rewrite[0] = 1;   // Ly == 1: the single block is inverted in place
   for (int b = 0; b < 3 * Ly; ++b) {
     pl.fill_all.push_back(b);
     if (rewrite[b]) pl.fill_step.push_back(b);
@@ -311,6 +320,7 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol) {
       const int b = blk_of(yi, yj);
       if (rewrite[b]) continue;
       pl.off_ph[(size_t)i * kSlots + s] = b * BB + (int64_t)xi * BP + (HP + xj);
+      pl.n_ph++;
     }
   pl.nblk = nblk;
   return pl;
@@ -375,7 +385,7 @@ struct dwh_ctx {
   CrPlan plan;
   double2* bpool = nullptr;   // CR block pool (nbatch x nblk blocks)
   dwh::CrTask* d_tasks = nullptr;
-  int *d_inv_blk = nullptr, *d_inv_slot = nullptr;
+  int *d_inv_blk = nullptr, *d_inv_dst = nullptr, *d_inv_slot = nullptr;
   int64_t *d_goff = nullptr, *d_doff = nullptr, *d_off_ph = nullptr;
   int *d_fill_all = nullptr, *d_fill_step = nullptr;
 
@@ -539,18 +549,21 @@ void cr_enqueue(dwh_ctx* ctx) {
   const dwh::CrDims& c = ctx->cr;
   const double bp3 = 8.0 * c.BP * (double)c.BP * c.BP * c.nbatch;
   {
-    // bytes written: the 3 Ly level-0 blocks of every batch item
-    // rewritten level-0 blocks (top halves) + pairing scatter, Δ/2 read directly
+    // algorithmic bytes: rewritten level-0 blocks (top halves, none with the
+    // out-of-place level-0 inversions) + the pairing entries Δ/2 scattered
+    // into the level-0 blocks of every batch item (16 B each)
     const CrPlan& pl = ctx->plan;
-    Scope s(ctx, T_ASSEMBLE, (double)pl.fill_step.size() * 8.0 * c.BP * (double)c.BP * c.nbatch);
+    Scope s(ctx, T_ASSEMBLE,
+            (double)pl.fill_step.size() * 8.0 * c.BP * (double)c.BP * c.nbatch +
+                16.0 * (double)pl.n_ph * c.nbatch);
     dwh::launch_cr_fill(c, ctx->bpool, ctx->d_fill_step, (int)pl.fill_step.size(), ctx->hcol, ctx->hval,
                         ctx->Dcol, ctx->Dsrc, ctx->Delta, ctx->d_y, ctx->d_off_ph, ctx->stream);
   }
   for (const CrStage& st : ctx->plan.stages) {
     if (st.kind == 0) {
       Scope s(ctx, T_CR_INV, st.n * bp3);
-      dwh::launch_cr_inv(c, ctx->bpool, ctx->d_inv_blk + st.first, ctx->d_inv_slot + st.first, st.n,
-                         ctx->ldpart, ctx->stream);
+      dwh::launch_cr_inv(c, ctx->bpool, ctx->d_inv_blk + st.first, ctx->d_inv_dst + st.first,
+                         ctx->d_inv_slot + st.first, st.n, ctx->ldpart, ctx->stream);
     } else {
       Scope s(ctx, T_CR_GEMM, st.flops * c.nbatch);
       dwh::launch_cr_gemm(c, ctx->bpool, ctx->d_tasks + st.first, st.n, st.maxt32, st.maxt16, st.cfg,
@@ -886,6 +899,7 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     ALLOC(bpool, (size_t)d.nbatch * ctx->cr.item);
     ALLOC(d_tasks, pl.tasks.size());
     ALLOC(d_inv_blk, pl.inv_blk.size());
+    ALLOC(d_inv_dst, pl.inv_dst.size());
     ALLOC(d_inv_slot, pl.inv_slot.size());
     ALLOC(d_goff, pl.goff.size());
     ALLOC(d_doff, pl.doff.size());
@@ -929,7 +943,7 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
   ctx->ndraws = 0;
   hipStream_t s = ctx->stream;
 #define UP(dst, src, n)                                                                     \
-  if (hipMemcpyAsync(ctx->dst, (src), (n) * sizeof(*ctx->dst), hipMemcpyHostToDevice, s) != \
+  if ((n) > 0 && hipMemcpyAsync(ctx->dst, (src), (n) * sizeof(*ctx->dst), hipMemcpyHostToDevice, s) != \
       hipSuccess) {                                                                         \
     ctx->err = "upload " #dst;                                                              \
     return bail(DWH_ERR_HIP);                                                               \
@@ -946,6 +960,7 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     const CrPlan& pl = ctx->plan;
     UP(d_tasks, pl.tasks.data(), pl.tasks.size());
     UP(d_inv_blk, pl.inv_blk.data(), pl.inv_blk.size());
+    UP(d_inv_dst, pl.inv_dst.data(), pl.inv_dst.size());
     UP(d_inv_slot, pl.inv_slot.data(), pl.inv_slot.size());
     UP(d_goff, pl.goff.data(), pl.goff.size());
     UP(d_doff, pl.doff.data(), pl.doff.size());

@@ -179,6 +179,7 @@ __device__ __forceinline__ void mma16_3m(d4& cr, d4& ci, const double2* A, const
 template <int NT>
 __global__ __launch_bounds__(64 * NT) void k_cr_inv(double2* __restrict__ pool, int64_t item,
                                                     const int* __restrict__ blk,
+                                                    const int* __restrict__ dst,
                                                     const int* __restrict__ slot,
                                                     double* __restrict__ ldpart, int nslots) {
   constexpr int BP = 16 * NT, HP = BP / 2, TSZ = 16 * 17;
@@ -186,7 +187,8 @@ __global__ __launch_bounds__(64 * NT) void k_cr_inv(double2* __restrict__ pool, 
   __shared__ double2 scr[NT][TSZ];
   __shared__ double ldw[NT];
   const int bi = blockIdx.y, li = blockIdx.x;
-  double2* M = pool + (int64_t)bi * item + (int64_t)blk[li] * HP * BP;
+  const double2* M = pool + (int64_t)bi * item + (int64_t)blk[li] * HP * BP;
+  double2* Mo = pool + (int64_t)bi * item + (int64_t)dst[li] * HP * BP;   // may equal M
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
   d4 ar[NT], ai[NT];
   CR_STAMP(0);
@@ -290,7 +292,7 @@ __global__ __launch_bounds__(64 * NT) void k_cr_inv(double2* __restrict__ pool, 
   for (int I = 0; I < NT / 2; ++I)
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr)
-      M[(int64_t)(I * 16 + lk + 4 * rr) * BP + w * 16 + lr] = make_double2(ar[I][rr], ai[I][rr]);
+      Mo[(int64_t)(I * 16 + lk + 4 * rr) * BP + w * 16 + lr] = make_double2(ar[I][rr], ai[I][rr]);
   if (l == 0) ldw[w] = ld;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -469,25 +471,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 // slot), F = -β/2J (Δ - J P) (src/Observables.jl:14-62), then the leapfrog
 // kick and the next step's drift (kick_drift).
 // ---------------------------------------------------------------------------
-__global__ void k_cr_pair_force(const double2* __restrict__ pool, int64_t item,
-                                const int64_t* __restrict__ goff, const int* __restrict__ bond_ij,
-                                const int* __restrict__ bond_ji, const double* __restrict__ cpole,
-                                int N, int P, double2* __restrict__ Delta,
-                                double2* __restrict__ Pair, double2* __restrict__ F,
-                                double2* __restrict__ Pi, double kick, double drift, double cap2,
-                                int* __restrict__ flag, double beta, double J) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+// 32 lanes per bond, one pole per lane (the G entries of the poles live in
+// different batch items: independent loads), shuffle reduction.
+__global__ __launch_bounds__(256) void k_cr_pair_force(
+    const double2* __restrict__ pool, int64_t item, const int64_t* __restrict__ goff,
+    const int* __restrict__ bond_ij, const int* __restrict__ bond_ji, const double* __restrict__ cpole,
+    int N, int P, double2* __restrict__ Delta, double2* __restrict__ Pair, double2* __restrict__ F,
+    double2* __restrict__ Pi, double kick, double drift, double cap2, int* __restrict__ flag,
+    double beta, double J) {
+  const int b = blockIdx.x * 8 + (threadIdx.x >> 5), sub = threadIdx.x & 31;
   const int c = blockIdx.y;
-  if (b >= 2 * N) return;
+  if (b >= 2 * N) return;   // uniform per 32-lane group
   const int64_t o1 = goff[bond_ij[b]], o2 = goff[bond_ji[b]];
   double2 Pv = make_double2(0.0, 0.0);
-  for (int q = 0; q < P; ++q) {
+  for (int q = sub; q < P; q += 32) {
     const double2* G = pool + (int64_t)(c * P + q) * item;
     const double2 g1 = G[o1], g2 = G[o2];
     const double cq = cpole[q];
     Pv.x += cq * (g1.x + g2.x);
     Pv.y += cq * (g1.y + g2.y);
   }
+#pragma unroll
+  for (int off = 16; off > 0; off >>= 1) {
+    Pv.x += __shfl_xor(Pv.x, off, 32);
+    Pv.y += __shfl_xor(Pv.y, off, 32);
+  }
+  if (sub != 0) return;
   const int64_t o = (int64_t)c * 2 * N + b;
   Pair[o] = Pv;
   const double2 d = Delta[o];
@@ -550,14 +559,14 @@ void launch_cr_fill(const CrDims& c, double2* pool, const int* list, int nlist, 
                      Delta, ypole, off_ph);
 }
 
-void launch_cr_inv(const CrDims& c, double2* pool, const int* blk, const int* slot, int n,
-                   double* ldpart, hipStream_t s) {
+void launch_cr_inv(const CrDims& c, double2* pool, const int* blk, const int* dst, const int* slot,
+                   int n, double* ldpart, hipStream_t s) {
   if (n <= 0) return;
   const dim3 g(n, c.nbatch);
   switch (c.BP) {
-    case 32: hipLaunchKernelGGL(k_cr_inv<2>, g, dim3(128), 0, s, pool, c.item, blk, slot, ldpart, c.Ly); break;
-    case 64: hipLaunchKernelGGL(k_cr_inv<4>, g, dim3(256), 0, s, pool, c.item, blk, slot, ldpart, c.Ly); break;
-    default: hipLaunchKernelGGL(k_cr_inv<6>, g, dim3(384), 0, s, pool, c.item, blk, slot, ldpart, c.Ly); break;
+    case 32: hipLaunchKernelGGL(k_cr_inv<2>, g, dim3(128), 0, s, pool, c.item, blk, dst, slot, ldpart, c.Ly); break;
+    case 64: hipLaunchKernelGGL(k_cr_inv<4>, g, dim3(256), 0, s, pool, c.item, blk, dst, slot, ldpart, c.Ly); break;
+    default: hipLaunchKernelGGL(k_cr_inv<6>, g, dim3(384), 0, s, pool, c.item, blk, dst, slot, ldpart, c.Ly); break;
   }
 }
 
@@ -618,7 +627,7 @@ void launch_cr_pair_force(const CrDims& c, const double2* pool, const int64_t* g
                           double2* Delta, double2* Pair, double2* F, double2* Pi,
                           const KickDrift& kd, double beta, double J, hipStream_t s) {
   const int nc = c.nbatch / c.P;
-  hipLaunchKernelGGL(k_cr_pair_force, dim3((2 * c.N + 255) / 256, nc), dim3(256), 0, s, pool, c.item,
+  hipLaunchKernelGGL(k_cr_pair_force, dim3((2 * c.N + 7) / 8, nc), dim3(256), 0, s, pool, c.item,
                      goff, bond_ij, bond_ji, cpole, c.N, c.P, Delta, Pair, F, Pi, kd.kick, kd.drift,
                      kd.cap * kd.cap, kd.flag, beta, J);
 }

@@ -65,8 +65,9 @@ void launch_cr_pair_force(const CrDims& c, const double2* pool, const int64_t* g
 void launch_cr_fermion_energy(const CrDims& c, const double2* pool, const int64_t* doff,
                               const double* ldpart, const double* cpole, double Cx, double beta,
                               double* Ef, double* Trhh, hipStream_t s);
-void launch_cr_inv(const CrDims& c, double2* pool, const int* blk, const int* slot, int n,
-                   double* ldpart, hipStream_t s);
+// inverts blocks blk[i] into dst[i] (dst == blk: in place); ln|det| into ldpart slots
+void launch_cr_inv(const CrDims& c, double2* pool, const int* blk, const int* dst, const int* slot,
+                   int n, double* ldpart, hipStream_t s);
 // block-product stage configuration: output tile TS x TS (16 or 32) and the
 // number of waves splitting each tile's K range (1, 2, 4)
 struct CrGemmCfg {

@@ -31,7 +31,7 @@ int main(int argc, char** argv) {
   for (int rep = 0; rep < 4; ++rep) {
     hipMemcpy(M, h.data(), h.size() * 16, hipMemcpyHostToDevice);
     hipEventRecord(e0);
-    launch_cr_inv(c, M, blk, slot, nblk, ld, 0);
+    launch_cr_inv(c, M, blk, blk, slot, nblk, ld, 0);
     hipEventRecord(e1);
     hipEventSynchronize(e1);
     float t; hipEventElapsedTime(&t, e0, e1);
