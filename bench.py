@@ -243,7 +243,7 @@ def main():
             ms, n, w = kern[dom]
             ach = w / n / (ms / n * 1e-3) / 1e12 if n and ms > 0 else None
             if cr:
-                kname = f"k_cr_gemm<{info['block']}>"
+                kname = f"k_cr_gemm<{info['block']},1,4>"   # 16x16 tiles, 4-way K split (every stage)
                 msi, ni, wi = kern["cr_inv"]
                 # the CR path's own algorithmic flops: block products + block inversions
                 # the CR path's own algorithmic flops per leapfrog step (block
