@@ -509,25 +509,26 @@ __global__ __launch_bounds__(256) void k_cr_pair_force(
 // E_f = -2N C - β Σ_q c_q ln|det(H - i y_q)| (block pivots) and
 // Tr ρ_hh = N/2 - Σ_q c_q Re Tr G22 (G22[x,x] = -conj(A[x,x]) of the M-form
 // diagonal G blocks); one block per chain (src/HMC.jl:21-27, Observables.jl:120-145)
-__global__ __launch_bounds__(256) void k_cr_fermion_energy(const double2* __restrict__ pool,
-                                                           int64_t item,
-                                                           const int64_t* __restrict__ doff,
-                                                           const double* __restrict__ ldpart,
-                                                           const double* __restrict__ cpole, int N,
-                                                           int nld, int P, double Cx, double beta,
-                                                           double* __restrict__ Ef,
-                                                           double* __restrict__ Trhh) {
+__global__ __launch_bounds__(1024) void k_cr_fermion_energy(const double2* __restrict__ pool,
+                                                            int64_t item,
+                                                            const int64_t* __restrict__ doff,
+                                                            const double* __restrict__ ldpart,
+                                                            const double* __restrict__ cpole, int N,
+                                                            int nld, int P, double Cx, double beta,
+                                                            double* __restrict__ Ef,
+                                                            double* __restrict__ Trhh) {
   const int c = blockIdx.x;
-  __shared__ double red[2][4];
+  __shared__ double red[2][16];
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  // flattened (pole, entry) loops: every load independent of the others
   double ef = 0.0, tr = 0.0;
-  for (int q = 0; q < P; ++q) {
-    const int bi = c * P + q;
-    double ld = 0.0, t = 0.0;
-    for (int k = threadIdx.x; k < nld; k += blockDim.x) ld += ldpart[(int64_t)bi * nld + k];
-    for (int i = threadIdx.x; i < N; i += blockDim.x) t -= pool[(int64_t)bi * item + doff[i]].x;
-    ef += cpole[q] * ld;
-    tr += cpole[q] * t;
+  for (int e = threadIdx.x; e < P * nld; e += blockDim.x) {
+    const int q = e / nld;
+    ef += cpole[q] * ldpart[(int64_t)(c * P) * nld + e];
+  }
+  for (int e = threadIdx.x; e < P * N; e += blockDim.x) {
+    const int q = e / N, i = e - q * N;
+    tr -= cpole[q] * pool[(int64_t)(c * P + q) * item + doff[i]].x;
   }
   ef = wave_sum(ef);
   tr = wave_sum(tr);
@@ -537,8 +538,13 @@ __global__ __launch_bounds__(256) void k_cr_fermion_energy(const double2* __rest
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    Ef[c] = -2.0 * N * Cx - beta * (red[0][0] + red[0][1] + red[0][2] + red[0][3]);
-    Trhh[c] = 0.5 * N - (red[1][0] + red[1][1] + red[1][2] + red[1][3]);
+    double se = 0.0, st = 0.0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) {
+      se += red[0][k];
+      st += red[1][k];
+    }
+    Ef[c] = -2.0 * N * Cx - beta * se;
+    Trhh[c] = 0.5 * N - st;
   }
 }
 
@@ -636,7 +642,7 @@ void launch_cr_fermion_energy(const CrDims& c, const double2* pool, const int64_
                               const double* ldpart, const double* cpole, double Cx, double beta,
                               double* Ef, double* Trhh, hipStream_t s) {
   const int nc = c.nbatch / c.P;
-  hipLaunchKernelGGL(k_cr_fermion_energy, dim3(nc), dim3(256), 0, s, pool, c.item, doff, ldpart,
+  hipLaunchKernelGGL(k_cr_fermion_energy, dim3(nc), dim3(1024), 0, s, pool, c.item, doff, ldpart,
                      cpole, c.N, c.Ly, c.P, Cx, beta, Ef, Trhh);
 }
 
