@@ -580,13 +580,15 @@ void launch_cr_inv(const CrDims& c, double2* pool, const int* blk, const int* ds
 // split measured fastest on every stage of the L=32 plan (tools/cr_cfg_sweep.sh,
 // profiles/r01_cr_gemm_config_sweep.txt): the stages are short and latency
 // bound, so short serial MFMA chains on many waves win over operand reuse.
-// DWHMC_CR_GEMM=TS:KSPLIT forces another configuration for every stage (A/B).
+// DWHMC_CR_GEMM=TS:KSPLIT forces another configuration for every stage (A/B
+// runs; tests/test_gpu_parity.py runs every compiled variant).
 CrGemmCfg cr_gemm_config(const CrDims& c, int ntasks, int maxt32, int maxt16, int ntmax) {
   (void)ntasks;
   (void)maxt32;
   (void)maxt16;
   (void)ntmax;
-  static const CrGemmCfg forced = [] {
+  // read at every context creation (tests switch it between contexts)
+  const CrGemmCfg forced = [] {
     CrGemmCfg f{0, 1};
     if (const char* e = std::getenv("DWHMC_CR_GEMM")) {
       f.ts = std::atoi(e);

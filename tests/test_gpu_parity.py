@@ -298,3 +298,25 @@ def test_cr_ragged_chains(dwhmc, oracle, Lx, Ly):
     hole_ref = O.measure_observables(cache, p, Delta)["hole_conc"]
     assert abs(2.0 * ctx.hole_trace()[0] / p.N - 1.0 - hole_ref) <= 1e-11
     ctx.close()
+
+
+@pytest.mark.parametrize("cfg", ["16:1", "16:2", "16:4", "32:1", "32:2"])
+@pytest.mark.parametrize("Lx,Ly", [(20, 6), (40, 3), (12, 5)])
+def test_cr_block_product_variants(dwhmc, oracle, monkeypatch, cfg, Lx, Ly):
+    """Every compiled block-product kernel variant (16x16 / 32x32 wave tiles,
+    K split 1/2/4; DWHMC_CR_GEMM, read at context creation) against the eigen
+    oracle, on BP = 64 (Lx = 20), 96 (Lx = 40) and 32 (Lx = 12) blocks.
+    32-wide tiles need BP/2 % 32 == 0 and fall back to 16x16 otherwise."""
+    O = oracle
+    monkeypatch.setenv("DWHMC_CR_GEMM", cfg)
+    p, dis, Delta = make_case(O, Lx, Ly, 8.0, seed=Lx * 7 + Ly)
+    cache, F_ref, Ef_ref = O.evaluate(p, dis, Delta)
+    P_ref, _ = O.pairing_P(cache.U, cache.E_n, p)
+    ctx = device_ctx(dwhmc, p, dis, "cr")
+    ctx.set_pairing(Delta)
+    ctx.factorize()
+    assert np.max(np.abs(ctx.pairing()[0] - P_ref)) <= 1e-11
+    assert np.max(np.abs(ctx.forces()[0] - F_ref)) <= 1e-10 * (1 + np.max(np.abs(F_ref)))
+    Ef = ctx.fermion_energy()[0]
+    assert abs(Ef - Ef_ref) <= 1e-11 * abs(Ef_ref), (Ef, Ef_ref)
+    ctx.close()
