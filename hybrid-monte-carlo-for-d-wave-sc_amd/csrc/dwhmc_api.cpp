@@ -50,6 +50,7 @@ struct CrStage {
   double sg;       // products: sign of the sum
   double flops;    // products: algorithmic fp64 flops per batch item (restricted ranges)
   int maxt32, maxt16, ntmax;
+  int tfirst, ntiles;   // products: range in CrPlan::tiles16 (the stage's (task, tile) pairs)
   dwh::CrGemmCfg cfg;   // products: tile / K-split chosen once per context
 };
 
@@ -57,6 +58,7 @@ struct CrPlan {
   int nblk = 0;
   std::vector<CrStage> stages;
   std::vector<dwh::CrTask> tasks;
+  std::vector<int2> tiles16;                 // per product stage: (task offset, 16 x 16 tile)
   std::vector<int> inv_blk, inv_dst, inv_slot;   // inversion source / destination block, ln|det| slot
   std::vector<int64_t> goff, doff;
   std::vector<int> fill_all, fill_step;      // level-0 blocks written at create / every step
@@ -101,7 +103,7 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol) {
   // per step only their pairing entries change), coarser blocks in place.
   // Returns the blocks that hold the inverses.
   auto add_inv = [&](const std::vector<int>& blocks, int& slot) {
-    CrStage st{0, (int)pl.inv_blk.size(), (int)blocks.size(), 0.0, 0.0, 0, 0, 0, {16, 1}};
+    CrStage st{0, (int)pl.inv_blk.size(), (int)blocks.size(), 0.0, 0.0, 0, 0, 0, 0, 0, {16, 1}};
     std::vector<int> dst;
     for (int b : blocks) {
       const int d = b < 3 * Ly ? nb() : b;
@@ -137,14 +139,18 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol) {
   };
   auto flush = [&](double sg) {
     if (cur_tasks.empty()) return;
-    CrStage st{1, (int)pl.tasks.size(), (int)cur_tasks.size(), sg, 0.0, 0, 0, 0, {16, 1}};
+    CrStage st{1, (int)pl.tasks.size(), (int)cur_tasks.size(), sg, 0.0, 0, 0, 0,
+               (int)pl.tiles16.size(), 0, {16, 1}};
     for (auto& t : cur_tasks) {
+      for (int k = 0; k < dwh::cr_task_tiles(t, 16); ++k)
+        pl.tiles16.push_back(make_int2((int)pl.tasks.size() - st.first, k));
       st.flops += 8.0 * t.nt * BP * (double)(t.r1 - t.r0) * (t.c1 - t.c0);
       st.maxt32 = std::max(st.maxt32, dwh::cr_task_tiles(t, 32));
       st.maxt16 = std::max(st.maxt16, dwh::cr_task_tiles(t, 16));
       st.ntmax = std::max(st.ntmax, t.nt);
       pl.tasks.push_back(t);
     }
+    st.ntiles = (int)pl.tiles16.size() - st.tfirst;
     pl.stages.push_back(st);
     cur_tasks.clear();
   };
@@ -385,6 +391,7 @@ struct dwh_ctx {
   CrPlan plan;
   double2* bpool = nullptr;   // CR block pool (nbatch x nblk blocks)
   dwh::CrTask* d_tasks = nullptr;
+  int2* d_tiles16 = nullptr;
   int *d_inv_blk = nullptr, *d_inv_dst = nullptr, *d_inv_slot = nullptr;
   int64_t *d_goff = nullptr, *d_doff = nullptr, *d_off_ph = nullptr;
   int *d_fill_all = nullptr, *d_fill_step = nullptr;
@@ -566,8 +573,8 @@ void cr_enqueue(dwh_ctx* ctx) {
                          ctx->d_inv_slot + st.first, st.n, ctx->ldpart, ctx->stream);
     } else {
       Scope s(ctx, T_CR_GEMM, st.flops * c.nbatch);
-      dwh::launch_cr_gemm(c, ctx->bpool, ctx->d_tasks + st.first, st.n, st.maxt32, st.maxt16, st.cfg,
-                          st.sg, ctx->stream);
+      dwh::launch_cr_gemm(c, ctx->bpool, ctx->d_tasks + st.first, st.n, st.maxt32, st.maxt16,
+                          ctx->d_tiles16 + st.tfirst, st.ntiles, st.cfg, st.sg, ctx->stream);
     }
   }
 }
@@ -898,6 +905,7 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     const CrPlan& pl = ctx->plan;
     ALLOC(bpool, (size_t)d.nbatch * ctx->cr.item);
     ALLOC(d_tasks, pl.tasks.size());
+    ALLOC(d_tiles16, pl.tiles16.size());
     ALLOC(d_inv_blk, pl.inv_blk.size());
     ALLOC(d_inv_dst, pl.inv_dst.size());
     ALLOC(d_inv_slot, pl.inv_slot.size());
@@ -959,6 +967,7 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
   if (ctx->algo == ALGO_CR) {
     const CrPlan& pl = ctx->plan;
     UP(d_tasks, pl.tasks.data(), pl.tasks.size());
+    UP(d_tiles16, pl.tiles16.data(), pl.tiles16.size());
     UP(d_inv_blk, pl.inv_blk.data(), pl.inv_blk.size());
     UP(d_inv_dst, pl.inv_dst.data(), pl.inv_dst.size());
     UP(d_inv_slot, pl.inv_slot.data(), pl.inv_slot.size());

@@ -382,17 +382,28 @@ __device__ __forceinline__ void cr_tile_part(const double2* base, const CrTask* 
 template <int BP, int MI, int KSPLIT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_cr_gemm(double2* __restrict__ pool, int64_t item,
                                                  const CrTask* __restrict__ tasks, int ntasks,
-                                                 int maxt, int total, double sg) {
+                                                 int maxt, const int2* __restrict__ tlist, int ntl,
+                                                 int total, double sg) {
   constexpr int TS = 16 * MI, TPW = 4 / KSPLIT, HP = BP / 2, NV = MI * MI * 4;
   constexpr int64_t BB = (int64_t)HP * BP;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
   const int kq = w % KSPLIT;
   const int gt = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x) * TPW + w / KSPLIT);
-  const int per_item = ntasks * maxt;
+  // 16 x 16 tiles: compact (task, tile) list of the stage (no idle waves for
+  // restricted tasks); 32 x 32 tiles: ntasks x maxt slots
+  const int per_item = tlist ? ntl : ntasks * maxt;
   const int bi = gt / per_item;
   const int rmd = gt - bi * per_item;
-  const int tsk = rmd / maxt, tile = rmd - tsk * maxt;
   bool valid = gt < total;
+  int tsk, tile;
+  if (tlist) {
+    const int2 e = tlist[valid ? rmd : 0];
+    tsk = e.x;
+    tile = e.y;
+  } else {
+    tsk = rmd / maxt;
+    tile = rmd - tsk * maxt;
+  }
   const CrTask* tk = tasks + (valid ? tsk : 0);
   const int tr0 = tk->r0 / TS, tc0 = tk->c0 / TS;
   const int ct = (tk->c1 + TS - 1) / TS - tc0;
@@ -604,14 +615,17 @@ CrGemmCfg cr_gemm_config(const CrDims& c, int ntasks, int maxt32, int maxt16, in
 }
 
 void launch_cr_gemm(const CrDims& c, double2* pool, const CrTask* tasks, int ntasks, int maxt32,
-                    int maxt16, const CrGemmCfg& cfg, double sg, hipStream_t s) {
+                    int maxt16, const int2* tl16, int ntl16, const CrGemmCfg& cfg, double sg,
+                    hipStream_t s) {
   if (ntasks <= 0) return;
   const int maxt = cfg.ts == 32 ? maxt32 : maxt16;
-  const int total = c.nbatch * ntasks * maxt;
+  const int2* tl = cfg.ts == 32 ? nullptr : tl16;
+  const int total = c.nbatch * (tl ? ntl16 : ntasks * maxt);
   const int tpw = 4 / cfg.ksplit;
   const dim3 g((total + tpw - 1) / tpw), b(256);
 #define CR_GEMM(BPV, MIV, KSV) \
-  hipLaunchKernelGGL((k_cr_gemm<BPV, MIV, KSV>), g, b, 0, s, pool, c.item, tasks, ntasks, maxt, total, sg)
+  hipLaunchKernelGGL((k_cr_gemm<BPV, MIV, KSV>), g, b, 0, s, pool, c.item, tasks, ntasks, maxt, tl, ntl16, \
+                     total, sg)
 #define CR_GEMM_BP(BPV)                        \
   if (cfg.ts == 16) {                          \
     if (cfg.ksplit == 4) CR_GEMM(BPV, 1, 4);   \

@@ -76,8 +76,10 @@ struct CrGemmCfg {
 // maxt32 / maxt16: the largest cr_task_tiles over the stage's tasks at ts = 32 / 16;
 // ntmax: the largest term count
 CrGemmCfg cr_gemm_config(const CrDims& c, int ntasks, int maxt32, int maxt16, int ntmax);
+// tl16: the stage's (task, tile) list at 16 x 16 tiles (ntl16 entries per batch item)
 void launch_cr_gemm(const CrDims& c, double2* pool, const CrTask* tasks, int ntasks, int maxt32,
-                    int maxt16, const CrGemmCfg& cfg, double sg, hipStream_t s);
+                    int maxt16, const int2* tl16, int ntl16, const CrGemmCfg& cfg, double sg,
+                    hipStream_t s);
 
 // dense h - i y_q (padded with identity) for every (chain, pole): R init input
 void launch_fill_hz(const Dims& d, double2* M, const int* hcol, const double* hval,
