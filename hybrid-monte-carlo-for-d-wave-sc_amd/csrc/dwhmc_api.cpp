@@ -395,6 +395,10 @@ struct dwh_ctx {
   int *d_inv_blk = nullptr, *d_inv_dst = nullptr, *d_inv_slot = nullptr;
   int64_t *d_goff = nullptr, *d_doff = nullptr, *d_off_ph = nullptr;
   int *d_fill_all = nullptr, *d_fill_step = nullptr;
+  // the pool's level-0 pairing entries already hold the current Δ (set by a
+  // drifting k_cr_pair_force, consumed by the next factorisation); every
+  // other path that changes Δ leaves it false
+  bool pairing_in_pool = false;
 
   // timing
   int timing = 0;   // bitmask over TimerName (bit i = kTimerNames[i])
@@ -559,12 +563,18 @@ void cr_enqueue(dwh_ctx* ctx) {
     // algorithmic bytes: rewritten level-0 blocks (top halves, none with the
     // out-of-place level-0 inversions) + the pairing entries Δ/2 scattered
     // into the level-0 blocks of every batch item (16 B each)
+    // inside a trajectory the previous step's force kernel already scattered
+    // the drifted Δ into the pool (pairing_in_pool)
     const CrPlan& pl = ctx->plan;
-    Scope s(ctx, T_ASSEMBLE,
-            (double)pl.fill_step.size() * 8.0 * c.BP * (double)c.BP * c.nbatch +
-                16.0 * (double)pl.n_ph * c.nbatch);
-    dwh::launch_cr_fill(c, ctx->bpool, ctx->d_fill_step, (int)pl.fill_step.size(), ctx->hcol, ctx->hval,
-                        ctx->Dcol, ctx->Dsrc, ctx->Delta, ctx->d_y, ctx->d_off_ph, ctx->stream);
+    if (!ctx->pairing_in_pool) {
+      Scope s(ctx, T_ASSEMBLE,
+              (double)pl.fill_step.size() * 8.0 * c.BP * (double)c.BP * c.nbatch +
+                  16.0 * (double)pl.n_ph * c.nbatch);
+      dwh::launch_cr_fill(c, ctx->bpool, ctx->d_fill_step, (int)pl.fill_step.size(), ctx->hcol,
+                          ctx->hval, ctx->Dcol, ctx->Dsrc, ctx->Delta, ctx->d_y, ctx->d_off_ph,
+                          ctx->stream);
+    }
+    ctx->pairing_in_pool = false;
   }
   for (const CrStage& st : ctx->plan.stages) {
     if (st.kind == 0) {
@@ -589,7 +599,10 @@ void factorize_enqueue(dwh_ctx* ctx, const dwh::KickDrift& kd) {
   Scope step(ctx, T_STEP, (double)d.nbatch * 8.0 * (double)d.N * d.N * d.N);
   if (ctx->algo == ALGO_CR) {
     cr_enqueue(ctx);
-    dwh::launch_cr_pair_force(ctx->cr, ctx->bpool, ctx->d_goff, ctx->bond_ij, ctx->bond_ji, ctx->d_c,
+    // the kernel scatters the drifted Δ into the pool only when it drifts
+    ctx->pairing_in_pool = kd.drift != 0.0;
+    dwh::launch_cr_pair_force(ctx->cr, ctx->bpool, ctx->d_goff, ctx->d_off_ph, ctx->Dsrc, ctx->bond_ij,
+                              ctx->bond_ji, ctx->d_c,
                               ctx->Delta, ctx->Pair, ctx->F, ctx->Pi, kd, ctx->beta, ctx->J,
                               ctx->stream);
     return;

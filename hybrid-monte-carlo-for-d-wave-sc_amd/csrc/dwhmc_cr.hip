@@ -483,11 +483,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 // kick and the next step's drift (kick_drift).
 // ---------------------------------------------------------------------------
 // 32 lanes per bond, one pole per lane (the G entries of the poles live in
-// different batch items: independent loads), shuffle reduction.
+// different batch items: independent loads), shuffle reduction.  With a
+// drift (inside a trajectory) the drifted Δ/2 is scattered straight into the
+// level-0 pairing entries of every pole (off_ph), so the next factorisation
+// needs no k_cr_fill launch.
 __global__ __launch_bounds__(256) void k_cr_pair_force(
-    const double2* __restrict__ pool, int64_t item, const int64_t* __restrict__ goff,
-    const int* __restrict__ bond_ij, const int* __restrict__ bond_ji, const double* __restrict__ cpole,
-    int N, int P, double2* __restrict__ Delta, double2* __restrict__ Pair, double2* __restrict__ F,
+    double2* __restrict__ pool, int64_t item, const int64_t* __restrict__ goff,
+    const int64_t* __restrict__ off_ph, const int* __restrict__ Dsrc, const int* __restrict__ bond_ij,
+    const int* __restrict__ bond_ji, const double* __restrict__ cpole, int N, int P,
+    double2* __restrict__ Delta, double2* __restrict__ Pair, double2* __restrict__ F,
     double2* __restrict__ Pi, double kick, double drift, double cap2, int* __restrict__ flag,
     double beta, double J) {
   const int b = blockIdx.x * 8 + (threadIdx.x >> 5), sub = threadIdx.x & 31;
@@ -507,14 +511,31 @@ __global__ __launch_bounds__(256) void k_cr_pair_force(
     Pv.x += __shfl_xor(Pv.x, off, 32);
     Pv.y += __shfl_xor(Pv.y, off, 32);
   }
-  if (sub != 0) return;
   const int64_t o = (int64_t)c * 2 * N + b;
-  Pair[o] = Pv;
-  const double2 d = Delta[o];
-  const double f = -beta / (2.0 * J);
-  const double2 Fv = make_double2(f * (d.x - J * Pv.x), f * (d.y - J * Pv.y));
-  F[o] = Fv;
-  kick_drift(Fv, o, Delta, Pi, kick, drift, cap2, flag);
+  double2 dn = make_double2(0.0, 0.0);
+  if (sub == 0) {
+    Pair[o] = Pv;
+    const double2 d = Delta[o];
+    const double f = -beta / (2.0 * J);
+    const double2 Fv = make_double2(f * (d.x - J * Pv.x), f * (d.y - J * Pv.y));
+    F[o] = Fv;
+    kick_drift(Fv, o, Delta, Pi, kick, drift, cap2, flag);
+    if (drift != 0.0) dn = Delta[o];
+  }
+  if (drift != 0.0 && off_ph != nullptr) {
+    dn.x = 0.5 * __shfl(dn.x, 0, 32);
+    dn.y = 0.5 * __shfl(dn.y, 0, 32);
+    // an entry is written only by the bond k_cr_fill takes its value from
+    // (small lattices map several bonds onto one entry: Dsrc picks the one
+    // the reference's overwrite order leaves, src/Hamiltonian.jl:68-83)
+    const int e1 = bond_ij[b], e2 = bond_ji[b];
+    const int64_t p1 = Dsrc[e1] == b ? off_ph[e1] : -1, p2 = Dsrc[e2] == b ? off_ph[e2] : -1;
+    for (int q = sub; q < P; q += 32) {
+      double2* G = pool + (int64_t)(c * P + q) * item;
+      if (p1 >= 0) G[p1] = dn;
+      if (p2 >= 0) G[p2] = dn;
+    }
+  }
 }
 
 // E_f = -2N C - β Σ_q c_q ln|det(H - i y_q)| (block pivots) and
@@ -644,14 +665,14 @@ void launch_cr_gemm(const CrDims& c, double2* pool, const CrTask* tasks, int nta
 #undef CR_GEMM
 }
 
-void launch_cr_pair_force(const CrDims& c, const double2* pool, const int64_t* goff,
-                          const int* bond_ij, const int* bond_ji, const double* cpole,
+void launch_cr_pair_force(const CrDims& c, double2* pool, const int64_t* goff, const int64_t* off_ph,
+                          const int* Dsrc, const int* bond_ij, const int* bond_ji, const double* cpole,
                           double2* Delta, double2* Pair, double2* F, double2* Pi,
                           const KickDrift& kd, double beta, double J, hipStream_t s) {
   const int nc = c.nbatch / c.P;
   hipLaunchKernelGGL(k_cr_pair_force, dim3((2 * c.N + 7) / 8, nc), dim3(256), 0, s, pool, c.item,
-                     goff, bond_ij, bond_ji, cpole, c.N, c.P, Delta, Pair, F, Pi, kd.kick, kd.drift,
-                     kd.cap * kd.cap, kd.flag, beta, J);
+                     goff, off_ph, Dsrc, bond_ij, bond_ji, cpole, c.N, c.P, Delta, Pair, F, Pi, kd.kick,
+                     kd.drift, kd.cap * kd.cap, kd.flag, beta, J);
 }
 
 void launch_cr_fermion_energy(const CrDims& c, const double2* pool, const int64_t* doff,

@@ -155,12 +155,14 @@ def _oracle_after_sweeps(O, p, dis, Delta0, draws, Nt, dt, factorize_first=True)
     return out
 
 
-@pytest.mark.parametrize("factorize_first", [True, False])
-def test_hmc_sweep_matches_oracle(dwhmc, oracle, factorize_first, algo):
+@pytest.mark.parametrize("factorize_first,Lx,Ly", [(True, 6, 6), (False, 6, 6), (True, 2, 4), (True, 3, 2)])
+def test_hmc_sweep_matches_oracle(dwhmc, oracle, factorize_first, Lx, Ly, algo):
     """hmc_sweep! (src/HMC.jl:71-144) with injected draws; factorize_first=False
-    reproduces the zeroed-cache first sweep of scripts/benchmark_clean.jl:82-88."""
+    reproduces the zeroed-cache first sweep of scripts/benchmark_clean.jl:82-88.
+    The 2x4 and 3x2 lattices map several bonds onto one pairing entry (the
+    reference's overwrite order, src/Hamiltonian.jl:68-83) inside trajectories."""
     O = oracle
-    p, dis, Delta0 = make_case(O, 6, 6, 8.0, seed=77, amp=0.1)
+    p, dis, Delta0 = make_case(O, Lx, Ly, 8.0, seed=77 + Lx, amp=0.1)
     Nt = 6
     dt = O.calc_optimal_dt(p.beta, p.J, p.mass, Nt)
     rng = np.random.default_rng(5)
