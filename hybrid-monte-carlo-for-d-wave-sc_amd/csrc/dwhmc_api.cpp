@@ -392,6 +392,8 @@ struct dwh_ctx {
   double2* bpool = nullptr;   // CR block pool (nbatch x nblk blocks)
   dwh::CrTask* d_tasks = nullptr;
   int2* d_tiles16 = nullptr;
+  double* efpart = nullptr;     // per (chain, pole) E_f / Tr G22 partials
+  unsigned* efdone = nullptr;   // per chain: pole blocks done (k_cr_fermion_energy)
   int *d_inv_blk = nullptr, *d_inv_dst = nullptr, *d_inv_slot = nullptr;
   int64_t *d_goff = nullptr, *d_doff = nullptr, *d_off_ph = nullptr;
   int *d_fill_all = nullptr, *d_fill_step = nullptr;
@@ -627,7 +629,7 @@ void factorize_enqueue(dwh_ctx* ctx, const dwh::KickDrift& kd) {
 void fermion_energy_enqueue(dwh_ctx* ctx) {
   if (ctx->algo == ALGO_CR)
     dwh::launch_cr_fermion_energy(ctx->cr, ctx->bpool, ctx->d_doff, ctx->ldpart, ctx->d_c, ctx->Cx,
-                                  ctx->beta, ctx->Ef, ctx->Trhh, ctx->stream);
+                                  ctx->beta, ctx->efpart, ctx->efdone, ctx->Ef, ctx->Trhh, ctx->stream);
   else
     dwh::launch_fermion_energy(ctx->d, ctx->ldstatic, ctx->ldpart, ctx->diagS, ctx->d_c, ctx->Cx,
                                ctx->beta, ctx->Ef, ctx->Trhh, ctx->stream);
@@ -919,6 +921,8 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     ALLOC(bpool, (size_t)d.nbatch * ctx->cr.item);
     ALLOC(d_tasks, pl.tasks.size());
     ALLOC(d_tiles16, pl.tiles16.size());
+    ALLOC(efpart, 2 * (size_t)d.nbatch);
+    ALLOC(efdone, (size_t)d.nc);
     ALLOC(d_inv_blk, pl.inv_blk.size());
     ALLOC(d_inv_dst, pl.inv_dst.size());
     ALLOC(d_inv_slot, pl.inv_slot.size());
@@ -993,6 +997,7 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
 #undef UP
   // zeroed cache, like initialize_cache (src/Types.jl:182-212): P = 0, E_f = 0
   (void)hipMemsetAsync(ctx->Delta, 0, nbond * sizeof(double2), s);
+  if (ctx->efdone) (void)hipMemsetAsync(ctx->efdone, 0, (size_t)d.nc * sizeof(unsigned), s);
   (void)hipMemsetAsync(ctx->Pi, 0, nbond * sizeof(double2), s);
   (void)hipMemsetAsync(ctx->Pair, 0, nbond * sizeof(double2), s);
   (void)hipMemsetAsync(ctx->F, 0, nbond * sizeof(double2), s);

@@ -541,43 +541,51 @@ __global__ __launch_bounds__(256) void k_cr_pair_force(
 // E_f = -2N C - β Σ_q c_q ln|det(H - i y_q)| (block pivots) and
 // Tr ρ_hh = N/2 - Σ_q c_q Re Tr G22 (G22[x,x] = -conj(A[x,x]) of the M-form
 // diagonal G blocks); one block per chain (src/HMC.jl:21-27, Observables.jl:120-145)
-__global__ __launch_bounds__(1024) void k_cr_fermion_energy(const double2* __restrict__ pool,
-                                                            int64_t item,
-                                                            const int64_t* __restrict__ doff,
-                                                            const double* __restrict__ ldpart,
-                                                            const double* __restrict__ cpole, int N,
-                                                            int nld, int P, double Cx, double beta,
-                                                            double* __restrict__ Ef,
-                                                            double* __restrict__ Trhh) {
-  const int c = blockIdx.x;
-  __shared__ double red[2][16];
+__global__ __launch_bounds__(256) void k_cr_fermion_energy(const double2* __restrict__ pool,
+                                                           int64_t item,
+                                                           const int64_t* __restrict__ doff,
+                                                           const double* __restrict__ ldpart,
+                                                           const double* __restrict__ cpole, int N,
+                                                           int nld, int P, double Cx, double beta,
+                                                           double* __restrict__ part,
+                                                           double* __restrict__ Ef,
+                                                           double* __restrict__ Trhh,
+                                                           unsigned* __restrict__ done) {
+  // one block per (pole, chain): its weighted Σ ln|pivots| and Re Tr G22
+  const int q = blockIdx.x, c = blockIdx.y, bi = c * P + q;
+  __shared__ double red[2][4];
+  __shared__ bool last;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-  // flattened (pole, entry) loops: every load independent of the others
-  double ef = 0.0, tr = 0.0;
-  for (int e = threadIdx.x; e < P * nld; e += blockDim.x) {
-    const int q = e / nld;
-    ef += cpole[q] * ldpart[(int64_t)(c * P) * nld + e];
-  }
-  for (int e = threadIdx.x; e < P * N; e += blockDim.x) {
-    const int q = e / N, i = e - q * N;
-    tr -= cpole[q] * pool[(int64_t)(c * P + q) * item + doff[i]].x;
-  }
-  ef = wave_sum(ef);
-  tr = wave_sum(tr);
+  double ld = 0.0, t = 0.0;
+  for (int k = threadIdx.x; k < nld; k += blockDim.x) ld += ldpart[(int64_t)bi * nld + k];
+  for (int i = threadIdx.x; i < N; i += blockDim.x) t -= pool[(int64_t)bi * item + doff[i]].x;
+  ld = wave_sum(ld);
+  t = wave_sum(t);
   if (l == 0) {
-    red[0][w] = ef;
-    red[1][w] = tr;
+    red[0][w] = ld;
+    red[1][w] = t;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    double se = 0.0, st = 0.0;
-    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) {
-      se += red[0][k];
-      st += red[1][k];
-    }
-    Ef[c] = -2.0 * N * Cx - beta * se;
-    Trhh[c] = 0.5 * N - st;
+    part[2 * bi] = cpole[q] * (red[0][0] + red[0][1] + red[0][2] + red[0][3]);
+    part[2 * bi + 1] = cpole[q] * (red[1][0] + red[1][1] + red[1][2] + red[1][3]);
+    // the last block of this chain sums the pole partials in pole order
+    // (deterministic); release / acquire through the counter at agent scope
+    __atomic_thread_fence(__ATOMIC_RELEASE);
+    const unsigned n = __hip_atomic_fetch_add(&done[c], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    last = (n == (unsigned)P - 1);
   }
+  __syncthreads();
+  if (!last || threadIdx.x != 0) return;
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);
+  double ef = 0.0, tr = 0.0;
+  for (int k = 0; k < P; ++k) {
+    ef += __hip_atomic_load(&part[2 * (c * P + k)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    tr += __hip_atomic_load(&part[2 * (c * P + k) + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  Ef[c] = -2.0 * N * Cx - beta * ef;
+  Trhh[c] = 0.5 * N - tr;
+  done[c] = 0;   // ready for the next launch (stream order)
 }
 
 // ---------------------------------------------------------------------------
@@ -677,10 +685,10 @@ void launch_cr_pair_force(const CrDims& c, double2* pool, const int64_t* goff, c
 
 void launch_cr_fermion_energy(const CrDims& c, const double2* pool, const int64_t* doff,
                               const double* ldpart, const double* cpole, double Cx, double beta,
-                              double* Ef, double* Trhh, hipStream_t s) {
+                              double* part, unsigned* done, double* Ef, double* Trhh, hipStream_t s) {
   const int nc = c.nbatch / c.P;
-  hipLaunchKernelGGL(k_cr_fermion_energy, dim3(nc), dim3(1024), 0, s, pool, c.item, doff, ldpart,
-                     cpole, c.N, c.Ly, c.P, Cx, beta, Ef, Trhh);
+  hipLaunchKernelGGL(k_cr_fermion_energy, dim3(c.P, nc), dim3(256), 0, s, pool, c.item, doff, ldpart,
+                     cpole, c.N, c.Ly, c.P, Cx, beta, part, Ef, Trhh, done);
 }
 
 }  // namespace dwh

@@ -64,9 +64,11 @@ void launch_cr_pair_force(const CrDims& c, double2* pool, const int64_t* goff, c
                           double2* Delta, double2* Pair, double2* F, double2* Pi,
                           const KickDrift& kd, double beta, double J, hipStream_t s);
 // E_f and Tr ρ_hh from the CR block pivots and the G22 diagonal (pool offsets doff)
+// part: 2 x nbatch scratch, done: nchains counters (zero at creation; the
+// kernel leaves them zero)
 void launch_cr_fermion_energy(const CrDims& c, const double2* pool, const int64_t* doff,
                               const double* ldpart, const double* cpole, double Cx, double beta,
-                              double* Ef, double* Trhh, hipStream_t s);
+                              double* part, unsigned* done, double* Ef, double* Trhh, hipStream_t s);
 // inverts blocks blk[i] into dst[i] (dst == blk: in place); ln|det| into ldpart slots
 void launch_cr_inv(const CrDims& c, double2* pool, const int* blk, const int* dst, const int* slot,
                    int n, double* ldpart, hipStream_t s);
