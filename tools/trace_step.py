@@ -12,7 +12,7 @@ import csv
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
-    ap.add_argument("--marker", default="k_cr_fill")
+    ap.add_argument("--marker", default="k_cr_pair_force", help="a kernel launched once per leapfrog step")
     ap.add_argument("--which", type=int, default=-2, help="which marker occurrence starts the step")
     ap.add_argument("--quiet", action="store_true")
     a = ap.parse_args()
