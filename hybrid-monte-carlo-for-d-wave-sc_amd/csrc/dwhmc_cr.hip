@@ -61,9 +61,10 @@ __device__ unsigned long long g_cr_stamps[1024][16];
 // Ly == 2: the single off-diagonal block lives in U (L = 0); Ly == 1:
 // everything in D.  Padded sites (Lx <= x < HP) are 1 on the diagonal of D
 // (hole -1 implied by the M-form), zero elsewhere.  All blocks are written
-// once at context creation; per factorisation only the blocks CR overwrites
-// (the level-0 eliminated D blocks) are rewritten and k_cr_pair_scatter
-// refreshes the pairing entries of the others.
+// once at context creation and CR never overwrites them (level-0 inverses go
+// to other blocks), so a factorisation only scatters the pairing entries Δ/2
+// (the trailing blocks of this launch) — and inside a trajectory not even
+// that: k_cr_pair_force scatters the drifted Δ itself.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ double2 half_delta(const double2* __restrict__ Delta, const int* __restrict__ Dsrc,
                                               int N, int c, int i, int s) {
