@@ -177,6 +177,26 @@ __device__ __forceinline__ void mma16_3m(d4& cr, d4& ci, const double2* A, const
   ci = t3 - t1 - t2;
 }
 
+// acc(16x16, C layout) += (NEG ? -1 : 1) * X^T * A^T: X given in the C layout
+// (its register rr is the A-operand fragment of k-step rr of X^T), A a 16 x 16
+// row-major LDS tile (stride 17) read transposed as the B operand.  Used for
+// a tile kept transposed: (T - A X)^T = T^T - X^T A^T.
+template <bool NEG>
+__device__ __forceinline__ void mma16_3m_T(d4& cr, d4& ci, const double2* A, const d4& xr, const d4& xi) {
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  d4 t1 = cr, t2 = {0.0, 0.0, 0.0, 0.0}, t3 = cr + ci;
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const double2 bv = A[lr * 17 + 4 * ks + lk];
+    const double a_r = NEG ? -xr[ks] : xr[ks], a_i = NEG ? -xi[ks] : xi[ks];
+    t1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a_r, bv.x, t1, 0, 0, 0);
+    t2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a_i, bv.y, t2, 0, 0, 0);
+    t3 = __builtin_amdgcn_mfma_f64_16x16x4f64(a_r + a_i, bv.x + bv.y, t3, 0, 0, 0);
+  }
+  cr = t1 - t2;
+  ci = t3 - t1 - t2;
+}
+
 template <int NT>
 __global__ __launch_bounds__(64 * NT) void k_cr_inv(double2* __restrict__ pool, int64_t item,
                                                     const int* __restrict__ blk,
@@ -185,7 +205,6 @@ __global__ __launch_bounds__(64 * NT) void k_cr_inv(double2* __restrict__ pool, 
                                                     double* __restrict__ ldpart, int nslots) {
   constexpr int BP = 16 * NT, HP = BP / 2, TSZ = 16 * 17;
   __shared__ double2 pan[2][NT][TSZ];
-  __shared__ double2 scr[NT][TSZ];
   __shared__ double ldw[NT];
   const int bi = blockIdx.y, li = blockIdx.x;
   const double2* M = pool + (int64_t)bi * item + (int64_t)blk[li] * HP * BP;
@@ -193,6 +212,12 @@ __global__ __launch_bounds__(64 * NT) void k_cr_inv(double2* __restrict__ pool, 
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
   d4 ar[NT], ai[NT];
   CR_STAMP(0);
+  // Tiles in the MFMA C layout (lane: rows lk + 4 rr, column lr), except the
+  // diagonal tile (w, w), which is kept TRANSPOSED until it becomes this
+  // wave's pivot: its C layout is then the strided inversion layout (lane:
+  // row lr, columns lk + 4 rr), so the pivot is inverted in registers with no
+  // LDS transpose, and its updates A_ww -= A_wk X_w run as
+  // A_ww^T -= X_w^T A_wk^T (mma16_3m_T: X from registers, A_wk^T from LDS).
 #pragma unroll
   for (int I = 0; I < NT; ++I)
 #pragma unroll
@@ -208,65 +233,92 @@ __global__ __launch_bounds__(64 * NT) void k_cr_inv(double2* __restrict__ pool, 
       ar[I][rr] = v.x;
       ai[I][rr] = v.y;
     }
-  CR_STAMP(1);
-  double ld = 0.0;
-  double2* S = scr[w];
-  // in-place inverse of a C-layout tile: transpose to the wave_inv16_dpp layout
-  // (lane: row l & 15, columns 4 (l >> 4) ..) through this wave's scratch
-  auto invert = [&](d4& tr, d4& ti) {
+  {   // transpose the diagonal tile once, through this wave's slot of panel 1
+    // (first written by the step-1 publisher, after the step-0 barrier)
+    double2* S = pan[1][w];
+    d4 dr = ar[0], di = ai[0];
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) S[(lk + 4 * rr) * 17 + lr] = make_double2(tr[rr], ti[rr]);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    double2 dv[4];
+    for (int I = 1; I < NT; ++I)
+      if (I == w) {
+        dr = ar[I];
+        di = ai[I];
+      }
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) dv[jj] = S[(l & 15) * 17 + (l >> 4) * 4 + jj];
-    ld += 0.5 * log(wave_inv16_dpp(dv));
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) S[(l & 15) * 17 + (l >> 4) * 4 + jj] = dv[jj];
+    for (int rr = 0; rr < 4; ++rr) S[(lk + 4 * rr) * 17 + lr] = make_double2(dr[rr], di[rr]);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
-      const double2 v = S[(lk + 4 * rr) * 17 + lr];
-      tr[rr] = v.x;
-      ti[rr] = v.y;
+      const double2 v = S[lr * 17 + lk + 4 * rr];
+      dr[rr] = v.x;
+      di[rr] = v.y;
     }
+#pragma unroll
+    for (int I = 0; I < NT; ++I)
+      if (I == w) {
+        ar[I] = dr;
+        ai[I] = di;
+      }
+  }
+  CR_STAMP(1);
+  double ld = 0.0;
+  // in-place inverse of the (transposed-stored) diagonal tile
+  auto invert = [&](d4& tr, d4& ti) -> double {
+    double2 dv[4];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) dv[jj] = make_double2(tr[jj], ti[jj]);
+    const double r = 0.5 * log(wave_inv16_dpp<true>(dv));
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      tr[jj] = dv[jj].x;
+      ti[jj] = dv[jj].y;
+    }
+    return r;
   };
-  if (w == 0) invert(ar[0], ai[0]);
+  if (w == 0) ld += invert(ar[0], ai[0]);
   CR_STAMP(2);
 #pragma unroll 1
   for (int kb = 0; kb < NT; ++kb) {
     double2(*P)[TSZ] = pan[kb & 1];
-    if (w == kb) {
+    if (w == kb) {   // publish column kb; tile kb holds P^-1 in the strided layout
 #pragma unroll
       for (int I = 0; I < NT; ++I)
 #pragma unroll
-        for (int rr = 0; rr < 4; ++rr) P[I][(lk + 4 * rr) * 17 + lr] = make_double2(ar[I][rr], ai[I][rr]);
+        for (int rr = 0; rr < 4; ++rr) {
+          const int o = (I == kb) ? lr * 17 + lk + 4 * rr : (lk + 4 * rr) * 17 + lr;
+          P[I][o] = make_double2(ar[I][rr], ai[I][rr]);
+        }
     }
     __syncthreads();
-    // this wave's tile kb (wave kb: P^-1; others: A_kJ)
-    d4 br = ar[0], bim = ai[0];
-#pragma unroll
-    for (int I = 1; I < NT; ++I)
-      if (I == kb) {
-        br = ar[I];
-        bim = ai[I];
-      }
     if (w == kb) {
+      d4 br, bim;   // P^-1 in the C layout, read back from the panel
 #pragma unroll
-      for (int I = 0; I < NT; ++I)
+      for (int rr = 0; rr < 4; ++rr) {
+        const double2 v = P[kb][(lk + 4 * rr) * 17 + lr];
+        br[rr] = v.x;
+        bim[rr] = v.y;
+      }
+#pragma unroll
+      for (int I = 0; I < NT; ++I) {
         if (I != kb) {
           ar[I] = d4{0.0, 0.0, 0.0, 0.0};
           ai[I] = d4{0.0, 0.0, 0.0, 0.0};
           mma16_3m<true>(ar[I], ai[I], P[I], br, bim);
+        } else {
+          ar[I] = br;
+          ai[I] = bim;
         }
+      }
     } else {
+      // this wave's tile kb (off-diagonal: C layout)
+      d4 br = ar[0], bim = ai[0];
+#pragma unroll
+      for (int I = 1; I < NT; ++I)
+        if (I == kb) {
+          br = ar[I];
+          bim = ai[I];
+        }
       d4 xr = {0.0, 0.0, 0.0, 0.0}, xi = {0.0, 0.0, 0.0, 0.0};
       mma16_3m<false>(xr, xi, P[kb], br, bim);
       const bool look = (w == kb + 1);
@@ -276,14 +328,17 @@ __global__ __launch_bounds__(64 * NT) void k_cr_inv(double2* __restrict__ pool, 
           ar[I] = xr;
           ai[I] = xi;
         }
-        if (look && I == kb + 1) {
-          mma16_3m<true>(ar[I], ai[I], P[I], xr, xi);
-          invert(ar[I], ai[I]);
+        if (look && I == kb + 1) {   // next pivot first: update (transposed) and invert
+          mma16_3m_T<true>(ar[I], ai[I], P[I], xr, xi);
+          ld += invert(ar[I], ai[I]);
         }
       }
 #pragma unroll
       for (int I = 0; I < NT; ++I)
-        if (I != kb && !(look && I == kb + 1)) mma16_3m<true>(ar[I], ai[I], P[I], xr, xi);
+        if (I != kb && !(look && I == kb + 1)) {
+          if (I == w && kb < w) mma16_3m_T<true>(ar[I], ai[I], P[I], xr, xi);   // still transposed
+          else mma16_3m<true>(ar[I], ai[I], P[I], xr, xi);
+        }
     }
     if (kb == 0) CR_STAMP(3);
   }

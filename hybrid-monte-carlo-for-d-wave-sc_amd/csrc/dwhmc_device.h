@@ -170,9 +170,12 @@ __device__ __forceinline__ double readlane_f64(double x, int lane) {
   return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
 }
 
-template <int P>
+// STRIDED: lane l holds columns q, q + 4, q + 8, q + 12 (q = l >> 4) instead
+// of 4q .. 4q + 3 — the MFMA C layout of the transposed tile, so a tile kept
+// transposed in MFMA registers is inverted in place without an LDS transpose.
+template <int P, bool STRIDED = false>
 __device__ __forceinline__ void inv16_step(double2 (&a)[4], double& pprod) {
-  constexpr int PS = P >> 2, PE = P & 3;
+  constexpr int PS = STRIDED ? (P & 3) : (P >> 2), PE = STRIDED ? (P >> 2) : (P & 3);
   const int l = threadIdx.x & 63, r = l & 15, q = l >> 4;
   double2 rowp[4];
 #pragma unroll
@@ -200,16 +203,17 @@ __device__ __forceinline__ void inv16_step(double2 (&a)[4], double& pprod) {
   if (q == PS) a[PE] = prow ? inv : make_double2(-fi.x, -fi.y);
 }
 
-template <int... Ps>
+template <bool STRIDED, int... Ps>
 __device__ __forceinline__ void inv16_all(double2 (&a)[4], double& pprod,
                                           std::integer_sequence<int, Ps...>) {
-  (inv16_step<Ps>(a, pprod), ...);
+  (inv16_step<Ps, STRIDED>(a, pprod), ...);
 }
 
 // returns Π |pivot|^2 of the 16 pivots
+template <bool STRIDED = false>
 __device__ __forceinline__ double wave_inv16_dpp(double2 (&a)[4]) {
   double pprod = 1.0;
-  inv16_all(a, pprod, std::make_integer_sequence<int, 16>{});
+  inv16_all<STRIDED>(a, pprod, std::make_integer_sequence<int, 16>{});
   return pprod;
 }
 
