@@ -14,8 +14,9 @@ The directory name is not a Python identifier; import it through
 from .hmc import (ComputeCache, ModelParameters, ObservablesResult, SimulationState, calc_optimal_dt,
                   compute_forces, compute_total_energy, diagonalize_H_BdG, hmc_sweep, init_static_H,
                   initialize_cache, initialize_state, measure_observables, neighbour_tables,
-                  refresh_momentum, standard_complex_normal, update_H_BdG)
-from .context import FermionContext, selftest_mfma
+                  refresh_momentum, standard_complex_normal, update_H_BdG, SpectrumResult,
+                  measure_transport_and_spectra)
+from .context import FermionContext, selftest_mfma, transport_grid
 from .simulation import AdaptiveNt, SimulationResult, run_simulation
 from ._lib import DwhError, SpectrumGuardError, lib_path, load as load_library
 
@@ -25,5 +26,5 @@ __all__ = [
     "initialize_cache", "initialize_state", "measure_observables", "neighbour_tables",
     "refresh_momentum", "standard_complex_normal", "update_H_BdG", "FermionContext", "selftest_mfma",
     "DwhError", "SpectrumGuardError", "lib_path", "load_library", "AdaptiveNt", "SimulationResult",
-    "run_simulation",
+    "run_simulation", "SpectrumResult", "measure_transport_and_spectra", "transport_grid",
 ]

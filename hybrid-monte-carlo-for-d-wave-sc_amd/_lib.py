@@ -79,6 +79,9 @@ SIGNATURES = {
     "dwh_timing_enable": (C.c_int, [_P, _I32]),
     "dwh_timing_read": (C.c_int, [_P, C.c_char_p, _DP, C.POINTER(_I64), _DP]),
     "dwh_timing_reset": (C.c_int, [_P]),
+    "dwh_eigensystem": (C.c_int, [_P, _I64, _P, _P]),
+    "dwh_transport_grid": (C.c_int, [_D, _D, _D, C.POINTER(_I64), C.POINTER(_I64)]),
+    "dwh_measure_transport": (C.c_int, [_P, _I64, _D, _D, _D, _DP, _DP, _P, _I64, _P, _P, _I64, _P]),
     "dwh_selftest_mfma": (C.c_int, [_I32]),
 }
 

@@ -15,7 +15,9 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libdwhmc.so")
 SOURCES = [os.path.join(CSRC, "dwhmc_kernels.hip"), os.path.join(CSRC, "dwhmc_cr.hip"),
-           os.path.join(CSRC, "dwhmc_api.cpp")]
+           os.path.join(CSRC, "dwhmc_transport.hip"), os.path.join(CSRC, "dwhmc_api.cpp")]
+# rocSOLVER (zheevd) and rocBLAS (zgemm) serve the transport measurement only
+LIBS = ["-L/opt/rocm/lib", "-lrocsolver", "-lrocblas", "-Wl,-rpath,/opt/rocm/lib"]
 DEPS = SOURCES + [os.path.join(CSRC, "dwhmc_internal.h"), os.path.join(CSRC, "dwhmc_device.h"),
                   os.path.join(CSRC, "pole_table.inc"),
                   os.path.join(ROOT, "include", "dwhmc.h")]
@@ -44,7 +46,7 @@ def build(force: bool = False, verbose: bool = False, out: str = LIB, defines=()
     tmp = out + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-Wall", "-Wno-unused-result", f"-I{os.path.join(ROOT, 'include')}",
-           *[f"-D{d}" for d in defines], *SOURCES, "-o", tmp]
+           *[f"-D{d}" for d in defines], *SOURCES, *LIBS, "-o", tmp]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

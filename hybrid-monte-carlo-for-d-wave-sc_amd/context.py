@@ -66,6 +66,7 @@ class FermionContext:
         check(rc, None)
         self._h = h
         self.info = self._info()
+        self.info_lattice = (int(Lx), int(Ly))
 
     # -- lifecycle -------------------------------------------------------
     def close(self):
@@ -169,6 +170,33 @@ class FermionContext:
         self._c(self._lib.dwh_stream(self._h, C.byref(s)))
         return s.value or 0
 
+    # -- measurement path (eigenpairs, transport / spectra) ---------------
+    def eigensystem(self, chain: int = 0, vectors: bool = True):
+        """(E, U) of H_BdG at the device Δ of `chain` (dwh_eigensystem):
+        E ascending (2N,), U (2N, 2N) with eigenvectors in columns."""
+        n2 = 2 * self.N
+        E = np.empty(n2)
+        Ucm = np.empty((n2, n2), dtype=np.complex128) if vectors else None   # row c = column c of U
+        self._c(self._lib.dwh_eigensystem(self._h, int(chain), ptr(E), ptr(Ucm)))
+        return E, (None if Ucm is None else Ucm.T)
+
+    def measure_transport(self, eta: float, domega: float, omega_max: float, chain: int = 0) -> dict:
+        """measure_transport_and_spectra (src/Observables.jl:314-526) for one
+        chain at the device Δ; keys are the SpectrumResult fields
+        (:293-308), A_k_omega0 indexed [kx, ky]."""
+        nw, nd = transport_grid(eta, domega, omega_max, self._lib)
+        Lx, Ly = self.info_lattice
+        st, dc = C.c_double(), C.c_double()
+        sigma, dos, dos_an = np.empty(nw), np.empty(nd), np.empty(nd)
+        ak = np.empty(Lx * Ly)
+        self._c(self._lib.dwh_measure_transport(self._h, int(chain), float(eta), float(domega),
+                                                float(omega_max), C.byref(st), C.byref(dc), ptr(sigma),
+                                                nw, ptr(dos), ptr(dos_an), nd, ptr(ak)))
+        return dict(superfluid_stiffness=st.value, dc_conductivity=dc.value,
+                    omega_grid=eta + domega * np.arange(nw), optical_conductivity=sigma,
+                    dos_omega_grid=-omega_max + domega * np.arange(nd), dos=dos, dos_AN=dos_an,
+                    A_k_omega0=ak.reshape(Ly, Lx).T.copy())
+
     # -- timing ----------------------------------------------------------
     TIMERS = ("gj_update", "gj_pivot", "assemble", "contract", "step", "gj_edge", "cr_gemm", "cr_inv")
 
@@ -191,6 +219,15 @@ class FermionContext:
         w = C.c_double()
         self._c(self._lib.dwh_timing_read(self._h, name.encode(), C.byref(ms), C.byref(n), C.byref(w)))
         return ms.value, n.value, w.value
+
+
+def transport_grid(eta: float, domega: float, omega_max: float, lib=None):
+    """(n_omega, n_dos): lengths of η:Δω:ω_max and -ω_max:Δω:ω_max as Julia
+    counts them (dwh_transport_grid; host arithmetic, no device)."""
+    lib = _lib.load() if lib is None else lib
+    nw, nd = C.c_int64(), C.c_int64()
+    check(lib.dwh_transport_grid(float(eta), float(domega), float(omega_max), C.byref(nw), C.byref(nd)))
+    return nw.value, nd.value
 
 
 def selftest_mfma(device: int = 0) -> int:

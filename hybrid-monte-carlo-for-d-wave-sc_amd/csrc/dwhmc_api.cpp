@@ -10,6 +10,8 @@
 // All arithmetic runs in the HIP kernels (dwhmc_kernels.hip); there is no CPU
 // fallback: a missing device is an error.
 #include <hip/hip_runtime.h>
+#include <rocblas/rocblas.h>
+#include <rocsolver/rocsolver.h>
 
 #include <algorithm>
 #include <cmath>
@@ -401,6 +403,20 @@ struct dwh_ctx {
   // drifting k_cr_pair_force, consumed by the next factorisation); every
   // other path that changes Δ leaves it false
   bool pairing_in_pool = false;
+
+  // transport / spectra measurement (device side allocated on first use): host
+  // copies of the x-current operator J (CSR of its imaginary parts, duplicates
+  // summed, src/Observables.jl:237-283) and of the +x, +x+y, +x-y neighbours;
+  // the rocBLAS handle (rocSOLVER zheevd, zgemm) runs on ctx->stream
+  std::vector<int> tr_nbr, tr_rowptr, tr_col;
+  std::vector<double> tr_val;
+  bool tr_ready = false;
+  rocblas_handle blas = nullptr;
+  dwh::TrBufs tr{};
+  int *d_tr_nbr = nullptr, *d_tr_rowptr = nullptr, *d_tr_col = nullptr, *d_tr_info = nullptr;
+  double* d_tr_val = nullptr;
+  double* d_tr_offd = nullptr;   // zheevd off-diagonal workspace (2N)
+  int64_t tr_nw = -1, tr_nd = -1;   // ω / DOS grid lengths the output buffers hold
 
   // timing
   int timing = 0;   // bitmask over TimerName (bit i = kTimerNames[i])
@@ -820,6 +836,30 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
   ctx->beta = beta;
   ctx->J = J;
   ctx->delta_cap = delta_cap;
+  // x-current operator J [src/Observables.jl:237-283]: i t at (i, i+x), i t' at
+  // (i, i+x+y) and (i, i+x-y), plus their conjugate transposes, summed into CSR
+  // (SparseArrays.sparse adds duplicates); stored as imaginary parts
+  {
+    std::vector<std::map<int, double>> jrow(N);
+    ctx->tr_nbr.assign(3 * (size_t)N, 0);
+    for (int i = 0; i < N; ++i) {
+      const int js[3] = {NN(i, 0), NNN(i, 0), NNN(i, 3)};
+      const double ts[3] = {t, tp, tp};
+      for (int b = 0; b < 3; ++b) {
+        jrow[i][js[b]] += ts[b];
+        jrow[js[b]][i] -= ts[b];
+        ctx->tr_nbr[(size_t)b * N + i] = js[b];
+      }
+    }
+    ctx->tr_rowptr.assign(N + 1, 0);
+    for (int r = 0; r < N; ++r) {
+      for (auto& kv : jrow[r]) {
+        ctx->tr_col.push_back(kv.first);
+        ctx->tr_val.push_back(kv.second);
+      }
+      ctx->tr_rowptr[r + 1] = (int)ctx->tr_col.size();
+    }
+  }
   if (const char* e = std::getenv("DWHMC_GJ_PAIR")) ctx->gj_pair = std::atoi(e) != 0;
   ctx->kappa = kappa;
   ctx->Ebound = Ep;
@@ -1025,9 +1065,188 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
   return DWH_OK;
 }
 
+// ---------------------------------------------------------------------------
+// transport / spectra measurement (src/Observables.jl:314-526)
+// ---------------------------------------------------------------------------
+
+// length(start:step:stop) of the Julia float ranges of src/Observables.jl:395,430:
+// the step count is rounded when (stop - start)/step is an integer up to
+// rounding (Base.floatrange), else floored
+int64_t julia_range_len(double start, double step, double stop) {
+  const double r = (stop - start) / step;
+  const double n = std::nearbyint(r);
+  const double k = std::fabs(r - n) < 1e-8 * std::max(1.0, std::fabs(r)) ? n : std::floor(r);
+  return k < 0 ? 0 : (int64_t)k + 1;
+}
+
+void drop_alloc(dwh_ctx* ctx, void* p) {
+  if (!p) return;
+  auto it = std::find(ctx->allocations.begin(), ctx->allocations.end(), p);
+  if (it != ctx->allocations.end()) ctx->allocations.erase(it);
+  (void)hipFree(p);
+}
+
+// device buffers + rocBLAS handle on first use; output buffers sized for (nw, nd)
+int transport_prepare(dwh_ctx* ctx, int64_t nw, int64_t nd) {
+  const int N = ctx->d.N;
+  const size_t n2 = 2 * (size_t)N;
+  dwh::TrBufs& b = ctx->tr;
+  int rc = DWH_OK;
+  if (!ctx->tr_ready) {
+    if (rocblas_create_handle(&ctx->blas) != rocblas_status_success)
+      return fail(ctx, DWH_ERR_HIP, "rocblas_create_handle failed");
+    if (rocblas_set_stream(ctx->blas, ctx->stream) != rocblas_status_success)
+      return fail(ctx, DWH_ERR_HIP, "rocblas_set_stream failed");
+    if ((rc = dalloc(ctx, &b.U, n2 * n2)) || (rc = dalloc(ctx, &b.JU, n2 * n2)) ||
+        (rc = dalloc(ctx, &b.Jmn, n2 * n2)))
+      return rc;
+    for (double** p : {&b.E, &b.f, &b.dia, &b.Wn, &b.wan, &b.w0, &b.lam, &b.dc, &ctx->d_tr_offd})
+      if ((rc = dalloc(ctx, p, n2))) return rc;
+    if ((rc = dalloc(ctx, &b.ak, (size_t)N)) || (rc = dalloc(ctx, &b.scalars, 2)) ||
+        (rc = dalloc(ctx, &ctx->d_tr_info, 1)) || (rc = dalloc(ctx, &ctx->d_tr_nbr, ctx->tr_nbr.size())) ||
+        (rc = dalloc(ctx, &ctx->d_tr_rowptr, ctx->tr_rowptr.size())) ||
+        (rc = dalloc(ctx, &ctx->d_tr_col, ctx->tr_col.size())) ||
+        (rc = dalloc(ctx, &ctx->d_tr_val, ctx->tr_val.size())))
+      return rc;
+    auto up = [&](void* dst, const void* src, size_t bytes) {
+      return bytes == 0 ? hipSuccess : hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream);
+    };
+    HIPCHECK(ctx, up(ctx->d_tr_nbr, ctx->tr_nbr.data(), ctx->tr_nbr.size() * sizeof(int)));
+    HIPCHECK(ctx, up(ctx->d_tr_rowptr, ctx->tr_rowptr.data(), ctx->tr_rowptr.size() * sizeof(int)));
+    HIPCHECK(ctx, up(ctx->d_tr_col, ctx->tr_col.data(), ctx->tr_col.size() * sizeof(int)));
+    HIPCHECK(ctx, up(ctx->d_tr_val, ctx->tr_val.data(), ctx->tr_val.size() * sizeof(double)));
+    HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->tr_ready = true;
+  }
+  if (nw != ctx->tr_nw) {
+    HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+    drop_alloc(ctx, b.part);
+    drop_alloc(ctx, b.sigma);
+    b.part = b.sigma = nullptr;
+    if ((rc = dalloc(ctx, &b.part, (size_t)dwh::tr_sigma_chunks(N) * nw)) ||
+        (rc = dalloc(ctx, &b.sigma, (size_t)nw)))
+      return rc;
+    ctx->tr_nw = nw;
+  }
+  if (nd != ctx->tr_nd) {
+    HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+    drop_alloc(ctx, b.dos);
+    drop_alloc(ctx, b.dos_an);
+    b.dos = b.dos_an = nullptr;
+    if ((rc = dalloc(ctx, &b.dos, (size_t)nd)) || (rc = dalloc(ctx, &b.dos_an, (size_t)nd))) return rc;
+    ctx->tr_nd = nd;
+  }
+  return DWH_OK;
+}
+
+// dense H_BdG(Δ) of one chain -> rocSOLVER zheevd: eigenvalues ascending into
+// tr.E, eigenvectors into the columns of tr.U (diagonalize_H_BdG!,
+// src/Hamiltonian.jl:96-114; the reference's zheevr and zheevd agree to rounding)
+int eigen_enqueue(dwh_ctx* ctx, int64_t chain) {
+  const int N = ctx->d.N, n2 = 2 * N;
+  dwh::TrBufs& b = ctx->tr;
+  HIPCHECK(ctx, hipMemsetAsync(b.U, 0, (size_t)n2 * n2 * sizeof(double2), ctx->stream));
+  dwh::launch_tr_assemble(b.U, N, ctx->hcol, ctx->hval + (size_t)chain * N * kHSlots, ctx->Dcol,
+                          ctx->Dsrc, ctx->Delta + (size_t)chain * 2 * N, ctx->stream);
+  HIPCHECK(ctx, hipGetLastError());
+  const rocblas_status st =
+      rocsolver_zheevd(ctx->blas, rocblas_evect_original, rocblas_fill_upper, n2,
+                       reinterpret_cast<rocblas_double_complex*>(b.U), n2, b.E, ctx->d_tr_offd,
+                       ctx->d_tr_info);
+  if (st != rocblas_status_success)
+    return fail(ctx, DWH_ERR_HIP, std::string("rocsolver_zheevd: ") + rocblas_status_to_string(st));
+  return DWH_OK;
+}
+
+int eigen_info_check(dwh_ctx* ctx) {
+  int info = 0;
+  HIPCHECK(ctx, hipMemcpyAsync(&info, ctx->d_tr_info, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+  HIPCHECK(ctx, hipGetLastError());
+  if (info != 0)
+    return fail(ctx, DWH_ERR_HIP, "rocsolver_zheevd did not converge (info = " + std::to_string(info) + ")");
+  return DWH_OK;
+}
+
 }  // namespace
 
 extern "C" {
+
+int dwh_transport_grid(double eta, double domega, double omega_max, int64_t* n_omega, int64_t* n_dos) {
+  if (!n_omega || !n_dos) return fail(nullptr, DWH_ERR_ARG, "NULL argument");
+  if (!(eta > 0) || !(domega > 0) || !(omega_max > 0) || !std::isfinite(eta + domega + omega_max))
+    return fail(nullptr, DWH_ERR_ARG, "eta, domega, omega_max must be finite and > 0");
+  *n_omega = julia_range_len(eta, domega, omega_max);
+  *n_dos = julia_range_len(-omega_max, domega, omega_max);
+  if (*n_omega > (1 << 24) || *n_dos > (1 << 24))
+    return fail(nullptr, DWH_ERR_ARG, "frequency grid longer than 2^24 points");
+  return DWH_OK;
+}
+
+int dwh_eigensystem(dwh_ctx* ctx, int64_t chain, double* E, dwh_c128* U) {
+  if (!ctx || !E) return fail(ctx, DWH_ERR_ARG, "NULL argument");
+  if (chain < 0 || chain >= ctx->d.nc) return fail(ctx, DWH_ERR_ARG, "chain index out of range");
+  HIPCHECK(ctx, hipSetDevice(ctx->device));
+  int rc;
+  if ((rc = transport_prepare(ctx, std::max<int64_t>(ctx->tr_nw, 0), std::max<int64_t>(ctx->tr_nd, 0))))
+    return rc;
+  if ((rc = eigen_enqueue(ctx, chain))) return rc;
+  const size_t n2 = 2 * (size_t)ctx->d.N;
+  HIPCHECK(ctx, hipMemcpyAsync(E, ctx->tr.E, n2 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+  if (U)
+    HIPCHECK(ctx, hipMemcpyAsync(U, ctx->tr.U, n2 * n2 * sizeof(double2), hipMemcpyDeviceToHost,
+                                 ctx->stream));
+  return eigen_info_check(ctx);
+}
+
+int dwh_measure_transport(dwh_ctx* ctx, int64_t chain, double eta, double domega, double omega_max,
+                          double* stiffness, double* dc_cond, double* sigma, int64_t n_omega,
+                          double* dos, double* dos_an, int64_t n_dos, double* ak0) {
+  if (!ctx || !stiffness || !dc_cond || !ak0) return fail(ctx, DWH_ERR_ARG, "NULL argument");
+  if (chain < 0 || chain >= ctx->d.nc) return fail(ctx, DWH_ERR_ARG, "chain index out of range");
+  int64_t nw = 0, nd = 0;
+  if (dwh_transport_grid(eta, domega, omega_max, &nw, &nd) != DWH_OK)
+    return fail(ctx, DWH_ERR_ARG, g_create_error);
+  if (n_omega != nw || n_dos != nd)
+    return fail(ctx, DWH_ERR_ARG, "n_omega / n_dos differ from dwh_transport_grid (" + std::to_string(nw) +
+                                      ", " + std::to_string(nd) + ")");
+  if ((nw > 0 && !sigma) || (nd > 0 && (!dos || !dos_an))) return fail(ctx, DWH_ERR_ARG, "NULL grid output");
+  HIPCHECK(ctx, hipSetDevice(ctx->device));
+  int rc;
+  if ((rc = transport_prepare(ctx, nw, nd))) return rc;
+  if ((rc = eigen_enqueue(ctx, chain))) return rc;
+  const int N = ctx->d.N, n2 = 2 * N;
+  dwh::TrBufs& b = ctx->tr;
+  hipStream_t s = ctx->stream;
+  dwh::launch_tr_colstats(b.U, N, (int)ctx->Lx, b.E, ctx->beta, eta, ctx->t, ctx->tp, ctx->d_tr_nbr, b.f,
+                          b.dia, b.Wn, b.wan, b.w0, s);
+  dwh::launch_tr_current(b.U, b.JU, N, ctx->d_tr_rowptr, ctx->d_tr_col, ctx->d_tr_val, s);
+  HIPCHECK(ctx, hipGetLastError());
+  // J_mn = U^H (J ⊕ J) U  (src/Observables.jl:334-335)
+  const rocblas_double_complex one(1.0, 0.0), zero(0.0, 0.0);
+  const rocblas_status st = rocblas_zgemm(
+      ctx->blas, rocblas_operation_conjugate_transpose, rocblas_operation_none, n2, n2, n2, &one,
+      reinterpret_cast<const rocblas_double_complex*>(b.U), n2,
+      reinterpret_cast<const rocblas_double_complex*>(b.JU), n2, &zero,
+      reinterpret_cast<rocblas_double_complex*>(b.Jmn), n2);
+  if (st != rocblas_status_success)
+    return fail(ctx, DWH_ERR_HIP, std::string("rocblas_zgemm: ") + rocblas_status_to_string(st));
+  const dwh::TrGrid g{eta, -omega_max, domega, (int)nw, (int)nd};
+  dwh::launch_tr_reduce(b, N, (int)ctx->Lx, (int)ctx->Ly, ctx->beta, eta, g, s);
+  HIPCHECK(ctx, hipGetLastError());
+  double sc[2];
+  HIPCHECK(ctx, hipMemcpyAsync(sc, b.scalars, sizeof(sc), hipMemcpyDeviceToHost, s));
+  if (nw > 0) HIPCHECK(ctx, hipMemcpyAsync(sigma, b.sigma, nw * sizeof(double), hipMemcpyDeviceToHost, s));
+  if (nd > 0) {
+    HIPCHECK(ctx, hipMemcpyAsync(dos, b.dos, nd * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPCHECK(ctx, hipMemcpyAsync(dos_an, b.dos_an, nd * sizeof(double), hipMemcpyDeviceToHost, s));
+  }
+  HIPCHECK(ctx, hipMemcpyAsync(ak0, b.ak, (size_t)N * sizeof(double), hipMemcpyDeviceToHost, s));
+  if ((rc = eigen_info_check(ctx))) return rc;
+  *stiffness = sc[0];
+  *dc_cond = sc[1];
+  return DWH_OK;
+}
 
 int dwh_create(dwh_ctx** ctx, int64_t Lx, int64_t Ly, double t, double tp, double mu, double beta,
                double J, const int64_t* nn_table, const int64_t* nnn_table, const double* disorder,
@@ -1061,6 +1280,7 @@ void dwh_destroy(dwh_ctx* ctx) {
     (void)hipEventDestroy(r.b);
   }
   for (auto e : ctx->pool) (void)hipEventDestroy(e);
+  if (ctx->blas) (void)rocblas_destroy_handle(ctx->blas);
   for (void* p : ctx->allocations) (void)hipFree(p);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;

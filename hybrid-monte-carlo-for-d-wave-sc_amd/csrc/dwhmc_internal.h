@@ -140,6 +140,34 @@ void launch_restore(const Dims& d, const uint8_t* accepted, const double2* Delta
                     double2* Delta, double2* Pair, double* Ef, double* Trhh, hipStream_t s);
 void launch_sum_ld(const Dims& d, const double* ldpart, double* ldsum, hipStream_t s);
 
+// Transport / spectra measurement (dwhmc_transport.hip): device buffers of one
+// measurement (n2 = 2N; U, JU, Jmn: n2 x n2 column-major)
+struct TrBufs {
+  double2 *U, *JU, *Jmn;
+  double *E, *f, *dia, *Wn, *wan, *w0, *lam, *dc;   // n2 each
+  double *part, *sigma, *dos, *dos_an, *ak, *scalars;
+};
+// ω grid: w0 + k dw (k < nw); DOS grid: d0 + k dw (k < nd)
+struct TrGrid {
+  double w0, d0, dw;
+  int nw, nd;
+};
+int tr_sigma_chunks(int N);   // rows of TrBufs::part (each nw long)
+// dense H_BdG of one chain into A (zeroed beforehand)
+void launch_tr_assemble(double2* A, int N, const int* hcol, const double* hval, const int* Dcol,
+                        const int* Dsrc, const double2* Delta, hipStream_t s);
+// f, the diamagnetic / DOS / antinodal weights and the A(k,0) weight per eigenstate;
+// nbr: 3 x N (+x, +x+y, +x-y neighbours, 0-based)
+void launch_tr_colstats(const double2* U, int N, int Lx, const double* E, double beta, double eta,
+                        double t, double tp, const int* nbr, double* f, double* dia, double* Wn,
+                        double* wan, double* w0, hipStream_t s);
+// JU = (J ⊕ J) U, J in CSR form (N rows, val = Im J)
+void launch_tr_current(const double2* U, double2* JU, int N, const int* rowptr, const int* col,
+                       const double* val, hipStream_t s);
+// everything after J_mn: Λ, dc, σ(ω), stiffness, DOS, A(k,0) (overwrites JU and Jmn)
+void launch_tr_reduce(const TrBufs& b, int N, int Lx, int Ly, double beta, double eta,
+                      const TrGrid& g, hipStream_t s);
+
 int selftest_mfma_layout(int device);
 
 }  // namespace dwh

@@ -1,0 +1,357 @@
+// Transport and spectra of measure_transport_and_spectra
+// [src/Observables.jl:320-526] from the exact eigenpairs of one chain's H_BdG.
+//
+// This is the measurement path the reference runs every measure_transport_freq
+// sweeps (src/Simulation.jl:170-186), not the leapfrog hot path: the
+// eigenpairs come from rocSOLVER zheevd and J_mn = U^H (J ⊕ J) U from rocBLAS
+// zgemm (dwhmc_api.cpp drives both); the kernels here are everything around
+// them.  All matrices are column-major with leading dimension n2 = 2N (the
+// eigenvector of E_n is column n of U, as Julia's eigen! returns it).
+//
+// The O(n2^2 · n_ω) optical-conductivity sum is the only heavy kernel: every
+// thread owns one ω and streams the (ΔE, c) pairs of a chunk of columns
+// through LDS (one broadcast read per pair per wave), writing one partial per
+// (chunk, ω); a second kernel adds the chunks in a fixed order, so results are
+// deterministic run to run.
+#include "dwhmc_internal.h"
+
+namespace dwh {
+namespace {
+
+constexpr int kTB = 256;   // threads per block of every kernel here
+constexpr double kInvPi = 0.31830988618379067154;
+
+// LogExpFunctions.logistic, overflow-safe (the fermi factor f_n = logistic(-βE_n))
+__device__ inline double logistic_d(double x) {
+  if (x >= 0) return 1.0 / (1.0 + exp(-x));
+  const double e = exp(x);
+  return e / (1.0 + e);
+}
+
+// fixed-order tree sum of NV values per thread over the block; result in sh[v][0]
+template <int NV>
+__device__ inline void block_sum(double (&v)[NV], double (*sh)[kTB]) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) sh[k][tid] = v[k];
+  __syncthreads();
+  for (int s = kTB / 2; s > 0; s >>= 1) {
+    if (tid < s) {
+#pragma unroll
+      for (int k = 0; k < NV; ++k) sh[k][tid] += sh[k][tid + s];
+    }
+    __syncthreads();
+  }
+}
+
+// Dense H_BdG = [[h, D], [conj(D), -h]] of one chain (init_static_H! +
+// update_H_BdG!, src/Hamiltonian.jl:10-86); hcol/hval hold h with the
+// reference's overwrite order already resolved, Dcol/Dsrc the pairing pattern
+// (D[i, Dcol] = Δ[Dsrc] / 2).  Every entry is written at most once; the rest of
+// A is zeroed beforehand.
+__global__ void k_tr_assemble(double2* __restrict__ A, int n2, int N, const int* __restrict__ hcol,
+                              const double* __restrict__ hval, const int* __restrict__ Dcol,
+                              const int* __restrict__ Dsrc, const double2* __restrict__ Delta) {
+  const int i = blockIdx.x * kTB + threadIdx.x;
+  if (i >= N) return;
+  for (int s = 0; s < kHSlots; ++s) {
+    const int c = hcol[i * kHSlots + s];
+    if (c < 0) continue;
+    const double v = hval[i * kHSlots + s];
+    A[i + (size_t)c * n2] = make_double2(v, 0.0);
+    A[(i + N) + (size_t)(c + N) * n2] = make_double2(-v, 0.0);
+  }
+  for (int s = 0; s < kSlots; ++s) {
+    const int c = Dcol[i * kSlots + s];
+    if (c < 0) continue;
+    const double2 d = Delta[Dsrc[i * kSlots + s]];
+    A[i + (size_t)(c + N) * n2] = make_double2(0.5 * d.x, 0.5 * d.y);
+    A[(i + N) + (size_t)c * n2] = make_double2(0.5 * d.x, -0.5 * d.y);
+  }
+}
+
+// Per eigenstate n (one block per column of U):
+//   f_n = logistic(-β E_n)                                   (compute_forces!, :50)
+//   dia_n = [E_n > 0] w_n tanh(β E_n / 2), w_n the x-bond kinetic weight  (:345-362)
+//   Wn_n = Σ_i |u_i|^2                                        (DOS weight, :452-456)
+//   wan_n = (|Σ_i (-1)^x u_i|^2 + |Σ_i (-1)^y u_i|^2) / 2N     (antinodal, :465-488)
+//   w0_n = L(-E_n) if > 1e-6 else 0                          (A(k, 0) weight, :497-503)
+// nbr: jx (+x), jpy (+x+y), jmy (+x-y) per site, 0-based.
+__global__ void k_tr_colstats(const double2* __restrict__ U, int n2, int N, int Lx,
+                              const double* __restrict__ E, double beta, double eta, double t,
+                              double tp, const int* __restrict__ nbr, double* __restrict__ f,
+                              double* __restrict__ dia, double* __restrict__ Wn,
+                              double* __restrict__ wan, double* __restrict__ w0) {
+  __shared__ double sh[6][kTB];
+  const int n = blockIdx.x;
+  const double2* u = U + (size_t)n * n2;
+  const double2* v = u + N;
+  double acc[6] = {0, 0, 0, 0, 0, 0};   // w, W, Re ax, Im ax, Re ay, Im ay
+  for (int i = threadIdx.x; i < N; i += kTB) {
+    const double2 ui = u[i], vi = v[i];
+    double w = 0;
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+      const int j = nbr[b * N + i];
+      const double2 uj = u[j], vj = v[j];
+      // 2 Re(v_i conj(v_j) - conj(u_i) u_j)
+      const double bond = 2.0 * ((vi.x * vj.x + vi.y * vj.y) - (ui.x * uj.x + ui.y * uj.y));
+      w += (b == 0 ? t : tp) * bond;
+    }
+    acc[0] += w;
+    acc[1] += ui.x * ui.x + ui.y * ui.y;
+    const int x = i % Lx + 1, y = i / Lx + 1;
+    const double sx = (x % 2 == 0) ? 1.0 : -1.0, sy = (y % 2 == 0) ? 1.0 : -1.0;
+    acc[2] += sx * ui.x;
+    acc[3] += sx * ui.y;
+    acc[4] += sy * ui.x;
+    acc[5] += sy * ui.y;
+  }
+  block_sum<6>(acc, sh);
+  if (threadIdx.x == 0) {
+    const double e = E[n];
+    f[n] = logistic_d(-beta * e);
+    dia[n] = e > 0 ? sh[0][0] * tanh(0.5 * beta * e) : 0.0;
+    Wn[n] = sh[1][0];
+    wan[n] = 0.5 * (sh[2][0] * sh[2][0] + sh[3][0] * sh[3][0] + sh[4][0] * sh[4][0] +
+                    sh[5][0] * sh[5][0]) / N;
+    const double l0 = kInvPi * (eta / (e * e + eta * eta));
+    w0[n] = l0 > 1e-6 ? l0 : 0.0;
+  }
+}
+
+// JU = (J ⊕ J) U with J the x-current operator in CSR form (duplicates summed,
+// build_current_operator!, src/Observables.jl:237-283); J is purely imaginary,
+// val holds Im J
+__global__ void k_tr_current(const double2* __restrict__ U, double2* __restrict__ JU, int n2, int N,
+                             const int* __restrict__ rowptr, const int* __restrict__ col,
+                             const double* __restrict__ val) {
+  const int r = blockIdx.x * kTB + threadIdx.x;
+  if (r >= n2) return;
+  const int n = blockIdx.y;
+  const int rr = r < N ? r : r - N, off = r < N ? 0 : N;
+  const double2* u = U + (size_t)n * n2 + off;
+  double2 acc = make_double2(0.0, 0.0);
+  for (int k = rowptr[rr]; k < rowptr[rr + 1]; ++k) {
+    const double a = val[k];
+    const double2 b = u[col[k]];
+    acc.x -= a * b.y;
+    acc.y += a * b.x;
+  }
+  JU[(size_t)n * n2 + r] = acc;
+}
+
+// Per column m of J_mn (threads over n): the paramagnetic sum Λ (:366-384)
+// and the DC conductivity (:405-413), before the 1/N (and π·(1/π)) factors.
+__global__ void k_tr_pairs(const double2* __restrict__ Jmn, int n2, const double* __restrict__ E,
+                           const double* __restrict__ f, double beta, double eta,
+                           double* __restrict__ lam_part, double* __restrict__ dc_part) {
+  __shared__ double sh[2][kTB];
+  const int m = blockIdx.x;
+  const double Em = E[m], fm = f[m], eta2 = eta * eta;
+  double acc[2] = {0, 0};
+  for (int n = threadIdx.x; n < n2; n += kTB) {
+    const double2 j = Jmn[(size_t)m * n2 + n];
+    const double J2 = j.x * j.x + j.y * j.y;
+    const double dE = Em - E[n], fn = f[n];
+    const double bf = beta * fn * (1.0 - fn);
+    const double ratio = fabs(dE) < 1e-8 ? bf : (fn - fm) / dE;
+    acc[0] += ratio * J2;
+    acc[1] += bf * J2 * (eta / (dE * dE + eta2));
+  }
+  block_sum<2>(acc, sh);
+  if (threadIdx.x == 0) {
+    lam_part[m] = sh[0][0];
+    dc_part[m] = sh[1][0];
+  }
+}
+
+__device__ inline double grid_point(double start, double step, int k) {
+  return __dadd_rn(start, __dmul_rn(step, (double)k));
+}
+
+// σ(ω) partials (:415-423): part[chunk][k] = Σ_{m in chunk, n} c_nm / ((ω_k - ΔE)^2 + η^2)
+// with c_nm = (f_n - f_m) |J_nm|^2 (0 where |f_n - f_m| < 1e-12), ΔE = E_m - E_n.
+__global__ void __launch_bounds__(kTB)
+k_tr_sigma(const double2* __restrict__ Jmn, int n2, const double* __restrict__ E,
+           const double* __restrict__ f, double eta, double w_start, double w_step, int nw,
+           int cols, double* __restrict__ part) {
+  __shared__ double sdE[kTB], sc[kTB];
+  const int tid = threadIdx.x;
+  const int k = blockIdx.x * kTB + tid;
+  const double w = grid_point(w_start, w_step, k < nw ? k : nw - 1);
+  const double eta2 = eta * eta;
+  const int m0 = blockIdx.y * cols, m1 = min(m0 + cols, n2);
+  double acc0 = 0, acc1 = 0;
+  for (int m = m0; m < m1; ++m) {
+    const double Em = E[m], fm = f[m];
+    for (int n0 = 0; n0 < n2; n0 += kTB) {
+      const int n = n0 + tid;
+      if (n < n2) {
+        const double2 j = Jmn[(size_t)m * n2 + n];
+        const double df = f[n] - fm;
+        sc[tid] = fabs(df) >= 1e-12 ? df * (j.x * j.x + j.y * j.y) : 0.0;
+        sdE[tid] = Em - E[n];
+      }
+      __syncthreads();
+      const int cnt = min(kTB, n2 - n0);
+      int q = 0;
+      for (; q + 1 < cnt; q += 2) {
+        const double d0 = w - sdE[q], d1 = w - sdE[q + 1];
+        acc0 += sc[q] / (d0 * d0 + eta2);
+        acc1 += sc[q + 1] / (d1 * d1 + eta2);
+      }
+      if (q < cnt) {
+        const double d0 = w - sdE[q];
+        acc0 += sc[q] / (d0 * d0 + eta2);
+      }
+      __syncthreads();
+    }
+  }
+  if (k < nw) part[(size_t)blockIdx.y * nw + k] = acc0 + acc1;
+}
+
+// σ(ω_k) = π/N Σ c/ω L(ω - ΔE) = η / (N ω) Σ_chunks part
+__global__ void k_tr_sigma_sum(const double* __restrict__ part, int nchunk, int nw, double eta,
+                               double w_start, double w_step, int N, double* __restrict__ sigma) {
+  const int k = blockIdx.x * kTB + threadIdx.x;
+  if (k >= nw) return;
+  double s = 0;
+  for (int c = 0; c < nchunk; ++c) s += part[(size_t)c * nw + k];
+  sigma[k] = s * eta / ((double)N * grid_point(w_start, w_step, k));
+}
+
+// out[0] = stiffness = Σ dia / N - Σ lam / N; out[1] = dc = Σ dc / N
+__global__ void k_tr_scalars(const double* __restrict__ dia, const double* __restrict__ lam,
+                             const double* __restrict__ dc, int n2, int N, double* __restrict__ out) {
+  __shared__ double sh[3][kTB];
+  double acc[3] = {0, 0, 0};
+  for (int n = threadIdx.x; n < n2; n += kTB) {
+    acc[0] += dia[n];
+    acc[1] += lam[n];
+    acc[2] += dc[n];
+  }
+  block_sum<3>(acc, sh);
+  if (threadIdx.x == 0) {
+    out[0] = sh[0][0] / N - sh[1][0] / N;
+    out[1] = sh[2][0] / N;
+  }
+}
+
+// DOS and antinodal DOS on the grid -ω_max:Δω:ω_max (:446-490)
+__global__ void k_tr_dos(const double* __restrict__ E, const double* __restrict__ Wn,
+                         const double* __restrict__ wan, int n2, int N, double eta, double w_start,
+                         double w_step, int nd, double* __restrict__ dos, double* __restrict__ dos_an) {
+  const int k = blockIdx.x * kTB + threadIdx.x;
+  if (k >= nd) return;
+  const double w = grid_point(w_start, w_step, k), eta2 = eta * eta;
+  double a = 0, b = 0;
+  for (int n = 0; n < n2; ++n) {
+    const double d = w - E[n];
+    const double l = kInvPi * (eta / (d * d + eta2));
+    a += Wn[n] * l;
+    b += wan[n] * l;
+  }
+  dos[k] = a / N;
+  dos_an[k] = b;
+}
+
+// A(k, ω=0) (:492-516): FFT2 of every particle column u_n as an Lx x Ly image
+// (site i = x + Lx y), done as two direct DFT passes.  Pass x:
+// T[kx + Lx y, n] = Σ_x u[x + Lx y, n] e^{-2πi kx x / Lx}
+__global__ void k_tr_dft_x(const double2* __restrict__ U, int n2, int Lx, int Ly,
+                           double2* __restrict__ T) {
+  const int N = Lx * Ly;
+  const int idx = blockIdx.x * kTB + threadIdx.x;
+  if (idx >= N) return;
+  const int n = blockIdx.y, kx = idx % Lx, y = idx / Lx;
+  const double2* u = U + (size_t)n * n2 + (size_t)y * Lx;
+  double2 acc = make_double2(0.0, 0.0);
+  for (int x = 0; x < Lx; ++x) {
+    double s, c;
+    sincospi(-2.0 * (double)((kx * x) % Lx) / Lx, &s, &c);
+    const double2 a = u[x];
+    acc.x += a.x * c - a.y * s;
+    acc.y += a.x * s + a.y * c;
+  }
+  T[(size_t)n * N + idx] = acc;
+}
+
+// Pass y and weight: Pw[kx + Lx ky, n] = w0_n |Σ_y T[kx + Lx y, n] e^{-2πi ky y / Ly}|^2
+__global__ void k_tr_dft_y(const double2* __restrict__ T, const double* __restrict__ w0, int Lx,
+                           int Ly, double* __restrict__ Pw) {
+  const int N = Lx * Ly;
+  const int idx = blockIdx.x * kTB + threadIdx.x;
+  if (idx >= N) return;
+  const int n = blockIdx.y, kx = idx % Lx, ky = idx / Lx;
+  const double2* tcol = T + (size_t)n * N + kx;
+  double2 acc = make_double2(0.0, 0.0);
+  for (int y = 0; y < Ly; ++y) {
+    double s, c;
+    sincospi(-2.0 * (double)((ky * y) % Ly) / Ly, &s, &c);
+    const double2 a = tcol[(size_t)y * Lx];
+    acc.x += a.x * c - a.y * s;
+    acc.y += a.x * s + a.y * c;
+  }
+  Pw[(size_t)n * N + idx] = w0[n] * (acc.x * acc.x + acc.y * acc.y);
+}
+
+// A_k[kx + Lx ky] = Σ_n Pw[k, n] / N, in n order
+__global__ void k_tr_ak_sum(const double* __restrict__ Pw, int n2, int N, double* __restrict__ ak) {
+  const int k = blockIdx.x * kTB + threadIdx.x;
+  if (k >= N) return;
+  double s = 0;
+  for (int n = 0; n < n2; ++n) s += Pw[(size_t)n * N + k];
+  ak[k] = s / N;
+}
+
+inline int cdiv(int64_t a, int b) { return (int)((a + b - 1) / b); }
+
+}  // namespace
+
+void launch_tr_assemble(double2* A, int N, const int* hcol, const double* hval, const int* Dcol,
+                        const int* Dsrc, const double2* Delta, hipStream_t s) {
+  hipLaunchKernelGGL(k_tr_assemble, dim3(cdiv(N, kTB)), dim3(kTB), 0, s, A, 2 * N, N, hcol, hval,
+                     Dcol, Dsrc, Delta);
+}
+
+void launch_tr_colstats(const double2* U, int N, int Lx, const double* E, double beta, double eta,
+                        double t, double tp, const int* nbr, double* f, double* dia, double* Wn,
+                        double* wan, double* w0, hipStream_t s) {
+  hipLaunchKernelGGL(k_tr_colstats, dim3(2 * N), dim3(kTB), 0, s, U, 2 * N, N, Lx, E, beta, eta, t,
+                     tp, nbr, f, dia, Wn, wan, w0);
+}
+
+void launch_tr_current(const double2* U, double2* JU, int N, const int* rowptr, const int* col,
+                       const double* val, hipStream_t s) {
+  hipLaunchKernelGGL(k_tr_current, dim3(cdiv(2 * N, kTB), 2 * N), dim3(kTB), 0, s, U, JU, 2 * N,
+                     N, rowptr, col, val);
+}
+
+int tr_sigma_chunks(int N) { return std::min(2 * N, 512); }
+
+void launch_tr_reduce(const TrBufs& b, int N, int Lx, int Ly, double beta, double eta,
+                      const TrGrid& g, hipStream_t s) {
+  const int n2 = 2 * N;
+  hipLaunchKernelGGL(k_tr_pairs, dim3(n2), dim3(kTB), 0, s, b.Jmn, n2, b.E, b.f, beta, eta, b.lam,
+                     b.dc);
+  if (g.nw > 0) {
+    const int nchunk = tr_sigma_chunks(N), cols = cdiv(n2, nchunk);
+    const int used = cdiv(n2, cols);
+    hipLaunchKernelGGL(k_tr_sigma, dim3(cdiv(g.nw, kTB), used), dim3(kTB), 0, s, b.Jmn, n2, b.E,
+                       b.f, eta, g.w0, g.dw, g.nw, cols, b.part);
+    hipLaunchKernelGGL(k_tr_sigma_sum, dim3(cdiv(g.nw, kTB)), dim3(kTB), 0, s, b.part, used, g.nw,
+                       eta, g.w0, g.dw, N, b.sigma);
+  }
+  hipLaunchKernelGGL(k_tr_scalars, dim3(1), dim3(kTB), 0, s, b.dia, b.lam, b.dc, n2, N, b.scalars);
+  if (g.nd > 0)
+    hipLaunchKernelGGL(k_tr_dos, dim3(cdiv(g.nd, kTB)), dim3(kTB), 0, s, b.E, b.Wn, b.wan, n2, N,
+                       eta, g.d0, g.dw, g.nd, b.dos, b.dos_an);
+  // A(k, 0): T reuses JU, the weighted |FFT|^2 reuses J_mn (both no longer needed)
+  hipLaunchKernelGGL(k_tr_dft_x, dim3(cdiv(N, kTB), n2), dim3(kTB), 0, s, b.U, n2, Lx, Ly, b.JU);
+  double* Pw = reinterpret_cast<double*>(b.Jmn);
+  hipLaunchKernelGGL(k_tr_dft_y, dim3(cdiv(N, kTB), n2), dim3(kTB), 0, s, b.JU, b.w0, Lx, Ly, Pw);
+  hipLaunchKernelGGL(k_tr_ak_sum, dim3(cdiv(N, kTB)), dim3(kTB), 0, s, Pw, n2, N, b.ak);
+}
+
+}  // namespace dwh

@@ -215,6 +215,27 @@ class ObservablesResult:
     Delta_localpair: float
 
 
+@dataclass
+class SpectrumResult:
+    """src/Observables.jl:293-308 (A_k_omega0 indexed [kx, ky])."""
+    superfluid_stiffness: float
+    dc_conductivity: float
+    omega_grid: np.ndarray
+    optical_conductivity: np.ndarray
+    dos_omega_grid: np.ndarray
+    dos: np.ndarray
+    dos_AN: np.ndarray
+    A_k_omega0: np.ndarray
+
+
+def measure_transport_and_spectra(cache: ComputeCache, p: ModelParameters, chain: int = 0) -> SpectrumResult:
+    """src/Observables.jl:314-526 on the device: eigenpairs of H_BdG at the Δ
+    the cache's context holds (rocSOLVER zheevd), J_mn = U^H J U (rocBLAS
+    zgemm), stiffness / conductivities / DOS / A(k, 0) in HIP kernels."""
+    r = cache.require().measure_transport(p.eta, p.domega, p.omega_max, chain=chain)
+    return SpectrumResult(**r)
+
+
 def measure_observables(cache: ComputeCache, p: ModelParameters, state: SimulationState) -> ObservablesResult:
     """src/Observables.jl:88-222 from the factorisation outputs: P_ij (from
     the same pole-LU as the force), E_f, and Tr ρ_hh for the hole density

@@ -6,15 +6,16 @@ reference; every sweep's fermionic work runs on the GPU through the C ABI
 (hmc.py -> FermionContext), and the lightweight measurements come from the
 factorisation outputs (P_ij, E_f, Tr ρ_hh; hmc.measure_observables).
 
-Not reproduced (out of the hot-path scope): the heavy
-transport/spectra measurement (`measure_transport_and_spectra`,
-src/Observables.jl:225-526, needs eigenvectors) — transport.csv gets its
-header only and the log says so — and the JLD2 spectra bins (no JLD2 writer in
-this image).  The reference's RNG is global and unseeded; here the caller
+Every measure_transport_freq sweeps the heavy measurement
+(`measure_transport_and_spectra`, src/Observables.jl:314-526) runs on the
+device as well (rocSOLVER eigenpairs + HIP kernels) and fills transport.csv;
+the JLD2 spectra bins become numpy files (no JLD2 writer in this image).
+The reference's RNG is global and unseeded; here the caller
 passes `rng` (draw order per sweep: randn(ComplexF64, N, 2), then rand()).
 """
 from __future__ import annotations
 
+import json
 import math
 import os
 import time
@@ -24,6 +25,7 @@ from datetime import datetime
 import numpy as np
 
 from . import hmc as H
+from .context import transport_grid
 
 OBS_HEADER = ("Sweep,Accepted,dH,Energy,Delta_Amp,Delta_Loc,Delta_Glob,S_Delta,Hole_p,Delta_Diff,"
               "Delta_Pair,Delta_LocalPair")
@@ -68,6 +70,50 @@ class SimulationResult:
     therm_acceptance: float
     meas_acceptance: float
     records: list = field(default_factory=list)   # (sweep, accepted, dH, ObservablesResult)
+    transport: list = field(default_factory=list)  # (sweep, SpectrumResult)
+
+
+def transport_csv_line(sweep: int, spec) -> str:
+    """src/Simulation.jl:174-177."""
+    return "%d,%.6f,%.6f\n" % (sweep, spec.superfluid_stiffness, spec.dc_conductivity)
+
+
+def write_spectra_header(spec_dir: str, p) -> None:
+    """jldsave(params, omega_grid) of src/Simulation.jl:89."""
+    os.makedirs(spec_dir, exist_ok=True)
+    params = {k: getattr(p, k) for k in ("Lx", "Ly", "t", "tp", "mu", "W", "n_imp", "beta", "J", "mass",
+                                         "eta", "domega", "omega_max")}
+    with open(os.path.join(spec_dir, "params.json"), "w") as f:
+        json.dump(params, f, indent=1)
+    n, _ = transport_grid(p.eta, p.domega, p.omega_max)
+    np.save(os.path.join(spec_dir, "omega_grid.npy"), p.eta + p.domega * np.arange(n))
+
+
+class SpectraBins:
+    """Bin accumulator of src/Simulation.jl:180-220: sums the spectra of
+    bin_size measurements, then writes their mean as group sweep_<i>."""
+
+    def __init__(self):
+        self.count = 0
+        self.acc = None
+
+    def add(self, spec) -> int:
+        arrs = [spec.optical_conductivity, spec.dos, spec.dos_AN, spec.A_k_omega0]
+        if self.count == 0:
+            self.acc = [np.array(a, dtype=np.float64, copy=True) for a in arrs]
+        else:
+            for a, b in zip(self.acc, arrs):
+                a += b
+        self.count += 1
+        return self.count
+
+    def flush(self, spec_dir: str, sweep: int) -> None:
+        c = self.count
+        oc, dos, dos_an, ak = (a / c for a in self.acc)
+        np.savez(os.path.join(spec_dir, f"sweep_{sweep}.npz"), opt_cond=oc, dos=dos, dos_AN=dos_an,
+                 A_k0=ak, count=c)
+        self.count = 0
+        self.acc = None
 
 
 def run_simulation(p: H.ModelParameters, out_dir: str, *, n_therm: int = 100, n_measure: int = 500,
@@ -76,7 +122,11 @@ def run_simulation(p: H.ModelParameters, out_dir: str, *, n_therm: int = 100, n_
                    device: int = 0, delta_cap: float = 2.0, state: H.SimulationState | None = None,
                    cache: H.ComputeCache | None = None) -> SimulationResult:
     """src/Simulation.jl:34-236.  Files in out_dir: simulation.log (appended),
-    observables.csv, transport.csv (header only)."""
+    observables.csv, transport.csv (one row per transport measurement, every
+    measure_transport_freq sweeps; <= 0 disables), and spectra_bins/ — the
+    reference's spectra_bins.jld2 (:52,89,206-214) as numpy files: params.json,
+    omega_grid.npy, and one sweep_<i>.npz per completed bin of bin_size
+    measurements (opt_cond, dos, dos_AN, A_k0 averaged; count)."""
     rng = rng if rng is not None else np.random.default_rng()
     os.makedirs(out_dir, exist_ok=True)
     f_log = open(os.path.join(out_dir, "simulation.log"), "a")
@@ -96,8 +146,6 @@ def run_simulation(p: H.ModelParameters, out_dir: str, *, n_therm: int = 100, n_
         tee(f"System: {p.Lx}x{p.Ly}, β={p.beta}, n_imp={p.n_imp}, J={p.J}")
         tee(f"Config: Therm={n_therm}, Sweep={n_measure}, TransFreq={measure_transport_freq}, "
             f"BinSize={bin_size}")
-        tee("Transport/spectra measurements need eigenvectors: not on the GPU path, "
-            "transport.csv holds the header only")
 
         tee("Initializing State...")
         if state is None:
@@ -107,6 +155,9 @@ def run_simulation(p: H.ModelParameters, out_dir: str, *, n_therm: int = 100, n_
         H.init_static_H(cache, p, state)
         H.update_H_BdG(cache, p, state)
         H.diagonalize_H_BdG(cache, p)
+        spec_dir = os.path.join(out_dir, "spectra_bins")
+        if measure_transport_freq > 0:
+            write_spectra_header(spec_dir, p)
 
         ctl = AdaptiveNt(Nt_therm_init)
         dt = H.calc_optimal_dt(p.beta, p.J, p.mass, ctl.Nt)
@@ -134,6 +185,7 @@ def run_simulation(p: H.ModelParameters, out_dir: str, *, n_therm: int = 100, n_
         t1 = time.time()
         acc_total = 0
         res = SimulationResult(ctl.Nt, acc_therm / max(n_therm, 1), 0.0)
+        bins = SpectraBins()
         for i in range(1, n_measure + 1):
             acc, dH = H.hmc_sweep(cache, p, state, Nt=Nt_measure, dt=dt_meas, rng=rng)
             acc_total += int(acc)
@@ -141,6 +193,13 @@ def run_simulation(p: H.ModelParameters, out_dir: str, *, n_therm: int = 100, n_
             f_obs.write(obs_csv_line(i, acc, dH, obs))
             f_obs.flush()
             res.records.append((i, acc, dH, obs))
+            if measure_transport_freq > 0 and i % measure_transport_freq == 0:
+                spec = H.measure_transport_and_spectra(cache, p)
+                f_trans.write(transport_csv_line(i, spec))
+                f_trans.flush()
+                res.transport.append((i, spec))
+                if bins.add(spec) >= bin_size:
+                    bins.flush(spec_dir, i)
             if i % 10 == 0:
                 tee("Meas %d/%d. Acc=%.2f. E=%.4f" % (i, n_measure, acc_total / i, obs.total_energy))
         res.meas_acceptance = acc_total / max(n_measure, 1)

@@ -152,6 +152,33 @@ int dwh_timing_read(dwh_ctx* ctx, const char* name, double* total_ms, int64_t* l
                     double* work);
 int dwh_timing_reset(dwh_ctx* ctx);
 
+/* ---- measurement path (not the leapfrog step) ----------------------------
+ * Eigen-decomposition of one chain's H_BdG(Δ) at the device Δ: what the
+ * reference's diagonalize_H_BdG! [src/Hamiltonian.jl:96-114] leaves in
+ * cache.E_n / cache.U, which the hot path replaces by the pole expansion but
+ * transport and spectra need.  rocSOLVER zheevd on the context's stream.
+ * E: 2N, ascending; U (nullable): 2N x 2N column-major, the eigenvector of
+ * E[n] in column n (phases are the solver's). */
+int dwh_eigensystem(dwh_ctx* ctx, int64_t chain, double* E, dwh_c128* U);
+
+/* Lengths of the frequency grids of measure_transport_and_spectra
+ * [src/Observables.jl:395,430]: ω = η:Δω:ω_max and -ω_max:Δω:ω_max, counted
+ * as Julia's float ranges count them; point k of either grid is start + k·Δω. */
+int dwh_transport_grid(double eta, double domega, double omega_max, int64_t* n_omega,
+                       int64_t* n_dos);
+
+/* measure_transport_and_spectra [src/Observables.jl:314-526] for one chain at
+ * the device Δ, i.e. the SpectrumResult fields [:293-308]: superfluid
+ * stiffness, DC conductivity, σ(ω) on the ω grid (n_omega values), DOS and
+ * antinodal DOS on the DOS grid (n_dos values each) and A(k, ω=0) as the
+ * column-major Lx x Ly map (element (kx, ky) at kx + Lx·ky, FFTW's forward
+ * sign).  n_omega / n_dos must equal dwh_transport_grid's.  The current
+ * operator J_x [:237-283] is built once per context; J_mn = U^H (J ⊕ J) U is a
+ * rocBLAS zgemm; the rest runs in dwhmc_transport.hip. */
+int dwh_measure_transport(dwh_ctx* ctx, int64_t chain, double eta, double domega, double omega_max,
+                          double* stiffness, double* dc_cond, double* sigma, int64_t n_omega,
+                          double* dos, double* dos_an, int64_t n_dos, double* ak0);
+
 /* Self-test of the f64 MFMA fragment layout (A = I, asymmetric B); 0 = pass. */
 int dwh_selftest_mfma(int32_t device);
 

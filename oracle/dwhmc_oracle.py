@@ -366,6 +366,127 @@ def measure_observables(cache: ComputeCache, p: ModelParameters, Delta) -> dict:
 
 
 # ---------------------------------------------------------------------------
+# Observables.jl:225-526 — transport and spectra (needs eigenpairs)
+# ---------------------------------------------------------------------------
+def julia_range(start: float, step: float, stop: float) -> np.ndarray:
+    """collect(start:step:stop) for the float ranges of Observables.jl:395,446
+    (Julia rounds the length to the nearest count when (stop-start)/step is
+    within rounding of an integer)."""
+    r = (stop - start) / step
+    n = int(round(r)) if abs(r - round(r)) < 1e-8 * max(1.0, abs(r)) else int(math.floor(r))
+    return start + step * np.arange(n + 1)
+
+
+def current_operator(p: ModelParameters) -> np.ndarray:
+    """Particle block of J_x, src/Observables.jl:237-278: i t (c†_i c_{i+x} -
+    h.c.) plus the two t' diagonals (+x+y, +x-y); duplicate (row, col) pairs
+    are summed (SparseArrays.sparse).  The Nambu operator is diag(Jx, Jx)."""
+    N = p.N
+    Jx = np.zeros((N, N), dtype=np.complex128)
+    for i in range(N):
+        for j, val in ((p.nn_table[i, 0] - 1, 1j * p.t), (p.nnn_table[i, 0] - 1, 1j * p.tp),
+                       (p.nnn_table[i, 3] - 1, 1j * p.tp)):
+            Jx[i, j] += val
+            Jx[j, i] += np.conj(val)
+    return Jx
+
+
+def lorentzian(x, eta):
+    """src/Observables.jl:399-401."""
+    return (1.0 / math.pi) * (eta / (x * x + eta * eta))
+
+
+def measure_transport_and_spectra(cache: ComputeCache, p: ModelParameters) -> dict:
+    """src/Observables.jl:320-526 from the eigenpairs of the cache (and its
+    fermi_factors, set by compute_forces!).  Returns the SpectrumResult fields
+    (src/Observables.jl:290-305)."""
+    N, beta, eta = p.N, p.beta, p.eta
+    U, E, f = cache.U, cache.E_n, cache.fermi_factors
+    u, v = U[:N], U[N:]
+    Jx = current_operator(p)
+    Jmn = U.conj().T @ np.vstack([Jx @ u, Jx @ v])        # :334-335, J_mn[n, m]
+    # B. superfluid stiffness: diamagnetic term (:345-362)
+    i = np.arange(N)
+    jx, jxpy, jxmy = p.nn_table[:, 0] - 1, p.nnn_table[:, 0] - 1, p.nnn_table[:, 3] - 1
+
+    def bond(j):
+        return 2.0 * np.real(v[i] * np.conj(v[j]) - np.conj(u[i]) * u[j]).sum(axis=0)
+
+    w = p.t * bond(jx) + p.tp * bond(jxpy) + p.tp * bond(jxmy)
+    pos = E > 0
+    val_dia = float(np.sum(w[pos] * np.tanh(0.5 * beta * E[pos]))) / N
+    # paramagnetic term (:366-384): [n, m] with diff_E = E_m - E_n, diff_f = f_n - f_m
+    dE = E[None, :] - E[:, None]
+    df = f[:, None] - f[None, :]
+    J2 = np.abs(Jmn) ** 2
+    deg = np.abs(dE) < 1e-8
+    ratio = np.where(deg, (beta * f * (1.0 - f))[:, None], df / np.where(deg, 1.0, dE))
+    Lambda_xx = float(np.sum(ratio * J2)) / N
+    # C. DC and optical conductivity (:395-423)
+    omega = julia_range(p.eta, p.domega, p.omega_max)
+    dc = math.pi / N * float(np.sum((beta * f * (1.0 - f))[:, None] * J2 * lorentzian(dE, eta)))
+    keep = np.abs(df) >= 1e-12
+    coef = np.where(keep, df * J2, 0.0).ravel()
+    dEr = dE.ravel()
+    sigma = np.array([np.sum(coef / om * lorentzian(om - dEr, eta)) for om in omega]) * (math.pi / N)
+    # D. DOS, antinodal DOS, A(k, 0) (:430-516)
+    dos_grid = julia_range(-p.omega_max, p.domega, p.omega_max)
+    Lg = lorentzian(dos_grid[:, None] - E[None, :], eta)          # [w, n]
+    Wn = np.sum(np.abs(u) ** 2, axis=0)
+    x = i % p.Lx + 1
+    y = i // p.Lx + 1
+    sx = np.where(x % 2 == 0, 1.0, -1.0)
+    sy = np.where(y % 2 == 0, 1.0, -1.0)
+    wAN = 0.5 * (np.abs(sx @ u) ** 2 + np.abs(sy @ u) ** 2) / N
+    dos = Lg @ Wn / N
+    dos_AN = Lg @ wAN
+    w0 = lorentzian(-E, eta)
+    sel = w0 > 1e-6
+    ur = u[:, sel].reshape(p.Ly, p.Lx, -1)                          # [y, x, n]: i = x + Lx y
+    uk = np.fft.fft2(ur, axes=(0, 1))
+    ak = np.einsum("yxn,n->xy", np.abs(uk) ** 2, w0[sel]) / N       # A_k_ω0[x, y]
+    return dict(superfluid_stiffness=val_dia - Lambda_xx, dc_conductivity=dc, omega_grid=omega,
+                optical_conductivity=sigma, dos_omega_grid=dos_grid, dos=dos, dos_AN=dos_AN,
+                A_k_omega0=ak)
+
+
+def measure_transport_loops(cache: ComputeCache, p: ModelParameters) -> dict:
+    """The same quantities as literal loops over (n, m) and sites in the
+    reference's order (src/Observables.jl:345-423), for small lattices: the
+    loop-order pin of the vectorised restatement above."""
+    N, n2, beta, eta = p.N, 2 * p.N, p.beta, p.eta
+    U, E, f = cache.U, cache.E_n, cache.fermi_factors
+    Jx = current_operator(p)
+    JU = np.vstack([Jx @ U[:N], Jx @ U[N:]])
+    Jmn = U.conj().T @ JU
+    val_dia = 0.0
+    for n in range(n2):
+        if E[n] > 0:
+            wn = 0.0
+            for i in range(N):
+                for j, tt in ((p.nn_table[i, 0] - 1, p.t), (p.nnn_table[i, 0] - 1, p.tp),
+                              (p.nnn_table[i, 3] - 1, p.tp)):
+                    wn += tt * 2.0 * np.real(U[i + N, n] * np.conj(U[j + N, n]) - np.conj(U[i, n]) * U[j, n])
+            val_dia += wn * math.tanh(0.5 * beta * E[n]) / N
+    lam = 0.0
+    dc = 0.0
+    omega = julia_range(p.eta, p.domega, p.omega_max)
+    sigma = np.zeros(len(omega))
+    for n in range(n2):
+        for m in range(n2):
+            dE = E[m] - E[n]
+            J2 = abs(Jmn[n, m]) ** 2
+            ratio = beta * f[n] * (1 - f[n]) if abs(dE) < 1e-8 else (f[n] - f[m]) / dE
+            lam += ratio * J2
+            dc += beta * f[n] * (1 - f[n]) * J2 * lorentzian(dE, eta)
+            fnm = f[n] - f[m]
+            if abs(fnm) >= 1e-12:
+                sigma += fnm / omega * J2 * lorentzian(omega - dE, eta)
+    return dict(superfluid_stiffness=val_dia - lam / N, dc_conductivity=dc * math.pi / N,
+                optical_conductivity=sigma * math.pi / N)
+
+
+# ---------------------------------------------------------------------------
 # Closed forms (pins)
 # ---------------------------------------------------------------------------
 def bcs_rhs(Delta_in, Lx, Ly, t, tp, mu, beta, J):

@@ -75,6 +75,14 @@ class OracleContext:
     def get_state(self):
         return self.Delta.copy(), self.pi.copy()
 
+    def measure_transport(self, eta, domega, omega_max, chain=0):
+        p = dataclasses.replace(self.p, eta=eta, domega=domega, omega_max=omega_max)
+        cache = self.caches[chain]
+        O.update_H_BdG(cache, p, self.Delta[chain])
+        O.diagonalize_H_BdG(cache, p)
+        O.compute_forces(cache, p, self.Delta[chain])      # fermi_factors
+        return O.measure_transport_and_spectra(cache, p)
+
     def hmc_sweep(self, noise, uniform, Nt, dt, mass):
         p = dataclasses.replace(self.p, mass=mass)
         noise = self._chains(noise)

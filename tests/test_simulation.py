@@ -65,7 +65,19 @@ def test_run_simulation_driver_on_oracle(sim, hmc_mod, dwhmc, tmp_path):
         assert s in log, s
     rows = (tmp_path / "observables.csv").read_text().splitlines()
     assert rows[0] == sim.OBS_HEADER and len(rows) == 11
-    assert (tmp_path / "transport.csv").read_text().splitlines() == [sim.TRANSPORT_HEADER]
+    trows = (tmp_path / "transport.csv").read_text().splitlines()
+    assert trows[0] == sim.TRANSPORT_HEADER and len(trows) == 11      # measure_transport_freq = 1
+    for k, (i, spec) in enumerate(res.transport):
+        assert trows[k + 1] == sim.transport_csv_line(i, spec).rstrip("\n")
+    # bins of 5 (src/Simulation.jl:180-220): sweep_5 and sweep_10, the mean of their members
+    spec_dir = tmp_path / "spectra_bins"
+    assert sorted(os.listdir(spec_dir)) == ["omega_grid.npy", "params.json", "sweep_10.npz", "sweep_5.npz"]
+    b = np.load(spec_dir / "sweep_10.npz")
+    assert int(b["count"]) == 5
+    want = np.mean([s.optical_conductivity for _, s in res.transport[5:]], axis=0)
+    assert np.allclose(b["opt_cond"], want, rtol=1e-13, atol=0)
+    assert np.allclose(b["A_k0"], np.mean([s.A_k_omega0 for _, s in res.transport[5:]], axis=0))
+    assert len(np.load(spec_dir / "omega_grid.npy")) == len(b["opt_cond"])
     for k, (i, acc, dH, obs) in enumerate(res.records):
         assert rows[k + 1] == sim.obs_csv_line(i, acc, dH, obs).rstrip("\n")
         assert np.isfinite(obs.total_energy) and -1.0 <= obs.hole_conc <= 1.0
@@ -86,3 +98,11 @@ def test_run_simulation_device_matches_oracle(sim, hmc_mod, dwhmc, tmp_path):
         for f in ("total_energy", "Delta_amp", "Delta_local", "Delta_global", "S_Delta", "hole_conc",
                   "Delta_diff", "Delta_pair", "Delta_localpair"):
             assert abs(getattr(o1, f) - getattr(o2, f)) <= 1e-9, (i, f, getattr(o1, f), getattr(o2, f))
+    # transport rows of the same trajectory (device eigenpairs vs LAPACK)
+    assert len(dev.transport) == len(ref.transport) == 10
+    for (i, s1), (j, s2) in zip(dev.transport, ref.transport):
+        assert i == j
+        for f in ("superfluid_stiffness", "dc_conductivity"):
+            assert abs(getattr(s1, f) - getattr(s2, f)) <= 1e-8 * (1 + abs(getattr(s2, f))), (i, f)
+        assert np.max(np.abs(s1.optical_conductivity - s2.optical_conductivity)) <= \
+            1e-8 * (1 + np.max(np.abs(s2.optical_conductivity)))

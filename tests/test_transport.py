@@ -1,0 +1,231 @@
+"""Transport and spectra (src/Observables.jl:225-526), SURVEY.md §8(f) row 4.
+
+CPU (not gpu): the oracle restatement pinned three ways —
+  * vectorised form vs the reference's literal (n, m) loops;
+  * the reference's own consistency check scripts/debug_transport.jl:50-95:
+    the diamagnetic term in its tanh form (the one measure_transport_and_spectra
+    uses) equals its Fermi-factor form (particle-hole symmetry of H_BdG);
+  * Julia's float-range lengths for the ω grids.
+The reference ships no transport fixtures, so these plus the
+loop form are the pins; the absolute values are otherwise "parity unpinned"
+against a Julia run.
+
+GPU: the device path (rocSOLVER zheevd + rocBLAS zgemm + dwhmc_transport.hip)
+through the C ABI vs the oracle on the same Δ.  Tolerances (fp64):
+  * eigenvalues          |E_gpu - E_ref| ≤ 1e-12 (1 + max|E|)
+  * stiffness, dc        |Δ| ≤ 1e-9 (1 + |ref|)
+  * σ(ω), DOS, DOS_AN    max|Δ| ≤ 1e-9 (1 + max|ref|)
+  * A(k, 0)              max|Δ| ≤ 1e-9 (1 + max|ref|)
+Every quantity is a sum over eigenstates of functions of E_n only, weighted by
+basis-invariant sums inside degenerate subspaces, so eigenvector phases and
+the solver's basis choice inside degenerate levels do not enter.
+"""
+import numpy as np
+import pytest
+
+T, TP, MU = 1.0, -0.35, -1.08
+
+
+def _case(O, Lx, Ly, beta, seed, W=1.0, nimp=0.1, amp=0.25, mu=MU):
+    p = O.ModelParameters(Lx, Ly, T, TP, mu, W, nimp, beta, 0.8, 1.0)
+    rng = np.random.default_rng(seed)
+    st = O.initialize_state(p, rng)
+    N = p.N
+    D = st.Delta + amp * np.stack([np.ones(N), -np.ones(N)], 1) * np.exp(0.3j * rng.standard_normal((N, 1)))
+    return p, st.disorder_pot, D
+
+
+def _kinetic_weights(p, U):
+    """Per-state x-bond weights of src/Observables.jl:350-359 split into the
+    particle (u) and hole (v) parts."""
+    N = p.N
+    u, v = U[:N], U[N:]
+    i = np.arange(N)
+    wu = np.zeros(U.shape[1])
+    wv = np.zeros(U.shape[1])
+    for j, tt in ((p.nn_table[:, 0] - 1, p.t), (p.nnn_table[:, 0] - 1, p.tp), (p.nnn_table[:, 3] - 1, p.tp)):
+        wu += tt * 2.0 * np.real(np.conj(u[i]) * u[j]).sum(axis=0)
+        wv += tt * 2.0 * np.real(v[i] * np.conj(v[j])).sum(axis=0)
+    return wu, wv
+
+
+# --------------------------------------------------------------------------- CPU
+@pytest.mark.parametrize("Lx,Ly", [(4, 4), (3, 5), (2, 4)])
+def test_oracle_vectorised_matches_loops(oracle, Lx, Ly):
+    O = oracle
+    p, dis, D = _case(O, Lx, Ly, 8.0, seed=Lx * 10 + Ly)
+    cache, _, _ = O.evaluate(p, dis, D)
+    r = O.measure_transport_and_spectra(cache, p)
+    q = O.measure_transport_loops(cache, p)
+    for k in ("superfluid_stiffness", "dc_conductivity"):
+        assert abs(r[k] - q[k]) <= 1e-12 * (1 + abs(q[k])), k
+    s, sq = r["optical_conductivity"], q["optical_conductivity"]
+    assert np.max(np.abs(s - sq)) <= 1e-12 * (1 + np.max(np.abs(sq)))
+
+
+def test_diamagnetic_forms_agree(oracle):
+    """scripts/debug_transport.jl:9-95 (10x10 clean, β = 1000, μ = -1, uniform
+    d-wave Δx = 0.2, Δy = -0.2): Σ_{E>0} w_n tanh(βE_n/2) (the form
+    measure_transport_and_spectra uses) equals the Fermi-factor form
+    Σ_n [w^u_n f_n + w^v_n (1 - f_n)]; the ordered state has ρ_s > 0."""
+    O = oracle
+    p = O.ModelParameters(10, 10, 1.0, -0.35, -1.0, 0.0, 0.0, 1000.0, 1.6, 0.1)
+    N = p.N
+    D = np.stack([np.full(N, 0.2), np.full(N, -0.2)], 1).astype(np.complex128)
+    cache, _, _ = O.evaluate(p, np.zeros(N), D)
+    E, f = cache.E_n, cache.fermi_factors
+    wu, wv = _kinetic_weights(p, cache.U)
+    w = wv - wu
+    dia1 = float(np.sum(np.where(E > 0, w * np.tanh(0.5 * p.beta * np.maximum(E, 0.0)), 0.0))) / N
+    dia2 = float(np.sum(wu * f + wv * (1.0 - f))) / N
+    assert abs(dia1 - dia2) <= 1e-10 * (1 + abs(dia1)), (dia1, dia2)
+    r = O.measure_transport_and_spectra(cache, p)
+    assert r["superfluid_stiffness"] > 0, r["superfluid_stiffness"]
+
+
+def test_julia_range_lengths(oracle):
+    O = oracle
+    assert len(O.julia_range(0.01, 0.002, 4.0)) == 1996       # ω_min:Δω:ω_max (defaults)
+    assert len(O.julia_range(-4.0, 0.002, 4.0)) == 4001       # DOS grid
+    assert len(O.julia_range(0.0, 0.25, 1.0)) == 5
+    assert len(O.julia_range(0.0, 0.3, 1.0)) == 4             # 0, .3, .6, .9
+    assert len(O.julia_range(1.0, 0.5, 0.0)) == 0
+
+
+def test_current_operator(oracle):
+    """Hermitian, purely imaginary; duplicates summed (sparse()): on Lx = 2 the
+    +x and -x neighbours coincide and the current cancels."""
+    O = oracle
+    p = O.ModelParameters(4, 3, T, TP, MU, 0.0, 0.0, 4.0, 1.0, 1.0)
+    Jx = O.current_operator(p)
+    assert np.allclose(Jx, Jx.conj().T) and np.allclose(Jx.real, 0)
+    assert np.count_nonzero(Jx) == 6 * p.N
+    p2 = O.ModelParameters(2, 3, T, TP, MU, 0.0, 0.0, 4.0, 1.0, 1.0)
+    assert np.allclose(O.current_operator(p2), 0)
+
+
+# --------------------------------------------------------------------------- GPU
+def _ctx(dwhmc, p, dis, **kw):
+    return dwhmc.FermionContext(p.Lx, p.Ly, p.t, p.tp, p.mu, p.beta, p.J, p.nn_table, p.nnn_table,
+                                dis, **kw)
+
+
+def test_transport_grid_matches_julia(dwhmc, oracle):
+    """dwh_transport_grid is host arithmetic: no device needed."""
+    for args in ((0.01, 0.002, 4.0), (0.05, 0.01, 2.0), (0.02, 0.3, 1.0)):
+        nw, nd = dwhmc.transport_grid(*args)
+        assert nw == len(oracle.julia_range(args[0], args[1], args[2]))
+        assert nd == len(oracle.julia_range(-args[2], args[1], args[2]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("Lx,Ly", [(4, 4), (6, 6), (5, 7), (2, 4)])
+def test_eigensystem_matches_oracle(dwhmc, oracle, Lx, Ly):
+    O = oracle
+    p, dis, D = _case(O, Lx, Ly, 8.0, seed=Lx * 7 + Ly)
+    cache, _, _ = O.evaluate(p, dis, D)
+    ctx = _ctx(dwhmc, p, dis)
+    ctx.set_pairing(D)
+    E, U = ctx.eigensystem(0)
+    ctx.close()
+    Href = O.hermitian_from_upper(cache.H_base)
+    scale = 1 + np.max(np.abs(cache.E_n))
+    assert np.max(np.abs(E - cache.E_n)) <= 1e-12 * scale
+    assert np.max(np.abs(Href @ U - U * E[None, :])) <= 1e-11 * scale
+    assert np.max(np.abs(U.conj().T @ U - np.eye(2 * p.N))) <= 1e-12
+
+
+def _check_transport(r, ref):
+    for k in ("superfluid_stiffness", "dc_conductivity"):
+        assert abs(r[k] - ref[k]) <= 1e-9 * (1 + abs(ref[k])), (k, r[k], ref[k])
+    for k in ("optical_conductivity", "dos", "dos_AN", "A_k_omega0"):
+        a, b = np.asarray(r[k]), np.asarray(ref[k])
+        assert a.shape == b.shape, (k, a.shape, b.shape)
+        err = np.max(np.abs(a - b)) if a.size else 0.0
+        assert err <= 1e-9 * (1 + np.max(np.abs(b))), (k, err)
+    for k in ("omega_grid", "dos_omega_grid"):
+        assert np.array_equal(np.asarray(r[k]), ref[k]), k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("Lx,Ly,beta", [(4, 4, 8.0), (6, 6, 16.0), (5, 7, 4.0), (2, 4, 8.0), (8, 8, 16.0)])
+def test_transport_matches_oracle(dwhmc, oracle, Lx, Ly, beta):
+    O = oracle
+    p, dis, D = _case(O, Lx, Ly, beta, seed=Lx * 13 + Ly)
+    cache, _, _ = O.evaluate(p, dis, D)
+    ref = O.measure_transport_and_spectra(cache, p)
+    ctx = _ctx(dwhmc, p, dis)
+    ctx.set_pairing(D)
+    r = ctx.measure_transport(p.eta, p.domega, p.omega_max)
+    ctx.close()
+    _check_transport(r, ref)
+
+
+@pytest.mark.gpu
+def test_transport_coarse_grid_and_chain_select(dwhmc, oracle):
+    """Non-default η, Δω, ω_max; chain 1 of a batched context."""
+    O = oracle
+    p, dis, D = _case(O, 6, 4, 8.0, seed=64)
+    p.eta, p.domega, p.omega_max = 0.05, 0.01, 2.5
+    _, dis2, D2 = _case(O, 6, 4, 8.0, seed=65)
+    cache, _, _ = O.evaluate(p, dis2, D2)
+    ref = O.measure_transport_and_spectra(cache, p)
+    ctx = _ctx(dwhmc, p, np.stack([dis, dis2]))
+    ctx.set_pairing(np.stack([D, D2]))
+    r = ctx.measure_transport(p.eta, p.domega, p.omega_max, chain=1)
+    ctx.close()
+    _check_transport(r, ref)
+
+
+@pytest.mark.gpu
+def test_transport_L32_properties(dwhmc, oracle):
+    """BASELINE C3 size (N = 1024): device vs oracle at full size, plus the
+    size-independent checks ∫DOS dω ≈ 1 on the grid and A(k,0) ≥ 0."""
+    O = oracle
+    p, dis, D = _case(O, 32, 32, 16.0, seed=3232)
+    cache, _, _ = O.evaluate(p, dis, D)
+    ref = O.measure_transport_and_spectra(cache, p)
+    ctx = _ctx(dwhmc, p, dis)
+    ctx.set_pairing(D)
+    r = ctx.measure_transport(p.eta, p.domega, p.omega_max)
+    ctx.close()
+    _check_transport(r, ref)
+    assert np.min(r["A_k_omega0"]) >= 0
+    # sum rule: ∫ DOS dω over the grid = (1/N) Σ_n W_n ∫_{-ω_max}^{ω_max} L(ω - E_n) dω
+    # (the band reaches past ω_max, so this is < 1)
+    E, Wn = cache.E_n, np.sum(np.abs(cache.U[:p.N]) ** 2, axis=0)
+    inside = (np.arctan((p.omega_max - E) / p.eta) - np.arctan((-p.omega_max - E) / p.eta)) / np.pi
+    assert abs(np.sum(r["dos"]) * p.domega - np.sum(Wn * inside) / p.N) < 2e-3
+
+
+@pytest.mark.gpu
+def test_transport_argument_errors(dwhmc, oracle):
+    O = oracle
+    p, dis, D = _case(O, 4, 4, 8.0, seed=1)
+    ctx = _ctx(dwhmc, p, dis)
+    ctx.set_pairing(D)
+    with pytest.raises(ValueError):
+        ctx.measure_transport(-0.01, p.domega, p.omega_max)
+    with pytest.raises(ValueError):
+        ctx.measure_transport(p.eta, p.domega, p.omega_max, chain=3)
+    ctx.close()
+
+
+@pytest.mark.gpu
+def test_host_mirror_measure_transport_and_spectra(dwhmc, oracle):
+    """hmc.measure_transport_and_spectra(cache, p) mirrors the reference call
+    (src/Simulation.jl:171) on the state the cache's context holds."""
+    m, O = dwhmc, oracle
+    p = m.ModelParameters(6, 6, T, TP, MU, 1.0, 0.1, 8.0, 0.8, 1.0)
+    rng = np.random.default_rng(5)
+    st = m.initialize_state(p, rng)
+    cache = m.initialize_cache(p)
+    m.init_static_H(cache, p, st)
+    m.update_H_BdG(cache, p, st)
+    m.diagonalize_H_BdG(cache, p)
+    res = m.measure_transport_and_spectra(cache, p)
+    cache.ctx.close()
+    po = O.ModelParameters(6, 6, T, TP, MU, 1.0, 0.1, 8.0, 0.8, 1.0)
+    oc, _, _ = O.evaluate(po, st.disorder_pot, st.Delta)
+    ref = O.measure_transport_and_spectra(oc, po)
+    _check_transport({k: getattr(res, k) for k in ref}, ref)
