@@ -9,9 +9,9 @@
 // eigenvector of E_n is column n of U, as Julia's eigen! returns it).
 //
 // The O(n2^2 · n_ω) optical-conductivity sum is the only heavy kernel: every
-// thread owns one ω and streams the (ΔE, c) pairs of a chunk of columns
-// through LDS (one broadcast read per pair per wave), writing one partial per
-// (chunk, ω); a second kernel adds the chunks in a fixed order, so results are
+// thread owns one ω and streams the (ΔE, c ΔE) pairs of a chunk of rows through
+// LDS (one broadcast read per pair per wave), writing one partial per (chunk,
+// ω); a second kernel adds the chunks in a fixed order, so results are
 // deterministic run to run.
 #include "dwhmc_internal.h"
 
@@ -170,40 +170,61 @@ __device__ inline double grid_point(double start, double step, int k) {
   return __dadd_rn(start, __dmul_rn(step, (double)k));
 }
 
-// σ(ω) partials (:415-423): part[chunk][k] = Σ_{m in chunk, n} c_nm / ((ω_k - ΔE)^2 + η^2)
-// with c_nm = (f_n - f_m) |J_nm|^2 (0 where |f_n - f_m| < 1e-12), ΔE = E_m - E_n.
+// σ(ω) partials (:415-423).  The reference sums c_nm L(ω - ΔE_nm) / ω over all
+// ordered pairs with c_nm = (f_n - f_m) |J_nm|^2 (skipped where |f_n - f_m| <
+// 1e-12) and ΔE_nm = E_m - E_n.  The pair (m, n) has c_mn = -c_nm and ΔE_mn =
+// -ΔE_nm, so the two add up to
+//     c_nm [1/a - 1/b] = c_nm · 4ω ΔE_nm / (a b),  a, b = (ω ∓ ΔE_nm)^2 + η^2,
+// and σ(ω) = π/N · (1/π) η/ω · Σ_{ordered} = 4η/N · Σ_{n<m} c_nm ΔE_nm / (a b):
+// half the pairs, one reciprocal per pair, and no 1/ω at small ω.  With E
+// ascending, f_n - f_m vanishes (< 1e-12) for whole runs of m on either side
+// of the Fermi level; a 256-pair tile whose c are all zero is skipped.
+// Block (x, y): ω_k for k in the x tile, rows n in [y·rows, (y+1)·rows),
+// m > n read down column n of J_mn (|J_nm| = |J_mn|, J_mn Hermitian).
+__device__ inline double rcp_nr(double p) {
+  double r = __builtin_amdgcn_rcp(p);          // v_rcp_f64, then two Newton steps
+  r = fma(r, fma(-p, r, 1.0), r);
+  r = fma(r, fma(-p, r, 1.0), r);
+  return r;
+}
+
 __global__ void __launch_bounds__(kTB)
 k_tr_sigma(const double2* __restrict__ Jmn, int n2, const double* __restrict__ E,
            const double* __restrict__ f, double eta, double w_start, double w_step, int nw,
-           int cols, double* __restrict__ part) {
-  __shared__ double sdE[kTB], sc[kTB];
+           int rows, double* __restrict__ part) {
+  __shared__ double sdE[kTB], scd[kTB];
   const int tid = threadIdx.x;
   const int k = blockIdx.x * kTB + tid;
   const double w = grid_point(w_start, w_step, k < nw ? k : nw - 1);
   const double eta2 = eta * eta;
-  const int m0 = blockIdx.y * cols, m1 = min(m0 + cols, n2);
+  const int n0 = blockIdx.y * rows, n1 = min(n0 + rows, n2);
   double acc0 = 0, acc1 = 0;
-  for (int m = m0; m < m1; ++m) {
-    const double Em = E[m], fm = f[m];
-    for (int n0 = 0; n0 < n2; n0 += kTB) {
-      const int n = n0 + tid;
-      if (n < n2) {
-        const double2 j = Jmn[(size_t)m * n2 + n];
-        const double df = f[n] - fm;
-        sc[tid] = fabs(df) >= 1e-12 ? df * (j.x * j.x + j.y * j.y) : 0.0;
-        sdE[tid] = Em - E[n];
+  for (int n = n0; n < n1; ++n) {
+    const double En = E[n], fn = f[n];
+    const double2* col = Jmn + (size_t)n * n2;
+    for (int m0 = ((n + 1) / kTB) * kTB; m0 < n2; m0 += kTB) {
+      const int m = m0 + tid;
+      double cd = 0.0, dE = 0.0;
+      if (m > n && m < n2) {
+        const double df = fn - f[m];
+        if (fabs(df) >= 1e-12) {
+          const double2 j = col[m];
+          dE = E[m] - En;
+          cd = df * (j.x * j.x + j.y * j.y) * dE;
+        }
       }
+      if (!__syncthreads_or(cd != 0.0)) continue;
+      scd[tid] = cd;
+      sdE[tid] = dE;
       __syncthreads();
-      const int cnt = min(kTB, n2 - n0);
-      int q = 0;
-      for (; q + 1 < cnt; q += 2) {
-        const double d0 = w - sdE[q], d1 = w - sdE[q + 1];
-        acc0 += sc[q] / (d0 * d0 + eta2);
-        acc1 += sc[q + 1] / (d1 * d1 + eta2);
-      }
-      if (q < cnt) {
-        const double d0 = w - sdE[q];
-        acc0 += sc[q] / (d0 * d0 + eta2);
+#pragma unroll 4
+      for (int q = 0; q < kTB; q += 2) {
+        const double a0 = w - sdE[q], b0 = w + sdE[q];
+        const double a1 = w - sdE[q + 1], b1 = w + sdE[q + 1];
+        const double p0 = fma(a0, a0, eta2) * fma(b0, b0, eta2);
+        const double p1 = fma(a1, a1, eta2) * fma(b1, b1, eta2);
+        acc0 = fma(scd[q], rcp_nr(p0), acc0);
+        acc1 = fma(scd[q + 1], rcp_nr(p1), acc1);
       }
       __syncthreads();
     }
@@ -211,14 +232,14 @@ k_tr_sigma(const double2* __restrict__ Jmn, int n2, const double* __restrict__ E
   if (k < nw) part[(size_t)blockIdx.y * nw + k] = acc0 + acc1;
 }
 
-// σ(ω_k) = π/N Σ c/ω L(ω - ΔE) = η / (N ω) Σ_chunks part
-__global__ void k_tr_sigma_sum(const double* __restrict__ part, int nchunk, int nw, double eta,
-                               double w_start, double w_step, int N, double* __restrict__ sigma) {
+// σ(ω_k) = 4η/N Σ_chunks part
+__global__ void k_tr_sigma_sum(const double* __restrict__ part, int nchunk, int nw, double eta, int N,
+                               double* __restrict__ sigma) {
   const int k = blockIdx.x * kTB + threadIdx.x;
   if (k >= nw) return;
   double s = 0;
   for (int c = 0; c < nchunk; ++c) s += part[(size_t)c * nw + k];
-  sigma[k] = s * eta / ((double)N * grid_point(w_start, w_step, k));
+  sigma[k] = s * (4.0 * eta / N);
 }
 
 // out[0] = stiffness = Σ dia / N - Σ lam / N; out[1] = dc = Σ dc / N
@@ -296,12 +317,23 @@ __global__ void k_tr_dft_y(const double2* __restrict__ T, const double* __restri
   Pw[(size_t)n * N + idx] = w0[n] * (acc.x * acc.x + acc.y * acc.y);
 }
 
-// A_k[kx + Lx ky] = Σ_n Pw[k, n] / N, in n order
-__global__ void k_tr_ak_sum(const double* __restrict__ Pw, int n2, int N, double* __restrict__ ak) {
+// A_k[kx + Lx ky] = Σ_n Pw[k, n] / N in two fixed-order stages: slice y of
+// the n range into part[y][k], then the slices in order
+__global__ void k_tr_ak_part(const double* __restrict__ Pw, int n2, int N, int per,
+                             double* __restrict__ part) {
+  const int k = blockIdx.x * kTB + threadIdx.x;
+  if (k >= N) return;
+  const int n0 = blockIdx.y * per, n1 = min(n0 + per, n2);
+  double s = 0;
+  for (int n = n0; n < n1; ++n) s += Pw[(size_t)n * N + k];
+  part[(size_t)blockIdx.y * N + k] = s;
+}
+
+__global__ void k_tr_ak_sum(const double* __restrict__ part, int nsl, int N, double* __restrict__ ak) {
   const int k = blockIdx.x * kTB + threadIdx.x;
   if (k >= N) return;
   double s = 0;
-  for (int n = 0; n < n2; ++n) s += Pw[(size_t)n * N + k];
+  for (int c = 0; c < nsl; ++c) s += part[(size_t)c * N + k];
   ak[k] = s / N;
 }
 
@@ -336,12 +368,12 @@ void launch_tr_reduce(const TrBufs& b, int N, int Lx, int Ly, double beta, doubl
   hipLaunchKernelGGL(k_tr_pairs, dim3(n2), dim3(kTB), 0, s, b.Jmn, n2, b.E, b.f, beta, eta, b.lam,
                      b.dc);
   if (g.nw > 0) {
-    const int nchunk = tr_sigma_chunks(N), cols = cdiv(n2, nchunk);
-    const int used = cdiv(n2, cols);
+    const int nchunk = tr_sigma_chunks(N), rows = cdiv(n2, nchunk);
+    const int used = cdiv(n2, rows);
     hipLaunchKernelGGL(k_tr_sigma, dim3(cdiv(g.nw, kTB), used), dim3(kTB), 0, s, b.Jmn, n2, b.E,
-                       b.f, eta, g.w0, g.dw, g.nw, cols, b.part);
+                       b.f, eta, g.w0, g.dw, g.nw, rows, b.part);
     hipLaunchKernelGGL(k_tr_sigma_sum, dim3(cdiv(g.nw, kTB)), dim3(kTB), 0, s, b.part, used, g.nw,
-                       eta, g.w0, g.dw, N, b.sigma);
+                       eta, N, b.sigma);
   }
   hipLaunchKernelGGL(k_tr_scalars, dim3(1), dim3(kTB), 0, s, b.dia, b.lam, b.dc, n2, N, b.scalars);
   if (g.nd > 0)
@@ -351,7 +383,11 @@ void launch_tr_reduce(const TrBufs& b, int N, int Lx, int Ly, double beta, doubl
   hipLaunchKernelGGL(k_tr_dft_x, dim3(cdiv(N, kTB), n2), dim3(kTB), 0, s, b.U, n2, Lx, Ly, b.JU);
   double* Pw = reinterpret_cast<double*>(b.Jmn);
   hipLaunchKernelGGL(k_tr_dft_y, dim3(cdiv(N, kTB), n2), dim3(kTB), 0, s, b.JU, b.w0, Lx, Ly, Pw);
-  hipLaunchKernelGGL(k_tr_ak_sum, dim3(cdiv(N, kTB)), dim3(kTB), 0, s, Pw, n2, N, b.ak);
+  // slices of the n sum: partials into JU (free again after k_tr_dft_y)
+  const int per = 64, nsl = cdiv(n2, per);
+  double* akp = reinterpret_cast<double*>(b.JU);
+  hipLaunchKernelGGL(k_tr_ak_part, dim3(cdiv(N, kTB), nsl), dim3(kTB), 0, s, Pw, n2, N, per, akp);
+  hipLaunchKernelGGL(k_tr_ak_sum, dim3(cdiv(N, kTB)), dim3(kTB), 0, s, akp, nsl, N, b.ak);
 }
 
 }  // namespace dwh
