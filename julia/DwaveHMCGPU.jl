@@ -11,7 +11,7 @@ module DwaveHMCGPU
 using DwaveHMC
 using Random
 import DwaveHMC: init_static_H!, update_H_BdG!, diagonalize_H_BdG!, compute_forces!,
-                 compute_total_energy, hmc_sweep!
+                 compute_total_energy, hmc_sweep!, measure_transport_and_spectra
 
 const libdwhmc = get(ENV, "DWHMC_LIB", joinpath(@__DIR__, "..", "hybrid-monte-carlo-for-d-wave-sc_amd", "libdwhmc.so"))
 
@@ -112,6 +112,23 @@ function hmc_sweep!(cache::GPUCache, p::ModelParameters, state::SimulationState;
                                (Ptr{Cvoid}, Ptr{ComplexF64}, Ptr{ComplexF64}), cache.ctx, state.Δ, state.π))
     end
     return acc[] != 0, dH[]
+end
+
+# src/Observables.jl:314-526 on the device (eigenpairs by rocSOLVER, sums in HIP
+# kernels) for the Δ the context holds; same SpectrumResult.
+function measure_transport_and_spectra(cache::GPUCache, p::ModelParameters)
+    nw, nd = Ref{Int64}(0), Ref{Int64}(0)
+    check(C_NULL, ccall((:dwh_transport_grid, libdwhmc), Cint,
+                        (Float64, Float64, Float64, Ref{Int64}, Ref{Int64}), p.η, p.Δω, p.ω_max, nw, nd))
+    st, dc = Ref{Float64}(0.0), Ref{Float64}(0.0)
+    σ, dos, dos_AN = zeros(nw[]), zeros(nd[]), zeros(nd[])
+    ak = zeros(p.Lx, p.Ly)
+    check(cache.ctx, ccall((:dwh_measure_transport, libdwhmc), Cint,
+                           (Ptr{Cvoid}, Int64, Float64, Float64, Float64, Ref{Float64}, Ref{Float64},
+                            Ptr{Float64}, Int64, Ptr{Float64}, Ptr{Float64}, Int64, Ptr{Float64}),
+                           cache.ctx, 0, p.η, p.Δω, p.ω_max, st, dc, σ, nw[], dos, dos_AN, nd[], ak))
+    return DwaveHMC.SpectrumResult(st[], dc[], collect(p.ω_min:p.Δω:p.ω_max), σ,
+                                   collect(-p.ω_max:p.Δω:p.ω_max), dos, dos_AN, ak)
 end
 
 end # module
