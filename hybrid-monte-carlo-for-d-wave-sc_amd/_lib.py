@@ -82,6 +82,7 @@ SIGNATURES = {
     "dwh_eigensystem": (C.c_int, [_P, _I64, _P, _P]),
     "dwh_transport_grid": (C.c_int, [_D, _D, _D, C.POINTER(_I64), C.POINTER(_I64)]),
     "dwh_measure_transport": (C.c_int, [_P, _I64, _D, _D, _D, _DP, _DP, _P, _I64, _P, _P, _I64, _P]),
+    "dwh_measure_transport_batched": (C.c_int, [_P, _D, _D, _D, _P, _P, _P, _I64, _P, _P, _I64, _P]),
     "dwh_selftest_mfma": (C.c_int, [_I32]),
 }
 

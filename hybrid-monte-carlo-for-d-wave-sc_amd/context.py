@@ -197,6 +197,24 @@ class FermionContext:
                     dos_omega_grid=-omega_max + domega * np.arange(nd), dos=dos, dos_AN=dos_an,
                     A_k_omega0=ak.reshape(Ly, Lx).T.copy())
 
+    def measure_transport_all(self, eta: float, domega: float, omega_max: float) -> list:
+        """measure_transport for every chain, the eigensolves and J_mn
+        products batched (dwh_measure_transport_batched); one dict per chain."""
+        nw, nd = transport_grid(eta, domega, omega_max, self._lib)
+        Lx, Ly = self.info_lattice
+        nc = self.nchains
+        st, dc = np.empty(nc), np.empty(nc)
+        sigma, dos, dos_an = np.empty((nc, nw)), np.empty((nc, nd)), np.empty((nc, nd))
+        ak = np.empty((nc, Lx * Ly))
+        self._c(self._lib.dwh_measure_transport_batched(self._h, float(eta), float(domega), float(omega_max),
+                                                        ptr(st), ptr(dc), ptr(sigma), nw, ptr(dos),
+                                                        ptr(dos_an), nd, ptr(ak)))
+        wg, dg = eta + domega * np.arange(nw), -omega_max + domega * np.arange(nd)
+        return [dict(superfluid_stiffness=float(st[c]), dc_conductivity=float(dc[c]), omega_grid=wg.copy(),
+                     optical_conductivity=sigma[c].copy(), dos_omega_grid=dg.copy(), dos=dos[c].copy(),
+                     dos_AN=dos_an[c].copy(), A_k_omega0=ak[c].reshape(Ly, Lx).T.copy())
+                for c in range(nc)]
+
     # -- timing ----------------------------------------------------------
     TIMERS = ("gj_update", "gj_pivot", "assemble", "contract", "step", "gj_edge", "cr_gemm", "cr_inv")
 

@@ -410,7 +410,7 @@ struct dwh_ctx {
   // the rocBLAS handle (rocSOLVER zheevd, zgemm) runs on ctx->stream
   std::vector<int> tr_nbr, tr_rowptr, tr_col;
   std::vector<double> tr_val;
-  bool tr_ready = false;
+  int tr_slots = 0;   // chains the per-chain transport buffers hold
   rocblas_handle blas = nullptr;
   dwh::TrBufs tr{};
   int *d_tr_nbr = nullptr, *d_tr_rowptr = nullptr, *d_tr_col = nullptr, *d_tr_info = nullptr;
@@ -1086,24 +1086,20 @@ void drop_alloc(dwh_ctx* ctx, void* p) {
   (void)hipFree(p);
 }
 
-// device buffers + rocBLAS handle on first use; output buffers sized for (nw, nd)
-int transport_prepare(dwh_ctx* ctx, int64_t nw, int64_t nd) {
+// device buffers + rocBLAS handle on first use.  Buffers hold `slots` chains
+// (one slot per chain of a batched measurement), each slot laid out as
+// TrBufs; the σ partials are shared (chains are reduced one after another).
+int transport_prepare(dwh_ctx* ctx, int64_t nw, int64_t nd, int slots) {
   const int N = ctx->d.N;
   const size_t n2 = 2 * (size_t)N;
   dwh::TrBufs& b = ctx->tr;
   int rc = DWH_OK;
-  if (!ctx->tr_ready) {
+  if (!ctx->blas) {
     if (rocblas_create_handle(&ctx->blas) != rocblas_status_success)
       return fail(ctx, DWH_ERR_HIP, "rocblas_create_handle failed");
     if (rocblas_set_stream(ctx->blas, ctx->stream) != rocblas_status_success)
       return fail(ctx, DWH_ERR_HIP, "rocblas_set_stream failed");
-    if ((rc = dalloc(ctx, &b.U, n2 * n2)) || (rc = dalloc(ctx, &b.JU, n2 * n2)) ||
-        (rc = dalloc(ctx, &b.Jmn, n2 * n2)))
-      return rc;
-    for (double** p : {&b.E, &b.f, &b.dia, &b.Wn, &b.wan, &b.w0, &b.lam, &b.dc, &ctx->d_tr_offd})
-      if ((rc = dalloc(ctx, p, n2))) return rc;
-    if ((rc = dalloc(ctx, &b.ak, (size_t)N)) || (rc = dalloc(ctx, &b.scalars, 2)) ||
-        (rc = dalloc(ctx, &ctx->d_tr_info, 1)) || (rc = dalloc(ctx, &ctx->d_tr_nbr, ctx->tr_nbr.size())) ||
+    if ((rc = dalloc(ctx, &ctx->d_tr_nbr, ctx->tr_nbr.size())) ||
         (rc = dalloc(ctx, &ctx->d_tr_rowptr, ctx->tr_rowptr.size())) ||
         (rc = dalloc(ctx, &ctx->d_tr_col, ctx->tr_col.size())) ||
         (rc = dalloc(ctx, &ctx->d_tr_val, ctx->tr_val.size())))
@@ -1116,7 +1112,24 @@ int transport_prepare(dwh_ctx* ctx, int64_t nw, int64_t nd) {
     HIPCHECK(ctx, up(ctx->d_tr_col, ctx->tr_col.data(), ctx->tr_col.size() * sizeof(int)));
     HIPCHECK(ctx, up(ctx->d_tr_val, ctx->tr_val.data(), ctx->tr_val.size() * sizeof(double)));
     HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
-    ctx->tr_ready = true;
+  }
+  if (slots > ctx->tr_slots) {
+    HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+    for (void* q : {(void*)b.U, (void*)b.JU, (void*)b.Jmn, (void*)b.E, (void*)b.f, (void*)b.dia, (void*)b.Wn,
+                    (void*)b.wan, (void*)b.w0, (void*)b.lam, (void*)b.dc, (void*)ctx->d_tr_offd, (void*)b.ak,
+                    (void*)b.scalars, (void*)ctx->d_tr_info})
+      drop_alloc(ctx, q);
+    const size_t m = (size_t)slots;
+    if ((rc = dalloc(ctx, &b.U, m * n2 * n2)) || (rc = dalloc(ctx, &b.JU, m * n2 * n2)) ||
+        (rc = dalloc(ctx, &b.Jmn, m * n2 * n2)))
+      return rc;
+    for (double** q : {&b.E, &b.f, &b.dia, &b.Wn, &b.wan, &b.w0, &b.lam, &b.dc, &ctx->d_tr_offd})
+      if ((rc = dalloc(ctx, q, m * n2))) return rc;
+    if ((rc = dalloc(ctx, &b.ak, m * N)) || (rc = dalloc(ctx, &b.scalars, 2 * m)) ||
+        (rc = dalloc(ctx, &ctx->d_tr_info, m)))
+      return rc;
+    ctx->tr_slots = slots;
+    ctx->tr_nw = ctx->tr_nd = -1;   // per-slot outputs below are re-sized too
   }
   if (nw != ctx->tr_nw) {
     HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
@@ -1124,7 +1137,7 @@ int transport_prepare(dwh_ctx* ctx, int64_t nw, int64_t nd) {
     drop_alloc(ctx, b.sigma);
     b.part = b.sigma = nullptr;
     if ((rc = dalloc(ctx, &b.part, (size_t)dwh::tr_sigma_chunks(N) * nw)) ||
-        (rc = dalloc(ctx, &b.sigma, (size_t)nw)))
+        (rc = dalloc(ctx, &b.sigma, (size_t)ctx->tr_slots * nw)))
       return rc;
     ctx->tr_nw = nw;
   }
@@ -1133,38 +1146,124 @@ int transport_prepare(dwh_ctx* ctx, int64_t nw, int64_t nd) {
     drop_alloc(ctx, b.dos);
     drop_alloc(ctx, b.dos_an);
     b.dos = b.dos_an = nullptr;
-    if ((rc = dalloc(ctx, &b.dos, (size_t)nd)) || (rc = dalloc(ctx, &b.dos_an, (size_t)nd))) return rc;
+    if ((rc = dalloc(ctx, &b.dos, (size_t)ctx->tr_slots * nd)) ||
+        (rc = dalloc(ctx, &b.dos_an, (size_t)ctx->tr_slots * nd)))
+      return rc;
     ctx->tr_nd = nd;
   }
   return DWH_OK;
 }
 
-// dense H_BdG(Δ) of one chain -> rocSOLVER zheevd: eigenvalues ascending into
-// tr.E, eigenvectors into the columns of tr.U (diagonalize_H_BdG!,
-// src/Hamiltonian.jl:96-114; the reference's zheevr and zheevd agree to rounding)
-int eigen_enqueue(dwh_ctx* ctx, int64_t chain) {
+// the buffers of slot k
+dwh::TrBufs tr_slot(const dwh_ctx* ctx, int k) {
+  const size_t n2 = 2 * (size_t)ctx->d.N, N = ctx->d.N;
+  dwh::TrBufs b = ctx->tr;
+  const size_t mat = n2 * n2 * k, vec = n2 * k;
+  b.U += mat;
+  b.JU += mat;
+  b.Jmn += mat;
+  for (double** q : {&b.E, &b.f, &b.dia, &b.Wn, &b.wan, &b.w0, &b.lam, &b.dc}) *q += vec;
+  b.ak += N * k;
+  b.scalars += 2 * k;
+  b.sigma += (size_t)std::max<int64_t>(ctx->tr_nw, 0) * k;
+  b.dos += (size_t)std::max<int64_t>(ctx->tr_nd, 0) * k;
+  b.dos_an += (size_t)std::max<int64_t>(ctx->tr_nd, 0) * k;
+  return b;
+}
+
+// dense H_BdG(Δ) of chains c0 .. c0+m-1 into slots 0 .. m-1 -> rocSOLVER zheevd
+// (strided-batched for m > 1: its latency-bound panel kernels then cover every
+// chain at once): eigenvalues ascending into E, eigenvectors into the columns
+// of U (diagonalize_H_BdG!, src/Hamiltonian.jl:96-114; the reference's zheevr
+// and zheevd agree to rounding)
+int eigen_enqueue(dwh_ctx* ctx, int64_t c0, int m) {
   const int N = ctx->d.N, n2 = 2 * N;
-  dwh::TrBufs& b = ctx->tr;
-  HIPCHECK(ctx, hipMemsetAsync(b.U, 0, (size_t)n2 * n2 * sizeof(double2), ctx->stream));
-  dwh::launch_tr_assemble(b.U, N, ctx->hcol, ctx->hval + (size_t)chain * N * kHSlots, ctx->Dcol,
-                          ctx->Dsrc, ctx->Delta + (size_t)chain * 2 * N, ctx->stream);
+  const dwh::TrBufs& b = ctx->tr;
+  const int64_t sA = (int64_t)n2 * n2;
+  HIPCHECK(ctx, hipMemsetAsync(b.U, 0, (size_t)m * sA * sizeof(double2), ctx->stream));
+  for (int k = 0; k < m; ++k)
+    dwh::launch_tr_assemble(b.U + k * sA, N, ctx->hcol, ctx->hval + (size_t)(c0 + k) * N * kHSlots,
+                            ctx->Dcol, ctx->Dsrc, ctx->Delta + (size_t)(c0 + k) * 2 * N, ctx->stream);
   HIPCHECK(ctx, hipGetLastError());
+  auto* A = reinterpret_cast<rocblas_double_complex*>(b.U);
   const rocblas_status st =
-      rocsolver_zheevd(ctx->blas, rocblas_evect_original, rocblas_fill_upper, n2,
-                       reinterpret_cast<rocblas_double_complex*>(b.U), n2, b.E, ctx->d_tr_offd,
-                       ctx->d_tr_info);
+      m == 1 ? rocsolver_zheevd(ctx->blas, rocblas_evect_original, rocblas_fill_upper, n2, A, n2, b.E,
+                                ctx->d_tr_offd, ctx->d_tr_info)
+             : rocsolver_zheevd_strided_batched(ctx->blas, rocblas_evect_original, rocblas_fill_upper, n2, A,
+                                                n2, sA, b.E, n2, ctx->d_tr_offd, n2, ctx->d_tr_info, m);
   if (st != rocblas_status_success)
     return fail(ctx, DWH_ERR_HIP, std::string("rocsolver_zheevd: ") + rocblas_status_to_string(st));
   return DWH_OK;
 }
 
-int eigen_info_check(dwh_ctx* ctx) {
-  int info = 0;
-  HIPCHECK(ctx, hipMemcpyAsync(&info, ctx->d_tr_info, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+int eigen_info_check(dwh_ctx* ctx, int m) {
+  std::vector<int> info(m, 0);
+  HIPCHECK(ctx, hipMemcpyAsync(info.data(), ctx->d_tr_info, m * sizeof(int), hipMemcpyDeviceToHost,
+                               ctx->stream));
   HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
   HIPCHECK(ctx, hipGetLastError());
-  if (info != 0)
-    return fail(ctx, DWH_ERR_HIP, "rocsolver_zheevd did not converge (info = " + std::to_string(info) + ")");
+  for (int k = 0; k < m; ++k)
+    if (info[k] != 0)
+      return fail(ctx, DWH_ERR_HIP, "rocsolver_zheevd did not converge (info = " + std::to_string(info[k]) + ")");
+  return DWH_OK;
+}
+
+int transport_args(dwh_ctx* ctx, double eta, double domega, double omega_max, int64_t n_omega, int64_t n_dos,
+                   int64_t* nw, int64_t* nd) {
+  if (dwh_transport_grid(eta, domega, omega_max, nw, nd) != DWH_OK)
+    return fail(ctx, DWH_ERR_ARG, g_create_error);
+  if (n_omega != *nw || n_dos != *nd)
+    return fail(ctx, DWH_ERR_ARG, "n_omega / n_dos differ from dwh_transport_grid (" + std::to_string(*nw) +
+                                      ", " + std::to_string(*nd) + ")");
+  return DWH_OK;
+}
+
+// measure_transport_and_spectra for chains c0 .. c0+m-1 (slots 0 .. m-1);
+// outputs per chain at strides 1 / nw / nd / N
+int transport_run(dwh_ctx* ctx, int64_t c0, int m, double eta, double domega, double omega_max, int64_t nw,
+                  int64_t nd, double* stiffness, double* dc_cond, double* sigma, double* dos, double* dos_an,
+                  double* ak0) {
+  int rc;
+  if ((rc = transport_prepare(ctx, nw, nd, m))) return rc;
+  if ((rc = eigen_enqueue(ctx, c0, m))) return rc;
+  const int N = ctx->d.N, n2 = 2 * N;
+  const int64_t sA = (int64_t)n2 * n2;
+  hipStream_t s = ctx->stream;
+  for (int k = 0; k < m; ++k) {
+    const dwh::TrBufs b = tr_slot(ctx, k);
+    dwh::launch_tr_colstats(b.U, N, (int)ctx->Lx, b.E, ctx->beta, eta, ctx->t, ctx->tp, ctx->d_tr_nbr, b.f,
+                            b.dia, b.Wn, b.wan, b.w0, s);
+    dwh::launch_tr_current(b.U, b.JU, N, ctx->d_tr_rowptr, ctx->d_tr_col, ctx->d_tr_val, s);
+  }
+  HIPCHECK(ctx, hipGetLastError());
+  // J_mn = U^H (J ⊕ J) U  (src/Observables.jl:334-335)
+  const rocblas_double_complex one(1.0, 0.0), zero(0.0, 0.0);
+  const dwh::TrBufs& b0 = ctx->tr;
+  const rocblas_status st = rocblas_zgemm_strided_batched(
+      ctx->blas, rocblas_operation_conjugate_transpose, rocblas_operation_none, n2, n2, n2, &one,
+      reinterpret_cast<const rocblas_double_complex*>(b0.U), n2, sA,
+      reinterpret_cast<const rocblas_double_complex*>(b0.JU), n2, sA, &zero,
+      reinterpret_cast<rocblas_double_complex*>(b0.Jmn), n2, sA, m);
+  if (st != rocblas_status_success)
+    return fail(ctx, DWH_ERR_HIP, std::string("rocblas_zgemm: ") + rocblas_status_to_string(st));
+  const dwh::TrGrid g{eta, -omega_max, domega, (int)nw, (int)nd};
+  for (int k = 0; k < m; ++k)
+    dwh::launch_tr_reduce(tr_slot(ctx, k), N, (int)ctx->Lx, (int)ctx->Ly, ctx->beta, eta, g, s);
+  HIPCHECK(ctx, hipGetLastError());
+  std::vector<double> sc(2 * (size_t)m);
+  HIPCHECK(ctx, hipMemcpyAsync(sc.data(), b0.scalars, sc.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+  if (nw > 0)
+    HIPCHECK(ctx, hipMemcpyAsync(sigma, b0.sigma, m * nw * sizeof(double), hipMemcpyDeviceToHost, s));
+  if (nd > 0) {
+    HIPCHECK(ctx, hipMemcpyAsync(dos, b0.dos, m * nd * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPCHECK(ctx, hipMemcpyAsync(dos_an, b0.dos_an, m * nd * sizeof(double), hipMemcpyDeviceToHost, s));
+  }
+  HIPCHECK(ctx, hipMemcpyAsync(ak0, b0.ak, (size_t)m * N * sizeof(double), hipMemcpyDeviceToHost, s));
+  if ((rc = eigen_info_check(ctx, m))) return rc;
+  for (int k = 0; k < m; ++k) {
+    stiffness[k] = sc[2 * k];
+    dc_cond[k] = sc[2 * k + 1];
+  }
   return DWH_OK;
 }
 
@@ -1188,15 +1287,15 @@ int dwh_eigensystem(dwh_ctx* ctx, int64_t chain, double* E, dwh_c128* U) {
   if (chain < 0 || chain >= ctx->d.nc) return fail(ctx, DWH_ERR_ARG, "chain index out of range");
   HIPCHECK(ctx, hipSetDevice(ctx->device));
   int rc;
-  if ((rc = transport_prepare(ctx, std::max<int64_t>(ctx->tr_nw, 0), std::max<int64_t>(ctx->tr_nd, 0))))
+  if ((rc = transport_prepare(ctx, std::max<int64_t>(ctx->tr_nw, 0), std::max<int64_t>(ctx->tr_nd, 0), 1)))
     return rc;
-  if ((rc = eigen_enqueue(ctx, chain))) return rc;
+  if ((rc = eigen_enqueue(ctx, chain, 1))) return rc;
   const size_t n2 = 2 * (size_t)ctx->d.N;
   HIPCHECK(ctx, hipMemcpyAsync(E, ctx->tr.E, n2 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
   if (U)
     HIPCHECK(ctx, hipMemcpyAsync(U, ctx->tr.U, n2 * n2 * sizeof(double2), hipMemcpyDeviceToHost,
                                  ctx->stream));
-  return eigen_info_check(ctx);
+  return eigen_info_check(ctx, 1);
 }
 
 int dwh_measure_transport(dwh_ctx* ctx, int64_t chain, double eta, double domega, double omega_max,
@@ -1205,46 +1304,34 @@ int dwh_measure_transport(dwh_ctx* ctx, int64_t chain, double eta, double domega
   if (!ctx || !stiffness || !dc_cond || !ak0) return fail(ctx, DWH_ERR_ARG, "NULL argument");
   if (chain < 0 || chain >= ctx->d.nc) return fail(ctx, DWH_ERR_ARG, "chain index out of range");
   int64_t nw = 0, nd = 0;
-  if (dwh_transport_grid(eta, domega, omega_max, &nw, &nd) != DWH_OK)
-    return fail(ctx, DWH_ERR_ARG, g_create_error);
-  if (n_omega != nw || n_dos != nd)
-    return fail(ctx, DWH_ERR_ARG, "n_omega / n_dos differ from dwh_transport_grid (" + std::to_string(nw) +
-                                      ", " + std::to_string(nd) + ")");
+  int rc;
+  if ((rc = transport_args(ctx, eta, domega, omega_max, n_omega, n_dos, &nw, &nd))) return rc;
   if ((nw > 0 && !sigma) || (nd > 0 && (!dos || !dos_an))) return fail(ctx, DWH_ERR_ARG, "NULL grid output");
   HIPCHECK(ctx, hipSetDevice(ctx->device));
+  return transport_run(ctx, chain, 1, eta, domega, omega_max, nw, nd, stiffness, dc_cond, sigma, dos, dos_an,
+                       ak0);
+}
+
+int dwh_measure_transport_batched(dwh_ctx* ctx, double eta, double domega, double omega_max,
+                                  double* stiffness, double* dc_cond, double* sigma, int64_t n_omega,
+                                  double* dos, double* dos_an, int64_t n_dos, double* ak0) {
+  if (!ctx || !stiffness || !dc_cond || !ak0) return fail(ctx, DWH_ERR_ARG, "NULL argument");
+  int64_t nw = 0, nd = 0;
   int rc;
-  if ((rc = transport_prepare(ctx, nw, nd))) return rc;
-  if ((rc = eigen_enqueue(ctx, chain))) return rc;
-  const int N = ctx->d.N, n2 = 2 * N;
-  dwh::TrBufs& b = ctx->tr;
-  hipStream_t s = ctx->stream;
-  dwh::launch_tr_colstats(b.U, N, (int)ctx->Lx, b.E, ctx->beta, eta, ctx->t, ctx->tp, ctx->d_tr_nbr, b.f,
-                          b.dia, b.Wn, b.wan, b.w0, s);
-  dwh::launch_tr_current(b.U, b.JU, N, ctx->d_tr_rowptr, ctx->d_tr_col, ctx->d_tr_val, s);
-  HIPCHECK(ctx, hipGetLastError());
-  // J_mn = U^H (J ⊕ J) U  (src/Observables.jl:334-335)
-  const rocblas_double_complex one(1.0, 0.0), zero(0.0, 0.0);
-  const rocblas_status st = rocblas_zgemm(
-      ctx->blas, rocblas_operation_conjugate_transpose, rocblas_operation_none, n2, n2, n2, &one,
-      reinterpret_cast<const rocblas_double_complex*>(b.U), n2,
-      reinterpret_cast<const rocblas_double_complex*>(b.JU), n2, &zero,
-      reinterpret_cast<rocblas_double_complex*>(b.Jmn), n2);
-  if (st != rocblas_status_success)
-    return fail(ctx, DWH_ERR_HIP, std::string("rocblas_zgemm: ") + rocblas_status_to_string(st));
-  const dwh::TrGrid g{eta, -omega_max, domega, (int)nw, (int)nd};
-  dwh::launch_tr_reduce(b, N, (int)ctx->Lx, (int)ctx->Ly, ctx->beta, eta, g, s);
-  HIPCHECK(ctx, hipGetLastError());
-  double sc[2];
-  HIPCHECK(ctx, hipMemcpyAsync(sc, b.scalars, sizeof(sc), hipMemcpyDeviceToHost, s));
-  if (nw > 0) HIPCHECK(ctx, hipMemcpyAsync(sigma, b.sigma, nw * sizeof(double), hipMemcpyDeviceToHost, s));
-  if (nd > 0) {
-    HIPCHECK(ctx, hipMemcpyAsync(dos, b.dos, nd * sizeof(double), hipMemcpyDeviceToHost, s));
-    HIPCHECK(ctx, hipMemcpyAsync(dos_an, b.dos_an, nd * sizeof(double), hipMemcpyDeviceToHost, s));
+  if ((rc = transport_args(ctx, eta, domega, omega_max, n_omega, n_dos, &nw, &nd))) return rc;
+  if ((nw > 0 && !sigma) || (nd > 0 && (!dos || !dos_an))) return fail(ctx, DWH_ERR_ARG, "NULL grid output");
+  HIPCHECK(ctx, hipSetDevice(ctx->device));
+  // chains in groups whose three n2 x n2 work matrices fit in 16 GiB
+  const int N = ctx->d.N, nc = ctx->d.nc;
+  const double per = 3.0 * 16.0 * 4.0 * N * (double)N;
+  const int group = std::max(1, std::min(nc, (int)(16.0 * (1 << 30) / per)));
+  for (int c0 = 0; c0 < nc; c0 += group) {
+    const int m = std::min(group, nc - c0);
+    if ((rc = transport_run(ctx, c0, m, eta, domega, omega_max, nw, nd, stiffness + c0, dc_cond + c0,
+                            sigma ? sigma + (size_t)c0 * nw : nullptr, dos ? dos + (size_t)c0 * nd : nullptr,
+                            dos_an ? dos_an + (size_t)c0 * nd : nullptr, ak0 + (size_t)c0 * N)))
+      return rc;
   }
-  HIPCHECK(ctx, hipMemcpyAsync(ak0, b.ak, (size_t)N * sizeof(double), hipMemcpyDeviceToHost, s));
-  if ((rc = eigen_info_check(ctx))) return rc;
-  *stiffness = sc[0];
-  *dc_cond = sc[1];
   return DWH_OK;
 }
 

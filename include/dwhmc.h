@@ -179,6 +179,15 @@ int dwh_measure_transport(dwh_ctx* ctx, int64_t chain, double eta, double domega
                           double* stiffness, double* dc_cond, double* sigma, int64_t n_omega,
                           double* dos, double* dos_an, int64_t n_dos, double* ak0);
 
+/* dwh_measure_transport for every chain of the context at once: the
+ * eigensolves and J_mn products are batched (rocSOLVER / rocBLAS
+ * strided-batched), which at n = 2048 costs ~1/3 per chain of separate calls.
+ * Outputs per chain c at stiffness[c], dc_cond[c], sigma[c*n_omega],
+ * dos[c*n_dos], dos_an[c*n_dos], ak0[c*Lx*Ly]. */
+int dwh_measure_transport_batched(dwh_ctx* ctx, double eta, double domega, double omega_max,
+                                  double* stiffness, double* dc_cond, double* sigma, int64_t n_omega,
+                                  double* dos, double* dos_an, int64_t n_dos, double* ak0);
+
 /* Self-test of the f64 MFMA fragment layout (A = I, asymmetric B); 0 = pass. */
 int dwh_selftest_mfma(int32_t device);
 

@@ -178,6 +178,25 @@ def test_transport_coarse_grid_and_chain_select(dwhmc, oracle):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("Lx,Ly,nc", [(6, 4, 3), (16, 16, 4)])
+def test_transport_batched_matches_per_chain(dwhmc, oracle, Lx, Ly, nc):
+    """dwh_measure_transport_batched (strided-batched eigensolves) = per-chain
+    dwh_measure_transport = oracle, for every chain of a batched context."""
+    O = oracle
+    cases = [_case(O, Lx, Ly, 8.0, seed=500 + c) for c in range(nc)]
+    p = cases[0][0]
+    ctx = _ctx(dwhmc, p, np.stack([c[1] for c in cases]))
+    ctx.set_pairing(np.stack([c[2] for c in cases]))
+    allr = ctx.measure_transport_all(p.eta, p.domega, p.omega_max)
+    one = ctx.measure_transport(p.eta, p.domega, p.omega_max, chain=nc - 1)
+    ctx.close()
+    _check_transport(allr[nc - 1], one)
+    for c, (pc, dis, D) in enumerate(cases):
+        cache, _, _ = O.evaluate(pc, dis, D)
+        _check_transport(allr[c], O.measure_transport_and_spectra(cache, pc))
+
+
+@pytest.mark.gpu
 def test_transport_L32_properties(dwhmc, oracle):
     """BASELINE C3 size (N = 1024): device vs oracle at full size, plus the
     size-independent checks ∫DOS dω ≈ 1 on the grid and A(k,0) ≥ 0."""

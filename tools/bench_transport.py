@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--cpu", action="store_true", help="also time the CPU restatement")
     ap.add_argument("--cpu-omega", type=int, default=40, help="ω points of the CPU σ sample")
+    ap.add_argument("--chains", type=int, default=4, help="chains of the batched measurement")
     a = ap.parse_args()
 
     import dwhmc_loader
@@ -57,6 +58,17 @@ def main():
         ctx.eigensystem(0, vectors=False)
     t_eig = (time.perf_counter() - t0) / a.steps
     ctx.close()
+    # batched: --chains chains in one context, dwh_measure_transport_batched
+    nc = a.chains
+    ctxb = m.FermionContext(p.Lx, p.Ly, p.t, p.tp, p.mu, p.beta, p.J, p.nn_table, p.nnn_table,
+                            np.stack([st.disorder_pot] * nc))
+    ctxb.set_pairing(np.stack([D] * nc))
+    ctxb.measure_transport_all(p.eta, p.domega, p.omega_max)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        ctxb.measure_transport_all(p.eta, p.domega, p.omega_max)
+    t_batch = (time.perf_counter() - t0) / a.steps
+    ctxb.close()
     nw, nd = len(r["omega_grid"]), len(r["dos_omega_grid"])
     n2 = 2 * N
     out = {
@@ -65,6 +77,7 @@ def main():
         "config": {"workload": f"measure_transport_and_spectra {L}x{L} beta={a.beta}", "n2": n2,
                    "n_omega": nw, "n_dos": nd},
         "sigma_pair_terms": n2 * n2 * nw,
+        "batched": {"chains": nc, "ms_per_call": 1e3 * t_batch, "ms_per_chain": 1e3 * t_batch / nc},
     }
     if a.cpu:
         from oracle import dwhmc_oracle as O
