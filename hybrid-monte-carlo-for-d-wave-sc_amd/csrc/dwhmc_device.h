@@ -8,6 +8,10 @@
 
 #include <utility>
 
+#ifndef DWHMC_INV_PERMLANE
+#define DWHMC_INV_PERMLANE 0
+#endif
+
 namespace dwh {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
@@ -160,7 +164,16 @@ __device__ __forceinline__ unsigned bcast_quarter_u32(unsigned u) {
 template <int QS>
 __device__ __forceinline__ double bcast_quarter(double x) {
   const unsigned long long b = __builtin_bit_cast(unsigned long long, x);
+#if DWHMC_INV_PERMLANE
   const unsigned lo = bcast_quarter_u32<QS>((unsigned)b), hi = bcast_quarter_u32<QS>((unsigned)(b >> 32));
+#else
+  // one LDS-crossbar permute per dword (no LDS storage): lane l reads lane
+  // 16 QS + (l & 15); 2 instructions per double instead of ~6 with the
+  // permlane swaps and their register copies (the inversion is issue-bound)
+  const int src = ((QS << 4) | (threadIdx.x & 15)) << 2;
+  const unsigned lo = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)(unsigned)b);
+  const unsigned hi = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)(unsigned)(b >> 32));
+#endif
   return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
 }
 __device__ __forceinline__ double readlane_f64(double x, int lane) {
@@ -181,7 +194,8 @@ __device__ __forceinline__ void inv16_step(double2 (&a)[4], double& pprod) {
 #pragma unroll
   for (int jj = 0; jj < 4; ++jj) rowp[jj] = make_double2(dpp_rowbcast<P>(a[jj].x), dpp_rowbcast<P>(a[jj].y));
   const double2 colp = make_double2(bcast_quarter<PS>(a[PE].x), bcast_quarter<PS>(a[PE].y));
-  const double2 piv = make_double2(readlane_f64(colp.x, P), readlane_f64(colp.y, P));
+  // the pivot straight from its owner lane, off the column broadcast's chain
+  const double2 piv = make_double2(readlane_f64(a[PE].x, PS * 16 + P), readlane_f64(a[PE].y, PS * 16 + P));
   const double m2 = fma(piv.x, piv.x, piv.y * piv.y);
   const double s = rcp_nr(m2);
   const double2 inv = make_double2(piv.x * s, -piv.y * s);
