@@ -8,6 +8,9 @@
 
 #include <utility>
 
+#ifndef DWHMC_INV_FOLD
+#define DWHMC_INV_FOLD 1
+#endif
 #ifndef DWHMC_INV_PERMLANE
 #define DWHMC_INV_PERMLANE 0
 #endif
@@ -200,11 +203,22 @@ __device__ __forceinline__ void inv16_step(double2 (&a)[4], double& pprod) {
   const double s = rcp_nr(m2);
   const double2 inv = make_double2(piv.x * s, -piv.y * s);
   pprod *= m2;
+  const bool prow = (r == P);
+#if DWHMC_INV_FOLD
+  // Select-free form: one update a <- a - f rowp' for every entry.  On the
+  // pivot row colp' = piv - 1, so f = (piv - 1)/piv = 1 - 1/piv and the row
+  // becomes a_p / piv; in column p rowp' = piv + 1, so the column becomes
+  // colp - f (piv + 1) = -colp/piv (1/piv on the pivot row) up to one rounding
+  // of colp - f piv.  Replaces ~12 per-lane selects by two adds.
+  const double2 fi = cmul(make_double2(colp.x - (prow ? 1.0 : 0.0), colp.y), inv);
+  rowp[PE].x += (q == PS) ? 1.0 : 0.0;
+  const double2 f = fi;
+#else
   // one update formula for every row: a <- a - f rowp with f = colp/piv, and
   // f = 1 - 1/piv on the pivot row (a_p - (1 - 1/piv) a_p = a_p / piv)
-  const bool prow = (r == P);
   const double2 fi = cmul(colp, inv);
   const double2 f = prow ? make_double2(1.0 - inv.x, -inv.y) : fi;
+#endif
 #pragma unroll
   for (int jj = 0; jj < 4; ++jj) {
     const double2 x = rowp[jj];
@@ -213,8 +227,10 @@ __device__ __forceinline__ void inv16_step(double2 (&a)[4], double& pprod) {
     v.y = fma(-f.x, x.y, fma(-f.y, x.x, a[jj].y));
     a[jj] = v;
   }
+#if !DWHMC_INV_FOLD
   // column p: 1/piv on the pivot row, -colp/piv elsewhere
   if (q == PS) a[PE] = prow ? inv : make_double2(-fi.x, -fi.y);
+#endif
 }
 
 template <bool STRIDED, int... Ps>
