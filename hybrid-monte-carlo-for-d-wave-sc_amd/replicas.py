@@ -6,6 +6,10 @@ every sweep it records 11 fp64 per chain — accepted, dH and the nine fields of
 ObservablesResult (src/Observables.jl:70-80) — and the records are gathered
 to rank 0 with torch.distributed (RCCL on MI355X, gloo in CPU tests), which
 writes the reference's observables.csv format (src/Simulation.jl:71,161-166).
+With transport_freq > 0 every rank also measures transport every
+transport_freq sweeps for all its chains at once
+(dwh_measure_transport_batched) and the (stiffness, dc) scalars are gathered
+the same way into transport.csv (src/Simulation.jl:73,171-177).
 """
 from __future__ import annotations
 
@@ -48,16 +52,22 @@ class ReplicaConfig:
     n_sweeps: int = 10
     Nt: int = 10
     seed: int = 1000
+    transport_freq: int = 0   # measure_transport_and_spectra every k sweeps (0: never)
 
 
 def replica_seed(cfg: ReplicaConfig, rank: int, chain: int) -> int:
     return cfg.seed + rank * cfg.chains + chain
 
 
+N_TR = 3   # transport record: sweep, superfluid stiffness, dc conductivity
+
+
 def run_local(p, cfg: ReplicaConfig, rank: int, device: int, make_context, initialize_state,
-              calc_optimal_dt):
+              calc_optimal_dt, transport_out: list | None = None):
     """Run cfg.n_sweeps HMC sweeps for this rank's chains; returns
-    (n_sweeps, chains, N_OBS).  `make_context(disorder) -> FermionContext`."""
+    (n_sweeps, chains, N_OBS).  `make_context(disorder) -> FermionContext`.
+    With cfg.transport_freq > 0, one (chains, N_TR) array per transport
+    measurement is appended to transport_out."""
     dis, D0, rngs = [], [], []
     for c in range(cfg.chains):
         rng = np.random.default_rng(replica_seed(cfg, rank, c))
@@ -83,6 +93,10 @@ def run_local(p, cfg: ReplicaConfig, rank: int, device: int, make_context, initi
             out[s, c, 0] = float(acc[c])
             out[s, c, 1] = dH[c]
             out[s, c, 2:] = observables_from_outputs(p, D[c], P[c], Ef[c], tr[c])
+        if cfg.transport_freq > 0 and transport_out is not None and (s + 1) % cfg.transport_freq == 0:
+            spec = ctx.measure_transport_all(p.eta, p.domega, p.omega_max)
+            transport_out.append(np.array([[s + 1, r["superfluid_stiffness"], r["dc_conductivity"]]
+                                           for r in spec]))
     ctx.close()
     return out
 
@@ -118,6 +132,17 @@ def write_observables_csv(path: str, records: np.ndarray):
                 x = records[r, s]
                 f.write("%d,%d,%d,%.5e,%.6f,%.6f,%.6f,%.6f,%.6f,%.6f,%.6f,%.6f,%.6f\n" %
                         (r, s + 1, int(x[0]), x[1], *x[2:]))
+
+
+def write_transport_csv(path: str, records: np.ndarray):
+    """transport.csv (src/Simulation.jl:73,174-177) with a Replica column;
+    records: (replica chains, measurements, N_TR)."""
+    with open(path, "w") as f:
+        f.write("Replica,Sweep,Superfluid_Stiffness,DC_Conductivity\n")
+        for r in range(records.shape[0]):
+            for m in range(records.shape[1]):
+                x = records[r, m]
+                f.write("%d,%d,%.6f,%.6f\n" % (r, int(x[0]), x[1], x[2]))
 
 
 # Launcher: tools/run_replicas.py (python -m torch.distributed.run ... tools/run_replicas.py)

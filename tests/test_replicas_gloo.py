@@ -38,6 +38,10 @@ class FakeContext:
     def hole_trace(self):
         return np.full(self.nchains, 0.4 * self.N)
 
+    def measure_transport_all(self, eta, domega, omega_max):
+        return [dict(superfluid_stiffness=float(np.abs(self.D[c]).sum()),
+                     dc_conductivity=float(self.dis[c].sum() + eta)) for c in range(self.nchains)]
+
     def close(self):
         pass
 
@@ -56,8 +60,11 @@ def _local(rank):
     from importlib import import_module
     rep = import_module(m.__name__ + ".replicas")
     p = m.ModelParameters(4, 4, 1.0, -0.35, -1.08, 1.0, 0.25, 4.0, 0.8, 1.0)
-    cfg = rep.ReplicaConfig(chains=2, n_sweeps=3, Nt=2)
-    return rep, rep.run_local(p, cfg, rank, 0, FakeContext, m.initialize_state, m.calc_optimal_dt)
+    cfg = rep.ReplicaConfig(chains=2, n_sweeps=3, Nt=2, transport_freq=2)
+    tr = []
+    obs = rep.run_local(p, cfg, rank, 0, FakeContext, m.initialize_state, m.calc_optimal_dt, transport_out=tr)
+    rep._test_transport = np.stack(tr)
+    return rep, obs
 
 
 def _worker(rank, world, port, out):
@@ -68,9 +75,12 @@ def _worker(rank, world, port, out):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     rep, local = _local(rank)
     rec = rep.gather_observables(local, dist)
+    trec = rep.gather_observables(rep._test_transport, dist)
     if rank == 0:
         np.save(out, rec)
+        np.save(out + ".tr.npy", trec)
         rep.write_observables_csv(out + ".csv", rec)
+        rep.write_transport_csv(out + ".tr.csv", trec)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -89,6 +99,15 @@ def test_two_rank_gather_matches_sequential(tmp_path):
     lines = open(out + ".csv").read().splitlines()
     assert lines[0].startswith("Replica,Sweep,Accepted,dH,Energy")
     assert len(lines) == 1 + 4 * 3
+    # transport every 2 sweeps of 3 -> one measurement per chain, gathered the same way
+    trec = np.load(out + ".tr.npy")
+    _local(0)
+    t0 = rep._test_transport
+    assert trec.shape == (4, 1, rep.N_TR)
+    assert np.array_equal(trec[:2], np.transpose(t0, (1, 0, 2)))
+    assert np.all(trec[:, 0, 0] == 2)
+    tl = open(out + ".tr.csv").read().splitlines()
+    assert tl[0] == "Replica,Sweep,Superfluid_Stiffness,DC_Conductivity" and len(tl) == 5
 
 
 def test_observables_from_outputs_matches_oracle(oracle, dwhmc):

@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--sweeps", type=int, default=10)
     ap.add_argument("--Nt", type=int, default=10)
     ap.add_argument("--seed", type=int, default=1000)
+    ap.add_argument("--transport-freq", type=int, default=0,
+                    help="measure transport every k sweeps (0: never) -> transport.csv")
     ap.add_argument("--out", default="runs/replicas")
     a = ap.parse_args()
 
@@ -49,19 +51,28 @@ def main():
             dist.init_process_group("gloo")
 
     p = m.ModelParameters(a.L, a.L, 1.0, -0.35, -1.08, 1.0, 0.05, a.beta, 0.8, 1.0)
-    cfg = rep.ReplicaConfig(chains=a.chains, n_sweeps=a.sweeps, Nt=a.Nt, seed=a.seed)
+    cfg = rep.ReplicaConfig(chains=a.chains, n_sweeps=a.sweeps, Nt=a.Nt, seed=a.seed,
+                            transport_freq=a.transport_freq)
 
     def make_context(disorder):
         return m.FermionContext(p.Lx, p.Ly, p.t, p.tp, p.mu, p.beta, p.J, p.nn_table, p.nnn_table,
                                 disorder, device=local)
 
-    local_rec = rep.run_local(p, cfg, rank, local, make_context, m.initialize_state, m.calc_optimal_dt)
+    tr_local = []
+    local_rec = rep.run_local(p, cfg, rank, local, make_context, m.initialize_state, m.calc_optimal_dt,
+                              transport_out=tr_local)
     allrec = rep.gather_observables(local_rec, dist if world > 1 else None, device)
+    alltr = None
+    if tr_local:
+        import numpy as np
+        alltr = rep.gather_observables(np.stack(tr_local), dist if world > 1 else None, device)
     if rank == 0:
         os.makedirs(a.out, exist_ok=True)
         path = os.path.join(a.out, "observables.csv")
         rep.write_observables_csv(path, allrec)
         print(f"{allrec.shape[0]} replica chains x {allrec.shape[1]} sweeps -> {path}", flush=True)
+        if alltr is not None:
+            rep.write_transport_csv(os.path.join(a.out, "transport.csv"), alltr)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
