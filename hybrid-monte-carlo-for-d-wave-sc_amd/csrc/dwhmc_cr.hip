@@ -278,7 +278,7 @@ __global__ __launch_bounds__(64 * NT) void k_cr_inv(double2* __restrict__ pool, 
   };
   if (w == 0) ld += invert(ar[0], ai[0]);
   CR_STAMP(2);
-#pragma unroll 1
+#pragma unroll
   for (int kb = 0; kb < NT; ++kb) {
     double2(*P)[TSZ] = pan[kb & 1];
     if (w == kb) {   // publish column kb; tile kb holds P^-1 in the strided layout
