@@ -476,6 +476,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
       t2[mi][ni] = d4{0.0, 0.0, 0.0, 0.0};
       t3[mi][ni] = d4{0.0, 0.0, 0.0, 0.0};
     }
+  const int cin = tk->cin;
+  double2* O = base + tk->out * BB + (int64_t)(tr * TS + lk) * BP + tc * TS + lr;
+  const double2* C = cin >= 0 ? base + cin * BB + (int64_t)(tr * TS + lk) * BP + tc * TS + lr : nullptr;
+  // register slot v of this wave's output share <-> offset in the block
+  auto slot_off = [&](int v) -> int64_t {
+    const int mi = v / (MI * 4), ni = (v / 4) % MI, rr = v % 4;
+    return (int64_t)(mi * 16 + 4 * rr) * BP + ni * 16;
+  };
+  constexpr int NPF = NV / KSPLIT;   // slots this wave writes (v % KSPLIT == kq)
+  double2 cpf[NPF];
+#pragma unroll
+  for (int i = 0; i < NPF; ++i) cpf[i] = make_double2(0.0, 0.0);
+#if DWHMC_GEMM_CPF
+  if (C && valid) {
+#pragma unroll
+    for (int i = 0; i < NPF; ++i) cpf[i] = C[slot_off(i * KSPLIT + kq)];
+  }
+#endif
   if (valid) {
     const int nt = tk->nt;
     if (KSPLIT == 1 || kq == 0) cr_tile_part<BP, MI, KSPLIT, 0>(base, tk, nt, tr, tc, sg, t1, t2, t3);
@@ -487,14 +505,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
       if (kq == 3) cr_tile_part<BP, MI, KSPLIT, 3>(base, tk, nt, tr, tc, sg, t1, t2, t3);
     }
   }
-  const int cin = tk->cin;
-  double2* O = base + tk->out * BB + (int64_t)(tr * TS + lk) * BP + tc * TS + lr;
-  const double2* C = cin >= 0 ? base + cin * BB + (int64_t)(tr * TS + lk) * BP + tc * TS + lr : nullptr;
   auto put = [&](int v, double2 x) {
-    const int mi = v / (MI * 4), ni = (v / 4) % MI, rr = v % 4;
-    const int64_t o = (int64_t)(mi * 16 + 4 * rr) * BP + ni * 16;
+    const int64_t o = slot_off(v);
     if (C) {
+#if DWHMC_GEMM_CPF
+      const double2 c = cpf[v / KSPLIT];
+#else
       const double2 c = C[o];
+#endif
       x.x += c.x;
       x.y += c.y;
     }

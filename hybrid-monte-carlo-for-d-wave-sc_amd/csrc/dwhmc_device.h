@@ -11,6 +11,11 @@
 #ifndef DWHMC_INV_FOLD
 #define DWHMC_INV_FOLD 1
 #endif
+// k_cr_gemm: load the accumulate-input block cin at the start of a tile (its
+// latency overlaps the operand loads) instead of after the K reduction
+#ifndef DWHMC_GEMM_CPF
+#define DWHMC_GEMM_CPF 1
+#endif
 #ifndef DWHMC_INV_PERMLANE
 #define DWHMC_INV_PERMLANE 0
 #endif

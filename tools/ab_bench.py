@@ -46,6 +46,10 @@ def main():
     for v in a.variants:
         kv = dict(x.split("=") for x in v.split(",") if x)
         os.environ["DWHMC_GJ_PAIR"] = kv.get("PAIR", "1")
+        # any other KEY=VAL of the variant sets the context knob DWHMC_KEY
+        for k, val in kv.items():
+            if k not in ("PAIR", "LIB"):
+                os.environ["DWHMC_" + k] = val
         ctx = m.FermionContext(p.Lx, p.Ly, p.t, p.tp, p.mu, p.beta, p.J, p.nn_table, p.nnn_table,
                                np.stack(dis), lib_path=kv.get("LIB"))
         ctx.set_pairing(np.stack(D0))
@@ -70,13 +74,16 @@ def main():
         ctx.timing_reset()
         ctx.run_sweeps(0, 1, a.Nt, dt, p.mass)
         ctx.synchronize()
-        kt = {k: ctx.timing_read(k) for k in ("gj_update", "gj_pivot", "assemble", "contract", "step")}
+        keys = ("cr_gemm", "cr_inv", "step") if ctx.info.get("algorithm", "cr") != "dense" else \
+            ("gj_update", "gj_pivot", "assemble", "contract", "step")
+        kt = {k: ctx.timing_read(k) for k in keys}
         ctx.timing_enable(False)
         x = np.array(res[v])
-        upd = kt["gj_update"]
-        print(f"{v:24s} ms/step median {np.median(x):.3f} min {x.min():.3f}  steps/s {1000*a.chains/np.median(x):.1f}  "
-              f"gj_update {upd[2]/upd[0]/1e9:.1f} TF  " +
-              " ".join(f"{k}={val[0]/a.Nt:.3f}ms/{val[1]//a.Nt}" for k, val in kt.items()), flush=True)
+        main = kt[keys[0]]
+        tf = main[2] / main[0] / 1e9 if main[0] > 0 else float("nan")
+        print(f"{v:24s} ms/step median {np.median(x):.4f} min {x.min():.4f}  steps/s {1000*a.chains/np.median(x):.1f}  "
+              f"{keys[0]} {tf:.1f} TF  " +
+              " ".join(f"{k}={val[0]/a.Nt:.4f}ms/{val[1]//a.Nt}" for k, val in kt.items()), flush=True)
         ctx.close()
 
 
