@@ -147,16 +147,20 @@ __global__ __launch_bounds__(256) void k_cr_fill(double2* __restrict__ pool, int
 // (BP = 16 NT) stored as top halves: the bottom rows are synthesised on load
 // (conj B | -conj A), only the top half of the (M-form) inverse is stored.
 // NT waves; wave w keeps block column w (NT 16 x 16 MFMA tiles, C layout) in
-// registers.  Pivot step kb:
-//   wave kb   publishes its column (tile kb already holds P^-1 = A_kk^-1, the
-//             others the old A_Ik) to an LDS panel, then A_Ik <- -A_Ik P^-1;
-//   wave J    X_J = P^-1 A_kJ (its tile kb, used in place as the MFMA B
-//             operand: the C layout of row 4s + lk is the B layout of k-step s),
-//             A_kJ <- X_J, A_IJ <- A_IJ - A_Ik X_J;
-//   wave kb+1 (lookahead) updates tile kb+1 first and inverts it (the next
-//             pivot) before its other tiles, while the other waves update.
-// One barrier per pivot step (double-buffered panel).  16 x 16 pivot tiles are
-// inverted in registers (wave_inv16_dpp); complex MACs are 3 real MFMAs.
+// registers.  Column kb (P^-1 = A_kk^-1 and the old A_Ik) sits in LDS panel
+// kb & 1 at the start of pivot step kb.  Step kb:
+//   phase 1   wave kb reads P^-1; every wave J != kb forms X_J = P^-1 A_kJ
+//             from its tile kb (used in place as the MFMA B operand: the C
+//             layout of row 4s + lk is the B layout of k-step s), A_kJ <- X_J;
+//             the lookahead wave kb+1 copies X and its other column tiles
+//             (not yet updated) into the next panel;
+//   phase 2   wave kb: A_Ik <- -A_Ik P^-1 for its column, and the lookahead
+//             column's update Q_I -= A_Ik X_{kb+1} inside the next panel;
+//             wave kb+1 updates tile kb+1 only, inverts it (the next pivot) and
+//             writes it to the next panel — its pivot chain carries no other
+//             tile updates; other waves J: A_IJ <- A_IJ - A_Ik X_J.
+// Two barriers per pivot step (double-buffered panel).  16 x 16 pivot tiles
+// are inverted in registers (wave_inv16_dpp); complex MACs are 3 real MFMAs.
 // ln|det| (= Σ ln|pivots|) goes to ldpart[bi][slot].
 // ---------------------------------------------------------------------------
 // acc(16x16, C layout) += (NEG ? -1 : 1) * A(16 x 16, LDS row-major, stride 17) * B
@@ -281,24 +285,83 @@ __global__ __launch_bounds__(64 * NT) void k_cr_inv(double2* __restrict__ pool, 
 #pragma unroll
   for (int kb = 0; kb < NT; ++kb) {
     double2(*P)[TSZ] = pan[kb & 1];
-    if (w == kb) {   // publish column kb; tile kb holds P^-1 in the strided layout
+    double2(*Q)[TSZ] = pan[(kb + 1) & 1];   // next step's panel, filled during this step
+    const bool has_next = kb + 1 < NT;
+    if (kb == 0 && w == 0) {   // publish column 0; tile 0 holds P^-1 in the strided layout
 #pragma unroll
       for (int I = 0; I < NT; ++I)
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
-          const int o = (I == kb) ? lr * 17 + lk + 4 * rr : (lk + 4 * rr) * 17 + lr;
+          const int o = (I == 0) ? lr * 17 + lk + 4 * rr : (lk + 4 * rr) * 17 + lr;
           P[I][o] = make_double2(ar[I][rr], ai[I][rr]);
         }
     }
     __syncthreads();
-    if (w == kb) {
-      d4 br, bim;   // P^-1 in the C layout, read back from the panel
+    // phase 1: the publisher reads P^-1; every other wave forms X = P^-1 A_kJ
+    // from its tile kb; the lookahead wave hands X and its not-yet-updated
+    // column tiles to the next panel (the publisher updates them there, off the
+    // lookahead's pivot chain)
+    d4 br = {0.0, 0.0, 0.0, 0.0}, bim = {0.0, 0.0, 0.0, 0.0};
+    d4 xr = {0.0, 0.0, 0.0, 0.0}, xi = {0.0, 0.0, 0.0, 0.0};
+    if (w == kb) {   // P^-1 in the C layout, read back from the panel
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const double2 v = P[kb][(lk + 4 * rr) * 17 + lr];
         br[rr] = v.x;
         bim[rr] = v.y;
       }
+    } else {
+      d4 tr = ar[0], ti = ai[0];   // this wave's tile kb (off-diagonal: C layout)
+#pragma unroll
+      for (int I = 1; I < NT; ++I)
+        if (I == kb) {
+          tr = ar[I];
+          ti = ai[I];
+        }
+      mma16_3m<false>(xr, xi, P[kb], tr, ti);
+#pragma unroll
+      for (int I = 0; I < NT; ++I)
+        if (I == kb) {
+          ar[I] = xr;
+          ai[I] = xi;
+        }
+      if (has_next && w == kb + 1) {
+#pragma unroll
+        for (int I = 0; I < NT; ++I)
+          if (I != kb + 1) {   // X (= new tile kb) and the old tiles I != kb, kb + 1
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr)
+              Q[I][(lk + 4 * rr) * 17 + lr] = make_double2(ar[I][rr], ai[I][rr]);
+          }
+      }
+    }
+    if (has_next) __syncthreads();
+    // phase 2
+    if (w == kb) {
+      if (has_next) {   // lookahead column: Q[I] -= A_Ik X_{kb+1} for I != kb, kb + 1
+        d4 yr, yi;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const double2 v = Q[kb][(lk + 4 * rr) * 17 + lr];
+          yr[rr] = v.x;
+          yi[rr] = v.y;
+        }
+#pragma unroll
+        for (int I = 0; I < NT; ++I)
+          if (I != kb && I != kb + 1) {
+            d4 cr, ci;
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+              const double2 v = Q[I][(lk + 4 * rr) * 17 + lr];
+              cr[rr] = v.x;
+              ci[rr] = v.y;
+            }
+            mma16_3m<true>(cr, ci, P[I], yr, yi);
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) Q[I][(lk + 4 * rr) * 17 + lr] = make_double2(cr[rr], ci[rr]);
+          }
+      }
+      // this wave's column: A_Ik <- -A_Ik P^-1, tile kb <- P^-1
 #pragma unroll
       for (int I = 0; I < NT; ++I) {
         if (I != kb) {
@@ -310,32 +373,22 @@ __global__ __launch_bounds__(64 * NT) void k_cr_inv(double2* __restrict__ pool, 
           ai[I] = bim;
         }
       }
-    } else {
-      // this wave's tile kb (off-diagonal: C layout)
-      d4 br = ar[0], bim = ai[0];
-#pragma unroll
-      for (int I = 1; I < NT; ++I)
-        if (I == kb) {
-          br = ar[I];
-          bim = ai[I];
-        }
-      d4 xr = {0.0, 0.0, 0.0, 0.0}, xi = {0.0, 0.0, 0.0, 0.0};
-      mma16_3m<false>(xr, xi, P[kb], br, bim);
-      const bool look = (w == kb + 1);
-#pragma unroll
-      for (int I = 0; I < NT; ++I) {
-        if (I == kb) {
-          ar[I] = xr;
-          ai[I] = xi;
-        }
-        if (look && I == kb + 1) {   // next pivot first: update (transposed) and invert
-          mma16_3m_T<true>(ar[I], ai[I], P[I], xr, xi);
-          ld += invert(ar[I], ai[I]);
-        }
-      }
+    } else if (has_next && w == kb + 1) {
+      // next pivot: update the (transposed) diagonal tile, invert it, publish
+      // it to the next panel in the strided layout; this wave's other tiles are
+      // rebuilt from the panel when it publishes at step kb + 1
 #pragma unroll
       for (int I = 0; I < NT; ++I)
-        if (I != kb && !(look && I == kb + 1)) {
+        if (I == kb + 1) {
+          mma16_3m_T<true>(ar[I], ai[I], P[I], xr, xi);
+          ld += invert(ar[I], ai[I]);
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) Q[I][lr * 17 + lk + 4 * rr] = make_double2(ar[I][rr], ai[I][rr]);
+        }
+    } else {
+#pragma unroll
+      for (int I = 0; I < NT; ++I)
+        if (I != kb) {
           if (I == w && kb < w) mma16_3m_T<true>(ar[I], ai[I], P[I], xr, xi);   // still transposed
           else mma16_3m<true>(ar[I], ai[I], P[I], xr, xi);
         }
