@@ -154,11 +154,12 @@ __global__ __launch_bounds__(256) void k_cr_fill(double2* __restrict__ pool, int
 //             layout of row 4s + lk is the B layout of k-step s), A_kJ <- X_J;
 //             the lookahead wave kb+1 copies X and its other column tiles
 //             (not yet updated) into the next panel;
-//   phase 2   wave kb: A_Ik <- -A_Ik P^-1 for its column, and the lookahead
-//             column's update Q_I -= A_Ik X_{kb+1} inside the next panel;
+//   phase 2   wave kb: A_Ik <- -A_Ik P^-1 for its column;
 //             wave kb+1 updates tile kb+1 only, inverts it (the next pivot) and
 //             writes it to the next panel — its pivot chain carries no other
-//             tile updates; other waves J: A_IJ <- A_IJ - A_Ik X_J.
+//             tile updates; other waves J: the lookahead column's tile J
+//             inside the next panel, Q_J -= A_Jk X_{kb+1}, then their own
+//             A_IJ <- A_IJ - A_Ik X_J.
 // Two barriers per pivot step (double-buffered panel).  16 x 16 pivot tiles
 // are inverted in registers (wave_inv16_dpp); complex MACs are 3 real MFMAs.
 // ln|det| (= Σ ln|pivots|) goes to ldpart[bi][slot].
@@ -338,29 +339,6 @@ __global__ __launch_bounds__(64 * NT) void k_cr_inv(double2* __restrict__ pool, 
     if (has_next) __syncthreads();
     // phase 2
     if (w == kb) {
-      if (has_next) {   // lookahead column: Q[I] -= A_Ik X_{kb+1} for I != kb, kb + 1
-        d4 yr, yi;
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          const double2 v = Q[kb][(lk + 4 * rr) * 17 + lr];
-          yr[rr] = v.x;
-          yi[rr] = v.y;
-        }
-#pragma unroll
-        for (int I = 0; I < NT; ++I)
-          if (I != kb && I != kb + 1) {
-            d4 cr, ci;
-#pragma unroll
-            for (int rr = 0; rr < 4; ++rr) {
-              const double2 v = Q[I][(lk + 4 * rr) * 17 + lr];
-              cr[rr] = v.x;
-              ci[rr] = v.y;
-            }
-            mma16_3m<true>(cr, ci, P[I], yr, yi);
-#pragma unroll
-            for (int rr = 0; rr < 4; ++rr) Q[I][(lk + 4 * rr) * 17 + lr] = make_double2(cr[rr], ci[rr]);
-          }
-      }
       // this wave's column: A_Ik <- -A_Ik P^-1, tile kb <- P^-1
 #pragma unroll
       for (int I = 0; I < NT; ++I) {
@@ -386,6 +364,21 @@ __global__ __launch_bounds__(64 * NT) void k_cr_inv(double2* __restrict__ pool, 
           for (int rr = 0; rr < 4; ++rr) Q[I][lr * 17 + lk + 4 * rr] = make_double2(ar[I][rr], ai[I][rr]);
         }
     } else {
+      if (has_next) {   // the lookahead column's tile w: Q[w] -= A_wk X_{kb+1}
+        d4 yr, yi, cr, ci;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const double2 v = Q[kb][(lk + 4 * rr) * 17 + lr];
+          const double2 u = Q[w][(lk + 4 * rr) * 17 + lr];
+          yr[rr] = v.x;
+          yi[rr] = v.y;
+          cr[rr] = u.x;
+          ci[rr] = u.y;
+        }
+        mma16_3m<true>(cr, ci, P[w], yr, yi);
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) Q[w][(lk + 4 * rr) * 17 + lr] = make_double2(cr[rr], ci[rr]);
+      }
 #pragma unroll
       for (int I = 0; I < NT; ++I)
         if (I != kb) {
