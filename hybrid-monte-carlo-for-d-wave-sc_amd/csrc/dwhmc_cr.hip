@@ -300,8 +300,8 @@ __global__ __launch_bounds__(64 * NT) void k_cr_inv(double2* __restrict__ pool, 
     __syncthreads();
     // phase 1: the publisher reads P^-1; every other wave forms X = P^-1 A_kJ
     // from its tile kb; the lookahead wave hands X and its not-yet-updated
-    // column tiles to the next panel (the publisher updates them there, off the
-    // lookahead's pivot chain)
+    // column tiles to the next panel (the other waves update them there, off
+    // the lookahead's pivot chain)
     d4 br = {0.0, 0.0, 0.0, 0.0}, bim = {0.0, 0.0, 0.0, 0.0};
     d4 xr = {0.0, 0.0, 0.0, 0.0}, xi = {0.0, 0.0, 0.0, 0.0};
     if (w == kb) {   // P^-1 in the C layout, read back from the panel
