@@ -221,13 +221,17 @@ __global__ __launch_bounds__(64 * NT) void k_cr_inv(double2* __restrict__ pool, 
   // diagonal tile (w, w), which is kept TRANSPOSED until it becomes this
   // wave's pivot: its C layout is then the strided inversion layout (lane:
   // row lr, columns lk + 4 rr), so the pivot is inverted in registers with no
-  // LDS transpose, and its updates A_ww -= A_wk X_w run as
+  // transpose, and its updates A_ww -= A_wk X_w run as
   // A_ww^T -= X_w^T A_wk^T (mma16_3m_T: X from registers, A_wk^T from LDS).
+  // The diagonal tile is loaded transposed straight from memory (lane: row lr,
+  // columns lk + 4 rr of the tile), so no LDS transpose precedes the first
+  // pivot inversion.
 #pragma unroll
   for (int I = 0; I < NT; ++I)
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
-      const int row = I * 16 + lk + 4 * rr, col = w * 16 + lr;
+      const bool diag = (I == w);
+      const int row = I * 16 + (diag ? lr : lk + 4 * rr), col = w * 16 + (diag ? lk + 4 * rr : lr);
       double2 v;
       if (row < HP) {
         v = M[(int64_t)row * BP + col];
@@ -238,34 +242,6 @@ __global__ __launch_bounds__(64 * NT) void k_cr_inv(double2* __restrict__ pool, 
       ar[I][rr] = v.x;
       ai[I][rr] = v.y;
     }
-  {   // transpose the diagonal tile once, through this wave's slot of panel 1
-    // (first written by the step-1 publisher, after the step-0 barrier)
-    double2* S = pan[1][w];
-    d4 dr = ar[0], di = ai[0];
-#pragma unroll
-    for (int I = 1; I < NT; ++I)
-      if (I == w) {
-        dr = ar[I];
-        di = ai[I];
-      }
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) S[(lk + 4 * rr) * 17 + lr] = make_double2(dr[rr], di[rr]);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      const double2 v = S[lr * 17 + lk + 4 * rr];
-      dr[rr] = v.x;
-      di[rr] = v.y;
-    }
-#pragma unroll
-    for (int I = 0; I < NT; ++I)
-      if (I == w) {
-        ar[I] = dr;
-        ai[I] = di;
-      }
-  }
   CR_STAMP(1);
   double ld = 0.0;
   // in-place inverse of the (transposed-stored) diagonal tile
