@@ -3,19 +3,28 @@
 (BASELINE.json metric) on MI355X, one process per GPU.
 
 A bench "step" is ONE leapfrog step of hmc_sweep! (src/HMC.jl:98-114) for
-every chain the rank owns: drift, pairing update, pole-expanded no-pivot LU of
-H_BdG(Δ) - i y_q for all poles, force contraction, kick.  The timed region
-runs steps/Nt complete sweeps (momentum refresh, H_old, backup, initial force,
-Nt leapfrog steps, H_new, Metropolis, restore), so Metropolis and energies
-are inside the timed work.  Workload (BASELINE configs[2] / C3): L=32
-(N=1024, BdG n=2048), β=16, one chain per GPU; t=1, t'=-0.35, μ=-1.08, W=1,
-n_imp=0.05, J=0.8, m=1, Nt=10, dt = calc_optimal_dt (src/Simulation.jl:11-14);
+every chain the rank owns: drift, pairing update, pole-expanded factorisation
+of H_BdG(Δ) - i y_q for all poles, force contraction, kick.  The timed region
+runs exactly --steps leapfrog steps as complete trajectories (momentum
+refresh, H_old, backup, initial force, Nt leapfrog steps, H_new, Metropolis,
+restore), the last one shortened to the remainder when --steps is not a
+multiple of Nt, so Metropolis and energies are inside the timed work.
+
+Before anything is timed the chain is thermalised the way the reference's
+driver does it (src/Simulation.jl:97-130: n_therm sweeps from Nt_therm_init
+= 10, Nt += 2 when a 5-sweep window accepts < 60 %, Nt -= 1 above 95 %,
+dt = calc_optimal_dt(β, J, m, Nt)); the timed region runs at the Nt the
+thermalisation ends with.  --warmup leapfrog steps are then rounded up to
+whole sweeps (untimed).
+
+Workload (BASELINE configs[2] / C3): L=32 (N=1024, BdG n=2048), β=16, one
+chain per GPU; t=1, t'=-0.35, μ=-1.08, W=1, n_imp=0.05, J=0.8, m=1;
 synthetic disorder/Δ₀/momenta from seed 1000+replica.  N>1: independent
 disorder replicas per rank (weak scaling), no collective in the data path;
 torch.distributed (RCCL) only for the barrier, the max-time reduction and the
 observable gather.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--L 32] [--beta 16]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3]
 """
 from __future__ import annotations
 
@@ -23,6 +32,7 @@ import argparse
 import json
 import math
 import os
+import platform
 import sys
 import time
 
@@ -34,30 +44,33 @@ sys.path.insert(0, ROOT)
 METRIC = "fp64 leapfrog steps/sec at L=32, 1→8 MI355X; % fp64 MFMA roofline"
 PEAK_F64_TFLOPS = 78.6        # MI355X dense fp64 matrix peak (= fp64 vector peak on CDNA4)
 PEAK_HBM_GBS = 8000.0         # MI355X HBM3E peak (MI355X_MICROARCH.md)
-TRAFFIC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_pmc_traffic.json")
+# newest committed PMC summary first (profiles/README.md)
+TRAFFIC_FILES = [os.path.join(ROOT, "profiles", f) for f in ("r02_pmc_traffic.json", "r01_pmc_traffic.json")]
 
 
 def measured_traffic(kernel, L, beta, chains):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
-    (tools/pmc_summary.py: FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md
+    (tools/pmc_summary.py: FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md
     gfx950 correction) for this exact workload, else None.  PMC counters cannot
     be read inside the timed run, so they come from their own profiled runs."""
-    try:
-        with open(TRAFFIC_FILE) as f:
-            rec = json.load(f)
-    except (OSError, ValueError):
-        return None, None
-    w = rec.get("workload", {})
-    if (w.get("L"), w.get("beta"), w.get("chains")) != (L, beta, chains):
-        return None, None
-    k = rec.get("kernels", {}).get(kernel)
-    if not k:
-        return None, None
-    return k["hbm_bytes_per_launch"], "profiles/" + os.path.basename(TRAFFIC_FILE)
+    for path in TRAFFIC_FILES:
+        try:
+            with open(path) as f:
+                rec = json.load(f)
+        except (OSError, ValueError):
+            continue
+        w = rec.get("workload", {})
+        if (w.get("L"), w.get("beta"), w.get("chains")) != (L, beta, chains):
+            continue
+        k = rec.get("kernels", {}).get(kernel)
+        if k:
+            return k["hbm_bytes_per_launch"], "profiles/" + os.path.basename(path)
+    return None, None
 
 
 # BASELINE.json configs (SURVEY.md §8d); the headline line is C3.
 PRESETS = {
+    "C1": dict(L=8, beta=4.0, chains=1, label="L=8 beta=4 single chain (BASELINE configs[0], C1)"),
     "C2": dict(L=16, beta=8.0, chains=1, label="L=16 beta=8 single-chain HMC (BASELINE configs[1], C2)"),
     "C3": dict(L=32, beta=16.0, chains=1, label="L=32 beta=16 single-chain HMC (BASELINE configs[2], C3)"),
     "C4": dict(L=32, beta=16.0, chains=1, label="L=32 beta=16 one disorder replica per GPU (BASELINE configs[3], C4)"),
@@ -65,48 +78,115 @@ PRESETS = {
 }
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50, help="leapfrog steps timed (multiple of --Nt)")
-    ap.add_argument("--warmup", type=int, default=10, help="untimed leapfrog steps (multiple of --Nt)")
+    ap.add_argument("--steps", type=int, default=50, help="leapfrog steps timed (any positive count)")
+    ap.add_argument("--warmup", type=int, default=10,
+                    help="untimed leapfrog steps after thermalisation (rounded up to whole sweeps)")
     ap.add_argument("--config", choices=sorted(PRESETS), default=None,
                     help="BASELINE config preset (default: C3, or C4 when launched on >1 GPU)")
     ap.add_argument("--L", type=int, default=None)
     ap.add_argument("--beta", type=float, default=None)
     ap.add_argument("--chains", type=int, default=None, help="chains per GPU")
-    ap.add_argument("--Nt", type=int, default=10)
+    ap.add_argument("--Nt", type=int, default=10, help="Nt_therm_init (src/Simulation.jl:38)")
+    ap.add_argument("--therm", type=int, default=100,
+                    help="thermalisation sweeps with the adaptive-Nt rule (src/Simulation.jl:104-130)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=0, help="oracle leapfrog steps for the CPU leg (0 = auto)")
+    ap.add_argument("--no-c1", action="store_true", help="skip the C1 (L=8, beta=4) side line")
     ap.add_argument("--no-timing", action="store_true", help="disable per-kernel HIP events")
     ap.add_argument("--algo", choices=["auto", "dense", "cr"], default="auto",
-                    help="factorisation (include/dwhmc.h DWH_ALGO_*); auto = cyclic reduction when 2L <= 96")
-    return ap.parse_args()
+                    help="factorisation (include/dwhmc.h DWH_ALGO_*); auto = cyclic reduction when 2L <= 128")
+    a = ap.parse_args(argv)
+    if a.steps < 1 or a.warmup < 0 or a.therm < 0 or a.Nt < 1:
+        ap.error("--steps must be >= 1, --warmup/--therm >= 0, --Nt >= 1")
+    return a
 
 
-def synthetic(p, O, replica, nchains, Nt, nsweeps):
-    """Disorder, Δ₀ and the sweep draws for `nchains` chains of one replica."""
+def schedule(first: int, steps: int, Nt: int):
+    """Exactly `steps` leapfrog steps as (first_draw, n_sweeps, Nt) pieces:
+    steps // Nt full trajectories, then one trajectory of steps % Nt."""
+    full, rem = divmod(steps, Nt)
+    out = []
+    if full:
+        out.append((first, full, Nt))
+    if rem:
+        out.append((first + full, 1, rem))
+    return out
+
+
+def n_draws(pieces) -> int:
+    return sum(n for _, n, _ in pieces)
+
+
+def synthetic_state(m, p, replica, nchains):
+    """Disorder and Δ₀ of `nchains` chains of one replica (src/Types.jl:118-134,
+    seeded per SURVEY.md §8d)."""
     dis, D0 = [], []
     for c in range(nchains):
-        rng = np.random.default_rng(1000 + replica * nchains + c)
-        st = O.initialize_state(p, rng)            # src/Types.jl:118-134
+        st = m.initialize_state(p, np.random.default_rng(1000 + replica * nchains + c))
         dis.append(st.disorder_pot)
         D0.append(st.Delta)
-    rng = np.random.default_rng(7_000_000 + replica)
-    shape = (nsweeps, nchains, p.N, 2)
-    noise = (rng.standard_normal(shape) + 1j * rng.standard_normal(shape)) * math.sqrt(0.5)
-    uni = rng.random((nsweeps, nchains))
-    return np.stack(dis), np.stack(D0), noise, uni
+    return np.stack(dis), np.stack(D0)
 
 
-def cpu_baseline(O, p, Delta0, disorder, steps):
-    """Oracle (numpy/scipy zheevr restatement) leapfrog steps on the host."""
+def synthetic_draws(m, N, replica, nchains, nsweeps, salt):
+    rng = np.random.default_rng([salt, replica])
+    noise = m.standard_complex_normal(rng, (nsweeps, nchains, N, 2))   # randn(ComplexF64), src/HMC.jl:53
+    return noise, rng.random((nsweeps, nchains))
+
+
+def thermalise(m, ctx, p, replica, nchains, n_therm, Nt0):
+    """src/Simulation.jl:97-130 with injected draws; returns (Nt, acceptance
+    of the last 20 sweeps).  Chains of one context share Nt (the majority
+    vote of their acceptances per window)."""
+    ad = m.AdaptiveNt(Nt0)
+    if n_therm == 0:
+        return ad.Nt, None
+    noise, uni = synthetic_draws(m, p.N, replica, nchains, n_therm, 11)
+    ctx.load_draws(noise, uni)
+    accs = []
+    for i in range(0, n_therm, ad.window):
+        k = min(ad.window, n_therm - i)
+        dt = m.calc_optimal_dt(p.beta, p.J, p.mass, ad.Nt)
+        ctx.run_sweeps(i, k, ad.Nt, dt, p.mass)
+        acc, _ = ctx.sweep_results(i, k)
+        for j in range(k):
+            accs.append(float(acc[j].mean()))
+            ad.record(i + j + 1, accs[-1] >= 0.5)
+    return ad.Nt, float(np.mean(accs[-20:]))
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def blas_threads() -> int:
     try:
         from threadpoolctl import threadpool_info
-        threads = max([i.get("num_threads", 1) for i in threadpool_info()
-                       if i.get("internal_api") in ("openblas", "mkl", "blis")] or [1])
+        n = [i.get("num_threads", 1) for i in threadpool_info()
+             if i.get("internal_api") in ("openblas", "mkl", "blis")]
+        if n:
+            return max(n)
     except Exception:
-        threads = os.cpu_count() or 1
+        pass
+    return int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+
+
+def cpu_leapfrog(p_args, disorder, Delta0, steps, Nt=10):
+    """The reference CPU path, restated (oracle: numpy/scipy zheevr with
+    uplo='U', src/Hamiltonian.jl:96-114, compute_forces!, src/Observables.jl:14-62,
+    leapfrog src/HMC.jl:101-113): returns (steps/s, seconds)."""
+    from oracle import dwhmc_oracle as O      # CPU baseline leg only
+    p = O.ModelParameters(*p_args)
     cache = O.initialize_cache(p)
     O.init_static_H(cache, p, disorder)
     Delta = Delta0.copy()
@@ -114,20 +194,70 @@ def cpu_baseline(O, p, Delta0, disorder, steps):
     O.update_H_BdG(cache, p, Delta)
     O.diagonalize_H_BdG(cache, p)
     O.compute_forces(cache, p, Delta)
-    dt = O.calc_optimal_dt(p.beta, p.J, p.mass, 10)
+    dt = O.calc_optimal_dt(p.beta, p.J, p.mass, Nt)
     t0 = time.perf_counter()
-    for _ in range(steps):                          # src/HMC.jl:101-113
+    for _ in range(steps):
         Delta += dt / (2 * p.mass) * pi
         O.update_H_BdG(cache, p, Delta)
         O.diagonalize_H_BdG(cache, p)
         O.compute_forces(cache, p, Delta)
         pi += dt * cache.forces
     el = time.perf_counter() - t0
-    return steps / el, threads, el
+    return steps / el, el
 
 
-def main():
-    a = parse()
+def cpu_baseline(p_args, disorder, Delta0, steps_all, steps_one):
+    """All BLAS threads, then 1 thread (core count and CPU model stated)."""
+    threads = blas_threads()
+    v, el = cpu_leapfrog(p_args, disorder, Delta0, steps_all)
+    rec = {"value": v, "unit": "leapfrog steps/s", "cores": threads, "kind": "port",
+           "cpu": cpu_model(),
+           "sample": f"{steps_all} leapfrog steps at L={p_args[0]}, beta={p_args[7]:g}, {threads} BLAS threads "
+                     f"(numpy/scipy zheevr restatement of src/Hamiltonian.jl:96-114 + compute_forces!, "
+                     f"{el:.1f} s)"}
+    if steps_one:
+        try:
+            from threadpoolctl import threadpool_limits
+            with threadpool_limits(limits=1):
+                v1, el1 = cpu_leapfrog(p_args, disorder, Delta0, steps_one)
+            rec["single_thread"] = {"value": v1, "cores": 1,
+                                    "sample": f"{steps_one} leapfrog step(s), 1 thread, {el1:.1f} s"}
+        except Exception as e:                  # threadpoolctl missing or BLAS not controllable
+            rec["single_thread"] = {"error": repr(e)}
+    return rec
+
+
+def c1_line(m, local):
+    """BASELINE configs[0] (C1: L=8, β=4, 10 trajectories x Nt=10 =
+    scripts/test_hmc.jl's workload) on the GPU and on the CPU restatement."""
+    pr = PRESETS["C1"]
+    p_args = (pr["L"], pr["L"], 1.0, -0.35, -1.08, 1.0, 0.05, pr["beta"], 0.8, 1.0)
+    p = m.ModelParameters(*p_args)
+    dis, D0 = synthetic_state(m, p, 0, 1)
+    ctx = m.FermionContext(p.Lx, p.Ly, p.t, p.tp, p.mu, p.beta, p.J, p.nn_table, p.nnn_table, dis,
+                           device=local)
+    ctx.set_pairing(D0)
+    ctx.factorize()
+    noise, uni = synthetic_draws(m, p.N, 0, 1, 12, 13)
+    ctx.load_draws(noise, uni)
+    dt = m.calc_optimal_dt(p.beta, p.J, p.mass, 10)
+    ctx.run_sweeps(0, 2, 10, dt, p.mass)        # warmup
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    ctx.run_sweeps(2, 10, 10, dt, p.mass)
+    ctx.synchronize()
+    el = time.perf_counter() - t0
+    acc, _ = ctx.sweep_results(2, 10)
+    ctx.close()
+    v_cpu, el_cpu = cpu_leapfrog(p_args, dis[0], D0[0], 100)
+    return {"workload": pr["label"], "trajectories": 10, "Nt": 10, "gpu_value": 100 / el,
+            "gpu_ms_per_step": 1000.0 * el / 100, "gpu_acceptance": float(acc.mean()),
+            "cpu_value": v_cpu, "cpu_cores": blas_threads(), "cpu_kind": "port", "unit": "leapfrog steps/s",
+            "cpu_sample": f"100 leapfrog steps (10 x Nt=10), {el_cpu:.2f} s"}
+
+
+def main(argv=None):
+    a = parse(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -137,8 +267,6 @@ def main():
         if getattr(a, k) is None:
             setattr(a, k, preset[k])
     workload = (f"L={a.L} beta={a.beta:g} {a.chains} chain(s)/GPU (custom)" if custom else preset["label"])
-    if a.steps % a.Nt or a.warmup % a.Nt:
-        raise SystemExit("--steps and --warmup must be multiples of --Nt")
     dist = None
     if world > 1:
         import torch
@@ -147,14 +275,12 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     import dwhmc_loader
-    from oracle import dwhmc_oracle as O   # synthetic-input generation + CPU leg only
     m = dwhmc_loader.load_package()
     m.load_library(build_if_missing=False)
 
-    p = O.ModelParameters(a.L, a.L, 1.0, -0.35, -1.08, 1.0, 0.05, a.beta, 0.8, 1.0)
-    n_warm, n_time = a.warmup // a.Nt, a.steps // a.Nt
-    dis, D0, noise, uni = synthetic(p, O, rank, a.chains, a.Nt, n_warm + n_time)
-    dt = m.calc_optimal_dt(p.beta, p.J, p.mass, a.Nt)
+    p_args = (a.L, a.L, 1.0, -0.35, -1.08, 1.0, 0.05, a.beta, 0.8, 1.0)
+    p = m.ModelParameters(*p_args)
+    dis, D0 = synthetic_state(m, p, rank, a.chains)
     ctx = m.FermionContext(p.Lx, p.Ly, p.t, p.tp, p.mu, p.beta, p.J, p.nn_table, p.nnn_table, dis,
                            device=local, algo=a.algo)
     cr = ctx.info["algo"] == 1
@@ -162,16 +288,25 @@ def main():
     dom = "cr_gemm" if cr else "gj_update"
     ctx.set_pairing(D0)
     ctx.factorize()                                 # src/Simulation.jl:84-86
+    t_th = time.perf_counter()
+    Nt, acc_therm = thermalise(m, ctx, p, rank, a.chains, a.therm, a.Nt)
+    t_th = time.perf_counter() - t_th
+    dt = m.calc_optimal_dt(p.beta, p.J, p.mass, Nt)
+    warm = schedule(0, -(-a.warmup // Nt) * Nt, Nt) if a.warmup else []
+    w_sw = n_draws(warm)
+    timed = schedule(w_sw, a.steps, Nt)
+    noise, uni = synthetic_draws(m, p.N, rank, a.chains, w_sw + n_draws(timed), 7)
     ctx.load_draws(noise, uni)                      # inputs resident in HBM before timing
-    if n_warm:
-        ctx.run_sweeps(0, n_warm, a.Nt, dt, p.mass)
+    for f, n, nt in warm:
+        ctx.run_sweeps(f, n, nt, dt, p.mass)
     ctx.synchronize()
 
     if dist is not None:
         dist.barrier()
     ctx.synchronize()
     t0 = time.perf_counter()
-    ctx.run_sweeps(n_warm, n_time, a.Nt, dt, p.mass)
+    for f, n, nt in timed:
+        ctx.run_sweeps(f, n, nt, dt, p.mass)
     ctx.synchronize()
     el = time.perf_counter() - t0
     if dist is not None:
@@ -181,23 +316,27 @@ def main():
         el = float(t.item())
         dist.barrier()
 
-    acc, dH = ctx.sweep_results(n_warm, n_time)
+    acc, dH = ctx.sweep_results(w_sw, n_draws(timed))
     info = ctx.info
     kern = {}
-    timed_sweeps = 0
+    replay_steps = 0
     if not a.no_timing:
         # Per-kernel HIP events (on the context's stream) in an instrumented
-        # replay of the first timed sweeps right after the timed region: each
-        # event record is a barrier packet that costs ~20 % of the step when
-        # interleaved with ~30 launches per step, so the timed region itself
-        # runs without them.  Same kernels, same sizes; rocprofv3 --stats of the
-        # same command (profiles/) agrees on the per-launch averages.
-        timed_sweeps = min(n_time, 2)
-        ctx.timing_enable([dom, "assemble"] + (["cr_inv"] if cr else []))
+        # replay of the timed schedule's first <= 2 Nt steps right after the
+        # timed region: each event record is a barrier packet that costs ~20 %
+        # of the step when interleaved with ~30 launches per step, so the
+        # timed region itself runs without them.  Same kernels, same sizes;
+        # rocprofv3 --stats of the same command (profiles/) agrees on the
+        # per-launch averages.
+        replay = schedule(w_sw, min(a.steps, 2 * Nt), Nt)
+        replay_steps = sum(n * nt for _, n, nt in replay)
+        names = [dom, "assemble"] + (["cr_inv"] if cr else [])
+        ctx.timing_enable(names)
         ctx.timing_reset()
-        ctx.run_sweeps(n_warm, timed_sweeps, a.Nt, dt, p.mass)
+        for f, n, nt in replay:
+            ctx.run_sweeps(f, n, nt, dt, p.mass)
         ctx.synchronize()
-        for k in [dom, "assemble"] + (["cr_inv"] if cr else []):
+        for k in names:
             kern[k] = ctx.timing_read(k)
         ctx.timing_enable(False)
     # observables gather over RCCL (the only collective): acceptance and <dH>
@@ -230,8 +369,12 @@ def main():
             "data": "synthetic",
             "config": {"workload": workload,
                        "L": a.L, "N": N, "bdg_dim": 2 * N, "beta": a.beta, "chains_per_gpu": a.chains,
-                       "Nt": a.Nt, "dt": dt, "poles": P, "kappa": info["kappa"],
+                       "Nt": Nt, "dt": dt, "therm_sweeps": a.therm, "poles": P, "kappa": info["kappa"],
                        "parallelism": f"replicas x{world}" if world > 1 else "single GPU"},
+            "timed_trajectories": [{"sweeps": n, "Nt": nt} for _, n, nt in timed],
+            "warmup_sweeps": w_sw,
+            "thermalisation": {"sweeps": a.therm, "Nt_init": a.Nt, "Nt_final": Nt,
+                               "acceptance_last20": acc_therm, "seconds": t_th},
             "acceptance": float(obs[0]), "mean_dH": float(obs[1]), "mean_exp_minus_dH": float(obs[2]),
             "algorithm": "block cyclic reduction" if cr else "dense Schur complement + Gauss-Jordan",
             "ref_equiv_tflops": leap * (40.0 / 3.0) * (2 * N) ** 3 / el / 1e12,
@@ -243,18 +386,16 @@ def main():
             ms, n, w = kern[dom]
             ach = w / n / (ms / n * 1e-3) / 1e12 if n and ms > 0 else None
             if cr:
-                kname = f"k_cr_gemm<{info['block']},1,4>"   # 16x16 tiles, 4-way K split (every stage)
+                kname = f"k_cr_gemm<{info['block']},1,4>"   # 16x16 tiles, 4-way K split
                 msi, ni, wi = kern["cr_inv"]
-                # the CR path's own algorithmic flops: block products + block inversions
                 # the CR path's own algorithmic flops per leapfrog step (block
-                # products + block inversions) x steps of the timed region
-                steps_t = timed_sweeps * a.Nt
-                rec["alg_tflops"] = (w + wi) / steps_t * a.steps * world / el / 1e12
-                rec["alg_flops_per_step"] = (w + wi) / steps_t / a.chains
+                # products + block inversions) x the timed steps
+                rec["alg_tflops"] = (w + wi) / replay_steps * a.steps * world / el / 1e12
+                rec["alg_flops_per_step"] = (w + wi) / replay_steps / a.chains
                 rec["cr_inv"] = {"bound": "latency", "kernel": f"k_cr_inv<{info['block'] // 16}>",
                                  "achieved_tflops": wi / (msi * 1e-3) / 1e12 if msi > 0 else None,
                                  "avg_launch_us": 1000.0 * msi / ni if ni else None,
-                                 "ms_per_step": msi / (timed_sweeps * a.Nt)}
+                                 "ms_per_step": msi / replay_steps}
             else:
                 nb = -(-info["N"] // 64)                 # GJ block steps; odd nb ends with one rank-64 step
                 kname = "k_gj_update<2>" if nb % 2 == 0 else "k_gj_update<2>+<0>"
@@ -264,8 +405,9 @@ def main():
                                "frac": ach / PEAK_F64_TFLOPS if ach else None, "traffic": traffic,
                                "traffic_unit": "bytes/launch", "traffic_source": tsrc,
                                "avg_launch_us": 1000.0 * ms / n if n else None,
-                               "flops_per_launch": w / n if n else None}
-            rec[f"{dom}_ms_per_step"] = ms / (timed_sweeps * a.Nt)
+                               "flops_per_launch": w / n if n else None,
+                               "replayed_steps": replay_steps}
+            rec[f"{dom}_ms_per_step"] = ms / replay_steps
             ms, n, w = kern["assemble"]
             if n and ms > 0:
                 gbs = w / n / (ms / n * 1e-3) / 1e9
@@ -273,13 +415,12 @@ def main():
                                    "achieved": gbs,
                                    "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS,
                                    "bytes_per_launch": w / n, "avg_launch_us": 1000.0 * ms / n}
+        if world == 1 and not a.no_c1 and a.L != PRESETS["C1"]["L"]:
+            rec["c1"] = c1_line(m, local)
         if not a.no_cpu_baseline and world == 1:
-            steps_cpu = a.cpu_steps or (1 if a.L >= 48 else 3 if a.L >= 32 else 20)
-            v, threads, el_cpu = cpu_baseline(O, p, D0[0], dis[0], steps_cpu)
-            rec["cpu_baseline"] = {"value": v, "unit": "leapfrog steps/s", "cores": threads,
-                                   "kind": "port",
-                                   "sample": f"{steps_cpu} leapfrog steps at L={a.L}, beta={a.beta:g} "
-                                             f"(numpy/scipy zheevr restatement, {el_cpu:.1f} s)"}
+            steps_all = a.cpu_steps or (1 if a.L >= 48 else 3 if a.L >= 32 else 20)
+            steps_one = 0 if a.L >= 48 else 1 if a.L >= 32 else 5
+            rec["cpu_baseline"] = cpu_baseline(p_args, dis[0], D0[0], steps_all, steps_one)
         print(json.dumps(rec), flush=True)
     ctx.close()
     if dist is not None:

@@ -1515,21 +1515,40 @@ int dwh_load_draws(dwh_ctx* ctx, int64_t nsweeps, const dwh_c128* noise, const d
   const size_t nbond = (size_t)d.nc * 2 * d.N;
   if (nsweeps > ctx->ndraws) {
     HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
-    auto drop = [&](void* p) {
+    auto drop = [&](void* p, size_t bytes) {
       if (!p) return;
       auto it = std::find(ctx->allocations.begin(), ctx->allocations.end(), p);
       if (it != ctx->allocations.end()) ctx->allocations.erase(it);
+      ctx->device_bytes -= (int64_t)std::max<size_t>(bytes, 1);
       (void)hipFree(p);
     };
-    drop(ctx->noise);
-    drop(ctx->uniform);
-    drop(ctx->acc);
-    drop(ctx->dH);
-    int rc;
-    if ((rc = dalloc(ctx, &ctx->noise, nbond * nsweeps)) != DWH_OK) return rc;
-    if ((rc = dalloc(ctx, &ctx->uniform, (size_t)d.nc * nsweeps)) != DWH_OK) return rc;
-    if ((rc = dalloc(ctx, &ctx->acc, (size_t)d.nc * nsweeps)) != DWH_OK) return rc;
-    if ((rc = dalloc(ctx, &ctx->dH, (size_t)d.nc * nsweeps)) != DWH_OK) return rc;
+    // allocate the new buffers first and swap them in only when all of them
+    // exist, so a failed allocation leaves the old draws (and ndraws) intact
+    double2* nz = nullptr;
+    double* un = nullptr;
+    uint8_t* ac = nullptr;
+    double* dh = nullptr;
+    const size_t ns = (size_t)nsweeps, nc = (size_t)d.nc;
+    int rc = dalloc(ctx, &nz, nbond * ns);
+    if (rc == DWH_OK) rc = dalloc(ctx, &un, nc * ns);
+    if (rc == DWH_OK) rc = dalloc(ctx, &ac, nc * ns);
+    if (rc == DWH_OK) rc = dalloc(ctx, &dh, nc * ns);
+    const size_t old = (size_t)ctx->ndraws;
+    if (rc != DWH_OK) {
+      drop(nz, nbond * ns * sizeof(double2));
+      drop(un, nc * ns * sizeof(double));
+      drop(ac, nc * ns);
+      drop(dh, nc * ns * sizeof(double));
+      return rc;
+    }
+    drop(ctx->noise, nbond * old * sizeof(double2));
+    drop(ctx->uniform, nc * old * sizeof(double));
+    drop(ctx->acc, nc * old);
+    drop(ctx->dH, nc * old * sizeof(double));
+    ctx->noise = nz;
+    ctx->uniform = un;
+    ctx->acc = ac;
+    ctx->dH = dh;
   }
   ctx->ndraws = std::max<int64_t>(ctx->ndraws, nsweeps);
   HIPCHECK(ctx, hipMemcpyAsync(ctx->noise, noise, nbond * nsweeps * sizeof(double2),
