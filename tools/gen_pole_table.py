@@ -45,8 +45,22 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EPS_TANH = 2.0e-14        # sup |tanh(κu) - r(u)| target on [-1, 1]
-KAPPA_EXPONENTS = range(0, 45)   # κ = 2^(j/4), 1 .. 2048
+KAPPA_EXPONENTS = range(0, 73)   # κ = 2^(j/4), 1 .. 262144 (β = 10^4 at E' ≈ 50)
 DPS = 40
+# Above COMPRESS_ABOVE the Matsubara atoms k > GROUP_K0 are compressed: the
+# atoms of k ∈ (a, 2a] (a = GROUP_K0·2^i) are equally weighted points of an
+# equispaced grid in k, so the GROUP_NODES-point Gauss rule of the discrete
+# uniform measure (Gram / discrete Chebyshev polynomials, closed-form
+# recurrence) integrates every function the Lanczos process of
+# multipoint_pade applies to them (polynomials in t = ((2k-1)π/2κ)² of degree
+# <= 2m+1 times 1/Π_j(t + s_j), analytic in k away from Re k = 1/2) to far
+# below double precision.  The κ <= 4096 entries keep every atom explicit
+# (they are the round-1 entries, unchanged).  The table is verified against
+# tanh itself on a dense grid either way, so the compression can only cost
+# optimality, never correctness.
+COMPRESS_ABOVE = 4096.0
+GROUP_K0 = 512
+GROUP_NODES = 100
 
 
 def _gauss_from_moments(M, n):
@@ -76,15 +90,50 @@ def _hurwitz(s, a):
     return (-1) ** s * mp.psi(s - 1, a) / mp.factorial(s - 1)
 
 
+_RULES = {}
+
+
+def discrete_gauss(M, n):
+    """n-point Gauss rule of the uniform measure on {0, 1, ..., M-1}:
+    monic recurrence α_j = (M-1)/2, β_j = j²(M²-j²)/(4(4j²-1)) (Gram
+    polynomials); nodes x_i, weights summing to M."""
+    key = (M, n)
+    if key not in _RULES:
+        Jm = mp.matrix(n, n)
+        for i in range(n):
+            Jm[i, i] = mp.mpf(M - 1) / 2
+            if i < n - 1:
+                j = i + 1
+                Jm[i, i + 1] = Jm[i + 1, i] = mp.sqrt(mp.mpf(j * j * (M * M - j * j)) / (4 * (4 * j * j - 1)))
+        E, V = mp.eigsy(Jm)
+        _RULES[key] = ([E[i] for i in range(n)], [M * V[0, i] ** 2 for i in range(n)])
+    return _RULES[key]
+
+
 def matsubara_measure(kappa, ntail=10):
     """Atoms (t_k, μ_k) of τ's Stieltjes measure; tail k > K folded into ntail
     Gauss atoms of ρ = Σ_{k>K} (w/t_k) δ(1/t_k) (moments via Hurwitz zeta)."""
     kap = mp.mpf(kappa)
     w = 2 / kap
+
+    def tk(k):
+        return ((2 * k - 1) * mp.pi / (2 * kap)) ** 2
+
     K = int(max(40, math.ceil(kappa)))
-    t = [((2 * k - 1) * mp.pi / (2 * kap)) ** 2 for k in range(1, K + 1)]
-    mu = [w] * K
-    tK = t[-1]
+    if kappa <= COMPRESS_ABOVE:
+        t = [tk(k) for k in range(1, K + 1)]
+        mu = [w] * K
+    else:
+        t = [tk(k) for k in range(1, GROUP_K0 + 1)]
+        mu = [w] * GROUP_K0
+        a = GROUP_K0
+        while a < K:                    # group k = a+1 .. 2a (M = a atoms)
+            x, wx = discrete_gauss(a, GROUP_NODES)
+            t += [tk(a + 1 + xi) for xi in x]
+            mu += [w * wi for wi in wx]
+            a *= 2
+        K = a
+    tK = tk(K)
     with mp.workdps(3 * DPS):
         # moments of ρ in the scaled variable x' = tK / t ∈ (0, 1]
         M = [w * tK ** p * (2 * kap / mp.pi) ** (2 * p + 2) * mp.mpf(2) ** (-2 * p - 2)
@@ -239,9 +288,20 @@ def write_outputs(entries):
 
 
 def main():
+    """python tools/gen_pole_table.py [j,j,...|a-b]: regenerate the listed
+    entries (default: all) and merge them into the committed table."""
     js = list(KAPPA_EXPONENTS)
+    keep = []
     if len(sys.argv) > 1:
-        js = [int(x) for x in sys.argv[1].split(",")]
+        js = []
+        for part in sys.argv[1].split(","):
+            lo, _, hi = part.partition("-")
+            js += list(range(int(lo), int(hi or lo) + 1))
+        try:
+            with open(os.path.join(ROOT, "tests", "golden", "pole_table.json")) as f:
+                keep = [e for e in json.load(f)["entries"] if e["j"] not in js]
+        except OSError:
+            pass
     t0 = time.time()
     procs = int(os.environ.get("GEN_PROCS", "7"))
     out = []
@@ -251,7 +311,7 @@ def main():
             out.append(e)
             print(f"kappa={e['kappa']:9.3f} m={e['m']:2d} err_tanh={e['err_tanh']:.2e} "
                   f"err_phi={e['err_phi']:.2e}  [{time.time()-t0:.0f}s]", flush=True)
-    print(write_outputs(out))
+    print(write_outputs(keep + out))
 
 
 if __name__ == "__main__":
