@@ -42,10 +42,13 @@ ALGOS = {"auto": -1, "dense": 0, "cr": 1}
 
 
 class FermionContext:
-    """Device-resident fermionic action/force evaluator for nchains chains."""
+    """Device-resident fermionic action/force evaluator for nchains chains.
+    delta_cap <= 0 selects the ABI default max(2, 6 sqrt(2J/β)) for the guard
+    on max|Δ_ij|; an uploaded Δ or a trajectory beyond it re-selects the pole
+    set (include/dwhmc.h)."""
 
     def __init__(self, Lx, Ly, t, tp, mu, beta, J, nn_table, nnn_table, disorder,
-                 delta_cap: float = 2.0, device: int = 0, lib_path: str | None = None,
+                 delta_cap: float = 0.0, device: int = 0, lib_path: str | None = None,
                  algo: str = "auto"):
         self._lib = _lib.load() if lib_path is None else _lib.load_path(lib_path)
         dis = np.ascontiguousarray(np.atleast_2d(np.asarray(disorder, dtype=np.float64)))
@@ -65,7 +68,6 @@ class FermionContext:
                                      int(device))
         check(rc, None)
         self._h = h
-        self.info = self._info()
         self.info_lattice = (int(Lx), int(Ly))
 
     # -- lifecycle -------------------------------------------------------
@@ -82,6 +84,12 @@ class FermionContext:
 
     def _c(self, rc):
         check(rc, self._h)
+
+    @property
+    def info(self) -> dict:
+        """dwh_info: sizes, pole set (kappa, npoles, delta_cap; a guard trip
+        re-selects it), algorithm, device bytes."""
+        return self._info()
 
     def _info(self):
         inf = _lib.dwh_info_t()
@@ -143,6 +151,20 @@ class FermionContext:
         self._c(self._lib.dwh_hmc_sweep(self._h, ptr(nz), ptr(u), int(Nt), float(dt), float(mass),
                                         ptr(acc), ptr(dH)))
         return acc.astype(bool), dH
+
+    def hmc_trajectory(self, noise, Nt: int, dt: float, mass: float) -> np.ndarray:
+        """hmc_sweep! up to H_new (dwh_hmc_trajectory); returns ΔH per chain.
+        Finish with hmc_finish(accepted)."""
+        nz = _to_abi(noise, self.nchains, self.N)
+        dH = np.zeros(self.nchains)
+        self._c(self._lib.dwh_hmc_trajectory(self._h, ptr(nz), int(Nt), float(dt), float(mass), ptr(dH)))
+        return dH
+
+    def hmc_finish(self, accepted):
+        a = np.ascontiguousarray(np.atleast_1d(np.asarray(accepted)).astype(np.uint8))
+        if a.shape != (self.nchains,):
+            raise ValueError("one accept flag per chain")
+        self._c(self._lib.dwh_hmc_finish(self._h, ptr(a)))
 
     # -- throughput path -------------------------------------------------
     def load_draws(self, noise, uniform):
@@ -214,6 +236,23 @@ class FermionContext:
                      optical_conductivity=sigma[c].copy(), dos_omega_grid=dg.copy(), dos=dos[c].copy(),
                      dos_AN=dos_an[c].copy(), A_k_omega0=ak[c].reshape(Ly, Lx).T.copy())
                 for c in range(nc)]
+
+    # -- assembly read-back (parity tests) --------------------------------
+    def debug_dense_H(self, chain: int = 0) -> np.ndarray:
+        """H_BdG(Δ) (2N, 2N) as the eigen/transport path assembles it (dwh_debug_dense_H)."""
+        n2 = 2 * self.N
+        Hcm = np.empty((n2, n2), dtype=np.complex128)          # row c = column c
+        self._c(self._lib.dwh_debug_dense_H(self._h, int(chain), ptr(Hcm)))
+        return Hcm.T.copy()
+
+    def debug_level0(self, chain: int = 0, pole: int = 0, refill: bool = True):
+        """(M, y): H_BdG(Δ) - i y_pole I (2N, 2N) from the CR level-0 blocks the
+        factorisation consumes (dwh_debug_level0), and the pole heights y_q."""
+        n2 = 2 * self.N
+        Mcm = np.empty((n2, n2), dtype=np.complex128)
+        y = np.empty(self.info["npoles"])
+        self._c(self._lib.dwh_debug_level0(self._h, int(chain), int(pole), int(bool(refill)), ptr(Mcm), ptr(y)))
+        return Mcm.T.copy(), y
 
     # -- timing ----------------------------------------------------------
     TIMERS = ("gj_update", "gj_pivot", "assemble", "contract", "step", "gj_edge", "cr_gemm", "cr_inv")

@@ -356,6 +356,10 @@ struct dwh_ctx {
   double t = 0, tp = 0, mu = 0, beta = 0, J = 0, delta_cap = 2.0;
   double kappa = 0, Ebound = 0, Cx = 0, err_tanh = 0, hmax = 0;
   std::vector<double> y, cq;
+  // creation inputs kept for a pole re-selection (reselect_poles)
+  std::vector<int64_t> nn_host, nnn_host;
+  std::vector<double> dis_host;
+  int reselections = 0;
   int64_t device_bytes = 0;
   bool factorized = false;
   std::string err;
@@ -403,6 +407,7 @@ struct dwh_ctx {
   // drifting k_cr_pair_force, consumed by the next factorisation); every
   // other path that changes Δ leaves it false
   bool pairing_in_pool = false;
+  bool pending = false;    // dwh_hmc_trajectory done, dwh_hmc_finish not yet
 
   // transport / spectra measurement (device side allocated on first use): host
   // copies of the x-current operator J (CSR of its imaginary parts, duplicates
@@ -651,9 +656,9 @@ void fermion_energy_enqueue(dwh_ctx* ctx) {
                                ctx->beta, ctx->Ef, ctx->Trhh, ctx->stream);
 }
 
-// One hmc_sweep! body reading draws from device pointers (src/HMC.jl:71-144).
-void sweep_enqueue(dwh_ctx* ctx, const double2* noise, const double* uniform, uint8_t* acc,
-                   double* dH, int64_t Nt, double dt, double mass) {
+// One hmc_sweep! trajectory reading its draws from device pointers
+// (src/HMC.jl:71-122): refresh, H_old, backup, leapfrog, H_new.
+void trajectory_enqueue(dwh_ctx* ctx, const double2* noise, int64_t Nt, double dt, double mass) {
   const Dims& d = ctx->d;
   hipStream_t s = ctx->stream;
   dwh::launch_refresh(d, noise, ctx->Pi, std::sqrt(2.0 * mass), s);                  // :77
@@ -678,6 +683,14 @@ void sweep_enqueue(dwh_ctx* ctx, const double2* noise, const double* uniform, ui
     fermion_energy_enqueue(ctx);
   dwh::launch_total_energy(d, ctx->Delta, ctx->Pi, ctx->Ef, ctx->beta, ctx->J, mass,  // :122
                            ctx->Hnew, s);
+}
+
+// One hmc_sweep! body (src/HMC.jl:71-144): trajectory, Metropolis, restore.
+void sweep_enqueue(dwh_ctx* ctx, const double2* noise, const double* uniform, uint8_t* acc,
+                   double* dH, int64_t Nt, double dt, double mass) {
+  const Dims& d = ctx->d;
+  hipStream_t s = ctx->stream;
+  trajectory_enqueue(ctx, noise, Nt, dt, mass);
   dwh::launch_metropolis(d, ctx->Hold, ctx->Hnew, uniform, acc, dH, s);               // :124-129
   dwh::launch_restore(d, acc, ctx->DeltaB, ctx->PairB, ctx->EfB, ctx->TrhhB, ctx->Delta,  // :130-141
                       ctx->Pair, ctx->Ef, ctx->Trhh, s);
@@ -699,6 +712,12 @@ int check_flag(dwh_ctx* ctx) {
   return DWH_OK;
 }
 
+// Default guard on max|Δ_ij|: 2 (the ordered phase), or 6 standard deviations
+// of the Gaussian boson fluctuations <|Δ|²> = 2J/β at high temperature.
+double default_delta_cap(double beta, double J) {
+  return std::max(2.0, 6.0 * std::sqrt(2.0 * std::fabs(J) / beta));
+}
+
 int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, double mu, double beta,
                 double J, const int64_t* nn, const int64_t* nnn, int64_t nchains,
                 const double* disorder, double delta_cap, int32_t algo_req, int32_t device) {
@@ -712,7 +731,7 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
   const int64_t N64 = Lx * Ly;
   if (N64 > 9216) return fail(nullptr, DWH_ERR_ARG, "N = Lx*Ly > 9216 not supported (LDS row staging)");
   const int N = (int)N64;
-  if (delta_cap <= 0) delta_cap = 2.0;
+  if (delta_cap <= 0) delta_cap = default_delta_cap(beta, J);
   for (int64_t e = 0; e < 4 * N64; ++e)
     if (nn[e] < 1 || nn[e] > N64 || nnn[e] < 1 || nnn[e] > N64)
       return fail(nullptr, DWH_ERR_ARG, "neighbour table entry out of [1, N]");
@@ -827,6 +846,9 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
   }
 
   dwh_ctx* ctx = new dwh_ctx();
+  ctx->nn_host.assign(nn, nn + 4 * N64);
+  ctx->nnn_host.assign(nnn, nnn + 4 * N64);
+  ctx->dis_host.assign(disorder, disorder + nchains * N64);
   ctx->device = device;
   ctx->Lx = Lx;
   ctx->Ly = Ly;
@@ -1338,7 +1360,7 @@ int dwh_measure_transport_batched(dwh_ctx* ctx, double eta, double domega, doubl
 int dwh_create(dwh_ctx** ctx, int64_t Lx, int64_t Ly, double t, double tp, double mu, double beta,
                double J, const int64_t* nn_table, const int64_t* nnn_table, const double* disorder,
                int32_t device) {
-  return create_impl(ctx, Lx, Ly, t, tp, mu, beta, J, nn_table, nnn_table, 1, disorder, 2.0,
+  return create_impl(ctx, Lx, Ly, t, tp, mu, beta, J, nn_table, nnn_table, 1, disorder, 0.0,
                      DWH_ALGO_AUTO, device);
 }
 
@@ -1393,9 +1415,110 @@ int dwh_info(dwh_ctx* ctx, dwh_info_t* out) {
   return DWH_OK;
 }
 
+namespace {
+
+// Re-create the device side of `ctx` for |Δ_ij| <= new_cap: a new pole-table
+// entry for the larger spectral bound E' = hmax + 2 new_cap, same lattice,
+// disorder and algorithm; Δ, π, the throughput draws and the timing state
+// carry over.  The context is left unfactorised.
+int reselect_poles(dwh_ctx* ctx, double new_cap) {
+  dwh_ctx* n = nullptr;
+  const int32_t algo = ctx->algo == ALGO_CR ? DWH_ALGO_CR : DWH_ALGO_DENSE;
+  int rc = create_impl(&n, ctx->Lx, ctx->Ly, ctx->t, ctx->tp, ctx->mu, ctx->beta, ctx->J,
+                       ctx->nn_host.data(), ctx->nnn_host.data(), ctx->d.nc, ctx->dis_host.data(), new_cap,
+                       algo, ctx->device);
+  if (rc != DWH_OK)
+    return fail(ctx, rc, "pole re-selection for delta_cap=" + std::to_string(new_cap) + ": " + g_create_error);
+  const size_t nb = (size_t)ctx->d.nc * 2 * ctx->d.N * sizeof(double2);
+  hipError_t e = hipStreamSynchronize(ctx->stream);
+  if (e == hipSuccess) e = hipMemcpy(n->Delta, ctx->Delta, nb, hipMemcpyDeviceToDevice);
+  if (e == hipSuccess) e = hipMemcpy(n->Pi, ctx->Pi, nb, hipMemcpyDeviceToDevice);
+  if (e != hipSuccess) {
+    dwh_destroy(n);
+    return fail(ctx, DWH_ERR_HIP, std::string("pole re-selection: ") + hipGetErrorString(e));
+  }
+  // the throughput draws move with the context
+  const size_t nbond = (size_t)ctx->d.nc * 2 * ctx->d.N, nc = ctx->d.nc, ns = (size_t)ctx->ndraws;
+  auto move = [&](void* p, size_t bytes) {
+    if (!p) return;
+    auto it = std::find(ctx->allocations.begin(), ctx->allocations.end(), p);
+    if (it != ctx->allocations.end()) ctx->allocations.erase(it);
+    bytes = std::max<size_t>(bytes, 1);
+    ctx->device_bytes -= (int64_t)bytes;
+    n->allocations.push_back(p);
+    n->device_bytes += (int64_t)bytes;
+  };
+  move(ctx->noise, nbond * ns * sizeof(double2));
+  move(ctx->uniform, nc * ns * sizeof(double));
+  move(ctx->acc, nc * ns);
+  move(ctx->dH, nc * ns * sizeof(double));
+  n->noise = ctx->noise;
+  n->uniform = ctx->uniform;
+  n->acc = ctx->acc;
+  n->dH = ctx->dH;
+  n->ndraws = ctx->ndraws;
+  ctx->noise = nullptr;
+  ctx->uniform = nullptr;
+  ctx->acc = nullptr;
+  ctx->dH = nullptr;
+  ctx->ndraws = 0;
+  n->timing = ctx->timing;
+  n->gj_pair = ctx->gj_pair;
+  std::copy(ctx->t_ms, ctx->t_ms + T_COUNT, n->t_ms);
+  std::copy(ctx->t_n, ctx->t_n + T_COUNT, n->t_n);
+  std::copy(ctx->t_work, ctx->t_work + T_COUNT, n->t_work);
+  n->reselections = ctx->reselections + 1;
+  std::swap(*ctx, *n);
+  dwh_destroy(n);
+  return DWH_OK;
+}
+
+// Host-side guard for an uploaded Δ: re-select the poles when max|Δ_ij| is
+// above the cap (the reference accepts any Δ, src/HMC.jl:98-114).
+int fit_cap(dwh_ctx* ctx, const dwh_c128* D, size_t n, bool* reselected = nullptr) {
+  if (reselected) *reselected = false;
+  double m = 0;
+  for (size_t k = 0; k < n; ++k) {
+    const double a = std::hypot(D[k].re, D[k].im);
+    if (!std::isfinite(a)) return fail(ctx, DWH_ERR_ARG, "non-finite Delta");
+    m = std::max(m, a);
+  }
+  if (m <= ctx->delta_cap) return DWH_OK;
+  if (reselected) *reselected = true;
+  return reselect_poles(ctx, std::max(2.0 * ctx->delta_cap, 1.5 * m));
+}
+
+// Reads and clears the device guard flag (set by the drift kernels when
+// max|Δ_ij| > delta_cap).
+int take_flag(dwh_ctx* ctx, int* f) {
+  *f = 0;
+  HIPCHECK(ctx, hipMemcpyAsync(f, ctx->flag, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+  if (*f) HIPCHECK(ctx, hipMemsetAsync(ctx->flag, 0, sizeof(int), ctx->stream));
+  return DWH_OK;
+}
+
+// A sweep drifted |Δ| past the cap, so its forces used poles not valid for
+// its spectrum: back to the sweep's starting point (Δ backed up by k_backup,
+// src/HMC.jl:84), re-select the poles for twice the cap and refactorise, so
+// the caller can run the same sweep again.
+constexpr int kMaxReselect = 12;
+int redo_after_guard(dwh_ctx* ctx, int attempt) {
+  if (attempt >= kMaxReselect)
+    return fail(ctx, DWH_ERR_SPECTRUM, "|Delta_ij| kept exceeding the re-selected pole sets");
+  const size_t nb = (size_t)ctx->d.nc * 2 * ctx->d.N * sizeof(double2);
+  HIPCHECK(ctx, hipMemcpyAsync(ctx->Delta, ctx->DeltaB, nb, hipMemcpyDeviceToDevice, ctx->stream));
+  int rc = reselect_poles(ctx, 2.0 * ctx->delta_cap);
+  if (rc != DWH_OK) return rc;
+  return dwh_factorize(ctx);
+}
+
+}  // namespace
+
 int dwh_update_pairing(dwh_ctx* ctx, const dwh_c128* Delta) {
   if (!ctx || !Delta) return fail(ctx, DWH_ERR_ARG, "NULL argument");
   HIPCHECK(ctx, hipSetDevice(ctx->device));
+  if (int rc = fit_cap(ctx, Delta, (size_t)ctx->d.nc * 2 * ctx->d.N)) return rc;
   HIPCHECK(ctx, hipMemcpyAsync(ctx->Delta, Delta, (size_t)ctx->d.nc * 2 * ctx->d.N * sizeof(double2),
                                hipMemcpyHostToDevice, ctx->stream));
   HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
@@ -1469,9 +1592,15 @@ int dwh_set_state(dwh_ctx* ctx, const dwh_c128* Delta, const dwh_c128* pi) {
   if (!ctx) return DWH_ERR_ARG;
   HIPCHECK(ctx, hipSetDevice(ctx->device));
   const size_t nb = (size_t)ctx->d.nc * 2 * ctx->d.N * sizeof(double2);
+  bool reselected = false;
+  if (Delta)
+    if (int rc = fit_cap(ctx, Delta, (size_t)ctx->d.nc * 2 * ctx->d.N, &reselected)) return rc;
   if (Delta) HIPCHECK(ctx, hipMemcpyAsync(ctx->Delta, Delta, nb, hipMemcpyHostToDevice, ctx->stream));
   if (pi) HIPCHECK(ctx, hipMemcpyAsync(ctx->Pi, pi, nb, hipMemcpyHostToDevice, ctx->stream));
   HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+  // a re-selected context has no factorisation yet: the cached P / E_f the next
+  // sweep starts from must belong to this Δ
+  if (reselected) return dwh_factorize(ctx);
   return DWH_OK;
 }
 
@@ -1489,23 +1618,72 @@ int dwh_hmc_sweep(dwh_ctx* ctx, const dwh_c128* noise, const double* uniform, in
                   double mass, uint8_t* accepted, double* dH) {
   if (!ctx || !noise || !uniform || !accepted || !dH) return fail(ctx, DWH_ERR_ARG, "NULL argument");
   if (Nt < 0 || !(mass > 0) || !std::isfinite(dt)) return fail(ctx, DWH_ERR_ARG, "bad Nt/dt/mass");
+  if (ctx->pending) return fail(ctx, DWH_ERR_STATE, "dwh_hmc_finish the pending trajectory first");
+  HIPCHECK(ctx, hipSetDevice(ctx->device));
+  for (int attempt = 0;; ++attempt) {
+    const Dims& d = ctx->d;
+    HIPCHECK(ctx, hipMemcpyAsync(ctx->s_noise, noise, (size_t)d.nc * 2 * d.N * sizeof(double2),
+                                 hipMemcpyHostToDevice, ctx->stream));
+    HIPCHECK(ctx, hipMemcpyAsync(ctx->s_uniform, uniform, d.nc * sizeof(double), hipMemcpyHostToDevice,
+                                 ctx->stream));
+    sweep_enqueue(ctx, ctx->s_noise, ctx->s_uniform, ctx->s_acc, ctx->s_dH, Nt, dt, mass);
+    HIPCHECK(ctx, hipGetLastError());
+    HIPCHECK(ctx, hipMemcpyAsync(accepted, ctx->s_acc, d.nc, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHECK(ctx, hipMemcpyAsync(dH, ctx->s_dH, d.nc * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+    if (Nt > 0) ctx->factorized = true;
+    drain_timing(ctx);
+    int f = 0;
+    if (int rc = take_flag(ctx, &f)) return rc;
+    if (!f) return DWH_OK;
+    if (int rc = redo_after_guard(ctx, attempt)) return rc;
+  }
+}
+
+int dwh_hmc_trajectory(dwh_ctx* ctx, const dwh_c128* noise, int64_t Nt, double dt, double mass,
+                       double* dH) {
+  if (!ctx || !noise || !dH) return fail(ctx, DWH_ERR_ARG, "NULL argument");
+  if (Nt < 0 || !(mass > 0) || !std::isfinite(dt)) return fail(ctx, DWH_ERR_ARG, "bad Nt/dt/mass");
+  if (ctx->pending) return fail(ctx, DWH_ERR_STATE, "dwh_hmc_finish the pending trajectory first");
+  HIPCHECK(ctx, hipSetDevice(ctx->device));
+  for (int attempt = 0;; ++attempt) {
+    const Dims& d = ctx->d;
+    HIPCHECK(ctx, hipMemcpyAsync(ctx->s_noise, noise, (size_t)d.nc * 2 * d.N * sizeof(double2),
+                                 hipMemcpyHostToDevice, ctx->stream));
+    // ΔH by the Metropolis kernel's own arithmetic (src/HMC.jl:124), with a
+    // uniform of 2 > exp(-ΔH) for ΔH >= 0: its accept flags are not used
+    std::vector<double> two((size_t)d.nc, 2.0);
+    HIPCHECK(ctx, hipMemcpyAsync(ctx->s_uniform, two.data(), d.nc * sizeof(double), hipMemcpyHostToDevice,
+                                 ctx->stream));
+    trajectory_enqueue(ctx, ctx->s_noise, Nt, dt, mass);
+    dwh::launch_metropolis(d, ctx->Hold, ctx->Hnew, ctx->s_uniform, ctx->s_acc, ctx->s_dH, ctx->stream);
+    HIPCHECK(ctx, hipGetLastError());
+    HIPCHECK(ctx, hipMemcpyAsync(dH, ctx->s_dH, d.nc * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+    if (Nt > 0) ctx->factorized = true;
+    drain_timing(ctx);
+    int f = 0;
+    if (int rc = take_flag(ctx, &f)) return rc;
+    if (!f) {
+      ctx->pending = true;
+      return DWH_OK;
+    }
+    if (int rc = redo_after_guard(ctx, attempt)) return rc;
+  }
+}
+
+int dwh_hmc_finish(dwh_ctx* ctx, const uint8_t* accepted) {
+  if (!ctx || !accepted) return fail(ctx, DWH_ERR_ARG, "NULL argument");
+  if (!ctx->pending) return fail(ctx, DWH_ERR_STATE, "no pending trajectory (dwh_hmc_trajectory first)");
   HIPCHECK(ctx, hipSetDevice(ctx->device));
   const Dims& d = ctx->d;
-  double2* nz = ctx->s_noise;
-  double* un = ctx->s_uniform;
-  uint8_t* ac = ctx->s_acc;
-  double* dh = ctx->s_dH;
-  HIPCHECK(ctx, hipMemcpyAsync(nz, noise, (size_t)d.nc * 2 * d.N * sizeof(double2),
-                               hipMemcpyHostToDevice, ctx->stream));
-  HIPCHECK(ctx, hipMemcpyAsync(un, uniform, d.nc * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
-  sweep_enqueue(ctx, nz, un, ac, dh, Nt, dt, mass);
+  HIPCHECK(ctx, hipMemcpyAsync(ctx->s_acc, accepted, d.nc, hipMemcpyHostToDevice, ctx->stream));
+  dwh::launch_restore(d, ctx->s_acc, ctx->DeltaB, ctx->PairB, ctx->EfB, ctx->TrhhB, ctx->Delta,  // :130-141
+                      ctx->Pair, ctx->Ef, ctx->Trhh, ctx->stream);
   HIPCHECK(ctx, hipGetLastError());
-  HIPCHECK(ctx, hipMemcpyAsync(accepted, ac, d.nc, hipMemcpyDeviceToHost, ctx->stream));
-  HIPCHECK(ctx, hipMemcpyAsync(dH, dh, d.nc * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
   HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
-  if (Nt > 0) ctx->factorized = true;
-  drain_timing(ctx);
-  return check_flag(ctx);
+  ctx->pending = false;
+  return DWH_OK;
 }
 
 int dwh_load_draws(dwh_ctx* ctx, int64_t nsweeps, const dwh_c128* noise, const double* uniform) {
@@ -1564,6 +1742,7 @@ int dwh_run_sweeps(dwh_ctx* ctx, int64_t first, int64_t nsweeps, int64_t Nt, dou
   if (first < 0 || nsweeps < 0 || first + nsweeps > ctx->ndraws)
     return fail(ctx, DWH_ERR_ARG, "sweep range outside the loaded draws");
   if (Nt < 0 || !(mass > 0)) return fail(ctx, DWH_ERR_ARG, "bad Nt/mass");
+  if (ctx->pending) return fail(ctx, DWH_ERR_STATE, "dwh_hmc_finish the pending trajectory first");
   HIPCHECK(ctx, hipSetDevice(ctx->device));
   const Dims& d = ctx->d;
   const size_t nbond = (size_t)d.nc * 2 * d.N;
@@ -1639,5 +1818,81 @@ int dwh_timing_reset(dwh_ctx* ctx) {
 }
 
 int dwh_selftest_mfma(int32_t device) { return dwh::selftest_mfma_layout(device); }
+
+// ---- assembly read-back (parity tests of init_static_H! / update_H_BdG!) ----
+
+int dwh_debug_dense_H(dwh_ctx* ctx, int64_t chain, dwh_c128* H) {
+  if (!ctx || !H) return fail(ctx, DWH_ERR_ARG, "NULL argument");
+  if (chain < 0 || chain >= ctx->d.nc) return fail(ctx, DWH_ERR_ARG, "chain index out of range");
+  HIPCHECK(ctx, hipSetDevice(ctx->device));
+  const int N = ctx->d.N;
+  const size_t n2 = 2 * (size_t)N;
+  double2* A = nullptr;
+  HIPCHECK(ctx, hipMalloc(&A, n2 * n2 * sizeof(double2)));
+  // the eigen path's assembly (eigen_enqueue): zero, then k_tr_assemble
+  hipError_t e = hipMemsetAsync(A, 0, n2 * n2 * sizeof(double2), ctx->stream);
+  if (e == hipSuccess) {
+    dwh::launch_tr_assemble(A, N, ctx->hcol, ctx->hval + (size_t)chain * N * kHSlots, ctx->Dcol, ctx->Dsrc,
+                            ctx->Delta + (size_t)chain * 2 * N, ctx->stream);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(H, A, n2 * n2 * sizeof(double2), hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  (void)hipFree(A);
+  if (e != hipSuccess) return fail(ctx, DWH_ERR_HIP, std::string("dense H read-back: ") + hipGetErrorString(e));
+  return DWH_OK;
+}
+
+int dwh_debug_level0(dwh_ctx* ctx, int64_t chain, int64_t pole, int32_t refill, dwh_c128* M, double* y) {
+  if (!ctx || !M) return fail(ctx, DWH_ERR_ARG, "NULL argument");
+  if (ctx->algo != ALGO_CR) return fail(ctx, DWH_ERR_STATE, "level-0 blocks exist only on the CR path");
+  const dwh::CrDims& c = ctx->cr;
+  if (chain < 0 || chain >= ctx->d.nc || pole < 0 || pole >= c.P)
+    return fail(ctx, DWH_ERR_ARG, "chain or pole index out of range");
+  HIPCHECK(ctx, hipSetDevice(ctx->device));
+  if (refill) {
+    // exactly cr_enqueue's assembly launch (rewritten blocks + Δ/2 scatter)
+    const CrPlan& pl = ctx->plan;
+    dwh::launch_cr_fill(c, ctx->bpool, ctx->d_fill_step, (int)pl.fill_step.size(), ctx->hcol, ctx->hval,
+                        ctx->Dcol, ctx->Dsrc, ctx->Delta, ctx->d_y, ctx->d_off_ph, ctx->stream);
+    HIPCHECK(ctx, hipGetLastError());
+  }
+  const int Lx = c.Lx, Ly = c.Ly, N = c.N, BP = c.BP, HP = BP / 2;
+  const size_t nblk0 = 3 * (size_t)Ly, bsz = (size_t)HP * BP;
+  std::vector<double2> h(nblk0 * bsz);
+  const int64_t bi = chain * c.P + pole;
+  HIPCHECK(ctx, hipMemcpyAsync(h.data(), ctx->bpool + bi * c.item, h.size() * sizeof(double2),
+                               hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+  // expand the M-form top halves [A | B] into the reference basis (particles
+  // i = y Lx + x, holes i + N): rows i: [A | B], rows i + N: [conj B | -conj A]
+  const size_t n2 = 2 * (size_t)N;
+  std::vector<uint8_t> seen(n2 * n2, 0);
+  for (size_t k = 0; k < n2 * n2; ++k) M[k] = dwh_c128{0.0, 0.0};
+  auto put = [&](size_t r, size_t col, double re, double im) -> bool {
+    const size_t o = r + col * n2;   // column-major
+    if (seen[o]) return false;
+    seen[o] = 1;
+    M[o] = dwh_c128{re, im};
+    return true;
+  };
+  for (int t = 0; t < 3; ++t) {
+    if ((t == 1 && Ly < 2) || (t == 2 && Ly < 3)) continue;   // k_cr_fill's zero blocks
+    for (int yb = 0; yb < Ly; ++yb) {
+      const int yr = (t == 2) ? (yb + 1) % Ly : yb, yc = (t == 1) ? (yb + 1) % Ly : yb;
+      const double2* blk = h.data() + (size_t)(t * Ly + yb) * bsz;
+      for (int r = 0; r < Lx; ++r)
+        for (int x = 0; x < Lx; ++x) {
+          const size_t i = (size_t)yr * Lx + r, j = (size_t)yc * Lx + x;
+          const double2 a = blk[(size_t)r * BP + x], b = blk[(size_t)r * BP + HP + x];
+          if (!put(i, j, a.x, a.y) || !put(i, j + N, b.x, b.y) || !put(i + N, j, b.x, -b.y) ||
+              !put(i + N, j + N, -a.x, a.y))
+            return fail(ctx, DWH_ERR_STATE, "level-0 blocks overlap");
+        }
+    }
+  }
+  if (y) std::copy(ctx->y.begin(), ctx->y.end(), y);
+  return DWH_OK;
+}
 
 }  // extern "C"

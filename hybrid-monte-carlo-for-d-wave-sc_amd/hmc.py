@@ -99,7 +99,7 @@ class ComputeCache:
     are replaced by the device context (created by init_static_H, which is
     where the reference first consumes the disorder)."""
 
-    def __init__(self, p: ModelParameters, device: int = 0, delta_cap: float = 2.0):
+    def __init__(self, p: ModelParameters, device: int = 0, delta_cap: float = 0.0):
         self.p = p
         self.device = device
         self.delta_cap = delta_cap
@@ -115,7 +115,7 @@ class ComputeCache:
         return self.ctx
 
 
-def initialize_cache(p: ModelParameters, device: int = 0, delta_cap: float = 2.0) -> ComputeCache:
+def initialize_cache(p: ModelParameters, device: int = 0, delta_cap: float = 0.0) -> ComputeCache:
     return ComputeCache(p, device=device, delta_cap=delta_cap)
 
 
@@ -178,21 +178,29 @@ def standard_complex_normal(rng: np.random.Generator, shape) -> np.ndarray:
 def hmc_sweep(cache: ComputeCache, p: ModelParameters, state: SimulationState, *, Nt: int, dt: float,
               rng: np.random.Generator | None = None, noise: np.ndarray | None = None,
               uniform: float | None = None):
-    """src/HMC.jl:71-144.  Draws come from `rng` unless injected.
-    Returns (accepted, ΔH); mutates state.Δ, state.π and the cache."""
+    """src/HMC.jl:71-144.  Draws come from `rng` unless injected.  With `rng`
+    and no injected uniform, the Metropolis uniform is drawn only when
+    ΔH >= 0 — the short-circuit of src/HMC.jl:128 — so the generator is
+    consumed exactly as the reference consumes its own (dwh_hmc_trajectory +
+    dwh_hmc_finish).  Returns (accepted, ΔH); mutates state.Δ, state.π and
+    the cache."""
     ctx = cache.require()
     if noise is None:
         noise = standard_complex_normal(rng, (p.N, 2))
-    if uniform is None:
-        uniform = float(rng.random())
     ctx.set_state(state.Delta, None)
-    acc, dH = ctx.hmc_sweep(noise, np.array([uniform]), Nt, dt, p.mass)
+    if uniform is None:
+        dH = float(ctx.hmc_trajectory(noise, Nt, dt, p.mass)[0])
+        acc = bool(dH < 0 or rng.random() < math.exp(-dH))
+        ctx.hmc_finish([acc])
+    else:
+        a, d = ctx.hmc_sweep(noise, np.array([uniform]), Nt, dt, p.mass)
+        acc, dH = bool(a[0]), float(d[0])
     D, P = ctx.get_state()
     state.Delta = D[0]
     state.pi = P[0]
     cache.E_fermion = float(ctx.fermion_energy()[0])
     cache.pairing = ctx.pairing()[0]
-    return bool(acc[0]), float(dH[0])
+    return acc, dH
 
 
 def calc_optimal_dt(beta, J, mass, Nt):

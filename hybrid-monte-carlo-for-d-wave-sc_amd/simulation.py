@@ -119,7 +119,7 @@ class SpectraBins:
 def run_simulation(p: H.ModelParameters, out_dir: str, *, n_therm: int = 100, n_measure: int = 500,
                    Nt_therm_init: int = 10, Nt_measure: int = 5, measure_transport_freq: int = 1,
                    bin_size: int = 5, verbose: bool = True, rng: np.random.Generator | None = None,
-                   device: int = 0, delta_cap: float = 2.0, state: H.SimulationState | None = None,
+                   device: int = 0, delta_cap: float = 0.0, state: H.SimulationState | None = None,
                    cache: H.ComputeCache | None = None) -> SimulationResult:
     """src/Simulation.jl:34-236.  Files in out_dir: simulation.log (appended),
     observables.csv, transport.csv (one row per transport measurement, every

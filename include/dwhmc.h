@@ -123,6 +123,18 @@ int dwh_get_state(dwh_ctx* ctx, dwh_c128* Delta, dwh_c128* pi);
 int dwh_hmc_sweep(dwh_ctx* ctx, const dwh_c128* noise, const double* uniform, int64_t Nt,
                   double dt, double mass, uint8_t* accepted, double* dH);
 
+/* hmc_sweep! split at its Metropolis test, so a host whose RNG must be
+ * consumed exactly as the reference consumes it (src/HMC.jl:128 draws
+ * rand() only when ΔH >= 0) decides acceptance itself:
+ *   dwh_hmc_trajectory: momentum refresh from `noise`, H_old, backup,
+ *     leapfrog, H_new [src/HMC.jl:76-122]; dH[nchains] = H_new - H_old.
+ *   dwh_hmc_finish: accepted[nchains] (0/1) from the host; rejected chains are
+ *     restored [src/HMC.jl:130-141].
+ * Between the two calls the context refuses another sweep (DWH_ERR_STATE). */
+int dwh_hmc_trajectory(dwh_ctx* ctx, const dwh_c128* noise, int64_t Nt, double dt, double mass,
+                       double* dH);
+int dwh_hmc_finish(dwh_ctx* ctx, const uint8_t* accepted);
+
 /* Throughput path: upload the draws of nsweeps sweeps once (noise:
  * nsweeps*nchains*2N, uniform: nsweeps*nchains), then enqueue sweeps that
  * read them from HBM without host round trips. */
@@ -187,6 +199,25 @@ int dwh_measure_transport(dwh_ctx* ctx, int64_t chain, double eta, double domega
 int dwh_measure_transport_batched(dwh_ctx* ctx, double eta, double domega, double omega_max,
                                   double* stiffness, double* dc_cond, double* sigma, int64_t n_omega,
                                   double* dos, double* dos_an, int64_t n_dos, double* ak0);
+
+/* ---- assembly read-back (parity tests; not on the hot path) -------------
+ * The BdG matrix H_BdG(Δ) exactly as the device assembles it, so tests can
+ * compare it bit-for-bit with init_static_H! + update_H_BdG!
+ * [src/Hamiltonian.jl:10-47, 55-86] (Hermitian completion of the reference's
+ * upper triangle, including its overwrite order on 1- and 2-site rings).
+ *
+ * dwh_debug_dense_H: the dense matrix the eigen/transport path builds
+ * (k_tr_assemble) from the device Δ of `chain`; H: 2N x 2N column-major.
+ *
+ * dwh_debug_level0 (CR path only): the level-0 blocks of batch item
+ * (chain, pole) — H_BdG(Δ) - i y_pole I as the factorisation consumes it —
+ * expanded from the stored M-form top halves into the reference basis
+ * (particles i = y Lx + x, holes i + N); M: 2N x 2N column-major, y (nullable):
+ * the npoles pole heights y_q.  refill != 0 first runs the factorisation's
+ * assembly launch on the device Δ; refill == 0 reads the pool as the last
+ * trajectory step left it (Δ/2 scattered by the force kernel). */
+int dwh_debug_dense_H(dwh_ctx* ctx, int64_t chain, dwh_c128* H);
+int dwh_debug_level0(dwh_ctx* ctx, int64_t chain, int64_t pole, int32_t refill, dwh_c128* M, double* y);
 
 /* Self-test of the f64 MFMA fragment layout (A = I, asymmetric B); 0 = pass. */
 int dwh_selftest_mfma(int32_t device);

@@ -1,17 +1,24 @@
 # DwaveHMCGPU.jl — Julia `ccall` binding of libdwhmc.so (include/dwhmc.h).
 #
 # Drop-in for the hot path of DwaveHMC.jl: `GPUCache` replaces `ComputeCache`
-# and the methods below shadow init_static_H!/update_H_BdG!/diagonalize_H_BdG!/
-# compute_forces!/compute_total_energy/hmc_sweep! for it, with the reference's
-# argument order and mutation semantics (src/Hamiltonian.jl, src/Observables.jl,
-# src/HMC.jl).  Not executable in this image (no Julia, SURVEY.md F4); the
-# ABI it binds is exercised through ctypes by tests/test_gpu_parity.py.
+# and the methods below extend init_static_H!/update_H_BdG!/diagonalize_H_BdG!/
+# compute_forces!/compute_total_energy/hmc_sweep!/measure_observables/
+# measure_transport_and_spectra for it, with the reference's argument order and
+# mutation semantics (src/Hamiltonian.jl, src/Observables.jl, src/HMC.jl) —
+# every call `run_simulation` (src/Simulation.jl:84-171) makes on its cache.
+# `DwaveHMCGPU.run_simulation` is the reference's own driver, evaluated from
+# its source with the one cache-constructing call swapped (see the end of
+# this file).  Not executable in this image (no Julia, SURVEY.md F4); the ABI
+# it binds is exercised through ctypes by tests/ (tests/test_gpu_parity.py,
+# tests/test_gpu_assembly.py, tests/test_simulation.py).
 module DwaveHMCGPU
 
 using DwaveHMC
 using Random
+using Dates, Printf, DelimitedFiles, JLD2          # what src/Simulation.jl:1-4 uses
 import DwaveHMC: init_static_H!, update_H_BdG!, diagonalize_H_BdG!, compute_forces!,
-                 compute_total_energy, hmc_sweep!, measure_transport_and_spectra
+                 compute_total_energy, hmc_sweep!, measure_observables,
+                 measure_transport_and_spectra
 
 const libdwhmc = get(ENV, "DWHMC_LIB", joinpath(@__DIR__, "..", "hybrid-monte-carlo-for-d-wave-sc_amd", "libdwhmc.so"))
 
@@ -36,7 +43,7 @@ mutable struct GPUCache
     delta_cap::Float64
 end
 
-function GPUCache(p::ModelParameters; device::Integer=0, delta_cap::Real=2.0)
+function GPUCache(p::ModelParameters; device::Integer=0, delta_cap::Real=0.0)   # <= 0: max(2, 6 sqrt(2J/β))
     c = GPUCache(C_NULL, zeros(ComplexF64, p.N, 2), 0.0, Int32(device), Float64(delta_cap))
     finalizer(c) do c
         c.ctx == C_NULL || ccall((:dwh_destroy, libdwhmc), Cvoid, (Ptr{Cvoid},), c.ctx)
@@ -94,24 +101,72 @@ function compute_total_energy(cache::GPUCache, p::ModelParameters, state::Simula
     return h[]
 end
 
-# src/HMC.jl:71-144: the reference's own RNG draws (randn!, rand) are taken
-# here and handed to the device, so a seeded Julia RNG reproduces a run.
+# src/HMC.jl:71-144.  The reference's own RNG draws are taken here in the
+# reference's order: randn! for the momenta (:53) before the trajectory, and
+# rand() only when ΔH >= 0 (the short-circuit `ΔH < 0 || rand() < exp(-ΔH)`
+# of :128), so a seeded Julia RNG is consumed exactly as DwaveHMC consumes it.
+# The device runs the trajectory (dwh_hmc_trajectory) and, after the host's
+# decision, restores a rejected chain (dwh_hmc_finish).
 function hmc_sweep!(cache::GPUCache, p::ModelParameters, state::SimulationState; Nt::Int, dt::Float64)
     noise = randn(ComplexF64, p.N, 2)
-    u = Ref(rand())
-    acc = Ref{UInt8}(0)
     dH = Ref{Float64}(0.0)
     GC.@preserve state noise begin
         check(cache.ctx, ccall((:dwh_set_state, libdwhmc), Cint,
                                (Ptr{Cvoid}, Ptr{ComplexF64}, Ptr{ComplexF64}), cache.ctx, state.Δ, C_NULL))
-        check(cache.ctx, ccall((:dwh_hmc_sweep, libdwhmc), Cint,
-                               (Ptr{Cvoid}, Ptr{ComplexF64}, Ref{Float64}, Int64, Float64, Float64,
-                                Ref{UInt8}, Ref{Float64}),
-                               cache.ctx, noise, u, Nt, dt, p.mass, acc, dH))
+        check(cache.ctx, ccall((:dwh_hmc_trajectory, libdwhmc), Cint,
+                               (Ptr{Cvoid}, Ptr{ComplexF64}, Int64, Float64, Float64, Ref{Float64}),
+                               cache.ctx, noise, Nt, dt, p.mass, dH))
+        ΔH = dH[]
+        accepted = ΔH < 0 || rand() < exp(-ΔH)
+        check(cache.ctx, ccall((:dwh_hmc_finish, libdwhmc), Cint, (Ptr{Cvoid}, Ref{UInt8}),
+                               cache.ctx, Ref{UInt8}(accepted ? 1 : 0)))
         check(cache.ctx, ccall((:dwh_get_state, libdwhmc), Cint,
                                (Ptr{Cvoid}, Ptr{ComplexF64}, Ptr{ComplexF64}), cache.ctx, state.Δ, state.π))
     end
-    return acc[] != 0, dH[]
+    ef = Ref{Float64}(0.0)
+    check(cache.ctx, ccall((:dwh_fermion_energy, libdwhmc), Cint, (Ptr{Cvoid}, Ref{Float64}), cache.ctx, ef))
+    cache.E_fermion = ef[]
+    return accepted, ΔH
+end
+
+# src/Observables.jl:88-222 from what the factorisation caches instead of the
+# eigenpairs: E_f (dwh_fermion_energy, = -Σ_{E>0}(βE + 2 log1pexp(-βE)) of
+# :147-156), P_ij (dwh_pairing, the ρ sums of :172-198) and Tr ρ_hh
+# (dwh_hole_trace; hole_conc = 2 Tr ρ_hh / N - 1, SURVEY.md I4, = the u/v
+# tanh sum of :120-145).  Same arithmetic as the reference on Δ, same fields.
+function measure_observables(cache::GPUCache, p::ModelParameters, state::SimulationState)
+    N = p.N
+    sum_amp = 0.0
+    sum_local = 0.0
+    sum_global = 0.0 + 0.0im
+    @inbounds for i in 1:N
+        dx = state.Δ[i, 1]
+        dy = state.Δ[i, 2]
+        sum_amp += 0.5 * (abs(dx) + abs(dy))
+        sum_local += 0.5 * abs(dx - dy)
+        sum_global += 0.5 * (dx - dy)
+    end
+    ef = Ref{Float64}(0.0)
+    trhh = Ref{Float64}(0.0)
+    P = zeros(ComplexF64, N, 2)
+    check(cache.ctx, ccall((:dwh_fermion_energy, libdwhmc), Cint, (Ptr{Cvoid}, Ref{Float64}), cache.ctx, ef))
+    check(cache.ctx, ccall((:dwh_hole_trace, libdwhmc), Cint, (Ptr{Cvoid}, Ref{Float64}), cache.ctx, trhh))
+    GC.@preserve P check(cache.ctx, ccall((:dwh_pairing, libdwhmc), Cint, (Ptr{Cvoid}, Ptr{ComplexF64}),
+                                          cache.ctx, P))
+    E_boson = p.β / (2 * p.J) * sum(abs2, state.Δ)
+    sum_diff = 0.0
+    sum_pair_global = 0.0 + 0.0im
+    sum_pair_local = 0.0
+    @inbounds for i in 1:N
+        P_x, P_y = P[i, 1], P[i, 2]
+        sum_diff += (abs(state.Δ[i, 1] - p.J * P_x) + abs(state.Δ[i, 2] - p.J * P_y)) / 2.0
+        term = p.J * 0.5 * (P_x - P_y)
+        sum_pair_local += abs(term)
+        sum_pair_global += term
+    end
+    return DwaveHMC.ObservablesResult((ef[] + E_boson) / N, sum_amp / N, sum_local / N,
+                                      abs(sum_global / N), abs2(sum_global / N), 2.0 * trhh[] / N - 1.0,
+                                      sum_diff / N, abs(sum_pair_global / N), sum_pair_local / N)
 end
 
 # src/Observables.jl:314-526 on the device (eigenpairs by rocSOLVER, sums in HIP
@@ -129,6 +184,41 @@ function measure_transport_and_spectra(cache::GPUCache, p::ModelParameters)
                            cache.ctx, 0, p.η, p.Δω, p.ω_max, st, dc, σ, nw[], dos, dos_AN, nd[], ak))
     return DwaveHMC.SpectrumResult(st[], dc[], collect(p.ω_min:p.Δω:p.ω_max), σ,
                                    collect(-p.ω_max:p.Δω:p.ω_max), dos, dos_AN, ak)
+end
+
+# ---------------------------------------------------------------------------
+# run_simulation on the GPU.  The reference constructs its cache inside the
+# driver (`cache = initialize_cache(p)`, src/Simulation.jl:82), so the driver
+# is taken from DwaveHMC's own source file and evaluated here with exactly
+# that call replaced by `GPUCache(p)`; every other line — adaptive Nt,
+# observables.csv, transport.csv, JLD2 bins, log — is the reference's, and
+# every cache-typed call in it (init_static_H!, update_H_BdG!,
+# diagonalize_H_BdG! :84-86, hmc_sweep! :105/:153, measure_observables :157,
+# measure_transport_and_spectra :171) dispatches to the methods above.
+# ---------------------------------------------------------------------------
+_swap_cache(x) = x
+function _swap_cache(ex::Expr)
+    if ex.head == :call && ex.args[1] === :initialize_cache
+        return Expr(:call, :GPUCache, map(_swap_cache, ex.args[2:end])...)
+    end
+    return Expr(ex.head, map(_swap_cache, ex.args)...)
+end
+
+_defines(ex, name) = ex isa Expr && ((ex.head == :function && ex.args[1] isa Expr &&
+                                      ex.args[1].args[1] === name) ||
+                                     (ex.head == :macrocall && any(a -> _defines(a, name), ex.args)))
+
+function __init__()
+    src = read(joinpath(dirname(pathof(DwaveHMC)), "Simulation.jl"), String)
+    top = Meta.parseall(src)
+    n = 0
+    for ex in top.args
+        if _defines(ex, :run_simulation)
+            Core.eval(@__MODULE__, _swap_cache(ex))
+            n += 1
+        end
+    end
+    n == 1 || error("DwaveHMCGPU: run_simulation not found in DwaveHMC's Simulation.jl")
 end
 
 end # module

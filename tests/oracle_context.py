@@ -96,5 +96,24 @@ class OracleContext:
             self.pi[c] = st.pi
         return acc, dH
 
+    def hmc_trajectory(self, noise, Nt, dt, mass):
+        """dwh_hmc_trajectory: the sweep with the Metropolis decision deferred
+        (run accepted, the pre-trajectory state kept for hmc_finish)."""
+        self._backup = [(self.Delta[c].copy(), cache.E_n.copy(), cache.U.copy())
+                        for c, cache in enumerate(self.caches)]
+        _, dH = self.hmc_sweep(noise, np.full(self.nchains, -1.0), Nt, dt, mass)
+        return dH
+
+    def hmc_finish(self, accepted):
+        acc = np.atleast_1d(np.asarray(accepted)).astype(bool)
+        for c, cache in enumerate(self.caches):
+            if not acc[c]:                                   # src/HMC.jl:130-141
+                D, E, U = self._backup[c]
+                self.Delta[c] = D
+                cache.E_n[:] = E
+                cache.U[:, :] = U
+                O.update_H_BdG(cache, self.p, self.Delta[c])
+        self._backup = None
+
     def close(self):
         pass

@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def header_symbols():
     src = open(os.path.join(ROOT, "include", "dwhmc.h")).read()
-    return sorted(set(re.findall(r"\b(dwh_[a-z_0-9]+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(dwh_[A-Za-z_0-9]+)\s*\(", src)))
 
 
 def test_library_exports_every_header_symbol(dwhmc):

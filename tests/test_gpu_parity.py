@@ -213,15 +213,93 @@ def test_throughput_path_equals_single_sweeps(dwhmc, oracle, algo):
     b.close()
 
 
-def test_spectrum_guard_trips(dwhmc, oracle, algo):
+def test_spectrum_guard_reselects_on_upload(dwhmc, oracle, algo):
+    """An uploaded Δ above delta_cap re-selects the pole set for it (the
+    reference accepts any Δ, src/HMC.jl:98-114) instead of silently using
+    poles that do not cover the spectrum."""
     O = oracle
     p, dis, Delta0 = make_case(O, 4, 4, 4.0, seed=1, amp=0.9)
     ctx = device_ctx(dwhmc, p, dis, algo, delta_cap=0.5)
+    kap0 = ctx.info["kappa"]
     ctx.set_pairing(Delta0)
+    inf = ctx.info
+    assert inf["delta_cap"] >= 1.5 * np.max(np.abs(Delta0)) and inf["kappa"] > kap0
     ctx.factorize()
-    noise = np.zeros((p.N, 2), dtype=np.complex128)
-    with pytest.raises(dwhmc.SpectrumGuardError):
-        ctx.hmc_sweep(noise, np.array([0.5]), 2, 0.05, 1.0)
+    _, F_ref, Ef_ref = O.evaluate(p, dis, Delta0)
+    assert np.max(np.abs(ctx.forces()[0] - F_ref)) <= 1e-10 * (1 + np.max(np.abs(F_ref)))
+    assert abs(ctx.fermion_energy()[0] - Ef_ref) <= 1e-11 * abs(Ef_ref)
+    ctx.close()
+
+
+def test_spectrum_guard_reselects_mid_sweep(dwhmc, oracle, algo):
+    """A trajectory that drifts |Δ| past the cap is rerun from its start with a
+    re-selected pole set; the result is that of a context built with the final
+    cap from the outset, and matches the oracle."""
+    O = oracle
+    p, dis, Delta0 = make_case(O, 4, 4, 4.0, seed=2, amp=0.0)
+    rng = np.random.default_rng(3)
+    noise = 8.0 * (rng.standard_normal((p.N, 2)) + 1j * rng.standard_normal((p.N, 2))) * math.sqrt(0.5)
+    Nt, dt = 4, 0.1
+    a = device_ctx(dwhmc, p, dis, algo, delta_cap=0.2)
+    a.set_pairing(Delta0)
+    a.factorize()
+    acc_a, dH_a = a.hmc_sweep(noise, np.array([0.3]), Nt, dt, p.mass)
+    cap = a.info["delta_cap"]
+    assert cap > 0.2
+    b = device_ctx(dwhmc, p, dis, algo, delta_cap=cap)
+    b.set_pairing(Delta0)
+    b.factorize()
+    acc_b, dH_b = b.hmc_sweep(noise, np.array([0.3]), Nt, dt, p.mass)
+    assert acc_a[0] == acc_b[0] and dH_a[0] == dH_b[0]
+    for x, y in zip(a.get_state(), b.get_state()):
+        assert np.array_equal(x, y)
+    cache = O.initialize_cache(p)
+    O.init_static_H(cache, p, dis)
+    O.update_H_BdG(cache, p, Delta0)
+    O.diagonalize_H_BdG(cache, p)
+    st = O.SimulationState(dis, Delta0.copy(), np.zeros_like(Delta0))
+    acc_r, dH_r = O.hmc_sweep(cache, p, st, Nt, dt, noise, 0.3)
+    assert acc_a[0] == acc_r and abs(dH_a[0] - dH_r) <= 1e-8 * (1 + abs(dH_r))
+    a.close()
+    b.close()
+
+
+def test_default_delta_cap_follows_temperature(dwhmc, oracle):
+    """delta_cap <= 0 selects max(2, 6 sqrt(2J/β)): wide enough for the boson
+    fluctuations of the reference's high-temperature scans
+    (scripts/batch_scan_T.jl:21-22 goes up to T = 1000)."""
+    O = oracle
+    for beta in (16.0, 0.5, 1e-3):
+        p, dis, _ = make_case(O, 4, 4, beta, seed=4)
+        ctx = device_ctx(dwhmc, p, dis, "auto", delta_cap=0.0)
+        assert ctx.info["delta_cap"] == pytest.approx(max(2.0, 6.0 * math.sqrt(2 * J / beta)))
+        ctx.close()
+
+
+def test_high_temperature_sweeps_match_oracle(dwhmc, oracle):
+    """T = 2 (β = 0.5): |Δ| ~ sqrt(2J/β) ~ 1.8, beyond the old fixed cap of 2 in a
+    few bonds; sweeps run without a guard failure and match the oracle."""
+    O = oracle
+    p, dis, _ = make_case(O, 6, 6, 0.5, seed=8)
+    rng = np.random.default_rng(12)
+    Delta = (rng.standard_normal((p.N, 2)) + 1j * rng.standard_normal((p.N, 2))) * math.sqrt(p.J / p.beta)
+    ctx = device_ctx(dwhmc, p, dis, "auto", delta_cap=0.0)
+    ctx.set_pairing(Delta)
+    ctx.factorize()
+    cache = O.initialize_cache(p)
+    O.init_static_H(cache, p, dis)
+    O.update_H_BdG(cache, p, Delta)
+    O.diagonalize_H_BdG(cache, p)
+    st = O.SimulationState(dis, Delta.copy(), np.zeros_like(Delta))
+    dt = O.calc_optimal_dt(p.beta, p.J, p.mass, 10)
+    for s in range(4):
+        noise = (rng.standard_normal((p.N, 2)) + 1j * rng.standard_normal((p.N, 2))) * math.sqrt(0.5)
+        u = rng.random()
+        acc, dH = ctx.hmc_sweep(noise, np.array([u]), 10, dt, p.mass)
+        acc_r, dH_r = O.hmc_sweep(cache, p, st, 10, dt, noise, u)
+        assert acc[0] == acc_r and abs(dH[0] - dH_r) <= 1e-8 * (1 + abs(dH_r)), (s, dH[0], dH_r)
+    D, _ = ctx.get_state()
+    assert np.max(np.abs(D[0] - st.Delta)) <= 1e-10
     ctx.close()
 
 
@@ -322,3 +400,43 @@ def test_cr_block_product_variants(dwhmc, oracle, monkeypatch, cfg, Lx, Ly):
     Ef = ctx.fermion_energy()[0]
     assert abs(Ef - Ef_ref) <= 1e-11 * abs(Ef_ref), (Ef, Ef_ref)
     ctx.close()
+
+
+def test_split_trajectory_matches_sweep(dwhmc, oracle):
+    """dwh_hmc_trajectory + dwh_hmc_finish (the host decides acceptance, as the
+    Julia binding does to consume its RNG like src/HMC.jl:128) reproduce
+    dwh_hmc_sweep bit for bit, accepted and rejected sweeps alike."""
+    O = oracle
+    p, dis, Delta = make_case(O, 4, 4, 8.0, seed=3)
+    a = device_ctx(dwhmc, p, dis)
+    b = device_ctx(dwhmc, p, dis)
+    for c in (a, b):
+        c.set_pairing(Delta)
+        c.factorize()
+    rng = np.random.default_rng(9)
+    dt = O.calc_optimal_dt(p.beta, p.J, p.mass, 2)      # coarse: some trajectories are rejected
+    seen = set()
+    for _ in range(8):
+        noise = (rng.standard_normal((p.N, 2)) + 1j * rng.standard_normal((p.N, 2))) * math.sqrt(0.5)
+        u = rng.random()
+        acc1, dH1 = a.hmc_sweep(noise, np.array([u]), 4, dt, p.mass)
+        dH2 = b.hmc_trajectory(noise, 4, dt, p.mass)
+        acc2 = bool(dH2[0] < 0 or u < math.exp(-dH2[0]))
+        b.hmc_finish([acc2])
+        assert acc1[0] == acc2 and dH1[0] == dH2[0]
+        seen.add(acc2)
+        for x, y in zip(a.get_state(), b.get_state()):
+            assert np.array_equal(x, y)
+        assert np.array_equal(a.pairing(), b.pairing())
+        assert np.array_equal(a.fermion_energy(), b.fermion_energy())
+    assert seen == {True, False}
+    # call order is enforced
+    noise = np.zeros((p.N, 2), dtype=np.complex128)
+    b.hmc_trajectory(noise, 1, dt, p.mass)
+    with pytest.raises(dwhmc.DwhError):
+        b.hmc_sweep(noise, np.array([0.5]), 1, dt, p.mass)
+    b.hmc_finish([False])
+    with pytest.raises(dwhmc.DwhError):
+        b.hmc_finish([True])
+    a.close()
+    b.close()

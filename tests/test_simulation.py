@@ -106,3 +106,34 @@ def test_run_simulation_device_matches_oracle(sim, hmc_mod, dwhmc, tmp_path):
             assert abs(getattr(s1, f) - getattr(s2, f)) <= 1e-8 * (1 + abs(getattr(s2, f))), (i, f)
         assert np.max(np.abs(s1.optical_conductivity - s2.optical_conductivity)) <= \
             1e-8 * (1 + np.max(np.abs(s2.optical_conductivity)))
+
+
+def test_host_sweep_consumes_rng_like_reference(hmc_mod, dwhmc):
+    """hmc_sweep with an rng draws the momenta, then rand() only when ΔH >= 0
+    (src/HMC.jl:53,128), so a seeded generator runs in the reference's order."""
+    p = dwhmc.ModelParameters(3, 3, 1.0, -0.35, -1.08, 1.0, 0.25, 8.0, 0.8, 1.0)
+    saved = hmc_mod.FermionContext
+    hmc_mod.FermionContext = OracleContext
+    try:
+        st = dwhmc.initialize_state(p, np.random.default_rng(1))
+        cache = dwhmc.initialize_cache(p)
+        dwhmc.init_static_H(cache, p, st)
+        dwhmc.update_H_BdG(cache, p, st)
+        dwhmc.diagonalize_H_BdG(cache, p)
+        rng = np.random.default_rng(42)
+        replay = np.random.default_rng(42)
+        dt = dwhmc.calc_optimal_dt(p.beta, p.J, p.mass, 2)
+        signs = set()
+        for _ in range(12):
+            acc, dH = dwhmc.hmc_sweep(cache, p, st, Nt=4, dt=dt, rng=rng)
+            dwhmc.standard_complex_normal(replay, (p.N, 2))
+            if dH >= 0:
+                u = replay.random()
+                assert acc == (u < np.exp(-dH))
+            else:
+                assert acc
+            signs.add(dH >= 0)
+        assert signs == {True, False}
+        assert rng.random() == replay.random()
+    finally:
+        hmc_mod.FermionContext = saved
