@@ -223,7 +223,7 @@ def test_spectrum_guard_reselects_on_upload(dwhmc, oracle, algo):
     kap0 = ctx.info["kappa"]
     ctx.set_pairing(Delta0)
     inf = ctx.info
-    assert inf["delta_cap"] >= 1.5 * np.max(np.abs(Delta0)) and inf["kappa"] > kap0
+    assert inf["delta_cap"] >= 1.5 * np.max(np.abs(Delta0)) * (1 - 1e-12) and inf["kappa"] > kap0
     ctx.factorize()
     _, F_ref, Ef_ref = O.evaluate(p, dis, Delta0)
     assert np.max(np.abs(ctx.forces()[0] - F_ref)) <= 1e-10 * (1 + np.max(np.abs(F_ref)))
@@ -414,11 +414,11 @@ def test_split_trajectory_matches_sweep(dwhmc, oracle):
         c.set_pairing(Delta)
         c.factorize()
     rng = np.random.default_rng(9)
-    dt = O.calc_optimal_dt(p.beta, p.J, p.mass, 2)      # coarse: some trajectories are rejected
-    seen = set()
-    for _ in range(8):
+    dt = O.calc_optimal_dt(p.beta, p.J, p.mass, 1)      # coarse, and u near 1 on odd sweeps:
+    seen = set()                                         # some trajectories are rejected
+    for k in range(8):
         noise = (rng.standard_normal((p.N, 2)) + 1j * rng.standard_normal((p.N, 2))) * math.sqrt(0.5)
-        u = rng.random()
+        u = 0.9999 if k % 2 else rng.random()
         acc1, dH1 = a.hmc_sweep(noise, np.array([u]), 4, dt, p.mass)
         dH2 = b.hmc_trajectory(noise, 4, dt, p.mass)
         acc2 = bool(dH2[0] < 0 or u < math.exp(-dH2[0]))
