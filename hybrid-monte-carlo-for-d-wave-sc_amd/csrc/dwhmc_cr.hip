@@ -399,12 +399,74 @@ __global__ __launch_bounds__(64 * NT) void k_cr_inv(double2* __restrict__ pool, 
 // 1D grid with the XCD-aware remap so one item's tasks share an XCD's L2.
 // out never aliases an operand (planner invariant); out == cin is allowed.
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ double flip_sign(double x, unsigned m) {
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, x);
+  return __builtin_bit_cast(double, b ^ ((unsigned long long)m << 32));
+}
+
+// One term's K range of this wave: t1 += Ar Br, t2 += Ai Bi, t3 += (Ar + Ai)(Br + Bi).
+// Synthesised B rows are sgn * conj(u): Br = sgn ux, Bi = -sgn uy,
+// Br + Bi = sgn (ux - uy).  The signs are applied by flipping the sign bit
+// with a 32-bit integer XOR (smask = 0x80000000 when sgn < 0), not by fp64
+// multiplies: fp64 VALU ops share the DP pipe with the f64 MFMAs and stall
+// it (tools/micro/mfma_valu_coexec.hip: ~10-15 cycles per interleaved
+// v_mul/v_add_f64).  The products are the ones the explicit sign multiplies
+// gave, bit for bit.
+template <int BP, int MI, int KSPLIT, int KQ>
+__device__ __forceinline__ void cr_term(const double2* A, const double2* Bt, int c0, int crot, unsigned smask,
+                                        d4 (&t1)[MI][MI], d4 (&t2)[MI][MI], d4 (&t3)[MI][MI]) {
+  constexpr int HP = BP / 2, KS = BP / 4, KH = HP / 4, KSS = KS / KSPLIT, S0 = KQ * KSS;
+  constexpr int PF = KSS < (MI == 1 ? 4 : 2) ? KSS : (MI == 1 ? 4 : 2);
+  auto load = [&](int s, double2 (&a)[MI], double2 (&b)[MI]) {
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi) a[mi] = A[(int64_t)16 * mi * BP + s * 4];
+#pragma unroll
+    for (int ni = 0; ni < MI; ++ni)
+      b[ni] = s < KH ? Bt[(int64_t)s * 4 * BP + c0 + 16 * ni] : Bt[(int64_t)(s - KH) * 4 * BP + crot + 16 * ni];
+  };
+  double2 fa[PF][MI], fb[PF][MI];
+#pragma unroll
+  for (int p = 0; p < PF; ++p) load(S0 + p, fa[p], fb[p]);
+#pragma unroll
+  for (int j = 0; j < KSS; ++j) {
+    const int cs = j % PF;
+    const bool syn = S0 + j >= KH;   // compile time
+    double ar[MI], ai[MI], as[MI], br[MI], bi[MI], bs[MI];
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi) {
+      ar[mi] = fa[cs][mi].x;
+      ai[mi] = fa[cs][mi].y;
+      as[mi] = ar[mi] + ai[mi];
+      if (syn) {
+        const double ux = fb[cs][mi].x, uy = fb[cs][mi].y;
+        br[mi] = flip_sign(ux, smask);
+        bi[mi] = flip_sign(uy, smask ^ 0x80000000u);
+        bs[mi] = flip_sign(ux - uy, smask);
+      } else {
+        br[mi] = fb[cs][mi].x;
+        bi[mi] = fb[cs][mi].y;
+        bs[mi] = br[mi] + bi[mi];
+      }
+    }
+    if (j + PF < KSS) load(S0 + j + PF, fa[cs], fb[cs]);
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < MI; ++ni) {
+        t1[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[mi], br[ni], t1[mi][ni], 0, 0, 0);
+        t2[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[mi], bi[ni], t2[mi][ni], 0, 0, 0);
+        t3[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(as[mi], bs[ni], t3[mi][ni], 0, 0, 0);
+      }
+  }
+}
+
+// This wave's share of an output tile over all terms (the stage sign sg is
+// applied in the epilogue: negating every A fragment negates the sums exactly).
 template <int BP, int MI, int KSPLIT, int KQ>
 __device__ __forceinline__ void cr_tile_part(const double2* base, const CrTask* tk, int nt, int tr,
-                                             int tc, double sg, d4 (&t1)[MI][MI], d4 (&t2)[MI][MI],
+                                             int tc, d4 (&t1)[MI][MI], d4 (&t2)[MI][MI],
                                              d4 (&t3)[MI][MI]) {
-  constexpr int TS = 16 * MI, HP = BP / 2, KS = BP / 4, KH = HP / 4, KSS = KS / KSPLIT, S0 = KQ * KSS;
-  constexpr int PF = KSS < (MI == 1 ? 4 : 2) ? KSS : (MI == 1 ? 4 : 2);
+  constexpr int TS = 16 * MI, HP = BP / 2;
   constexpr int64_t BB = (int64_t)HP * BP;
   const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
   const int c0 = tc * TS, crot = c0 < HP ? c0 + HP : c0 - HP;
@@ -413,47 +475,9 @@ __device__ __forceinline__ void cr_tile_part(const double2* base, const CrTask* 
     const double2* A = base + tk->a[h] * BB + (int64_t)(tr * TS + lr) * BP + lk;
     const double2* Bt = base + tk->b[h] * BB + (int64_t)lk * BP + lr;
     // synthesised rows: sgn * conj(.), sgn = -s (left column half) / +s (right), s = +1 Q, -1 M
-    const double sb = ((tk->bq >> h) & 1) ? 1.0 : -1.0;
-    const double sgn = c0 < HP ? -sb : sb;
-    auto load = [&](int s, double2 (&a)[MI], double2 (&b)[MI]) {
-#pragma unroll
-      for (int mi = 0; mi < MI; ++mi) a[mi] = A[(int64_t)16 * mi * BP + s * 4];
-#pragma unroll
-      for (int ni = 0; ni < MI; ++ni) {
-        if (s < KH) {
-          b[ni] = Bt[(int64_t)s * 4 * BP + c0 + 16 * ni];
-        } else {
-          const double2 u = Bt[(int64_t)(s - KH) * 4 * BP + crot + 16 * ni];
-          b[ni] = make_double2(sgn * u.x, -sgn * u.y);
-        }
-      }
-    };
-    double2 fa[PF][MI], fb[PF][MI];
-#pragma unroll
-    for (int p = 0; p < PF; ++p) load(S0 + p, fa[p], fb[p]);
-#pragma unroll
-    for (int j = 0; j < KSS; ++j) {
-      const int cs = j % PF;
-      double ar[MI], ai[MI], as[MI], br[MI], bi[MI], bs[MI];
-#pragma unroll
-      for (int mi = 0; mi < MI; ++mi) {
-        ar[mi] = sg * fa[cs][mi].x;
-        ai[mi] = sg * fa[cs][mi].y;
-        as[mi] = ar[mi] + ai[mi];
-        br[mi] = fb[cs][mi].x;
-        bi[mi] = fb[cs][mi].y;
-        bs[mi] = br[mi] + bi[mi];
-      }
-      if (j + PF < KSS) load(S0 + j + PF, fa[cs], fb[cs]);
-#pragma unroll
-      for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < MI; ++ni) {
-          t1[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[mi], br[ni], t1[mi][ni], 0, 0, 0);
-          t2[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[mi], bi[ni], t2[mi][ni], 0, 0, 0);
-          t3[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(as[mi], bs[ni], t3[mi][ni], 0, 0, 0);
-        }
-    }
+    const bool q = (tk->bq >> h) & 1;
+    const unsigned smask = ((c0 < HP) == q) ? 0x80000000u : 0u;   // sgn < 0
+    cr_term<BP, MI, KSPLIT, KQ>(A, Bt, c0, crot, smask, t1, t2, t3);
   }
 }
 
@@ -518,13 +542,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 #endif
   if (valid) {
     const int nt = tk->nt;
-    if (KSPLIT == 1 || kq == 0) cr_tile_part<BP, MI, KSPLIT, 0>(base, tk, nt, tr, tc, sg, t1, t2, t3);
+    if (KSPLIT == 1 || kq == 0) cr_tile_part<BP, MI, KSPLIT, 0>(base, tk, nt, tr, tc, t1, t2, t3);
     if constexpr (KSPLIT >= 2) {
-      if (kq == 1) cr_tile_part<BP, MI, KSPLIT, 1>(base, tk, nt, tr, tc, sg, t1, t2, t3);
+      if (kq == 1) cr_tile_part<BP, MI, KSPLIT, 1>(base, tk, nt, tr, tc, t1, t2, t3);
     }
     if constexpr (KSPLIT == 4) {
-      if (kq == 2) cr_tile_part<BP, MI, KSPLIT, 2>(base, tk, nt, tr, tc, sg, t1, t2, t3);
-      if (kq == 3) cr_tile_part<BP, MI, KSPLIT, 3>(base, tk, nt, tr, tc, sg, t1, t2, t3);
+      if (kq == 2) cr_tile_part<BP, MI, KSPLIT, 2>(base, tk, nt, tr, tc, t1, t2, t3);
+      if (kq == 3) cr_tile_part<BP, MI, KSPLIT, 3>(base, tk, nt, tr, tc, t1, t2, t3);
     }
   }
   auto put = [&](int v, double2 x) {
@@ -544,7 +568,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
   auto partial = [&](int v) {
     const int mi = v / (MI * 4), ni = (v / 4) % MI, rr = v % 4;
     const double a = t1[mi][ni][rr], b = t2[mi][ni][rr], c = t3[mi][ni][rr];
-    return make_double2(a - b, c - a - b);
+    return make_double2(sg * (a - b), sg * (c - a - b));
   };
   if constexpr (KSPLIT == 1) {
     if (!valid) return;
