@@ -712,6 +712,109 @@ int check_flag(dwh_ctx* ctx) {
   return DWH_OK;
 }
 
+// Spectral radius of the static particle block h of one chain (real
+// symmetric, rows hrow + diagonal w_i - mu), by Lanczos with full
+// reorthogonalisation from a fixed pseudo-random start: the extreme Ritz
+// values converge first; the returned bound adds the residual |β s_m| of the
+// extreme Ritz pairs and a 2 % margin.  For
+// N <= the step count the Krylov space is all of R^N and the Ritz values are
+// the spectrum.  The caller takes min(this, the Gershgorin bound).
+double spectral_radius_bound(const std::vector<std::vector<std::pair<int, double>>>& hrow,
+                             const double* diag, int N) {
+  const int k = std::min(N, 160);
+  std::vector<std::vector<double>> Q;
+  std::vector<double> alpha, beta;
+  std::vector<double> q(N), w(N);
+  uint64_t st = 0x9E3779B97F4A7C15ull;
+  double nrm = 0;
+  for (int i = 0; i < N; ++i) {
+    st ^= st << 13;
+    st ^= st >> 7;
+    st ^= st << 17;
+    q[i] = (double)(st >> 11) * 0x1.0p-53 - 0.5;
+    nrm += q[i] * q[i];
+  }
+  for (double& x : q) x /= std::sqrt(nrm);
+  double bnext = 0;
+  for (int j = 0; j < k; ++j) {
+    Q.push_back(q);
+    for (int i = 0; i < N; ++i) {
+      double v = diag[i] * q[i];
+      for (const auto& e : hrow[i]) v += e.second * q[e.first];
+      w[i] = v;
+    }
+    double a = 0;
+    for (int i = 0; i < N; ++i) a += w[i] * q[i];
+    alpha.push_back(a);
+    for (int pass = 0; pass < 2; ++pass)
+      for (const auto& qq : Q) {
+        double c = 0;
+        for (int i = 0; i < N; ++i) c += w[i] * qq[i];
+        for (int i = 0; i < N; ++i) w[i] -= c * qq[i];
+      }
+    double b = 0;
+    for (int i = 0; i < N; ++i) b += w[i] * w[i];
+    b = std::sqrt(b);
+    bnext = b;
+    if (j + 1 == k || b < 1e-12) break;
+    beta.push_back(b);
+    for (int i = 0; i < N; ++i) q[i] = w[i] / b;
+  }
+  // extreme eigenvalues of the tridiagonal T by bisection on Sturm counts
+  const int m = (int)alpha.size();
+  double lo = 0, hi = 0;
+  for (int i = 0; i < m; ++i) {
+    const double r = (i > 0 ? std::fabs(beta[i - 1]) : 0.0) + (i + 1 < m ? std::fabs(beta[i]) : 0.0);
+    lo = std::min(lo, alpha[i] - r);
+    hi = std::max(hi, alpha[i] + r);
+  }
+  auto count_below = [&](double x) {   // eigenvalues of T < x
+    int c = 0;
+    double d = 1.0;
+    for (int i = 0; i < m; ++i) {
+      d = alpha[i] - x - (i > 0 ? beta[i - 1] * beta[i - 1] / d : 0.0);
+      if (d == 0.0) d = 1e-300;
+      if (d < 0) ++c;
+    }
+    return c;
+  };
+  auto kth = [&](int idx) {   // idx-th smallest (0-based)
+    double a = lo, b = hi;
+    for (int it = 0; it < 200 && b - a > 1e-13 * std::max(1.0, std::fabs(b)); ++it) {
+      const double mid = 0.5 * (a + b);
+      if (count_below(mid) > idx) b = mid;
+      else a = mid;
+    }
+    return b;
+  };
+  // residual of the Ritz pair (θ, Q s) is |β_m s_m|: last component of the
+  // eigenvector s of T for θ, by inverse iteration on the tridiagonal system
+  auto resid_of = [&](double th) {
+    if (m == N) return 0.0;
+    std::vector<double> x(m, 1.0), c(m), d(m), y(m);
+    const double sh = th + 1e-10 * std::max(1.0, std::fabs(th));
+    for (int it = 0; it < 3; ++it) {
+      // Thomas solve (T - sh I) y = x
+      for (int i = 0; i < m; ++i) {
+        const double b = alpha[i] - sh - (i > 0 ? beta[i - 1] * c[i - 1] : 0.0);
+        const double bb = (b == 0.0) ? 1e-300 : b;
+        c[i] = (i + 1 < m) ? beta[i] / bb : 0.0;
+        d[i] = (x[i] - (i > 0 ? beta[i - 1] * d[i - 1] : 0.0)) / bb;
+      }
+      y[m - 1] = d[m - 1];
+      for (int i = m - 2; i >= 0; --i) y[i] = d[i] - c[i] * y[i + 1];
+      double n2 = 0;
+      for (double v : y) n2 += v * v;
+      const double inv = 1.0 / std::sqrt(n2);
+      for (int i = 0; i < m; ++i) x[i] = y[i] * inv;
+    }
+    return std::fabs(bnext * x[m - 1]);
+  };
+  const double tmin = kth(0), tmax = kth(m - 1);
+  const double rho = std::max(std::fabs(tmin) + resid_of(tmin), std::fabs(tmax) + resid_of(tmax));
+  return 1.02 * rho + 1e-12;
+}
+
 // Default guard on max|Δ_ij|: 2 (the ordered phase), or 6 standard deviations
 // of the Gaussian boson fluctuations <|Δ|²> = 2J/β at high temperature.
 double default_delta_cap(double beta, double J) {
@@ -819,7 +922,18 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
       bji[(size_t)dir * N + i] = j * kSlots + sji;
     }
 
-  // --- pole selection: E' >= Gershgorin bound of H_BdG with |Δ| <= delta_cap
+  // --- pole selection: E' >= ‖H_BdG‖ <= ‖h‖ + ‖pairing block‖ with
+  // ‖h‖ <= min(Gershgorin, Lanczos bound) and the pairing block's norm <= its
+  // max row sum 4 |Δ|/2 <= 2 delta_cap
+  {
+    double rho = 0;
+    std::vector<double> diag(N);
+    for (int64_t c = 0; c < nchains; ++c) {
+      for (int i = 0; i < N; ++i) diag[i] = disorder[c * N64 + i] - mu;
+      rho = std::max(rho, spectral_radius_bound(hrow, diag.data(), N));
+    }
+    hmax = std::min(hmax, rho);
+  }
   const double Eb = hmax + 2.0 * delta_cap;
   const double kneed = 0.5 * beta * Eb;
   int sel = -1;
