@@ -1029,7 +1029,7 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     }
     const bool ok = dwh::cr_supported_bp(BP);
     if (want == "cr" && !ok) {
-      ctx->err = "DWHMC_ALGO=cr needs 2*Lx <= 96";
+      ctx->err = "DWHMC_ALGO=cr needs 2*Lx <= 128";
       g_create_error = ctx->err;
       delete ctx;
       return DWH_ERR_ARG;

@@ -711,7 +711,7 @@ __global__ __launch_bounds__(256) void k_cr_fermion_energy(const double2* __rest
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
-bool cr_supported_bp(int BP) { return BP == 32 || BP == 64 || BP == 96; }
+bool cr_supported_bp(int BP) { return BP == 32 || BP == 64 || BP == 96 || BP == 128; }
 
 void launch_cr_fill(const CrDims& c, double2* pool, const int* list, int nlist, const int* hcol,
                     const double* hval, const int* Dcol, const int* Dsrc, const double2* Delta,
@@ -732,7 +732,8 @@ void launch_cr_inv(const CrDims& c, double2* pool, const int* blk, const int* ds
   switch (c.BP) {
     case 32: hipLaunchKernelGGL(k_cr_inv<2>, g, dim3(128), 0, s, pool, c.item, blk, dst, slot, ldpart, c.Ly); break;
     case 64: hipLaunchKernelGGL(k_cr_inv<4>, g, dim3(256), 0, s, pool, c.item, blk, dst, slot, ldpart, c.Ly); break;
-    default: hipLaunchKernelGGL(k_cr_inv<6>, g, dim3(384), 0, s, pool, c.item, blk, dst, slot, ldpart, c.Ly); break;
+    case 96: hipLaunchKernelGGL(k_cr_inv<6>, g, dim3(384), 0, s, pool, c.item, blk, dst, slot, ldpart, c.Ly); break;
+    default: hipLaunchKernelGGL(k_cr_inv<8>, g, dim3(512), 0, s, pool, c.item, blk, dst, slot, ldpart, c.Ly); break;
   }
 }
 
@@ -787,7 +788,8 @@ void launch_cr_gemm(const CrDims& c, double2* pool, const CrTask* tasks, int nta
   switch (c.BP) {
     case 32: CR_GEMM_BP(32) break;
     case 64: CR_GEMM_BP(64) break;
-    default: CR_GEMM_BP(96) break;
+    case 96: CR_GEMM_BP(96) break;
+    default: CR_GEMM_BP(128) break;
   }
 #undef CR_GEMM_BP
 #undef CR_GEMM

@@ -349,9 +349,9 @@ def test_golden_fixture_on_device(dwhmc, L, algo):
 
 
 def test_cr_block_limit(dwhmc, oracle):
-    """DWH_ALGO_CR needs the padded lattice-row block 2 Lx <= 96; auto falls back to dense."""
+    """DWH_ALGO_CR needs the padded lattice-row block 2 Lx <= 128; auto falls back to dense."""
     O = oracle
-    p, dis, _ = make_case(O, 49, 2, 4.0, seed=1)
+    p, dis, _ = make_case(O, 65, 2, 4.0, seed=1)
     with pytest.raises(ValueError):
         device_ctx(dwhmc, p, dis, "cr")
     ctx = device_ctx(dwhmc, p, dis)
@@ -359,7 +359,8 @@ def test_cr_block_limit(dwhmc, oracle):
     ctx.close()
 
 
-@pytest.mark.parametrize("Lx,Ly", [(4, 1), (6, 2), (5, 3), (3, 9), (7, 6), (48, 5), (16, 13)])
+@pytest.mark.parametrize("Lx,Ly", [(4, 1), (6, 2), (5, 3), (3, 9), (7, 6), (48, 5), (16, 13), (64, 1), (64, 2),
+                                   (64, 3), (50, 4), (57, 2)])
 def test_cr_ragged_chains(dwhmc, oracle, Lx, Ly):
     """Cyclic-reduction chains of every shape: Ly = 1 (one block), 2 (single
     off-diagonal block), odd lengths at every level, padded blocks (2 Lx not a
@@ -440,3 +441,56 @@ def test_split_trajectory_matches_sweep(dwhmc, oracle):
         b.hmc_finish([True])
     a.close()
     b.close()
+
+
+def test_cr_bp128_matches_dense_L64(dwhmc, oracle):
+    """L = 64 (BP = 128 lattice-row blocks, k_cr_inv<8>): the CR path against the
+    dense Schur-complement path of the same context parameters (both through
+    the C ABI; the eigen oracle at n = 8192 is too slow for a unit test; the
+    small-Ly BP = 128 lattices are checked against the oracle in
+    test_cr_ragged_chains)."""
+    O = oracle
+    p, dis, Delta = make_case(O, 64, 64, 8.0, seed=64)
+    res = {}
+    for algo in ("cr", "dense"):
+        ctx = device_ctx(dwhmc, p, dis, algo)
+        assert ctx.info["block"] == (128 if algo == "cr" else 64)
+        ctx.set_pairing(Delta)
+        ctx.factorize()
+        res[algo] = (ctx.forces()[0], ctx.fermion_energy()[0], ctx.pairing()[0], ctx.hole_trace()[0])
+        ctx.close()
+    Fc, Ec, Pc, Tc = res["cr"]
+    Fd, Ed, Pd, Td = res["dense"]
+    assert np.max(np.abs(Fc - Fd)) <= 1e-10 * (1 + np.max(np.abs(Fd)))
+    assert np.max(np.abs(Pc - Pd)) <= 1e-11
+    assert abs(Ec - Ed) <= 1e-11 * abs(Ed)
+    assert abs(Tc - Td) <= 1e-11 * p.N
+
+
+def test_c1_workload_matches_oracle(dwhmc, oracle, algo):
+    """BASELINE configs[0] (C1): L = 8, β = 4, W = 1, n_imp = 0.05, 10
+    trajectories of Nt = 10 from initialize_state's Δ₀ — the workload of the
+    (stale) scripts/test_hmc.jl:26-29 — device vs oracle sweep by sweep with
+    the same injected draws (dt = calc_optimal_dt(β, J, m, 10))."""
+    O = oracle
+    p = O.ModelParameters(8, 8, T, TP, MU, 1.0, 0.05, 4.0, J, 1.0)
+    st = O.initialize_state(p, np.random.default_rng(1000))
+    ctx = device_ctx(dwhmc, p, st.disorder_pot, algo)
+    ctx.set_pairing(st.Delta)
+    ctx.factorize()
+    cache = O.initialize_cache(p)
+    O.init_static_H(cache, p, st.disorder_pot)
+    O.update_H_BdG(cache, p, st.Delta)
+    O.diagonalize_H_BdG(cache, p)
+    ref = O.SimulationState(st.disorder_pot, st.Delta.copy(), np.zeros_like(st.Delta))
+    dt = O.calc_optimal_dt(p.beta, p.J, p.mass, 10)
+    rng = np.random.default_rng(11)
+    for s in range(10):
+        noise = (rng.standard_normal((p.N, 2)) + 1j * rng.standard_normal((p.N, 2))) * math.sqrt(0.5)
+        u = rng.random()
+        acc, dH = ctx.hmc_sweep(noise, np.array([u]), 10, dt, p.mass)
+        acc_r, dH_r = O.hmc_sweep(cache, p, ref, 10, dt, noise, u)
+        assert acc[0] == acc_r and abs(dH[0] - dH_r) <= 1e-8 * (1 + abs(dH_r)), (s, dH[0], dH_r)
+    D, _ = ctx.get_state()
+    assert np.max(np.abs(D[0] - ref.Delta)) <= 1e-10
+    ctx.close()
