@@ -37,7 +37,7 @@ def table_to_abi(table: np.ndarray) -> np.ndarray:
 
 
 # factorisation algorithm (include/dwhmc.h DWH_ALGO_*): "auto" = env DWHMC_ALGO,
-# else block cyclic reduction when 2 Lx <= 96
+# else block cyclic reduction when 2 Lx <= 128
 ALGOS = {"auto": -1, "dense": 0, "cr": 1}
 
 

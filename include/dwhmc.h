@@ -56,13 +56,16 @@ typedef struct {
 
 /* ModelParameters + initialize_cache + init_static_H!
  * [src/Types.jl:49-91, src/Types.jl:182-212, src/Hamiltonian.jl:10-47].
- * One chain, delta_cap = 2.0.  disorder: length N (state.disorder_pot). */
+ * One chain, default delta_cap (max(2, 6 sqrt(2J/β))).  disorder: length N
+ * (state.disorder_pot). */
 int dwh_create(dwh_ctx** ctx, int64_t Lx, int64_t Ly, double t, double tp, double mu,
                double beta, double J, const int64_t* nn_table, const int64_t* nnn_table,
                const double* disorder, int32_t device);
 
 /* Batched form: nchains independent Markov chains / disorder realisations on one
- * device (disorder: nchains*N).  delta_cap <= 0 selects the default 2.0. */
+ * device (disorder: nchains*N).  delta_cap <= 0 selects the default
+ * max(2, 6 sqrt(2J/β)); the pole set covers |Δ_ij| <= delta_cap and is
+ * re-selected for a larger cap when an uploaded Δ or a trajectory exceeds it. */
 int dwh_create_batched(dwh_ctx** ctx, int64_t Lx, int64_t Ly, double t, double tp, double mu,
                        double beta, double J, const int64_t* nn_table, const int64_t* nnn_table,
                        int64_t nchains, const double* disorder, double delta_cap, int32_t device);
@@ -71,7 +74,7 @@ int dwh_create_batched(dwh_ctx** ctx, int64_t Lx, int64_t Ly, double t, double t
  *   DWH_ALGO_DENSE  Schur complement over the static particle block + blocked
  *                   Gauss-Jordan of the dense N x N complement per pole;
  *   DWH_ALGO_CR     block cyclic reduction of the block-tridiagonal (lattice-row
- *                   blocks, periodic) BdG matrix per pole; needs 2 Lx <= 96;
+ *                   blocks, periodic) BdG matrix per pole; needs 2 Lx <= 128;
  *   DWH_ALGO_AUTO   DWHMC_ALGO from the environment (dense | cr | auto), else CR
  *                   when supported.  Both give the same results to fp64 rounding. */
 enum { DWH_ALGO_AUTO = -1, DWH_ALGO_DENSE = 0, DWH_ALGO_CR = 1 };

@@ -9,4 +9,4 @@ mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_VMEM_RD TCC_HIT_sum TCC_MISS_sum \
   --output-format csv -d "$O/sq2" -o run -- \
-  python3 "$R/bench.py" --steps 10 --warmup 10 --no-cpu-baseline --no-timing > "$O/sq2.log" 2>&1
+  python3 "$R/bench.py" --steps 10 --warmup 10 --therm 0 --no-c1 --no-cpu-baseline --no-timing > "$O/sq2.log" 2>&1
