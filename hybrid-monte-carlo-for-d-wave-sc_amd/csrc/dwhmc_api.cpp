@@ -121,7 +121,13 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol) {
   std::vector<dwh::CrTask> cur_tasks;
   // output window of the next tasks (full block unless restricted)
   int w_r0 = 0, w_r1 = HP, w_c0 = 0, w_c1 = BP;
+  // per task of cur_tasks: compute only the A-part diagonal tiles and the
+  // B part (level-0 G_ee: the force reads its pairing (B) entries, E_f and
+  // Tr rho_hh its diagonal; nothing reads the rest)
+  std::vector<char> cur_adiag;
+  bool adiag_next = false;
   auto task = [&](int out, int cin, std::initializer_list<Term> terms) {
+    cur_adiag.push_back(adiag_next ? 1 : 0);
     dwh::CrTask t{};
     t.out = out;
     t.cin = cin;
@@ -143,10 +149,17 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol) {
     if (cur_tasks.empty()) return;
     CrStage st{1, (int)pl.tasks.size(), (int)cur_tasks.size(), sg, 0.0, 0, 0, 0,
                (int)pl.tiles16.size(), 0, {16, 1}};
-    for (auto& t : cur_tasks) {
-      for (int k = 0; k < dwh::cr_task_tiles(t, 16); ++k)
+    for (size_t ti = 0; ti < cur_tasks.size(); ++ti) {
+      const dwh::CrTask& t = cur_tasks[ti];
+      const int nk = dwh::cr_task_tiles(t, 16), ct = (t.c1 + 15) / 16 - t.c0 / 16;
+      int kept = 0;
+      for (int k = 0; k < nk; ++k) {
+        const int tr = t.r0 / 16 + k / ct, tc = t.c0 / 16 + k % ct;
+        if (cur_adiag[ti] && tc < HP / 16 && tc != tr) continue;
         pl.tiles16.push_back(make_int2((int)pl.tasks.size() - st.first, k));
-      st.flops += 8.0 * t.nt * BP * (double)(t.r1 - t.r0) * (t.c1 - t.c0);
+        kept++;
+      }
+      st.flops += 8.0 * t.nt * BP * (double)(t.r1 - t.r0) * (t.c1 - t.c0) * kept / nk;
       st.maxt32 = std::max(st.maxt32, dwh::cr_task_tiles(t, 32));
       st.maxt16 = std::max(st.maxt16, dwh::cr_task_tiles(t, 16));
       st.ntmax = std::max(st.ntmax, t.nt);
@@ -155,6 +168,7 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol) {
     st.ntiles = (int)pl.tiles16.size() - st.tfirst;
     pl.stages.push_back(st);
     cur_tasks.clear();
+    cur_adiag.clear();
   };
 
   Level cur;
@@ -278,10 +292,12 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol) {
       Gce[e] = gce;
     }
     flush(1.0);
+    adiag_next = sel;
     for (int e : lv.E) {
       task(lv.Dinv[e], lv.Dinv[e], {{lv.W1[e], Gae[e]}, {lv.W2[e], Gce[e]}});
       gd[e] = lv.Dinv[e];
     }
+    adiag_next = false;
     flush(1.0);
     GD = gd;
     GU = gu;

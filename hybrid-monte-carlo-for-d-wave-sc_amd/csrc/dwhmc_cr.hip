@@ -399,6 +399,16 @@ __global__ __launch_bounds__(64 * NT) void k_cr_inv(double2* __restrict__ pool, 
 // 1D grid with the XCD-aware remap so one item's tasks share an XCD's L2.
 // out never aliases an operand (planner invariant); out == cin is allowed.
 // ---------------------------------------------------------------------------
+// A/B knobs of variant builds (tools/ab_bench.py LIB=...): minimum waves per
+// SIMD the 16 x 16 tile kernels are compiled for, and their operand prefetch
+// depth in k-steps
+#ifndef DWHMC_GEMM_WAVES
+#define DWHMC_GEMM_WAVES 2
+#endif
+#ifndef DWHMC_GEMM_PF
+#define DWHMC_GEMM_PF 4
+#endif
+
 __device__ __forceinline__ double flip_sign(double x, unsigned m) {
   const unsigned long long b = __builtin_bit_cast(unsigned long long, x);
   return __builtin_bit_cast(double, b ^ ((unsigned long long)m << 32));
@@ -416,7 +426,7 @@ template <int BP, int MI, int KSPLIT, int KQ>
 __device__ __forceinline__ void cr_term(const double2* A, const double2* Bt, int c0, int crot, unsigned smask,
                                         d4 (&t1)[MI][MI], d4 (&t2)[MI][MI], d4 (&t3)[MI][MI]) {
   constexpr int HP = BP / 2, KS = BP / 4, KH = HP / 4, KSS = KS / KSPLIT, S0 = KQ * KSS;
-  constexpr int PF = KSS < (MI == 1 ? 4 : 2) ? KSS : (MI == 1 ? 4 : 2);
+  constexpr int PF = KSS < (MI == 1 ? DWHMC_GEMM_PF : 2) ? KSS : (MI == 1 ? DWHMC_GEMM_PF : 2);
   auto load = [&](int s, double2 (&a)[MI], double2 (&b)[MI]) {
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi) a[mi] = A[(int64_t)16 * mi * BP + s * 4];
@@ -482,7 +492,7 @@ __device__ __forceinline__ void cr_tile_part(const double2* base, const CrTask* 
 }
 
 template <int BP, int MI, int KSPLIT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_cr_gemm(double2* __restrict__ pool, int64_t item,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MI == 1 ? DWHMC_GEMM_WAVES : 2))) void k_cr_gemm(double2* __restrict__ pool, int64_t item,
                                                  const CrTask* __restrict__ tasks, int ntasks,
                                                  int maxt, const int2* __restrict__ tlist, int ntl,
                                                  int total, double sg) {

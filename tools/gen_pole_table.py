@@ -238,6 +238,10 @@ def entry(j):
     kappa = 2.0 ** (j / 4.0)
     t, mu = matsubara_measure(kappa)
     m = max(2, int(math.floor(2.0 + 2.35 * math.log(kappa + 1.0))))
+    if kappa > COMPRESS_ABOVE:
+        # the table's own trend (m ~ 3.6 ln κ - 1.5 from κ = 512 .. 2048), one
+        # below it: the search below moves up or down one pole at a time
+        m = max(m, int(round(3.6 * math.log(kappa) - 2.5)))
     tried = {}
     while True:
         sup, (tq, a) = optimise(kappa, m, t, mu)
