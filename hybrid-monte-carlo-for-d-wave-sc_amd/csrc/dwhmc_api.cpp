@@ -60,7 +60,7 @@ struct CrPlan {
   int nblk = 0;
   std::vector<CrStage> stages;
   std::vector<dwh::CrTask> tasks;
-  std::vector<int2> tiles16;                 // per product stage: (task offset, 16 x 16 tile)
+  std::vector<dwh::CrTile> tiles16;          // per product stage: its 16 x 16 tiles with their operands
   std::vector<int> inv_blk, inv_dst, inv_slot;   // inversion source / destination block, ln|det| slot
   std::vector<int64_t> goff, doff;
   std::vector<int> fill_all, fill_step;      // level-0 blocks written at create / every step
@@ -156,7 +156,18 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol) {
       for (int k = 0; k < nk; ++k) {
         const int tr = t.r0 / 16 + k / ct, tc = t.c0 / 16 + k % ct;
         if (cur_adiag[ti] && tc < HP / 16 && tc != tr) continue;
-        pl.tiles16.push_back(make_int2((int)pl.tasks.size() - st.first, k));
+        dwh::CrTile d{};
+        d.out = t.out;
+        d.cin = t.cin;
+        d.nt = t.nt;
+        d.bq = t.bq;
+        for (int h = 0; h < 4; ++h) {
+          d.a[h] = t.a[h];
+          d.b[h] = t.b[h];
+        }
+        d.tr = tr;
+        d.tc = tc;
+        pl.tiles16.push_back(d);
         kept++;
       }
       st.flops += 8.0 * t.nt * BP * (double)(t.r1 - t.r0) * (t.c1 - t.c0) * kept / nk;
@@ -413,7 +424,7 @@ struct dwh_ctx {
   CrPlan plan;
   double2* bpool = nullptr;   // CR block pool (nbatch x nblk blocks)
   dwh::CrTask* d_tasks = nullptr;
-  int2* d_tiles16 = nullptr;
+  dwh::CrTile* d_tiles16 = nullptr;
   double* efpart = nullptr;     // per (chain, pole) E_f / Tr G22 partials
   unsigned* efdone = nullptr;   // per chain: pole blocks done (k_cr_fermion_energy)
   int *d_inv_blk = nullptr, *d_inv_dst = nullptr, *d_inv_slot = nullptr;
@@ -1071,8 +1082,8 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
           if (st.kind == 0)
             std::fprintf(stderr, "cr stage %2d: inv   blocks=%d\n", i, st.n);
           else
-            std::fprintf(stderr, "cr stage %2d: gemm  tasks=%d maxt32=%d maxt16=%d ntmax=%d flops/item=%.3g cfg=%d:%d\n",
-                         i, st.n, st.maxt32, st.maxt16, st.ntmax, st.flops, st.cfg.ts, st.cfg.ksplit);
+            std::fprintf(stderr, "cr stage %2d: gemm  tasks=%d maxt32=%d maxt16=%d ntmax=%d flops/item=%.3g cfg=%d:%d ntiles=%d\n",
+                         i, st.n, st.maxt32, st.maxt16, st.ntmax, st.flops, st.cfg.ts, st.cfg.ksplit, st.ntiles);
           ++i;
         }
       }

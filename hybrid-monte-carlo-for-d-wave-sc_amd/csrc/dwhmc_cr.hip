@@ -52,6 +52,28 @@ __device__ unsigned long long g_cr_stamps[1024][16];
   } while (0)
 #endif
 
+// Diagnostic build only (-DCR_GEMM_STAMPS, tools/gemm_stamps.py): per-workgroup
+// phase stamps of the k_cr_gemm launch whose total tile count equals
+// g_gemm_sel (wave 0's view): [0] s_memrealtime at entry, [1..4] s_memtime at
+// entry / descriptor loaded / partials in LDS / after the reduction barrier,
+// [5] s_memtime at the end, [6] s_memrealtime at the end, [7] HW_ID.
+#ifdef CR_GEMM_STAMPS
+__device__ unsigned long long g_gemm_stamps[65536][8];
+__device__ int g_gemm_sel;
+#define GEMM_STAMP(i, sel)                                                             \
+  do {                                                                                 \
+    __builtin_amdgcn_sched_barrier(0);                                                 \
+    if ((sel) && threadIdx.x == 0 && blockIdx.x < 65536)                               \
+      g_gemm_stamps[blockIdx.x][i] = (i) == 0 || (i) == 6 ? __builtin_amdgcn_s_memrealtime() \
+                                                          : __builtin_amdgcn_s_memtime(); \
+    __builtin_amdgcn_sched_barrier(0);                                                 \
+  } while (0)
+#else
+#define GEMM_STAMP(i, sel) \
+  do {                     \
+  } while (0)
+#endif
+
 // ---------------------------------------------------------------------------
 // Level-0 blocks D[y] (pool block y), U[y] = A[y, y+1] (Ly + y), L[y] =
 // A[y+1, y] (2 Ly + y) of A = H_BdG - i y_q for every (chain, pole), top
@@ -472,20 +494,21 @@ __device__ __forceinline__ void cr_term(const double2* A, const double2* Bt, int
 
 // This wave's share of an output tile over all terms (the stage sign sg is
 // applied in the epilogue: negating every A fragment negates the sums exactly).
-template <int BP, int MI, int KSPLIT, int KQ>
-__device__ __forceinline__ void cr_tile_part(const double2* base, const CrTask* tk, int nt, int tr,
-                                             int tc, d4 (&t1)[MI][MI], d4 (&t2)[MI][MI],
-                                             d4 (&t3)[MI][MI]) {
+// D: CrTile or CrTask (operand fields read through the uniform pointer: scalar loads)
+template <int BP, int MI, int KSPLIT, int KQ, typename D>
+__device__ __forceinline__ void cr_tile_part(const double2* base, const D* __restrict__ tk, int tr, int tc,
+                                             d4 (&t1)[MI][MI], d4 (&t2)[MI][MI], d4 (&t3)[MI][MI]) {
   constexpr int TS = 16 * MI, HP = BP / 2;
   constexpr int64_t BB = (int64_t)HP * BP;
   const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
   const int c0 = tc * TS, crot = c0 < HP ? c0 + HP : c0 - HP;
+  const int nt = tk->nt, bq = tk->bq;
 #pragma unroll 1
   for (int h = 0; h < nt; ++h) {
     const double2* A = base + tk->a[h] * BB + (int64_t)(tr * TS + lr) * BP + lk;
     const double2* Bt = base + tk->b[h] * BB + (int64_t)lk * BP + lr;
     // synthesised rows: sgn * conj(.), sgn = -s (left column half) / +s (right), s = +1 Q, -1 M
-    const bool q = (tk->bq >> h) & 1;
+    const bool q = (bq >> h) & 1;
     const unsigned smask = ((c0 < HP) == q) ? 0x80000000u : 0u;   // sgn < 0
     cr_term<BP, MI, KSPLIT, KQ>(A, Bt, c0, crot, smask, t1, t2, t3);
   }
@@ -494,34 +517,49 @@ __device__ __forceinline__ void cr_tile_part(const double2* base, const CrTask* 
 template <int BP, int MI, int KSPLIT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MI == 1 ? DWHMC_GEMM_WAVES : 2))) void k_cr_gemm(double2* __restrict__ pool, int64_t item,
                                                  const CrTask* __restrict__ tasks, int ntasks,
-                                                 int maxt, const int2* __restrict__ tlist, int ntl,
+                                                 int maxt, const CrTile* __restrict__ tlist, int ntl,
                                                  int total, double sg) {
   constexpr int TS = 16 * MI, TPW = 4 / KSPLIT, HP = BP / 2, NV = MI * MI * 4;
   constexpr int64_t BB = (int64_t)HP * BP;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
   const int kq = w % KSPLIT;
+#ifdef CR_GEMM_STAMPS
+  const bool stamp = (total == g_gemm_sel);
+  GEMM_STAMP(0, stamp);
+  GEMM_STAMP(1, stamp);
+  if (stamp && threadIdx.x == 0 && blockIdx.x < 65536)
+    g_gemm_stamps[blockIdx.x][7] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
+#endif
   const int gt = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x) * TPW + w / KSPLIT);
-  // 16 x 16 tiles: compact (task, tile) list of the stage (no idle waves for
-  // restricted tasks); 32 x 32 tiles: ntasks x maxt slots
-  const int per_item = tlist ? ntl : ntasks * maxt;
+  // 16 x 16 tiles: the stage's compact tile list, one 64-byte descriptor per
+  // tile (one scalar load, no idle waves for restricted tasks); 32 x 32
+  // tiles: ntasks x maxt slots of the task list
+  // launch_cr_gemm passes the tile list exactly for the 16 x 16 kernels
+  const int per_item = MI == 1 ? ntl : ntasks * maxt;
   const int bi = gt / per_item;
   const int rmd = gt - bi * per_item;
   bool valid = gt < total;
-  int tsk, tile;
-  if (tlist) {
-    const int2 e = tlist[valid ? rmd : 0];
-    tsk = e.x;
-    tile = e.y;
+  const CrTile* tp = nullptr;
+  const CrTask* tk = nullptr;
+  int tr, tc, cin, out;
+  if constexpr (MI == 1) {
+    tp = tlist + (valid ? rmd : 0);
+    tr = tp->tr;
+    tc = tp->tc;
+    cin = tp->cin;
+    out = tp->out;
   } else {
-    tsk = rmd / maxt;
-    tile = rmd - tsk * maxt;
+    const int tsk = rmd / maxt, tile = rmd - tsk * maxt;
+    tk = tasks + (valid ? tsk : 0);
+    const int tr0 = tk->r0 / TS, tc0 = tk->c0 / TS;
+    const int ct = (tk->c1 + TS - 1) / TS - tc0;
+    const int rt = (tk->r1 + TS - 1) / TS - tr0;
+    valid = valid && tile < rt * ct;   // restricted task: fewer tiles than the stage maximum
+    tr = tr0 + (valid ? tile / ct : 0);
+    tc = tc0 + (valid ? tile % ct : 0);
+    cin = tk->cin;
+    out = tk->out;
   }
-  const CrTask* tk = tasks + (valid ? tsk : 0);
-  const int tr0 = tk->r0 / TS, tc0 = tk->c0 / TS;
-  const int ct = (tk->c1 + TS - 1) / TS - tc0;
-  const int rt = (tk->r1 + TS - 1) / TS - tr0;
-  valid = valid && tile < rt * ct;   // restricted task: fewer tiles than the stage maximum
-  const int tr = tr0 + (valid ? tile / ct : 0), tc = tc0 + (valid ? tile % ct : 0);
   double2* base = pool + (int64_t)(valid ? bi : 0) * item;
   d4 t1[MI][MI], t2[MI][MI], t3[MI][MI];
 #pragma unroll
@@ -532,8 +570,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MI == 1 ? D
       t2[mi][ni] = d4{0.0, 0.0, 0.0, 0.0};
       t3[mi][ni] = d4{0.0, 0.0, 0.0, 0.0};
     }
-  const int cin = tk->cin;
-  double2* O = base + tk->out * BB + (int64_t)(tr * TS + lk) * BP + tc * TS + lr;
+#ifdef CR_GEMM_STAMPS
+  if (stamp) __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  GEMM_STAMP(2, stamp);
+#endif
+  double2* O = base + out * BB + (int64_t)(tr * TS + lk) * BP + tc * TS + lr;
   const double2* C = cin >= 0 ? base + cin * BB + (int64_t)(tr * TS + lk) * BP + tc * TS + lr : nullptr;
   // register slot v of this wave's output share <-> offset in the block
   auto slot_off = [&](int v) -> int64_t {
@@ -550,15 +591,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MI == 1 ? D
     for (int i = 0; i < NPF; ++i) cpf[i] = C[slot_off(i * KSPLIT + kq)];
   }
 #endif
+  auto run = [&](auto kqc) {
+    constexpr int KQ = decltype(kqc)::value;
+    if constexpr (MI == 1) cr_tile_part<BP, MI, KSPLIT, KQ>(base, tp, tr, tc, t1, t2, t3);
+    else cr_tile_part<BP, MI, KSPLIT, KQ>(base, tk, tr, tc, t1, t2, t3);
+  };
   if (valid) {
-    const int nt = tk->nt;
-    if (KSPLIT == 1 || kq == 0) cr_tile_part<BP, MI, KSPLIT, 0>(base, tk, nt, tr, tc, t1, t2, t3);
+    if (KSPLIT == 1 || kq == 0) run(std::integral_constant<int, 0>{});
     if constexpr (KSPLIT >= 2) {
-      if (kq == 1) cr_tile_part<BP, MI, KSPLIT, 1>(base, tk, nt, tr, tc, t1, t2, t3);
+      if (kq == 1) run(std::integral_constant<int, 1>{});
     }
     if constexpr (KSPLIT == 4) {
-      if (kq == 2) cr_tile_part<BP, MI, KSPLIT, 2>(base, tk, nt, tr, tc, t1, t2, t3);
-      if (kq == 3) cr_tile_part<BP, MI, KSPLIT, 3>(base, tk, nt, tr, tc, t1, t2, t3);
+      if (kq == 2) run(std::integral_constant<int, 2>{});
+      if (kq == 3) run(std::integral_constant<int, 3>{});
     }
   }
   auto put = [&](int v, double2 x) {
@@ -588,7 +633,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MI == 1 ? D
     __shared__ double2 red[4][NV][64];
 #pragma unroll
     for (int v = 0; v < NV; ++v) red[w][v][l] = partial(v);
+#ifdef CR_GEMM_STAMPS
+    if (stamp) __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    GEMM_STAMP(3, stamp);
+#endif
     __syncthreads();
+#ifdef CR_GEMM_STAMPS
+    GEMM_STAMP(4, stamp);
+#endif
     if (!valid) return;
     const int g0 = w - kq;   // first wave of this tile's group
 #pragma unroll
@@ -603,6 +655,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MI == 1 ? D
       }
       put(v, x);
     }
+#ifdef CR_GEMM_STAMPS
+    if (stamp) __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    GEMM_STAMP(5, stamp);
+    GEMM_STAMP(6, stamp);
+#endif
   }
 }
 
@@ -775,11 +832,11 @@ CrGemmCfg cr_gemm_config(const CrDims& c, int ntasks, int maxt32, int maxt16, in
 }
 
 void launch_cr_gemm(const CrDims& c, double2* pool, const CrTask* tasks, int ntasks, int maxt32,
-                    int maxt16, const int2* tl16, int ntl16, const CrGemmCfg& cfg, double sg,
+                    int maxt16, const CrTile* tl16, int ntl16, const CrGemmCfg& cfg, double sg,
                     hipStream_t s) {
   if (ntasks <= 0) return;
   const int maxt = cfg.ts == 32 ? maxt32 : maxt16;
-  const int2* tl = cfg.ts == 32 ? nullptr : tl16;
+  const CrTile* tl = cfg.ts == 32 ? nullptr : tl16;
   const int total = c.nbatch * (tl ? ntl16 : ntasks * maxt);
   const int tpw = 4 / cfg.ksplit;
   const dim3 g((total + tpw - 1) / tpw), b(256);
@@ -824,3 +881,14 @@ void launch_cr_fermion_energy(const CrDims& c, const double2* pool, const int64_
 }
 
 }  // namespace dwh
+
+#ifdef CR_GEMM_STAMPS
+extern "C" int dwh_debug_gemm_stamps_select(int total) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(dwh::g_gemm_sel), &total, sizeof(int)) == hipSuccess ? 0 : -2;
+}
+extern "C" int dwh_debug_gemm_stamps_read(unsigned long long* out, int nblocks) {
+  if (nblocks > 65536) nblocks = 65536;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(dwh::g_gemm_stamps), (size_t)nblocks * 8 * sizeof(unsigned long long)) ==
+                 hipSuccess ? 0 : -2;
+}
+#endif

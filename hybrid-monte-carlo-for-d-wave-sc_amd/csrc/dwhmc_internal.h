@@ -45,6 +45,14 @@ struct CrTask {
   int a[4], b[4];
   int r0, r1, c0, c1;
 };
+// One 16 x 16 output tile of a product stage with its task's operands, so a
+// workgroup reads its whole descriptor with one 64-byte scalar load (tr, tc:
+// tile row / column in 16-tile units)
+struct alignas(64) CrTile {
+  int out, cin, nt, bq;
+  int a[4], b[4];
+  int tr, tc, pad0, pad1;
+};
 // wave tiles of a task at tile size ts
 inline int cr_task_tiles(const CrTask& t, int ts) {
   return ((t.r1 + ts - 1) / ts - t.r0 / ts) * ((t.c1 + ts - 1) / ts - t.c0 / ts);
@@ -82,7 +90,7 @@ struct CrGemmCfg {
 CrGemmCfg cr_gemm_config(const CrDims& c, int ntasks, int maxt32, int maxt16, int ntmax);
 // tl16: the stage's (task, tile) list at 16 x 16 tiles (ntl16 entries per batch item)
 void launch_cr_gemm(const CrDims& c, double2* pool, const CrTask* tasks, int ntasks, int maxt32,
-                    int maxt16, const int2* tl16, int ntl16, const CrGemmCfg& cfg, double sg,
+                    int maxt16, const CrTile* tl16, int ntl16, const CrGemmCfg& cfg, double sg,
                     hipStream_t s);
 
 // dense h - i y_q (padded with identity) for every (chain, pole): R init input
