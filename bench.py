@@ -29,6 +29,7 @@ Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3]
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import math
 import os
@@ -301,14 +302,18 @@ def main(argv=None):
         ctx.run_sweeps(f, n, nt, dt, p.mass)
     ctx.synchronize()
 
+    gc.collect()
+    gc.disable()                                    # no collector pause inside the ~7 ms timed region
     if dist is not None:
         dist.barrier()
     ctx.synchronize()
     t0 = time.perf_counter()
     for f, n, nt in timed:
         ctx.run_sweeps(f, n, nt, dt, p.mass)
+    t_enq = time.perf_counter() - t0           # host enqueue time of the timed launches
     ctx.synchronize()
     el = time.perf_counter() - t0
+    gc.enable()
     if dist is not None:
         import torch
         t = torch.tensor([el], dtype=torch.float64, device=f"cuda:{local}")
@@ -372,6 +377,7 @@ def main(argv=None):
                        "Nt": Nt, "dt": dt, "therm_sweeps": a.therm, "poles": P, "kappa": info["kappa"],
                        "parallelism": f"replicas x{world}" if world > 1 else "single GPU"},
             "timed_trajectories": [{"sweeps": n, "Nt": nt} for _, n, nt in timed],
+            "host_enqueue_ms": 1000.0 * t_enq,
             "warmup_sweeps": w_sw,
             "thermalisation": {"sweeps": a.therm, "Nt_init": a.Nt, "Nt_final": Nt,
                                "acceptance_last20": acc_therm, "seconds": t_th},
