@@ -255,7 +255,8 @@ class FermionContext:
         return Mcm.T.copy(), y
 
     # -- timing ----------------------------------------------------------
-    TIMERS = ("gj_update", "gj_pivot", "assemble", "contract", "step", "gj_edge", "cr_gemm", "cr_inv")
+    TIMERS = ("gj_update", "gj_pivot", "assemble", "contract", "step", "gj_edge", "cr_gemm", "cr_inv",
+              "cr_inv_side")
 
     def timing_enable(self, on=True):
         """on: True (all timers), False, or an iterable of timer names."""

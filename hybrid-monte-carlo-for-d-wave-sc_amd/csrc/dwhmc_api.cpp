@@ -37,10 +37,12 @@ namespace {
 thread_local std::string g_create_error;
 
 enum TimerName {
-  T_GJ_UPDATE = 0, T_GJ_PIVOT, T_ASSEMBLE, T_CONTRACT, T_STEP, T_GJ_EDGE, T_CR_GEMM, T_CR_INV, T_COUNT
+  T_GJ_UPDATE = 0, T_GJ_PIVOT, T_ASSEMBLE, T_CONTRACT, T_STEP, T_GJ_EDGE, T_CR_GEMM, T_CR_INV, T_CR_INVSIDE,
+  T_COUNT
 };
 const char* kTimerNames[T_COUNT] = {"gj_update", "gj_pivot", "assemble", "contract",
-                                    "step",      "gj_edge",  "cr_gemm",  "cr_inv"};
+                                    "step",      "gj_edge",  "cr_gemm",  "cr_inv",
+                                    "cr_inv_side"};
 
 enum Algo { ALGO_DENSE = 0, ALGO_CR = 1 };
 
@@ -52,7 +54,9 @@ struct CrStage {
   double sg;       // products: sign of the sum
   double flops;    // products: algorithmic fp64 flops per batch item (restricted ranges)
   int maxt32, maxt16, ntmax;
-  int tfirst, ntiles;   // products: range in CrPlan::tiles16 (the stage's (task, tile) pairs)
+  int tfirst, ntiles;   // products: range in CrPlan::tiles16 (the stage's (task, tile) pairs);
+                        // inversions: their side-work tasks in CrPlan::tasks (launch_cr_inv_side,
+                        // maxt32 tiles each), flops in `flops`
   dwh::CrGemmCfg cfg;   // products: tile / K-split chosen once per context
 };
 
@@ -81,7 +85,28 @@ struct CrPlan {
 // Backward (G of the next level known at its kept blocks and adjacent pairs):
 //   G_ea = W1 G_aa + W2 G_ca,  G_ec = W1 G_ac + W2 G_cc,
 //   G_ae = G_aa V1 + G_ac V2,  G_ce = G_ca V1 + G_cc V2,  G_ee = D_e^-1 + W1 G_ae + W2 G_ce.
-CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol) {
+//
+// side: products off the critical path (W1/W2: operands of the backward pass
+// only; U'/L': operands of the next level's products, which follow its
+// inversion) leave the product stages and run as side work of a later
+// inversion stage, on the CUs its few inversion workgroups leave idle; the
+// product stages on the critical path keep only V1/V2 and D'.  Levels down
+// to m = 4 (below that the stages are pure latency) and only where the
+// receiving inversion stage leaves a quarter of the ncu CUs idle (nbatch =
+// chains x poles inversion workgroups per block).
+// DWHMC_CR_SIDE_W (default 2): inversion stages between a level and the one
+// that runs its W products; DWHMC_CR_SIDE_M (default 4): smallest level size
+// m whose products move (A/B knobs; profiles/r02_exp_cr_side_work.txt).
+CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol, bool side, int nbatch,
+                     int ncu) {
+  const int side_woff = [] {
+    const char* e = std::getenv("DWHMC_CR_SIDE_W");
+    return e ? std::max(1, std::atoi(e)) : 2;
+  }();
+  const int side_m = [] {
+    const char* e = std::getenv("DWHMC_CR_SIDE_M");
+    return e ? std::max(2, std::atoi(e)) : 4;
+  }();
   CrPlan pl;
   const int HP = BP / 2;
   int nblk = 3 * Ly;
@@ -104,8 +129,26 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol) {
   // Level-0 blocks are inverted out of place (they are never overwritten, so
   // per step only their pairing entries change), coarser blocks in place.
   // Returns the blocks that hold the inverses.
+  // pending side work per inversion stage (ordinal: 0 = level 0, ..., the
+  // last = the final single-block inversion)
+  int n_inv = 1;
+  std::vector<int> inv_wgs;   // inversion workgroups of each inversion stage
+  for (int m = Ly; m > 1; m = (m + 1) / 2) {
+    ++n_inv;
+    inv_wgs.push_back(nbatch * (m / 2));
+  }
+  inv_wgs.push_back(nbatch);
+  auto idle_ok = [&](int ord) { return 4 * inv_wgs[ord] <= 3 * ncu; };
+  std::vector<std::vector<dwh::CrTask>> side_tasks(n_inv);
+  std::vector<double> side_flops(n_inv, 0.0);
+  int inv_ord = 0;
   auto add_inv = [&](const std::vector<int>& blocks, int& slot) {
-    CrStage st{0, (int)pl.inv_blk.size(), (int)blocks.size(), 0.0, 0.0, 0, 0, 0, 0, 0, {16, 1}};
+    std::vector<dwh::CrTask>& stk = side_tasks[inv_ord];
+    CrStage st{0, (int)pl.inv_blk.size(), (int)blocks.size(), side_flops[inv_ord], 0.0, 0, 0, 0,
+               (int)pl.tasks.size(), (int)stk.size(), {32, 1}};
+    for (const dwh::CrTask& t : stk) st.maxt32 = std::max(st.maxt32, dwh::cr_task_tiles(t, 32));
+    pl.tasks.insert(pl.tasks.end(), stk.begin(), stk.end());
+    ++inv_ord;
     std::vector<int> dst;
     for (int b : blocks) {
       const int d = b < 3 * Ly ? nb() : b;
@@ -145,8 +188,20 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol) {
     }
     cur_tasks.push_back(t);
   };
-  auto flush = [&](double sg) {
+  // to_side: the tasks become side work of inversion stage `ord` (tiles
+  // with their own sign) instead of a product stage
+  auto flush = [&](double sg, bool to_side = false, int ord = 0) {
     if (cur_tasks.empty()) return;
+    if (to_side) {
+      for (dwh::CrTask t : cur_tasks) {
+        if (sg < 0) t.bq |= dwh::kCrNegBit;
+        side_tasks[ord].push_back(t);
+        side_flops[ord] += 8.0 * t.nt * BP * (double)(t.r1 - t.r0) * (t.c1 - t.c0);
+      }
+      cur_tasks.clear();
+      cur_adiag.clear();
+      return;
+    }
     CrStage st{1, (int)pl.tasks.size(), (int)cur_tasks.size(), sg, 0.0, 0, 0, 0,
                (int)pl.tiles16.size(), 0, {16, 1}};
     for (size_t ti = 0; ti < cur_tasks.size(); ++ti) {
@@ -193,6 +248,10 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol) {
   int slot = 0;
   while (cur.m > 1) {
     const int m = cur.m;
+    // inv_ord: this level's inversion stage (added below)
+    const bool side_ul = side && m >= side_m && idle_ok(inv_ord + 1);
+    const int w_ord = std::min(n_inv - 1, inv_ord + side_woff);
+    const bool side_w = side && m >= side_m && idle_ok(w_ord);
     cur.elim.assign(m, 0);
     cur.E.clear();
     cur.K.clear();
@@ -216,14 +275,22 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol) {
       task(cur.V1[e], -1, {{cur.U[a], cur.Dinv[e]}});
       cur.V2[e] = nbq();
       task(cur.V2[e], -1, {{cur.L[e], cur.Dinv[e]}});
+    }
+    if (side_w) flush(-1.0);
+    for (int e : cur.E) {
+      const int a = e - 1;
       cur.W1[e] = nbq();
       task(cur.W1[e], -1, {{cur.Dinv[e], cur.L[a]}});
       cur.W2[e] = nbq();
       task(cur.W2[e], -1, {{cur.Dinv[e], cur.U[e]}});
     }
-    flush(-1.0);
+    // W_l: first needed by the backward pass; placed three inversion stages
+    // later (the coarse inversions leave ~240 of 256 CUs idle), the U'/L'
+    // products of this level take the next one
+    flush(-1.0, side_w, w_ord);
     Level nxt;
     nxt.m = (int)cur.K.size();
+    std::vector<dwh::CrTask> ul_tasks;   // U'/L' (side work when `side`)
     for (int k : cur.K) {
       if (m == 2) {
         const int e = 1, Dn = nb();
@@ -248,6 +315,12 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol) {
         const int Un = nb(), Ln = nb();
         task(Un, -1, {{cur.V1[er], cur.U[er]}});
         task(Ln, -1, {{cur.V2[er], cur.L[k]}});
+        if (side_ul) {   // move them behind the D' tasks of this stage
+          ul_tasks.push_back(cur_tasks[cur_tasks.size() - 2]);
+          ul_tasks.push_back(cur_tasks.back());
+          cur_tasks.resize(cur_tasks.size() - 2);
+          cur_adiag.resize(cur_adiag.size() - 2);
+        }
         nxt.U.push_back(Un);
         nxt.L.push_back(Ln);
       } else {   // odd m: the kept pair (m-1, 0) keeps its direct coupling
@@ -256,6 +329,11 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol) {
       }
     }
     flush(1.0);
+    if (!ul_tasks.empty()) {
+      cur_tasks = ul_tasks;
+      cur_adiag.assign(ul_tasks.size(), 0);
+      flush(1.0, true, inv_ord);
+    }
     levels.push_back(cur);
     cur = nxt;
   }
@@ -627,7 +705,12 @@ void cr_enqueue(dwh_ctx* ctx) {
     ctx->pairing_in_pool = false;
   }
   for (const CrStage& st : ctx->plan.stages) {
-    if (st.kind == 0) {
+    if (st.kind == 0 && st.ntiles > 0) {
+      Scope s(ctx, T_CR_INVSIDE, st.n * bp3 + st.flops * c.nbatch);
+      dwh::launch_cr_inv_side(c, ctx->bpool, ctx->d_inv_blk + st.first, ctx->d_inv_dst + st.first,
+                              ctx->d_inv_slot + st.first, st.n, ctx->ldpart, ctx->d_tasks + st.tfirst,
+                              st.ntiles, st.maxt32, ctx->stream);
+    } else if (st.kind == 0) {
       Scope s(ctx, T_CR_INV, st.n * bp3);
       dwh::launch_cr_inv(c, ctx->bpool, ctx->d_inv_blk + st.first, ctx->d_inv_dst + st.first,
                          ctx->d_inv_slot + st.first, st.n, ctx->ldpart, ctx->stream);
@@ -1063,7 +1146,13 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     }
     ctx->algo = (want == "dense" || !ok) ? ALGO_DENSE : ALGO_CR;
     if (ctx->algo == ALGO_CR) {
-      ctx->plan = build_cr_plan((int)Lx, (int)Ly, BP, Dcol);
+      // DWHMC_CR_SIDE=0: every product on its own stage (A/B runs, tests)
+      const char* es = std::getenv("DWHMC_CR_SIDE");
+      const bool side = dwh::cr_supported_side(BP) && !(es && *es == '0');
+      int ncu = 256;
+      if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu <= 0)
+        ncu = 256;
+      ctx->plan = build_cr_plan((int)Lx, (int)Ly, BP, Dcol, side, d.nbatch, ncu);
       dwh::CrDims& c = ctx->cr;
       c.Lx = (int)Lx;
       c.Ly = (int)Ly;
@@ -1080,7 +1169,8 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
         int i = 0;
         for (const CrStage& st : ctx->plan.stages) {
           if (st.kind == 0)
-            std::fprintf(stderr, "cr stage %2d: inv   blocks=%d\n", i, st.n);
+            std::fprintf(stderr, "cr stage %2d: inv   blocks=%d side_tiles=%d side_flops/item=%.3g\n", i, st.n,
+                         st.ntiles, st.flops);
           else
             std::fprintf(stderr, "cr stage %2d: gemm  tasks=%d maxt32=%d maxt16=%d ntmax=%d flops/item=%.3g cfg=%d:%d ntiles=%d\n",
                          i, st.n, st.maxt32, st.maxt16, st.ntmax, st.flops, st.cfg.ts, st.cfg.ksplit, st.ntiles);

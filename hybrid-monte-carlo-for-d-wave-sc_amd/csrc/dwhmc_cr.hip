@@ -224,16 +224,14 @@ __device__ __forceinline__ void mma16_3m_T(d4& cr, d4& ci, const double2* A, con
   ci = t3 - t1 - t2;
 }
 
+// one workgroup (NT waves) inverts block blk[li] of batch item bi; pan / ldw:
+// the caller's LDS (double-buffered panel, per-wave ln|det| partials)
 template <int NT>
-__global__ __launch_bounds__(64 * NT) void k_cr_inv(double2* __restrict__ pool, int64_t item,
-                                                    const int* __restrict__ blk,
-                                                    const int* __restrict__ dst,
-                                                    const int* __restrict__ slot,
-                                                    double* __restrict__ ldpart, int nslots) {
+__device__ __forceinline__ void cr_inv_wg(double2* __restrict__ pool, int64_t item, int bi, int li,
+                                          const int* __restrict__ blk, const int* __restrict__ dst,
+                                          const int* __restrict__ slot, double* __restrict__ ldpart,
+                                          int nslots, double2 (*pan)[NT][16 * 17], double* ldw) {
   constexpr int BP = 16 * NT, HP = BP / 2, TSZ = 16 * 17;
-  __shared__ double2 pan[2][NT][TSZ];
-  __shared__ double ldw[NT];
-  const int bi = blockIdx.y, li = blockIdx.x;
   const double2* M = pool + (int64_t)bi * item + (int64_t)blk[li] * HP * BP;
   double2* Mo = pool + (int64_t)bi * item + (int64_t)dst[li] * HP * BP;   // may equal M
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
@@ -404,6 +402,17 @@ __global__ __launch_bounds__(64 * NT) void k_cr_inv(double2* __restrict__ pool, 
   CR_STAMP(5);
 }
 
+template <int NT>
+__global__ __launch_bounds__(64 * NT) void k_cr_inv(double2* __restrict__ pool, int64_t item,
+                                                    const int* __restrict__ blk,
+                                                    const int* __restrict__ dst,
+                                                    const int* __restrict__ slot,
+                                                    double* __restrict__ ldpart, int nslots) {
+  __shared__ double2 pan[2][NT][16 * 17];
+  __shared__ double ldw[NT];
+  cr_inv_wg<NT>(pool, item, blockIdx.y, blockIdx.x, blk, dst, slot, ldpart, nslots, pan, ldw);
+}
+
 // ---------------------------------------------------------------------------
 // Batched block products on top halves: task t of batch item bi writes
 //   out = [cin] + sg Σ_{h < nt} A_h B_h      (top halves, HP x BP)
@@ -444,11 +453,12 @@ __device__ __forceinline__ double flip_sign(double x, unsigned m) {
 // it (tools/micro/mfma_valu_coexec.hip: ~10-15 cycles per interleaved
 // v_mul/v_add_f64).  The products are the ones the explicit sign multiplies
 // gave, bit for bit.
-template <int BP, int MI, int KSPLIT, int KQ>
+template <int BP, int MI, int KSPLIT, int KQ, int PFX = 0>
 __device__ __forceinline__ void cr_term(const double2* A, const double2* Bt, int c0, int crot, unsigned smask,
                                         d4 (&t1)[MI][MI], d4 (&t2)[MI][MI], d4 (&t3)[MI][MI]) {
   constexpr int HP = BP / 2, KS = BP / 4, KH = HP / 4, KSS = KS / KSPLIT, S0 = KQ * KSS;
-  constexpr int PF = KSS < (MI == 1 ? DWHMC_GEMM_PF : 2) ? KSS : (MI == 1 ? DWHMC_GEMM_PF : 2);
+  constexpr int PFD = PFX > 0 ? PFX : (MI == 1 ? DWHMC_GEMM_PF : 2);
+  constexpr int PF = KSS < PFD ? KSS : PFD;
   auto load = [&](int s, double2 (&a)[MI], double2 (&b)[MI]) {
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi) a[mi] = A[(int64_t)16 * mi * BP + s * 4];
@@ -495,7 +505,7 @@ __device__ __forceinline__ void cr_term(const double2* A, const double2* Bt, int
 // This wave's share of an output tile over all terms (the stage sign sg is
 // applied in the epilogue: negating every A fragment negates the sums exactly).
 // D: CrTile or CrTask (operand fields read through the uniform pointer: scalar loads)
-template <int BP, int MI, int KSPLIT, int KQ, typename D>
+template <int BP, int MI, int KSPLIT, int KQ, int PFX = 0, typename D>
 __device__ __forceinline__ void cr_tile_part(const double2* base, const D* __restrict__ tk, int tr, int tc,
                                              d4 (&t1)[MI][MI], d4 (&t2)[MI][MI], d4 (&t3)[MI][MI]) {
   constexpr int TS = 16 * MI, HP = BP / 2;
@@ -510,15 +520,20 @@ __device__ __forceinline__ void cr_tile_part(const double2* base, const D* __res
     // synthesised rows: sgn * conj(.), sgn = -s (left column half) / +s (right), s = +1 Q, -1 M
     const bool q = (bq >> h) & 1;
     const unsigned smask = ((c0 < HP) == q) ? 0x80000000u : 0u;   // sgn < 0
-    cr_term<BP, MI, KSPLIT, KQ>(A, Bt, c0, crot, smask, t1, t2, t3);
+    cr_term<BP, MI, KSPLIT, KQ, PFX>(A, Bt, c0, crot, smask, t1, t2, t3);
   }
 }
 
-template <int BP, int MI, int KSPLIT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MI == 1 ? DWHMC_GEMM_WAVES : 2))) void k_cr_gemm(double2* __restrict__ pool, int64_t item,
-                                                 const CrTask* __restrict__ tasks, int ntasks,
-                                                 int maxt, const CrTile* __restrict__ tlist, int ntl,
-                                                 int total, double sg) {
+// One workgroup's share of a product stage: workgroup slot g of the 1D
+// grid (already XCD-remapped by the caller) covers tiles g * TPW .. + TPW - 1.
+// TILESIGN: the sign of each tile comes from its descriptor (CrTile::neg;
+// side-work tile lists mix stages of both signs) instead of sg.  PFX: operand
+// prefetch depth in k-steps (0: the DWHMC_GEMM_PF default).
+template <int BP, int MI, int KSPLIT, int PFX = 0, bool TILESIGN = false>
+__device__ __forceinline__ void cr_gemm_wg(double2* __restrict__ pool, int64_t item,
+                                           const CrTask* __restrict__ tasks, int ntasks, int maxt,
+                                           const CrTile* __restrict__ tlist, int ntl, int total,
+                                           double sg, int g) {
   constexpr int TS = 16 * MI, TPW = 4 / KSPLIT, HP = BP / 2, NV = MI * MI * 4;
   constexpr int64_t BB = (int64_t)HP * BP;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
@@ -530,7 +545,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MI == 1 ? D
   if (stamp && threadIdx.x == 0 && blockIdx.x < 65536)
     g_gemm_stamps[blockIdx.x][7] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
 #endif
-  const int gt = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x) * TPW + w / KSPLIT);
+  const int gt = __builtin_amdgcn_readfirstlane(g * TPW + w / KSPLIT);
   // 16 x 16 tiles: the stage's compact tile list, one 64-byte descriptor per
   // tile (one scalar load, no idle waves for restricted tasks); 32 x 32
   // tiles: ntasks x maxt slots of the task list
@@ -548,9 +563,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MI == 1 ? D
     tc = tp->tc;
     cin = tp->cin;
     out = tp->out;
+    if constexpr (TILESIGN) sg = tp->neg ? -1.0 : 1.0;
   } else {
     const int tsk = rmd / maxt, tile = rmd - tsk * maxt;
     tk = tasks + (valid ? tsk : 0);
+    if constexpr (TILESIGN) sg = (tk->bq & kCrNegBit) ? -1.0 : 1.0;
     const int tr0 = tk->r0 / TS, tc0 = tk->c0 / TS;
     const int ct = (tk->c1 + TS - 1) / TS - tc0;
     const int rt = (tk->r1 + TS - 1) / TS - tr0;
@@ -593,8 +610,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MI == 1 ? D
 #endif
   auto run = [&](auto kqc) {
     constexpr int KQ = decltype(kqc)::value;
-    if constexpr (MI == 1) cr_tile_part<BP, MI, KSPLIT, KQ>(base, tp, tr, tc, t1, t2, t3);
-    else cr_tile_part<BP, MI, KSPLIT, KQ>(base, tk, tr, tc, t1, t2, t3);
+    if constexpr (MI == 1) cr_tile_part<BP, MI, KSPLIT, KQ, PFX>(base, tp, tr, tc, t1, t2, t3);
+    else cr_tile_part<BP, MI, KSPLIT, KQ, PFX>(base, tk, tr, tc, t1, t2, t3);
   };
   if (valid) {
     if (KSPLIT == 1 || kq == 0) run(std::integral_constant<int, 0>{});
@@ -661,6 +678,55 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MI == 1 ? D
     GEMM_STAMP(6, stamp);
 #endif
   }
+}
+
+template <int BP, int MI, int KSPLIT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MI == 1 ? DWHMC_GEMM_WAVES : 2))) void k_cr_gemm(double2* __restrict__ pool, int64_t item,
+                                                 const CrTask* __restrict__ tasks, int ntasks,
+                                                 int maxt, const CrTile* __restrict__ tlist, int ntl,
+                                                 int total, double sg) {
+  cr_gemm_wg<BP, MI, KSPLIT>(pool, item, tasks, ntasks, maxt, tlist, ntl, total, sg,
+                             xcd_remap(blockIdx.x, gridDim.x));
+}
+
+// ---------------------------------------------------------------------------
+// An inversion stage with side work: the first ninv x nbatch workgroups
+// invert (k_cr_inv), the rest run product tiles that are off the critical
+// path (the previous level's W1/W2 and U'/L'): an inversion
+// stage occupies only ninv x nbatch CUs (224 of 256 at the finest level of
+// L = 32, 14 at the coarsest) for its whole ~16 us, and the side tiles fill
+// the idle CUs instead of lengthening the product launches of the critical
+// path.  The inversions have the lowest workgroup ids, so they are
+// dispatched first and keep a CU each; the side workgroups run one per CU
+// (the inversion's register budget), so each wave computes a 32 x 32 output
+// tile over the full K (12 independent MFMA chains: a wave alone on its SIMD
+// must hide its own MFMA and memory latency; one 16 x 16 tile per wave ran at
+// a third of that rate).
+// ---------------------------------------------------------------------------
+template <int NT>
+__global__ __launch_bounds__(64 * NT) void k_cr_inv_side(double2* __restrict__ pool, int64_t item,
+                                                         const int* __restrict__ blk,
+                                                         const int* __restrict__ dst,
+                                                         const int* __restrict__ slot,
+                                                         double* __restrict__ ldpart, int nslots,
+                                                         int ninv, int nbatch,
+                                                         const CrTask* __restrict__ stasks, int nst,
+                                                         int maxt, int total) {
+  static_assert(NT == 4, "side work runs 4-wave workgroups");
+  __shared__ double2 pan[2][NT][16 * 17];
+  __shared__ double ldw[NT];
+  const int b = blockIdx.x, nall = ninv * nbatch;
+#if defined(DWHMC_SIDE_NOP)     // diagnostic builds (tools/ab_bench.py LIB=...): side part empty
+  if (b >= nall) return;
+#elif defined(DWHMC_SIDE_NOINV)  // inversion part empty
+  if (b < nall) return;
+#endif
+  if (b < nall) {
+    cr_inv_wg<NT>(pool, item, b / ninv, b - (b / ninv) * ninv, blk, dst, slot, ldpart, nslots, pan, ldw);
+    return;
+  }
+  cr_gemm_wg<16 * NT, 2, 1, 0, true>(pool, item, stasks, nst, maxt, nullptr, 0, total, 1.0,
+                                    xcd_remap(b - nall, (int)gridDim.x - nall));
 }
 
 // ---------------------------------------------------------------------------
@@ -779,6 +845,7 @@ __global__ __launch_bounds__(256) void k_cr_fermion_energy(const double2* __rest
 // launchers
 // ---------------------------------------------------------------------------
 bool cr_supported_bp(int BP) { return BP == 32 || BP == 64 || BP == 96 || BP == 128; }
+bool cr_supported_side(int BP) { return BP == 64; }
 
 void launch_cr_fill(const CrDims& c, double2* pool, const int* list, int nlist, const int* hcol,
                     const double* hval, const int* Dcol, const int* Dsrc, const double2* Delta,
@@ -802,6 +869,18 @@ void launch_cr_inv(const CrDims& c, double2* pool, const int* blk, const int* ds
     case 96: hipLaunchKernelGGL(k_cr_inv<6>, g, dim3(384), 0, s, pool, c.item, blk, dst, slot, ldpart, c.Ly); break;
     default: hipLaunchKernelGGL(k_cr_inv<8>, g, dim3(512), 0, s, pool, c.item, blk, dst, slot, ldpart, c.Ly); break;
   }
+}
+
+void launch_cr_inv_side(const CrDims& c, double2* pool, const int* blk, const int* dst, const int* slot,
+                        int n, double* ldpart, const CrTask* stasks, int nst, int maxt32, hipStream_t s) {
+  if (nst <= 0) {
+    launch_cr_inv(c, pool, blk, dst, slot, n, ldpart, s);
+    return;
+  }
+  const int total = c.nbatch * nst * maxt32;
+  const int side_wg = (total + 3) / 4;
+  hipLaunchKernelGGL(k_cr_inv_side<4>, dim3(n * c.nbatch + side_wg), dim3(256), 0, s, pool, c.item, blk,
+                     dst, slot, ldpart, c.Ly, n, c.nbatch, stasks, nst, maxt32, total);
 }
 
 // Stage configuration (tile TS, K split).  16 x 16 tiles with a 4-way K

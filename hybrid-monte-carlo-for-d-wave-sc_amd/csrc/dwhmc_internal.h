@@ -45,13 +45,16 @@ struct CrTask {
   int a[4], b[4];
   int r0, r1, c0, c1;
 };
+// CrTask::bq bit of side-work tasks whose stage sign is negative (side-work
+// task lists mix stages of both signs)
+constexpr int kCrNegBit = 1 << 8;
 // One 16 x 16 output tile of a product stage with its task's operands, so a
 // workgroup reads its whole descriptor with one 64-byte scalar load (tr, tc:
 // tile row / column in 16-tile units)
 struct alignas(64) CrTile {
   int out, cin, nt, bq;
   int a[4], b[4];
-  int tr, tc, pad0, pad1;
+  int tr, tc, neg, pad1;   // neg: 1 = negative sign (TILESIGN lists)
 };
 // wave tiles of a task at tile size ts
 inline int cr_task_tiles(const CrTask& t, int ts) {
@@ -80,6 +83,12 @@ void launch_cr_fermion_energy(const CrDims& c, const double2* pool, const int64_
 // inverts blocks blk[i] into dst[i] (dst == blk: in place); ln|det| into ldpart slots
 void launch_cr_inv(const CrDims& c, double2* pool, const int* blk, const int* dst, const int* slot,
                    int n, double* ldpart, hipStream_t s);
+// the same inversions plus nst side-work product tasks per batch item
+// (32 x 32 wave tiles, maxt32 per task, each task's sign in bq & kCrNegBit)
+// on the CUs the inversions leave idle
+bool cr_supported_side(int BP);
+void launch_cr_inv_side(const CrDims& c, double2* pool, const int* blk, const int* dst, const int* slot,
+                        int n, double* ldpart, const CrTask* stasks, int nst, int maxt32, hipStream_t s);
 // block-product stage configuration: output tile TS x TS (16 or 32) and the
 // number of waves splitting each tile's K range (1, 2, 4)
 struct CrGemmCfg {
