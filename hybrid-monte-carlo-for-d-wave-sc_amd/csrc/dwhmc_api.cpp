@@ -167,10 +167,12 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol, bool 
   // per task of cur_tasks: compute only the A-part diagonal tiles and the
   // B part (level-0 G_ee: the force reads its pairing (B) entries, E_f and
   // Tr rho_hh its diagonal; nothing reads the rest)
+  // 2: only the diagonal tiles of the B part (level-0 G_ea / G_ec: the force
+  // reads their entries (x, HP + x) of the vertical bonds, nothing else)
   std::vector<char> cur_adiag;
-  bool adiag_next = false;
+  char adiag_next = 0;
   auto task = [&](int out, int cin, std::initializer_list<Term> terms) {
-    cur_adiag.push_back(adiag_next ? 1 : 0);
+    cur_adiag.push_back(adiag_next);
     dwh::CrTask t{};
     t.out = out;
     t.cin = cin;
@@ -210,7 +212,8 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol, bool 
       int kept = 0;
       for (int k = 0; k < nk; ++k) {
         const int tr = t.r0 / 16 + k / ct, tc = t.c0 / 16 + k % ct;
-        if (cur_adiag[ti] && tc < HP / 16 && tc != tr) continue;
+        if (cur_adiag[ti] == 1 && tc < HP / 16 && tc != tr) continue;
+        if (cur_adiag[ti] == 2 && tc != HP / 16 + tr) continue;
         dwh::CrTile d{};
         d.out = t.out;
         d.cin = t.cin;
@@ -352,9 +355,10 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol, bool 
       }
     }
     // Level 0 is the last backward level: G_ea, G_ec (cross-row bonds, not
-    // operands of anything after them) are formed only on their pairing
-    // columns HP .. HP+Lx-1 there; G_ae, G_ce (right operands of G_ee) and
-    // G_ee (in-row bonds, hole diagonal) need their whole top half.
+    // operands of anything after them) are formed only on the diagonal tiles
+    // of their B part there (the vertical pairing bonds read (x, HP + x));
+    // G_ae, G_ce (right operands of G_ee) need their whole top half, G_ee
+    // (in-row bonds, hole diagonal) its A-part diagonal tiles and B part.
     const bool sel = (li == 0);
     const int H0 = sel ? HP : 0, H1 = sel ? HP + Lx : BP;
     std::vector<int> Gae(m, -1), Gce(m, -1);
@@ -367,8 +371,10 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol, bool 
       const int gea = nb(), gec = nb(), gae = nb(), gce = nb();
       w_c0 = H0;
       w_c1 = H1;
+      adiag_next = sel ? 2 : 0;
       task(gea, -1, {{lv.W1[e], Gaa}, {lv.W2[e], Gca}});
       task(gec, -1, {{lv.W1[e], Gac}, {lv.W2[e], Gcc}});
+      adiag_next = 0;
       w_c0 = 0;
       w_c1 = BP;
       task(gae, -1, {{Gaa, lv.V1[e]}, {Gac, lv.V2[e]}});
@@ -381,12 +387,12 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol, bool 
       Gce[e] = gce;
     }
     flush(1.0);
-    adiag_next = sel;
+    adiag_next = sel ? 1 : 0;
     for (int e : lv.E) {
       task(lv.Dinv[e], lv.Dinv[e], {{lv.W1[e], Gae[e]}, {lv.W2[e], Gce[e]}});
       gd[e] = lv.Dinv[e];
     }
-    adiag_next = false;
+    adiag_next = 0;
     flush(1.0);
     GD = gd;
     GU = gu;
