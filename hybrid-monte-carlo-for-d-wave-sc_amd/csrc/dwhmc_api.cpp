@@ -58,6 +58,7 @@ struct CrStage {
                         // inversions: their side-work tasks in CrPlan::tasks (launch_cr_inv_side,
                         // maxt32 tiles each), flops in `flops`
   dwh::CrGemmCfg cfg;   // products: tile / K-split chosen once per context
+  int l0 = 0;           // inversions: level 0 from the static R = A^-1 blocks (k_cr_inv0)
 };
 
 struct CrPlan {
@@ -66,6 +67,7 @@ struct CrPlan {
   std::vector<dwh::CrTask> tasks;
   std::vector<dwh::CrTile> tiles16;          // per product stage: its 16 x 16 tiles with their operands
   std::vector<int> inv_blk, inv_dst, inv_slot;   // inversion source / destination block, ln|det| slot
+  std::vector<int> inv0_r;                       // level-0 inversions (l0 stage): R = A^-1 block per entry
   std::vector<int64_t> goff, doff;
   std::vector<int> fill_all, fill_step;      // level-0 blocks written at create / every step
   std::vector<int64_t> off_ph;               // pairing entries outside fill_step (-1: none)
@@ -97,8 +99,11 @@ struct CrPlan {
 // DWHMC_CR_SIDE_W (default 2): inversion stages between a level and the one
 // that runs its W products; DWHMC_CR_SIDE_M (default 4): smallest level size
 // m whose products move (A/B knobs; profiles/r02_exp_cr_side_work.txt).
+//
+// inv0: the level-0 inversions use static R = A^-1 blocks (k_cr_inv0), one
+// per eliminated row, computed at context creation.
 CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol, bool side, int nbatch,
-                     int ncu) {
+                     int ncu, bool inv0) {
   const int side_woff = [] {
     const char* e = std::getenv("DWHMC_CR_SIDE_W");
     return e ? std::max(1, std::atoi(e)) : 2;
@@ -150,6 +155,11 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol, bool 
     pl.tasks.insert(pl.tasks.end(), stk.begin(), stk.end());
     ++inv_ord;
     std::vector<int> dst;
+    // level-0 blocks (the first inversion stage): from their static R blocks
+    if (inv0 && std::all_of(blocks.begin(), blocks.end(), [&](int b) { return b < 3 * Ly; })) {
+      st.l0 = 1;
+      for (size_t i = 0; i < blocks.size(); ++i) pl.inv0_r.push_back(nb());
+    }
     for (int b : blocks) {
       const int d = b < 3 * Ly ? nb() : b;
       pl.inv_blk.push_back(b);
@@ -511,7 +521,8 @@ struct dwh_ctx {
   dwh::CrTile* d_tiles16 = nullptr;
   double* efpart = nullptr;     // per (chain, pole) E_f / Tr G22 partials
   unsigned* efdone = nullptr;   // per chain: pole blocks done (k_cr_fermion_energy)
-  int *d_inv_blk = nullptr, *d_inv_dst = nullptr, *d_inv_slot = nullptr;
+  int *d_inv_blk = nullptr, *d_inv_dst = nullptr, *d_inv_slot = nullptr, *d_inv0_r = nullptr;
+  double* ldA = nullptr;   // static ln|det| of the Δ = 0 level-0 blocks (= 2 ln|det A|) per slot
   int64_t *d_goff = nullptr, *d_doff = nullptr, *d_off_ph = nullptr;
   int *d_fill_all = nullptr, *d_fill_step = nullptr;
   // the pool's level-0 pairing entries already hold the current Δ (set by a
@@ -716,6 +727,10 @@ void cr_enqueue(dwh_ctx* ctx) {
       dwh::launch_cr_inv_side(c, ctx->bpool, ctx->d_inv_blk + st.first, ctx->d_inv_dst + st.first,
                               ctx->d_inv_slot + st.first, st.n, ctx->ldpart, ctx->d_tasks + st.tfirst,
                               st.ntiles, st.maxt32, ctx->stream);
+    } else if (st.kind == 0 && st.l0) {
+      Scope s(ctx, T_CR_INV, st.n * bp3);
+      dwh::launch_cr_inv0(c, ctx->bpool, ctx->d_inv_blk + st.first, ctx->d_inv0_r, ctx->d_inv_dst + st.first,
+                          ctx->d_inv_slot + st.first, st.n, ctx->ldpart, ctx->ldA, ctx->stream);
     } else if (st.kind == 0) {
       Scope s(ctx, T_CR_INV, st.n * bp3);
       dwh::launch_cr_inv(c, ctx->bpool, ctx->d_inv_blk + st.first, ctx->d_inv_dst + st.first,
@@ -1158,7 +1173,10 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
       int ncu = 256;
       if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu <= 0)
         ncu = 256;
-      ctx->plan = build_cr_plan((int)Lx, (int)Ly, BP, Dcol, side, d.nbatch, ncu);
+      // DWHMC_CR_INV0=0: level-0 blocks inverted whole (k_cr_inv) like the rest
+      const char* e0 = std::getenv("DWHMC_CR_INV0");
+      const bool inv0 = dwh::cr_supported_inv0(BP) && !(e0 && *e0 == '0');
+      ctx->plan = build_cr_plan((int)Lx, (int)Ly, BP, Dcol, side, d.nbatch, ncu, inv0);
       dwh::CrDims& c = ctx->cr;
       c.Lx = (int)Lx;
       c.Ly = (int)Ly;
@@ -1175,8 +1193,8 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
         int i = 0;
         for (const CrStage& st : ctx->plan.stages) {
           if (st.kind == 0)
-            std::fprintf(stderr, "cr stage %2d: inv   blocks=%d side_tiles=%d side_flops/item=%.3g\n", i, st.n,
-                         st.ntiles, st.flops);
+            std::fprintf(stderr, "cr stage %2d: inv%s blocks=%d side_tasks=%d side_flops/item=%.3g\n", i,
+                         st.l0 ? "0 " : "  ", st.n, st.ntiles, st.flops);
           else
             std::fprintf(stderr, "cr stage %2d: gemm  tasks=%d maxt32=%d maxt16=%d ntmax=%d flops/item=%.3g cfg=%d:%d ntiles=%d\n",
                          i, st.n, st.maxt32, st.maxt16, st.ntmax, st.flops, st.cfg.ts, st.cfg.ksplit, st.ntiles);
@@ -1225,6 +1243,8 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     ALLOC(d_inv_blk, pl.inv_blk.size());
     ALLOC(d_inv_dst, pl.inv_dst.size());
     ALLOC(d_inv_slot, pl.inv_slot.size());
+    ALLOC(d_inv0_r, pl.inv0_r.size());
+    ALLOC(ldA, (size_t)d.nbatch * Ly);
     ALLOC(d_goff, pl.goff.size());
     ALLOC(d_doff, pl.doff.size());
     ALLOC(d_off_ph, pl.off_ph.size());
@@ -1287,6 +1307,7 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     UP(d_inv_blk, pl.inv_blk.data(), pl.inv_blk.size());
     UP(d_inv_dst, pl.inv_dst.data(), pl.inv_dst.size());
     UP(d_inv_slot, pl.inv_slot.data(), pl.inv_slot.size());
+    UP(d_inv0_r, pl.inv0_r.data(), pl.inv0_r.size());
     UP(d_goff, pl.goff.data(), pl.goff.size());
     UP(d_doff, pl.doff.data(), pl.doff.size());
     UP(d_off_ph, pl.off_ph.data(), pl.off_ph.size());
@@ -1315,6 +1336,13 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     (void)hipMemsetAsync(ctx->ldstatic, 0, d.nbatch * sizeof(double), s);
     dwh::launch_cr_fill(ctx->cr, ctx->bpool, ctx->d_fill_all, (int)ctx->plan.fill_all.size(), ctx->hcol,
                         ctx->hval, ctx->Dcol, ctx->Dsrc, ctx->Delta, ctx->d_y, nullptr, s);
+    // static R = A^-1 of the level-0 blocks k_cr_inv0 inverts: the Δ = 0
+    // blocks [[A, 0], [0, -conj A]] inverted out of place give [R | 0] and
+    // 2 ln|det A| (the pairing entries are still zero here)
+    for (const CrStage& st : ctx->plan.stages)
+      if (st.kind == 0 && st.l0)
+        dwh::launch_cr_inv(ctx->cr, ctx->bpool, ctx->d_inv_blk + st.first, ctx->d_inv0_r, ctx->d_inv_slot + st.first,
+                           st.n, ctx->ldA, s);
   }
   if (hipStreamSynchronize(s) != hipSuccess || hipGetLastError() != hipSuccess) {
     ctx->err = "static R initialisation failed on the device";

@@ -414,6 +414,154 @@ __global__ __launch_bounds__(64 * NT) void k_cr_inv(double2* __restrict__ pool, 
 }
 
 // ---------------------------------------------------------------------------
+// Level-0 inversions from the static particle block.  A level-0 diagonal
+// block is D = [[A, B], [conj B, -conj A]] with A = h_row - i y (hopping,
+// disorder, mu: Δ-independent) and B = Δ/2 (in-row pairing).  Its M-form
+// inverse [[X, Y], [conj Y, -conj X]] follows from R = A^-1, kept per (row,
+// pole) since context creation (k_cr_inv on the Δ = 0 blocks, out of place:
+// top half [R | 0], ln|det D0| = 2 ln|det A|):
+//   Z = R B,  S = A + B conj(Z)  (the Schur complement of -conj A in D),
+//   X = S^-1,  Y = Z conj(X),  ln|det D| = ln|det A| + ln|det S|.
+// i S has Hermitian part >= y I like i D (a Schur complement), so S needs no
+// pivoting either.  S^-1 by 2 x 2 tile blocks (HP = 32): S00^-1 in registers,
+// P = S00^-1 S01, Q = S10 S00^-1, T = S11 - S10 P, T^-1 in registers,
+// X01 = -P T^-1, X10 = -T^-1 Q, X11 = T^-1, X00 = S00^-1 - X01 Q.  The serial
+// chain is two 16 x 16 register inversions and six 16 x 16 tile products
+// instead of four inversions and their panel updates (k_cr_inv<4>).  Wave w
+// owns tile (w >> 1, w & 1) of every 32 x 32 matrix; tiles meet in LDS
+// (row-major, stride 17); MFMA operands in the C layout as in mma16_3m.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void tile_to_lds(double2* T, const d4& cr, const d4& ci) {
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) T[(lk + 4 * rr) * 17 + lr] = make_double2(cr[rr], ci[rr]);
+}
+// C-layout registers of an LDS tile; CONJ: of its complex conjugate
+template <bool CONJ = false>
+__device__ __forceinline__ void tile_from_lds(const double2* T, d4& cr, d4& ci) {
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const double2 v = T[(lk + 4 * rr) * 17 + lr];
+    cr[rr] = v.x;
+    ci[rr] = CONJ ? -v.y : v.y;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_cr_inv0(double2* __restrict__ pool, int64_t item,
+                                                 const int* __restrict__ blk, const int* __restrict__ rblk,
+                                                 const int* __restrict__ dst, const int* __restrict__ slot,
+                                                 double* __restrict__ ldpart,
+                                                 const double* __restrict__ ldA, int nslots) {
+  constexpr int BP = 64, HP = 32, TSZ = 16 * 17;
+  __shared__ double2 sR[4][TSZ], sB[4][TSZ], sZ[4][TSZ], sS[4][TSZ], sX[4][TSZ], sA[4][TSZ];
+  __shared__ double ldw[2];
+  const int bi = blockIdx.y, li = blockIdx.x;
+  const double2* D = pool + (int64_t)bi * item + (int64_t)blk[li] * HP * BP;
+  const double2* Rm = pool + (int64_t)bi * item + (int64_t)rblk[li] * HP * BP;
+  double2* Mo = pool + (int64_t)bi * item + (int64_t)dst[li] * HP * BP;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  const int ti = w >> 1, tj = w & 1;
+  // this wave's tiles: A (C layout, registers), R and B (LDS)
+  d4 acr, aci;
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int row = ti * 16 + lk + 4 * rr, col = tj * 16 + lr;
+    const double2 a = D[(int64_t)row * BP + col];
+    const double2 b = D[(int64_t)row * BP + HP + col];
+    const double2 r = Rm[(int64_t)row * BP + col];
+    acr[rr] = a.x;
+    aci[rr] = a.y;
+    sB[w][(lk + 4 * rr) * 17 + lr] = b;
+    sR[w][(lk + 4 * rr) * 17 + lr] = r;
+  }
+  __syncthreads();
+  // Z = R B
+  d4 zr = {0.0, 0.0, 0.0, 0.0}, zi = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    d4 br, bim;
+    tile_from_lds(sB[2 * k + tj], br, bim);
+    mma16_3m<false>(zr, zi, sR[2 * ti + k], br, bim);
+  }
+  tile_to_lds(sZ[w], zr, zi);
+  __syncthreads();
+  // S = A + B conj(Z)
+  d4 sr = acr, si = aci;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    d4 br, bim;
+    tile_from_lds<true>(sZ[2 * k + tj], br, bim);
+    mma16_3m<false>(sr, si, sB[2 * ti + k], br, bim);
+  }
+  double ld = 0.0;
+  if (w == 0) ld += 0.5 * log(wave_inv16_c(sr, si));   // S00^-1 (C layout in, C layout out)
+  tile_to_lds(sS[w], sr, si);                           // S00^-1, S01, S10, S11
+  __syncthreads();
+  // P = S00^-1 S01 (wave 1, kept in sA[1]); Q = S10 S00^-1 (wave 2, sA[2])
+  if (w == 1) {
+    d4 pr = {0.0, 0.0, 0.0, 0.0}, pi = {0.0, 0.0, 0.0, 0.0};
+    mma16_3m<false>(pr, pi, sS[0], sr, si);
+    tile_to_lds(sA[1], pr, pi);
+  } else if (w == 2) {
+    d4 qr = {0.0, 0.0, 0.0, 0.0}, qi = {0.0, 0.0, 0.0, 0.0}, br, bim;
+    tile_from_lds(sS[0], br, bim);
+    mma16_3m<false>(qr, qi, sS[2], br, bim);
+    tile_to_lds(sA[2], qr, qi);
+  }
+  __syncthreads();
+  // T = S11 - S10 P, T^-1 (wave 3, sX[3] = X11)
+  if (w == 3) {
+    d4 br, bim;
+    tile_from_lds(sA[1], br, bim);
+    mma16_3m<true>(sr, si, sS[2], br, bim);
+    ld += 0.5 * log(wave_inv16_c(sr, si));
+    tile_to_lds(sX[3], sr, si);
+  }
+  __syncthreads();
+  // X01 = -P T^-1 (wave 1), X10 = -T^-1 Q (wave 2)
+  d4 xr = sr, xi = si;   // wave 0: S00^-1; wave 3: T^-1 = X11
+  if (w == 1 || w == 2) {
+    d4 br, bim;
+    tile_from_lds(w == 1 ? sX[3] : sA[2], br, bim);
+    xr = d4{0.0, 0.0, 0.0, 0.0};
+    xi = d4{0.0, 0.0, 0.0, 0.0};
+    mma16_3m<true>(xr, xi, w == 1 ? sA[1] : sX[3], br, bim);
+    tile_to_lds(sX[w], xr, xi);
+  }
+  __syncthreads();
+  // X00 = S00^-1 - X01 Q (wave 0)
+  if (w == 0) {
+    d4 br, bim;
+    tile_from_lds(sA[2], br, bim);
+    mma16_3m<true>(xr, xi, sX[1], br, bim);
+    tile_to_lds(sX[0], xr, xi);
+  }
+  __syncthreads();
+  // Y = Z conj(X)
+  d4 yr = {0.0, 0.0, 0.0, 0.0}, yi = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    d4 br, bim;
+    tile_from_lds<true>(sX[2 * k + tj], br, bim);
+    mma16_3m<false>(yr, yi, sZ[2 * ti + k], br, bim);
+  }
+  // top half of D^-1 = [X | Y]
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int row = ti * 16 + lk + 4 * rr, col = tj * 16 + lr;
+    Mo[(int64_t)row * BP + col] = make_double2(xr[rr], xi[rr]);
+    Mo[(int64_t)row * BP + HP + col] = make_double2(yr[rr], yi[rr]);
+  }
+  if (l == 0 && (w == 0 || w == 3)) ldw[w == 3] = ld;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int64_t o = (int64_t)bi * nslots + slot[li];
+    ldpart[o] = 0.5 * ldA[o] + ldw[0] + ldw[1];
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Batched block products on top halves: task t of batch item bi writes
 //   out = [cin] + sg Σ_{h < nt} A_h B_h      (top halves, HP x BP)
 // K runs over all BP rows of B_h: rows 0..HP-1 are stored, rows HP..BP-1 are
@@ -846,6 +994,14 @@ __global__ __launch_bounds__(256) void k_cr_fermion_energy(const double2* __rest
 // ---------------------------------------------------------------------------
 bool cr_supported_bp(int BP) { return BP == 32 || BP == 64 || BP == 96 || BP == 128; }
 bool cr_supported_side(int BP) { return BP == 64; }
+bool cr_supported_inv0(int BP) { return BP == 64; }
+
+void launch_cr_inv0(const CrDims& c, double2* pool, const int* blk, const int* rblk, const int* dst,
+                    const int* slot, int n, double* ldpart, const double* ldA, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_cr_inv0, dim3(n, c.nbatch), dim3(256), 0, s, pool, c.item, blk, rblk, dst, slot, ldpart,
+                     ldA, c.Ly);
+}
 
 void launch_cr_fill(const CrDims& c, double2* pool, const int* list, int nlist, const int* hcol,
                     const double* hval, const int* Dcol, const int* Dsrc, const double2* Delta,

@@ -252,4 +252,21 @@ __device__ __forceinline__ double wave_inv16_dpp(double2 (&a)[4]) {
   return pprod;
 }
 
+// In-place inverse of a 16 x 16 tile held in the MFMA C layout (lane: rows
+// lk + 4 rr, column lr).  Those registers are the strided layout of the
+// transposed tile, and inverting M^T in that layout leaves (M^T)^-1 =
+// (M^-1)^T strided, i.e. M^-1 in the C layout.  Returns Π |pivot|^2.
+__device__ __forceinline__ double wave_inv16_c(d4& cr, d4& ci) {
+  double2 dv[4];
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) dv[jj] = make_double2(cr[jj], ci[jj]);
+  const double p = wave_inv16_dpp<true>(dv);
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) {
+    cr[jj] = dv[jj].x;
+    ci[jj] = dv[jj].y;
+  }
+  return p;
+}
+
 }  // namespace dwh

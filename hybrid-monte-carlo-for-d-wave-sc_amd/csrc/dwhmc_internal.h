@@ -83,6 +83,11 @@ void launch_cr_fermion_energy(const CrDims& c, const double2* pool, const int64_
 // inverts blocks blk[i] into dst[i] (dst == blk: in place); ln|det| into ldpart slots
 void launch_cr_inv(const CrDims& c, double2* pool, const int* blk, const int* dst, const int* slot,
                    int n, double* ldpart, hipStream_t s);
+// level-0 inversions of blocks blk[i] (BP = 64) from the static R = A^-1
+// blocks rblk[i] (k_cr_inv0); ln|det| = ldA/2 + ln|det S| into ldpart slots
+bool cr_supported_inv0(int BP);
+void launch_cr_inv0(const CrDims& c, double2* pool, const int* blk, const int* rblk, const int* dst,
+                    const int* slot, int n, double* ldpart, const double* ldA, hipStream_t s);
 // the same inversions plus nst side-work product tasks per batch item
 // (32 x 32 wave tiles, maxt32 per task, each task's sign in bq & kCrNegBit)
 // on the CUs the inversions leave idle
