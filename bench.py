@@ -335,7 +335,7 @@ def main(argv=None):
         # per-launch averages.
         replay = schedule(w_sw, min(a.steps, 2 * Nt), Nt)
         replay_steps = sum(n * nt for _, n, nt in replay)
-        names = [dom, "assemble"] + (["cr_inv"] if cr else [])
+        names = [dom, "assemble"] + (["cr_inv", "cr_inv_side"] if cr else [])
         ctx.timing_enable(names)
         ctx.timing_reset()
         for f, n, nt in replay:
@@ -394,14 +394,30 @@ def main(argv=None):
             if cr:
                 kname = f"k_cr_gemm<{info['block']},1,4>"   # 16x16 tiles, 4-way K split
                 msi, ni, wi = kern["cr_inv"]
+                mss, ns, ws = kern["cr_inv_side"]
                 # the CR path's own algorithmic flops per leapfrog step (block
-                # products + block inversions) x the timed steps
-                rec["alg_tflops"] = (w + wi) / replay_steps * a.steps * world / el / 1e12
-                rec["alg_flops_per_step"] = (w + wi) / replay_steps / a.chains
-                rec["cr_inv"] = {"bound": "latency", "kernel": f"k_cr_inv<{info['block'] // 16}>",
+                # products, incl. the side work of the inversion stages, and
+                # block inversions at 8 BP^3 each) x the timed steps
+                rec["alg_tflops"] = (w + wi + ws) / replay_steps * a.steps * world / el / 1e12
+                rec["alg_flops_per_step"] = (w + wi + ws) / replay_steps / a.chains
+                nt = info["block"] // 16
+                # level-0 inversions: k_cr_inv0 (static particle block, BP = 64)
+                # when the plan has no plain k_cr_inv stage besides it
+                rec["cr_inv"] = {"bound": "latency",
+                                 "kernel": ("k_cr_inv0" if info["block"] == 64 else f"k_cr_inv<{nt}>")
+                                 + (f" + k_cr_inv<{nt}>" if info["block"] == 64 and ni > replay_steps else ""),
+                                 "launches_per_step": ni / replay_steps,
                                  "achieved_tflops": wi / (msi * 1e-3) / 1e12 if msi > 0 else None,
                                  "avg_launch_us": 1000.0 * msi / ni if ni else None,
                                  "ms_per_step": msi / replay_steps}
+                if ns:
+                    rec["cr_inv_side"] = {"bound": "latency", "kernel": f"k_cr_inv_side<{nt}>",
+                                          "what": "block inversions + off-critical-path block products "
+                                                  "on the CUs the inversions leave idle",
+                                          "launches_per_step": ns / replay_steps,
+                                          "avg_launch_us": 1000.0 * mss / ns,
+                                          "flops_per_launch": ws / ns,
+                                          "ms_per_step": mss / replay_steps}
             else:
                 nb = -(-info["N"] // 64)                 # GJ block steps; odd nb ends with one rank-64 step
                 kname = "k_gj_update<2>" if nb % 2 == 0 else "k_gj_update<2>+<0>"

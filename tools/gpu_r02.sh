@@ -9,7 +9,7 @@ O=$R/gpurun_out/$TAG
 mkdir -p "$O"
 if [ "$2" != "skip-tests" ]; then
   timeout -k 10 600 python -u -m pytest "$R/tests" -m gpu -x -v --timeout 300 --timeout-method thread \
-    > "$O/tests.log" 2>&1
+    ${PYTEST_K:+-k "$PYTEST_K"} > "$O/tests.log" 2>&1
 fi
 timeout -k 10 400 python3 "$R/bench.py" --gpus 1 --steps 20 --warmup 5 > "$O/bench_driver.json" 2> "$O/bench_driver.err"
 bash "$R/tools/profile_round.sh" "$TAG"
