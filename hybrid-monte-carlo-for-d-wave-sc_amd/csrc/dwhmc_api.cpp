@@ -789,18 +789,17 @@ void fermion_energy_enqueue(dwh_ctx* ctx) {
 
 // One hmc_sweep! trajectory reading its draws from device pointers
 // (src/HMC.jl:71-122): refresh, H_old, backup, leapfrog, H_new.
-void trajectory_enqueue(dwh_ctx* ctx, const double2* noise, int64_t Nt, double dt, double mass) {
+// with_hnew = false: the caller's k_traj_end forms H_new (with the Metropolis test)
+void trajectory_enqueue(dwh_ctx* ctx, const double2* noise, int64_t Nt, double dt, double mass,
+                        bool with_hnew = true) {
   const Dims& d = ctx->d;
   hipStream_t s = ctx->stream;
-  dwh::launch_refresh(d, noise, ctx->Pi, std::sqrt(2.0 * mass), s);                  // :77
-  dwh::launch_total_energy(d, ctx->Delta, ctx->Pi, ctx->Ef, ctx->beta, ctx->J, mass,  // :80
-                           ctx->Hold, s);
-  dwh::launch_backup(d, ctx->Delta, ctx->Pair, ctx->Ef, ctx->Trhh, ctx->DeltaB, ctx->PairB,  // :84-86
-                     ctx->EfB, ctx->TrhhB, s);
   const double coef_field = dt / (2.0 * mass);                                        // :95
-  // :91-92 half kick, fused with step 1's drift (:101)
-  dwh::launch_force_from_pair(d, ctx->Pair, ctx->Delta, ctx->F, ctx->Pi,
-                              kickdrift(ctx, 0.5 * dt, Nt > 0 ? coef_field : 0.0), ctx->beta, ctx->J, s);
+  // :77 refresh, :80 H_old, :84-86 backup, :91-92 half kick fused with step
+  // 1's drift (:101): one launch (k_traj_begin)
+  dwh::launch_traj_begin(d, noise, std::sqrt(2.0 * mass), ctx->Pi, ctx->Delta, ctx->Pair, ctx->F, ctx->Ef,
+                         ctx->Trhh, ctx->DeltaB, ctx->PairB, ctx->EfB, ctx->TrhhB, ctx->Hold, ctx->beta, ctx->J,
+                         mass, kickdrift(ctx, 0.5 * dt, Nt > 0 ? coef_field : 0.0), s);
   for (int64_t step = 1; step <= Nt; ++step) {                                        // :98
     // :105-107 update_H_BdG! + diagonalize + compute_forces!, then the kick of
     // :111-113 (dt) and the next step's drift (:101), or the final half kick
@@ -812,8 +811,9 @@ void trajectory_enqueue(dwh_ctx* ctx, const double2* noise, int64_t Nt, double d
                                 ctx->beta, ctx->J, s);
   else
     fermion_energy_enqueue(ctx);
-  dwh::launch_total_energy(d, ctx->Delta, ctx->Pi, ctx->Ef, ctx->beta, ctx->J, mass,  // :122
-                           ctx->Hnew, s);
+  if (with_hnew)
+    dwh::launch_total_energy(d, ctx->Delta, ctx->Pi, ctx->Ef, ctx->beta, ctx->J, mass,  // :122
+                             ctx->Hnew, s);
 }
 
 // One hmc_sweep! body (src/HMC.jl:71-144): trajectory, Metropolis, restore.
@@ -821,10 +821,10 @@ void sweep_enqueue(dwh_ctx* ctx, const double2* noise, const double* uniform, ui
                    double* dH, int64_t Nt, double dt, double mass) {
   const Dims& d = ctx->d;
   hipStream_t s = ctx->stream;
-  trajectory_enqueue(ctx, noise, Nt, dt, mass);
-  dwh::launch_metropolis(d, ctx->Hold, ctx->Hnew, uniform, acc, dH, s);               // :124-129
-  dwh::launch_restore(d, acc, ctx->DeltaB, ctx->PairB, ctx->EfB, ctx->TrhhB, ctx->Delta,  // :130-141
-                      ctx->Pair, ctx->Ef, ctx->Trhh, s);
+  trajectory_enqueue(ctx, noise, Nt, dt, mass, false);
+  // :122 H_new, :124-129 Metropolis, :130-141 restore: one launch
+  dwh::launch_traj_end(d, ctx->Delta, ctx->Pi, ctx->Pair, ctx->Ef, ctx->Trhh, ctx->DeltaB, ctx->PairB, ctx->EfB,
+                       ctx->TrhhB, ctx->Hold, ctx->Hnew, uniform, acc, dH, ctx->beta, ctx->J, mass, s);
 }
 
 int check_flag(dwh_ctx* ctx) {

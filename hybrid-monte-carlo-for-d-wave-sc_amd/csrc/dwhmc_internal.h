@@ -148,6 +148,17 @@ void launch_fermion_energy(const Dims& d, const double* ldstatic, const double* 
                            const double2* diagS, const double* cpole, double Cx, double beta,
                            double* Ef, double* Trhh, hipStream_t s);
 // H = Σ|π|²/2m + β/2J Σ|Δ|² + E_f into Hout[c]
+// trajectory start / end of the throughput path in one launch each (k_traj_begin:
+// refresh + H_old + backup + force from the cached P + kick/drift; k_traj_end:
+// H_new + Metropolis + restore)
+void launch_traj_begin(const Dims& d, const double2* noise, double scale, double2* Pi, double2* Delta,
+                       const double2* Pair, double2* F, const double* Ef, const double* Trhh, double2* DeltaB,
+                       double2* PairB, double* EfB, double* TrhhB, double* Hold, double beta, double J,
+                       double mass, const KickDrift& kd, hipStream_t s);
+void launch_traj_end(const Dims& d, double2* Delta, const double2* Pi, double2* Pair, double* Ef, double* Trhh,
+                     const double2* DeltaB, const double2* PairB, const double* EfB, const double* TrhhB,
+                     const double* Hold, double* Hnew, const double* uniform, uint8_t* accepted, double* dH,
+                     double beta, double J, double mass, hipStream_t s);
 void launch_total_energy(const Dims& d, const double2* Delta, const double2* Pi,
                          const double* Ef, double beta, double J, double mass, double* Hout,
                          hipStream_t s);

@@ -758,6 +758,101 @@ __global__ void k_restore(const uint8_t* __restrict__ accepted, const double2* _
   }
 }
 
+// ---------------------------------------------------------------------------
+// Trajectory start and end of the throughput path, one workgroup per chain
+// (src/HMC.jl:71-144); the energy sums keep k_total_energy's order (256
+// threads, strided bonds, wave sums, 4 partials), so H_old / H_new are the
+// same bits as the separate kernels give.
+//   begin: π = noise·sqrt(2m) (:77), H_old (:80), backup of Δ, P, E_f, Tr ρ_hh
+//          (:84-86), F from the cached P, the first half kick and (Nt > 0) the
+//          first drift (:91-92, :101)
+//   end:   H_new (:122), Metropolis (:124-129), restore on rejection (:130-141)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double block_sum256(double v, double* red) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  v = wave_sum(v);
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  const double t = red[0] + red[1] + red[2] + red[3];
+  __syncthreads();
+  return t;
+}
+
+__global__ __launch_bounds__(256) void k_traj_begin(const double2* __restrict__ noise, double scale,
+                                                    double2* __restrict__ Pi, double2* __restrict__ Delta,
+                                                    const double2* __restrict__ Pair, double2* __restrict__ F,
+                                                    const double* __restrict__ Ef, const double* __restrict__ Trhh,
+                                                    double2* __restrict__ DeltaB, double2* __restrict__ PairB,
+                                                    double* __restrict__ EfB, double* __restrict__ TrhhB,
+                                                    double* __restrict__ Hold, int N, double beta, double J,
+                                                    double mass, double kick, double drift, double cap2,
+                                                    int* __restrict__ flag) {
+  const int c = blockIdx.x;
+  __shared__ double red[4];
+  double sd = 0.0, sp = 0.0;
+  const double f = -beta / (2.0 * J);
+  for (int b = threadIdx.x; b < 2 * N; b += blockDim.x) {
+    const int64_t o = (int64_t)c * 2 * N + b;
+    const double2 z = noise[o], d = Delta[o], P = Pair[o];
+    const double2 p = make_double2(z.x * scale, z.y * scale);
+    sd += d.x * d.x + d.y * d.y;
+    sp += p.x * p.x + p.y * p.y;
+    DeltaB[o] = d;
+    PairB[o] = P;
+    Pi[o] = p;
+    const double2 Fv = make_double2(f * (d.x - J * P.x), f * (d.y - J * P.y));
+    F[o] = Fv;
+    kick_drift(Fv, o, Delta, Pi, kick, drift, cap2, flag);
+  }
+  const double SD = block_sum256(sd, red), SP = block_sum256(sp, red);
+  if (threadIdx.x == 0) {
+    Hold[c] = (1.0 / (2.0 * mass)) * SP + (beta / (2.0 * J)) * SD + Ef[c];
+    EfB[c] = Ef[c];
+    TrhhB[c] = Trhh[c];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_traj_end(double2* __restrict__ Delta, const double2* __restrict__ Pi,
+                                                  double2* __restrict__ Pair, double* __restrict__ Ef,
+                                                  double* __restrict__ Trhh, const double2* __restrict__ DeltaB,
+                                                  const double2* __restrict__ PairB, const double* __restrict__ EfB,
+                                                  const double* __restrict__ TrhhB, const double* __restrict__ Hold,
+                                                  double* __restrict__ Hnew, const double* __restrict__ uniform,
+                                                  uint8_t* __restrict__ accepted, double* __restrict__ dH, int N,
+                                                  double beta, double J, double mass) {
+  const int c = blockIdx.x;
+  __shared__ double red[4];
+  __shared__ int acc_s;
+  double sd = 0.0, sp = 0.0;
+  for (int b = threadIdx.x; b < 2 * N; b += blockDim.x) {
+    const double2 d = Delta[(int64_t)c * 2 * N + b];
+    const double2 p = Pi[(int64_t)c * 2 * N + b];
+    sd += d.x * d.x + d.y * d.y;
+    sp += p.x * p.x + p.y * p.y;
+  }
+  const double SD = block_sum256(sd, red), SP = block_sum256(sp, red);
+  if (threadIdx.x == 0) {
+    const double h = (1.0 / (2.0 * mass)) * SP + (beta / (2.0 * J)) * SD + Ef[c];
+    Hnew[c] = h;
+    const double dd = h - Hold[c];
+    const bool acc = (dd < 0.0) || (uniform[c] < exp(-dd));   // src/HMC.jl:128
+    accepted[c] = acc ? 1 : 0;
+    dH[c] = dd;
+    acc_s = acc;
+  }
+  __syncthreads();
+  if (acc_s) return;
+  for (int b = threadIdx.x; b < 2 * N; b += blockDim.x) {
+    const int64_t o = (int64_t)c * 2 * N + b;
+    Delta[o] = DeltaB[o];
+    Pair[o] = PairB[o];
+  }
+  if (threadIdx.x == 0) {
+    Ef[c] = EfB[c];
+    Trhh[c] = TrhhB[c];
+  }
+}
+
 __global__ void k_sum_ld(const double* __restrict__ ldpart, double* __restrict__ ldsum, int nb,
                          int nbatch) {
   const int bi = blockIdx.x * blockDim.x + threadIdx.x;
@@ -873,6 +968,21 @@ void launch_restore(const Dims& d, const uint8_t* accepted, const double2* Delta
                     double2* Delta, double2* Pair, double* Ef, double* Trhh, hipStream_t s) {
   hipLaunchKernelGGL(k_restore, bonds_grid(d), dim3(256), 0, s, accepted, DeltaB, PairB, EfB,
                      TrhhB, Delta, Pair, Ef, Trhh, d.N);
+}
+void launch_traj_begin(const Dims& d, const double2* noise, double scale, double2* Pi, double2* Delta,
+                       const double2* Pair, double2* F, const double* Ef, const double* Trhh, double2* DeltaB,
+                       double2* PairB, double* EfB, double* TrhhB, double* Hold, double beta, double J,
+                       double mass, const KickDrift& kd, hipStream_t s) {
+  hipLaunchKernelGGL(k_traj_begin, dim3(d.nc), dim3(256), 0, s, noise, scale, Pi, Delta, Pair, F, Ef, Trhh,
+                     DeltaB, PairB, EfB, TrhhB, Hold, d.N, beta, J, mass, kd.kick, kd.drift, kd.cap * kd.cap,
+                     kd.flag);
+}
+void launch_traj_end(const Dims& d, double2* Delta, const double2* Pi, double2* Pair, double* Ef, double* Trhh,
+                     const double2* DeltaB, const double2* PairB, const double* EfB, const double* TrhhB,
+                     const double* Hold, double* Hnew, const double* uniform, uint8_t* accepted, double* dH,
+                     double beta, double J, double mass, hipStream_t s) {
+  hipLaunchKernelGGL(k_traj_end, dim3(d.nc), dim3(256), 0, s, Delta, Pi, Pair, Ef, Trhh, DeltaB, PairB, EfB,
+                     TrhhB, Hold, Hnew, uniform, accepted, dH, d.N, beta, J, mass);
 }
 void launch_sum_ld(const Dims& d, const double* ldpart, double* ldsum, hipStream_t s) {
   hipLaunchKernelGGL(k_sum_ld, dim3((d.nbatch + 63) / 64), dim3(64), 0, s, ldpart, ldsum, d.nb,
