@@ -2084,6 +2084,98 @@ int dwh_timing_reset(dwh_ctx* ctx) {
 
 int dwh_selftest_mfma(int32_t device) { return dwh::selftest_mfma_layout(device); }
 
+// ---- host-only check of the CR schedule (no device) -------------------------
+// Builds the plan dwh_create would for an Lx x Ly periodic lattice (NN pairing
+// bonds) and nbatch = chains x poles batch items, then checks its dataflow:
+// every block a stage reads is a level-0 / static block or was written by an
+// EARLIER stage (launches are stream ordered, workgroups of one launch are
+// not), no block is read and written in one stage except a task's own
+// accumulate input, no two tasks of a stage write the same block, and every
+// block the force / E_f gather reads was written.
+int dwh_debug_cr_plan_check(int64_t Lx, int64_t Ly, int64_t nbatch, int32_t side, int32_t inv0, int64_t* stats) {
+  if (Lx < 1 || Ly < 1 || nbatch < 1) return fail(nullptr, DWH_ERR_ARG, "bad lattice / batch");
+  const int N = (int)(Lx * Ly);
+  std::vector<int> Dcol((size_t)N * kSlots);
+  for (int i = 0; i < N; ++i) {
+    const int x = i % (int)Lx, y = i / (int)Lx;
+    Dcol[(size_t)i * kSlots + 0] = y * (int)Lx + (x + 1) % (int)Lx;
+    Dcol[(size_t)i * kSlots + 1] = ((y + 1) % (int)Ly) * (int)Lx + x;
+    Dcol[(size_t)i * kSlots + 2] = y * (int)Lx + (x - 1 + (int)Lx) % (int)Lx;
+    Dcol[(size_t)i * kSlots + 3] = ((y - 1 + (int)Ly) % (int)Ly) * (int)Lx + x;
+  }
+  const int BP = (int)(2 * ((Lx + 15) / 16 * 16));
+  if (!dwh::cr_supported_bp(BP)) return fail(nullptr, DWH_ERR_ARG, "lattice row too wide for the CR path");
+  const CrPlan pl = build_cr_plan((int)Lx, (int)Ly, BP, Dcol, side && dwh::cr_supported_side(BP), (int)nbatch,
+                                  256, inv0 && dwh::cr_supported_inv0(BP));
+  std::vector<int> written(pl.nblk, -1);   // stage of the first write; -2: ready from the start
+  for (int b = 0; b < 3 * (int)Ly && b < pl.nblk; ++b) written[b] = -2;
+  for (int r : pl.inv0_r) written[r] = -2;
+  int64_t nside = 0, ninv = 0, ngemm = 0, ntask = 0;
+  char buf[256];
+  for (int si = 0; si < (int)pl.stages.size(); ++si) {
+    const CrStage& st = pl.stages[si];
+    std::vector<std::pair<int, int>> rd;   // (block, task id or -1)
+    std::vector<std::pair<int, int>> wr;
+    // ids: task k -> k (its accumulate input may be its output), its
+    // operands -> k + 2^20 (never its output); inversion entry k -> -1 - k
+    // (in place: reads and writes its own block)
+    auto add_task = [&](const dwh::CrTask& t, int id) {
+      for (int h = 0; h < t.nt; ++h) {
+        rd.push_back({t.a[h], id + (1 << 20)});
+        rd.push_back({t.b[h], id + (1 << 20)});
+      }
+      if (t.cin >= 0) rd.push_back({t.cin, id});
+      wr.push_back({t.out, id});
+    };
+    if (st.kind == 0) {
+      ++ninv;
+      for (int k = 0; k < st.n; ++k) {
+        rd.push_back({pl.inv_blk[st.first + k], -1 - k});
+        wr.push_back({pl.inv_dst[st.first + k], -1 - k});
+      }
+      if (st.ntiles > 0) ++nside;
+      for (int k = 0; k < st.ntiles; ++k) add_task(pl.tasks[st.tfirst + k], k);
+    } else {
+      ++ngemm;
+      for (int k = 0; k < st.n; ++k) add_task(pl.tasks[st.first + k], k);
+    }
+    ntask += (int64_t)wr.size();
+    for (const auto& r : rd) {
+      if (r.first < 0 || r.first >= pl.nblk || written[r.first] == -1) {
+        std::snprintf(buf, sizeof buf, "stage %d reads block %d before any stage writes it", si, r.first);
+        return fail(nullptr, DWH_ERR_STATE, buf);
+      }
+      for (const auto& w : wr)
+        if (w.first == r.first && w.second != r.second) {
+          std::snprintf(buf, sizeof buf, "stage %d reads block %d that the same stage writes", si, r.first);
+          return fail(nullptr, DWH_ERR_STATE, buf);
+        }
+    }
+    for (size_t i = 0; i < wr.size(); ++i)
+      for (size_t j = i + 1; j < wr.size(); ++j)
+        if (wr[i].first == wr[j].first && wr[i].second != wr[j].second) {
+          std::snprintf(buf, sizeof buf, "stage %d writes block %d from two tasks", si, wr[i].first);
+          return fail(nullptr, DWH_ERR_STATE, buf);
+        }
+    for (const auto& w : wr)
+      if (w.first >= 0 && w.first < pl.nblk && written[w.first] == -1) written[w.first] = si;
+  }
+  const int64_t BB = (int64_t)(BP / 2) * BP;
+  for (int64_t o : pl.goff)
+    if (o >= 0 && written[o / BB] == -1) return fail(nullptr, DWH_ERR_STATE, "force gather reads an unwritten block");
+  for (int64_t o : pl.doff)
+    if (written[o / BB] == -1) return fail(nullptr, DWH_ERR_STATE, "E_f gather reads an unwritten block");
+  if (stats) {
+    stats[0] = (int64_t)pl.stages.size();
+    stats[1] = ninv;
+    stats[2] = nside;
+    stats[3] = ngemm;
+    stats[4] = ntask;
+    stats[5] = pl.nblk;
+  }
+  return DWH_OK;
+}
+
 // ---- assembly read-back (parity tests of init_static_H! / update_H_BdG!) ----
 
 int dwh_debug_dense_H(dwh_ctx* ctx, int64_t chain, dwh_c128* H) {

@@ -224,6 +224,19 @@ int dwh_measure_transport_batched(dwh_ctx* ctx, double eta, double domega, doubl
 int dwh_debug_dense_H(dwh_ctx* ctx, int64_t chain, dwh_c128* H);
 int dwh_debug_level0(dwh_ctx* ctx, int64_t chain, int64_t pole, int32_t refill, dwh_c128* M, double* y);
 
+/* Host-only check of the cyclic-reduction schedule dwh_create builds for an
+ * Lx x Ly periodic lattice with nearest-neighbour pairing and nbatch = chains x
+ * poles batch items (side / inv0: enable the side-work placement and the
+ * static level-0 particle blocks, as dwh_create does where the block size
+ * supports them): every block a stage reads was written by an earlier stage
+ * (or is a level-0 / static block), no stage reads what it writes except a
+ * task's own accumulate input, no block is written by two tasks of one stage,
+ * and the force / E_f gathers read written blocks.  No device is touched.
+ * stats (nullable, 6): stages, inversion stages, inversion stages with side
+ * work, product stages, writes, pool blocks.  DWH_ERR_STATE with the first
+ * violation in dwh_last_error(NULL). */
+int dwh_debug_cr_plan_check(int64_t Lx, int64_t Ly, int64_t nbatch, int32_t side, int32_t inv0, int64_t* stats);
+
 /* Self-test of the f64 MFMA fragment layout (A = I, asymmetric B); 0 = pass. */
 int dwh_selftest_mfma(int32_t device);
 

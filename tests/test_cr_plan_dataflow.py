@@ -1,0 +1,51 @@
+"""CPU check of the cyclic-reduction schedule the C ABI builds (no device):
+dwh_debug_cr_plan_check builds the plan dwh_create would and verifies its
+dataflow -- every block a launch reads was written by an earlier launch (or
+is a level-0 / static block), no launch reads a block it writes (other than a
+task's own accumulate input or an in-place inversion), no two tasks of one
+launch write the same block, and the force / E_f gathers read written blocks.
+This is what the side-work placement (products run inside later inversion
+launches) must respect; a schedule that read U'/L' in the launch producing
+them would fail here before it could race on the GPU."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+LATTICES = [(4, 1), (4, 2), (3, 3), (5, 7), (8, 8), (6, 9), (17, 4), (20, 6), (32, 2), (32, 3), (32, 5),
+            (32, 16), (32, 31), (32, 32), (32, 33), (40, 3), (48, 12), (64, 2), (64, 9)]
+
+
+def check(lib, Lx, Ly, nbatch, side, inv0):
+    stats = np.zeros(6, dtype=np.int64)
+    rc = lib.dwh_debug_cr_plan_check(Lx, Ly, nbatch, side, inv0, stats.ctypes.data_as(C.c_void_p))
+    return rc, stats, lib.dwh_last_error(None).decode()
+
+
+@pytest.mark.parametrize("Lx,Ly", LATTICES)
+@pytest.mark.parametrize("nbatch", [14, 56])
+def test_cr_schedule_dataflow(dwhmc, Lx, Ly, nbatch):
+    lib = dwhmc.load_library()
+    for side in (0, 1):
+        for inv0 in (0, 1):
+            rc, stats, err = check(lib, Lx, Ly, nbatch, side, inv0)
+            assert rc == 0, (Lx, Ly, nbatch, side, inv0, err)
+            assert stats[0] == stats[1] + stats[3] and stats[1] >= 1
+
+
+def test_cr_schedule_c3_shape(dwhmc):
+    """The C3 plan (L = 32, 14 poles): 6 inversion launches, 5 of them with
+    side work, 20 product launches."""
+    lib = dwhmc.load_library()
+    rc, stats, err = check(lib, 32, 32, 14, 1, 1)
+    assert rc == 0, err
+    assert list(stats[:4]) == [26, 6, 5, 20]
+    rc, stats, err = check(lib, 32, 32, 14, 0, 1)
+    assert rc == 0, err
+    assert list(stats[:4]) == [26, 6, 0, 20]
+
+
+def test_cr_schedule_rejects_wide_rows(dwhmc):
+    lib = dwhmc.load_library()
+    rc, _, err = check(lib, 65, 4, 14, 1, 1)
+    assert rc != 0 and "too wide" in err
