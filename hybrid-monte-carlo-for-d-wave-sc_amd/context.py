@@ -37,8 +37,9 @@ def table_to_abi(table: np.ndarray) -> np.ndarray:
 
 
 # factorisation algorithm (include/dwhmc.h DWH_ALGO_*): "auto" = env DWHMC_ALGO,
-# else block cyclic reduction when 2 Lx <= 128
-ALGOS = {"auto": -1, "dense": 0, "cr": 1}
+# else block cyclic reduction when 2 Lx <= 128, eigendecomposition ("eig") when
+# β·E'/2 is beyond the pole table
+ALGOS = {"auto": -1, "dense": 0, "cr": 1, "eig": 2}
 
 
 class FermionContext:

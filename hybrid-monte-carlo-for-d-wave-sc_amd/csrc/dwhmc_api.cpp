@@ -5,7 +5,9 @@
 //     upper-triangle overwrite order        (src/Hamiltonian.jl:10-47)
 //   * pairing pattern D[r, c] <- Δ[src]/2 with the reference's overwrite order
 //                                            (src/Hamiltonian.jl:55-86)
-//   * pole selection from the compiled table for κ = β E'/2
+//   * pole selection from the compiled table for κ = β E'/2; beyond the
+//     table the eigendecomposition path (algo eig: rocSOLVER zheevd per step,
+//     the reference's own diagonalize + compute_forces!)
 //   * the per-sweep launch sequence of hmc_sweep! (src/HMC.jl:71-144)
 // All arithmetic runs in the HIP kernels (dwhmc_kernels.hip); there is no CPU
 // fallback: a missing device is an error.
@@ -18,6 +20,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <map>
 #include <string>
 #include <utility>
@@ -44,7 +47,7 @@ const char* kTimerNames[T_COUNT] = {"gj_update", "gj_pivot", "assemble", "contra
                                     "step",      "gj_edge",  "cr_gemm",  "cr_inv",
                                     "cr_inv_side"};
 
-enum Algo { ALGO_DENSE = 0, ALGO_CR = 1 };
+enum Algo { ALGO_DENSE = 0, ALGO_CR = 1, ALGO_EIG = 2 };
 
 // One stage of the cyclic-reduction plan: a batch of block inversions or a
 // task list of block products (all batch items at once).
@@ -530,6 +533,7 @@ struct dwh_ctx {
   // other path that changes Δ leaves it false
   bool pairing_in_pool = false;
   bool pending = false;    // dwh_hmc_trajectory done, dwh_hmc_finish not yet
+  int async_rc = 0;        // eig path: a rocSOLVER / rocBLAS call refused while enqueuing
 
   // transport / spectra measurement (device side allocated on first use): host
   // copies of the x-current operator J (CSR of its imaginary parts, duplicates
@@ -541,6 +545,7 @@ struct dwh_ctx {
   rocblas_handle blas = nullptr;
   dwh::TrBufs tr{};
   int *d_tr_nbr = nullptr, *d_tr_rowptr = nullptr, *d_tr_col = nullptr, *d_tr_info = nullptr;
+  int* d_tr_bad = nullptr;   // eigen_solve: non-finite E / U after zheevd
   double* d_tr_val = nullptr;
   double* d_tr_offd = nullptr;   // zheevd off-diagonal workspace (2N)
   int64_t tr_nw = -1, tr_nd = -1;   // ω / DOS grid lengths the output buffers hold
@@ -747,10 +752,58 @@ dwh::KickDrift kickdrift(dwh_ctx* ctx, double kick, double drift) {
   return dwh::KickDrift{kick, drift, ctx->delta_cap, ctx->flag};
 }
 
+int transport_prepare(dwh_ctx* ctx, int64_t nw, int64_t nd, int slots);
+int eigen_solve(dwh_ctx* ctx, int64_t c0, int m);
+int eigen_info_check(dwh_ctx* ctx, int m);
+
+// algo eig: zheevd of every chain's H_BdG (src/Hamiltonian.jl:96-114), ρ =
+// U diag(f) U^H by one batched zgemm, then P, Tr ρ_hh and E_f
+// (src/Observables.jl:14-62, src/HMC.jl:21-27) in k_eig_gather
+void eig_enqueue(dwh_ctx* ctx) {
+  const int N = ctx->d.N, n2 = 2 * N, nc = ctx->d.nc;
+  if (int rc = eigen_solve(ctx, 0, nc)) {
+    ctx->async_rc = rc;
+    return;
+  }
+  const dwh::TrBufs& b = ctx->tr;
+  dwh::launch_eig_scale(b.U, b.JU, b.E, N, nc, ctx->beta, ctx->stream);
+  const rocblas_double_complex one(1.0, 0.0), zero(0.0, 0.0);
+  const int64_t sA = (int64_t)n2 * n2;
+  const rocblas_status st = rocblas_zgemm_strided_batched(
+      ctx->blas, rocblas_operation_none, rocblas_operation_conjugate_transpose, n2, n2, n2, &one,
+      reinterpret_cast<const rocblas_double_complex*>(b.JU), n2, sA,
+      reinterpret_cast<const rocblas_double_complex*>(b.U), n2, sA, &zero,
+      reinterpret_cast<rocblas_double_complex*>(b.Jmn), n2, sA, nc);
+  if (st != rocblas_status_success) {
+    ctx->async_rc = fail(ctx, DWH_ERR_HIP, std::string("rocblas_zgemm: ") + rocblas_status_to_string(st));
+    return;
+  }
+  dwh::launch_eig_gather(b.Jmn, b.E, N, nc, ctx->Dcol, ctx->bond_ij, ctx->beta, ctx->Pair, ctx->Ef, ctx->Trhh,
+                         ctx->stream);
+}
+
+// eig path, after a stream synchronisation: an enqueue-time refusal, then
+// zheevd's convergence flags
+int eig_check(dwh_ctx* ctx) {
+  if (ctx->algo != ALGO_EIG) return DWH_OK;
+  if (ctx->async_rc != DWH_OK) {
+    const int rc = ctx->async_rc;
+    ctx->async_rc = DWH_OK;
+    return rc;
+  }
+  return eigen_info_check(ctx, ctx->d.nc);
+}
+
 // assemble -> factorisation -> P -> F (+ kick / next drift); E_f separately
 void factorize_enqueue(dwh_ctx* ctx, const dwh::KickDrift& kd) {
   const Dims& d = ctx->d;
   Scope step(ctx, T_STEP, (double)d.nbatch * 8.0 * (double)d.N * d.N * d.N);
+  if (ctx->algo == ALGO_EIG) {
+    // E_f and Tr ρ_hh come with every decomposition (k_eig_gather)
+    eig_enqueue(ctx);
+    dwh::launch_force_from_pair(d, ctx->Pair, ctx->Delta, ctx->F, ctx->Pi, kd, ctx->beta, ctx->J, ctx->stream);
+    return;
+  }
   if (ctx->algo == ALGO_CR) {
     cr_enqueue(ctx);
     // the kernel scatters the drifted Δ into the pool only when it drifts
@@ -779,6 +832,7 @@ void factorize_enqueue(dwh_ctx* ctx, const dwh::KickDrift& kd) {
 }
 
 void fermion_energy_enqueue(dwh_ctx* ctx) {
+  if (ctx->algo == ALGO_EIG) return;   // written by k_eig_gather with P
   if (ctx->algo == ALGO_CR)
     dwh::launch_cr_fermion_energy(ctx->cr, ctx->bpool, ctx->d_doff, ctx->ldpart, ctx->d_c, ctx->Cx,
                                   ctx->beta, ctx->efpart, ctx->efdone, ctx->Ef, ctx->Trhh, ctx->stream);
@@ -1067,27 +1121,42 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
   }
   const double Eb = hmax + 2.0 * delta_cap;
   const double kneed = 0.5 * beta * Eb;
+  // algorithm: explicit request, else DWHMC_ALGO = dense | cr | eig | auto
+  // (auto: cr when the lattice-row block 2 Lx fits a supported padded size,
+  // else dense; eig when κ = β E'/2 is beyond the pole table)
+  std::string want = "auto";
+  if (algo_req == DWH_ALGO_DENSE) want = "dense";
+  else if (algo_req == DWH_ALGO_CR) want = "cr";
+  else if (algo_req == DWH_ALGO_EIG) want = "eig";
+  else if (const char* e = std::getenv("DWHMC_ALGO")) want = e;
+  if (want != "auto" && want != "dense" && want != "cr" && want != "eig")
+    return fail(nullptr, DWH_ERR_ARG, "DWHMC_ALGO must be auto, dense, cr or eig");
   int sel = -1;
   for (int e = 0; e < kPoleTableSize; ++e)
     if (kPoleEntries[e].kappa >= kneed * (1.0 - 1e-12)) {
       sel = e;
       break;
     }
-  if (sel < 0) {
+  if (sel < 0 && want == "auto") want = "eig";
+  if (sel < 0 && want != "eig") {
     char buf[256];
     std::snprintf(buf, sizeof buf, "beta*E_bound/2 = %g exceeds the pole table (max kappa %g)", kneed,
                   kPoleEntries[kPoleTableSize - 1].kappa);
     return fail(nullptr, DWH_ERR_TABLE, buf);
   }
-  const PoleEntry& pe = kPoleEntries[sel];
-  const double kappa = pe.kappa;
-  const double Ep = 2.0 * kappa / beta;
-  std::vector<double> y(pe.m), cq(pe.m);
+  const bool eig = want == "eig";
+  // the eigen path is exact for any Δ: no pole set, no |Δ| guard
+  if (eig) delta_cap = std::numeric_limits<double>::max();
+  const PoleEntry* pe = eig ? nullptr : &kPoleEntries[sel];
+  const double kappa = eig ? kneed : pe->kappa;
+  const double Ep = eig ? Eb : 2.0 * kappa / beta;
+  const int npole = eig ? 1 : pe->m;   // eig: one dummy batch item per chain
+  std::vector<double> y(npole, 0.0), cq(npole, 0.0);
   double suma = 0;
-  for (int q = 0; q < pe.m; ++q) {
-    y[q] = Ep * std::sqrt(kPoleT[pe.off + q]);
-    cq[q] = 0.5 * kPoleA[pe.off + q] * Ep;
-    suma += kPoleA[pe.off + q];
+  for (int q = 0; q < (eig ? 0 : npole); ++q) {
+    y[q] = Ep * std::sqrt(kPoleT[pe->off + q]);
+    cq[q] = 0.5 * kPoleA[pe->off + q] * Ep;
+    suma += kPoleA[pe->off + q];
   }
 
   dwh_ctx* ctx = new dwh_ctx();
@@ -1131,8 +1200,8 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
   ctx->kappa = kappa;
   ctx->Ebound = Ep;
   ctx->hmax = hmax;
-  ctx->err_tanh = pe.err_tanh;
-  ctx->Cx = pe.C_u - kappa * std::log(Ep) * suma;
+  ctx->err_tanh = eig ? 0.0 : pe->err_tanh;
+  ctx->Cx = eig ? 0.0 : pe->C_u - kappa * std::log(Ep) * suma;
   ctx->y = y;
   ctx->cq = cq;
   Dims& d = ctx->d;
@@ -1140,24 +1209,12 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
   d.Np = ((N + kGJ - 1) / kGJ) * kGJ;
   d.nb = d.Np / kGJ;
   d.nc = (int)nchains;
-  d.P = pe.m;
+  d.P = npole;
   d.nbatch = d.nc * d.P;
   d.mat = (int64_t)d.Np * d.Np;
   d.nld = d.nb;
-  // algorithm: explicit request, else DWHMC_ALGO = dense | cr | auto (default:
-  // cr when the lattice-row block 2 Lx fits a supported padded size)
   {
     const int BP = (int)(2 * ((Lx + 15) / 16 * 16));   // top halves HP x BP, HP = Lx rounded to 16
-    std::string want = "auto";
-    if (algo_req == DWH_ALGO_DENSE) want = "dense";
-    else if (algo_req == DWH_ALGO_CR) want = "cr";
-    else if (const char* e = std::getenv("DWHMC_ALGO")) want = e;
-    if (want != "auto" && want != "dense" && want != "cr") {
-      ctx->err = "DWHMC_ALGO must be auto, dense or cr";
-      g_create_error = ctx->err;
-      delete ctx;
-      return DWH_ERR_ARG;
-    }
     const bool ok = dwh::cr_supported_bp(BP);
     if (want == "cr" && !ok) {
       ctx->err = "DWHMC_ALGO=cr needs 2*Lx <= 128";
@@ -1165,7 +1222,7 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
       delete ctx;
       return DWH_ERR_ARG;
     }
-    ctx->algo = (want == "dense" || !ok) ? ALGO_DENSE : ALGO_CR;
+    ctx->algo = eig ? ALGO_EIG : (want == "dense" || !ok) ? ALGO_DENSE : ALGO_CR;
     if (ctx->algo == ALGO_CR) {
       // DWHMC_CR_SIDE=0: every product on its own stage (A/B runs, tests)
       const char* es = std::getenv("DWHMC_CR_SIDE");
@@ -1233,7 +1290,7 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     ALLOC(XR2, npanel);
     ALLOC(Pb1, (size_t)d.nbatch * kGJ * kGJ);
     ALLOC(Pb2, (size_t)d.nbatch * kGJ * kGJ);
-  } else {
+  } else if (ctx->algo == ALGO_CR) {
     const CrPlan& pl = ctx->plan;
     ALLOC(bpool, (size_t)d.nbatch * ctx->cr.item);
     ALLOC(d_tasks, pl.tasks.size());
@@ -1330,7 +1387,7 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     dwh::launch_fill_hz(d, ctx->R, ctx->hcol, ctx->hval, ctx->d_y, s);
     run_gj(ctx, ctx->R);
     dwh::launch_sum_ld(d, ctx->ldpart, ctx->ldstatic, s);
-  } else {
+  } else if (ctx->algo == ALGO_CR) {
     // the CR path factorises the whole BdG matrix: no static part; every
     // level-0 block written once (pairing entries 0 until the first factorize)
     (void)hipMemsetAsync(ctx->ldstatic, 0, d.nbatch * sizeof(double), s);
@@ -1348,6 +1405,8 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     ctx->err = "static R initialisation failed on the device";
     return bail(DWH_ERR_HIP);
   }
+  // eig: rocBLAS handle and the per-chain U, JU (= U diag f), ρ, E buffers
+  if (ctx->algo == ALGO_EIG && (rc = transport_prepare(ctx, 0, 0, d.nc)) != DWH_OK) return bail(rc);
   *out = ctx;
   return DWH_OK;
 }
@@ -1389,7 +1448,7 @@ int transport_prepare(dwh_ctx* ctx, int64_t nw, int64_t nd, int slots) {
     if ((rc = dalloc(ctx, &ctx->d_tr_nbr, ctx->tr_nbr.size())) ||
         (rc = dalloc(ctx, &ctx->d_tr_rowptr, ctx->tr_rowptr.size())) ||
         (rc = dalloc(ctx, &ctx->d_tr_col, ctx->tr_col.size())) ||
-        (rc = dalloc(ctx, &ctx->d_tr_val, ctx->tr_val.size())))
+        (rc = dalloc(ctx, &ctx->d_tr_val, ctx->tr_val.size())) || (rc = dalloc(ctx, &ctx->d_tr_bad, 1)))
       return rc;
     auto up = [&](void* dst, const void* src, size_t bytes) {
       return bytes == 0 ? hipSuccess : hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream);
@@ -1463,7 +1522,7 @@ dwh::TrBufs tr_slot(const dwh_ctx* ctx, int k) {
 // chain at once): eigenvalues ascending into E, eigenvectors into the columns
 // of U (diagonalize_H_BdG!, src/Hamiltonian.jl:96-114; the reference's zheevr
 // and zheevd agree to rounding)
-int eigen_enqueue(dwh_ctx* ctx, int64_t c0, int m) {
+int eigen_enqueue(dwh_ctx* ctx, int64_t c0, int m, bool qr) {
   const int N = ctx->d.N, n2 = 2 * N;
   const dwh::TrBufs& b = ctx->tr;
   const int64_t sA = (int64_t)n2 * n2;
@@ -1473,14 +1532,40 @@ int eigen_enqueue(dwh_ctx* ctx, int64_t c0, int m) {
                             ctx->Dcol, ctx->Dsrc, ctx->Delta + (size_t)(c0 + k) * 2 * N, ctx->stream);
   HIPCHECK(ctx, hipGetLastError());
   auto* A = reinterpret_cast<rocblas_double_complex*>(b.U);
-  const rocblas_status st =
-      m == 1 ? rocsolver_zheevd(ctx->blas, rocblas_evect_original, rocblas_fill_upper, n2, A, n2, b.E,
-                                ctx->d_tr_offd, ctx->d_tr_info)
-             : rocsolver_zheevd_strided_batched(ctx->blas, rocblas_evect_original, rocblas_fill_upper, n2, A,
-                                                n2, sA, b.E, n2, ctx->d_tr_offd, n2, ctx->d_tr_info, m);
+  rocblas_status st;
+  if (qr)
+    st = m == 1 ? rocsolver_zheev(ctx->blas, rocblas_evect_original, rocblas_fill_upper, n2, A, n2, b.E,
+                                  ctx->d_tr_offd, ctx->d_tr_info)
+                : rocsolver_zheev_strided_batched(ctx->blas, rocblas_evect_original, rocblas_fill_upper, n2, A, n2,
+                                                  sA, b.E, n2, ctx->d_tr_offd, n2, ctx->d_tr_info, m);
+  else
+    st = m == 1 ? rocsolver_zheevd(ctx->blas, rocblas_evect_original, rocblas_fill_upper, n2, A, n2, b.E,
+                                   ctx->d_tr_offd, ctx->d_tr_info)
+                : rocsolver_zheevd_strided_batched(ctx->blas, rocblas_evect_original, rocblas_fill_upper, n2, A,
+                                                   n2, sA, b.E, n2, ctx->d_tr_offd, n2, ctx->d_tr_info, m);
   if (st != rocblas_status_success)
     return fail(ctx, DWH_ERR_HIP, std::string("rocsolver_zheevd: ") + rocblas_status_to_string(st));
   return DWH_OK;
+}
+
+// eigen_enqueue with the divide-and-conquer zheevd, then a scan of E and U for
+// non-finite values: rocSOLVER's zheevd returns NaN eigenvectors for spectra
+// with exactly degenerate eigenvalues (the clean lattice, W = 0), so those
+// chains are decomposed again with the QR-iteration zheev (slower, robust).
+// Synchronises the stream.  DWHMC_EIG_SOLVER=ev: zheev from the start.
+int eigen_solve(dwh_ctx* ctx, int64_t c0, int m) {
+  const char* es = std::getenv("DWHMC_EIG_SOLVER");
+  const bool qr = es && std::strcmp(es, "ev") == 0;
+  int rc = eigen_enqueue(ctx, c0, m, qr);
+  if (rc || qr) return rc;
+  const int64_t n2 = 2 * (int64_t)ctx->d.N;
+  HIPCHECK(ctx, hipMemsetAsync(ctx->d_tr_bad, 0, sizeof(int), ctx->stream));
+  dwh::launch_nonfinite(ctx->tr.U, m * n2 * n2, ctx->tr.E, m * n2, ctx->d_tr_bad, ctx->stream);
+  int bad = 0;
+  HIPCHECK(ctx, hipMemcpyAsync(&bad, ctx->d_tr_bad, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+  if (bad) rc = eigen_enqueue(ctx, c0, m, true);
+  return rc;
 }
 
 int eigen_info_check(dwh_ctx* ctx, int m) {
@@ -1512,7 +1597,7 @@ int transport_run(dwh_ctx* ctx, int64_t c0, int m, double eta, double domega, do
                   double* ak0) {
   int rc;
   if ((rc = transport_prepare(ctx, nw, nd, m))) return rc;
-  if ((rc = eigen_enqueue(ctx, c0, m))) return rc;
+  if ((rc = eigen_solve(ctx, c0, m))) return rc;
   const int N = ctx->d.N, n2 = 2 * N;
   const int64_t sA = (int64_t)n2 * n2;
   hipStream_t s = ctx->stream;
@@ -1576,7 +1661,7 @@ int dwh_eigensystem(dwh_ctx* ctx, int64_t chain, double* E, dwh_c128* U) {
   int rc;
   if ((rc = transport_prepare(ctx, std::max<int64_t>(ctx->tr_nw, 0), std::max<int64_t>(ctx->tr_nd, 0), 1)))
     return rc;
-  if ((rc = eigen_enqueue(ctx, chain, 1))) return rc;
+  if ((rc = eigen_solve(ctx, chain, 1))) return rc;
   const size_t n2 = 2 * (size_t)ctx->d.N;
   HIPCHECK(ctx, hipMemcpyAsync(E, ctx->tr.E, n2 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
   if (U)
@@ -1639,8 +1724,8 @@ int dwh_create_batched(dwh_ctx** ctx, int64_t Lx, int64_t Ly, double t, double t
 int dwh_create_ex(dwh_ctx** ctx, int64_t Lx, int64_t Ly, double t, double tp, double mu, double beta,
                   double J, const int64_t* nn_table, const int64_t* nnn_table, int64_t nchains,
                   const double* disorder, double delta_cap, int32_t algo, int32_t device) {
-  if (algo != DWH_ALGO_AUTO && algo != DWH_ALGO_DENSE && algo != DWH_ALGO_CR)
-    return fail(nullptr, DWH_ERR_ARG, "algo must be DWH_ALGO_AUTO, DWH_ALGO_DENSE or DWH_ALGO_CR");
+  if (algo != DWH_ALGO_AUTO && algo != DWH_ALGO_DENSE && algo != DWH_ALGO_CR && algo != DWH_ALGO_EIG)
+    return fail(nullptr, DWH_ERR_ARG, "algo must be DWH_ALGO_AUTO, DWH_ALGO_DENSE, DWH_ALGO_CR or DWH_ALGO_EIG");
   return create_impl(ctx, Lx, Ly, t, tp, mu, beta, J, nn_table, nnn_table, nchains, disorder,
                      delta_cap, algo, device);
 }
@@ -1669,14 +1754,14 @@ int dwh_info(dwh_ctx* ctx, dwh_info_t* out) {
   out->N = ctx->d.N;
   out->Np = ctx->d.Np;
   out->nchains = ctx->d.nc;
-  out->npoles = ctx->d.P;
+  out->npoles = ctx->algo == ALGO_EIG ? 0 : ctx->d.P;
   out->kappa = ctx->kappa;
   out->e_bound = ctx->Ebound;
   out->err_tanh = ctx->err_tanh;
   out->delta_cap = ctx->delta_cap;
   out->device_bytes = ctx->device_bytes;
   out->algo = ctx->algo;
-  out->block = ctx->algo == ALGO_CR ? ctx->cr.BP : kGJ;
+  out->block = ctx->algo == ALGO_CR ? ctx->cr.BP : ctx->algo == ALGO_EIG ? 0 : kGJ;
   return DWH_OK;
 }
 
@@ -1688,10 +1773,14 @@ namespace {
 // carry over.  The context is left unfactorised.
 int reselect_poles(dwh_ctx* ctx, double new_cap) {
   dwh_ctx* n = nullptr;
-  const int32_t algo = ctx->algo == ALGO_CR ? DWH_ALGO_CR : DWH_ALGO_DENSE;
+  const int32_t algo = ctx->algo == ALGO_CR ? DWH_ALGO_CR : ctx->algo == ALGO_EIG ? DWH_ALGO_EIG : DWH_ALGO_DENSE;
   int rc = create_impl(&n, ctx->Lx, ctx->Ly, ctx->t, ctx->tp, ctx->mu, ctx->beta, ctx->J,
                        ctx->nn_host.data(), ctx->nnn_host.data(), ctx->d.nc, ctx->dis_host.data(), new_cap,
                        algo, ctx->device);
+  // a spectral bound beyond the pole table: the eigendecomposition path
+  if (rc == DWH_ERR_TABLE)
+    rc = create_impl(&n, ctx->Lx, ctx->Ly, ctx->t, ctx->tp, ctx->mu, ctx->beta, ctx->J, ctx->nn_host.data(),
+                     ctx->nnn_host.data(), ctx->d.nc, ctx->dis_host.data(), new_cap, DWH_ALGO_EIG, ctx->device);
   if (rc != DWH_OK)
     return fail(ctx, rc, "pole re-selection for delta_cap=" + std::to_string(new_cap) + ": " + g_create_error);
   const size_t nb = (size_t)ctx->d.nc * 2 * ctx->d.N * sizeof(double2);
@@ -1797,6 +1886,7 @@ int dwh_factorize(dwh_ctx* ctx) {
   fermion_energy_enqueue(ctx);
   HIPCHECK(ctx, hipGetLastError());
   HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+  if (int rc = eig_check(ctx)) return rc;
   ctx->factorized = true;
   drain_timing(ctx);
   return DWH_OK;
@@ -1896,6 +1986,7 @@ int dwh_hmc_sweep(dwh_ctx* ctx, const dwh_c128* noise, const double* uniform, in
     HIPCHECK(ctx, hipMemcpyAsync(accepted, ctx->s_acc, d.nc, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHECK(ctx, hipMemcpyAsync(dH, ctx->s_dH, d.nc * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+    if (int rc = eig_check(ctx)) return rc;
     if (Nt > 0) ctx->factorized = true;
     drain_timing(ctx);
     int f = 0;
@@ -1925,6 +2016,7 @@ int dwh_hmc_trajectory(dwh_ctx* ctx, const dwh_c128* noise, int64_t Nt, double d
     HIPCHECK(ctx, hipGetLastError());
     HIPCHECK(ctx, hipMemcpyAsync(dH, ctx->s_dH, d.nc * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+    if (int rc = eig_check(ctx)) return rc;
     if (Nt > 0) ctx->factorized = true;
     drain_timing(ctx);
     int f = 0;
@@ -2032,6 +2124,7 @@ int dwh_sweep_results(dwh_ctx* ctx, int64_t first, int64_t nsweeps, uint8_t* acc
     HIPCHECK(ctx, hipMemcpyAsync(dH, ctx->dH + nc * first, nc * nsweeps * sizeof(double),
                                  hipMemcpyDeviceToHost, ctx->stream));
   HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+  if (int rc = eig_check(ctx)) return rc;
   return check_flag(ctx);
 }
 

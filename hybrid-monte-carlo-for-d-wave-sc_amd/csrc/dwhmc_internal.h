@@ -201,6 +201,16 @@ void launch_tr_current(const double2* U, double2* JU, int N, const int* rowptr, 
 void launch_tr_reduce(const TrBufs& b, int N, int Lx, int Ly, double beta, double eta,
                       const TrGrid& g, hipStream_t s);
 
+// Eigendecomposition leapfrog step (algo eig; U, JU, rho: nc chains of n2 x n2
+// column-major, E: nc x n2): JU = U diag(logistic(-β E)); after rho = JU U^H,
+// P at the bonds, Tr ρ_hh and E_f per chain
+void launch_eig_scale(const double2* U, double2* JU, const double* E, int N, int nc, double beta, hipStream_t s);
+void launch_eig_gather(const double2* rho, const double* E, int N, int nc, const int* Dcol, const int* bond_ij,
+                       double beta, double2* Pair, double* Ef, double* Trhh, hipStream_t s);
+
+// *bad = 1 when any entry of U (nu complex) or E (ne real) is not finite
+void launch_nonfinite(const double2* U, int64_t nu, const double* E, int64_t ne, int* bad, hipStream_t s);
+
 int selftest_mfma_layout(int device);
 
 }  // namespace dwh

@@ -3,7 +3,7 @@
 //
 // This is the measurement path the reference runs every measure_transport_freq
 // sweeps (src/Simulation.jl:170-186), not the leapfrog hot path: the
-// eigenpairs come from rocSOLVER zheevd and J_mn = U^H (J ⊕ J) U from rocBLAS
+// eigenpairs come from rocSOLVER zheevd (zheev where it fails) and J_mn = U^H (J ⊕ J) U from rocBLAS
 // zgemm (dwhmc_api.cpp drives both); the kernels here are everything around
 // them.  All matrices are column-major with leading dimension n2 = 2N (the
 // eigenvector of E_n is column n of U, as Julia's eigen! returns it).
@@ -337,9 +337,85 @@ __global__ void k_tr_ak_sum(const double* __restrict__ part, int nsl, int N, dou
   ak[k] = s / N;
 }
 
+// ---------------------------------------------------------------------------
+// Eigendecomposition leapfrog step (algo eig): the reference's own method —
+// diagonalize_H_BdG! (src/Hamiltonian.jl:96-114), compute_forces!
+// (src/Observables.jl:14-62) and the E_f of compute_total_energy
+// (src/HMC.jl:21-27) — for β·E'/2 beyond the pole table.  zheevd gives E, U
+// per chain; ρ = U diag(f) U^H is one zgemm of JU = U diag(f) with U^H; the
+// kernels here form JU and gather P_ij = -ρ_{i,j+N} - ρ_{j,i+N}, Tr ρ_hh and E_f.
+// ---------------------------------------------------------------------------
+__global__ void k_eig_scale(const double2* __restrict__ U, double2* __restrict__ JU, const double* __restrict__ E,
+                            int n2, double beta) {
+  const int a = blockIdx.x * kTB + threadIdx.x;
+  const int n = blockIdx.y, k = blockIdx.z;
+  if (a >= n2) return;
+  const double f = logistic_d(-beta * E[(int64_t)k * n2 + n]);
+  const int64_t o = ((int64_t)k * n2 + n) * n2 + a;
+  const double2 u = U[o];
+  JU[o] = make_double2(u.x * f, u.y * f);
+}
+
+// one block per chain; bond b = i + N·dir with partner j = Dcol[bond_ij[b]]
+__global__ void k_eig_gather(const double2* __restrict__ rho, const double* __restrict__ E, int N,
+                             const int* __restrict__ Dcol, const int* __restrict__ bond_ij, double beta,
+                             double2* __restrict__ Pair, double* __restrict__ Ef, double* __restrict__ Trhh) {
+  __shared__ double sh[2][kTB];
+  const int c = blockIdx.x, n2 = 2 * N;
+  const double2* R = rho + (int64_t)c * n2 * n2;
+  for (int b = threadIdx.x; b < n2; b += kTB) {
+    const int i = b < N ? b : b - N;
+    const int j = Dcol[bond_ij[b]];
+    const double2 r1 = R[i + (int64_t)(j + N) * n2], r2 = R[j + (int64_t)(i + N) * n2];
+    Pair[(int64_t)c * n2 + b] = make_double2(-(r1.x + r2.x), -(r1.y + r2.y));
+  }
+  double v[2] = {0.0, 0.0};
+  for (int i = threadIdx.x; i < N; i += kTB) v[0] += R[(i + N) + (int64_t)(i + N) * n2].x;
+  for (int n = threadIdx.x; n < n2; n += kTB) {
+    const double e = E[(int64_t)c * n2 + n];
+    if (e > 0) {
+      const double x = beta * e;
+      v[1] += x + 2.0 * log1p(exp(-x));
+    }
+  }
+  block_sum<2>(v, sh);
+  if (threadIdx.x == 0) {
+    Trhh[c] = sh[0][0];
+    Ef[c] = -sh[1][0];
+  }
+}
+
+// any non-finite entry of U (nu complex) or E (ne real) -> *bad = 1
+__global__ void k_nonfinite(const double2* __restrict__ U, int64_t nu, const double* __restrict__ E, int64_t ne,
+                            int* __restrict__ bad) {
+  bool nf = false;
+  const int64_t stride = (int64_t)gridDim.x * kTB;
+  for (int64_t k = (int64_t)blockIdx.x * kTB + threadIdx.x; k < nu; k += stride) {
+    const double2 u = U[k];
+    nf |= !isfinite(u.x) || !isfinite(u.y);
+  }
+  for (int64_t k = (int64_t)blockIdx.x * kTB + threadIdx.x; k < ne; k += stride) nf |= !isfinite(E[k]);
+  if (nf) *bad = 1;
+}
+
 inline int cdiv(int64_t a, int b) { return (int)((a + b - 1) / b); }
 
 }  // namespace
+
+void launch_nonfinite(const double2* U, int64_t nu, const double* E, int64_t ne, int* bad, hipStream_t s) {
+  const int64_t n = nu > ne ? nu : ne;
+  const int grid = (int)std::min<int64_t>(std::max<int64_t>(cdiv(n, kTB), 1), 2048);
+  hipLaunchKernelGGL(k_nonfinite, dim3(grid), dim3(kTB), 0, s, U, nu, E, ne, bad);
+}
+
+void launch_eig_scale(const double2* U, double2* JU, const double* E, int N, int nc, double beta, hipStream_t s) {
+  hipLaunchKernelGGL(k_eig_scale, dim3(cdiv(2 * N, kTB), 2 * N, nc), dim3(kTB), 0, s, U, JU, E, 2 * N, beta);
+}
+
+void launch_eig_gather(const double2* rho, const double* E, int N, int nc, const int* Dcol, const int* bond_ij,
+                       double beta, double2* Pair, double* Ef, double* Trhh, hipStream_t s) {
+  hipLaunchKernelGGL(k_eig_gather, dim3(nc), dim3(kTB), 0, s, rho, E, N, Dcol, bond_ij, beta, Pair, Ef, Trhh);
+}
 
 void launch_tr_assemble(double2* A, int N, const int* hcol, const double* hval, const int* Dcol,
                         const int* Dsrc, const double2* Delta, hipStream_t s) {

@@ -37,21 +37,22 @@ enum {
   DWH_ERR_HIP = -2,       /* HIP runtime failure (no device, OOM, launch failure) */
   DWH_ERR_STATE = -3,     /* call out of order */
   DWH_ERR_SPECTRUM = -4,  /* |Δ| left the guarded range the pole set was built for */
-  DWH_ERR_TABLE = -5      /* β·E_bound outside the compiled pole table */
+  DWH_ERR_TABLE = -5      /* β·E_bound outside the pole table with DWH_ALGO_DENSE / _CR requested */
 };
 
 typedef struct {
   int64_t N;          /* sites Lx*Ly */
   int64_t Np;         /* N padded to the 64-row GJ block */
   int64_t nchains;
-  int64_t npoles;     /* imaginary-axis pole pairs = no-pivot LUs per chain per step */
-  double kappa;       /* β·E'/2 of the pole table entry in use */
+  int64_t npoles;     /* imaginary-axis pole pairs = no-pivot LUs per chain per step (eig: 0) */
+  double kappa;       /* β·E'/2 of the pole table entry in use (eig: of the spectral bound) */
   double e_bound;     /* E' : spectral bound the poles are valid on */
-  double err_tanh;    /* sup |tanh - rational| of the table entry */
-  double delta_cap;   /* guard on max|Δ_ij| */
+  double err_tanh;    /* sup |tanh - rational| of the table entry (eig: 0) */
+  double delta_cap;   /* guard on max|Δ_ij| (eig: DBL_MAX, no guard) */
   int64_t device_bytes;
-  int64_t algo;       /* 0 = dense Schur-complement Gauss-Jordan, 1 = block cyclic reduction */
-  int64_t block;      /* dense: GJ block (64); cr: padded lattice-row block BP >= 2 Lx */
+  int64_t algo;       /* 0 = dense Schur-complement Gauss-Jordan, 1 = block cyclic reduction,
+                         2 = eigendecomposition */
+  int64_t block;      /* dense: GJ block (64); cr: padded lattice-row block BP >= 2 Lx; eig: 0 */
 } dwh_info_t;
 
 /* ModelParameters + initialize_cache + init_static_H!
@@ -75,9 +76,15 @@ int dwh_create_batched(dwh_ctx** ctx, int64_t Lx, int64_t Ly, double t, double t
  *                   Gauss-Jordan of the dense N x N complement per pole;
  *   DWH_ALGO_CR     block cyclic reduction of the block-tridiagonal (lattice-row
  *                   blocks, periodic) BdG matrix per pole; needs 2 Lx <= 128;
- *   DWH_ALGO_AUTO   DWHMC_ALGO from the environment (dense | cr | auto), else CR
- *                   when supported.  Both give the same results to fp64 rounding. */
-enum { DWH_ALGO_AUTO = -1, DWH_ALGO_DENSE = 0, DWH_ALGO_CR = 1 };
+ *   DWH_ALGO_EIG    the reference's own method: rocSOLVER zheevd of every chain's
+ *                   2N x 2N H_BdG per step, ρ = U diag(f) U^H by zgemm
+ *                   [src/Hamiltonian.jl:96-114, src/Observables.jl:14-62]; any β,
+ *                   no pole set, no |Δ| guard; O(N^3) with a large constant;
+ *   DWH_ALGO_AUTO   DWHMC_ALGO from the environment (dense | cr | eig | auto),
+ *                   else CR when supported, else dense; EIG when β·E'/2 is beyond
+ *                   the pole table (β above a few hundred).  All give the same
+ *                   results to fp64 rounding. */
+enum { DWH_ALGO_AUTO = -1, DWH_ALGO_DENSE = 0, DWH_ALGO_CR = 1, DWH_ALGO_EIG = 2 };
 
 /* dwh_create_batched with an explicit algorithm. */
 int dwh_create_ex(dwh_ctx** ctx, int64_t Lx, int64_t Ly, double t, double tp, double mu,

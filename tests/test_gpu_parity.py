@@ -34,11 +34,18 @@ def algo(request):
     return request.param
 
 
+@pytest.fixture(params=["cr", "dense", "eig"])
+def algo3(request):
+    """The two pole factorisations and the eigendecomposition path (the one
+    the context falls back to beyond the pole table)."""
+    return request.param
+
+
 def device_ctx(dwhmc, p, disorder, algo="auto", **kw):
     ctx = dwhmc.FermionContext(p.Lx, p.Ly, p.t, p.tp, p.mu, p.beta, p.J, p.nn_table, p.nnn_table,
                                disorder, algo=algo, **kw)
     if algo != "auto":
-        assert ctx.info["algo"] == {"dense": 0, "cr": 1}[algo]
+        assert ctx.info["algo"] == {"dense": 0, "cr": 1, "eig": 2}[algo]
     return ctx
 
 
@@ -49,7 +56,8 @@ def test_mfma_f64_layout(dwhmc):
 @pytest.mark.parametrize("Lx,Ly,beta", [(4, 4, 4.0), (6, 6, 8.0), (5, 7, 16.0), (8, 8, 16.0),
                                         (16, 16, 8.0), (16, 8, 16.0), (3, 3, 4.0), (2, 2, 4.0),
                                         (2, 5, 8.0)])
-def test_factorize_matches_oracle(dwhmc, oracle, Lx, Ly, beta, algo):
+def test_factorize_matches_oracle(dwhmc, oracle, Lx, Ly, beta, algo3):
+    algo = algo3
     O = oracle
     p, dis, Delta = make_case(O, Lx, Ly, beta, seed=Lx * 100 + Ly)
     cache, F_ref, Ef_ref = O.evaluate(p, dis, Delta)
@@ -70,7 +78,8 @@ def test_factorize_matches_oracle(dwhmc, oracle, Lx, Ly, beta, algo):
     ctx.close()
 
 
-def test_full_size_L32_beta16(dwhmc, oracle, algo):
+def test_full_size_L32_beta16(dwhmc, oracle, algo3):
+    algo = algo3
     """BASELINE config C3 size (N = 1024, n = 2048) against the eigen oracle."""
     O = oracle
     p, dis, Delta = make_case(O, 32, 32, 16.0, seed=3232)
@@ -104,7 +113,8 @@ def test_full_size_L48_beta32_batched(dwhmc, oracle, algo):
     ctx.close()
 
 
-def test_batched_chains_independent(dwhmc, oracle, algo):
+def test_batched_chains_independent(dwhmc, oracle, algo3):
+    algo = algo3
     O = oracle
     cases = [make_case(O, 6, 6, 8.0, seed=s) for s in (1, 2, 3)]
     p = cases[0][0]
@@ -122,7 +132,8 @@ def test_batched_chains_independent(dwhmc, oracle, algo):
     ctx.close()
 
 
-def test_clean_dwave_closed_form_on_device(dwhmc, oracle, algo):
+def test_clean_dwave_closed_form_on_device(dwhmc, oracle, algo3):
+    algo = algo3
     """I5 / scripts/benchmark_clean.jl:15-43 directly on the HIP path."""
     O = oracle
     L, beta, D0 = 8, 16.0, 0.25
@@ -156,7 +167,8 @@ def _oracle_after_sweeps(O, p, dis, Delta0, draws, Nt, dt, factorize_first=True)
 
 
 @pytest.mark.parametrize("factorize_first,Lx,Ly", [(True, 6, 6), (False, 6, 6), (True, 2, 4), (True, 3, 2)])
-def test_hmc_sweep_matches_oracle(dwhmc, oracle, factorize_first, Lx, Ly, algo):
+def test_hmc_sweep_matches_oracle(dwhmc, oracle, factorize_first, Lx, Ly, algo3):
+    algo = algo3
     """hmc_sweep! (src/HMC.jl:71-144) with injected draws; factorize_first=False
     reproduces the zeroed-cache first sweep of scripts/benchmark_clean.jl:82-88.
     The 2x4 and 3x2 lattices map several bonds onto one pairing entry (the
@@ -183,7 +195,8 @@ def test_hmc_sweep_matches_oracle(dwhmc, oracle, factorize_first, Lx, Ly, algo):
     ctx.close()
 
 
-def test_throughput_path_equals_single_sweeps(dwhmc, oracle, algo):
+def test_throughput_path_equals_single_sweeps(dwhmc, oracle, algo3):
+    algo = algo3
     O = oracle
     p, dis, Delta0 = make_case(O, 8, 8, 8.0, seed=9, amp=0.1)
     Nt, ns = 4, 3
@@ -360,11 +373,14 @@ def test_cr_block_limit(dwhmc, oracle):
 
 
 @pytest.mark.parametrize("Lx,Ly", [(4, 1), (6, 2), (5, 3), (3, 9), (7, 6), (48, 5), (16, 13), (64, 1), (64, 2),
-                                   (64, 3), (50, 4), (57, 2)])
+                                   (64, 3), (50, 4), (57, 2), (24, 7), (32, 5), (17, 9), (20, 11), (32, 3),
+                                   (29, 2), (32, 1)])
 def test_cr_ragged_chains(dwhmc, oracle, Lx, Ly):
     """Cyclic-reduction chains of every shape: Ly = 1 (one block), 2 (single
     off-diagonal block), odd lengths at every level, padded blocks (2 Lx not a
-    multiple of 32), against the eigen oracle."""
+    multiple of 32), against the eigen oracle.  The BP = 64 cases (17 <= Lx <=
+    32) run the static-particle-block level-0 inversions (k_cr_inv0) and the
+    side-work schedule (k_cr_inv_side) on odd and short chains."""
     O = oracle
     p, dis, Delta = make_case(O, Lx, Ly, 8.0, seed=Lx * 31 + Ly)
     cache, F_ref, Ef_ref = O.evaluate(p, dis, Delta)
@@ -493,4 +509,93 @@ def test_c1_workload_matches_oracle(dwhmc, oracle, algo):
         assert acc[0] == acc_r and abs(dH[0] - dH_r) <= 1e-8 * (1 + abs(dH_r)), (s, dH[0], dH_r)
     D, _ = ctx.get_state()
     assert np.max(np.abs(D[0] - ref.Delta)) <= 1e-10
+    ctx.close()
+
+
+@pytest.mark.parametrize("L,beta", [(10, 1000.0), (12, 5000.0), (10, 10000.0)])
+def test_low_temperature_matches_oracle(dwhmc, oracle, L, beta):
+    """The reference's production β range: scripts/batch_scan_T.jl:21-24 goes to
+    T = 1e-4 (β = 10⁴), scripts/benchmark_beta_scan.jl:37-40 to β = 5000.
+    β·E'/2 is beyond the pole table there, so the context runs the
+    eigendecomposition path (algo eig); same tolerances as everywhere else."""
+    O = oracle
+    p, dis, Delta = make_case(O, L, L, beta, seed=L + int(beta))
+    cache, F_ref, Ef_ref = O.evaluate(p, dis, Delta)
+    P_ref, _ = O.pairing_P(cache.U, cache.E_n, p)
+    ctx = device_ctx(dwhmc, p, dis)
+    assert ctx.info["algo"] == 2 and ctx.info["npoles"] == 0
+    ctx.set_pairing(Delta)
+    ctx.factorize()
+    assert np.max(np.abs(ctx.pairing()[0] - P_ref)) <= 1e-11
+    assert np.max(np.abs(ctx.forces()[0] - F_ref)) <= 1e-10 * (1 + np.max(np.abs(F_ref)))
+    Ef = ctx.fermion_energy()[0]
+    assert abs(Ef - Ef_ref) <= 1e-11 * abs(Ef_ref), (Ef, Ef_ref)
+    hole_ref = O.measure_observables(cache, p, Delta)["hole_conc"]
+    assert abs(2.0 * ctx.hole_trace()[0] / p.N - 1.0 - hole_ref) <= 1e-11
+    ctx.close()
+
+
+def test_clean_closed_form_beta5000(dwhmc, oracle):
+    """I5 (scripts/benchmark_clean.jl:15-43) at β = 5000 on 12 x 12."""
+    O = oracle
+    L, beta, D0 = 12, 5000.0, 0.25
+    p = O.ModelParameters(L, L, T, TP, MU, 0.0, 0.0, beta, J, 1.0)
+    Delta = np.stack([np.full(p.N, D0), np.full(p.N, -D0)], axis=1).astype(np.complex128)
+    _, Px, Fx, Ef = O.clean_dwave_closed_form(D0, L, L, T, TP, MU, beta, J)
+    ctx = device_ctx(dwhmc, p, np.zeros(p.N))
+    assert ctx.info["algo"] == 2
+    ctx.set_pairing(Delta)
+    ctx.factorize()
+    P = ctx.pairing()[0]
+    F = ctx.forces()[0]
+    assert np.max(np.abs(P[:, 0] - Px)) <= 1e-11
+    assert np.max(np.abs(P[:, 1] + Px)) <= 1e-11
+    assert np.max(np.abs(F[:, 0] - Fx)) <= 1e-10 * (1 + abs(Fx))
+    assert abs(ctx.fermion_energy()[0] - Ef) <= 1e-11 * abs(Ef)
+    ctx.close()
+
+
+def test_low_temperature_sweeps_match_oracle(dwhmc, oracle):
+    """hmc_sweep! at β = 1000 (T = 1e-3, scripts/batch_scan_T.jl:21-24) through
+    the eigendecomposition path, two chains batched, against the oracle."""
+    O = oracle
+    cases = [make_case(O, 6, 6, 1000.0, seed=s, amp=0.1) for s in (61, 62)]
+    p = cases[0][0]
+    Nt = 5
+    dt = O.calc_optimal_dt(p.beta, p.J, p.mass, Nt)
+    rng = np.random.default_rng(21)
+    draws = [((rng.standard_normal((2, p.N, 2)) + 1j * rng.standard_normal((2, p.N, 2))) * math.sqrt(0.5),
+              rng.random(2)) for _ in range(3)]
+    refs = [_oracle_after_sweeps(O, pc, dc, Dc, [(n[c], float(u[c])) for n, u in draws], Nt, dt)
+            for c, (pc, dc, Dc) in enumerate(cases)]
+    ctx = device_ctx(dwhmc, p, np.stack([c[1] for c in cases]))
+    assert ctx.info["algo"] == 2
+    ctx.set_pairing(np.stack([c[2] for c in cases]))
+    ctx.factorize()
+    for s, (noise, u) in enumerate(draws):
+        acc, dH = ctx.hmc_sweep(noise, u, Nt, dt, p.mass)
+        D, _ = ctx.get_state()
+        for c in range(2):
+            acc_r, dH_r, D_r, _ = refs[c][s]
+            assert bool(acc[c]) == acc_r
+            assert abs(dH[c] - dH_r) <= 1e-8 * (1 + abs(dH_r)), (s, c, dH[c], dH_r)
+            assert np.max(np.abs(D[c] - D_r)) <= 1e-10
+    ctx.close()
+
+
+def test_guard_falls_back_to_eig_beyond_table(dwhmc, oracle):
+    """β = 300 fits the pole table at the default cap; an uploaded Δ whose
+    re-selected cap would need κ beyond the table moves the context to the
+    eigendecomposition path instead of failing."""
+    O = oracle
+    p, dis, Delta = make_case(O, 8, 8, 300.0, seed=300)
+    Delta = Delta * (3.0 / np.max(np.abs(Delta)))
+    ctx = device_ctx(dwhmc, p, dis)
+    assert ctx.info["algo"] in (0, 1)
+    ctx.set_pairing(Delta)
+    assert ctx.info["algo"] == 2
+    ctx.factorize()
+    _, F_ref, Ef_ref = O.evaluate(p, dis, Delta)
+    assert np.max(np.abs(ctx.forces()[0] - F_ref)) <= 1e-10 * (1 + np.max(np.abs(F_ref)))
+    assert abs(ctx.fermion_energy()[0] - Ef_ref) <= 1e-11 * abs(Ef_ref)
     ctx.close()

@@ -10,7 +10,8 @@ The reference ships no transport fixtures, so these plus the
 loop form are the pins; the absolute values are otherwise "parity unpinned"
 against a Julia run.
 
-GPU: the device path (rocSOLVER zheevd + rocBLAS zgemm + dwhmc_transport.hip)
+GPU: the device path (rocSOLVER zheevd, zheev where zheevd leaves non-finite
+vectors, + rocBLAS zgemm + dwhmc_transport.hip)
 through the C ABI vs the oracle on the same Δ.  Tolerances (fp64):
   * eigenvalues          |E_gpu - E_ref| ≤ 1e-12 (1 + max|E|)
   * stiffness, dc        |Δ| ≤ 1e-9 (1 + |ref|)
@@ -156,6 +157,28 @@ def test_transport_matches_oracle(dwhmc, oracle, Lx, Ly, beta):
     ref = O.measure_transport_and_spectra(cache, p)
     ctx = _ctx(dwhmc, p, dis)
     ctx.set_pairing(D)
+    r = ctx.measure_transport(p.eta, p.domega, p.omega_max)
+    ctx.close()
+    _check_transport(r, ref)
+
+
+@pytest.mark.gpu
+def test_transport_clean_degenerate_spectrum(dwhmc, oracle):
+    """scripts/debug_transport.jl:9-95's case (10x10 clean, β = 1000, uniform
+    d-wave): exactly degenerate levels, on which rocSOLVER's zheevd returns NaN
+    eigenvectors; eigen_solve detects them and re-solves with zheev."""
+    O = oracle
+    p = O.ModelParameters(10, 10, 1.0, -0.35, -1.0, 0.0, 0.0, 1000.0, 1.6, 0.1)
+    N = p.N
+    D = np.stack([np.full(N, 0.2), np.full(N, -0.2)], 1).astype(np.complex128)
+    cache, _, _ = O.evaluate(p, np.zeros(N), D)
+    ref = O.measure_transport_and_spectra(cache, p)
+    ctx = _ctx(dwhmc, p, np.zeros(N))
+    ctx.set_pairing(D)
+    E, U = ctx.eigensystem(0)
+    assert np.all(np.isfinite(U))
+    assert np.max(np.abs(E - cache.E_n)) <= 1e-12 * (1 + np.max(np.abs(E)))
+    assert np.max(np.abs(U.conj().T @ U - np.eye(2 * N))) <= 1e-12
     r = ctx.measure_transport(p.eta, p.domega, p.omega_max)
     ctx.close()
     _check_transport(r, ref)
