@@ -335,7 +335,7 @@ def main(argv=None):
         # per-launch averages.
         replay = schedule(w_sw, min(a.steps, 2 * Nt), Nt)
         replay_steps = sum(n * nt for _, n, nt in replay)
-        names = [dom, "assemble"] + (["cr_inv", "cr_inv_side"] if cr else [])
+        names = [dom, "assemble"] + (["cr_inv", "cr_inv_side", "cr_tail"] if cr else [])
         ctx.timing_enable(names)
         ctx.timing_reset()
         for f, n, nt in replay:
@@ -395,11 +395,12 @@ def main(argv=None):
                 kname = f"k_cr_gemm<{info['block']},1,4>"   # 16x16 tiles, 4-way K split
                 msi, ni, wi = kern["cr_inv"]
                 mss, ns, ws = kern["cr_inv_side"]
+                mst, nt_, wt = kern["cr_tail"]
                 # the CR path's own algorithmic flops per leapfrog step (block
-                # products, incl. the side work of the inversion stages, and
-                # block inversions at 8 BP^3 each) x the timed steps
-                rec["alg_tflops"] = (w + wi + ws) / replay_steps * a.steps * world / el / 1e12
-                rec["alg_flops_per_step"] = (w + wi + ws) / replay_steps / a.chains
+                # products, incl. the side work of the inversion stages and the
+                # coarse tail, and block inversions at 8 BP^3 each) x the timed steps
+                rec["alg_tflops"] = (w + wi + ws + wt) / replay_steps * a.steps * world / el / 1e12
+                rec["alg_flops_per_step"] = (w + wi + ws + wt) / replay_steps / a.chains
                 nt = info["block"] // 16
                 # level-0 inversions: k_cr_inv0 (static particle block, BP = 64)
                 # when the plan has no plain k_cr_inv stage besides it
@@ -418,6 +419,14 @@ def main(argv=None):
                                           "avg_launch_us": 1000.0 * mss / ns,
                                           "flops_per_launch": ws / ns,
                                           "ms_per_step": mss / replay_steps}
+                if nt_:
+                    rec["cr_tail"] = {"bound": "latency", "kernel": "k_cr_tail<4>",
+                                      "what": "the coarse CR levels' stages in one launch with device-wide "
+                                              "stage barriers",
+                                      "launches_per_step": nt_ / replay_steps,
+                                      "avg_launch_us": 1000.0 * mst / nt_,
+                                      "flops_per_launch": wt / nt_,
+                                      "ms_per_step": mst / replay_steps}
             else:
                 nb = -(-info["N"] // 64)                 # GJ block steps; odd nb ends with one rank-64 step
                 kname = "k_gj_update<2>" if nb % 2 == 0 else "k_gj_update<2>+<0>"

@@ -41,11 +41,11 @@ thread_local std::string g_create_error;
 
 enum TimerName {
   T_GJ_UPDATE = 0, T_GJ_PIVOT, T_ASSEMBLE, T_CONTRACT, T_STEP, T_GJ_EDGE, T_CR_GEMM, T_CR_INV, T_CR_INVSIDE,
-  T_COUNT
+  T_CR_TAIL, T_COUNT
 };
 const char* kTimerNames[T_COUNT] = {"gj_update", "gj_pivot", "assemble", "contract",
                                     "step",      "gj_edge",  "cr_gemm",  "cr_inv",
-                                    "cr_inv_side"};
+                                    "cr_inv_side", "cr_tail"};
 
 enum Algo { ALGO_DENSE = 0, ALGO_CR = 1, ALGO_EIG = 2 };
 
@@ -64,9 +64,18 @@ struct CrStage {
   int l0 = 0;           // inversions: level 0 from the static R = A^-1 blocks (k_cr_inv0)
 };
 
+// a run of consecutive small stages executed by one k_cr_tail launch
+struct CrTailSeg {
+  int first, n;   // stages [first, first + n)
+  int tfirst;     // their CrTailStage entries in CrPlan::tail_stages
+  int grid;       // resident workgroups
+};
+
 struct CrPlan {
   int nblk = 0;
   std::vector<CrStage> stages;
+  std::vector<CrTailSeg> tails;
+  std::vector<dwh::CrTailStage> tail_stages;
   std::vector<dwh::CrTask> tasks;
   std::vector<dwh::CrTile> tiles16;          // per product stage: its 16 x 16 tiles with their operands
   std::vector<int> inv_blk, inv_dst, inv_slot;   // inversion source / destination block, ln|det| slot
@@ -458,6 +467,58 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol, bool 
   return pl;
 }
 
+// Coarse tail: runs of >= 2 consecutive stages of at most two rounds of the
+// resident grid each (cap workgroups: occupancy x CUs; DWHMC_CR_TAIL_MAX sets
+// the per-stage limit) become one k_cr_tail launch on min(largest stage, cap)
+// workgroups.  Level-0 inversions (k_cr_inv0) and product stages with another
+// tile configuration stay separate launches.
+void build_cr_tails(CrPlan& pl, int nbatch, int cap) {
+  int maxwg = 2 * cap;
+  if (const char* e = std::getenv("DWHMC_CR_TAIL_MAX")) maxwg = std::atoi(e);
+  auto nwg = [&](const CrStage& st) -> int {
+    if (st.kind == 0) {
+      if (st.l0) return -1;
+      const int side = st.ntiles > 0 ? (nbatch * st.ntiles * st.maxt32 + 3) / 4 : 0;
+      return st.n * nbatch + side;
+    }
+    if (st.cfg.ts != 16 || st.cfg.ksplit != 4) return -1;
+    return nbatch * st.ntiles;
+  };
+  size_t i = 0;
+  while (i < pl.stages.size()) {
+    size_t j = i;
+    int gmax = 0;
+    while (j < pl.stages.size()) {
+      const int w = nwg(pl.stages[j]);
+      if (w < 0 || w > maxwg) break;
+      gmax = std::max(gmax, w);
+      ++j;
+    }
+    if (j - i >= 2) {
+      pl.tails.push_back(CrTailSeg{(int)i, (int)(j - i), (int)pl.tail_stages.size(), std::max(1, std::min(gmax, cap))});
+      for (size_t k = i; k < j; ++k) {
+        const CrStage& st = pl.stages[k];
+        dwh::CrTailStage t{};
+        if (st.kind == 0) {
+          t.inv_first = st.first;
+          t.ninv = st.n;
+          t.side_first = st.tfirst;
+          t.nside = st.ntiles;
+          t.side_maxt = st.maxt32;
+        } else {
+          t.tl_first = st.tfirst;
+          t.ntl = st.ntiles;
+          t.neg = st.sg < 0 ? 1 : 0;
+        }
+        pl.tail_stages.push_back(t);
+      }
+      i = j;
+    } else {
+      i = std::max(j, i + 1);
+    }
+  }
+}
+
 struct TimingRec {
   int name;
   hipEvent_t a, b;
@@ -525,6 +586,12 @@ struct dwh_ctx {
   double* efpart = nullptr;     // per (chain, pole) E_f / Tr G22 partials
   unsigned* efdone = nullptr;   // per chain: pole blocks done (k_cr_fermion_energy)
   int *d_inv_blk = nullptr, *d_inv_dst = nullptr, *d_inv_slot = nullptr, *d_inv0_r = nullptr;
+  // coarse tail (k_cr_tail): stage descriptors, barrier counter (monotonic; its
+  // value before the next launch in tail_base), timeout flag
+  dwh::CrTailStage* d_tail_stages = nullptr;
+  unsigned long long* d_tail_bar = nullptr;
+  unsigned long long tail_base = 0;
+  int* d_tail_err = nullptr;
   double* ldA = nullptr;   // static ln|det| of the Δ = 0 level-0 blocks (= 2 ln|det A|) per slot
   int64_t *d_goff = nullptr, *d_doff = nullptr, *d_off_ph = nullptr;
   int *d_fill_all = nullptr, *d_fill_step = nullptr;
@@ -726,7 +793,25 @@ void cr_enqueue(dwh_ctx* ctx) {
     }
     ctx->pairing_in_pool = false;
   }
-  for (const CrStage& st : ctx->plan.stages) {
+  const CrPlan& plan = ctx->plan;
+  size_t next_tail = 0;
+  for (size_t si = 0; si < plan.stages.size(); ++si) {
+    if (next_tail < plan.tails.size() && plan.tails[next_tail].first == (int)si) {
+      const CrTailSeg& tg = plan.tails[next_tail++];
+      double work = 0;
+      for (int k = 0; k < tg.n; ++k) {
+        const CrStage& st = plan.stages[si + k];
+        work += (st.kind == 0 ? st.n * bp3 : 0.0) + st.flops * c.nbatch;
+      }
+      Scope s(ctx, T_CR_TAIL, work);
+      dwh::launch_cr_tail(c, ctx->bpool, ctx->d_inv_blk, ctx->d_inv_dst, ctx->d_inv_slot, ctx->ldpart, ctx->d_tasks,
+                          ctx->d_tiles16, ctx->d_tail_stages + tg.tfirst, tg.n, tg.grid, ctx->d_tail_bar,
+                          ctx->tail_base, ctx->d_tail_err, ctx->stream);
+      ctx->tail_base += (unsigned long long)(tg.n - 1) * tg.grid;
+      si += tg.n - 1;
+      continue;
+    }
+    const CrStage& st = plan.stages[si];
     if (st.kind == 0 && st.ntiles > 0) {
       Scope s(ctx, T_CR_INVSIDE, st.n * bp3 + st.flops * c.nbatch);
       dwh::launch_cr_inv_side(c, ctx->bpool, ctx->d_inv_blk + st.first, ctx->d_inv_dst + st.first,
@@ -782,9 +867,14 @@ void eig_enqueue(dwh_ctx* ctx) {
                          ctx->stream);
 }
 
-// eig path, after a stream synchronisation: an enqueue-time refusal, then
-// zheevd's convergence flags
+// after a stream synchronisation: a coarse-tail barrier timeout (CR); an
+// enqueue-time refusal, then zheevd's convergence flags (eig)
 int eig_check(dwh_ctx* ctx) {
+  if (ctx->d_tail_err) {
+    int e = 0;
+    HIPCHECK(ctx, hipMemcpy(&e, ctx->d_tail_err, sizeof(int), hipMemcpyDeviceToHost));
+    if (e) return fail(ctx, DWH_ERR_HIP, "k_cr_tail: a stage barrier timed out (workgroups not co-resident)");
+  }
   if (ctx->algo != ALGO_EIG) return DWH_OK;
   if (ctx->async_rc != DWH_OK) {
     const int rc = ctx->async_rc;
@@ -1246,6 +1336,14 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
       d.nld = (int)Ly;
       for (CrStage& st : ctx->plan.stages)
         if (st.kind == 1) st.cfg = dwh::cr_gemm_config(c, st.n, st.maxt32, st.maxt16, st.ntmax);
+      // DWHMC_CR_TAIL=1: the coarse tail in one k_cr_tail launch (measured slower
+      // on MI355X: a device-wide stage barrier costs more than a launch boundary,
+      // profiles/r02_exp_cr_coarse_tail_grid_barrier.txt; off by default)
+      const char* et = std::getenv("DWHMC_CR_TAIL");
+      if (dwh::cr_supported_tail(BP) && et && *et == '1') {
+        const int occ = dwh::cr_tail_occupancy();
+        if (occ > 0) build_cr_tails(ctx->plan, d.nbatch, occ * ncu);
+      }
       if (const char* e = std::getenv("DWHMC_CR_PLAN_DUMP"); e && *e == '1') {
         int i = 0;
         for (const CrStage& st : ctx->plan.stages) {
@@ -1257,6 +1355,9 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
                          i, st.n, st.maxt32, st.maxt16, st.ntmax, st.flops, st.cfg.ts, st.cfg.ksplit, st.ntiles);
           ++i;
         }
+        for (const CrTailSeg& tg : ctx->plan.tails)
+          std::fprintf(stderr, "cr tail: stages %d..%d in one launch, %d workgroups\n", tg.first, tg.first + tg.n - 1,
+                       tg.grid);
       }
     }
   }
@@ -1307,6 +1408,11 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     ALLOC(d_off_ph, pl.off_ph.size());
     ALLOC(d_fill_all, pl.fill_all.size());
     ALLOC(d_fill_step, pl.fill_step.size());
+    if (!pl.tails.empty()) {
+      ALLOC(d_tail_stages, pl.tail_stages.size());
+      ALLOC(d_tail_bar, 1);
+      ALLOC(d_tail_err, 1);
+    }
   }
   if (ctx->algo == ALGO_DENSE) {
     ALLOC(Dv, (size_t)d.nc * N * kSlots);
@@ -1370,6 +1476,11 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     UP(d_off_ph, pl.off_ph.data(), pl.off_ph.size());
     UP(d_fill_all, pl.fill_all.data(), pl.fill_all.size());
     UP(d_fill_step, pl.fill_step.data(), pl.fill_step.size());
+    if (!pl.tails.empty()) {
+      UP(d_tail_stages, pl.tail_stages.data(), pl.tail_stages.size());
+      (void)hipMemsetAsync(ctx->d_tail_bar, 0, sizeof(unsigned long long), s);
+      (void)hipMemsetAsync(ctx->d_tail_err, 0, sizeof(int), s);
+    }
   }
 #undef UP
   // zeroed cache, like initialize_cache (src/Types.jl:182-212): P = 0, E_f = 0

@@ -878,6 +878,88 @@ __global__ __launch_bounds__(64 * NT) void k_cr_inv_side(double2* __restrict__ p
 }
 
 // ---------------------------------------------------------------------------
+// Coarse tail: the stages of the coarse CR levels each carry a few dozen
+// workgroups and last a few microseconds — kernel boundaries, not work, set
+// their pace.  k_cr_tail runs a run of such stages in one launch: the grid is
+// sized so that every workgroup is resident at once (host: occupancy x CUs),
+// each stage's items are spread over it grid-stride, and a device-wide
+// barrier separates the stages.  Barrier: every wave makes its stores visible
+// at agent scope (release: L2 write-back; L2s are per XCD), the workgroup
+// arrives on a 64-bit monotonic counter and waits for base + (s + 1) x grid
+// arrivals, then every wave acquires (L2 invalidate).  A wait that exceeds
+// ~2 s sets *err and gives up, so a broken residency assumption ends the
+// kernel with an error instead of hanging the device.
+// Measured at C3 (profiles/r02_exp_cr_coarse_tail_grid_barrier.txt): stages
+// 8..17 take 400 us in the tail against 92 us as ten launches — the barrier
+// alone (no fences) costs ~8.5 us, the agent-scope release (L2 write-back on
+// every workgroup) and acquire (L2 invalidate) ~25 us more, while a launch
+// boundary costs 1-2 us.  Off by default (DWHMC_CR_TAIL=1 enables it).
+// ---------------------------------------------------------------------------
+#ifndef DWHMC_TAIL_FENCE
+#define DWHMC_TAIL_FENCE 2   // A/B diagnostics: 0 no fences, 1 acquire only, 3 release by one wave
+#endif
+__device__ __forceinline__ void tail_barrier(unsigned long long* bar, unsigned long long target, int* err) {
+#if DWHMC_TAIL_FENCE == 2
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#endif
+  __syncthreads();
+#if DWHMC_TAIL_FENCE == 3
+  if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#endif
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(bar, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned spins = 0;
+    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 26)) {
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+#if DWHMC_TAIL_FENCE != 0
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
+}
+
+template <int NT>
+__global__ __launch_bounds__(64 * NT) void k_cr_tail(double2* __restrict__ pool, int64_t item,
+                                                     const int* __restrict__ blk, const int* __restrict__ dst,
+                                                     const int* __restrict__ slot, double* __restrict__ ldpart,
+                                                     int nslots, int nbatch, const CrTask* __restrict__ tasks,
+                                                     const CrTile* __restrict__ tl16,
+                                                     const CrTailStage* __restrict__ stages, int nst,
+                                                     unsigned long long* bar, unsigned long long base, int* err) {
+  static_assert(NT == 4, "the tail runs 4-wave workgroups");
+  __shared__ double2 pan[2][NT][16 * 17];
+  __shared__ double ldw[NT];
+  for (int si = 0; si < nst; ++si) {
+    const CrTailStage S = stages[si];
+    const int nall = S.ninv * nbatch;
+    const int side_total = nbatch * S.nside * S.side_maxt;
+    const int nside_wg = (side_total + 3) / 4;
+    const int tl_total = nbatch * S.ntl;
+    const int nwg = nall + nside_wg + tl_total;
+    for (int g = blockIdx.x; g < nwg; g += gridDim.x) {
+      if (g < nall) {
+        const int bi = g / S.ninv;
+        cr_inv_wg<NT>(pool, item, bi, g - bi * S.ninv, blk + S.inv_first, dst + S.inv_first, slot + S.inv_first,
+                      ldpart, nslots, pan, ldw);
+      } else if (g < nall + nside_wg) {
+        cr_gemm_wg<16 * NT, 2, 1, 0, true>(pool, item, tasks + S.side_first, S.nside, S.side_maxt, nullptr, 0,
+                                          side_total, 1.0, g - nall);
+      } else {
+        cr_gemm_wg<16 * NT, 1, 4>(pool, item, nullptr, 0, 0, tl16 + S.tl_first, S.ntl, tl_total,
+                                  S.neg ? -1.0 : 1.0, g - nall - nside_wg);
+      }
+      __syncthreads();   // the panel / K-split partials in LDS are reused by the next item
+    }
+    if (si + 1 < nst) tail_barrier(bar, base + (unsigned long long)(si + 1) * gridDim.x, err);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Force from the level-0 G blocks: P_ij = Σ_q c_q (G12[i,j] + G12[j,i]) with
 // G12 read straight from the B parts of the pool (offsets goff per pairing
 // slot), F = -β/2J (Δ - J P) (src/Observables.jl:14-62), then the leapfrog
@@ -995,6 +1077,21 @@ __global__ __launch_bounds__(256) void k_cr_fermion_energy(const double2* __rest
 bool cr_supported_bp(int BP) { return BP == 32 || BP == 64 || BP == 96 || BP == 128; }
 bool cr_supported_side(int BP) { return BP == 64; }
 bool cr_supported_inv0(int BP) { return BP == 64; }
+bool cr_supported_tail(int BP) { return BP == 64; }
+
+int cr_tail_occupancy() {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_cr_tail<4>, 256, 0) != hipSuccess) return 0;
+  return n;
+}
+
+void launch_cr_tail(const CrDims& c, double2* pool, const int* blk, const int* dst, const int* slot,
+                    double* ldpart, const CrTask* tasks, const CrTile* tl16, const CrTailStage* stages, int nst,
+                    int grid, unsigned long long* bar, unsigned long long base, int* err, hipStream_t s) {
+  if (nst <= 0 || grid <= 0) return;
+  hipLaunchKernelGGL(k_cr_tail<4>, dim3(grid), dim3(256), 0, s, pool, c.item, blk, dst, slot, ldpart, c.Ly,
+                     c.nbatch, tasks, tl16, stages, nst, bar, base, err);
+}
 
 void launch_cr_inv0(const CrDims& c, double2* pool, const int* blk, const int* rblk, const int* dst,
                     const int* slot, int n, double* ldpart, const double* ldA, hipStream_t s) {

@@ -94,6 +94,25 @@ void launch_cr_inv0(const CrDims& c, double2* pool, const int* blk, const int* r
 bool cr_supported_side(int BP);
 void launch_cr_inv_side(const CrDims& c, double2* pool, const int* blk, const int* dst, const int* slot,
                         int n, double* ldpart, const CrTask* stasks, int nst, int maxt32, hipStream_t s);
+// Coarse tail (BP = 64): consecutive small stages in one launch with a
+// device-wide barrier between them.  A stage is an inversion list (+ side
+// tasks, as launch_cr_inv_side) or a 16 x 16 / 4-way K-split product list.
+struct CrTailStage {
+  int inv_first, ninv;                  // entries of the inversion lists
+  int side_first, nside, side_maxt;     // side tasks (CrTask, 32 x 32 tiles, sign in bq)
+  int tl_first, ntl;                    // product tiles (CrTile)
+  int neg;                              // product stage sign: 1 = negative
+};
+bool cr_supported_tail(int BP);
+// workgroups of k_cr_tail that one CU holds at once (the grid is sized so every
+// workgroup is resident: the stage barrier needs all of them running)
+int cr_tail_occupancy();
+// stages [0, nst) of `stages` (device array) on `grid` workgroups; bar: the
+// device barrier counter (64-bit, monotonic), base: its value at launch; err:
+// set to 1 when a barrier wait times out (then the results are invalid)
+void launch_cr_tail(const CrDims& c, double2* pool, const int* blk, const int* dst, const int* slot,
+                    double* ldpart, const CrTask* tasks, const CrTile* tl16, const CrTailStage* stages, int nst,
+                    int grid, unsigned long long* bar, unsigned long long base, int* err, hipStream_t s);
 // block-product stage configuration: output tile TS x TS (16 or 32) and the
 // number of waves splitting each tile's K range (1, 2, 4)
 struct CrGemmCfg {
