@@ -541,17 +541,20 @@ def test_c1_workload_matches_oracle(dwhmc, oracle, algo):
 
 
 @pytest.mark.parametrize("L,beta", [(10, 1000.0), (12, 5000.0), (10, 10000.0)])
-def test_low_temperature_matches_oracle(dwhmc, oracle, L, beta):
+def test_low_temperature_matches_oracle(dwhmc, oracle, L, beta, algo3):
     """The reference's production β range: scripts/batch_scan_T.jl:21-24 goes to
     T = 1e-4 (β = 10⁴), scripts/benchmark_beta_scan.jl:37-40 to β = 5000.
-    β·E'/2 is beyond the pole table there, so the context runs the
-    eigendecomposition path (algo eig); same tolerances as everywhere else."""
+    The pole table reaches κ = 262144 (β·E'/2; 31-43 pole pairs here), so
+    auto selects the CR path; the pole GJ path and the eigendecomposition path
+    (algo eig) must meet the same tolerances as everywhere else."""
     O = oracle
     p, dis, Delta = make_case(O, L, L, beta, seed=L + int(beta))
     cache, F_ref, Ef_ref = O.evaluate(p, dis, Delta)
     P_ref, _ = O.pairing_P(cache.U, cache.E_n, p)
-    ctx = device_ctx(dwhmc, p, dis)
-    assert ctx.info["algo"] == 2 and ctx.info["npoles"] == 0
+    if algo3 == "cr":
+        assert device_ctx(dwhmc, p, dis).info["algo"] == 1   # auto: CR inside the table
+    ctx = device_ctx(dwhmc, p, dis, algo3)
+    assert (ctx.info["npoles"] == 0) == (algo3 == "eig")
     ctx.set_pairing(Delta)
     ctx.factorize()
     assert np.max(np.abs(ctx.pairing()[0] - P_ref)) <= 1e-11
@@ -563,15 +566,37 @@ def test_low_temperature_matches_oracle(dwhmc, oracle, L, beta):
     ctx.close()
 
 
-def test_clean_closed_form_beta5000(dwhmc, oracle):
-    """I5 (scripts/benchmark_clean.jl:15-43) at β = 5000 on 12 x 12."""
+@pytest.mark.parametrize("L,beta", [(32, 1000.0), (24, 10000.0)])
+def test_low_temperature_large_lattice_cr(dwhmc, oracle, L, beta):
+    """The CR path at the extended table's κ (29-40 pole pairs) on the C3
+    lattice and a 24 x 24 one: the longest CR chains at the worst-conditioned
+    resolvents (cond ≈ βE'/π), same tolerances."""
+    O = oracle
+    p, dis, Delta = make_case(O, L, L, beta, seed=7 * L + int(beta))
+    cache, F_ref, Ef_ref = O.evaluate(p, dis, Delta)
+    P_ref, _ = O.pairing_P(cache.U, cache.E_n, p)
+    ctx = device_ctx(dwhmc, p, dis, "cr")
+    assert ctx.info["npoles"] >= 25
+    ctx.set_pairing(Delta)
+    ctx.factorize()
+    assert np.max(np.abs(ctx.pairing()[0] - P_ref)) <= 1e-11
+    assert np.max(np.abs(ctx.forces()[0] - F_ref)) <= 1e-10 * (1 + np.max(np.abs(F_ref)))
+    assert abs(ctx.fermion_energy()[0] - Ef_ref) <= 1e-11 * abs(Ef_ref)
+    hole_ref = O.measure_observables(cache, p, Delta)["hole_conc"]
+    assert abs(2.0 * ctx.hole_trace()[0] / p.N - 1.0 - hole_ref) <= 1e-11
+    ctx.close()
+
+
+def test_clean_closed_form_beta5000(dwhmc, oracle, algo3):
+    """I5 (scripts/benchmark_clean.jl:15-43) at β = 5000 on 12 x 12, every
+    algorithm (the degenerate clean spectrum is the hard case for the eigen
+    path, the large κ for the pole paths)."""
     O = oracle
     L, beta, D0 = 12, 5000.0, 0.25
     p = O.ModelParameters(L, L, T, TP, MU, 0.0, 0.0, beta, J, 1.0)
     Delta = np.stack([np.full(p.N, D0), np.full(p.N, -D0)], axis=1).astype(np.complex128)
     _, Px, Fx, Ef = O.clean_dwave_closed_form(D0, L, L, T, TP, MU, beta, J)
-    ctx = device_ctx(dwhmc, p, np.zeros(p.N))
-    assert ctx.info["algo"] == 2
+    ctx = device_ctx(dwhmc, p, np.zeros(p.N), algo3)
     ctx.set_pairing(Delta)
     ctx.factorize()
     P = ctx.pairing()[0]
@@ -583,9 +608,11 @@ def test_clean_closed_form_beta5000(dwhmc, oracle):
     ctx.close()
 
 
-def test_low_temperature_sweeps_match_oracle(dwhmc, oracle):
+@pytest.mark.parametrize("algo_lt", ["cr", "eig"])
+def test_low_temperature_sweeps_match_oracle(dwhmc, oracle, algo_lt):
     """hmc_sweep! at β = 1000 (T = 1e-3, scripts/batch_scan_T.jl:21-24) through
-    the eigendecomposition path, two chains batched, against the oracle."""
+    the CR path (κ inside the extended table) and the eigendecomposition path,
+    two chains batched, against the oracle."""
     O = oracle
     cases = [make_case(O, 6, 6, 1000.0, seed=s, amp=0.1) for s in (61, 62)]
     p = cases[0][0]
@@ -596,8 +623,7 @@ def test_low_temperature_sweeps_match_oracle(dwhmc, oracle):
               rng.random(2)) for _ in range(3)]
     refs = [_oracle_after_sweeps(O, pc, dc, Dc, [(n[c], float(u[c])) for n, u in draws], Nt, dt)
             for c, (pc, dc, Dc) in enumerate(cases)]
-    ctx = device_ctx(dwhmc, p, np.stack([c[1] for c in cases]))
-    assert ctx.info["algo"] == 2
+    ctx = device_ctx(dwhmc, p, np.stack([c[1] for c in cases]), algo_lt)
     ctx.set_pairing(np.stack([c[2] for c in cases]))
     ctx.factorize()
     for s, (noise, u) in enumerate(draws):
@@ -612,11 +638,11 @@ def test_low_temperature_sweeps_match_oracle(dwhmc, oracle):
 
 
 def test_guard_falls_back_to_eig_beyond_table(dwhmc, oracle):
-    """β = 300 fits the pole table at the default cap; an uploaded Δ whose
-    re-selected cap would need κ beyond the table moves the context to the
-    eigendecomposition path instead of failing."""
+    """β = 40000 fits the pole table at the default cap (κ <= 2.3e5 of
+    262144); an uploaded Δ whose re-selected cap would need κ beyond the table
+    moves the context to the eigendecomposition path instead of failing."""
     O = oracle
-    p, dis, Delta = make_case(O, 8, 8, 300.0, seed=300)
+    p, dis, Delta = make_case(O, 8, 8, 40000.0, seed=300)
     Delta = Delta * (3.0 / np.max(np.abs(Delta)))
     ctx = device_ctx(dwhmc, p, dis)
     assert ctx.info["algo"] in (0, 1)

@@ -40,6 +40,9 @@ import sys
 import time
 from multiprocessing import Pool
 
+import ctypes
+import subprocess
+
 import mpmath as mp
 import numpy as np
 
@@ -99,14 +102,9 @@ def discrete_gauss(M, n):
     polynomials); nodes x_i, weights summing to M."""
     key = (M, n)
     if key not in _RULES:
-        Jm = mp.matrix(n, n)
-        for i in range(n):
-            Jm[i, i] = mp.mpf(M - 1) / 2
-            if i < n - 1:
-                j = i + 1
-                Jm[i, i + 1] = Jm[i + 1, i] = mp.sqrt(mp.mpf(j * j * (M * M - j * j)) / (4 * (4 * j * j - 1)))
-        E, V = mp.eigsy(Jm)
-        _RULES[key] = ([E[i] for i in range(n)], [M * V[0, i] ** 2 for i in range(n)])
+        alpha = [mp.mpf(M - 1) / 2] * n
+        beta = [mp.sqrt(mp.mpf(j * j * (M * M - j * j)) / (4 * (4 * j * j - 1))) for j in range(1, n)]
+        _RULES[key] = gauss_jacobi_q(alpha, beta, M)
     return _RULES[key]
 
 
@@ -144,6 +142,73 @@ def matsubara_measure(kappa, ntail=10):
         t.append(ti)
         mu.append(ri * ti)
     return t, mu
+
+
+_QLIB = None
+
+
+def _qlib():
+    """tools/pole_gauss.c (binary128 Lanczos + Golub-Welsch), built on first use."""
+    global _QLIB
+    if _QLIB is None:
+        src = os.path.join(ROOT, "tools", "pole_gauss.c")
+        so = os.path.join(ROOT, "tools", "_pole_gauss.so")
+        if not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(src):
+            subprocess.check_call(["gcc", "-O2", "-shared", "-fPIC", src, "-lquadmath", "-o", so])
+        lib = ctypes.CDLL(so)
+        P = ctypes.POINTER(ctypes.c_double)
+        lib.pg_multipoint_pade.argtypes = [ctypes.c_int, P, P, P, P, ctypes.c_int, ctypes.c_int, P, P, P]
+        lib.pg_gauss_jacobi.argtypes = [ctypes.c_int, P, P, P, P, ctypes.c_double, ctypes.c_double, P, P, P, P]
+        _QLIB = lib
+    return _QLIB
+
+
+def _dd(xs):
+    """mpf list -> double-double (hi, lo) arrays"""
+    hi = np.array([float(x) for x in xs])
+    lo = np.array([float(x - mp.mpf(h)) for x, h in zip(xs, hi)])
+    return hi, lo
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+def gauss_jacobi_q(alpha, beta, mu0):
+    """Gauss rule of a Jacobi matrix in binary128 (nodes ascending), as mpf."""
+    n = len(alpha)
+    ah, al = _dd(alpha)
+    bh, bl = _dd(list(beta) + [mp.mpf(0)])
+    m0 = mp.mpf(mu0)
+    xh, xl, wh, wl = (np.zeros(n) for _ in range(4))
+    rc = _qlib().pg_gauss_jacobi(n, _ptr(ah), _ptr(al), _ptr(bh), _ptr(bl), float(m0), float(m0 - mp.mpf(float(m0))),
+                                 _ptr(xh), _ptr(xl), _ptr(wh), _ptr(wl))
+    if rc != 0:
+        raise RuntimeError(f"pg_gauss_jacobi failed ({rc})")
+    return ([mp.mpf(float(a)) + mp.mpf(float(b)) for a, b in zip(xh, xl)],
+            [mp.mpf(float(a)) + mp.mpf(float(b)) for a, b in zip(wh, wl)])
+
+
+class QAtoms:
+    """Atoms of a Stieltjes measure prepared once for the binary128 kernel."""
+
+    def __init__(self, t, mu):
+        self.K = len(t)
+        self.th, self.tl = _dd(t)
+        self.mh, self.ml = _dd(mu)
+
+
+def multipoint_pade_q(atoms, m, nodes_s):
+    """multipoint_pade through tools/pole_gauss.c (same Lanczos / Golub-Welsch
+    process in binary128): the κ > 2048 entries, where the 40-digit mpmath
+    process takes minutes per Remez iterate."""
+    s = np.ascontiguousarray(np.asarray(nodes_s, dtype=np.float64))
+    tq, a = np.zeros(m), np.zeros(m)
+    rc = _qlib().pg_multipoint_pade(atoms.K, _ptr(atoms.th), _ptr(atoms.tl), _ptr(atoms.mh), _ptr(atoms.ml), m,
+                                    len(s), _ptr(s), _ptr(tq), _ptr(a))
+    if rc != 0:
+        raise RuntimeError(f"pg_multipoint_pade failed ({rc})")
+    return tq, a
 
 
 def multipoint_pade(t, mu, m, nodes_s):
@@ -204,6 +269,11 @@ def phi_fit(kappa, tq, a, u):
     return 0.5 * (d.max() + d.min()), 0.5 * (d.max() - d.min())
 
 
+# entries above this κ use the binary128 kernel (tools/pole_gauss.c); the
+# committed κ <= 2048 entries came from the 40-digit mpmath process
+QUAD_ABOVE = 2048.0
+
+
 def optimise(kappa, m, t, mu, iters=40):
     a0 = (math.pi / (2 * kappa)) ** 2
     lo, hi = math.log(a0), math.log(1 + a0)
@@ -211,9 +281,13 @@ def optimise(kappa, m, t, mu, iters=40):
     u = ugrid(kappa, 20001)
     best = (np.inf, None)
     stall = 0
+    atoms = QAtoms(t, mu) if kappa > QUAD_ABOVE or os.environ.get("GEN_QUAD") == "1" else None
     for _ in range(iters):
         s = np.exp(lo + np.cumsum(L)[:-1]) - a0
-        tq, a = multipoint_pade(t, mu, m, s)
+        if atoms is not None:
+            tq, a = multipoint_pade_q(atoms, m, s)
+        else:
+            tq, a = multipoint_pade(t, mu, m, s)
         e = tanh_error(kappa, tq, a, u)
         sup = float(np.max(np.abs(e)))
         if sup < 0.97 * best[0]:
