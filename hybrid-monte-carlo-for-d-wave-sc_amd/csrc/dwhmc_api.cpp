@@ -1333,6 +1333,9 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
       c.nbatch = d.nbatch;
       c.nblk = ctx->plan.nblk;
       c.item = (int64_t)c.nblk * (BP / 2) * BP;
+      // DWHMC_CR_INV2=1: BP = 64 inversions by particle-hole 2 x 2 pivots (k_cr_inv2)
+      const char* ei = std::getenv("DWHMC_CR_INV2");
+      c.inv2 = BP == 64 && ei && *ei == '1';
       d.nld = (int)Ly;
       for (CrStage& st : ctx->plan.stages)
         if (st.kind == 1) st.cfg = dwh::cr_gemm_config(c, st.n, st.maxt32, st.maxt16, st.ntmax);

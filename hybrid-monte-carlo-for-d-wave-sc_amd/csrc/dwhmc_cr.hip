@@ -414,6 +414,141 @@ __global__ __launch_bounds__(64 * NT) void k_cr_inv(double2* __restrict__ pool, 
 }
 
 // ---------------------------------------------------------------------------
+// Block inversion by particle-hole 2 x 2 pivots (BP = 64, HP = 32).
+// An M-form block W = [[A, B], [conj B, -conj A]] is pivoted on the index
+// pairs {k, k + HP} (particle k and hole k): Gauss-Jordan in place with the
+// 2 x 2 pivot p = W[K, K] = [[a, b], [conj b, -conj a]] (a = W[k, k],
+// b = W[k, k + HP]), whose inverse is [[conj a, b], [conj b, -a]] / (|a|² + |b|²)
+// — no 16 x 16 pivot inversions on the chain, 32 pivot steps instead of 64
+// scalar ones, and only the top half is ever stored.  A swept set K of pairs
+// keeps the symmetry up to signs: W[i + HP, c] = σ(c) d(i) d(c) conj W[i, τ(c)]
+// with τ(c) = c ± HP, σ(c) = +1 (c < HP) / -1, d(x) = -1 when x's pair is
+// swept (sweep_K(-X) = -D_K sweep_K(X) D_K), so the pivot's hole row k + HP
+// is synthesised from the particle row k.  Each pivot block of i(W) has
+// Hermitian part >= y I like every Schur complement of i(H - i y): no
+// pivoting.  ln|det W| = Σ_k ln(|a_k|² + |b_k|²).
+// Layout: wave w owns rows 8w .. 8w + 7 of the top half, lane c = column c
+// (8 complex per lane in VGPRs); per step the pivot row k goes through LDS
+// (double-buffered by step parity) and each wave's column pair (k, k + HP)
+// through its own LDS slot; one barrier per step.  Rank-2 update with 4-mult
+// complex FMAs on the VALU (the update is rank 2: MFMA would pad K to 4);
+// the pivot columns are folded into the same FMAs (R_k -> 1 + P00 / P01,
+// R_h -> P10 / 1 + P11 on lanes k / k + HP), the pivot row is a select.
+// ---------------------------------------------------------------------------
+template <int NW>
+struct Inv2Lds {
+  static constexpr int RPW = 32 / NW;   // top-half rows per wave
+  double2 row[2][64];
+  double2 col[2][NW][RPW][2];
+};
+
+// acc - (u x + v y), two independent partial chains per component
+__device__ __forceinline__ double2 cmsub2(double2 acc, double2 u, double2 x, double2 v, double2 y) {
+  const double r1 = fma(-u.x, x.x, fma(u.y, x.y, acc.x));
+  const double r2 = fma(-v.x, y.x, v.y * y.y);
+  const double i1 = fma(-u.x, x.y, fma(-u.y, x.x, acc.y));
+  const double i2 = fma(-v.x, y.y, -v.y * y.x);
+  return make_double2(r1 + r2, i1 + i2);
+}
+// u x + v y
+__device__ __forceinline__ double2 cmadd2(double2 u, double2 x, double2 v, double2 y) {
+  const double r1 = fma(u.x, x.x, -u.y * x.y), r2 = fma(v.x, y.x, -v.y * y.y);
+  const double i1 = fma(u.x, x.y, u.y * x.x), i2 = fma(v.x, y.y, v.y * y.x);
+  return make_double2(r1 + r2, i1 + i2);
+}
+
+// NW waves (64 NW threads): wave w owns rows RPW w .. RPW w + RPW - 1
+template <int NW>
+__device__ __forceinline__ void cr_inv2_wg(double2* __restrict__ pool, int64_t item, int bi, int li,
+                                           const int* __restrict__ blk, const int* __restrict__ dst,
+                                           const int* __restrict__ slot, double* __restrict__ ldpart,
+                                           int nslots, Inv2Lds<NW>& S) {
+  constexpr int HP = 32, BP = 64, RPW = Inv2Lds<NW>::RPW;
+  const double2* M = pool + (int64_t)bi * item + (int64_t)blk[li] * HP * BP;
+  double2* Mo = pool + (int64_t)bi * item + (int64_t)dst[li] * HP * BP;   // may equal M
+  const int w = threadIdx.x >> 6, c = threadIdx.x & 63, cm = c & (HP - 1), tc = c ^ HP;
+  const double sg = c < HP ? 1.0 : -1.0;
+  double2 W[RPW];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) W[r] = M[(int64_t)(RPW * w + r) * BP + c];
+  if (w == 0) S.row[0][c] = W[0];
+  if (cm == 0) {
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) S.col[0][w][r][c >> 5] = W[r];
+  }
+  __syncthreads();
+  double myden = 1.0;   // lane k of wave 0 keeps |det p_k|
+#pragma unroll
+  for (int k = 0; k < HP; ++k) {
+    const int b = k & 1;
+    // every LDS operand of the step up front (one round trip)
+    const double2 a = S.row[b][k], bb = S.row[b][k + HP];
+    const double2 x = S.row[b][c], yv = S.row[b][tc];
+    double2 u[RPW], v[RPW];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+      u[r] = S.col[b][w][r][0];
+      v[r] = S.col[b][w][r][1];
+    }
+    const double s = cm < k ? -sg : sg;
+    const double2 z = make_double2(s * yv.x, -s * yv.y);   // W[k + HP, c]
+    const double den = fma(a.x, a.x, a.y * a.y) + fma(bb.x, bb.x, bb.y * bb.y);
+    if (c == k) myden = den;
+    // 1/den: v_rcp_f64 + two Newton steps (den > 0, far from the range ends)
+    double inv = __builtin_amdgcn_rcp(den);
+    inv = fma(inv, fma(-den, inv, 1.0), inv);
+    inv = fma(inv, fma(-den, inv, 1.0), inv);
+    const double2 P00 = make_double2(a.x * inv, -a.y * inv), P01 = make_double2(bb.x * inv, bb.y * inv);
+    const double2 P10 = make_double2(bb.x * inv, -bb.y * inv), P11 = make_double2(-a.x * inv, -a.y * inv);
+    double2 Rk = cmadd2(P00, x, P01, z), Rh = cmadd2(P10, x, P11, z);
+    const double2 rowk = c == k ? P00 : c == k + HP ? P01 : Rk;   // new pivot row entry
+    if (c == k) {
+      Rk = make_double2(1.0 + P00.x, P00.y);
+      Rh = P10;
+    } else if (c == k + HP) {
+      Rk = P01;
+      Rh = make_double2(1.0 + P11.x, P11.y);
+    }
+    const int k1 = k + 1, nb = b ^ 1;
+    // the next pivot row first (its owner publishes it before its other rows)
+    if (k1 < HP && w == k1 / RPW) {
+      const int r1 = (k + 1) % RPW;
+      W[r1] = cmsub2(W[r1], u[r1], Rk, v[r1], Rh);
+      S.row[nb][c] = W[r1];
+    }
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+      if (RPW * w + r == k) W[r] = rowk;
+      else if (!(k1 < HP && RPW * w + r == k1)) W[r] = cmsub2(W[r], u[r], Rk, v[r], Rh);
+    }
+    if (k1 < HP) {
+      if (cm == k1) {
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) S.col[nb][w][r][c >> 5] = W[r];
+      }
+      __syncthreads();
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) Mo[(int64_t)(RPW * w + r) * BP + c] = W[r];
+  if (w == 0) {
+    const double t = wave_sum(c < HP ? log(myden) : 0.0);
+    if (c == 0) ldpart[(int64_t)bi * nslots + slot[li]] = t;
+  }
+}
+
+#ifndef DWHMC_INV2_WAVES
+#define DWHMC_INV2_WAVES 4
+#endif
+__global__ __launch_bounds__(64 * DWHMC_INV2_WAVES) void k_cr_inv2(double2* __restrict__ pool, int64_t item,
+                                                 const int* __restrict__ blk, const int* __restrict__ dst,
+                                                 const int* __restrict__ slot, double* __restrict__ ldpart,
+                                                 int nslots) {
+  __shared__ Inv2Lds<DWHMC_INV2_WAVES> S;
+  cr_inv2_wg<DWHMC_INV2_WAVES>(pool, item, blockIdx.y, blockIdx.x, blk, dst, slot, ldpart, nslots, S);
+}
+
+// ---------------------------------------------------------------------------
 // Level-0 inversions from the static particle block.  A level-0 diagonal
 // block is D = [[A, B], [conj B, -conj A]] with A = h_row - i y (hopping,
 // disorder, mu: Δ-independent) and B = Δ/2 (in-row pairing).  Its M-form
@@ -851,7 +986,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MI == 1 ? D
 // must hide its own MFMA and memory latency; one 16 x 16 tile per wave ran at
 // a third of that rate).
 // ---------------------------------------------------------------------------
-template <int NT>
+template <int NT, bool INV2 = false>
 __global__ __launch_bounds__(64 * NT) void k_cr_inv_side(double2* __restrict__ pool, int64_t item,
                                                          const int* __restrict__ blk,
                                                          const int* __restrict__ dst,
@@ -870,7 +1005,12 @@ __global__ __launch_bounds__(64 * NT) void k_cr_inv_side(double2* __restrict__ p
   if (b < nall) return;
 #endif
   if (b < nall) {
-    cr_inv_wg<NT>(pool, item, b / ninv, b - (b / ninv) * ninv, blk, dst, slot, ldpart, nslots, pan, ldw);
+    if constexpr (INV2) {
+      cr_inv2_wg<NT>(pool, item, b / ninv, b - (b / ninv) * ninv, blk, dst, slot, ldpart, nslots,
+                     *reinterpret_cast<Inv2Lds<NT>*>(&pan[0][0][0]));
+    } else {
+      cr_inv_wg<NT>(pool, item, b / ninv, b - (b / ninv) * ninv, blk, dst, slot, ldpart, nslots, pan, ldw);
+    }
     return;
   }
   cr_gemm_wg<16 * NT, 2, 1, 0, true>(pool, item, stasks, nst, maxt, nullptr, 0, total, 1.0,
@@ -1118,7 +1258,11 @@ void launch_cr_inv(const CrDims& c, double2* pool, const int* blk, const int* ds
   const dim3 g(n, c.nbatch);
   switch (c.BP) {
     case 32: hipLaunchKernelGGL(k_cr_inv<2>, g, dim3(128), 0, s, pool, c.item, blk, dst, slot, ldpart, c.Ly); break;
-    case 64: hipLaunchKernelGGL(k_cr_inv<4>, g, dim3(256), 0, s, pool, c.item, blk, dst, slot, ldpart, c.Ly); break;
+    case 64:
+      if (c.inv2)
+        hipLaunchKernelGGL(k_cr_inv2, g, dim3(64 * DWHMC_INV2_WAVES), 0, s, pool, c.item, blk, dst, slot, ldpart, c.Ly);
+      else hipLaunchKernelGGL(k_cr_inv<4>, g, dim3(256), 0, s, pool, c.item, blk, dst, slot, ldpart, c.Ly);
+      break;
     case 96: hipLaunchKernelGGL(k_cr_inv<6>, g, dim3(384), 0, s, pool, c.item, blk, dst, slot, ldpart, c.Ly); break;
     default: hipLaunchKernelGGL(k_cr_inv<8>, g, dim3(512), 0, s, pool, c.item, blk, dst, slot, ldpart, c.Ly); break;
   }
@@ -1132,8 +1276,12 @@ void launch_cr_inv_side(const CrDims& c, double2* pool, const int* blk, const in
   }
   const int total = c.nbatch * nst * maxt32;
   const int side_wg = (total + 3) / 4;
-  hipLaunchKernelGGL(k_cr_inv_side<4>, dim3(n * c.nbatch + side_wg), dim3(256), 0, s, pool, c.item, blk,
-                     dst, slot, ldpart, c.Ly, n, c.nbatch, stasks, nst, maxt32, total);
+  if (c.inv2)
+    hipLaunchKernelGGL((k_cr_inv_side<4, true>), dim3(n * c.nbatch + side_wg), dim3(256), 0, s, pool, c.item,
+                       blk, dst, slot, ldpart, c.Ly, n, c.nbatch, stasks, nst, maxt32, total);
+  else
+    hipLaunchKernelGGL((k_cr_inv_side<4, false>), dim3(n * c.nbatch + side_wg), dim3(256), 0, s, pool, c.item,
+                       blk, dst, slot, ldpart, c.Ly, n, c.nbatch, stasks, nst, maxt32, total);
 }
 
 // Stage configuration (tile TS, K split).  16 x 16 tiles with a 4-way K

@@ -447,6 +447,37 @@ def test_cr_coarse_tail_kernel(dwhmc, oracle, monkeypatch, Lx, Ly):
     ctx.close()
 
 
+@pytest.mark.parametrize("side", ["1", "0"])
+@pytest.mark.parametrize("Lx,Ly", [(32, 32), (20, 13)])
+def test_cr_inv2_kernel(dwhmc, oracle, monkeypatch, Lx, Ly, side):
+    """The opt-in particle-hole 2 x 2 pivot inversion (DWHMC_CR_INV2=1,
+    k_cr_inv2 / k_cr_inv_side<4, true>; BP = 64) gives the oracle's results,
+    inside the side-work launches and alone, across a trajectory."""
+    O = oracle
+    monkeypatch.setenv("DWHMC_CR_INV2", "1")
+    monkeypatch.setenv("DWHMC_CR_SIDE", side)
+    p, dis, Delta = make_case(O, Lx, Ly, 8.0, seed=Lx * 7 + Ly, amp=0.1)
+    cache, F_ref, Ef_ref = O.evaluate(p, dis, Delta)
+    ctx = device_ctx(dwhmc, p, dis, "cr")
+    ctx.set_pairing(Delta)
+    ctx.factorize()
+    assert np.max(np.abs(ctx.forces()[0] - F_ref)) <= 1e-10 * (1 + np.max(np.abs(F_ref)))
+    assert abs(ctx.fermion_energy()[0] - Ef_ref) <= 1e-11 * abs(Ef_ref)
+    hole_ref = O.measure_observables(cache, p, Delta)["hole_conc"]
+    assert abs(2.0 * ctx.hole_trace()[0] / p.N - 1.0 - hole_ref) <= 1e-11
+    Nt = 3
+    dt = O.calc_optimal_dt(p.beta, p.J, p.mass, Nt)
+    rng = np.random.default_rng(4)
+    draws = [((rng.standard_normal((p.N, 2)) + 1j * rng.standard_normal((p.N, 2))) * math.sqrt(0.5),
+              float(rng.random())) for _ in range(2)]
+    ref = _oracle_after_sweeps(O, p, dis, Delta, draws, Nt, dt)
+    for (noise, u), (acc_r, dH_r, D_r, _) in zip(draws, ref):
+        acc, dH = ctx.hmc_sweep(noise, np.array([u]), Nt, dt, p.mass)
+        assert bool(acc[0]) == acc_r and abs(dH[0] - dH_r) <= 1e-8 * (1 + abs(dH_r))
+        assert np.max(np.abs(ctx.get_state()[0][0] - D_r)) <= 1e-10
+    ctx.close()
+
+
 def test_split_trajectory_matches_sweep(dwhmc, oracle):
     """dwh_hmc_trajectory + dwh_hmc_finish (the host decides acceptance, as the
     Julia binding does to consume its RNG like src/HMC.jl:128) reproduce
