@@ -269,11 +269,21 @@ def main(argv=None):
             setattr(a, k, preset[k])
     workload = (f"L={a.L} beta={a.beta:g} {a.chains} chain(s)/GPU (custom)" if custom else preset["label"])
     dist = None
+    # DWHMC_BENCH_BACKEND=gloo: rehearsal of the multi-rank logic with ranks
+    # sharing fewer GPUs (collectives on host tensors); the driver's runs use
+    # the default, RCCL over xGMI with one GPU per rank
+    backend = os.environ.get("DWHMC_BENCH_BACKEND", "nccl")
+    tdev = "cpu"
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "gloo":
+            local = local % max(1, torch.cuda.device_count())
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            tdev = f"cuda:{local}"
 
     import dwhmc_loader
     m = dwhmc_loader.load_package()
@@ -316,7 +326,7 @@ def main(argv=None):
     gc.enable()
     if dist is not None:
         import torch
-        t = torch.tensor([el], dtype=torch.float64, device=f"cuda:{local}")
+        t = torch.tensor([el], dtype=torch.float64, device=tdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
         dist.barrier()
@@ -348,7 +358,7 @@ def main(argv=None):
     obs = np.array([acc.mean(), dH.mean(), float(np.mean(np.exp(-dH)))], dtype=np.float64)
     if dist is not None:
         import torch
-        t = torch.tensor(obs, device=f"cuda:{local}")
+        t = torch.tensor(obs, device=tdev)
         gl = [torch.zeros_like(t) for _ in range(world)] if rank == 0 else None
         dist.gather(t, gl, dst=0)
         if rank == 0:
@@ -386,6 +396,8 @@ def main(argv=None):
             "ref_equiv_tflops": leap * (40.0 / 3.0) * (2 * N) ** 3 / el / 1e12,
             "dense_equiv_tflops": leap * P * 8.0 * N ** 3 / el / 1e12,
         }
+        if world > 1 and backend == "gloo":
+            rec["rehearsal"] = f"gloo collectives, {world} ranks on {torch.cuda.device_count()} GPU(s): not a scaling measurement"
         if not cr:
             rec["alg_tflops"] = rec["dense_equiv_tflops"]
         if kern:
