@@ -597,13 +597,15 @@ def test_low_temperature_matches_oracle(dwhmc, oracle, L, beta, algo3):
     ctx.close()
 
 
-@pytest.mark.parametrize("L,beta", [(32, 1000.0), (24, 10000.0)])
-def test_low_temperature_large_lattice_cr(dwhmc, oracle, L, beta):
-    """The CR path at the extended table's κ (29-40 pole pairs) on the C3
-    lattice and a 24 x 24 one: the longest CR chains at the worst-conditioned
-    resolvents (cond ≈ βE'/π), same tolerances."""
+@pytest.mark.parametrize("Lx,Ly,beta", [(32, 32, 1000.0), (24, 24, 10000.0), (64, 4, 1000.0), (48, 6, 5000.0),
+                                        (13, 9, 20000.0)])
+def test_low_temperature_large_lattice_cr(dwhmc, oracle, Lx, Ly, beta):
+    """The CR path at the extended table's κ (29-43 pole pairs) on the C3
+    lattice, a 24 x 24 one and the BP = 128 / 96 / 32 block sizes: the longest
+    CR chains at the worst-conditioned resolvents (cond ≈ βE'/π), same
+    tolerances."""
     O = oracle
-    p, dis, Delta = make_case(O, L, L, beta, seed=7 * L + int(beta))
+    p, dis, Delta = make_case(O, Lx, Ly, beta, seed=7 * Lx + Ly + int(beta))
     cache, F_ref, Ef_ref = O.evaluate(p, dis, Delta)
     P_ref, _ = O.pairing_P(cache.U, cache.E_n, p)
     ctx = device_ctx(dwhmc, p, dis, "cr")
