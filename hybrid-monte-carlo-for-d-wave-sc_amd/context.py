@@ -44,7 +44,9 @@ ALGOS = {"auto": -1, "dense": 0, "cr": 1, "eig": 2}
 
 class FermionContext:
     """Device-resident fermionic action/force evaluator for nchains chains.
-    delta_cap <= 0 selects the ABI default max(2, 6 sqrt(2J/β)) for the guard
+    delta_cap <= 0 selects the ABI default for the guard (bond guard on
+    max|Δ_ij|: max(2, 6 sqrt(2J/β)); site guard on the mean |Δ| of a site's
+    4 bonds, CR path with 2 Lx in 33..64: max(1.25, 4 sqrt(2J/β)))
     on max|Δ_ij|; an uploaded Δ or a trajectory beyond it re-selects the pole
     set (include/dwhmc.h)."""
 

@@ -539,6 +539,11 @@ struct dwh_ctx {
   Dims d{};
   int64_t Lx = 0, Ly = 0;
   double t = 0, tp = 0, mu = 0, beta = 0, J = 0, delta_cap = 2.0;
+  // guard: per site (mean |Δ| of its 4 bonds <= delta_cap, checked by the
+  // level-0 inversion launch) or per bond (|Δ_ij| <= delta_cap, the drift kernels)
+  bool site_guard = false;
+  std::vector<int> site4_host;   // per site: the Delta indices of its 4 bonds
+  int* site4 = nullptr;
   double kappa = 0, Ebound = 0, Cx = 0, err_tanh = 0, hmax = 0;
   std::vector<double> y, cq;
   // creation inputs kept for a pole re-selection (reselect_poles)
@@ -820,7 +825,8 @@ void cr_enqueue(dwh_ctx* ctx) {
     } else if (st.kind == 0 && st.l0) {
       Scope s(ctx, T_CR_INV, st.n * bp3);
       dwh::launch_cr_inv0(c, ctx->bpool, ctx->d_inv_blk + st.first, ctx->d_inv0_r, ctx->d_inv_dst + st.first,
-                          ctx->d_inv_slot + st.first, st.n, ctx->ldpart, ctx->ldA, ctx->stream);
+                          ctx->d_inv_slot + st.first, st.n, ctx->ldpart, ctx->ldA, ctx->stream,
+                          ctx->site_guard ? ctx->Delta : nullptr, ctx->site4, 4.0 * ctx->delta_cap, ctx->flag);
     } else if (st.kind == 0) {
       Scope s(ctx, T_CR_INV, st.n * bp3);
       dwh::launch_cr_inv(c, ctx->bpool, ctx->d_inv_blk + st.first, ctx->d_inv_dst + st.first,
@@ -834,7 +840,9 @@ void cr_enqueue(dwh_ctx* ctx) {
 }
 
 dwh::KickDrift kickdrift(dwh_ctx* ctx, double kick, double drift) {
-  return dwh::KickDrift{kick, drift, ctx->delta_cap, ctx->flag};
+  // the site guard is checked by k_cr_inv0, not per bond by the drift
+  const double cap = ctx->site_guard ? std::numeric_limits<double>::infinity() : ctx->delta_cap;
+  return dwh::KickDrift{kick, drift, cap, ctx->flag};
 }
 
 int transport_prepare(dwh_ctx* ctx, int64_t nw, int64_t nd, int slots);
@@ -979,9 +987,10 @@ int check_flag(dwh_ctx* ctx) {
     HIPCHECK(ctx, hipMemsetAsync(ctx->flag, 0, sizeof(int), ctx->stream));
     char buf[256];
     std::snprintf(buf, sizeof buf,
-                  "|Delta_ij| exceeded delta_cap=%g: the pole set was built for spectra within "
+                  "%s exceeded delta_cap=%g: the pole set was built for spectra within "
                   "E'=%g; recreate the context with a larger delta_cap",
-                  ctx->delta_cap, ctx->Ebound);
+                  ctx->site_guard ? "the mean |Delta| of a site's bonds" : "|Delta_ij|", ctx->delta_cap,
+                  ctx->Ebound);
     return fail(ctx, DWH_ERR_SPECTRUM, buf);
   }
   return DWH_OK;
@@ -1090,10 +1099,17 @@ double spectral_radius_bound(const std::vector<std::vector<std::pair<int, double
   return 1.02 * rho + 1e-12;
 }
 
-// Default guard on max|Δ_ij|: 2 (the ordered phase), or 6 standard deviations
-// of the Gaussian boson fluctuations <|Δ|²> = 2J/β at high temperature.
-double default_delta_cap(double beta, double J) {
-  return std::max(2.0, 6.0 * std::sqrt(2.0 * std::fabs(J) / beta));
+// Default guard cap.  Bond guard (max|Δ_ij| <= cap): 2 (the ordered phase), or
+// 6 standard deviations of the Gaussian boson fluctuations <|Δ|²> = 2J/β at
+// high temperature.  Site guard (the mean of |Δ| over each site's four bonds
+// <= cap, CR path with k_cr_inv0): max(1.25, 4 sqrt(2J/β)) — the same ≈ 1.6x
+// margin over the largest value thermalised L = 32 chains reach (site mean
+// 0.79 / 1.08 / 1.49 at β = 16 / 8 / 4 over 300 sweeps against max|Δ_ij|
+// 1.27 / 1.78 / 2.49, tools/delta_stats.py, profiles/r02_delta_stats.txt).
+// Either way the pairing block's norm is at most its max row sum <= 2 cap.
+double default_delta_cap(double beta, double J, bool site_guard) {
+  const double s = std::sqrt(2.0 * std::fabs(J) / beta);
+  return site_guard ? std::max(1.25, 4.0 * s) : std::max(2.0, 6.0 * s);
 }
 
 int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, double mu, double beta,
@@ -1109,7 +1125,6 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
   const int64_t N64 = Lx * Ly;
   if (N64 > 9216) return fail(nullptr, DWH_ERR_ARG, "N = Lx*Ly > 9216 not supported (LDS row staging)");
   const int N = (int)N64;
-  if (delta_cap <= 0) delta_cap = default_delta_cap(beta, J);
   for (int64_t e = 0; e < 4 * N64; ++e)
     if (nn[e] < 1 || nn[e] > N64 || nnn[e] < 1 || nnn[e] > N64)
       return fail(nullptr, DWH_ERR_ARG, "neighbour table entry out of [1, N]");
@@ -1199,7 +1214,8 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
 
   // --- pole selection: E' >= ‖H_BdG‖ <= ‖h‖ + ‖pairing block‖ with
   // ‖h‖ <= min(Gershgorin, Lanczos bound) and the pairing block's norm <= its
-  // max row sum 4 |Δ|/2 <= 2 delta_cap
+  // max row sum Σ_j |Δ_ij|/2 <= 2 delta_cap (bond guard: each of the 4 bonds
+  // <= cap; site guard: their mean <= cap)
   {
     double rho = 0;
     std::vector<double> diag(N);
@@ -1209,8 +1225,6 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     }
     hmax = std::min(hmax, rho);
   }
-  const double Eb = hmax + 2.0 * delta_cap;
-  const double kneed = 0.5 * beta * Eb;
   // algorithm: explicit request, else DWHMC_ALGO = dense | cr | eig | auto
   // (auto: cr when the lattice-row block 2 Lx fits a supported padded size,
   // else dense; eig when κ = β E'/2 is beyond the pole table)
@@ -1221,6 +1235,16 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
   else if (const char* e = std::getenv("DWHMC_ALGO")) want = e;
   if (want != "auto" && want != "dense" && want != "cr" && want != "eig")
     return fail(nullptr, DWH_ERR_ARG, "DWHMC_ALGO must be auto, dense, cr or eig");
+  // site guard where the CR path's level-0 inversions (k_cr_inv0) check it
+  const bool site_guard = [&] {
+    const int BPc = (int)(2 * ((Lx + 15) / 16 * 16));
+    const char* e0 = std::getenv("DWHMC_CR_INV0");
+    const bool cr = want == "cr" || (want == "auto" && dwh::cr_supported_bp(BPc));
+    return cr && dwh::cr_supported_inv0(BPc) && !(e0 && *e0 == '0');
+  }();
+  if (delta_cap <= 0) delta_cap = default_delta_cap(beta, J, site_guard);
+  const double Eb = hmax + 2.0 * delta_cap;
+  const double kneed = 0.5 * beta * Eb;
   int sel = -1;
   for (int e = 0; e < kPoleTableSize; ++e)
     if (kPoleEntries[e].kappa >= kneed * (1.0 - 1e-12)) {
@@ -1262,6 +1286,7 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
   ctx->beta = beta;
   ctx->J = J;
   ctx->delta_cap = delta_cap;
+  ctx->site_guard = site_guard && !eig;
   // x-current operator J [src/Observables.jl:237-283]: i t at (i, i+x), i t' at
   // (i, i+x+y) and (i, i+x-y), plus their conjugate transposes, summed into CSR
   // (SparseArrays.sparse adds duplicates); stored as imaginary parts
@@ -1445,6 +1470,7 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
   ALLOC(Hold, (size_t)d.nc);
   ALLOC(Hnew, (size_t)d.nc);
   ALLOC(flag, 1);
+  if (ctx->site_guard) ALLOC(site4, 4 * (size_t)N);
   ALLOC(s_noise, nbond);
   ALLOC(s_uniform, (size_t)d.nc);
   ALLOC(s_acc, (size_t)d.nc);
@@ -1466,6 +1492,17 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
   UP(hval, hval.data(), hval.size());
   UP(bond_ij, bij.data(), bij.size());
   UP(bond_ji, bji.data(), bji.size());
+  if (ctx->site_guard) {
+    // site i: bonds (i, +x), (i, +y), (i - x, +x), (i - y, +y) in the N x 2 Δ layout
+    ctx->site4_host.resize(4 * (size_t)N);
+    for (int i = 0; i < N; ++i) {
+      ctx->site4_host[4 * i + 0] = i;
+      ctx->site4_host[4 * i + 1] = N + i;
+      ctx->site4_host[4 * i + 2] = (int)(nn[2 * N64 + i] - 1);
+      ctx->site4_host[4 * i + 3] = N + (int)(nn[3 * N64 + i] - 1);
+    }
+    UP(site4, ctx->site4_host.data(), ctx->site4_host.size());
+  }
   if (ctx->algo == ALGO_CR) {
     const CrPlan& pl = ctx->plan;
     UP(d_tasks, pl.tasks.data(), pl.tasks.size());
@@ -1941,8 +1978,9 @@ int reselect_poles(dwh_ctx* ctx, double new_cap) {
   return DWH_OK;
 }
 
-// Host-side guard for an uploaded Δ: re-select the poles when max|Δ_ij| is
-// above the cap (the reference accepts any Δ, src/HMC.jl:98-114).
+// Host-side guard for an uploaded Δ: re-select the poles when max|Δ_ij| (bond
+// guard) or the largest mean |Δ| over a site's bonds (site guard) is above
+// the cap (the reference accepts any Δ, src/HMC.jl:98-114).
 int fit_cap(dwh_ctx* ctx, const dwh_c128* D, size_t n, bool* reselected = nullptr) {
   if (reselected) *reselected = false;
   double m = 0;
@@ -1950,6 +1988,19 @@ int fit_cap(dwh_ctx* ctx, const dwh_c128* D, size_t n, bool* reselected = nullpt
     const double a = std::hypot(D[k].re, D[k].im);
     if (!std::isfinite(a)) return fail(ctx, DWH_ERR_ARG, "non-finite Delta");
     m = std::max(m, a);
+  }
+  if (ctx->site_guard) {
+    const size_t N = (size_t)ctx->d.N, nc = n / (2 * N);
+    m = 0;
+    for (size_t c = 0; c < nc; ++c)
+      for (size_t i = 0; i < N; ++i) {
+        double sm = 0;
+        for (int k = 0; k < 4; ++k) {
+          const dwh_c128 v = D[c * 2 * N + ctx->site4_host[4 * i + k]];
+          sm += std::hypot(v.re, v.im);
+        }
+        m = std::max(m, 0.25 * sm);
+      }
   }
   if (m <= ctx->delta_cap) return DWH_OK;
   if (reselected) *reselected = true;

@@ -587,11 +587,32 @@ __global__ __launch_bounds__(256) void k_cr_inv0(double2* __restrict__ pool, int
                                                  const int* __restrict__ blk, const int* __restrict__ rblk,
                                                  const int* __restrict__ dst, const int* __restrict__ slot,
                                                  double* __restrict__ ldpart,
-                                                 const double* __restrict__ ldA, int nslots) {
+                                                 const double* __restrict__ ldA, int nslots,
+                                                 const double2* __restrict__ Delta,
+                                                 const int* __restrict__ site4, int N, int P, double cap4,
+                                                 int* __restrict__ flag) {
   constexpr int BP = 64, HP = 32, TSZ = 16 * 17;
   __shared__ double2 sR[4][TSZ], sB[4][TSZ], sZ[4][TSZ], sS[4][TSZ], sX[4][TSZ], sA[4][TSZ];
   __shared__ double ldw[2];
   const int bi = blockIdx.y, li = blockIdx.x;
+  // site guard (launch_cr_inv0 with Delta): the extra last workgroup column,
+  // pole 0 of each chain, on a CU the inversions leave idle
+  if (Delta != nullptr && li == (int)gridDim.x - 1) {
+    if (bi % P != 0) return;
+    const double2* D = Delta + (int64_t)(bi / P) * 2 * N;
+    bool over = false;
+    for (int i = threadIdx.x; i < N; i += blockDim.x) {
+      double sm = 0.0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const double2 v = D[site4[4 * i + k]];
+        sm += sqrt(fma(v.x, v.x, v.y * v.y));
+      }
+      over = over || !(sm <= cap4);
+    }
+    if (over) *flag = 1;
+    return;
+  }
   const double2* D = pool + (int64_t)bi * item + (int64_t)blk[li] * HP * BP;
   const double2* Rm = pool + (int64_t)bi * item + (int64_t)rblk[li] * HP * BP;
   double2* Mo = pool + (int64_t)bi * item + (int64_t)dst[li] * HP * BP;
@@ -1234,10 +1255,12 @@ void launch_cr_tail(const CrDims& c, double2* pool, const int* blk, const int* d
 }
 
 void launch_cr_inv0(const CrDims& c, double2* pool, const int* blk, const int* rblk, const int* dst,
-                    const int* slot, int n, double* ldpart, const double* ldA, hipStream_t s) {
+                    const int* slot, int n, double* ldpart, const double* ldA, hipStream_t s,
+                    const double2* Delta, const int* site4, double cap4, int* flag) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_cr_inv0, dim3(n, c.nbatch), dim3(256), 0, s, pool, c.item, blk, rblk, dst, slot, ldpart,
-                     ldA, c.Ly);
+  const bool guard = Delta != nullptr && site4 != nullptr && flag != nullptr;
+  hipLaunchKernelGGL(k_cr_inv0, dim3(n + (guard ? 1 : 0), c.nbatch), dim3(256), 0, s, pool, c.item, blk, rblk,
+                     dst, slot, ldpart, ldA, c.Ly, guard ? Delta : nullptr, site4, c.N, c.P, cap4, flag);
 }
 
 void launch_cr_fill(const CrDims& c, double2* pool, const int* list, int nlist, const int* hcol,

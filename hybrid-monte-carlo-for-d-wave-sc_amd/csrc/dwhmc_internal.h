@@ -87,8 +87,12 @@ void launch_cr_inv(const CrDims& c, double2* pool, const int* blk, const int* ds
 // level-0 inversions of blocks blk[i] (BP = 64) from the static R = A^-1
 // blocks rblk[i] (k_cr_inv0); ln|det| = ldA/2 + ln|det S| into ldpart slots
 bool cr_supported_inv0(int BP);
+// Delta != nullptr: one extra workgroup per chain checks the site guard
+// (Σ of |Δ| over each site's 4 bonds site4[4 i ..] <= cap4, else *flag = 1)
 void launch_cr_inv0(const CrDims& c, double2* pool, const int* blk, const int* rblk, const int* dst,
-                    const int* slot, int n, double* ldpart, const double* ldA, hipStream_t s);
+                    const int* slot, int n, double* ldpart, const double* ldA, hipStream_t s,
+                    const double2* Delta = nullptr, const int* site4 = nullptr, double cap4 = 0.0,
+                    int* flag = nullptr);
 // the same inversions plus nst side-work product tasks per batch item
 // (32 x 32 wave tiles, maxt32 per task, each task's sign in bq & kCrNegBit)
 // on the CUs the inversions leave idle

@@ -48,7 +48,9 @@ typedef struct {
   double kappa;       /* β·E'/2 of the pole table entry in use (eig: of the spectral bound) */
   double e_bound;     /* E' : spectral bound the poles are valid on */
   double err_tanh;    /* sup |tanh - rational| of the table entry (eig: 0) */
-  double delta_cap;   /* guard on max|Δ_ij| (eig: DBL_MAX, no guard) */
+  double delta_cap;   /* guard cap: on max|Δ_ij| (bond guard), or on the mean |Δ| of each site's
+                         4 bonds (site guard: the CR path with 2 Lx in 33..64, whose level-0
+                         inversion launch checks it); eig: DBL_MAX, no guard */
   int64_t device_bytes;
   int64_t algo;       /* 0 = dense Schur-complement Gauss-Jordan, 1 = block cyclic reduction,
                          2 = eigendecomposition */
@@ -57,7 +59,8 @@ typedef struct {
 
 /* ModelParameters + initialize_cache + init_static_H!
  * [src/Types.jl:49-91, src/Types.jl:182-212, src/Hamiltonian.jl:10-47].
- * One chain, default delta_cap (max(2, 6 sqrt(2J/β))).  disorder: length N
+ * One chain, default delta_cap (bond guard max(2, 6 sqrt(2J/β)); site guard
+ * max(1.25, 4 sqrt(2J/β))).  disorder: length N
  * (state.disorder_pot). */
 int dwh_create(dwh_ctx** ctx, int64_t Lx, int64_t Ly, double t, double tp, double mu,
                double beta, double J, const int64_t* nn_table, const int64_t* nnn_table,
@@ -65,7 +68,9 @@ int dwh_create(dwh_ctx** ctx, int64_t Lx, int64_t Ly, double t, double tp, doubl
 
 /* Batched form: nchains independent Markov chains / disorder realisations on one
  * device (disorder: nchains*N).  delta_cap <= 0 selects the default
- * max(2, 6 sqrt(2J/β)); the pole set covers |Δ_ij| <= delta_cap and is
+ * (bond guard max(2, 6 sqrt(2J/β)), site guard max(1.25, 4 sqrt(2J/β)));
+ * either guard bounds the pairing block's norm by 2 delta_cap; the pole set
+ * covers spectra within ‖h‖ + 2 delta_cap and is
  * re-selected for a larger cap when an uploaded Δ or a trajectory exceeds it. */
 int dwh_create_batched(dwh_ctx** ctx, int64_t Lx, int64_t Ly, double t, double tp, double mu,
                        double beta, double J, const int64_t* nn_table, const int64_t* nnn_table,

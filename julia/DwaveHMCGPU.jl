@@ -43,7 +43,7 @@ mutable struct GPUCache
     delta_cap::Float64
 end
 
-function GPUCache(p::ModelParameters; device::Integer=0, delta_cap::Real=0.0)   # <= 0: max(2, 6 sqrt(2J/β))
+function GPUCache(p::ModelParameters; device::Integer=0, delta_cap::Real=0.0)   # <= 0: the ABI default (include/dwhmc.h)
     c = GPUCache(C_NULL, zeros(ComplexF64, p.N, 2), 0.0, Int32(device), Float64(delta_cap))
     finalizer(c) do c
         c.ctx == C_NULL || ccall((:dwh_destroy, libdwhmc), Cvoid, (Ptr{Cvoid},), c.ctx)

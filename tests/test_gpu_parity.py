@@ -289,6 +289,98 @@ def test_default_delta_cap_follows_temperature(dwhmc, oracle):
         ctx.close()
 
 
+def _site_mean_max(D, p):
+    a = np.abs(D)
+    nn = p.nn_table - 1
+    return float(np.max(0.25 * (a[:, 0] + a[:, 1] + a[nn[:, 2], 0] + a[nn[:, 3], 1])))
+
+
+def test_site_guard_default_cap(dwhmc, oracle):
+    """CR contexts with 2 Lx in 33..64 guard the mean |Δ| over each site's four
+    bonds (checked by the level-0 inversion launch), default max(1.25,
+    4 sqrt(2J/β)); E' = ‖h‖ + 2 cap bounds the spectrum either way.  At the
+    C3 workload that is 13 pole pairs instead of 14."""
+    O = oracle
+    for beta in (16.0, 2.0):
+        p, dis, _ = make_case(O, 20, 20, beta, seed=5)
+        ctx = device_ctx(dwhmc, p, dis, "cr", delta_cap=0.0)
+        assert ctx.info["delta_cap"] == pytest.approx(max(1.25, 4.0 * math.sqrt(2 * J / beta)))
+        assert ctx.info["e_bound"] >= ctx.info["delta_cap"] * 2
+        ctx.close()
+    p, dis, _ = make_case(O, 32, 32, 16.0, seed=1000)
+    ctx = device_ctx(dwhmc, p, dis, "cr", delta_cap=0.0)
+    assert ctx.info["npoles"] == 13
+    ctx.close()
+
+
+def test_site_guard_reselects_on_upload(dwhmc, oracle):
+    """Site guard: an uploaded Δ whose largest site mean exceeds the cap
+    re-selects the poles for 1.5 x that mean; results match the oracle."""
+    O = oracle
+    p, dis, Delta = make_case(O, 20, 6, 8.0, seed=21, amp=0.9)
+    ctx = device_ctx(dwhmc, p, dis, "cr", delta_cap=0.3)
+    kap0 = ctx.info["kappa"]
+    ctx.set_pairing(Delta)
+    m = _site_mean_max(Delta, p)
+    assert ctx.info["delta_cap"] >= 1.5 * m * (1 - 1e-12) and ctx.info["kappa"] > kap0
+    ctx.factorize()
+    _, F_ref, Ef_ref = O.evaluate(p, dis, Delta)
+    assert np.max(np.abs(ctx.forces()[0] - F_ref)) <= 1e-10 * (1 + np.max(np.abs(F_ref)))
+    assert abs(ctx.fermion_energy()[0] - Ef_ref) <= 1e-11 * abs(Ef_ref)
+    ctx.close()
+
+
+def test_site_guard_reselects_mid_sweep(dwhmc, oracle):
+    """Site guard: a trajectory whose drift takes a site mean past the cap is
+    rerun from its start with re-selected poles (the level-0 inversion launch
+    sets the flag); the result equals a context built with the final cap and
+    matches the oracle."""
+    O = oracle
+    p, dis, Delta0 = make_case(O, 20, 4, 4.0, seed=22, amp=0.0)
+    rng = np.random.default_rng(23)
+    noise = 8.0 * (rng.standard_normal((p.N, 2)) + 1j * rng.standard_normal((p.N, 2))) * math.sqrt(0.5)
+    Nt, dt = 4, 0.1
+    a = device_ctx(dwhmc, p, dis, "cr", delta_cap=0.2)
+    a.set_pairing(Delta0)
+    a.factorize()
+    acc_a, dH_a = a.hmc_sweep(noise, np.array([0.3]), Nt, dt, p.mass)
+    cap = a.info["delta_cap"]
+    assert cap > 0.2
+    b = device_ctx(dwhmc, p, dis, "cr", delta_cap=cap)
+    b.set_pairing(Delta0)
+    b.factorize()
+    acc_b, dH_b = b.hmc_sweep(noise, np.array([0.3]), Nt, dt, p.mass)
+    assert acc_a[0] == acc_b[0] and dH_a[0] == dH_b[0]
+    for x, y in zip(a.get_state(), b.get_state()):
+        assert np.array_equal(x, y)
+    cache = O.initialize_cache(p)
+    O.init_static_H(cache, p, dis)
+    O.update_H_BdG(cache, p, Delta0)
+    O.diagonalize_H_BdG(cache, p)
+    st = O.SimulationState(dis, Delta0.copy(), np.zeros_like(Delta0))
+    acc_r, dH_r = O.hmc_sweep(cache, p, st, Nt, dt, noise, 0.3)
+    assert acc_a[0] == acc_r and abs(dH_a[0] - dH_r) <= 1e-8 * (1 + abs(dH_r))
+    a.close()
+    b.close()
+
+
+def test_site_guard_throughput_path_reports(dwhmc, oracle):
+    """The throughput path (dwh_run_sweeps) does not return to the host between
+    sweeps: a site-guard trip there is reported by dwh_sweep_results."""
+    O = oracle
+    p, dis, Delta0 = make_case(O, 20, 4, 4.0, seed=24, amp=0.0)
+    rng = np.random.default_rng(25)
+    noise = 8.0 * (rng.standard_normal((1, 1, p.N, 2)) + 1j * rng.standard_normal((1, 1, p.N, 2))) * math.sqrt(0.5)
+    ctx = device_ctx(dwhmc, p, dis, "cr", delta_cap=0.2)
+    ctx.set_pairing(Delta0)
+    ctx.factorize()
+    ctx.load_draws(noise, np.array([[0.3]]))
+    ctx.run_sweeps(0, 1, 4, 0.1, p.mass)
+    with pytest.raises(Exception):
+        ctx.sweep_results(0, 1)
+    ctx.close()
+
+
 def test_high_temperature_sweeps_match_oracle(dwhmc, oracle):
     """T = 2 (β = 0.5): |Δ| ~ sqrt(2J/β) ~ 1.8, beyond the old fixed cap of 2 in a
     few bonds; sweeps run without a guard failure and match the oracle."""
