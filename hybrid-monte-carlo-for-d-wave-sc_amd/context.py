@@ -46,7 +46,7 @@ class FermionContext:
     """Device-resident fermionic action/force evaluator for nchains chains.
     delta_cap <= 0 selects the ABI default for the guard (bond guard on
     max|Δ_ij|: max(2, 6 sqrt(2J/β)); site guard on the mean |Δ| of a site's
-    4 bonds, CR path with 2 Lx in 33..64: max(1.25, 4 sqrt(2J/β)))
+    4 bonds, CR path: max(1.25, 4 sqrt(2J/β)))
     on max|Δ_ij|; an uploaded Δ or a trajectory beyond it re-selects the pole
     set (include/dwhmc.h)."""
 

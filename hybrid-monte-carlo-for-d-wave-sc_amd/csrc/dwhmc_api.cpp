@@ -800,6 +800,10 @@ void cr_enqueue(dwh_ctx* ctx) {
   }
   const CrPlan& plan = ctx->plan;
   size_t next_tail = 0;
+  // the site guard rides on the first (level-0) inversion launch: every
+  // factorised Δ passes through it
+  dwh::SiteGuard guard;
+  if (ctx->site_guard) guard = dwh::SiteGuard{ctx->Delta, ctx->site4, 4.0 * ctx->delta_cap, ctx->flag};
   for (size_t si = 0; si < plan.stages.size(); ++si) {
     if (next_tail < plan.tails.size() && plan.tails[next_tail].first == (int)si) {
       const CrTailSeg& tg = plan.tails[next_tail++];
@@ -821,16 +825,19 @@ void cr_enqueue(dwh_ctx* ctx) {
       Scope s(ctx, T_CR_INVSIDE, st.n * bp3 + st.flops * c.nbatch);
       dwh::launch_cr_inv_side(c, ctx->bpool, ctx->d_inv_blk + st.first, ctx->d_inv_dst + st.first,
                               ctx->d_inv_slot + st.first, st.n, ctx->ldpart, ctx->d_tasks + st.tfirst,
-                              st.ntiles, st.maxt32, ctx->stream);
+                              st.ntiles, st.maxt32, ctx->stream, guard);
+      guard = dwh::SiteGuard{};
     } else if (st.kind == 0 && st.l0) {
       Scope s(ctx, T_CR_INV, st.n * bp3);
       dwh::launch_cr_inv0(c, ctx->bpool, ctx->d_inv_blk + st.first, ctx->d_inv0_r, ctx->d_inv_dst + st.first,
-                          ctx->d_inv_slot + st.first, st.n, ctx->ldpart, ctx->ldA, ctx->stream,
-                          ctx->site_guard ? ctx->Delta : nullptr, ctx->site4, 4.0 * ctx->delta_cap, ctx->flag);
+                          ctx->d_inv_slot + st.first, st.n, ctx->ldpart, ctx->ldA, ctx->stream, guard.Delta,
+                          guard.site4, guard.cap4, guard.flag);
+      guard = dwh::SiteGuard{};
     } else if (st.kind == 0) {
       Scope s(ctx, T_CR_INV, st.n * bp3);
       dwh::launch_cr_inv(c, ctx->bpool, ctx->d_inv_blk + st.first, ctx->d_inv_dst + st.first,
-                         ctx->d_inv_slot + st.first, st.n, ctx->ldpart, ctx->stream);
+                         ctx->d_inv_slot + st.first, st.n, ctx->ldpart, ctx->stream, guard);
+      guard = dwh::SiteGuard{};
     } else {
       Scope s(ctx, T_CR_GEMM, st.flops * c.nbatch);
       dwh::launch_cr_gemm(c, ctx->bpool, ctx->d_tasks + st.first, st.n, st.maxt32, st.maxt16,
@@ -1102,7 +1109,7 @@ double spectral_radius_bound(const std::vector<std::vector<std::pair<int, double
 // Default guard cap.  Bond guard (max|Δ_ij| <= cap): 2 (the ordered phase), or
 // 6 standard deviations of the Gaussian boson fluctuations <|Δ|²> = 2J/β at
 // high temperature.  Site guard (the mean of |Δ| over each site's four bonds
-// <= cap, CR path with k_cr_inv0): max(1.25, 4 sqrt(2J/β)) — the same ≈ 1.6x
+// <= cap, CR path: its level-0 inversion launch checks it): max(1.25, 4 sqrt(2J/β)) — the same ≈ 1.6x
 // margin over the largest value thermalised L = 32 chains reach (site mean
 // 0.79 / 1.08 / 1.49 at β = 16 / 8 / 4 over 300 sweeps against max|Δ_ij|
 // 1.27 / 1.78 / 2.49, tools/delta_stats.py, profiles/r02_delta_stats.txt).
@@ -1235,12 +1242,10 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
   else if (const char* e = std::getenv("DWHMC_ALGO")) want = e;
   if (want != "auto" && want != "dense" && want != "cr" && want != "eig")
     return fail(nullptr, DWH_ERR_ARG, "DWHMC_ALGO must be auto, dense, cr or eig");
-  // site guard where the CR path's level-0 inversions (k_cr_inv0) check it
+  // site guard on the CR path (checked by its level-0 inversion launch)
   const bool site_guard = [&] {
     const int BPc = (int)(2 * ((Lx + 15) / 16 * 16));
-    const char* e0 = std::getenv("DWHMC_CR_INV0");
-    const bool cr = want == "cr" || (want == "auto" && dwh::cr_supported_bp(BPc));
-    return cr && dwh::cr_supported_inv0(BPc) && !(e0 && *e0 == '0');
+    return want == "cr" || (want == "auto" && dwh::cr_supported_bp(BPc));
   }();
   if (delta_cap <= 0) delta_cap = default_delta_cap(beta, J, site_guard);
   const double Eb = hmax + 2.0 * delta_cap;

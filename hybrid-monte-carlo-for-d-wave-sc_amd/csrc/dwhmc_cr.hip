@@ -402,14 +402,35 @@ __device__ __forceinline__ void cr_inv_wg(double2* __restrict__ pool, int64_t it
   CR_STAMP(5);
 }
 
+// the site guard of chain c (SiteGuard, dwhmc_internal.h): one workgroup
+__device__ __forceinline__ void site_guard_wg(const SiteGuard& sg, int N, int c) {
+  const double2* D = sg.Delta + (int64_t)c * 2 * N;
+  bool over = false;
+  for (int i = threadIdx.x; i < N; i += blockDim.x) {
+    double sm = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const double2 v = D[sg.site4[4 * i + k]];
+      sm += sqrt(fma(v.x, v.x, v.y * v.y));
+    }
+    over = over || !(sm <= sg.cap4);
+  }
+  if (over) *sg.flag = 1;
+}
+
 template <int NT>
 __global__ __launch_bounds__(64 * NT) void k_cr_inv(double2* __restrict__ pool, int64_t item,
                                                     const int* __restrict__ blk,
                                                     const int* __restrict__ dst,
                                                     const int* __restrict__ slot,
-                                                    double* __restrict__ ldpart, int nslots) {
+                                                    double* __restrict__ ldpart, int nslots,
+                                                    SiteGuard sg, int N, int P) {
   __shared__ double2 pan[2][NT][16 * 17];
   __shared__ double ldw[NT];
+  if (sg.Delta != nullptr && blockIdx.x == gridDim.x - 1) {   // the guard column, pole 0 of each chain
+    if (blockIdx.y % P == 0) site_guard_wg(sg, N, blockIdx.y / P);
+    return;
+  }
   cr_inv_wg<NT>(pool, item, blockIdx.y, blockIdx.x, blk, dst, slot, ldpart, nslots, pan, ldw);
 }
 
@@ -1015,11 +1036,18 @@ __global__ __launch_bounds__(64 * NT) void k_cr_inv_side(double2* __restrict__ p
                                                          double* __restrict__ ldpart, int nslots,
                                                          int ninv, int nbatch,
                                                          const CrTask* __restrict__ stasks, int nst,
-                                                         int maxt, int total) {
+                                                         int maxt, int total, SiteGuard sg, int N,
+                                                         int nchains) {
   static_assert(NT == 4, "side work runs 4-wave workgroups");
   __shared__ double2 pan[2][NT][16 * 17];
   __shared__ double ldw[NT];
   const int b = blockIdx.x, nall = ninv * nbatch;
+  // the last nchains workgroups check the site guard (level-0 launches)
+  const int ng = sg.Delta != nullptr ? nchains : 0, nside = (int)gridDim.x - nall - ng;
+  if (b >= nall + nside) {
+    site_guard_wg(sg, N, b - nall - nside);
+    return;
+  }
 #if defined(DWHMC_SIDE_NOP)     // diagnostic builds (tools/ab_bench.py LIB=...): side part empty
   if (b >= nall) return;
 #elif defined(DWHMC_SIDE_NOINV)  // inversion part empty
@@ -1035,7 +1063,7 @@ __global__ __launch_bounds__(64 * NT) void k_cr_inv_side(double2* __restrict__ p
     return;
   }
   cr_gemm_wg<16 * NT, 2, 1, 0, true>(pool, item, stasks, nst, maxt, nullptr, 0, total, 1.0,
-                                    xcd_remap(b - nall, (int)gridDim.x - nall));
+                                    xcd_remap(b - nall, nside));
 }
 
 // ---------------------------------------------------------------------------
@@ -1276,35 +1304,51 @@ void launch_cr_fill(const CrDims& c, double2* pool, const int* list, int nlist, 
 }
 
 void launch_cr_inv(const CrDims& c, double2* pool, const int* blk, const int* dst, const int* slot,
-                   int n, double* ldpart, hipStream_t s) {
+                   int n, double* ldpart, hipStream_t s, const SiteGuard& sg) {
   if (n <= 0) return;
-  const dim3 g(n, c.nbatch);
+  const bool guard = sg.Delta != nullptr;
+  if (c.BP == 64 && c.inv2) {
+    const dim3 g(n, c.nbatch);
+    hipLaunchKernelGGL(k_cr_inv2, g, dim3(64 * DWHMC_INV2_WAVES), 0, s, pool, c.item, blk, dst, slot, ldpart, c.Ly);
+    if (guard)   // the guard column alone (grid x = 1)
+      hipLaunchKernelGGL(k_cr_inv<4>, dim3(1, c.nbatch), dim3(256), 0, s, pool, c.item, blk, dst, slot, ldpart, c.Ly,
+                         sg, c.N, c.P);
+    return;
+  }
+  const dim3 g(n + (guard ? 1 : 0), c.nbatch);
   switch (c.BP) {
-    case 32: hipLaunchKernelGGL(k_cr_inv<2>, g, dim3(128), 0, s, pool, c.item, blk, dst, slot, ldpart, c.Ly); break;
-    case 64:
-      if (c.inv2)
-        hipLaunchKernelGGL(k_cr_inv2, g, dim3(64 * DWHMC_INV2_WAVES), 0, s, pool, c.item, blk, dst, slot, ldpart, c.Ly);
-      else hipLaunchKernelGGL(k_cr_inv<4>, g, dim3(256), 0, s, pool, c.item, blk, dst, slot, ldpart, c.Ly);
+    case 32:
+      hipLaunchKernelGGL(k_cr_inv<2>, g, dim3(128), 0, s, pool, c.item, blk, dst, slot, ldpart, c.Ly, sg, c.N, c.P);
       break;
-    case 96: hipLaunchKernelGGL(k_cr_inv<6>, g, dim3(384), 0, s, pool, c.item, blk, dst, slot, ldpart, c.Ly); break;
-    default: hipLaunchKernelGGL(k_cr_inv<8>, g, dim3(512), 0, s, pool, c.item, blk, dst, slot, ldpart, c.Ly); break;
+    case 64:
+      hipLaunchKernelGGL(k_cr_inv<4>, g, dim3(256), 0, s, pool, c.item, blk, dst, slot, ldpart, c.Ly, sg, c.N, c.P);
+      break;
+    case 96:
+      hipLaunchKernelGGL(k_cr_inv<6>, g, dim3(384), 0, s, pool, c.item, blk, dst, slot, ldpart, c.Ly, sg, c.N, c.P);
+      break;
+    default:
+      hipLaunchKernelGGL(k_cr_inv<8>, g, dim3(512), 0, s, pool, c.item, blk, dst, slot, ldpart, c.Ly, sg, c.N, c.P);
+      break;
   }
 }
 
 void launch_cr_inv_side(const CrDims& c, double2* pool, const int* blk, const int* dst, const int* slot,
-                        int n, double* ldpart, const CrTask* stasks, int nst, int maxt32, hipStream_t s) {
+                        int n, double* ldpart, const CrTask* stasks, int nst, int maxt32, hipStream_t s,
+                        const SiteGuard& sg) {
   if (nst <= 0) {
-    launch_cr_inv(c, pool, blk, dst, slot, n, ldpart, s);
+    launch_cr_inv(c, pool, blk, dst, slot, n, ldpart, s, sg);
     return;
   }
   const int total = c.nbatch * nst * maxt32;
   const int side_wg = (total + 3) / 4;
+  const int nc = c.nbatch / c.P;
+  const dim3 g(n * c.nbatch + side_wg + (sg.Delta != nullptr ? nc : 0));
   if (c.inv2)
-    hipLaunchKernelGGL((k_cr_inv_side<4, true>), dim3(n * c.nbatch + side_wg), dim3(256), 0, s, pool, c.item,
-                       blk, dst, slot, ldpart, c.Ly, n, c.nbatch, stasks, nst, maxt32, total);
+    hipLaunchKernelGGL((k_cr_inv_side<4, true>), g, dim3(256), 0, s, pool, c.item, blk, dst, slot, ldpart, c.Ly, n,
+                       c.nbatch, stasks, nst, maxt32, total, sg, c.N, nc);
   else
-    hipLaunchKernelGGL((k_cr_inv_side<4, false>), dim3(n * c.nbatch + side_wg), dim3(256), 0, s, pool, c.item,
-                       blk, dst, slot, ldpart, c.Ly, n, c.nbatch, stasks, nst, maxt32, total);
+    hipLaunchKernelGGL((k_cr_inv_side<4, false>), g, dim3(256), 0, s, pool, c.item, blk, dst, slot, ldpart, c.Ly, n,
+                       c.nbatch, stasks, nst, maxt32, total, sg, c.N, nc);
 }
 
 // Stage configuration (tile TS, K split).  16 x 16 tiles with a 4-way K

@@ -82,8 +82,17 @@ void launch_cr_fermion_energy(const CrDims& c, const double2* pool, const int64_
                               const double* ldpart, const double* cpole, double Cx, double beta,
                               double* part, unsigned* done, double* Ef, double* Trhh, hipStream_t s);
 // inverts blocks blk[i] into dst[i] (dst == blk: in place); ln|det| into ldpart slots
+// Site spectral guard, checked by one extra workgroup per chain of the level-0
+// inversion launch: Σ of |Δ| over each site's 4 bonds (site4[4 i ..], indices
+// into a chain's N x 2 Δ) <= cap4, else *flag = 1.  Delta == nullptr: off.
+struct SiteGuard {
+  const double2* Delta = nullptr;
+  const int* site4 = nullptr;
+  double cap4 = 0.0;
+  int* flag = nullptr;
+};
 void launch_cr_inv(const CrDims& c, double2* pool, const int* blk, const int* dst, const int* slot,
-                   int n, double* ldpart, hipStream_t s);
+                   int n, double* ldpart, hipStream_t s, const SiteGuard& sg = SiteGuard{});
 // level-0 inversions of blocks blk[i] (BP = 64) from the static R = A^-1
 // blocks rblk[i] (k_cr_inv0); ln|det| = ldA/2 + ln|det S| into ldpart slots
 bool cr_supported_inv0(int BP);
@@ -98,7 +107,8 @@ void launch_cr_inv0(const CrDims& c, double2* pool, const int* blk, const int* r
 // on the CUs the inversions leave idle
 bool cr_supported_side(int BP);
 void launch_cr_inv_side(const CrDims& c, double2* pool, const int* blk, const int* dst, const int* slot,
-                        int n, double* ldpart, const CrTask* stasks, int nst, int maxt32, hipStream_t s);
+                        int n, double* ldpart, const CrTask* stasks, int nst, int maxt32, hipStream_t s,
+                        const SiteGuard& sg = SiteGuard{});
 // Coarse tail (BP = 64): consecutive small stages in one launch with a
 // device-wide barrier between them.  A stage is an inversion list (+ side
 // tasks, as launch_cr_inv_side) or a 16 x 16 / 4-way K-split product list.

@@ -49,7 +49,7 @@ typedef struct {
   double e_bound;     /* E' : spectral bound the poles are valid on */
   double err_tanh;    /* sup |tanh - rational| of the table entry (eig: 0) */
   double delta_cap;   /* guard cap: on max|Δ_ij| (bond guard), or on the mean |Δ| of each site's
-                         4 bonds (site guard: the CR path with 2 Lx in 33..64, whose level-0
+                         4 bonds (site guard: the CR path, whose level-0
                          inversion launch checks it); eig: DBL_MAX, no guard */
   int64_t device_bytes;
   int64_t algo;       /* 0 = dense Schur-complement Gauss-Jordan, 1 = block cyclic reduction,

@@ -229,14 +229,16 @@ def test_throughput_path_equals_single_sweeps(dwhmc, oracle, algo3):
 def test_spectrum_guard_reselects_on_upload(dwhmc, oracle, algo):
     """An uploaded Δ above delta_cap re-selects the pole set for it (the
     reference accepts any Δ, src/HMC.jl:98-114) instead of silently using
-    poles that do not cover the spectrum."""
+    poles that do not cover the spectrum.  dense: bond guard (max|Δ_ij|);
+    cr: site guard (the largest mean |Δ| over a site's bonds)."""
     O = oracle
     p, dis, Delta0 = make_case(O, 4, 4, 4.0, seed=1, amp=0.9)
     ctx = device_ctx(dwhmc, p, dis, algo, delta_cap=0.5)
     kap0 = ctx.info["kappa"]
     ctx.set_pairing(Delta0)
     inf = ctx.info
-    assert inf["delta_cap"] >= 1.5 * np.max(np.abs(Delta0)) * (1 - 1e-12) and inf["kappa"] > kap0
+    m = np.max(np.abs(Delta0)) if algo == "dense" else _site_mean_max(Delta0, p)
+    assert inf["delta_cap"] >= 1.5 * m * (1 - 1e-12) and inf["kappa"] > kap0
     ctx.factorize()
     _, F_ref, Ef_ref = O.evaluate(p, dis, Delta0)
     assert np.max(np.abs(ctx.forces()[0] - F_ref)) <= 1e-10 * (1 + np.max(np.abs(F_ref)))
@@ -278,14 +280,19 @@ def test_spectrum_guard_reselects_mid_sweep(dwhmc, oracle, algo):
 
 
 def test_default_delta_cap_follows_temperature(dwhmc, oracle):
-    """delta_cap <= 0 selects max(2, 6 sqrt(2J/β)): wide enough for the boson
-    fluctuations of the reference's high-temperature scans
+    """delta_cap <= 0 selects max(2, 6 sqrt(2J/β)) for the bond guard (dense
+    path) and max(1.25, 4 sqrt(2J/β)) for the site guard (CR path): wide enough
+    for the boson fluctuations of the reference's high-temperature scans
     (scripts/batch_scan_T.jl:21-22 goes up to T = 1000)."""
     O = oracle
     for beta in (16.0, 0.5, 1e-3):
         p, dis, _ = make_case(O, 4, 4, beta, seed=4)
-        ctx = device_ctx(dwhmc, p, dis, "auto", delta_cap=0.0)
+        ctx = device_ctx(dwhmc, p, dis, "dense", delta_cap=0.0)
         assert ctx.info["delta_cap"] == pytest.approx(max(2.0, 6.0 * math.sqrt(2 * J / beta)))
+        ctx.close()
+        ctx = device_ctx(dwhmc, p, dis, "auto", delta_cap=0.0)
+        assert ctx.info["algo"] == 1
+        assert ctx.info["delta_cap"] == pytest.approx(max(1.25, 4.0 * math.sqrt(2 * J / beta)))
         ctx.close()
 
 
@@ -296,13 +303,13 @@ def _site_mean_max(D, p):
 
 
 def test_site_guard_default_cap(dwhmc, oracle):
-    """CR contexts with 2 Lx in 33..64 guard the mean |Δ| over each site's four
-    bonds (checked by the level-0 inversion launch), default max(1.25,
-    4 sqrt(2J/β)); E' = ‖h‖ + 2 cap bounds the spectrum either way.  At the
-    C3 workload that is 13 pole pairs instead of 14."""
+    """CR contexts guard the mean |Δ| over each site's four bonds (checked by
+    the level-0 inversion launch: k_cr_inv0, k_cr_inv or k_cr_inv_side),
+    default max(1.25, 4 sqrt(2J/β)); E' = ‖h‖ + 2 cap bounds the spectrum
+    either way.  At the C3 workload that is 13 pole pairs instead of 14."""
     O = oracle
-    for beta in (16.0, 2.0):
-        p, dis, _ = make_case(O, 20, 20, beta, seed=5)
+    for (Lx, Ly), beta in (((20, 20), 16.0), ((20, 20), 2.0), ((12, 6), 8.0), ((40, 4), 8.0)):
+        p, dis, _ = make_case(O, Lx, Ly, beta, seed=5)
         ctx = device_ctx(dwhmc, p, dis, "cr", delta_cap=0.0)
         assert ctx.info["delta_cap"] == pytest.approx(max(1.25, 4.0 * math.sqrt(2 * J / beta)))
         assert ctx.info["e_bound"] >= ctx.info["delta_cap"] * 2
@@ -330,13 +337,14 @@ def test_site_guard_reselects_on_upload(dwhmc, oracle):
     ctx.close()
 
 
-def test_site_guard_reselects_mid_sweep(dwhmc, oracle):
+@pytest.mark.parametrize("Lx,Ly", [(20, 4), (40, 3), (12, 5)])
+def test_site_guard_reselects_mid_sweep(dwhmc, oracle, Lx, Ly):
     """Site guard: a trajectory whose drift takes a site mean past the cap is
     rerun from its start with re-selected poles (the level-0 inversion launch
     sets the flag); the result equals a context built with the final cap and
     matches the oracle."""
     O = oracle
-    p, dis, Delta0 = make_case(O, 20, 4, 4.0, seed=22, amp=0.0)
+    p, dis, Delta0 = make_case(O, Lx, Ly, 4.0, seed=22 + Lx, amp=0.0)
     rng = np.random.default_rng(23)
     noise = 8.0 * (rng.standard_normal((p.N, 2)) + 1j * rng.standard_normal((p.N, 2))) * math.sqrt(0.5)
     Nt, dt = 4, 0.1
