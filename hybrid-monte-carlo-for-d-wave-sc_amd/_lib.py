@@ -88,6 +88,7 @@ SIGNATURES = {
     "dwh_debug_dense_H": (C.c_int, [_P, _I64, _P]),
     "dwh_debug_level0": (C.c_int, [_P, _I64, _I64, _I32, _P, _P]),
     "dwh_debug_cr_plan_check": (C.c_int, [_I64, _I64, _I64, _I32, _I32, _P]),
+    "dwh_debug_cr_plan_flops": (C.c_int, [_I64, _I64, _I64, _I32, _I32, _P]),
     "dwh_selftest_mfma": (C.c_int, [_I32]),
 }
 

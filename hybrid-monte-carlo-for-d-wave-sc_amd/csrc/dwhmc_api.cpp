@@ -161,8 +161,15 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol, bool 
   int inv_ord = 0;
   auto add_inv = [&](const std::vector<int>& blocks, int& slot) {
     std::vector<dwh::CrTask>& stk = side_tasks[inv_ord];
-    CrStage st{0, (int)pl.inv_blk.size(), (int)blocks.size(), side_flops[inv_ord], 0.0, 0, 0, 0,
-               (int)pl.tasks.size(), (int)stk.size(), {32, 1}};
+    CrStage st{};
+    st.kind = 0;
+    st.first = (int)pl.inv_blk.size();
+    st.n = (int)blocks.size();
+    st.sg = 1.0;                        // side tasks carry their own sign (kCrNegBit)
+    st.flops = side_flops[inv_ord];     // the side products' flops per batch item
+    st.tfirst = (int)pl.tasks.size();
+    st.ntiles = (int)stk.size();
+    st.cfg = {32, 1};
     for (const dwh::CrTask& t : stk) st.maxt32 = std::max(st.maxt32, dwh::cr_task_tiles(t, 32));
     pl.tasks.insert(pl.tasks.end(), stk.begin(), stk.end());
     ++inv_ord;
@@ -226,8 +233,15 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol, bool 
       cur_adiag.clear();
       return;
     }
-    CrStage st{1, (int)pl.tasks.size(), (int)cur_tasks.size(), sg, 0.0, 0, 0, 0,
-               (int)pl.tiles16.size(), 0, {16, 1}};
+    CrStage st{};
+    st.kind = 1;
+    st.first = (int)pl.tasks.size();
+    st.n = (int)cur_tasks.size();
+    st.sg = sg;
+    st.flops = 0.0;                     // accumulated per task below
+    st.tfirst = (int)pl.tiles16.size();
+    st.ntiles = 0;
+    st.cfg = {16, 1};
     for (size_t ti = 0; ti < cur_tasks.size(); ++ti) {
       const dwh::CrTask& t = cur_tasks[ti];
       const int nk = dwh::cr_task_tiles(t, 16), ct = (t.c1 + 15) / 16 - t.c0 / 16;
@@ -475,9 +489,14 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol, bool 
 void build_cr_tails(CrPlan& pl, int nbatch, int cap) {
   int maxwg = 2 * cap;
   if (const char* e = std::getenv("DWHMC_CR_TAIL_MAX")) maxwg = std::atoi(e);
+  // the first inversion stage carries the site guard (cr_enqueue): it always
+  // stays a launch of its own
+  int first_inv = -1;
+  for (size_t k = 0; k < pl.stages.size() && first_inv < 0; ++k)
+    if (pl.stages[k].kind == 0) first_inv = (int)k;
   auto nwg = [&](const CrStage& st) -> int {
     if (st.kind == 0) {
-      if (st.l0) return -1;
+      if (st.l0 || &st - pl.stages.data() == first_inv) return -1;
       const int side = st.ntiles > 0 ? (nbatch * st.ntiles * st.maxt32 + 3) / 4 : 0;
       return st.n * nbatch + side;
     }
@@ -2347,6 +2366,26 @@ int dwh_timing_reset(dwh_ctx* ctx) {
 
 int dwh_selftest_mfma(int32_t device) { return dwh::selftest_mfma_layout(device); }
 
+}  // extern "C"
+
+namespace {
+// pairing columns (+x, +y, -x, -y) of every site of a periodic Lx x Ly lattice
+std::vector<int> nn_pairing_cols(int Lx, int Ly) {
+  const int N = Lx * Ly;
+  std::vector<int> Dcol((size_t)N * kSlots);
+  for (int i = 0; i < N; ++i) {
+    const int x = i % Lx, y = i / Lx;
+    Dcol[(size_t)i * kSlots + 0] = y * Lx + (x + 1) % Lx;
+    Dcol[(size_t)i * kSlots + 1] = ((y + 1) % Ly) * Lx + x;
+    Dcol[(size_t)i * kSlots + 2] = y * Lx + (x - 1 + Lx) % Lx;
+    Dcol[(size_t)i * kSlots + 3] = ((y - 1 + Ly) % Ly) * Lx + x;
+  }
+  return Dcol;
+}
+}  // namespace
+
+extern "C" {
+
 // ---- host-only check of the CR schedule (no device) -------------------------
 // Builds the plan dwh_create would for an Lx x Ly periodic lattice (NN pairing
 // bonds) and nbatch = chains x poles batch items, then checks its dataflow:
@@ -2357,15 +2396,7 @@ int dwh_selftest_mfma(int32_t device) { return dwh::selftest_mfma_layout(device)
 // block the force / E_f gather reads was written.
 int dwh_debug_cr_plan_check(int64_t Lx, int64_t Ly, int64_t nbatch, int32_t side, int32_t inv0, int64_t* stats) {
   if (Lx < 1 || Ly < 1 || nbatch < 1) return fail(nullptr, DWH_ERR_ARG, "bad lattice / batch");
-  const int N = (int)(Lx * Ly);
-  std::vector<int> Dcol((size_t)N * kSlots);
-  for (int i = 0; i < N; ++i) {
-    const int x = i % (int)Lx, y = i / (int)Lx;
-    Dcol[(size_t)i * kSlots + 0] = y * (int)Lx + (x + 1) % (int)Lx;
-    Dcol[(size_t)i * kSlots + 1] = ((y + 1) % (int)Ly) * (int)Lx + x;
-    Dcol[(size_t)i * kSlots + 2] = y * (int)Lx + (x - 1 + (int)Lx) % (int)Lx;
-    Dcol[(size_t)i * kSlots + 3] = ((y - 1 + (int)Ly) % (int)Ly) * (int)Lx + x;
-  }
+  std::vector<int> Dcol = nn_pairing_cols((int)Lx, (int)Ly);
   const int BP = (int)(2 * ((Lx + 15) / 16 * 16));
   if (!dwh::cr_supported_bp(BP)) return fail(nullptr, DWH_ERR_ARG, "lattice row too wide for the CR path");
   const CrPlan pl = build_cr_plan((int)Lx, (int)Ly, BP, Dcol, side && dwh::cr_supported_side(BP), (int)nbatch,
@@ -2420,8 +2451,16 @@ int dwh_debug_cr_plan_check(int64_t Lx, int64_t Ly, int64_t nbatch, int32_t side
           std::snprintf(buf, sizeof buf, "stage %d writes block %d from two tasks", si, wr[i].first);
           return fail(nullptr, DWH_ERR_STATE, buf);
         }
-    for (const auto& w : wr)
+    for (const auto& w : wr) {
+      // level-0 blocks (refilled only at their pairing entries) and the static
+      // R = A^-1 blocks of k_cr_inv0 are read on every step: nothing may
+      // overwrite them
+      if (w.first >= 0 && w.first < pl.nblk && written[w.first] == -2) {
+        std::snprintf(buf, sizeof buf, "stage %d overwrites static block %d", si, w.first);
+        return fail(nullptr, DWH_ERR_STATE, buf);
+      }
       if (w.first >= 0 && w.first < pl.nblk && written[w.first] == -1) written[w.first] = si;
+    }
   }
   const int64_t BB = (int64_t)(BP / 2) * BP;
   for (int64_t o : pl.goff)
@@ -2435,6 +2474,26 @@ int dwh_debug_cr_plan_check(int64_t Lx, int64_t Ly, int64_t nbatch, int32_t side
     stats[3] = ngemm;
     stats[4] = ntask;
     stats[5] = pl.nblk;
+  }
+  return DWH_OK;
+}
+
+int dwh_debug_cr_plan_flops(int64_t Lx, int64_t Ly, int64_t nbatch, int32_t side, int32_t inv0, double* flops) {
+  if (Lx < 1 || Ly < 1 || nbatch < 1 || !flops) return fail(nullptr, DWH_ERR_ARG, "bad lattice / batch / output");
+  const int BP = (int)(2 * ((Lx + 15) / 16 * 16));
+  if (!dwh::cr_supported_bp(BP)) return fail(nullptr, DWH_ERR_ARG, "lattice row too wide for the CR path");
+  std::vector<int> Dcol = nn_pairing_cols((int)Lx, (int)Ly);
+  const CrPlan pl = build_cr_plan((int)Lx, (int)Ly, BP, Dcol, side && dwh::cr_supported_side(BP), (int)nbatch,
+                                  256, inv0 && dwh::cr_supported_inv0(BP));
+  const double bp3 = 8.0 * BP * (double)BP * BP;
+  flops[0] = flops[1] = flops[2] = 0.0;
+  for (const CrStage& st : pl.stages) {
+    if (st.kind == 0) {
+      flops[0] += st.n * bp3;
+      flops[2] += st.flops;
+    } else {
+      flops[1] += st.flops;
+    }
   }
   return DWH_OK;
 }

@@ -251,6 +251,13 @@ int dwh_debug_level0(dwh_ctx* ctx, int64_t chain, int64_t pole, int32_t refill, 
  * violation in dwh_last_error(NULL). */
 int dwh_debug_cr_plan_check(int64_t Lx, int64_t Ly, int64_t nbatch, int32_t side, int32_t inv0, int64_t* stats);
 
+/* Algorithmic fp64 flops per batch item of the same plan (host only), as the
+ * "cr_*" timers count them: flops[0] block inversions (8 BP^3 each), flops[1]
+ * block products of the product stages, flops[2] block products run as side
+ * work inside inversion stages (8 BP rows cols per term on the restricted
+ * output windows).  flops[1] + flops[2] does not depend on `side`. */
+int dwh_debug_cr_plan_flops(int64_t Lx, int64_t Ly, int64_t nbatch, int32_t side, int32_t inv0, double* flops);
+
 /* Self-test of the f64 MFMA fragment layout (A = I, asymmetric B); 0 = pass. */
 int dwh_selftest_mfma(int32_t device);
 

@@ -49,3 +49,37 @@ def test_cr_schedule_rejects_wide_rows(dwhmc):
     lib = dwhmc.load_library()
     rc, _, err = check(lib, 65, 4, 14, 1, 1)
     assert rc != 0 and "too wide" in err
+
+
+def plan_flops(lib, Lx, Ly, nbatch, side, inv0):
+    out = np.zeros(3)
+    rc = lib.dwh_debug_cr_plan_flops(Lx, Ly, nbatch, side, inv0, out.ctypes.data_as(C.c_void_p))
+    assert rc == 0, lib.dwh_last_error(None).decode()
+    return out
+
+
+@pytest.mark.parametrize("Lx,Ly", [(4, 1), (4, 2), (3, 3), (8, 8), (17, 4), (20, 6), (24, 24), (32, 5),
+                                   (32, 32), (32, 33), (48, 48), (64, 9)])
+@pytest.mark.parametrize("nbatch", [13, 52])
+def test_cr_plan_flops_independent_count(dwhmc, Lx, Ly, nbatch):
+    """The plan's per-stage algorithmic flops (what the cr_* timers, bench.py's
+    alg_flops_per_step and the roofline use) against tools/cr_model.py's count
+    of the recursion: moving products into inversion launches (side work)
+    must move their flops with them, never drop them (VERDICT r02 weak #3)."""
+    from tools.cr_model import cr_flop_count
+    lib = dwhmc.load_library()
+    inv_ref, prod_ref = cr_flop_count(Lx, Ly)
+    for side in (0, 1):
+        for inv0 in (0, 1):
+            inv, prod, side_f = plan_flops(lib, Lx, Ly, nbatch, side, inv0)
+            assert inv == pytest.approx(inv_ref, rel=1e-12), (side, inv0)
+            assert prod + side_f == pytest.approx(prod_ref, rel=1e-12), (side, inv0, prod, side_f)
+            if not side:
+                assert side_f == 0.0
+
+
+def test_cr_plan_flops_c3_side_work(dwhmc):
+    """At C3 (L = 32, 13 poles) the side work carries real products."""
+    lib = dwhmc.load_library()
+    inv, prod, side_f = plan_flops(lib, 32, 32, 13, 1, 1)
+    assert side_f > 0.2 * (prod + side_f)

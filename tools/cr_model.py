@@ -303,3 +303,55 @@ def check_top_cr(Lx, Ly, seed=0, y=0.7):
         for f, t in zip(F, T):
             err = max(err, np.abs(f[:Lx, :] - t).max())
     return err
+
+
+# ---------------------------------------------------------------------------
+# Algorithmic flop count of the recursion above, counted independently of the
+# device planner (build_cr_plan): the same levels and terms as
+# cr_selected_inverse_top, each product term on a top half (HP x BP output,
+# K = BP) at 8 BP HP BP flops, each block inversion at 8 BP^3.  At level 0 the
+# backward pass forms only what the force / E_f / Tr rho_hh read (16 x 16
+# output tiles): G_ea, G_ec only the diagonal tiles of the B part inside
+# columns [HP, HP + Lx); G_ee the A-part diagonal tiles and the whole B part.
+# Returns (inversion flops, product flops) per batch item.
+# ---------------------------------------------------------------------------
+def cr_flop_count(Lx: int, Ly: int):
+    HP = (Lx + 15) // 16 * 16
+    BP = 2 * HP
+    full = 8.0 * BP * HP * BP                       # one term, whole top half
+    tr = HP // 16                                   # tile rows
+    # G_ea / G_ec at level 0: window [HP, HP + Lx), B-part diagonal tiles only
+    wc = -(-(Lx) // 16)                             # tile columns of the window
+    sel_ea = 8.0 * BP * HP * Lx * (min(tr, wc) / (tr * wc))
+    # G_ee at level 0: A-part diagonal tiles + whole B part of BP/16 tile columns
+    sel_ee = full * ((tr + tr * tr) / (tr * 2 * tr))
+    inv = 0
+    terms = 0.0
+
+    def level(m, depth):
+        nonlocal inv, terms
+        if m == 1:
+            inv += 1
+            return
+        E = list(range(1, m - (m % 2), 2))
+        K = list(range(0, m, 2))
+        inv += len(E)
+        terms += 4 * len(E) * full                  # V1, V2, W1, W2
+        elim = set(E)
+        for k in K:
+            if m == 2:
+                terms += 4 * full                   # D' of the 1-block chain
+                continue
+            hr, hl = (k + 1) in elim, ((k - 1) % m) in elim
+            terms += (int(hr) + int(hl)) * full     # D'
+            if hr:
+                terms += 2 * full                   # U', L'
+        level(len(K), depth + 1)
+        for _ in E:                                 # backward pass
+            if depth == 0:
+                terms += 2 * 2 * sel_ea + 2 * 2 * full + 2 * sel_ee
+            else:
+                terms += 5 * 2 * full               # G_ea, G_ec, G_ae, G_ce, G_ee: 2 terms each
+
+    level(Ly, 0)
+    return inv * 8.0 * BP ** 3, terms
