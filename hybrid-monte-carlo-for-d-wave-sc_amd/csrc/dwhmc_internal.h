@@ -184,15 +184,25 @@ void launch_fermion_energy(const Dims& d, const double* ldstatic, const double* 
 // H = Σ|π|²/2m + β/2J Σ|Δ|² + E_f into Hout[c]
 // trajectory start / end of the throughput path in one launch each (k_traj_begin:
 // refresh + H_old + backup + force from the cached P + kick/drift; k_traj_end:
-// H_new + Metropolis + restore)
+// H_new + Metropolis + restore).
+// Guard trips inside a batch of sweeps (SweepHalt): k_traj_end of the sweep
+// whose kernels set *flag records its sequence number in halt[1] and sets
+// halt[0]; every later k_traj_begin / k_traj_end of the batch then returns at
+// once, so the backups (Δ, P, E_f, Tr ρ_hh) keep the tripped sweep's starting
+// point for the host to resume from.  halt == nullptr: off.
+struct SweepHalt {
+  int* halt = nullptr;   // [0] halted, [1] sequence number of the tripped sweep
+  int seq = 0;           // this sweep's sequence number in the batch
+  const int* flag = nullptr;
+};
 void launch_traj_begin(const Dims& d, const double2* noise, double scale, double2* Pi, double2* Delta,
                        const double2* Pair, double2* F, const double* Ef, const double* Trhh, double2* DeltaB,
                        double2* PairB, double* EfB, double* TrhhB, double* Hold, double beta, double J,
-                       double mass, const KickDrift& kd, hipStream_t s);
+                       double mass, const KickDrift& kd, const SweepHalt& sh, hipStream_t s);
 void launch_traj_end(const Dims& d, double2* Delta, const double2* Pi, double2* Pair, double* Ef, double* Trhh,
                      const double2* DeltaB, const double2* PairB, const double* EfB, const double* TrhhB,
                      const double* Hold, double* Hnew, const double* uniform, uint8_t* accepted, double* dH,
-                     double beta, double J, double mass, hipStream_t s);
+                     double beta, double J, double mass, const SweepHalt& sh, hipStream_t s);
 void launch_total_energy(const Dims& d, const double2* Delta, const double2* Pi,
                          const double* Ef, double beta, double J, double mass, double* Hout,
                          hipStream_t s);

@@ -786,8 +786,10 @@ __global__ __launch_bounds__(256) void k_traj_begin(const double2* __restrict__ 
                                                     double* __restrict__ EfB, double* __restrict__ TrhhB,
                                                     double* __restrict__ Hold, int N, double beta, double J,
                                                     double mass, double kick, double drift, double cap2,
-                                                    int* __restrict__ flag) {
+                                                    int* __restrict__ flag, const int* __restrict__ halt) {
   const int c = blockIdx.x;
+  // a guard trip earlier in this batch (SweepHalt): keep the backups
+  if (halt != nullptr && halt[0] != 0) return;
   __shared__ double red[4];
   double sd = 0.0, sp = 0.0;
   const double f = -beta / (2.0 * J);
@@ -819,8 +821,21 @@ __global__ __launch_bounds__(256) void k_traj_end(double2* __restrict__ Delta, c
                                                   const double* __restrict__ TrhhB, const double* __restrict__ Hold,
                                                   double* __restrict__ Hnew, const double* __restrict__ uniform,
                                                   uint8_t* __restrict__ accepted, double* __restrict__ dH, int N,
-                                                  double beta, double J, double mass) {
+                                                  double beta, double J, double mass, int* __restrict__ halt,
+                                                  int seq, const int* __restrict__ flag) {
   const int c = blockIdx.x;
+  if (halt != nullptr) {
+    // *flag comes from earlier launches; halt[0] may also be set by chain 0's
+    // workgroup of this launch, which only makes the others return as well
+    if (halt[0] != 0) return;
+    if (*flag != 0) {
+      if (c == 0 && threadIdx.x == 0) {
+        halt[1] = seq;
+        halt[0] = 1;
+      }
+      return;
+    }
+  }
   __shared__ double red[4];
   __shared__ int acc_s;
   double sd = 0.0, sp = 0.0;
@@ -972,17 +987,17 @@ void launch_restore(const Dims& d, const uint8_t* accepted, const double2* Delta
 void launch_traj_begin(const Dims& d, const double2* noise, double scale, double2* Pi, double2* Delta,
                        const double2* Pair, double2* F, const double* Ef, const double* Trhh, double2* DeltaB,
                        double2* PairB, double* EfB, double* TrhhB, double* Hold, double beta, double J,
-                       double mass, const KickDrift& kd, hipStream_t s) {
+                       double mass, const KickDrift& kd, const SweepHalt& sh, hipStream_t s) {
   hipLaunchKernelGGL(k_traj_begin, dim3(d.nc), dim3(256), 0, s, noise, scale, Pi, Delta, Pair, F, Ef, Trhh,
                      DeltaB, PairB, EfB, TrhhB, Hold, d.N, beta, J, mass, kd.kick, kd.drift, kd.cap * kd.cap,
-                     kd.flag);
+                     kd.flag, (const int*)sh.halt);
 }
 void launch_traj_end(const Dims& d, double2* Delta, const double2* Pi, double2* Pair, double* Ef, double* Trhh,
                      const double2* DeltaB, const double2* PairB, const double* EfB, const double* TrhhB,
                      const double* Hold, double* Hnew, const double* uniform, uint8_t* accepted, double* dH,
-                     double beta, double J, double mass, hipStream_t s) {
+                     double beta, double J, double mass, const SweepHalt& sh, hipStream_t s) {
   hipLaunchKernelGGL(k_traj_end, dim3(d.nc), dim3(256), 0, s, Delta, Pi, Pair, Ef, Trhh, DeltaB, PairB, EfB,
-                     TrhhB, Hold, Hnew, uniform, accepted, dH, d.N, beta, J, mass);
+                     TrhhB, Hold, Hnew, uniform, accepted, dH, d.N, beta, J, mass, sh.halt, sh.seq, sh.flag);
 }
 void launch_sum_ld(const Dims& d, const double* ldpart, double* ldsum, hipStream_t s) {
   hipLaunchKernelGGL(k_sum_ld, dim3((d.nbatch + 63) / 64), dim3(64), 0, s, ldpart, ldsum, d.nb,

@@ -185,6 +185,10 @@ def hmc_sweep(cache: ComputeCache, p: ModelParameters, state: SimulationState, *
     dwh_hmc_finish).  Returns (accepted, ΔH); mutates state.Δ, state.π and
     the cache."""
     ctx = cache.require()
+    if rng is None and (noise is None or uniform is None):
+        # checked before any device call: a missing generator must not leave
+        # a trajectory pending on the context
+        raise ValueError("hmc_sweep needs `rng` unless both noise and uniform are injected")
     if noise is None:
         noise = standard_complex_normal(rng, (p.N, 2))
     ctx.set_state(state.Delta, None)

@@ -152,7 +152,12 @@ int dwh_hmc_finish(dwh_ctx* ctx, const uint8_t* accepted);
 
 /* Throughput path: upload the draws of nsweeps sweeps once (noise:
  * nsweeps*nchains*2N, uniform: nsweeps*nchains), then enqueue sweeps that
- * read them from HBM without host round trips. */
+ * read them from HBM without host round trips.  A guard trip inside a batch
+ * makes the batch's later sweeps no-ops on the device; the next
+ * dwh_sweep_results / dwh_synchronize (or any call that reads or changes the
+ * state) re-selects the pole set, resumes from the tripped sweep's starting Δ
+ * and replays the remaining sweeps — the same steps dwh_hmc_sweep takes — so
+ * the results equal the single-sweep path's bit for bit. */
 int dwh_load_draws(dwh_ctx* ctx, int64_t nsweeps, const dwh_c128* noise, const double* uniform);
 int dwh_run_sweeps(dwh_ctx* ctx, int64_t first_sweep, int64_t nsweeps, int64_t Nt, double dt,
                    double mass);
@@ -160,7 +165,8 @@ int dwh_sweep_results(dwh_ctx* ctx, int64_t first_sweep, int64_t nsweeps, uint8_
                       double* dH);
 int dwh_synchronize(dwh_ctx* ctx);
 
-/* hipStream_t the context launches on (for events / interop). */
+/* hipStream_t the context launches on (for events / interop).  The handle
+ * stays valid for the context's lifetime, pole re-selections included. */
 int dwh_stream(dwh_ctx* ctx, void** stream);
 
 /* Kernel timing with HIP events on the stream each kernel runs on

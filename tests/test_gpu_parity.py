@@ -372,20 +372,65 @@ def test_site_guard_reselects_mid_sweep(dwhmc, oracle, Lx, Ly):
     b.close()
 
 
-def test_site_guard_throughput_path_reports(dwhmc, oracle):
-    """The throughput path (dwh_run_sweeps) does not return to the host between
-    sweeps: a site-guard trip there is reported by dwh_sweep_results."""
+@pytest.mark.parametrize("algo_g,Lx,Ly", [("cr", 20, 4), ("cr", 12, 5), ("dense", 6, 6)])
+def test_guard_trip_recovers_in_throughput_path(dwhmc, oracle, algo_g, Lx, Ly):
+    """A guard trip in the middle of a dwh_run_sweeps batch (sweep 2 of 5, in
+    chain 1 of 2): the later sweeps of the batch become no-ops on the device,
+    and dwh_sweep_results re-selects the poles, resumes from the tripped
+    sweep's backed-up Δ and replays sweeps 2..4 — the same steps
+    dwh_hmc_sweep takes for a trip (src/HMC.jl:98-114 accepts any Δ).  Every
+    sweep's accept flag and ΔH, the final Δ, π and the re-selected pole set
+    equal the single-sweep path bit for bit.  cr: site guard (level-0
+    inversion launch); dense: bond guard (drift kernels)."""
     O = oracle
-    p, dis, Delta0 = make_case(O, 20, 4, 4.0, seed=24, amp=0.0)
+    p, dis, Delta0 = make_case(O, Lx, Ly, 4.0, seed=24 + Lx, amp=0.0)
+    ns, Nt, dt = 5, 4, 0.1
     rng = np.random.default_rng(25)
-    noise = 8.0 * (rng.standard_normal((1, 1, p.N, 2)) + 1j * rng.standard_normal((1, 1, p.N, 2))) * math.sqrt(0.5)
-    ctx = device_ctx(dwhmc, p, dis, "cr", delta_cap=0.2)
-    ctx.set_pairing(Delta0)
+    noise = (rng.standard_normal((ns, 2, p.N, 2)) + 1j * rng.standard_normal((ns, 2, p.N, 2))) * math.sqrt(0.5)
+    scale = np.full((ns, 2), 0.05)
+    scale[2, 1] = 8.0                                  # the trip: sweep 2, chain 1
+    noise *= scale[:, :, None, None]
+    uni = rng.random((ns, 2))
+    dis2 = np.stack([dis, dis[::-1].copy()])
+    D2 = np.stack([Delta0, Delta0[::-1].copy()])
+    cap0 = 0.2
+    a = device_ctx(dwhmc, p, dis2, algo_g, delta_cap=cap0)
+    a.set_pairing(D2)
+    a.factorize()
+    ref = []
+    for s in range(ns):
+        ref.append(a.hmc_sweep(noise[s], uni[s], Nt, dt, p.mass))
+        if s == 1:
+            assert a.info["delta_cap"] == cap0          # no trip before sweep 2
+    assert a.info["delta_cap"] > cap0                   # sweep 2 tripped
+    b = device_ctx(dwhmc, p, dis2, algo_g, delta_cap=cap0)
+    b.set_pairing(D2)
+    b.factorize()
+    b.load_draws(noise, uni)
+    b.run_sweeps(0, ns, Nt, dt, p.mass)
+    acc, dH = b.sweep_results(0, ns)
+    for s in range(ns):
+        assert np.array_equal(acc[s], ref[s][0]), s
+        assert np.array_equal(dH[s], ref[s][1]), s
+    for x, y in zip(a.get_state(), b.get_state()):
+        assert np.array_equal(x, y)
+    ia, ib = a.info, b.info
+    assert (ia["delta_cap"], ia["kappa"], ia["npoles"]) == (ib["delta_cap"], ib["kappa"], ib["npoles"])
+    # a stream handle taken before the re-selection stays the context's stream
+    a.close()
+    b.close()
+
+
+def test_reselection_keeps_stream(dwhmc, oracle):
+    """dwh_stream's handle stays valid across a guard re-selection."""
+    O = oracle
+    p, dis, Delta0 = make_case(O, 20, 4, 4.0, seed=31, amp=0.9)
+    ctx = device_ctx(dwhmc, p, dis, "cr", delta_cap=0.3)
+    s0 = ctx.stream()
+    ctx.set_pairing(Delta0)                            # re-selects (site mean > 0.3)
+    assert ctx.info["delta_cap"] > 0.3
+    assert ctx.stream() == s0
     ctx.factorize()
-    ctx.load_draws(noise, np.array([[0.3]]))
-    ctx.run_sweeps(0, 1, 4, 0.1, p.mass)
-    with pytest.raises(Exception):
-        ctx.sweep_results(0, 1)
     ctx.close()
 
 
