@@ -17,7 +17,7 @@ from .hmc import (ComputeCache, ModelParameters, ObservablesResult, SimulationSt
                   refresh_momentum, standard_complex_normal, update_H_BdG, SpectrumResult,
                   measure_transport_and_spectra)
 from .context import FermionContext, selftest_mfma, transport_grid
-from .simulation import AdaptiveNt, SimulationResult, run_simulation
+from .simulation import AdaptiveNt, SimulationResult, run_simulation, run_simulation_chains
 from ._lib import DwhError, SpectrumGuardError, lib_path, load as load_library
 
 __all__ = [
@@ -26,5 +26,5 @@ __all__ = [
     "initialize_cache", "initialize_state", "measure_observables", "neighbour_tables",
     "refresh_momentum", "standard_complex_normal", "update_H_BdG", "FermionContext", "selftest_mfma",
     "DwhError", "SpectrumGuardError", "lib_path", "load_library", "AdaptiveNt", "SimulationResult",
-    "run_simulation", "SpectrumResult", "measure_transport_and_spectra", "transport_grid",
+    "run_simulation", "run_simulation_chains", "SpectrumResult", "measure_transport_and_spectra", "transport_grid",
 ]

@@ -19,7 +19,7 @@ SOURCES = [os.path.join(CSRC, "dwhmc_kernels.hip"), os.path.join(CSRC, "dwhmc_cr
 # rocSOLVER (zheevd) and rocBLAS (zgemm) serve the transport measurement only
 LIBS = ["-L/opt/rocm/lib", "-lrocsolver", "-lrocblas", "-Wl,-rpath,/opt/rocm/lib"]
 DEPS = SOURCES + [os.path.join(CSRC, "dwhmc_internal.h"), os.path.join(CSRC, "dwhmc_device.h"),
-                  os.path.join(CSRC, "pole_table.inc"),
+                  os.path.join(CSRC, "pole_table.inc"), os.path.join(CSRC, "pole_table_eps5e-12.inc"),
                   os.path.join(ROOT, "include", "dwhmc.h")]
 ARCH = os.environ.get("DWHMC_OFFLOAD_ARCH", "gfx950")
 

@@ -28,7 +28,17 @@
 
 #include "../../include/dwhmc.h"
 #include "dwhmc_internal.h"
+// Two compiled pole tables (tools/gen_pole_table.py): "budget", sup|tanh
+// error| <= 5e-12 — half the 1e-11 absolute budget the pairing tolerance
+// leaves for the expansion (|δP_ij| <= ε; E_f and F budgets are looser,
+// DESIGN.md §2) — and "strict" (<= 2e-14).  DWHMC_POLE_TABLE selects one;
+// default "budget".
+namespace tab_strict {
 #include "pole_table.inc"
+}
+namespace tab_budget {
+#include "pole_table_eps5e-12.inc"
+}
 
 using dwh::Dims;
 using dwh::kGJ;
@@ -38,6 +48,35 @@ using dwh::kSlots;
 namespace {
 
 thread_local std::string g_create_error;
+
+struct PoleView {
+  double kappa;
+  int m;
+  double C_u, err_tanh;
+  const double *t, *a;
+};
+template <typename E>
+PoleView pole_view(const E& e, const double* T, const double* A) {
+  return PoleView{e.kappa, e.m, e.C_u, e.err_tanh, T + e.off, A + e.off};
+}
+struct PoleTable {
+  const char* name;
+  int size;
+  PoleView (*at)(int);
+};
+const PoleTable kPoleTables[2] = {
+    {"budget", tab_budget::kPoleTableSize,
+     [](int e) { return pole_view(tab_budget::kPoleEntries[e], tab_budget::kPoleT, tab_budget::kPoleA); }},
+    {"strict", tab_strict::kPoleTableSize,
+     [](int e) { return pole_view(tab_strict::kPoleEntries[e], tab_strict::kPoleT, tab_strict::kPoleA); }},
+};
+const PoleTable* pole_table(std::string* err) {
+  const char* e = std::getenv("DWHMC_POLE_TABLE");
+  if (!e || !*e || std::strcmp(e, "budget") == 0) return &kPoleTables[0];
+  if (std::strcmp(e, "strict") == 0) return &kPoleTables[1];
+  *err = "DWHMC_POLE_TABLE must be budget or strict";
+  return nullptr;
+}
 
 enum TimerName {
   T_GJ_UPDATE = 0, T_GJ_PIVOT, T_ASSEMBLE, T_CONTRACT, T_STEP, T_GJ_EDGE, T_CR_GEMM, T_CR_INV, T_CR_INVSIDE,
@@ -1268,9 +1307,12 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
   if (delta_cap <= 0) delta_cap = default_delta_cap(beta, J, site_guard);
   const double Eb = hmax + 2.0 * delta_cap;
   const double kneed = 0.5 * beta * Eb;
+  std::string terr;
+  const PoleTable* tab = pole_table(&terr);
+  if (!tab) return fail(nullptr, DWH_ERR_ARG, terr);
   int sel = -1;
-  for (int e = 0; e < kPoleTableSize; ++e)
-    if (kPoleEntries[e].kappa >= kneed * (1.0 - 1e-12)) {
+  for (int e = 0; e < tab->size; ++e)
+    if (tab->at(e).kappa >= kneed * (1.0 - 1e-12)) {
       sel = e;
       break;
     }
@@ -1278,22 +1320,23 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
   if (sel < 0 && want != "eig") {
     char buf[256];
     std::snprintf(buf, sizeof buf, "beta*E_bound/2 = %g exceeds the pole table (max kappa %g)", kneed,
-                  kPoleEntries[kPoleTableSize - 1].kappa);
+                  tab->at(tab->size - 1).kappa);
     return fail(nullptr, DWH_ERR_TABLE, buf);
   }
   const bool eig = want == "eig";
   // the eigen path is exact for any Δ: no pole set, no |Δ| guard
   if (eig) delta_cap = std::numeric_limits<double>::max();
-  const PoleEntry* pe = eig ? nullptr : &kPoleEntries[sel];
+  const PoleView pv = eig ? PoleView{} : tab->at(sel);
+  const PoleView* pe = eig ? nullptr : &pv;
   const double kappa = eig ? kneed : pe->kappa;
   const double Ep = eig ? Eb : 2.0 * kappa / beta;
   const int npole = eig ? 1 : pe->m;   // eig: one dummy batch item per chain
   std::vector<double> y(npole, 0.0), cq(npole, 0.0);
   double suma = 0;
   for (int q = 0; q < (eig ? 0 : npole); ++q) {
-    y[q] = Ep * std::sqrt(kPoleT[pe->off + q]);
-    cq[q] = 0.5 * kPoleA[pe->off + q] * Ep;
-    suma += kPoleA[pe->off + q];
+    y[q] = Ep * std::sqrt(pe->t[q]);
+    cq[q] = 0.5 * pe->a[q] * Ep;
+    suma += pe->a[q];
   }
 
   dwh_ctx* ctx = new dwh_ctx();

@@ -244,11 +244,82 @@ __device__ __forceinline__ void inv16_all(double2 (&a)[4], double& pprod,
   (inv16_step<Ps, STRIDED>(a, pprod), ...);
 }
 
+// Gauss-Jordan step on the 2 x 2 pivot block B = {P, P+1} (P even): 8 steps
+// per 16 x 16 tile instead of 16, so half the dependent broadcast ->
+// reciprocal -> update chains.  With C = A[:, B], R = A[B, :], Π = A[B, B]
+// and E the columns e_P, e_{P+1}, one update covers every entry:
+//   A <- A - (C - E) Π^-1 (R + E^T)
+// (rows of B become Π^-1 R, columns of B become -C Π^-1, the block Π^-1).
+// Π^-1 by the closed 2 x 2 formula; every principal block of i(H - i y) has
+// Hermitian part >= y I, so |det Π| >= y^2 and the block pivots are as safe
+// as the scalar ones.  Accumulates |det Π|^2 (= the two scalar pivots' product).
+#ifndef DWHMC_INV_PAIR
+#define DWHMC_INV_PAIR 0
+#endif
+template <int P, bool STRIDED>
+__device__ __forceinline__ void inv16_step2(double2 (&a)[4], double& pprod) {
+  static_assert((P & 1) == 0, "pivot pairs start at even P");
+  // element (row i, column j): STRIDED lane (j & 3) * 16 + i, register j >> 2;
+  // else lane (j >> 2) * 16 + i, register j & 3
+  constexpr int PS0 = STRIDED ? (P & 3) : (P >> 2), PE0 = STRIDED ? (P >> 2) : (P & 3);
+  constexpr int PS1 = STRIDED ? ((P + 1) & 3) : ((P + 1) >> 2), PE1 = STRIDED ? ((P + 1) >> 2) : ((P + 1) & 3);
+  const int l = threadIdx.x & 63, r = l & 15, q = l >> 4;
+  double2 row0[4], row1[4];
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) {
+    row0[jj] = make_double2(dpp_rowbcast<P>(a[jj].x), dpp_rowbcast<P>(a[jj].y));
+    row1[jj] = make_double2(dpp_rowbcast<P + 1>(a[jj].x), dpp_rowbcast<P + 1>(a[jj].y));
+  }
+  const double2 c0 = make_double2(bcast_quarter<PS0>(a[PE0].x), bcast_quarter<PS0>(a[PE0].y));
+  const double2 c1 = make_double2(bcast_quarter<PS1>(a[PE1].x), bcast_quarter<PS1>(a[PE1].y));
+  const double2 p00 = make_double2(readlane_f64(a[PE0].x, PS0 * 16 + P), readlane_f64(a[PE0].y, PS0 * 16 + P));
+  const double2 p01 = make_double2(readlane_f64(a[PE1].x, PS1 * 16 + P), readlane_f64(a[PE1].y, PS1 * 16 + P));
+  const double2 p10 =
+      make_double2(readlane_f64(a[PE0].x, PS0 * 16 + P + 1), readlane_f64(a[PE0].y, PS0 * 16 + P + 1));
+  const double2 p11 =
+      make_double2(readlane_f64(a[PE1].x, PS1 * 16 + P + 1), readlane_f64(a[PE1].y, PS1 * 16 + P + 1));
+  const double2 det = csub(cmul(p00, p11), cmul(p01, p10));
+  const double m2 = fma(det.x, det.x, det.y * det.y);
+  const double s = rcp_nr(m2);
+  const double2 idet = make_double2(det.x * s, -det.y * s);
+  pprod *= m2;
+  const double2 i00 = cmul(p11, idet), i11 = cmul(p00, idet);
+  const double2 i01 = cmul(make_double2(-p01.x, -p01.y), idet), i10 = cmul(make_double2(-p10.x, -p10.y), idet);
+  // F = (C - E) Π^-1 for this lane's row
+  const double2 cc0 = make_double2(c0.x - (r == P ? 1.0 : 0.0), c0.y);
+  const double2 cc1 = make_double2(c1.x - (r == P + 1 ? 1.0 : 0.0), c1.y);
+  const double2 f0 = cadd(cmul(cc0, i00), cmul(cc1, i10));
+  const double2 f1 = cadd(cmul(cc0, i01), cmul(cc1, i11));
+  // R' = R + E^T
+  row0[PE0].x += (q == PS0) ? 1.0 : 0.0;
+  row1[PE1].x += (q == PS1) ? 1.0 : 0.0;
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) {
+    const double2 x0 = row0[jj], x1 = row1[jj];
+    double2 v;
+    v.x = fma(-f0.x, x0.x, fma(f0.y, x0.y, a[jj].x));
+    v.y = fma(-f0.x, x0.y, fma(-f0.y, x0.x, a[jj].y));
+    v.x = fma(-f1.x, x1.x, fma(f1.y, x1.y, v.x));
+    v.y = fma(-f1.x, x1.y, fma(-f1.y, x1.x, v.y));
+    a[jj] = v;
+  }
+}
+
+template <bool STRIDED, int... Ps>
+__device__ __forceinline__ void inv16_all2(double2 (&a)[4], double& pprod,
+                                           std::integer_sequence<int, Ps...>) {
+  (inv16_step2<2 * Ps, STRIDED>(a, pprod), ...);
+}
+
 // returns Π |pivot|^2 of the 16 pivots
 template <bool STRIDED = false>
 __device__ __forceinline__ double wave_inv16_dpp(double2 (&a)[4]) {
   double pprod = 1.0;
+#if DWHMC_INV_PAIR
+  inv16_all2<STRIDED>(a, pprod, std::make_integer_sequence<int, 8>{});
+#else
   inv16_all<STRIDED>(a, pprod, std::make_integer_sequence<int, 16>{});
+#endif
   return pprod;
 }
 

@@ -248,29 +248,34 @@ def measure_transport_and_spectra(cache: ComputeCache, p: ModelParameters, chain
     return SpectrumResult(**r)
 
 
-def measure_observables(cache: ComputeCache, p: ModelParameters, state: SimulationState) -> ObservablesResult:
-    """src/Observables.jl:88-222 from the factorisation outputs: P_ij (from
-    the same pole-LU as the force), E_f, and Tr ρ_hh for the hole density
-    (hole_conc = 2 Tr ρ_hh / N - 1 by particle-hole symmetry)."""
-    ctx = cache.require()
+def observables_from_outputs(p: ModelParameters, Delta, P, Ef: float, tr_hh: float) -> ObservablesResult:
+    """src/Observables.jl:88-222 for one chain from the factorisation outputs:
+    P_ij (the same pole-LU as the force), E_f, and Tr ρ_hh for the hole
+    density (hole_conc = 2 Tr ρ_hh / N - 1 by particle-hole symmetry,
+    SURVEY.md I4)."""
     N = p.N
-    D = np.asarray(state.Delta)
+    D = np.asarray(Delta)
     dx, dy = D[:, 0], D[:, 1]
     g = np.sum(0.5 * (dx - dy)) / N
-    Ef = float(ctx.fermion_energy()[0])
     Eb = p.beta / (2 * p.J) * float(np.sum(np.abs(D) ** 2))
-    P = ctx.pairing()[0]
     Px, Py = P[:, 0], P[:, 1]
     term = p.J * 0.5 * (Px - Py)
-    tr_hh = float(ctx.hole_trace()[0])
     return ObservablesResult(
-        total_energy=(Ef + Eb) / N,
+        total_energy=(float(Ef) + Eb) / N,
         Delta_amp=float(np.sum(0.5 * (np.abs(dx) + np.abs(dy)))) / N,
         Delta_local=float(np.sum(0.5 * np.abs(dx - dy))) / N,
         Delta_global=abs(g),
         S_Delta=abs(g) ** 2,
-        hole_conc=2.0 * tr_hh / N - 1.0,
+        hole_conc=2.0 * float(tr_hh) / N - 1.0,
         Delta_diff=float(np.sum((np.abs(dx - p.J * Px) + np.abs(dy - p.J * Py)) / 2.0)) / N,
         Delta_pair=abs(np.sum(term) / N),
         Delta_localpair=float(np.sum(np.abs(term))) / N,
     )
+
+
+def measure_observables(cache: ComputeCache, p: ModelParameters, state: SimulationState) -> ObservablesResult:
+    """src/Observables.jl:88-222 from the factorisation outputs (see
+    observables_from_outputs)."""
+    ctx = cache.require()
+    return observables_from_outputs(p, state.Delta, ctx.pairing()[0], float(ctx.fermion_energy()[0]),
+                                    float(ctx.hole_trace()[0]))

@@ -116,6 +116,76 @@ class SpectraBins:
         self.acc = None
 
 
+class ChainOutput:
+    """The files of one run_simulation (src/Simulation.jl:45-56,69-73):
+    simulation.log (appended, timestamped tee), observables.csv and
+    transport.csv (truncated, headers written), spectra_bins/."""
+
+    def __init__(self, out_dir: str, verbose: bool):
+        os.makedirs(out_dir, exist_ok=True)
+        self.verbose = verbose
+        self.spec_dir = os.path.join(out_dir, "spectra_bins")
+        self.f_log = open(os.path.join(out_dir, "simulation.log"), "a")
+        self.f_obs = open(os.path.join(out_dir, "observables.csv"), "w")
+        self.f_trans = open(os.path.join(out_dir, "transport.csv"), "w")
+        self.f_obs.write(OBS_HEADER + "\n")
+        self.f_trans.write(TRANSPORT_HEADER + "\n")
+        self.bins = SpectraBins()
+
+    def tee(self, msg: str):
+        line = f"[{datetime.now().strftime('%Y-%m-%d %H:%M:%S')}] {msg}"
+        print(line, file=self.f_log, flush=True)
+        if self.verbose:
+            print(line, flush=True)
+
+    def header(self, p, n_therm, n_measure, measure_transport_freq, bin_size):
+        self.tee("Starting Simulation...")
+        self.tee(f"System: {p.Lx}x{p.Ly}, β={p.beta}, n_imp={p.n_imp}, J={p.J}")
+        self.tee(f"Config: Therm={n_therm}, Sweep={n_measure}, TransFreq={measure_transport_freq}, "
+                 f"BinSize={bin_size}")
+        self.tee("Initializing State...")
+
+    def observables(self, i, acc, dH, obs):
+        self.f_obs.write(obs_csv_line(i, acc, dH, obs))
+        self.f_obs.flush()
+
+    def transport(self, i, spec, bin_size):
+        self.f_trans.write(transport_csv_line(i, spec))
+        self.f_trans.flush()
+        if self.bins.add(spec) >= bin_size:
+            self.bins.flush(self.spec_dir, i)
+
+    def close(self):
+        self.f_log.close()
+        self.f_obs.close()
+        self.f_trans.close()
+
+
+def thermalize(cache, p, state, out: ChainOutput, n_therm: int, Nt_therm_init: int, rng):
+    """The adaptive thermalisation of src/Simulation.jl:92-130 for one chain;
+    returns (final Nt, acceptance rate)."""
+    ctl = AdaptiveNt(Nt_therm_init)
+    dt = H.calc_optimal_dt(p.beta, p.J, p.mass, ctl.Nt)
+    out.tee("--- Thermalization Start ---")
+    out.tee(f"Init: Nt={ctl.Nt}, dt={round(dt, 5)}")
+    t0 = time.time()
+    acc_therm = 0
+    for i in range(1, n_therm + 1):
+        acc, _ = H.hmc_sweep(cache, p, state, Nt=ctl.Nt, dt=dt, rng=rng)
+        acc_therm += int(acc)
+        r = ctl.record(i, acc)
+        if r is None:
+            continue
+        rate, old, new = r
+        if new != old:
+            dt = H.calc_optimal_dt(p.beta, p.J, p.mass, new)
+            out.tee("Therm %d/%d. Rate=%.2f. Adjust Nt: %d -> %d, dt: %.4f" % (i, n_therm, rate, old, new, dt))
+        elif i % 20 == 0:
+            out.tee("Therm %d/%d. Rate=%.2f. Nt=%d (Stable)" % (i, n_therm, rate, new))
+    out.tee(f"Thermalization Done. Time: {round(time.time() - t0, 2)}s")
+    return ctl.Nt, acc_therm / max(n_therm, 1)
+
+
 def run_simulation(p: H.ModelParameters, out_dir: str, *, n_therm: int = 100, n_measure: int = 500,
                    Nt_therm_init: int = 10, Nt_measure: int = 5, measure_transport_freq: int = 1,
                    bin_size: int = 5, verbose: bool = True, rng: np.random.Generator | None = None,
@@ -128,26 +198,9 @@ def run_simulation(p: H.ModelParameters, out_dir: str, *, n_therm: int = 100, n_
     omega_grid.npy, and one sweep_<i>.npz per completed bin of bin_size
     measurements (opt_cond, dos, dos_AN, A_k0 averaged; count)."""
     rng = rng if rng is not None else np.random.default_rng()
-    os.makedirs(out_dir, exist_ok=True)
-    f_log = open(os.path.join(out_dir, "simulation.log"), "a")
-    f_obs = open(os.path.join(out_dir, "observables.csv"), "w")
-    f_trans = open(os.path.join(out_dir, "transport.csv"), "w")
-
-    def tee(msg: str):
-        line = f"[{datetime.now().strftime('%Y-%m-%d %H:%M:%S')}] {msg}"
-        print(line, file=f_log, flush=True)
-        if verbose:
-            print(line, flush=True)
-
+    out = ChainOutput(out_dir, verbose)
     try:
-        f_obs.write(OBS_HEADER + "\n")
-        f_trans.write(TRANSPORT_HEADER + "\n")
-        tee("Starting Simulation...")
-        tee(f"System: {p.Lx}x{p.Ly}, β={p.beta}, n_imp={p.n_imp}, J={p.J}")
-        tee(f"Config: Therm={n_therm}, Sweep={n_measure}, TransFreq={measure_transport_freq}, "
-            f"BinSize={bin_size}")
-
-        tee("Initializing State...")
+        out.header(p, n_therm, n_measure, measure_transport_freq, bin_size)
         if state is None:
             state = H.initialize_state(p, rng)
         if cache is None:
@@ -155,57 +208,109 @@ def run_simulation(p: H.ModelParameters, out_dir: str, *, n_therm: int = 100, n_
         H.init_static_H(cache, p, state)
         H.update_H_BdG(cache, p, state)
         H.diagonalize_H_BdG(cache, p)
-        spec_dir = os.path.join(out_dir, "spectra_bins")
         if measure_transport_freq > 0:
-            write_spectra_header(spec_dir, p)
-
-        ctl = AdaptiveNt(Nt_therm_init)
-        dt = H.calc_optimal_dt(p.beta, p.J, p.mass, ctl.Nt)
-        tee("--- Thermalization Start ---")
-        tee(f"Init: Nt={ctl.Nt}, dt={round(dt, 5)}")
-        t0 = time.time()
-        acc_therm = 0
-        for i in range(1, n_therm + 1):
-            acc, _ = H.hmc_sweep(cache, p, state, Nt=ctl.Nt, dt=dt, rng=rng)
-            acc_therm += int(acc)
-            r = ctl.record(i, acc)
-            if r is None:
-                continue
-            rate, old, new = r
-            if new != old:
-                dt = H.calc_optimal_dt(p.beta, p.J, p.mass, new)
-                tee("Therm %d/%d. Rate=%.2f. Adjust Nt: %d -> %d, dt: %.4f" % (i, n_therm, rate, old, new, dt))
-            elif i % 20 == 0:
-                tee("Therm %d/%d. Rate=%.2f. Nt=%d (Stable)" % (i, n_therm, rate, new))
-        tee(f"Thermalization Done. Time: {round(time.time() - t0, 2)}s")
+            write_spectra_header(out.spec_dir, p)
+        Nt_fin, acc_th = thermalize(cache, p, state, out, n_therm, Nt_therm_init, rng)
 
         dt_meas = H.calc_optimal_dt(p.beta, p.J, p.mass, Nt_measure)
-        tee("--- Measurement Start ---")
-        tee(f"Settings: Nt={Nt_measure}, dt={round(dt_meas, 5)}")
+        out.tee("--- Measurement Start ---")
+        out.tee(f"Settings: Nt={Nt_measure}, dt={round(dt_meas, 5)}")
         t1 = time.time()
         acc_total = 0
-        res = SimulationResult(ctl.Nt, acc_therm / max(n_therm, 1), 0.0)
-        bins = SpectraBins()
+        res = SimulationResult(Nt_fin, acc_th, 0.0)
         for i in range(1, n_measure + 1):
             acc, dH = H.hmc_sweep(cache, p, state, Nt=Nt_measure, dt=dt_meas, rng=rng)
             acc_total += int(acc)
             obs = H.measure_observables(cache, p, state)
-            f_obs.write(obs_csv_line(i, acc, dH, obs))
-            f_obs.flush()
+            out.observables(i, acc, dH, obs)
             res.records.append((i, acc, dH, obs))
             if measure_transport_freq > 0 and i % measure_transport_freq == 0:
                 spec = H.measure_transport_and_spectra(cache, p)
-                f_trans.write(transport_csv_line(i, spec))
-                f_trans.flush()
+                out.transport(i, spec, bin_size)
                 res.transport.append((i, spec))
-                if bins.add(spec) >= bin_size:
-                    bins.flush(spec_dir, i)
             if i % 10 == 0:
-                tee("Meas %d/%d. Acc=%.2f. E=%.4f" % (i, n_measure, acc_total / i, obs.total_energy))
+                out.tee("Meas %d/%d. Acc=%.2f. E=%.4f" % (i, n_measure, acc_total / i, obs.total_energy))
         res.meas_acceptance = acc_total / max(n_measure, 1)
-        tee(f"Measurement Done. Total Time: {round(time.time() - t1, 2)}s")
+        out.tee(f"Measurement Done. Total Time: {round(time.time() - t1, 2)}s")
         return res
     finally:
-        f_log.close()
-        f_obs.close()
-        f_trans.close()
+        out.close()
+
+
+def run_simulation_chains(p: H.ModelParameters, out_dirs, rngs, *, n_therm: int = 100, n_measure: int = 500,
+                          Nt_therm_init: int = 10, Nt_measure: int = 5, measure_transport_freq: int = 1,
+                          bin_size: int = 5, verbose: bool = False, device: int = 0,
+                          delta_cap: float = 0.0) -> list:
+    """len(out_dirs) independent run_simulation's (src/Simulation.jl:34-236),
+    chain k writing out_dirs[k] and drawing from rngs[k] in the reference's
+    order (initialize_state, then per sweep randn(ComplexF64) and rand() only
+    when ΔH >= 0).  Each chain is thermalised on its own single-chain context
+    (its own adaptive Nt, :92-130); the measurement phase, whose Nt_measure is
+    common to all chains (:133-228), runs every chain in one batched context
+    (one factorisation launch sequence per leapfrog step for all chains, and
+    one batched eigensolve per transport measurement,
+    dwh_measure_transport_batched).  Returns one SimulationResult per chain;
+    each chain's files equal what run_simulation writes for it."""
+    K = len(out_dirs)
+    if len(rngs) != K or K < 1:
+        raise ValueError("one rng per output directory")
+    outs = [ChainOutput(d, verbose) for d in out_dirs]
+    try:
+        states, results = [], []
+        for k in range(K):
+            outs[k].header(p, n_therm, n_measure, measure_transport_freq, bin_size)
+            st = H.initialize_state(p, rngs[k])
+            cache = H.initialize_cache(p, device=device, delta_cap=delta_cap)
+            H.init_static_H(cache, p, st)
+            H.update_H_BdG(cache, p, st)
+            H.diagonalize_H_BdG(cache, p)
+            if measure_transport_freq > 0:
+                write_spectra_header(outs[k].spec_dir, p)
+            Nt_fin, acc_th = thermalize(cache, p, st, outs[k], n_therm, Nt_therm_init, rngs[k])
+            cache.ctx.close()
+            states.append(st)
+            results.append(SimulationResult(Nt_fin, acc_th, 0.0))
+
+        dis = np.stack([st.disorder_pot for st in states])
+        ctx = H.FermionContext(p.Lx, p.Ly, p.t, p.tp, p.mu, p.beta, p.J, p.nn_table, p.nnn_table, dis,
+                             delta_cap=delta_cap, device=device)
+        try:
+            ctx.set_pairing(np.stack([st.Delta for st in states]))
+            ctx.factorize()
+            dt_meas = H.calc_optimal_dt(p.beta, p.J, p.mass, Nt_measure)
+            for o in outs:
+                o.tee("--- Measurement Start ---")
+                o.tee(f"Settings: Nt={Nt_measure}, dt={round(dt_meas, 5)}")
+            t1 = time.time()
+            acc_total = np.zeros(K, dtype=np.int64)
+            for i in range(1, n_measure + 1):
+                noise = np.stack([H.standard_complex_normal(r, (p.N, 2)) for r in rngs])
+                dH = ctx.hmc_trajectory(noise, Nt_measure, dt_meas, p.mass)
+                acc = np.array([bool(dH[k] < 0 or rngs[k].random() < math.exp(-dH[k])) for k in range(K)])
+                ctx.hmc_finish(acc)
+                acc_total += acc
+                D, _ = ctx.get_state()
+                P, Ef, tr = ctx.pairing(), ctx.fermion_energy(), ctx.hole_trace()
+                specs = None
+                if measure_transport_freq > 0 and i % measure_transport_freq == 0:
+                    specs = ctx.measure_transport_all(p.eta, p.domega, p.omega_max)
+                for k in range(K):
+                    obs = H.observables_from_outputs(p, D[k], P[k], Ef[k], tr[k])
+                    outs[k].observables(i, acc[k], float(dH[k]), obs)
+                    results[k].records.append((i, bool(acc[k]), float(dH[k]), obs))
+                    if specs is not None:
+                        spec = H.SpectrumResult(**specs[k])
+                        outs[k].transport(i, spec, bin_size)
+                        results[k].transport.append((i, spec))
+                    if i % 10 == 0:
+                        outs[k].tee("Meas %d/%d. Acc=%.2f. E=%.4f" % (i, n_measure, acc_total[k] / i,
+                                                                     obs.total_energy))
+            for k in range(K):
+                results[k].meas_acceptance = acc_total[k] / max(n_measure, 1)
+                outs[k].tee(f"Measurement Done. Total Time: {round(time.time() - t1, 2)}s")
+        finally:
+            ctx.close()
+        return results
+    finally:
+        for o in outs:
+            o.close()

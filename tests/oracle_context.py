@@ -83,6 +83,12 @@ class OracleContext:
         O.compute_forces(cache, p, self.Delta[chain])      # fermi_factors
         return O.measure_transport_and_spectra(cache, p)
 
+    def measure_transport_all(self, eta, domega, omega_max):
+        out = []
+        for c in range(self.nchains):
+            out.append(dict(self.measure_transport(eta, domega, omega_max, chain=c)))
+        return out
+
     def hmc_sweep(self, noise, uniform, Nt, dt, mass):
         p = dataclasses.replace(self.p, mass=mass)
         noise = self._chains(noise)

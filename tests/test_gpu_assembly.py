@@ -126,7 +126,7 @@ def test_cr_trajectory_scatter_bit_exact(dwhmc, oracle, Lx, Ly):
 
 @pytest.mark.parametrize("L", [4, 8])
 def test_golden_fixture_assembly(dwhmc, L):
-    """The committed fixtures' H_upper (tests/golden, tools/make_golden.py)."""
+    """The committed fixtures' H_upper (tests/golden, tests/make_golden.py)."""
     import dwhmc_loader  # noqa: F401  (package on sys.path)
     g = np.load(os.path.join(ROOT, "tests", "golden", f"oracle_L{L}.npz"))
     Hu = g["H_upper"]

@@ -9,6 +9,7 @@ Tolerances (fp64; the pole set approximates tanh to <= 2e-14 on the spectrum):
 The oracle restates the reference with LAPACK zheevr (oracle/dwhmc_oracle.py).
 """
 import math
+import os
 
 import numpy as np
 import pytest
@@ -95,13 +96,15 @@ def test_full_size_L32_beta16(dwhmc, oracle, algo3):
 
 
 def test_full_size_L48_beta32_batched(dwhmc, oracle, algo):
-    """BASELINE config C5 size (N = 2304, n = 4608, β = 32), two batched
-    chains with different disorder, against the eigen oracle."""
+    """BASELINE config C5 (N = 2304, n = 4608, β = 32) at its real batch: four
+    chains with different disorder in one context (nbatch = 4 x the poles,
+    the side-work placement of the bench's schedule), against the eigen
+    oracle."""
     O = oracle
-    cases = [make_case(O, 48, 48, 32.0, seed=s) for s in (4848, 4849)]
+    cases = [make_case(O, 48, 48, 32.0, seed=s) for s in (4848, 4849, 4850, 4851)]
     p = cases[0][0]
     ctx = device_ctx(dwhmc, p, np.stack([c[1] for c in cases]), algo)
-    assert ctx.info["npoles"] >= 15
+    assert ctx.info["npoles"] >= 12 and ctx.info["nchains"] == 4
     ctx.set_pairing(np.stack([c[2] for c in cases]))
     ctx.factorize()
     F = ctx.forces()
@@ -316,7 +319,9 @@ def test_site_guard_default_cap(dwhmc, oracle):
         ctx.close()
     p, dis, _ = make_case(O, 32, 32, 16.0, seed=1000)
     ctx = device_ctx(dwhmc, p, dis, "cr", delta_cap=0.0)
-    assert ctx.info["npoles"] == 13
+    # κ = 73.7 takes the κ = 76.1 entry: 12 pole pairs in the default
+    # (5e-12) table, 13 in the strict one
+    assert ctx.info["npoles"] == (13 if os.environ.get("DWHMC_POLE_TABLE") == "strict" else 12)
     ctx.close()
 
 
@@ -487,7 +492,7 @@ def test_host_mirror_api_roundtrip(dwhmc, oracle):
 
 @pytest.mark.parametrize("L", [4, 8])
 def test_golden_fixture_on_device(dwhmc, L, algo):
-    """Committed oracle vectors (tests/golden/oracle_L*.npz, tools/make_golden.py)."""
+    """Committed oracle vectors (tests/golden/oracle_L*.npz, tests/make_golden.py)."""
     import os
     g = np.load(os.path.join(os.path.dirname(__file__), "golden", f"oracle_L{L}.npz"), allow_pickle=False)
     beta = float(g["beta"])
@@ -754,7 +759,7 @@ def test_low_temperature_large_lattice_cr(dwhmc, oracle, Lx, Ly, beta):
     cache, F_ref, Ef_ref = O.evaluate(p, dis, Delta)
     P_ref, _ = O.pairing_P(cache.U, cache.E_n, p)
     ctx = device_ctx(dwhmc, p, dis, "cr")
-    assert ctx.info["npoles"] >= 25
+    assert ctx.info["npoles"] >= 20
     ctx.set_pairing(Delta)
     ctx.factorize()
     assert np.max(np.abs(ctx.pairing()[0] - P_ref)) <= 1e-11

@@ -9,7 +9,7 @@ by closed forms and identities that the reference's own scripts rely on:
                                          F = -∂H/∂Δ* (Wirtinger), ρ-block symmetry
   * src/HMC.jl leapfrog                   reversibility, O(dt²) energy error
 plus the committed golden fixture (tests/golden/oracle_L4.npz, made by
-tools/make_golden.py) as a regression vector.
+tests/make_golden.py) as a regression vector.
 """
 import math
 import os

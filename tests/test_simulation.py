@@ -137,3 +137,27 @@ def test_host_sweep_consumes_rng_like_reference(hmc_mod, dwhmc):
         assert rng.random() == replay.random()
     finally:
         hmc_mod.FermionContext = saved
+
+
+def test_run_simulation_chains_equals_single_runs(sim, hmc_mod, dwhmc, tmp_path):
+    """run_simulation_chains (per-chain thermalisation, batched measurement
+    phase) writes, for every chain, the files run_simulation writes for the
+    same rng: the batching changes how the sweeps are launched, not the
+    Markov chains (oracle backend, so the arithmetic is the same bits)."""
+    kw = dict(n_therm=10, n_measure=6, Nt_therm_init=2, Nt_measure=3, measure_transport_freq=2, bin_size=2)
+    p = dwhmc.ModelParameters(4, 4, 1.0, -0.35, -1.08, 1.0, 0.25, 8.0, 0.8, 1.0)
+    saved = hmc_mod.FermionContext
+    hmc_mod.FermionContext = OracleContext
+    try:
+        singles = [sim.run_simulation(p, str(tmp_path / f"single{k}"), rng=np.random.default_rng(100 + k),
+                                      verbose=False, **kw) for k in range(2)]
+        multi = sim.run_simulation_chains(p, [str(tmp_path / f"chain{k}") for k in range(2)],
+                                          [np.random.default_rng(100 + k) for k in range(2)], **kw)
+    finally:
+        hmc_mod.FermionContext = saved
+    for k in range(2):
+        for f in ("observables.csv", "transport.csv"):
+            assert (tmp_path / f"single{k}" / f).read_text() == (tmp_path / f"chain{k}" / f).read_text(), (k, f)
+        assert multi[k].Nt_final == singles[k].Nt_final
+        assert sorted(os.listdir(tmp_path / f"chain{k}" / "spectra_bins")) == \
+            sorted(os.listdir(tmp_path / f"single{k}" / "spectra_bins"))

@@ -29,12 +29,11 @@ def main():
     ap.add_argument("--variants", nargs="+", default=["PAIR=1", "PAIR=0"])
     a = ap.parse_args()
     import dwhmc_loader
-    from oracle import dwhmc_oracle as O
     m = dwhmc_loader.load_package()
-    p = O.ModelParameters(a.L, a.L, 1.0, -0.35, -1.08, 1.0, 0.05, a.beta, 0.8, 1.0)
+    p = m.ModelParameters(a.L, a.L, 1.0, -0.35, -1.08, 1.0, 0.05, a.beta, 0.8, 1.0)
     dis, D0 = [], []
     for c in range(a.chains):
-        st = O.initialize_state(p, np.random.default_rng(1000 + c))
+        st = m.initialize_state(p, np.random.default_rng(1000 + c))
         dis.append(st.disorder_pot)
         D0.append(st.Delta)
     rng = np.random.default_rng(7)
