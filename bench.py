@@ -413,6 +413,8 @@ def main(argv=None):
                 # coarse tail, and block inversions at 8 BP^3 each) x the timed steps
                 rec["alg_tflops"] = (w + wi + ws + wt) / replay_steps * a.steps * world / el / 1e12
                 rec["alg_flops_per_step"] = (w + wi + ws + wt) / replay_steps / a.chains
+                # the whole leapfrog step against the fp64 MFMA peak (north_star: >= 0.30 at L=32)
+                rec["alg_frac_of_peak"] = rec["alg_tflops"] / world / PEAK_F64_TFLOPS
                 nt = info["block"] // 16
                 # level-0 inversions: k_cr_inv0 (static particle block, BP = 64)
                 # when the plan has no plain k_cr_inv stage besides it

@@ -42,13 +42,17 @@ def main():
     uni = rng.random((a.sweeps, a.chains))
     dt = m.calc_optimal_dt(p.beta, p.J, p.mass, a.Nt)
     ctxs = {}
+    touched = set()
     for v in a.variants:
         kv = dict(x.split("=") for x in v.split(",") if x)
+        for k in touched:                       # knobs of the previous variant do not leak
+            os.environ.pop(k, None)
         os.environ["DWHMC_GJ_PAIR"] = kv.get("PAIR", "1")
         # any other KEY=VAL of the variant sets the context knob DWHMC_KEY
         for k, val in kv.items():
             if k not in ("PAIR", "LIB"):
                 os.environ["DWHMC_" + k] = val
+                touched.add("DWHMC_" + k)
         ctx = m.FermionContext(p.Lx, p.Ly, p.t, p.tp, p.mu, p.beta, p.J, p.nn_table, p.nnn_table,
                                np.stack(dis), lib_path=kv.get("LIB"))
         ctx.set_pairing(np.stack(D0))
