@@ -581,9 +581,11 @@ __global__ __launch_bounds__(64 * DWHMC_INV2_WAVES) void k_cr_inv2(double2* __re
 // i S has Hermitian part >= y I like i D (a Schur complement), so S needs no
 // pivoting either.  S^-1 by 2 x 2 tile blocks (HP = 32): S00^-1 in registers,
 // P = S00^-1 S01, Q = S10 S00^-1, T = S11 - S10 P, T^-1 in registers,
-// X01 = -P T^-1, X10 = -T^-1 Q, X11 = T^-1, X00 = S00^-1 - X01 Q.  The serial
-// chain is two 16 x 16 register inversions and six 16 x 16 tile products
-// instead of four inversions and their panel updates (k_cr_inv<4>).  Wave w
+// X01 = -P T^-1, X10 = -T^-1 Q, X11 = T^-1, X00 = S00^-1 + P (T^-1 Q).  The
+// serial chain is two 16 x 16 register inversions and six 16 x 16 tile
+// products in five barrier-separated phases (the wave that inverts T forms
+// its own P; X00 is formed from T^-1 directly) instead of four inversions and
+// their panel updates (k_cr_inv<4>).  Wave w
 // owns tile (w >> 1, w & 1) of every 32 x 32 matrix; tiles meet in LDS
 // (row-major, stride 17); MFMA operands in the C layout as in mma16_3m.
 // ---------------------------------------------------------------------------
@@ -639,6 +641,7 @@ __global__ __launch_bounds__(256) void k_cr_inv0(double2* __restrict__ pool, int
   double2* Mo = pool + (int64_t)bi * item + (int64_t)dst[li] * HP * BP;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
   const int ti = w >> 1, tj = w & 1;
+  CR_STAMP(0);
   // this wave's tiles: A (C layout, registers), R and B (LDS)
   d4 acr, aci;
 #pragma unroll
@@ -653,6 +656,7 @@ __global__ __launch_bounds__(256) void k_cr_inv0(double2* __restrict__ pool, int
     sR[w][(lk + 4 * rr) * 17 + lr] = r;
   }
   __syncthreads();
+  CR_STAMP(1);
   // Z = R B
   d4 zr = {0.0, 0.0, 0.0, 0.0}, zi = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -663,6 +667,7 @@ __global__ __launch_bounds__(256) void k_cr_inv0(double2* __restrict__ pool, int
   }
   tile_to_lds(sZ[w], zr, zi);
   __syncthreads();
+  CR_STAMP(2);
   // S = A + B conj(Z)
   d4 sr = acr, si = aci;
 #pragma unroll
@@ -675,46 +680,55 @@ __global__ __launch_bounds__(256) void k_cr_inv0(double2* __restrict__ pool, int
   if (w == 0) ld += 0.5 * log(wave_inv16_c(sr, si));   // S00^-1 (C layout in, C layout out)
   tile_to_lds(sS[w], sr, si);                           // S00^-1, S01, S10, S11
   __syncthreads();
-  // P = S00^-1 S01 (wave 1, kept in sA[1]); Q = S10 S00^-1 (wave 2, sA[2])
+  CR_STAMP(3);
+  // P = S00^-1 S01 (wave 1, sA[1]); Q = S10 S00^-1 (wave 2, registers + sA[2]);
+  // wave 3 forms P itself (no barrier in its chain), T = S11 - S10 P and T^-1
+  d4 qr = {0.0, 0.0, 0.0, 0.0}, qi = {0.0, 0.0, 0.0, 0.0};
   if (w == 1) {
     d4 pr = {0.0, 0.0, 0.0, 0.0}, pi = {0.0, 0.0, 0.0, 0.0};
     mma16_3m<false>(pr, pi, sS[0], sr, si);
     tile_to_lds(sA[1], pr, pi);
   } else if (w == 2) {
-    d4 qr = {0.0, 0.0, 0.0, 0.0}, qi = {0.0, 0.0, 0.0, 0.0}, br, bim;
+    d4 br, bim;
     tile_from_lds(sS[0], br, bim);
     mma16_3m<false>(qr, qi, sS[2], br, bim);
     tile_to_lds(sA[2], qr, qi);
-  }
-  __syncthreads();
-  // T = S11 - S10 P, T^-1 (wave 3, sX[3] = X11)
-  if (w == 3) {
-    d4 br, bim;
-    tile_from_lds(sA[1], br, bim);
-    mma16_3m<true>(sr, si, sS[2], br, bim);
+  } else if (w == 3) {
+    d4 br, bim, pr = {0.0, 0.0, 0.0, 0.0}, pi = {0.0, 0.0, 0.0, 0.0};
+    tile_from_lds(sS[1], br, bim);
+    mma16_3m<false>(pr, pi, sS[0], br, bim);   // P
+    mma16_3m<true>(sr, si, sS[2], pr, pi);     // T = S11 - S10 P
     ld += 0.5 * log(wave_inv16_c(sr, si));
     tile_to_lds(sX[3], sr, si);
   }
   __syncthreads();
-  // X01 = -P T^-1 (wave 1), X10 = -T^-1 Q (wave 2)
+  CR_STAMP(4);
+  CR_STAMP(5);
+  // X01 = -P T^-1 (wave 1), X10 = -T^-1 Q (wave 2), X00 = S00^-1 + P (T^-1 Q)
+  // (wave 0; = S00^-1 - X01 Q), X11 = T^-1 (wave 3)
   d4 xr = sr, xi = si;   // wave 0: S00^-1; wave 3: T^-1 = X11
-  if (w == 1 || w == 2) {
+  if (w == 1) {
     d4 br, bim;
-    tile_from_lds(w == 1 ? sX[3] : sA[2], br, bim);
+    tile_from_lds(sX[3], br, bim);
     xr = d4{0.0, 0.0, 0.0, 0.0};
     xi = d4{0.0, 0.0, 0.0, 0.0};
-    mma16_3m<true>(xr, xi, w == 1 ? sA[1] : sX[3], br, bim);
-    tile_to_lds(sX[w], xr, xi);
-  }
-  __syncthreads();
-  // X00 = S00^-1 - X01 Q (wave 0)
-  if (w == 0) {
-    d4 br, bim;
+    mma16_3m<true>(xr, xi, sA[1], br, bim);
+    tile_to_lds(sX[1], xr, xi);
+  } else if (w == 2) {
+    xr = d4{0.0, 0.0, 0.0, 0.0};
+    xi = d4{0.0, 0.0, 0.0, 0.0};
+    mma16_3m<true>(xr, xi, sX[3], qr, qi);
+    tile_to_lds(sX[2], xr, xi);
+  } else if (w == 0) {
+    d4 br, bim, ur = {0.0, 0.0, 0.0, 0.0}, ui = {0.0, 0.0, 0.0, 0.0};
     tile_from_lds(sA[2], br, bim);
-    mma16_3m<true>(xr, xi, sX[1], br, bim);
+    mma16_3m<false>(ur, ui, sX[3], br, bim);   // U = T^-1 Q
+    mma16_3m<false>(xr, xi, sA[1], ur, ui);    // X00 = S00^-1 + P U
     tile_to_lds(sX[0], xr, xi);
   }
   __syncthreads();
+  CR_STAMP(6);
+  CR_STAMP(7);
   // Y = Z conj(X)
   d4 yr = {0.0, 0.0, 0.0, 0.0}, yi = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -723,6 +737,7 @@ __global__ __launch_bounds__(256) void k_cr_inv0(double2* __restrict__ pool, int
     tile_from_lds<true>(sX[2 * k + tj], br, bim);
     mma16_3m<false>(yr, yi, sZ[2 * ti + k], br, bim);
   }
+  CR_STAMP(8);
   // top half of D^-1 = [X | Y]
 #pragma unroll
   for (int rr = 0; rr < 4; ++rr) {
@@ -736,6 +751,7 @@ __global__ __launch_bounds__(256) void k_cr_inv0(double2* __restrict__ pool, int
     const int64_t o = (int64_t)bi * nslots + slot[li];
     ldpart[o] = 0.5 * ldA[o] + ldw[0] + ldw[1];
   }
+  CR_STAMP(9);
 }
 
 // ---------------------------------------------------------------------------
