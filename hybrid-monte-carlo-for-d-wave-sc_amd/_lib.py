@@ -85,6 +85,8 @@ SIGNATURES = {
     "dwh_transport_grid": (C.c_int, [_D, _D, _D, C.POINTER(_I64), C.POINTER(_I64)]),
     "dwh_measure_transport": (C.c_int, [_P, _I64, _D, _D, _D, _DP, _DP, _P, _I64, _P, _P, _I64, _P]),
     "dwh_measure_transport_batched": (C.c_int, [_P, _D, _D, _D, _P, _P, _P, _I64, _P, _P, _I64, _P]),
+    "dwh_measure_transport_deltas": (C.c_int, [_P, _I64, _I64, _P, _D, _D, _D, _P, _P, _P, _I64, _P, _P, _I64,
+                                               _P]),
     "dwh_debug_dense_H": (C.c_int, [_P, _I64, _P]),
     "dwh_debug_level0": (C.c_int, [_P, _I64, _I64, _I32, _P, _P]),
     "dwh_debug_cr_plan_check": (C.c_int, [_I64, _I64, _I64, _I32, _I32, _P]),

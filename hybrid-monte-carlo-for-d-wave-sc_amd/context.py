@@ -240,6 +240,30 @@ class FermionContext:
                      dos_AN=dos_an[c].copy(), A_k_omega0=ak[c].reshape(Ly, Lx).T.copy())
                 for c in range(nc)]
 
+    def measure_transport_deltas(self, deltas, eta: float, domega: float, omega_max: float,
+                                 chain: int = 0) -> list:
+        """measure_transport at a list of pairing fields (each (N, 2)) on the
+        lattice and disorder of `chain`, eigensolves batched over the list
+        (dwh_measure_transport_deltas); one dict per field, in order."""
+        D = np.asarray(deltas, dtype=np.complex128)
+        if D.ndim != 3 or D.shape[1:] != (self.N, 2):
+            raise ValueError(f"expected (nstates, {self.N}, 2) pairing fields")
+        ns = D.shape[0]
+        d = np.ascontiguousarray(np.transpose(D, (0, 2, 1)))
+        nw, nd = transport_grid(eta, domega, omega_max, self._lib)
+        Lx, Ly = self.info_lattice
+        st, dc = np.empty(ns), np.empty(ns)
+        sigma, dos, dos_an = np.empty((ns, nw)), np.empty((ns, nd)), np.empty((ns, nd))
+        ak = np.empty((ns, Lx * Ly))
+        self._c(self._lib.dwh_measure_transport_deltas(self._h, int(chain), ns, ptr(d), float(eta), float(domega),
+                                                       float(omega_max), ptr(st), ptr(dc), ptr(sigma), nw,
+                                                       ptr(dos), ptr(dos_an), nd, ptr(ak)))
+        wg, dg = eta + domega * np.arange(nw), -omega_max + domega * np.arange(nd)
+        return [dict(superfluid_stiffness=float(st[k]), dc_conductivity=float(dc[k]), omega_grid=wg.copy(),
+                     optical_conductivity=sigma[k].copy(), dos_omega_grid=dg.copy(), dos=dos[k].copy(),
+                     dos_AN=dos_an[k].copy(), A_k_omega0=ak[k].reshape(Ly, Lx).T.copy())
+                for k in range(ns)]
+
     # -- assembly read-back (parity tests) --------------------------------
     def debug_dense_H(self, chain: int = 0) -> np.ndarray:
         """H_BdG(Δ) (2N, 2N) as the eigen/transport path assembles it (dwh_debug_dense_H)."""

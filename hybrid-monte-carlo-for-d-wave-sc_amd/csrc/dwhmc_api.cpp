@@ -687,6 +687,8 @@ struct dwh_ctx {
   double* d_tr_val = nullptr;
   double* d_tr_offd = nullptr;   // zheevd off-diagonal workspace (2N)
   int64_t tr_nw = -1, tr_nd = -1;   // ω / DOS grid lengths the output buffers hold
+  double2* d_tr_stage = nullptr;     // Δ snapshots of dwh_measure_transport_deltas
+  int64_t tr_nstage = 0;
 
   // timing
   int timing = 0;   // bitmask over TimerName (bit i = kTimerNames[i])
@@ -927,7 +929,17 @@ dwh::KickDrift kickdrift(dwh_ctx* ctx, double kick, double drift) {
 }
 
 int transport_prepare(dwh_ctx* ctx, int64_t nw, int64_t nd, int slots);
-int eigen_solve(dwh_ctx* ctx, int64_t c0, int m);
+// where the slots of a batched eigensolve take their H_BdG(Δ) from: slot k
+// assembles Δ = Delta + k dstride with the hopping / disorder of chain
+// chain0 + k cstep
+struct TrSrc {
+  const double2* Delta;
+  int64_t dstride;
+  int64_t chain0;
+  int cstep;
+};
+TrSrc chains_src(const dwh_ctx* ctx, int64_t c0);
+int eigen_solve(dwh_ctx* ctx, const TrSrc& src, int m);
 int eigen_info_check(dwh_ctx* ctx, int m);
 
 // algo eig: zheevd of every chain's H_BdG (src/Hamiltonian.jl:96-114), ρ =
@@ -935,7 +947,7 @@ int eigen_info_check(dwh_ctx* ctx, int m);
 // (src/Observables.jl:14-62, src/HMC.jl:21-27) in k_eig_gather
 void eig_enqueue(dwh_ctx* ctx) {
   const int N = ctx->d.N, n2 = 2 * N, nc = ctx->d.nc;
-  if (int rc = eigen_solve(ctx, 0, nc)) {
+  if (int rc = eigen_solve(ctx, chains_src(ctx, 0), nc)) {
     ctx->async_rc = rc;
     return;
   }
@@ -1741,14 +1753,20 @@ dwh::TrBufs tr_slot(const dwh_ctx* ctx, int k) {
 // chain at once): eigenvalues ascending into E, eigenvectors into the columns
 // of U (diagonalize_H_BdG!, src/Hamiltonian.jl:96-114; the reference's zheevr
 // and zheevd agree to rounding)
-int eigen_enqueue(dwh_ctx* ctx, int64_t c0, int m, bool qr) {
+TrSrc chains_src(const dwh_ctx* ctx, int64_t c0) {
+  const int64_t n2 = 2 * (int64_t)ctx->d.N;
+  return TrSrc{ctx->Delta + c0 * n2, n2, c0, 1};
+}
+
+int eigen_enqueue(dwh_ctx* ctx, const TrSrc& src, int m, bool qr) {
   const int N = ctx->d.N, n2 = 2 * N;
   const dwh::TrBufs& b = ctx->tr;
   const int64_t sA = (int64_t)n2 * n2;
   HIPCHECK(ctx, hipMemsetAsync(b.U, 0, (size_t)m * sA * sizeof(double2), ctx->stream));
   for (int k = 0; k < m; ++k)
-    dwh::launch_tr_assemble(b.U + k * sA, N, ctx->hcol, ctx->hval + (size_t)(c0 + k) * N * kHSlots,
-                            ctx->Dcol, ctx->Dsrc, ctx->Delta + (size_t)(c0 + k) * 2 * N, ctx->stream);
+    dwh::launch_tr_assemble(b.U + k * sA, N, ctx->hcol,
+                            ctx->hval + (size_t)(src.chain0 + (int64_t)k * src.cstep) * N * kHSlots, ctx->Dcol,
+                            ctx->Dsrc, src.Delta + (size_t)k * src.dstride, ctx->stream);
   HIPCHECK(ctx, hipGetLastError());
   auto* A = reinterpret_cast<rocblas_double_complex*>(b.U);
   rocblas_status st;
@@ -1772,10 +1790,10 @@ int eigen_enqueue(dwh_ctx* ctx, int64_t c0, int m, bool qr) {
 // with exactly degenerate eigenvalues (the clean lattice, W = 0), so those
 // chains are decomposed again with the QR-iteration zheev (slower, robust).
 // Synchronises the stream.  DWHMC_EIG_SOLVER=ev: zheev from the start.
-int eigen_solve(dwh_ctx* ctx, int64_t c0, int m) {
+int eigen_solve(dwh_ctx* ctx, const TrSrc& src, int m) {
   const char* es = std::getenv("DWHMC_EIG_SOLVER");
   const bool qr = es && std::strcmp(es, "ev") == 0;
-  int rc = eigen_enqueue(ctx, c0, m, qr);
+  int rc = eigen_enqueue(ctx, src, m, qr);
   if (rc || qr) return rc;
   const int64_t n2 = 2 * (int64_t)ctx->d.N;
   HIPCHECK(ctx, hipMemsetAsync(ctx->d_tr_bad, 0, sizeof(int), ctx->stream));
@@ -1783,7 +1801,7 @@ int eigen_solve(dwh_ctx* ctx, int64_t c0, int m) {
   int bad = 0;
   HIPCHECK(ctx, hipMemcpyAsync(&bad, ctx->d_tr_bad, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
   HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
-  if (bad) rc = eigen_enqueue(ctx, c0, m, true);
+  if (bad) rc = eigen_enqueue(ctx, src, m, true);
   return rc;
 }
 
@@ -1811,12 +1829,12 @@ int transport_args(dwh_ctx* ctx, double eta, double domega, double omega_max, in
 
 // measure_transport_and_spectra for chains c0 .. c0+m-1 (slots 0 .. m-1);
 // outputs per chain at strides 1 / nw / nd / N
-int transport_run(dwh_ctx* ctx, int64_t c0, int m, double eta, double domega, double omega_max, int64_t nw,
+int transport_run(dwh_ctx* ctx, const TrSrc& src, int m, double eta, double domega, double omega_max, int64_t nw,
                   int64_t nd, double* stiffness, double* dc_cond, double* sigma, double* dos, double* dos_an,
                   double* ak0) {
   int rc;
   if ((rc = transport_prepare(ctx, nw, nd, m))) return rc;
-  if ((rc = eigen_solve(ctx, c0, m))) return rc;
+  if ((rc = eigen_solve(ctx, src, m))) return rc;
   const int N = ctx->d.N, n2 = 2 * N;
   const int64_t sA = (int64_t)n2 * n2;
   hipStream_t s = ctx->stream;
@@ -1881,7 +1899,7 @@ int dwh_eigensystem(dwh_ctx* ctx, int64_t chain, double* E, dwh_c128* U) {
   int rc;
   if ((rc = transport_prepare(ctx, std::max<int64_t>(ctx->tr_nw, 0), std::max<int64_t>(ctx->tr_nd, 0), 1)))
     return rc;
-  if ((rc = eigen_solve(ctx, chain, 1))) return rc;
+  if ((rc = eigen_solve(ctx, chains_src(ctx, chain), 1))) return rc;
   const size_t n2 = 2 * (size_t)ctx->d.N;
   HIPCHECK(ctx, hipMemcpyAsync(E, ctx->tr.E, n2 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
   if (U)
@@ -1901,7 +1919,7 @@ int dwh_measure_transport(dwh_ctx* ctx, int64_t chain, double eta, double domega
   if ((nw > 0 && !sigma) || (nd > 0 && (!dos || !dos_an))) return fail(ctx, DWH_ERR_ARG, "NULL grid output");
   HIPCHECK(ctx, hipSetDevice(ctx->device));
   SETTLE(ctx);
-  return transport_run(ctx, chain, 1, eta, domega, omega_max, nw, nd, stiffness, dc_cond, sigma, dos, dos_an,
+  return transport_run(ctx, chains_src(ctx, chain), 1, eta, domega, omega_max, nw, nd, stiffness, dc_cond, sigma, dos, dos_an,
                        ak0);
 }
 
@@ -1921,9 +1939,51 @@ int dwh_measure_transport_batched(dwh_ctx* ctx, double eta, double domega, doubl
   const int group = std::max(1, std::min(nc, (int)(16.0 * (1 << 30) / per)));
   for (int c0 = 0; c0 < nc; c0 += group) {
     const int m = std::min(group, nc - c0);
-    if ((rc = transport_run(ctx, c0, m, eta, domega, omega_max, nw, nd, stiffness + c0, dc_cond + c0,
+    if ((rc = transport_run(ctx, chains_src(ctx, c0), m, eta, domega, omega_max, nw, nd, stiffness + c0, dc_cond + c0,
                             sigma ? sigma + (size_t)c0 * nw : nullptr, dos ? dos + (size_t)c0 * nd : nullptr,
                             dos_an ? dos_an + (size_t)c0 * nd : nullptr, ak0 + (size_t)c0 * N)))
+      return rc;
+  }
+  return DWH_OK;
+}
+
+int dwh_measure_transport_deltas(dwh_ctx* ctx, int64_t chain, int64_t nstates, const dwh_c128* Delta,
+                                 double eta, double domega, double omega_max, double* stiffness,
+                                 double* dc_cond, double* sigma, int64_t n_omega, double* dos, double* dos_an,
+                                 int64_t n_dos, double* ak0) {
+  if (!ctx || !Delta || !stiffness || !dc_cond || !ak0) return fail(ctx, DWH_ERR_ARG, "NULL argument");
+  if (chain < 0 || chain >= ctx->d.nc) return fail(ctx, DWH_ERR_ARG, "chain index out of range");
+  if (nstates < 1) return fail(ctx, DWH_ERR_ARG, "nstates must be >= 1");
+  int64_t nw = 0, nd = 0;
+  int rc;
+  if ((rc = transport_args(ctx, eta, domega, omega_max, n_omega, n_dos, &nw, &nd))) return rc;
+  if ((nw > 0 && !sigma) || (nd > 0 && (!dos || !dos_an))) return fail(ctx, DWH_ERR_ARG, "NULL grid output");
+  HIPCHECK(ctx, hipSetDevice(ctx->device));
+  SETTLE(ctx);
+  const int N = ctx->d.N;
+  const int64_t n2 = 2 * (int64_t)N;
+  for (int64_t e = 0; e < nstates * n2; ++e)
+    if (!std::isfinite(Delta[e].re) || !std::isfinite(Delta[e].im)) return fail(ctx, DWH_ERR_ARG, "non-finite Delta");
+  // staging buffer for the snapshots (grown on demand)
+  if (nstates > ctx->tr_nstage) {
+    HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+    drop_alloc(ctx, ctx->d_tr_stage);
+    ctx->d_tr_stage = nullptr;
+    ctx->tr_nstage = 0;
+    if ((rc = dalloc(ctx, &ctx->d_tr_stage, (size_t)nstates * n2))) return rc;
+    ctx->tr_nstage = nstates;
+  }
+  HIPCHECK(ctx, hipMemcpyAsync(ctx->d_tr_stage, Delta, (size_t)nstates * n2 * sizeof(double2),
+                               hipMemcpyHostToDevice, ctx->stream));
+  // groups whose three n2 x n2 work matrices fit in 16 GiB, as the batched call
+  const double per = 3.0 * 16.0 * 4.0 * N * (double)N;
+  const int group = std::max(1, std::min((int)nstates, (int)(16.0 * (1 << 30) / per)));
+  for (int64_t s0 = 0; s0 < nstates; s0 += group) {
+    const int m = (int)std::min<int64_t>(group, nstates - s0);
+    const TrSrc src{ctx->d_tr_stage + s0 * n2, n2, chain, 0};
+    if ((rc = transport_run(ctx, src, m, eta, domega, omega_max, nw, nd, stiffness + s0, dc_cond + s0,
+                            sigma ? sigma + (size_t)s0 * nw : nullptr, dos ? dos + (size_t)s0 * nd : nullptr,
+                            dos_an ? dos_an + (size_t)s0 * nd : nullptr, ak0 + (size_t)s0 * N)))
       return rc;
   }
   return DWH_OK;

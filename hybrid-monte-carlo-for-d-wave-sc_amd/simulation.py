@@ -186,17 +186,54 @@ def thermalize(cache, p, state, out: ChainOutput, n_therm: int, Nt_therm_init: i
     return ctl.Nt, acc_therm / max(n_therm, 1)
 
 
+class TransportQueue:
+    """Transport measurements (src/Simulation.jl:169-220) of one chain taken at
+    the Δ of their sweeps and evaluated `batch` at a time: the eigensolves of
+    a batch run as one batched call (dwh_measure_transport_deltas), ~3x the
+    throughput of one call per sweep at L = 32.  Rows and bins come out in
+    sweep order, each when its batch is measured (batch = 1: right away, as
+    the reference writes them)."""
+
+    def __init__(self, ctx, p, out: ChainOutput, res: SimulationResult, bin_size: int, batch: int, chain: int = 0):
+        self.ctx, self.p, self.out, self.res = ctx, p, out, res
+        self.bin_size, self.batch, self.chain = bin_size, max(1, int(batch)), chain
+        self.pending = []            # (sweep, Δ snapshot)
+
+    def add(self, sweep: int, Delta):
+        self.pending.append((sweep, np.array(Delta, dtype=np.complex128, copy=True)))
+        if len(self.pending) >= self.batch:
+            self.flush()
+
+    def flush(self):
+        if not self.pending:
+            return
+        p = self.p
+        if self.batch == 1:
+            specs = [self.ctx.measure_transport(p.eta, p.domega, p.omega_max, chain=self.chain)]
+        else:
+            specs = self.ctx.measure_transport_deltas(np.stack([d for _, d in self.pending]), p.eta, p.domega,
+                                                      p.omega_max, chain=self.chain)
+        for (i, _), r in zip(self.pending, specs):
+            spec = H.SpectrumResult(**r)
+            self.out.transport(i, spec, self.bin_size)
+            self.res.transport.append((i, spec))
+        self.pending = []
+
+
 def run_simulation(p: H.ModelParameters, out_dir: str, *, n_therm: int = 100, n_measure: int = 500,
                    Nt_therm_init: int = 10, Nt_measure: int = 5, measure_transport_freq: int = 1,
                    bin_size: int = 5, verbose: bool = True, rng: np.random.Generator | None = None,
                    device: int = 0, delta_cap: float = 0.0, state: H.SimulationState | None = None,
-                   cache: H.ComputeCache | None = None) -> SimulationResult:
+                   cache: H.ComputeCache | None = None, transport_batch: int = 1) -> SimulationResult:
     """src/Simulation.jl:34-236.  Files in out_dir: simulation.log (appended),
     observables.csv, transport.csv (one row per transport measurement, every
     measure_transport_freq sweeps; <= 0 disables), and spectra_bins/ — the
     reference's spectra_bins.jld2 (:52,89,206-214) as numpy files: params.json,
     omega_grid.npy, and one sweep_<i>.npz per completed bin of bin_size
-    measurements (opt_cond, dos, dos_AN, A_k0 averaged; count)."""
+    measurements (opt_cond, dos, dos_AN, A_k0 averaged; count).
+    transport_batch > 1 evaluates that many measurement sweeps' transport in
+    one batched call (TransportQueue): same rows and bins, written up to
+    transport_batch - 1 sweeps later."""
     rng = rng if rng is not None else np.random.default_rng()
     out = ChainOutput(out_dir, verbose)
     try:
@@ -218,6 +255,7 @@ def run_simulation(p: H.ModelParameters, out_dir: str, *, n_therm: int = 100, n_
         t1 = time.time()
         acc_total = 0
         res = SimulationResult(Nt_fin, acc_th, 0.0)
+        tq = TransportQueue(cache.require(), p, out, res, bin_size, transport_batch)
         for i in range(1, n_measure + 1):
             acc, dH = H.hmc_sweep(cache, p, state, Nt=Nt_measure, dt=dt_meas, rng=rng)
             acc_total += int(acc)
@@ -225,11 +263,10 @@ def run_simulation(p: H.ModelParameters, out_dir: str, *, n_therm: int = 100, n_
             out.observables(i, acc, dH, obs)
             res.records.append((i, acc, dH, obs))
             if measure_transport_freq > 0 and i % measure_transport_freq == 0:
-                spec = H.measure_transport_and_spectra(cache, p)
-                out.transport(i, spec, bin_size)
-                res.transport.append((i, spec))
+                tq.add(i, state.Delta)
             if i % 10 == 0:
                 out.tee("Meas %d/%d. Acc=%.2f. E=%.4f" % (i, n_measure, acc_total / i, obs.total_energy))
+        tq.flush()
         res.meas_acceptance = acc_total / max(n_measure, 1)
         out.tee(f"Measurement Done. Total Time: {round(time.time() - t1, 2)}s")
         return res
@@ -240,7 +277,7 @@ def run_simulation(p: H.ModelParameters, out_dir: str, *, n_therm: int = 100, n_
 def run_simulation_chains(p: H.ModelParameters, out_dirs, rngs, *, n_therm: int = 100, n_measure: int = 500,
                           Nt_therm_init: int = 10, Nt_measure: int = 5, measure_transport_freq: int = 1,
                           bin_size: int = 5, verbose: bool = False, device: int = 0,
-                          delta_cap: float = 0.0) -> list:
+                          delta_cap: float = 0.0, transport_batch: int = 1) -> list:
     """len(out_dirs) independent run_simulation's (src/Simulation.jl:34-236),
     chain k writing out_dirs[k] and drawing from rngs[k] in the reference's
     order (initialize_state, then per sweep randn(ComplexF64) and rand() only
@@ -249,8 +286,10 @@ def run_simulation_chains(p: H.ModelParameters, out_dirs, rngs, *, n_therm: int 
     common to all chains (:133-228), runs every chain in one batched context
     (one factorisation launch sequence per leapfrog step for all chains, and
     one batched eigensolve per transport measurement,
-    dwh_measure_transport_batched).  Returns one SimulationResult per chain;
-    each chain's files equal what run_simulation writes for it."""
+    dwh_measure_transport_batched; with transport_batch > 1, per chain
+    transport_batch sweeps at once, TransportQueue).  Returns one
+    SimulationResult per chain; each chain's files equal what run_simulation
+    writes for it."""
     K = len(out_dirs)
     if len(rngs) != K or K < 1:
         raise ValueError("one rng per output directory")
@@ -283,6 +322,8 @@ def run_simulation_chains(p: H.ModelParameters, out_dirs, rngs, *, n_therm: int 
                 o.tee(f"Settings: Nt={Nt_measure}, dt={round(dt_meas, 5)}")
             t1 = time.time()
             acc_total = np.zeros(K, dtype=np.int64)
+            tqs = [TransportQueue(ctx, p, outs[k], results[k], bin_size, transport_batch, chain=k)
+                   for k in range(K)] if transport_batch > 1 else None
             for i in range(1, n_measure + 1):
                 noise = np.stack([H.standard_complex_normal(r, (p.N, 2)) for r in rngs])
                 dH = ctx.hmc_trajectory(noise, Nt_measure, dt_meas, p.mass)
@@ -293,7 +334,11 @@ def run_simulation_chains(p: H.ModelParameters, out_dirs, rngs, *, n_therm: int 
                 P, Ef, tr = ctx.pairing(), ctx.fermion_energy(), ctx.hole_trace()
                 specs = None
                 if measure_transport_freq > 0 and i % measure_transport_freq == 0:
-                    specs = ctx.measure_transport_all(p.eta, p.domega, p.omega_max)
+                    if tqs is None:
+                        specs = ctx.measure_transport_all(p.eta, p.domega, p.omega_max)
+                    else:
+                        for k in range(K):
+                            tqs[k].add(i, D[k])
                 for k in range(K):
                     obs = H.observables_from_outputs(p, D[k], P[k], Ef[k], tr[k])
                     outs[k].observables(i, acc[k], float(dH[k]), obs)
@@ -305,6 +350,8 @@ def run_simulation_chains(p: H.ModelParameters, out_dirs, rngs, *, n_therm: int 
                     if i % 10 == 0:
                         outs[k].tee("Meas %d/%d. Acc=%.2f. E=%.4f" % (i, n_measure, acc_total[k] / i,
                                                                      obs.total_energy))
+            for tq in tqs or []:
+                tq.flush()
             for k in range(K):
                 results[k].meas_acceptance = acc_total[k] / max(n_measure, 1)
                 outs[k].tee(f"Measurement Done. Total Time: {round(time.time() - t1, 2)}s")

@@ -225,6 +225,19 @@ int dwh_measure_transport_batched(dwh_ctx* ctx, double eta, double domega, doubl
                                   double* stiffness, double* dc_cond, double* sigma, int64_t n_omega,
                                   double* dos, double* dos_an, int64_t n_dos, double* ak0);
 
+/* measure_transport_and_spectra at nstates pairing fields of one chain's
+ * lattice and disorder: Delta[k] (nstates x 2N, the Δ layout above), e.g. the
+ * states of nstates consecutive measurement sweeps [src/Simulation.jl:169-171]
+ * kept by the host and measured in one call.  The eigensolves and J_mn
+ * products are batched over the snapshots as in
+ * dwh_measure_transport_batched; outputs per snapshot k at stiffness[k],
+ * dc_cond[k], sigma[k*n_omega], dos[k*n_dos], dos_an[k*n_dos], ak0[k*Lx*Ly].
+ * The context's own Δ is not touched. */
+int dwh_measure_transport_deltas(dwh_ctx* ctx, int64_t chain, int64_t nstates, const dwh_c128* Delta,
+                                 double eta, double domega, double omega_max, double* stiffness,
+                                 double* dc_cond, double* sigma, int64_t n_omega, double* dos, double* dos_an,
+                                 int64_t n_dos, double* ak0);
+
 /* ---- assembly read-back (parity tests; not on the hot path) -------------
  * The BdG matrix H_BdG(Δ) exactly as the device assembles it, so tests can
  * compare it bit-for-bit with init_static_H! + update_H_BdG!

@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--cpu", action="store_true", help="also time the CPU restatement")
     ap.add_argument("--cpu-omega", type=int, default=40, help="ω points of the CPU σ sample")
     ap.add_argument("--chains", type=int, default=4, help="chains of the batched measurement")
+    ap.add_argument("--snapshots", default="4,8", help="Δ-snapshot batch sizes (dwh_measure_transport_deltas)")
     a = ap.parse_args()
 
     import dwhmc_loader
@@ -57,6 +58,16 @@ def main():
     for _ in range(a.steps):
         ctx.eigensystem(0, vectors=False)
     t_eig = (time.perf_counter() - t0) / a.steps
+    # Δ snapshots of one chain in one call (run_simulation(transport_batch=K))
+    snaps = {}
+    for K in [int(x) for x in a.snapshots.split(",") if x]:
+        Ds = np.stack([D + 0.01 * k * rng.standard_normal((N, 2)) for k in range(K)])
+        ctx.measure_transport_deltas(Ds, p.eta, p.domega, p.omega_max)
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            ctx.measure_transport_deltas(Ds, p.eta, p.domega, p.omega_max)
+        t = (time.perf_counter() - t0) / a.steps
+        snaps[str(K)] = {"ms_per_call": 1e3 * t, "ms_per_measurement": 1e3 * t / K}
     ctx.close()
     # batched: --chains chains in one context, dwh_measure_transport_batched
     nc = a.chains
@@ -78,6 +89,7 @@ def main():
                    "n_omega": nw, "n_dos": nd},
         "sigma_pair_terms": n2 * n2 * nw,
         "batched": {"chains": nc, "ms_per_call": 1e3 * t_batch, "ms_per_chain": 1e3 * t_batch / nc},
+        "snapshots": snaps,
     }
     if a.cpu:
         from oracle import dwhmc_oracle as O

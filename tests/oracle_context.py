@@ -83,6 +83,15 @@ class OracleContext:
         O.compute_forces(cache, p, self.Delta[chain])      # fermi_factors
         return O.measure_transport_and_spectra(cache, p)
 
+    def measure_transport_deltas(self, deltas, eta, domega, omega_max, chain=0):
+        keep = self.Delta[chain].copy()
+        out = []
+        for D in np.asarray(deltas):
+            self.Delta[chain] = D
+            out.append(dict(self.measure_transport(eta, domega, omega_max, chain=chain)))
+        self.Delta[chain] = keep
+        return out
+
     def measure_transport_all(self, eta, domega, omega_max):
         out = []
         for c in range(self.nchains):

@@ -161,3 +161,34 @@ def test_run_simulation_chains_equals_single_runs(sim, hmc_mod, dwhmc, tmp_path)
         assert multi[k].Nt_final == singles[k].Nt_final
         assert sorted(os.listdir(tmp_path / f"chain{k}" / "spectra_bins")) == \
             sorted(os.listdir(tmp_path / f"single{k}" / "spectra_bins"))
+
+
+def test_transport_batch_writes_the_same_files(sim, hmc_mod, dwhmc, tmp_path):
+    """transport_batch > 1 (TransportQueue: Δ snapshots measured in one
+    batched call) delays the transport rows, it does not change them: same
+    transport.csv and spectra bins as one measurement per sweep, for the
+    single-chain driver and the batched-chains driver, a batch size that does
+    not divide the measurement count included (the tail is flushed)."""
+    kw = dict(n_therm=6, n_measure=7, Nt_therm_init=2, Nt_measure=3, measure_transport_freq=1, bin_size=2)
+    p = dwhmc.ModelParameters(4, 4, 1.0, -0.35, -1.08, 1.0, 0.25, 8.0, 0.8, 1.0)
+    saved = hmc_mod.FermionContext
+    hmc_mod.FermionContext = OracleContext
+    try:
+        for tb in (1, 3):
+            sim.run_simulation(p, str(tmp_path / f"s{tb}"), rng=np.random.default_rng(7), verbose=False,
+                               transport_batch=tb, **kw)
+            sim.run_simulation_chains(p, [str(tmp_path / f"c{tb}_{k}") for k in range(2)],
+                                      [np.random.default_rng(7 + k) for k in range(2)], transport_batch=tb, **kw)
+    finally:
+        hmc_mod.FermionContext = saved
+    for a, b in [("s1", "s3"), ("c1_0", "c3_0"), ("c1_1", "c3_1"), ("s1", "c3_0")]:
+        for f in ("observables.csv", "transport.csv"):
+            assert (tmp_path / a / f).read_text() == (tmp_path / b / f).read_text(), (a, b, f)
+        names = sorted(os.listdir(tmp_path / a / "spectra_bins"))
+        assert names == sorted(os.listdir(tmp_path / b / "spectra_bins"))
+        assert len((tmp_path / a / "transport.csv").read_text().splitlines()) == 8
+        for n in names:
+            if n.endswith(".npz"):
+                x, y = np.load(tmp_path / a / "spectra_bins" / n), np.load(tmp_path / b / "spectra_bins" / n)
+                for key in x.files:
+                    assert np.array_equal(x[key], y[key]), (a, b, n, key)

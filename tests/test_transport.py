@@ -220,6 +220,33 @@ def test_transport_batched_matches_per_chain(dwhmc, oracle, Lx, Ly, nc):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("Lx,Ly,ns", [(6, 4, 5), (16, 16, 3)])
+def test_transport_deltas_matches_per_state(dwhmc, oracle, Lx, Ly, ns):
+    """dwh_measure_transport_deltas (Δ snapshots of chain 1, eigensolves
+    batched over the snapshots) = the oracle at each snapshot on chain 1's
+    disorder, and the device state is left as it was."""
+    O = oracle
+    p, dis0, D0 = _case(O, Lx, Ly, 8.0, seed=700)
+    _, dis1, D1 = _case(O, Lx, Ly, 8.0, seed=701)
+    snaps = [_case(O, Lx, Ly, 8.0, seed=710 + k)[2] for k in range(ns)]
+    ctx = _ctx(dwhmc, p, np.stack([dis0, dis1]))
+    ctx.set_pairing(np.stack([D0, D1]))
+    rs = ctx.measure_transport_deltas(np.stack(snaps), p.eta, p.domega, p.omega_max, chain=1)
+    Dnow, _ = ctx.get_state()
+    one = ctx.measure_transport(p.eta, p.domega, p.omega_max, chain=1)
+    with pytest.raises(ValueError):
+        ctx.measure_transport_deltas(np.stack(snaps), p.eta, p.domega, p.omega_max, chain=2)
+    ctx.close()
+    assert np.array_equal(Dnow, np.stack([D0, D1]))
+    cache, _, _ = O.evaluate(p, dis1, D1)
+    _check_transport(one, O.measure_transport_and_spectra(cache, p))
+    assert len(rs) == ns
+    for k, D in enumerate(snaps):
+        cache, _, _ = O.evaluate(p, dis1, D)
+        _check_transport(rs[k], O.measure_transport_and_spectra(cache, p))
+
+
+@pytest.mark.gpu
 def test_transport_L32_properties(dwhmc, oracle):
     """BASELINE C3 size (N = 1024): device vs oracle at full size, plus the
     size-independent checks ∫DOS dω ≈ 1 on the grid and A(k,0) ≥ 0."""
