@@ -1175,6 +1175,62 @@ double spectral_radius_bound(const std::vector<std::vector<std::pair<int, double
   return 1.02 * rho + 1e-12;
 }
 
+// Certifies rho >= ‖h‖ for the real symmetric h (off-diagonal hrow, diagonal
+// diag): rho I - h and rho I + h are positive definite iff every pivot of
+// their LDLᵀ factorisations is > 0 (Sylvester's law of inertia), so a
+// Lanczos estimate that missed an eigenvalue fails here.  Band LDLᵀ in the
+// folded row order (lattice rows 0, Ly-1, 1, Ly-2, ...: with the periodic
+// corner folded in, the lattice couplings lie within 3 Lx - 1 of the
+// diagonal), O(N b²); a bandwidth over 512 (a table that is not a lattice of
+// rows) is not certified and the caller keeps the Gershgorin bound.
+bool certify_spectral_bound(const std::vector<std::vector<std::pair<int, double>>>& hrow, const double* diag,
+                            int N, int Lx, int Ly, double rho) {
+  auto pos = [&](int i) {
+    const int x = i % Lx, y = i / Lx;
+    const int f = 2 * y < Ly ? 2 * y : 2 * (Ly - 1 - y) + 1;
+    return f * Lx + x;
+  };
+  std::vector<int> p(N), inv(N);
+  int b = 0;
+  for (int i = 0; i < N; ++i) {
+    p[i] = pos(i);
+    inv[p[i]] = i;
+  }
+  for (int i = 0; i < N; ++i)
+    for (const auto& e : hrow[i]) b = std::max(b, std::abs(p[i] - p[e.first]));
+  if (b > 512) return false;
+  const size_t W = (size_t)b + 1;
+  std::vector<double> A((size_t)N * W), Lw((size_t)N * W), d(N);
+  for (int sgn = -1; sgn <= 1; sgn += 2) {   // rho I + sgn h
+    std::fill(A.begin(), A.end(), 0.0);
+    for (int k = 0; k < N; ++k) {   // row k of the lower band: A[k][k - j] at k * W + j
+      const int i = inv[k];
+      A[(size_t)k * W] = rho + sgn * diag[i];
+      for (const auto& e : hrow[i]) {
+        const int c = p[e.first];
+        if (c < k) A[(size_t)k * W + (k - c)] += sgn * e.second;
+      }
+    }
+    // L[k][j] d[j] kept as Lw (the row's W entries), L[k][j] recovered on use
+    for (int k = 0; k < N; ++k) {
+      const int j0 = std::max(0, k - b);
+      double dk = A[(size_t)k * W];
+      for (int j = j0; j < k; ++j) {
+        // s = A[k][j] - Σ_{i < j} L[k][i] d[i] L[j][i]
+        double sacc = A[(size_t)k * W + (k - j)];
+        const int i0 = std::max(j0, j - b);
+        for (int i = i0; i < j; ++i)
+          sacc -= Lw[(size_t)k * W + (k - i)] * (Lw[(size_t)j * W + (j - i)] / d[i]);
+        Lw[(size_t)k * W + (k - j)] = sacc;   // = L[k][j] d[j]
+        dk -= sacc * sacc / d[j];
+      }
+      if (!(dk > 0)) return false;
+      d[k] = dk;
+    }
+  }
+  return true;
+}
+
 // Default guard cap.  Bond guard (max|Δ_ij| <= cap): 2 (the ordered phase), or
 // 6 standard deviations of the Gaussian boson fluctuations <|Δ|²> = 2J/β at
 // high temperature.  Site guard (the mean of |Δ| over each site's four bonds
@@ -1186,6 +1242,52 @@ double spectral_radius_bound(const std::vector<std::vector<std::pair<int, double
 double default_delta_cap(double beta, double J, bool site_guard) {
   const double s = std::sqrt(2.0 * std::fabs(J) / beta);
   return site_guard ? std::max(1.25, 4.0 * s) : std::max(2.0, 6.0 * s);
+}
+
+// ‖h‖ bound over the chains: min(Gershgorin, Lanczos) when every chain's
+// h certifies the Lanczos value, else Gershgorin
+double h_norm_bound(const std::vector<std::vector<std::pair<int, double>>>& hrow, const double* disorder, double mu,
+                    int N, int Lx, int Ly, int64_t nchains, double gersh, double* lanczos = nullptr,
+                    bool* certified = nullptr) {
+  double rho = 0;
+  std::vector<double> diag(N);
+  for (int64_t c = 0; c < nchains; ++c) {
+    for (int i = 0; i < N; ++i) diag[i] = disorder[c * (int64_t)N + i] - mu;
+    rho = std::max(rho, spectral_radius_bound(hrow, diag.data(), N));
+  }
+  bool ok = rho < gersh;
+  for (int64_t c = 0; c < nchains && ok; ++c) {
+    for (int i = 0; i < N; ++i) diag[i] = disorder[c * (int64_t)N + i] - mu;
+    ok = certify_spectral_bound(hrow, diag.data(), N, Lx, Ly, rho);
+  }
+  if (lanczos) *lanczos = rho;
+  if (certified) *certified = ok;
+  return ok ? rho : gersh;
+}
+
+// static h (off-diagonal rows): the reference's upper-triangle loop with
+// overwrite (Hamiltonian.jl:26-44), nnn after nn
+std::vector<std::vector<std::pair<int, double>>> build_hrow(int N, double t, double tp, const int64_t* nn,
+                                                            const int64_t* nnn) {
+  auto NN = [&](int i, int dir) { return (int)(nn[(int64_t)dir * N + i] - 1); };
+  auto NNN = [&](int i, int dir) { return (int)(nnn[(int64_t)dir * N + i] - 1); };
+  std::map<std::pair<int, int>, double> up;
+  for (int i = 0; i < N; ++i) {
+    for (int dir = 0; dir < 4; ++dir) {
+      const int j = NN(i, dir);
+      if (j > i) up[{i, j}] = -t;
+    }
+    for (int dir = 0; dir < 4; ++dir) {
+      const int j = NNN(i, dir);
+      if (j > i) up[{i, j}] = -tp;
+    }
+  }
+  std::vector<std::vector<std::pair<int, double>>> hrow(N);
+  for (auto& kv : up) {
+    hrow[kv.first.first].push_back({kv.first.second, kv.second});
+    hrow[kv.first.second].push_back({kv.first.first, kv.second});
+  }
+  return hrow;
 }
 
 int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, double mu, double beta,
@@ -1213,22 +1315,7 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
   auto NNN = [&](int i, int dir) { return (int)(nnn[(int64_t)dir * N + i] - 1); };
 
   // --- static h: reference upper-triangle loop with overwrite (Hamiltonian.jl:26-44)
-  std::map<std::pair<int, int>, double> up;
-  for (int i = 0; i < N; ++i) {
-    for (int dir = 0; dir < 4; ++dir) {
-      const int j = NN(i, dir);
-      if (j > i) up[{i, j}] = -t;
-    }
-    for (int dir = 0; dir < 4; ++dir) {
-      const int j = NNN(i, dir);
-      if (j > i) up[{i, j}] = -tp;
-    }
-  }
-  std::vector<std::vector<std::pair<int, double>>> hrow(N);
-  for (auto& kv : up) {
-    hrow[kv.first.first].push_back({kv.first.second, kv.second});
-    hrow[kv.first.second].push_back({kv.first.first, kv.second});
-  }
+  const std::vector<std::vector<std::pair<int, double>>> hrow = build_hrow(N, t, tp, nn, nnn);
   std::vector<int> hcol((size_t)N * kHSlots, -1);
   std::vector<double> hval((size_t)nchains * N * kHSlots, 0.0);
   double hmax = 0;
@@ -1292,15 +1379,8 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
   // ‖h‖ <= min(Gershgorin, Lanczos bound) and the pairing block's norm <= its
   // max row sum Σ_j |Δ_ij|/2 <= 2 delta_cap (bond guard: each of the 4 bonds
   // <= cap; site guard: their mean <= cap)
-  {
-    double rho = 0;
-    std::vector<double> diag(N);
-    for (int64_t c = 0; c < nchains; ++c) {
-      for (int i = 0; i < N; ++i) diag[i] = disorder[c * N64 + i] - mu;
-      rho = std::max(rho, spectral_radius_bound(hrow, diag.data(), N));
-    }
-    hmax = std::min(hmax, rho);
-  }
+  // (the Lanczos bound only where certified, certify_spectral_bound)
+  hmax = h_norm_bound(hrow, disorder, mu, N, (int)Lx, (int)Ly, nchains, hmax);
   // algorithm: explicit request, else DWHMC_ALGO = dense | cr | eig | auto
   // (auto: cr when the lattice-row block 2 Lx fits a supported padded size,
   // else dense; eig when κ = β E'/2 is beyond the pole table)
@@ -2667,6 +2747,34 @@ int dwh_debug_cr_plan_flops(int64_t Lx, int64_t Ly, int64_t nbatch, int32_t side
       flops[1] += st.flops;
     }
   }
+  return DWH_OK;
+}
+
+int dwh_debug_h_bound(int64_t Lx, int64_t Ly, double t, double tp, double mu, const int64_t* nn_table,
+                      const int64_t* nnn_table, int64_t nchains, const double* disorder, double* out) {
+  if (Lx < 1 || Ly < 1 || nchains < 1 || !nn_table || !nnn_table || !disorder || !out)
+    return fail(nullptr, DWH_ERR_ARG, "bad lattice / NULL argument");
+  const int64_t N64 = Lx * Ly;
+  if (N64 > 9216) return fail(nullptr, DWH_ERR_ARG, "N = Lx*Ly > 9216 not supported");
+  for (int64_t e = 0; e < 4 * N64; ++e)
+    if (nn_table[e] < 1 || nn_table[e] > N64 || nnn_table[e] < 1 || nnn_table[e] > N64)
+      return fail(nullptr, DWH_ERR_ARG, "neighbour table entry out of [1, N]");
+  const int N = (int)N64;
+  const auto hrow = build_hrow(N, t, tp, nn_table, nnn_table);
+  double gersh = 0;
+  for (int64_t c = 0; c < nchains; ++c)
+    for (int i = 0; i < N; ++i) {
+      double off = 0;
+      for (const auto& e : hrow[i]) off += std::fabs(e.second);
+      gersh = std::max(gersh, std::fabs(disorder[c * N64 + i] - mu) + off);
+    }
+  double lz = 0;
+  bool ok = false;
+  out[3] = h_norm_bound(hrow, disorder, mu, N, (int)Lx, (int)Ly, nchains, gersh, &lz, &ok);
+  out[0] = gersh;
+  out[1] = lz;
+  out[2] = ok ? 1.0 : 0.0;
+  out[4] = certify_spectral_bound(hrow, std::vector<double>(N, -mu).data(), N, (int)Lx, (int)Ly, 0.0) ? 1.0 : 0.0;
   return DWH_OK;
 }
 

@@ -277,6 +277,15 @@ int dwh_debug_cr_plan_check(int64_t Lx, int64_t Ly, int64_t nbatch, int32_t side
  * output windows).  flops[1] + flops[2] does not depend on `side`. */
 int dwh_debug_cr_plan_flops(int64_t Lx, int64_t Ly, int64_t nbatch, int32_t side, int32_t inv0, double* flops);
 
+/* The ‖h‖ bound pole selection uses (host only; h = the static particle block
+ * of src/Hamiltonian.jl:10-44 with w_i - mu on the diagonal, per chain):
+ * out[0] Gershgorin, out[1] the Lanczos estimate, out[2] 1 if every chain
+ * certified it (rho I -/+ h positive definite by band LDLᵀ), out[3] the bound
+ * used (the Lanczos value if certified, else Gershgorin), out[4] a negative
+ * control (1 if rho = 0 "certified": must be 0). */
+int dwh_debug_h_bound(int64_t Lx, int64_t Ly, double t, double tp, double mu, const int64_t* nn_table,
+                      const int64_t* nnn_table, int64_t nchains, const double* disorder, double* out);
+
 /* Self-test of the f64 MFMA fragment layout (A = I, asymmetric B); 0 = pass. */
 int dwh_selftest_mfma(int32_t device);
 
