@@ -22,7 +22,9 @@
 #include <cstring>
 #include <limits>
 #include <map>
+#include <set>
 #include <string>
+#include <tuple>
 #include <utility>
 #include <vector>
 
@@ -80,11 +82,11 @@ const PoleTable* pole_table(std::string* err) {
 
 enum TimerName {
   T_GJ_UPDATE = 0, T_GJ_PIVOT, T_ASSEMBLE, T_CONTRACT, T_STEP, T_GJ_EDGE, T_CR_GEMM, T_CR_INV, T_CR_INVSIDE,
-  T_CR_TAIL, T_COUNT
+  T_CR_TAIL, T_CR_FUSED, T_COUNT
 };
 const char* kTimerNames[T_COUNT] = {"gj_update", "gj_pivot", "assemble", "contract",
                                     "step",      "gj_edge",  "cr_gemm",  "cr_inv",
-                                    "cr_inv_side", "cr_tail"};
+                                    "cr_inv_side", "cr_tail", "cr_fused"};
 
 enum Algo { ALGO_DENSE = 0, ALGO_CR = 1, ALGO_EIG = 2 };
 
@@ -110,9 +112,21 @@ struct CrTailSeg {
   int grid;       // resident workgroups
 };
 
+// two consecutive stages run as one k_cr_fused launch (BP = 32, build_cr_fusion)
+struct CrFuse {
+  int first;            // stages first, first + 1
+  int mode;             // 1: an inversion stage + the product stage after it; 2: two product stages
+  int gfirst, ngrp;     // CrPlan::groups
+  int pfirst, nplain;   // plain tiles (first stage, no group) in CrPlan::ftiles
+  int r1, r2;           // tile rounds of the phases
+};
+
 struct CrPlan {
   int nblk = 0;
   std::vector<CrStage> stages;
+  std::vector<CrFuse> fuses;
+  std::vector<dwh::CrGroup> groups;
+  std::vector<dwh::CrTile> ftiles;
   std::vector<CrTailSeg> tails;
   std::vector<dwh::CrTailStage> tail_stages;
   std::vector<dwh::CrTask> tasks;
@@ -577,6 +591,137 @@ void build_cr_tails(CrPlan& pl, int nbatch, int cap) {
   }
 }
 
+// Launch fusion of the BP = 32 path (k_cr_fused, dwhmc_cr.hip): a pair of
+// consecutive stages (A, B) becomes one launch when B's work splits into
+// groups that each read A's outputs from one group only —
+//   mode 1: A an inversion stage (no side work), B the product stage after
+//   it, every B tile reading exactly one block A inverts (V1/V2/W1/W2 of the
+//   forward levels; the coarsest backward products of the final inversion);
+//   mode 2: A, B product stages, every A task read by at most one B task
+//   (backward: G_ae, G_ce, then G_ee of the same eliminated block).
+// A's tiles no group needs run as plain tiles of the launch.  A pair is left
+// unfused when any tile of one group (or a plain tile) would read a block
+// another group writes in the same launch, or when a phase needs more than
+// two rounds of tiles.  Pairs are taken greedily from the first stage.
+void build_cr_fusion(CrPlan& pl) {
+  constexpr int NW = 8;
+  auto reads = [](const dwh::CrTile& t, int b) {
+    if (t.cin == b) return true;
+    for (int h = 0; h < t.nt; ++h)
+      if (t.a[h] == b || t.b[h] == b) return true;
+    return false;
+  };
+  size_t si = 0;
+  while (si + 1 < pl.stages.size()) {
+    const CrStage& A = pl.stages[si];
+    const CrStage& B = pl.stages[si + 1];
+    const dwh::CrTile* at = pl.tiles16.data() + A.tfirst;
+    const dwh::CrTile* bt = pl.tiles16.data() + B.tfirst;
+    std::vector<std::vector<dwh::CrTile>> ph1, ph2;   // per group
+    std::vector<int> ginv;
+    std::vector<dwh::CrTile> plainv;
+    std::vector<int> bgroup(B.kind == 1 ? B.ntiles : 0, -1);   // group of each B tile
+    bool ok = B.kind == 1;
+    int mode = 0, T1 = 1, T2 = 1;
+    auto signed_tile = [](dwh::CrTile t, double sg) {
+      t.neg = sg < 0 ? 1 : 0;
+      return t;
+    };
+    if (ok && A.kind == 0 && A.ntiles == 0 && !A.l0) {
+      mode = 1;
+      T1 = NW;
+      T2 = NW / 4;
+      ph1.resize(A.n);
+      ph2.resize(A.n);
+      for (int k = 0; k < A.n; ++k) ginv.push_back(k);
+      for (int t = 0; t < B.ntiles && ok; ++t) {
+        int hit = 0;
+        for (int k = 0; k < A.n; ++k)
+          if (reads(bt[t], pl.inv_dst[A.first + k])) {
+            ++hit;
+            bgroup[t] = k;
+          }
+        ok = hit == 1;
+        if (ok) ph1[bgroup[t]].push_back(signed_tile(bt[t], B.sg));
+      }
+      // no B tile may write a block an inversion of the launch reads or writes
+      for (int t = 0; t < B.ntiles && ok; ++t)
+        for (int k = 0; k < A.n && ok; ++k)
+          ok = bt[t].out != pl.inv_blk[A.first + k] && bt[t].out != pl.inv_dst[A.first + k];
+    } else if (ok && A.kind == 1) {
+      mode = 2;
+      T1 = NW / 2;
+      T2 = NW / 4;
+      // B tasks = distinct B outputs; each A output is owned by at most one B task
+      std::map<int, int> bout_group, aout_owner;
+      for (int t = 0; t < B.ntiles; ++t)
+        if (!bout_group.count(bt[t].out)) bout_group[bt[t].out] = (int)bout_group.size();
+      ph1.resize(bout_group.size());
+      ph2.resize(bout_group.size());
+      ginv.assign(bout_group.size(), -1);
+      for (int t = 0; t < B.ntiles && ok; ++t) {
+        const int g = bout_group[bt[t].out];
+        bgroup[t] = g;
+        ph2[g].push_back(signed_tile(bt[t], B.sg));
+        for (int u = 0; u < A.ntiles && ok; ++u)
+          if (reads(bt[t], at[u].out)) {
+            auto it = aout_owner.find(at[u].out);
+            if (it == aout_owner.end()) aout_owner[at[u].out] = g;
+            else ok = it->second == g;
+          }
+      }
+      for (int u = 0; u < A.ntiles && ok; ++u) {
+        auto it = aout_owner.find(at[u].out);
+        if (it == aout_owner.end()) plainv.push_back(signed_tile(at[u], A.sg));
+        else ph1[it->second].push_back(signed_tile(at[u], A.sg));
+      }
+      // an A tile may read a block B writes only inside its own group (phase 1
+      // runs before phase 2 there); plain tiles not at all
+      for (int u = 0; u < A.ntiles && ok; ++u) {
+        auto it = aout_owner.find(at[u].out);
+        const int ga = it == aout_owner.end() ? -2 : it->second;
+        for (int t = 0; t < B.ntiles && ok; ++t)
+          if (reads(at[u], bt[t].out)) ok = ga == bgroup[t];
+      }
+    } else {
+      ok = false;
+    }
+    int m1 = 0, m2 = 0;
+    for (size_t g = 0; g < ph1.size(); ++g) {
+      m1 = std::max(m1, (int)ph1[g].size());
+      m2 = std::max(m2, (int)ph2[g].size());
+    }
+    const int r1 = (m1 + T1 - 1) / T1, r2 = (m2 + T2 - 1) / T2;
+    if (!ok || ph1.empty() || r1 > 2 || r2 > 2) {
+      ++si;
+      continue;
+    }
+    CrFuse f{};
+    f.first = (int)si;
+    f.mode = mode;
+    f.gfirst = (int)pl.groups.size();
+    f.ngrp = (int)ph1.size();
+    f.r1 = r1;
+    f.r2 = r2;
+    for (size_t g = 0; g < ph1.size(); ++g) {
+      dwh::CrGroup G{};
+      G.inv = ginv[g];
+      G.p1 = (int)pl.ftiles.size();
+      G.n1 = (int)ph1[g].size();
+      pl.ftiles.insert(pl.ftiles.end(), ph1[g].begin(), ph1[g].end());
+      G.p2 = (int)pl.ftiles.size();
+      G.n2 = (int)ph2[g].size();
+      pl.ftiles.insert(pl.ftiles.end(), ph2[g].begin(), ph2[g].end());
+      pl.groups.push_back(G);
+    }
+    f.pfirst = (int)pl.ftiles.size();
+    f.nplain = (int)plainv.size();
+    pl.ftiles.insert(pl.ftiles.end(), plainv.begin(), plainv.end());
+    pl.fuses.push_back(f);
+    si += 2;
+  }
+}
+
 struct TimingRec {
   int name;
   hipEvent_t a, b;
@@ -654,6 +799,8 @@ struct dwh_ctx {
   double2* bpool = nullptr;   // CR block pool (nbatch x nblk blocks)
   dwh::CrTask* d_tasks = nullptr;
   dwh::CrTile* d_tiles16 = nullptr;
+  dwh::CrGroup* d_groups = nullptr;   // fused launches (BP = 32)
+  dwh::CrTile* d_ftiles = nullptr;
   double* efpart = nullptr;     // per (chain, pole) E_f / Tr G22 partials
   unsigned* efdone = nullptr;   // per chain: pole blocks done (k_cr_fermion_energy)
   int *d_inv_blk = nullptr, *d_inv_dst = nullptr, *d_inv_slot = nullptr, *d_inv0_r = nullptr;
@@ -875,7 +1022,7 @@ void cr_enqueue(dwh_ctx* ctx) {
     ctx->pairing_in_pool = false;
   }
   const CrPlan& plan = ctx->plan;
-  size_t next_tail = 0;
+  size_t next_tail = 0, next_fuse = 0;
   // the site guard rides on the first (level-0) inversion launch: every
   // factorised Δ passes through it
   dwh::SiteGuard guard;
@@ -894,6 +1041,19 @@ void cr_enqueue(dwh_ctx* ctx) {
                           ctx->tail_base, ctx->d_tail_err, ctx->stream);
       ctx->tail_base += (unsigned long long)(tg.n - 1) * tg.grid;
       si += tg.n - 1;
+      continue;
+    }
+    if (next_fuse < plan.fuses.size() && plan.fuses[next_fuse].first == (int)si) {
+      const CrFuse& f = plan.fuses[next_fuse++];
+      const CrStage& A = plan.stages[si];
+      const CrStage& B = plan.stages[si + 1];
+      Scope s(ctx, T_CR_FUSED, (A.kind == 0 ? A.n * bp3 : A.flops * c.nbatch) + B.flops * c.nbatch);
+      const int o = f.mode == 1 ? A.first : 0;
+      dwh::launch_cr_fused(c, ctx->bpool, ctx->d_inv_blk + o, ctx->d_inv_dst + o, ctx->d_inv_slot + o, ctx->ldpart,
+                           ctx->d_groups + f.gfirst, f.ngrp, ctx->d_ftiles, ctx->d_ftiles + f.pfirst, f.nplain,
+                           f.mode, f.r1, f.r2, ctx->stream, f.mode == 1 ? guard : dwh::SiteGuard{});
+      if (f.mode == 1) guard = dwh::SiteGuard{};
+      ++si;
       continue;
     }
     const CrStage& st = plan.stages[si];
@@ -1530,6 +1690,9 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
         const int occ = dwh::cr_tail_occupancy();
         if (occ > 0) build_cr_tails(ctx->plan, d.nbatch, occ * ncu);
       }
+      // DWHMC_CR_FUSE=0: BP = 32 stages as separate launches (A/B runs)
+      const char* ef = std::getenv("DWHMC_CR_FUSE");
+      if (dwh::cr_supported_fuse(BP) && !(ef && *ef == '0')) build_cr_fusion(ctx->plan);
       if (const char* e = std::getenv("DWHMC_CR_PLAN_DUMP"); e && *e == '1') {
         int i = 0;
         for (const CrStage& st : ctx->plan.stages) {
@@ -1544,6 +1707,9 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
         for (const CrTailSeg& tg : ctx->plan.tails)
           std::fprintf(stderr, "cr tail: stages %d..%d in one launch, %d workgroups\n", tg.first, tg.first + tg.n - 1,
                        tg.grid);
+        for (const CrFuse& f : ctx->plan.fuses)
+          std::fprintf(stderr, "cr fused: stages %d,%d mode %d groups=%d plain=%d rounds=%d,%d\n", f.first,
+                       f.first + 1, f.mode, f.ngrp, f.nplain, f.r1, f.r2);
       }
     }
   }
@@ -1582,6 +1748,10 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     ALLOC(bpool, (size_t)d.nbatch * ctx->cr.item);
     ALLOC(d_tasks, pl.tasks.size());
     ALLOC(d_tiles16, pl.tiles16.size());
+    if (!pl.fuses.empty()) {
+      ALLOC(d_groups, pl.groups.size());
+      ALLOC(d_ftiles, pl.ftiles.size());
+    }
     ALLOC(efpart, 2 * (size_t)d.nbatch);
     ALLOC(efdone, (size_t)d.nc);
     ALLOC(d_inv_blk, pl.inv_blk.size());
@@ -1666,6 +1836,10 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     const CrPlan& pl = ctx->plan;
     UP(d_tasks, pl.tasks.data(), pl.tasks.size());
     UP(d_tiles16, pl.tiles16.data(), pl.tiles16.size());
+    if (!pl.fuses.empty()) {
+      UP(d_groups, pl.groups.data(), pl.groups.size());
+      UP(d_ftiles, pl.ftiles.data(), pl.ftiles.size());
+    }
     UP(d_inv_blk, pl.inv_blk.data(), pl.inv_blk.size());
     UP(d_inv_dst, pl.inv_dst.data(), pl.inv_dst.size());
     UP(d_inv_slot, pl.inv_slot.data(), pl.inv_slot.size());
@@ -2646,6 +2820,91 @@ extern "C" {
 // not), no block is read and written in one stage except a task's own
 // accumulate input, no two tasks of a stage write the same block, and every
 // block the force / E_f gather reads was written.
+// The fused launches of a BP = 32 plan (build_cr_fusion) against the two
+// stages each replaces: the tiles are exactly the stages' tiles (mode 1: the
+// second stage's), and groups running concurrently neither write the same
+// block nor read a block another group or a plain tile writes (inside a
+// group, phase 1 runs before phase 2: the order of the two stages).  Returns
+// an error message or nullptr.
+static const char* verify_cr_fusion(const CrPlan& plan, int BP) {
+  if (!dwh::cr_supported_fuse(BP)) return nullptr;
+  CrPlan pl = plan;
+  build_cr_fusion(pl);
+  static thread_local char buf[256];
+  auto tile_reads = [](const dwh::CrTile& t, std::vector<int>& r) {
+    if (t.cin >= 0) r.push_back(t.cin);
+    for (int h = 0; h < t.nt; ++h) {
+      r.push_back(t.a[h]);
+      r.push_back(t.b[h]);
+    }
+  };
+  for (const CrFuse& f : pl.fuses) {
+    const CrStage& A = pl.stages[f.first];
+    const CrStage& B = pl.stages[f.first + 1];
+    // coverage: (out, tr, tc) of the launch's tiles = the stages' tiles
+    std::multiset<std::tuple<int, int, int>> want, got;
+    auto key = [](const dwh::CrTile& t) { return std::make_tuple(t.out, t.tr, t.tc); };
+    if (A.kind == 1)
+      for (int t = 0; t < A.ntiles; ++t) want.insert(key(pl.tiles16[A.tfirst + t]));
+    for (int t = 0; t < B.ntiles; ++t) want.insert(key(pl.tiles16[B.tfirst + t]));
+    std::vector<std::vector<int>> R(f.ngrp + 1), W(f.ngrp + 1);   // last: plain tiles
+    for (int g = 0; g < f.ngrp; ++g) {
+      const dwh::CrGroup& G = pl.groups[f.gfirst + g];
+      if ((f.mode == 1) != (G.inv >= 0)) return "fused group without its inversion";
+      if (G.inv >= 0) {
+        R[g].push_back(pl.inv_blk[A.first + G.inv]);
+        W[g].push_back(pl.inv_dst[A.first + G.inv]);
+      }
+      for (int t = 0; t < G.n1 + G.n2; ++t) {
+        const dwh::CrTile& x = pl.ftiles[G.p1 + t];
+        got.insert(key(x));
+        tile_reads(x, R[g]);
+        W[g].push_back(x.out);
+      }
+    }
+    for (int t = 0; t < f.nplain; ++t) {
+      const dwh::CrTile& x = pl.ftiles[f.pfirst + t];
+      got.insert(key(x));
+      tile_reads(x, R[f.ngrp]);
+      W[f.ngrp].push_back(x.out);
+    }
+    if (want != got) {
+      std::snprintf(buf, sizeof buf, "fused stages %d,%d do not cover the stages' tiles", f.first, f.first + 1);
+      return buf;
+    }
+    for (int g = 0; g <= f.ngrp; ++g)
+      for (int h = 0; h <= f.ngrp; ++h) {
+        if (g == h && g < f.ngrp) continue;   // inside a group the phases are ordered
+        for (int w : W[h]) {
+          if (std::find(R[g].begin(), R[g].end(), w) != R[g].end() ||
+              (g != h && std::find(W[g].begin(), W[g].end(), w) != W[g].end())) {
+            std::snprintf(buf, sizeof buf, "fused stages %d,%d: block %d shared by concurrent groups", f.first,
+                          f.first + 1, w);
+            return buf;
+          }
+        }
+      }
+  }
+  return nullptr;
+}
+
+int dwh_debug_cr_fusion(int64_t Lx, int64_t Ly, int64_t nbatch, int64_t* out) {
+  if (Lx < 1 || Ly < 1 || nbatch < 1 || !out) return fail(nullptr, DWH_ERR_ARG, "bad lattice / batch / output");
+  const int BP = (int)(2 * ((Lx + 15) / 16 * 16));
+  if (!dwh::cr_supported_bp(BP)) return fail(nullptr, DWH_ERR_ARG, "lattice row too wide for the CR path");
+  std::vector<int> Dcol = nn_pairing_cols((int)Lx, (int)Ly);
+  CrPlan pl = build_cr_plan((int)Lx, (int)Ly, BP, Dcol, dwh::cr_supported_side(BP), (int)nbatch, 256,
+                            dwh::cr_supported_inv0(BP));
+  if (dwh::cr_supported_fuse(BP)) build_cr_fusion(pl);
+  int64_t m1 = 0, m2 = 0;
+  for (const CrFuse& f : pl.fuses) (f.mode == 1 ? m1 : m2)++;
+  out[0] = (int64_t)pl.stages.size();
+  out[1] = (int64_t)pl.stages.size() - (int64_t)pl.fuses.size();   // launches
+  out[2] = m1;
+  out[3] = m2;
+  return DWH_OK;
+}
+
 int dwh_debug_cr_plan_check(int64_t Lx, int64_t Ly, int64_t nbatch, int32_t side, int32_t inv0, int64_t* stats) {
   if (Lx < 1 || Ly < 1 || nbatch < 1) return fail(nullptr, DWH_ERR_ARG, "bad lattice / batch");
   std::vector<int> Dcol = nn_pairing_cols((int)Lx, (int)Ly);
@@ -2714,6 +2973,7 @@ int dwh_debug_cr_plan_check(int64_t Lx, int64_t Ly, int64_t nbatch, int32_t side
       if (w.first >= 0 && w.first < pl.nblk && written[w.first] == -1) written[w.first] = si;
     }
   }
+  if (const char* e = verify_cr_fusion(pl, BP)) return fail(nullptr, DWH_ERR_STATE, e);
   const int64_t BB = (int64_t)(BP / 2) * BP;
   for (int64_t o : pl.goff)
     if (o >= 0 && written[o / BB] == -1) return fail(nullptr, DWH_ERR_STATE, "force gather reads an unwritten block");

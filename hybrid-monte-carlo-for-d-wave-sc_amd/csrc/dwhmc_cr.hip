@@ -225,8 +225,10 @@ __device__ __forceinline__ void mma16_3m_T(d4& cr, d4& ci, const double2* A, con
 }
 
 // one workgroup (NT waves) inverts block blk[li] of batch item bi; pan / ldw:
-// the caller's LDS (double-buffered panel, per-wave ln|det| partials)
-template <int NT>
+// the caller's LDS (double-buffered panel, per-wave ln|det| partials).  NWG:
+// waves of the workgroup (k_cr_fused: NWG > NT, the extra waves only join the
+// barriers)
+template <int NT, int NWG = NT>
 __device__ __forceinline__ void cr_inv_wg(double2* __restrict__ pool, int64_t item, int bi, int li,
                                           const int* __restrict__ blk, const int* __restrict__ dst,
                                           const int* __restrict__ slot, double* __restrict__ ldpart,
@@ -235,6 +237,7 @@ __device__ __forceinline__ void cr_inv_wg(double2* __restrict__ pool, int64_t it
   const double2* M = pool + (int64_t)bi * item + (int64_t)blk[li] * HP * BP;
   double2* Mo = pool + (int64_t)bi * item + (int64_t)dst[li] * HP * BP;   // may equal M
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  const bool act = NWG == NT || w < NT;
   d4 ar[NT], ai[NT];
   CR_STAMP(0);
   // Tiles in the MFMA C layout (lane: rows lk + 4 rr, column lr), except the
@@ -250,6 +253,7 @@ __device__ __forceinline__ void cr_inv_wg(double2* __restrict__ pool, int64_t it
   for (int I = 0; I < NT; ++I)
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
+      if (!act) break;
       const bool diag = (I == w);
       const int row = I * 16 + (diag ? lr : lk + 4 * rr), col = w * 16 + (diag ? lk + 4 * rr : lr);
       double2 v;
@@ -307,7 +311,7 @@ __device__ __forceinline__ void cr_inv_wg(double2* __restrict__ pool, int64_t it
         br[rr] = v.x;
         bim[rr] = v.y;
       }
-    } else {
+    } else if (act) {
       d4 tr = ar[0], ti = ai[0];   // this wave's tile kb (off-diagonal: C layout)
 #pragma unroll
       for (int I = 1; I < NT; ++I)
@@ -359,7 +363,7 @@ __device__ __forceinline__ void cr_inv_wg(double2* __restrict__ pool, int64_t it
 #pragma unroll
           for (int rr = 0; rr < 4; ++rr) Q[I][lr * 17 + lk + 4 * rr] = make_double2(ar[I][rr], ai[I][rr]);
         }
-    } else {
+    } else if (act) {
       if (has_next) {   // the lookahead column's tile w: Q[w] -= A_wk X_{kb+1}
         d4 yr, yi, cr, ci;
 #pragma unroll
@@ -390,8 +394,8 @@ __device__ __forceinline__ void cr_inv_wg(double2* __restrict__ pool, int64_t it
   for (int I = 0; I < NT / 2; ++I)
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr)
-      Mo[(int64_t)(I * 16 + lk + 4 * rr) * BP + w * 16 + lr] = make_double2(ar[I][rr], ai[I][rr]);
-  if (l == 0) ldw[w] = ld;
+      if (act) Mo[(int64_t)(I * 16 + lk + 4 * rr) * BP + w * 16 + lr] = make_double2(ar[I][rr], ai[I][rr]);
+  if (l == 0 && act) ldw[w] = ld;
   __syncthreads();
   if (threadIdx.x == 0) {
     double t = 0.0;
@@ -1080,6 +1084,157 @@ __global__ __launch_bounds__(64 * NT) void k_cr_inv_side(double2* __restrict__ p
   }
   cr_gemm_wg<16 * NT, 2, 1, 0, true>(pool, item, stasks, nst, maxt, nullptr, 0, total, 1.0,
                                     xcd_remap(b - nall, nside));
+}
+
+// ---------------------------------------------------------------------------
+// Fused launches of the BP = 32 path (host: build_cr_fusion).  At L = 16 every
+// CR stage is a few dozen workgroups of 32 x 32 blocks: each launch costs its
+// ~4 us of launch + memory round trip + drain whatever it computes.  A fused
+// launch runs two consecutive stages: one workgroup per GROUP computes
+// [its block inversion (mode 1), then] its phase-1 tiles, then its phase-2
+// tiles, where a later phase reads only what the same workgroup wrote (the
+// planner checks it): the backward G_ae / G_ce then G_ee of one eliminated
+// block (mode 2), or an inversion then the V1 / V2 / W1 / W2 products of the
+// inverted block (mode 1).  Tiles of the first stage that no group needs run
+// as plain workgroups of the same launch.  Phases are separated by
+// __syncthreads(), whose workgroup-scope release / acquire makes the global
+// stores of one wave visible to the other waves of the workgroup (one CU,
+// one vector L1; no tgsplit).  A 32 x 32 block product is 96 MFMAs, so a
+// workgroup's serial phases cost less than the launch they remove (at BP = 64
+// they are 8x that: profiles/r02_exp_cr_fused_v_products.txt).
+// ---------------------------------------------------------------------------
+// One round of up to NW / KS tiles of a list: KS waves per tile split its K
+// range (cr_tile_part), partials summed through LDS (red: NW x 4 x 64).  Every
+// wave of the workgroup calls it the same number of times (barriers inside).
+// Sign and accumulate input per tile (CrTile::neg, cin).
+template <int BP, int NW, int KS>
+__device__ __forceinline__ void cr_tiles_wg(double2* __restrict__ base, const CrTile* __restrict__ tl, int nt,
+                                            double2 (*red)[4][64]) {
+  constexpr int64_t BB = (int64_t)(BP / 2) * BP;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  const int ti = w / KS, kq = w % KS;
+  const bool valid = ti < nt;
+  const CrTile* tp = tl + (valid ? ti : 0);
+  d4 t1[1][1], t2[1][1], t3[1][1];
+  t1[0][0] = d4{0.0, 0.0, 0.0, 0.0};
+  t2[0][0] = d4{0.0, 0.0, 0.0, 0.0};
+  t3[0][0] = d4{0.0, 0.0, 0.0, 0.0};
+  int tr = 0, tc = 0;
+  if (valid) {
+    tr = tp->tr;
+    tc = tp->tc;
+    auto run = [&](auto kqc) {
+      constexpr int KQ = decltype(kqc)::value;
+      cr_tile_part<BP, 1, KS, KQ>(base, tp, tr, tc, t1, t2, t3);
+    };
+    if (kq == 0) run(std::integral_constant<int, 0>{});
+    if constexpr (KS >= 2) {
+      if (kq == 1) run(std::integral_constant<int, 1>{});
+    }
+    if constexpr (KS >= 4) {
+      if (kq == 2) run(std::integral_constant<int, 2>{});
+      if (kq == 3) run(std::integral_constant<int, 3>{});
+    }
+  }
+  const double sg = (valid && tp->neg) ? -1.0 : 1.0;
+  auto partial = [&](int rr) {
+    const double a = t1[0][0][rr], b = t2[0][0][rr], c = t3[0][0][rr];
+    return make_double2(sg * (a - b), sg * (c - a - b));
+  };
+  auto put = [&](int rr, double2 x) {
+    const int64_t o = (int64_t)(tr * 16 + lk + 4 * rr) * BP + tc * 16 + lr;
+    const int cin = tp->cin;
+    if (cin >= 0) {
+      const double2 c = base[cin * BB + o];
+      x.x += c.x;
+      x.y += c.y;
+    }
+    base[tp->out * BB + o] = x;
+  };
+  if constexpr (KS == 1) {
+    if (valid) {
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) put(rr, partial(rr));
+    }
+  } else {
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) red[w][rr][l] = partial(rr);
+    __syncthreads();
+    if (valid) {
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        if (rr % KS != kq) continue;
+        double2 x = red[w - kq][rr][l];
+#pragma unroll
+        for (int k = 1; k < KS; ++k) {
+          const double2 y = red[w - kq + k][rr][l];
+          x.x += y.x;
+          x.y += y.y;
+        }
+        put(rr, x);
+      }
+    }
+    __syncthreads();   // red is rewritten by the next round
+  }
+}
+
+// grid (ngrp + plain workgroups [+ 1 guard column], nbatch); NW waves per
+// workgroup; KS1 / KS2: K split of phase-1 / phase-2 (and plain) tiles
+template <int BP, int NT, int NW, int KS1, int KS2>
+__global__ __launch_bounds__(64 * NW) void k_cr_fused(double2* __restrict__ pool, int64_t item,
+                                                      const int* __restrict__ blk, const int* __restrict__ dst,
+                                                      const int* __restrict__ slot, double* __restrict__ ldpart,
+                                                      int nslots, const CrGroup* __restrict__ grp, int ngrp,
+                                                      const CrTile* __restrict__ ftl,
+                                                      const CrTile* __restrict__ plain, int nplain, int r1,
+                                                      int r2, SiteGuard sg, int N, int P) {
+  static_assert(BP == 16 * NT && NW >= NT && NW % KS1 == 0 && NW % KS2 == 0, "fused launch shape");
+  __shared__ double2 red[NW][4][64];
+  __shared__ double2 pan[2][NT][16 * 17];
+  __shared__ double ldw[NT];
+  if (sg.Delta != nullptr && blockIdx.x == gridDim.x - 1) {   // the guard column, pole 0 of each chain
+    if (blockIdx.y % P == 0) site_guard_wg(sg, N, blockIdx.y / P);
+    return;
+  }
+  const int bi = blockIdx.y, j = blockIdx.x;
+  double2* base = pool + (int64_t)bi * item;
+  constexpr int T1 = NW / KS1, T2 = NW / KS2;   // tiles per round
+  if (j < ngrp) {
+    const CrGroup G = grp[j];
+    if (G.inv >= 0) {
+      cr_inv_wg<NT, NW>(pool, item, bi, G.inv, blk, dst, slot, ldpart, nslots, pan, ldw);
+      __syncthreads();   // the inverse (global) is read by the phase-1 tiles
+    }
+    for (int r = 0; r < r1; ++r) cr_tiles_wg<BP, NW, KS1>(base, ftl + G.p1 + r * T1, G.n1 - r * T1, red);
+    if (r2 > 0) {
+      __syncthreads();   // phase-1 outputs (global) are phase-2 operands
+      for (int r = 0; r < r2; ++r) cr_tiles_wg<BP, NW, KS2>(base, ftl + G.p2 + r * T2, G.n2 - r * T2, red);
+    }
+  } else {
+    const int p0 = (j - ngrp) * T2;
+    cr_tiles_wg<BP, NW, KS2>(base, plain + p0, nplain - p0, red);
+  }
+}
+
+bool cr_supported_fuse(int BP) { return BP == 32; }
+
+void launch_cr_fused(const CrDims& c, double2* pool, const int* blk, const int* dst, const int* slot,
+                     double* ldpart, const CrGroup* grp, int ngrp, const CrTile* ftl, const CrTile* plain,
+                     int nplain, int mode, int r1, int r2, hipStream_t s, const SiteGuard& sg) {
+  constexpr int NW = 8;
+  if (c.BP != 32 || ngrp + nplain <= 0) return;
+  const bool guard = sg.Delta != nullptr;
+  if (mode == 1) {   // inversion + products: one tile per wave
+    const int nplain_wg = (nplain + NW / 4 - 1) / (NW / 4);
+    const dim3 g(ngrp + nplain_wg + (guard ? 1 : 0), c.nbatch);
+    hipLaunchKernelGGL((k_cr_fused<32, 2, NW, 1, 4>), g, dim3(64 * NW), 0, s, pool, c.item, blk, dst, slot, ldpart,
+                       c.Ly, grp, ngrp, ftl, plain, nplain, r1, r2, sg, c.N, c.P);
+  } else {           // two product phases: 2 waves per phase-1 tile, 4 per phase-2 tile
+    const int nplain_wg = (nplain + NW / 4 - 1) / (NW / 4);
+    const dim3 g(ngrp + nplain_wg + (guard ? 1 : 0), c.nbatch);
+    hipLaunchKernelGGL((k_cr_fused<32, 2, NW, 2, 4>), g, dim3(64 * NW), 0, s, pool, c.item, blk, dst, slot, ldpart,
+                       c.Ly, grp, ngrp, ftl, plain, nplain, r1, r2, sg, c.N, c.P);
+  }
 }
 
 // ---------------------------------------------------------------------------

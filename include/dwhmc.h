@@ -270,6 +270,13 @@ int dwh_debug_level0(dwh_ctx* ctx, int64_t chain, int64_t pole, int32_t refill, 
  * violation in dwh_last_error(NULL). */
 int dwh_debug_cr_plan_check(int64_t Lx, int64_t Ly, int64_t nbatch, int32_t side, int32_t inv0, int64_t* stats);
 
+/* Launch fusion of the same plan (BP = 32 lattices, host only): out[0]
+ * stages, out[1] launches after fusion, out[2] inversion + product launches
+ * (mode 1), out[3] product pair launches (mode 2).  dwh_debug_cr_plan_check
+ * also verifies the fused launches (tile coverage, no block shared by
+ * concurrent workgroup groups). */
+int dwh_debug_cr_fusion(int64_t Lx, int64_t Ly, int64_t nbatch, int64_t* out);
+
 /* Algorithmic fp64 flops per batch item of the same plan (host only), as the
  * "cr_*" timers count them: flops[0] block inversions (8 BP^3 each), flops[1]
  * block products of the product stages, flops[2] block products run as side
