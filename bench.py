@@ -346,7 +346,7 @@ def main(argv=None):
         # per-launch averages.
         replay = schedule(w_sw, min(a.steps, 2 * Nt), Nt)
         replay_steps = sum(n * nt for _, n, nt in replay)
-        names = [dom, "assemble"] + (["cr_inv", "cr_inv_side", "cr_tail"] if cr else [])
+        names = [dom, "assemble"] + (["cr_inv", "cr_inv_side", "cr_tail", "cr_fused"] if cr else [])
         ctx.timing_enable(names)
         ctx.timing_reset()
         for f, n, nt in replay:
@@ -409,11 +409,14 @@ def main(argv=None):
                 msi, ni, wi = kern["cr_inv"]
                 mss, ns, ws = kern["cr_inv_side"]
                 mst, nt_, wt = kern["cr_tail"]
+                msf, nf, wf = kern["cr_fused"]
                 # the CR path's own algorithmic flops per leapfrog step (block
-                # products, incl. the side work of the inversion stages and the
-                # coarse tail, and block inversions at 8 BP^3 each) x the timed steps
-                rec["alg_tflops"] = (w + wi + ws + wt) / replay_steps * a.steps * world / el / 1e12
-                rec["alg_flops_per_step"] = (w + wi + ws + wt) / replay_steps / a.chains
+                # products, incl. the side work of the inversion stages, the
+                # coarse tail and the fused BP = 32 launches, and block
+                # inversions at 8 BP^3 each) x the timed steps
+                wall = w + wi + ws + wt + wf
+                rec["alg_tflops"] = wall / replay_steps * a.steps * world / el / 1e12
+                rec["alg_flops_per_step"] = wall / replay_steps / a.chains
                 # the whole leapfrog step against the fp64 MFMA peak (north_star: >= 0.30 at L=32)
                 rec["alg_frac_of_peak"] = rec["alg_tflops"] / world / PEAK_F64_TFLOPS
                 nt = info["block"] // 16
@@ -434,6 +437,14 @@ def main(argv=None):
                                           "avg_launch_us": 1000.0 * mss / ns,
                                           "flops_per_launch": ws / ns,
                                           "ms_per_step": mss / replay_steps}
+                if nf:
+                    rec["cr_fused"] = {"bound": "latency", "kernel": f"k_cr_fused<{info['block']},...>",
+                                       "what": "two consecutive CR stages per launch (BP = 32): an inversion "
+                                               "with its V/W products, or a backward G_ae/G_ce -> G_ee pair",
+                                       "launches_per_step": nf / replay_steps,
+                                       "avg_launch_us": 1000.0 * msf / nf,
+                                       "flops_per_launch": wf / nf,
+                                       "ms_per_step": msf / replay_steps}
                 if nt_:
                     rec["cr_tail"] = {"bound": "latency", "kernel": "k_cr_tail<4>",
                                       "what": "the coarse CR levels' stages in one launch with device-wide "

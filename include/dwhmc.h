@@ -173,7 +173,7 @@ int dwh_stream(dwh_ctx* ctx, void** stream);
  * (bench/profiling).  enable is a bitmask over the timer names below
  * (bit 0 "gj_update", bit 1 "gj_pivot", bit 2 "assemble", bit 3 "contract",
  * bit 4 "step", bit 5 "gj_edge", bit 6 "cr_gemm", bit 7 "cr_inv", bit 8 "cr_inv_side",
- * bit 9 "cr_tail");
+ * bit 9 "cr_tail", bit 10 "cr_fused");
  * 0 disables, -1 times everything. */
 int dwh_timing_enable(dwh_ctx* ctx, int32_t enable);
 /* name: "gj_update" (rank-128 paired / rank-64 trailing updates),
@@ -181,7 +181,9 @@ int dwh_timing_enable(dwh_ctx* ctx, int32_t enable);
  * "cr_gemm" (cyclic-reduction block products), "cr_inv" (its block
  * inversions), "cr_inv_side" (inversion stages that also run the products off
  * the critical path; work = inversion + side-product flops), "cr_tail" (the
- * coarse levels' stages in one launch; work = their inversion + product flops), "assemble",
+ * coarse levels' stages in one launch; work = their inversion + product flops), "cr_fused"
+ * (BP = 32 launches that run two consecutive stages; work = both stages'
+ * flops), "assemble",
  * "contract", "step"; returns total milliseconds, launches and the
  * algorithmic work summed over launches (fp64 flops; HBM bytes for
  * "assemble"). */
