@@ -114,11 +114,11 @@ struct CrTailSeg {
 
 // two consecutive stages run as one k_cr_fused launch (BP = 32, build_cr_fusion)
 struct CrFuse {
-  int first;            // stages first, first + 1
-  int mode;             // 1: an inversion stage + the product stage after it; 2: two product stages
+  int first, nst;       // stages [first, first + nst)
+  int mode;             // 1: inversion + products; 2: two product stages; 3: products + inversion + products
   int gfirst, ngrp;     // CrPlan::groups
   int pfirst, nplain;   // plain tiles (first stage, no group) in CrPlan::ftiles
-  int r1, r2;           // tile rounds of the phases
+  int r0, r1, r2;       // tile rounds of the phases
 };
 
 struct CrPlan {
@@ -591,134 +591,223 @@ void build_cr_tails(CrPlan& pl, int nbatch, int cap) {
   }
 }
 
-// Launch fusion of the BP = 32 path (k_cr_fused, dwhmc_cr.hip): a pair of
-// consecutive stages (A, B) becomes one launch when B's work splits into
-// groups that each read A's outputs from one group only —
-//   mode 1: A an inversion stage (no side work), B the product stage after
-//   it, every B tile reading exactly one block A inverts (V1/V2/W1/W2 of the
-//   forward levels; the coarsest backward products of the final inversion);
-//   mode 2: A, B product stages, every A task read by at most one B task
-//   (backward: G_ae, G_ce, then G_ee of the same eliminated block).
-// A's tiles no group needs run as plain tiles of the launch.  A pair is left
-// unfused when any tile of one group (or a plain tile) would read a block
-// another group writes in the same launch, or when a phase needs more than
-// two rounds of tiles.  Pairs are taken greedily from the first stage.
-void build_cr_fusion(CrPlan& pl) {
-  constexpr int NW = 8;
-  auto reads = [](const dwh::CrTile& t, int b) {
-    if (t.cin == b) return true;
-    for (int h = 0; h < t.nt; ++h)
-      if (t.a[h] == b || t.b[h] == b) return true;
-    return false;
-  };
-  size_t si = 0;
-  while (si + 1 < pl.stages.size()) {
-    const CrStage& A = pl.stages[si];
-    const CrStage& B = pl.stages[si + 1];
-    const dwh::CrTile* at = pl.tiles16.data() + A.tfirst;
-    const dwh::CrTile* bt = pl.tiles16.data() + B.tfirst;
-    std::vector<std::vector<dwh::CrTile>> ph1, ph2;   // per group
-    std::vector<int> ginv;
-    std::vector<dwh::CrTile> plainv;
-    std::vector<int> bgroup(B.kind == 1 ? B.ntiles : 0, -1);   // group of each B tile
-    bool ok = B.kind == 1;
-    int mode = 0, T1 = 1, T2 = 1;
-    auto signed_tile = [](dwh::CrTile t, double sg) {
-      t.neg = sg < 0 ? 1 : 0;
-      return t;
+// Launch fusion of the BP = 32 path (k_cr_fused, dwhmc_cr.hip): consecutive
+// stages become one launch when their work splits into groups, one
+// workgroup each, that read the blocks the launch writes only inside their
+// own group —
+//   mode 1: an inversion stage I (no side work) + the product stage V after
+//     it, every V tile reading exactly one block I inverts (the forward
+//     V1/V2/W1/W2; the coarsest backward products of the final inversion);
+//   mode 3: a product stage D + I + V: group k also computes, before its
+//     inversion, the Schur complement I inverts and the U'/L' blocks its V
+//     tiles read (one launch per forward level);
+//   mode 2: two product stages A, B, every A task read by at most one B task
+//     (backward: G_ae, G_ce, then G_ee of the same eliminated block).
+// The first stage's tiles no group claims run as plain tiles of the launch.
+// A candidate is dropped when two concurrent groups (or a group and a plain
+// tile) would share a written block, or a phase needs more than two rounds
+// of tiles.  Candidates are taken greedily from the first stage, the
+// three-stage form first.
+struct FuseTry {
+  int mode = 0, nst = 0;
+  std::vector<std::vector<dwh::CrTile>> ph0, ph1, ph2;   // per group
+  std::vector<int> ginv;
+  std::vector<dwh::CrTile> plainv;
+  int r0 = 0, r1 = 0, r2 = 0;
+};
+
+bool tile_reads(const dwh::CrTile& t, int b) {
+  if (t.cin == b) return true;
+  for (int h = 0; h < t.nt; ++h)
+    if (t.a[h] == b || t.b[h] == b) return true;
+  return false;
+}
+
+void tile_blocks(const dwh::CrTile& t, std::vector<int>& r) {
+  if (t.cin >= 0) r.push_back(t.cin);
+  for (int h = 0; h < t.nt; ++h) {
+    r.push_back(t.a[h]);
+    r.push_back(t.b[h]);
+  }
+}
+
+// concurrent groups / plain tiles of a fused launch: no block written by one
+// is read or written by another (inversion entries: inv_blk read, inv_dst
+// written); nullptr if fine
+const char* fuse_conflict(const CrPlan& pl, int inv_first, const FuseTry& f) {
+  const int ng = (int)f.ph1.size();
+  std::vector<std::vector<int>> R(ng + 1), W(ng + 1);
+  for (int g = 0; g <= ng; ++g) {
+    auto add = [&](const std::vector<dwh::CrTile>& v) {
+      for (const dwh::CrTile& t : v) {
+        tile_blocks(t, R[g]);
+        W[g].push_back(t.out);
+      }
     };
-    if (ok && A.kind == 0 && A.ntiles == 0 && !A.l0) {
-      mode = 1;
-      T1 = NW;
-      T2 = NW / 4;
-      ph1.resize(A.n);
-      ph2.resize(A.n);
-      for (int k = 0; k < A.n; ++k) ginv.push_back(k);
-      for (int t = 0; t < B.ntiles && ok; ++t) {
-        int hit = 0;
-        for (int k = 0; k < A.n; ++k)
-          if (reads(bt[t], pl.inv_dst[A.first + k])) {
-            ++hit;
-            bgroup[t] = k;
-          }
-        ok = hit == 1;
-        if (ok) ph1[bgroup[t]].push_back(signed_tile(bt[t], B.sg));
-      }
-      // no B tile may write a block an inversion of the launch reads or writes
-      for (int t = 0; t < B.ntiles && ok; ++t)
-        for (int k = 0; k < A.n && ok; ++k)
-          ok = bt[t].out != pl.inv_blk[A.first + k] && bt[t].out != pl.inv_dst[A.first + k];
-    } else if (ok && A.kind == 1) {
-      mode = 2;
-      T1 = NW / 2;
-      T2 = NW / 4;
-      // B tasks = distinct B outputs; each A output is owned by at most one B task
-      std::map<int, int> bout_group, aout_owner;
-      for (int t = 0; t < B.ntiles; ++t)
-        if (!bout_group.count(bt[t].out)) bout_group[bt[t].out] = (int)bout_group.size();
-      ph1.resize(bout_group.size());
-      ph2.resize(bout_group.size());
-      ginv.assign(bout_group.size(), -1);
-      for (int t = 0; t < B.ntiles && ok; ++t) {
-        const int g = bout_group[bt[t].out];
-        bgroup[t] = g;
-        ph2[g].push_back(signed_tile(bt[t], B.sg));
-        for (int u = 0; u < A.ntiles && ok; ++u)
-          if (reads(bt[t], at[u].out)) {
-            auto it = aout_owner.find(at[u].out);
-            if (it == aout_owner.end()) aout_owner[at[u].out] = g;
-            else ok = it->second == g;
-          }
-      }
-      for (int u = 0; u < A.ntiles && ok; ++u) {
-        auto it = aout_owner.find(at[u].out);
-        if (it == aout_owner.end()) plainv.push_back(signed_tile(at[u], A.sg));
-        else ph1[it->second].push_back(signed_tile(at[u], A.sg));
-      }
-      // an A tile may read a block B writes only inside its own group (phase 1
-      // runs before phase 2 there); plain tiles not at all
-      for (int u = 0; u < A.ntiles && ok; ++u) {
-        auto it = aout_owner.find(at[u].out);
-        const int ga = it == aout_owner.end() ? -2 : it->second;
-        for (int t = 0; t < B.ntiles && ok; ++t)
-          if (reads(at[u], bt[t].out)) ok = ga == bgroup[t];
+    if (g < ng) {
+      add(f.ph0[g]);
+      add(f.ph1[g]);
+      add(f.ph2[g]);
+      if (f.ginv[g] >= 0) {
+        R[g].push_back(pl.inv_blk[inv_first + f.ginv[g]]);
+        W[g].push_back(pl.inv_dst[inv_first + f.ginv[g]]);
       }
     } else {
-      ok = false;
+      add(f.plainv);
     }
-    int m1 = 0, m2 = 0;
-    for (size_t g = 0; g < ph1.size(); ++g) {
-      m1 = std::max(m1, (int)ph1[g].size());
-      m2 = std::max(m2, (int)ph2[g].size());
+  }
+  for (int g = 0; g <= ng; ++g)
+    for (int h = 0; h <= ng; ++h) {
+      if (g == h) continue;
+      for (int w : W[h])
+        if (std::find(R[g].begin(), R[g].end(), w) != R[g].end() ||
+            std::find(W[g].begin(), W[g].end(), w) != W[g].end())
+          return "block shared by concurrent groups";
     }
-    const int r1 = (m1 + T1 - 1) / T1, r2 = (m2 + T2 - 1) / T2;
-    if (!ok || ph1.empty() || r1 > 2 || r2 > 2) {
+  return nullptr;
+}
+
+bool try_fuse(const CrPlan& pl, size_t si, int mode, FuseTry& f) {
+  constexpr int NW = 8;
+  const size_t nst = mode == 3 ? 3 : 2;
+  if (si + nst > pl.stages.size()) return false;
+  f = FuseTry{};
+  f.mode = mode;
+  f.nst = (int)nst;
+  auto tiles = [&](const CrStage& st) { return pl.tiles16.data() + st.tfirst; };
+  auto signed_tile = [](dwh::CrTile t, double sg) {
+    t.neg = sg < 0 ? 1 : 0;
+    return t;
+  };
+  int T0 = NW, T1 = NW, T2 = NW / 4;
+  if (mode == 1 || mode == 3) {
+    const CrStage& I = pl.stages[si + (mode == 3)];
+    const CrStage& V = pl.stages[si + (mode == 3) + 1];
+    if (I.kind != 0 || I.ntiles > 0 || I.l0 || V.kind != 1) return false;
+    const dwh::CrTile* vt = tiles(V);
+    f.ph0.resize(I.n);
+    f.ph1.resize(I.n);
+    f.ph2.resize(I.n);
+    for (int k = 0; k < I.n; ++k) f.ginv.push_back(k);
+    for (int t = 0; t < V.ntiles; ++t) {
+      int hit = 0, g = -1;
+      for (int k = 0; k < I.n; ++k)
+        if (tile_reads(vt[t], pl.inv_dst[I.first + k])) {
+          ++hit;
+          g = k;
+        }
+      if (hit != 1) return false;
+      f.ph1[g].push_back(signed_tile(vt[t], V.sg));
+    }
+    if (mode == 3) {
+      const CrStage& D = pl.stages[si];
+      if (D.kind != 1) return false;
+      const dwh::CrTile* dt = tiles(D);
+      std::map<int, int> owner;   // D output block -> group
+      auto claim = [&](int blk, int g) {
+        auto it = owner.find(blk);
+        if (it == owner.end()) owner[blk] = g;
+        return it == owner.end() || it->second == g;
+      };
+      bool any = false;
+      for (int t = 0; t < D.ntiles; ++t)
+        for (int k = 0; k < I.n; ++k) {
+          bool need = dt[t].out == pl.inv_blk[I.first + k];
+          for (const dwh::CrTile& x : f.ph1[k]) need = need || tile_reads(x, dt[t].out);
+          if (need) {
+            if (!claim(dt[t].out, k)) return false;
+            any = true;
+          }
+        }
+      if (!any) return false;
+      for (int t = 0; t < D.ntiles; ++t) {
+        auto it = owner.find(dt[t].out);
+        if (it == owner.end()) f.plainv.push_back(signed_tile(dt[t], D.sg));
+        else f.ph0[it->second].push_back(signed_tile(dt[t], D.sg));
+      }
+    }
+  } else {
+    const CrStage& A = pl.stages[si];
+    const CrStage& B = pl.stages[si + 1];
+    if (A.kind != 1 || B.kind != 1) return false;
+    T1 = NW / 2;
+    const dwh::CrTile* at = tiles(A);
+    const dwh::CrTile* bt = tiles(B);
+    std::map<int, int> bout_group, aout_owner;
+    for (int t = 0; t < B.ntiles; ++t)
+      if (!bout_group.count(bt[t].out)) bout_group[bt[t].out] = (int)bout_group.size();
+    const size_t ng = bout_group.size();
+    f.ph0.resize(ng);
+    f.ph1.resize(ng);
+    f.ph2.resize(ng);
+    f.ginv.assign(ng, -1);
+    for (int t = 0; t < B.ntiles; ++t) {
+      const int g = bout_group[bt[t].out];
+      f.ph2[g].push_back(signed_tile(bt[t], B.sg));
+      for (int u = 0; u < A.ntiles; ++u)
+        if (tile_reads(bt[t], at[u].out)) {
+          auto it = aout_owner.find(at[u].out);
+          if (it == aout_owner.end()) aout_owner[at[u].out] = g;
+          else if (it->second != g) return false;
+        }
+    }
+    for (int u = 0; u < A.ntiles; ++u) {
+      auto it = aout_owner.find(at[u].out);
+      if (it == aout_owner.end()) f.plainv.push_back(signed_tile(at[u], A.sg));
+      else f.ph1[it->second].push_back(signed_tile(at[u], A.sg));
+    }
+  }
+  if (f.ph1.empty()) return false;
+  int m0 = 0, m1 = 0, m2 = 0;
+  for (size_t g = 0; g < f.ph1.size(); ++g) {
+    m0 = std::max(m0, (int)f.ph0[g].size());
+    m1 = std::max(m1, (int)f.ph1[g].size());
+    m2 = std::max(m2, (int)f.ph2[g].size());
+  }
+  f.r0 = (m0 + T0 - 1) / T0;
+  f.r1 = (m1 + T1 - 1) / T1;
+  f.r2 = (m2 + T2 - 1) / T2;
+  if (f.r0 > 2 || f.r1 > 2 || f.r2 > 2) return false;
+  const int inv_first = mode == 2 ? 0 : pl.stages[si + (mode == 3)].first;
+  return fuse_conflict(pl, inv_first, f) == nullptr;
+}
+
+void build_cr_fusion(CrPlan& pl) {
+  size_t si = 0;
+  while (si < pl.stages.size()) {
+    FuseTry f;
+    if (!try_fuse(pl, si, 3, f) && !try_fuse(pl, si, 1, f) && !try_fuse(pl, si, 2, f)) {
       ++si;
       continue;
     }
-    CrFuse f{};
-    f.first = (int)si;
-    f.mode = mode;
-    f.gfirst = (int)pl.groups.size();
-    f.ngrp = (int)ph1.size();
-    f.r1 = r1;
-    f.r2 = r2;
-    for (size_t g = 0; g < ph1.size(); ++g) {
+    CrFuse cf{};
+    cf.first = (int)si;
+    cf.nst = f.nst;
+    cf.mode = f.mode;
+    cf.gfirst = (int)pl.groups.size();
+    cf.ngrp = (int)f.ph1.size();
+    cf.r0 = f.r0;
+    cf.r1 = f.r1;
+    cf.r2 = f.r2;
+    for (size_t g = 0; g < f.ph1.size(); ++g) {
       dwh::CrGroup G{};
-      G.inv = ginv[g];
+      G.inv = f.ginv[g];
+      G.p0 = (int)pl.ftiles.size();
+      G.n0 = (int)f.ph0[g].size();
+      pl.ftiles.insert(pl.ftiles.end(), f.ph0[g].begin(), f.ph0[g].end());
       G.p1 = (int)pl.ftiles.size();
-      G.n1 = (int)ph1[g].size();
-      pl.ftiles.insert(pl.ftiles.end(), ph1[g].begin(), ph1[g].end());
+      G.n1 = (int)f.ph1[g].size();
+      pl.ftiles.insert(pl.ftiles.end(), f.ph1[g].begin(), f.ph1[g].end());
       G.p2 = (int)pl.ftiles.size();
-      G.n2 = (int)ph2[g].size();
-      pl.ftiles.insert(pl.ftiles.end(), ph2[g].begin(), ph2[g].end());
+      G.n2 = (int)f.ph2[g].size();
+      pl.ftiles.insert(pl.ftiles.end(), f.ph2[g].begin(), f.ph2[g].end());
       pl.groups.push_back(G);
     }
-    f.pfirst = (int)pl.ftiles.size();
-    f.nplain = (int)plainv.size();
-    pl.ftiles.insert(pl.ftiles.end(), plainv.begin(), plainv.end());
-    pl.fuses.push_back(f);
-    si += 2;
+    cf.pfirst = (int)pl.ftiles.size();
+    cf.nplain = (int)f.plainv.size();
+    pl.ftiles.insert(pl.ftiles.end(), f.plainv.begin(), f.plainv.end());
+    pl.fuses.push_back(cf);
+    si += f.nst;
   }
 }
 
@@ -1045,15 +1134,20 @@ void cr_enqueue(dwh_ctx* ctx) {
     }
     if (next_fuse < plan.fuses.size() && plan.fuses[next_fuse].first == (int)si) {
       const CrFuse& f = plan.fuses[next_fuse++];
-      const CrStage& A = plan.stages[si];
-      const CrStage& B = plan.stages[si + 1];
-      Scope s(ctx, T_CR_FUSED, (A.kind == 0 ? A.n * bp3 : A.flops * c.nbatch) + B.flops * c.nbatch);
-      const int o = f.mode == 1 ? A.first : 0;
+      double work = 0;
+      int o = 0;
+      for (int k = 0; k < f.nst; ++k) {
+        const CrStage& st = plan.stages[si + k];
+        work += st.kind == 0 ? st.n * bp3 : st.flops * c.nbatch;
+        if (st.kind == 0) o = st.first;
+      }
+      Scope s(ctx, T_CR_FUSED, work);
+      const bool inv = f.mode != 2;
       dwh::launch_cr_fused(c, ctx->bpool, ctx->d_inv_blk + o, ctx->d_inv_dst + o, ctx->d_inv_slot + o, ctx->ldpart,
                            ctx->d_groups + f.gfirst, f.ngrp, ctx->d_ftiles, ctx->d_ftiles + f.pfirst, f.nplain,
-                           f.mode, f.r1, f.r2, ctx->stream, f.mode == 1 ? guard : dwh::SiteGuard{});
-      if (f.mode == 1) guard = dwh::SiteGuard{};
-      ++si;
+                           f.mode, f.r0, f.r1, f.r2, ctx->stream, inv ? guard : dwh::SiteGuard{});
+      if (inv) guard = dwh::SiteGuard{};
+      si += f.nst - 1;
       continue;
     }
     const CrStage& st = plan.stages[si];
@@ -1708,8 +1802,8 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
           std::fprintf(stderr, "cr tail: stages %d..%d in one launch, %d workgroups\n", tg.first, tg.first + tg.n - 1,
                        tg.grid);
         for (const CrFuse& f : ctx->plan.fuses)
-          std::fprintf(stderr, "cr fused: stages %d,%d mode %d groups=%d plain=%d rounds=%d,%d\n", f.first,
-                       f.first + 1, f.mode, f.ngrp, f.nplain, f.r1, f.r2);
+          std::fprintf(stderr, "cr fused: stages %d..%d mode %d groups=%d plain=%d rounds=%d,%d,%d\n", f.first,
+                       f.first + f.nst - 1, f.mode, f.ngrp, f.nplain, f.r0, f.r1, f.r2);
       }
     }
   }
@@ -2820,69 +2914,74 @@ extern "C" {
 // not), no block is read and written in one stage except a task's own
 // accumulate input, no two tasks of a stage write the same block, and every
 // block the force / E_f gather reads was written.
-// The fused launches of a BP = 32 plan (build_cr_fusion) against the two
-// stages each replaces: the tiles are exactly the stages' tiles (mode 1: the
-// second stage's), and groups running concurrently neither write the same
-// block nor read a block another group or a plain tile writes (inside a
-// group, phase 1 runs before phase 2: the order of the two stages).  Returns
-// an error message or nullptr.
+// The fused launches of a BP = 32 plan (build_cr_fusion) against the stages
+// each replaces: the launch's tiles are exactly the product stages' tiles,
+// its inversions the inversion stage's, and groups running concurrently
+// neither write the same block nor read a block another group or a plain
+// tile writes (inside a group the phases run in stage order).  Returns an
+// error message or nullptr.
 static const char* verify_cr_fusion(const CrPlan& plan, int BP) {
   if (!dwh::cr_supported_fuse(BP)) return nullptr;
   CrPlan pl = plan;
   build_cr_fusion(pl);
   static thread_local char buf[256];
-  auto tile_reads = [](const dwh::CrTile& t, std::vector<int>& r) {
-    if (t.cin >= 0) r.push_back(t.cin);
-    for (int h = 0; h < t.nt; ++h) {
-      r.push_back(t.a[h]);
-      r.push_back(t.b[h]);
-    }
-  };
   for (const CrFuse& f : pl.fuses) {
-    const CrStage& A = pl.stages[f.first];
-    const CrStage& B = pl.stages[f.first + 1];
-    // coverage: (out, tr, tc) of the launch's tiles = the stages' tiles
     std::multiset<std::tuple<int, int, int>> want, got;
     auto key = [](const dwh::CrTile& t) { return std::make_tuple(t.out, t.tr, t.tc); };
-    if (A.kind == 1)
-      for (int t = 0; t < A.ntiles; ++t) want.insert(key(pl.tiles16[A.tfirst + t]));
-    for (int t = 0; t < B.ntiles; ++t) want.insert(key(pl.tiles16[B.tfirst + t]));
-    std::vector<std::vector<int>> R(f.ngrp + 1), W(f.ngrp + 1);   // last: plain tiles
-    for (int g = 0; g < f.ngrp; ++g) {
-      const dwh::CrGroup& G = pl.groups[f.gfirst + g];
-      if ((f.mode == 1) != (G.inv >= 0)) return "fused group without its inversion";
-      if (G.inv >= 0) {
-        R[g].push_back(pl.inv_blk[A.first + G.inv]);
-        W[g].push_back(pl.inv_dst[A.first + G.inv]);
+    int inv_first = -1, ninv = 0;
+    for (int k = 0; k < f.nst; ++k) {
+      const CrStage& st = pl.stages[f.first + k];
+      if (st.kind == 0) {
+        if (inv_first >= 0 || st.ntiles > 0) return "fused launch with two or side-work inversion stages";
+        inv_first = st.first;
+        ninv = st.n;
+      } else {
+        for (int t = 0; t < st.ntiles; ++t) want.insert(key(pl.tiles16[st.tfirst + t]));
       }
-      for (int t = 0; t < G.n1 + G.n2; ++t) {
-        const dwh::CrTile& x = pl.ftiles[G.p1 + t];
+    }
+    if ((f.mode == 2) != (inv_first < 0)) return "fused launch mode does not match its stages";
+    std::vector<std::vector<int>> R(f.ngrp + 1), W(f.ngrp + 1);   // last: plain tiles
+    std::vector<int> seen_inv;
+    auto add = [&](int g, int p, int n) {
+      for (int t = 0; t < n; ++t) {
+        const dwh::CrTile& x = pl.ftiles[p + t];
         got.insert(key(x));
-        tile_reads(x, R[g]);
+        tile_blocks(x, R[g]);
         W[g].push_back(x.out);
       }
+    };
+    for (int g = 0; g < f.ngrp; ++g) {
+      const dwh::CrGroup& G = pl.groups[f.gfirst + g];
+      if ((G.inv >= 0) != (inv_first >= 0) || G.inv >= ninv) return "fused group without its inversion";
+      if (G.inv >= 0) {
+        seen_inv.push_back(G.inv);
+        R[g].push_back(pl.inv_blk[inv_first + G.inv]);
+        W[g].push_back(pl.inv_dst[inv_first + G.inv]);
+      }
+      add(g, G.p0, G.n0);
+      add(g, G.p1, G.n1);
+      add(g, G.p2, G.n2);
     }
-    for (int t = 0; t < f.nplain; ++t) {
-      const dwh::CrTile& x = pl.ftiles[f.pfirst + t];
-      got.insert(key(x));
-      tile_reads(x, R[f.ngrp]);
-      W[f.ngrp].push_back(x.out);
-    }
+    add(f.ngrp, f.pfirst, f.nplain);
+    std::sort(seen_inv.begin(), seen_inv.end());
+    for (int k = 0; k < (int)seen_inv.size(); ++k)
+      if (seen_inv[k] != k) return "fused launch does not run every inversion once";
+    if (inv_first >= 0 && (int)seen_inv.size() != ninv) return "fused launch does not run every inversion once";
     if (want != got) {
-      std::snprintf(buf, sizeof buf, "fused stages %d,%d do not cover the stages' tiles", f.first, f.first + 1);
+      std::snprintf(buf, sizeof buf, "fused stages %d..%d do not cover the stages' tiles", f.first,
+                    f.first + f.nst - 1);
       return buf;
     }
     for (int g = 0; g <= f.ngrp; ++g)
       for (int h = 0; h <= f.ngrp; ++h) {
-        if (g == h && g < f.ngrp) continue;   // inside a group the phases are ordered
-        for (int w : W[h]) {
+        if (g == h) continue;
+        for (int w : W[h])
           if (std::find(R[g].begin(), R[g].end(), w) != R[g].end() ||
-              (g != h && std::find(W[g].begin(), W[g].end(), w) != W[g].end())) {
-            std::snprintf(buf, sizeof buf, "fused stages %d,%d: block %d shared by concurrent groups", f.first,
-                          f.first + 1, w);
+              std::find(W[g].begin(), W[g].end(), w) != W[g].end()) {
+            std::snprintf(buf, sizeof buf, "fused stages %d..%d: block %d shared by concurrent groups", f.first,
+                          f.first + f.nst - 1, w);
             return buf;
           }
-        }
       }
   }
   return nullptr;
@@ -2896,12 +2995,16 @@ int dwh_debug_cr_fusion(int64_t Lx, int64_t Ly, int64_t nbatch, int64_t* out) {
   CrPlan pl = build_cr_plan((int)Lx, (int)Ly, BP, Dcol, dwh::cr_supported_side(BP), (int)nbatch, 256,
                             dwh::cr_supported_inv0(BP));
   if (dwh::cr_supported_fuse(BP)) build_cr_fusion(pl);
-  int64_t m1 = 0, m2 = 0;
-  for (const CrFuse& f : pl.fuses) (f.mode == 1 ? m1 : m2)++;
+  int64_t launches = (int64_t)pl.stages.size(), nm[4] = {0, 0, 0, 0};
+  for (const CrFuse& f : pl.fuses) {
+    launches -= f.nst - 1;
+    nm[f.mode]++;
+  }
   out[0] = (int64_t)pl.stages.size();
-  out[1] = (int64_t)pl.stages.size() - (int64_t)pl.fuses.size();   // launches
-  out[2] = m1;
-  out[3] = m2;
+  out[1] = launches;
+  out[2] = nm[1];
+  out[3] = nm[2];
+  out[4] = nm[3];
   return DWH_OK;
 }
 

@@ -1091,11 +1091,13 @@ __global__ __launch_bounds__(64 * NT) void k_cr_inv_side(double2* __restrict__ p
 // CR stage is a few dozen workgroups of 32 x 32 blocks: each launch costs its
 // ~4 us of launch + memory round trip + drain whatever it computes.  A fused
 // launch runs two consecutive stages: one workgroup per GROUP computes
-// [its block inversion (mode 1), then] its phase-1 tiles, then its phase-2
+// [its phase-0 tiles, its block inversion,] its phase-1 tiles, its phase-2
 // tiles, where a later phase reads only what the same workgroup wrote (the
 // planner checks it): the backward G_ae / G_ce then G_ee of one eliminated
-// block (mode 2), or an inversion then the V1 / V2 / W1 / W2 products of the
-// inverted block (mode 1).  Tiles of the first stage that no group needs run
+// block (mode 2); an inversion then the V1 / V2 / W1 / W2 products of the
+// inverted block (mode 1); or, one launch per forward level (mode 3), the
+// Schur complement D' of the block, the U' / L' its products read, the
+// inversion and those products.  Tiles of the first stage that no group needs run
 // as plain workgroups of the same launch.  Phases are separated by
 // __syncthreads(), whose workgroup-scope release / acquire makes the global
 // stores of one wave visible to the other waves of the workgroup (one CU,
@@ -1186,8 +1188,8 @@ __global__ __launch_bounds__(64 * NW) void k_cr_fused(double2* __restrict__ pool
                                                       const int* __restrict__ slot, double* __restrict__ ldpart,
                                                       int nslots, const CrGroup* __restrict__ grp, int ngrp,
                                                       const CrTile* __restrict__ ftl,
-                                                      const CrTile* __restrict__ plain, int nplain, int r1,
-                                                      int r2, SiteGuard sg, int N, int P) {
+                                                      const CrTile* __restrict__ plain, int nplain, int r0,
+                                                      int r1, int r2, SiteGuard sg, int N, int P) {
   static_assert(BP == 16 * NT && NW >= NT && NW % KS1 == 0 && NW % KS2 == 0, "fused launch shape");
   __shared__ double2 red[NW][4][64];
   __shared__ double2 pan[2][NT][16 * 17];
@@ -1201,6 +1203,8 @@ __global__ __launch_bounds__(64 * NW) void k_cr_fused(double2* __restrict__ pool
   constexpr int T1 = NW / KS1, T2 = NW / KS2;   // tiles per round
   if (j < ngrp) {
     const CrGroup G = grp[j];
+    for (int r = 0; r < r0; ++r) cr_tiles_wg<BP, NW, 1>(base, ftl + G.p0 + r * NW, G.n0 - r * NW, red);
+    if (r0 > 0) __syncthreads();   // phase-0 outputs (global) are the inversion's input and phase-1 operands
     if (G.inv >= 0) {
       cr_inv_wg<NT, NW>(pool, item, bi, G.inv, blk, dst, slot, ldpart, nslots, pan, ldw);
       __syncthreads();   // the inverse (global) is read by the phase-1 tiles
@@ -1220,20 +1224,20 @@ bool cr_supported_fuse(int BP) { return BP == 32; }
 
 void launch_cr_fused(const CrDims& c, double2* pool, const int* blk, const int* dst, const int* slot,
                      double* ldpart, const CrGroup* grp, int ngrp, const CrTile* ftl, const CrTile* plain,
-                     int nplain, int mode, int r1, int r2, hipStream_t s, const SiteGuard& sg) {
+                     int nplain, int mode, int r0, int r1, int r2, hipStream_t s, const SiteGuard& sg) {
   constexpr int NW = 8;
   if (c.BP != 32 || ngrp + nplain <= 0) return;
   const bool guard = sg.Delta != nullptr;
-  if (mode == 1) {   // inversion + products: one tile per wave
+  if (mode != 2) {   // [products +] inversion + products: one tile per wave
     const int nplain_wg = (nplain + NW / 4 - 1) / (NW / 4);
     const dim3 g(ngrp + nplain_wg + (guard ? 1 : 0), c.nbatch);
     hipLaunchKernelGGL((k_cr_fused<32, 2, NW, 1, 4>), g, dim3(64 * NW), 0, s, pool, c.item, blk, dst, slot, ldpart,
-                       c.Ly, grp, ngrp, ftl, plain, nplain, r1, r2, sg, c.N, c.P);
+                       c.Ly, grp, ngrp, ftl, plain, nplain, r0, r1, r2, sg, c.N, c.P);
   } else {           // two product phases: 2 waves per phase-1 tile, 4 per phase-2 tile
     const int nplain_wg = (nplain + NW / 4 - 1) / (NW / 4);
     const dim3 g(ngrp + nplain_wg + (guard ? 1 : 0), c.nbatch);
     hipLaunchKernelGGL((k_cr_fused<32, 2, NW, 2, 4>), g, dim3(64 * NW), 0, s, pool, c.item, blk, dst, slot, ldpart,
-                       c.Ly, grp, ngrp, ftl, plain, nplain, r1, r2, sg, c.N, c.P);
+                       c.Ly, grp, ngrp, ftl, plain, nplain, r0, r1, r2, sg, c.N, c.P);
   }
 }
 

@@ -106,21 +106,24 @@ void launch_cr_inv0(const CrDims& c, double2* pool, const int* blk, const int* r
 // (32 x 32 wave tiles, maxt32 per task, each task's sign in bq & kCrNegBit)
 // on the CUs the inversions leave idle
 // Fused launches of the BP = 32 path (dwhmc_cr.hip k_cr_fused, host
-// build_cr_fusion): one workgroup per group runs [inversion entry `inv` of
-// the stage (mode 1), then] its phase-1 tiles, then its phase-2 tiles (mode
-// 2), each later phase reading only what the group wrote; `plain` tiles (no
-// group) run in the same launch.  r1 / r2: rounds of 8 / 4 (mode 1) or 4 / 2
-// (mode 2) tiles per phase, the maximum over the groups.
+// build_cr_fusion): one workgroup per group runs its phase-0 tiles (mode 3),
+// inversion entry `inv` of the stage (modes 1, 3), its phase-1 tiles, its
+// phase-2 tiles (mode 2), each later phase reading only what the group wrote;
+// `plain` tiles (no group) run in the same launch.  r0 / r1 / r2: rounds of
+// tiles per phase (8 per round in phases 0 and 1 of modes 1 and 3; 4 and 2
+// in mode 2), the maximum over the groups.
 struct alignas(32) CrGroup {
   int inv;       // inversion entry of the stage, or -1
-  int p1, n1;    // phase-1 tiles (fused tile list)
+  int p0, n0;    // phase-0 tiles (before the inversion; fused tile list)
+  int p1, n1;    // phase-1 tiles
   int p2, n2;    // phase-2 tiles
-  int pad[3];
+  int pad;
 };
 bool cr_supported_fuse(int BP);
 void launch_cr_fused(const CrDims& c, double2* pool, const int* blk, const int* dst, const int* slot,
                      double* ldpart, const CrGroup* grp, int ngrp, const CrTile* ftl, const CrTile* plain,
-                     int nplain, int mode, int r1, int r2, hipStream_t s, const SiteGuard& sg = SiteGuard{});
+                     int nplain, int mode, int r0, int r1, int r2, hipStream_t s,
+                     const SiteGuard& sg = SiteGuard{});
 bool cr_supported_side(int BP);
 void launch_cr_inv_side(const CrDims& c, double2* pool, const int* blk, const int* dst, const int* slot,
                         int n, double* ldpart, const CrTask* stasks, int nst, int maxt32, hipStream_t s,

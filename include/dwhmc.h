@@ -274,7 +274,8 @@ int dwh_debug_cr_plan_check(int64_t Lx, int64_t Ly, int64_t nbatch, int32_t side
 
 /* Launch fusion of the same plan (BP = 32 lattices, host only): out[0]
  * stages, out[1] launches after fusion, out[2] inversion + product launches
- * (mode 1), out[3] product pair launches (mode 2).  dwh_debug_cr_plan_check
+ * (mode 1), out[3] product pair launches (mode 2), out[4] product +
+ * inversion + product launches (mode 3, one per forward level).  dwh_debug_cr_plan_check
  * also verifies the fused launches (tile coverage, no block shared by
  * concurrent workgroup groups). */
 int dwh_debug_cr_fusion(int64_t Lx, int64_t Ly, int64_t nbatch, int64_t* out);
