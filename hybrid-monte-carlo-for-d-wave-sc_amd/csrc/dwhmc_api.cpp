@@ -772,11 +772,13 @@ bool try_fuse(const CrPlan& pl, size_t si, int mode, FuseTry& f) {
   return fuse_conflict(pl, inv_first, f) == nullptr;
 }
 
-void build_cr_fusion(CrPlan& pl) {
+// modes: bit m-1 allows mode m (DWHMC_CR_FUSE)
+void build_cr_fusion(CrPlan& pl, int modes = 7) {
   size_t si = 0;
   while (si < pl.stages.size()) {
     FuseTry f;
-    if (!try_fuse(pl, si, 3, f) && !try_fuse(pl, si, 1, f) && !try_fuse(pl, si, 2, f)) {
+    if (!((modes & 4) && try_fuse(pl, si, 3, f)) && !((modes & 1) && try_fuse(pl, si, 1, f)) &&
+        !((modes & 2) && try_fuse(pl, si, 2, f))) {
       ++si;
       continue;
     }
@@ -1784,9 +1786,12 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
         const int occ = dwh::cr_tail_occupancy();
         if (occ > 0) build_cr_tails(ctx->plan, d.nbatch, occ * ncu);
       }
-      // DWHMC_CR_FUSE=0: BP = 32 stages as separate launches (A/B runs)
+      // DWHMC_CR_FUSE=m (bitmask of fusion modes 1 / 2 / 3 = bits 0 / 1 / 2):
+      // BP = 32 stages fused into k_cr_fused launches; default off (measured no
+      // faster than separate launches)
       const char* ef = std::getenv("DWHMC_CR_FUSE");
-      if (dwh::cr_supported_fuse(BP) && !(ef && *ef == '0')) build_cr_fusion(ctx->plan);
+      const int fmodes = ef ? std::atoi(ef) : 0;
+      if (dwh::cr_supported_fuse(BP) && fmodes > 0) build_cr_fusion(ctx->plan, fmodes);
       if (const char* e = std::getenv("DWHMC_CR_PLAN_DUMP"); e && *e == '1') {
         int i = 0;
         for (const CrStage& st : ctx->plan.stages) {

@@ -597,12 +597,13 @@ def test_cr_coarse_tail_kernel(dwhmc, oracle, monkeypatch, Lx, Ly):
     ctx.close()
 
 
-@pytest.mark.parametrize("fuse", ["1", "0"])
+@pytest.mark.parametrize("fuse", ["7", "3", "0"])
 @pytest.mark.parametrize("Lx,Ly", [(16, 16), (12, 5), (5, 7), (16, 3), (16, 2)])
 def test_cr_fused_launches(dwhmc, oracle, monkeypatch, fuse, Lx, Ly):
-    """BP = 32 lattices run fused launches by default (k_cr_fused: an inversion
-    with its V/W products, a backward G_ae/G_ce -> G_ee pair; DWHMC_CR_FUSE=0:
-    every stage its own launch): the oracle's results either way, within a
+    """The opt-in fused launches of BP = 32 lattices (DWHMC_CR_FUSE = mode
+    bitmask; k_cr_fused: an inversion with its V/W products, a backward
+    G_ae/G_ce -> G_ee pair, a whole forward level; 0: every stage its own
+    launch, the default): the oracle's results either way, within a
     factorisation and across the sweeps of a trajectory (the site guard rides
     on the fused level-0 launch)."""
     O = oracle
@@ -640,14 +641,14 @@ def test_cr_fused_matches_unfused_batched(dwhmc, oracle, monkeypatch):
     dis = np.stack([c[1] for c in cases])
     D = np.stack([c[2] for c in cases])
     out = {}
-    for fuse in ("1", "0"):
+    for fuse in ("7", "0"):
         monkeypatch.setenv("DWHMC_CR_FUSE", fuse)
         ctx = device_ctx(dwhmc, p, dis, "cr")
         ctx.set_pairing(D)
         ctx.factorize()
         out[fuse] = (ctx.forces(), ctx.fermion_energy(), ctx.hole_trace())
         ctx.close()
-    F1, E1, T1 = out["1"]
+    F1, E1, T1 = out["7"]
     F0, E0, T0 = out["0"]
     assert np.max(np.abs(F1 - F0)) <= 1e-12 * (1 + np.max(np.abs(F0)))
     assert np.max(np.abs(E1 - E0)) <= 1e-13 * np.max(np.abs(E0))
