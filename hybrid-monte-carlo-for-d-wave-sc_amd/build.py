@@ -44,7 +44,11 @@ def build(force: bool = False, verbose: bool = False, out: str = LIB, defines=()
     if not force and out == LIB and not needs_build():
         return LIB
     tmp = out + ".tmp"
+    # kernel arguments preloaded into SGPRs (gfx950): a launch's first loads no
+    # longer wait for the kernarg s_load (C3 -1.8 %, C2 -4.1 % per leapfrog step,
+    # profiles/r03_exp_kernarg_preload.txt)
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-mllvm", "-amdgpu-kernarg-preload-count=16",
            "-Wall", "-Wno-unused-result", f"-I{os.path.join(ROOT, 'include')}",
            *[f"-D{d}" for d in defines], *SOURCES, *LIBS, "-o", tmp]
     if verbose:
