@@ -422,16 +422,17 @@ __device__ __forceinline__ void site_guard_wg(const SiteGuard& sg, int N, int c)
   if (over) *sg.flag = 1;
 }
 
+// gcol: the guard column's x (-1: no guard); arguments in first-use order
 template <int NT>
 __global__ __launch_bounds__(64 * NT) void k_cr_inv(double2* __restrict__ pool, int64_t item,
                                                     const int* __restrict__ blk,
-                                                    const int* __restrict__ dst,
+                                                    const int* __restrict__ dst, int gcol,
                                                     const int* __restrict__ slot,
                                                     double* __restrict__ ldpart, int nslots,
                                                     SiteGuard sg, int N, int P) {
   __shared__ double2 pan[2][NT][16 * 17];
   __shared__ double ldw[NT];
-  if (sg.Delta != nullptr && blockIdx.x == gridDim.x - 1) {   // the guard column, pole 0 of each chain
+  if ((int)blockIdx.x == gcol) {   // the guard column, pole 0 of each chain
     if (blockIdx.y % P == 0) site_guard_wg(sg, N, blockIdx.y / P);
     return;
   }
@@ -610,10 +611,11 @@ __device__ __forceinline__ void tile_from_lds(const double2* T, d4& cr, d4& ci) 
   }
 }
 
+// gcol: the guard column's x (-1: no guard); arguments in first-use order
 __global__ __launch_bounds__(256) void k_cr_inv0(double2* __restrict__ pool, int64_t item,
                                                  const int* __restrict__ blk, const int* __restrict__ rblk,
-                                                 const int* __restrict__ dst, const int* __restrict__ slot,
-                                                 double* __restrict__ ldpart,
+                                                 const int* __restrict__ dst, int gcol,
+                                                 const int* __restrict__ slot, double* __restrict__ ldpart,
                                                  const double* __restrict__ ldA, int nslots,
                                                  const double2* __restrict__ Delta,
                                                  const int* __restrict__ site4, int N, int P, double cap4,
@@ -624,7 +626,7 @@ __global__ __launch_bounds__(256) void k_cr_inv0(double2* __restrict__ pool, int
   const int bi = blockIdx.y, li = blockIdx.x;
   // site guard (launch_cr_inv0 with Delta): the extra last workgroup column,
   // pole 0 of each chain, on a CU the inversions leave idle
-  if (Delta != nullptr && li == (int)gridDim.x - 1) {
+  if (li == gcol) {
     if (bi % P != 0) return;
     const double2* D = Delta + (int64_t)(bi / P) * 2 * N;
     bool over = false;
@@ -1025,13 +1027,15 @@ __device__ __forceinline__ void cr_gemm_wg(double2* __restrict__ pool, int64_t i
   }
 }
 
+// Argument order: what the first loads need leads (the build preloads the
+// leading kernel-argument dwords into SGPRs, build.py), and the grid size is
+// an argument (gridDim is a hidden argument, read by an s_load)
 template <int BP, int MI, int KSPLIT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MI == 1 ? DWHMC_GEMM_WAVES : 2))) void k_cr_gemm(double2* __restrict__ pool, int64_t item,
-                                                 const CrTask* __restrict__ tasks, int ntasks,
-                                                 int maxt, const CrTile* __restrict__ tlist, int ntl,
-                                                 int total, double sg) {
-  cr_gemm_wg<BP, MI, KSPLIT>(pool, item, tasks, ntasks, maxt, tlist, ntl, total, sg,
-                             xcd_remap(blockIdx.x, gridDim.x));
+                                                 const CrTile* __restrict__ tlist, int ntl, int total,
+                                                 double sg, int nwg, int ntasks, int maxt,
+                                                 const CrTask* __restrict__ tasks) {
+  cr_gemm_wg<BP, MI, KSPLIT>(pool, item, tasks, ntasks, maxt, tlist, ntl, total, sg, xcd_remap(blockIdx.x, nwg));
 }
 
 // ---------------------------------------------------------------------------
@@ -1048,31 +1052,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MI == 1 ? D
 // must hide its own MFMA and memory latency; one 16 x 16 tile per wave ran at
 // a third of that rate).
 // ---------------------------------------------------------------------------
+// arguments in first-use order: the inversion workgroups (the first
+// ninv x nbatch) need only the leading ones; nside: side-work workgroups
 template <int NT, bool INV2 = false>
 __global__ __launch_bounds__(64 * NT) void k_cr_inv_side(double2* __restrict__ pool, int64_t item,
                                                          const int* __restrict__ blk,
-                                                         const int* __restrict__ dst,
+                                                         const int* __restrict__ dst, int ninv, int nbatch,
                                                          const int* __restrict__ slot,
                                                          double* __restrict__ ldpart, int nslots,
-                                                         int ninv, int nbatch,
-                                                         const CrTask* __restrict__ stasks, int nst,
-                                                         int maxt, int total, SiteGuard sg, int N,
-                                                         int nchains) {
+                                                         int nside, const CrTask* __restrict__ stasks, int nst,
+                                                         int maxt, int total, SiteGuard sg, int N) {
   static_assert(NT == 4, "side work runs 4-wave workgroups");
   __shared__ double2 pan[2][NT][16 * 17];
   __shared__ double ldw[NT];
   const int b = blockIdx.x, nall = ninv * nbatch;
-  // the last nchains workgroups check the site guard (level-0 launches)
-  const int ng = sg.Delta != nullptr ? nchains : 0, nside = (int)gridDim.x - nall - ng;
-  if (b >= nall + nside) {
-    site_guard_wg(sg, N, b - nall - nside);
-    return;
-  }
 #if defined(DWHMC_SIDE_NOP)     // diagnostic builds (tools/ab_bench.py LIB=...): side part empty
   if (b >= nall) return;
 #elif defined(DWHMC_SIDE_NOINV)  // inversion part empty
   if (b < nall) return;
 #endif
+  // inversions first: their branch needs only the leading (preloaded) arguments
   if (b < nall) {
     if constexpr (INV2) {
       cr_inv2_wg<NT>(pool, item, b / ninv, b - (b / ninv) * ninv, blk, dst, slot, ldpart, nslots,
@@ -1080,6 +1079,11 @@ __global__ __launch_bounds__(64 * NT) void k_cr_inv_side(double2* __restrict__ p
     } else {
       cr_inv_wg<NT>(pool, item, b / ninv, b - (b / ninv) * ninv, blk, dst, slot, ldpart, nslots, pan, ldw);
     }
+    return;
+  }
+  // the workgroups after the side work check the site guard (level-0 launches)
+  if (b >= nall + nside) {
+    site_guard_wg(sg, N, b - nall - nside);
     return;
   }
   cr_gemm_wg<16 * NT, 2, 1, 0, true>(pool, item, stasks, nst, maxt, nullptr, 0, total, 1.0,
@@ -1101,9 +1105,10 @@ __global__ __launch_bounds__(64 * NT) void k_cr_inv_side(double2* __restrict__ p
 // as plain workgroups of the same launch.  Phases are separated by
 // __syncthreads(), whose workgroup-scope release / acquire makes the global
 // stores of one wave visible to the other waves of the workgroup (one CU,
-// one vector L1; no tgsplit).  A 32 x 32 block product is 96 MFMAs, so a
-// workgroup's serial phases cost less than the launch they remove (at BP = 64
-// they are 8x that: profiles/r02_exp_cr_fused_v_products.txt).
+// one vector L1; no tgsplit).  Opt-in (DWHMC_CR_FUSE): measured slower than
+// the separate launches -- each phase pays its own store / reload chain on
+// fewer workgroups, and a launch boundary costs little
+// (profiles/r03_exp_cr_fused_launches_bp32.txt).
 // ---------------------------------------------------------------------------
 // One round of up to NW / KS tiles of a list: KS waves per tile split its K
 // range (cr_tile_part), partials summed through LDS (red: NW x 4 x 64).  Every
@@ -1334,10 +1339,11 @@ __global__ __launch_bounds__(64 * NT) void k_cr_tail(double2* __restrict__ pool,
 // drift (inside a trajectory) the drifted Δ/2 is scattered straight into the
 // level-0 pairing entries of every pole (off_ph), so the next factorisation
 // needs no k_cr_fill launch.
+// arguments in first-use order (kernel-argument preload)
 __global__ __launch_bounds__(256) void k_cr_pair_force(
     double2* __restrict__ pool, int64_t item, const int64_t* __restrict__ goff,
-    const int64_t* __restrict__ off_ph, const int* __restrict__ Dsrc, const int* __restrict__ bond_ij,
-    const int* __restrict__ bond_ji, const double* __restrict__ cpole, int N, int P,
+    const int* __restrict__ bond_ij, const int* __restrict__ bond_ji, int N, int P,
+    const double* __restrict__ cpole, const int64_t* __restrict__ off_ph, const int* __restrict__ Dsrc,
     double2* __restrict__ Delta, double2* __restrict__ Pair, double2* __restrict__ F,
     double2* __restrict__ Pi, double kick, double drift, double cap2, int* __restrict__ flag,
     double beta, double J) {
@@ -1463,7 +1469,7 @@ void launch_cr_inv0(const CrDims& c, double2* pool, const int* blk, const int* r
   if (n <= 0) return;
   const bool guard = Delta != nullptr && site4 != nullptr && flag != nullptr;
   hipLaunchKernelGGL(k_cr_inv0, dim3(n + (guard ? 1 : 0), c.nbatch), dim3(256), 0, s, pool, c.item, blk, rblk,
-                     dst, slot, ldpart, ldA, c.Ly, guard ? Delta : nullptr, site4, c.N, c.P, cap4, flag);
+                     dst, guard ? n : -1, slot, ldpart, ldA, c.Ly, guard ? Delta : nullptr, site4, c.N, c.P, cap4, flag);
 }
 
 void launch_cr_fill(const CrDims& c, double2* pool, const int* list, int nlist, const int* hcol,
@@ -1486,23 +1492,28 @@ void launch_cr_inv(const CrDims& c, double2* pool, const int* blk, const int* ds
     const dim3 g(n, c.nbatch);
     hipLaunchKernelGGL(k_cr_inv2, g, dim3(64 * DWHMC_INV2_WAVES), 0, s, pool, c.item, blk, dst, slot, ldpart, c.Ly);
     if (guard)   // the guard column alone (grid x = 1)
-      hipLaunchKernelGGL(k_cr_inv<4>, dim3(1, c.nbatch), dim3(256), 0, s, pool, c.item, blk, dst, slot, ldpart, c.Ly,
-                         sg, c.N, c.P);
+      hipLaunchKernelGGL(k_cr_inv<4>, dim3(1, c.nbatch), dim3(256), 0, s, pool, c.item, blk, dst, 0, slot, ldpart,
+                         c.Ly, sg, c.N, c.P);
     return;
   }
   const dim3 g(n + (guard ? 1 : 0), c.nbatch);
+  const int gcol = guard ? n : -1;
   switch (c.BP) {
     case 32:
-      hipLaunchKernelGGL(k_cr_inv<2>, g, dim3(128), 0, s, pool, c.item, blk, dst, slot, ldpart, c.Ly, sg, c.N, c.P);
+      hipLaunchKernelGGL(k_cr_inv<2>, g, dim3(128), 0, s, pool, c.item, blk, dst, gcol, slot, ldpart, c.Ly, sg, c.N,
+                         c.P);
       break;
     case 64:
-      hipLaunchKernelGGL(k_cr_inv<4>, g, dim3(256), 0, s, pool, c.item, blk, dst, slot, ldpart, c.Ly, sg, c.N, c.P);
+      hipLaunchKernelGGL(k_cr_inv<4>, g, dim3(256), 0, s, pool, c.item, blk, dst, gcol, slot, ldpart, c.Ly, sg, c.N,
+                         c.P);
       break;
     case 96:
-      hipLaunchKernelGGL(k_cr_inv<6>, g, dim3(384), 0, s, pool, c.item, blk, dst, slot, ldpart, c.Ly, sg, c.N, c.P);
+      hipLaunchKernelGGL(k_cr_inv<6>, g, dim3(384), 0, s, pool, c.item, blk, dst, gcol, slot, ldpart, c.Ly, sg, c.N,
+                         c.P);
       break;
     default:
-      hipLaunchKernelGGL(k_cr_inv<8>, g, dim3(512), 0, s, pool, c.item, blk, dst, slot, ldpart, c.Ly, sg, c.N, c.P);
+      hipLaunchKernelGGL(k_cr_inv<8>, g, dim3(512), 0, s, pool, c.item, blk, dst, gcol, slot, ldpart, c.Ly, sg, c.N,
+                         c.P);
       break;
   }
 }
@@ -1519,11 +1530,11 @@ void launch_cr_inv_side(const CrDims& c, double2* pool, const int* blk, const in
   const int nc = c.nbatch / c.P;
   const dim3 g(n * c.nbatch + side_wg + (sg.Delta != nullptr ? nc : 0));
   if (c.inv2)
-    hipLaunchKernelGGL((k_cr_inv_side<4, true>), g, dim3(256), 0, s, pool, c.item, blk, dst, slot, ldpart, c.Ly, n,
-                       c.nbatch, stasks, nst, maxt32, total, sg, c.N, nc);
+    hipLaunchKernelGGL((k_cr_inv_side<4, true>), g, dim3(256), 0, s, pool, c.item, blk, dst, n, c.nbatch, slot,
+                       ldpart, c.Ly, side_wg, stasks, nst, maxt32, total, sg, c.N);
   else
-    hipLaunchKernelGGL((k_cr_inv_side<4, false>), g, dim3(256), 0, s, pool, c.item, blk, dst, slot, ldpart, c.Ly, n,
-                       c.nbatch, stasks, nst, maxt32, total, sg, c.N, nc);
+    hipLaunchKernelGGL((k_cr_inv_side<4, false>), g, dim3(256), 0, s, pool, c.item, blk, dst, n, c.nbatch, slot,
+                       ldpart, c.Ly, side_wg, stasks, nst, maxt32, total, sg, c.N);
 }
 
 // Stage configuration (tile TS, K split).  16 x 16 tiles with a 4-way K
@@ -1563,8 +1574,8 @@ void launch_cr_gemm(const CrDims& c, double2* pool, const CrTask* tasks, int nta
   const int tpw = 4 / cfg.ksplit;
   const dim3 g((total + tpw - 1) / tpw), b(256);
 #define CR_GEMM(BPV, MIV, KSV) \
-  hipLaunchKernelGGL((k_cr_gemm<BPV, MIV, KSV>), g, b, 0, s, pool, c.item, tasks, ntasks, maxt, tl, ntl16, \
-                     total, sg)
+  hipLaunchKernelGGL((k_cr_gemm<BPV, MIV, KSV>), g, b, 0, s, pool, c.item, tl, ntl16, total, sg, (int)g.x, \
+                     ntasks, maxt, tasks)
 #define CR_GEMM_BP(BPV)                        \
   if (cfg.ts == 16) {                          \
     if (cfg.ksplit == 4) CR_GEMM(BPV, 1, 4);   \
@@ -1590,7 +1601,7 @@ void launch_cr_pair_force(const CrDims& c, double2* pool, const int64_t* goff, c
                           const KickDrift& kd, double beta, double J, hipStream_t s) {
   const int nc = c.nbatch / c.P;
   hipLaunchKernelGGL(k_cr_pair_force, dim3((2 * c.N + 7) / 8, nc), dim3(256), 0, s, pool, c.item,
-                     goff, off_ph, Dsrc, bond_ij, bond_ji, cpole, c.N, c.P, Delta, Pair, F, Pi, kd.kick,
+                     goff, bond_ij, bond_ji, c.N, c.P, cpole, off_ph, Dsrc, Delta, Pair, F, Pi, kd.kick,
                      kd.drift, kd.cap * kd.cap, kd.flag, beta, J);
 }
 
