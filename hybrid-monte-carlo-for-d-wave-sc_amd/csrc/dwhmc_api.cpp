@@ -902,7 +902,8 @@ struct dwh_ctx {
   unsigned long long tail_base = 0;
   int* d_tail_err = nullptr;
   double* ldA = nullptr;   // static ln|det| of the Δ = 0 level-0 blocks (= 2 ln|det A|) per slot
-  int64_t *d_goff = nullptr, *d_doff = nullptr, *d_off_ph = nullptr;
+  int64_t *d_doff = nullptr, *d_off_ph = nullptr;
+  int64_t* d_bond4 = nullptr;   // k_cr_pair_force: per bond its G12 offsets and pairing-entry offsets
   int *d_fill_all = nullptr, *d_fill_step = nullptr;
   // the pool's level-0 pairing entries already hold the current Δ (set by a
   // drifting k_cr_pair_force, consumed by the next factorisation); every
@@ -1255,10 +1256,8 @@ void factorize_enqueue(dwh_ctx* ctx, const dwh::KickDrift& kd) {
     cr_enqueue(ctx);
     // the kernel scatters the drifted Δ into the pool only when it drifts
     ctx->pairing_in_pool = kd.drift != 0.0;
-    dwh::launch_cr_pair_force(ctx->cr, ctx->bpool, ctx->d_goff, ctx->d_off_ph, ctx->Dsrc, ctx->bond_ij,
-                              ctx->bond_ji, ctx->d_c,
-                              ctx->Delta, ctx->Pair, ctx->F, ctx->Pi, kd, ctx->beta, ctx->J,
-                              ctx->stream);
+    dwh::launch_cr_pair_force(ctx->cr, ctx->bpool, ctx->d_bond4, ctx->d_c, ctx->Delta, ctx->Pair, ctx->F, ctx->Pi,
+                              kd, ctx->beta, ctx->J, ctx->stream);
     return;
   }
   dwh::launch_dvals(d, ctx->Dsrc, ctx->Delta, ctx->Dv, ctx->stream);
@@ -1858,9 +1857,9 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     ALLOC(d_inv_slot, pl.inv_slot.size());
     ALLOC(d_inv0_r, pl.inv0_r.size());
     ALLOC(ldA, (size_t)d.nbatch * Ly);
-    ALLOC(d_goff, pl.goff.size());
     ALLOC(d_doff, pl.doff.size());
     ALLOC(d_off_ph, pl.off_ph.size());
+    ALLOC(d_bond4, 4 * bij.size());
     ALLOC(d_fill_all, pl.fill_all.size());
     ALLOC(d_fill_step, pl.fill_step.size());
     if (!pl.tails.empty()) {
@@ -1931,6 +1930,21 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     }
     UP(site4, ctx->site4_host.data(), ctx->site4_host.size());
   }
+  // per bond b (2N of them, CR path): G12[i, j], G12[j, i] and the pairing
+  // entries it writes (Dsrc picks the bond whose value an entry holds); kept
+  // alive until the uploads below have been synchronised
+  std::vector<int64_t> bond4;
+  if (ctx->algo == ALGO_CR) {
+    const CrPlan& pl = ctx->plan;
+    bond4.resize(4 * bij.size());
+    for (size_t b = 0; b < bij.size(); ++b) {
+      const int e1 = bij[b], e2 = bji[b];
+      bond4[4 * b] = pl.goff[e1];
+      bond4[4 * b + 1] = pl.goff[e2];
+      bond4[4 * b + 2] = Dsrc[e1] == (int)b ? pl.off_ph[e1] : -1;
+      bond4[4 * b + 3] = Dsrc[e2] == (int)b ? pl.off_ph[e2] : -1;
+    }
+  }
   if (ctx->algo == ALGO_CR) {
     const CrPlan& pl = ctx->plan;
     UP(d_tasks, pl.tasks.data(), pl.tasks.size());
@@ -1943,9 +1957,9 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     UP(d_inv_dst, pl.inv_dst.data(), pl.inv_dst.size());
     UP(d_inv_slot, pl.inv_slot.data(), pl.inv_slot.size());
     UP(d_inv0_r, pl.inv0_r.data(), pl.inv0_r.size());
-    UP(d_goff, pl.goff.data(), pl.goff.size());
     UP(d_doff, pl.doff.data(), pl.doff.size());
     UP(d_off_ph, pl.off_ph.data(), pl.off_ph.size());
+    UP(d_bond4, bond4.data(), bond4.size());
     UP(d_fill_all, pl.fill_all.data(), pl.fill_all.size());
     UP(d_fill_step, pl.fill_step.data(), pl.fill_step.size());
     if (!pl.tails.empty()) {

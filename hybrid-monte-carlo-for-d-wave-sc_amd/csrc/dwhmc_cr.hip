@@ -1337,20 +1337,21 @@ __global__ __launch_bounds__(64 * NT) void k_cr_tail(double2* __restrict__ pool,
 // 32 lanes per bond, one pole per lane (the G entries of the poles live in
 // different batch items: independent loads), shuffle reduction.  With a
 // drift (inside a trajectory) the drifted Δ/2 is scattered straight into the
-// level-0 pairing entries of every pole (off_ph), so the next factorisation
-// needs no k_cr_fill launch.
+// level-0 pairing entries of every pole, so the next factorisation needs no
+// k_cr_fill launch.  bond4[4 b ..]: the pool offsets of G12[i, j], G12[j, i]
+// and of the two pairing entries bond b writes (-1: written by another bond;
+// small lattices map several bonds onto one entry), resolved at context
+// creation so the G loads wait for one index load, not two.
 // arguments in first-use order (kernel-argument preload)
 __global__ __launch_bounds__(256) void k_cr_pair_force(
-    double2* __restrict__ pool, int64_t item, const int64_t* __restrict__ goff,
-    const int* __restrict__ bond_ij, const int* __restrict__ bond_ji, int N, int P,
-    const double* __restrict__ cpole, const int64_t* __restrict__ off_ph, const int* __restrict__ Dsrc,
-    double2* __restrict__ Delta, double2* __restrict__ Pair, double2* __restrict__ F,
-    double2* __restrict__ Pi, double kick, double drift, double cap2, int* __restrict__ flag,
-    double beta, double J) {
+    double2* __restrict__ pool, int64_t item, const int64_t* __restrict__ bond4, int N, int P,
+    const double* __restrict__ cpole, double2* __restrict__ Delta, double2* __restrict__ Pair,
+    double2* __restrict__ F, double2* __restrict__ Pi, double kick, double drift, double cap2,
+    int* __restrict__ flag, double beta, double J) {
   const int b = blockIdx.x * 8 + (threadIdx.x >> 5), sub = threadIdx.x & 31;
   const int c = blockIdx.y;
   if (b >= 2 * N) return;   // uniform per 32-lane group
-  const int64_t o1 = goff[bond_ij[b]], o2 = goff[bond_ji[b]];
+  const int64_t o1 = bond4[4 * b], o2 = bond4[4 * b + 1];
   double2 Pv = make_double2(0.0, 0.0);
   for (int q = sub; q < P; q += 32) {
     const double2* G = pool + (int64_t)(c * P + q) * item;
@@ -1375,14 +1376,12 @@ __global__ __launch_bounds__(256) void k_cr_pair_force(
     kick_drift(Fv, o, Delta, Pi, kick, drift, cap2, flag);
     if (drift != 0.0) dn = Delta[o];
   }
-  if (drift != 0.0 && off_ph != nullptr) {
+  if (drift != 0.0) {
     dn.x = 0.5 * __shfl(dn.x, 0, 32);
     dn.y = 0.5 * __shfl(dn.y, 0, 32);
     // an entry is written only by the bond k_cr_fill takes its value from
-    // (small lattices map several bonds onto one entry: Dsrc picks the one
-    // the reference's overwrite order leaves, src/Hamiltonian.jl:68-83)
-    const int e1 = bond_ij[b], e2 = bond_ji[b];
-    const int64_t p1 = Dsrc[e1] == b ? off_ph[e1] : -1, p2 = Dsrc[e2] == b ? off_ph[e2] : -1;
+    // (Dsrc: the one the reference's overwrite order leaves, src/Hamiltonian.jl:68-83)
+    const int64_t p1 = bond4[4 * b + 2], p2 = bond4[4 * b + 3];
     for (int q = sub; q < P; q += 32) {
       double2* G = pool + (int64_t)(c * P + q) * item;
       if (p1 >= 0) G[p1] = dn;
@@ -1595,14 +1594,12 @@ void launch_cr_gemm(const CrDims& c, double2* pool, const CrTask* tasks, int nta
 #undef CR_GEMM
 }
 
-void launch_cr_pair_force(const CrDims& c, double2* pool, const int64_t* goff, const int64_t* off_ph,
-                          const int* Dsrc, const int* bond_ij, const int* bond_ji, const double* cpole,
+void launch_cr_pair_force(const CrDims& c, double2* pool, const int64_t* bond4, const double* cpole,
                           double2* Delta, double2* Pair, double2* F, double2* Pi,
                           const KickDrift& kd, double beta, double J, hipStream_t s) {
   const int nc = c.nbatch / c.P;
-  hipLaunchKernelGGL(k_cr_pair_force, dim3((2 * c.N + 7) / 8, nc), dim3(256), 0, s, pool, c.item,
-                     goff, bond_ij, bond_ji, c.N, c.P, cpole, off_ph, Dsrc, Delta, Pair, F, Pi, kd.kick,
-                     kd.drift, kd.cap * kd.cap, kd.flag, beta, J);
+  hipLaunchKernelGGL(k_cr_pair_force, dim3((2 * c.N + 7) / 8, nc), dim3(256), 0, s, pool, c.item, bond4, c.N,
+                     c.P, cpole, Delta, Pair, F, Pi, kd.kick, kd.drift, kd.cap * kd.cap, kd.flag, beta, J);
 }
 
 void launch_cr_fermion_energy(const CrDims& c, const double2* pool, const int64_t* doff,

@@ -68,11 +68,11 @@ bool cr_supported_bp(int BP);
 void launch_cr_fill(const CrDims& c, double2* pool, const int* list, int nlist, const int* hcol,
                     const double* hval, const int* Dcol, const int* Dsrc, const double2* Delta,
                     const double* ypole, const int64_t* off_ph, hipStream_t s);
-// P from the level-0 G blocks (pool offsets goff, pole weights), F, kick / drift
-// off_ph (nullable): with kd.drift != 0 the drifted Δ/2 is also scattered
-// into the level-0 pairing entries of the pool (k_cr_fill's scatter)
-void launch_cr_pair_force(const CrDims& c, double2* pool, const int64_t* goff, const int64_t* off_ph,
-                          const int* Dsrc, const int* bond_ij, const int* bond_ji, const double* cpole,
+// P from the level-0 G blocks (pole weights), F, kick / drift; per bond b,
+// bond4[4 b ..] = pool offsets of G12[i, j], G12[j, i] and of the two
+// pairing entries the bond writes (-1: none); with kd.drift != 0 the drifted
+// Δ/2 is also scattered into those level-0 entries (k_cr_fill's scatter)
+void launch_cr_pair_force(const CrDims& c, double2* pool, const int64_t* bond4, const double* cpole,
                           double2* Delta, double2* Pair, double2* F, double2* Pi,
                           const KickDrift& kd, double beta, double J, hipStream_t s);
 // E_f and Tr ρ_hh from the CR block pivots and the G22 diagonal (pool offsets doff)
