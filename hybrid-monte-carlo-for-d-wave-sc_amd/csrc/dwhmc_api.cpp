@@ -1776,7 +1776,7 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
       c.inv2 = BP == 64 && ei && *ei == '1';
       d.nld = (int)Ly;
       for (CrStage& st : ctx->plan.stages)
-        if (st.kind == 1) st.cfg = dwh::cr_gemm_config(c, st.n, st.maxt32, st.maxt16, st.ntmax);
+        if (st.kind == 1) st.cfg = dwh::cr_gemm_config(c, st.n, st.maxt32, st.maxt16, st.ntmax, st.ntiles);
       // DWHMC_CR_TAIL=1: the coarse tail in one k_cr_tail launch (measured slower
       // on MI355X: a device-wide stage barrier costs more than a launch boundary,
       // profiles/r02_exp_cr_coarse_tail_grid_barrier.txt; off by default)

@@ -1536,13 +1536,19 @@ void launch_cr_inv_side(const CrDims& c, double2* pool, const int* blk, const in
                        ldpart, c.Ly, side_wg, stasks, nst, maxt32, total, sg, c.N);
 }
 
-// Stage configuration (tile TS, K split).  16 x 16 tiles with a 4-way K
-// split measured fastest on every stage of the L=32 plan (tools/cr_cfg_sweep.sh,
-// profiles/r01_cr_gemm_config_sweep.txt): the stages are short and latency
-// bound, so short serial MFMA chains on many waves win over operand reuse.
-// DWHMC_CR_GEMM=TS:KSPLIT forces another configuration for every stage (A/B
-// runs; tests/test_gpu_parity.py runs every compiled variant).
-CrGemmCfg cr_gemm_config(const CrDims& c, int ntasks, int maxt32, int maxt16, int ntmax) {
+// Stage configuration (tile TS, K split).  16 x 16 tiles; the K split by the
+// stage's size (ntiles16 16 x 16 output tiles per batch item x nbatch): a
+// 4-way split (short serial MFMA chains on many waves) for the stages of a
+// single L = 32 chain, whose stages are short and latency bound
+// (profiles/r01_cr_gemm_config_sweep.txt: fastest on every stage there), no
+// split once a stage has enough tiles to fill the chip by itself (batched
+// chains, L = 48: no LDS reduction, one tile per wave;
+// profiles/r03_exp_gemm_ksplit_by_size.txt: from 2048 tiles, C3 -0.9 %,
+// C5 -5 %, 4 chains at L = 32 -3 %; C2's stages stay below it).
+// DWHMC_CR_KS_T2 / _T1: the tile counts from which the split is 2 / 1.  DWHMC_CR_GEMM=TS:KSPLIT forces one
+// configuration for every stage (A/B runs; tests/test_gpu_parity.py runs
+// every compiled variant).
+CrGemmCfg cr_gemm_config(const CrDims& c, int ntasks, int maxt32, int maxt16, int ntmax, int ntiles16) {
   (void)ntasks;
   (void)maxt32;
   (void)maxt16;
@@ -1560,7 +1566,13 @@ CrGemmCfg cr_gemm_config(const CrDims& c, int ntasks, int maxt32, int maxt16, in
   }();
   const bool ts32_ok = (c.BP / 2) % 32 == 0;   // 32-wide tiles must not straddle A | B
   if (forced.ts == 16 || (forced.ts == 32 && ts32_ok)) return forced;
-  return CrGemmCfg{16, 4};
+  auto knob = [](const char* name, int dflt) {
+    const char* e = std::getenv(name);
+    return e ? std::atoi(e) : dflt;
+  };
+  const int64_t T = (int64_t)ntiles16 * c.nbatch;
+  const int t1 = knob("DWHMC_CR_KS_T1", 2048), t2 = knob("DWHMC_CR_KS_T2", t1);
+  return CrGemmCfg{16, T >= t1 ? 1 : T >= t2 ? 2 : 4};
 }
 
 void launch_cr_gemm(const CrDims& c, double2* pool, const CrTask* tasks, int ntasks, int maxt32,

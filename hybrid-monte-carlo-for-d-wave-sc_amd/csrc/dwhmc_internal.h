@@ -154,7 +154,7 @@ struct CrGemmCfg {
 };
 // maxt32 / maxt16: the largest cr_task_tiles over the stage's tasks at ts = 32 / 16;
 // ntmax: the largest term count
-CrGemmCfg cr_gemm_config(const CrDims& c, int ntasks, int maxt32, int maxt16, int ntmax);
+CrGemmCfg cr_gemm_config(const CrDims& c, int ntasks, int maxt32, int maxt16, int ntmax, int ntiles16);
 // tl16: the stage's (task, tile) list at 16 x 16 tiles (ntl16 entries per batch item)
 void launch_cr_gemm(const CrDims& c, double2* pool, const CrTask* tasks, int ntasks, int maxt32,
                     int maxt16, const CrTile* tl16, int ntl16, const CrGemmCfg& cfg, double sg,
