@@ -64,9 +64,14 @@ def measured_traffic(kernel, L, beta, chains):
         w = rec.get("workload", {})
         if (w.get("L"), w.get("beta"), w.get("chains")) != (L, beta, chains):
             continue
-        k = rec.get("kernels", {}).get(kernel)
-        if k:
-            return k["hbm_bytes_per_launch"], "profiles/" + os.path.basename(path)
+        # a kernel family (the block products at K split 4 and 1): launch-weighted
+        names = kernel if isinstance(kernel, (list, tuple)) else [kernel]
+        ks = [rec.get("kernels", {}).get(n) for n in names]
+        ks = [k for k in ks if k]
+        if ks:
+            n = sum(k.get("launches_fetch_pass", 1) for k in ks)
+            b = sum(k["hbm_bytes_per_launch"] * k.get("launches_fetch_pass", 1) for k in ks)
+            return b / n, "profiles/" + os.path.basename(path)
     return None, None
 
 
@@ -405,7 +410,10 @@ def main(argv=None):
             ms, n, w = kern[dom]
             ach = w / n / (ms / n * 1e-3) / 1e12 if n and ms > 0 else None
             if cr:
-                kname = f"k_cr_gemm<{info['block']},1,4>"   # 16x16 tiles, 4-way K split
+                # 16x16 tiles, 4-way K split below 2048 tiles per stage, none from there
+                # (cr_gemm_config): one timer family, two rocprofv3 rows
+                kname = f"k_cr_gemm<{info['block']},1,4|1>"
+                kfam = [f"k_cr_gemm<{info['block']},1,4>", f"k_cr_gemm<{info['block']},1,1>"]
                 msi, ni, wi = kern["cr_inv"]
                 mss, ns, ws = kern["cr_inv_side"]
                 mst, nt_, wt = kern["cr_tail"]
@@ -456,7 +464,7 @@ def main(argv=None):
             else:
                 nb = -(-info["N"] // 64)                 # GJ block steps; odd nb ends with one rank-64 step
                 kname = "k_gj_update<2>" if nb % 2 == 0 else "k_gj_update<2>+<0>"
-            traffic, tsrc = measured_traffic(kname, a.L, a.beta, a.chains)
+            traffic, tsrc = measured_traffic(kfam if cr else kname, a.L, a.beta, a.chains)
             rec["roofline"] = {"bound": "mfma", "kernel": kname, "achieved": ach,
                                "peak": PEAK_F64_TFLOPS, "unit": "TFLOP/s",
                                "frac": ach / PEAK_F64_TFLOPS if ach else None, "traffic": traffic,
