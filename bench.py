@@ -314,13 +314,24 @@ def main(argv=None):
     timed = schedule(w_sw, a.steps, Nt)
     noise, uni = synthetic_draws(m, p.N, rank, a.chains, w_sw + n_draws(timed), 7)
     ctx.load_draws(noise, uni)                      # inputs resident in HBM before timing
+    gc_first = os.environ.get("DWHMC_BENCH_GC_FIRST", "1") != "0"
+    if gc_first:
+        # host housekeeping before the warmup, so the warmup runs right before
+        # the timed region (no idle GPU gap between them)
+        gc.collect()
+        gc.disable()                                # no collector pause inside the timed region
+        if dist is not None:
+            dist.barrier()
     for f, n, nt in warm:
         ctx.run_sweeps(f, n, nt, dt, p.mass)
     ctx.synchronize()
 
-    gc.collect()
-    gc.disable()                                    # no collector pause inside the ~7 ms timed region
-    if dist is not None:
+    if not gc_first:
+        gc.collect()
+        gc.disable()
+        if dist is not None:
+            dist.barrier()
+    elif dist is not None:
         dist.barrier()
     ctx.synchronize()
     t0 = time.perf_counter()
