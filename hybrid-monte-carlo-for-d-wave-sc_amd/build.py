@@ -46,9 +46,12 @@ def build(force: bool = False, verbose: bool = False, out: str = LIB, defines=()
     tmp = out + ".tmp"
     # kernel arguments preloaded into SGPRs (gfx950): a launch's first loads no
     # longer wait for the kernarg s_load (C3 -1.8 %, C2 -4.1 % per leapfrog step,
-    # profiles/r03_exp_kernarg_preload.txt)
+    # profiles/r03_exp_kernarg_preload.txt); MFMA accumulators in VGPRs instead
+    # of AGPRs: the register inversions mix MFMA tiles and VALU pivot steps, and
+    # drop ~90 % of their accvgpr copies (C3 -2.0 %,
+    # profiles/r03_exp_mfma_vgpr_form.txt)
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-mllvm", "-amdgpu-kernarg-preload-count=16",
+           "-mllvm", "-amdgpu-kernarg-preload-count=16", "-mllvm", "-amdgpu-mfma-vgpr-form",
            "-Wall", "-Wno-unused-result", f"-I{os.path.join(ROOT, 'include')}",
            *[f"-D{d}" for d in defines], *SOURCES, *LIBS, "-o", tmp]
     if verbose:
