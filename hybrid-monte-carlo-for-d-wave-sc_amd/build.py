@@ -15,8 +15,11 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libdwhmc.so")
 SOURCES = [os.path.join(CSRC, "dwhmc_kernels.hip"), os.path.join(CSRC, "dwhmc_cr.hip"),
+           os.path.join(CSRC, "dwhmc_eig.hip"),
            os.path.join(CSRC, "dwhmc_transport.hip"), os.path.join(CSRC, "dwhmc_api.cpp")]
-# rocSOLVER (zheevd) and rocBLAS (zgemm) serve the transport measurement only
+# rocBLAS (zgemm / dgemm products of the eigensolver and J_mn) and rocSOLVER
+# (zheevd / zheev: opt-in via DWHMC_EIG_SOLVER, and the fallback) serve the
+# transport measurement and the eig path only
 LIBS = ["-L/opt/rocm/lib", "-lrocsolver", "-lrocblas", "-Wl,-rpath,/opt/rocm/lib"]
 DEPS = SOURCES + [os.path.join(CSRC, "dwhmc_internal.h"), os.path.join(CSRC, "dwhmc_device.h"),
                   os.path.join(CSRC, "pole_table.inc"), os.path.join(CSRC, "pole_table_eps5e-12.inc"),

@@ -82,11 +82,12 @@ const PoleTable* pole_table(std::string* err) {
 
 enum TimerName {
   T_GJ_UPDATE = 0, T_GJ_PIVOT, T_ASSEMBLE, T_CONTRACT, T_STEP, T_GJ_EDGE, T_CR_GEMM, T_CR_INV, T_CR_INVSIDE,
-  T_CR_TAIL, T_CR_FUSED, T_COUNT
+  T_CR_TAIL, T_CR_FUSED, T_EIG_OWN, T_EIG_VENDOR, T_COUNT
 };
 const char* kTimerNames[T_COUNT] = {"gj_update", "gj_pivot", "assemble", "contract",
                                     "step",      "gj_edge",  "cr_gemm",  "cr_inv",
-                                    "cr_inv_side", "cr_tail", "cr_fused"};
+                                    "cr_inv_side", "cr_tail", "cr_fused",
+                                    "eig_own",   "eig_vendor"};   // eigensolves (work: matrices)
 
 enum Algo { ALGO_DENSE = 0, ALGO_CR = 1, ALGO_EIG = 2 };
 
@@ -928,6 +929,14 @@ struct dwh_ctx {
   int64_t tr_nw = -1, tr_nd = -1;   // ω / DOS grid lengths the output buffers hold
   double2* d_tr_stage = nullptr;     // Δ snapshots of dwh_measure_transport_deltas
   int64_t tr_nstage = 0;
+  // own eigensolver (dwhmc_eig.hip) workspace for eig_slots matrices: hemv
+  // partials, v ping-pong, w, tridiagonal (d, e), tau, compact-WY T blocks and
+  // the back-transform's two nb x n products; the n x n work lives in the
+  // slots' JU (A -> V), Jmn and U (eigenvector / LU scratch) buffers
+  int eig_slots = 0;
+  double2 *d_eig_part = nullptr, *d_eig_vv = nullptr, *d_eig_ww = nullptr, *d_eig_tau = nullptr;
+  double2 *d_eig_T = nullptr, *d_eig_W = nullptr, *d_eig_W2 = nullptr;
+  double *d_eig_d = nullptr, *d_eig_e = nullptr, *d_eig_tn = nullptr;
 
   // timing
   int timing = 0;   // bitmask over TimerName (bit i = kTimerNames[i])
@@ -2125,16 +2134,141 @@ TrSrc chains_src(const dwh_ctx* ctx, int64_t c0) {
   return TrSrc{ctx->Delta + c0 * n2, n2, c0, 1};
 }
 
+// dense H_BdG(Δ) of the m slots' chains into A (m matrices at stride n2^2)
+int assemble_slots(dwh_ctx* ctx, const TrSrc& src, int m, double2* A) {
+  const int N = ctx->d.N;
+  const int64_t sA = 4 * (int64_t)N * N;
+  HIPCHECK(ctx, hipMemsetAsync(A, 0, (size_t)m * sA * sizeof(double2), ctx->stream));
+  for (int k = 0; k < m; ++k)
+    dwh::launch_tr_assemble(A + k * sA, N, ctx->hcol,
+                            ctx->hval + (size_t)(src.chain0 + (int64_t)k * src.cstep) * N * kHSlots, ctx->Dcol,
+                            ctx->Dsrc, src.Delta + (size_t)k * src.dstride, ctx->stream);
+  HIPCHECK(ctx, hipGetLastError());
+  return DWH_OK;
+}
+
+// The own eigensolver (dwhmc_eig.hip): H assembled into the slots' JU, reduced
+// to tridiagonal form in place (JU becomes the reflectors V), eigenvalues by
+// bisection into E, eigenvectors of T by inverse iteration (Jmn and U as
+// scratch), then U = V-reflectors · Z by blocked compact-WY zgemms
+int own_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m) {
+  const int N = ctx->d.N, n = 2 * N;
+  const dwh::TrBufs& b = ctx->tr;
+  const int64_t sA = (int64_t)n * n, sZ = 2 * sA;   // sZ in doubles
+  const int T = (n + dwh::kEigTB - 1) / dwh::kEigTB, NB = dwh::kEigNB;
+  const int nblk = std::max(1, (n - 1 + NB - 1) / NB);
+  // back-transform: W = V^H U is only NB x n, so with fewer than 4 matrices
+  // its K range is split into up to KS chunks (one batched zgemm per matrix)
+  constexpr int KS = 8;
+  const int ks = m >= 4 ? 1 : KS;
+  const int64_t sP = (int64_t)T * n, sT = (int64_t)nblk * NB * NB, sW = (int64_t)NB * n, sWs = ks * sW;
+  int rc;
+  if (m > ctx->eig_slots) {
+    HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+    for (void* q : {(void*)ctx->d_eig_part, (void*)ctx->d_eig_vv, (void*)ctx->d_eig_ww, (void*)ctx->d_eig_tau,
+                    (void*)ctx->d_eig_T, (void*)ctx->d_eig_W, (void*)ctx->d_eig_W2, (void*)ctx->d_eig_d,
+                    (void*)ctx->d_eig_e, (void*)ctx->d_eig_tn})
+      drop_alloc(ctx, q);
+    const size_t mm = (size_t)m;
+    if ((rc = dalloc(ctx, &ctx->d_eig_part, mm * sP)) || (rc = dalloc(ctx, &ctx->d_eig_vv, mm * 2 * n)) ||
+        (rc = dalloc(ctx, &ctx->d_eig_ww, mm * n)) || (rc = dalloc(ctx, &ctx->d_eig_tau, mm * n)) ||
+        (rc = dalloc(ctx, &ctx->d_eig_T, mm * sT)) || (rc = dalloc(ctx, &ctx->d_eig_W, mm * std::max<int64_t>(KS * sW, (int64_t)nblk * dwh::kEigGS * NB * NB))) ||
+        (rc = dalloc(ctx, &ctx->d_eig_W2, mm * sW)) || (rc = dalloc(ctx, &ctx->d_eig_d, mm * n)) ||
+        (rc = dalloc(ctx, &ctx->d_eig_e, mm * n)) || (rc = dalloc(ctx, &ctx->d_eig_tn, mm)))
+      return rc;
+    ctx->eig_slots = m;
+  }
+  hipStream_t s = ctx->stream;
+  double2* A = b.JU;
+  if ((rc = assemble_slots(ctx, src, m, A))) return rc;
+  for (int i = 0; i < n; ++i) {
+    dwh::launch_eig_step(A, n, i, sA, ctx->d_eig_part, sP, ctx->d_eig_vv, ctx->d_eig_ww, ctx->d_eig_d,
+                         ctx->d_eig_e, ctx->d_eig_tau, m, s);
+    if (i < n - 1)
+      dwh::launch_eig_pass(A, n, i, sA, ctx->d_eig_part, sP, ctx->d_eig_vv, ctx->d_eig_ww, m, s);
+  }
+  dwh::launch_eig_bisect(ctx->d_eig_d, ctx->d_eig_e, n, b.E, ctx->d_eig_tn, m, s);
+  double* Zt = reinterpret_cast<double*>(b.Jmn);
+  double* Ud = reinterpret_cast<double*>(b.U);
+  dwh::launch_eig_invit(ctx->d_eig_d, ctx->d_eig_e, n, b.E, ctx->d_eig_tn, Zt, Zt + sA, Ud, Ud + sA, sZ,
+                        ctx->d_tr_bad, m, s);
+  // One symmetric (Löwdin) orthogonalisation step over all vectors: with
+  // Y = Z^T (column-major Zt) and G = Y Y^T = I + F, Y <- (3/2 I - 1/2 G) Y
+  // leaves ||F|| -> O(||F||^2).  Outside clusters F_jl ~ c eps ||T|| / |λ_j - λ_l|
+  // (inverse iteration's per-vector error), so the mixing moves each residual
+  // by ~ F_jl |λ_j - λ_l| ~ c eps ||T||: orthogonality to rounding, accuracy kept.
+  double* G = Ud;          // the slots' U buffers (LU scratch until now)
+  double* Y2 = Zt + sA;    // second half of the slots' Jmn buffers
+  {
+    const double one = 1.0, zero = 0.0, mhalf = -0.5, thalf = 1.5;
+    rocblas_status st = rocblas_dgemm_strided_batched(ctx->blas, rocblas_operation_none,
+                                                      rocblas_operation_transpose, n, n, n, &one, Zt, n, sZ, Zt,
+                                                      n, sZ, &zero, G, n, sZ, m);
+    if (st == rocblas_status_success) {
+      HIPCHECK(ctx, hipMemcpy2DAsync(Y2, sZ * sizeof(double), Zt, sZ * sizeof(double), sA * sizeof(double), m,
+                                     hipMemcpyDeviceToDevice, s));
+      st = rocblas_dgemm_strided_batched(ctx->blas, rocblas_operation_none, rocblas_operation_none, n, n, n,
+                                         &mhalf, G, n, sZ, Zt, n, sZ, &thalf, Y2, n, sZ, m);
+    }
+    if (st != rocblas_status_success)
+      return fail(ctx, DWH_ERR_HIP, std::string("rocblas_dgemm (eigenvector orthogonalisation): ") +
+                                        rocblas_status_to_string(st));
+  }
+  dwh::launch_eig_zt_to_u(Y2, b.U, n, sZ, sA, m, s);
+  HIPCHECK(ctx, hipGetLastError());
+  if (n < 2) return DWH_OK;
+  dwh::launch_eig_tfac(A, n, sA, ctx->d_eig_tau, ctx->d_eig_W, ctx->d_eig_T, sT, m, s);   // W as Gram scratch
+  HIPCHECK(ctx, hipGetLastError());
+  // U = (I - V_0 T_0 V_0^H) ... (I - V_last T_last V_last^H) Z, last block first
+  using C = rocblas_double_complex;
+  const C one(1.0, 0.0), zero(0.0, 0.0), mone(-1.0, 0.0);
+  for (int blk = nblk - 1; blk >= 0; --blk) {
+    const int j0 = blk * NB, kb = std::min(NB, n - 1 - j0), ms = n - j0 - 1;
+    const C* Vb = reinterpret_cast<const C*>(A + (j0 + 1) + (int64_t)j0 * n);
+    C* Us = reinterpret_cast<C*>(b.U + (j0 + 1));
+    C* W = reinterpret_cast<C*>(ctx->d_eig_W);
+    C* W2 = reinterpret_cast<C*>(ctx->d_eig_W2);
+    const int ldw = ks * NB;
+    // chunks of c rows (a multiple of 16), the last one shorter
+    const int c = ks == 1 ? ms : std::max(16, ((ms + ks - 1) / ks + 15) / 16 * 16);
+    const int nfull = ms / c, rem = ms - nfull * c, S = nfull + (rem > 0);
+    rocblas_status st = rocblas_status_success;
+    if (ks == 1) {
+      st = rocblas_zgemm_strided_batched(ctx->blas, rocblas_operation_conjugate_transpose, rocblas_operation_none,
+                                         kb, n, ms, &one, Vb, n, sA, Us, n, sA, &zero, W, ldw, sWs, m);
+    } else {
+      for (int k = 0; k < m && st == rocblas_status_success; ++k) {
+        const C* Vk = Vb + k * sA;
+        const C* Uk = Us + k * sA;
+        C* Wk = W + k * sWs;
+        if (nfull > 0)
+          st = rocblas_zgemm_strided_batched(ctx->blas, rocblas_operation_conjugate_transpose,
+                                             rocblas_operation_none, kb, n, c, &one, Vk, n, c, Uk, n, c, &zero, Wk,
+                                             ldw, kb, nfull);
+        if (st == rocblas_status_success && rem > 0)
+          st = rocblas_zgemm(ctx->blas, rocblas_operation_conjugate_transpose, rocblas_operation_none, kb, n, rem,
+                             &one, Vk + (int64_t)nfull * c, n, Uk + (int64_t)nfull * c, n, &zero,
+                             Wk + (int64_t)nfull * kb, ldw);
+      }
+    }
+    if (st == rocblas_status_success) {
+      dwh::launch_eig_tw(ctx->d_eig_T + (int64_t)blk * NB * NB, sT, ctx->d_eig_W, ldw, sWs, S, kb, n,
+                         ctx->d_eig_W2, sW, m, s);
+      st = rocblas_zgemm_strided_batched(ctx->blas, rocblas_operation_none, rocblas_operation_none, ms, n, kb,
+                                         &mone, Vb, n, sA, W2, NB, sW, &one, Us, n, sA, m);
+    }
+    if (st != rocblas_status_success)
+      return fail(ctx, DWH_ERR_HIP, std::string("rocblas_zgemm (eigenvector back-transform): ") +
+                                        rocblas_status_to_string(st));
+  }
+  return DWH_OK;
+}
+
 int eigen_enqueue(dwh_ctx* ctx, const TrSrc& src, int m, bool qr) {
   const int N = ctx->d.N, n2 = 2 * N;
   const dwh::TrBufs& b = ctx->tr;
   const int64_t sA = (int64_t)n2 * n2;
-  HIPCHECK(ctx, hipMemsetAsync(b.U, 0, (size_t)m * sA * sizeof(double2), ctx->stream));
-  for (int k = 0; k < m; ++k)
-    dwh::launch_tr_assemble(b.U + k * sA, N, ctx->hcol,
-                            ctx->hval + (size_t)(src.chain0 + (int64_t)k * src.cstep) * N * kHSlots, ctx->Dcol,
-                            ctx->Dsrc, src.Delta + (size_t)k * src.dstride, ctx->stream);
-  HIPCHECK(ctx, hipGetLastError());
+  if (int rc = assemble_slots(ctx, src, m, b.U)) return rc;
   auto* A = reinterpret_cast<rocblas_double_complex*>(b.U);
   rocblas_status st;
   if (qr)
@@ -2160,15 +2294,29 @@ int eigen_enqueue(dwh_ctx* ctx, const TrSrc& src, int m, bool qr) {
 int eigen_solve(dwh_ctx* ctx, const TrSrc& src, int m) {
   const char* es = std::getenv("DWHMC_EIG_SOLVER");
   const bool qr = es && std::strcmp(es, "ev") == 0;
-  int rc = eigen_enqueue(ctx, src, m, qr);
+  const bool evd = es && std::strcmp(es, "evd") == 0;
+  int rc;
+  HIPCHECK(ctx, hipMemsetAsync(ctx->d_tr_bad, 0, sizeof(int), ctx->stream));
+  if (!qr && !evd && 2 * ctx->d.N <= dwh::kEigMaxN) {
+    // default: the own solver (k_eig_orth flags an over-long cluster in
+    // d_tr_bad); rocSOLVER zheev only if it flagged or produced non-finite values
+    HIPCHECK(ctx, hipMemsetAsync(ctx->d_tr_info, 0, m * sizeof(int), ctx->stream));
+    Scope sc(ctx, T_EIG_OWN, m);
+    rc = own_heev_enqueue(ctx, src, m);
+  } else {
+    Scope sc(ctx, T_EIG_VENDOR, m);
+    rc = eigen_enqueue(ctx, src, m, qr);
+  }
   if (rc || qr) return rc;
   const int64_t n2 = 2 * (int64_t)ctx->d.N;
-  HIPCHECK(ctx, hipMemsetAsync(ctx->d_tr_bad, 0, sizeof(int), ctx->stream));
   dwh::launch_nonfinite(ctx->tr.U, m * n2 * n2, ctx->tr.E, m * n2, ctx->d_tr_bad, ctx->stream);
   int bad = 0;
   HIPCHECK(ctx, hipMemcpyAsync(&bad, ctx->d_tr_bad, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
   HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
-  if (bad) rc = eigen_enqueue(ctx, src, m, true);
+  if (bad) {
+    Scope sc(ctx, T_EIG_VENDOR, m);
+    rc = eigen_enqueue(ctx, src, m, true);
+  }
   return rc;
 }
 

@@ -1,0 +1,740 @@
+// Hermitian eigensolver of the measurement path and of the eig fallback:
+// every eigenpair of m dense n x n H_BdG matrices (column-major, lower
+// triangle referenced), replacing LAPACK's eigen!(Hermitian(H)) of
+// diagonalize_H_BdG! [src/Hamiltonian.jl:96-114] as measure_transport_and_spectra
+// [src/Observables.jl:314-526] and the eig path use it.  No vendor solver:
+//
+//  1. Householder tridiagonalisation, LAPACK zhetd2 'L' algebra (reflectors
+//     H_i = I - tau_i v_i v_i^H, v_i[i+1] = 1, beta_i real so T is real
+//     symmetric).  Two launches per column, both batched over the m matrices:
+//       k_eig_step  (one workgroup per matrix): reduces the previous pass's
+//                   hemv partials to p = A v_{i-1}, forms w_{i-1} = tau p -
+//                   1/2 tau (tau p)^H v v, applies the deferred rank-2 update
+//                   to column i only and generates the reflector of column i
+//                   (zlarfg); column i of A becomes v_i (zeros above i+1), so
+//                   A ends as the dense V the back-transform multiplies by.
+//       k_eig_pass  (one workgroup per 64 x 64 lower-triangle tile of the
+//                   trailing matrix): applies the deferred update of column
+//                   i-1 to the tile and accumulates the tile's share of
+//                   A v_i in the same sweep: one read + write of the trailing
+//                   triangle per column (HBM-bound; early columns ~67 MB per
+//                   matrix at n = 2048), partials written once per slot and
+//                   summed in a fixed order (bit-reproducible).
+//  2. k_eig_bisect: every eigenvalue of T on Sturm counts, one wave per
+//     eigenvalue index, 64-section per round down to the last bit.
+//  3. k_eig_invit: inverse iteration, T - lambda I = LU with partial pivoting
+//     streamed per thread (two solves from a fixed pseudo-random start,
+//     one thread per eigenvalue); k_eig_orth: the vectors of eigenvalue
+//     clusters (consecutive gaps <= 2.5e-4 ||T||, so every other pair is
+//     orthogonal to ~1e-12 already) orthonormalised by Cholesky QR, twice
+//     (exact degeneracies of clean lattices included).
+//     Then one symmetric orthogonalisation step over all vectors (rocBLAS
+//     dgemm, dwhmc_api.cpp).
+//  4. U = H_0 H_1 ... H_{n-2} Z: reflectors in blocks of kEigNB as
+//     I - V T V^H (k_eig_tfac: compact-WY T per block), applied last block
+//     first: W = V^H U by rocBLAS zgemm (split over K into chunks when few
+//     matrices are batched, its output being only kEigNB x n), W2 = T sum of
+//     the chunks (k_eig_tw), U -= V W2 by rocBLAS zgemm.
+//
+// The numpy prototype with the same operation order: tools/eig_proto.py.
+#include <cfloat>
+
+#include "dwhmc_device.h"
+#include "dwhmc_internal.h"
+
+namespace dwh {
+namespace {
+
+constexpr int kStepT = 1024;   // threads of k_eig_step
+constexpr int kMaxR = kEigMaxN / kStepT;   // rows per k_eig_step thread
+
+// sums over the workgroup (fixed order: xor-shuffle tree per wave, then the
+// waves in index order); every thread returns the totals.  sh: one slot per
+// wave and value, not shared with another reduction of the same phase.
+__device__ __forceinline__ double group_sum(double v, double* sh) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if ((threadIdx.x & 63) == 0) sh[w] = v;
+  __syncthreads();
+  double s = 0.0;
+  for (int k = 0; k < nw; ++k) s += sh[k];
+  return s;
+}
+__device__ __forceinline__ double2 group_sum2(double2 v, double2* sh) {
+  v.x = wave_sum(v.x);
+  v.y = wave_sum(v.y);
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if ((threadIdx.x & 63) == 0) sh[w] = v;
+  __syncthreads();
+  double2 s = make_double2(0.0, 0.0);
+  for (int k = 0; k < nw; ++k) {
+    s.x += sh[k].x;
+    s.y += sh[k].y;
+  }
+  return s;
+}
+
+__device__ __forceinline__ double2 cz() { return make_double2(0.0, 0.0); }
+
+// sum over Y in [t0, T) of part[Y n + r], ascending Y, eight loads in flight
+__device__ __forceinline__ double2 sum_partials(const double2* __restrict__ part, int n, int r, int t0, int T) {
+  double2 p = cz();
+  for (int Y0 = t0; Y0 < T; Y0 += 8) {
+    double2 q[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) q[u] = Y0 + u < T ? part[(int64_t)(Y0 + u) * n + r] : cz();
+#pragma unroll
+    for (int u = 0; u < 8; ++u) p = cadd(p, q[u]);
+  }
+  return p;
+}
+
+// Every load of the step is issued up front (column i, v_{i-1}, the pass
+// partials of this thread's rows and of row i): two workgroup reductions
+// (x^H v, then the reflector norm) are its only barriers.
+__global__ __launch_bounds__(kStepT) void k_eig_step(double2* __restrict__ A, int n, int i, int64_t sA,
+                                                     const double2* __restrict__ part, int64_t sP,
+                                                     double2* __restrict__ vv, double2* __restrict__ ww,
+                                                     double* __restrict__ d, double* __restrict__ e,
+                                                     double2* __restrict__ tau) {
+  const int k = blockIdx.x, tid = threadIdx.x;
+  A += k * sA;
+  part += k * sP;
+  vv += (int64_t)k * 2 * n;
+  ww += (int64_t)k * n;
+  d += (int64_t)k * n;
+  e += (int64_t)k * n;
+  tau += (int64_t)k * n;
+  __shared__ double2 sh1[kStepT / 64];
+  __shared__ double sh2[kStepT / 64];
+  __shared__ double2 bc;
+  double2* vcur = vv + (int64_t)(i & 1) * n;
+  const double2* vprv = vv + (int64_t)((i & 1) ^ 1) * n;
+  const int t0 = i / kEigTB, T = (n + kEigTB - 1) / kEigTB;
+  double2 cr[kMaxR], vp[kMaxR], wr[kMaxR];
+#pragma unroll
+  for (int s = 0; s < kMaxR; ++s) {
+    const int r = i + tid + s * kStepT;
+    cr[s] = vp[s] = wr[s] = cz();
+    if (r < n) {
+      cr[s] = A[r + (int64_t)i * n];
+      if (i > 0) {
+        vp[s] = vprv[r];
+        wr[s] = sum_partials(part, n, r, t0, T);
+      }
+    }
+  }
+  double2 wi = cz();
+  if (i > 0) {
+    // p = A^{(i-1)} v_{i-1}; x = tau p; w = x - 1/2 tau (x^H v) v  (zhetd2 'L')
+    const double2 tp = tau[i - 1];
+    // p[i], every thread (v_{i-1}[i] = 1: w[i] = x[i] + alpha)
+    const double2 pi = sum_partials(part, n, i, t0, T);
+    double2 g = cz();
+#pragma unroll
+    for (int s = 0; s < kMaxR; ++s) {
+      wr[s] = cmul(tp, wr[s]);
+      g.x += wr[s].x * vp[s].x + wr[s].y * vp[s].y;
+      g.y += wr[s].x * vp[s].y - wr[s].y * vp[s].x;
+    }
+    g = group_sum2(g, sh1);
+    const double2 al = cmul(tp, make_double2(-0.5 * g.x, -0.5 * g.y));
+    wi = cadd(cmul(tp, pi), al);
+#pragma unroll
+    for (int s = 0; s < kMaxR; ++s) {
+      const int r = i + tid + s * kStepT;
+      wr[s] = cadd(wr[s], cmul(al, vp[s]));
+      if (r < n) ww[r] = wr[s];
+    }
+  }
+  // column i with the deferred update of column i-1 (v_{i-1}[i] = 1)
+  double xn = 0.0;
+#pragma unroll
+  for (int s = 0; s < kMaxR; ++s) {
+    const int r = i + tid + s * kStepT;
+    if (r < n) {
+      double2 c = cr[s];
+      if (i > 0) c = csub(csub(c, cmulc(vp[s], wi)), wr[s]);
+      cr[s] = c;
+      if (r >= i + 2) xn += c.x * c.x + c.y * c.y;
+      if (r == i) d[i] = c.x;
+      if (r == i + 1) bc = c;
+    }
+  }
+  if (i == n - 1) return;
+  xn = group_sum(xn, sh2);   // its barrier publishes bc
+  const double2 al = bc;
+  // zlarfg: beta = -sign(Re alpha) ||(alpha, x)||, tau = (beta - alpha) / beta, v = x / (alpha - beta)
+  double2 t = cz(), sc = cz();
+  double beta = al.x;
+  if (!(xn == 0.0 && al.y == 0.0)) {
+    beta = -copysign(sqrt(al.x * al.x + al.y * al.y + xn), al.x);
+    t = make_double2((beta - al.x) / beta, -al.y / beta);
+    sc = cinv(make_double2(al.x - beta, al.y));
+  }
+#pragma unroll
+  for (int s = 0; s < kMaxR; ++s) {
+    const int r = i + tid + s * kStepT;
+    if (r >= i + 1 && r < n) {
+      const double2 v = r == i + 1 ? make_double2(1.0, 0.0) : cmul(cr[s], sc);
+      vcur[r] = v;
+      A[r + (int64_t)i * n] = v;
+    }
+  }
+  for (int r = tid; r <= i; r += kStepT) A[r + (int64_t)i * n] = cz();
+  if (tid == 0) {
+    e[i] = beta;
+    tau[i] = t;
+  }
+}
+
+// tile (R, C), R >= C, of the trailing lower triangle [t0, T)^2 from a linear index
+__device__ __forceinline__ void tri_decode(int b, int& R, int& C) {
+  int r = (int)((sqrt(8.0 * b + 1.0) - 1.0) * 0.5);
+  while ((r + 1) * (r + 2) / 2 <= b) ++r;
+  while (r * (r + 1) / 2 > b) --r;
+  R = r;
+  C = b - r * (r + 1) / 2;
+}
+
+__global__ __launch_bounds__(256) void k_eig_pass(double2* __restrict__ A, int n, int i, int64_t sA,
+                                                  double2* __restrict__ part, int64_t sP,
+                                                  const double2* __restrict__ vv, const double2* __restrict__ ww,
+                                                  int t0) {
+  const int k = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  A += k * sA;
+  part += k * sP;
+  vv += (int64_t)k * 2 * n;
+  ww += (int64_t)k * n;
+  const double2* v = vv + (int64_t)(i & 1) * n;
+  const double2* vp = vv + (int64_t)((i & 1) ^ 1) * n;
+  const bool pend = i > 0;
+  int R, C;
+  tri_decode(blockIdx.x, R, C);
+  R += t0;
+  C += t0;
+  __shared__ double2 cv[64], cvp[64], cwp[64], csum[64];
+  __shared__ double2 colc[64][65];
+  __shared__ double2 rowp[4][64];
+  if (tid < 64) {
+    const int gc = C * kEigTB + tid;
+    const bool ok = gc >= i + 1 && gc < n;
+    cv[tid] = ok ? v[gc] : cz();
+    cvp[tid] = ok && pend ? vp[gc] : cz();
+    cwp[tid] = ok && pend ? ww[gc] : cz();
+  }
+  const int gr = R * kEigTB + lane;
+  const bool rok = gr >= i + 1 && gr < n;
+  const double2 vr = rok ? v[gr] : cz();
+  const double2 vpr = rok && pend ? vp[gr] : cz();
+  const double2 wpr = rok && pend ? ww[gr] : cz();
+  __syncthreads();
+  double2 pr = cz();
+  constexpr int NCW = kEigTB / 4;   // columns per wave
+  double2 a[NCW];
+  unsigned act = 0;
+#pragma unroll
+  for (int u = 0; u < NCW; ++u) {
+    const int gc = C * kEigTB + w + 4 * u;
+    const bool ok = rok && gc >= i + 1 && gr >= gc;
+    act |= (unsigned)ok << u;
+    a[u] = ok ? A[gr + (int64_t)gc * n] : cz();
+  }
+#pragma unroll
+  for (int u = 0; u < NCW; ++u) {
+    const int cc = w + 4 * u, gc = C * kEigTB + cc;
+    double2 t = cz();
+    if ((act >> u) & 1) {
+      if (pend) {
+        a[u] = csub(csub(a[u], cmulc(vpr, cwp[cc])), cmulc(wpr, cvp[cc]));
+        A[gr + (int64_t)gc * n] = a[u];
+      }
+      pr = cadd(pr, cmul(a[u], cv[cc]));
+      if (gr > gc) t = make_double2(a[u].x * vr.x + a[u].y * vr.y, a[u].x * vr.y - a[u].y * vr.x);   // conj(a) v_r
+    }
+    colc[cc][lane] = t;
+  }
+  rowp[w][lane] = pr;
+  __syncthreads();
+  {
+    const int cc = tid >> 2, q = tid & 3;
+    double2 s = cz();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s = cadd(s, colc[cc][q * 16 + r]);
+    s.x += __shfl_xor(s.x, 1, 64);
+    s.y += __shfl_xor(s.y, 1, 64);
+    s.x += __shfl_xor(s.x, 2, 64);
+    s.y += __shfl_xor(s.y, 2, 64);
+    if (q == 0) csum[cc] = s;
+  }
+  __syncthreads();
+  if (tid < 64) {
+    const double2 rs = cadd(cadd(rowp[0][tid], rowp[1][tid]), cadd(rowp[2][tid], rowp[3][tid]));
+    const double2 cs = csum[tid];
+    const int r = R * kEigTB + tid, c = C * kEigTB + tid;
+    if (R == C) {
+      if (r < n) part[(int64_t)R * n + r] = cadd(rs, cs);
+    } else {
+      if (r < n) part[(int64_t)C * n + r] = rs;
+      if (c < n) part[(int64_t)R * n + c] = cs;
+    }
+  }
+}
+
+// Gershgorin interval of T (lo, hi), ||T|| bound and max e^2 over the workgroup
+__device__ void gersh(const double* __restrict__ d, const double* __restrict__ e, int n, double* sh, double& lo,
+                      double& hi, double& emax) {
+  double a = DBL_MAX, b = -DBL_MAX, c = 0.0;
+  for (int r = threadIdx.x; r < n; r += blockDim.x) {
+    const double er = r < n - 1 ? e[r] : 0.0, el = r > 0 ? e[r - 1] : 0.0;
+    const double rad = fabs(er) + fabs(el);
+    a = fmin(a, d[r] - rad);
+    b = fmax(b, d[r] + rad);
+    c = fmax(c, er * er);
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    a = fmin(a, __shfl_xor(a, off, 64));
+    b = fmax(b, __shfl_xor(b, off, 64));
+    c = fmax(c, __shfl_xor(c, off, 64));
+  }
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) {
+    sh[3 * w] = a;
+    sh[3 * w + 1] = b;
+    sh[3 * w + 2] = c;
+  }
+  __syncthreads();
+  lo = DBL_MAX;
+  hi = -DBL_MAX;
+  emax = 0.0;
+  for (int k = 0; k < nw; ++k) {
+    lo = fmin(lo, sh[3 * k]);
+    hi = fmax(hi, sh[3 * k + 1]);
+    emax = fmax(emax, sh[3 * k + 2]);
+  }
+}
+
+// One wave per eigenvalue index j: 64-section of [lo, hi] per round (lane l
+// counts at lo + (l+1)(hi-lo)/65; the counts are monotone in l, so a ballot
+// finds the sub-interval holding eigenvalue j), ~9 rounds to the last bit
+// instead of ~53 bisection steps.  Sturm count: the dstebz recurrence with
+// d and e^2 broadcast from LDS and 1/q by v_rcp_f64 + two Newton steps.
+constexpr int kBisW = 8;   // waves (eigenvalues) per workgroup
+__global__ __launch_bounds__(64 * kBisW) void k_eig_bisect(const double* __restrict__ d,
+                                                           const double* __restrict__ e, int n,
+                                                           double* __restrict__ E, double* __restrict__ tnorm) {
+  extern __shared__ double lds[];   // d[0, n), e^2[n, 2n)
+  const int k = blockIdx.y, lane = threadIdx.x & 63;
+  d += (int64_t)k * n;
+  e += (int64_t)k * n;
+  E += (int64_t)k * n;
+  __shared__ double sh[3 * kBisW];
+  for (int r = threadIdx.x; r < n; r += blockDim.x) {
+    lds[r] = d[r];
+    const double er = r < n - 1 ? e[r] : 0.0;
+    lds[n + r] = er * er;
+  }
+  double gl, gu, emax;
+  gersh(d, e, n, sh, gl, gu, emax);   // its barriers publish the LDS copies
+  const double tn = fmax(fabs(gl), fabs(gu));
+  if (blockIdx.x == 0 && threadIdx.x == 0) tnorm[k] = tn;
+  gl -= 2.0 * DBL_EPSILON * tn * n + 1e-300;
+  gu += 2.0 * DBL_EPSILON * tn * n + 1e-300;
+  const double pivmin = DBL_MIN * fmax(1.0, emax);
+  const int j = blockIdx.x * kBisW + (threadIdx.x >> 6);
+  if (j >= n) return;
+  const double* ld = lds;
+  const double* le2 = lds + n;
+  double lo = gl, hi = gu;
+  for (int it = 0; it < 64; ++it) {
+    const double mid = 0.5 * (lo + hi);
+    if (mid <= lo || mid >= hi) break;
+    const double x = fmin(lo + (lane + 1) * ((hi - lo) * (1.0 / 65.0)), hi);
+    double q = ld[0] - x;
+    if (fabs(q) < pivmin) q = -pivmin;
+    int c = q < 0.0;
+#pragma unroll 8
+    for (int r = 1; r < n; ++r) {
+      q = (ld[r] - x) - le2[r - 1] * rcp_nr(q);
+      if (fabs(q) < pivmin) q = -pivmin;
+      c += q < 0.0;
+    }
+    // first lane whose count exceeds j: eigenvalue j lies in (x_{f-1}, x_f]
+    const unsigned long long above = __ballot(c > j);
+    const int f = above ? __builtin_ctzll(above) : 64;
+    const double xf = __shfl(x, f < 64 ? f : 63, 64), xp = __shfl(x, f > 0 ? f - 1 : 0, 64);
+    const double nlo = f > 0 ? xp : lo, nhi = f < 64 ? xf : hi;
+    if (nlo == lo && nhi == hi) break;
+    lo = nlo;
+    hi = nhi;
+  }
+  if (lane == 0) E[j] = 0.5 * (lo + hi);
+}
+
+// start vector entry r of eigenvalue m: splitmix64 of (m, r) in [-1/2, 1/2)
+// (independent-looking starts: the vectors of a degenerate level are the
+// starts' projections onto its eigenspace, so correlated starts would leave
+// them nearly dependent)
+__device__ __forceinline__ double start_entry(int m, int r) {
+  unsigned long long z = ((unsigned long long)(unsigned)m << 32 | (unsigned)r) + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (double)(z >> 11) * 0x1.0p-53 - 0.5;
+}
+
+__device__ __forceinline__ double clamp_small(double x, double small) {
+  return fabs(x) < small ? (x != 0.0 ? copysign(small, x) : small) : x;
+}
+
+// inverse iteration for eigenvalue m (vector: column m of Zt, Zt[r n + m];
+// LU scratch: columns m of U0/U1/U2, U0 holding the reciprocal pivots): two
+// solves with T - lam I from a fixed pseudo-random start (lam is accurate to
+// a few ulps of ||T||, so one solve already leaves neighbours at ~ulp / gap),
+// normalised
+__device__ void invit_one(const double* __restrict__ d, const double* __restrict__ e, int n, double lam, int m,
+                          double small, double* __restrict__ Zt, double* __restrict__ U0, double* __restrict__ U1,
+                          double* __restrict__ U2) {
+  double* x = Zt + m;
+  double* u0 = U0 + m;
+  double* u1 = U1 + m;
+  double* u2 = U2 + m;
+  const int64_t ld = n;
+  double scale = 1.0;
+  for (int it = 0; it < 2; ++it) {
+    const bool first = it == 0;
+    // forward: factor T - lam I (row interchanges) and eliminate y in one sweep
+    double cu0 = d[0] - lam, cu1 = n > 1 ? e[0] : 0.0;
+    double yk = first ? start_entry(m, 0) : x[0] * scale;
+#pragma unroll 8
+    for (int r = 0; r < n - 1; ++r) {
+      const double b = e[r], nd = d[r + 1] - lam, ne = r + 1 < n - 1 ? e[r + 1] : 0.0;
+      const double yk1 = first ? start_entry(m, r + 1) : x[(r + 1) * ld] * scale;
+      if (fabs(cu0) >= fabs(b)) {
+        if (cu0 == 0.0) cu0 = small;
+        const double mu = b / cu0;
+        u0[r * ld] = 1.0 / clamp_small(cu0, small);
+        u1[r * ld] = cu1;
+        u2[r * ld] = 0.0;
+        x[r * ld] = yk;
+        cu0 = nd - mu * cu1;
+        cu1 = ne;
+        yk = yk1 - mu * yk;
+      } else {
+        const double mu = cu0 / b;
+        u0[r * ld] = 1.0 / clamp_small(b, small);
+        u1[r * ld] = nd;
+        u2[r * ld] = ne;
+        x[r * ld] = yk1;
+        cu0 = cu1 - mu * nd;
+        cu1 = -mu * ne;
+        yk = yk - mu * yk1;
+      }
+    }
+    u0[(n - 1) * ld] = 1.0 / clamp_small(cu0, small);
+    u1[(n - 1) * ld] = 0.0;
+    u2[(n - 1) * ld] = 0.0;
+    x[(n - 1) * ld] = yk;
+    // backward substitution
+    double x1 = 0.0, x2 = 0.0, nrm = 0.0;
+#pragma unroll 8
+    for (int r = n - 1; r >= 0; --r) {
+      const double xr = (x[r * ld] - u1[r * ld] * x1 - u2[r * ld] * x2) * u0[r * ld];
+      x[r * ld] = xr;
+      x2 = x1;
+      x1 = xr;
+      nrm += xr * xr;
+    }
+    scale = 1.0 / sqrt(nrm);
+  }
+#pragma unroll 8
+  for (int r = 0; r < n; ++r) x[r * ld] *= scale;
+}
+
+__global__ __launch_bounds__(64) void k_eig_invit(const double* __restrict__ d, const double* __restrict__ e,
+                                                  int n, const double* __restrict__ E,
+                                                  const double* __restrict__ tnorm, double* __restrict__ Zt,
+                                                  double* __restrict__ U0, double* __restrict__ U1,
+                                                  double* __restrict__ U2, int64_t sZ) {
+  const int k = blockIdx.y;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const double tn = tnorm[k];
+  const double small = tn > 0.0 ? DBL_EPSILON * tn : DBL_EPSILON;
+  invit_one(d + (int64_t)k * n, e + (int64_t)k * n, n, E[(int64_t)k * n + j], j, small, Zt + k * sZ,
+            U0 + k * sZ, U1 + k * sZ, U2 + k * sZ);
+}
+
+// Clusters (runs of eigenvalues with consecutive gaps <= ctol ||T||, up to
+// kEigMaxCluster long) get their inverse-iteration vectors orthonormalised:
+// two rounds of Cholesky QR on the cluster's columns of Zt (G = Z^T Z = L L^T,
+// Z <- Z L^-T; the rows of a cluster are contiguous in Zt).  Vectors of
+// separated eigenvalues are orthogonal to ~2 eps ||T|| / gap already; inside a
+// cluster the rotation is O(that) for distinct eigenvalues, and an orthonormal
+// basis of the eigenspace for exactly degenerate ones.  One workgroup per
+// candidate first index; *bad = 1 when a cluster is too long or G is not
+// positive definite (the caller then re-solves with rocSOLVER's zheev).
+__global__ __launch_bounds__(256) void k_eig_orth(const double* __restrict__ E, const double* __restrict__ tnorm,
+                                                  int n, double* __restrict__ Zt, int64_t sZ, double ctol,
+                                                  int* __restrict__ bad) {
+  constexpr int MC = kEigMaxCluster;
+  const int k = blockIdx.y, j = blockIdx.x, tid = threadIdx.x;
+  E += (int64_t)k * n;
+  Zt += k * sZ;
+  const double tol = ctol * tnorm[k];
+  if (j > 0 && E[j] - E[j - 1] <= tol) return;
+  int end = j + 1;
+  while (end < n && end - j <= MC && E[end] - E[end - 1] <= tol) ++end;
+  const int kc = end - j;
+  if (kc == 1) return;
+  if (kc > MC) {
+    if (tid == 0) *bad = 1;
+    return;
+  }
+  constexpr int RC = 16;   // rows per LDS chunk of the Gram sums
+  __shared__ double G[MC][MC + 1];
+  __shared__ double Zs[RC][MC + 1];
+  __shared__ int fail;
+  for (int round = 0; round < 2; ++round) {
+    // G = Z_c^T Z_c (lower triangle): rows staged RC at a time in LDS, each
+    // thread accumulating its pairs over the rows in order
+    constexpr int NPT = (MC * (MC + 1) / 2 + 255) / 256;
+    const int npair = kc * (kc + 1) / 2;
+    double acc[NPT];
+#pragma unroll
+    for (int u = 0; u < NPT; ++u) acc[u] = 0.0;
+    for (int r0 = 0; r0 < n; r0 += RC) {
+      for (int q = tid; q < RC * kc; q += 256) {
+        const int rr = q / kc, c = q % kc, r = r0 + rr;
+        Zs[rr][c] = r < n ? Zt[(int64_t)r * n + j + c] : 0.0;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < NPT; ++u) {
+        const int pq = tid + 256 * u;
+        if (pq < npair) {
+          int p = (int)((sqrt(8.0 * pq + 1.0) - 1.0) * 0.5);
+          while ((p + 1) * (p + 2) / 2 <= pq) ++p;
+          while (p * (p + 1) / 2 > pq) --p;
+          const int q = pq - p * (p + 1) / 2;
+          double a = acc[u];
+          for (int rr = 0; rr < RC; ++rr) a += Zs[rr][p] * Zs[rr][q];
+          acc[u] = a;
+        }
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int u = 0; u < NPT; ++u) {
+      const int pq = tid + 256 * u;
+      if (pq < npair) {
+        int p = (int)((sqrt(8.0 * pq + 1.0) - 1.0) * 0.5);
+        while ((p + 1) * (p + 2) / 2 <= pq) ++p;
+        while (p * (p + 1) / 2 > pq) --p;
+        G[p][pq - p * (p + 1) / 2] = acc[u];
+      }
+    }
+    if (tid == 0) fail = 0;
+    __syncthreads();
+    // Cholesky, right-looking, in place (lower)
+    for (int c = 0; c < kc; ++c) {
+      if (tid == 0) {
+        // the columns are normalised: a pivot this small means cond(Z) > ~1e7,
+        // beyond what two rounds of Cholesky QR repair
+        const double g = G[c][c];
+        if (!(g > 1e-14)) fail = 1;
+        G[c][c] = sqrt(fmax(g, DBL_MIN));
+      }
+      __syncthreads();
+      for (int r = c + 1 + tid; r < kc; r += 256) G[r][c] /= G[c][c];
+      __syncthreads();
+      for (int pq = tid; pq < kc * kc; pq += 256) {
+        const int p = pq / kc, q = pq % kc;
+        if (q > c && p >= q) G[p][q] -= G[p][c] * G[q][c];
+      }
+      __syncthreads();
+    }
+    if (fail) {
+      if (tid == 0) *bad = 1;
+      return;
+    }
+    // each row z (1 x kc) <- z L^-T: forward substitution L x = z^T
+    for (int r = tid; r < n; r += 256) {
+      double* z = Zt + (int64_t)r * n + j;
+      for (int p = 0; p < kc; ++p) {
+        double s = z[p];
+        for (int q = 0; q < p; ++q) s -= G[p][q] * z[q];
+        z[p] = s / G[p][p];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// U[r + c n] = (Zt[r n + c], 0), through a 64 x 64 LDS tile
+__global__ __launch_bounds__(256) void k_eig_zt_to_u(const double* __restrict__ Zt, double2* __restrict__ U, int n,
+                                                     int64_t sZ, int64_t sA) {
+  const int k = blockIdx.z;
+  Zt += k * sZ;
+  U += k * sA;
+  __shared__ double t[64][65];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  for (int q = threadIdx.x; q < 64 * 64; q += 256) {
+    const int rr = q >> 6, cc = q & 63;   // read row r0+rr of Zt: columns c0+cc contiguous
+    const int r = r0 + rr, c = c0 + cc;
+    t[rr][cc] = (r < n && c < n) ? Zt[(int64_t)r * n + c] : 0.0;
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < 64 * 64; q += 256) {
+    const int cc = q >> 6, rr = q & 63;   // write column c0+cc of U: rows r0+rr contiguous
+    const int r = r0 + rr, c = c0 + cc;
+    if (r < n && c < n) U[r + (int64_t)c * n] = make_double2(t[rr][cc], 0.0);
+  }
+}
+
+// compact-WY T of reflector block b (columns j0 .. j0+kb-1 of V, rows j0+1 ..):
+// G = V^H V, T[j][j] = tau_j, T[0:j, j] = -tau_j T[0:j, 0:j] G[0:j, j].
+// k_eig_tgram: partial G of row slice g (kEigGS slices per block, so the
+// blocks' Gram sums fill the chip); k_eig_tfac: the slices summed in order,
+// then the recurrence.
+__global__ __launch_bounds__(256) void k_eig_tgram(const double2* __restrict__ V, int n, int64_t sA,
+                                                   double2* __restrict__ Gp) {
+  constexpr int NB = kEigNB;
+  const int blk = blockIdx.x, g = blockIdx.y, k = blockIdx.z, tid = threadIdx.x;
+  const int nblk = gridDim.x;
+  const int j0 = blk * NB, kb = min(NB, n - 1 - j0), ms = n - 1 - j0;
+  const int rc = ((ms + kEigGS - 1) / kEigGS + NB - 1) / NB * NB;
+  const int rb = j0 + 1 + g * rc, re = min(n, rb + rc);
+  V += k * sA;
+  Gp += (((int64_t)k * nblk + blk) * kEigGS + g) * NB * NB;
+  __shared__ double2 S[NB][NB + 1];
+  double2 acc[NB * NB / 256];
+#pragma unroll
+  for (int u = 0; u < NB * NB / 256; ++u) acc[u] = cz();
+  for (int r0 = rb; r0 < re; r0 += NB) {
+    for (int q = tid; q < NB * NB; q += 256) {
+      const int cc = q / NB, rr = q % NB, r = r0 + rr;
+      S[rr][cc] = (r < re && cc < kb) ? V[r + (int64_t)(j0 + cc) * n] : cz();
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < NB * NB / 256; ++u) {
+      const int pq = tid + 256 * u, p = pq / NB, q = pq % NB;
+      double2 a = acc[u];
+      for (int rr = 0; rr < NB; ++rr) {
+        const double2 x = S[rr][p], y = S[rr][q];   // conj(x) y
+        a.x += x.x * y.x + x.y * y.y;
+        a.y += x.x * y.y - x.y * y.x;
+      }
+      acc[u] = a;
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int u = 0; u < NB * NB / 256; ++u) Gp[tid + 256 * u] = acc[u];
+}
+
+__global__ __launch_bounds__(256) void k_eig_tfac(const double2* __restrict__ Gp, int n,
+                                                  const double2* __restrict__ tau, double2* __restrict__ Tb,
+                                                  int64_t sT) {
+  constexpr int NB = kEigNB;
+  const int blk = blockIdx.x, k = blockIdx.y, tid = threadIdx.x, nblk = gridDim.x;
+  const int j0 = blk * NB, kb = min(NB, n - 1 - j0);
+  tau += (int64_t)k * n;
+  Tb += k * sT + (int64_t)blk * NB * NB;
+  Gp += ((int64_t)k * nblk + blk) * kEigGS * NB * NB;
+  __shared__ double2 G[NB][NB + 1];
+  __shared__ double2 S[NB][NB + 1];   // T
+  for (int pq = tid; pq < NB * NB; pq += 256) {
+    double2 a = cz();
+    for (int g = 0; g < kEigGS; ++g) a = cadd(a, Gp[(int64_t)g * NB * NB + pq]);
+    G[pq / NB][pq % NB] = a;
+  }
+  for (int q = tid; q < NB * NB; q += 256) S[q / NB][q % NB] = cz();
+  __syncthreads();
+  for (int j = 0; j < kb; ++j) {
+    const double2 tj = tau[j0 + j];
+    double2 s = cz();
+    if (tid < j) {
+      for (int q = tid; q < j; ++q) s = cadd(s, cmul(S[tid][q], G[q][j]));
+    }
+    __syncthreads();
+    if (tid < j) S[tid][j] = cmul(make_double2(-tj.x, -tj.y), s);
+    if (tid == j) S[j][j] = tj;
+    __syncthreads();
+  }
+  for (int q = tid; q < NB * NB; q += 256) {
+    const int p = q % NB, c = q / NB;
+    Tb[p + (int64_t)c * NB] = S[p][c];
+  }
+}
+
+// W2 = T (sum over the S K-chunks of W): T kb x kb (ld kEigNB), chunk s of W
+// at rows s kb (ld ldw); one thread per output entry
+__global__ __launch_bounds__(256) void k_eig_tw(const double2* __restrict__ Tb, int64_t sT,
+                                                const double2* __restrict__ W, int ldw, int64_t sW, int S, int kb,
+                                                int n, double2* __restrict__ W2, int64_t sW2) {
+  __shared__ double2 Ts[kEigNB][kEigNB + 1];
+  const int k = blockIdx.y, p = threadIdx.x & 63, w = threadIdx.x >> 6;
+  Tb += k * sT;
+  for (int q = threadIdx.x; q < kEigNB * kEigNB; q += 256) Ts[q % kEigNB][q / kEigNB] = Tb[q];
+  __syncthreads();
+  // 4 waves x 4 columns each
+  for (int cj = 0; cj < 4; ++cj) {
+    const int col = blockIdx.x * 16 + w * 4 + cj;
+    if (col >= n) break;
+    const double2* Wc = W + k * sW + (int64_t)col * ldw;
+    double2 acc = cz();
+    for (int s = 0; s < S; ++s) {
+#pragma unroll 8
+      for (int q = 0; q < kb; ++q) acc = cadd(acc, cmul(Ts[p][q], Wc[s * kb + q]));
+    }
+    if (p < kb) W2[k * sW2 + p + (int64_t)col * kEigNB] = acc;
+  }
+}
+
+}  // namespace
+
+void launch_eig_step(double2* A, int n, int i, int64_t sA, const double2* part, int64_t sP, double2* vv,
+                     double2* ww, double* d, double* e, double2* tau, int m, hipStream_t s) {
+  hipLaunchKernelGGL(k_eig_step, dim3(m), dim3(kStepT), 0, s, A, n, i, sA, part, sP, vv, ww, d, e, tau);
+}
+
+void launch_eig_pass(double2* A, int n, int i, int64_t sA, double2* part, int64_t sP, const double2* vv,
+                     const double2* ww, int m, hipStream_t s) {
+  const int T = (n + kEigTB - 1) / kEigTB, t0 = (i + 1) / kEigTB, nT = T - t0;
+  if (nT <= 0) return;
+  hipLaunchKernelGGL(k_eig_pass, dim3(nT * (nT + 1) / 2, m), dim3(256), 0, s, A, n, i, sA, part, sP, vv, ww, t0);
+}
+
+void launch_eig_bisect(const double* d, const double* e, int n, double* E, double* tnorm, int m, hipStream_t s) {
+  hipLaunchKernelGGL(k_eig_bisect, dim3((n + kBisW - 1) / kBisW, m), dim3(64 * kBisW), 2 * n * sizeof(double), s, d, e,
+                     n, E, tnorm);
+}
+
+void launch_eig_invit(const double* d, const double* e, int n, const double* E, const double* tnorm, double* Zt,
+                      double* U0, double* U1, double* U2, int64_t sZ, int* bad, int m, hipStream_t s) {
+  hipLaunchKernelGGL(k_eig_invit, dim3((n + 63) / 64, m), dim3(64), 0, s, d, e, n, E, tnorm, Zt, U0, U1, U2, sZ);
+  hipLaunchKernelGGL(k_eig_orth, dim3(n, m), dim3(256), 0, s, E, tnorm, n, Zt, sZ, kEigClusterTol, bad);
+}
+
+void launch_eig_zt_to_u(const double* Zt, double2* U, int n, int64_t sZ, int64_t sA, int m, hipStream_t s) {
+  const int T = (n + 63) / 64;
+  hipLaunchKernelGGL(k_eig_zt_to_u, dim3(T, T, m), dim3(256), 0, s, Zt, U, n, sZ, sA);
+}
+
+void launch_eig_tfac(const double2* V, int n, int64_t sA, const double2* tau, double2* Gp, double2* Tb, int64_t sT,
+                     int m, hipStream_t s) {
+  const int nblk = (n - 1 + kEigNB - 1) / kEigNB;
+  if (nblk <= 0) return;
+  hipLaunchKernelGGL(k_eig_tgram, dim3(nblk, kEigGS, m), dim3(256), 0, s, V, n, sA, Gp);
+  hipLaunchKernelGGL(k_eig_tfac, dim3(nblk, m), dim3(256), 0, s, Gp, n, tau, Tb, sT);
+}
+
+void launch_eig_tw(const double2* Tb, int64_t sT, const double2* W, int ldw, int64_t sW, int S, int kb, int n,
+                   double2* W2, int64_t sW2, int m, hipStream_t s) {
+  hipLaunchKernelGGL(k_eig_tw, dim3((n + 15) / 16, m), dim3(256), 0, s, Tb, sT, W, ldw, sW, S, kb, n, W2, sW2);
+}
+
+}  // namespace dwh

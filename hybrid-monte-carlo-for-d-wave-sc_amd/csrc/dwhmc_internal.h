@@ -274,6 +274,33 @@ void launch_eig_gather(const double2* rho, const double* E, int N, int nc, const
 // *bad = 1 when any entry of U (nu complex) or E (ne real) is not finite
 void launch_nonfinite(const double2* U, int64_t nu, const double* E, int64_t ne, int* bad, hipStream_t s);
 
+// Hermitian eigensolver (dwhmc_eig.hip): m matrices of order n <= kEigMaxN,
+// column-major, per-matrix stride sA (complex) / sZ (double)
+constexpr int kEigTB = 64;                  // trailing-update tile
+constexpr int kEigNB = 64;                  // reflectors per back-transform block
+constexpr int kEigMaxN = 5120;              // rows k_eig_step holds in registers
+constexpr double kEigClusterTol = 2.5e-4;   // eigenvalue gap / ||T|| below which vectors are orthogonalised
+constexpr int kEigMaxCluster = 128;         // longest such run (else *bad: vendor fallback)
+// column i of the tridiagonalisation: partial sums -> w_{i-1}, column i -> v_i (d, e, tau)
+void launch_eig_step(double2* A, int n, int i, int64_t sA, const double2* part, int64_t sP, double2* vv,
+                     double2* ww, double* d, double* e, double2* tau, int m, hipStream_t s);
+// deferred rank-2 update of column i-1 on the trailing triangle + hemv partials of v_i
+void launch_eig_pass(double2* A, int n, int i, int64_t sA, double2* part, int64_t sP, const double2* vv,
+                     const double2* ww, int m, hipStream_t s);
+// eigenvalues ascending into E, ||T|| bound per matrix into tnorm
+void launch_eig_bisect(const double* d, const double* e, int n, double* E, double* tnorm, int m, hipStream_t s);
+// eigenvectors of T into Zt (Zt[r n + j]: component r of vector j), clusters orthonormalised
+void launch_eig_invit(const double* d, const double* e, int n, const double* E, const double* tnorm, double* Zt,
+                      double* U0, double* U1, double* U2, int64_t sZ, int* bad, int m, hipStream_t s);
+void launch_eig_zt_to_u(const double* Zt, double2* U, int n, int64_t sZ, int64_t sA, int m, hipStream_t s);
+constexpr int kEigGS = 8;                   // row slices of each block's Gram sum
+// compact-WY T of every reflector block; Gp: m x nblk x kEigGS x kEigNB^2 scratch
+void launch_eig_tfac(const double2* V, int n, int64_t sA, const double2* tau, double2* Gp, double2* Tb, int64_t sT,
+                     int m, hipStream_t s);
+// W2 (kb x n, ld kEigNB) = T (sum of the S row chunks of W, chunk s at rows s kb, ld ldw)
+void launch_eig_tw(const double2* Tb, int64_t sT, const double2* W, int ldw, int64_t sW, int S, int kb, int n,
+                   double2* W2, int64_t sW2, int m, hipStream_t s);
+
 int selftest_mfma_layout(int device);
 
 }  // namespace dwh

@@ -8,7 +8,7 @@ factorisation outputs (P_ij, E_f, Tr ρ_hh; hmc.measure_observables).
 
 Every measure_transport_freq sweeps the heavy measurement
 (`measure_transport_and_spectra`, src/Observables.jl:314-526) runs on the
-device as well (rocSOLVER eigenpairs + HIP kernels) and fills transport.csv;
+device as well (own eigensolver + HIP kernels) and fills transport.csv;
 the JLD2 spectra bins become numpy files (no JLD2 writer in this image).
 The reference's RNG is global and unseeded; here the caller
 passes `rng` (draw order per sweep: randn(ComplexF64, N, 2), then rand()).

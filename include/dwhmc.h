@@ -81,8 +81,8 @@ int dwh_create_batched(dwh_ctx** ctx, int64_t Lx, int64_t Ly, double t, double t
  *                   Gauss-Jordan of the dense N x N complement per pole;
  *   DWH_ALGO_CR     block cyclic reduction of the block-tridiagonal (lattice-row
  *                   blocks, periodic) BdG matrix per pole; needs 2 Lx <= 128;
- *   DWH_ALGO_EIG    the reference's own method: rocSOLVER zheevd of every chain's
- *                   2N x 2N H_BdG per step, ρ = U diag(f) U^H by zgemm
+ *   DWH_ALGO_EIG    the reference's own method: the eigendecomposition of every chain's
+ *                   2N x 2N H_BdG per step (dwh_eigensystem's solver), ρ = U diag(f) U^H by zgemm
  *                   [src/Hamiltonian.jl:96-114, src/Observables.jl:14-62]; any β,
  *                   no pole set, no |Δ| guard; O(N^3) with a large constant;
  *   DWH_ALGO_AUTO   DWHMC_ALGO from the environment (dense | cr | eig | auto),
@@ -173,7 +173,7 @@ int dwh_stream(dwh_ctx* ctx, void** stream);
  * (bench/profiling).  enable is a bitmask over the timer names below
  * (bit 0 "gj_update", bit 1 "gj_pivot", bit 2 "assemble", bit 3 "contract",
  * bit 4 "step", bit 5 "gj_edge", bit 6 "cr_gemm", bit 7 "cr_inv", bit 8 "cr_inv_side",
- * bit 9 "cr_tail", bit 10 "cr_fused");
+ * bit 9 "cr_tail", bit 10 "cr_fused", bit 11 "eig_own", bit 12 "eig_vendor");
  * 0 disables, -1 times everything. */
 int dwh_timing_enable(dwh_ctx* ctx, int32_t enable);
 /* name: "gj_update" (rank-128 paired / rank-64 trailing updates),
@@ -183,7 +183,8 @@ int dwh_timing_enable(dwh_ctx* ctx, int32_t enable);
  * the critical path; work = inversion + side-product flops), "cr_tail" (the
  * coarse levels' stages in one launch; work = their inversion + product flops), "cr_fused"
  * (BP = 32 launches that run two consecutive stages; work = both stages'
- * flops), "assemble",
+ * flops), "eig_own" / "eig_vendor" (eigensolves by the library's solver /
+ * by rocSOLVER, opt-in or fallback; work = matrices), "assemble",
  * "contract", "step"; returns total milliseconds, launches and the
  * algorithmic work summed over launches (fp64 flops; HBM bytes for
  * "assemble"). */
@@ -195,7 +196,13 @@ int dwh_timing_reset(dwh_ctx* ctx);
  * Eigen-decomposition of one chain's H_BdG(Δ) at the device Δ: what the
  * reference's diagonalize_H_BdG! [src/Hamiltonian.jl:96-114] leaves in
  * cache.E_n / cache.U, which the hot path replaces by the pole expansion but
- * transport and spectra need.  rocSOLVER zheevd on the context's stream.
+ * transport and spectra need.  The library's own Hermitian eigensolver on
+ * the context's stream (dwhmc_eig.hip: Householder tridiagonalisation,
+ * multisection on Sturm counts, inverse iteration with cluster
+ * orthonormalisation, blocked back-transform; rocBLAS zgemm / dgemm for the
+ * plain products); DWHMC_EIG_SOLVER=evd / ev selects rocSOLVER zheevd / zheev
+ * instead, and rocSOLVER zheev is the fallback when the own solver flags a
+ * result (eigenvalue cluster longer than 128, non-finite values).
  * E: 2N, ascending; U (nullable): 2N x 2N column-major, the eigenvector of
  * E[n] in column n (phases are the solver's). */
 int dwh_eigensystem(dwh_ctx* ctx, int64_t chain, double* E, dwh_c128* U);
@@ -219,8 +226,8 @@ int dwh_measure_transport(dwh_ctx* ctx, int64_t chain, double eta, double domega
                           double* dos, double* dos_an, int64_t n_dos, double* ak0);
 
 /* dwh_measure_transport for every chain of the context at once: the
- * eigensolves and J_mn products are batched (rocSOLVER / rocBLAS
- * strided-batched), which at n = 2048 costs ~1/3 per chain of separate calls.
+ * eigensolves and J_mn products are batched over the chains (every kernel
+ * of the eigensolver and the rocBLAS products take all chains per launch).
  * Outputs per chain c at stiffness[c], dc_cond[c], sigma[c*n_omega],
  * dos[c*n_dos], dos_an[c*n_dos], ak0[c*Lx*Ly]. */
 int dwh_measure_transport_batched(dwh_ctx* ctx, double eta, double domega, double omega_max,

@@ -10,8 +10,9 @@ The reference ships no transport fixtures, so these plus the
 loop form are the pins; the absolute values are otherwise "parity unpinned"
 against a Julia run.
 
-GPU: the device path (rocSOLVER zheevd, zheev where zheevd leaves non-finite
-vectors, + rocBLAS zgemm + dwhmc_transport.hip)
+GPU: the device path (the hand-written eigensolver csrc/dwhmc_eig.hip, with
+rocSOLVER zheev only where it flags a result, + rocBLAS zgemm +
+dwhmc_transport.hip)
 through the C ABI vs the oracle on the same Δ.  Tolerances (fp64):
   * eigenvalues          |E_gpu - E_ref| ≤ 1e-12 (1 + max|E|)
   * stiffness, dc        |Δ| ≤ 1e-9 (1 + |ref|)
@@ -133,6 +134,41 @@ def test_eigensystem_matches_oracle(dwhmc, oracle, Lx, Ly):
     scale = 1 + np.max(np.abs(cache.E_n))
     assert np.max(np.abs(E - cache.E_n)) <= 1e-12 * scale
     assert np.max(np.abs(Href @ U - U * E[None, :])) <= 1e-11 * scale
+    assert np.max(np.abs(U.conj().T @ U - np.eye(2 * p.N))) <= 1e-12
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("Lx,Ly,beta,clean", [(8, 8, 16.0, False), (16, 16, 8.0, False), (32, 32, 16.0, False),
+                                              (16, 16, 8.0, True), (12, 10, 4.0, True)])
+def test_own_eigensolver_full_size(dwhmc, oracle, Lx, Ly, beta, clean):
+    """The hand-written eigensolver (csrc/dwhmc_eig.hip: Householder
+    tridiagonalisation, bisection, inverse iteration + cluster Cholesky QR,
+    blocked back-transform) at BASELINE sizes (n = 2N up to 2048) against
+    LAPACK zheevr (the oracle, as eigen!(Hermitian(H)) in
+    src/Hamiltonian.jl:96-114): eigenvalues within 1e-12 (1 + max|E|),
+    ‖H U − U E‖ within 1e-11 (1 + max|E|), ‖UᴴU − I‖ ≤ 1e-12.  Clean lattices
+    (W = 0, uniform d-wave Δ) have exactly degenerate levels: their vectors
+    come out of the cluster orthonormalisation."""
+    O = oracle
+    if clean:
+        p = O.ModelParameters(Lx, Ly, T, TP, -1.0, 0.0, 0.0, beta, 0.8, 1.0)
+        dis = np.zeros(p.N)
+        D = np.stack([np.full(p.N, 0.2), np.full(p.N, -0.2)], 1).astype(np.complex128)
+    else:
+        p, dis, D = _case(O, Lx, Ly, beta, seed=Lx * 31 + Ly)
+    cache, _, _ = O.evaluate(p, dis, D)
+    ctx = _ctx(dwhmc, p, dis)
+    ctx.set_pairing(D)
+    ctx.timing_enable(["eig_own", "eig_vendor"])
+    E, U = ctx.eigensystem(0)
+    own, vendor = ctx.timing_read("eig_own")[1], ctx.timing_read("eig_vendor")[1]
+    ctx.close()
+    assert (own, vendor) == (1, 0), "the own solver ran without the rocSOLVER fallback"
+    H = O.hermitian_from_upper(cache.H_base)
+    scale = 1 + np.max(np.abs(cache.E_n))
+    assert np.all(np.isfinite(U))
+    assert np.max(np.abs(E - cache.E_n)) <= 1e-12 * scale
+    assert np.max(np.abs(H @ U - U * E[None, :])) <= 1e-11 * scale
     assert np.max(np.abs(U.conj().T @ U - np.eye(2 * p.N))) <= 1e-12
 
 
