@@ -46,7 +46,6 @@ namespace dwh {
 namespace {
 
 constexpr int kStepT = 1024;   // threads of k_eig_step
-constexpr int kMaxR = kEigMaxN / kStepT;   // rows per k_eig_step thread
 
 // sums over the workgroup (fixed order: xor-shuffle tree per wave, then the
 // waves in index order); every thread returns the totals.  sh: one slot per
@@ -76,22 +75,10 @@ __device__ __forceinline__ double2 group_sum2(double2 v, double2* sh) {
 
 __device__ __forceinline__ double2 cz() { return make_double2(0.0, 0.0); }
 
-// sum over Y in [t0, T) of part[Y n + r], ascending Y, eight loads in flight
-__device__ __forceinline__ double2 sum_partials(const double2* __restrict__ part, int n, int r, int t0, int T) {
-  double2 p = cz();
-  for (int Y0 = t0; Y0 < T; Y0 += 8) {
-    double2 q[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) q[u] = Y0 + u < T ? part[(int64_t)(Y0 + u) * n + r] : cz();
-#pragma unroll
-    for (int u = 0; u < 8; ++u) p = cadd(p, q[u]);
-  }
-  return p;
-}
-
 // Every load of the step is issued up front (column i, v_{i-1}, the pass
 // partials of this thread's rows and of row i): two workgroup reductions
 // (x^H v, then the reflector norm) are its only barriers.
+template <int kMaxR>   // row slots per thread: ceil(n / kStepT)
 __global__ __launch_bounds__(kStepT) void k_eig_step(double2* __restrict__ A, int n, int i, int64_t sA,
                                                      const double2* __restrict__ part, int64_t sP,
                                                      double2* __restrict__ vv, double2* __restrict__ ww,
@@ -118,9 +105,30 @@ __global__ __launch_bounds__(kStepT) void k_eig_step(double2* __restrict__ A, in
     cr[s] = vp[s] = wr[s] = cz();
     if (r < n) {
       cr[s] = A[r + (int64_t)i * n];
-      if (i > 0) {
-        vp[s] = vprv[r];
-        wr[s] = sum_partials(part, n, r, t0, T);
+      if (i > 0) vp[s] = vprv[r];
+    }
+  }
+  double2 pi = cz();   // p[i], every thread (v_{i-1}[i] = 1: w[i] = x[i] + alpha)
+  if (i > 0) {
+    // the pass partials of every row slot and of row i, 4 Y values per round
+    // for all of them at once (ascending Y per row: fixed summation order)
+    for (int Y0 = t0; Y0 < T; Y0 += 4) {
+      double2 q[kMaxR + 1][4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const bool yok = Y0 + u < T;
+#pragma unroll
+        for (int s = 0; s < kMaxR; ++s) {
+          const int r = i + tid + s * kStepT;
+          q[s][u] = (yok && r < n) ? part[(int64_t)(Y0 + u) * n + r] : cz();
+        }
+        q[kMaxR][u] = yok ? part[(int64_t)(Y0 + u) * n + i] : cz();
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+#pragma unroll
+        for (int s = 0; s < kMaxR; ++s) wr[s] = cadd(wr[s], q[s][u]);
+        pi = cadd(pi, q[kMaxR][u]);
       }
     }
   }
@@ -128,8 +136,6 @@ __global__ __launch_bounds__(kStepT) void k_eig_step(double2* __restrict__ A, in
   if (i > 0) {
     // p = A^{(i-1)} v_{i-1}; x = tau p; w = x - 1/2 tau (x^H v) v  (zhetd2 'L')
     const double2 tp = tau[i - 1];
-    // p[i], every thread (v_{i-1}[i] = 1: w[i] = x[i] + alpha)
-    const double2 pi = sum_partials(part, n, i, t0, T);
     double2 g = cz();
 #pragma unroll
     for (int s = 0; s < kMaxR; ++s) {
@@ -319,7 +325,7 @@ __device__ void gersh(const double* __restrict__ d, const double* __restrict__ e
 // counts at lo + (l+1)(hi-lo)/65; the counts are monotone in l, so a ballot
 // finds the sub-interval holding eigenvalue j), ~9 rounds to the last bit
 // instead of ~53 bisection steps.  Sturm count: the dstebz recurrence with
-// d and e^2 broadcast from LDS and 1/q by v_rcp_f64 + two Newton steps.
+// d and e^2 broadcast from LDS and 1/q by v_rcp_f64 + one Newton step.
 constexpr int kBisW = 8;   // waves (eigenvalues) per workgroup
 __global__ __launch_bounds__(64 * kBisW) void k_eig_bisect(const double* __restrict__ d,
                                                            const double* __restrict__ e, int n,
@@ -356,7 +362,11 @@ __global__ __launch_bounds__(64 * kBisW) void k_eig_bisect(const double* __restr
     int c = q < 0.0;
 #pragma unroll 8
     for (int r = 1; r < n; ++r) {
-      q = (ld[r] - x) - le2[r - 1] * rcp_nr(q);
+      // 1/q: v_rcp_f64 + one Newton step (<= 11 ulp; a relative error of 1/q is a
+      // relative perturbation of e^2_{r-1}, far below the count's resolution)
+      const double r0 = __builtin_amdgcn_rcp(q);
+      const double rq = fma(r0, fma(-q, r0, 1.0), r0);
+      q = (ld[r] - x) - le2[r - 1] * rq;
       if (fabs(q) < pivmin) q = -pivmin;
       c += q < 0.0;
     }
@@ -393,63 +403,96 @@ __device__ __forceinline__ double clamp_small(double x, double small) {
 // solves with T - lam I from a fixed pseudo-random start (lam is accurate to
 // a few ulps of ||T||, so one solve already leaves neighbours at ~ulp / gap),
 // normalised
-__device__ void invit_one(const double* __restrict__ d, const double* __restrict__ e, int n, double lam, int m,
+__device__ void invit_one(const double* d, const double* e, int n, double lam, int m,
                           double small, double* __restrict__ Zt, double* __restrict__ U0, double* __restrict__ U1,
                           double* __restrict__ U2) {
-  double* x = Zt + m;
-  double* u0 = U0 + m;
-  double* u1 = U1 + m;
-  double* u2 = U2 + m;
+  double* __restrict__ x = Zt + m;
+  double* __restrict__ u0 = U0 + m;
+  double* __restrict__ u1 = U1 + m;
+  double* __restrict__ u2 = U2 + m;
   const int64_t ld = n;
+  constexpr int PB = 16;   // rows per prefetch block
   double scale = 1.0;
   for (int it = 0; it < 2; ++it) {
     const bool first = it == 0;
     // forward: factor T - lam I (row interchanges) and eliminate y in one sweep
     double cu0 = d[0] - lam, cu1 = n > 1 ? e[0] : 0.0;
     double yk = first ? start_entry(m, 0) : x[0] * scale;
-#pragma unroll 8
-    for (int r = 0; r < n - 1; ++r) {
-      const double b = e[r], nd = d[r + 1] - lam, ne = r + 1 < n - 1 ? e[r + 1] : 0.0;
-      const double yk1 = first ? start_entry(m, r + 1) : x[(r + 1) * ld] * scale;
-      if (fabs(cu0) >= fabs(b)) {
-        if (cu0 == 0.0) cu0 = small;
-        const double mu = b / cu0;
-        u0[r * ld] = 1.0 / clamp_small(cu0, small);
-        u1[r * ld] = cu1;
-        u2[r * ld] = 0.0;
-        x[r * ld] = yk;
-        cu0 = nd - mu * cu1;
-        cu1 = ne;
-        yk = yk1 - mu * yk;
-      } else {
-        const double mu = cu0 / b;
-        u0[r * ld] = 1.0 / clamp_small(b, small);
-        u1[r * ld] = nd;
-        u2[r * ld] = ne;
-        x[r * ld] = yk1;
-        cu0 = cu1 - mu * nd;
-        cu1 = -mu * ne;
-        yk = yk - mu * yk1;
+    for (int r0 = 0; r0 < n - 1; r0 += PB) {
+      double yb[PB];
+#pragma unroll
+      for (int u = 0; u < PB; ++u) {
+        const int r = r0 + u;
+        yb[u] = r < n - 1 ? (first ? start_entry(m, r + 1) : x[(r + 1) * ld] * scale) : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < PB; ++u) {
+        const int r = r0 + u;
+        if (r >= n - 1) break;
+        const double b = e[r], nd = d[r + 1] - lam, ne = r + 1 < n - 1 ? e[r + 1] : 0.0;
+        const double yk1 = yb[u];
+        if (fabs(cu0) >= fabs(b)) {
+          if (cu0 == 0.0) cu0 = small;
+          const double rc = rcp_nr(cu0);
+          const double mu = b * rc;
+          u0[r * ld] = fabs(cu0) < small ? rcp_nr(clamp_small(cu0, small)) : rc;
+          u1[r * ld] = cu1;
+          u2[r * ld] = 0.0;
+          x[r * ld] = yk;
+          cu0 = nd - mu * cu1;
+          cu1 = ne;
+          yk = yk1 - mu * yk;
+        } else {
+          const double rb = rcp_nr(b);
+          const double mu = cu0 * rb;
+          u0[r * ld] = fabs(b) < small ? rcp_nr(clamp_small(b, small)) : rb;
+          u1[r * ld] = nd;
+          u2[r * ld] = ne;
+          x[r * ld] = yk1;
+          cu0 = cu1 - mu * nd;
+          cu1 = -mu * ne;
+          yk = yk - mu * yk1;
+        }
       }
     }
     u0[(n - 1) * ld] = 1.0 / clamp_small(cu0, small);
     u1[(n - 1) * ld] = 0.0;
     u2[(n - 1) * ld] = 0.0;
     x[(n - 1) * ld] = yk;
-    // backward substitution
+    // backward substitution, PB rows loaded ahead of their use
     double x1 = 0.0, x2 = 0.0, nrm = 0.0;
-#pragma unroll 8
-    for (int r = n - 1; r >= 0; --r) {
-      const double xr = (x[r * ld] - u1[r * ld] * x1 - u2[r * ld] * x2) * u0[r * ld];
-      x[r * ld] = xr;
-      x2 = x1;
-      x1 = xr;
-      nrm += xr * xr;
+    for (int rt = n - 1; rt >= 0; rt -= PB) {
+      double yb[PB], a0[PB], a1[PB], a2[PB];
+#pragma unroll
+      for (int u = 0; u < PB; ++u) {
+        const int r = rt - u;
+        const bool ok = r >= 0;
+        yb[u] = ok ? x[r * ld] : 0.0;
+        a0[u] = ok ? u0[r * ld] : 0.0;
+        a1[u] = ok ? u1[r * ld] : 0.0;
+        a2[u] = ok ? u2[r * ld] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < PB; ++u) {
+        const int r = rt - u;
+        if (r < 0) break;
+        const double xr = (yb[u] - a1[u] * x1 - a2[u] * x2) * a0[u];
+        x[r * ld] = xr;
+        x2 = x1;
+        x1 = xr;
+        nrm += xr * xr;
+      }
     }
     scale = 1.0 / sqrt(nrm);
   }
-#pragma unroll 8
-  for (int r = 0; r < n; ++r) x[r * ld] *= scale;
+  for (int r0 = 0; r0 < n; r0 += 16) {
+    double t[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) t[u] = r0 + u < n ? x[(r0 + u) * ld] : 0.0;
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+      if (r0 + u < n) x[(r0 + u) * ld] = t[u] * scale;
+  }
 }
 
 __global__ __launch_bounds__(64) void k_eig_invit(const double* __restrict__ d, const double* __restrict__ e,
@@ -457,13 +500,19 @@ __global__ __launch_bounds__(64) void k_eig_invit(const double* __restrict__ d, 
                                                   const double* __restrict__ tnorm, double* __restrict__ Zt,
                                                   double* __restrict__ U0, double* __restrict__ U1,
                                                   double* __restrict__ U2, int64_t sZ) {
+  extern __shared__ double lds[];   // d[0, n), e[n, 2n)
   const int k = blockIdx.y;
+  for (int r = threadIdx.x; r < n; r += blockDim.x) {
+    lds[r] = d[(int64_t)k * n + r];
+    lds[n + r] = r < n - 1 ? e[(int64_t)k * n + r] : 0.0;
+  }
+  __syncthreads();
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
   const double tn = tnorm[k];
   const double small = tn > 0.0 ? DBL_EPSILON * tn : DBL_EPSILON;
-  invit_one(d + (int64_t)k * n, e + (int64_t)k * n, n, E[(int64_t)k * n + j], j, small, Zt + k * sZ,
-            U0 + k * sZ, U1 + k * sZ, U2 + k * sZ);
+  invit_one(lds, lds + n, n, E[(int64_t)k * n + j], j, small, Zt + k * sZ, U0 + k * sZ, U1 + k * sZ,
+            U2 + k * sZ);
 }
 
 // Clusters (runs of eigenvalues with consecutive gaps <= ctol ||T||, up to
@@ -492,7 +541,7 @@ __global__ __launch_bounds__(256) void k_eig_orth(const double* __restrict__ E, 
     if (tid == 0) *bad = 1;
     return;
   }
-  constexpr int RC = 16;   // rows per LDS chunk of the Gram sums
+  constexpr int RC = 64;   // rows per LDS chunk (Gram sums, substitution)
   __shared__ double G[MC][MC + 1];
   __shared__ double Zs[RC][MC + 1];
   __shared__ int fail;
@@ -559,16 +608,28 @@ __global__ __launch_bounds__(256) void k_eig_orth(const double* __restrict__ E, 
       if (tid == 0) *bad = 1;
       return;
     }
-    // each row z (1 x kc) <- z L^-T: forward substitution L x = z^T
-    for (int r = tid; r < n; r += 256) {
-      double* z = Zt + (int64_t)r * n + j;
-      for (int p = 0; p < kc; ++p) {
-        double s = z[p];
-        for (int q = 0; q < p; ++q) s -= G[p][q] * z[q];
-        z[p] = s / G[p][p];
+    // each row z (1 x kc) <- z L^-T: forward substitution L x = z^T, on RC-row
+    // chunks staged in LDS (one row per thread)
+    for (int r0 = 0; r0 < n; r0 += RC) {
+      for (int q = tid; q < RC * kc; q += 256) {
+        const int rr = q / kc, c = q % kc, r = r0 + rr;
+        Zs[rr][c] = r < n ? Zt[(int64_t)r * n + j + c] : 0.0;
       }
+      __syncthreads();
+      if (tid < RC) {
+        for (int p = 0; p < kc; ++p) {
+          double v = Zs[tid][p];
+          for (int q = 0; q < p; ++q) v -= G[p][q] * Zs[tid][q];
+          Zs[tid][p] = v / G[p][p];
+        }
+      }
+      __syncthreads();
+      for (int q = tid; q < RC * kc; q += 256) {
+        const int rr = q / kc, c = q % kc, r = r0 + rr;
+        if (r < n) Zt[(int64_t)r * n + j + c] = Zs[rr][c];
+      }
+      __syncthreads();
     }
-    __syncthreads();
   }
 }
 
@@ -618,16 +679,16 @@ __global__ __launch_bounds__(256) void k_eig_tgram(const double2* __restrict__ V
       S[rr][cc] = (r < re && cc < kb) ? V[r + (int64_t)(j0 + cc) * n] : cz();
     }
     __syncthreads();
+    // thread: column q = tid % NB, rows p = tid / NB + 4 u of G
+#pragma unroll 2
+    for (int rr = 0; rr < NB; ++rr) {
+      const double2 y = S[rr][tid % NB];
 #pragma unroll
-    for (int u = 0; u < NB * NB / 256; ++u) {
-      const int pq = tid + 256 * u, p = pq / NB, q = pq % NB;
-      double2 a = acc[u];
-      for (int rr = 0; rr < NB; ++rr) {
-        const double2 x = S[rr][p], y = S[rr][q];   // conj(x) y
-        a.x += x.x * y.x + x.y * y.y;
-        a.y += x.x * y.y - x.y * y.x;
+      for (int u = 0; u < NB * NB / 256; ++u) {
+        const double2 x = S[rr][(tid + 256 * u) / NB];   // conj(x) y
+        acc[u].x += x.x * y.x + x.y * y.y;
+        acc[u].y += x.x * y.y - x.y * y.x;
       }
-      acc[u] = a;
     }
     __syncthreads();
   }
@@ -671,26 +732,33 @@ __global__ __launch_bounds__(256) void k_eig_tfac(const double2* __restrict__ Gp
 }
 
 // W2 = T (sum over the S K-chunks of W): T kb x kb (ld kEigNB), chunk s of W
-// at rows s kb (ld ldw); one thread per output entry
+// at rows s kb (ld ldw).  One workgroup per 16 columns: the chunk sums of its
+// columns (coalesced over the rows) and T staged in LDS, then 64 MACs per output.
 __global__ __launch_bounds__(256) void k_eig_tw(const double2* __restrict__ Tb, int64_t sT,
                                                 const double2* __restrict__ W, int ldw, int64_t sW, int S, int kb,
                                                 int n, double2* __restrict__ W2, int64_t sW2) {
-  __shared__ double2 Ts[kEigNB][kEigNB + 1];
-  const int k = blockIdx.y, p = threadIdx.x & 63, w = threadIdx.x >> 6;
+  constexpr int NB = kEigNB, CW = 16;
+  __shared__ double2 Ts[NB][NB + 1];
+  __shared__ double2 Ws[CW][NB + 1];
+  const int k = blockIdx.y, tid = threadIdx.x, c0 = blockIdx.x * CW;
   Tb += k * sT;
-  for (int q = threadIdx.x; q < kEigNB * kEigNB; q += 256) Ts[q % kEigNB][q / kEigNB] = Tb[q];
+  W += k * sW;
+  for (int q = tid; q < NB * NB; q += 256) Ts[q % NB][q / NB] = Tb[q];
+  for (int q = tid; q < NB * CW; q += 256) {
+    const int p = q % NB, cj = q / NB, col = c0 + cj;
+    double2 a = cz();
+    if (p < kb && col < n)
+      for (int s = 0; s < S; ++s) a = cadd(a, W[(int64_t)col * ldw + s * kb + p]);
+    Ws[cj][p] = a;
+  }
   __syncthreads();
-  // 4 waves x 4 columns each
-  for (int cj = 0; cj < 4; ++cj) {
-    const int col = blockIdx.x * 16 + w * 4 + cj;
-    if (col >= n) break;
-    const double2* Wc = W + k * sW + (int64_t)col * ldw;
-    double2 acc = cz();
-    for (int s = 0; s < S; ++s) {
+  for (int q = tid; q < NB * CW; q += 256) {
+    const int p = q % NB, cj = q / NB, col = c0 + cj;
+    if (p >= kb || col >= n) continue;
+    double2 a = cz();
 #pragma unroll 8
-      for (int q = 0; q < kb; ++q) acc = cadd(acc, cmul(Ts[p][q], Wc[s * kb + q]));
-    }
-    if (p < kb) W2[k * sW2 + p + (int64_t)col * kEigNB] = acc;
+    for (int r = 0; r < kb; ++r) a = cadd(a, cmul(Ts[p][r], Ws[cj][r]));
+    W2[k * sW2 + p + (int64_t)col * NB] = a;
   }
 }
 
@@ -698,7 +766,15 @@ __global__ __launch_bounds__(256) void k_eig_tw(const double2* __restrict__ Tb, 
 
 void launch_eig_step(double2* A, int n, int i, int64_t sA, const double2* part, int64_t sP, double2* vv,
                      double2* ww, double* d, double* e, double2* tau, int m, hipStream_t s) {
-  hipLaunchKernelGGL(k_eig_step, dim3(m), dim3(kStepT), 0, s, A, n, i, sA, part, sP, vv, ww, d, e, tau);
+  const int rs = (n - i + kStepT - 1) / kStepT;   // row slots the rows i..n-1 need
+  static_assert(kEigMaxN <= 5 * kStepT, "k_eig_step instantiations");
+  switch (rs) {
+    case 1: hipLaunchKernelGGL(k_eig_step<1>, dim3(m), dim3(kStepT), 0, s, A, n, i, sA, part, sP, vv, ww, d, e, tau); break;
+    case 2: hipLaunchKernelGGL(k_eig_step<2>, dim3(m), dim3(kStepT), 0, s, A, n, i, sA, part, sP, vv, ww, d, e, tau); break;
+    case 3: hipLaunchKernelGGL(k_eig_step<3>, dim3(m), dim3(kStepT), 0, s, A, n, i, sA, part, sP, vv, ww, d, e, tau); break;
+    case 4: hipLaunchKernelGGL(k_eig_step<4>, dim3(m), dim3(kStepT), 0, s, A, n, i, sA, part, sP, vv, ww, d, e, tau); break;
+    default: hipLaunchKernelGGL(k_eig_step<5>, dim3(m), dim3(kStepT), 0, s, A, n, i, sA, part, sP, vv, ww, d, e, tau); break;
+  }
 }
 
 void launch_eig_pass(double2* A, int n, int i, int64_t sA, double2* part, int64_t sP, const double2* vv,
@@ -715,7 +791,8 @@ void launch_eig_bisect(const double* d, const double* e, int n, double* E, doubl
 
 void launch_eig_invit(const double* d, const double* e, int n, const double* E, const double* tnorm, double* Zt,
                       double* U0, double* U1, double* U2, int64_t sZ, int* bad, int m, hipStream_t s) {
-  hipLaunchKernelGGL(k_eig_invit, dim3((n + 63) / 64, m), dim3(64), 0, s, d, e, n, E, tnorm, Zt, U0, U1, U2, sZ);
+  hipLaunchKernelGGL(k_eig_invit, dim3((n + 63) / 64, m), dim3(64), 2 * n * sizeof(double), s, d, e, n, E, tnorm, Zt,
+                     U0, U1, U2, sZ);
   hipLaunchKernelGGL(k_eig_orth, dim3(n, m), dim3(256), 0, s, E, tnorm, n, Zt, sZ, kEigClusterTol, bad);
 }
 

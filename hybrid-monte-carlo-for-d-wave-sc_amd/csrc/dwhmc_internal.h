@@ -276,11 +276,11 @@ void launch_nonfinite(const double2* U, int64_t nu, const double* E, int64_t ne,
 
 // Hermitian eigensolver (dwhmc_eig.hip): m matrices of order n <= kEigMaxN,
 // column-major, per-matrix stride sA (complex) / sZ (double)
-constexpr int kEigTB = 64;                  // trailing-update tile
+constexpr int kEigTB = 64;                  // trailing-update tile (one workgroup; hemv partial slots)
 constexpr int kEigNB = 64;                  // reflectors per back-transform block
 constexpr int kEigMaxN = 5120;              // rows k_eig_step holds in registers
 constexpr double kEigClusterTol = 2.5e-4;   // eigenvalue gap / ||T|| below which vectors are orthogonalised
-constexpr int kEigMaxCluster = 128;         // longest such run (else *bad: vendor fallback)
+constexpr int kEigMaxCluster = 64;          // longest such run (else *bad: vendor fallback)
 // column i of the tridiagonalisation: partial sums -> w_{i-1}, column i -> v_i (d, e, tau)
 void launch_eig_step(double2* A, int n, int i, int64_t sA, const double2* part, int64_t sP, double2* vv,
                      double2* ww, double* d, double* e, double2* tau, int m, hipStream_t s);

@@ -202,7 +202,7 @@ int dwh_timing_reset(dwh_ctx* ctx);
  * orthonormalisation, blocked back-transform; rocBLAS zgemm / dgemm for the
  * plain products); DWHMC_EIG_SOLVER=evd / ev selects rocSOLVER zheevd / zheev
  * instead, and rocSOLVER zheev is the fallback when the own solver flags a
- * result (eigenvalue cluster longer than 128, non-finite values).
+ * result (eigenvalue cluster longer than 64, non-finite values).
  * E: 2N, ascending; U (nullable): 2N x 2N column-major, the eigenvector of
  * E[n] in column n (phases are the solver's). */
 int dwh_eigensystem(dwh_ctx* ctx, int64_t chain, double* E, dwh_c128* U);

@@ -24,7 +24,7 @@ DWHMC_EIG_SOLVER=evd timeout -k 10 300 python -u tests/bench_transport.py --step
 cat "$O/transport_own.json" "$O/transport_evd.json"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof" -o run -- \
-  python3 "$R/tests/bench_transport.py" --steps 1 --snapshots 8 --chains 2 > "$O/prof_bench.json" 2> "$O/prof.err" \
+  python3 "$R/tests/bench_transport.py" --steps 2 --snapshots "" --chains 1 > "$O/prof_bench.json" 2> "$O/prof.err" \
   || { tail -5 "$O/prof.err"; exit 1; }
 rm -f "$O/prof/run_kernel_trace.csv"
 head -25 "$O/prof/run_kernel_stats.csv" | cut -c1-160
