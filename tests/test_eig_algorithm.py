@@ -1,0 +1,74 @@
+"""The eigensolver's algorithm (csrc/dwhmc_eig.hip) in its numpy prototype
+(tools/eig_proto.py: the same operation order — zhetd2 'L' tridiagonalisation
+with the rank-2 update deferred into the next hemv sweep, Sturm-count
+bisection, inverse iteration with cluster Cholesky QR and one symmetric
+orthogonalisation step, blocked compact-WY back-transform) against LAPACK on
+random, BdG-structured and exactly degenerate Hermitian matrices.  CPU only;
+the device solver itself is checked against the oracle in
+tests/test_transport.py (GPU)."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+import eig_proto as P  # noqa: E402
+
+
+def _check(A, lam, U, tol=1e-12):
+    scale = 1 + np.max(np.abs(np.linalg.eigvalsh(A)))
+    assert np.max(np.abs(lam - np.linalg.eigvalsh(A))) <= tol * scale
+    assert np.max(np.abs(A @ U - U * lam[None, :])) <= 10 * tol * scale
+    assert np.max(np.abs(U.conj().T @ U - np.eye(A.shape[0]))) <= tol
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 17, 40])
+def test_random_hermitian(n):
+    rng = np.random.default_rng(n)
+    X = rng.standard_normal((n, n)) + 1j * rng.standard_normal((n, n))
+    A = X + X.conj().T
+    lam, U = P.eigh(A)
+    _check(A, lam, U)
+
+
+def test_degenerate_levels():
+    """Exact multiplicities (a clean lattice has them): Cholesky QR turns the
+    inverse-iteration vectors of each level into an orthonormal basis."""
+    rng = np.random.default_rng(5)
+    n = 24
+    Q, _ = np.linalg.qr(rng.standard_normal((n, n)) + 1j * rng.standard_normal((n, n)))
+    ev = np.repeat([-1.0, 0.5, 2.0], 8)
+    A = (Q * ev) @ Q.conj().T
+    A = 0.5 * (A + A.conj().T)
+    lam, U = P.eigh(A)
+    _check(A, lam, U)
+
+
+def test_bdg_matrix(oracle):
+    """A small H_BdG(Δ) of the oracle (src/Hamiltonian.jl:10-86): particle-hole
+    symmetric spectrum, complex pairing."""
+    O = oracle
+    p = O.ModelParameters(4, 3, 1.0, -0.35, -1.08, 1.0, 0.1, 8.0, 0.8, 1.0)
+    rng = np.random.default_rng(3)
+    st = O.initialize_state(p, rng)
+    D = st.Delta + 0.25 * np.exp(0.3j * rng.standard_normal((p.N, 2)))
+    cache, _, _ = O.evaluate(p, st.disorder_pot, D)
+    H = O.hermitian_from_upper(cache.H_base)
+    lam, U = P.eigh(H)
+    _check(H, lam, U)
+    assert np.max(np.abs(lam + lam[::-1])) <= 1e-12 * (1 + np.max(np.abs(lam)))
+
+
+def test_tridiagonal_is_similar():
+    """T = Qᴴ A Q with Q the product of the stored reflectors (real T)."""
+    rng = np.random.default_rng(11)
+    n = 12
+    X = rng.standard_normal((n, n)) + 1j * rng.standard_normal((n, n))
+    A = X + X.conj().T
+    d, e, V, tau = P.tridiagonalize(A)
+    Q = np.eye(n, dtype=complex)
+    for i in range(n - 1):
+        Q = Q @ (np.eye(n) - tau[i] * np.outer(V[:, i], V[:, i].conj()))
+    T = np.diag(d) + np.diag(e, 1) + np.diag(e, -1)
+    assert np.max(np.abs(Q.conj().T @ A @ Q - T)) <= 1e-12 * np.max(np.abs(A))
