@@ -75,38 +75,62 @@ __device__ __forceinline__ double2 group_sum2(double2 v, double2* sh) {
 
 __device__ __forceinline__ double2 cz() { return make_double2(0.0, 0.0); }
 
+// pass i reads A without writing it back (the pending pair i-1 is applied by
+// the next, writing pass together with pair i): even i >= 2, when deferring
+// (batches of 4+ matrices, where the passes are HBM-bound; a single matrix is
+// latency-bound and the step's extra corrections would cost more)
+__host__ __device__ __forceinline__ bool eig_read_pass(int i, bool defer) { return defer && i >= 2 && (i & 1) == 0; }
+
 // Every load of the step is issued up front (column i, v_{i-1}, the pass
 // partials of this thread's rows and of row i): two workgroup reductions
 // (x^H v, then the reflector norm) are its only barriers.
-template <int kMaxR>   // row slots per thread: ceil(n / kStepT)
+template <int kMaxR, bool DEFER>   // row slots per thread: ceil(n / kStepT); DEFER: read-only passes in use
 __global__ __launch_bounds__(kStepT) void k_eig_step(double2* __restrict__ A, int n, int i, int64_t sA,
                                                      const double2* __restrict__ part, int64_t sP,
                                                      double2* __restrict__ vv, double2* __restrict__ ww,
                                                      double* __restrict__ d, double* __restrict__ e,
-                                                     double2* __restrict__ tau) {
+                                                     double2* __restrict__ tau,
+                                                     const double2* __restrict__ dpart) {
   const int k = blockIdx.x, tid = threadIdx.x;
   A += k * sA;
   part += k * sP;
-  vv += (int64_t)k * 2 * n;
-  ww += (int64_t)k * n;
+  vv += (int64_t)k * 3 * n;
+  ww += (int64_t)k * 2 * n;
   d += (int64_t)k * n;
   e += (int64_t)k * n;
   tau += (int64_t)k * n;
   __shared__ double2 sh1[kStepT / 64];
   __shared__ double sh2[kStepT / 64];
   __shared__ double2 bc;
-  double2* vcur = vv + (int64_t)(i & 1) * n;
-  const double2* vprv = vv + (int64_t)((i & 1) ^ 1) * n;
+  double2* vcur = vv + (int64_t)(i % 3) * n;
+  const double2* vprv = vv + (int64_t)((i + 2) % 3) * n;   // v_{i-1}
+  const double2* vp2 = vv + (int64_t)((i + 1) % 3) * n;    // v_{i-2}
+  const double2* wp2 = ww + (int64_t)(i & 1) * n;          // w_{i-2}
+  double2* wout = ww + (int64_t)((i + 1) & 1) * n;         // w_{i-1}
+  // pass i-1 was read-only (eig_read_pass): its hemv used A without pair i-2,
+  // which is also still missing from column i
+  const bool rp = eig_read_pass(i - 1, DEFER);
   const int t0 = i / kEigTB, T = (n + kEigTB - 1) / kEigTB;
-  double2 cr[kMaxR], vp[kMaxR], wr[kMaxR];
+  double2 cr[kMaxR], vp[kMaxR], wr[kMaxR], v2[kMaxR], w2[kMaxR];
 #pragma unroll
   for (int s = 0; s < kMaxR; ++s) {
     const int r = i + tid + s * kStepT;
-    cr[s] = vp[s] = wr[s] = cz();
+    cr[s] = vp[s] = wr[s] = v2[s] = w2[s] = cz();
     if (r < n) {
       cr[s] = A[r + (int64_t)i * n];
       if (i > 0) vp[s] = vprv[r];
+      if (rp) {
+        v2[s] = vp2[r];
+        w2[s] = wp2[r];
+      }
     }
+  }
+  // the read-only pass's dots w_{i-2}^H v_{i-1}, v_{i-2}^H v_{i-1} (one per
+  // diagonal tile), summed with the partials below
+  double2 dw = cz(), dv = cz(), v2i = cz(), w2i = cz();
+  if (rp) {
+    v2i = vp2[i];
+    w2i = wp2[i];
   }
   double2 pi = cz();   // p[i], every thread (v_{i-1}[i] = 1: w[i] = x[i] + alpha)
   if (i > 0) {
@@ -124,18 +148,34 @@ __global__ __launch_bounds__(kStepT) void k_eig_step(double2* __restrict__ A, in
         }
         q[kMaxR][u] = yok ? part[(int64_t)(Y0 + u) * n + i] : cz();
       }
+      double2 qd[4][2];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const bool ok = rp && Y0 + u < T;
+        qd[u][0] = ok ? dpart[(int64_t)(k * T + Y0 + u) * 2] : cz();
+        qd[u][1] = ok ? dpart[(int64_t)(k * T + Y0 + u) * 2 + 1] : cz();
+      }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
 #pragma unroll
         for (int s = 0; s < kMaxR; ++s) wr[s] = cadd(wr[s], q[s][u]);
         pi = cadd(pi, q[kMaxR][u]);
+        dw = cadd(dw, qd[u][0]);
+        dv = cadd(dv, qd[u][1]);
       }
     }
   }
   double2 wi = cz();
   if (i > 0) {
-    // p = A^{(i-1)} v_{i-1}; x = tau p; w = x - 1/2 tau (x^H v) v  (zhetd2 'L')
+    // p = A^{(i-1)} v_{i-1} (less the pending pair i-2 after a read-only
+    // pass: A v = A_stale v - v2 (w2^H v) - w2 (v2^H v)); x = tau p;
+    // w = x - 1/2 tau (x^H v) v  (zhetd2 'L')
     const double2 tp = tau[i - 1];
+    if (rp) {
+#pragma unroll
+      for (int s = 0; s < kMaxR; ++s) wr[s] = csub(csub(wr[s], cmul(v2[s], dw)), cmul(w2[s], dv));
+      pi = csub(csub(pi, cmul(v2i, dw)), cmul(w2i, dv));
+    }
     double2 g = cz();
 #pragma unroll
     for (int s = 0; s < kMaxR; ++s) {
@@ -150,10 +190,11 @@ __global__ __launch_bounds__(kStepT) void k_eig_step(double2* __restrict__ A, in
     for (int s = 0; s < kMaxR; ++s) {
       const int r = i + tid + s * kStepT;
       wr[s] = cadd(wr[s], cmul(al, vp[s]));
-      if (r < n) ww[r] = wr[s];
+      if (r < n) wout[r] = wr[s];
     }
   }
-  // column i with the deferred update of column i-1 (v_{i-1}[i] = 1)
+  // column i with the deferred updates of column i-1 (v_{i-1}[i] = 1) and,
+  // after a read-only pass, of column i-2
   double xn = 0.0;
 #pragma unroll
   for (int s = 0; s < kMaxR; ++s) {
@@ -161,6 +202,7 @@ __global__ __launch_bounds__(kStepT) void k_eig_step(double2* __restrict__ A, in
     if (r < n) {
       double2 c = cr[s];
       if (i > 0) c = csub(csub(c, cmulc(vp[s], wi)), wr[s]);
+      if (rp) c = csub(csub(c, cmulc(v2[s], w2i)), cmulc(w2[s], v2i));
       cr[s] = c;
       if (r >= i + 2) xn += c.x * c.x + c.y * c.y;
       if (r == i) d[i] = c.x;
@@ -203,37 +245,56 @@ __device__ __forceinline__ void tri_decode(int b, int& R, int& C) {
   C = b - r * (r + 1) / 2;
 }
 
+// Pass i over the trailing lower triangle (rows / cols >= i+1), one
+// workgroup per 64 x 64 tile.  Write passes (all of them for fewer than
+// kEigDeferMin matrices; else odd i, and i = 0 with nothing pending) apply the
+// pending rank-2 pairs (column i-1, and i-2 after a
+// read-only pass) to the tile and write it back; read-only passes
+// (eig_read_pass: even i >= 2) leave A stale by pair i-1 and the diagonal
+// tiles add the dots w_{i-1}^H v_i, v_{i-1}^H v_i for the step's correction:
+// two column sweeps of three write A (25 % fewer HBM bytes).  Both
+// accumulate the tile's share of A v_i into fixed partial slots.
 __global__ __launch_bounds__(256) void k_eig_pass(double2* __restrict__ A, int n, int i, int64_t sA,
                                                   double2* __restrict__ part, int64_t sP,
                                                   const double2* __restrict__ vv, const double2* __restrict__ ww,
-                                                  int t0) {
+                                                  int t0, double2* __restrict__ dpart, int T, int defer) {
   const int k = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   A += k * sA;
   part += k * sP;
-  vv += (int64_t)k * 2 * n;
-  ww += (int64_t)k * n;
-  const double2* v = vv + (int64_t)(i & 1) * n;
-  const double2* vp = vv + (int64_t)((i & 1) ^ 1) * n;
-  const bool pend = i > 0;
+  vv += (int64_t)k * 3 * n;
+  ww += (int64_t)k * 2 * n;
+  const double2* v = vv + (int64_t)(i % 3) * n;
+  const double2* va = vv + (int64_t)((i + 2) % 3) * n;   // pair i-1
+  const double2* wa = ww + (int64_t)((i + 1) & 1) * n;
+  const double2* vb = vv + (int64_t)((i + 1) % 3) * n;   // pair i-2
+  const double2* wb = ww + (int64_t)(i & 1) * n;
+  const bool rd = eig_read_pass(i, defer);
+  // pairs applied to A: none on a read pass (or before any pair exists);
+  // deferring, odd i >= 3 applies pairs i-2 and i-1; else pair i-1
+  const int np = rd || i == 0 ? 0 : (defer && i >= 3 ? 2 : 1);
   int R, C;
   tri_decode(blockIdx.x, R, C);
   R += t0;
   C += t0;
-  __shared__ double2 cv[64], cvp[64], cwp[64], csum[64];
+  __shared__ double2 cv[64], cva[64], cwa[64], cvb[64], cwb[64], csum[64];
   __shared__ double2 colc[64][65];
   __shared__ double2 rowp[4][64];
   if (tid < 64) {
     const int gc = C * kEigTB + tid;
     const bool ok = gc >= i + 1 && gc < n;
     cv[tid] = ok ? v[gc] : cz();
-    cvp[tid] = ok && pend ? vp[gc] : cz();
-    cwp[tid] = ok && pend ? ww[gc] : cz();
+    cva[tid] = ok && np >= 1 ? va[gc] : cz();
+    cwa[tid] = ok && np >= 1 ? wa[gc] : cz();
+    cvb[tid] = ok && np >= 2 ? vb[gc] : cz();
+    cwb[tid] = ok && np >= 2 ? wb[gc] : cz();
   }
   const int gr = R * kEigTB + lane;
   const bool rok = gr >= i + 1 && gr < n;
   const double2 vr = rok ? v[gr] : cz();
-  const double2 vpr = rok && pend ? vp[gr] : cz();
-  const double2 wpr = rok && pend ? ww[gr] : cz();
+  const double2 var = rok && (np >= 1 || rd) ? va[gr] : cz();
+  const double2 war = rok && (np >= 1 || rd) ? wa[gr] : cz();
+  const double2 vbr = rok && np >= 2 ? vb[gr] : cz();
+  const double2 wbr = rok && np >= 2 ? wb[gr] : cz();
   __syncthreads();
   double2 pr = cz();
   constexpr int NCW = kEigTB / 4;   // columns per wave
@@ -251,8 +312,9 @@ __global__ __launch_bounds__(256) void k_eig_pass(double2* __restrict__ A, int n
     const int cc = w + 4 * u, gc = C * kEigTB + cc;
     double2 t = cz();
     if ((act >> u) & 1) {
-      if (pend) {
-        a[u] = csub(csub(a[u], cmulc(vpr, cwp[cc])), cmulc(wpr, cvp[cc]));
+      if (np >= 1) {
+        a[u] = csub(csub(a[u], cmulc(var, cwa[cc])), cmulc(war, cva[cc]));
+        if (np >= 2) a[u] = csub(csub(a[u], cmulc(vbr, cwb[cc])), cmulc(wbr, cvb[cc]));
         A[gr + (int64_t)gc * n] = a[u];
       }
       pr = cadd(pr, cmul(a[u], cv[cc]));
@@ -261,6 +323,19 @@ __global__ __launch_bounds__(256) void k_eig_pass(double2* __restrict__ A, int n
     colc[cc][lane] = t;
   }
   rowp[w][lane] = pr;
+  if (rd && R == C && w == 0) {
+    // dots of the pending pair i-1 with v_i over this tile's rows
+    double2 dw = make_double2(war.x * vr.x + war.y * vr.y, war.x * vr.y - war.y * vr.x);
+    double2 dv = make_double2(var.x * vr.x + var.y * vr.y, var.x * vr.y - var.y * vr.x);
+    dw.x = wave_sum(dw.x);
+    dw.y = wave_sum(dw.y);
+    dv.x = wave_sum(dv.x);
+    dv.y = wave_sum(dv.y);
+    if (lane == 0) {
+      dpart[(int64_t)(k * T + R) * 2] = dw;
+      dpart[(int64_t)(k * T + R) * 2 + 1] = dv;
+    }
+  }
   __syncthreads();
   {
     const int cc = tid >> 2, q = tid & 3;
@@ -765,23 +840,38 @@ __global__ __launch_bounds__(256) void k_eig_tw(const double2* __restrict__ Tb, 
 }  // namespace
 
 void launch_eig_step(double2* A, int n, int i, int64_t sA, const double2* part, int64_t sP, double2* vv,
-                     double2* ww, double* d, double* e, double2* tau, int m, hipStream_t s) {
+                     double2* ww, double* d, double* e, double2* tau, const double2* dpart, int m, hipStream_t s) {
+  const int defer = m >= kEigDeferMin;
   const int rs = (n - i + kStepT - 1) / kStepT;   // row slots the rows i..n-1 need
   static_assert(kEigMaxN <= 5 * kStepT, "k_eig_step instantiations");
-  switch (rs) {
-    case 1: hipLaunchKernelGGL(k_eig_step<1>, dim3(m), dim3(kStepT), 0, s, A, n, i, sA, part, sP, vv, ww, d, e, tau); break;
-    case 2: hipLaunchKernelGGL(k_eig_step<2>, dim3(m), dim3(kStepT), 0, s, A, n, i, sA, part, sP, vv, ww, d, e, tau); break;
-    case 3: hipLaunchKernelGGL(k_eig_step<3>, dim3(m), dim3(kStepT), 0, s, A, n, i, sA, part, sP, vv, ww, d, e, tau); break;
-    case 4: hipLaunchKernelGGL(k_eig_step<4>, dim3(m), dim3(kStepT), 0, s, A, n, i, sA, part, sP, vv, ww, d, e, tau); break;
-    default: hipLaunchKernelGGL(k_eig_step<5>, dim3(m), dim3(kStepT), 0, s, A, n, i, sA, part, sP, vv, ww, d, e, tau); break;
+#define DWH_EIG_STEP(R, D) \
+  hipLaunchKernelGGL((k_eig_step<R, D>), dim3(m), dim3(kStepT), 0, s, A, n, i, sA, part, sP, vv, ww, d, e, tau, dpart)
+  if (defer) {
+    switch (rs) {
+      case 1: DWH_EIG_STEP(1, true); break;
+      case 2: DWH_EIG_STEP(2, true); break;
+      case 3: DWH_EIG_STEP(3, true); break;
+      case 4: DWH_EIG_STEP(4, true); break;
+      default: DWH_EIG_STEP(5, true); break;
+    }
+  } else {
+    switch (rs) {
+      case 1: DWH_EIG_STEP(1, false); break;
+      case 2: DWH_EIG_STEP(2, false); break;
+      case 3: DWH_EIG_STEP(3, false); break;
+      case 4: DWH_EIG_STEP(4, false); break;
+      default: DWH_EIG_STEP(5, false); break;
+    }
   }
+#undef DWH_EIG_STEP
 }
 
 void launch_eig_pass(double2* A, int n, int i, int64_t sA, double2* part, int64_t sP, const double2* vv,
-                     const double2* ww, int m, hipStream_t s) {
+                     const double2* ww, double2* dpart, int m, hipStream_t s) {
   const int T = (n + kEigTB - 1) / kEigTB, t0 = (i + 1) / kEigTB, nT = T - t0;
   if (nT <= 0) return;
-  hipLaunchKernelGGL(k_eig_pass, dim3(nT * (nT + 1) / 2, m), dim3(256), 0, s, A, n, i, sA, part, sP, vv, ww, t0);
+  hipLaunchKernelGGL(k_eig_pass, dim3(nT * (nT + 1) / 2, m), dim3(256), 0, s, A, n, i, sA, part, sP, vv, ww, t0,
+                     dpart, T, (int)(m >= kEigDeferMin));
 }
 
 void launch_eig_bisect(const double* d, const double* e, int n, double* E, double* tnorm, int m, hipStream_t s) {

@@ -282,17 +282,20 @@ constexpr int kEigMaxN = 5120;              // rows k_eig_step holds in register
 constexpr double kEigClusterTol = 2.5e-4;   // eigenvalue gap / ||T|| below which vectors are orthogonalised
 constexpr int kEigMaxCluster = 64;          // longest such run (else *bad: vendor fallback)
 // column i of the tridiagonalisation: partial sums -> w_{i-1}, column i -> v_i (d, e, tau)
+// vv: 3 x n per matrix (v_j in slot j % 3), ww: 2 x n (w_j in slot j % 2),
+// dpart: ceil(n / kEigTB) x 2 per matrix (the read-only passes' dots)
 void launch_eig_step(double2* A, int n, int i, int64_t sA, const double2* part, int64_t sP, double2* vv,
-                     double2* ww, double* d, double* e, double2* tau, int m, hipStream_t s);
+                     double2* ww, double* d, double* e, double2* tau, const double2* dpart, int m, hipStream_t s);
 // deferred rank-2 update of column i-1 on the trailing triangle + hemv partials of v_i
 void launch_eig_pass(double2* A, int n, int i, int64_t sA, double2* part, int64_t sP, const double2* vv,
-                     const double2* ww, int m, hipStream_t s);
+                     const double2* ww, double2* dpart, int m, hipStream_t s);
 // eigenvalues ascending into E, ||T|| bound per matrix into tnorm
 void launch_eig_bisect(const double* d, const double* e, int n, double* E, double* tnorm, int m, hipStream_t s);
 // eigenvectors of T into Zt (Zt[r n + j]: component r of vector j), clusters orthonormalised
 void launch_eig_invit(const double* d, const double* e, int n, const double* E, const double* tnorm, double* Zt,
                       double* U0, double* U1, double* U2, int64_t sZ, int* bad, int m, hipStream_t s);
 void launch_eig_zt_to_u(const double* Zt, double2* U, int n, int64_t sZ, int64_t sA, int m, hipStream_t s);
+constexpr int kEigDeferMin = 4;             // batches from this many matrices defer every other rank-2 update
 constexpr int kEigGS = 8;                   // row slices of each block's Gram sum
 // compact-WY T of every reflector block; Gp: m x nblk x kEigGS x kEigNB^2 scratch
 void launch_eig_tfac(const double2* V, int n, int64_t sA, const double2* tau, double2* Gp, double2* Tb, int64_t sT,
