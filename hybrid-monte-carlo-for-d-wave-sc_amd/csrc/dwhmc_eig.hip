@@ -506,28 +506,22 @@ __device__ void invit_one(const double* d, const double* e, int n, double lam, i
         if (r >= n - 1) break;
         const double b = e[r], nd = d[r + 1] - lam, ne = r + 1 < n - 1 ? e[r + 1] : 0.0;
         const double yk1 = yb[u];
-        if (fabs(cu0) >= fabs(b)) {
-          if (cu0 == 0.0) cu0 = small;
-          const double rc = rcp_nr(cu0);
-          const double mu = b * rc;
-          u0[r * ld] = fabs(cu0) < small ? rcp_nr(clamp_small(cu0, small)) : rc;
-          u1[r * ld] = cu1;
-          u2[r * ld] = 0.0;
-          x[r * ld] = yk;
-          cu0 = nd - mu * cu1;
-          cu1 = ne;
-          yk = yk1 - mu * yk;
-        } else {
-          const double rb = rcp_nr(b);
-          const double mu = cu0 * rb;
-          u0[r * ld] = fabs(b) < small ? rcp_nr(clamp_small(b, small)) : rb;
-          u1[r * ld] = nd;
-          u2[r * ld] = ne;
-          x[r * ld] = yk1;
-          cu0 = cu1 - mu * nd;
-          cu1 = -mu * ne;
-          yk = yk - mu * yk1;
-        }
+        // branch-free (lanes hold different shifts): keep = no row interchange
+        const bool keep = fabs(cu0) >= fabs(b);
+        const double c0 = (keep && cu0 == 0.0) ? small : cu0;
+        const double piv = keep ? c0 : b;
+        const double rp = rcp_nr(piv);
+        const double mu = (keep ? b : c0) * rp;
+        u0[r * ld] = rcp_nr(clamp_small(piv, small));
+        u1[r * ld] = keep ? cu1 : nd;
+        u2[r * ld] = keep ? 0.0 : ne;
+        x[r * ld] = keep ? yk : yk1;
+        const double ncu0 = keep ? nd - mu * cu1 : cu1 - mu * nd;
+        const double ncu1 = keep ? ne : -mu * ne;
+        const double nyk = keep ? yk1 - mu * yk : yk - mu * yk1;
+        cu0 = ncu0;
+        cu1 = ncu1;
+        yk = nyk;
       }
     }
     u0[(n - 1) * ld] = 1.0 / clamp_small(cu0, small);
