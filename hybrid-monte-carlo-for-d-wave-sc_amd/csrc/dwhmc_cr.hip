@@ -1351,7 +1351,17 @@ __global__ __launch_bounds__(256) void k_cr_pair_force(
   const int b = blockIdx.x * 8 + (threadIdx.x >> 5), sub = threadIdx.x & 31;
   const int c = blockIdx.y;
   if (b >= 2 * N) return;   // uniform per 32-lane group
-  const int64_t o1 = bond4[4 * b], o2 = bond4[4 * b + 1];
+  const int64_t o1 = bond4[4 * b], o2 = bond4[4 * b + 1], p1 = bond4[4 * b + 2], p2 = bond4[4 * b + 3];
+  // Δ and π of the bond, loaded beside the G entries (not after the reduction)
+  const int64_t o = (int64_t)c * 2 * N + b;
+  double2 d0 = make_double2(0.0, 0.0), p0 = make_double2(0.0, 0.0);
+#ifndef DWHMC_PAIR_PREFETCH
+#define DWHMC_PAIR_PREFETCH 1
+#endif
+  if (DWHMC_PAIR_PREFETCH && sub == 0) {
+    d0 = Delta[o];
+    p0 = Pi[o];
+  }
   double2 Pv = make_double2(0.0, 0.0);
   for (int q = sub; q < P; q += 32) {
     const double2* G = pool + (int64_t)(c * P + q) * item;
@@ -1365,23 +1375,24 @@ __global__ __launch_bounds__(256) void k_cr_pair_force(
     Pv.x += __shfl_xor(Pv.x, off, 32);
     Pv.y += __shfl_xor(Pv.y, off, 32);
   }
-  const int64_t o = (int64_t)c * 2 * N + b;
   double2 dn = make_double2(0.0, 0.0);
   if (sub == 0) {
     Pair[o] = Pv;
-    const double2 d = Delta[o];
+    if (!DWHMC_PAIR_PREFETCH) {   // A/B knob: the loads after the reduction (the round-3 layout)
+      d0 = Delta[o];
+      p0 = Pi[o];
+    }
+    const double2 d = d0;
     const double f = -beta / (2.0 * J);
     const double2 Fv = make_double2(f * (d.x - J * Pv.x), f * (d.y - J * Pv.y));
     F[o] = Fv;
-    kick_drift(Fv, o, Delta, Pi, kick, drift, cap2, flag);
-    if (drift != 0.0) dn = Delta[o];
+    dn = kick_drift_pre(Fv, o, p0, d0, Delta, Pi, kick, drift, cap2, flag);
   }
   if (drift != 0.0) {
     dn.x = 0.5 * __shfl(dn.x, 0, 32);
     dn.y = 0.5 * __shfl(dn.y, 0, 32);
     // an entry is written only by the bond k_cr_fill takes its value from
     // (Dsrc: the one the reference's overwrite order leaves, src/Hamiltonian.jl:68-83)
-    const int64_t p1 = bond4[4 * b + 2], p2 = bond4[4 * b + 3];
     for (int q = sub; q < P; q += 32) {
       double2* G = pool + (int64_t)(c * P + q) * item;
       if (p1 >= 0) G[p1] = dn;

@@ -147,6 +147,24 @@ __device__ __forceinline__ void kick_drift(double2 Fv, int64_t o, double2* __res
   }
 }
 
+// kick_drift with Pi[o] and Delta[o] already loaded (p, d): the caller issues
+// those loads before its own long-latency work; returns the drifted Δ
+__device__ __forceinline__ double2 kick_drift_pre(double2 Fv, int64_t o, double2 p, double2 d,
+                                                  double2* __restrict__ Delta, double2* __restrict__ Pi,
+                                                  double kick, double drift, double cap2, int* __restrict__ flag) {
+  if (kick == 0.0 && drift == 0.0) return d;
+  p.x += kick * Fv.x;
+  p.y += kick * Fv.y;
+  Pi[o] = p;
+  if (drift != 0.0) {
+    d.x += drift * p.x;
+    d.y += drift * p.y;
+    Delta[o] = d;
+    if (d.x * d.x + d.y * d.y > cap2) atomicOr(flag, 1);
+  }
+  return d;
+}
+
 // ---------------------------------------------------------------------------
 // Register-only 16x16 complex no-pivot Gauss-Jordan inversion in one wave.
 // Layout: lane l holds row r = l & 15, columns 4q .. 4q+3 with q = l >> 4.
