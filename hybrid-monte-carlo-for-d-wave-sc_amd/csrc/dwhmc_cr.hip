@@ -1343,14 +1343,18 @@ __global__ __launch_bounds__(64 * NT) void k_cr_tail(double2* __restrict__ pool,
 // small lattices map several bonds onto one entry), resolved at context
 // creation so the G loads wait for one index load, not two.
 // arguments in first-use order (kernel-argument preload)
+#ifndef DWHMC_PF_LANES
+#define DWHMC_PF_LANES 32
+#endif
 __global__ __launch_bounds__(256) void k_cr_pair_force(
     double2* __restrict__ pool, int64_t item, const int64_t* __restrict__ bond4, int N, int P,
     const double* __restrict__ cpole, double2* __restrict__ Delta, double2* __restrict__ Pair,
     double2* __restrict__ F, double2* __restrict__ Pi, double kick, double drift, double cap2,
     int* __restrict__ flag, double beta, double J) {
-  const int b = blockIdx.x * 8 + (threadIdx.x >> 5), sub = threadIdx.x & 31;
+  constexpr int LB = DWHMC_PF_LANES;   // lanes per bond (poles strided over them)
+  const int b = blockIdx.x * (256 / LB) + (threadIdx.x / LB), sub = threadIdx.x % LB;
   const int c = blockIdx.y;
-  if (b >= 2 * N) return;   // uniform per 32-lane group
+  if (b >= 2 * N) return;   // uniform per lane group
   const int64_t o1 = bond4[4 * b], o2 = bond4[4 * b + 1], p1 = bond4[4 * b + 2], p2 = bond4[4 * b + 3];
   // Δ and π of the bond, loaded beside the G entries (not after the reduction)
   const int64_t o = (int64_t)c * 2 * N + b;
@@ -1363,7 +1367,7 @@ __global__ __launch_bounds__(256) void k_cr_pair_force(
     p0 = Pi[o];
   }
   double2 Pv = make_double2(0.0, 0.0);
-  for (int q = sub; q < P; q += 32) {
+  for (int q = sub; q < P; q += LB) {
     const double2* G = pool + (int64_t)(c * P + q) * item;
     const double2 g1 = G[o1], g2 = G[o2];
     const double cq = cpole[q];
@@ -1371,9 +1375,9 @@ __global__ __launch_bounds__(256) void k_cr_pair_force(
     Pv.y += cq * (g1.y + g2.y);
   }
 #pragma unroll
-  for (int off = 16; off > 0; off >>= 1) {
-    Pv.x += __shfl_xor(Pv.x, off, 32);
-    Pv.y += __shfl_xor(Pv.y, off, 32);
+  for (int off = LB / 2; off > 0; off >>= 1) {
+    Pv.x += __shfl_xor(Pv.x, off, LB);
+    Pv.y += __shfl_xor(Pv.y, off, LB);
   }
   double2 dn = make_double2(0.0, 0.0);
   if (sub == 0) {
@@ -1389,11 +1393,11 @@ __global__ __launch_bounds__(256) void k_cr_pair_force(
     dn = kick_drift_pre(Fv, o, p0, d0, Delta, Pi, kick, drift, cap2, flag);
   }
   if (drift != 0.0) {
-    dn.x = 0.5 * __shfl(dn.x, 0, 32);
-    dn.y = 0.5 * __shfl(dn.y, 0, 32);
+    dn.x = 0.5 * __shfl(dn.x, 0, LB);
+    dn.y = 0.5 * __shfl(dn.y, 0, LB);
     // an entry is written only by the bond k_cr_fill takes its value from
     // (Dsrc: the one the reference's overwrite order leaves, src/Hamiltonian.jl:68-83)
-    for (int q = sub; q < P; q += 32) {
+    for (int q = sub; q < P; q += LB) {
       double2* G = pool + (int64_t)(c * P + q) * item;
       if (p1 >= 0) G[p1] = dn;
       if (p2 >= 0) G[p2] = dn;
@@ -1621,7 +1625,8 @@ void launch_cr_pair_force(const CrDims& c, double2* pool, const int64_t* bond4, 
                           double2* Delta, double2* Pair, double2* F, double2* Pi,
                           const KickDrift& kd, double beta, double J, hipStream_t s) {
   const int nc = c.nbatch / c.P;
-  hipLaunchKernelGGL(k_cr_pair_force, dim3((2 * c.N + 7) / 8, nc), dim3(256), 0, s, pool, c.item, bond4, c.N,
+  constexpr int BPW = 256 / DWHMC_PF_LANES;   // bonds per workgroup
+  hipLaunchKernelGGL(k_cr_pair_force, dim3((2 * c.N + BPW - 1) / BPW, nc), dim3(256), 0, s, pool, c.item, bond4, c.N,
                      c.P, cpole, Delta, Pair, F, Pi, kd.kick, kd.drift, kd.cap * kd.cap, kd.flag, beta, J);
 }
 
