@@ -362,7 +362,7 @@ def main(argv=None):
         # per-launch averages.
         replay = schedule(w_sw, min(a.steps, 2 * Nt), Nt)
         replay_steps = sum(n * nt for _, n, nt in replay)
-        names = [dom, "assemble"] + (["cr_inv", "cr_inv_side", "cr_tail", "cr_fused"] if cr else [])
+        names = [dom, "assemble"] + (["cr_inv", "cr_inv_side"] if cr else [])
         ctx.timing_enable(names)
         ctx.timing_reset()
         for f, n, nt in replay:
@@ -427,13 +427,10 @@ def main(argv=None):
                 kfam = [f"k_cr_gemm<{info['block']},1,4>", f"k_cr_gemm<{info['block']},1,1>"]
                 msi, ni, wi = kern["cr_inv"]
                 mss, ns, ws = kern["cr_inv_side"]
-                mst, nt_, wt = kern["cr_tail"]
-                msf, nf, wf = kern["cr_fused"]
                 # the CR path's own algorithmic flops per leapfrog step (block
-                # products, incl. the side work of the inversion stages, the
-                # coarse tail and the fused BP = 32 launches, and block
-                # inversions at 8 BP^3 each) x the timed steps
-                wall = w + wi + ws + wt + wf
+                # products, incl. the side work of the inversion stages, and
+                # block inversions at 8 BP^3 each) x the timed steps
+                wall = w + wi + ws
                 rec["alg_tflops"] = wall / replay_steps * a.steps * world / el / 1e12
                 rec["alg_flops_per_step"] = wall / replay_steps / a.chains
                 # the whole leapfrog step against the fp64 MFMA peak (north_star: >= 0.30 at L=32)
@@ -456,22 +453,6 @@ def main(argv=None):
                                           "avg_launch_us": 1000.0 * mss / ns,
                                           "flops_per_launch": ws / ns,
                                           "ms_per_step": mss / replay_steps}
-                if nf:
-                    rec["cr_fused"] = {"bound": "latency", "kernel": f"k_cr_fused<{info['block']},...>",
-                                       "what": "two consecutive CR stages per launch (BP = 32): an inversion "
-                                               "with its V/W products, or a backward G_ae/G_ce -> G_ee pair",
-                                       "launches_per_step": nf / replay_steps,
-                                       "avg_launch_us": 1000.0 * msf / nf,
-                                       "flops_per_launch": wf / nf,
-                                       "ms_per_step": msf / replay_steps}
-                if nt_:
-                    rec["cr_tail"] = {"bound": "latency", "kernel": "k_cr_tail<4>",
-                                      "what": "the coarse CR levels' stages in one launch with device-wide "
-                                              "stage barriers",
-                                      "launches_per_step": nt_ / replay_steps,
-                                      "avg_launch_us": 1000.0 * mst / nt_,
-                                      "flops_per_launch": wt / nt_,
-                                      "ms_per_step": mst / replay_steps}
             else:
                 nb = -(-info["N"] // 64)                 # GJ block steps; odd nb ends with one rank-64 step
                 kname = "k_gj_update<2>" if nb % 2 == 0 else "k_gj_update<2>+<0>"

@@ -91,7 +91,6 @@ SIGNATURES = {
     "dwh_debug_level0": (C.c_int, [_P, _I64, _I64, _I32, _P, _P]),
     "dwh_debug_cr_plan_check": (C.c_int, [_I64, _I64, _I64, _I32, _I32, _P]),
     "dwh_debug_cr_plan_flops": (C.c_int, [_I64, _I64, _I64, _I32, _I32, _P]),
-    "dwh_debug_cr_fusion": (C.c_int, [_I64, _I64, _I64, _P]),
     "dwh_debug_h_bound": (C.c_int, [_I64, _I64, _D, _D, _D, _P, _P, _I64, _P, _P]),
     "dwh_selftest_mfma": (C.c_int, [_I32]),
 }

@@ -82,11 +82,11 @@ const PoleTable* pole_table(std::string* err) {
 
 enum TimerName {
   T_GJ_UPDATE = 0, T_GJ_PIVOT, T_ASSEMBLE, T_CONTRACT, T_STEP, T_GJ_EDGE, T_CR_GEMM, T_CR_INV, T_CR_INVSIDE,
-  T_CR_TAIL, T_CR_FUSED, T_EIG_OWN, T_EIG_VENDOR, T_COUNT
+  T_EIG_OWN, T_EIG_VENDOR, T_COUNT
 };
 const char* kTimerNames[T_COUNT] = {"gj_update", "gj_pivot", "assemble", "contract",
                                     "step",      "gj_edge",  "cr_gemm",  "cr_inv",
-                                    "cr_inv_side", "cr_tail", "cr_fused",
+                                    "cr_inv_side",
                                     "eig_own",   "eig_vendor"};   // eigensolves (work: matrices)
 
 enum Algo { ALGO_DENSE = 0, ALGO_CR = 1, ALGO_EIG = 2 };
@@ -106,30 +106,9 @@ struct CrStage {
   int l0 = 0;           // inversions: level 0 from the static R = A^-1 blocks (k_cr_inv0)
 };
 
-// a run of consecutive small stages executed by one k_cr_tail launch
-struct CrTailSeg {
-  int first, n;   // stages [first, first + n)
-  int tfirst;     // their CrTailStage entries in CrPlan::tail_stages
-  int grid;       // resident workgroups
-};
-
-// two consecutive stages run as one k_cr_fused launch (BP = 32, build_cr_fusion)
-struct CrFuse {
-  int first, nst;       // stages [first, first + nst)
-  int mode;             // 1: inversion + products; 2: two product stages; 3: products + inversion + products
-  int gfirst, ngrp;     // CrPlan::groups
-  int pfirst, nplain;   // plain tiles (first stage, no group) in CrPlan::ftiles
-  int r0, r1, r2;       // tile rounds of the phases
-};
-
 struct CrPlan {
   int nblk = 0;
   std::vector<CrStage> stages;
-  std::vector<CrFuse> fuses;
-  std::vector<dwh::CrGroup> groups;
-  std::vector<dwh::CrTile> ftiles;
-  std::vector<CrTailSeg> tails;
-  std::vector<dwh::CrTailStage> tail_stages;
   std::vector<dwh::CrTask> tasks;
   std::vector<dwh::CrTile> tiles16;          // per product stage: its 16 x 16 tiles with their operands
   std::vector<int> inv_blk, inv_dst, inv_slot;   // inversion source / destination block, ln|det| slot
@@ -535,285 +514,6 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol, bool 
   return pl;
 }
 
-// Coarse tail: runs of >= 2 consecutive stages of at most two rounds of the
-// resident grid each (cap workgroups: occupancy x CUs; DWHMC_CR_TAIL_MAX sets
-// the per-stage limit) become one k_cr_tail launch on min(largest stage, cap)
-// workgroups.  Level-0 inversions (k_cr_inv0) and product stages with another
-// tile configuration stay separate launches.
-void build_cr_tails(CrPlan& pl, int nbatch, int cap) {
-  int maxwg = 2 * cap;
-  if (const char* e = std::getenv("DWHMC_CR_TAIL_MAX")) maxwg = std::atoi(e);
-  // the first inversion stage carries the site guard (cr_enqueue): it always
-  // stays a launch of its own
-  int first_inv = -1;
-  for (size_t k = 0; k < pl.stages.size() && first_inv < 0; ++k)
-    if (pl.stages[k].kind == 0) first_inv = (int)k;
-  auto nwg = [&](const CrStage& st) -> int {
-    if (st.kind == 0) {
-      if (st.l0 || &st - pl.stages.data() == first_inv) return -1;
-      const int side = st.ntiles > 0 ? (nbatch * st.ntiles * st.maxt32 + 3) / 4 : 0;
-      return st.n * nbatch + side;
-    }
-    if (st.cfg.ts != 16 || st.cfg.ksplit != 4) return -1;
-    return nbatch * st.ntiles;
-  };
-  size_t i = 0;
-  while (i < pl.stages.size()) {
-    size_t j = i;
-    int gmax = 0;
-    while (j < pl.stages.size()) {
-      const int w = nwg(pl.stages[j]);
-      if (w < 0 || w > maxwg) break;
-      gmax = std::max(gmax, w);
-      ++j;
-    }
-    if (j - i >= 2) {
-      pl.tails.push_back(CrTailSeg{(int)i, (int)(j - i), (int)pl.tail_stages.size(), std::max(1, std::min(gmax, cap))});
-      for (size_t k = i; k < j; ++k) {
-        const CrStage& st = pl.stages[k];
-        dwh::CrTailStage t{};
-        if (st.kind == 0) {
-          t.inv_first = st.first;
-          t.ninv = st.n;
-          t.side_first = st.tfirst;
-          t.nside = st.ntiles;
-          t.side_maxt = st.maxt32;
-        } else {
-          t.tl_first = st.tfirst;
-          t.ntl = st.ntiles;
-          t.neg = st.sg < 0 ? 1 : 0;
-        }
-        pl.tail_stages.push_back(t);
-      }
-      i = j;
-    } else {
-      i = std::max(j, i + 1);
-    }
-  }
-}
-
-// Launch fusion of the BP = 32 path (k_cr_fused, dwhmc_cr.hip): consecutive
-// stages become one launch when their work splits into groups, one
-// workgroup each, that read the blocks the launch writes only inside their
-// own group —
-//   mode 1: an inversion stage I (no side work) + the product stage V after
-//     it, every V tile reading exactly one block I inverts (the forward
-//     V1/V2/W1/W2; the coarsest backward products of the final inversion);
-//   mode 3: a product stage D + I + V: group k also computes, before its
-//     inversion, the Schur complement I inverts and the U'/L' blocks its V
-//     tiles read (one launch per forward level);
-//   mode 2: two product stages A, B, every A task read by at most one B task
-//     (backward: G_ae, G_ce, then G_ee of the same eliminated block).
-// The first stage's tiles no group claims run as plain tiles of the launch.
-// A candidate is dropped when two concurrent groups (or a group and a plain
-// tile) would share a written block, or a phase needs more than two rounds
-// of tiles.  Candidates are taken greedily from the first stage, the
-// three-stage form first.
-struct FuseTry {
-  int mode = 0, nst = 0;
-  std::vector<std::vector<dwh::CrTile>> ph0, ph1, ph2;   // per group
-  std::vector<int> ginv;
-  std::vector<dwh::CrTile> plainv;
-  int r0 = 0, r1 = 0, r2 = 0;
-};
-
-bool tile_reads(const dwh::CrTile& t, int b) {
-  if (t.cin == b) return true;
-  for (int h = 0; h < t.nt; ++h)
-    if (t.a[h] == b || t.b[h] == b) return true;
-  return false;
-}
-
-void tile_blocks(const dwh::CrTile& t, std::vector<int>& r) {
-  if (t.cin >= 0) r.push_back(t.cin);
-  for (int h = 0; h < t.nt; ++h) {
-    r.push_back(t.a[h]);
-    r.push_back(t.b[h]);
-  }
-}
-
-// concurrent groups / plain tiles of a fused launch: no block written by one
-// is read or written by another (inversion entries: inv_blk read, inv_dst
-// written); nullptr if fine
-const char* fuse_conflict(const CrPlan& pl, int inv_first, const FuseTry& f) {
-  const int ng = (int)f.ph1.size();
-  std::vector<std::vector<int>> R(ng + 1), W(ng + 1);
-  for (int g = 0; g <= ng; ++g) {
-    auto add = [&](const std::vector<dwh::CrTile>& v) {
-      for (const dwh::CrTile& t : v) {
-        tile_blocks(t, R[g]);
-        W[g].push_back(t.out);
-      }
-    };
-    if (g < ng) {
-      add(f.ph0[g]);
-      add(f.ph1[g]);
-      add(f.ph2[g]);
-      if (f.ginv[g] >= 0) {
-        R[g].push_back(pl.inv_blk[inv_first + f.ginv[g]]);
-        W[g].push_back(pl.inv_dst[inv_first + f.ginv[g]]);
-      }
-    } else {
-      add(f.plainv);
-    }
-  }
-  for (int g = 0; g <= ng; ++g)
-    for (int h = 0; h <= ng; ++h) {
-      if (g == h) continue;
-      for (int w : W[h])
-        if (std::find(R[g].begin(), R[g].end(), w) != R[g].end() ||
-            std::find(W[g].begin(), W[g].end(), w) != W[g].end())
-          return "block shared by concurrent groups";
-    }
-  return nullptr;
-}
-
-bool try_fuse(const CrPlan& pl, size_t si, int mode, FuseTry& f) {
-  constexpr int NW = 8;
-  const size_t nst = mode == 3 ? 3 : 2;
-  if (si + nst > pl.stages.size()) return false;
-  f = FuseTry{};
-  f.mode = mode;
-  f.nst = (int)nst;
-  auto tiles = [&](const CrStage& st) { return pl.tiles16.data() + st.tfirst; };
-  auto signed_tile = [](dwh::CrTile t, double sg) {
-    t.neg = sg < 0 ? 1 : 0;
-    return t;
-  };
-  int T0 = NW, T1 = NW, T2 = NW / 4;
-  if (mode == 1 || mode == 3) {
-    const CrStage& I = pl.stages[si + (mode == 3)];
-    const CrStage& V = pl.stages[si + (mode == 3) + 1];
-    if (I.kind != 0 || I.ntiles > 0 || I.l0 || V.kind != 1) return false;
-    const dwh::CrTile* vt = tiles(V);
-    f.ph0.resize(I.n);
-    f.ph1.resize(I.n);
-    f.ph2.resize(I.n);
-    for (int k = 0; k < I.n; ++k) f.ginv.push_back(k);
-    for (int t = 0; t < V.ntiles; ++t) {
-      int hit = 0, g = -1;
-      for (int k = 0; k < I.n; ++k)
-        if (tile_reads(vt[t], pl.inv_dst[I.first + k])) {
-          ++hit;
-          g = k;
-        }
-      if (hit != 1) return false;
-      f.ph1[g].push_back(signed_tile(vt[t], V.sg));
-    }
-    if (mode == 3) {
-      const CrStage& D = pl.stages[si];
-      if (D.kind != 1) return false;
-      const dwh::CrTile* dt = tiles(D);
-      std::map<int, int> owner;   // D output block -> group
-      auto claim = [&](int blk, int g) {
-        auto it = owner.find(blk);
-        if (it == owner.end()) owner[blk] = g;
-        return it == owner.end() || it->second == g;
-      };
-      bool any = false;
-      for (int t = 0; t < D.ntiles; ++t)
-        for (int k = 0; k < I.n; ++k) {
-          bool need = dt[t].out == pl.inv_blk[I.first + k];
-          for (const dwh::CrTile& x : f.ph1[k]) need = need || tile_reads(x, dt[t].out);
-          if (need) {
-            if (!claim(dt[t].out, k)) return false;
-            any = true;
-          }
-        }
-      if (!any) return false;
-      for (int t = 0; t < D.ntiles; ++t) {
-        auto it = owner.find(dt[t].out);
-        if (it == owner.end()) f.plainv.push_back(signed_tile(dt[t], D.sg));
-        else f.ph0[it->second].push_back(signed_tile(dt[t], D.sg));
-      }
-    }
-  } else {
-    const CrStage& A = pl.stages[si];
-    const CrStage& B = pl.stages[si + 1];
-    if (A.kind != 1 || B.kind != 1) return false;
-    T1 = NW / 2;
-    const dwh::CrTile* at = tiles(A);
-    const dwh::CrTile* bt = tiles(B);
-    std::map<int, int> bout_group, aout_owner;
-    for (int t = 0; t < B.ntiles; ++t)
-      if (!bout_group.count(bt[t].out)) bout_group[bt[t].out] = (int)bout_group.size();
-    const size_t ng = bout_group.size();
-    f.ph0.resize(ng);
-    f.ph1.resize(ng);
-    f.ph2.resize(ng);
-    f.ginv.assign(ng, -1);
-    for (int t = 0; t < B.ntiles; ++t) {
-      const int g = bout_group[bt[t].out];
-      f.ph2[g].push_back(signed_tile(bt[t], B.sg));
-      for (int u = 0; u < A.ntiles; ++u)
-        if (tile_reads(bt[t], at[u].out)) {
-          auto it = aout_owner.find(at[u].out);
-          if (it == aout_owner.end()) aout_owner[at[u].out] = g;
-          else if (it->second != g) return false;
-        }
-    }
-    for (int u = 0; u < A.ntiles; ++u) {
-      auto it = aout_owner.find(at[u].out);
-      if (it == aout_owner.end()) f.plainv.push_back(signed_tile(at[u], A.sg));
-      else f.ph1[it->second].push_back(signed_tile(at[u], A.sg));
-    }
-  }
-  if (f.ph1.empty()) return false;
-  int m0 = 0, m1 = 0, m2 = 0;
-  for (size_t g = 0; g < f.ph1.size(); ++g) {
-    m0 = std::max(m0, (int)f.ph0[g].size());
-    m1 = std::max(m1, (int)f.ph1[g].size());
-    m2 = std::max(m2, (int)f.ph2[g].size());
-  }
-  f.r0 = (m0 + T0 - 1) / T0;
-  f.r1 = (m1 + T1 - 1) / T1;
-  f.r2 = (m2 + T2 - 1) / T2;
-  if (f.r0 > 2 || f.r1 > 2 || f.r2 > 2) return false;
-  const int inv_first = mode == 2 ? 0 : pl.stages[si + (mode == 3)].first;
-  return fuse_conflict(pl, inv_first, f) == nullptr;
-}
-
-// modes: bit m-1 allows mode m (DWHMC_CR_FUSE)
-void build_cr_fusion(CrPlan& pl, int modes = 7) {
-  size_t si = 0;
-  while (si < pl.stages.size()) {
-    FuseTry f;
-    if (!((modes & 4) && try_fuse(pl, si, 3, f)) && !((modes & 1) && try_fuse(pl, si, 1, f)) &&
-        !((modes & 2) && try_fuse(pl, si, 2, f))) {
-      ++si;
-      continue;
-    }
-    CrFuse cf{};
-    cf.first = (int)si;
-    cf.nst = f.nst;
-    cf.mode = f.mode;
-    cf.gfirst = (int)pl.groups.size();
-    cf.ngrp = (int)f.ph1.size();
-    cf.r0 = f.r0;
-    cf.r1 = f.r1;
-    cf.r2 = f.r2;
-    for (size_t g = 0; g < f.ph1.size(); ++g) {
-      dwh::CrGroup G{};
-      G.inv = f.ginv[g];
-      G.p0 = (int)pl.ftiles.size();
-      G.n0 = (int)f.ph0[g].size();
-      pl.ftiles.insert(pl.ftiles.end(), f.ph0[g].begin(), f.ph0[g].end());
-      G.p1 = (int)pl.ftiles.size();
-      G.n1 = (int)f.ph1[g].size();
-      pl.ftiles.insert(pl.ftiles.end(), f.ph1[g].begin(), f.ph1[g].end());
-      G.p2 = (int)pl.ftiles.size();
-      G.n2 = (int)f.ph2[g].size();
-      pl.ftiles.insert(pl.ftiles.end(), f.ph2[g].begin(), f.ph2[g].end());
-      pl.groups.push_back(G);
-    }
-    cf.pfirst = (int)pl.ftiles.size();
-    cf.nplain = (int)f.plainv.size();
-    pl.ftiles.insert(pl.ftiles.end(), f.plainv.begin(), f.plainv.end());
-    pl.fuses.push_back(cf);
-    si += f.nst;
-  }
-}
-
 struct TimingRec {
   int name;
   hipEvent_t a, b;
@@ -891,17 +591,9 @@ struct dwh_ctx {
   double2* bpool = nullptr;   // CR block pool (nbatch x nblk blocks)
   dwh::CrTask* d_tasks = nullptr;
   dwh::CrTile* d_tiles16 = nullptr;
-  dwh::CrGroup* d_groups = nullptr;   // fused launches (BP = 32)
-  dwh::CrTile* d_ftiles = nullptr;
   double* efpart = nullptr;     // per (chain, pole) E_f / Tr G22 partials
   unsigned* efdone = nullptr;   // per chain: pole blocks done (k_cr_fermion_energy)
   int *d_inv_blk = nullptr, *d_inv_dst = nullptr, *d_inv_slot = nullptr, *d_inv0_r = nullptr;
-  // coarse tail (k_cr_tail): stage descriptors, barrier counter (monotonic; its
-  // value before the next launch in tail_base), timeout flag
-  dwh::CrTailStage* d_tail_stages = nullptr;
-  unsigned long long* d_tail_bar = nullptr;
-  unsigned long long tail_base = 0;
-  int* d_tail_err = nullptr;
   double* ldA = nullptr;   // static ln|det| of the Δ = 0 level-0 blocks (= 2 ln|det A|) per slot
   int64_t *d_doff = nullptr, *d_off_ph = nullptr;
   int64_t* d_bond4 = nullptr;   // k_cr_pair_force: per bond its G12 offsets and pairing-entry offsets
@@ -1123,45 +815,11 @@ void cr_enqueue(dwh_ctx* ctx) {
     ctx->pairing_in_pool = false;
   }
   const CrPlan& plan = ctx->plan;
-  size_t next_tail = 0, next_fuse = 0;
   // the site guard rides on the first (level-0) inversion launch: every
   // factorised Δ passes through it
   dwh::SiteGuard guard;
   if (ctx->site_guard) guard = dwh::SiteGuard{ctx->Delta, ctx->site4, 4.0 * ctx->delta_cap, ctx->flag};
   for (size_t si = 0; si < plan.stages.size(); ++si) {
-    if (next_tail < plan.tails.size() && plan.tails[next_tail].first == (int)si) {
-      const CrTailSeg& tg = plan.tails[next_tail++];
-      double work = 0;
-      for (int k = 0; k < tg.n; ++k) {
-        const CrStage& st = plan.stages[si + k];
-        work += (st.kind == 0 ? st.n * bp3 : 0.0) + st.flops * c.nbatch;
-      }
-      Scope s(ctx, T_CR_TAIL, work);
-      dwh::launch_cr_tail(c, ctx->bpool, ctx->d_inv_blk, ctx->d_inv_dst, ctx->d_inv_slot, ctx->ldpart, ctx->d_tasks,
-                          ctx->d_tiles16, ctx->d_tail_stages + tg.tfirst, tg.n, tg.grid, ctx->d_tail_bar,
-                          ctx->tail_base, ctx->d_tail_err, ctx->stream);
-      ctx->tail_base += (unsigned long long)(tg.n - 1) * tg.grid;
-      si += tg.n - 1;
-      continue;
-    }
-    if (next_fuse < plan.fuses.size() && plan.fuses[next_fuse].first == (int)si) {
-      const CrFuse& f = plan.fuses[next_fuse++];
-      double work = 0;
-      int o = 0;
-      for (int k = 0; k < f.nst; ++k) {
-        const CrStage& st = plan.stages[si + k];
-        work += st.kind == 0 ? st.n * bp3 : st.flops * c.nbatch;
-        if (st.kind == 0) o = st.first;
-      }
-      Scope s(ctx, T_CR_FUSED, work);
-      const bool inv = f.mode != 2;
-      dwh::launch_cr_fused(c, ctx->bpool, ctx->d_inv_blk + o, ctx->d_inv_dst + o, ctx->d_inv_slot + o, ctx->ldpart,
-                           ctx->d_groups + f.gfirst, f.ngrp, ctx->d_ftiles, ctx->d_ftiles + f.pfirst, f.nplain,
-                           f.mode, f.r0, f.r1, f.r2, ctx->stream, inv ? guard : dwh::SiteGuard{});
-      if (inv) guard = dwh::SiteGuard{};
-      si += f.nst - 1;
-      continue;
-    }
     const CrStage& st = plan.stages[si];
     if (st.kind == 0 && st.ntiles > 0) {
       Scope s(ctx, T_CR_INVSIDE, st.n * bp3 + st.flops * c.nbatch);
@@ -1234,14 +892,9 @@ void eig_enqueue(dwh_ctx* ctx) {
                          ctx->stream);
 }
 
-// after a stream synchronisation: a coarse-tail barrier timeout (CR); an
-// enqueue-time refusal, then zheevd's convergence flags (eig)
+// after a stream synchronisation (eig): an enqueue-time refusal, then the
+// eigensolver's convergence flags
 int eig_check(dwh_ctx* ctx) {
-  if (ctx->d_tail_err) {
-    int e = 0;
-    HIPCHECK(ctx, hipMemcpy(&e, ctx->d_tail_err, sizeof(int), hipMemcpyDeviceToHost));
-    if (e) return fail(ctx, DWH_ERR_HIP, "k_cr_tail: a stage barrier timed out (workgroups not co-resident)");
-  }
   if (ctx->algo != ALGO_EIG) return DWH_OK;
   if (ctx->async_rc != DWH_OK) {
     const int rc = ctx->async_rc;
@@ -1780,26 +1433,9 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
       c.nbatch = d.nbatch;
       c.nblk = ctx->plan.nblk;
       c.item = (int64_t)c.nblk * (BP / 2) * BP;
-      // DWHMC_CR_INV2=1: BP = 64 inversions by particle-hole 2 x 2 pivots (k_cr_inv2)
-      const char* ei = std::getenv("DWHMC_CR_INV2");
-      c.inv2 = BP == 64 && ei && *ei == '1';
       d.nld = (int)Ly;
       for (CrStage& st : ctx->plan.stages)
         if (st.kind == 1) st.cfg = dwh::cr_gemm_config(c, st.n, st.maxt32, st.maxt16, st.ntmax, st.ntiles);
-      // DWHMC_CR_TAIL=1: the coarse tail in one k_cr_tail launch (measured slower
-      // on MI355X: a device-wide stage barrier costs more than a launch boundary,
-      // profiles/r02_exp_cr_coarse_tail_grid_barrier.txt; off by default)
-      const char* et = std::getenv("DWHMC_CR_TAIL");
-      if (dwh::cr_supported_tail(BP) && et && *et == '1') {
-        const int occ = dwh::cr_tail_occupancy();
-        if (occ > 0) build_cr_tails(ctx->plan, d.nbatch, occ * ncu);
-      }
-      // DWHMC_CR_FUSE=m (bitmask of fusion modes 1 / 2 / 3 = bits 0 / 1 / 2):
-      // BP = 32 stages fused into k_cr_fused launches; default off (measured no
-      // faster than separate launches)
-      const char* ef = std::getenv("DWHMC_CR_FUSE");
-      const int fmodes = ef ? std::atoi(ef) : 0;
-      if (dwh::cr_supported_fuse(BP) && fmodes > 0) build_cr_fusion(ctx->plan, fmodes);
       if (const char* e = std::getenv("DWHMC_CR_PLAN_DUMP"); e && *e == '1') {
         int i = 0;
         for (const CrStage& st : ctx->plan.stages) {
@@ -1811,12 +1447,6 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
                          i, st.n, st.maxt32, st.maxt16, st.ntmax, st.flops, st.cfg.ts, st.cfg.ksplit, st.ntiles);
           ++i;
         }
-        for (const CrTailSeg& tg : ctx->plan.tails)
-          std::fprintf(stderr, "cr tail: stages %d..%d in one launch, %d workgroups\n", tg.first, tg.first + tg.n - 1,
-                       tg.grid);
-        for (const CrFuse& f : ctx->plan.fuses)
-          std::fprintf(stderr, "cr fused: stages %d..%d mode %d groups=%d plain=%d rounds=%d,%d,%d\n", f.first,
-                       f.first + f.nst - 1, f.mode, f.ngrp, f.nplain, f.r0, f.r1, f.r2);
       }
     }
   }
@@ -1855,10 +1485,6 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     ALLOC(bpool, (size_t)d.nbatch * ctx->cr.item);
     ALLOC(d_tasks, pl.tasks.size());
     ALLOC(d_tiles16, pl.tiles16.size());
-    if (!pl.fuses.empty()) {
-      ALLOC(d_groups, pl.groups.size());
-      ALLOC(d_ftiles, pl.ftiles.size());
-    }
     ALLOC(efpart, 2 * (size_t)d.nbatch);
     ALLOC(efdone, (size_t)d.nc);
     ALLOC(d_inv_blk, pl.inv_blk.size());
@@ -1871,11 +1497,6 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     ALLOC(d_bond4, 4 * bij.size());
     ALLOC(d_fill_all, pl.fill_all.size());
     ALLOC(d_fill_step, pl.fill_step.size());
-    if (!pl.tails.empty()) {
-      ALLOC(d_tail_stages, pl.tail_stages.size());
-      ALLOC(d_tail_bar, 1);
-      ALLOC(d_tail_err, 1);
-    }
   }
   if (ctx->algo == ALGO_DENSE) {
     ALLOC(Dv, (size_t)d.nc * N * kSlots);
@@ -1958,10 +1579,6 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     const CrPlan& pl = ctx->plan;
     UP(d_tasks, pl.tasks.data(), pl.tasks.size());
     UP(d_tiles16, pl.tiles16.data(), pl.tiles16.size());
-    if (!pl.fuses.empty()) {
-      UP(d_groups, pl.groups.data(), pl.groups.size());
-      UP(d_ftiles, pl.ftiles.data(), pl.ftiles.size());
-    }
     UP(d_inv_blk, pl.inv_blk.data(), pl.inv_blk.size());
     UP(d_inv_dst, pl.inv_dst.data(), pl.inv_dst.size());
     UP(d_inv_slot, pl.inv_slot.data(), pl.inv_slot.size());
@@ -1971,11 +1588,6 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     UP(d_bond4, bond4.data(), bond4.size());
     UP(d_fill_all, pl.fill_all.data(), pl.fill_all.size());
     UP(d_fill_step, pl.fill_step.data(), pl.fill_step.size());
-    if (!pl.tails.empty()) {
-      UP(d_tail_stages, pl.tail_stages.data(), pl.tail_stages.size());
-      (void)hipMemsetAsync(ctx->d_tail_bar, 0, sizeof(unsigned long long), s);
-      (void)hipMemsetAsync(ctx->d_tail_err, 0, sizeof(int), s);
-    }
   }
 #undef UP
   // zeroed cache, like initialize_cache (src/Types.jl:182-212): P = 0, E_f = 0
@@ -2924,6 +2536,9 @@ int dwh_hmc_finish(dwh_ctx* ctx, const uint8_t* accepted) {
 int dwh_load_draws(dwh_ctx* ctx, int64_t nsweeps, const dwh_c128* noise, const double* uniform) {
   if (!ctx || nsweeps < 1 || !noise || !uniform) return fail(ctx, DWH_ERR_ARG, "bad argument");
   HIPCHECK(ctx, hipSetDevice(ctx->device));
+  // pending throughput sweeps replay from the loaded draws after a guard trip
+  // (settle): finish them before the draws are replaced
+  SETTLE(ctx);
   const Dims& d = ctx->d;
   const size_t nbond = (size_t)d.nc * 2 * d.N;
   if (nsweeps > ctx->ndraws) {
@@ -3083,100 +2698,6 @@ extern "C" {
 // not), no block is read and written in one stage except a task's own
 // accumulate input, no two tasks of a stage write the same block, and every
 // block the force / E_f gather reads was written.
-// The fused launches of a BP = 32 plan (build_cr_fusion) against the stages
-// each replaces: the launch's tiles are exactly the product stages' tiles,
-// its inversions the inversion stage's, and groups running concurrently
-// neither write the same block nor read a block another group or a plain
-// tile writes (inside a group the phases run in stage order).  Returns an
-// error message or nullptr.
-static const char* verify_cr_fusion(const CrPlan& plan, int BP) {
-  if (!dwh::cr_supported_fuse(BP)) return nullptr;
-  CrPlan pl = plan;
-  build_cr_fusion(pl);
-  static thread_local char buf[256];
-  for (const CrFuse& f : pl.fuses) {
-    std::multiset<std::tuple<int, int, int>> want, got;
-    auto key = [](const dwh::CrTile& t) { return std::make_tuple(t.out, t.tr, t.tc); };
-    int inv_first = -1, ninv = 0;
-    for (int k = 0; k < f.nst; ++k) {
-      const CrStage& st = pl.stages[f.first + k];
-      if (st.kind == 0) {
-        if (inv_first >= 0 || st.ntiles > 0) return "fused launch with two or side-work inversion stages";
-        inv_first = st.first;
-        ninv = st.n;
-      } else {
-        for (int t = 0; t < st.ntiles; ++t) want.insert(key(pl.tiles16[st.tfirst + t]));
-      }
-    }
-    if ((f.mode == 2) != (inv_first < 0)) return "fused launch mode does not match its stages";
-    std::vector<std::vector<int>> R(f.ngrp + 1), W(f.ngrp + 1);   // last: plain tiles
-    std::vector<int> seen_inv;
-    auto add = [&](int g, int p, int n) {
-      for (int t = 0; t < n; ++t) {
-        const dwh::CrTile& x = pl.ftiles[p + t];
-        got.insert(key(x));
-        tile_blocks(x, R[g]);
-        W[g].push_back(x.out);
-      }
-    };
-    for (int g = 0; g < f.ngrp; ++g) {
-      const dwh::CrGroup& G = pl.groups[f.gfirst + g];
-      if ((G.inv >= 0) != (inv_first >= 0) || G.inv >= ninv) return "fused group without its inversion";
-      if (G.inv >= 0) {
-        seen_inv.push_back(G.inv);
-        R[g].push_back(pl.inv_blk[inv_first + G.inv]);
-        W[g].push_back(pl.inv_dst[inv_first + G.inv]);
-      }
-      add(g, G.p0, G.n0);
-      add(g, G.p1, G.n1);
-      add(g, G.p2, G.n2);
-    }
-    add(f.ngrp, f.pfirst, f.nplain);
-    std::sort(seen_inv.begin(), seen_inv.end());
-    for (int k = 0; k < (int)seen_inv.size(); ++k)
-      if (seen_inv[k] != k) return "fused launch does not run every inversion once";
-    if (inv_first >= 0 && (int)seen_inv.size() != ninv) return "fused launch does not run every inversion once";
-    if (want != got) {
-      std::snprintf(buf, sizeof buf, "fused stages %d..%d do not cover the stages' tiles", f.first,
-                    f.first + f.nst - 1);
-      return buf;
-    }
-    for (int g = 0; g <= f.ngrp; ++g)
-      for (int h = 0; h <= f.ngrp; ++h) {
-        if (g == h) continue;
-        for (int w : W[h])
-          if (std::find(R[g].begin(), R[g].end(), w) != R[g].end() ||
-              std::find(W[g].begin(), W[g].end(), w) != W[g].end()) {
-            std::snprintf(buf, sizeof buf, "fused stages %d..%d: block %d shared by concurrent groups", f.first,
-                          f.first + f.nst - 1, w);
-            return buf;
-          }
-      }
-  }
-  return nullptr;
-}
-
-int dwh_debug_cr_fusion(int64_t Lx, int64_t Ly, int64_t nbatch, int64_t* out) {
-  if (Lx < 1 || Ly < 1 || nbatch < 1 || !out) return fail(nullptr, DWH_ERR_ARG, "bad lattice / batch / output");
-  const int BP = (int)(2 * ((Lx + 15) / 16 * 16));
-  if (!dwh::cr_supported_bp(BP)) return fail(nullptr, DWH_ERR_ARG, "lattice row too wide for the CR path");
-  std::vector<int> Dcol = nn_pairing_cols((int)Lx, (int)Ly);
-  CrPlan pl = build_cr_plan((int)Lx, (int)Ly, BP, Dcol, dwh::cr_supported_side(BP), (int)nbatch, 256,
-                            dwh::cr_supported_inv0(BP));
-  if (dwh::cr_supported_fuse(BP)) build_cr_fusion(pl);
-  int64_t launches = (int64_t)pl.stages.size(), nm[4] = {0, 0, 0, 0};
-  for (const CrFuse& f : pl.fuses) {
-    launches -= f.nst - 1;
-    nm[f.mode]++;
-  }
-  out[0] = (int64_t)pl.stages.size();
-  out[1] = launches;
-  out[2] = nm[1];
-  out[3] = nm[2];
-  out[4] = nm[3];
-  return DWH_OK;
-}
-
 int dwh_debug_cr_plan_check(int64_t Lx, int64_t Ly, int64_t nbatch, int32_t side, int32_t inv0, int64_t* stats) {
   if (Lx < 1 || Ly < 1 || nbatch < 1) return fail(nullptr, DWH_ERR_ARG, "bad lattice / batch");
   std::vector<int> Dcol = nn_pairing_cols((int)Lx, (int)Ly);
@@ -3245,7 +2766,6 @@ int dwh_debug_cr_plan_check(int64_t Lx, int64_t Ly, int64_t nbatch, int32_t side
       if (w.first >= 0 && w.first < pl.nblk && written[w.first] == -1) written[w.first] = si;
     }
   }
-  if (const char* e = verify_cr_fusion(pl, BP)) return fail(nullptr, DWH_ERR_STATE, e);
   const int64_t BB = (int64_t)(BP / 2) * BP;
   for (int64_t o : pl.goff)
     if (o >= 0 && written[o / BB] == -1) return fail(nullptr, DWH_ERR_STATE, "force gather reads an unwritten block");

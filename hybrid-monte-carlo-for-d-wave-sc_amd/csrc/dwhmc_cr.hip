@@ -225,10 +225,8 @@ __device__ __forceinline__ void mma16_3m_T(d4& cr, d4& ci, const double2* A, con
 }
 
 // one workgroup (NT waves) inverts block blk[li] of batch item bi; pan / ldw:
-// the caller's LDS (double-buffered panel, per-wave ln|det| partials).  NWG:
-// waves of the workgroup (k_cr_fused: NWG > NT, the extra waves only join the
-// barriers)
-template <int NT, int NWG = NT>
+// the caller's LDS (double-buffered panel, per-wave ln|det| partials)
+template <int NT>
 __device__ __forceinline__ void cr_inv_wg(double2* __restrict__ pool, int64_t item, int bi, int li,
                                           const int* __restrict__ blk, const int* __restrict__ dst,
                                           const int* __restrict__ slot, double* __restrict__ ldpart,
@@ -237,7 +235,6 @@ __device__ __forceinline__ void cr_inv_wg(double2* __restrict__ pool, int64_t it
   const double2* M = pool + (int64_t)bi * item + (int64_t)blk[li] * HP * BP;
   double2* Mo = pool + (int64_t)bi * item + (int64_t)dst[li] * HP * BP;   // may equal M
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
-  const bool act = NWG == NT || w < NT;
   d4 ar[NT], ai[NT];
   CR_STAMP(0);
   // Tiles in the MFMA C layout (lane: rows lk + 4 rr, column lr), except the
@@ -253,7 +250,6 @@ __device__ __forceinline__ void cr_inv_wg(double2* __restrict__ pool, int64_t it
   for (int I = 0; I < NT; ++I)
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
-      if (!act) break;
       const bool diag = (I == w);
       const int row = I * 16 + (diag ? lr : lk + 4 * rr), col = w * 16 + (diag ? lk + 4 * rr : lr);
       double2 v;
@@ -311,7 +307,7 @@ __device__ __forceinline__ void cr_inv_wg(double2* __restrict__ pool, int64_t it
         br[rr] = v.x;
         bim[rr] = v.y;
       }
-    } else if (act) {
+    } else {
       d4 tr = ar[0], ti = ai[0];   // this wave's tile kb (off-diagonal: C layout)
 #pragma unroll
       for (int I = 1; I < NT; ++I)
@@ -363,7 +359,7 @@ __device__ __forceinline__ void cr_inv_wg(double2* __restrict__ pool, int64_t it
 #pragma unroll
           for (int rr = 0; rr < 4; ++rr) Q[I][lr * 17 + lk + 4 * rr] = make_double2(ar[I][rr], ai[I][rr]);
         }
-    } else if (act) {
+    } else {
       if (has_next) {   // the lookahead column's tile w: Q[w] -= A_wk X_{kb+1}
         d4 yr, yi, cr, ci;
 #pragma unroll
@@ -394,8 +390,8 @@ __device__ __forceinline__ void cr_inv_wg(double2* __restrict__ pool, int64_t it
   for (int I = 0; I < NT / 2; ++I)
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr)
-      if (act) Mo[(int64_t)(I * 16 + lk + 4 * rr) * BP + w * 16 + lr] = make_double2(ar[I][rr], ai[I][rr]);
-  if (l == 0 && act) ldw[w] = ld;
+      Mo[(int64_t)(I * 16 + lk + 4 * rr) * BP + w * 16 + lr] = make_double2(ar[I][rr], ai[I][rr]);
+  if (l == 0) ldw[w] = ld;
   __syncthreads();
   if (threadIdx.x == 0) {
     double t = 0.0;
@@ -437,141 +433,6 @@ __global__ __launch_bounds__(64 * NT) void k_cr_inv(double2* __restrict__ pool, 
     return;
   }
   cr_inv_wg<NT>(pool, item, blockIdx.y, blockIdx.x, blk, dst, slot, ldpart, nslots, pan, ldw);
-}
-
-// ---------------------------------------------------------------------------
-// Block inversion by particle-hole 2 x 2 pivots (BP = 64, HP = 32).
-// An M-form block W = [[A, B], [conj B, -conj A]] is pivoted on the index
-// pairs {k, k + HP} (particle k and hole k): Gauss-Jordan in place with the
-// 2 x 2 pivot p = W[K, K] = [[a, b], [conj b, -conj a]] (a = W[k, k],
-// b = W[k, k + HP]), whose inverse is [[conj a, b], [conj b, -a]] / (|a|² + |b|²)
-// — no 16 x 16 pivot inversions on the chain, 32 pivot steps instead of 64
-// scalar ones, and only the top half is ever stored.  A swept set K of pairs
-// keeps the symmetry up to signs: W[i + HP, c] = σ(c) d(i) d(c) conj W[i, τ(c)]
-// with τ(c) = c ± HP, σ(c) = +1 (c < HP) / -1, d(x) = -1 when x's pair is
-// swept (sweep_K(-X) = -D_K sweep_K(X) D_K), so the pivot's hole row k + HP
-// is synthesised from the particle row k.  Each pivot block of i(W) has
-// Hermitian part >= y I like every Schur complement of i(H - i y): no
-// pivoting.  ln|det W| = Σ_k ln(|a_k|² + |b_k|²).
-// Layout: wave w owns rows 8w .. 8w + 7 of the top half, lane c = column c
-// (8 complex per lane in VGPRs); per step the pivot row k goes through LDS
-// (double-buffered by step parity) and each wave's column pair (k, k + HP)
-// through its own LDS slot; one barrier per step.  Rank-2 update with 4-mult
-// complex FMAs on the VALU (the update is rank 2: MFMA would pad K to 4);
-// the pivot columns are folded into the same FMAs (R_k -> 1 + P00 / P01,
-// R_h -> P10 / 1 + P11 on lanes k / k + HP), the pivot row is a select.
-// ---------------------------------------------------------------------------
-template <int NW>
-struct Inv2Lds {
-  static constexpr int RPW = 32 / NW;   // top-half rows per wave
-  double2 row[2][64];
-  double2 col[2][NW][RPW][2];
-};
-
-// acc - (u x + v y), two independent partial chains per component
-__device__ __forceinline__ double2 cmsub2(double2 acc, double2 u, double2 x, double2 v, double2 y) {
-  const double r1 = fma(-u.x, x.x, fma(u.y, x.y, acc.x));
-  const double r2 = fma(-v.x, y.x, v.y * y.y);
-  const double i1 = fma(-u.x, x.y, fma(-u.y, x.x, acc.y));
-  const double i2 = fma(-v.x, y.y, -v.y * y.x);
-  return make_double2(r1 + r2, i1 + i2);
-}
-// u x + v y
-__device__ __forceinline__ double2 cmadd2(double2 u, double2 x, double2 v, double2 y) {
-  const double r1 = fma(u.x, x.x, -u.y * x.y), r2 = fma(v.x, y.x, -v.y * y.y);
-  const double i1 = fma(u.x, x.y, u.y * x.x), i2 = fma(v.x, y.y, v.y * y.x);
-  return make_double2(r1 + r2, i1 + i2);
-}
-
-// NW waves (64 NW threads): wave w owns rows RPW w .. RPW w + RPW - 1
-template <int NW>
-__device__ __forceinline__ void cr_inv2_wg(double2* __restrict__ pool, int64_t item, int bi, int li,
-                                           const int* __restrict__ blk, const int* __restrict__ dst,
-                                           const int* __restrict__ slot, double* __restrict__ ldpart,
-                                           int nslots, Inv2Lds<NW>& S) {
-  constexpr int HP = 32, BP = 64, RPW = Inv2Lds<NW>::RPW;
-  const double2* M = pool + (int64_t)bi * item + (int64_t)blk[li] * HP * BP;
-  double2* Mo = pool + (int64_t)bi * item + (int64_t)dst[li] * HP * BP;   // may equal M
-  const int w = threadIdx.x >> 6, c = threadIdx.x & 63, cm = c & (HP - 1), tc = c ^ HP;
-  const double sg = c < HP ? 1.0 : -1.0;
-  double2 W[RPW];
-#pragma unroll
-  for (int r = 0; r < RPW; ++r) W[r] = M[(int64_t)(RPW * w + r) * BP + c];
-  if (w == 0) S.row[0][c] = W[0];
-  if (cm == 0) {
-#pragma unroll
-    for (int r = 0; r < RPW; ++r) S.col[0][w][r][c >> 5] = W[r];
-  }
-  __syncthreads();
-  double myden = 1.0;   // lane k of wave 0 keeps |det p_k|
-#pragma unroll
-  for (int k = 0; k < HP; ++k) {
-    const int b = k & 1;
-    // every LDS operand of the step up front (one round trip)
-    const double2 a = S.row[b][k], bb = S.row[b][k + HP];
-    const double2 x = S.row[b][c], yv = S.row[b][tc];
-    double2 u[RPW], v[RPW];
-#pragma unroll
-    for (int r = 0; r < RPW; ++r) {
-      u[r] = S.col[b][w][r][0];
-      v[r] = S.col[b][w][r][1];
-    }
-    const double s = cm < k ? -sg : sg;
-    const double2 z = make_double2(s * yv.x, -s * yv.y);   // W[k + HP, c]
-    const double den = fma(a.x, a.x, a.y * a.y) + fma(bb.x, bb.x, bb.y * bb.y);
-    if (c == k) myden = den;
-    // 1/den: v_rcp_f64 + two Newton steps (den > 0, far from the range ends)
-    double inv = __builtin_amdgcn_rcp(den);
-    inv = fma(inv, fma(-den, inv, 1.0), inv);
-    inv = fma(inv, fma(-den, inv, 1.0), inv);
-    const double2 P00 = make_double2(a.x * inv, -a.y * inv), P01 = make_double2(bb.x * inv, bb.y * inv);
-    const double2 P10 = make_double2(bb.x * inv, -bb.y * inv), P11 = make_double2(-a.x * inv, -a.y * inv);
-    double2 Rk = cmadd2(P00, x, P01, z), Rh = cmadd2(P10, x, P11, z);
-    const double2 rowk = c == k ? P00 : c == k + HP ? P01 : Rk;   // new pivot row entry
-    if (c == k) {
-      Rk = make_double2(1.0 + P00.x, P00.y);
-      Rh = P10;
-    } else if (c == k + HP) {
-      Rk = P01;
-      Rh = make_double2(1.0 + P11.x, P11.y);
-    }
-    const int k1 = k + 1, nb = b ^ 1;
-    // the next pivot row first (its owner publishes it before its other rows)
-    if (k1 < HP && w == k1 / RPW) {
-      const int r1 = (k + 1) % RPW;
-      W[r1] = cmsub2(W[r1], u[r1], Rk, v[r1], Rh);
-      S.row[nb][c] = W[r1];
-    }
-#pragma unroll
-    for (int r = 0; r < RPW; ++r) {
-      if (RPW * w + r == k) W[r] = rowk;
-      else if (!(k1 < HP && RPW * w + r == k1)) W[r] = cmsub2(W[r], u[r], Rk, v[r], Rh);
-    }
-    if (k1 < HP) {
-      if (cm == k1) {
-#pragma unroll
-        for (int r = 0; r < RPW; ++r) S.col[nb][w][r][c >> 5] = W[r];
-      }
-      __syncthreads();
-    }
-  }
-#pragma unroll
-  for (int r = 0; r < RPW; ++r) Mo[(int64_t)(RPW * w + r) * BP + c] = W[r];
-  if (w == 0) {
-    const double t = wave_sum(c < HP ? log(myden) : 0.0);
-    if (c == 0) ldpart[(int64_t)bi * nslots + slot[li]] = t;
-  }
-}
-
-#ifndef DWHMC_INV2_WAVES
-#define DWHMC_INV2_WAVES 4
-#endif
-__global__ __launch_bounds__(64 * DWHMC_INV2_WAVES) void k_cr_inv2(double2* __restrict__ pool, int64_t item,
-                                                 const int* __restrict__ blk, const int* __restrict__ dst,
-                                                 const int* __restrict__ slot, double* __restrict__ ldpart,
-                                                 int nslots) {
-  __shared__ Inv2Lds<DWHMC_INV2_WAVES> S;
-  cr_inv2_wg<DWHMC_INV2_WAVES>(pool, item, blockIdx.y, blockIdx.x, blk, dst, slot, ldpart, nslots, S);
 }
 
 // ---------------------------------------------------------------------------
@@ -777,15 +638,9 @@ __global__ __launch_bounds__(256) void k_cr_inv0(double2* __restrict__ pool, int
 // 1D grid with the XCD-aware remap so one item's tasks share an XCD's L2.
 // out never aliases an operand (planner invariant); out == cin is allowed.
 // ---------------------------------------------------------------------------
-// A/B knobs of variant builds (tools/ab_bench.py LIB=...): minimum waves per
-// SIMD the 16 x 16 tile kernels are compiled for, and their operand prefetch
-// depth in k-steps
-#ifndef DWHMC_GEMM_WAVES
-#define DWHMC_GEMM_WAVES 2
-#endif
-#ifndef DWHMC_GEMM_PF
-#define DWHMC_GEMM_PF 4
-#endif
+// minimum waves per SIMD the 16 x 16 tile kernels are compiled for, and their
+// operand prefetch depth in k-steps
+constexpr int kGemmWaves = 2, kGemmPf = 4;
 
 __device__ __forceinline__ double flip_sign(double x, unsigned m) {
   const unsigned long long b = __builtin_bit_cast(unsigned long long, x);
@@ -804,7 +659,7 @@ template <int BP, int MI, int KSPLIT, int KQ, int PFX = 0>
 __device__ __forceinline__ void cr_term(const double2* A, const double2* Bt, int c0, int crot, unsigned smask,
                                         d4 (&t1)[MI][MI], d4 (&t2)[MI][MI], d4 (&t3)[MI][MI]) {
   constexpr int HP = BP / 2, KS = BP / 4, KH = HP / 4, KSS = KS / KSPLIT, S0 = KQ * KSS;
-  constexpr int PFD = PFX > 0 ? PFX : (MI == 1 ? DWHMC_GEMM_PF : 2);
+  constexpr int PFD = PFX > 0 ? PFX : (MI == 1 ? kGemmPf : 2);
   constexpr int PF = KSS < PFD ? KSS : PFD;
   auto load = [&](int s, double2 (&a)[MI], double2 (&b)[MI]) {
 #pragma unroll
@@ -875,7 +730,7 @@ __device__ __forceinline__ void cr_tile_part(const double2* base, const D* __res
 // grid (already XCD-remapped by the caller) covers tiles g * TPW .. + TPW - 1.
 // TILESIGN: the sign of each tile comes from its descriptor (CrTile::neg;
 // side-work tile lists mix stages of both signs) instead of sg.  PFX: operand
-// prefetch depth in k-steps (0: the DWHMC_GEMM_PF default).
+// prefetch depth in k-steps (0: the kGemmPf default).
 template <int BP, int MI, int KSPLIT, int PFX = 0, bool TILESIGN = false>
 __device__ __forceinline__ void cr_gemm_wg(double2* __restrict__ pool, int64_t item,
                                            const CrTask* __restrict__ tasks, int ntasks, int maxt,
@@ -949,12 +804,11 @@ __device__ __forceinline__ void cr_gemm_wg(double2* __restrict__ pool, int64_t i
   double2 cpf[NPF];
 #pragma unroll
   for (int i = 0; i < NPF; ++i) cpf[i] = make_double2(0.0, 0.0);
-#if DWHMC_GEMM_CPF
+  // the accumulate input is loaded at tile start (its latency overlaps the operand loads)
   if (C && valid) {
 #pragma unroll
     for (int i = 0; i < NPF; ++i) cpf[i] = C[slot_off(i * KSPLIT + kq)];
   }
-#endif
   auto run = [&](auto kqc) {
     constexpr int KQ = decltype(kqc)::value;
     if constexpr (MI == 1) cr_tile_part<BP, MI, KSPLIT, KQ, PFX>(base, tp, tr, tc, t1, t2, t3);
@@ -973,11 +827,7 @@ __device__ __forceinline__ void cr_gemm_wg(double2* __restrict__ pool, int64_t i
   auto put = [&](int v, double2 x) {
     const int64_t o = slot_off(v);
     if (C) {
-#if DWHMC_GEMM_CPF
       const double2 c = cpf[v / KSPLIT];
-#else
-      const double2 c = C[o];
-#endif
       x.x += c.x;
       x.y += c.y;
     }
@@ -1031,7 +881,7 @@ __device__ __forceinline__ void cr_gemm_wg(double2* __restrict__ pool, int64_t i
 // leading kernel-argument dwords into SGPRs, build.py), and the grid size is
 // an argument (gridDim is a hidden argument, read by an s_load)
 template <int BP, int MI, int KSPLIT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MI == 1 ? DWHMC_GEMM_WAVES : 2))) void k_cr_gemm(double2* __restrict__ pool, int64_t item,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MI == 1 ? kGemmWaves : 2))) void k_cr_gemm(double2* __restrict__ pool, int64_t item,
                                                  const CrTile* __restrict__ tlist, int ntl, int total,
                                                  double sg, int nwg, int ntasks, int maxt,
                                                  const CrTask* __restrict__ tasks) {
@@ -1054,7 +904,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MI == 1 ? D
 // ---------------------------------------------------------------------------
 // arguments in first-use order: the inversion workgroups (the first
 // ninv x nbatch) need only the leading ones; nside: side-work workgroups
-template <int NT, bool INV2 = false>
+template <int NT>
 __global__ __launch_bounds__(64 * NT) void k_cr_inv_side(double2* __restrict__ pool, int64_t item,
                                                          const int* __restrict__ blk,
                                                          const int* __restrict__ dst, int ninv, int nbatch,
@@ -1066,19 +916,9 @@ __global__ __launch_bounds__(64 * NT) void k_cr_inv_side(double2* __restrict__ p
   __shared__ double2 pan[2][NT][16 * 17];
   __shared__ double ldw[NT];
   const int b = blockIdx.x, nall = ninv * nbatch;
-#if defined(DWHMC_SIDE_NOP)     // diagnostic builds (tools/ab_bench.py LIB=...): side part empty
-  if (b >= nall) return;
-#elif defined(DWHMC_SIDE_NOINV)  // inversion part empty
-  if (b < nall) return;
-#endif
   // inversions first: their branch needs only the leading (preloaded) arguments
   if (b < nall) {
-    if constexpr (INV2) {
-      cr_inv2_wg<NT>(pool, item, b / ninv, b - (b / ninv) * ninv, blk, dst, slot, ldpart, nslots,
-                     *reinterpret_cast<Inv2Lds<NT>*>(&pan[0][0][0]));
-    } else {
-      cr_inv_wg<NT>(pool, item, b / ninv, b - (b / ninv) * ninv, blk, dst, slot, ldpart, nslots, pan, ldw);
-    }
+    cr_inv_wg<NT>(pool, item, b / ninv, b - (b / ninv) * ninv, blk, dst, slot, ldpart, nslots, pan, ldw);
     return;
   }
   // the workgroups after the side work check the site guard (level-0 launches)
@@ -1088,244 +928,6 @@ __global__ __launch_bounds__(64 * NT) void k_cr_inv_side(double2* __restrict__ p
   }
   cr_gemm_wg<16 * NT, 2, 1, 0, true>(pool, item, stasks, nst, maxt, nullptr, 0, total, 1.0,
                                     xcd_remap(b - nall, nside));
-}
-
-// ---------------------------------------------------------------------------
-// Fused launches of the BP = 32 path (host: build_cr_fusion).  At L = 16 every
-// CR stage is a few dozen workgroups of 32 x 32 blocks: each launch costs its
-// ~4 us of launch + memory round trip + drain whatever it computes.  A fused
-// launch runs two consecutive stages: one workgroup per GROUP computes
-// [its phase-0 tiles, its block inversion,] its phase-1 tiles, its phase-2
-// tiles, where a later phase reads only what the same workgroup wrote (the
-// planner checks it): the backward G_ae / G_ce then G_ee of one eliminated
-// block (mode 2); an inversion then the V1 / V2 / W1 / W2 products of the
-// inverted block (mode 1); or, one launch per forward level (mode 3), the
-// Schur complement D' of the block, the U' / L' its products read, the
-// inversion and those products.  Tiles of the first stage that no group needs run
-// as plain workgroups of the same launch.  Phases are separated by
-// __syncthreads(), whose workgroup-scope release / acquire makes the global
-// stores of one wave visible to the other waves of the workgroup (one CU,
-// one vector L1; no tgsplit).  Opt-in (DWHMC_CR_FUSE): measured slower than
-// the separate launches -- each phase pays its own store / reload chain on
-// fewer workgroups, and a launch boundary costs little
-// (profiles/r03_exp_cr_fused_launches_bp32.txt).
-// ---------------------------------------------------------------------------
-// One round of up to NW / KS tiles of a list: KS waves per tile split its K
-// range (cr_tile_part), partials summed through LDS (red: NW x 4 x 64).  Every
-// wave of the workgroup calls it the same number of times (barriers inside).
-// Sign and accumulate input per tile (CrTile::neg, cin).
-template <int BP, int NW, int KS>
-__device__ __forceinline__ void cr_tiles_wg(double2* __restrict__ base, const CrTile* __restrict__ tl, int nt,
-                                            double2 (*red)[4][64]) {
-  constexpr int64_t BB = (int64_t)(BP / 2) * BP;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
-  const int ti = w / KS, kq = w % KS;
-  const bool valid = ti < nt;
-  const CrTile* tp = tl + (valid ? ti : 0);
-  d4 t1[1][1], t2[1][1], t3[1][1];
-  t1[0][0] = d4{0.0, 0.0, 0.0, 0.0};
-  t2[0][0] = d4{0.0, 0.0, 0.0, 0.0};
-  t3[0][0] = d4{0.0, 0.0, 0.0, 0.0};
-  int tr = 0, tc = 0;
-  if (valid) {
-    tr = tp->tr;
-    tc = tp->tc;
-    auto run = [&](auto kqc) {
-      constexpr int KQ = decltype(kqc)::value;
-      cr_tile_part<BP, 1, KS, KQ>(base, tp, tr, tc, t1, t2, t3);
-    };
-    if (kq == 0) run(std::integral_constant<int, 0>{});
-    if constexpr (KS >= 2) {
-      if (kq == 1) run(std::integral_constant<int, 1>{});
-    }
-    if constexpr (KS >= 4) {
-      if (kq == 2) run(std::integral_constant<int, 2>{});
-      if (kq == 3) run(std::integral_constant<int, 3>{});
-    }
-  }
-  const double sg = (valid && tp->neg) ? -1.0 : 1.0;
-  auto partial = [&](int rr) {
-    const double a = t1[0][0][rr], b = t2[0][0][rr], c = t3[0][0][rr];
-    return make_double2(sg * (a - b), sg * (c - a - b));
-  };
-  auto put = [&](int rr, double2 x) {
-    const int64_t o = (int64_t)(tr * 16 + lk + 4 * rr) * BP + tc * 16 + lr;
-    const int cin = tp->cin;
-    if (cin >= 0) {
-      const double2 c = base[cin * BB + o];
-      x.x += c.x;
-      x.y += c.y;
-    }
-    base[tp->out * BB + o] = x;
-  };
-  if constexpr (KS == 1) {
-    if (valid) {
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) put(rr, partial(rr));
-    }
-  } else {
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) red[w][rr][l] = partial(rr);
-    __syncthreads();
-    if (valid) {
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        if (rr % KS != kq) continue;
-        double2 x = red[w - kq][rr][l];
-#pragma unroll
-        for (int k = 1; k < KS; ++k) {
-          const double2 y = red[w - kq + k][rr][l];
-          x.x += y.x;
-          x.y += y.y;
-        }
-        put(rr, x);
-      }
-    }
-    __syncthreads();   // red is rewritten by the next round
-  }
-}
-
-// grid (ngrp + plain workgroups [+ 1 guard column], nbatch); NW waves per
-// workgroup; KS1 / KS2: K split of phase-1 / phase-2 (and plain) tiles
-template <int BP, int NT, int NW, int KS1, int KS2>
-__global__ __launch_bounds__(64 * NW) void k_cr_fused(double2* __restrict__ pool, int64_t item,
-                                                      const int* __restrict__ blk, const int* __restrict__ dst,
-                                                      const int* __restrict__ slot, double* __restrict__ ldpart,
-                                                      int nslots, const CrGroup* __restrict__ grp, int ngrp,
-                                                      const CrTile* __restrict__ ftl,
-                                                      const CrTile* __restrict__ plain, int nplain, int r0,
-                                                      int r1, int r2, SiteGuard sg, int N, int P) {
-  static_assert(BP == 16 * NT && NW >= NT && NW % KS1 == 0 && NW % KS2 == 0, "fused launch shape");
-  __shared__ double2 red[NW][4][64];
-  __shared__ double2 pan[2][NT][16 * 17];
-  __shared__ double ldw[NT];
-  if (sg.Delta != nullptr && blockIdx.x == gridDim.x - 1) {   // the guard column, pole 0 of each chain
-    if (blockIdx.y % P == 0) site_guard_wg(sg, N, blockIdx.y / P);
-    return;
-  }
-  const int bi = blockIdx.y, j = blockIdx.x;
-  double2* base = pool + (int64_t)bi * item;
-  constexpr int T1 = NW / KS1, T2 = NW / KS2;   // tiles per round
-  if (j < ngrp) {
-    const CrGroup G = grp[j];
-    for (int r = 0; r < r0; ++r) cr_tiles_wg<BP, NW, 1>(base, ftl + G.p0 + r * NW, G.n0 - r * NW, red);
-    if (r0 > 0) __syncthreads();   // phase-0 outputs (global) are the inversion's input and phase-1 operands
-    if (G.inv >= 0) {
-      cr_inv_wg<NT, NW>(pool, item, bi, G.inv, blk, dst, slot, ldpart, nslots, pan, ldw);
-      __syncthreads();   // the inverse (global) is read by the phase-1 tiles
-    }
-    for (int r = 0; r < r1; ++r) cr_tiles_wg<BP, NW, KS1>(base, ftl + G.p1 + r * T1, G.n1 - r * T1, red);
-    if (r2 > 0) {
-      __syncthreads();   // phase-1 outputs (global) are phase-2 operands
-      for (int r = 0; r < r2; ++r) cr_tiles_wg<BP, NW, KS2>(base, ftl + G.p2 + r * T2, G.n2 - r * T2, red);
-    }
-  } else {
-    const int p0 = (j - ngrp) * T2;
-    cr_tiles_wg<BP, NW, KS2>(base, plain + p0, nplain - p0, red);
-  }
-}
-
-bool cr_supported_fuse(int BP) { return BP == 32; }
-
-void launch_cr_fused(const CrDims& c, double2* pool, const int* blk, const int* dst, const int* slot,
-                     double* ldpart, const CrGroup* grp, int ngrp, const CrTile* ftl, const CrTile* plain,
-                     int nplain, int mode, int r0, int r1, int r2, hipStream_t s, const SiteGuard& sg) {
-  constexpr int NW = 8;
-  if (c.BP != 32 || ngrp + nplain <= 0) return;
-  const bool guard = sg.Delta != nullptr;
-  if (mode != 2) {   // [products +] inversion + products: one tile per wave
-    const int nplain_wg = (nplain + NW / 4 - 1) / (NW / 4);
-    const dim3 g(ngrp + nplain_wg + (guard ? 1 : 0), c.nbatch);
-    hipLaunchKernelGGL((k_cr_fused<32, 2, NW, 1, 4>), g, dim3(64 * NW), 0, s, pool, c.item, blk, dst, slot, ldpart,
-                       c.Ly, grp, ngrp, ftl, plain, nplain, r0, r1, r2, sg, c.N, c.P);
-  } else {           // two product phases: 2 waves per phase-1 tile, 4 per phase-2 tile
-    const int nplain_wg = (nplain + NW / 4 - 1) / (NW / 4);
-    const dim3 g(ngrp + nplain_wg + (guard ? 1 : 0), c.nbatch);
-    hipLaunchKernelGGL((k_cr_fused<32, 2, NW, 2, 4>), g, dim3(64 * NW), 0, s, pool, c.item, blk, dst, slot, ldpart,
-                       c.Ly, grp, ngrp, ftl, plain, nplain, r0, r1, r2, sg, c.N, c.P);
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Coarse tail: the stages of the coarse CR levels each carry a few dozen
-// workgroups and last a few microseconds — kernel boundaries, not work, set
-// their pace.  k_cr_tail runs a run of such stages in one launch: the grid is
-// sized so that every workgroup is resident at once (host: occupancy x CUs),
-// each stage's items are spread over it grid-stride, and a device-wide
-// barrier separates the stages.  Barrier: every wave makes its stores visible
-// at agent scope (release: L2 write-back; L2s are per XCD), the workgroup
-// arrives on a 64-bit monotonic counter and waits for base + (s + 1) x grid
-// arrivals, then every wave acquires (L2 invalidate).  A wait that exceeds
-// ~2 s sets *err and gives up, so a broken residency assumption ends the
-// kernel with an error instead of hanging the device.
-// Measured at C3 (profiles/r02_exp_cr_coarse_tail_grid_barrier.txt): stages
-// 8..17 take 400 us in the tail against 92 us as ten launches — the barrier
-// alone (no fences) costs ~8.5 us, the agent-scope release (L2 write-back on
-// every workgroup) and acquire (L2 invalidate) ~25 us more, while a launch
-// boundary costs 1-2 us.  Off by default (DWHMC_CR_TAIL=1 enables it).
-// ---------------------------------------------------------------------------
-#ifndef DWHMC_TAIL_FENCE
-#define DWHMC_TAIL_FENCE 2   // A/B diagnostics: 0 no fences, 1 acquire only, 3 release by one wave
-#endif
-__device__ __forceinline__ void tail_barrier(unsigned long long* bar, unsigned long long target, int* err) {
-#if DWHMC_TAIL_FENCE == 2
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-#endif
-  __syncthreads();
-#if DWHMC_TAIL_FENCE == 3
-  if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-#endif
-  if (threadIdx.x == 0) {
-    __hip_atomic_fetch_add(bar, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    unsigned spins = 0;
-    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > (1u << 26)) {
-        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-  }
-  __syncthreads();
-#if DWHMC_TAIL_FENCE != 0
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#endif
-}
-
-template <int NT>
-__global__ __launch_bounds__(64 * NT) void k_cr_tail(double2* __restrict__ pool, int64_t item,
-                                                     const int* __restrict__ blk, const int* __restrict__ dst,
-                                                     const int* __restrict__ slot, double* __restrict__ ldpart,
-                                                     int nslots, int nbatch, const CrTask* __restrict__ tasks,
-                                                     const CrTile* __restrict__ tl16,
-                                                     const CrTailStage* __restrict__ stages, int nst,
-                                                     unsigned long long* bar, unsigned long long base, int* err) {
-  static_assert(NT == 4, "the tail runs 4-wave workgroups");
-  __shared__ double2 pan[2][NT][16 * 17];
-  __shared__ double ldw[NT];
-  for (int si = 0; si < nst; ++si) {
-    const CrTailStage S = stages[si];
-    const int nall = S.ninv * nbatch;
-    const int side_total = nbatch * S.nside * S.side_maxt;
-    const int nside_wg = (side_total + 3) / 4;
-    const int tl_total = nbatch * S.ntl;
-    const int nwg = nall + nside_wg + tl_total;
-    for (int g = blockIdx.x; g < nwg; g += gridDim.x) {
-      if (g < nall) {
-        const int bi = g / S.ninv;
-        cr_inv_wg<NT>(pool, item, bi, g - bi * S.ninv, blk + S.inv_first, dst + S.inv_first, slot + S.inv_first,
-                      ldpart, nslots, pan, ldw);
-      } else if (g < nall + nside_wg) {
-        cr_gemm_wg<16 * NT, 2, 1, 0, true>(pool, item, tasks + S.side_first, S.nside, S.side_maxt, nullptr, 0,
-                                          side_total, 1.0, g - nall);
-      } else {
-        cr_gemm_wg<16 * NT, 1, 4>(pool, item, nullptr, 0, 0, tl16 + S.tl_first, S.ntl, tl_total,
-                                  S.neg ? -1.0 : 1.0, g - nall - nside_wg);
-      }
-      __syncthreads();   // the panel / K-split partials in LDS are reused by the next item
-    }
-    if (si + 1 < nst) tail_barrier(bar, base + (unsigned long long)(si + 1) * gridDim.x, err);
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1343,15 +945,13 @@ __global__ __launch_bounds__(64 * NT) void k_cr_tail(double2* __restrict__ pool,
 // small lattices map several bonds onto one entry), resolved at context
 // creation so the G loads wait for one index load, not two.
 // arguments in first-use order (kernel-argument preload)
-#ifndef DWHMC_PF_LANES
-#define DWHMC_PF_LANES 32
-#endif
+constexpr int kPfLanes = 32;   // lanes per bond (poles strided over them)
 __global__ __launch_bounds__(256) void k_cr_pair_force(
     double2* __restrict__ pool, int64_t item, const int64_t* __restrict__ bond4, int N, int P,
     const double* __restrict__ cpole, double2* __restrict__ Delta, double2* __restrict__ Pair,
     double2* __restrict__ F, double2* __restrict__ Pi, double kick, double drift, double cap2,
     int* __restrict__ flag, double beta, double J) {
-  constexpr int LB = DWHMC_PF_LANES;   // lanes per bond (poles strided over them)
+  constexpr int LB = kPfLanes;
   const int b = blockIdx.x * (256 / LB) + (threadIdx.x / LB), sub = threadIdx.x % LB;
   const int c = blockIdx.y;
   if (b >= 2 * N) return;   // uniform per lane group
@@ -1359,10 +959,7 @@ __global__ __launch_bounds__(256) void k_cr_pair_force(
   // Δ and π of the bond, loaded beside the G entries (not after the reduction)
   const int64_t o = (int64_t)c * 2 * N + b;
   double2 d0 = make_double2(0.0, 0.0), p0 = make_double2(0.0, 0.0);
-#ifndef DWHMC_PAIR_PREFETCH
-#define DWHMC_PAIR_PREFETCH 1
-#endif
-  if (DWHMC_PAIR_PREFETCH && sub == 0) {
+  if (sub == 0) {
     d0 = Delta[o];
     p0 = Pi[o];
   }
@@ -1382,10 +979,6 @@ __global__ __launch_bounds__(256) void k_cr_pair_force(
   double2 dn = make_double2(0.0, 0.0);
   if (sub == 0) {
     Pair[o] = Pv;
-    if (!DWHMC_PAIR_PREFETCH) {   // A/B knob: the loads after the reduction (the round-3 layout)
-      d0 = Delta[o];
-      p0 = Pi[o];
-    }
     const double2 d = d0;
     const double f = -beta / (2.0 * J);
     const double2 Fv = make_double2(f * (d.x - J * Pv.x), f * (d.y - J * Pv.y));
@@ -1461,21 +1054,6 @@ __global__ __launch_bounds__(256) void k_cr_fermion_energy(const double2* __rest
 bool cr_supported_bp(int BP) { return BP == 32 || BP == 64 || BP == 96 || BP == 128; }
 bool cr_supported_side(int BP) { return BP == 64; }
 bool cr_supported_inv0(int BP) { return BP == 64; }
-bool cr_supported_tail(int BP) { return BP == 64; }
-
-int cr_tail_occupancy() {
-  int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_cr_tail<4>, 256, 0) != hipSuccess) return 0;
-  return n;
-}
-
-void launch_cr_tail(const CrDims& c, double2* pool, const int* blk, const int* dst, const int* slot,
-                    double* ldpart, const CrTask* tasks, const CrTile* tl16, const CrTailStage* stages, int nst,
-                    int grid, unsigned long long* bar, unsigned long long base, int* err, hipStream_t s) {
-  if (nst <= 0 || grid <= 0) return;
-  hipLaunchKernelGGL(k_cr_tail<4>, dim3(grid), dim3(256), 0, s, pool, c.item, blk, dst, slot, ldpart, c.Ly,
-                     c.nbatch, tasks, tl16, stages, nst, bar, base, err);
-}
 
 void launch_cr_inv0(const CrDims& c, double2* pool, const int* blk, const int* rblk, const int* dst,
                     const int* slot, int n, double* ldpart, const double* ldA, hipStream_t s,
@@ -1502,14 +1080,6 @@ void launch_cr_inv(const CrDims& c, double2* pool, const int* blk, const int* ds
                    int n, double* ldpart, hipStream_t s, const SiteGuard& sg) {
   if (n <= 0) return;
   const bool guard = sg.Delta != nullptr;
-  if (c.BP == 64 && c.inv2) {
-    const dim3 g(n, c.nbatch);
-    hipLaunchKernelGGL(k_cr_inv2, g, dim3(64 * DWHMC_INV2_WAVES), 0, s, pool, c.item, blk, dst, slot, ldpart, c.Ly);
-    if (guard)   // the guard column alone (grid x = 1)
-      hipLaunchKernelGGL(k_cr_inv<4>, dim3(1, c.nbatch), dim3(256), 0, s, pool, c.item, blk, dst, 0, slot, ldpart,
-                         c.Ly, sg, c.N, c.P);
-    return;
-  }
   const dim3 g(n + (guard ? 1 : 0), c.nbatch);
   const int gcol = guard ? n : -1;
   switch (c.BP) {
@@ -1543,12 +1113,8 @@ void launch_cr_inv_side(const CrDims& c, double2* pool, const int* blk, const in
   const int side_wg = (total + 3) / 4;
   const int nc = c.nbatch / c.P;
   const dim3 g(n * c.nbatch + side_wg + (sg.Delta != nullptr ? nc : 0));
-  if (c.inv2)
-    hipLaunchKernelGGL((k_cr_inv_side<4, true>), g, dim3(256), 0, s, pool, c.item, blk, dst, n, c.nbatch, slot,
-                       ldpart, c.Ly, side_wg, stasks, nst, maxt32, total, sg, c.N);
-  else
-    hipLaunchKernelGGL((k_cr_inv_side<4, false>), g, dim3(256), 0, s, pool, c.item, blk, dst, n, c.nbatch, slot,
-                       ldpart, c.Ly, side_wg, stasks, nst, maxt32, total, sg, c.N);
+  hipLaunchKernelGGL(k_cr_inv_side<4>, g, dim3(256), 0, s, pool, c.item, blk, dst, n, c.nbatch, slot, ldpart,
+                     c.Ly, side_wg, stasks, nst, maxt32, total, sg, c.N);
 }
 
 // Stage configuration (tile TS, K split).  16 x 16 tiles; the K split by the
@@ -1560,7 +1126,7 @@ void launch_cr_inv_side(const CrDims& c, double2* pool, const int* blk, const in
 // chains, L = 48: no LDS reduction, one tile per wave;
 // profiles/r03_exp_gemm_ksplit_by_size.txt: from 2048 tiles, C3 -0.9 %,
 // C5 -5 %, 4 chains at L = 32 -3 %; C2's stages stay below it).
-// DWHMC_CR_KS_T2 / _T1: the tile counts from which the split is 2 / 1.  DWHMC_CR_GEMM=TS:KSPLIT forces one
+// DWHMC_CR_GEMM=TS:KSPLIT forces one
 // configuration for every stage (A/B runs; tests/test_gpu_parity.py runs
 // every compiled variant).
 CrGemmCfg cr_gemm_config(const CrDims& c, int ntasks, int maxt32, int maxt16, int ntmax, int ntiles16) {
@@ -1581,13 +1147,8 @@ CrGemmCfg cr_gemm_config(const CrDims& c, int ntasks, int maxt32, int maxt16, in
   }();
   const bool ts32_ok = (c.BP / 2) % 32 == 0;   // 32-wide tiles must not straddle A | B
   if (forced.ts == 16 || (forced.ts == 32 && ts32_ok)) return forced;
-  auto knob = [](const char* name, int dflt) {
-    const char* e = std::getenv(name);
-    return e ? std::atoi(e) : dflt;
-  };
   const int64_t T = (int64_t)ntiles16 * c.nbatch;
-  const int t1 = knob("DWHMC_CR_KS_T1", 2048), t2 = knob("DWHMC_CR_KS_T2", t1);
-  return CrGemmCfg{16, T >= t1 ? 1 : T >= t2 ? 2 : 4};
+  return CrGemmCfg{16, T >= 2048 ? 1 : 4};
 }
 
 void launch_cr_gemm(const CrDims& c, double2* pool, const CrTask* tasks, int ntasks, int maxt32,
@@ -1625,7 +1186,7 @@ void launch_cr_pair_force(const CrDims& c, double2* pool, const int64_t* bond4, 
                           double2* Delta, double2* Pair, double2* F, double2* Pi,
                           const KickDrift& kd, double beta, double J, hipStream_t s) {
   const int nc = c.nbatch / c.P;
-  constexpr int BPW = 256 / DWHMC_PF_LANES;   // bonds per workgroup
+  constexpr int BPW = 256 / kPfLanes;   // bonds per workgroup
   hipLaunchKernelGGL(k_cr_pair_force, dim3((2 * c.N + BPW - 1) / BPW, nc), dim3(256), 0, s, pool, c.item, bond4, c.N,
                      c.P, cpole, Delta, Pair, F, Pi, kd.kick, kd.drift, kd.cap * kd.cap, kd.flag, beta, J);
 }

@@ -8,17 +8,6 @@
 
 #include <utility>
 
-#ifndef DWHMC_INV_FOLD
-#define DWHMC_INV_FOLD 1
-#endif
-// k_cr_gemm: load the accumulate-input block cin at the start of a tile (its
-// latency overlaps the operand loads) instead of after the K reduction
-#ifndef DWHMC_GEMM_CPF
-#define DWHMC_GEMM_CPF 1
-#endif
-#ifndef DWHMC_INV_PERMLANE
-#define DWHMC_INV_PERMLANE 0
-#endif
 
 namespace dwh {
 
@@ -170,8 +159,8 @@ __device__ __forceinline__ double2 kick_drift_pre(double2 Fv, int64_t o, double2
 // Layout: lane l holds row r = l & 15, columns 4q .. 4q+3 with q = l >> 4.
 // Pivot p (compile time): row p reaches every lane of its 16-lane row through
 // DPP row_newbcast:p, column p reaches the other column quarters through
-// v_permlane16_swap / v_permlane32_swap, the pivot value through readlane.
-// No LDS, no barriers.  pprod accumulates Π |pivot|^2 (uniform in the wave).
+// ds_bpermute (LDS crossbar, no LDS storage), the pivot value through
+// readlane.  No barriers.  pprod accumulates Π |pivot|^2 (uniform in the wave).
 // ---------------------------------------------------------------------------
 template <int P>
 __device__ __forceinline__ double dpp_rowbcast(double x) {
@@ -181,25 +170,15 @@ __device__ __forceinline__ double dpp_rowbcast(double x) {
 
 // value of quarter QS (lanes 16 QS .. 16 QS + 15) broadcast to all quarters, per row position
 template <int QS>
-__device__ __forceinline__ unsigned bcast_quarter_u32(unsigned u) {
-  const auto s16 = __builtin_amdgcn_permlane16_swap(u, u, false, false);   // [u0 u0 u2 u2], [u1 u1 u3 u3]
-  const unsigned y = (QS & 1) ? s16[1] : s16[0];
-  const auto s32 = __builtin_amdgcn_permlane32_swap(y, y, false, false);   // [y_lo y_lo], [y_hi y_hi]
-  return (QS & 2) ? s32[1] : s32[0];
-}
-template <int QS>
 __device__ __forceinline__ double bcast_quarter(double x) {
   const unsigned long long b = __builtin_bit_cast(unsigned long long, x);
-#if DWHMC_INV_PERMLANE
-  const unsigned lo = bcast_quarter_u32<QS>((unsigned)b), hi = bcast_quarter_u32<QS>((unsigned)(b >> 32));
-#else
   // one LDS-crossbar permute per dword (no LDS storage): lane l reads lane
   // 16 QS + (l & 15); 2 instructions per double instead of ~6 with the
-  // permlane swaps and their register copies (the inversion is issue-bound)
+  // v_permlane16/32_swap pair and their register copies (the inversion is
+  // issue-bound)
   const int src = ((QS << 4) | (threadIdx.x & 15)) << 2;
   const unsigned lo = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)(unsigned)b);
   const unsigned hi = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)(unsigned)(b >> 32));
-#endif
   return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
 }
 __device__ __forceinline__ double readlane_f64(double x, int lane) {
@@ -227,7 +206,6 @@ __device__ __forceinline__ void inv16_step(double2 (&a)[4], double& pprod) {
   const double2 inv = make_double2(piv.x * s, -piv.y * s);
   pprod *= m2;
   const bool prow = (r == P);
-#if DWHMC_INV_FOLD
   // Select-free form: one update a <- a - f rowp' for every entry.  On the
   // pivot row colp' = piv - 1, so f = (piv - 1)/piv = 1 - 1/piv and the row
   // becomes a_p / piv; in column p rowp' = piv + 1, so the column becomes
@@ -236,12 +214,6 @@ __device__ __forceinline__ void inv16_step(double2 (&a)[4], double& pprod) {
   const double2 fi = cmul(make_double2(colp.x - (prow ? 1.0 : 0.0), colp.y), inv);
   rowp[PE].x += (q == PS) ? 1.0 : 0.0;
   const double2 f = fi;
-#else
-  // one update formula for every row: a <- a - f rowp with f = colp/piv, and
-  // f = 1 - 1/piv on the pivot row (a_p - (1 - 1/piv) a_p = a_p / piv)
-  const double2 fi = cmul(colp, inv);
-  const double2 f = prow ? make_double2(1.0 - inv.x, -inv.y) : fi;
-#endif
 #pragma unroll
   for (int jj = 0; jj < 4; ++jj) {
     const double2 x = rowp[jj];
@@ -250,10 +222,6 @@ __device__ __forceinline__ void inv16_step(double2 (&a)[4], double& pprod) {
     v.y = fma(-f.x, x.y, fma(-f.y, x.x, a[jj].y));
     a[jj] = v;
   }
-#if !DWHMC_INV_FOLD
-  // column p: 1/piv on the pivot row, -colp/piv elsewhere
-  if (q == PS) a[PE] = prow ? inv : make_double2(-fi.x, -fi.y);
-#endif
 }
 
 template <bool STRIDED, int... Ps>
@@ -262,82 +230,11 @@ __device__ __forceinline__ void inv16_all(double2 (&a)[4], double& pprod,
   (inv16_step<Ps, STRIDED>(a, pprod), ...);
 }
 
-// Gauss-Jordan step on the 2 x 2 pivot block B = {P, P+1} (P even): 8 steps
-// per 16 x 16 tile instead of 16, so half the dependent broadcast ->
-// reciprocal -> update chains.  With C = A[:, B], R = A[B, :], Π = A[B, B]
-// and E the columns e_P, e_{P+1}, one update covers every entry:
-//   A <- A - (C - E) Π^-1 (R + E^T)
-// (rows of B become Π^-1 R, columns of B become -C Π^-1, the block Π^-1).
-// Π^-1 by the closed 2 x 2 formula; every principal block of i(H - i y) has
-// Hermitian part >= y I, so |det Π| >= y^2 and the block pivots are as safe
-// as the scalar ones.  Accumulates |det Π|^2 (= the two scalar pivots' product).
-#ifndef DWHMC_INV_PAIR
-#define DWHMC_INV_PAIR 0
-#endif
-template <int P, bool STRIDED>
-__device__ __forceinline__ void inv16_step2(double2 (&a)[4], double& pprod) {
-  static_assert((P & 1) == 0, "pivot pairs start at even P");
-  // element (row i, column j): STRIDED lane (j & 3) * 16 + i, register j >> 2;
-  // else lane (j >> 2) * 16 + i, register j & 3
-  constexpr int PS0 = STRIDED ? (P & 3) : (P >> 2), PE0 = STRIDED ? (P >> 2) : (P & 3);
-  constexpr int PS1 = STRIDED ? ((P + 1) & 3) : ((P + 1) >> 2), PE1 = STRIDED ? ((P + 1) >> 2) : ((P + 1) & 3);
-  const int l = threadIdx.x & 63, r = l & 15, q = l >> 4;
-  double2 row0[4], row1[4];
-#pragma unroll
-  for (int jj = 0; jj < 4; ++jj) {
-    row0[jj] = make_double2(dpp_rowbcast<P>(a[jj].x), dpp_rowbcast<P>(a[jj].y));
-    row1[jj] = make_double2(dpp_rowbcast<P + 1>(a[jj].x), dpp_rowbcast<P + 1>(a[jj].y));
-  }
-  const double2 c0 = make_double2(bcast_quarter<PS0>(a[PE0].x), bcast_quarter<PS0>(a[PE0].y));
-  const double2 c1 = make_double2(bcast_quarter<PS1>(a[PE1].x), bcast_quarter<PS1>(a[PE1].y));
-  const double2 p00 = make_double2(readlane_f64(a[PE0].x, PS0 * 16 + P), readlane_f64(a[PE0].y, PS0 * 16 + P));
-  const double2 p01 = make_double2(readlane_f64(a[PE1].x, PS1 * 16 + P), readlane_f64(a[PE1].y, PS1 * 16 + P));
-  const double2 p10 =
-      make_double2(readlane_f64(a[PE0].x, PS0 * 16 + P + 1), readlane_f64(a[PE0].y, PS0 * 16 + P + 1));
-  const double2 p11 =
-      make_double2(readlane_f64(a[PE1].x, PS1 * 16 + P + 1), readlane_f64(a[PE1].y, PS1 * 16 + P + 1));
-  const double2 det = csub(cmul(p00, p11), cmul(p01, p10));
-  const double m2 = fma(det.x, det.x, det.y * det.y);
-  const double s = rcp_nr(m2);
-  const double2 idet = make_double2(det.x * s, -det.y * s);
-  pprod *= m2;
-  const double2 i00 = cmul(p11, idet), i11 = cmul(p00, idet);
-  const double2 i01 = cmul(make_double2(-p01.x, -p01.y), idet), i10 = cmul(make_double2(-p10.x, -p10.y), idet);
-  // F = (C - E) Π^-1 for this lane's row
-  const double2 cc0 = make_double2(c0.x - (r == P ? 1.0 : 0.0), c0.y);
-  const double2 cc1 = make_double2(c1.x - (r == P + 1 ? 1.0 : 0.0), c1.y);
-  const double2 f0 = cadd(cmul(cc0, i00), cmul(cc1, i10));
-  const double2 f1 = cadd(cmul(cc0, i01), cmul(cc1, i11));
-  // R' = R + E^T
-  row0[PE0].x += (q == PS0) ? 1.0 : 0.0;
-  row1[PE1].x += (q == PS1) ? 1.0 : 0.0;
-#pragma unroll
-  for (int jj = 0; jj < 4; ++jj) {
-    const double2 x0 = row0[jj], x1 = row1[jj];
-    double2 v;
-    v.x = fma(-f0.x, x0.x, fma(f0.y, x0.y, a[jj].x));
-    v.y = fma(-f0.x, x0.y, fma(-f0.y, x0.x, a[jj].y));
-    v.x = fma(-f1.x, x1.x, fma(f1.y, x1.y, v.x));
-    v.y = fma(-f1.x, x1.y, fma(-f1.y, x1.x, v.y));
-    a[jj] = v;
-  }
-}
-
-template <bool STRIDED, int... Ps>
-__device__ __forceinline__ void inv16_all2(double2 (&a)[4], double& pprod,
-                                           std::integer_sequence<int, Ps...>) {
-  (inv16_step2<2 * Ps, STRIDED>(a, pprod), ...);
-}
-
 // returns Π |pivot|^2 of the 16 pivots
 template <bool STRIDED = false>
 __device__ __forceinline__ double wave_inv16_dpp(double2 (&a)[4]) {
   double pprod = 1.0;
-#if DWHMC_INV_PAIR
-  inv16_all2<STRIDED>(a, pprod, std::make_integer_sequence<int, 8>{});
-#else
   inv16_all<STRIDED>(a, pprod, std::make_integer_sequence<int, 16>{});
-#endif
   return pprod;
 }
 

@@ -35,7 +35,6 @@ struct KickDrift {
 struct CrDims {
   int Lx, Ly, N, BP, P, nbatch, nblk;
   int64_t item;   // elements per batch item pool (nblk * HP * BP)
-  bool inv2 = false;   // BP = 64 inversions by particle-hole 2 x 2 pivots (k_cr_inv2)
 };
 // out = [cin] + sg * sum_{h<nt} A_h B_h over pool block indices (cin = -1: zero),
 // computed only on the output rows [r0, r1) x columns [c0, c1) (rounded out to
@@ -55,7 +54,7 @@ constexpr int kCrNegBit = 1 << 8;
 struct alignas(64) CrTile {
   int out, cin, nt, bq;
   int a[4], b[4];
-  int tr, tc, neg, pad1;   // neg: 1 = negative sign (TILESIGN lists)
+  int tr, tc, neg, pad1;   // neg: 1 = negative sign
 };
 // wave tiles of a task at tile size ts
 inline int cr_task_tiles(const CrTask& t, int ts) {
@@ -105,48 +104,10 @@ void launch_cr_inv0(const CrDims& c, double2* pool, const int* blk, const int* r
 // the same inversions plus nst side-work product tasks per batch item
 // (32 x 32 wave tiles, maxt32 per task, each task's sign in bq & kCrNegBit)
 // on the CUs the inversions leave idle
-// Fused launches of the BP = 32 path (dwhmc_cr.hip k_cr_fused, host
-// build_cr_fusion): one workgroup per group runs its phase-0 tiles (mode 3),
-// inversion entry `inv` of the stage (modes 1, 3), its phase-1 tiles, its
-// phase-2 tiles (mode 2), each later phase reading only what the group wrote;
-// `plain` tiles (no group) run in the same launch.  r0 / r1 / r2: rounds of
-// tiles per phase (8 per round in phases 0 and 1 of modes 1 and 3; 4 and 2
-// in mode 2), the maximum over the groups.
-struct alignas(32) CrGroup {
-  int inv;       // inversion entry of the stage, or -1
-  int p0, n0;    // phase-0 tiles (before the inversion; fused tile list)
-  int p1, n1;    // phase-1 tiles
-  int p2, n2;    // phase-2 tiles
-  int pad;
-};
-bool cr_supported_fuse(int BP);
-void launch_cr_fused(const CrDims& c, double2* pool, const int* blk, const int* dst, const int* slot,
-                     double* ldpart, const CrGroup* grp, int ngrp, const CrTile* ftl, const CrTile* plain,
-                     int nplain, int mode, int r0, int r1, int r2, hipStream_t s,
-                     const SiteGuard& sg = SiteGuard{});
 bool cr_supported_side(int BP);
 void launch_cr_inv_side(const CrDims& c, double2* pool, const int* blk, const int* dst, const int* slot,
                         int n, double* ldpart, const CrTask* stasks, int nst, int maxt32, hipStream_t s,
                         const SiteGuard& sg = SiteGuard{});
-// Coarse tail (BP = 64): consecutive small stages in one launch with a
-// device-wide barrier between them.  A stage is an inversion list (+ side
-// tasks, as launch_cr_inv_side) or a 16 x 16 / 4-way K-split product list.
-struct CrTailStage {
-  int inv_first, ninv;                  // entries of the inversion lists
-  int side_first, nside, side_maxt;     // side tasks (CrTask, 32 x 32 tiles, sign in bq)
-  int tl_first, ntl;                    // product tiles (CrTile)
-  int neg;                              // product stage sign: 1 = negative
-};
-bool cr_supported_tail(int BP);
-// workgroups of k_cr_tail that one CU holds at once (the grid is sized so every
-// workgroup is resident: the stage barrier needs all of them running)
-int cr_tail_occupancy();
-// stages [0, nst) of `stages` (device array) on `grid` workgroups; bar: the
-// device barrier counter (64-bit, monotonic), base: its value at launch; err:
-// set to 1 when a barrier wait times out (then the results are invalid)
-void launch_cr_tail(const CrDims& c, double2* pool, const int* blk, const int* dst, const int* slot,
-                    double* ldpart, const CrTask* tasks, const CrTile* tl16, const CrTailStage* stages, int nst,
-                    int grid, unsigned long long* bar, unsigned long long base, int* err, hipStream_t s);
 // block-product stage configuration: output tile TS x TS (16 or 32) and the
 // number of waves splitting each tile's K range (1, 2, 4)
 struct CrGemmCfg {

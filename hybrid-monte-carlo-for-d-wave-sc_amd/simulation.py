@@ -288,8 +288,12 @@ def run_simulation_chains(p: H.ModelParameters, out_dirs, rngs, *, n_therm: int 
     one batched eigensolve per transport measurement,
     dwh_measure_transport_batched; with transport_batch > 1, per chain
     transport_batch sweeps at once, TransportQueue).  Returns one
-    SimulationResult per chain; each chain's files equal what run_simulation
-    writes for it."""
+    SimulationResult per chain; each chain runs the same Markov chain as
+    run_simulation up to the pole approximation (bit-equal on the oracle
+    backend: on the device the batched context selects one pole set for the
+    largest spectral bound over the chains, and a guard trip re-selects it
+    for every chain, so dH differs at ~1e-12 and a Metropolis decision can
+    differ)."""
     K = len(out_dirs)
     if len(rngs) != K or K < 1:
         raise ValueError("one rng per output directory")

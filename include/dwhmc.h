@@ -173,17 +173,14 @@ int dwh_stream(dwh_ctx* ctx, void** stream);
  * (bench/profiling).  enable is a bitmask over the timer names below
  * (bit 0 "gj_update", bit 1 "gj_pivot", bit 2 "assemble", bit 3 "contract",
  * bit 4 "step", bit 5 "gj_edge", bit 6 "cr_gemm", bit 7 "cr_inv", bit 8 "cr_inv_side",
- * bit 9 "cr_tail", bit 10 "cr_fused", bit 11 "eig_own", bit 12 "eig_vendor");
+ * bit 9 "eig_own", bit 10 "eig_vendor");
  * 0 disables, -1 times everything. */
 int dwh_timing_enable(dwh_ctx* ctx, int32_t enable);
 /* name: "gj_update" (rank-128 paired / rank-64 trailing updates),
  * "gj_edge" (edge update between the two pivots of a pair), "gj_pivot",
  * "cr_gemm" (cyclic-reduction block products), "cr_inv" (its block
  * inversions), "cr_inv_side" (inversion stages that also run the products off
- * the critical path; work = inversion + side-product flops), "cr_tail" (the
- * coarse levels' stages in one launch; work = their inversion + product flops), "cr_fused"
- * (BP = 32 launches that run two consecutive stages; work = both stages'
- * flops), "eig_own" / "eig_vendor" (eigensolves by the library's solver /
+ * the critical path; work = inversion + side-product flops), "eig_own" / "eig_vendor" (eigensolves by the library's solver /
  * by rocSOLVER, opt-in or fallback; work = matrices), "assemble",
  * "contract", "step"; returns total milliseconds, launches and the
  * algorithmic work summed over launches (fp64 flops; HBM bytes for
@@ -278,14 +275,6 @@ int dwh_debug_level0(dwh_ctx* ctx, int64_t chain, int64_t pole, int32_t refill, 
  * work, product stages, writes, pool blocks.  DWH_ERR_STATE with the first
  * violation in dwh_last_error(NULL). */
 int dwh_debug_cr_plan_check(int64_t Lx, int64_t Ly, int64_t nbatch, int32_t side, int32_t inv0, int64_t* stats);
-
-/* Launch fusion of the same plan (BP = 32 lattices, host only): out[0]
- * stages, out[1] launches after fusion, out[2] inversion + product launches
- * (mode 1), out[3] product pair launches (mode 2), out[4] product +
- * inversion + product launches (mode 3, one per forward level).  dwh_debug_cr_plan_check
- * also verifies the fused launches (tile coverage, no block shared by
- * concurrent workgroup groups). */
-int dwh_debug_cr_fusion(int64_t Lx, int64_t Ly, int64_t nbatch, int64_t* out);
 
 /* Algorithmic fp64 flops per batch item of the same plan (host only), as the
  * "cr_*" timers count them: flops[0] block inversions (8 BP^3 each), flops[1]

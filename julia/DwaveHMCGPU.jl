@@ -169,8 +169,8 @@ function measure_observables(cache::GPUCache, p::ModelParameters, state::Simulat
                                       sum_diff / N, abs(sum_pair_global / N), sum_pair_local / N)
 end
 
-# src/Observables.jl:314-526 on the device (eigenpairs by rocSOLVER, sums in HIP
-# kernels) for the Δ the context holds; same SpectrumResult.
+# src/Observables.jl:314-526 on the device (eigenpairs by the library's own
+# Hermitian eigensolver, sums in HIP kernels) for the Δ the context holds; same SpectrumResult.
 function measure_transport_and_spectra(cache::GPUCache, p::ModelParameters)
     nw, nd = Ref{Int64}(0), Ref{Int64}(0)
     check(C_NULL, ccall((:dwh_transport_grid, libdwhmc), Cint,

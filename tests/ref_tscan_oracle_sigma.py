@@ -1,11 +1,13 @@
-"""Test infrastructure (CPU oracle, not a test): σ_DC of the reference's
-formula (src/Observables.jl:404-425) at T = 1000 for i.i.d. Gaussian pairing
+"""Test infrastructure (CPU oracle): σ_DC of the reference's formula
+(src/Observables.jl:404-425) at high temperature for i.i.d. Gaussian pairing
 fields, where the fermion weight is negligible (E_f ≈ -2N ln 2 + O(β²)) and
 the HMC ensemble is Gaussian with <|Δ_ij|²> = 2J/β, at several broadenings
-η, plus the share of the diagonal (n = m) terms.  Backs the η inference of
-tests/test_ref_tscan.py (profiles/r03_ref_tscan_investigation.md).
+η, plus the share of the diagonal (n = m) terms.  Pins the oracle to the
+reference's published R(T = 1000) and backs the η inference of
+tests/test_ref_tscan.py (tests/test_ref_tscan_oracle.py,
+profiles/r03_ref_tscan_investigation.md).
 
-Usage: python tests/ref_tscan_oracle_sigma.py [T] [samples]   (~1 s per sample)
+Usage: python tests/ref_tscan_oracle_sigma.py [T] [samples]   (~0.5 s per sample)
 """
 import math
 import os
@@ -15,6 +17,8 @@ import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from oracle import dwhmc_oracle as O  # noqa: E402
+
+MULTS = (1.0, 1.1, 1.2, 1.25, 1.3)
 
 
 def current_operator(p):
@@ -29,12 +33,15 @@ def current_operator(p):
     return np.block([[Jp, Z], [Z, Jp]])
 
 
-def main(T=1000.0, ns=40, L=24, J=0.8, mu=-1.4, mults=(1.0, 1.1, 1.2, 1.25, 1.3)):
+def sigma_samples(T=1000.0, ns=40, L=24, J=0.8, mu=-1.4, mults=MULTS, seed=None):
+    """σ_DC per sample (ns x len(mults)) at η = mult · 8/L² (batch_scan_T.jl:17)
+    and the diagonal share of each sample at η = 8/L², for the published
+    model (plot_stiffness.ipynb cell 1: W = 1, n_imp = 0)."""
     beta = 1.0 / T
     eta0 = 8.0 / (L * L)
     p = O.ModelParameters(L, L, 1.0, -0.35, mu, 1.0, 0.0, beta, J, 1.0, eta=eta0, domega=0.2 * eta0, omega_max=4.0)
     Jb = current_operator(p)
-    rng = np.random.default_rng(int(T * 10) + 3)
+    rng = np.random.default_rng(int(T * 10) + 3 if seed is None else seed)
     sig, diag = [], []
     for _ in range(ns):
         D = (rng.standard_normal((p.N, 2)) + 1j * rng.standard_normal((p.N, 2))) * math.sqrt(J / beta)
@@ -55,8 +62,12 @@ def main(T=1000.0, ns=40, L=24, J=0.8, mu=-1.4, mults=(1.0, 1.1, 1.2, 1.25, 1.3)
             if m == 1.0:
                 diag.append(np.trace(terms) / terms.sum())
         sig.append(row)
-    a = np.array(sig)
-    for k, m in enumerate(mults):
+    return np.array(sig), np.array(diag)
+
+
+def main(T=1000.0, ns=40):
+    a, diag = sigma_samples(T, ns)
+    for k, m in enumerate(MULTS):
         se = a[:, k].std(ddof=1) / math.sqrt(ns)
         print(f"T={T:g} eta={m:g} x 8/L^2: sigma_DC {a[:, k].mean():.4e} +- {se:.1e}  R {1 / a[:, k].mean():.1f}")
     print(f"diagonal (n = m) share of sigma_DC at eta = 8/L^2: {np.mean(diag):.3f}")

@@ -83,28 +83,3 @@ def test_cr_plan_flops_c3_side_work(dwhmc):
     lib = dwhmc.load_library()
     inv, prod, side_f = plan_flops(lib, 32, 32, 13, 1, 1)
     assert side_f > 0.2 * (prod + side_f)
-
-
-def test_cr_fusion_bp32_shapes(dwhmc):
-    """BP = 32 plans fuse stages into k_cr_fused launches
-    (dwh_debug_cr_fusion; dwh_debug_cr_plan_check verifies the fused groups):
-    C2 (L = 16) runs its 21 stages in 9 launches — level 0's inversion with
-    its V/W products, one launch per coarser forward level (Schur
-    complements, inversion, products; the last one with the coarsest
-    backward products), the coarsest G_ee alone, three backward
-    G_ae/G_ce -> G_ee pairs; BP = 64 plans are not fused."""
-    lib = dwhmc.load_library()
-
-    def fusion(Lx, Ly, nb):
-        out = np.zeros(5, dtype=np.int64)
-        assert lib.dwh_debug_cr_fusion(Lx, Ly, nb, out.ctypes.data_as(C.c_void_p)) == 0
-        return list(out)
-
-    print(fusion(16, 16, 10), fusion(8, 8, 6), fusion(16, 1, 3))
-    assert fusion(16, 16, 10) == [21, 9, 1, 3, 4]
-    assert fusion(16, 1, 3) == [1, 1, 0, 0, 0]
-    s32 = fusion(32, 32, 12)
-    assert s32[0] == s32[1] and s32[2:] == [0, 0, 0]
-    for Lx, Ly in [(16, 16), (8, 8), (5, 7), (16, 33), (12, 7), (16, 2), (3, 3)]:
-        rc, _, err = check(lib, Lx, Ly, 10, 1, 1)
-        assert rc == 0, (Lx, Ly, err)

@@ -1,6 +1,7 @@
 """GPU parity: the HIP path through the C ABI vs the CPU oracle.
 
-Tolerances (fp64; the pole set approximates tanh to <= 2e-14 on the spectrum):
+Tolerances (fp64; the default pole set approximates tanh to <= 5e-12 on the
+spectrum, the strict one to <= 2e-14):
   * forces          ‖F_gpu - F_ref‖∞ ≤ 1e-10 (1 + ‖F_ref‖∞)
   * pairing P_ij    ‖P_gpu - P_ref‖∞ ≤ 1e-11
   * E_f             |ΔE_f| ≤ 1e-11 |E_f|
@@ -566,123 +567,6 @@ def test_cr_block_product_variants(dwhmc, oracle, monkeypatch, cfg, Lx, Ly):
     assert np.max(np.abs(ctx.forces()[0] - F_ref)) <= 1e-10 * (1 + np.max(np.abs(F_ref)))
     Ef = ctx.fermion_energy()[0]
     assert abs(Ef - Ef_ref) <= 1e-11 * abs(Ef_ref), (Ef, Ef_ref)
-    ctx.close()
-
-
-@pytest.mark.parametrize("Lx,Ly", [(32, 32), (20, 13), (24, 6)])
-def test_cr_coarse_tail_kernel(dwhmc, oracle, monkeypatch, Lx, Ly):
-    """The opt-in coarse tail (DWHMC_CR_TAIL=1: consecutive small stages in one
-    k_cr_tail launch with device-wide stage barriers) gives the oracle's
-    results, within a factorisation and across the sweeps of a trajectory
-    (the barrier counter carries over launches)."""
-    O = oracle
-    monkeypatch.setenv("DWHMC_CR_TAIL", "1")
-    p, dis, Delta = make_case(O, Lx, Ly, 8.0, seed=Lx * 5 + Ly, amp=0.1)
-    cache, F_ref, Ef_ref = O.evaluate(p, dis, Delta)
-    ctx = device_ctx(dwhmc, p, dis, "cr")
-    ctx.set_pairing(Delta)
-    ctx.factorize()
-    assert np.max(np.abs(ctx.forces()[0] - F_ref)) <= 1e-10 * (1 + np.max(np.abs(F_ref)))
-    assert abs(ctx.fermion_energy()[0] - Ef_ref) <= 1e-11 * abs(Ef_ref)
-    Nt = 3
-    dt = O.calc_optimal_dt(p.beta, p.J, p.mass, Nt)
-    rng = np.random.default_rng(2)
-    draws = [((rng.standard_normal((p.N, 2)) + 1j * rng.standard_normal((p.N, 2))) * math.sqrt(0.5),
-              float(rng.random())) for _ in range(2)]
-    ref = _oracle_after_sweeps(O, p, dis, Delta, draws, Nt, dt)
-    for (noise, u), (acc_r, dH_r, D_r, _) in zip(draws, ref):
-        acc, dH = ctx.hmc_sweep(noise, np.array([u]), Nt, dt, p.mass)
-        assert bool(acc[0]) == acc_r and abs(dH[0] - dH_r) <= 1e-8 * (1 + abs(dH_r))
-        assert np.max(np.abs(ctx.get_state()[0][0] - D_r)) <= 1e-10
-    ctx.close()
-
-
-@pytest.mark.parametrize("fuse", ["7", "3", "0"])
-@pytest.mark.parametrize("Lx,Ly", [(16, 16), (12, 5), (5, 7), (16, 3), (16, 2)])
-def test_cr_fused_launches(dwhmc, oracle, monkeypatch, fuse, Lx, Ly):
-    """The opt-in fused launches of BP = 32 lattices (DWHMC_CR_FUSE = mode
-    bitmask; k_cr_fused: an inversion with its V/W products, a backward
-    G_ae/G_ce -> G_ee pair, a whole forward level; 0: every stage its own
-    launch, the default): the oracle's results either way, within a
-    factorisation and across the sweeps of a trajectory (the site guard rides
-    on the fused level-0 launch)."""
-    O = oracle
-    monkeypatch.setenv("DWHMC_CR_FUSE", fuse)
-    p, dis, Delta = make_case(O, Lx, Ly, 8.0, seed=Lx * 11 + Ly, amp=0.1)
-    cache, F_ref, Ef_ref = O.evaluate(p, dis, Delta)
-    P_ref, _ = O.pairing_P(cache.U, cache.E_n, p)
-    ctx = device_ctx(dwhmc, p, dis, "cr")
-    ctx.set_pairing(Delta)
-    ctx.factorize()
-    assert np.max(np.abs(ctx.pairing()[0] - P_ref)) <= 1e-11
-    assert np.max(np.abs(ctx.forces()[0] - F_ref)) <= 1e-10 * (1 + np.max(np.abs(F_ref)))
-    assert abs(ctx.fermion_energy()[0] - Ef_ref) <= 1e-11 * abs(Ef_ref)
-    hole_ref = O.measure_observables(cache, p, Delta)["hole_conc"]
-    assert abs(2.0 * ctx.hole_trace()[0] / p.N - 1.0 - hole_ref) <= 1e-11
-    Nt = 3
-    dt = O.calc_optimal_dt(p.beta, p.J, p.mass, Nt)
-    rng = np.random.default_rng(6)
-    draws = [((rng.standard_normal((p.N, 2)) + 1j * rng.standard_normal((p.N, 2))) * math.sqrt(0.5),
-              float(rng.random())) for _ in range(2)]
-    ref = _oracle_after_sweeps(O, p, dis, Delta, draws, Nt, dt)
-    for (noise, u), (acc_r, dH_r, D_r, _) in zip(draws, ref):
-        acc, dH = ctx.hmc_sweep(noise, np.array([u]), Nt, dt, p.mass)
-        assert bool(acc[0]) == acc_r and abs(dH[0] - dH_r) <= 1e-8 * (1 + abs(dH_r))
-        assert np.max(np.abs(ctx.get_state()[0][0] - D_r)) <= 1e-10
-    ctx.close()
-
-
-def test_cr_fused_matches_unfused_batched(dwhmc, oracle, monkeypatch):
-    """Fused and unfused launches of the C2 lattice with 3 chains agree to
-    rounding (the fused tiles split K differently), on every chain."""
-    O = oracle
-    cases = [make_case(O, 16, 16, 8.0, seed=900 + c, amp=0.15) for c in range(3)]
-    p = cases[0][0]
-    dis = np.stack([c[1] for c in cases])
-    D = np.stack([c[2] for c in cases])
-    out = {}
-    for fuse in ("7", "0"):
-        monkeypatch.setenv("DWHMC_CR_FUSE", fuse)
-        ctx = device_ctx(dwhmc, p, dis, "cr")
-        ctx.set_pairing(D)
-        ctx.factorize()
-        out[fuse] = (ctx.forces(), ctx.fermion_energy(), ctx.hole_trace())
-        ctx.close()
-    F1, E1, T1 = out["7"]
-    F0, E0, T0 = out["0"]
-    assert np.max(np.abs(F1 - F0)) <= 1e-12 * (1 + np.max(np.abs(F0)))
-    assert np.max(np.abs(E1 - E0)) <= 1e-13 * np.max(np.abs(E0))
-    assert np.max(np.abs(T1 - T0)) <= 1e-12 * (1 + np.max(np.abs(T0)))
-
-
-@pytest.mark.parametrize("side", ["1", "0"])
-@pytest.mark.parametrize("Lx,Ly", [(32, 32), (20, 13)])
-def test_cr_inv2_kernel(dwhmc, oracle, monkeypatch, Lx, Ly, side):
-    """The opt-in particle-hole 2 x 2 pivot inversion (DWHMC_CR_INV2=1,
-    k_cr_inv2 / k_cr_inv_side<4, true>; BP = 64) gives the oracle's results,
-    inside the side-work launches and alone, across a trajectory."""
-    O = oracle
-    monkeypatch.setenv("DWHMC_CR_INV2", "1")
-    monkeypatch.setenv("DWHMC_CR_SIDE", side)
-    p, dis, Delta = make_case(O, Lx, Ly, 8.0, seed=Lx * 7 + Ly, amp=0.1)
-    cache, F_ref, Ef_ref = O.evaluate(p, dis, Delta)
-    ctx = device_ctx(dwhmc, p, dis, "cr")
-    ctx.set_pairing(Delta)
-    ctx.factorize()
-    assert np.max(np.abs(ctx.forces()[0] - F_ref)) <= 1e-10 * (1 + np.max(np.abs(F_ref)))
-    assert abs(ctx.fermion_energy()[0] - Ef_ref) <= 1e-11 * abs(Ef_ref)
-    hole_ref = O.measure_observables(cache, p, Delta)["hole_conc"]
-    assert abs(2.0 * ctx.hole_trace()[0] / p.N - 1.0 - hole_ref) <= 1e-11
-    Nt = 3
-    dt = O.calc_optimal_dt(p.beta, p.J, p.mass, Nt)
-    rng = np.random.default_rng(4)
-    draws = [((rng.standard_normal((p.N, 2)) + 1j * rng.standard_normal((p.N, 2))) * math.sqrt(0.5),
-              float(rng.random())) for _ in range(2)]
-    ref = _oracle_after_sweeps(O, p, dis, Delta, draws, Nt, dt)
-    for (noise, u), (acc_r, dH_r, D_r, _) in zip(draws, ref):
-        acc, dH = ctx.hmc_sweep(noise, np.array([u]), Nt, dt, p.mass)
-        assert bool(acc[0]) == acc_r and abs(dH[0] - dH_r) <= 1e-8 * (1 + abs(dH_r))
-        assert np.max(np.abs(ctx.get_state()[0][0] - D_r)) <= 1e-10
     ctx.close()
 
 

@@ -1,0 +1,67 @@
+#!/bin/bash
+# Round-4 GPU passes: bash tools/gpu_r04.sh TAG step [step ...]
+#   suite   full `pytest -m gpu` (DWHMC_TSCAN_RECORD -> tscan_record.json)
+#   tscan   the published T scan's low-temperature rows (investigation, 8 chains)
+#   bench   the driver's command + C3 x200 + C2 + C5
+#   prof    rocprofv3 kernel stats + PMC traffic passes (tools/profile_round.sh) + step trace
+#   sq      SQ / MFMA-busy counters of the bench (tools/pmc_sq.sh) + the f64 MFMA peak micro
+#   trans   transport timing (single measurement + snapshot batches)
+# Every GPU step runs under its own timeout; the first failure ends the script.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+TAG=${1:?tag}
+shift
+O=$R/gpurun_out/$TAG
+mkdir -p "$O"
+cd "$R"
+for step in "$@"; do
+  echo "== $step $(date +%T)"
+  case $step in
+    suite)
+      DWHMC_TSCAN_RECORD=$O/tscan_record.json timeout -k 10 900 python -u -m pytest tests -m gpu -x -q \
+        --timeout 450 --timeout-method thread > "$O/tests.log" 2>&1 || { tail -40 "$O/tests.log"; exit 1; }
+      tail -3 "$O/tests.log" ;;
+    tscan)
+      timeout -k 10 600 python -u tools/ref_tscan.py --rows ${TSCAN_ROWS:-6 5 4} --chains ${TSCAN_CHAINS:-8} \
+        --extra-eta-mults 1.25 --out "$O/tscan" > "$O/tscan.log" 2>&1 || { tail -20 "$O/tscan.log"; exit 1; }
+      tail -5 "$O/tscan.log" ;;
+    bench)
+      timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 > "$O/bench_driver.json" 2> "$O/bench_driver.err" \
+        || { tail -20 "$O/bench_driver.err"; exit 1; }
+      timeout -k 10 300 python -u bench.py --gpus 1 --steps 200 --warmup 20 --no-cpu-baseline --no-c1 \
+        > "$O/bench_C3_200.json" 2> "$O/bench_C3_200.err" || exit 1
+      timeout -k 10 300 python -u bench.py --config C2 --steps 200 --warmup 20 --no-cpu-baseline --no-c1 \
+        > "$O/bench_C2.json" 2> "$O/bench_C2.err" || exit 1
+      timeout -k 10 300 python -u bench.py --config C5 --steps 40 --warmup 8 --no-cpu-baseline --no-c1 \
+        > "$O/bench_C5.json" 2> "$O/bench_C5.err" || exit 1
+      python - "$O" <<'PY'
+import json, sys, glob, os
+for f in sorted(glob.glob(os.path.join(sys.argv[1], "bench_*.json"))):
+    try:
+        d = json.loads(open(f).read().strip().splitlines()[-1])
+        print(os.path.basename(f), round(d["value"], 1), "steps/s", "poles", d["config"]["poles"],
+              "frac", round((d.get("roofline") or {}).get("frac") or 0, 3), "alg_frac", d.get("alg_frac_of_peak"))
+    except Exception as e:
+        print(f, e)
+PY
+      ;;
+    prof)
+      bash tools/profile_round.sh "$TAG" r04 || exit 1
+      python3 tools/trace_step.py "$R/gpurun_out/prof_$TAG/stats/run_kernel_trace.csv" > "$O/step.txt" || exit 1
+      rm -f "$R/gpurun_out/prof_$TAG/stats/run_kernel_trace.csv" ;;
+    sq)
+      bash tools/pmc_sq.sh "$TAG" || exit 1
+      /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 tools/micro/mfma_f64_peak.hip -o "$O/mfma_f64_peak" || exit 1
+      timeout -k 10 60 "$O/mfma_f64_peak" > "$O/mfma_f64_peak.txt" 2>&1 || exit 1
+      cat "$O/mfma_f64_peak.txt"
+      (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 60 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES \
+        SQ_WAVE_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$O/peak_pmc" -o run -- "$O/mfma_f64_peak" \
+        > "$O/peak_pmc.log" 2>&1) || exit 1
+      rm -f "$O/mfma_f64_peak" ;;
+    trans)
+      timeout -k 10 200 python -u tests/bench_transport.py --steps 3 --snapshots 4,8,16 > "$O/transport.json" \
+        2> "$O/transport.err" || exit 1 ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "== done $(date +%T)"
