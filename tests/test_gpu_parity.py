@@ -422,9 +422,24 @@ def test_guard_trip_recovers_in_throughput_path(dwhmc, oracle, algo_g, Lx, Ly):
         assert np.array_equal(x, y)
     ia, ib = a.info, b.info
     assert (ia["delta_cap"], ia["kappa"], ia["npoles"]) == (ib["delta_cap"], ib["kappa"], ib["npoles"])
-    # a stream handle taken before the re-selection stays the context's stream
+    # load_draws / run_sweeps / load_draws / sweep_results: the
+    # second upload settles the pending batch first, so its replay after the
+    # trip reads the draws it was enqueued with, not the new ones
+    c = device_ctx(dwhmc, p, dis2, algo_g, delta_cap=cap0)
+    c.set_pairing(D2)
+    c.factorize()
+    c.load_draws(noise, uni)
+    c.run_sweeps(0, ns, Nt, dt, p.mass)
+    c.load_draws(noise[::-1].copy() * 3.0, uni[::-1].copy())
+    acc, dH = c.sweep_results(0, ns)
+    for s in range(ns):
+        assert np.array_equal(acc[s], ref[s][0]), s
+        assert np.array_equal(dH[s], ref[s][1]), s
+    for x, y in zip(a.get_state(), c.get_state()):
+        assert np.array_equal(x, y)
     a.close()
     b.close()
+    c.close()
 
 
 def test_reselection_keeps_stream(dwhmc, oracle):
