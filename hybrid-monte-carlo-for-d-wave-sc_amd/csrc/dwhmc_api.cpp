@@ -119,6 +119,20 @@ struct CrPlan {
   int n_ph = 0;                              // entries of off_ph >= 0
 };
 
+// Lattice rows per CR block: DWHMC_CR_ROWS = 1 | 2 (default 1).  With two,
+// the blocks are pairs of rows (Ly / 2 blocks of 4 Lx BdG dimensions): one
+// CR level less (one inversion and three product launches fewer per step)
+// for 8x the work per block — a trade for narrow lattices, where every stage
+// is latency-bound.  Falls back to 1 when Ly is odd or the wider block is not
+// a supported size.
+int cr_rows_per_block(int64_t Lx, int64_t Ly) {
+  int r = 1;
+  if (const char* e = std::getenv("DWHMC_CR_ROWS")) r = std::atoi(e);
+  if (r != 2) return 1;
+  const int BP = (int)(2 * ((2 * Lx + 15) / 16 * 16));
+  return (Ly % 2 == 0 && dwh::cr_supported_bp(BP)) ? 2 : 1;
+}
+
 // Block cyclic reduction of the periodic block-tridiagonal H_BdG - i y (blocks
 // = lattice rows) into stages; restates tools/cr_model.py
 // cr_selected_inverse_top (checked there against dense inverses for Ly = 1 ..
@@ -147,6 +161,13 @@ struct CrPlan {
 //
 // inv0: the level-0 inversions use static R = A^-1 blocks (k_cr_inv0), one
 // per eliminated row, computed at context creation.
+//
+// Lx, Ly: the CR lattice — a block holds Lx consecutive sites of the linear
+// site index i = y * Lx + x, i.e. R = Lx / Lx_lattice lattice rows when the
+// context groups rows (cr_rows_per_block): every coupling stays between
+// neighbouring blocks (hopping and pairing span one lattice row), so the
+// recursion is the same; only which entries of the level-0 G blocks the
+// force reads changes (computed from Dcol below, not assumed diagonal).
 CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol, bool side, int nbatch,
                      int ncu, bool inv0) {
   const int side_woff = [] {
@@ -226,15 +247,38 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol, bool 
   std::vector<dwh::CrTask> cur_tasks;
   // output window of the next tasks (full block unless restricted)
   int w_r0 = 0, w_r1 = HP, w_c0 = 0, w_c1 = BP;
-  // per task of cur_tasks: compute only the A-part diagonal tiles and the
-  // B part (level-0 G_ee: the force reads its pairing (B) entries, E_f and
-  // Tr rho_hh its diagonal; nothing reads the rest)
-  // 2: only the diagonal tiles of the B part (level-0 G_ea / G_ec: the force
-  // reads their entries (x, HP + x) of the vertical bonds, nothing else)
-  std::vector<char> cur_adiag;
-  char adiag_next = 0;
+  // The level-0 G blocks are read only by the gathers: the force reads the
+  // pairing (B-part) entries (p_i, HP + p_j) of every bond, E_f and Tr rho_hh
+  // the diagonal (p, p) of G_D.  need[k][y]: the 16 x 16 top-half tiles
+  // (tr * (BP / 16) + tc) of G_D[y] (k = 0), G_U[y] = G[y, y+1] (1),
+  // G_L[y] = G[y+1, y] (2) that hold such entries — the block the gathers
+  // below resolve each bond to.  The last backward level computes only those
+  // tiles of its G_ea (= G_L), G_ec (= G_U) and G_ee (= G_D).  One lattice
+  // row per block: the diagonal B tiles of G_U / G_L (vertical bonds at
+  // (x, HP + x)); two rows: the off-diagonal ones.
+  const int ntc = BP / 16;
+  std::vector<std::vector<std::set<int>>> need(3, std::vector<std::set<int>>(Ly));
+  {
+    const int Ns = Lx * Ly;
+    for (int i = 0; i < Ns; ++i) {
+      const int pi = i % Lx, y = i / Lx;
+      need[0][y].insert((pi / 16) * ntc + pi / 16);
+      for (int s = 0; s < kSlots; ++s) {
+        const int j = Dcol[(size_t)i * kSlots + s];
+        if (j < 0) continue;
+        const int pj = j % Lx, yj = j / Lx;
+        const int tile = (pi / 16) * ntc + (HP + pj) / 16;
+        if (Ly == 1 || yj == y) need[0][y].insert(tile);
+        else if (yj == (y + 1) % Ly) need[1][y].insert(tile);
+        else need[2][(y - 1 + Ly) % Ly].insert(tile);
+      }
+    }
+  }
+  // per task of cur_tasks: the tiles to compute (nullptr: every tile of the window)
+  std::vector<const std::set<int>*> cur_keep;
+  const std::set<int>* keep_next = nullptr;
   auto task = [&](int out, int cin, std::initializer_list<Term> terms) {
-    cur_adiag.push_back(adiag_next);
+    cur_keep.push_back(keep_next);
     dwh::CrTask t{};
     t.out = out;
     t.cin = cin;
@@ -263,7 +307,7 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol, bool 
         side_flops[ord] += 8.0 * t.nt * BP * (double)(t.r1 - t.r0) * (t.c1 - t.c0);
       }
       cur_tasks.clear();
-      cur_adiag.clear();
+      cur_keep.clear();
       return;
     }
     CrStage st{};
@@ -281,8 +325,7 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol, bool 
       int kept = 0;
       for (int k = 0; k < nk; ++k) {
         const int tr = t.r0 / 16 + k / ct, tc = t.c0 / 16 + k % ct;
-        if (cur_adiag[ti] == 1 && tc < HP / 16 && tc != tr) continue;
-        if (cur_adiag[ti] == 2 && tc != HP / 16 + tr) continue;
+        if (cur_keep[ti] && !cur_keep[ti]->count(tr * ntc + tc)) continue;
         dwh::CrTile d{};
         d.out = t.out;
         d.cin = t.cin;
@@ -306,7 +349,7 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol, bool 
     st.ntiles = (int)pl.tiles16.size() - st.tfirst;
     pl.stages.push_back(st);
     cur_tasks.clear();
-    cur_adiag.clear();
+    cur_keep.clear();
   };
 
   Level cur;
@@ -391,7 +434,7 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol, bool 
           ul_tasks.push_back(cur_tasks[cur_tasks.size() - 2]);
           ul_tasks.push_back(cur_tasks.back());
           cur_tasks.resize(cur_tasks.size() - 2);
-          cur_adiag.resize(cur_adiag.size() - 2);
+          cur_keep.resize(cur_keep.size() - 2);
         }
         nxt.U.push_back(Un);
         nxt.L.push_back(Ln);
@@ -403,7 +446,7 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol, bool 
     flush(1.0);
     if (!ul_tasks.empty()) {
       cur_tasks = ul_tasks;
-      cur_adiag.assign(ul_tasks.size(), 0);
+      cur_keep.assign(ul_tasks.size(), nullptr);
       flush(1.0, true, inv_ord);
     }
     levels.push_back(cur);
@@ -423,11 +466,11 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol, bool 
         gl[k] = GL[kk];
       }
     }
-    // Level 0 is the last backward level: G_ea, G_ec (cross-row bonds, not
-    // operands of anything after them) are formed only on the diagonal tiles
-    // of their B part there (the vertical pairing bonds read (x, HP + x));
-    // G_ae, G_ce (right operands of G_ee) need their whole top half, G_ee
-    // (in-row bonds, hole diagonal) its A-part diagonal tiles and B part.
+    // Level 0 is the last backward level: G_ea, G_ec (cross-block bonds, not
+    // operands of anything after them) are formed only on the B-part tiles
+    // the vertical pairing bonds read (need); G_ae, G_ce (right operands of
+    // G_ee) need their whole top half, G_ee (in-block bonds, hole diagonal)
+    // its need tiles.
     const bool sel = (li == 0);
     const int H0 = sel ? HP : 0, H1 = sel ? HP + Lx : BP;
     std::vector<int> Gae(m, -1), Gce(m, -1);
@@ -440,10 +483,11 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol, bool 
       const int gea = nb(), gec = nb(), gae = nb(), gce = nb();
       w_c0 = H0;
       w_c1 = H1;
-      adiag_next = sel ? 2 : 0;
+      keep_next = sel ? &need[2][a] : nullptr;   // G_ea = G[a + 1, a] = G_L[a]
       task(gea, -1, {{lv.W1[e], Gaa}, {lv.W2[e], Gca}});
+      keep_next = sel ? &need[1][e] : nullptr;   // G_ec = G[e, e + 1] = G_U[e]
       task(gec, -1, {{lv.W1[e], Gac}, {lv.W2[e], Gcc}});
-      adiag_next = 0;
+      keep_next = nullptr;
       w_c0 = 0;
       w_c1 = BP;
       task(gae, -1, {{Gaa, lv.V1[e]}, {Gac, lv.V2[e]}});
@@ -456,12 +500,12 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol, bool 
       Gce[e] = gce;
     }
     flush(1.0);
-    adiag_next = sel ? 1 : 0;
     for (int e : lv.E) {
+      keep_next = sel ? &need[0][e] : nullptr;
       task(lv.Dinv[e], lv.Dinv[e], {{lv.W1[e], Gae[e]}, {lv.W2[e], Gce[e]}});
       gd[e] = lv.Dinv[e];
     }
-    adiag_next = 0;
+    keep_next = nullptr;
     flush(1.0);
     GD = gd;
     GU = gu;
@@ -1404,8 +1448,11 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
   d.mat = (int64_t)d.Np * d.Np;
   d.nld = d.nb;
   {
-    const int BP = (int)(2 * ((Lx + 15) / 16 * 16));   // top halves HP x BP, HP = Lx rounded to 16
-    const bool ok = dwh::cr_supported_bp(BP);
+    const bool ok = dwh::cr_supported_bp((int)(2 * ((Lx + 15) / 16 * 16)));
+    // the CR lattice: R lattice rows per block (cr_rows_per_block)
+    const int rows = ok ? cr_rows_per_block(Lx, Ly) : 1;
+    const int Lxc = (int)Lx * rows, Lyc = (int)Ly / rows;
+    const int BP = 2 * ((Lxc + 15) / 16 * 16);   // top halves HP x BP, HP = Lxc rounded to 16
     if (want == "cr" && !ok) {
       ctx->err = "DWHMC_ALGO=cr needs 2*Lx <= 128";
       g_create_error = ctx->err;
@@ -1423,17 +1470,17 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
       // DWHMC_CR_INV0=0: level-0 blocks inverted whole (k_cr_inv) like the rest
       const char* e0 = std::getenv("DWHMC_CR_INV0");
       const bool inv0 = dwh::cr_supported_inv0(BP) && !(e0 && *e0 == '0');
-      ctx->plan = build_cr_plan((int)Lx, (int)Ly, BP, Dcol, side, d.nbatch, ncu, inv0);
+      ctx->plan = build_cr_plan(Lxc, Lyc, BP, Dcol, side, d.nbatch, ncu, inv0);
       dwh::CrDims& c = ctx->cr;
-      c.Lx = (int)Lx;
-      c.Ly = (int)Ly;
+      c.Lx = Lxc;
+      c.Ly = Lyc;
       c.N = N;
       c.BP = BP;
       c.P = d.P;
       c.nbatch = d.nbatch;
       c.nblk = ctx->plan.nblk;
       c.item = (int64_t)c.nblk * (BP / 2) * BP;
-      d.nld = (int)Ly;
+      d.nld = Lyc;
       for (CrStage& st : ctx->plan.stages)
         if (st.kind == 1) st.cfg = dwh::cr_gemm_config(c, st.n, st.maxt32, st.maxt16, st.ntmax, st.ntiles);
       if (const char* e = std::getenv("DWHMC_CR_PLAN_DUMP"); e && *e == '1') {
@@ -1491,7 +1538,7 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     ALLOC(d_inv_dst, pl.inv_dst.size());
     ALLOC(d_inv_slot, pl.inv_slot.size());
     ALLOC(d_inv0_r, pl.inv0_r.size());
-    ALLOC(ldA, (size_t)d.nbatch * Ly);
+    ALLOC(ldA, (size_t)d.nbatch * ctx->cr.Ly);
     ALLOC(d_doff, pl.doff.size());
     ALLOC(d_off_ph, pl.off_ph.size());
     ALLOC(d_bond4, 4 * bij.size());
@@ -2701,17 +2748,35 @@ extern "C" {
 int dwh_debug_cr_plan_check(int64_t Lx, int64_t Ly, int64_t nbatch, int32_t side, int32_t inv0, int64_t* stats) {
   if (Lx < 1 || Ly < 1 || nbatch < 1) return fail(nullptr, DWH_ERR_ARG, "bad lattice / batch");
   std::vector<int> Dcol = nn_pairing_cols((int)Lx, (int)Ly);
-  const int BP = (int)(2 * ((Lx + 15) / 16 * 16));
-  if (!dwh::cr_supported_bp(BP)) return fail(nullptr, DWH_ERR_ARG, "lattice row too wide for the CR path");
-  const CrPlan pl = build_cr_plan((int)Lx, (int)Ly, BP, Dcol, side && dwh::cr_supported_side(BP), (int)nbatch,
+  if (!dwh::cr_supported_bp((int)(2 * ((Lx + 15) / 16 * 16))))
+    return fail(nullptr, DWH_ERR_ARG, "lattice row too wide for the CR path");
+  const int rows = cr_rows_per_block(Lx, Ly), Lxc = (int)Lx * rows, Lyc = (int)Ly / rows;
+  const int BP = 2 * ((Lxc + 15) / 16 * 16);
+  const CrPlan pl = build_cr_plan(Lxc, Lyc, BP, Dcol, side && dwh::cr_supported_side(BP), (int)nbatch,
                                   256, inv0 && dwh::cr_supported_inv0(BP));
   std::vector<int> written(pl.nblk, -1);   // stage of the first write; -2: ready from the start
-  for (int b = 0; b < 3 * (int)Ly && b < pl.nblk; ++b) written[b] = -2;
+  for (int b = 0; b < 3 * Lyc && b < pl.nblk; ++b) written[b] = -2;
   for (int r : pl.inv0_r) written[r] = -2;
   int64_t nside = 0, ninv = 0, ngemm = 0, ntask = 0;
   char buf[256];
+  // 16 x 16 tiles written so far (block, tile row, tile column): product
+  // stages write only their tile lists (restricted level-0 G blocks);
+  // inversions and side-work tasks whole blocks (whole[b])
+  const int ntc = BP / 16;
+  std::set<std::pair<int, int>> tiles_written;   // (block, tr * ntc + tc)
+  std::vector<char> whole(pl.nblk, 0);
+  for (int b = 0; b < pl.nblk; ++b) whole[b] = written[b] == -2;
   for (int si = 0; si < (int)pl.stages.size(); ++si) {
     const CrStage& st = pl.stages[si];
+    if (st.kind == 0) {
+      for (int k = 0; k < st.n; ++k) whole[pl.inv_dst[st.first + k]] = 1;
+      for (int k = 0; k < st.ntiles; ++k) whole[pl.tasks[st.tfirst + k].out] = 1;
+    } else {
+      for (int k = 0; k < st.ntiles; ++k) {
+        const dwh::CrTile& t = pl.tiles16[st.tfirst + k];
+        tiles_written.insert({t.out, t.tr * ntc + t.tc});
+      }
+    }
     std::vector<std::pair<int, int>> rd;   // (block, task id or -1)
     std::vector<std::pair<int, int>> wr;
     // ids: task k -> k (its accumulate input may be its output), its
@@ -2767,10 +2832,17 @@ int dwh_debug_cr_plan_check(int64_t Lx, int64_t Ly, int64_t nbatch, int32_t side
     }
   }
   const int64_t BB = (int64_t)(BP / 2) * BP;
+  // the gathers read entries of tiles some stage wrote (the level-0 backward
+  // stages compute only the tiles of their need sets, build_cr_plan)
+  auto tile_ok = [&](int64_t o) {
+    const int b = (int)(o / BB), r = (int)((o % BB) / BP), col = (int)(o % BP);
+    return whole[b] || tiles_written.count({b, (r / 16) * ntc + col / 16}) > 0;
+  };
   for (int64_t o : pl.goff)
-    if (o >= 0 && written[o / BB] == -1) return fail(nullptr, DWH_ERR_STATE, "force gather reads an unwritten block");
+    if (o >= 0 && (written[o / BB] == -1 || !tile_ok(o)))
+      return fail(nullptr, DWH_ERR_STATE, "force gather reads an unwritten block / tile");
   for (int64_t o : pl.doff)
-    if (written[o / BB] == -1) return fail(nullptr, DWH_ERR_STATE, "E_f gather reads an unwritten block");
+    if (written[o / BB] == -1 || !tile_ok(o)) return fail(nullptr, DWH_ERR_STATE, "E_f gather reads an unwritten block / tile");
   if (stats) {
     stats[0] = (int64_t)pl.stages.size();
     stats[1] = ninv;
@@ -2784,10 +2856,12 @@ int dwh_debug_cr_plan_check(int64_t Lx, int64_t Ly, int64_t nbatch, int32_t side
 
 int dwh_debug_cr_plan_flops(int64_t Lx, int64_t Ly, int64_t nbatch, int32_t side, int32_t inv0, double* flops) {
   if (Lx < 1 || Ly < 1 || nbatch < 1 || !flops) return fail(nullptr, DWH_ERR_ARG, "bad lattice / batch / output");
-  const int BP = (int)(2 * ((Lx + 15) / 16 * 16));
-  if (!dwh::cr_supported_bp(BP)) return fail(nullptr, DWH_ERR_ARG, "lattice row too wide for the CR path");
+  if (!dwh::cr_supported_bp((int)(2 * ((Lx + 15) / 16 * 16))))
+    return fail(nullptr, DWH_ERR_ARG, "lattice row too wide for the CR path");
+  const int rows = cr_rows_per_block(Lx, Ly), Lxc = (int)Lx * rows, Lyc = (int)Ly / rows;
+  const int BP = 2 * ((Lxc + 15) / 16 * 16);
   std::vector<int> Dcol = nn_pairing_cols((int)Lx, (int)Ly);
-  const CrPlan pl = build_cr_plan((int)Lx, (int)Ly, BP, Dcol, side && dwh::cr_supported_side(BP), (int)nbatch,
+  const CrPlan pl = build_cr_plan(Lxc, Lyc, BP, Dcol, side && dwh::cr_supported_side(BP), (int)nbatch,
                                   256, inv0 && dwh::cr_supported_inv0(BP));
   const double bp3 = 8.0 * BP * (double)BP * BP;
   flops[0] = flops[1] = flops[2] = 0.0;

@@ -310,21 +310,46 @@ def check_top_cr(Lx, Ly, seed=0, y=0.7):
 # device planner (build_cr_plan): the same levels and terms as
 # cr_selected_inverse_top, each product term on a top half (HP x BP output,
 # K = BP) at 8 BP HP BP flops, each block inversion at 8 BP^3.  At level 0 the
-# backward pass forms only what the force / E_f / Tr rho_hh read (16 x 16
-# output tiles): G_ea, G_ec only the diagonal tiles of the B part inside
-# columns [HP, HP + Lx); G_ee the A-part diagonal tiles and the whole B part.
+# backward pass forms only the 16 x 16 output tiles the gathers read: the
+# pairing entries G12[i, j] = G[b_i, b_j][p_i, HP + p_j] of every NN bond of
+# the periodic Lx x Ly lattice (both orders) and, in G_ee, the diagonal
+# (p, p).  rows: lattice rows per block (the device's DWHMC_CR_ROWS); block b
+# holds rows rows*b .. rows*b + rows - 1, site (x, y) at p = (y % rows) Lx + x.
+# G_ea / G_ec count per tile of their column window [HP, HP + Lxb), G_ee per
+# tile of the whole top half.  For a 2-block chain (m = 2) G_ea and G_ec are
+# both G[1, 0]; its reads are G_ec's (the planner's G_U[1]).
 # Returns (inversion flops, product flops) per batch item.
 # ---------------------------------------------------------------------------
-def cr_flop_count(Lx: int, Ly: int):
-    HP = (Lx + 15) // 16 * 16
+def level0_read_tiles(Lx: int, Ly: int, rows: int = 1):
+    """{(row block, column block): set of (tile row, tile column)} read by the
+    force (pairing entries) and E_f / Tr rho_hh (diagonal of the G_D blocks)."""
+    Lxb, m = Lx * rows, Ly // rows
+    HP = (Lxb + 15) // 16 * 16
+    reads = {}
+
+    def pos(x, y):
+        return y // rows, (y % rows) * Lx + x
+
+    for y in range(Ly):
+        for x in range(Lx):
+            bi, pi = pos(x, y)
+            reads.setdefault((bi, bi), set()).add((pi // 16, pi // 16))
+            for xj, yj in ((x + 1) % Lx, y), (x, (y + 1) % Ly), ((x - 1) % Lx, y), (x, (y - 1) % Ly):
+                bj, pj = pos(xj, yj)
+                reads.setdefault((bi, bj), set()).add((pi // 16, (HP + pj) // 16))
+    return reads
+
+
+def cr_flop_count(Lx: int, Ly: int, rows: int = 1):
+    Lxb, Lyb = Lx * rows, Ly // rows
+    HP = (Lxb + 15) // 16 * 16
     BP = 2 * HP
     full = 8.0 * BP * HP * BP                       # one term, whole top half
     tr = HP // 16                                   # tile rows
-    # G_ea / G_ec at level 0: window [HP, HP + Lx), B-part diagonal tiles only
-    wc = -(-(Lx) // 16)                             # tile columns of the window
-    sel_ea = 8.0 * BP * HP * Lx * (min(tr, wc) / (tr * wc))
-    # G_ee at level 0: A-part diagonal tiles + whole B part of BP/16 tile columns
-    sel_ee = full * ((tr + tr * tr) / (tr * 2 * tr))
+    wc = -(-(Lxb) // 16)                            # tile columns of the G_ea / G_ec window
+    per_ea = 8.0 * BP * HP * Lxb / (tr * wc)        # one term, one tile of that window
+    per_ee = full / (tr * 2 * tr)                   # one term, one tile of the top half
+    reads = level0_read_tiles(Lx, Ly, rows)
     inv = 0
     terms = 0.0
 
@@ -347,11 +372,15 @@ def cr_flop_count(Lx: int, Ly: int):
             if hr:
                 terms += 2 * full                   # U', L'
         level(len(K), depth + 1)
-        for _ in E:                                 # backward pass
+        for e in E:                                 # backward pass
             if depth == 0:
-                terms += 2 * 2 * sel_ea + 2 * 2 * full + 2 * sel_ee
+                a, c = e - 1, (e + 1) % m
+                n_ec = len(reads.get((e, c), ()))
+                n_ea = 0 if a == c else len(reads.get((e, a), ()))
+                n_ee = len(reads.get((e, e), ()))
+                terms += 2 * (n_ea + n_ec) * per_ea + 2 * 2 * full + 2 * n_ee * per_ee
             else:
                 terms += 5 * 2 * full               # G_ea, G_ec, G_ae, G_ce, G_ee: 2 terms each
 
-    level(Ly, 0)
+    level(Lyb, 0)
     return inv * 8.0 * BP ** 3, terms

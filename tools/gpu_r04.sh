@@ -5,6 +5,7 @@
 #   bench   the driver's command + C3 x200 + C2 + C5
 #   prof    rocprofv3 kernel stats + PMC traffic passes (tools/profile_round.sh) + step trace
 #   sq      SQ / MFMA-busy counters of the bench (tools/pmc_sq.sh) + the f64 MFMA peak micro
+#   c2rows  C2 with one and two lattice rows per CR block (DWHMC_CR_ROWS), alternated
 #   trans   transport timing (single measurement + snapshot batches)
 # Every GPU step runs under its own timeout; the first failure ends the script.
 set -o pipefail
@@ -58,6 +59,12 @@ PY
         SQ_WAVE_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$O/peak_pmc" -o run -- "$O/mfma_f64_peak" \
         > "$O/peak_pmc.log" 2>&1) || exit 1
       rm -f "$O/mfma_f64_peak" ;;
+    c2rows)
+      for r in 1 2 1 2; do
+        DWHMC_CR_ROWS=$r timeout -k 10 300 python -u bench.py --config C2 --steps 200 --warmup 20 --no-cpu-baseline \
+          --no-c1 > "$O/bench_C2_rows$r.json" 2> "$O/bench_C2_rows$r.err" || exit 1
+        python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[1], round(d['value'],1), d['config']['poles'], d.get('cr_inv'), d.get('cr_inv_side'))" "$O/bench_C2_rows$r.json"
+      done ;;
     trans)
       timeout -k 10 200 python -u tests/bench_transport.py --steps 3 --snapshots 4,8,16 > "$O/transport.json" \
         2> "$O/transport.err" || exit 1 ;;
