@@ -48,6 +48,9 @@ PEAK_HBM_GBS = 8000.0         # MI355X HBM3E peak (MI355X_MICROARCH.md)
 # newest committed PMC summary first (profiles/README.md)
 TRAFFIC_FILES = [os.path.join(ROOT, "profiles", f) for f in ("r03_pmc_traffic.json", "r02_pmc_traffic.json",
                                                                      "r01_pmc_traffic.json")]
+# SQ counter passes (tools/pmc_sq.sh -> tools/pmc_mfma.py): executed MFMA work per launch
+MFMA_FILES = [os.path.join(ROOT, "profiles", f) for f in ("r04_sq_mfma_L32.json",)]
+CLOCK_GHZ = 2.4                # the clock PEAK_F64_TFLOPS is quoted at (1024 SIMDs x 32 flop/cycle)
 
 
 def measured_traffic(kernel, L, beta, chains):
@@ -73,6 +76,29 @@ def measured_traffic(kernel, L, beta, chains):
             b = sum(k["hbm_bytes_per_launch"] * k.get("launches_fetch_pass", 1) for k in ks)
             return b / n, "profiles/" + os.path.basename(path)
     return None, None
+
+
+def measured_mfma(kernels, L, beta, chains):
+    """Executed MFMA flops and SQ_VALU_MFMA_BUSY_CYCLES per launch of a kernel
+    family (launch-weighted) from the committed SQ counter pass of this
+    workload, the attainable f64 MFMA rate measured beside it, and the file."""
+    for path in MFMA_FILES:
+        try:
+            with open(path) as f:
+                rec = json.load(f)
+        except (OSError, ValueError):
+            continue
+        w = rec.get("workload", {})
+        if (w.get("L"), w.get("beta"), w.get("chains")) != (L, beta, chains):
+            continue
+        ks = [rec.get("kernels", {}).get(n.replace(" ", "")) for n in kernels]
+        ks = [k for k in ks if k]
+        if ks:
+            n = sum(k["launches_per_step"] for k in ks)
+            busy = sum(k["mfma_busy_cycles_per_launch"] * k["launches_per_step"] for k in ks) / n
+            flops = sum(k["mfma_exec_flops_per_launch"] * k["launches_per_step"] for k in ks) / n
+            return busy, flops, rec.get("attainable_tflops"), "profiles/" + os.path.basename(path)
+    return None, None, None, None
 
 
 # BASELINE.json configs (SURVEY.md §8d); the headline line is C3.
@@ -464,6 +490,22 @@ def main(argv=None):
                                "avg_launch_us": 1000.0 * ms / n if n else None,
                                "flops_per_launch": w / n if n else None,
                                "replayed_steps": replay_steps}
+            # hardware view from the SQ counters of the same workload: the
+            # MFMA pipe's busy cycles per launch over the launch's duration
+            # (this run's HIP events) x 1024 SIMDs at the peak's clock, and the
+            # executed MFMA flops (3-multiplication complex MACs: 6 of every 8
+            # counted flops) against the peak and the attainable f64 MFMA rate
+            busy, xfl, att, msrc = measured_mfma(kfam if cr else [kname], a.L, a.beta, a.chains)
+            if busy is not None and n and ms > 0:
+                dur = ms / n * 1e-3
+                rf = rec["roofline"]
+                rf["mfma_busy_frac"] = busy / (dur * CLOCK_GHZ * 1e9 * 1024)
+                rf["hw_frac"] = xfl / dur / 1e12 / PEAK_F64_TFLOPS
+                rf["hw_flops_per_launch"] = xfl
+                rf["hw_over_alg_flops"] = xfl / (w / n) if w else None
+                rf["attainable_peak"] = att
+                rf["hw_frac_of_attainable"] = xfl / dur / 1e12 / att if att else None
+                rf["mfma_source"] = msrc
             rec[f"{dom}_ms_per_step"] = ms / replay_steps
             ms, n, w = kern["assemble"]
             if n and ms > 0:

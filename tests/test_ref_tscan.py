@@ -77,16 +77,23 @@ def loglog_fit(T, y):
 # ---------------------------------------------------------------------------
 ROWS_FIT = [16, 17, 18, 19, 20, 21, 22]          # T > 10 (cells 3 and 5)
 ROWS_R_LOW = [7, 8, 9, 10, 11, 12, 13, 14, 15]  # 0.027 <= T < 10 (cell 8)
+# the low-temperature rows (cell 8): β = 301, 149, 74 — the largest pole sets
+# of the scan (κ ≈ 1500, 730, 360: 23, 20, 18 pole pairs) and the worst-conditioned
+# no-pivot resolvents of the scan, across the resistive upturn (R = 0.51 ->
+# 20.8 -> 182149); 8 chains each (profiles/r04_ref_tscan_lowT.md)
+ROWS_R_COLD = [4, 5, 6]
 CHAINS = 4
+CHAINS_COLD = 8
 Z = 4.0
-# η of the published run, inferred (DESIGN.md §5,
-# profiles/r03_ref_tscan_investigation.md): with the 8/L² that
-# batch_scan_T.jl:17 sets today, R is 10-19 % below the published values at
-# T >= 30, where σ_DC is ~94 % diagonal (n = m) terms ∝ 1/η, while every
-# η-independent observable (Δ_Loc, Δ_LocalPair) matches; η = 10/L² (the
-# script's `* 1.0` factor at 1.25) reproduces the whole published R(T) curve,
-# 16 temperatures over five decades, within the statistical errors.  The
-# Markov chains do not depend on η (measurement only).
+# η of the published run.  The CPU oracle alone fixes it from the reference's
+# own T = 1000 point (tests/test_ref_tscan_oracle.py: R = 12368.6 is matched at
+# η = 10/L² and excludes the 8/L² that batch_scan_T.jl:17 sets today, where
+# σ_DC is ~93 % diagonal (n = m) terms ∝ 1/η).  At that η the HIP path is then
+# checked against the whole published curve here — a consistency check of
+# the path at the run's broadening, not a fit: the Markov chains do not depend
+# on η (measurement only), and with 8/L² the same chains miss the published
+# R by 10-19 % at T >= 30 (profiles/r03_ref_tscan_investigation.md; R(T)
+# against 8/L² stays parity-unpinned, the published run's η being inferred).
 ETA_MULT = 1.25
 
 
@@ -106,8 +113,9 @@ def _stat_tol(vals, ses, quantum):
 def scan(dwhmc, tmp_path_factory):
     out = str(tmp_path_factory.mktemp("tscan"))
     res = {}
-    for r in ROWS_FIT + ROWS_R_LOW:
-        res[r] = S.run_point(dwhmc, FX, r, CHAINS, out, seed=2024, eta_mult=ETA_MULT)
+    for r in ROWS_FIT + ROWS_R_LOW + ROWS_R_COLD:
+        res[r] = S.run_point(dwhmc, FX, r, CHAINS_COLD if r in ROWS_R_COLD else CHAINS, out, seed=2024,
+                             eta_mult=ETA_MULT)
     rec = os.environ.get("DWHMC_TSCAN_RECORD")
     if rec:
         with open(rec, "w") as f:
@@ -117,17 +125,19 @@ def scan(dwhmc, tmp_path_factory):
 
 @pytest.mark.gpu
 def test_published_dc_resistance(scan):
-    """R(T) = 1/⟨σ_DC⟩ (plot_stiffness.ipynb cell 8) at T >= 0.027 (rows 7 ..
-    22 of the summary) with η = 10/L² (ETA_MULT),
-    compared as σ_DC with the statistical tolerance of _stat_tol (Z = 4,
-    binned errors over 10 bins of 10 measurements per chain, K = 4 chains)
-    plus the %.6f rounding of the published mean (5e-7)."""
+    """R(T) = 1/⟨σ_DC⟩ (plot_stiffness.ipynb cell 8) at T >= 0.0033 (rows 4 ..
+    22 of the summary) with η = 10/L² (ETA_MULT), compared as σ_DC with the
+    statistical tolerance of _stat_tol (Z = 4, binned errors over 10 bins of
+    10 measurements per chain, K = 4 chains; K = 8 at the cold rows 4-6) plus
+    the rounding allowance: 5e-7 (the %.6f format of each measurement) at the
+    rows of round 3, 1e-8 (the resolution of a mean of 100 such values) at the
+    cold rows, where σ_DC is down to 5.5e-6."""
     bad = []
     for r, res in sorted(scan.items()):
         R_ref = FX["R_rows"][str(r)]
         vals = [c["DC_Conductivity"][0] for c in res["chains"]]
         ses = [c["DC_Conductivity"][1] for c in res["chains"]]
-        tol = _stat_tol(vals, ses, 5e-7)
+        tol = _stat_tol(vals, ses, 1e-8 if r in ROWS_R_COLD else 5e-7)
         diff = float(np.mean(vals)) - 1.0 / R_ref
         if abs(diff) > tol:
             bad.append((r, res["T"], 1.0 / float(np.mean(vals)), R_ref, diff, tol))
