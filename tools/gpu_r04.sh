@@ -6,6 +6,9 @@
 #   prof    rocprofv3 kernel stats + PMC traffic passes (tools/profile_round.sh) + step trace
 #   sq      SQ / MFMA-busy counters of the bench (tools/pmc_sq.sh) + the f64 MFMA peak micro
 #   c2rows  C2 with one and two lattice rows per CR block (DWHMC_CR_ROWS), alternated
+#   micro   tools/micro/inv16_variants and launch_floor (prebuilt in-tree)
+#   tscantest  tests/test_ref_tscan.py on the GPU
+#   driver  the driver's bench command only
 #   trans   transport timing (single measurement + snapshot batches)
 # Every GPU step runs under its own timeout; the first failure ends the script.
 set -o pipefail
@@ -65,6 +68,19 @@ PY
           --no-c1 > "$O/bench_C2_rows$r.json" 2> "$O/bench_C2_rows$r.err" || exit 1
         python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[1], round(d['value'],1), d['config']['poles'], d.get('cr_inv'), d.get('cr_inv_side'))" "$O/bench_C2_rows$r.json"
       done ;;
+    micro)
+      for m in inv16_variants launch_floor; do
+        timeout -k 10 120 tools/micro/$m > "$O/$m.txt" 2>&1 || { cat "$O/$m.txt"; exit 1; }
+        cat "$O/$m.txt"
+      done ;;
+    tscantest)
+      DWHMC_TSCAN_RECORD=$O/tscan_record.json timeout -k 10 900 python -u -m pytest tests/test_ref_tscan.py -m gpu -x -q \
+        --timeout 600 --timeout-method thread > "$O/tscantest.log" 2>&1 || { tail -40 "$O/tscantest.log"; exit 1; }
+      tail -3 "$O/tscantest.log" ;;
+    driver)
+      timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 > "$O/bench_driver.json" 2> "$O/bench_driver.err" \
+        || { tail -20 "$O/bench_driver.err"; exit 1; }
+      tail -c 1500 "$O/bench_driver.json" ;;
     trans)
       timeout -k 10 200 python -u tests/bench_transport.py --steps 3 --snapshots 4,8,16 > "$O/transport.json" \
         2> "$O/transport.err" || exit 1 ;;
