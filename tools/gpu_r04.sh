@@ -9,6 +9,8 @@
 #   micro   tools/micro/inv16_variants and launch_floor (prebuilt in-tree)
 #   tscantest  tests/test_ref_tscan.py on the GPU
 #   driver  the driver's bench command only
+#   ab      tools/ab_bench.py in-process A/B (AB_VARIANTS, AB_ARGS, AB_TAG)
+#   parity  a GPU parity subset (PARITY_K)
 #   trans   transport timing (single measurement + snapshot batches)
 # Every GPU step runs under its own timeout; the first failure ends the script.
 set -o pipefail
@@ -77,6 +79,14 @@ PY
       DWHMC_TSCAN_RECORD=$O/tscan_record.json timeout -k 10 900 python -u -m pytest tests/test_ref_tscan.py -m gpu -x -q \
         --timeout 600 --timeout-method thread > "$O/tscantest.log" 2>&1 || { tail -40 "$O/tscantest.log"; exit 1; }
       tail -3 "$O/tscantest.log" ;;
+    ab)   # AB_VARIANTS / AB_ARGS: tools/ab_bench.py variants and extra arguments (C3 by default)
+      timeout -k 10 400 python -u tools/ab_bench.py ${AB_ARGS:-} --variants ${AB_VARIANTS:?AB_VARIANTS} \
+        > "$O/ab${AB_TAG:-}.txt" 2>&1 || { tail -20 "$O/ab${AB_TAG:-}.txt"; exit 1; }
+      cat "$O/ab${AB_TAG:-}.txt" ;;
+    parity)   # a quick GPU parity subset (PARITY_K selects)
+      timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -k "${PARITY_K:-factorize_matches or full_size or hmc_sweep_matches}" \
+        --timeout 300 --timeout-method thread > "$O/parity.log" 2>&1 || { tail -40 "$O/parity.log"; exit 1; }
+      tail -3 "$O/parity.log" ;;
     driver)
       timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 > "$O/bench_driver.json" 2> "$O/bench_driver.err" \
         || { tail -20 "$O/bench_driver.err"; exit 1; }

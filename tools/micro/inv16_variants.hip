@@ -12,6 +12,7 @@
 //   V=3 panel-blocked: four 4-column panels, scalar steps on the panel only,
 //       rank-4 MFMA update of the rest (inv16_panel)
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 inv16_variants.hip -o inv16_variants
+#define DWHMC_INV_LA 0   // V=0 is the round-3 pivot step
 #include "../../hybrid-monte-carlo-for-d-wave-sc_amd/csrc/dwhmc_device.h"
 #include <cmath>
 #include <cstdio>
