@@ -93,6 +93,8 @@ SIGNATURES = {
     "dwh_debug_cr_plan_flops": (C.c_int, [_I64, _I64, _I64, _I32, _I32, _P]),
     "dwh_debug_h_bound": (C.c_int, [_I64, _I64, _D, _D, _D, _P, _P, _I64, _P, _P]),
     "dwh_selftest_mfma": (C.c_int, [_I32]),
+    "dwh_debug_gemm": (C.c_int, [_I32, _I32, C.c_char, C.c_char, _I64, _I64, _I64, _P, _P, _I64, _P, _I64, _P,
+                                 _P, _I64, _I64]),
 }
 
 _lib = None

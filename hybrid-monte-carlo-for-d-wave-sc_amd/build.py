@@ -15,7 +15,7 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libdwhmc.so")
 SOURCES = [os.path.join(CSRC, "dwhmc_kernels.hip"), os.path.join(CSRC, "dwhmc_cr.hip"),
-           os.path.join(CSRC, "dwhmc_eig.hip"),
+           os.path.join(CSRC, "dwhmc_eig.hip"), os.path.join(CSRC, "dwhmc_gemm.hip"),
            os.path.join(CSRC, "dwhmc_transport.hip"), os.path.join(CSRC, "dwhmc_api.cpp")]
 # rocBLAS (zgemm / dgemm products of the eigensolver and J_mn) and rocSOLVER
 # (zheevd / zheev: opt-in via DWHMC_EIG_SOLVER, and the fallback) serve the

@@ -921,17 +921,10 @@ void eig_enqueue(dwh_ctx* ctx) {
   }
   const dwh::TrBufs& b = ctx->tr;
   dwh::launch_eig_scale(b.U, b.JU, b.E, N, nc, ctx->beta, ctx->stream);
-  const rocblas_double_complex one(1.0, 0.0), zero(0.0, 0.0);
   const int64_t sA = (int64_t)n2 * n2;
-  const rocblas_status st = rocblas_zgemm_strided_batched(
-      ctx->blas, rocblas_operation_none, rocblas_operation_conjugate_transpose, n2, n2, n2, &one,
-      reinterpret_cast<const rocblas_double_complex*>(b.JU), n2, sA,
-      reinterpret_cast<const rocblas_double_complex*>(b.U), n2, sA, &zero,
-      reinterpret_cast<rocblas_double_complex*>(b.Jmn), n2, sA, nc);
-  if (st != rocblas_status_success) {
-    ctx->async_rc = fail(ctx, DWH_ERR_HIP, std::string("rocblas_zgemm: ") + rocblas_status_to_string(st));
-    return;
-  }
+  // rho = (U f) U^H, the library's own product
+  dwh::gemm_z('N', 'C', n2, n2, n2, make_double2(1.0, 0.0), b.JU, n2, sA, b.U, n2, sA, make_double2(0.0, 0.0),
+              b.Jmn, n2, sA, nc, ctx->stream);
   dwh::launch_eig_gather(b.Jmn, b.E, N, nc, ctx->Dcol, ctx->bond_ij, ctx->beta, ctx->Pair, ctx->Ef, ctx->Trhh,
                          ctx->stream);
 }
@@ -1860,68 +1853,34 @@ int own_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m) {
   // by ~ F_jl |λ_j - λ_l| ~ c eps ||T||: orthogonality to rounding, accuracy kept.
   double* G = Ud;          // the slots' U buffers (LU scratch until now)
   double* Y2 = Zt + sA;    // second half of the slots' Jmn buffers
-  {
-    const double one = 1.0, zero = 0.0, mhalf = -0.5, thalf = 1.5;
-    rocblas_status st = rocblas_dgemm_strided_batched(ctx->blas, rocblas_operation_none,
-                                                      rocblas_operation_transpose, n, n, n, &one, Zt, n, sZ, Zt,
-                                                      n, sZ, &zero, G, n, sZ, m);
-    if (st == rocblas_status_success) {
-      HIPCHECK(ctx, hipMemcpy2DAsync(Y2, sZ * sizeof(double), Zt, sZ * sizeof(double), sA * sizeof(double), m,
-                                     hipMemcpyDeviceToDevice, s));
-      st = rocblas_dgemm_strided_batched(ctx->blas, rocblas_operation_none, rocblas_operation_none, n, n, n,
-                                         &mhalf, G, n, sZ, Zt, n, sZ, &thalf, Y2, n, sZ, m);
-    }
-    if (st != rocblas_status_success)
-      return fail(ctx, DWH_ERR_HIP, std::string("rocblas_dgemm (eigenvector orthogonalisation): ") +
-                                        rocblas_status_to_string(st));
-  }
+  dwh::gemm_d('N', 'T', n, n, n, 1.0, Zt, n, sZ, Zt, n, sZ, 0.0, G, n, sZ, m, s);
+  HIPCHECK(ctx, hipMemcpy2DAsync(Y2, sZ * sizeof(double), Zt, sZ * sizeof(double), sA * sizeof(double), m,
+                                 hipMemcpyDeviceToDevice, s));
+  dwh::gemm_d('N', 'N', n, n, n, -0.5, G, n, sZ, Zt, n, sZ, 1.5, Y2, n, sZ, m, s);
   dwh::launch_eig_zt_to_u(Y2, b.U, n, sZ, sA, m, s);
   HIPCHECK(ctx, hipGetLastError());
   if (n < 2) return DWH_OK;
   dwh::launch_eig_tfac(A, n, sA, ctx->d_eig_tau, ctx->d_eig_W, ctx->d_eig_T, sT, m, s);   // W as Gram scratch
   HIPCHECK(ctx, hipGetLastError());
-  // U = (I - V_0 T_0 V_0^H) ... (I - V_last T_last V_last^H) Z, last block first
-  using C = rocblas_double_complex;
-  const C one(1.0, 0.0), zero(0.0, 0.0), mone(-1.0, 0.0);
+  // U = (I - V_0 T_0 V_0^H) ... (I - V_last T_last V_last^H) Z, last block first,
+  // on the library's own products (dwhmc_gemm.hip)
+  const double2 one = make_double2(1.0, 0.0), zero = make_double2(0.0, 0.0), mone = make_double2(-1.0, 0.0);
   for (int blk = nblk - 1; blk >= 0; --blk) {
     const int j0 = blk * NB, kb = std::min(NB, n - 1 - j0), ms = n - j0 - 1;
-    const C* Vb = reinterpret_cast<const C*>(A + (j0 + 1) + (int64_t)j0 * n);
-    C* Us = reinterpret_cast<C*>(b.U + (j0 + 1));
-    C* W = reinterpret_cast<C*>(ctx->d_eig_W);
-    C* W2 = reinterpret_cast<C*>(ctx->d_eig_W2);
+    const double2* Vb = A + (j0 + 1) + (int64_t)j0 * n;
+    double2* Us = b.U + (j0 + 1);
     const int ldw = ks * NB;
-    // chunks of c rows (a multiple of 16), the last one shorter
+    // W = V^H U in K chunks of c rows (a multiple of 16, the last one shorter),
+    // chunk s at rows s kb of W: one launch for every (matrix, chunk)
     const int c = ks == 1 ? ms : std::max(16, ((ms + ks - 1) / ks + 15) / 16 * 16);
     const int nfull = ms / c, rem = ms - nfull * c, S = nfull + (rem > 0);
-    rocblas_status st = rocblas_status_success;
-    if (ks == 1) {
-      st = rocblas_zgemm_strided_batched(ctx->blas, rocblas_operation_conjugate_transpose, rocblas_operation_none,
-                                         kb, n, ms, &one, Vb, n, sA, Us, n, sA, &zero, W, ldw, sWs, m);
-    } else {
-      for (int k = 0; k < m && st == rocblas_status_success; ++k) {
-        const C* Vk = Vb + k * sA;
-        const C* Uk = Us + k * sA;
-        C* Wk = W + k * sWs;
-        if (nfull > 0)
-          st = rocblas_zgemm_strided_batched(ctx->blas, rocblas_operation_conjugate_transpose,
-                                             rocblas_operation_none, kb, n, c, &one, Vk, n, c, Uk, n, c, &zero, Wk,
-                                             ldw, kb, nfull);
-        if (st == rocblas_status_success && rem > 0)
-          st = rocblas_zgemm(ctx->blas, rocblas_operation_conjugate_transpose, rocblas_operation_none, kb, n, rem,
-                             &one, Vk + (int64_t)nfull * c, n, Uk + (int64_t)nfull * c, n, &zero,
-                             Wk + (int64_t)nfull * kb, ldw);
-      }
-    }
-    if (st == rocblas_status_success) {
-      dwh::launch_eig_tw(ctx->d_eig_T + (int64_t)blk * NB * NB, sT, ctx->d_eig_W, ldw, sWs, S, kb, n,
-                         ctx->d_eig_W2, sW, m, s);
-      st = rocblas_zgemm_strided_batched(ctx->blas, rocblas_operation_none, rocblas_operation_none, ms, n, kb,
-                                         &mone, Vb, n, sA, W2, NB, sW, &one, Us, n, sA, m);
-    }
-    if (st != rocblas_status_success)
-      return fail(ctx, DWH_ERR_HIP, std::string("rocblas_zgemm (eigenvector back-transform): ") +
-                                        rocblas_status_to_string(st));
+    dwh::gemm_z_chunked('C', 'N', kb, n, c, rem > 0 ? rem : c, S, one, Vb, n, c, sA, Us, n, c, sA, zero,
+                        ctx->d_eig_W, ldw, kb, sWs, m, s);
+    dwh::launch_eig_tw(ctx->d_eig_T + (int64_t)blk * NB * NB, sT, ctx->d_eig_W, ldw, sWs, S, kb, n,
+                       ctx->d_eig_W2, sW, m, s);
+    dwh::gemm_z('N', 'N', ms, n, kb, mone, Vb, n, sA, ctx->d_eig_W2, NB, sW, one, Us, n, sA, m, s);
   }
+  HIPCHECK(ctx, hipGetLastError());
   return DWH_OK;
 }
 
@@ -2021,16 +1980,11 @@ int transport_run(dwh_ctx* ctx, const TrSrc& src, int m, double eta, double dome
     dwh::launch_tr_current(b.U, b.JU, N, ctx->d_tr_rowptr, ctx->d_tr_col, ctx->d_tr_val, s);
   }
   HIPCHECK(ctx, hipGetLastError());
-  // J_mn = U^H (J ⊕ J) U  (src/Observables.jl:334-335)
-  const rocblas_double_complex one(1.0, 0.0), zero(0.0, 0.0);
+  // J_mn = U^H (J ⊕ J) U  (src/Observables.jl:334-335), the library's own product
   const dwh::TrBufs& b0 = ctx->tr;
-  const rocblas_status st = rocblas_zgemm_strided_batched(
-      ctx->blas, rocblas_operation_conjugate_transpose, rocblas_operation_none, n2, n2, n2, &one,
-      reinterpret_cast<const rocblas_double_complex*>(b0.U), n2, sA,
-      reinterpret_cast<const rocblas_double_complex*>(b0.JU), n2, sA, &zero,
-      reinterpret_cast<rocblas_double_complex*>(b0.Jmn), n2, sA, m);
-  if (st != rocblas_status_success)
-    return fail(ctx, DWH_ERR_HIP, std::string("rocblas_zgemm: ") + rocblas_status_to_string(st));
+  dwh::gemm_z('C', 'N', n2, n2, n2, make_double2(1.0, 0.0), b0.U, n2, sA, b0.JU, n2, sA, make_double2(0.0, 0.0),
+              b0.Jmn, n2, sA, m, s);
+  HIPCHECK(ctx, hipGetLastError());
   const dwh::TrGrid g{eta, -omega_max, domega, (int)nw, (int)nd};
   for (int k = 0; k < m; ++k)
     dwh::launch_tr_reduce(tr_slot(ctx, k), N, (int)ctx->Lx, (int)ctx->Ly, ctx->beta, eta, g, s);
@@ -2716,6 +2670,52 @@ int dwh_timing_reset(dwh_ctx* ctx) {
 }
 
 int dwh_selftest_mfma(int32_t device) { return dwh::selftest_mfma_layout(device); }
+
+int dwh_debug_gemm(int32_t device, int32_t cplx, char opa, char opb, int64_t M, int64_t N, int64_t K,
+                   const double* alpha, const void* A, int64_t lda, const void* B, int64_t ldb, const double* beta,
+                   void* C, int64_t ldc, int64_t batch) {
+  if (M < 1 || N < 1 || K < 0 || batch < 1 || !alpha || !beta || !A || !B || !C)
+    return fail(nullptr, DWH_ERR_ARG, "bad gemm arguments");
+  if ((opa != 'N' && opa != 'C') || (opb != 'N' && opb != 'C'))
+    return fail(nullptr, DWH_ERR_ARG, "op must be 'N' or 'C'");
+  const int64_t acols = opa == 'N' ? K : M, bcols = opb == 'N' ? N : K;
+  const int64_t arows = opa == 'N' ? M : K, brows = opb == 'N' ? K : N;
+  if (lda < std::max<int64_t>(1, arows) || ldb < std::max<int64_t>(1, brows) || ldc < M)
+    return fail(nullptr, DWH_ERR_ARG, "leading dimension too small");
+  const size_t es = cplx ? sizeof(double2) : sizeof(double);
+  const int64_t sA = lda * std::max<int64_t>(acols, 1), sB = ldb * std::max<int64_t>(bcols, 1), sC = ldc * N;
+  if (hipSetDevice(device) != hipSuccess) return fail(nullptr, DWH_ERR_HIP, "hipSetDevice failed");
+  void *dA = nullptr, *dB = nullptr, *dC = nullptr;
+  auto cleanup = [&]() {
+    (void)hipFree(dA);
+    (void)hipFree(dB);
+    (void)hipFree(dC);
+  };
+  if (hipMalloc(&dA, es * sA * batch) != hipSuccess || hipMalloc(&dB, es * sB * batch) != hipSuccess ||
+      hipMalloc(&dC, es * sC * batch) != hipSuccess) {
+    cleanup();
+    return fail(nullptr, DWH_ERR_HIP, "hipMalloc (gemm test buffers)");
+  }
+  hipError_t e = hipMemcpy(dA, A, es * sA * batch, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(dB, B, es * sB * batch, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(dC, C, es * sC * batch, hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    if (cplx)
+      dwh::gemm_z(opa, opb, (int)M, (int)N, (int)K, make_double2(alpha[0], alpha[1]), (const double2*)dA, (int)lda,
+                  sA, (const double2*)dB, (int)ldb, sB, make_double2(beta[0], beta[1]), (double2*)dC, (int)ldc, sC,
+                  (int)batch, nullptr);
+    else
+      dwh::gemm_d(opa == 'C' ? 'T' : 'N', opb == 'C' ? 'T' : 'N', (int)M, (int)N, (int)K, alpha[0],
+                  (const double*)dA, (int)lda, sA, (const double*)dB, (int)ldb, sB, beta[0], (double*)dC, (int)ldc,
+                  sC, (int)batch, nullptr);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpy(C, dC, es * sC * batch, hipMemcpyDeviceToHost);
+  cleanup();
+  if (e != hipSuccess) return fail(nullptr, DWH_ERR_HIP, std::string("gemm test: ") + hipGetErrorString(e));
+  return DWH_OK;
+}
 
 }  // extern "C"
 

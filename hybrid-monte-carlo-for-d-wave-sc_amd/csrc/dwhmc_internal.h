@@ -265,6 +265,21 @@ void launch_eig_tfac(const double2* V, int n, int64_t sA, const double2* tau, do
 void launch_eig_tw(const double2* Tb, int64_t sT, const double2* W, int ldw, int64_t sW, int S, int kb, int n,
                    double2* W2, int64_t sW2, int m, hipStream_t s);
 
+// The library's own batched fp64 products (dwhmc_gemm.hip):
+// C = alpha op(A) op(B) + beta C, column-major, op 'N' or 'C' (conjugate
+// transpose; 'T' for real), per-matrix strides sA / sB / sC (elements)
+void gemm_z(char opa, char opb, int M, int N, int K, double2 alpha, const double2* A, int lda, int64_t sA,
+            const double2* B, int ldb, int64_t sB, double2 beta, double2* C, int ldc, int64_t sC, int batch,
+            hipStream_t s);
+// two-level batch: batch x S products, operands at outer * x2 + s * x1; the
+// last inner one (s = S - 1) with K = Klast
+void gemm_z_chunked(char opa, char opb, int M, int N, int K, int Klast, int S, double2 alpha, const double2* A,
+                    int lda, int64_t a1, int64_t a2, const double2* B, int ldb, int64_t b1, int64_t b2,
+                    double2 beta, double2* C, int ldc, int64_t c1, int64_t c2, int batch, hipStream_t s);
+void gemm_d(char opa, char opb, int M, int N, int K, double alpha, const double* A, int lda, int64_t sA,
+            const double* B, int ldb, int64_t sB, double beta, double* C, int ldc, int64_t sC, int batch,
+            hipStream_t s);
+
 int selftest_mfma_layout(int device);
 
 }  // namespace dwh

@@ -295,6 +295,17 @@ int dwh_debug_h_bound(int64_t Lx, int64_t Ly, double t, double tp, double mu, co
 /* Self-test of the f64 MFMA fragment layout (A = I, asymmetric B); 0 = pass. */
 int dwh_selftest_mfma(int32_t device);
 
+/* The library's own batched fp64 MFMA product (the measurement path's
+ * J_mn = U^H J U, the eigensolver's back-transform and orthogonalisation, the
+ * eig path's rho), through host buffers for tests:
+ * C_k = alpha op(A_k) op(B_k) + beta C_k, k < batch, column-major, op 'N' or
+ * 'C' (conjugate transpose; transpose when real); cplx 1: dwh_c128 data and
+ * alpha / beta as {re, im}, 0: double (alpha[0], beta[0]).  Batch strides:
+ * lda * (columns of A), ldb * (columns of B), ldc * N elements. */
+int dwh_debug_gemm(int32_t device, int32_t cplx, char opa, char opb, int64_t M, int64_t N, int64_t K,
+                   const double* alpha, const void* A, int64_t lda, const void* B, int64_t ldb, const double* beta,
+                   void* C, int64_t ldc, int64_t batch);
+
 #ifdef __cplusplus
 }
 #endif
