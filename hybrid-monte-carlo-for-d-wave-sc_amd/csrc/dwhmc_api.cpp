@@ -1844,8 +1844,12 @@ int own_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m) {
   dwh::launch_eig_bisect(ctx->d_eig_d, ctx->d_eig_e, n, b.E, ctx->d_eig_tn, m, s);
   double* Zt = reinterpret_cast<double*>(b.Jmn);
   double* Ud = reinterpret_cast<double*>(b.U);
+  // DWHMC_EIG_MAX_CLUSTER (tests): a shorter cluster limit, to exercise the
+  // rocSOLVER fallback of eigen_solve
+  int maxc = dwh::kEigMaxCluster;
+  if (const char* e = std::getenv("DWHMC_EIG_MAX_CLUSTER")) maxc = std::max(1, std::min(maxc, std::atoi(e)));
   dwh::launch_eig_invit(ctx->d_eig_d, ctx->d_eig_e, n, b.E, ctx->d_eig_tn, Zt, Zt + sA, Ud, Ud + sA, sZ,
-                        ctx->d_tr_bad, m, s);
+                        ctx->d_tr_bad, m, s, maxc);
   // One symmetric (Löwdin) orthogonalisation step over all vectors: with
   // Y = Z^T (column-major Zt) and G = Y Y^T = I + F, Y <- (3/2 I - 1/2 G) Y
   // leaves ||F|| -> O(||F||^2).  Outside clusters F_jl ~ c eps ||T|| / |λ_j - λ_l|
@@ -1948,7 +1952,8 @@ int eigen_info_check(dwh_ctx* ctx, int m) {
   HIPCHECK(ctx, hipGetLastError());
   for (int k = 0; k < m; ++k)
     if (info[k] != 0)
-      return fail(ctx, DWH_ERR_HIP, "rocsolver_zheevd did not converge (info = " + std::to_string(info[k]) + ")");
+      return fail(ctx, DWH_ERR_HIP, "the rocSOLVER eigensolver (zheevd / zheev fallback) did not converge (info = " +
+                                        std::to_string(info[k]) + ")");
   return DWH_OK;
 }
 

@@ -595,7 +595,7 @@ __global__ __launch_bounds__(64) void k_eig_invit(const double* __restrict__ d, 
 // positive definite (the caller then re-solves with rocSOLVER's zheev).
 __global__ __launch_bounds__(256) void k_eig_orth(const double* __restrict__ E, const double* __restrict__ tnorm,
                                                   int n, double* __restrict__ Zt, int64_t sZ, double ctol,
-                                                  int* __restrict__ bad) {
+                                                  int* __restrict__ bad, int maxc) {
   constexpr int MC = kEigMaxCluster;
   const int k = blockIdx.y, j = blockIdx.x, tid = threadIdx.x;
   E += (int64_t)k * n;
@@ -606,7 +606,7 @@ __global__ __launch_bounds__(256) void k_eig_orth(const double* __restrict__ E, 
   while (end < n && end - j <= MC && E[end] - E[end - 1] <= tol) ++end;
   const int kc = end - j;
   if (kc == 1) return;
-  if (kc > MC) {
+  if (kc > maxc) {
     if (tid == 0) *bad = 1;
     return;
   }
@@ -874,10 +874,11 @@ void launch_eig_bisect(const double* d, const double* e, int n, double* E, doubl
 }
 
 void launch_eig_invit(const double* d, const double* e, int n, const double* E, const double* tnorm, double* Zt,
-                      double* U0, double* U1, double* U2, int64_t sZ, int* bad, int m, hipStream_t s) {
+                      double* U0, double* U1, double* U2, int64_t sZ, int* bad, int m, hipStream_t s, int maxc) {
   hipLaunchKernelGGL(k_eig_invit, dim3((n + 63) / 64, m), dim3(64), 2 * n * sizeof(double), s, d, e, n, E, tnorm, Zt,
                      U0, U1, U2, sZ);
-  hipLaunchKernelGGL(k_eig_orth, dim3(n, m), dim3(256), 0, s, E, tnorm, n, Zt, sZ, kEigClusterTol, bad);
+  hipLaunchKernelGGL(k_eig_orth, dim3(n, m), dim3(256), 0, s, E, tnorm, n, Zt, sZ, kEigClusterTol, bad,
+                     maxc < 1 || maxc > kEigMaxCluster ? kEigMaxCluster : maxc);
 }
 
 void launch_eig_zt_to_u(const double* Zt, double2* U, int n, int64_t sZ, int64_t sA, int m, hipStream_t s) {

@@ -252,9 +252,11 @@ void launch_eig_pass(double2* A, int n, int i, int64_t sA, double2* part, int64_
                      const double2* ww, double2* dpart, int m, hipStream_t s);
 // eigenvalues ascending into E, ||T|| bound per matrix into tnorm
 void launch_eig_bisect(const double* d, const double* e, int n, double* E, double* tnorm, int m, hipStream_t s);
-// eigenvectors of T into Zt (Zt[r n + j]: component r of vector j), clusters orthonormalised
+// eigenvectors of T into Zt (Zt[r n + j]: component r of vector j), clusters orthonormalised;
+// a cluster longer than maxc (<= kEigMaxCluster) sets *bad (the caller's vendor fallback)
 void launch_eig_invit(const double* d, const double* e, int n, const double* E, const double* tnorm, double* Zt,
-                      double* U0, double* U1, double* U2, int64_t sZ, int* bad, int m, hipStream_t s);
+                      double* U0, double* U1, double* U2, int64_t sZ, int* bad, int m, hipStream_t s,
+                      int maxc = kEigMaxCluster);
 void launch_eig_zt_to_u(const double* Zt, double2* U, int n, int64_t sZ, int64_t sA, int m, hipStream_t s);
 constexpr int kEigDeferMin = 4;             // batches from this many matrices defer every other rank-2 update
 constexpr int kEigGS = 8;                   // row slices of each block's Gram sum

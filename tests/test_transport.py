@@ -172,6 +172,58 @@ def test_own_eigensolver_full_size(dwhmc, oracle, Lx, Ly, beta, clean):
     assert np.max(np.abs(U.conj().T @ U - np.eye(2 * p.N))) <= 1e-12
 
 
+@pytest.mark.gpu
+def test_own_eigensolver_L48(dwhmc, oracle):
+    """C5's lattice (48 x 48, n = 4608: the k_eig_step row slots beyond 2048,
+    the 73.7 KiB of dynamic LDS of k_eig_bisect / k_eig_invit, the cluster
+    density of 4608 levels) through the own solver with no rocSOLVER fallback,
+    against LAPACK zheevr at the tolerances of test_own_eigensolver_full_size
+    (kEigMaxN covers it)."""
+    O = oracle
+    p, dis, D = _case(O, 48, 48, 32.0, seed=4848)
+    cache, _, _ = O.evaluate(p, dis, D)
+    ctx = _ctx(dwhmc, p, dis)
+    ctx.set_pairing(D)
+    ctx.timing_enable(["eig_own", "eig_vendor"])
+    E, U = ctx.eigensystem(0)
+    own, vendor = ctx.timing_read("eig_own")[1], ctx.timing_read("eig_vendor")[1]
+    ctx.close()
+    assert (own, vendor) == (1, 0)
+    H = O.hermitian_from_upper(cache.H_base)
+    scale = 1 + np.max(np.abs(cache.E_n))
+    assert np.all(np.isfinite(U))
+    assert np.max(np.abs(E - cache.E_n)) <= 1e-12 * scale
+    assert np.max(np.abs(H @ U - U * E[None, :])) <= 1e-11 * scale
+    assert np.max(np.abs(U.conj().T @ U - np.eye(2 * p.N))) <= 1e-12
+
+
+@pytest.mark.gpu
+def test_eigensolver_vendor_fallback(dwhmc, oracle, monkeypatch):
+    """The rocSOLVER fallback of eigen_solve (k_eig_orth flags a cluster
+    longer than its limit): DWHMC_EIG_MAX_CLUSTER=1 makes every degenerate
+    pair of a clean lattice a flagged cluster, so the own solve is followed by
+    rocSOLVER's zheev (eig_vendor counts it), whose eigenpairs meet the same
+    tolerances (the bad-flag hand-off was never exercised)."""
+    O = oracle
+    monkeypatch.setenv("DWHMC_EIG_MAX_CLUSTER", "1")
+    p = O.ModelParameters(12, 10, T, TP, -1.0, 0.0, 0.0, 4.0, 0.8, 1.0)
+    dis = np.zeros(p.N)
+    D = np.stack([np.full(p.N, 0.2), np.full(p.N, -0.2)], 1).astype(np.complex128)
+    cache, _, _ = O.evaluate(p, dis, D)
+    ctx = _ctx(dwhmc, p, dis)
+    ctx.set_pairing(D)
+    ctx.timing_enable(["eig_own", "eig_vendor"])
+    E, U = ctx.eigensystem(0)
+    own, vendor = ctx.timing_read("eig_own")[1], ctx.timing_read("eig_vendor")[1]
+    ctx.close()
+    assert (own, vendor) == (1, 1)
+    H = O.hermitian_from_upper(cache.H_base)
+    scale = 1 + np.max(np.abs(cache.E_n))
+    assert np.max(np.abs(E - cache.E_n)) <= 1e-12 * scale
+    assert np.max(np.abs(H @ U - U * E[None, :])) <= 1e-11 * scale
+    assert np.max(np.abs(U.conj().T @ U - np.eye(2 * p.N))) <= 1e-12
+
+
 def _check_transport(r, ref):
     for k in ("superfluid_stiffness", "dc_conductivity"):
         assert abs(r[k] - ref[k]) <= 1e-9 * (1 + abs(ref[k])), (k, r[k], ref[k])
