@@ -11,8 +11,8 @@ loop form are the pins; the absolute values are otherwise "parity unpinned"
 against a Julia run.
 
 GPU: the device path (the hand-written eigensolver csrc/dwhmc_eig.hip, with
-rocSOLVER zheev only where it flags a result, + rocBLAS zgemm +
-dwhmc_transport.hip)
+rocSOLVER zheev only where it flags a result, + the library's own MFMA
+products csrc/dwhmc_gemm.hip + dwhmc_transport.hip)
 through the C ABI vs the oracle on the same Δ.  Tolerances (fp64):
   * eigenvalues          |E_gpu - E_ref| ≤ 1e-12 (1 + max|E|)
   * stiffness, dc        |Δ| ≤ 1e-9 (1 + |ref|)
