@@ -11,6 +11,8 @@
 //   V=2 V=1 with one Newton step on v_rcp_f64 instead of two
 //   V=3 panel-blocked: four 4-column panels, scalar steps on the panel only,
 //       rank-4 MFMA update of the rest (inv16_panel)
+//   V=4 V=1 with the DPP row broadcast fused into the update FMAs
+//       (v_fmac_f64_dpp row_newbcast, la_step_fused)
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 inv16_variants.hip -o inv16_variants
 #define DWHMC_INV_LA 0   // V=0 is the round-3 pivot step
 #include "../../hybrid-monte-carlo-for-d-wave-sc_amd/csrc/dwhmc_device.h"
@@ -67,6 +69,60 @@ __device__ __forceinline__ void la_step(double2 (&a)[4], double2& cp, double& pp
     cp = v;
   }
 }
+// V=4: the column-lookahead step with the DPP row broadcast fused into the
+// update FMAs (v_fmac_f64_dpp row_newbcast: src0 read from lane P of each
+// 16-lane row), one v_mov_b64 copy per complex entry for the in-place hazard
+// (the pivot row's own lanes need their unscaled value after the first FMA);
+// the fold's +1 of column P goes onto the pivot element itself (and off again
+// after: (a + 1)(1 - f_P) - 1 = 1/piv).
+template <int P>
+__device__ __forceinline__ void fused_upd(double& ax, double& ay, double nfx, double nfy, double fy) {
+  double t;
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_mov_b64 %[t], %[ay]\n\t"
+      "v_fmac_f64_dpp %[ay], %[ax], %[nfy] row_newbcast:%c[p] row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[ax], %[ax], %[nfx] row_newbcast:%c[p] row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[ax], %[t], %[fy] row_newbcast:%c[p] row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f64_dpp %[ay], %[t], %[nfx] row_newbcast:%c[p] row_mask:0xf bank_mask:0xf"
+      : [ax] "+v"(ax), [ay] "+v"(ay), [t] "=&v"(t)
+      : [nfx] "v"(nfx), [nfy] "v"(nfy), [fy] "v"(fy), [p] "i"(P));
+}
+template <int P>
+__device__ __forceinline__ void la_step_fused(double2 (&a)[4], double2& cp, double& pprod) {
+  constexpr int PS = P & 3, PE = P >> 2;
+  constexpr int QN = (P + 1) & 3, EN = (P + 1) >> 2;
+  const int l = threadIdx.x & 63, r = l & 15;
+  double2 cn = make_double2(0.0, 0.0), apn = make_double2(0.0, 0.0);
+  if constexpr (P < 15) {
+    cn = make_double2(bcast_quarter<QN>(a[EN].x), bcast_quarter<QN>(a[EN].y));
+    apn = make_double2(readlane_f64(a[EN].x, QN * 16 + P), readlane_f64(a[EN].y, QN * 16 + P));
+  }
+  const double2 piv = make_double2(dpp_rowbcast<P>(cp.x), dpp_rowbcast<P>(cp.y));
+  const double m2 = fma(piv.x, piv.x, piv.y * piv.y);
+  const double s = rcp_n<2>(m2);
+  const double2 inv = make_double2(piv.x * s, -piv.y * s);
+  pprod *= m2;
+  const bool prow = (r == P);
+  const double2 f = cmul(make_double2(cp.x - (prow ? 1.0 : 0.0), cp.y), inv);
+  const bool pl = l == PS * 16 + P;   // the pivot element's lane
+  a[PE].x += pl ? 1.0 : 0.0;
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) fused_upd<P>(a[jj].x, a[jj].y, -f.x, -f.y, f.y);
+  a[PE].x -= pl ? 1.0 : 0.0;
+  if constexpr (P < 15) {
+    double2 v;
+    v.x = fma(-f.x, apn.x, fma(f.y, apn.y, cn.x));
+    v.y = fma(-f.x, apn.y, fma(-f.y, apn.x, cn.y));
+    cp = v;
+  }
+}
+template <int... Ps>
+__device__ __forceinline__ void la_fused_all(double2 (&a)[4], double& pprod, std::integer_sequence<int, Ps...>) {
+  double2 cp = make_double2(bcast_quarter<0>(a[0].x), bcast_quarter<0>(a[0].y));
+  (la_step_fused<Ps>(a, cp, pprod), ...);
+}
+
 template <int NR, int... Ps>
 __device__ __forceinline__ void la_all(double2 (&a)[4], double& pprod, std::integer_sequence<int, Ps...>) {
   double2 cp = make_double2(bcast_quarter<0>(a[0].x), bcast_quarter<0>(a[0].y));
@@ -156,6 +212,10 @@ __device__ __forceinline__ double inv16(double2 (&a)[4], double2* S) {
     return wave_inv16_dpp<true>(a);
   } else if constexpr (V == 3) {
     return inv16_panel<2>(a, S);
+  } else if constexpr (V == 4) {
+    double pp = 1.0;
+    la_fused_all(a, pp, std::make_integer_sequence<int, 16>{});
+    return pp;
   } else {
     double pp = 1.0;
     la_all<V == 2 ? 1 : 2>(a, pp, std::make_integer_sequence<int, 16>{});
@@ -244,8 +304,9 @@ int main() {
   Res r1 = run<1>(in, out, pm, cyc, nblk, rep);
   Res r2 = run<2>(in, out, pm, cyc, nblk, rep);
   Res r3 = run<3>(in, out, pm, cyc, nblk, rep);
-  Res* rs[4] = {&r0, &r1, &r2, &r3};
-  for (int v = 0; v < 4; ++v) {
+  Res r4 = run<4>(in, out, pm, cyc, nblk, rep);
+  Res* rs[5] = {&r0, &r1, &r2, &r3, &r4};
+  for (int v = 0; v < 5; ++v) {
     double d = 0, mx = 0, dp = 0;
     bool same = true;
     for (size_t i = 0; i < r0.out.size(); ++i) {
