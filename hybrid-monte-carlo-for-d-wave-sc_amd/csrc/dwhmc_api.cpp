@@ -119,18 +119,24 @@ struct CrPlan {
   int n_ph = 0;                              // entries of off_ph >= 0
 };
 
-// Lattice rows per CR block: DWHMC_CR_ROWS = 1 | 2 (default 1).  With two,
-// the blocks are pairs of rows (Ly / 2 blocks of 4 Lx BdG dimensions): one
-// CR level less (one inversion and three product launches fewer per step)
-// for 8x the work per block — a trade for narrow lattices, where every stage
-// is latency-bound.  Falls back to 1 when Ly is odd or the wider block is not
-// a supported size.
+// Lattice rows per CR block.  Default: as many rows as fill the narrowest
+// block half (16 sites) — R = 16 / Lx, lowered to a divisor of Ly — so a
+// lattice with Lx <= 8 runs fewer, unpadded blocks at no extra cost per block
+// (8 x 8: 4 blocks of two rows instead of 8 half-empty ones, one CR level
+// less).  Wider lattices keep one row per block: more rows would widen the
+// blocks, and at L = 16 two rows per block (BP 64) measured slower than one
+// (profiles/r04_exp_cr_two_row_blocks_C2.txt).  DWHMC_CR_ROWS = r forces r
+// (tests, A/B), falling back to the default when Ly % r != 0 or the block
+// r Lx is not a supported size.
 int cr_rows_per_block(int64_t Lx, int64_t Ly) {
-  int r = 1;
-  if (const char* e = std::getenv("DWHMC_CR_ROWS")) r = std::atoi(e);
-  if (r != 2) return 1;
-  const int BP = (int)(2 * ((2 * Lx + 15) / 16 * 16));
-  return (Ly % 2 == 0 && dwh::cr_supported_bp(BP)) ? 2 : 1;
+  auto ok = [&](int64_t r) { return r >= 1 && Ly % r == 0 && dwh::cr_supported_bp((int)(2 * ((r * Lx + 15) / 16 * 16))); };
+  if (const char* e = std::getenv("DWHMC_CR_ROWS")) {
+    const int r = std::atoi(e);
+    if (ok(r)) return r;
+  }
+  int64_t r = std::max<int64_t>(1, 16 / Lx);
+  while (r > 1 && !ok(r)) --r;
+  return (int)r;
 }
 
 // Block cyclic reduction of the periodic block-tridiagonal H_BdG - i y (blocks

@@ -51,6 +51,15 @@ def test_cr_schedule_rejects_wide_rows(dwhmc):
     assert rc != 0 and "too wide" in err
 
 
+def default_rows(Lx, Ly):
+    """Lattice rows per CR block the context picks (cr_rows_per_block): as many
+    as fill a 16-site block half, lowered to a divisor of Ly."""
+    r = max(1, 16 // Lx)
+    while r > 1 and Ly % r:
+        r -= 1
+    return r
+
+
 def plan_flops(lib, Lx, Ly, nbatch, side, inv0):
     out = np.zeros(3)
     rc = lib.dwh_debug_cr_plan_flops(Lx, Ly, nbatch, side, inv0, out.ctypes.data_as(C.c_void_p))
@@ -68,7 +77,7 @@ def test_cr_plan_flops_independent_count(dwhmc, Lx, Ly, nbatch):
     must move their flops with them, never drop them (VERDICT r02 weak #3)."""
     from tools.cr_model import cr_flop_count
     lib = dwhmc.load_library()
-    inv_ref, prod_ref = cr_flop_count(Lx, Ly)
+    inv_ref, prod_ref = cr_flop_count(Lx, Ly, default_rows(Lx, Ly))
     for side in (0, 1):
         for inv0 in (0, 1):
             inv, prod, side_f = plan_flops(lib, Lx, Ly, nbatch, side, inv0)
@@ -98,7 +107,7 @@ def test_cr_two_row_blocks_dataflow_and_flops(dwhmc, monkeypatch, Lx, Ly):
     from tools.cr_model import cr_flop_count
     monkeypatch.setenv("DWHMC_CR_ROWS", "2")
     lib = dwhmc.load_library()
-    rows = 2 if 2 * 2 * ((2 * Lx + 15) // 16 * 16) <= 256 and Ly % 2 == 0 else 1
+    rows = 2 if 2 * 2 * ((2 * Lx + 15) // 16 * 16) <= 256 and Ly % 2 == 0 else default_rows(Lx, Ly)
     inv_ref, prod_ref = cr_flop_count(Lx, Ly, rows)
     for side in (0, 1):
         for inv0 in (0, 1):
@@ -121,3 +130,22 @@ def test_cr_two_row_blocks_c2_shape(dwhmc, monkeypatch):
     assert rc == 0, err
     assert list(s1[:4]) == [21, 5, 0, 16]
     assert list(s2[:4]) == [16, 4, 3, 12]
+
+
+@pytest.mark.parametrize("Lx,Ly,rows,blocks", [(8, 8, 2, 4), (4, 4, 4, 1), (4, 6, 3, 2), (6, 9, 1, 9), (5, 7, 1, 7),
+                                               (3, 3, 3, 1), (16, 16, 1, 16), (8, 5, 1, 5), (2, 10, 5, 2)])
+def test_cr_default_rows_per_block(dwhmc, monkeypatch, Lx, Ly, rows, blocks):
+    """Narrow lattices (Lx <= 8) group rows into 16-site blocks by default
+    (cr_rows_per_block): 8 x 8 (C1) runs 4 two-row blocks, one CR level less
+    than 8 half-empty one-row blocks; the inversion count of the plan shows the
+    block count."""
+    monkeypatch.delenv("DWHMC_CR_ROWS", raising=False)
+    assert default_rows(Lx, Ly) == rows
+    lib = dwhmc.load_library()
+    rc, st, err = check(lib, Lx, Ly, 10, 1, 1)
+    assert rc == 0, err
+    m, ninv = blocks, 0
+    while m > 1:
+        ninv += 1
+        m = (m + 1) // 2
+    assert st[1] == ninv + 1
