@@ -84,16 +84,38 @@ __host__ __device__ __forceinline__ bool eig_read_pass(int i, bool defer) { retu
 // Every load of the step is issued up front (column i, v_{i-1}, the pass
 // partials of this thread's rows and of row i): two workgroup reductions
 // (x^H v, then the reflector norm) are its only barriers.
+// k_eig_reduce: the pass partials of every row summed (ascending tile index,
+// the order the step used when it read them itself), one thread per row and
+// many workgroups, so the single-workgroup step reads n values instead of the
+// ~n T / 3 partials (1 MB at i = 0 for n = 2048): its latency was that read.
+__global__ __launch_bounds__(256) void k_eig_reduce(const double2* __restrict__ part, int64_t sP, int n, int i,
+                                                    double2* __restrict__ pfin) {
+  const int k = blockIdx.y, r = i + blockIdx.x * 256 + threadIdx.x;
+  if (r >= n) return;
+  part += k * sP;
+  const int t0 = i / kEigTB, T = (n + kEigTB - 1) / kEigTB;
+  double2 s = cz();
+  for (int Y0 = t0; Y0 < T; Y0 += 8) {
+    double2 q[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) q[u] = Y0 + u < T ? part[(int64_t)(Y0 + u) * n + r] : cz();
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (Y0 + u < T) s = cadd(s, q[u]);
+  }
+  pfin[(int64_t)k * n + r] = s;
+}
+
 template <int kMaxR, bool DEFER>   // row slots per thread: ceil(n / kStepT); DEFER: read-only passes in use
 __global__ __launch_bounds__(kStepT) void k_eig_step(double2* __restrict__ A, int n, int i, int64_t sA,
-                                                     const double2* __restrict__ part, int64_t sP,
+                                                     const double2* __restrict__ pfin,
                                                      double2* __restrict__ vv, double2* __restrict__ ww,
                                                      double* __restrict__ d, double* __restrict__ e,
                                                      double2* __restrict__ tau,
                                                      const double2* __restrict__ dpart) {
   const int k = blockIdx.x, tid = threadIdx.x;
   A += k * sA;
-  part += k * sP;
+  pfin += (int64_t)k * n;
   vv += (int64_t)k * 3 * n;
   ww += (int64_t)k * 2 * n;
   d += (int64_t)k * n;
@@ -134,34 +156,17 @@ __global__ __launch_bounds__(kStepT) void k_eig_step(double2* __restrict__ A, in
   }
   double2 pi = cz();   // p[i], every thread (v_{i-1}[i] = 1: w[i] = x[i] + alpha)
   if (i > 0) {
-    // the pass partials of every row slot and of row i, 4 Y values per round
-    // for all of them at once (ascending Y per row: fixed summation order)
-    for (int Y0 = t0; Y0 < T; Y0 += 4) {
-      double2 q[kMaxR + 1][4];
+    // the pass's hemv, reduced per row by k_eig_reduce
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const bool yok = Y0 + u < T;
-#pragma unroll
-        for (int s = 0; s < kMaxR; ++s) {
-          const int r = i + tid + s * kStepT;
-          q[s][u] = (yok && r < n) ? part[(int64_t)(Y0 + u) * n + r] : cz();
-        }
-        q[kMaxR][u] = yok ? part[(int64_t)(Y0 + u) * n + i] : cz();
-      }
-      double2 qd[4][2];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const bool ok = rp && Y0 + u < T;
-        qd[u][0] = ok ? dpart[(int64_t)(k * T + Y0 + u) * 2] : cz();
-        qd[u][1] = ok ? dpart[(int64_t)(k * T + Y0 + u) * 2 + 1] : cz();
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-#pragma unroll
-        for (int s = 0; s < kMaxR; ++s) wr[s] = cadd(wr[s], q[s][u]);
-        pi = cadd(pi, q[kMaxR][u]);
-        dw = cadd(dw, qd[u][0]);
-        dv = cadd(dv, qd[u][1]);
+    for (int s = 0; s < kMaxR; ++s) {
+      const int r = i + tid + s * kStepT;
+      if (r < n) wr[s] = pfin[r];
+    }
+    pi = pfin[i];
+    if (rp) {   // the read-only pass's dots, ascending tile index
+      for (int Y = t0; Y < T; ++Y) {
+        dw = cadd(dw, dpart[(int64_t)(k * T + Y) * 2]);
+        dv = cadd(dv, dpart[(int64_t)(k * T + Y) * 2 + 1]);
       }
     }
   }
@@ -833,13 +838,16 @@ __global__ __launch_bounds__(256) void k_eig_tw(const double2* __restrict__ Tb, 
 
 }  // namespace
 
-void launch_eig_step(double2* A, int n, int i, int64_t sA, const double2* part, int64_t sP, double2* vv,
-                     double2* ww, double* d, double* e, double2* tau, const double2* dpart, int m, hipStream_t s) {
+void launch_eig_step(double2* A, int n, int i, int64_t sA, const double2* part, int64_t sP, double2* pfin,
+                     double2* vv, double2* ww, double* d, double* e, double2* tau, const double2* dpart, int m,
+                     hipStream_t s) {
   const int defer = m >= kEigDeferMin;
+  if (i > 0)
+    hipLaunchKernelGGL(k_eig_reduce, dim3((n - i + 255) / 256, m), dim3(256), 0, s, part, sP, n, i, pfin);
   const int rs = (n - i + kStepT - 1) / kStepT;   // row slots the rows i..n-1 need
   static_assert(kEigMaxN <= 5 * kStepT, "k_eig_step instantiations");
 #define DWH_EIG_STEP(R, D) \
-  hipLaunchKernelGGL((k_eig_step<R, D>), dim3(m), dim3(kStepT), 0, s, A, n, i, sA, part, sP, vv, ww, d, e, tau, dpart)
+  hipLaunchKernelGGL((k_eig_step<R, D>), dim3(m), dim3(kStepT), 0, s, A, n, i, sA, pfin, vv, ww, d, e, tau, dpart)
   if (defer) {
     switch (rs) {
       case 1: DWH_EIG_STEP(1, true); break;

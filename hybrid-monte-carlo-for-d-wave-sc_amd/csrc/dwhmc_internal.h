@@ -244,9 +244,11 @@ constexpr double kEigClusterTol = 2.5e-4;   // eigenvalue gap / ||T|| below whic
 constexpr int kEigMaxCluster = 64;          // longest such run (else *bad: vendor fallback)
 // column i of the tridiagonalisation: partial sums -> w_{i-1}, column i -> v_i (d, e, tau)
 // vv: 3 x n per matrix (v_j in slot j % 3), ww: 2 x n (w_j in slot j % 2),
-// dpart: ceil(n / kEigTB) x 2 per matrix (the read-only passes' dots)
-void launch_eig_step(double2* A, int n, int i, int64_t sA, const double2* part, int64_t sP, double2* vv,
-                     double2* ww, double* d, double* e, double2* tau, const double2* dpart, int m, hipStream_t s);
+// dpart: ceil(n / kEigTB) x 2 per matrix (the read-only passes' dots),
+// pfin: n per matrix (the partials reduced per row, k_eig_reduce)
+void launch_eig_step(double2* A, int n, int i, int64_t sA, const double2* part, int64_t sP, double2* pfin,
+                     double2* vv, double2* ww, double* d, double* e, double2* tau, const double2* dpart, int m,
+                     hipStream_t s);
 // deferred rank-2 update of column i-1 on the trailing triangle + hemv partials of v_i
 void launch_eig_pass(double2* A, int n, int i, int64_t sA, double2* part, int64_t sP, const double2* vv,
                      const double2* ww, double2* dpart, int m, hipStream_t s);
