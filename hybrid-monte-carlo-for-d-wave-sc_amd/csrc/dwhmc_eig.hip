@@ -38,6 +38,8 @@
 //
 // The numpy prototype with the same operation order: tools/eig_proto.py.
 #include <cfloat>
+#include <cstdlib>
+#include <algorithm>
 
 #include "dwhmc_device.h"
 #include "dwhmc_internal.h"
@@ -838,10 +840,17 @@ __global__ __launch_bounds__(256) void k_eig_tw(const double2* __restrict__ Tb, 
 
 }  // namespace
 
+// batch size from which every other pass is read-only (DWHMC_EIG_DEFER_MIN
+// overrides kEigDeferMin for A/B runs); read at each solve
+int eig_defer_min() {
+  const char* e = std::getenv("DWHMC_EIG_DEFER_MIN");
+  return e ? std::max(1, std::atoi(e)) : kEigDeferMin;
+}
+
 void launch_eig_step(double2* A, int n, int i, int64_t sA, const double2* part, int64_t sP, double2* pfin,
                      double2* vv, double2* ww, double* d, double* e, double2* tau, const double2* dpart, int m,
                      hipStream_t s) {
-  const int defer = m >= kEigDeferMin;
+  const int defer = m >= eig_defer_min();
   if (i > 0)
     hipLaunchKernelGGL(k_eig_reduce, dim3((n - i + 255) / 256, m), dim3(256), 0, s, part, sP, n, i, pfin);
   const int rs = (n - i + kStepT - 1) / kStepT;   // row slots the rows i..n-1 need
@@ -873,7 +882,7 @@ void launch_eig_pass(double2* A, int n, int i, int64_t sA, double2* part, int64_
   const int T = (n + kEigTB - 1) / kEigTB, t0 = (i + 1) / kEigTB, nT = T - t0;
   if (nT <= 0) return;
   hipLaunchKernelGGL(k_eig_pass, dim3(nT * (nT + 1) / 2, m), dim3(256), 0, s, A, n, i, sA, part, sP, vv, ww, t0,
-                     dpart, T, (int)(m >= kEigDeferMin));
+                     dpart, T, (int)(m >= eig_defer_min()));
 }
 
 void launch_eig_bisect(const double* d, const double* e, int n, double* E, double* tnorm, int m, hipStream_t s) {

@@ -261,6 +261,7 @@ void launch_eig_invit(const double* d, const double* e, int n, const double* E, 
                       int maxc = kEigMaxCluster);
 void launch_eig_zt_to_u(const double* Zt, double2* U, int n, int64_t sZ, int64_t sA, int m, hipStream_t s);
 constexpr int kEigDeferMin = 4;             // batches from this many matrices defer every other rank-2 update
+int eig_defer_min();                        // kEigDeferMin or DWHMC_EIG_DEFER_MIN
 constexpr int kEigGS = 8;                   // row slices of each block's Gram sum
 // compact-WY T of every reflector block; Gp: m x nblk x kEigGS x kEigNB^2 scratch
 void launch_eig_tfac(const double2* V, int n, int64_t sA, const double2* tau, double2* Gp, double2* Tb, int64_t sT,

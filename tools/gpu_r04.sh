@@ -11,6 +11,7 @@
 #   driver  the driver's bench command only
 #   ab      tools/ab_bench.py in-process A/B (AB_VARIANTS, AB_ARGS, AB_TAG)
 #   parity  a GPU parity subset (PARITY_K)
+#   transab transport timing with DWHMC_EIG_DEFER_MIN = 4 / 1
 #   trans   transport timing (single measurement + snapshot batches)
 # Every GPU step runs under its own timeout; the first failure ends the script.
 set -o pipefail
@@ -91,6 +92,12 @@ PY
       timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 > "$O/bench_driver.json" 2> "$O/bench_driver.err" \
         || { tail -20 "$O/bench_driver.err"; exit 1; }
       tail -c 1500 "$O/bench_driver.json" ;;
+    transab)   # single-measurement latency: every pass writing (defer from 4 matrices) vs deferred from 1
+      for dm in 4 1; do
+        DWHMC_EIG_DEFER_MIN=$dm timeout -k 10 300 python -u tests/bench_transport.py --steps 4 --chains 4 --snapshots 16 \
+          > "$O/transport_defer$dm.json" 2> "$O/transport_defer$dm.err" || exit 1
+        tail -c 600 "$O/transport_defer$dm.json"; echo
+      done ;;
     trans)
       timeout -k 10 200 python -u tests/bench_transport.py --steps 3 --snapshots 4,8,16 > "$O/transport.json" \
         2> "$O/transport.err" || exit 1 ;;
