@@ -230,69 +230,11 @@ __device__ __forceinline__ void inv16_all(double2 (&a)[4], double& pprod,
   (inv16_step<Ps, STRIDED>(a, pprod), ...);
 }
 
-// The same pivot step with column lookahead: cp carries column P of the
-// current tile in every lane of its row.  Column P + 1 is broadcast
-// (ds_bpermute) at the start of step P from the pre-update tile and updated
-// by every lane with the FMAs its owner applies (with A[P][P+1] read from its
-// owner lane), so the LDS-crossbar round trip is off the pivot chain; the
-// pivot reaches every lane by a DPP row broadcast of cp (no v_readlane).
-// The arithmetic is the owner's: results equal inv16_step's bit for bit.
-#ifndef DWHMC_INV_LA
-#define DWHMC_INV_LA 1
-#endif
-template <int P, bool STRIDED>
-__device__ __forceinline__ void inv16_la_step(double2 (&a)[4], double2& cp, double& pprod) {
-  constexpr int PS = STRIDED ? (P & 3) : (P >> 2), PE = STRIDED ? (P >> 2) : (P & 3);
-  constexpr int QN = STRIDED ? ((P + 1) & 3) : ((P + 1) >> 2), EN = STRIDED ? ((P + 1) >> 2) : ((P + 1) & 3);
-  const int l = threadIdx.x & 63, r = l & 15, q = l >> 4;
-  double2 cn = make_double2(0.0, 0.0), apn = make_double2(0.0, 0.0);
-  if constexpr (P < 15) {
-    cn = make_double2(bcast_quarter<QN>(a[EN].x), bcast_quarter<QN>(a[EN].y));
-    apn = make_double2(readlane_f64(a[EN].x, QN * 16 + P), readlane_f64(a[EN].y, QN * 16 + P));
-  }
-  double2 rowp[4];
-#pragma unroll
-  for (int jj = 0; jj < 4; ++jj) rowp[jj] = make_double2(dpp_rowbcast<P>(a[jj].x), dpp_rowbcast<P>(a[jj].y));
-  const double2 piv = make_double2(dpp_rowbcast<P>(cp.x), dpp_rowbcast<P>(cp.y));
-  const double m2 = fma(piv.x, piv.x, piv.y * piv.y);
-  const double s = rcp_nr(m2);
-  const double2 inv = make_double2(piv.x * s, -piv.y * s);
-  pprod *= m2;
-  const bool prow = (r == P);
-  const double2 f = cmul(make_double2(cp.x - (prow ? 1.0 : 0.0), cp.y), inv);
-  rowp[PE].x += (q == PS) ? 1.0 : 0.0;
-#pragma unroll
-  for (int jj = 0; jj < 4; ++jj) {
-    const double2 x = rowp[jj];
-    double2 v;
-    v.x = fma(-f.x, x.x, fma(f.y, x.y, a[jj].x));
-    v.y = fma(-f.x, x.y, fma(-f.y, x.x, a[jj].y));
-    a[jj] = v;
-  }
-  if constexpr (P < 15) {
-    double2 v;
-    v.x = fma(-f.x, apn.x, fma(f.y, apn.y, cn.x));
-    v.y = fma(-f.x, apn.y, fma(-f.y, apn.x, cn.y));
-    cp = v;
-  }
-}
-
-template <bool STRIDED, int... Ps>
-__device__ __forceinline__ void inv16_la_all(double2 (&a)[4], double& pprod,
-                                             std::integer_sequence<int, Ps...>) {
-  double2 cp = make_double2(bcast_quarter<0>(a[0].x), bcast_quarter<0>(a[0].y));
-  (inv16_la_step<Ps, STRIDED>(a, cp, pprod), ...);
-}
-
 // returns Π |pivot|^2 of the 16 pivots
 template <bool STRIDED = false>
 __device__ __forceinline__ double wave_inv16_dpp(double2 (&a)[4]) {
   double pprod = 1.0;
-#if DWHMC_INV_LA
-  inv16_la_all<STRIDED>(a, pprod, std::make_integer_sequence<int, 16>{});
-#else
   inv16_all<STRIDED>(a, pprod, std::make_integer_sequence<int, 16>{});
-#endif
   return pprod;
 }
 

@@ -14,7 +14,6 @@
 //   V=4 V=1 with the DPP row broadcast fused into the update FMAs
 //       (v_fmac_f64_dpp row_newbcast, la_step_fused)
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 inv16_variants.hip -o inv16_variants
-#define DWHMC_INV_LA 0   // V=0 is the round-3 pivot step
 #include "../../hybrid-monte-carlo-for-d-wave-sc_amd/csrc/dwhmc_device.h"
 #include <cmath>
 #include <cstdio>
