@@ -652,6 +652,12 @@ struct dwh_ctx {
   // drifting k_cr_pair_force, consumed by the next factorisation); every
   // other path that changes Δ leaves it false
   bool pairing_in_pool = false;
+  // pole split (DWHMC_CR_SPLIT = S, one chain): the CR stages of poles
+  // [s P/S, (s+1) P/S) run on stream s (0: ctx->stream), forked after the fill
+  // and joined before the force, so the latency chains of the sub-batches overlap
+  int cr_split = 1;
+  std::vector<hipStream_t> cr_sub;   // streams 1 .. S-1
+  std::vector<hipEvent_t> cr_ev;     // fork + one join per sub-stream
   bool pending = false;    // dwh_hmc_trajectory done, dwh_hmc_finish not yet
   int async_rc = 0;        // eig path: a rocSOLVER / rocBLAS call refused while enqueuing
 
@@ -679,6 +685,7 @@ struct dwh_ctx {
   double2 *d_eig_part = nullptr, *d_eig_vv = nullptr, *d_eig_ww = nullptr, *d_eig_tau = nullptr;
   double2 *d_eig_T = nullptr, *d_eig_W = nullptr, *d_eig_W2 = nullptr, *d_eig_dpart = nullptr;
   double2* d_eig_pfin = nullptr;   // the hemv partials reduced per row (k_eig_reduce)
+  int* d_eig_c0 = nullptr;         // particle-hole half solve: first computed eigenvector per matrix
   double *d_eig_d = nullptr, *d_eig_e = nullptr, *d_eig_tn = nullptr;
 
   // timing
@@ -748,7 +755,7 @@ struct Scope {
   hipEvent_t a{};
   bool on;
   Scope(dwh_ctx* c, int n, double w)
-      : ctx(c), name(n), work(w), st(c->stream), on(((c->timing >> n) & 1) != 0) {
+      : ctx(c), name(n), work(w), st(c->stream), on(n < T_COUNT && ((c->timing >> n) & 1) != 0) {
     if (on) {
       a = take_event(ctx);
       (void)hipEventRecord(a, st);
@@ -867,32 +874,53 @@ void cr_enqueue(dwh_ctx* ctx) {
   }
   const CrPlan& plan = ctx->plan;
   // the site guard rides on the first (level-0) inversion launch: every
-  // factorised Δ passes through it
+  // factorised Δ passes through it (sub-batch 0 only: it checks the chain's sites)
   dwh::SiteGuard guard;
   if (ctx->site_guard) guard = dwh::SiteGuard{ctx->Delta, ctx->site4, 4.0 * ctx->delta_cap, ctx->flag};
+  const int S = ctx->cr_split;
+  dwh::CrDims cs = c;
+  cs.nbatch = c.nbatch / S;
+  const int nld = ctx->d.nld;
+  if (S > 1) {
+    (void)hipEventRecord(ctx->cr_ev[0], ctx->stream);
+    for (int q = 1; q < S; ++q) (void)hipStreamWaitEvent(ctx->cr_sub[q - 1], ctx->cr_ev[0], 0);
+  }
   for (size_t si = 0; si < plan.stages.size(); ++si) {
     const CrStage& st = plan.stages[si];
-    if (st.kind == 0 && st.ntiles > 0) {
-      Scope s(ctx, T_CR_INVSIDE, st.n * bp3 + st.flops * c.nbatch);
-      dwh::launch_cr_inv_side(c, ctx->bpool, ctx->d_inv_blk + st.first, ctx->d_inv_dst + st.first,
-                              ctx->d_inv_slot + st.first, st.n, ctx->ldpart, ctx->d_tasks + st.tfirst,
-                              st.ntiles, st.maxt32, ctx->stream, guard);
-      guard = dwh::SiteGuard{};
-    } else if (st.kind == 0 && st.l0) {
-      Scope s(ctx, T_CR_INV, st.n * bp3);
-      dwh::launch_cr_inv0(c, ctx->bpool, ctx->d_inv_blk + st.first, ctx->d_inv0_r, ctx->d_inv_dst + st.first,
-                          ctx->d_inv_slot + st.first, st.n, ctx->ldpart, ctx->ldA, ctx->stream, guard.Delta,
-                          guard.site4, guard.cap4, guard.flag);
-      guard = dwh::SiteGuard{};
-    } else if (st.kind == 0) {
-      Scope s(ctx, T_CR_INV, st.n * bp3);
-      dwh::launch_cr_inv(c, ctx->bpool, ctx->d_inv_blk + st.first, ctx->d_inv_dst + st.first,
-                         ctx->d_inv_slot + st.first, st.n, ctx->ldpart, ctx->stream, guard);
-      guard = dwh::SiteGuard{};
-    } else {
-      Scope s(ctx, T_CR_GEMM, st.flops * c.nbatch);
-      dwh::launch_cr_gemm(c, ctx->bpool, ctx->d_tasks + st.first, st.n, st.maxt32, st.maxt16,
-                          ctx->d_tiles16 + st.tfirst, st.ntiles, st.cfg, st.sg, ctx->stream);
+    for (int q = 0; q < S; ++q) {
+      const hipStream_t strm = q == 0 ? ctx->stream : ctx->cr_sub[q - 1];
+      const int64_t b0 = (int64_t)q * cs.nbatch;
+      double2* pool = ctx->bpool + b0 * c.item;
+      double* ldp = ctx->ldpart + b0 * nld;
+      const double* lda = ctx->ldA ? ctx->ldA + b0 * c.Ly : nullptr;
+      const dwh::SiteGuard g = q == 0 ? guard : dwh::SiteGuard{};
+      // timers (ctx->stream) bracket sub-batch 0
+      const double wsc = 1.0 / S;
+      if (st.kind == 0 && st.ntiles > 0) {
+        Scope s(ctx, q == 0 ? T_CR_INVSIDE : T_COUNT, wsc * (st.n * bp3 + st.flops * c.nbatch));
+        dwh::launch_cr_inv_side(cs, pool, ctx->d_inv_blk + st.first, ctx->d_inv_dst + st.first,
+                                ctx->d_inv_slot + st.first, st.n, ldp, ctx->d_tasks + st.tfirst, st.ntiles,
+                                st.maxt32, strm, g);
+      } else if (st.kind == 0 && st.l0) {
+        Scope s(ctx, q == 0 ? T_CR_INV : T_COUNT, wsc * st.n * bp3);
+        dwh::launch_cr_inv0(cs, pool, ctx->d_inv_blk + st.first, ctx->d_inv0_r, ctx->d_inv_dst + st.first,
+                            ctx->d_inv_slot + st.first, st.n, ldp, lda, strm, g.Delta, g.site4, g.cap4, g.flag);
+      } else if (st.kind == 0) {
+        Scope s(ctx, q == 0 ? T_CR_INV : T_COUNT, wsc * st.n * bp3);
+        dwh::launch_cr_inv(cs, pool, ctx->d_inv_blk + st.first, ctx->d_inv_dst + st.first,
+                           ctx->d_inv_slot + st.first, st.n, ldp, strm, g);
+      } else {
+        Scope s(ctx, q == 0 ? T_CR_GEMM : T_COUNT, wsc * st.flops * c.nbatch);
+        dwh::launch_cr_gemm(cs, pool, ctx->d_tasks + st.first, st.n, st.maxt32, st.maxt16,
+                            ctx->d_tiles16 + st.tfirst, st.ntiles, st.cfg, st.sg, strm);
+      }
+    }
+    if (st.kind == 0) guard = dwh::SiteGuard{};
+  }
+  if (S > 1) {
+    for (int q = 1; q < S; ++q) {
+      (void)hipEventRecord(ctx->cr_ev[q], ctx->cr_sub[q - 1]);
+      (void)hipStreamWaitEvent(ctx->stream, ctx->cr_ev[q], 0);
     }
   }
 }
@@ -1511,6 +1539,29 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     ctx->err = "hipStreamCreate failed";
     return bail(DWH_ERR_HIP);
   }
+  if (ctx->algo == ALGO_CR) {
+    const char* e = std::getenv("DWHMC_CR_SPLIT");
+    const int S = e ? std::atoi(e) : 1;
+    if (S > 1 && S <= 4 && d.nc == 1 && d.P % S == 0) {
+      ctx->cr_split = S;
+      for (int q = 1; q < S; ++q) {
+        hipStream_t st{};
+        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
+          ctx->err = "hipStreamCreate failed";
+          return bail(DWH_ERR_HIP);
+        }
+        ctx->cr_sub.push_back(st);
+      }
+      for (int q = 0; q < S; ++q) {
+        hipEvent_t ev{};
+        if (hipEventCreateWithFlags(&ev, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess) {
+          ctx->err = "hipEventCreate failed";
+          return bail(DWH_ERR_HIP);
+        }
+        ctx->cr_ev.push_back(ev);
+      }
+    }
+  }
   const size_t nmat = (size_t)d.nbatch * d.mat;
   const size_t nbond = (size_t)d.nc * 2 * N;
   int rc = DWH_OK;
@@ -1825,7 +1876,7 @@ int own_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m) {
   if (m > ctx->eig_slots) {
     HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
     for (void* q : {(void*)ctx->d_eig_part, (void*)ctx->d_eig_vv, (void*)ctx->d_eig_ww, (void*)ctx->d_eig_tau,
-                    (void*)ctx->d_eig_dpart, (void*)ctx->d_eig_pfin,
+                    (void*)ctx->d_eig_dpart, (void*)ctx->d_eig_pfin, (void*)ctx->d_eig_c0,
                     (void*)ctx->d_eig_T, (void*)ctx->d_eig_W, (void*)ctx->d_eig_W2, (void*)ctx->d_eig_d,
                     (void*)ctx->d_eig_e, (void*)ctx->d_eig_tn})
       drop_alloc(ctx, q);
@@ -1835,7 +1886,8 @@ int own_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m) {
         (rc = dalloc(ctx, &ctx->d_eig_dpart, mm * 2 * T)) || (rc = dalloc(ctx, &ctx->d_eig_pfin, mm * n)) ||
         (rc = dalloc(ctx, &ctx->d_eig_T, mm * sT)) || (rc = dalloc(ctx, &ctx->d_eig_W, mm * std::max<int64_t>(KS * sW, (int64_t)nblk * dwh::kEigGS * NB * NB))) ||
         (rc = dalloc(ctx, &ctx->d_eig_W2, mm * sW)) || (rc = dalloc(ctx, &ctx->d_eig_d, mm * n)) ||
-        (rc = dalloc(ctx, &ctx->d_eig_e, mm * n)) || (rc = dalloc(ctx, &ctx->d_eig_tn, mm)))
+        (rc = dalloc(ctx, &ctx->d_eig_e, mm * n)) || (rc = dalloc(ctx, &ctx->d_eig_tn, mm)) ||
+        (rc = dalloc(ctx, &ctx->d_eig_c0, mm)))
       return rc;
     ctx->eig_slots = m;
   }
@@ -1855,42 +1907,57 @@ int own_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m) {
   // rocSOLVER fallback of eigen_solve
   int maxc = dwh::kEigMaxCluster;
   if (const char* e = std::getenv("DWHMC_EIG_MAX_CLUSTER")) maxc = std::max(1, std::min(maxc, std::atoi(e)));
+  // Particle-hole half solve (H_BdG: E <-> -E with eigenvectors (u; v) <->
+  // (-v*; u*)): eigenvectors of T only for the indices from
+  // c0 — n/2, or the start of an eigenvalue cluster that straddles zero (exact
+  // zero modes of clean lattices), which is then solved whole — on the columns
+  // [j0, n), j0 = n/2 - kEigMaxCluster; the columns below c0 are the partners
+  // of the columns above n - c0 (k_eig_theta after the back-transform).
+  // Inverse iteration, the orthogonalisation and the back-transform run on
+  // ~half the columns.  DWHMC_EIG_HALF=0: every column (A/B).
+  const char* eh = std::getenv("DWHMC_EIG_HALF");
+  const bool half = n % 2 == 0 && !(eh && *eh == '0');
+  const int j0 = half ? std::max(0, N - dwh::kEigMaxCluster) : 0;
+  const int M = n - j0;   // eigenvector columns computed
+  if (half) dwh::launch_eig_c0(b.E, ctx->d_eig_tn, n, maxc, ctx->d_eig_c0, ctx->d_tr_bad, m, s);
   dwh::launch_eig_invit(ctx->d_eig_d, ctx->d_eig_e, n, b.E, ctx->d_eig_tn, Zt, Zt + sA, Ud, Ud + sA, sZ,
-                        ctx->d_tr_bad, m, s, maxc);
-  // One symmetric (Löwdin) orthogonalisation step over all vectors: with
-  // Y = Z^T (column-major Zt) and G = Y Y^T = I + F, Y <- (3/2 I - 1/2 G) Y
-  // leaves ||F|| -> O(||F||^2).  Outside clusters F_jl ~ c eps ||T|| / |λ_j - λ_l|
-  // (inverse iteration's per-vector error), so the mixing moves each residual
-  // by ~ F_jl |λ_j - λ_l| ~ c eps ||T||: orthogonality to rounding, accuracy kept.
+                        ctx->d_tr_bad, m, s, maxc, j0, half ? ctx->d_eig_c0 : nullptr);
+  // One symmetric (Löwdin) orthogonalisation step over the computed vectors:
+  // with Y = Z^T (column-major Zt, its rows j0.. the vectors) and G = Y Y^T =
+  // I + F, Y <- (3/2 I - 1/2 G) Y leaves ||F|| -> O(||F||^2).  Outside clusters
+  // F_jl ~ c eps ||T|| / |λ_j - λ_l| (inverse iteration's per-vector error), so
+  // the mixing moves each residual by ~ F_jl |λ_j - λ_l| ~ c eps ||T||:
+  // orthogonality to rounding, accuracy kept.  (Zeroed partner rows stay zero.)
   double* G = Ud;          // the slots' U buffers (LU scratch until now)
   double* Y2 = Zt + sA;    // second half of the slots' Jmn buffers
-  dwh::gemm_d('N', 'T', n, n, n, 1.0, Zt, n, sZ, Zt, n, sZ, 0.0, G, n, sZ, m, s);
+  dwh::gemm_d('N', 'T', M, M, n, 1.0, Zt + j0, n, sZ, Zt + j0, n, sZ, 0.0, G, M, sZ, m, s);
   HIPCHECK(ctx, hipMemcpy2DAsync(Y2, sZ * sizeof(double), Zt, sZ * sizeof(double), sA * sizeof(double), m,
                                  hipMemcpyDeviceToDevice, s));
-  dwh::gemm_d('N', 'N', n, n, n, -0.5, G, n, sZ, Zt, n, sZ, 1.5, Y2, n, sZ, m, s);
-  dwh::launch_eig_zt_to_u(Y2, b.U, n, sZ, sA, m, s);
+  dwh::gemm_d('N', 'N', M, n, M, -0.5, G, M, sZ, Zt + j0, n, sZ, 1.5, Y2 + j0, n, sZ, m, s);
+  dwh::launch_eig_zt_to_u(Y2, b.U, n, sZ, sA, m, s, j0);
   HIPCHECK(ctx, hipGetLastError());
   if (n < 2) return DWH_OK;
   dwh::launch_eig_tfac(A, n, sA, ctx->d_eig_tau, ctx->d_eig_W, ctx->d_eig_T, sT, m, s);   // W as Gram scratch
   HIPCHECK(ctx, hipGetLastError());
   // U = (I - V_0 T_0 V_0^H) ... (I - V_last T_last V_last^H) Z, last block first,
-  // on the library's own products (dwhmc_gemm.hip)
+  // on the library's own products (dwhmc_gemm.hip), columns j0.. only
   const double2 one = make_double2(1.0, 0.0), zero = make_double2(0.0, 0.0), mone = make_double2(-1.0, 0.0);
   for (int blk = nblk - 1; blk >= 0; --blk) {
-    const int j0 = blk * NB, kb = std::min(NB, n - 1 - j0), ms = n - j0 - 1;
-    const double2* Vb = A + (j0 + 1) + (int64_t)j0 * n;
-    double2* Us = b.U + (j0 + 1);
+    const int r0 = blk * NB, kb = std::min(NB, n - 1 - r0), ms = n - r0 - 1;
+    const double2* Vb = A + (r0 + 1) + (int64_t)r0 * n;
+    double2* Us = b.U + (r0 + 1) + (int64_t)j0 * n;
     const int ldw = ks * NB;
     // W = V^H U in K chunks of c rows (a multiple of 16, the last one shorter),
     // chunk s at rows s kb of W: one launch for every (matrix, chunk)
     const int c = ks == 1 ? ms : std::max(16, ((ms + ks - 1) / ks + 15) / 16 * 16);
     const int nfull = ms / c, rem = ms - nfull * c, S = nfull + (rem > 0);
-    dwh::gemm_z_chunked('C', 'N', kb, n, c, rem > 0 ? rem : c, S, one, Vb, n, c, sA, Us, n, c, sA, zero,
+    dwh::gemm_z_chunked('C', 'N', kb, M, c, rem > 0 ? rem : c, S, one, Vb, n, c, sA, Us, n, c, sA, zero,
                         ctx->d_eig_W, ldw, kb, sWs, m, s);
-    dwh::launch_eig_tw(ctx->d_eig_T + (int64_t)blk * NB * NB, sT, ctx->d_eig_W, ldw, sWs, S, kb, n,
+    dwh::launch_eig_tw(ctx->d_eig_T + (int64_t)blk * NB * NB, sT, ctx->d_eig_W, ldw, sWs, S, kb, M,
                        ctx->d_eig_W2, sW, m, s);
-    dwh::gemm_z('N', 'N', ms, n, kb, mone, Vb, n, sA, ctx->d_eig_W2, NB, sW, one, Us, n, sA, m, s);
+    dwh::gemm_z('N', 'N', ms, M, kb, mone, Vb, n, sA, ctx->d_eig_W2, NB, sW, one, Us, n, sA, m, s);
   }
+  if (half) dwh::launch_eig_theta(b.U, n, sA, ctx->d_eig_c0, m, s);
   HIPCHECK(ctx, hipGetLastError());
   return DWH_OK;
 }
@@ -2165,6 +2232,8 @@ void dwh_destroy(dwh_ctx* ctx) {
   for (auto e : ctx->pool) (void)hipEventDestroy(e);
   if (ctx->blas) (void)rocblas_destroy_handle(ctx->blas);
   for (void* p : ctx->allocations) (void)hipFree(p);
+  for (auto e : ctx->cr_ev) (void)hipEventDestroy(e);
+  for (auto q : ctx->cr_sub) (void)hipStreamDestroy(q);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }

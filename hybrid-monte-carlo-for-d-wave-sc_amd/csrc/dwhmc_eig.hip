@@ -575,7 +575,8 @@ __global__ __launch_bounds__(64) void k_eig_invit(const double* __restrict__ d, 
                                                   int n, const double* __restrict__ E,
                                                   const double* __restrict__ tnorm, double* __restrict__ Zt,
                                                   double* __restrict__ U0, double* __restrict__ U1,
-                                                  double* __restrict__ U2, int64_t sZ) {
+                                                  double* __restrict__ U2, int64_t sZ, int j0,
+                                                  const int* __restrict__ c0) {
   extern __shared__ double lds[];   // d[0, n), e[n, 2n)
   const int k = blockIdx.y;
   for (int r = threadIdx.x; r < n; r += blockDim.x) {
@@ -583,8 +584,13 @@ __global__ __launch_bounds__(64) void k_eig_invit(const double* __restrict__ d, 
     lds[n + r] = r < n - 1 ? e[(int64_t)k * n + r] : 0.0;
   }
   __syncthreads();
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  const int j = j0 + blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
+  if (c0 && j < c0[k]) {   // a particle-hole partner column: zero (the Löwdin step reads it)
+    double* z = Zt + k * sZ + j;
+    for (int r = 0; r < n; ++r) z[(int64_t)r * n] = 0.0;
+    return;
+  }
   const double tn = tnorm[k];
   const double small = tn > 0.0 ? DBL_EPSILON * tn : DBL_EPSILON;
   invit_one(lds, lds + n, n, E[(int64_t)k * n + j], j, small, Zt + k * sZ, U0 + k * sZ, U1 + k * sZ,
@@ -602,9 +608,11 @@ __global__ __launch_bounds__(64) void k_eig_invit(const double* __restrict__ d, 
 // positive definite (the caller then re-solves with rocSOLVER's zheev).
 __global__ __launch_bounds__(256) void k_eig_orth(const double* __restrict__ E, const double* __restrict__ tnorm,
                                                   int n, double* __restrict__ Zt, int64_t sZ, double ctol,
-                                                  int* __restrict__ bad, int maxc) {
+                                                  int* __restrict__ bad, int maxc, int j0,
+                                                  const int* __restrict__ c0) {
   constexpr int MC = kEigMaxCluster;
-  const int k = blockIdx.y, j = blockIdx.x, tid = threadIdx.x;
+  const int k = blockIdx.y, j = j0 + blockIdx.x, tid = threadIdx.x;
+  if (c0 && j < c0[k]) return;
   E += (int64_t)k * n;
   Zt += k * sZ;
   const double tol = ctol * tnorm[k];
@@ -711,12 +719,12 @@ __global__ __launch_bounds__(256) void k_eig_orth(const double* __restrict__ E, 
 
 // U[r + c n] = (Zt[r n + c], 0), through a 64 x 64 LDS tile
 __global__ __launch_bounds__(256) void k_eig_zt_to_u(const double* __restrict__ Zt, double2* __restrict__ U, int n,
-                                                     int64_t sZ, int64_t sA) {
+                                                     int64_t sZ, int64_t sA, int j0) {
   const int k = blockIdx.z;
   Zt += k * sZ;
   U += k * sA;
   __shared__ double t[64][65];
-  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int r0 = blockIdx.y * 64, c0 = j0 + blockIdx.x * 64;
   for (int q = threadIdx.x; q < 64 * 64; q += 256) {
     const int rr = q >> 6, cc = q & 63;   // read row r0+rr of Zt: columns c0+cc contiguous
     const int r = r0 + rr, c = c0 + cc;
@@ -728,6 +736,38 @@ __global__ __launch_bounds__(256) void k_eig_zt_to_u(const double* __restrict__ 
     const int r = r0 + rr, c = c0 + cc;
     if (r < n && c < n) U[r + (int64_t)c * n] = make_double2(t[rr][cc], 0.0);
   }
+}
+
+// c0 of the particle-hole half solve (launch_eig_c0), one thread per matrix
+__global__ void k_eig_c0(const double* __restrict__ E, const double* __restrict__ tnorm, int n, double ctol, int maxc,
+                         int* __restrict__ c0, int* __restrict__ bad, int m) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= m) return;
+  E += (int64_t)k * n;
+  const double tol = ctol * tnorm[k];
+  const int h = n / 2;
+  int c = h;
+  while (c > 0 && E[c] - E[c - 1] <= tol) {
+    --c;
+    if (h - c >= maxc) {   // beyond the computed range [n/2 - maxc, n): vendor fallback
+      *bad = 1;
+      break;
+    }
+  }
+  c0[k] = c;
+}
+
+// U[:, j] = Θ U[:, n-1-j] for j < c0[k]: Θ (u; v) = (-conj v; conj u), one
+// thread per row
+__global__ __launch_bounds__(256) void k_eig_theta(double2* __restrict__ U, int n, int64_t sA,
+                                                   const int* __restrict__ c0) {
+  const int k = blockIdx.z, j = blockIdx.y, r = blockIdx.x * 256 + threadIdx.x;
+  if (j >= c0[k] || r >= n) return;
+  U += k * sA;
+  const int N = n / 2;
+  const double2* src = U + (int64_t)(n - 1 - j) * n;
+  const double2 v = r < N ? src[r + N] : src[r - N];
+  U[r + (int64_t)j * n] = r < N ? make_double2(-v.x, v.y) : make_double2(v.x, -v.y);
 }
 
 // compact-WY T of reflector block b (columns j0 .. j0+kb-1 of V, rows j0+1 ..):
@@ -891,16 +931,30 @@ void launch_eig_bisect(const double* d, const double* e, int n, double* E, doubl
 }
 
 void launch_eig_invit(const double* d, const double* e, int n, const double* E, const double* tnorm, double* Zt,
-                      double* U0, double* U1, double* U2, int64_t sZ, int* bad, int m, hipStream_t s, int maxc) {
-  hipLaunchKernelGGL(k_eig_invit, dim3((n + 63) / 64, m), dim3(64), 2 * n * sizeof(double), s, d, e, n, E, tnorm, Zt,
-                     U0, U1, U2, sZ);
-  hipLaunchKernelGGL(k_eig_orth, dim3(n, m), dim3(256), 0, s, E, tnorm, n, Zt, sZ, kEigClusterTol, bad,
-                     maxc < 1 || maxc > kEigMaxCluster ? kEigMaxCluster : maxc);
+                      double* U0, double* U1, double* U2, int64_t sZ, int* bad, int m, hipStream_t s, int maxc, int j0,
+                      const int* c0) {
+  const int nj = n - j0;
+  if (nj <= 0) return;
+  hipLaunchKernelGGL(k_eig_invit, dim3((nj + 63) / 64, m), dim3(64), 2 * n * sizeof(double), s, d, e, n, E, tnorm,
+                     Zt, U0, U1, U2, sZ, j0, c0);
+  hipLaunchKernelGGL(k_eig_orth, dim3(nj, m), dim3(256), 0, s, E, tnorm, n, Zt, sZ, kEigClusterTol, bad,
+                     maxc < 1 || maxc > kEigMaxCluster ? kEigMaxCluster : maxc, j0, c0);
 }
 
-void launch_eig_zt_to_u(const double* Zt, double2* U, int n, int64_t sZ, int64_t sA, int m, hipStream_t s) {
-  const int T = (n + 63) / 64;
-  hipLaunchKernelGGL(k_eig_zt_to_u, dim3(T, T, m), dim3(256), 0, s, Zt, U, n, sZ, sA);
+void launch_eig_c0(const double* E, const double* tnorm, int n, int maxc, int* c0, int* bad, int m, hipStream_t s) {
+  hipLaunchKernelGGL(k_eig_c0, dim3((m + 63) / 64), dim3(64), 0, s, E, tnorm, n, kEigClusterTol,
+                     maxc < 1 || maxc > kEigMaxCluster ? kEigMaxCluster : maxc, c0, bad, m);
+}
+
+void launch_eig_theta(double2* U, int n, int64_t sA, const int* c0, int m, hipStream_t s) {
+  if (n < 2) return;
+  hipLaunchKernelGGL(k_eig_theta, dim3((n + 255) / 256, n / 2, m), dim3(256), 0, s, U, n, sA, c0);
+}
+
+void launch_eig_zt_to_u(const double* Zt, double2* U, int n, int64_t sZ, int64_t sA, int m, hipStream_t s, int j0) {
+  const int T = (n + 63) / 64, TC = (n - j0 + 63) / 64;
+  if (TC <= 0) return;
+  hipLaunchKernelGGL(k_eig_zt_to_u, dim3(TC, T, m), dim3(256), 0, s, Zt, U, n, sZ, sA, j0);
 }
 
 void launch_eig_tfac(const double2* V, int n, int64_t sA, const double2* tau, double2* Gp, double2* Tb, int64_t sT,

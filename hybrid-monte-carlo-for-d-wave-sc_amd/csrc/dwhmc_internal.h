@@ -256,10 +256,21 @@ void launch_eig_pass(double2* A, int n, int i, int64_t sA, double2* part, int64_
 void launch_eig_bisect(const double* d, const double* e, int n, double* E, double* tnorm, int m, hipStream_t s);
 // eigenvectors of T into Zt (Zt[r n + j]: component r of vector j), clusters orthonormalised;
 // a cluster longer than maxc (<= kEigMaxCluster) sets *bad (the caller's vendor fallback)
+// Only the indices [j0, n), and with c0 (per matrix, device) only those >= c0
+// (the columns j0 <= j < c0 of Zt are zeroed): the particle-hole half solve
 void launch_eig_invit(const double* d, const double* e, int n, const double* E, const double* tnorm, double* Zt,
                       double* U0, double* U1, double* U2, int64_t sZ, int* bad, int m, hipStream_t s,
-                      int maxc = kEigMaxCluster);
-void launch_eig_zt_to_u(const double* Zt, double2* U, int n, int64_t sZ, int64_t sA, int m, hipStream_t s);
+                      int maxc = kEigMaxCluster, int j0 = 0, const int* c0 = nullptr);
+// particle-hole half solve (BdG matrices, n even): c0[k] = the first index of
+// the eigenvalue cluster that contains n/2 when it straddles zero, else n/2;
+// *bad when that cluster reaches more than maxc below n/2
+void launch_eig_c0(const double* E, const double* tnorm, int n, int maxc, int* c0, int* bad, int m, hipStream_t s);
+// columns j < c0[k] of U = the particle-hole partners of columns n-1-j:
+// (u; v) -> (-conj v; conj u)
+void launch_eig_theta(double2* U, int n, int64_t sA, const int* c0, int m, hipStream_t s);
+// U[:, j0:] from Zt[:, j0:] (real -> complex, transposed through LDS)
+void launch_eig_zt_to_u(const double* Zt, double2* U, int n, int64_t sZ, int64_t sA, int m, hipStream_t s,
+                        int j0 = 0);
 constexpr int kEigDeferMin = 4;             // batches from this many matrices defer every other rank-2 update
 int eig_defer_min();                        // kEigDeferMin or DWHMC_EIG_DEFER_MIN
 constexpr int kEigGS = 8;                   // row slices of each block's Gram sum

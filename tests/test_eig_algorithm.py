@@ -72,3 +72,42 @@ def test_tridiagonal_is_similar():
         Q = Q @ (np.eye(n) - tau[i] * np.outer(V[:, i], V[:, i].conj()))
     T = np.diag(d) + np.diag(e, 1) + np.diag(e, -1)
     assert np.max(np.abs(Q.conj().T @ A @ Q - T)) <= 1e-12 * np.max(np.abs(A))
+
+
+def _bdg(O, Lx, Ly, clean=False, mu=-1.08, seed=3):
+    if clean:
+        p = O.ModelParameters(Lx, Ly, 1.0, -0.35, mu, 0.0, 0.0, 8.0, 0.8, 1.0)
+        dis = np.zeros(p.N)
+        D = np.stack([np.full(p.N, 0.2), np.full(p.N, -0.2)], 1).astype(np.complex128)
+    else:
+        p = O.ModelParameters(Lx, Ly, 1.0, -0.35, mu, 1.0, 0.1, 8.0, 0.8, 1.0)
+        rng = np.random.default_rng(seed)
+        st = O.initialize_state(p, rng)
+        dis = st.disorder_pot
+        D = st.Delta + 0.25 * np.exp(0.3j * rng.standard_normal((p.N, 2)))
+    cache = O.initialize_cache(p)
+    O.init_static_H(cache, p, dis)
+    O.update_H_BdG(cache, p, D)
+    return O.hermitian_from_upper(cache.H_base)
+
+
+@pytest.mark.parametrize("Lx,Ly,clean,mu", [(4, 3, False, -1.08), (2, 4, False, -1.08), (5, 7, False, -1.08),
+                                             (6, 6, True, -1.08), (8, 8, True, 0.0), (4, 4, True, 0.0)])
+def test_bdg_half_spectrum_vectors(oracle, Lx, Ly, clean, mu):
+    """eigh_bdg: eigenvectors of the upper half only (from the start of a
+    cluster straddling zero), the lower half as particle-hole partners
+    Θ(u; v) = (−v*; u*) — the same eigenpair tolerances as
+    the full solve.  Clean lattices at μ = 0 with L % 4 == 0 have exact zero
+    modes (the nodes of g_k on the grid): a cluster across zero, computed
+    whole."""
+    H = _bdg(oracle, Lx, Ly, clean, mu)
+    lam, U = P.eigh_bdg(H)
+    _check(H, lam, U)
+    n = H.shape[0]
+    d, e, V, tau = P.tridiagonalize(H)
+    lam2, tn = P.bisect_all(d, e)
+    c0 = P.zero_cluster_start(lam2, tn)
+    if clean and mu == 0.0 and Lx % 4 == 0 and Ly % 4 == 0:
+        assert c0 < n // 2          # the zero modes straddle
+    else:
+        assert c0 == n // 2

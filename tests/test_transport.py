@@ -138,9 +138,12 @@ def test_eigensystem_matches_oracle(dwhmc, oracle, Lx, Ly):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("Lx,Ly,beta,clean", [(8, 8, 16.0, False), (16, 16, 8.0, False), (32, 32, 16.0, False),
-                                              (16, 16, 8.0, True), (12, 10, 4.0, True)])
-def test_own_eigensolver_full_size(dwhmc, oracle, Lx, Ly, beta, clean):
+@pytest.mark.parametrize("Lx,Ly,beta,clean,half", [(8, 8, 16.0, False, "1"), (16, 16, 8.0, False, "1"),
+                                                   (32, 32, 16.0, False, "1"), (32, 32, 16.0, False, "0"),
+                                                   (16, 16, 8.0, True, "1"), (12, 10, 4.0, True, "1"),
+                                                   (16, 16, 8.0, "zero", "1"), (8, 12, 8.0, "zero", "1"),
+                                                   (16, 16, 8.0, "zero", "0")])
+def test_own_eigensolver_full_size(dwhmc, oracle, monkeypatch, Lx, Ly, beta, clean, half):
     """The hand-written eigensolver (csrc/dwhmc_eig.hip: Householder
     tridiagonalisation, bisection, inverse iteration + cluster Cholesky QR,
     blocked back-transform) at BASELINE sizes (n = 2N up to 2048) against
@@ -148,10 +151,15 @@ def test_own_eigensolver_full_size(dwhmc, oracle, Lx, Ly, beta, clean):
     src/Hamiltonian.jl:96-114): eigenvalues within 1e-12 (1 + max|E|),
     ‖H U − U E‖ within 1e-11 (1 + max|E|), ‖UᴴU − I‖ ≤ 1e-12.  Clean lattices
     (W = 0, uniform d-wave Δ) have exactly degenerate levels: their vectors
-    come out of the cluster orthonormalisation."""
+    come out of the cluster orthonormalisation; at μ = 0 ("zero") with L % 4
+    == 0 the d-wave nodes sit on the grid and give exact zero modes, a cluster
+    across E = 0 that the particle-hole half solve (default; half = "0": every
+    column, DWHMC_EIG_HALF=0) computes whole."""
     O = oracle
+    monkeypatch.setenv("DWHMC_EIG_HALF", half)
     if clean:
-        p = O.ModelParameters(Lx, Ly, T, TP, -1.0, 0.0, 0.0, beta, 0.8, 1.0)
+        mu = 0.0 if clean == "zero" else -1.0
+        p = O.ModelParameters(Lx, Ly, T, TP, mu, 0.0, 0.0, beta, 0.8, 1.0)
         dis = np.zeros(p.N)
         D = np.stack([np.full(p.N, 0.2), np.full(p.N, -0.2)], 1).astype(np.complex128)
     else:

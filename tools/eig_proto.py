@@ -230,6 +230,81 @@ def back_transform(V, tau, Z, nb=8):
     return U
 
 
+def zero_cluster_start(lam, tnorm, cluster_tol=2.5e-4, maxc=64):
+    """First index c0 <= n/2 of the eigenvalue cluster that contains index
+    n/2 (the smallest of the upper half) when that cluster straddles zero, else
+    n/2; None when it is longer than maxc back (the caller falls back)."""
+    n = len(lam)
+    h = n // 2
+    c0 = h
+    while c0 > 0 and lam[c0] - lam[c0 - 1] <= cluster_tol * tnorm:
+        c0 -= 1
+        if h - c0 > maxc:
+            return None
+    return c0
+
+
+def theta_partner(U, j_src):
+    """Theta (u; v) = (-conj v; conj u): the particle-hole partner of an
+    eigenvector of a BdG matrix [[h, D], [D^*, -h]] (h real symmetric, D
+    symmetric), eigenvalue -E."""
+    N = U.shape[0] // 2
+    u, v = U[:N, j_src], U[N:, j_src]
+    return np.concatenate([-np.conj(v), np.conj(u)])
+
+
+def inverse_iteration_range(d, e, lam, tnorm, j0, cluster_tol=2.5e-4, iters=3):
+    """inverse_iteration for the eigenvalue indices [j0, n) only (vectors of T
+    in Z[:, j0:]); clusters inside the range, then one symmetric
+    orthogonalisation step over those columns."""
+    n = len(d)
+    eps = np.finfo(float).eps
+    small = eps * tnorm if tnorm > 0 else eps
+    Z = np.zeros((n, n - j0))
+    for m in range(j0, n):
+        fac = lu_tridiag(d, e, lam[m], small)
+        x = start_vector(m, n)
+        for _ in range(iters):
+            x = lu_solve(*fac, x)
+            x /= np.linalg.norm(x)
+        Z[:, m - j0] = x
+    j = j0
+    while j < n:
+        k = j + 1
+        while k < n and lam[k] - lam[k - 1] <= cluster_tol * tnorm:
+            k += 1
+        if k - j > 1:
+            for _ in range(2):
+                C = Z[:, j - j0:k - j0]
+                L = np.linalg.cholesky(C.T @ C)
+                Z[:, j - j0:k - j0] = np.linalg.solve(L, C.T).T
+        j = k
+    G = Z.T @ Z
+    return Z @ (1.5 * np.eye(n - j0) - 0.5 * G)
+
+
+def eigh_bdg(A: np.ndarray):
+    """eigh for a BdG matrix: every eigenvalue, but eigenvectors only for the
+    upper half of the spectrum (from c0, the start of a cluster straddling
+    zero, if any); the lower half's vectors are the particle-hole partners of
+    the upper half's (index j <-> n-1-j), so inverse iteration, the
+    orthogonalisation and the back-transform run on ~half the columns."""
+    n = A.shape[0]
+    d, e, V, tau = tridiagonalize(A)
+    lam, tnorm = bisect_all(d, e)
+    c0 = zero_cluster_start(lam, tnorm)
+    if c0 is None or n % 2:
+        Z = inverse_iteration(d, e, lam, tnorm)
+        return lam, back_transform(V, tau, Z)
+    Zr = inverse_iteration_range(d, e, lam, tnorm, c0)
+    Uh = back_transform(V, tau, Zr)
+    U = np.zeros((n, n), complex)
+    U[:, c0:] = Uh
+    for j in range(c0):
+        U[:, j] = theta_partner(U, n - 1 - j)
+    return lam, U
+
+
 def eigh(A: np.ndarray):
     d, e, V, tau = tridiagonalize(A)
     lam, tnorm = bisect_all(d, e)
