@@ -686,6 +686,11 @@ struct dwh_ctx {
   double2 *d_eig_T = nullptr, *d_eig_W = nullptr, *d_eig_W2 = nullptr, *d_eig_dpart = nullptr;
   double2* d_eig_pfin = nullptr;   // the hemv partials reduced per row (k_eig_reduce)
   int* d_eig_c0 = nullptr;         // particle-hole half solve: first computed eigenvector per matrix
+  bool eig_half = false;           // the last own solve ran the particle-hole half solve
+  // the last eigen_solve's U of every slot is closed under the particle-hole
+  // map column by column (half solve, c0 = N everywhere, no fallback):
+  // transport's pair sums then run over half the pairs
+  bool eig_ph = false;
   double *d_eig_d = nullptr, *d_eig_e = nullptr, *d_eig_tn = nullptr;
 
   // timing
@@ -1917,6 +1922,7 @@ int own_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m) {
   // ~half the columns.  DWHMC_EIG_HALF=0: every column (A/B).
   const char* eh = std::getenv("DWHMC_EIG_HALF");
   const bool half = n % 2 == 0 && !(eh && *eh == '0');
+  ctx->eig_half = half;
   const int j0 = half ? std::max(0, N - dwh::kEigMaxCluster) : 0;
   const int M = n - j0;   // eigenvector columns computed
   if (half) dwh::launch_eig_c0(b.E, ctx->d_eig_tn, n, maxc, ctx->d_eig_c0, ctx->d_tr_bad, m, s);
@@ -2005,12 +2011,19 @@ int eigen_solve(dwh_ctx* ctx, const TrSrc& src, int m) {
     Scope sc(ctx, T_EIG_VENDOR, m);
     rc = eigen_enqueue(ctx, src, m, qr);
   }
+  ctx->eig_ph = false;
   if (rc || qr) return rc;
   const int64_t n2 = 2 * (int64_t)ctx->d.N;
+  const bool own = !evd && n2 <= dwh::kEigMaxN;   // the own solver ran (see above)
   dwh::launch_nonfinite(ctx->tr.U, m * n2 * n2, ctx->tr.E, m * n2, ctx->d_tr_bad, ctx->stream);
   int bad = 0;
+  std::vector<int> c0(own && ctx->eig_half ? m : 0);
   HIPCHECK(ctx, hipMemcpyAsync(&bad, ctx->d_tr_bad, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  if (!c0.empty())
+    HIPCHECK(ctx, hipMemcpyAsync(c0.data(), ctx->d_eig_c0, m * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
   HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+  if (!bad && !c0.empty())
+    ctx->eig_ph = std::all_of(c0.begin(), c0.end(), [&](int c) { return c == ctx->d.N; });
   if (bad) {
     Scope sc(ctx, T_EIG_VENDOR, m);
     rc = eigen_enqueue(ctx, src, m, true);
@@ -2052,21 +2065,24 @@ int transport_run(dwh_ctx* ctx, const TrSrc& src, int m, double eta, double dome
   const int N = ctx->d.N, n2 = 2 * N;
   const int64_t sA = (int64_t)n2 * n2;
   hipStream_t s = ctx->stream;
+  // particle-hole closed U (eig_ph): only the columns < N of J_mn are read
+  const bool ph = ctx->eig_ph;
+  const int ncol = ph ? N : n2;
   for (int k = 0; k < m; ++k) {
     const dwh::TrBufs b = tr_slot(ctx, k);
     dwh::launch_tr_colstats(b.U, N, (int)ctx->Lx, b.E, ctx->beta, eta, ctx->t, ctx->tp, ctx->d_tr_nbr, b.f,
                             b.dia, b.Wn, b.wan, b.w0, s);
-    dwh::launch_tr_current(b.U, b.JU, N, ctx->d_tr_rowptr, ctx->d_tr_col, ctx->d_tr_val, s);
+    dwh::launch_tr_current(b.U, b.JU, N, ctx->d_tr_rowptr, ctx->d_tr_col, ctx->d_tr_val, ncol, s);
   }
   HIPCHECK(ctx, hipGetLastError());
   // J_mn = U^H (J ⊕ J) U  (src/Observables.jl:334-335), the library's own product
   const dwh::TrBufs& b0 = ctx->tr;
-  dwh::gemm_z('C', 'N', n2, n2, n2, make_double2(1.0, 0.0), b0.U, n2, sA, b0.JU, n2, sA, make_double2(0.0, 0.0),
+  dwh::gemm_z('C', 'N', n2, ncol, n2, make_double2(1.0, 0.0), b0.U, n2, sA, b0.JU, n2, sA, make_double2(0.0, 0.0),
               b0.Jmn, n2, sA, m, s);
   HIPCHECK(ctx, hipGetLastError());
   const dwh::TrGrid g{eta, -omega_max, domega, (int)nw, (int)nd};
   for (int k = 0; k < m; ++k)
-    dwh::launch_tr_reduce(tr_slot(ctx, k), N, (int)ctx->Lx, (int)ctx->Ly, ctx->beta, eta, g, s);
+    dwh::launch_tr_reduce(tr_slot(ctx, k), N, (int)ctx->Lx, (int)ctx->Ly, ctx->beta, eta, g, ph, s);
   HIPCHECK(ctx, hipGetLastError());
   std::vector<double> sc(2 * (size_t)m);
   HIPCHECK(ctx, hipMemcpyAsync(sc.data(), b0.scalars, sc.size() * sizeof(double), hipMemcpyDeviceToHost, s));

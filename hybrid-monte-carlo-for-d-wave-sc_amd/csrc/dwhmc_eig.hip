@@ -30,6 +30,11 @@
 //     (exact degeneracies of clean lattices included).
 //     Then one symmetric orthogonalisation step over all vectors (rocBLAS
 //     dgemm, dwhmc_api.cpp).
+//     For H_BdG (the only matrices the library decomposes) steps 3-4 run on
+//     the upper half of the spectrum only: k_eig_c0 finds c0 (n/2, or the
+//     start of a cluster straddling zero, solved whole), and k_eig_theta
+//     fills the columns below c0 with the particle-hole partners
+//     (u; v) -> (-conj v; conj u) of the columns above n - c0.
 //  4. U = H_0 H_1 ... H_{n-2} Z: reflectors in blocks of kEigNB as
 //     I - V T V^H (k_eig_tfac: compact-WY T per block), applied last block
 //     first: W = V^H U by rocBLAS zgemm (split over K into chunks when few

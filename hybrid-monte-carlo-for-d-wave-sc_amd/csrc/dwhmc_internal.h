@@ -219,11 +219,17 @@ void launch_tr_colstats(const double2* U, int N, int Lx, const double* E, double
                         double t, double tp, const int* nbr, double* f, double* dia, double* Wn,
                         double* wan, double* w0, hipStream_t s);
 // JU = (J ⊕ J) U, J in CSR form (N rows, val = Im J)
+// JU[:, :ncol] = (J ⊕ J) U[:, :ncol]
 void launch_tr_current(const double2* U, double2* JU, int N, const int* rowptr, const int* col,
-                       const double* val, hipStream_t s);
-// everything after J_mn: Λ, dc, σ(ω), stiffness, DOS, A(k,0) (overwrites JU and Jmn)
+                       const double* val, int ncol, hipStream_t s);
+// everything after J_mn: Λ, dc, σ(ω), stiffness, DOS, A(k,0) (overwrites JU and Jmn).
+// ph: U is closed under the particle-hole map (column n2-1-j = Θ column j for
+// every j, dwh eigensolver's half solve without a zero-straddling cluster), so
+// J_mn is needed (and computed) only in its columns < N and every pair sum
+// runs over half the pairs (the pair (n, m) and its partner (n2-1-m, n2-1-n)
+// carry the same |J|², E differences and Fermi-factor differences)
 void launch_tr_reduce(const TrBufs& b, int N, int Lx, int Ly, double beta, double eta,
-                      const TrGrid& g, hipStream_t s);
+                      const TrGrid& g, bool ph, hipStream_t s);
 
 // Eigendecomposition leapfrog step (algo eig; U, JU, rho: nc chains of n2 x n2
 // column-major, E: nc x n2): JU = U diag(logistic(-β E)); after rho = JU U^H,

@@ -188,29 +188,34 @@ __device__ inline double rcp_nr(double p) {
   return r;
 }
 
+// ph (launch_tr_reduce): rows n < N only, m in (n, n2-1-n], the pairs
+// strictly inside counted twice (each stands for its particle-hole partner
+// (n2-1-m, n2-1-n)), the self-partnered m = n2-1-n once.
 __global__ void __launch_bounds__(kTB)
 k_tr_sigma(const double2* __restrict__ Jmn, int n2, const double* __restrict__ E,
            const double* __restrict__ f, double eta, double w_start, double w_step, int nw,
-           int rows, double* __restrict__ part) {
+           int rows, int nrow, int ph, double* __restrict__ part) {
   __shared__ double sdE[kTB], scd[kTB];
   const int tid = threadIdx.x;
   const int k = blockIdx.x * kTB + tid;
   const double w = grid_point(w_start, w_step, k < nw ? k : nw - 1);
   const double eta2 = eta * eta;
-  const int n0 = blockIdx.y * rows, n1 = min(n0 + rows, n2);
+  const int n0 = blockIdx.y * rows, n1 = min(n0 + rows, nrow);
   double acc0 = 0, acc1 = 0;
   for (int n = n0; n < n1; ++n) {
     const double En = E[n], fn = f[n];
     const double2* col = Jmn + (size_t)n * n2;
-    for (int m0 = ((n + 1) / kTB) * kTB; m0 < n2; m0 += kTB) {
+    const int mend = ph ? n2 - 1 - n : n2 - 1;   // last m of row n
+    for (int m0 = ((n + 1) / kTB) * kTB; m0 <= mend; m0 += kTB) {
       const int m = m0 + tid;
       double cd = 0.0, dE = 0.0;
-      if (m > n && m < n2) {
+      if (m > n && m <= mend) {
         const double df = fn - f[m];
         if (fabs(df) >= 1e-12) {
           const double2 j = col[m];
           dE = E[m] - En;
           cd = df * (j.x * j.x + j.y * j.y) * dE;
+          if (ph && m < mend) cd *= 2.0;
         }
       }
       if (!__syncthreads_or(cd != 0.0)) continue;
@@ -243,19 +248,24 @@ __global__ void k_tr_sigma_sum(const double* __restrict__ part, int nchunk, int 
 }
 
 // out[0] = stiffness = Σ dia / N - Σ lam / N; out[1] = dc = Σ dc / N
+// (lam, dc over the npair columns k_tr_pairs computed, times pw: 2 when
+// they are the half whose particle-hole partners carry the same sums)
 __global__ void k_tr_scalars(const double* __restrict__ dia, const double* __restrict__ lam,
-                             const double* __restrict__ dc, int n2, int N, double* __restrict__ out) {
+                             const double* __restrict__ dc, int n2, int N, int npair, double pw,
+                             double* __restrict__ out) {
   __shared__ double sh[3][kTB];
   double acc[3] = {0, 0, 0};
   for (int n = threadIdx.x; n < n2; n += kTB) {
     acc[0] += dia[n];
-    acc[1] += lam[n];
-    acc[2] += dc[n];
+    if (n < npair) {
+      acc[1] += lam[n];
+      acc[2] += dc[n];
+    }
   }
   block_sum<3>(acc, sh);
   if (threadIdx.x == 0) {
-    out[0] = sh[0][0] / N - sh[1][0] / N;
-    out[1] = sh[2][0] / N;
+    out[0] = sh[0][0] / N - pw * sh[1][0] / N;
+    out[1] = pw * sh[2][0] / N;
   }
 }
 
@@ -431,27 +441,29 @@ void launch_tr_colstats(const double2* U, int N, int Lx, const double* E, double
 }
 
 void launch_tr_current(const double2* U, double2* JU, int N, const int* rowptr, const int* col,
-                       const double* val, hipStream_t s) {
-  hipLaunchKernelGGL(k_tr_current, dim3(cdiv(2 * N, kTB), 2 * N), dim3(kTB), 0, s, U, JU, 2 * N,
+                       const double* val, int ncol, hipStream_t s) {
+  hipLaunchKernelGGL(k_tr_current, dim3(cdiv(2 * N, kTB), ncol), dim3(kTB), 0, s, U, JU, 2 * N,
                      N, rowptr, col, val);
 }
 
 int tr_sigma_chunks(int N) { return std::min(2 * N, 512); }
 
 void launch_tr_reduce(const TrBufs& b, int N, int Lx, int Ly, double beta, double eta,
-                      const TrGrid& g, hipStream_t s) {
+                      const TrGrid& g, bool ph, hipStream_t s) {
   const int n2 = 2 * N;
-  hipLaunchKernelGGL(k_tr_pairs, dim3(n2), dim3(kTB), 0, s, b.Jmn, n2, b.E, b.f, beta, eta, b.lam,
+  const int npair = ph ? N : n2;   // columns of J_mn the pair sums read
+  hipLaunchKernelGGL(k_tr_pairs, dim3(npair), dim3(kTB), 0, s, b.Jmn, n2, b.E, b.f, beta, eta, b.lam,
                      b.dc);
   if (g.nw > 0) {
-    const int nchunk = tr_sigma_chunks(N), rows = cdiv(n2, nchunk);
-    const int used = cdiv(n2, rows);
+    const int nchunk = std::min(tr_sigma_chunks(N), npair), rows = cdiv(npair, nchunk);
+    const int used = cdiv(npair, rows);
     hipLaunchKernelGGL(k_tr_sigma, dim3(cdiv(g.nw, kTB), used), dim3(kTB), 0, s, b.Jmn, n2, b.E,
-                       b.f, eta, g.w0, g.dw, g.nw, rows, b.part);
+                       b.f, eta, g.w0, g.dw, g.nw, rows, npair, (int)ph, b.part);
     hipLaunchKernelGGL(k_tr_sigma_sum, dim3(cdiv(g.nw, kTB)), dim3(kTB), 0, s, b.part, used, g.nw,
                        eta, N, b.sigma);
   }
-  hipLaunchKernelGGL(k_tr_scalars, dim3(1), dim3(kTB), 0, s, b.dia, b.lam, b.dc, n2, N, b.scalars);
+  hipLaunchKernelGGL(k_tr_scalars, dim3(1), dim3(kTB), 0, s, b.dia, b.lam, b.dc, n2, N, npair, ph ? 2.0 : 1.0,
+                     b.scalars);
   if (g.nd > 0)
     hipLaunchKernelGGL(k_tr_dos, dim3(cdiv(g.nd, kTB)), dim3(kTB), 0, s, b.E, b.Wn, b.wan, n2, N,
                        eta, g.d0, g.dw, g.nd, b.dos, b.dos_an);

@@ -292,6 +292,32 @@ def test_transport_clean_degenerate_spectrum(dwhmc, oracle):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("Lx,Ly,mu,half", [(8, 8, 0.0, "1"), (12, 8, 0.0, "1"), (8, 8, -1.0, "1"), (6, 6, -1.08, "0")])
+def test_transport_particle_hole_half(dwhmc, oracle, monkeypatch, Lx, Ly, mu, half):
+    """The particle-hole half measurement: with the eigensolver's half solve
+    (columns j < N the partners Θ of columns n2-1-j) J_mn is formed in its
+    columns < N only and Λ, the DC sum and σ(ω) run over half the pairs.  A
+    clean lattice at μ = 0 with L % 4 == 0 has exact zero modes (a cluster
+    across E = 0, solved whole, so U is not partner-closed there): every pair
+    is summed.  half = "0" (DWHMC_EIG_HALF=0): the full solve and sums."""
+    O = oracle
+    monkeypatch.setenv("DWHMC_EIG_HALF", half)
+    p = O.ModelParameters(Lx, Ly, 1.0, -0.35, mu, 0.0, 0.0, 16.0, 0.8, 1.0)
+    N = p.N
+    D = np.stack([np.full(N, 0.2), np.full(N, -0.2)], 1).astype(np.complex128)
+    D = D * np.exp(0.2j * np.random.default_rng(Lx + Ly).standard_normal((N, 1)))   # complex, non-uniform phases
+    if mu == 0.0:
+        D = np.stack([np.full(N, 0.2), np.full(N, -0.2)], 1).astype(np.complex128)   # the clean nodes
+    cache, _, _ = O.evaluate(p, np.zeros(N), D)
+    ref = O.measure_transport_and_spectra(cache, p)
+    ctx = _ctx(dwhmc, p, np.zeros(N))
+    ctx.set_pairing(D)
+    r = ctx.measure_transport(p.eta, p.domega, p.omega_max)
+    ctx.close()
+    _check_transport(r, ref)
+
+
+@pytest.mark.gpu
 def test_transport_coarse_grid_and_chain_select(dwhmc, oracle):
     """Non-default η, Δω, ω_max; chain 1 of a batched context."""
     O = oracle
