@@ -685,6 +685,7 @@ struct dwh_ctx {
   double2 *d_eig_part = nullptr, *d_eig_vv = nullptr, *d_eig_ww = nullptr, *d_eig_tau = nullptr;
   double2 *d_eig_T = nullptr, *d_eig_W = nullptr, *d_eig_W2 = nullptr, *d_eig_dpart = nullptr;
   double2* d_eig_pfin = nullptr;   // the hemv partials reduced per row (k_eig_reduce)
+  double2* d_eig_colfin = nullptr;   // column i with its pending pairs (k_eig_reduce)
   int* d_eig_c0 = nullptr;         // particle-hole half solve: first computed eigenvector per matrix
   bool eig_half = false;           // the last own solve ran the particle-hole half solve
   // the last eigen_solve's U of every slot is closed under the particle-hole
@@ -1881,14 +1882,15 @@ int own_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m) {
   if (m > ctx->eig_slots) {
     HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
     for (void* q : {(void*)ctx->d_eig_part, (void*)ctx->d_eig_vv, (void*)ctx->d_eig_ww, (void*)ctx->d_eig_tau,
-                    (void*)ctx->d_eig_dpart, (void*)ctx->d_eig_pfin, (void*)ctx->d_eig_c0,
+                    (void*)ctx->d_eig_dpart, (void*)ctx->d_eig_pfin, (void*)ctx->d_eig_c0, (void*)ctx->d_eig_colfin,
                     (void*)ctx->d_eig_T, (void*)ctx->d_eig_W, (void*)ctx->d_eig_W2, (void*)ctx->d_eig_d,
                     (void*)ctx->d_eig_e, (void*)ctx->d_eig_tn})
       drop_alloc(ctx, q);
     const size_t mm = (size_t)m;
-    if ((rc = dalloc(ctx, &ctx->d_eig_part, mm * sP)) || (rc = dalloc(ctx, &ctx->d_eig_vv, mm * 3 * n)) ||
-        (rc = dalloc(ctx, &ctx->d_eig_ww, mm * 2 * n)) || (rc = dalloc(ctx, &ctx->d_eig_tau, mm * n)) ||
-        (rc = dalloc(ctx, &ctx->d_eig_dpart, mm * 2 * T)) || (rc = dalloc(ctx, &ctx->d_eig_pfin, mm * n)) ||
+    if ((rc = dalloc(ctx, &ctx->d_eig_part, mm * sP)) || (rc = dalloc(ctx, &ctx->d_eig_vv, mm * dwh::kEigRing * n)) ||
+        (rc = dalloc(ctx, &ctx->d_eig_ww, mm * dwh::kEigRing * n)) || (rc = dalloc(ctx, &ctx->d_eig_tau, mm * n)) ||
+        (rc = dalloc(ctx, &ctx->d_eig_dpart, mm * 2 * dwh::kEigDeferMax * T)) ||
+        (rc = dalloc(ctx, &ctx->d_eig_pfin, mm * n)) || (rc = dalloc(ctx, &ctx->d_eig_colfin, mm * n)) ||
         (rc = dalloc(ctx, &ctx->d_eig_T, mm * sT)) || (rc = dalloc(ctx, &ctx->d_eig_W, mm * std::max<int64_t>(KS * sW, (int64_t)nblk * dwh::kEigGS * NB * NB))) ||
         (rc = dalloc(ctx, &ctx->d_eig_W2, mm * sW)) || (rc = dalloc(ctx, &ctx->d_eig_d, mm * n)) ||
         (rc = dalloc(ctx, &ctx->d_eig_e, mm * n)) || (rc = dalloc(ctx, &ctx->d_eig_tn, mm)) ||
@@ -1900,8 +1902,8 @@ int own_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m) {
   double2* A = b.JU;
   if ((rc = assemble_slots(ctx, src, m, A))) return rc;
   for (int i = 0; i < n; ++i) {
-    dwh::launch_eig_step(A, n, i, sA, ctx->d_eig_part, sP, ctx->d_eig_pfin, ctx->d_eig_vv, ctx->d_eig_ww,
-                         ctx->d_eig_d, ctx->d_eig_e, ctx->d_eig_tau, ctx->d_eig_dpart, m, s);
+    dwh::launch_eig_step(A, n, i, sA, ctx->d_eig_part, sP, ctx->d_eig_pfin, ctx->d_eig_colfin, ctx->d_eig_vv,
+                         ctx->d_eig_ww, ctx->d_eig_d, ctx->d_eig_e, ctx->d_eig_tau, ctx->d_eig_dpart, m, s);
     if (i < n - 1)
       dwh::launch_eig_pass(A, n, i, sA, ctx->d_eig_part, sP, ctx->d_eig_vv, ctx->d_eig_ww, ctx->d_eig_dpart, m, s);
   }

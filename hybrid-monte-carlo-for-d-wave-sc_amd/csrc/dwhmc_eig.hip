@@ -82,25 +82,46 @@ __device__ __forceinline__ double2 group_sum2(double2 v, double2* sh) {
 
 __device__ __forceinline__ double2 cz() { return make_double2(0.0, 0.0); }
 
-// pass i reads A without writing it back (the pending pair i-1 is applied by
-// the next, writing pass together with pair i): even i >= 2, when deferring
-// (batches of 4+ matrices, where the passes are HBM-bound; a single matrix is
-// latency-bound and the step's extra corrections would cost more)
-__host__ __device__ __forceinline__ bool eig_read_pass(int i, bool defer) { return defer && i >= 2 && (i & 1) == 0; }
+// Deferred rank-2 pairs (pair j = (v_j, w_j), the update zhetd2 applies after
+// column j).  Pass i (trailing rows / columns >= i+1) writes A only when
+// eig_write_pass(i, K): it applies every pending pair j in
+// [eig_pend_first(i, K), i-1] (at most K) to its tile before the hemv.  The
+// other passes read A as it stands, stale by those pairs, and their diagonal
+// tiles add the dots w_j^H v_i, v_j^H v_i over their rows, with which
+// k_eig_reduce corrects the hemv: A v = A_stale v - sum_j v_j (w_j^H v) +
+// w_j (v_j^H v).  K = 1: every pass writes, pending = {pair i-1}.  Batches of
+// kEigDeferMin+ matrices use K = kEigDefer (HBM-bound passes: (K-1)/K of the
+// column sweeps only read); one matrix K = 1 (latency-bound).  Same algebra:
+// tools/eig_proto.py tridiagonalize_deferred.
+__host__ __device__ __forceinline__ bool eig_write_pass(int i, int K) { return i % K == K - 1; }
+__host__ __device__ __forceinline__ int eig_pend_first(int i, int K) { return i >= K ? (i / K) * K - 1 : 0; }
+constexpr int KD = kEigDeferMax;
 
-// Every load of the step is issued up front (column i, v_{i-1}, the pass
-// partials of this thread's rows and of row i): two workgroup reductions
-// (x^H v, then the reflector norm) are its only barriers.
-// k_eig_reduce: the pass partials of every row summed (ascending tile index,
-// the order the step used when it read them itself), one thread per row and
-// many workgroups, so the single-workgroup step reads n values instead of the
-// ~n T / 3 partials (1 MB at i = 0 for n = 2048): its latency was that read.
+// k_eig_reduce (before step i >= 1): the pass i-1 partials of every row summed
+// (ascending tile index), less the pairs pass i-1 left out (read pass), into
+// pfin = A^{(i-1)} v_{i-1}; column i of A with those pairs applied into colfin
+// (the step applies pair i-1 itself).  One thread per row, many workgroups,
+// so the single-workgroup step reads 2 n values.
 __global__ __launch_bounds__(256) void k_eig_reduce(const double2* __restrict__ part, int64_t sP, int n, int i,
-                                                    double2* __restrict__ pfin) {
-  const int k = blockIdx.y, r = i + blockIdx.x * 256 + threadIdx.x;
+                                                    double2* __restrict__ pfin, const double2* __restrict__ A,
+                                                    int64_t sA, double2* __restrict__ colfin,
+                                                    const double2* __restrict__ vv, const double2* __restrict__ ww,
+                                                    const double2* __restrict__ dpart, int K) {
+  const int k = blockIdx.y, tid = threadIdx.x, r = i + blockIdx.x * 256 + tid;
+  const int t0 = i / kEigTB, T = (n + kEigTB - 1) / kEigTB;
+  const bool rd = !eig_write_pass(i - 1, K);
+  const int f = eig_pend_first(i - 1, K), np = rd ? i - 1 - f : 0;
+  __shared__ double2 dots[2 * KD];
+  if (tid < 2 * np) {   // ascending tile order
+    double2 s = cz();
+    for (int Y = t0; Y < T; ++Y) s = cadd(s, dpart[((int64_t)k * T + Y) * 2 * KD + tid]);
+    dots[tid] = s;
+  }
+  __syncthreads();
   if (r >= n) return;
   part += k * sP;
-  const int t0 = i / kEigTB, T = (n + kEigTB - 1) / kEigTB;
+  vv += (int64_t)k * kEigRing * n;
+  ww += (int64_t)k * kEigRing * n;
   double2 s = cz();
   for (int Y0 = t0; Y0 < T; Y0 += 8) {
     double2 q[8];
@@ -110,84 +131,61 @@ __global__ __launch_bounds__(256) void k_eig_reduce(const double2* __restrict__ 
     for (int u = 0; u < 8; ++u)
       if (Y0 + u < T) s = cadd(s, q[u]);
   }
+  double2 c = A[k * sA + r + (int64_t)i * n];
+  for (int q = 0; q < np; ++q) {
+    const int sl = (f + q) % kEigRing;
+    const double2 vj = vv[(int64_t)sl * n + r], wj = ww[(int64_t)sl * n + r];
+    s = csub(csub(s, cmul(vj, dots[2 * q])), cmul(wj, dots[2 * q + 1]));
+    const double2 vji = vv[(int64_t)sl * n + i], wji = ww[(int64_t)sl * n + i];
+    c = csub(csub(c, cmulc(vj, wji)), cmulc(wj, vji));
+  }
   pfin[(int64_t)k * n + r] = s;
+  colfin[(int64_t)k * n + r] = c;
 }
 
-template <int kMaxR, bool DEFER>   // row slots per thread: ceil(n / kStepT); DEFER: read-only passes in use
+// Step i: w_{i-1} from p = pfin (w = x - 1/2 tau (x^H v) v, x = tau p, zhetd2
+// 'L'), pair i-1 applied to column i (colfin, or A for i = 0), the reflector
+// of column i (zlarfg) into v_i and column i of A.  Every load is issued up
+// front; two workgroup reductions are its only barriers.
+template <int kMaxR>   // row slots per thread: ceil(n / kStepT)
 __global__ __launch_bounds__(kStepT) void k_eig_step(double2* __restrict__ A, int n, int i, int64_t sA,
                                                      const double2* __restrict__ pfin,
+                                                     const double2* __restrict__ colfin,
                                                      double2* __restrict__ vv, double2* __restrict__ ww,
                                                      double* __restrict__ d, double* __restrict__ e,
-                                                     double2* __restrict__ tau,
-                                                     const double2* __restrict__ dpart) {
+                                                     double2* __restrict__ tau) {
   const int k = blockIdx.x, tid = threadIdx.x;
   A += k * sA;
   pfin += (int64_t)k * n;
-  vv += (int64_t)k * 3 * n;
-  ww += (int64_t)k * 2 * n;
+  colfin += (int64_t)k * n;
+  vv += (int64_t)k * kEigRing * n;
+  ww += (int64_t)k * kEigRing * n;
   d += (int64_t)k * n;
   e += (int64_t)k * n;
   tau += (int64_t)k * n;
   __shared__ double2 sh1[kStepT / 64];
   __shared__ double sh2[kStepT / 64];
   __shared__ double2 bc;
-  double2* vcur = vv + (int64_t)(i % 3) * n;
-  const double2* vprv = vv + (int64_t)((i + 2) % 3) * n;   // v_{i-1}
-  const double2* vp2 = vv + (int64_t)((i + 1) % 3) * n;    // v_{i-2}
-  const double2* wp2 = ww + (int64_t)(i & 1) * n;          // w_{i-2}
-  double2* wout = ww + (int64_t)((i + 1) & 1) * n;         // w_{i-1}
-  // pass i-1 was read-only (eig_read_pass): its hemv used A without pair i-2,
-  // which is also still missing from column i
-  const bool rp = eig_read_pass(i - 1, DEFER);
-  const int t0 = i / kEigTB, T = (n + kEigTB - 1) / kEigTB;
-  double2 cr[kMaxR], vp[kMaxR], wr[kMaxR], v2[kMaxR], w2[kMaxR];
+  double2* vcur = vv + (int64_t)(i % kEigRing) * n;
+  const double2* vprv = vv + (int64_t)((i + kEigRing - 1) % kEigRing) * n;   // v_{i-1}
+  double2* wout = ww + (int64_t)((i + kEigRing - 1) % kEigRing) * n;        // w_{i-1}
+  double2 cr[kMaxR], vp[kMaxR], wr[kMaxR];
 #pragma unroll
   for (int s = 0; s < kMaxR; ++s) {
     const int r = i + tid + s * kStepT;
-    cr[s] = vp[s] = wr[s] = v2[s] = w2[s] = cz();
+    cr[s] = vp[s] = wr[s] = cz();
     if (r < n) {
-      cr[s] = A[r + (int64_t)i * n];
-      if (i > 0) vp[s] = vprv[r];
-      if (rp) {
-        v2[s] = vp2[r];
-        w2[s] = wp2[r];
-      }
-    }
-  }
-  // the read-only pass's dots w_{i-2}^H v_{i-1}, v_{i-2}^H v_{i-1} (one per
-  // diagonal tile), summed with the partials below
-  double2 dw = cz(), dv = cz(), v2i = cz(), w2i = cz();
-  if (rp) {
-    v2i = vp2[i];
-    w2i = wp2[i];
-  }
-  double2 pi = cz();   // p[i], every thread (v_{i-1}[i] = 1: w[i] = x[i] + alpha)
-  if (i > 0) {
-    // the pass's hemv, reduced per row by k_eig_reduce
-#pragma unroll
-    for (int s = 0; s < kMaxR; ++s) {
-      const int r = i + tid + s * kStepT;
-      if (r < n) wr[s] = pfin[r];
-    }
-    pi = pfin[i];
-    if (rp) {   // the read-only pass's dots, ascending tile index
-      for (int Y = t0; Y < T; ++Y) {
-        dw = cadd(dw, dpart[(int64_t)(k * T + Y) * 2]);
-        dv = cadd(dv, dpart[(int64_t)(k * T + Y) * 2 + 1]);
+      cr[s] = i > 0 ? colfin[r] : A[r];
+      if (i > 0) {
+        vp[s] = vprv[r];
+        wr[s] = pfin[r];
       }
     }
   }
   double2 wi = cz();
   if (i > 0) {
-    // p = A^{(i-1)} v_{i-1} (less the pending pair i-2 after a read-only
-    // pass: A v = A_stale v - v2 (w2^H v) - w2 (v2^H v)); x = tau p;
-    // w = x - 1/2 tau (x^H v) v  (zhetd2 'L')
+    const double2 pi = pfin[i];   // p[i] (v_{i-1}[i] = 1: w[i] = x[i] + alpha)
     const double2 tp = tau[i - 1];
-    if (rp) {
-#pragma unroll
-      for (int s = 0; s < kMaxR; ++s) wr[s] = csub(csub(wr[s], cmul(v2[s], dw)), cmul(w2[s], dv));
-      pi = csub(csub(pi, cmul(v2i, dw)), cmul(w2i, dv));
-    }
     double2 g = cz();
 #pragma unroll
     for (int s = 0; s < kMaxR; ++s) {
@@ -205,8 +203,7 @@ __global__ __launch_bounds__(kStepT) void k_eig_step(double2* __restrict__ A, in
       if (r < n) wout[r] = wr[s];
     }
   }
-  // column i with the deferred updates of column i-1 (v_{i-1}[i] = 1) and,
-  // after a read-only pass, of column i-2
+  // column i with pair i-1 (v_{i-1}[i] = 1)
   double xn = 0.0;
 #pragma unroll
   for (int s = 0; s < kMaxR; ++s) {
@@ -214,7 +211,6 @@ __global__ __launch_bounds__(kStepT) void k_eig_step(double2* __restrict__ A, in
     if (r < n) {
       double2 c = cr[s];
       if (i > 0) c = csub(csub(c, cmulc(vp[s], wi)), wr[s]);
-      if (rp) c = csub(csub(c, cmulc(v2[s], w2i)), cmulc(w2[s], v2i));
       cr[s] = c;
       if (r >= i + 2) xn += c.x * c.x + c.y * c.y;
       if (r == i) d[i] = c.x;
@@ -258,57 +254,49 @@ __device__ __forceinline__ void tri_decode(int b, int& R, int& C) {
 }
 
 // Pass i over the trailing lower triangle (rows / cols >= i+1), one
-// workgroup per 64 x 64 tile.  Write passes (all of them for fewer than
-// kEigDeferMin matrices; else odd i, and i = 0 with nothing pending) apply the
-// pending rank-2 pairs (column i-1, and i-2 after a
-// read-only pass) to the tile and write it back; read-only passes
-// (eig_read_pass: even i >= 2) leave A stale by pair i-1 and the diagonal
-// tiles add the dots w_{i-1}^H v_i, v_{i-1}^H v_i for the step's correction:
-// two column sweeps of three write A (25 % fewer HBM bytes).  Both
-// accumulate the tile's share of A v_i into fixed partial slots.
+// workgroup per 64 x 64 tile: a write pass applies the pending pairs to the
+// tile and writes it back; every pass accumulates the tile's share of A v_i
+// into fixed partial slots, and a read pass's diagonal tiles the dots of the
+// pending pairs with v_i.
 __global__ __launch_bounds__(256) void k_eig_pass(double2* __restrict__ A, int n, int i, int64_t sA,
                                                   double2* __restrict__ part, int64_t sP,
                                                   const double2* __restrict__ vv, const double2* __restrict__ ww,
-                                                  int t0, double2* __restrict__ dpart, int T, int defer) {
+                                                  int t0, double2* __restrict__ dpart, int T, int K) {
   const int k = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   A += k * sA;
   part += k * sP;
-  vv += (int64_t)k * 3 * n;
-  ww += (int64_t)k * 2 * n;
-  const double2* v = vv + (int64_t)(i % 3) * n;
-  const double2* va = vv + (int64_t)((i + 2) % 3) * n;   // pair i-1
-  const double2* wa = ww + (int64_t)((i + 1) & 1) * n;
-  const double2* vb = vv + (int64_t)((i + 1) % 3) * n;   // pair i-2
-  const double2* wb = ww + (int64_t)(i & 1) * n;
-  const bool rd = eig_read_pass(i, defer);
-  // pairs applied to A: none on a read pass (or before any pair exists);
-  // deferring, odd i >= 3 applies pairs i-2 and i-1; else pair i-1
-  const int np = rd || i == 0 ? 0 : (defer && i >= 3 ? 2 : 1);
+  vv += (int64_t)k * kEigRing * n;
+  ww += (int64_t)k * kEigRing * n;
+  const double2* v = vv + (int64_t)(i % kEigRing) * n;
+  const bool wp = eig_write_pass(i, K);
+  const int f = eig_pend_first(i, K), np = i - f;   // pending pairs f .. i-1
   int R, C;
   tri_decode(blockIdx.x, R, C);
   R += t0;
   C += t0;
-  __shared__ double2 cv[64], cva[64], cwa[64], cvb[64], cwb[64], csum[64];
-  __shared__ double2 colc[64][65];
+  __shared__ double2 cv[64], csum[64];
   __shared__ double2 rowp[4][64];
-  if (tid < 64) {
-    const int gc = C * kEigTB + tid;
-    const bool ok = gc >= i + 1 && gc < n;
-    cv[tid] = ok ? v[gc] : cz();
-    cva[tid] = ok && np >= 1 ? va[gc] : cz();
-    cwa[tid] = ok && np >= 1 ? wa[gc] : cz();
-    cvb[tid] = ok && np >= 2 ? vb[gc] : cz();
-    cwb[tid] = ok && np >= 2 ? wb[gc] : cz();
-  }
+  // the pending pairs' column values (write pass), then the column-sum
+  // transpose: one LDS region, the two phases split by a barrier
+  __shared__ double2 lds[64 * 65];
+  double2(*colc)[65] = reinterpret_cast<double2(*)[65]>(lds);
+  double2* cpv = lds;            // [KD][64]: v_j of the tile's columns
+  double2* cpw = lds + KD * 64;  // [KD][64]: w_j
   const int gr = R * kEigTB + lane;
   const bool rok = gr >= i + 1 && gr < n;
+  if (tid < 64) {
+    const int gc = C * kEigTB + tid;
+    cv[tid] = gc >= i + 1 && gc < n ? v[gc] : cz();
+  }
+  if (wp) {
+    for (int q = w; q < np; q += 4) {   // wave w stages pairs w, w+4
+      const int sl = (f + q) % kEigRing, gc = C * kEigTB + lane;
+      const bool ok = gc >= i + 1 && gc < n;
+      cpv[q * 64 + lane] = ok ? vv[(int64_t)sl * n + gc] : cz();
+      cpw[q * 64 + lane] = ok ? ww[(int64_t)sl * n + gc] : cz();
+    }
+  }
   const double2 vr = rok ? v[gr] : cz();
-  const double2 var = rok && (np >= 1 || rd) ? va[gr] : cz();
-  const double2 war = rok && (np >= 1 || rd) ? wa[gr] : cz();
-  const double2 vbr = rok && np >= 2 ? vb[gr] : cz();
-  const double2 wbr = rok && np >= 2 ? wb[gr] : cz();
-  __syncthreads();
-  double2 pr = cz();
   constexpr int NCW = kEigTB / 4;   // columns per wave
   double2 a[NCW];
   unsigned act = 0;
@@ -319,33 +307,56 @@ __global__ __launch_bounds__(256) void k_eig_pass(double2* __restrict__ A, int n
     act |= (unsigned)ok << u;
     a[u] = ok ? A[gr + (int64_t)gc * n] : cz();
   }
+  __syncthreads();
+  if (wp && np > 0) {
+    double2 rv[KD], rw[KD];
+#pragma unroll
+    for (int q = 0; q < KD; ++q) {
+      const int sl = (f + q) % kEigRing;
+      rv[q] = rok && q < np ? vv[(int64_t)sl * n + gr] : cz();
+      rw[q] = rok && q < np ? ww[(int64_t)sl * n + gr] : cz();
+    }
+#pragma unroll
+    for (int u = 0; u < NCW; ++u) {
+      const int cc = w + 4 * u, gc = C * kEigTB + cc;
+      if ((act >> u) & 1) {
+        double2 x = a[u];
+#pragma unroll
+        for (int q = 0; q < KD; ++q)
+          if (q < np) x = csub(csub(x, cmulc(rv[q], cpw[q * 64 + cc])), cmulc(rw[q], cpv[q * 64 + cc]));
+        a[u] = x;
+        A[gr + (int64_t)gc * n] = x;
+      }
+    }
+    __syncthreads();   // the pair values are dead: the region becomes colc
+  }
+  double2 pr = cz();
 #pragma unroll
   for (int u = 0; u < NCW; ++u) {
     const int cc = w + 4 * u, gc = C * kEigTB + cc;
     double2 t = cz();
     if ((act >> u) & 1) {
-      if (np >= 1) {
-        a[u] = csub(csub(a[u], cmulc(var, cwa[cc])), cmulc(war, cva[cc]));
-        if (np >= 2) a[u] = csub(csub(a[u], cmulc(vbr, cwb[cc])), cmulc(wbr, cvb[cc]));
-        A[gr + (int64_t)gc * n] = a[u];
-      }
       pr = cadd(pr, cmul(a[u], cv[cc]));
       if (gr > gc) t = make_double2(a[u].x * vr.x + a[u].y * vr.y, a[u].x * vr.y - a[u].y * vr.x);   // conj(a) v_r
     }
     colc[cc][lane] = t;
   }
   rowp[w][lane] = pr;
-  if (rd && R == C && w == 0) {
-    // dots of the pending pair i-1 with v_i over this tile's rows
-    double2 dw = make_double2(war.x * vr.x + war.y * vr.y, war.x * vr.y - war.y * vr.x);
-    double2 dv = make_double2(var.x * vr.x + var.y * vr.y, var.x * vr.y - var.y * vr.x);
-    dw.x = wave_sum(dw.x);
-    dw.y = wave_sum(dw.y);
-    dv.x = wave_sum(dv.x);
-    dv.y = wave_sum(dv.y);
-    if (lane == 0) {
-      dpart[(int64_t)(k * T + R) * 2] = dw;
-      dpart[(int64_t)(k * T + R) * 2 + 1] = dv;
+  if (!wp && np > 0 && R == C && w == 0) {
+    // dots of the pending pairs with v_i over this tile's rows
+    for (int q = 0; q < np; ++q) {
+      const int sl = (f + q) % kEigRing;
+      const double2 vj = rok ? vv[(int64_t)sl * n + gr] : cz(), wj = rok ? ww[(int64_t)sl * n + gr] : cz();
+      double2 dw = make_double2(wj.x * vr.x + wj.y * vr.y, wj.x * vr.y - wj.y * vr.x);
+      double2 dv = make_double2(vj.x * vr.x + vj.y * vr.y, vj.x * vr.y - vj.y * vr.x);
+      dw.x = wave_sum(dw.x);
+      dw.y = wave_sum(dw.y);
+      dv.x = wave_sum(dv.x);
+      dv.y = wave_sum(dv.y);
+      if (lane == 0) {
+        dpart[((int64_t)k * T + R) * 2 * KD + 2 * q] = dw;
+        dpart[((int64_t)k * T + R) * 2 * KD + 2 * q + 1] = dv;
+      }
     }
   }
   __syncthreads();
@@ -885,39 +896,36 @@ __global__ __launch_bounds__(256) void k_eig_tw(const double2* __restrict__ Tb, 
 
 }  // namespace
 
-// batch size from which every other pass is read-only (DWHMC_EIG_DEFER_MIN
-// overrides kEigDeferMin for A/B runs); read at each solve
+// batch size from which passes defer their pairs (DWHMC_EIG_DEFER_MIN
+// overrides kEigDeferMin), and the deferral depth K (DWHMC_EIG_DEFER_K
+// overrides kEigDefer, 1 .. kEigDeferMax); read at each launch
 int eig_defer_min() {
   const char* e = std::getenv("DWHMC_EIG_DEFER_MIN");
   return e ? std::max(1, std::atoi(e)) : kEigDeferMin;
 }
+int eig_defer_k(int m) {
+  if (m < eig_defer_min()) return 1;
+  const char* e = std::getenv("DWHMC_EIG_DEFER_K");
+  return e ? std::min(kEigDeferMax, std::max(1, std::atoi(e))) : kEigDefer;
+}
 
 void launch_eig_step(double2* A, int n, int i, int64_t sA, const double2* part, int64_t sP, double2* pfin,
-                     double2* vv, double2* ww, double* d, double* e, double2* tau, const double2* dpart, int m,
-                     hipStream_t s) {
-  const int defer = m >= eig_defer_min();
+                     double2* colfin, double2* vv, double2* ww, double* d, double* e, double2* tau,
+                     const double2* dpart, int m, hipStream_t s) {
+  const int K = eig_defer_k(m);
   if (i > 0)
-    hipLaunchKernelGGL(k_eig_reduce, dim3((n - i + 255) / 256, m), dim3(256), 0, s, part, sP, n, i, pfin);
+    hipLaunchKernelGGL(k_eig_reduce, dim3((n - i + 255) / 256, m), dim3(256), 0, s, part, sP, n, i, pfin, A, sA,
+                       colfin, vv, ww, dpart, K);
   const int rs = (n - i + kStepT - 1) / kStepT;   // row slots the rows i..n-1 need
   static_assert(kEigMaxN <= 5 * kStepT, "k_eig_step instantiations");
-#define DWH_EIG_STEP(R, D) \
-  hipLaunchKernelGGL((k_eig_step<R, D>), dim3(m), dim3(kStepT), 0, s, A, n, i, sA, pfin, vv, ww, d, e, tau, dpart)
-  if (defer) {
-    switch (rs) {
-      case 1: DWH_EIG_STEP(1, true); break;
-      case 2: DWH_EIG_STEP(2, true); break;
-      case 3: DWH_EIG_STEP(3, true); break;
-      case 4: DWH_EIG_STEP(4, true); break;
-      default: DWH_EIG_STEP(5, true); break;
-    }
-  } else {
-    switch (rs) {
-      case 1: DWH_EIG_STEP(1, false); break;
-      case 2: DWH_EIG_STEP(2, false); break;
-      case 3: DWH_EIG_STEP(3, false); break;
-      case 4: DWH_EIG_STEP(4, false); break;
-      default: DWH_EIG_STEP(5, false); break;
-    }
+#define DWH_EIG_STEP(R) \
+  hipLaunchKernelGGL((k_eig_step<R>), dim3(m), dim3(kStepT), 0, s, A, n, i, sA, pfin, colfin, vv, ww, d, e, tau)
+  switch (rs) {
+    case 1: DWH_EIG_STEP(1); break;
+    case 2: DWH_EIG_STEP(2); break;
+    case 3: DWH_EIG_STEP(3); break;
+    case 4: DWH_EIG_STEP(4); break;
+    default: DWH_EIG_STEP(5); break;
   }
 #undef DWH_EIG_STEP
 }
@@ -927,7 +935,7 @@ void launch_eig_pass(double2* A, int n, int i, int64_t sA, double2* part, int64_
   const int T = (n + kEigTB - 1) / kEigTB, t0 = (i + 1) / kEigTB, nT = T - t0;
   if (nT <= 0) return;
   hipLaunchKernelGGL(k_eig_pass, dim3(nT * (nT + 1) / 2, m), dim3(256), 0, s, A, n, i, sA, part, sP, vv, ww, t0,
-                     dpart, T, (int)(m >= eig_defer_min()));
+                     dpart, T, eig_defer_k(m));
 }
 
 void launch_eig_bisect(const double* d, const double* e, int n, double* E, double* tnorm, int m, hipStream_t s) {

@@ -248,14 +248,22 @@ constexpr int kEigNB = 64;                  // reflectors per back-transform blo
 constexpr int kEigMaxN = 5120;              // rows k_eig_step holds in registers
 constexpr double kEigClusterTol = 2.5e-4;   // eigenvalue gap / ||T|| below which vectors are orthogonalised
 constexpr int kEigMaxCluster = 64;          // longest such run (else *bad: vendor fallback)
-// column i of the tridiagonalisation: partial sums -> w_{i-1}, column i -> v_i (d, e, tau)
-// vv: 3 x n per matrix (v_j in slot j % 3), ww: 2 x n (w_j in slot j % 2),
-// dpart: ceil(n / kEigTB) x 2 per matrix (the read-only passes' dots),
-// pfin: n per matrix (the partials reduced per row, k_eig_reduce)
+// deferral of the tridiagonalisation's rank-2 pairs (dwhmc_eig.hip): batches
+// of kEigDeferMin+ matrices apply them every kEigDefer-th pass (at most
+// kEigDeferMax pending); v_j / w_j live in a ring of kEigRing slots per matrix
+constexpr int kEigDefer = 8;
+constexpr int kEigDeferMax = 8;
+constexpr int kEigRing = kEigDeferMax + 2;
+// column i of the tridiagonalisation (k_eig_reduce + k_eig_step): the pass
+// partials (+ the read pass's pending-pair corrections) -> pfin, column i with
+// the pending pairs -> colfin, then w_{i-1}, v_i (d, e, tau).
+// vv, ww: kEigRing x n per matrix (v_j, w_j in slot j % kEigRing);
+// dpart: ceil(n / kEigTB) x 2 kEigDeferMax per matrix (a read pass's dots);
+// pfin, colfin: n per matrix
 void launch_eig_step(double2* A, int n, int i, int64_t sA, const double2* part, int64_t sP, double2* pfin,
-                     double2* vv, double2* ww, double* d, double* e, double2* tau, const double2* dpart, int m,
-                     hipStream_t s);
-// deferred rank-2 update of column i-1 on the trailing triangle + hemv partials of v_i
+                     double2* colfin, double2* vv, double2* ww, double* d, double* e, double2* tau,
+                     const double2* dpart, int m, hipStream_t s);
+// the pending pairs on the trailing triangle (write passes) + hemv partials of v_i
 void launch_eig_pass(double2* A, int n, int i, int64_t sA, double2* part, int64_t sP, const double2* vv,
                      const double2* ww, double2* dpart, int m, hipStream_t s);
 // eigenvalues ascending into E, ||T|| bound per matrix into tnorm
@@ -277,8 +285,9 @@ void launch_eig_theta(double2* U, int n, int64_t sA, const int* c0, int m, hipSt
 // U[:, j0:] from Zt[:, j0:] (real -> complex, transposed through LDS)
 void launch_eig_zt_to_u(const double* Zt, double2* U, int n, int64_t sZ, int64_t sA, int m, hipStream_t s,
                         int j0 = 0);
-constexpr int kEigDeferMin = 4;             // batches from this many matrices defer every other rank-2 update
+constexpr int kEigDeferMin = 4;             // batches from this many matrices defer their rank-2 pairs
 int eig_defer_min();                        // kEigDeferMin or DWHMC_EIG_DEFER_MIN
+int eig_defer_k(int m);                     // deferral depth for m matrices (1: none)
 constexpr int kEigGS = 8;                   // row slices of each block's Gram sum
 // compact-WY T of every reflector block; Gp: m x nblk x kEigGS x kEigNB^2 scratch
 void launch_eig_tfac(const double2* V, int n, int64_t sA, const double2* tau, double2* Gp, double2* Tb, int64_t sT,

@@ -111,3 +111,21 @@ def test_bdg_half_spectrum_vectors(oracle, Lx, Ly, clean, mu):
         assert c0 < n // 2          # the zero modes straddle
     else:
         assert c0 == n // 2
+
+
+@pytest.mark.parametrize("K", [1, 2, 3, 8])
+@pytest.mark.parametrize("n", [1, 2, 9, 17, 40])
+def test_deferred_pairs_same_reduction(K, n):
+    """tridiagonalize_deferred (the device's deferral: the rank-2 pairs reach
+    the trailing triangle only every K-th pass; read-only passes' hemv
+    corrected by the pending pairs' dots, the next column by the pairs
+    themselves) gives the reduction of tridiagonalize to rounding."""
+    rng = np.random.default_rng(100 + n)
+    X = rng.standard_normal((n, n)) + 1j * rng.standard_normal((n, n))
+    A = X + X.conj().T
+    ref = P.tridiagonalize(A)
+    got = P.tridiagonalize_deferred(A, K)
+    scale = 1 + np.max(np.abs(A))
+    for a, b in zip(ref, got):
+        if np.size(a):
+            assert np.max(np.abs(a - b)) <= 1e-13 * scale * max(n, 1)

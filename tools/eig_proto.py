@@ -72,6 +72,62 @@ def tridiagonalize(A: np.ndarray):
     return d, e, V, tau
 
 
+def defer_write_pass(i: int, K: int) -> bool:
+    """Pass i applies every pending rank-2 pair to the trailing triangle when
+    i % K == K - 1 (with K = 1 every pass); the others only read A."""
+    return i % K == K - 1
+
+
+def tridiagonalize_deferred(A: np.ndarray, K: int = 8):
+    """tridiagonalize with the rank-2 pairs applied to the trailing triangle
+    only every K-th pass (csrc/dwhmc_eig.hip with kEigDefer = K): a read-only
+    pass forms A_stale v_i, and the reduction of its partials corrects it with
+    the pending pairs j (A v = A_stale v - sum_j v_j (w_j^H v) + w_j (v_j^H v),
+    the dots from the pass); the next column gets the pending pairs (all but
+    the newest, which the step applies) before the reflector."""
+    A = A.copy()
+    n = A.shape[0]
+    d = np.zeros(n)
+    e = np.zeros(max(n - 1, 0))
+    tau = np.zeros(max(n - 1, 0), complex)
+    V = np.zeros((n, n), complex)
+    pend = []          # pairs (v_j, w_j) not yet applied to A's trailing triangle
+    newest = None      # pair i-1: known once the step has formed w
+    for i in range(n - 1):
+        col = A[i:, i].copy()
+        for (vj, wj) in pend + ([newest] if newest is not None else []):
+            col -= vj[i:] * np.conj(wj[i]) + wj[i:] * np.conj(vj[i])
+        if newest is not None:
+            pend.append(newest)
+        d[i] = col[0].real
+        t, beta, v = larfg(col[1], col[2:])
+        e[i] = beta
+        tau[i] = t
+        vi = np.zeros(n, complex)
+        vi[i + 1] = 1.0
+        vi[i + 2:] = v
+        V[:, i] = vi
+        s = slice(i + 1, n)
+        if defer_write_pass(i, K):
+            for (vj, wj) in pend:
+                A[s, s] -= np.outer(vj[s], np.conj(wj[s])) + np.outer(wj[s], np.conj(vj[s]))
+            pend = []
+        L = np.tril(A[s, s])
+        p = L @ vi[s] + np.conj(np.tril(A[s, s], -1)).T @ vi[s]
+        for (vj, wj) in pend:   # read-only pass: the pairs A still lacks
+            p -= vj[s] * np.vdot(wj[s], vi[s]) + wj[s] * np.vdot(vj[s], vi[s])
+        x = t * p
+        alpha = -0.5 * t * np.vdot(x, vi[s])
+        w = np.zeros(n, complex)
+        w[s] = x + alpha * vi[s]
+        newest = (vi, w)
+    col = A[n - 1:, n - 1].copy()
+    for (vj, wj) in pend + ([newest] if newest is not None else []):
+        col -= vj[n - 1:] * np.conj(wj[n - 1]) + wj[n - 1:] * np.conj(vj[n - 1])
+    d[n - 1] = col[0].real
+    return d, e, V, tau
+
+
 def sturm_count(d, e2, lam, pivmin):
     """Number of eigenvalues of T below lam (dstebz recurrence)."""
     q = d[0] - lam
