@@ -6,20 +6,22 @@
 //
 //  1. Householder tridiagonalisation, LAPACK zhetd2 'L' algebra (reflectors
 //     H_i = I - tau_i v_i v_i^H, v_i[i+1] = 1, beta_i real so T is real
-//     symmetric).  Two launches per column, both batched over the m matrices:
-//       k_eig_step  (one workgroup per matrix): reduces the previous pass's
-//                   hemv partials to p = A v_{i-1}, forms w_{i-1} = tau p -
-//                   1/2 tau (tau p)^H v v, applies the deferred rank-2 update
-//                   to column i only and generates the reflector of column i
-//                   (zlarfg); column i of A becomes v_i (zeros above i+1), so
-//                   A ends as the dense V the back-transform multiplies by.
+//     symmetric).  Per column, batched over the m matrices:
+//       k_eig_reduce (one thread per row): the previous pass's hemv partials
+//                   summed per row into p = A v_{i-1} and column i, both with
+//                   the rank-2 pairs the trailing triangle still lacks;
+//       k_eig_step  (one workgroup per matrix): w_{i-1} = tau p - 1/2 tau
+//                   (tau p)^H v v, pair i-1 on column i, the reflector of
+//                   column i (zlarfg); column i of A becomes v_i (zeros above
+//                   i+1), so A ends as the dense V the back-transform uses;
 //       k_eig_pass  (one workgroup per 64 x 64 lower-triangle tile of the
-//                   trailing matrix): applies the deferred update of column
-//                   i-1 to the tile and accumulates the tile's share of
-//                   A v_i in the same sweep: one read + write of the trailing
-//                   triangle per column (HBM-bound; early columns ~67 MB per
-//                   matrix at n = 2048), partials written once per slot and
-//                   summed in a fixed order (bit-reproducible).
+//                   trailing matrix): every K-th pass applies the pending
+//                   pairs to the tile and writes it back, the others only
+//                   read it (K = 8 for batches: HBM-bound, 9/16 of the
+//                   read + write traffic; K = 1 for one matrix); each
+//                   accumulates the tile's share of A v_i, partials written
+//                   once per slot and summed in a fixed order
+//                   (bit-reproducible).
 //  2. k_eig_bisect: every eigenvalue of T on Sturm counts, one wave per
 //     eigenvalue index, 64-section per round down to the last bit.
 //  3. k_eig_invit: inverse iteration, T - lambda I = LU with partial pivoting
@@ -28,8 +30,8 @@
 //     clusters (consecutive gaps <= 2.5e-4 ||T||, so every other pair is
 //     orthogonal to ~1e-12 already) orthonormalised by Cholesky QR, twice
 //     (exact degeneracies of clean lattices included).
-//     Then one symmetric orthogonalisation step over all vectors (rocBLAS
-//     dgemm, dwhmc_api.cpp).
+//     Then one symmetric orthogonalisation step over all vectors (the
+//     library's real products, dwhmc_gemm.hip, driven by dwhmc_api.cpp).
 //     For H_BdG (the only matrices the library decomposes) steps 3-4 run on
 //     the upper half of the spectrum only: k_eig_c0 finds c0 (n/2, or the
 //     start of a cluster straddling zero, solved whole), and k_eig_theta
@@ -37,9 +39,9 @@
 //     (u; v) -> (-conj v; conj u) of the columns above n - c0.
 //  4. U = H_0 H_1 ... H_{n-2} Z: reflectors in blocks of kEigNB as
 //     I - V T V^H (k_eig_tfac: compact-WY T per block), applied last block
-//     first: W = V^H U by rocBLAS zgemm (split over K into chunks when few
-//     matrices are batched, its output being only kEigNB x n), W2 = T sum of
-//     the chunks (k_eig_tw), U -= V W2 by rocBLAS zgemm.
+//     first: W = V^H U (the library's complex product, split over K into
+//     chunks when few matrices are batched, its output being only kEigNB x
+//     n), W2 = T sum of the chunks (k_eig_tw), U -= V W2.
 //
 // The numpy prototype with the same operation order: tools/eig_proto.py.
 #include <cfloat>
