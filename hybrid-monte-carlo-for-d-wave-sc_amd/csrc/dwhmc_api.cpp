@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -1867,6 +1868,27 @@ int assemble_slots(dwh_ctx* ctx, const TrSrc& src, int m, double2* A) {
 // to tridiagonal form in place (JU becomes the reflectors V), eigenvalues by
 // bisection into E, eigenvectors of T by inverse iteration (Jmn and U as
 // scratch), then U = V-reflectors · Z by blocked compact-WY zgemms
+// DWHMC_EIG_DEBUG=1: synchronise after each phase of the own solver and print
+// its wall time to stderr (diagnosing a slow or stuck phase on the device)
+struct EigPhase {
+  bool on;
+  hipStream_t s;
+  std::chrono::steady_clock::time_point t;
+  explicit EigPhase(hipStream_t st) : s(st), t(std::chrono::steady_clock::now()) {
+    const char* e = std::getenv("DWHMC_EIG_DEBUG");
+    on = e && *e == '1';
+  }
+  void mark(const char* what) {
+    if (!on) return;
+    const hipError_t err = hipStreamSynchronize(s);
+    const auto now = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "eig phase %-14s %9.3f ms  %s\n", what,
+                 std::chrono::duration<double, std::milli>(now - t).count(), hipGetErrorString(err));
+    std::fflush(stderr);
+    t = now;
+  }
+};
+
 int own_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m) {
   const int N = ctx->d.N, n = 2 * N;
   const dwh::TrBufs& b = ctx->tr;
@@ -1900,14 +1922,19 @@ int own_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m) {
   }
   hipStream_t s = ctx->stream;
   double2* A = b.JU;
+  EigPhase ph(s);
   if ((rc = assemble_slots(ctx, src, m, A))) return rc;
+  ph.mark("assemble");
   for (int i = 0; i < n; ++i) {
+    if (ph.on && i % 512 == 0 && i > 0) ph.mark("tridiag/512");
     dwh::launch_eig_step(A, n, i, sA, ctx->d_eig_part, sP, ctx->d_eig_pfin, ctx->d_eig_colfin, ctx->d_eig_vv,
                          ctx->d_eig_ww, ctx->d_eig_d, ctx->d_eig_e, ctx->d_eig_tau, ctx->d_eig_dpart, m, s);
     if (i < n - 1)
       dwh::launch_eig_pass(A, n, i, sA, ctx->d_eig_part, sP, ctx->d_eig_vv, ctx->d_eig_ww, ctx->d_eig_dpart, m, s);
   }
+  ph.mark("tridiag");
   dwh::launch_eig_bisect(ctx->d_eig_d, ctx->d_eig_e, n, b.E, ctx->d_eig_tn, m, s);
+  ph.mark("bisect");
   double* Zt = reinterpret_cast<double*>(b.Jmn);
   double* Ud = reinterpret_cast<double*>(b.U);
   // DWHMC_EIG_MAX_CLUSTER (tests): a shorter cluster limit, to exercise the
@@ -1930,6 +1957,7 @@ int own_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m) {
   if (half) dwh::launch_eig_c0(b.E, ctx->d_eig_tn, n, maxc, ctx->d_eig_c0, ctx->d_tr_bad, m, s);
   dwh::launch_eig_invit(ctx->d_eig_d, ctx->d_eig_e, n, b.E, ctx->d_eig_tn, Zt, Zt + sA, Ud, Ud + sA, sZ,
                         ctx->d_tr_bad, m, s, maxc, j0, half ? ctx->d_eig_c0 : nullptr);
+  ph.mark("invit+orth");
   // One symmetric (Löwdin) orthogonalisation step over the computed vectors:
   // with Y = Z^T (column-major Zt, its rows j0.. the vectors) and G = Y Y^T =
   // I + F, Y <- (3/2 I - 1/2 G) Y leaves ||F|| -> O(||F||^2).  Outside clusters
@@ -1944,6 +1972,7 @@ int own_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m) {
   dwh::gemm_d('N', 'N', M, n, M, -0.5, G, M, sZ, Zt + j0, n, sZ, 1.5, Y2 + j0, n, sZ, m, s);
   dwh::launch_eig_zt_to_u(Y2, b.U, n, sZ, sA, m, s, j0);
   HIPCHECK(ctx, hipGetLastError());
+  ph.mark("lowdin");
   if (n < 2) return DWH_OK;
   dwh::launch_eig_tfac(A, n, sA, ctx->d_eig_tau, ctx->d_eig_W, ctx->d_eig_T, sT, m, s);   // W as Gram scratch
   HIPCHECK(ctx, hipGetLastError());
@@ -1966,6 +1995,7 @@ int own_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m) {
     dwh::gemm_z('N', 'N', ms, M, kb, mone, Vb, n, sA, ctx->d_eig_W2, NB, sW, one, Us, n, sA, m, s);
   }
   if (half) dwh::launch_eig_theta(b.U, n, sA, ctx->d_eig_c0, m, s);
+  ph.mark("backtransform");
   HIPCHECK(ctx, hipGetLastError());
   return DWH_OK;
 }
