@@ -187,10 +187,9 @@ def test_own_eigensolver_L48(dwhmc, oracle):
     density of 4608 levels) through the own solver with no rocSOLVER fallback,
     at the tolerances of test_own_eigensolver_full_size (kEigMaxN
     covers it).  Eigenvalues against LAPACK (zheevr, values only); the
-    residual ‖H U − U E‖ and ‖UᴴU − I‖ are formed on the GPU (torch fp64
-    products), since n = 4608 products on the host take minutes."""
+    residual ‖H U − U E‖ and ‖UᴴU − I‖ by numpy products (seconds; LAPACK's
+    eigenvectors at n = 4608 would take minutes)."""
     import scipy.linalg as sla
-    import torch
     O = oracle
     p, dis, D = _case(O, 48, 48, 32.0, seed=4848)
     cache = O.initialize_cache(p)
@@ -207,11 +206,9 @@ def test_own_eigensolver_L48(dwhmc, oracle):
     assert np.all(np.isfinite(U))
     scale = 1 + np.max(np.abs(Eref))
     assert np.max(np.abs(E - Eref)) <= 1e-12 * scale
-    H = torch.from_numpy(O.hermitian_from_upper(cache.H_base)).to("cuda:0")
-    Ug = torch.from_numpy(np.ascontiguousarray(U)).to("cuda:0")
-    Eg = torch.from_numpy(np.asarray(E)).to("cuda:0")
-    res = (H @ Ug - Ug * Eg[None, :]).abs().max().item()
-    orth = (Ug.conj().T @ Ug - torch.eye(2 * p.N, dtype=Ug.dtype, device=Ug.device)).abs().max().item()
+    H = O.hermitian_from_upper(cache.H_base)
+    res = np.max(np.abs(H @ U - U * E[None, :]))
+    orth = np.max(np.abs(U.conj().T @ U - np.eye(2 * p.N)))
     assert res <= 1e-11 * scale, res
     assert orth <= 1e-12, orth
 

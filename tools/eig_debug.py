@@ -1,6 +1,6 @@
 """One own-solver eigendecomposition of a disordered H_BdG at L x L with the
-per-phase timing of DWHMC_EIG_DEBUG=1 (stderr), then the residual and
-orthogonality on the device.  Usage: python tools/eig_debug.py L [chains]."""
+per-phase timing of DWHMC_EIG_DEBUG=1 (stderr), then the eigenvalue symmetry and
+orthogonality (numpy).  Usage: python tools/eig_debug.py L [chains]."""
 import os
 import sys
 import time
@@ -24,9 +24,7 @@ def main():
     t0 = time.perf_counter()
     E, U = ctx.eigensystem(0)
     print(f"L={L} n={2 * p.N} eigensystem {1e3 * (time.perf_counter() - t0):.1f} ms", flush=True)
-    import torch
-    Ug = torch.from_numpy(np.ascontiguousarray(U)).to("cuda:0")
-    orth = (Ug.conj().T @ Ug - torch.eye(2 * p.N, dtype=Ug.dtype, device=Ug.device)).abs().max().item()
+    orth = np.max(np.abs(U.conj().T @ U - np.eye(2 * p.N)))
     print(f"L={L} max|E|={np.max(np.abs(E)):.3f} |E+E[::-1]|={np.max(np.abs(E + E[::-1])):.2e} orth={orth:.2e}",
           flush=True)
     ctx.close()
