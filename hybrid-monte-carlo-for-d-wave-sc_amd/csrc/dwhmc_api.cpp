@@ -689,6 +689,7 @@ struct dwh_ctx {
   double2* d_eig_colfin = nullptr;   // column i with its pending pairs (k_eig_reduce)
   int* d_eig_c0 = nullptr;         // particle-hole half solve: first computed eigenvector per matrix
   bool eig_half = false;           // the last own solve ran the particle-hole half solve
+  std::vector<int> eig_c0h;        // its c0 per matrix (N: no zero crowding)
   // the last eigen_solve's U of every slot is closed under the particle-hole
   // map column by column (half solve, c0 = N everywhere, no fallback):
   // transport's pair sums then run over half the pairs
@@ -1943,18 +1944,38 @@ int own_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m) {
   if (const char* e = std::getenv("DWHMC_EIG_MAX_CLUSTER")) maxc = std::max(1, std::min(maxc, std::atoi(e)));
   // Particle-hole half solve (H_BdG: E <-> -E with eigenvectors (u; v) <->
   // (-v*; u*)): eigenvectors of T only for the indices from
-  // c0 — n/2, or the start of an eigenvalue cluster that straddles zero (exact
-  // zero modes of clean lattices), which is then solved whole — on the columns
-  // [j0, n), j0 = n/2 - kEigMaxCluster; the columns below c0 are the partners
-  // of the columns above n - c0 (k_eig_theta after the back-transform).
-  // Inverse iteration, the orthogonalisation and the back-transform run on
-  // ~half the columns.  DWHMC_EIG_HALF=0: every column (A/B).
+  // c0, the largest index <= n/2 below which the spectrum has a gap wider
+  // than kEigZeroTol ||T|| (n/2 unless levels crowd around zero, e.g. the
+  // exact zero modes of clean lattices, which are then computed whole); the
+  // columns below c0 are the partners of the columns above n - c0
+  // (k_eig_theta after the back-transform).  c0 comes from the eigenvalues
+  // on the host (one synchronisation); every matrix computes the columns
+  // [j0, n), j0 = min c0, the ones below its own c0 zeroed.  Inverse
+  // iteration, the orthogonalisation and the back-transform run on ~half the
+  // columns.  DWHMC_EIG_HALF=0: every column (A/B).
   const char* eh = std::getenv("DWHMC_EIG_HALF");
   const bool half = n % 2 == 0 && !(eh && *eh == '0');
   ctx->eig_half = half;
-  const int j0 = half ? std::max(0, N - dwh::kEigMaxCluster) : 0;
+  ctx->eig_c0h.assign(half ? m : 0, N);
+  int j0 = 0;
+  if (half) {
+    std::vector<double> Eh((size_t)m * n), tn(m);
+    HIPCHECK(ctx, hipMemcpyAsync(Eh.data(), b.E, Eh.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPCHECK(ctx, hipMemcpyAsync(tn.data(), ctx->d_eig_tn, m * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPCHECK(ctx, hipStreamSynchronize(s));
+    j0 = N;
+    for (int k = 0; k < m; ++k) {
+      const double* E = Eh.data() + (size_t)k * n;
+      const double tol = dwh::kEigZeroTol * tn[k];
+      int c = N;
+      while (c > 0 && !(E[c] - E[c - 1] > tol)) --c;   // (NaN gaps: keep going, c -> 0)
+      ctx->eig_c0h[k] = c;
+      j0 = std::min(j0, c);
+    }
+    HIPCHECK(ctx, hipMemcpyAsync(ctx->d_eig_c0, ctx->eig_c0h.data(), m * sizeof(int), hipMemcpyHostToDevice, s));
+    ph.mark("c0");
+  }
   const int M = n - j0;   // eigenvector columns computed
-  if (half) dwh::launch_eig_c0(b.E, ctx->d_eig_tn, n, maxc, ctx->d_eig_c0, ctx->d_tr_bad, m, s);
   dwh::launch_eig_invit(ctx->d_eig_d, ctx->d_eig_e, n, b.E, ctx->d_eig_tn, Zt, Zt + sA, Ud, Ud + sA, sZ,
                         ctx->d_tr_bad, m, s, maxc, j0, half ? ctx->d_eig_c0 : nullptr);
   ph.mark("invit+orth");
@@ -2049,13 +2070,10 @@ int eigen_solve(dwh_ctx* ctx, const TrSrc& src, int m) {
   const bool own = !evd && n2 <= dwh::kEigMaxN;   // the own solver ran (see above)
   dwh::launch_nonfinite(ctx->tr.U, m * n2 * n2, ctx->tr.E, m * n2, ctx->d_tr_bad, ctx->stream);
   int bad = 0;
-  std::vector<int> c0(own && ctx->eig_half ? m : 0);
   HIPCHECK(ctx, hipMemcpyAsync(&bad, ctx->d_tr_bad, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-  if (!c0.empty())
-    HIPCHECK(ctx, hipMemcpyAsync(c0.data(), ctx->d_eig_c0, m * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
   HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
-  if (!bad && !c0.empty())
-    ctx->eig_ph = std::all_of(c0.begin(), c0.end(), [&](int c) { return c == ctx->d.N; });
+  if (!bad && own && ctx->eig_half && (int)ctx->eig_c0h.size() == m)
+    ctx->eig_ph = std::all_of(ctx->eig_c0h.begin(), ctx->eig_c0h.end(), [&](int c) { return c == ctx->d.N; });
   if (bad) {
     Scope sc(ctx, T_EIG_VENDOR, m);
     rc = eigen_enqueue(ctx, src, m, true);

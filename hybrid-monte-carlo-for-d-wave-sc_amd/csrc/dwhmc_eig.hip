@@ -33,8 +33,9 @@
 //     Then one symmetric orthogonalisation step over all vectors (the
 //     library's real products, dwhmc_gemm.hip, driven by dwhmc_api.cpp).
 //     For H_BdG (the only matrices the library decomposes) steps 3-4 run on
-//     the upper half of the spectrum only: k_eig_c0 finds c0 (n/2, or the
-//     start of a cluster straddling zero, solved whole), and k_eig_theta
+//     the upper half of the spectrum only: from c0 (n/2, or lower when the
+//     levels around zero are closer than kEigZeroTol, found on the host from
+//     the eigenvalues), and k_eig_theta
 //     fills the columns below c0 with the particle-hole partners
 //     (u; v) -> (-conj v; conj u) of the columns above n - c0.
 //  4. U = H_0 H_1 ... H_{n-2} Z: reflectors in blocks of kEigNB as
@@ -756,25 +757,6 @@ __global__ __launch_bounds__(256) void k_eig_zt_to_u(const double* __restrict__ 
   }
 }
 
-// c0 of the particle-hole half solve (launch_eig_c0), one thread per matrix
-__global__ void k_eig_c0(const double* __restrict__ E, const double* __restrict__ tnorm, int n, double ctol, int maxc,
-                         int* __restrict__ c0, int* __restrict__ bad, int m) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= m) return;
-  E += (int64_t)k * n;
-  const double tol = ctol * tnorm[k];
-  const int h = n / 2;
-  int c = h;
-  while (c > 0 && E[c] - E[c - 1] <= tol) {
-    --c;
-    if (h - c >= maxc) {   // beyond the computed range [n/2 - maxc, n): vendor fallback
-      *bad = 1;
-      break;
-    }
-  }
-  c0[k] = c;
-}
-
 // U[:, j] = Θ U[:, n-1-j] for j < c0[k]: Θ (u; v) = (-conj v; conj u), one
 // thread per row
 __global__ __launch_bounds__(256) void k_eig_theta(double2* __restrict__ U, int n, int64_t sA,
@@ -954,11 +936,6 @@ void launch_eig_invit(const double* d, const double* e, int n, const double* E, 
                      Zt, U0, U1, U2, sZ, j0, c0);
   hipLaunchKernelGGL(k_eig_orth, dim3(nj, m), dim3(256), 0, s, E, tnorm, n, Zt, sZ, kEigClusterTol, bad,
                      maxc < 1 || maxc > kEigMaxCluster ? kEigMaxCluster : maxc, j0, c0);
-}
-
-void launch_eig_c0(const double* E, const double* tnorm, int n, int maxc, int* c0, int* bad, int m, hipStream_t s) {
-  hipLaunchKernelGGL(k_eig_c0, dim3((m + 63) / 64), dim3(64), 0, s, E, tnorm, n, kEigClusterTol,
-                     maxc < 1 || maxc > kEigMaxCluster ? kEigMaxCluster : maxc, c0, bad, m);
 }
 
 void launch_eig_theta(double2* U, int n, int64_t sA, const int* c0, int m, hipStream_t s) {

@@ -246,7 +246,16 @@ void launch_nonfinite(const double2* U, int64_t nu, const double* E, int64_t ne,
 constexpr int kEigTB = 64;                  // trailing-update tile (one workgroup; hemv partial slots)
 constexpr int kEigNB = 64;                  // reflectors per back-transform block
 constexpr int kEigMaxN = 5120;              // rows k_eig_step holds in registers
-constexpr double kEigClusterTol = 2.5e-4;   // eigenvalue gap / ||T|| below which vectors are orthogonalised
+// eigenvalue gap / ||T|| below which inverse-iteration vectors are
+// orthonormalised together (Cholesky QR); wider gaps leave overlaps <= ~eps /
+// 1e-6 that the symmetric orthogonalisation step squares away.  (2.5e-4 in
+// round 3 made runs of >64 "clustered" levels from n ~ 3000 on, and with them
+// the rocSOLVER fallback.)
+constexpr double kEigClusterTol = 1e-6;
+// the particle-hole half solve computes the partners' vectors itself unless
+// the gap below c0 exceeds this (the partner images are not orthogonalised
+// against the computed vectors: their overlap is ~eps ||T|| / gap)
+constexpr double kEigZeroTol = 2.5e-4;
 constexpr int kEigMaxCluster = 64;          // longest such run (else *bad: vendor fallback)
 // deferral of the tridiagonalisation's rank-2 pairs (dwhmc_eig.hip): batches
 // of kEigDeferMin+ matrices apply them every kEigDefer-th pass (at most
@@ -275,10 +284,6 @@ void launch_eig_bisect(const double* d, const double* e, int n, double* E, doubl
 void launch_eig_invit(const double* d, const double* e, int n, const double* E, const double* tnorm, double* Zt,
                       double* U0, double* U1, double* U2, int64_t sZ, int* bad, int m, hipStream_t s,
                       int maxc = kEigMaxCluster, int j0 = 0, const int* c0 = nullptr);
-// particle-hole half solve (BdG matrices, n even): c0[k] = the first index of
-// the eigenvalue cluster that contains n/2 when it straddles zero, else n/2;
-// *bad when that cluster reaches more than maxc below n/2
-void launch_eig_c0(const double* E, const double* tnorm, int n, int maxc, int* c0, int* bad, int m, hipStream_t s);
 // columns j < c0[k] of U = the particle-hole partners of columns n-1-j:
 // (u; v) -> (-conj v; conj u)
 void launch_eig_theta(double2* U, int n, int64_t sA, const int* c0, int m, hipStream_t s);

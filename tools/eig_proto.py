@@ -235,7 +235,7 @@ def start_vector(m, n):
     return out
 
 
-def inverse_iteration(d, e, lam, tnorm, cluster_tol=2.5e-4, iters=3):
+def inverse_iteration(d, e, lam, tnorm, cluster_tol=1e-6, iters=3):
     """Independent inverse iteration per eigenvalue, Cholesky QR (twice) on
     every cluster (consecutive gaps <= cluster_tol ||T||), then one symmetric
     orthogonalisation step Z <- Z (3/2 I - 1/2 Z^T Z) over all vectors."""
@@ -286,18 +286,15 @@ def back_transform(V, tau, Z, nb=8):
     return U
 
 
-def zero_cluster_start(lam, tnorm, cluster_tol=2.5e-4, maxc=64):
-    """First index c0 <= n/2 of the eigenvalue cluster that contains index
-    n/2 (the smallest of the upper half) when that cluster straddles zero, else
-    n/2; None when it is longer than maxc back (the caller falls back)."""
-    n = len(lam)
-    h = n // 2
-    c0 = h
-    while c0 > 0 and lam[c0] - lam[c0 - 1] <= cluster_tol * tnorm:
-        c0 -= 1
-        if h - c0 > maxc:
-            return None
-    return c0
+def zero_cluster_start(lam, tnorm, zero_tol=2.5e-4):
+    """c0 of the particle-hole half solve: the largest index c <= n/2 with
+    lam[c] - lam[c-1] > zero_tol ||T|| (0 if none): n/2 unless levels crowd
+    around zero (then their vectors are computed, not taken as partners)."""
+    h = len(lam) // 2
+    c = h
+    while c > 0 and not (lam[c] - lam[c - 1] > zero_tol * tnorm):
+        c -= 1
+    return c
 
 
 def theta_partner(U, j_src):
@@ -309,7 +306,7 @@ def theta_partner(U, j_src):
     return np.concatenate([-np.conj(v), np.conj(u)])
 
 
-def inverse_iteration_range(d, e, lam, tnorm, j0, cluster_tol=2.5e-4, iters=3):
+def inverse_iteration_range(d, e, lam, tnorm, j0, cluster_tol=1e-6, iters=3):
     """inverse_iteration for the eigenvalue indices [j0, n) only (vectors of T
     in Z[:, j0:]); clusters inside the range, then one symmetric
     orthogonalisation step over those columns."""
@@ -349,7 +346,7 @@ def eigh_bdg(A: np.ndarray):
     d, e, V, tau = tridiagonalize(A)
     lam, tnorm = bisect_all(d, e)
     c0 = zero_cluster_start(lam, tnorm)
-    if c0 is None or n % 2:
+    if n % 2:
         Z = inverse_iteration(d, e, lam, tnorm)
         return lam, back_transform(V, tau, Z)
     Zr = inverse_iteration_range(d, e, lam, tnorm, c0)
