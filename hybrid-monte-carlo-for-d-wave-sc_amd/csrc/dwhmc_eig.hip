@@ -150,13 +150,18 @@ __global__ __launch_bounds__(256) void k_eig_reduce(const double2* __restrict__ 
 // 'L'), pair i-1 applied to column i (colfin, or A for i = 0), the reflector
 // of column i (zlarfg) into v_i and column i of A.  Every load is issued up
 // front; two workgroup reductions are its only barriers.
-template <int kMaxR>   // row slots per thread: ceil(n / kStepT)
+// DIRECT (K = 1: no pending pairs to correct): the step sums the pass
+// partials of its rows and of row i itself, 4 tile rows per round for all of
+// them at once (ascending tile index, k_eig_reduce's order), and reads column
+// i from A: one launch less per column for one matrix.
+template <int kMaxR, bool DIRECT>   // row slots per thread: ceil(n / kStepT)
 __global__ __launch_bounds__(kStepT) void k_eig_step(double2* __restrict__ A, int n, int i, int64_t sA,
                                                      const double2* __restrict__ pfin,
                                                      const double2* __restrict__ colfin,
                                                      double2* __restrict__ vv, double2* __restrict__ ww,
                                                      double* __restrict__ d, double* __restrict__ e,
-                                                     double2* __restrict__ tau) {
+                                                     double2* __restrict__ tau, const double2* __restrict__ part,
+                                                     int64_t sP) {
   const int k = blockIdx.x, tid = threadIdx.x;
   A += k * sA;
   pfin += (int64_t)k * n;
@@ -166,6 +171,7 @@ __global__ __launch_bounds__(kStepT) void k_eig_step(double2* __restrict__ A, in
   d += (int64_t)k * n;
   e += (int64_t)k * n;
   tau += (int64_t)k * n;
+  part += k * sP;
   __shared__ double2 sh1[kStepT / 64];
   __shared__ double sh2[kStepT / 64];
   __shared__ double2 bc;
@@ -178,16 +184,42 @@ __global__ __launch_bounds__(kStepT) void k_eig_step(double2* __restrict__ A, in
     const int r = i + tid + s * kStepT;
     cr[s] = vp[s] = wr[s] = cz();
     if (r < n) {
-      cr[s] = i > 0 ? colfin[r] : A[r];
+      cr[s] = i > 0 && !DIRECT ? colfin[r] : A[r + (int64_t)i * n];
       if (i > 0) {
         vp[s] = vprv[r];
-        wr[s] = pfin[r];
+        if (!DIRECT) wr[s] = pfin[r];
       }
+    }
+  }
+  double2 pi = cz();   // p[i] (v_{i-1}[i] = 1: w[i] = x[i] + alpha)
+  if (i > 0) {
+    if (DIRECT) {
+      const int t0 = i / kEigTB, T = (n + kEigTB - 1) / kEigTB;
+      for (int Y0 = t0; Y0 < T; Y0 += 4) {
+        double2 q[kMaxR + 1][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const bool yok = Y0 + u < T;
+#pragma unroll
+          for (int s = 0; s < kMaxR; ++s) {
+            const int r = i + tid + s * kStepT;
+            q[s][u] = (yok && r < n) ? part[(int64_t)(Y0 + u) * n + r] : cz();
+          }
+          q[kMaxR][u] = yok ? part[(int64_t)(Y0 + u) * n + i] : cz();
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+#pragma unroll
+          for (int s = 0; s < kMaxR; ++s) wr[s] = cadd(wr[s], q[s][u]);
+          pi = cadd(pi, q[kMaxR][u]);
+        }
+      }
+    } else {
+      pi = pfin[i];
     }
   }
   double2 wi = cz();
   if (i > 0) {
-    const double2 pi = pfin[i];   // p[i] (v_{i-1}[i] = 1: w[i] = x[i] + alpha)
     const double2 tp = tau[i - 1];
     double2 g = cz();
 #pragma unroll
@@ -261,6 +293,7 @@ __device__ __forceinline__ void tri_decode(int b, int& R, int& C) {
 // tile and writes it back; every pass accumulates the tile's share of A v_i
 // into fixed partial slots, and a read pass's diagonal tiles the dots of the
 // pending pairs with v_i.
+template <int KM>   // most pending pairs: 1 (K = 1) or kEigDeferMax
 __global__ __launch_bounds__(256) void k_eig_pass(double2* __restrict__ A, int n, int i, int64_t sA,
                                                   double2* __restrict__ part, int64_t sP,
                                                   const double2* __restrict__ vv, const double2* __restrict__ ww,
@@ -272,19 +305,20 @@ __global__ __launch_bounds__(256) void k_eig_pass(double2* __restrict__ A, int n
   ww += (int64_t)k * kEigRing * n;
   const double2* v = vv + (int64_t)(i % kEigRing) * n;
   const bool wp = eig_write_pass(i, K);
-  const int f = eig_pend_first(i, K), np = i - f;   // pending pairs f .. i-1
+  const int f = eig_pend_first(i, K), np = i - f;   // pending pairs f .. i-1 (<= KM)
   int R, C;
   tri_decode(blockIdx.x, R, C);
   R += t0;
   C += t0;
   __shared__ double2 cv[64], csum[64];
   __shared__ double2 rowp[4][64];
-  // the pending pairs' column values (write pass), then the column-sum
-  // transpose: one LDS region, the two phases split by a barrier
-  __shared__ double2 lds[64 * 65];
+  // the pending pairs' column values (write pass) and the column-sum
+  // transpose; for KM > 2 one LDS region, the two phases split by a barrier
+  constexpr bool kAlias = KM > 2;
+  __shared__ double2 lds[64 * 65 + (kAlias ? 0 : 2 * KM * 64)];
   double2(*colc)[65] = reinterpret_cast<double2(*)[65]>(lds);
-  double2* cpv = lds;            // [KD][64]: v_j of the tile's columns
-  double2* cpw = lds + KD * 64;  // [KD][64]: w_j
+  double2* cpv = kAlias ? lds : lds + 64 * 65;   // [KM][64]: v_j of the tile's columns
+  double2* cpw = cpv + KM * 64;                  // [KM][64]: w_j
   const int gr = R * kEigTB + lane;
   const bool rok = gr >= i + 1 && gr < n;
   if (tid < 64) {
@@ -300,6 +334,17 @@ __global__ __launch_bounds__(256) void k_eig_pass(double2* __restrict__ A, int n
     }
   }
   const double2 vr = rok ? v[gr] : cz();
+  // the pending pairs at this lane's row: the write pass's update, or a read
+  // pass's dots (diagonal tiles), loaded with the tile
+  const bool rowpairs = wp || R == C;
+  double2 rv[KM], rw[KM];
+#pragma unroll
+  for (int q = 0; q < KM; ++q) {
+    const int sl = (f + q) % kEigRing;
+    const bool ok = rowpairs && rok && q < np;
+    rv[q] = ok ? vv[(int64_t)sl * n + gr] : cz();
+    rw[q] = ok ? ww[(int64_t)sl * n + gr] : cz();
+  }
   constexpr int NCW = kEigTB / 4;   // columns per wave
   double2 a[NCW];
   unsigned act = 0;
@@ -312,26 +357,19 @@ __global__ __launch_bounds__(256) void k_eig_pass(double2* __restrict__ A, int n
   }
   __syncthreads();
   if (wp && np > 0) {
-    double2 rv[KD], rw[KD];
-#pragma unroll
-    for (int q = 0; q < KD; ++q) {
-      const int sl = (f + q) % kEigRing;
-      rv[q] = rok && q < np ? vv[(int64_t)sl * n + gr] : cz();
-      rw[q] = rok && q < np ? ww[(int64_t)sl * n + gr] : cz();
-    }
 #pragma unroll
     for (int u = 0; u < NCW; ++u) {
       const int cc = w + 4 * u, gc = C * kEigTB + cc;
       if ((act >> u) & 1) {
         double2 x = a[u];
 #pragma unroll
-        for (int q = 0; q < KD; ++q)
+        for (int q = 0; q < KM; ++q)
           if (q < np) x = csub(csub(x, cmulc(rv[q], cpw[q * 64 + cc])), cmulc(rw[q], cpv[q * 64 + cc]));
         a[u] = x;
         A[gr + (int64_t)gc * n] = x;
       }
     }
-    __syncthreads();   // the pair values are dead: the region becomes colc
+    if (kAlias) __syncthreads();   // the pair values are dead: the region becomes colc
   }
   double2 pr = cz();
 #pragma unroll
@@ -347,11 +385,11 @@ __global__ __launch_bounds__(256) void k_eig_pass(double2* __restrict__ A, int n
   rowp[w][lane] = pr;
   if (!wp && np > 0 && R == C && w == 0) {
     // dots of the pending pairs with v_i over this tile's rows
-    for (int q = 0; q < np; ++q) {
-      const int sl = (f + q) % kEigRing;
-      const double2 vj = rok ? vv[(int64_t)sl * n + gr] : cz(), wj = rok ? ww[(int64_t)sl * n + gr] : cz();
-      double2 dw = make_double2(wj.x * vr.x + wj.y * vr.y, wj.x * vr.y - wj.y * vr.x);
-      double2 dv = make_double2(vj.x * vr.x + vj.y * vr.y, vj.x * vr.y - vj.y * vr.x);
+#pragma unroll
+    for (int q = 0; q < KM; ++q) {
+      if (q >= np) break;
+      double2 dw = make_double2(rw[q].x * vr.x + rw[q].y * vr.y, rw[q].x * vr.y - rw[q].y * vr.x);
+      double2 dv = make_double2(rv[q].x * vr.x + rv[q].y * vr.y, rv[q].x * vr.y - rv[q].y * vr.x);
       dw.x = wave_sum(dw.x);
       dw.y = wave_sum(dw.y);
       dv.x = wave_sum(dv.x);
@@ -897,20 +935,37 @@ void launch_eig_step(double2* A, int n, int i, int64_t sA, const double2* part, 
                      double2* colfin, double2* vv, double2* ww, double* d, double* e, double2* tau,
                      const double2* dpart, int m, hipStream_t s) {
   const int K = eig_defer_k(m);
-  if (i > 0)
+  // K = 1: the step sums the partials itself (DWHMC_EIG_REDUCE=1: the
+  // separate k_eig_reduce launch anyway, A/B)
+  const char* er = std::getenv("DWHMC_EIG_REDUCE");
+  const int rs = (n - i + kStepT - 1) / kStepT;   // row slots the rows i..n-1 need
+  // (from 4 row slots the direct step's prefetch spills: the reduce launch)
+  const bool direct = K == 1 && rs <= 3 && !(er && *er == '1');
+  if (i > 0 && !direct)
     hipLaunchKernelGGL(k_eig_reduce, dim3((n - i + 255) / 256, m), dim3(256), 0, s, part, sP, n, i, pfin, A, sA,
                        colfin, vv, ww, dpart, K);
-  const int rs = (n - i + kStepT - 1) / kStepT;   // row slots the rows i..n-1 need
   static_assert(kEigMaxN <= 5 * kStepT, "k_eig_step instantiations");
-#define DWH_EIG_STEP(R) \
-  hipLaunchKernelGGL((k_eig_step<R>), dim3(m), dim3(kStepT), 0, s, A, n, i, sA, pfin, colfin, vv, ww, d, e, tau)
-  switch (rs) {
-    case 1: DWH_EIG_STEP(1); break;
-    case 2: DWH_EIG_STEP(2); break;
-    case 3: DWH_EIG_STEP(3); break;
-    case 4: DWH_EIG_STEP(4); break;
-    default: DWH_EIG_STEP(5); break;
+#define DWH_EIG_STEP(R, D)                                                                                        \
+  hipLaunchKernelGGL((k_eig_step<R, D>), dim3(m), dim3(kStepT), 0, s, A, n, i, sA, pfin, colfin, vv, ww, d, e, tau, \
+                     part, sP)
+#define DWH_EIG_STEPS(D)               \
+  switch (rs) {                        \
+    case 1: DWH_EIG_STEP(1, D); break; \
+    case 2: DWH_EIG_STEP(2, D); break; \
+    case 3: DWH_EIG_STEP(3, D); break; \
+    case 4: DWH_EIG_STEP(4, D); break; \
+    default: DWH_EIG_STEP(5, D); break; \
   }
+  if (direct) {
+    switch (rs) {
+      case 1: DWH_EIG_STEP(1, true); break;
+      case 2: DWH_EIG_STEP(2, true); break;
+      default: DWH_EIG_STEP(3, true); break;
+    }
+  } else {
+    DWH_EIG_STEPS(false)
+  }
+#undef DWH_EIG_STEPS
 #undef DWH_EIG_STEP
 }
 
@@ -918,8 +973,13 @@ void launch_eig_pass(double2* A, int n, int i, int64_t sA, double2* part, int64_
                      const double2* ww, double2* dpart, int m, hipStream_t s) {
   const int T = (n + kEigTB - 1) / kEigTB, t0 = (i + 1) / kEigTB, nT = T - t0;
   if (nT <= 0) return;
-  hipLaunchKernelGGL(k_eig_pass, dim3(nT * (nT + 1) / 2, m), dim3(256), 0, s, A, n, i, sA, part, sP, vv, ww, t0,
-                     dpart, T, eig_defer_k(m));
+  const int K = eig_defer_k(m);
+  if (K == 1)
+    hipLaunchKernelGGL(k_eig_pass<1>, dim3(nT * (nT + 1) / 2, m), dim3(256), 0, s, A, n, i, sA, part, sP, vv, ww, t0,
+                       dpart, T, K);
+  else
+    hipLaunchKernelGGL(k_eig_pass<KD>, dim3(nT * (nT + 1) / 2, m), dim3(256), 0, s, A, n, i, sA, part, sP, vv, ww,
+                       t0, dpart, T, K);
 }
 
 void launch_eig_bisect(const double* d, const double* e, int n, double* E, double* tnorm, int m, hipStream_t s) {
