@@ -150,18 +150,14 @@ __global__ __launch_bounds__(256) void k_eig_reduce(const double2* __restrict__ 
 // 'L'), pair i-1 applied to column i (colfin, or A for i = 0), the reflector
 // of column i (zlarfg) into v_i and column i of A.  Every load is issued up
 // front; two workgroup reductions are its only barriers.
-// DIRECT (K = 1: no pending pairs to correct): the step sums the pass
-// partials of its rows and of row i itself, 4 tile rows per round for all of
-// them at once (ascending tile index, k_eig_reduce's order), and reads column
-// i from A: one launch less per column for one matrix.
-template <int kMaxR, bool DIRECT>   // row slots per thread: ceil(n / kStepT)
+// Step i: see k_eig_reduce; every load is issued up front.
+template <int kMaxR>   // row slots per thread: ceil(n / kStepT)
 __global__ __launch_bounds__(kStepT) void k_eig_step(double2* __restrict__ A, int n, int i, int64_t sA,
                                                      const double2* __restrict__ pfin,
                                                      const double2* __restrict__ colfin,
                                                      double2* __restrict__ vv, double2* __restrict__ ww,
                                                      double* __restrict__ d, double* __restrict__ e,
-                                                     double2* __restrict__ tau, const double2* __restrict__ part,
-                                                     int64_t sP) {
+                                                     double2* __restrict__ tau) {
   const int k = blockIdx.x, tid = threadIdx.x;
   A += k * sA;
   pfin += (int64_t)k * n;
@@ -171,7 +167,6 @@ __global__ __launch_bounds__(kStepT) void k_eig_step(double2* __restrict__ A, in
   d += (int64_t)k * n;
   e += (int64_t)k * n;
   tau += (int64_t)k * n;
-  part += k * sP;
   __shared__ double2 sh1[kStepT / 64];
   __shared__ double sh2[kStepT / 64];
   __shared__ double2 bc;
@@ -184,40 +179,14 @@ __global__ __launch_bounds__(kStepT) void k_eig_step(double2* __restrict__ A, in
     const int r = i + tid + s * kStepT;
     cr[s] = vp[s] = wr[s] = cz();
     if (r < n) {
-      cr[s] = i > 0 && !DIRECT ? colfin[r] : A[r + (int64_t)i * n];
+      cr[s] = i > 0 ? colfin[r] : A[r];
       if (i > 0) {
         vp[s] = vprv[r];
-        if (!DIRECT) wr[s] = pfin[r];
+        wr[s] = pfin[r];
       }
     }
   }
-  double2 pi = cz();   // p[i] (v_{i-1}[i] = 1: w[i] = x[i] + alpha)
-  if (i > 0) {
-    if (DIRECT) {
-      const int t0 = i / kEigTB, T = (n + kEigTB - 1) / kEigTB;
-      for (int Y0 = t0; Y0 < T; Y0 += 4) {
-        double2 q[kMaxR + 1][4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const bool yok = Y0 + u < T;
-#pragma unroll
-          for (int s = 0; s < kMaxR; ++s) {
-            const int r = i + tid + s * kStepT;
-            q[s][u] = (yok && r < n) ? part[(int64_t)(Y0 + u) * n + r] : cz();
-          }
-          q[kMaxR][u] = yok ? part[(int64_t)(Y0 + u) * n + i] : cz();
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-#pragma unroll
-          for (int s = 0; s < kMaxR; ++s) wr[s] = cadd(wr[s], q[s][u]);
-          pi = cadd(pi, q[kMaxR][u]);
-        }
-      }
-    } else {
-      pi = pfin[i];
-    }
-  }
+  const double2 pi = i > 0 ? pfin[i] : cz();   // p[i] (v_{i-1}[i] = 1: w[i] = x[i] + alpha)
   double2 wi = cz();
   if (i > 0) {
     const double2 tp = tau[i - 1];
@@ -934,38 +903,20 @@ int eig_defer_k(int m) {
 void launch_eig_step(double2* A, int n, int i, int64_t sA, const double2* part, int64_t sP, double2* pfin,
                      double2* colfin, double2* vv, double2* ww, double* d, double* e, double2* tau,
                      const double2* dpart, int m, hipStream_t s) {
-  const int K = eig_defer_k(m);
-  // K = 1: the step sums the partials itself (DWHMC_EIG_REDUCE=1: the
-  // separate k_eig_reduce launch anyway, A/B)
-  const char* er = std::getenv("DWHMC_EIG_REDUCE");
-  const int rs = (n - i + kStepT - 1) / kStepT;   // row slots the rows i..n-1 need
-  // (from 4 row slots the direct step's prefetch spills: the reduce launch)
-  const bool direct = K == 1 && rs <= 3 && !(er && *er == '1');
-  if (i > 0 && !direct)
+  if (i > 0)
     hipLaunchKernelGGL(k_eig_reduce, dim3((n - i + 255) / 256, m), dim3(256), 0, s, part, sP, n, i, pfin, A, sA,
-                       colfin, vv, ww, dpart, K);
+                       colfin, vv, ww, dpart, eig_defer_k(m));
+  const int rs = (n - i + kStepT - 1) / kStepT;   // row slots the rows i..n-1 need
   static_assert(kEigMaxN <= 5 * kStepT, "k_eig_step instantiations");
-#define DWH_EIG_STEP(R, D)                                                                                        \
-  hipLaunchKernelGGL((k_eig_step<R, D>), dim3(m), dim3(kStepT), 0, s, A, n, i, sA, pfin, colfin, vv, ww, d, e, tau, \
-                     part, sP)
-#define DWH_EIG_STEPS(D)               \
-  switch (rs) {                        \
-    case 1: DWH_EIG_STEP(1, D); break; \
-    case 2: DWH_EIG_STEP(2, D); break; \
-    case 3: DWH_EIG_STEP(3, D); break; \
-    case 4: DWH_EIG_STEP(4, D); break; \
-    default: DWH_EIG_STEP(5, D); break; \
+#define DWH_EIG_STEP(R) \
+  hipLaunchKernelGGL((k_eig_step<R>), dim3(m), dim3(kStepT), 0, s, A, n, i, sA, pfin, colfin, vv, ww, d, e, tau)
+  switch (rs) {
+    case 1: DWH_EIG_STEP(1); break;
+    case 2: DWH_EIG_STEP(2); break;
+    case 3: DWH_EIG_STEP(3); break;
+    case 4: DWH_EIG_STEP(4); break;
+    default: DWH_EIG_STEP(5); break;
   }
-  if (direct) {
-    switch (rs) {
-      case 1: DWH_EIG_STEP(1, true); break;
-      case 2: DWH_EIG_STEP(2, true); break;
-      default: DWH_EIG_STEP(3, true); break;
-    }
-  } else {
-    DWH_EIG_STEPS(false)
-  }
-#undef DWH_EIG_STEPS
 #undef DWH_EIG_STEP
 }
 
