@@ -653,12 +653,6 @@ struct dwh_ctx {
   // drifting k_cr_pair_force, consumed by the next factorisation); every
   // other path that changes Δ leaves it false
   bool pairing_in_pool = false;
-  // pole split (DWHMC_CR_SPLIT = S, one chain): the CR stages of poles
-  // [s P/S, (s+1) P/S) run on stream s (0: ctx->stream), forked after the fill
-  // and joined before the force, so the latency chains of the sub-batches overlap
-  int cr_split = 1;
-  std::vector<hipStream_t> cr_sub;   // streams 1 .. S-1
-  std::vector<hipEvent_t> cr_ev;     // fork + one join per sub-stream
   bool pending = false;    // dwh_hmc_trajectory done, dwh_hmc_finish not yet
   int async_rc = 0;        // eig path: a rocSOLVER / rocBLAS call refused while enqueuing
 
@@ -763,7 +757,7 @@ struct Scope {
   hipEvent_t a{};
   bool on;
   Scope(dwh_ctx* c, int n, double w)
-      : ctx(c), name(n), work(w), st(c->stream), on(n < T_COUNT && ((c->timing >> n) & 1) != 0) {
+      : ctx(c), name(n), work(w), st(c->stream), on(((c->timing >> n) & 1) != 0) {
     if (on) {
       a = take_event(ctx);
       (void)hipEventRecord(a, st);
@@ -882,53 +876,32 @@ void cr_enqueue(dwh_ctx* ctx) {
   }
   const CrPlan& plan = ctx->plan;
   // the site guard rides on the first (level-0) inversion launch: every
-  // factorised Δ passes through it (sub-batch 0 only: it checks the chain's sites)
+  // factorised Δ passes through it
   dwh::SiteGuard guard;
   if (ctx->site_guard) guard = dwh::SiteGuard{ctx->Delta, ctx->site4, 4.0 * ctx->delta_cap, ctx->flag};
-  const int S = ctx->cr_split;
-  dwh::CrDims cs = c;
-  cs.nbatch = c.nbatch / S;
-  const int nld = ctx->d.nld;
-  if (S > 1) {
-    (void)hipEventRecord(ctx->cr_ev[0], ctx->stream);
-    for (int q = 1; q < S; ++q) (void)hipStreamWaitEvent(ctx->cr_sub[q - 1], ctx->cr_ev[0], 0);
-  }
   for (size_t si = 0; si < plan.stages.size(); ++si) {
     const CrStage& st = plan.stages[si];
-    for (int q = 0; q < S; ++q) {
-      const hipStream_t strm = q == 0 ? ctx->stream : ctx->cr_sub[q - 1];
-      const int64_t b0 = (int64_t)q * cs.nbatch;
-      double2* pool = ctx->bpool + b0 * c.item;
-      double* ldp = ctx->ldpart + b0 * nld;
-      const double* lda = ctx->ldA ? ctx->ldA + b0 * c.Ly : nullptr;
-      const dwh::SiteGuard g = q == 0 ? guard : dwh::SiteGuard{};
-      // timers (ctx->stream) bracket sub-batch 0
-      const double wsc = 1.0 / S;
-      if (st.kind == 0 && st.ntiles > 0) {
-        Scope s(ctx, q == 0 ? T_CR_INVSIDE : T_COUNT, wsc * (st.n * bp3 + st.flops * c.nbatch));
-        dwh::launch_cr_inv_side(cs, pool, ctx->d_inv_blk + st.first, ctx->d_inv_dst + st.first,
-                                ctx->d_inv_slot + st.first, st.n, ldp, ctx->d_tasks + st.tfirst, st.ntiles,
-                                st.maxt32, strm, g);
-      } else if (st.kind == 0 && st.l0) {
-        Scope s(ctx, q == 0 ? T_CR_INV : T_COUNT, wsc * st.n * bp3);
-        dwh::launch_cr_inv0(cs, pool, ctx->d_inv_blk + st.first, ctx->d_inv0_r, ctx->d_inv_dst + st.first,
-                            ctx->d_inv_slot + st.first, st.n, ldp, lda, strm, g.Delta, g.site4, g.cap4, g.flag);
-      } else if (st.kind == 0) {
-        Scope s(ctx, q == 0 ? T_CR_INV : T_COUNT, wsc * st.n * bp3);
-        dwh::launch_cr_inv(cs, pool, ctx->d_inv_blk + st.first, ctx->d_inv_dst + st.first,
-                           ctx->d_inv_slot + st.first, st.n, ldp, strm, g);
-      } else {
-        Scope s(ctx, q == 0 ? T_CR_GEMM : T_COUNT, wsc * st.flops * c.nbatch);
-        dwh::launch_cr_gemm(cs, pool, ctx->d_tasks + st.first, st.n, st.maxt32, st.maxt16,
-                            ctx->d_tiles16 + st.tfirst, st.ntiles, st.cfg, st.sg, strm);
-      }
-    }
-    if (st.kind == 0) guard = dwh::SiteGuard{};
-  }
-  if (S > 1) {
-    for (int q = 1; q < S; ++q) {
-      (void)hipEventRecord(ctx->cr_ev[q], ctx->cr_sub[q - 1]);
-      (void)hipStreamWaitEvent(ctx->stream, ctx->cr_ev[q], 0);
+    if (st.kind == 0 && st.ntiles > 0) {
+      Scope s(ctx, T_CR_INVSIDE, st.n * bp3 + st.flops * c.nbatch);
+      dwh::launch_cr_inv_side(c, ctx->bpool, ctx->d_inv_blk + st.first, ctx->d_inv_dst + st.first,
+                              ctx->d_inv_slot + st.first, st.n, ctx->ldpart, ctx->d_tasks + st.tfirst,
+                              st.ntiles, st.maxt32, ctx->stream, guard);
+      guard = dwh::SiteGuard{};
+    } else if (st.kind == 0 && st.l0) {
+      Scope s(ctx, T_CR_INV, st.n * bp3);
+      dwh::launch_cr_inv0(c, ctx->bpool, ctx->d_inv_blk + st.first, ctx->d_inv0_r, ctx->d_inv_dst + st.first,
+                          ctx->d_inv_slot + st.first, st.n, ctx->ldpart, ctx->ldA, ctx->stream, guard.Delta,
+                          guard.site4, guard.cap4, guard.flag);
+      guard = dwh::SiteGuard{};
+    } else if (st.kind == 0) {
+      Scope s(ctx, T_CR_INV, st.n * bp3);
+      dwh::launch_cr_inv(c, ctx->bpool, ctx->d_inv_blk + st.first, ctx->d_inv_dst + st.first,
+                         ctx->d_inv_slot + st.first, st.n, ctx->ldpart, ctx->stream, guard);
+      guard = dwh::SiteGuard{};
+    } else {
+      Scope s(ctx, T_CR_GEMM, st.flops * c.nbatch);
+      dwh::launch_cr_gemm(c, ctx->bpool, ctx->d_tasks + st.first, st.n, st.maxt32, st.maxt16,
+                          ctx->d_tiles16 + st.tfirst, st.ntiles, st.cfg, st.sg, ctx->stream);
     }
   }
 }
@@ -1546,29 +1519,6 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
     ctx->err = "hipStreamCreate failed";
     return bail(DWH_ERR_HIP);
-  }
-  if (ctx->algo == ALGO_CR) {
-    const char* e = std::getenv("DWHMC_CR_SPLIT");
-    const int S = e ? std::atoi(e) : 1;
-    if (S > 1 && S <= 4 && d.nc == 1 && d.P % S == 0) {
-      ctx->cr_split = S;
-      for (int q = 1; q < S; ++q) {
-        hipStream_t st{};
-        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
-          ctx->err = "hipStreamCreate failed";
-          return bail(DWH_ERR_HIP);
-        }
-        ctx->cr_sub.push_back(st);
-      }
-      for (int q = 0; q < S; ++q) {
-        hipEvent_t ev{};
-        if (hipEventCreateWithFlags(&ev, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess) {
-          ctx->err = "hipEventCreate failed";
-          return bail(DWH_ERR_HIP);
-        }
-        ctx->cr_ev.push_back(ev);
-      }
-    }
   }
   const size_t nmat = (size_t)d.nbatch * d.mat;
   const size_t nbond = (size_t)d.nc * 2 * N;
@@ -2298,8 +2248,6 @@ void dwh_destroy(dwh_ctx* ctx) {
   for (auto e : ctx->pool) (void)hipEventDestroy(e);
   if (ctx->blas) (void)rocblas_destroy_handle(ctx->blas);
   for (void* p : ctx->allocations) (void)hipFree(p);
-  for (auto e : ctx->cr_ev) (void)hipEventDestroy(e);
-  for (auto q : ctx->cr_sub) (void)hipStreamDestroy(q);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }

@@ -828,37 +828,3 @@ def test_cr_two_row_blocks(dwhmc, oracle, monkeypatch, Lx, Ly):
         assert np.max(np.abs(ctx.get_state()[0][0] - D_r)) <= 1e-10
     ctx.close()
 
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("S", [2, 4])
-def test_cr_pole_split_streams_bitwise(dwhmc, oracle, monkeypatch, S):
-    """DWHMC_CR_SPLIT = S (one chain): the CR stages of each pole sub-batch on
-    their own stream, forked after the fill and joined before the force —
-    the same kernels on the same batch items, so P, F, E_f and a run of
-    throughput sweeps equal the single-stream context bit for bit."""
-    O = oracle
-    p, dis, Delta = make_case(O, 16, 16, 8.0, seed=1616, amp=0.1)
-    rng = np.random.default_rng(3)
-    sweeps = 2
-    noise = (rng.standard_normal((sweeps, 1, p.N, 2)) + 1j * rng.standard_normal((sweeps, 1, p.N, 2))) * math.sqrt(0.5)
-    uni = rng.random((sweeps, 1))
-    Nt = 4
-    dt = O.calc_optimal_dt(p.beta, p.J, p.mass, Nt)
-    out = []
-    for split in ("1", str(S)):
-        monkeypatch.setenv("DWHMC_CR_SPLIT", split)
-        ctx = device_ctx(dwhmc, p, dis, "cr")
-        if ctx.info["npoles"] % S:
-            ctx.close()
-            pytest.skip("pole count not divisible by S")
-        ctx.set_pairing(Delta)
-        ctx.factorize()
-        r = [ctx.pairing()[0], ctx.forces()[0], ctx.fermion_energy()[0], ctx.hole_trace()[0]]
-        ctx.load_draws(noise, uni)
-        ctx.run_sweeps(0, sweeps, Nt, dt, p.mass)
-        acc, dH = ctx.sweep_results(0, sweeps)
-        r += [acc, dH, ctx.get_state()[0][0]]
-        ctx.close()
-        out.append(r)
-    for a, b in zip(*out):
-        assert np.array_equal(np.asarray(a), np.asarray(b))
