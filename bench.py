@@ -46,7 +46,7 @@ METRIC = "fp64 leapfrog steps/sec at L=32, 1→8 MI355X; % fp64 MFMA roofline"
 PEAK_F64_TFLOPS = 78.6        # MI355X dense fp64 matrix peak (= fp64 vector peak on CDNA4)
 PEAK_HBM_GBS = 8000.0         # MI355X HBM3E peak (MI355X_MICROARCH.md)
 # newest committed PMC summary first (profiles/README.md)
-TRAFFIC_FILES = [os.path.join(ROOT, "profiles", f) for f in ("r03_pmc_traffic.json", "r02_pmc_traffic.json",
+TRAFFIC_FILES = [os.path.join(ROOT, "profiles", f) for f in ("r04_pmc_traffic.json", "r03_pmc_traffic.json", "r02_pmc_traffic.json",
                                                                      "r01_pmc_traffic.json")]
 # SQ counter passes (tools/pmc_sq.sh -> tools/pmc_mfma.py): executed MFMA work per launch
 MFMA_FILES = [os.path.join(ROOT, "profiles", f) for f in ("r04_sq_mfma_L32.json",)]
