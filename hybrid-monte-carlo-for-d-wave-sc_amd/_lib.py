@@ -125,7 +125,14 @@ def load_path(path: str) -> C.CDLL:
     if path not in _variants:
         lib = C.CDLL(path)
         for name, (res, args) in SIGNATURES.items():
-            fn = getattr(lib, name)
+            try:
+                fn = getattr(lib, name)
+            except AttributeError:
+                # an older build (A/B against an earlier round's library):
+                # the entry is missing there, and calling it says so
+                if path == os.path.abspath(_build.LIB):
+                    raise
+                continue
             fn.restype = res
             fn.argtypes = args
         _variants[path] = lib

@@ -262,7 +262,7 @@ __device__ __forceinline__ void tri_decode(int b, int& R, int& C) {
 // tile and writes it back; every pass accumulates the tile's share of A v_i
 // into fixed partial slots, and a read pass's diagonal tiles the dots of the
 // pending pairs with v_i.
-template <int KM>   // most pending pairs: 1 (K = 1) or kEigDeferMax
+template <int KM>   // most pending pairs (kEigDeferMax; K = 1 runs k_eig_pass1)
 __global__ __launch_bounds__(256) void k_eig_pass(double2* __restrict__ A, int n, int i, int64_t sA,
                                                   double2* __restrict__ part, int64_t sP,
                                                   const double2* __restrict__ vv, const double2* __restrict__ ww,
@@ -283,7 +283,7 @@ __global__ __launch_bounds__(256) void k_eig_pass(double2* __restrict__ A, int n
   __shared__ double2 rowp[4][64];
   // the pending pairs' column values (write pass) and the column-sum
   // transpose; for KM > 2 one LDS region, the two phases split by a barrier
-  constexpr bool kAlias = KM > 2;
+  constexpr bool kAlias = KM > 2;   // (KM <= 2: a separate region)
   __shared__ double2 lds[64 * 65 + (kAlias ? 0 : 2 * KM * 64)];
   double2(*colc)[65] = reinterpret_cast<double2(*)[65]>(lds);
   double2* cpv = kAlias ? lds : lds + 64 * 65;   // [KM][64]: v_j of the tile's columns
@@ -314,6 +314,7 @@ __global__ __launch_bounds__(256) void k_eig_pass(double2* __restrict__ A, int n
     rv[q] = ok ? vv[(int64_t)sl * n + gr] : cz();
     rw[q] = ok ? ww[(int64_t)sl * n + gr] : cz();
   }
+  __syncthreads();
   constexpr int NCW = kEigTB / 4;   // columns per wave
   double2 a[NCW];
   unsigned act = 0;
@@ -324,7 +325,6 @@ __global__ __launch_bounds__(256) void k_eig_pass(double2* __restrict__ A, int n
     act |= (unsigned)ok << u;
     a[u] = ok ? A[gr + (int64_t)gc * n] : cz();
   }
-  __syncthreads();
   if (wp && np > 0) {
 #pragma unroll
     for (int u = 0; u < NCW; ++u) {
@@ -369,6 +369,94 @@ __global__ __launch_bounds__(256) void k_eig_pass(double2* __restrict__ A, int n
       }
     }
   }
+  __syncthreads();
+  {
+    const int cc = tid >> 2, q = tid & 3;
+    double2 s = cz();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s = cadd(s, colc[cc][q * 16 + r]);
+    s.x += __shfl_xor(s.x, 1, 64);
+    s.y += __shfl_xor(s.y, 1, 64);
+    s.x += __shfl_xor(s.x, 2, 64);
+    s.y += __shfl_xor(s.y, 2, 64);
+    if (q == 0) csum[cc] = s;
+  }
+  __syncthreads();
+  if (tid < 64) {
+    const double2 rs = cadd(cadd(rowp[0][tid], rowp[1][tid]), cadd(rowp[2][tid], rowp[3][tid]));
+    const double2 cs = csum[tid];
+    const int r = R * kEigTB + tid, c = C * kEigTB + tid;
+    if (R == C) {
+      if (r < n) part[(int64_t)R * n + r] = cadd(rs, cs);
+    } else {
+      if (r < n) part[(int64_t)C * n + r] = rs;
+      if (c < n) part[(int64_t)R * n + c] = cs;
+    }
+  }
+}
+
+// K = 1 pass in one sweep over the tile (round-3 form: the pending pair i-1
+// applied, written back, and the hemv accumulated per column in one loop;
+// tile loads after the staging barrier)
+__global__ __launch_bounds__(256) void k_eig_pass1(double2* __restrict__ A, int n, int i, int64_t sA,
+                                                   double2* __restrict__ part, int64_t sP,
+                                                   const double2* __restrict__ vv, const double2* __restrict__ ww,
+                                                   int t0) {
+  const int k = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  A += k * sA;
+  part += k * sP;
+  vv += (int64_t)k * kEigRing * n;
+  ww += (int64_t)k * kEigRing * n;
+  const double2* v = vv + (int64_t)(i % kEigRing) * n;
+  const double2* va = vv + (int64_t)((i + kEigRing - 1) % kEigRing) * n;   // pair i-1
+  const double2* wa = ww + (int64_t)((i + kEigRing - 1) % kEigRing) * n;
+  const int np = i == 0 ? 0 : 1;
+  int R, C;
+  tri_decode(blockIdx.x, R, C);
+  R += t0;
+  C += t0;
+  __shared__ double2 cv[64], cva[64], cwa[64], csum[64];
+  __shared__ double2 colc[64][65];
+  __shared__ double2 rowp[4][64];
+  if (tid < 64) {
+    const int gc = C * kEigTB + tid;
+    const bool ok = gc >= i + 1 && gc < n;
+    cv[tid] = ok ? v[gc] : cz();
+    cva[tid] = ok && np ? va[gc] : cz();
+    cwa[tid] = ok && np ? wa[gc] : cz();
+  }
+  const int gr = R * kEigTB + lane;
+  const bool rok = gr >= i + 1 && gr < n;
+  const double2 vr = rok ? v[gr] : cz();
+  const double2 var = rok && np ? va[gr] : cz();
+  const double2 war = rok && np ? wa[gr] : cz();
+  __syncthreads();
+  double2 pr = cz();
+  constexpr int NCW = kEigTB / 4;   // columns per wave
+  double2 a[NCW];
+  unsigned act = 0;
+#pragma unroll
+  for (int u = 0; u < NCW; ++u) {
+    const int gc = C * kEigTB + w + 4 * u;
+    const bool ok = rok && gc >= i + 1 && gr >= gc;
+    act |= (unsigned)ok << u;
+    a[u] = ok ? A[gr + (int64_t)gc * n] : cz();
+  }
+#pragma unroll
+  for (int u = 0; u < NCW; ++u) {
+    const int cc = w + 4 * u, gc = C * kEigTB + cc;
+    double2 t = cz();
+    if ((act >> u) & 1) {
+      if (np) {
+        a[u] = csub(csub(a[u], cmulc(var, cwa[cc])), cmulc(war, cva[cc]));
+        A[gr + (int64_t)gc * n] = a[u];
+      }
+      pr = cadd(pr, cmul(a[u], cv[cc]));
+      if (gr > gc) t = make_double2(a[u].x * vr.x + a[u].y * vr.y, a[u].x * vr.y - a[u].y * vr.x);   // conj(a) v_r
+    }
+    colc[cc][lane] = t;
+  }
+  rowp[w][lane] = pr;
   __syncthreads();
   {
     const int cc = tid >> 2, q = tid & 3;
@@ -926,8 +1014,7 @@ void launch_eig_pass(double2* A, int n, int i, int64_t sA, double2* part, int64_
   if (nT <= 0) return;
   const int K = eig_defer_k(m);
   if (K == 1)
-    hipLaunchKernelGGL(k_eig_pass<1>, dim3(nT * (nT + 1) / 2, m), dim3(256), 0, s, A, n, i, sA, part, sP, vv, ww, t0,
-                       dpart, T, K);
+    hipLaunchKernelGGL(k_eig_pass1, dim3(nT * (nT + 1) / 2, m), dim3(256), 0, s, A, n, i, sA, part, sP, vv, ww, t0);
   else
     hipLaunchKernelGGL(k_eig_pass<KD>, dim3(nT * (nT + 1) / 2, m), dim3(256), 0, s, A, n, i, sA, part, sP, vv, ww,
                        t0, dpart, T, K);

@@ -45,8 +45,9 @@ def main():
     st = m.initialize_state(p, rng)
     N = p.N
     D = st.Delta + 0.25 * np.stack([np.ones(N), -np.ones(N)], 1)
+    lib = os.environ.get("DWHMC_LIB")   # another build of the library (A/B)
     ctx = m.FermionContext(p.Lx, p.Ly, p.t, p.tp, p.mu, p.beta, p.J, p.nn_table, p.nnn_table,
-                           st.disorder_pot)
+                           st.disorder_pot, lib_path=lib)
     ctx.set_pairing(D)
     ctx.measure_transport(p.eta, p.domega, p.omega_max)          # warmup (allocations, handle)
     t0 = time.perf_counter()
@@ -72,7 +73,7 @@ def main():
     # batched: --chains chains in one context, dwh_measure_transport_batched
     nc = a.chains
     ctxb = m.FermionContext(p.Lx, p.Ly, p.t, p.tp, p.mu, p.beta, p.J, p.nn_table, p.nnn_table,
-                            np.stack([st.disorder_pot] * nc))
+                            np.stack([st.disorder_pot] * nc), lib_path=lib)
     ctxb.set_pairing(np.stack([D] * nc))
     ctxb.measure_transport_all(p.eta, p.domega, p.omega_max)
     t0 = time.perf_counter()

@@ -18,7 +18,9 @@ def main():
     p = m.ModelParameters(L, L, 1.0, -0.35, -1.08, 1.0, 0.1, 16.0, 0.8, 1.0)
     st = m.initialize_state(p, np.random.default_rng(7))
     D = st.Delta + 0.25 * np.stack([np.ones(p.N), -np.ones(p.N)], 1)
-    ctx = m.FermionContext(p.Lx, p.Ly, p.t, p.tp, p.mu, p.beta, p.J, p.nn_table, p.nnn_table, st.disorder_pot)
+    # DWHMC_LIB: another build of the library (A/B, e.g. an earlier round's)
+    ctx = m.FermionContext(p.Lx, p.Ly, p.t, p.tp, p.mu, p.beta, p.J, p.nn_table, p.nnn_table, st.disorder_pot,
+                           lib_path=os.environ.get("DWHMC_LIB"))
     ctx.set_pairing(D)
     ctx.measure_transport(p.eta, p.domega, p.omega_max)
     t0 = time.perf_counter()
