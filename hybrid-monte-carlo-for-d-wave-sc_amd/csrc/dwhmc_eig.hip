@@ -126,12 +126,13 @@ __global__ __launch_bounds__(256) void k_eig_reduce(const double2* __restrict__ 
   vv += (int64_t)k * kEigRing * n;
   ww += (int64_t)k * kEigRing * n;
   double2 s = cz();
-  for (int Y0 = t0; Y0 < T; Y0 += 8) {
-    double2 q[8];
+  constexpr int YB = 16;   // partial rows in flight per thread
+  for (int Y0 = t0; Y0 < T; Y0 += YB) {
+    double2 q[YB];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) q[u] = Y0 + u < T ? part[(int64_t)(Y0 + u) * n + r] : cz();
+    for (int u = 0; u < YB; ++u) q[u] = Y0 + u < T ? part[(int64_t)(Y0 + u) * n + r] : cz();
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
+    for (int u = 0; u < YB; ++u)
       if (Y0 + u < T) s = cadd(s, q[u]);
   }
   double2 c = A[k * sA + r + (int64_t)i * n];
