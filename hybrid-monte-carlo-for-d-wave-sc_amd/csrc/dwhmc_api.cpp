@@ -2849,6 +2849,18 @@ int dwh_debug_cr_plan_check(int64_t Lx, int64_t Ly, int64_t nbatch, int32_t side
   const int BP = 2 * ((Lxc + 15) / 16 * 16);
   const CrPlan pl = build_cr_plan(Lxc, Lyc, BP, Dcol, side && dwh::cr_supported_side(BP), (int)nbatch,
                                   256, inv0 && dwh::cr_supported_inv0(BP));
+  if (const char* e = std::getenv("DWHMC_CR_PLAN_DUMP"); e && *e == '1') {
+    int i = 0;
+    for (const CrStage& st : pl.stages) {
+      if (st.kind == 0)
+        std::fprintf(stderr, "cr stage %2d: inv%s blocks=%d (x%lld wg) side_tasks=%d maxt32=%d side_flops/item=%.3g\n", i,
+                     st.l0 ? "0 " : "  ", st.n, (long long)nbatch, st.ntiles, st.maxt32, st.flops);
+      else
+        std::fprintf(stderr, "cr stage %2d: gemm  tasks=%d maxt32=%d maxt16=%d ntmax=%d flops/item=%.3g ntiles=%d\n", i,
+                     st.n, st.maxt32, st.maxt16, st.ntmax, st.flops, st.ntiles);
+      ++i;
+    }
+  }
   std::vector<int> written(pl.nblk, -1);   // stage of the first write; -2: ready from the start
   for (int b = 0; b < 3 * Lyc && b < pl.nblk; ++b) written[b] = -2;
   for (int r : pl.inv0_r) written[r] = -2;
