@@ -681,6 +681,7 @@ struct dwh_ctx {
   double2 *d_eig_T = nullptr, *d_eig_W = nullptr, *d_eig_W2 = nullptr, *d_eig_dpart = nullptr;
   double2* d_eig_pfin = nullptr;   // the hemv partials reduced per row (k_eig_reduce)
   double2* d_eig_colfin = nullptr;   // column i with its pending pairs (k_eig_reduce)
+  double2* d_eig_gpart = nullptr;    // k_eig_reduce's g partials (one matrix)
   int* d_eig_c0 = nullptr;         // particle-hole half solve: first computed eigenvector per matrix
   bool eig_half = false;           // the last own solve ran the particle-hole half solve
   std::vector<int> eig_c0h;        // its c0 per matrix (N: no zero crowding)
@@ -1855,7 +1856,7 @@ int own_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m) {
   if (m > ctx->eig_slots) {
     HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
     for (void* q : {(void*)ctx->d_eig_part, (void*)ctx->d_eig_vv, (void*)ctx->d_eig_ww, (void*)ctx->d_eig_tau,
-                    (void*)ctx->d_eig_dpart, (void*)ctx->d_eig_pfin, (void*)ctx->d_eig_c0, (void*)ctx->d_eig_colfin,
+                    (void*)ctx->d_eig_dpart, (void*)ctx->d_eig_pfin, (void*)ctx->d_eig_c0, (void*)ctx->d_eig_colfin, (void*)ctx->d_eig_gpart,
                     (void*)ctx->d_eig_T, (void*)ctx->d_eig_W, (void*)ctx->d_eig_W2, (void*)ctx->d_eig_d,
                     (void*)ctx->d_eig_e, (void*)ctx->d_eig_tn})
       drop_alloc(ctx, q);
@@ -1864,6 +1865,7 @@ int own_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m) {
         (rc = dalloc(ctx, &ctx->d_eig_ww, mm * dwh::kEigRing * n)) || (rc = dalloc(ctx, &ctx->d_eig_tau, mm * n)) ||
         (rc = dalloc(ctx, &ctx->d_eig_dpart, mm * 2 * dwh::kEigDeferMax * T)) ||
         (rc = dalloc(ctx, &ctx->d_eig_pfin, mm * n)) || (rc = dalloc(ctx, &ctx->d_eig_colfin, mm * n)) ||
+        (rc = dalloc(ctx, &ctx->d_eig_gpart, mm * dwh::kEigGP)) ||
         (rc = dalloc(ctx, &ctx->d_eig_T, mm * sT)) || (rc = dalloc(ctx, &ctx->d_eig_W, mm * std::max<int64_t>(KS * sW, (int64_t)nblk * dwh::kEigGS * NB * NB))) ||
         (rc = dalloc(ctx, &ctx->d_eig_W2, mm * sW)) || (rc = dalloc(ctx, &ctx->d_eig_d, mm * n)) ||
         (rc = dalloc(ctx, &ctx->d_eig_e, mm * n)) || (rc = dalloc(ctx, &ctx->d_eig_tn, mm)) ||
@@ -1878,10 +1880,9 @@ int own_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m) {
   ph.mark("assemble");
   for (int i = 0; i < n; ++i) {
     if (ph.on && i % 512 == 0 && i > 0) ph.mark("tridiag/512");
-    dwh::launch_eig_step(A, n, i, sA, ctx->d_eig_part, sP, ctx->d_eig_pfin, ctx->d_eig_colfin, ctx->d_eig_vv,
-                         ctx->d_eig_ww, ctx->d_eig_d, ctx->d_eig_e, ctx->d_eig_tau, ctx->d_eig_dpart, m, s);
-    if (i < n - 1)
-      dwh::launch_eig_pass(A, n, i, sA, ctx->d_eig_part, sP, ctx->d_eig_vv, ctx->d_eig_ww, ctx->d_eig_dpart, m, s);
+    dwh::launch_eig_column(A, n, i, sA, ctx->d_eig_part, sP, ctx->d_eig_pfin, ctx->d_eig_colfin, ctx->d_eig_vv,
+                           ctx->d_eig_ww, ctx->d_eig_d, ctx->d_eig_e, ctx->d_eig_tau, ctx->d_eig_dpart,
+                           ctx->d_eig_gpart, m, s);
   }
   ph.mark("tridiag");
   dwh::launch_eig_bisect(ctx->d_eig_d, ctx->d_eig_e, n, b.E, ctx->d_eig_tn, m, s);

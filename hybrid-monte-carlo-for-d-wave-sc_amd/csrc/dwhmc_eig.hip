@@ -105,11 +105,14 @@ constexpr int KD = kEigDeferMax;
 // pfin = A^{(i-1)} v_{i-1}; column i of A with those pairs applied into colfin
 // (the step applies pair i-1 itself).  One thread per row, many workgroups,
 // so the single-workgroup step reads 2 n values.
+// gpart (one matrix, k_eig_pass1f follows): this workgroup's share of
+// g = sum_r conj(tau_{i-1} p_r) v_{i-1}[r], summed in a fixed order.
 __global__ __launch_bounds__(256) void k_eig_reduce(const double2* __restrict__ part, int64_t sP, int n, int i,
                                                     double2* __restrict__ pfin, const double2* __restrict__ A,
                                                     int64_t sA, double2* __restrict__ colfin,
                                                     const double2* __restrict__ vv, const double2* __restrict__ ww,
-                                                    const double2* __restrict__ dpart, int K) {
+                                                    const double2* __restrict__ dpart, int K,
+                                                    const double2* __restrict__ tau, double2* __restrict__ gpart) {
   const int k = blockIdx.y, tid = threadIdx.x, r = i + blockIdx.x * 256 + tid;
   const int t0 = i / kEigTB, T = (n + kEigTB - 1) / kEigTB;
   const bool rd = !eig_write_pass(i - 1, K);
@@ -121,30 +124,41 @@ __global__ __launch_bounds__(256) void k_eig_reduce(const double2* __restrict__ 
     dots[tid] = s;
   }
   __syncthreads();
-  if (r >= n) return;
+  const bool ok = r < n;
   part += k * sP;
   vv += (int64_t)k * kEigRing * n;
   ww += (int64_t)k * kEigRing * n;
   double2 s = cz();
-  constexpr int YB = 16;   // partial rows in flight per thread
-  for (int Y0 = t0; Y0 < T; Y0 += YB) {
-    double2 q[YB];
+  if (ok) {
+    constexpr int YB = 16;   // partial rows in flight per thread
+    for (int Y0 = t0; Y0 < T; Y0 += YB) {
+      double2 q[YB];
 #pragma unroll
-    for (int u = 0; u < YB; ++u) q[u] = Y0 + u < T ? part[(int64_t)(Y0 + u) * n + r] : cz();
+      for (int u = 0; u < YB; ++u) q[u] = Y0 + u < T ? part[(int64_t)(Y0 + u) * n + r] : cz();
 #pragma unroll
-    for (int u = 0; u < YB; ++u)
-      if (Y0 + u < T) s = cadd(s, q[u]);
+      for (int u = 0; u < YB; ++u)
+        if (Y0 + u < T) s = cadd(s, q[u]);
+    }
+    double2 c = A[k * sA + r + (int64_t)i * n];
+    for (int q = 0; q < np; ++q) {
+      const int sl = (f + q) % kEigRing;
+      const double2 vj = vv[(int64_t)sl * n + r], wj = ww[(int64_t)sl * n + r];
+      s = csub(csub(s, cmul(vj, dots[2 * q])), cmul(wj, dots[2 * q + 1]));
+      const double2 vji = vv[(int64_t)sl * n + i], wji = ww[(int64_t)sl * n + i];
+      c = csub(csub(c, cmulc(vj, wji)), cmulc(wj, vji));
+    }
+    pfin[(int64_t)k * n + r] = s;
+    colfin[(int64_t)k * n + r] = c;
   }
-  double2 c = A[k * sA + r + (int64_t)i * n];
-  for (int q = 0; q < np; ++q) {
-    const int sl = (f + q) % kEigRing;
-    const double2 vj = vv[(int64_t)sl * n + r], wj = ww[(int64_t)sl * n + r];
-    s = csub(csub(s, cmul(vj, dots[2 * q])), cmul(wj, dots[2 * q + 1]));
-    const double2 vji = vv[(int64_t)sl * n + i], wji = ww[(int64_t)sl * n + i];
-    c = csub(csub(c, cmulc(vj, wji)), cmulc(wj, vji));
+  if (gpart) {
+    __shared__ double2 sg[4];
+    const double2 tp = tau[(int64_t)k * n + i - 1];
+    const double2 x = cmul(tp, s);
+    const double2 v = ok ? vv[(int64_t)((i + kEigRing - 1) % kEigRing) * n + r] : cz();
+    double2 gq = make_double2(x.x * v.x + x.y * v.y, x.x * v.y - x.y * v.x);   // conj(x) v
+    gq = group_sum2(gq, sg);
+    if (tid == 0) gpart[(int64_t)k * kEigGP + blockIdx.x] = gq;
   }
-  pfin[(int64_t)k * n + r] = s;
-  colfin[(int64_t)k * n + r] = c;
 }
 
 // Step i: w_{i-1} from p = pfin (w = x - 1/2 tau (x^H v) v, x = tau p, zhetd2
@@ -456,6 +470,156 @@ __global__ __launch_bounds__(256) void k_eig_pass1(double2* __restrict__ A, int 
       if (gr > gc) t = make_double2(a[u].x * vr.x + a[u].y * vr.y, a[u].x * vr.y - a[u].y * vr.x);   // conj(a) v_r
     }
     colc[cc][lane] = t;
+  }
+  rowp[w][lane] = pr;
+  __syncthreads();
+  {
+    const int cc = tid >> 2, q = tid & 3;
+    double2 s = cz();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s = cadd(s, colc[cc][q * 16 + r]);
+    s.x += __shfl_xor(s.x, 1, 64);
+    s.y += __shfl_xor(s.y, 1, 64);
+    s.x += __shfl_xor(s.x, 2, 64);
+    s.y += __shfl_xor(s.y, 2, 64);
+    if (q == 0) csum[cc] = s;
+  }
+  __syncthreads();
+  if (tid < 64) {
+    const double2 rs = cadd(cadd(rowp[0][tid], rowp[1][tid]), cadd(rowp[2][tid], rowp[3][tid]));
+    const double2 cs = csum[tid];
+    const int r = R * kEigTB + tid, c = C * kEigTB + tid;
+    if (R == C) {
+      if (r < n) part[(int64_t)R * n + r] = cadd(rs, cs);
+    } else {
+      if (r < n) part[(int64_t)C * n + r] = rs;
+      if (c < n) part[(int64_t)R * n + c] = cs;
+    }
+  }
+}
+
+// One matrix (K = 1), 1 <= i <= n-2: step i folded into pass i.  Every
+// workgroup forms the scalars of column i itself from k_eig_reduce's
+// outputs — g (the reduce workgroups' partials, fixed order), w_{i-1}[i] and
+// bu = conj(w_{i-1}[i]) + al of the updated column c = c0 - tau p - bu v_{i-1},
+// the norm of c over the rows >= i+2 (a sweep over p, c0, v_{i-1} in a fixed
+// order: the same bits in every workgroup), the reflector (zlarfg) — and
+// then v_i and w_{i-1} on its tile's rows and columns.  The diagonal tiles
+// write v_i and column i of A (tile t0 also the rows above and d, e, tau).
+// Saves the single-workgroup step launch of every column.
+__global__ __launch_bounds__(256) void k_eig_pass1f(double2* __restrict__ A, int n, int i, int64_t sA,
+                                                    double2* __restrict__ part, int64_t sP,
+                                                    double2* __restrict__ vv, const double2* __restrict__ pfin,
+                                                    const double2* __restrict__ colfin,
+                                                    const double2* __restrict__ gpart, int ngp,
+                                                    double* __restrict__ d, double* __restrict__ e,
+                                                    double2* __restrict__ tau, int t0) {
+  const int k = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  A += k * sA;
+  part += k * sP;
+  vv += (int64_t)k * kEigRing * n;
+  pfin += (int64_t)k * n;
+  colfin += (int64_t)k * n;
+  gpart += (int64_t)k * kEigGP;
+  const double2* vp = vv + (int64_t)((i + kEigRing - 1) % kEigRing) * n;   // v_{i-1}
+  double2* vcur = vv + (int64_t)(i % kEigRing) * n;
+  int R, C;
+  tri_decode(blockIdx.x, R, C);
+  R += t0;
+  C += t0;
+  const int gr = R * kEigTB + lane;
+  const bool rok = gr >= i + 1 && gr < n;
+  // the tile, in flight while the scalars are formed
+  constexpr int NCW = kEigTB / 4;   // columns per wave
+  double2 a[NCW];
+  unsigned act = 0;
+#pragma unroll
+  for (int u = 0; u < NCW; ++u) {
+    const int gc = C * kEigTB + w + 4 * u;
+    const bool ok = rok && gc >= i + 1 && gr >= gc;
+    act |= (unsigned)ok << u;
+    a[u] = ok ? A[gr + (int64_t)gc * n] : cz();
+  }
+  // scalars of column i (zhetd2 'L': x = tau p, w = x - 1/2 tau (x^H v) v)
+  const double2 tp = tau[(int64_t)k * n + i - 1];
+  double2 g = cz();
+  for (int b = 0; b < ngp; ++b) g = cadd(g, gpart[b]);
+  const double2 al = cmul(tp, make_double2(-0.5 * g.x, -0.5 * g.y));
+  const double2 wi = cadd(cmul(tp, pfin[i]), al);
+  const double2 bu = make_double2(wi.x + al.x, al.y - wi.y);   // conj(wi) + al
+  double xn = 0.0;
+  for (int r = i + 2 + tid; r < n; r += 256) {
+    const double2 c = csub(csub(colfin[r], cmul(tp, pfin[r])), cmul(bu, vp[r]));
+    xn += c.x * c.x + c.y * c.y;
+  }
+  __shared__ double sx[4];
+  xn = group_sum(xn, sx);
+  const double2 ci = csub(csub(colfin[i], cmul(tp, pfin[i])), bu);                       // v_{i-1}[i] = 1
+  const double2 alpha = csub(csub(colfin[i + 1], cmul(tp, pfin[i + 1])), cmul(bu, vp[i + 1]));
+  // zlarfg: beta = -sign(Re alpha) ||(alpha, x)||, tau = (beta - alpha) / beta, v = x / (alpha - beta)
+  double2 t = cz(), sc = cz();
+  double beta = alpha.x;
+  if (!(xn == 0.0 && alpha.y == 0.0)) {
+    beta = -copysign(sqrt(alpha.x * alpha.x + alpha.y * alpha.y + xn), alpha.x);
+    t = make_double2((beta - alpha.x) / beta, -alpha.y / beta);
+    sc = cinv(make_double2(alpha.x - beta, alpha.y));
+  }
+  // v_i, v_{i-1}, w_{i-1} at index x >= i + 1
+  auto vnew = [&](int x, double2 px, double2 cx, double2 vx) {
+    return x == i + 1 ? make_double2(1.0, 0.0) : cmul(csub(csub(cx, cmul(tp, px)), cmul(bu, vx)), sc);
+  };
+  __shared__ double2 cv[64], cva[64], cwa[64], csum[64];
+  __shared__ double2 colc[64][65];
+  __shared__ double2 rowp[4][64];
+  if (tid < 64) {
+    const int gc = C * kEigTB + tid;
+    const bool ok = gc >= i + 1 && gc < n;
+    double2 pc = cz(), cc0 = cz(), vc = cz();
+    if (ok) {
+      pc = pfin[gc];
+      cc0 = colfin[gc];
+      vc = vp[gc];
+    }
+    cv[tid] = ok ? vnew(gc, pc, cc0, vc) : cz();
+    cva[tid] = vc;
+    cwa[tid] = ok ? cadd(cmul(tp, pc), cmul(al, vc)) : cz();
+  }
+  double2 vr = cz(), var = cz(), war = cz();
+  if (rok) {
+    const double2 pr0 = pfin[gr], cr0 = colfin[gr];
+    var = vp[gr];
+    vr = vnew(gr, pr0, cr0, var);
+    war = cadd(cmul(tp, pr0), cmul(al, var));
+  }
+  if (R == C) {   // column i of A and v_i on this tile's rows
+    if (rok) {
+      vcur[gr] = vr;
+      A[gr + (int64_t)i * n] = vr;
+    } else if (gr < n && gr <= i) {
+      A[gr + (int64_t)i * n] = cz();
+    }
+    if (R == t0) {
+      for (int r = tid; r < t0 * kEigTB && r <= i; r += 256) A[r + (int64_t)i * n] = cz();
+      if (tid == 0) {
+        d[(int64_t)k * n + i] = ci.x;
+        e[(int64_t)k * n + i] = beta;
+        tau[(int64_t)k * n + i] = t;
+      }
+    }
+  }
+  __syncthreads();
+  double2 pr = cz();
+#pragma unroll
+  for (int u = 0; u < NCW; ++u) {
+    const int cc = w + 4 * u, gc = C * kEigTB + cc;
+    double2 tt = cz();
+    if ((act >> u) & 1) {
+      a[u] = csub(csub(a[u], cmulc(var, cwa[cc])), cmulc(war, cva[cc]));
+      A[gr + (int64_t)gc * n] = a[u];
+      pr = cadd(pr, cmul(a[u], cv[cc]));
+      if (gr > gc) tt = make_double2(a[u].x * vr.x + a[u].y * vr.y, a[u].x * vr.y - a[u].y * vr.x);   // conj(a) v_r
+    }
+    colc[cc][lane] = tt;
   }
   rowp[w][lane] = pr;
   __syncthreads();
@@ -994,7 +1158,7 @@ void launch_eig_step(double2* A, int n, int i, int64_t sA, const double2* part, 
                      const double2* dpart, int m, hipStream_t s) {
   if (i > 0)
     hipLaunchKernelGGL(k_eig_reduce, dim3((n - i + 255) / 256, m), dim3(256), 0, s, part, sP, n, i, pfin, A, sA,
-                       colfin, vv, ww, dpart, eig_defer_k(m));
+                       colfin, vv, ww, dpart, eig_defer_k(m), (const double2*)tau, (double2*)nullptr);
   const int rs = (n - i + kStepT - 1) / kStepT;   // row slots the rows i..n-1 need
   static_assert(kEigMaxN <= 5 * kStepT, "k_eig_step instantiations");
 #define DWH_EIG_STEP(R) \
@@ -1019,6 +1183,27 @@ void launch_eig_pass(double2* A, int n, int i, int64_t sA, double2* part, int64_
   else
     hipLaunchKernelGGL(k_eig_pass<KD>, dim3(nT * (nT + 1) / 2, m), dim3(256), 0, s, A, n, i, sA, part, sP, vv, ww,
                        t0, dpart, T, K);
+}
+
+// Column i of the reduction: one matrix (K = 1) folds step i into pass i for
+// 1 <= i <= n-2 (k_eig_reduce with the g partials, then k_eig_pass1f;
+// DWHMC_EIG_FUSED=0: step + pass, A/B); else step i, then pass i.
+void launch_eig_column(double2* A, int n, int i, int64_t sA, double2* part, int64_t sP, double2* pfin,
+                       double2* colfin, double2* vv, double2* ww, double* d, double* e, double2* tau,
+                       double2* dpart, double2* gpart, int m, hipStream_t s) {
+  const int K = eig_defer_k(m);
+  const char* ef = std::getenv("DWHMC_EIG_FUSED");
+  if (K == 1 && i >= 1 && i <= n - 2 && !(ef && *ef == '0')) {
+    const int ngp = (n - i + 255) / 256;
+    hipLaunchKernelGGL(k_eig_reduce, dim3(ngp, m), dim3(256), 0, s, part, sP, n, i, pfin, A, sA, colfin, vv, ww,
+                       dpart, K, (const double2*)tau, gpart);
+    const int T = (n + kEigTB - 1) / kEigTB, t0 = (i + 1) / kEigTB, nT = T - t0;
+    hipLaunchKernelGGL(k_eig_pass1f, dim3(nT * (nT + 1) / 2, m), dim3(256), 0, s, A, n, i, sA, part, sP, vv, pfin,
+                       colfin, gpart, ngp, d, e, tau, t0);
+    return;
+  }
+  launch_eig_step(A, n, i, sA, part, sP, pfin, colfin, vv, ww, d, e, tau, dpart, m, s);
+  if (i < n - 1) launch_eig_pass(A, n, i, sA, part, sP, vv, ww, dpart, m, s);
 }
 
 void launch_eig_bisect(const double* d, const double* e, int n, double* E, double* tnorm, int m, hipStream_t s) {

@@ -263,6 +263,7 @@ constexpr int kEigMaxCluster = 64;          // longest such run (else *bad: vend
 constexpr int kEigDefer = 8;
 constexpr int kEigDeferMax = 8;
 constexpr int kEigRing = kEigDeferMax + 2;
+constexpr int kEigGP = (kEigMaxN + 255) / 256;   // k_eig_reduce workgroups per matrix (g partials)
 // column i of the tridiagonalisation (k_eig_reduce + k_eig_step): the pass
 // partials (+ the read pass's pending-pair corrections) -> pfin, column i with
 // the pending pairs -> colfin, then w_{i-1}, v_i (d, e, tau).
@@ -272,6 +273,10 @@ constexpr int kEigRing = kEigDeferMax + 2;
 void launch_eig_step(double2* A, int n, int i, int64_t sA, const double2* part, int64_t sP, double2* pfin,
                      double2* colfin, double2* vv, double2* ww, double* d, double* e, double2* tau,
                      const double2* dpart, int m, hipStream_t s);
+// step i + pass i (one matrix: folded into one pass launch); gpart: kEigGP per matrix
+void launch_eig_column(double2* A, int n, int i, int64_t sA, double2* part, int64_t sP, double2* pfin,
+                       double2* colfin, double2* vv, double2* ww, double* d, double* e, double2* tau,
+                       double2* dpart, double2* gpart, int m, hipStream_t s);
 // the pending pairs on the trailing triangle (write passes) + hemv partials of v_i
 void launch_eig_pass(double2* A, int n, int i, int64_t sA, double2* part, int64_t sP, const double2* vv,
                      const double2* ww, double2* dpart, int m, hipStream_t s);
