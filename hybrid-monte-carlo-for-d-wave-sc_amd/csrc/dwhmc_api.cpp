@@ -1897,7 +1897,8 @@ int own_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m) {
   // (-v*; u*)): eigenvectors of T only for the indices from
   // c0, the largest index <= n/2 below which the spectrum has a gap wider
   // than kEigZeroTol ||T|| (n/2 unless levels crowd around zero, e.g. the
-  // exact zero modes of clean lattices, which are then computed whole); the
+  // exact zero modes of clean lattices, which are then computed whole; 0 for
+  // a spectrum with degenerate levels anywhere); the
   // columns below c0 are the partners of the columns above n - c0
   // (k_eig_theta after the back-transform).  c0 comes from the eigenvalues
   // on the host (one synchronisation); every matrix computes the columns
@@ -1920,6 +1921,12 @@ int own_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m) {
       const double tol = dwh::kEigZeroTol * tn[k];
       int c = N;
       while (c > 0 && !(E[c] - E[c - 1] > tol)) --c;   // (NaN gaps: keep going, c -> 0)
+      // degenerate levels (clean lattices: most levels in clusters) leave the
+      // partner images' overlaps with the computed vectors at ~1e-13 and
+      // above; such a matrix computes every vector (c0 = 0)
+      const double ctol = dwh::kEigClusterTol * tn[k];
+      for (int j = 1; j < n && c > 0; ++j)
+        if (!(E[j] - E[j - 1] > ctol)) c = 0;
       ctx->eig_c0h[k] = c;
       j0 = std::min(j0, c);
     }

@@ -111,6 +111,8 @@ def test_bdg_half_spectrum_vectors(oracle, Lx, Ly, clean, mu):
         assert c0 < n // 2          # the zero modes straddle
     else:
         assert c0 == n // 2
+    if clean:                       # degenerate levels: eigh_bdg computes every vector
+        assert np.any(np.diff(lam2) <= 1e-6 * tn)
 
 
 @pytest.mark.parametrize("K", [1, 2, 3, 8])
