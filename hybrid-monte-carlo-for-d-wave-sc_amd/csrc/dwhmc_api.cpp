@@ -1865,7 +1865,7 @@ int own_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m) {
         (rc = dalloc(ctx, &ctx->d_eig_ww, mm * dwh::kEigRing * n)) || (rc = dalloc(ctx, &ctx->d_eig_tau, mm * n)) ||
         (rc = dalloc(ctx, &ctx->d_eig_dpart, mm * 2 * dwh::kEigDeferMax * T)) ||
         (rc = dalloc(ctx, &ctx->d_eig_pfin, mm * n)) || (rc = dalloc(ctx, &ctx->d_eig_colfin, mm * n)) ||
-        (rc = dalloc(ctx, &ctx->d_eig_gpart, mm * dwh::kEigGP)) ||
+        (rc = dalloc(ctx, &ctx->d_eig_gpart, mm * 3 * dwh::kEigGP)) ||
         (rc = dalloc(ctx, &ctx->d_eig_T, mm * sT)) || (rc = dalloc(ctx, &ctx->d_eig_W, mm * std::max<int64_t>(KS * sW, (int64_t)nblk * dwh::kEigGS * NB * NB))) ||
         (rc = dalloc(ctx, &ctx->d_eig_W2, mm * sW)) || (rc = dalloc(ctx, &ctx->d_eig_d, mm * n)) ||
         (rc = dalloc(ctx, &ctx->d_eig_e, mm * n)) || (rc = dalloc(ctx, &ctx->d_eig_tn, mm)) ||

@@ -151,13 +151,29 @@ __global__ __launch_bounds__(256) void k_eig_reduce(const double2* __restrict__ 
     colfin[(int64_t)k * n + r] = c;
   }
   if (gpart) {
-    __shared__ double2 sg[4];
+    // g = sum conj(x_r) v_r (x = tau p, rows >= i), and for the norm of the
+    // updated column c = a - bu v (a = c0 - x) over the rows >= i+2:
+    // S1 = sum |a|^2, S2 = sum conj(v) a, S3 = sum |v|^2
+    __shared__ double2 sg[4], s12[4], s23[4];
     const double2 tp = tau[(int64_t)k * n + i - 1];
     const double2 x = cmul(tp, s);
     const double2 v = ok ? vv[(int64_t)((i + kEigRing - 1) % kEigRing) * n + r] : cz();
     double2 gq = make_double2(x.x * v.x + x.y * v.y, x.x * v.y - x.y * v.x);   // conj(x) v
+    double2 s1 = cz(), s2 = cz();
+    if (ok && r >= i + 2) {
+      const double2 av = csub(colfin[(int64_t)k * n + r], x);
+      s1 = make_double2(av.x * av.x + av.y * av.y, v.x * v.x + v.y * v.y);      // (S1, S3)
+      s2 = make_double2(v.x * av.x + v.y * av.y, v.x * av.y - v.y * av.x);      // conj(v) a
+    }
     gq = group_sum2(gq, sg);
-    if (tid == 0) gpart[(int64_t)k * kEigGP + blockIdx.x] = gq;
+    s1 = group_sum2(s1, s12);
+    s2 = group_sum2(s2, s23);
+    if (tid == 0) {
+      double2* gp = gpart + ((int64_t)k * kEigGP + blockIdx.x) * 3;
+      gp[0] = gq;
+      gp[1] = s1;
+      gp[2] = s2;
+    }
   }
 }
 
@@ -520,7 +536,7 @@ __global__ __launch_bounds__(256) void k_eig_pass1f(double2* __restrict__ A, int
   vv += (int64_t)k * kEigRing * n;
   pfin += (int64_t)k * n;
   colfin += (int64_t)k * n;
-  gpart += (int64_t)k * kEigGP;
+  gpart += (int64_t)k * kEigGP * 3;
   const double2* vp = vv + (int64_t)((i + kEigRing - 1) % kEigRing) * n;   // v_{i-1}
   double2* vcur = vv + (int64_t)(i % kEigRing) * n;
   int R, C;
@@ -542,18 +558,28 @@ __global__ __launch_bounds__(256) void k_eig_pass1f(double2* __restrict__ A, int
   }
   // scalars of column i (zhetd2 'L': x = tau p, w = x - 1/2 tau (x^H v) v)
   const double2 tp = tau[(int64_t)k * n + i - 1];
-  double2 g = cz();
-  for (int b = 0; b < ngp; ++b) g = cadd(g, gpart[b]);
+  double2 g = cz(), s13 = cz(), s2 = cz();
+  for (int b = 0; b < ngp; ++b) {
+    g = cadd(g, gpart[3 * b]);
+    s13 = cadd(s13, gpart[3 * b + 1]);
+    s2 = cadd(s2, gpart[3 * b + 2]);
+  }
   const double2 al = cmul(tp, make_double2(-0.5 * g.x, -0.5 * g.y));
   const double2 wi = cadd(cmul(tp, pfin[i]), al);
   const double2 bu = make_double2(wi.x + al.x, al.y - wi.y);   // conj(wi) + al
-  double xn = 0.0;
-  for (int r = i + 2 + tid; r < n; r += 256) {
-    const double2 c = csub(csub(colfin[r], cmul(tp, pfin[r])), cmul(bu, vp[r]));
-    xn += c.x * c.x + c.y * c.y;
+  // ||c||^2 = S1 - 2 Re(conj(bu) S2) + |bu|^2 S3 unless that cancels (then
+  // by a sweep over the rows: the same decision and bits in every workgroup)
+  const double b2 = bu.x * bu.x + bu.y * bu.y;
+  double xn = s13.x - 2.0 * (bu.x * s2.x + bu.y * s2.y) + b2 * s13.y;
+  if (!(xn >= 1e-3 * (s13.x + b2 * s13.y))) {
+    __shared__ double sx[4];
+    xn = 0.0;
+    for (int r = i + 2 + tid; r < n; r += 256) {
+      const double2 c = csub(csub(colfin[r], cmul(tp, pfin[r])), cmul(bu, vp[r]));
+      xn += c.x * c.x + c.y * c.y;
+    }
+    xn = group_sum(xn, sx);
   }
-  __shared__ double sx[4];
-  xn = group_sum(xn, sx);
   const double2 ci = csub(csub(colfin[i], cmul(tp, pfin[i])), bu);                       // v_{i-1}[i] = 1
   const double2 alpha = csub(csub(colfin[i + 1], cmul(tp, pfin[i + 1])), cmul(bu, vp[i + 1]));
   // zlarfg: beta = -sign(Re alpha) ||(alpha, x)||, tau = (beta - alpha) / beta, v = x / (alpha - beta)

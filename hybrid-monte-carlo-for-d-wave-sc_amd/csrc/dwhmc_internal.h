@@ -273,7 +273,7 @@ constexpr int kEigGP = (kEigMaxN + 255) / 256;   // k_eig_reduce workgroups per 
 void launch_eig_step(double2* A, int n, int i, int64_t sA, const double2* part, int64_t sP, double2* pfin,
                      double2* colfin, double2* vv, double2* ww, double* d, double* e, double2* tau,
                      const double2* dpart, int m, hipStream_t s);
-// step i + pass i (one matrix: folded into one pass launch); gpart: kEigGP per matrix
+// step i + pass i (one matrix: folded into one pass launch); gpart: 3 kEigGP per matrix
 void launch_eig_column(double2* A, int n, int i, int64_t sA, double2* part, int64_t sP, double2* pfin,
                        double2* colfin, double2* vv, double2* ww, double* d, double* e, double2* tau,
                        double2* dpart, double2* gpart, int m, hipStream_t s);
