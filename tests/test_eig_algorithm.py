@@ -131,3 +131,32 @@ def test_deferred_pairs_same_reduction(K, n):
     for a, b in zip(ref, got):
         if np.size(a):
             assert np.max(np.abs(a - b)) <= 1e-13 * scale * max(n, 1)
+
+
+def test_fused_step_scalars():
+    """The scalars k_eig_pass1f forms from k_eig_reduce's partials equal the
+    step's: w = τp − ½τ(τp)ᴴv·v, column c = c0 − v·conj(w_i) − w, and
+    ‖c_{i+2:}‖² by the expansion S1 − 2 Re(b̄ S2) + |b|² S3 with c = a − b v,
+    a = c0 − τp, b = conj(w_i) + al (al = −½ τ g, g = Σ conj(τp) v)."""
+    rng = np.random.default_rng(21)
+    n, i = 40, 7
+    z = lambda: rng.standard_normal(n) + 1j * rng.standard_normal(n)
+    p, c0, v = z(), z(), z()
+    v[:i] = 0.0
+    v[i] = 1.0
+    tp = 1.3 - 0.4j
+    r = slice(i, n)
+    x = tp * p
+    g = np.vdot(x[r], v[r])                    # sum conj(x) v
+    al = tp * (-0.5 * g)
+    w = x + al * v
+    wi = w[i]
+    c_step = c0 - v * np.conj(wi) - w
+    a = c0 - x
+    b = np.conj(wi) + al
+    c_fused = a - b * v
+    assert np.max(np.abs(c_step[i:] - c_fused[i:])) <= 1e-13 * np.max(np.abs(c_step[i:]))
+    q = slice(i + 2, n)
+    S1, S2, S3 = np.sum(np.abs(a[q]) ** 2), np.vdot(v[q], a[q]), np.sum(np.abs(v[q]) ** 2)
+    xn = S1 - 2.0 * np.real(np.conj(b) * S2) + abs(b) ** 2 * S3
+    assert abs(xn - np.sum(np.abs(c_step[q]) ** 2)) <= 1e-12 * (S1 + abs(b) ** 2 * S3)
