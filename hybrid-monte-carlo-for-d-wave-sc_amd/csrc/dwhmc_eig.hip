@@ -293,17 +293,83 @@ __device__ __forceinline__ void tri_decode(int b, int& R, int& C) {
 // tile and writes it back; every pass accumulates the tile's share of A v_i
 // into fixed partial slots, and a read pass's diagonal tiles the dots of the
 // pending pairs with v_i.
-template <int KM>   // most pending pairs (kEigDeferMax; K = 1 runs k_eig_pass1)
+// The scalars of column i that k_eig_step forms, from k_eig_reduce's
+// per-workgroup partials (g, S1/S3, S2; fixed order): al = -1/2 tau g,
+// w_{i-1}[i], bu = conj(w_{i-1}[i]) + al (column c = c0 - tau p - bu v_{i-1}),
+// ||c_{i+2:}||^2 = S1 - 2 Re(conj(bu) S2) + |bu|^2 S3 (a sweep over the rows
+// where that cancels), and the reflector (zlarfg).  Every thread of every
+// workgroup gets the same bits; sx: 4 doubles of LDS.
+struct ColScal {
+  double2 tp, al, bu, sc, t;
+  double beta, di;
+};
+__device__ __forceinline__ ColScal col_scalars(int n, int i, const double2* __restrict__ pfin,
+                                               const double2* __restrict__ colfin, const double2* __restrict__ vp,
+                                               const double2* __restrict__ gpart, int ngp, double2 tp, double* sx) {
+  ColScal q;
+  q.tp = tp;
+  double2 g = cz(), s13 = cz(), s2 = cz();
+  for (int b = 0; b < ngp; ++b) {
+    g = cadd(g, gpart[3 * b]);
+    s13 = cadd(s13, gpart[3 * b + 1]);
+    s2 = cadd(s2, gpart[3 * b + 2]);
+  }
+  q.al = cmul(tp, make_double2(-0.5 * g.x, -0.5 * g.y));
+  const double2 wi = cadd(cmul(tp, pfin[i]), q.al);
+  q.bu = make_double2(wi.x + q.al.x, q.al.y - wi.y);   // conj(wi) + al
+  const double b2 = q.bu.x * q.bu.x + q.bu.y * q.bu.y;
+  double xn = s13.x - 2.0 * (q.bu.x * s2.x + q.bu.y * s2.y) + b2 * s13.y;
+  if (!(xn >= 1e-3 * (s13.x + b2 * s13.y))) {
+    xn = 0.0;
+    for (int r = i + 2 + (int)threadIdx.x; r < n; r += blockDim.x) {
+      const double2 c = csub(csub(colfin[r], cmul(tp, pfin[r])), cmul(q.bu, vp[r]));
+      xn += c.x * c.x + c.y * c.y;
+    }
+    xn = group_sum(xn, sx);
+  }
+  const double2 ci = csub(csub(colfin[i], cmul(tp, pfin[i])), q.bu);   // v_{i-1}[i] = 1
+  q.di = ci.x;
+  const double2 alpha = csub(csub(colfin[i + 1], cmul(tp, pfin[i + 1])), cmul(q.bu, vp[i + 1]));
+  // zlarfg: beta = -sign(Re alpha) ||(alpha, x)||, tau = (beta - alpha) / beta, v = x / (alpha - beta)
+  q.t = cz();
+  q.sc = cz();
+  q.beta = alpha.x;
+  if (!(xn == 0.0 && alpha.y == 0.0)) {
+    q.beta = -copysign(sqrt(alpha.x * alpha.x + alpha.y * alpha.y + xn), alpha.x);
+    q.t = make_double2((q.beta - alpha.x) / q.beta, -alpha.y / q.beta);
+    q.sc = cinv(make_double2(alpha.x - q.beta, alpha.y));
+  }
+  return q;
+}
+// v_i and w_{i-1} at an index x >= i+1 from (p, c0, v_{i-1}) there
+__device__ __forceinline__ double2 col_vnew(const ColScal& q, int x, int i, double2 px, double2 cx, double2 vx) {
+  return x == i + 1 ? make_double2(1.0, 0.0) : cmul(csub(csub(cx, cmul(q.tp, px)), cmul(q.bu, vx)), q.sc);
+}
+__device__ __forceinline__ double2 col_wnew(const ColScal& q, double2 px, double2 vx) {
+  return cadd(cmul(q.tp, px), cmul(q.al, vx));
+}
+
+// FUSED (1 <= i <= n-2): step i folded in, as in k_eig_pass1f — the column
+// scalars from k_eig_reduce's partials (col_scalars), v_i and the newest
+// pair's w_{i-1} formed on the tile's rows and columns, the diagonal tiles
+// writing v_i, w_{i-1}, column i (tile t0 also d, e, tau).
+template <int KM, bool FUSED>   // most pending pairs (kEigDeferMax; K = 1 runs k_eig_pass1 / 1f)
 __global__ __launch_bounds__(256) void k_eig_pass(double2* __restrict__ A, int n, int i, int64_t sA,
                                                   double2* __restrict__ part, int64_t sP,
-                                                  const double2* __restrict__ vv, const double2* __restrict__ ww,
-                                                  int t0, double2* __restrict__ dpart, int T, int K) {
+                                                  double2* __restrict__ vv, double2* __restrict__ ww,
+                                                  int t0, double2* __restrict__ dpart, int T, int K,
+                                                  const double2* __restrict__ pfin,
+                                                  const double2* __restrict__ colfin,
+                                                  const double2* __restrict__ gpart, int ngp,
+                                                  double* __restrict__ d, double* __restrict__ e,
+                                                  double2* __restrict__ tau) {
   const int k = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   A += k * sA;
   part += k * sP;
   vv += (int64_t)k * kEigRing * n;
   ww += (int64_t)k * kEigRing * n;
-  const double2* v = vv + (int64_t)(i % kEigRing) * n;
+  double2* v = vv + (int64_t)(i % kEigRing) * n;
+  const double2* vp = vv + (int64_t)((i + kEigRing - 1) % kEigRing) * n;   // v_{i-1}
   const bool wp = eig_write_pass(i, K);
   const int f = eig_pend_first(i, K), np = i - f;   // pending pairs f .. i-1 (<= KM)
   int R, C;
@@ -312,6 +378,7 @@ __global__ __launch_bounds__(256) void k_eig_pass(double2* __restrict__ A, int n
   C += t0;
   __shared__ double2 cv[64], csum[64];
   __shared__ double2 rowp[4][64];
+  __shared__ double sx[4];
   // the pending pairs' column values (write pass) and the column-sum
   // transpose; for KM > 2 one LDS region, the two phases split by a barrier
   constexpr bool kAlias = KM > 2;   // (KM <= 2: a separate region)
@@ -321,29 +388,62 @@ __global__ __launch_bounds__(256) void k_eig_pass(double2* __restrict__ A, int n
   double2* cpw = cpv + KM * 64;                  // [KM][64]: w_j
   const int gr = R * kEigTB + lane;
   const bool rok = gr >= i + 1 && gr < n;
+  ColScal cs{};
+  if (FUSED) {
+    pfin += (int64_t)k * n;
+    colfin += (int64_t)k * n;
+    gpart += (int64_t)k * kEigGP * 3;
+    cs = col_scalars(n, i, pfin, colfin, vp, gpart, ngp, tau[(int64_t)k * n + i - 1], sx);
+  }
+  // v_i and the newest pair's w_{i-1} at index x (FUSED: formed here)
+  auto vi_at = [&](int x) {
+    if (!FUSED) return v[x];
+    return col_vnew(cs, x, i, pfin[x], colfin[x], vp[x]);
+  };
+  auto pair_at = [&](int q, int x, double2& pv, double2& pw) {
+    const int sl = (f + q) % kEigRing;
+    pv = vv[(int64_t)sl * n + x];
+    pw = FUSED && f + q == i - 1 ? col_wnew(cs, pfin[x], pv) : ww[(int64_t)sl * n + x];
+  };
   if (tid < 64) {
     const int gc = C * kEigTB + tid;
-    cv[tid] = gc >= i + 1 && gc < n ? v[gc] : cz();
+    cv[tid] = gc >= i + 1 && gc < n ? vi_at(gc) : cz();
   }
   if (wp) {
     for (int q = w; q < np; q += 4) {   // wave w stages pairs w, w+4
-      const int sl = (f + q) % kEigRing, gc = C * kEigTB + lane;
-      const bool ok = gc >= i + 1 && gc < n;
-      cpv[q * 64 + lane] = ok ? vv[(int64_t)sl * n + gc] : cz();
-      cpw[q * 64 + lane] = ok ? ww[(int64_t)sl * n + gc] : cz();
+      const int gc = C * kEigTB + lane;
+      double2 pv = cz(), pw = cz();
+      if (gc >= i + 1 && gc < n) pair_at(q, gc, pv, pw);
+      cpv[q * 64 + lane] = pv;
+      cpw[q * 64 + lane] = pw;
     }
   }
-  const double2 vr = rok ? v[gr] : cz();
+  const double2 vr = rok ? vi_at(gr) : cz();
   // the pending pairs at this lane's row: the write pass's update, or a read
   // pass's dots (diagonal tiles), loaded with the tile
   const bool rowpairs = wp || R == C;
   double2 rv[KM], rw[KM];
 #pragma unroll
   for (int q = 0; q < KM; ++q) {
-    const int sl = (f + q) % kEigRing;
-    const bool ok = rowpairs && rok && q < np;
-    rv[q] = ok ? vv[(int64_t)sl * n + gr] : cz();
-    rw[q] = ok ? ww[(int64_t)sl * n + gr] : cz();
+    rv[q] = rw[q] = cz();
+    if (rowpairs && rok && q < np) pair_at(q, gr, rv[q], rw[q]);
+  }
+  if (FUSED && R == C) {   // v_i, w_{i-1} and column i of A on this tile's rows
+    if (rok) {
+      v[gr] = vr;
+      A[gr + (int64_t)i * n] = vr;
+      ww[(int64_t)((i + kEigRing - 1) % kEigRing) * n + gr] = col_wnew(cs, pfin[gr], vp[gr]);
+    } else if (gr < n && gr <= i) {
+      A[gr + (int64_t)i * n] = cz();
+    }
+    if (R == t0) {
+      for (int r = tid; r < t0 * kEigTB && r <= i; r += 256) A[r + (int64_t)i * n] = cz();
+      if (tid == 0) {
+        d[(int64_t)k * n + i] = cs.di;
+        e[(int64_t)k * n + i] = cs.beta;
+        tau[(int64_t)k * n + i] = cs.t;
+      }
+    }
   }
   __syncthreads();
   constexpr int NCW = kEigTB / 4;   // columns per wave
@@ -557,43 +657,10 @@ __global__ __launch_bounds__(256) void k_eig_pass1f(double2* __restrict__ A, int
     a[u] = ok ? A[gr + (int64_t)gc * n] : cz();
   }
   // scalars of column i (zhetd2 'L': x = tau p, w = x - 1/2 tau (x^H v) v)
-  const double2 tp = tau[(int64_t)k * n + i - 1];
-  double2 g = cz(), s13 = cz(), s2 = cz();
-  for (int b = 0; b < ngp; ++b) {
-    g = cadd(g, gpart[3 * b]);
-    s13 = cadd(s13, gpart[3 * b + 1]);
-    s2 = cadd(s2, gpart[3 * b + 2]);
-  }
-  const double2 al = cmul(tp, make_double2(-0.5 * g.x, -0.5 * g.y));
-  const double2 wi = cadd(cmul(tp, pfin[i]), al);
-  const double2 bu = make_double2(wi.x + al.x, al.y - wi.y);   // conj(wi) + al
-  // ||c||^2 = S1 - 2 Re(conj(bu) S2) + |bu|^2 S3 unless that cancels (then
-  // by a sweep over the rows: the same decision and bits in every workgroup)
-  const double b2 = bu.x * bu.x + bu.y * bu.y;
-  double xn = s13.x - 2.0 * (bu.x * s2.x + bu.y * s2.y) + b2 * s13.y;
-  if (!(xn >= 1e-3 * (s13.x + b2 * s13.y))) {
-    __shared__ double sx[4];
-    xn = 0.0;
-    for (int r = i + 2 + tid; r < n; r += 256) {
-      const double2 c = csub(csub(colfin[r], cmul(tp, pfin[r])), cmul(bu, vp[r]));
-      xn += c.x * c.x + c.y * c.y;
-    }
-    xn = group_sum(xn, sx);
-  }
-  const double2 ci = csub(csub(colfin[i], cmul(tp, pfin[i])), bu);                       // v_{i-1}[i] = 1
-  const double2 alpha = csub(csub(colfin[i + 1], cmul(tp, pfin[i + 1])), cmul(bu, vp[i + 1]));
-  // zlarfg: beta = -sign(Re alpha) ||(alpha, x)||, tau = (beta - alpha) / beta, v = x / (alpha - beta)
-  double2 t = cz(), sc = cz();
-  double beta = alpha.x;
-  if (!(xn == 0.0 && alpha.y == 0.0)) {
-    beta = -copysign(sqrt(alpha.x * alpha.x + alpha.y * alpha.y + xn), alpha.x);
-    t = make_double2((beta - alpha.x) / beta, -alpha.y / beta);
-    sc = cinv(make_double2(alpha.x - beta, alpha.y));
-  }
-  // v_i, v_{i-1}, w_{i-1} at index x >= i + 1
-  auto vnew = [&](int x, double2 px, double2 cx, double2 vx) {
-    return x == i + 1 ? make_double2(1.0, 0.0) : cmul(csub(csub(cx, cmul(tp, px)), cmul(bu, vx)), sc);
-  };
+  __shared__ double sx[4];
+  const ColScal cs = col_scalars(n, i, pfin, colfin, vp, gpart, ngp, tau[(int64_t)k * n + i - 1], sx);
+  const double2 tp = cs.tp, al = cs.al;
+  auto vnew = [&](int x, double2 px, double2 cx, double2 vx) { return col_vnew(cs, x, i, px, cx, vx); };
   __shared__ double2 cv[64], cva[64], cwa[64], csum[64];
   __shared__ double2 colc[64][65];
   __shared__ double2 rowp[4][64];
@@ -627,9 +694,9 @@ __global__ __launch_bounds__(256) void k_eig_pass1f(double2* __restrict__ A, int
     if (R == t0) {
       for (int r = tid; r < t0 * kEigTB && r <= i; r += 256) A[r + (int64_t)i * n] = cz();
       if (tid == 0) {
-        d[(int64_t)k * n + i] = ci.x;
-        e[(int64_t)k * n + i] = beta;
-        tau[(int64_t)k * n + i] = t;
+        d[(int64_t)k * n + i] = cs.di;
+        e[(int64_t)k * n + i] = cs.beta;
+        tau[(int64_t)k * n + i] = cs.t;
       }
     }
   }
@@ -1207,8 +1274,10 @@ void launch_eig_pass(double2* A, int n, int i, int64_t sA, double2* part, int64_
   if (K == 1)
     hipLaunchKernelGGL(k_eig_pass1, dim3(nT * (nT + 1) / 2, m), dim3(256), 0, s, A, n, i, sA, part, sP, vv, ww, t0);
   else
-    hipLaunchKernelGGL(k_eig_pass<KD>, dim3(nT * (nT + 1) / 2, m), dim3(256), 0, s, A, n, i, sA, part, sP, vv, ww,
-                       t0, dpart, T, K);
+    hipLaunchKernelGGL((k_eig_pass<KD, false>), dim3(nT * (nT + 1) / 2, m), dim3(256), 0, s, A, n, i, sA, part, sP,
+                       const_cast<double2*>(vv), const_cast<double2*>(ww), t0, dpart, T, K, (const double2*)nullptr,
+                       (const double2*)nullptr, (const double2*)nullptr, 0, (double*)nullptr, (double*)nullptr,
+                       (double2*)nullptr);
 }
 
 // Column i of the reduction: one matrix (K = 1) folds step i into pass i for
@@ -1218,14 +1287,21 @@ void launch_eig_column(double2* A, int n, int i, int64_t sA, double2* part, int6
                        double2* colfin, double2* vv, double2* ww, double* d, double* e, double2* tau,
                        double2* dpart, double2* gpart, int m, hipStream_t s) {
   const int K = eig_defer_k(m);
+  // DWHMC_EIG_FUSED: 0 none, 1 one matrix only, 2 (default) every batch
   const char* ef = std::getenv("DWHMC_EIG_FUSED");
-  if (K == 1 && i >= 1 && i <= n - 2 && !(ef && *ef == '0')) {
+  const int fz = ef ? std::atoi(ef) : 2;
+  if (i >= 1 && i <= n - 2 && (K == 1 ? fz >= 1 : fz >= 2)) {
     const int ngp = (n - i + 255) / 256;
     hipLaunchKernelGGL(k_eig_reduce, dim3(ngp, m), dim3(256), 0, s, part, sP, n, i, pfin, A, sA, colfin, vv, ww,
                        dpart, K, (const double2*)tau, gpart);
     const int T = (n + kEigTB - 1) / kEigTB, t0 = (i + 1) / kEigTB, nT = T - t0;
-    hipLaunchKernelGGL(k_eig_pass1f, dim3(nT * (nT + 1) / 2, m), dim3(256), 0, s, A, n, i, sA, part, sP, vv, pfin,
-                       colfin, gpart, ngp, d, e, tau, t0);
+    if (K == 1)
+      hipLaunchKernelGGL(k_eig_pass1f, dim3(nT * (nT + 1) / 2, m), dim3(256), 0, s, A, n, i, sA, part, sP, vv, pfin,
+                         colfin, gpart, ngp, d, e, tau, t0);
+    else
+      hipLaunchKernelGGL((k_eig_pass<KD, true>), dim3(nT * (nT + 1) / 2, m), dim3(256), 0, s, A, n, i, sA, part, sP,
+                         vv, ww, t0, dpart, T, K, (const double2*)pfin, (const double2*)colfin,
+                         (const double2*)gpart, ngp, d, e, tau);
     return;
   }
   launch_eig_step(A, n, i, sA, part, sP, pfin, colfin, vv, ww, d, e, tau, dpart, m, s);
