@@ -1287,9 +1287,9 @@ void launch_eig_column(double2* A, int n, int i, int64_t sA, double2* part, int6
                        double2* colfin, double2* vv, double2* ww, double* d, double* e, double2* tau,
                        double2* dpart, double2* gpart, int m, hipStream_t s) {
   const int K = eig_defer_k(m);
-  // DWHMC_EIG_FUSED: 0 none, 1 one matrix only, 2 (default) every batch
+  // DWHMC_EIG_FUSED: 0 (default) none, 1 one matrix only, 2 every batch
   const char* ef = std::getenv("DWHMC_EIG_FUSED");
-  const int fz = ef ? std::atoi(ef) : 2;
+  const int fz = ef ? std::atoi(ef) : 0;
   if (i >= 1 && i <= n - 2 && (K == 1 ? fz >= 1 : fz >= 2)) {
     const int ngp = (n - i + 255) / 256;
     hipLaunchKernelGGL(k_eig_reduce, dim3(ngp, m), dim3(256), 0, s, part, sP, n, i, pfin, A, sA, colfin, vv, ww,
