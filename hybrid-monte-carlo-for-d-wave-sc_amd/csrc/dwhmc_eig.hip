@@ -349,27 +349,17 @@ __device__ __forceinline__ double2 col_wnew(const ColScal& q, double2 px, double
   return cadd(cmul(q.tp, px), cmul(q.al, vx));
 }
 
-// FUSED (1 <= i <= n-2): step i folded in, as in k_eig_pass1f — the column
-// scalars from k_eig_reduce's partials (col_scalars), v_i and the newest
-// pair's w_{i-1} formed on the tile's rows and columns, the diagonal tiles
-// writing v_i, w_{i-1}, column i (tile t0 also d, e, tau).
-template <int KM, bool FUSED>   // most pending pairs (kEigDeferMax; K = 1 runs k_eig_pass1 / 1f)
+template <int KM>   // most pending pairs (kEigDeferMax; K = 1 runs k_eig_pass1 / 1f)
 __global__ __launch_bounds__(256) void k_eig_pass(double2* __restrict__ A, int n, int i, int64_t sA,
                                                   double2* __restrict__ part, int64_t sP,
-                                                  double2* __restrict__ vv, double2* __restrict__ ww,
-                                                  int t0, double2* __restrict__ dpart, int T, int K,
-                                                  const double2* __restrict__ pfin,
-                                                  const double2* __restrict__ colfin,
-                                                  const double2* __restrict__ gpart, int ngp,
-                                                  double* __restrict__ d, double* __restrict__ e,
-                                                  double2* __restrict__ tau) {
+                                                  const double2* __restrict__ vv, const double2* __restrict__ ww,
+                                                  int t0, double2* __restrict__ dpart, int T, int K) {
   const int k = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   A += k * sA;
   part += k * sP;
   vv += (int64_t)k * kEigRing * n;
   ww += (int64_t)k * kEigRing * n;
-  double2* v = vv + (int64_t)(i % kEigRing) * n;
-  const double2* vp = vv + (int64_t)((i + kEigRing - 1) % kEigRing) * n;   // v_{i-1}
+  const double2* v = vv + (int64_t)(i % kEigRing) * n;
   const bool wp = eig_write_pass(i, K);
   const int f = eig_pend_first(i, K), np = i - f;   // pending pairs f .. i-1 (<= KM)
   int R, C;
@@ -378,7 +368,6 @@ __global__ __launch_bounds__(256) void k_eig_pass(double2* __restrict__ A, int n
   C += t0;
   __shared__ double2 cv[64], csum[64];
   __shared__ double2 rowp[4][64];
-  __shared__ double sx[4];
   // the pending pairs' column values (write pass) and the column-sum
   // transpose; for KM > 2 one LDS region, the two phases split by a barrier
   constexpr bool kAlias = KM > 2;   // (KM <= 2: a separate region)
@@ -388,62 +377,29 @@ __global__ __launch_bounds__(256) void k_eig_pass(double2* __restrict__ A, int n
   double2* cpw = cpv + KM * 64;                  // [KM][64]: w_j
   const int gr = R * kEigTB + lane;
   const bool rok = gr >= i + 1 && gr < n;
-  ColScal cs{};
-  if (FUSED) {
-    pfin += (int64_t)k * n;
-    colfin += (int64_t)k * n;
-    gpart += (int64_t)k * kEigGP * 3;
-    cs = col_scalars(n, i, pfin, colfin, vp, gpart, ngp, tau[(int64_t)k * n + i - 1], sx);
-  }
-  // v_i and the newest pair's w_{i-1} at index x (FUSED: formed here)
-  auto vi_at = [&](int x) {
-    if (!FUSED) return v[x];
-    return col_vnew(cs, x, i, pfin[x], colfin[x], vp[x]);
-  };
-  auto pair_at = [&](int q, int x, double2& pv, double2& pw) {
-    const int sl = (f + q) % kEigRing;
-    pv = vv[(int64_t)sl * n + x];
-    pw = FUSED && f + q == i - 1 ? col_wnew(cs, pfin[x], pv) : ww[(int64_t)sl * n + x];
-  };
   if (tid < 64) {
     const int gc = C * kEigTB + tid;
-    cv[tid] = gc >= i + 1 && gc < n ? vi_at(gc) : cz();
+    cv[tid] = gc >= i + 1 && gc < n ? v[gc] : cz();
   }
   if (wp) {
     for (int q = w; q < np; q += 4) {   // wave w stages pairs w, w+4
-      const int gc = C * kEigTB + lane;
-      double2 pv = cz(), pw = cz();
-      if (gc >= i + 1 && gc < n) pair_at(q, gc, pv, pw);
-      cpv[q * 64 + lane] = pv;
-      cpw[q * 64 + lane] = pw;
+      const int sl = (f + q) % kEigRing, gc = C * kEigTB + lane;
+      const bool ok = gc >= i + 1 && gc < n;
+      cpv[q * 64 + lane] = ok ? vv[(int64_t)sl * n + gc] : cz();
+      cpw[q * 64 + lane] = ok ? ww[(int64_t)sl * n + gc] : cz();
     }
   }
-  const double2 vr = rok ? vi_at(gr) : cz();
+  const double2 vr = rok ? v[gr] : cz();
   // the pending pairs at this lane's row: the write pass's update, or a read
   // pass's dots (diagonal tiles), loaded with the tile
   const bool rowpairs = wp || R == C;
   double2 rv[KM], rw[KM];
 #pragma unroll
   for (int q = 0; q < KM; ++q) {
-    rv[q] = rw[q] = cz();
-    if (rowpairs && rok && q < np) pair_at(q, gr, rv[q], rw[q]);
-  }
-  if (FUSED && R == C) {   // v_i, w_{i-1} and column i of A on this tile's rows
-    if (rok) {
-      v[gr] = vr;
-      A[gr + (int64_t)i * n] = vr;
-      ww[(int64_t)((i + kEigRing - 1) % kEigRing) * n + gr] = col_wnew(cs, pfin[gr], vp[gr]);
-    } else if (gr < n && gr <= i) {
-      A[gr + (int64_t)i * n] = cz();
-    }
-    if (R == t0) {
-      for (int r = tid; r < t0 * kEigTB && r <= i; r += 256) A[r + (int64_t)i * n] = cz();
-      if (tid == 0) {
-        d[(int64_t)k * n + i] = cs.di;
-        e[(int64_t)k * n + i] = cs.beta;
-        tau[(int64_t)k * n + i] = cs.t;
-      }
-    }
+    const int sl = (f + q) % kEigRing;
+    const bool ok = rowpairs && rok && q < np;
+    rv[q] = ok ? vv[(int64_t)sl * n + gr] : cz();
+    rw[q] = ok ? ww[(int64_t)sl * n + gr] : cz();
   }
   __syncthreads();
   constexpr int NCW = kEigTB / 4;   // columns per wave
@@ -1274,10 +1230,8 @@ void launch_eig_pass(double2* A, int n, int i, int64_t sA, double2* part, int64_
   if (K == 1)
     hipLaunchKernelGGL(k_eig_pass1, dim3(nT * (nT + 1) / 2, m), dim3(256), 0, s, A, n, i, sA, part, sP, vv, ww, t0);
   else
-    hipLaunchKernelGGL((k_eig_pass<KD, false>), dim3(nT * (nT + 1) / 2, m), dim3(256), 0, s, A, n, i, sA, part, sP,
-                       const_cast<double2*>(vv), const_cast<double2*>(ww), t0, dpart, T, K, (const double2*)nullptr,
-                       (const double2*)nullptr, (const double2*)nullptr, 0, (double*)nullptr, (double*)nullptr,
-                       (double2*)nullptr);
+    hipLaunchKernelGGL(k_eig_pass<KD>, dim3(nT * (nT + 1) / 2, m), dim3(256), 0, s, A, n, i, sA, part, sP, vv, ww,
+                       t0, dpart, T, K);
 }
 
 // Column i of the reduction: one matrix (K = 1) folds step i into pass i for
@@ -1287,21 +1241,18 @@ void launch_eig_column(double2* A, int n, int i, int64_t sA, double2* part, int6
                        double2* colfin, double2* vv, double2* ww, double* d, double* e, double2* tau,
                        double2* dpart, double2* gpart, int m, hipStream_t s) {
   const int K = eig_defer_k(m);
-  // DWHMC_EIG_FUSED: 0 (default) none, 1 one matrix only, 2 every batch
+  // DWHMC_EIG_FUSED=0: step + pass for one matrix too (A/B).  (Batches keep
+  // the step: folding it into the deferred pass measured slower, every pass
+  // workgroup re-reading the column's vectors: 14.1 vs 13.2 ms per
+  // measurement at 16 snapshots, profiles/r04_exp_eig_fused_step.txt.)
   const char* ef = std::getenv("DWHMC_EIG_FUSED");
-  const int fz = ef ? std::atoi(ef) : 0;
-  if (i >= 1 && i <= n - 2 && (K == 1 ? fz >= 1 : fz >= 2)) {
+  if (K == 1 && i >= 1 && i <= n - 2 && !(ef && *ef == '0')) {
     const int ngp = (n - i + 255) / 256;
     hipLaunchKernelGGL(k_eig_reduce, dim3(ngp, m), dim3(256), 0, s, part, sP, n, i, pfin, A, sA, colfin, vv, ww,
                        dpart, K, (const double2*)tau, gpart);
     const int T = (n + kEigTB - 1) / kEigTB, t0 = (i + 1) / kEigTB, nT = T - t0;
-    if (K == 1)
-      hipLaunchKernelGGL(k_eig_pass1f, dim3(nT * (nT + 1) / 2, m), dim3(256), 0, s, A, n, i, sA, part, sP, vv, pfin,
-                         colfin, gpart, ngp, d, e, tau, t0);
-    else
-      hipLaunchKernelGGL((k_eig_pass<KD, true>), dim3(nT * (nT + 1) / 2, m), dim3(256), 0, s, A, n, i, sA, part, sP,
-                         vv, ww, t0, dpart, T, K, (const double2*)pfin, (const double2*)colfin,
-                         (const double2*)gpart, ngp, d, e, tau);
+    hipLaunchKernelGGL(k_eig_pass1f, dim3(nT * (nT + 1) / 2, m), dim3(256), 0, s, A, n, i, sA, part, sP, vv, pfin,
+                       colfin, gpart, ngp, d, e, tau, t0);
     return;
   }
   launch_eig_step(A, n, i, sA, part, sP, pfin, colfin, vv, ww, d, e, tau, dpart, m, s);
