@@ -154,7 +154,7 @@ __global__ __launch_bounds__(256) void k_eig_reduce(const double2* __restrict__ 
     // g = sum conj(x_r) v_r (x = tau p, rows >= i), and for the norm of the
     // updated column c = a - bu v (a = c0 - x) over the rows >= i+2:
     // S1 = sum |a|^2, S2 = sum conj(v) a, S3 = sum |v|^2
-    __shared__ double2 sg[4], s12[4], s23[4];
+    __shared__ double2 sg[3][kStepT / 64];
     const double2 tp = tau[(int64_t)k * n + i - 1];
     const double2 x = cmul(tp, s);
     const double2 v = ok ? vv[(int64_t)((i + kEigRing - 1) % kEigRing) * n + r] : cz();
@@ -165,10 +165,28 @@ __global__ __launch_bounds__(256) void k_eig_reduce(const double2* __restrict__ 
       s1 = make_double2(av.x * av.x + av.y * av.y, v.x * v.x + v.y * v.y);      // (S1, S3)
       s2 = make_double2(v.x * av.x + v.y * av.y, v.x * av.y - v.y * av.x);      // conj(v) a
     }
-    gq = group_sum2(gq, sg);
-    s1 = group_sum2(s1, s12);
-    s2 = group_sum2(s2, s23);
+    // the three sums in one workgroup reduction (wave trees, then the waves
+    // in index order: one barrier)
+    gq.x = wave_sum(gq.x);
+    gq.y = wave_sum(gq.y);
+    s1.x = wave_sum(s1.x);
+    s1.y = wave_sum(s1.y);
+    s2.x = wave_sum(s2.x);
+    s2.y = wave_sum(s2.y);
+    const int wv = tid >> 6, nw = blockDim.x >> 6;
+    if ((tid & 63) == 0) {
+      sg[0][wv] = gq;
+      sg[1][wv] = s1;
+      sg[2][wv] = s2;
+    }
+    __syncthreads();
     if (tid == 0) {
+      gq = s1 = s2 = cz();
+      for (int q = 0; q < nw; ++q) {
+        gq = cadd(gq, sg[0][q]);
+        s1 = cadd(s1, sg[1][q]);
+        s2 = cadd(s2, sg[2][q]);
+      }
       double2* gp = gpart + ((int64_t)k * kEigGP + blockIdx.x) * 3;
       gp[0] = gq;
       gp[1] = s1;
