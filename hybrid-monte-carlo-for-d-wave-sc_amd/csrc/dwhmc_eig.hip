@@ -630,32 +630,36 @@ __global__ __launch_bounds__(256) void k_eig_pass1f(double2* __restrict__ A, int
     act |= (unsigned)ok << u;
     a[u] = ok ? A[gr + (int64_t)gc * n] : cz();
   }
+  // this workgroup's column / row inputs, loaded before the scalars they
+  // combine with (independent loads: one round trip)
+  const int gcs = C * kEigTB + (tid & 63);
+  const bool cok = tid < 64 && gcs >= i + 1 && gcs < n;
+  double2 pc = cz(), cc0 = cz(), vc = cz(), pr0 = cz(), cr0 = cz(), var = cz();
+  if (cok) {
+    pc = pfin[gcs];
+    cc0 = colfin[gcs];
+    vc = vp[gcs];
+  }
+  if (rok) {
+    pr0 = pfin[gr];
+    cr0 = colfin[gr];
+    var = vp[gr];
+  }
   // scalars of column i (zhetd2 'L': x = tau p, w = x - 1/2 tau (x^H v) v)
   __shared__ double sx[4];
   const ColScal cs = col_scalars(n, i, pfin, colfin, vp, gpart, ngp, tau[(int64_t)k * n + i - 1], sx);
   const double2 tp = cs.tp, al = cs.al;
-  auto vnew = [&](int x, double2 px, double2 cx, double2 vx) { return col_vnew(cs, x, i, px, cx, vx); };
   __shared__ double2 cv[64], cva[64], cwa[64], csum[64];
   __shared__ double2 colc[64][65];
   __shared__ double2 rowp[4][64];
   if (tid < 64) {
-    const int gc = C * kEigTB + tid;
-    const bool ok = gc >= i + 1 && gc < n;
-    double2 pc = cz(), cc0 = cz(), vc = cz();
-    if (ok) {
-      pc = pfin[gc];
-      cc0 = colfin[gc];
-      vc = vp[gc];
-    }
-    cv[tid] = ok ? vnew(gc, pc, cc0, vc) : cz();
+    cv[tid] = cok ? col_vnew(cs, gcs, i, pc, cc0, vc) : cz();
     cva[tid] = vc;
-    cwa[tid] = ok ? cadd(cmul(tp, pc), cmul(al, vc)) : cz();
+    cwa[tid] = cok ? cadd(cmul(tp, pc), cmul(al, vc)) : cz();
   }
-  double2 vr = cz(), var = cz(), war = cz();
+  double2 vr = cz(), war = cz();
   if (rok) {
-    const double2 pr0 = pfin[gr], cr0 = colfin[gr];
-    var = vp[gr];
-    vr = vnew(gr, pr0, cr0, var);
+    vr = col_vnew(cs, gr, i, pr0, cr0, var);
     war = cadd(cmul(tp, pr0), cmul(al, var));
   }
   if (R == C) {   // column i of A and v_i on this tile's rows
