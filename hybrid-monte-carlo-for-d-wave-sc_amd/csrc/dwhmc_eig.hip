@@ -588,57 +588,6 @@ __global__ __launch_bounds__(256) void k_eig_pass1(double2* __restrict__ A, int 
   }
 }
 
-// Step i for batches (K > 1), 1 <= i <= n-2, spread over many workgroups:
-// every workgroup forms column i's scalars from k_eig_reduce's partials
-// (col_scalars: no reduction over the rows unless the norm expansion
-// cancels), then writes v_i, w_{i-1} and column i of A on its rows; workgroup
-// 0 also the rows above and d, e, tau.  Replaces the one-workgroup step and
-// its two block reductions.
-__global__ __launch_bounds__(256) void k_eig_stepw(double2* __restrict__ A, int n, int i, int64_t sA,
-                                                   double2* __restrict__ vv, double2* __restrict__ ww,
-                                                   const double2* __restrict__ pfin,
-                                                   const double2* __restrict__ colfin,
-                                                   const double2* __restrict__ gpart, int ngp,
-                                                   double* __restrict__ d, double* __restrict__ e,
-                                                   double2* __restrict__ tau) {
-  const int k = blockIdx.y, tid = threadIdx.x, r = i + blockIdx.x * 256 + tid;
-  A += k * sA;
-  vv += (int64_t)k * kEigRing * n;
-  ww += (int64_t)k * kEigRing * n;
-  pfin += (int64_t)k * n;
-  colfin += (int64_t)k * n;
-  gpart += (int64_t)k * kEigGP * 3;
-  const double2* vp = vv + (int64_t)((i + kEigRing - 1) % kEigRing) * n;   // v_{i-1}
-  double2* vcur = vv + (int64_t)(i % kEigRing) * n;
-  double2* wout = ww + (int64_t)((i + kEigRing - 1) % kEigRing) * n;        // w_{i-1}
-  double2 pr = cz(), cr = cz(), vr = cz();
-  if (r < n) {
-    pr = pfin[r];
-    cr = colfin[r];
-    vr = vp[r];
-  }
-  __shared__ double sx[4];
-  const ColScal cs = col_scalars(n, i, pfin, colfin, vp, gpart, ngp, tau[(int64_t)k * n + i - 1], sx);
-  if (r < n) {
-    wout[r] = col_wnew(cs, pr, vr);
-    if (r >= i + 1) {
-      const double2 v = col_vnew(cs, r, i, pr, cr, vr);
-      vcur[r] = v;
-      A[r + (int64_t)i * n] = v;
-    } else {
-      A[r + (int64_t)i * n] = cz();   // r = i
-    }
-  }
-  if (blockIdx.x == 0) {
-    for (int q = tid; q < i; q += 256) A[q + (int64_t)i * n] = cz();
-    if (tid == 0) {
-      d[(int64_t)k * n + i] = cs.di;
-      e[(int64_t)k * n + i] = cs.beta;
-      tau[(int64_t)k * n + i] = cs.t;
-    }
-  }
-}
-
 // One matrix (K = 1), 1 <= i <= n-2: step i folded into pass i.  Every
 // workgroup forms the scalars of column i itself from k_eig_reduce's
 // outputs — g (the reduce workgroups' partials, fixed order), w_{i-1}[i] and
@@ -1326,18 +1275,6 @@ void launch_eig_column(double2* A, int n, int i, int64_t sA, double2* part, int6
     const int T = (n + kEigTB - 1) / kEigTB, t0 = (i + 1) / kEigTB, nT = T - t0;
     hipLaunchKernelGGL(k_eig_pass1f, dim3(nT * (nT + 1) / 2, m), dim3(256), 0, s, A, n, i, sA, part, sP, vv, pfin,
                        colfin, gpart, ngp, d, e, tau, t0);
-    return;
-  }
-  // batches: the step spread over many workgroups (DWHMC_EIG_STEPW=0: the
-  // one-workgroup step, A/B)
-  const char* ew = std::getenv("DWHMC_EIG_STEPW");
-  if (K > 1 && i >= 1 && i <= n - 2 && !(ew && *ew == '0')) {
-    const int ngp = (n - i + 255) / 256;
-    hipLaunchKernelGGL(k_eig_reduce, dim3(ngp, m), dim3(256), 0, s, part, sP, n, i, pfin, A, sA, colfin, vv, ww,
-                       dpart, K, (const double2*)tau, gpart);
-    hipLaunchKernelGGL(k_eig_stepw, dim3(ngp, m), dim3(256), 0, s, A, n, i, sA, vv, ww, (const double2*)pfin,
-                       (const double2*)colfin, (const double2*)gpart, ngp, d, e, tau);
-    launch_eig_pass(A, n, i, sA, part, sP, vv, ww, dpart, m, s);
     return;
   }
   launch_eig_step(A, n, i, sA, part, sP, pfin, colfin, vv, ww, d, e, tau, dpart, m, s);
