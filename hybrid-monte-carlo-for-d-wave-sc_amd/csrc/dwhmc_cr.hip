@@ -472,6 +472,22 @@ __device__ __forceinline__ void tile_from_lds(const double2* T, d4& cr, d4& ci) 
   }
 }
 
+// site guard of launch_cr_inv0 (Σ_k |Δ| over each site's four bonds <= cap4)
+__device__ __forceinline__ void inv0_site_guard(const double2* __restrict__ D, const int* __restrict__ site4,
+                                                int N, double cap4, int* __restrict__ flag) {
+  bool over = false;
+  for (int i = threadIdx.x; i < N; i += blockDim.x) {
+    double sm = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const double2 v = D[site4[4 * i + k]];
+      sm += sqrt(fma(v.x, v.x, v.y * v.y));
+    }
+    over = over || !(sm <= cap4);
+  }
+  if (over) *flag = 1;
+}
+
 // gcol: the guard column's x (-1: no guard); arguments in first-use order
 __global__ __launch_bounds__(256) void k_cr_inv0(double2* __restrict__ pool, int64_t item,
                                                  const int* __restrict__ blk, const int* __restrict__ rblk,
@@ -488,19 +504,7 @@ __global__ __launch_bounds__(256) void k_cr_inv0(double2* __restrict__ pool, int
   // site guard (launch_cr_inv0 with Delta): the extra last workgroup column,
   // pole 0 of each chain, on a CU the inversions leave idle
   if (li == gcol) {
-    if (bi % P != 0) return;
-    const double2* D = Delta + (int64_t)(bi / P) * 2 * N;
-    bool over = false;
-    for (int i = threadIdx.x; i < N; i += blockDim.x) {
-      double sm = 0.0;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const double2 v = D[site4[4 * i + k]];
-        sm += sqrt(fma(v.x, v.x, v.y * v.y));
-      }
-      over = over || !(sm <= cap4);
-    }
-    if (over) *flag = 1;
+    if (bi % P == 0) inv0_site_guard(Delta + (int64_t)(bi / P) * 2 * N, site4, N, cap4, flag);
     return;
   }
   const double2* D = pool + (int64_t)bi * item + (int64_t)blk[li] * HP * BP;
@@ -619,6 +623,66 @@ __global__ __launch_bounds__(256) void k_cr_inv0(double2* __restrict__ pool, int
     ldpart[o] = 0.5 * ldA[o] + ldw[0] + ldw[1];
   }
   CR_STAMP(9);
+}
+
+// HP = 16 (BP = 32): every matrix is one tile and one wave does the whole
+// chain: Z = R B, S = A + B conj(Z), S^-1 (one register inversion), Y = Z
+// conj(X) -- one 16 x 16 inversion and three tile products where k_cr_inv<2>
+// runs two inversions and their panel updates.  LDS only carries tiles
+// between the wave's own lanes (the barriers are wave-local).
+__global__ __launch_bounds__(64) void k_cr_inv0_32(double2* __restrict__ pool, int64_t item,
+                                                   const int* __restrict__ blk, const int* __restrict__ rblk,
+                                                   const int* __restrict__ dst, int gcol,
+                                                   const int* __restrict__ slot, double* __restrict__ ldpart,
+                                                   const double* __restrict__ ldA, int nslots,
+                                                   const double2* __restrict__ Delta,
+                                                   const int* __restrict__ site4, int N, int P, double cap4,
+                                                   int* __restrict__ flag) {
+  constexpr int BP = 32, HP = 16, TSZ = 16 * 17;
+  __shared__ double2 sR[TSZ], sB[TSZ], sZ[TSZ], sX[TSZ];
+  const int bi = blockIdx.y, li = blockIdx.x;
+  if (li == gcol) {
+    if (bi % P == 0) inv0_site_guard(Delta + (int64_t)(bi / P) * 2 * N, site4, N, cap4, flag);
+    return;
+  }
+  const double2* D = pool + (int64_t)bi * item + (int64_t)blk[li] * HP * BP;
+  const double2* Rm = pool + (int64_t)bi * item + (int64_t)rblk[li] * HP * BP;
+  double2* Mo = pool + (int64_t)bi * item + (int64_t)dst[li] * HP * BP;
+  const int l = threadIdx.x, lr = l & 15, lk = l >> 4;
+  d4 sr, si;   // A, then S, then X = S^-1
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int row = lk + 4 * rr;
+    const double2 a = D[(int64_t)row * BP + lr];
+    sB[row * 17 + lr] = D[(int64_t)row * BP + HP + lr];
+    sR[row * 17 + lr] = Rm[(int64_t)row * BP + lr];
+    sr[rr] = a.x;
+    si[rr] = a.y;
+  }
+  __syncthreads();
+  d4 br, bim, zr = {0.0, 0.0, 0.0, 0.0}, zi = {0.0, 0.0, 0.0, 0.0};
+  tile_from_lds(sB, br, bim);
+  mma16_3m<false>(zr, zi, sR, br, bim);   // Z = R B
+  tile_to_lds(sZ, zr, zi);
+  __syncthreads();
+  tile_from_lds<true>(sZ, br, bim);
+  mma16_3m<false>(sr, si, sB, br, bim);   // S = A + B conj(Z)
+  const double ld = 0.5 * log(wave_inv16_c(sr, si));
+  tile_to_lds(sX, sr, si);
+  __syncthreads();
+  d4 yr = {0.0, 0.0, 0.0, 0.0}, yi = {0.0, 0.0, 0.0, 0.0};
+  tile_from_lds<true>(sX, br, bim);
+  mma16_3m<false>(yr, yi, sZ, br, bim);   // Y = Z conj(X)
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int row = lk + 4 * rr;
+    Mo[(int64_t)row * BP + lr] = make_double2(sr[rr], si[rr]);
+    Mo[(int64_t)row * BP + HP + lr] = make_double2(yr[rr], yi[rr]);
+  }
+  if (l == 0) {
+    const int64_t o = (int64_t)bi * nslots + slot[li];
+    ldpart[o] = 0.5 * ldA[o] + ld;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1053,14 +1117,15 @@ __global__ __launch_bounds__(256) void k_cr_fermion_energy(const double2* __rest
 // ---------------------------------------------------------------------------
 bool cr_supported_bp(int BP) { return BP == 32 || BP == 64 || BP == 96 || BP == 128; }
 bool cr_supported_side(int BP) { return BP == 64; }
-bool cr_supported_inv0(int BP) { return BP == 64; }
+bool cr_supported_inv0(int BP) { return BP == 64 || BP == 32; }
 
 void launch_cr_inv0(const CrDims& c, double2* pool, const int* blk, const int* rblk, const int* dst,
                     const int* slot, int n, double* ldpart, const double* ldA, hipStream_t s,
                     const double2* Delta, const int* site4, double cap4, int* flag) {
   if (n <= 0) return;
   const bool guard = Delta != nullptr && site4 != nullptr && flag != nullptr;
-  hipLaunchKernelGGL(k_cr_inv0, dim3(n + (guard ? 1 : 0), c.nbatch), dim3(256), 0, s, pool, c.item, blk, rblk,
+  hipLaunchKernelGGL(c.BP == 32 ? k_cr_inv0_32 : k_cr_inv0, dim3(n + (guard ? 1 : 0), c.nbatch),
+                     dim3(c.BP == 32 ? 64 : 256), 0, s, pool, c.item, blk, rblk,
                      dst, guard ? n : -1, slot, ldpart, ldA, c.Ly, guard ? Delta : nullptr, site4, c.N, c.P, cap4, flag);
 }
 

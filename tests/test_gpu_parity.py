@@ -544,9 +544,11 @@ def test_cr_block_limit(dwhmc, oracle):
 def test_cr_ragged_chains(dwhmc, oracle, Lx, Ly):
     """Cyclic-reduction chains of every shape: Ly = 1 (one block), 2 (single
     off-diagonal block), odd lengths at every level, padded blocks (2 Lx not a
-    multiple of 32), against the eigen oracle.  The BP = 64 cases (17 <= Lx <=
-    32) run the static-particle-block level-0 inversions (k_cr_inv0) and the
-    side-work schedule (k_cr_inv_side) on odd and short chains."""
+    multiple of 32), against the eigen oracle.  Every case runs the
+    static-particle-block level-0 inversions: k_cr_inv0_32 on the BP = 32
+    chains (Lx <= 16, one-wave Schur complement), k_cr_inv0 on the BP = 64
+    ones (17 <= Lx <= 32, which also run the side-work schedule,
+    k_cr_inv_side) on odd and short chains."""
     O = oracle
     p, dis, Delta = make_case(O, Lx, Ly, 8.0, seed=Lx * 31 + Ly)
     cache, F_ref, Ef_ref = O.evaluate(p, dis, Delta)
