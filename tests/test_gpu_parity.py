@@ -308,7 +308,8 @@ def _site_mean_max(D, p):
 
 def test_site_guard_default_cap(dwhmc, oracle):
     """CR contexts guard the mean |Δ| over each site's four bonds (checked by
-    the level-0 inversion launch: k_cr_inv0, k_cr_inv or k_cr_inv_side),
+    the level-0 inversion launch: k_cr_inv0 / k_cr_inv0_32, k_cr_inv or
+    k_cr_inv_side),
     default max(1.25, 4 sqrt(2J/β)); E' = ‖h‖ + 2 cap bounds the spectrum
     either way.  At the C3 workload that is 13 pole pairs instead of 14."""
     O = oracle
