@@ -1490,6 +1490,9 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
       c.nbatch = d.nbatch;
       c.nblk = ctx->plan.nblk;
       c.item = (int64_t)c.nblk * (BP / 2) * BP;
+      // DWHMC_CR_INV32=0: BP = 32 inversions by k_cr_inv<2> (A/B knob)
+      const char* e32 = std::getenv("DWHMC_CR_INV32");
+      c.inv32 = !(e32 && *e32 == '0');
       d.nld = Lyc;
       for (CrStage& st : ctx->plan.stages)
         if (st.kind == 1) st.cfg = dwh::cr_gemm_config(c, st.n, st.maxt32, st.maxt16, st.ntmax, st.ntiles);

@@ -630,34 +630,48 @@ __global__ __launch_bounds__(256) void k_cr_inv0(double2* __restrict__ pool, int
 // conj(X) -- one 16 x 16 inversion and three tile products where k_cr_inv<2>
 // runs two inversions and their panel updates.  LDS only carries tiles
 // between the wave's own lanes (the barriers are wave-local).
-__global__ __launch_bounds__(64) void k_cr_inv0_32(double2* __restrict__ pool, int64_t item,
-                                                   const int* __restrict__ blk, const int* __restrict__ rblk,
-                                                   const int* __restrict__ dst, int gcol,
-                                                   const int* __restrict__ slot, double* __restrict__ ldpart,
-                                                   const double* __restrict__ ldA, int nslots,
-                                                   const double2* __restrict__ Delta,
-                                                   const int* __restrict__ site4, int N, int P, double cap4,
-                                                   int* __restrict__ flag) {
+// STATIC: R = A^-1 from the static block rblk (ln|det A| = ldA / 2); else R
+// is A^-1 formed here (k_cr_inv32: any M-form block, the same Schur
+// complement after one more register inversion; no pivoting, as i A is a
+// principal block of i D).  In place when dst == blk: every read precedes
+// the wave's first store.
+template <bool STATIC>
+__device__ __forceinline__ void cr_inv32_wave(double2* __restrict__ pool, int64_t item, int bi, int li,
+                                              const int* __restrict__ blk, const int* __restrict__ rblk,
+                                              const int* __restrict__ dst, const int* __restrict__ slot,
+                                              double* __restrict__ ldpart, const double* __restrict__ ldA,
+                                              int nslots) {
   constexpr int BP = 32, HP = 16, TSZ = 16 * 17;
   __shared__ double2 sR[TSZ], sB[TSZ], sZ[TSZ], sX[TSZ];
-  const int bi = blockIdx.y, li = blockIdx.x;
-  if (li == gcol) {
-    if (bi % P == 0) inv0_site_guard(Delta + (int64_t)(bi / P) * 2 * N, site4, N, cap4, flag);
-    return;
-  }
   const double2* D = pool + (int64_t)bi * item + (int64_t)blk[li] * HP * BP;
-  const double2* Rm = pool + (int64_t)bi * item + (int64_t)rblk[li] * HP * BP;
   double2* Mo = pool + (int64_t)bi * item + (int64_t)dst[li] * HP * BP;
   const int l = threadIdx.x, lr = l & 15, lk = l >> 4;
   d4 sr, si;   // A, then S, then X = S^-1
+  double ld = 0.0;
+  if constexpr (STATIC) {
+    const double2* Rm = pool + (int64_t)bi * item + (int64_t)rblk[li] * HP * BP;
 #pragma unroll
-  for (int rr = 0; rr < 4; ++rr) {
-    const int row = lk + 4 * rr;
-    const double2 a = D[(int64_t)row * BP + lr];
-    sB[row * 17 + lr] = D[(int64_t)row * BP + HP + lr];
-    sR[row * 17 + lr] = Rm[(int64_t)row * BP + lr];
-    sr[rr] = a.x;
-    si[rr] = a.y;
+    for (int rr = 0; rr < 4; ++rr) {
+      const int row = lk + 4 * rr;
+      const double2 a = D[(int64_t)row * BP + lr];
+      sB[row * 17 + lr] = D[(int64_t)row * BP + HP + lr];
+      sR[row * 17 + lr] = Rm[(int64_t)row * BP + lr];
+      sr[rr] = a.x;
+      si[rr] = a.y;
+    }
+    ld = 0.5 * ldA[(int64_t)bi * nslots + slot[li]];
+  } else {
+    d4 rr_, ri_;
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int row = lk + 4 * rr;
+      const double2 a = D[(int64_t)row * BP + lr];
+      sB[row * 17 + lr] = D[(int64_t)row * BP + HP + lr];
+      sr[rr] = rr_[rr] = a.x;
+      si[rr] = ri_[rr] = a.y;
+    }
+    ld = 0.5 * log(wave_inv16_c(rr_, ri_));   // R = A^-1
+    tile_to_lds(sR, rr_, ri_);
   }
   __syncthreads();
   d4 br, bim, zr = {0.0, 0.0, 0.0, 0.0}, zi = {0.0, 0.0, 0.0, 0.0};
@@ -667,7 +681,7 @@ __global__ __launch_bounds__(64) void k_cr_inv0_32(double2* __restrict__ pool, i
   __syncthreads();
   tile_from_lds<true>(sZ, br, bim);
   mma16_3m<false>(sr, si, sB, br, bim);   // S = A + B conj(Z)
-  const double ld = 0.5 * log(wave_inv16_c(sr, si));
+  ld += 0.5 * log(wave_inv16_c(sr, si));
   tile_to_lds(sX, sr, si);
   __syncthreads();
   d4 yr = {0.0, 0.0, 0.0, 0.0}, yi = {0.0, 0.0, 0.0, 0.0};
@@ -679,10 +693,37 @@ __global__ __launch_bounds__(64) void k_cr_inv0_32(double2* __restrict__ pool, i
     Mo[(int64_t)row * BP + lr] = make_double2(sr[rr], si[rr]);
     Mo[(int64_t)row * BP + HP + lr] = make_double2(yr[rr], yi[rr]);
   }
-  if (l == 0) {
-    const int64_t o = (int64_t)bi * nslots + slot[li];
-    ldpart[o] = 0.5 * ldA[o] + ld;
+  if (l == 0) ldpart[(int64_t)bi * nslots + slot[li]] = ld;
+}
+
+__global__ __launch_bounds__(64) void k_cr_inv0_32(double2* __restrict__ pool, int64_t item,
+                                                   const int* __restrict__ blk, const int* __restrict__ rblk,
+                                                   const int* __restrict__ dst, int gcol,
+                                                   const int* __restrict__ slot, double* __restrict__ ldpart,
+                                                   const double* __restrict__ ldA, int nslots,
+                                                   const double2* __restrict__ Delta,
+                                                   const int* __restrict__ site4, int N, int P, double cap4,
+                                                   int* __restrict__ flag) {
+  const int bi = blockIdx.y, li = blockIdx.x;
+  if (li == gcol) {
+    if (bi % P == 0) inv0_site_guard(Delta + (int64_t)(bi / P) * 2 * N, site4, N, cap4, flag);
+    return;
   }
+  cr_inv32_wave<true>(pool, item, bi, li, blk, rblk, dst, slot, ldpart, ldA, nslots);
+}
+
+// gcol: the guard column's x (-1: no guard), as k_cr_inv
+__global__ __launch_bounds__(64) void k_cr_inv32(double2* __restrict__ pool, int64_t item,
+                                                 const int* __restrict__ blk, const int* __restrict__ dst,
+                                                 int gcol, const int* __restrict__ slot,
+                                                 double* __restrict__ ldpart, int nslots, SiteGuard sg, int N,
+                                                 int P) {
+  const int bi = blockIdx.y, li = blockIdx.x;
+  if (li == gcol) {
+    if (bi % P == 0) site_guard_wg(sg, N, bi / P);
+    return;
+  }
+  cr_inv32_wave<false>(pool, item, bi, li, blk, nullptr, dst, slot, ldpart, nullptr, nslots);
 }
 
 // ---------------------------------------------------------------------------
@@ -1149,8 +1190,12 @@ void launch_cr_inv(const CrDims& c, double2* pool, const int* blk, const int* ds
   const int gcol = guard ? n : -1;
   switch (c.BP) {
     case 32:
-      hipLaunchKernelGGL(k_cr_inv<2>, g, dim3(128), 0, s, pool, c.item, blk, dst, gcol, slot, ldpart, c.Ly, sg, c.N,
-                         c.P);
+      if (c.inv32)
+        hipLaunchKernelGGL(k_cr_inv32, g, dim3(64), 0, s, pool, c.item, blk, dst, gcol, slot, ldpart, c.Ly, sg, c.N,
+                           c.P);
+      else
+        hipLaunchKernelGGL(k_cr_inv<2>, g, dim3(128), 0, s, pool, c.item, blk, dst, gcol, slot, ldpart, c.Ly, sg,
+                           c.N, c.P);
       break;
     case 64:
       hipLaunchKernelGGL(k_cr_inv<4>, g, dim3(256), 0, s, pool, c.item, blk, dst, gcol, slot, ldpart, c.Ly, sg, c.N,

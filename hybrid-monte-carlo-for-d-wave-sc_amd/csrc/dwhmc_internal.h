@@ -35,6 +35,7 @@ struct KickDrift {
 struct CrDims {
   int Lx, Ly, N, BP, P, nbatch, nblk;
   int64_t item;   // elements per batch item pool (nblk * HP * BP)
+  int inv32 = 1;  // BP = 32 inversions by the one-wave Schur complement (k_cr_inv32; else k_cr_inv<2>)
 };
 // out = [cin] + sg * sum_{h<nt} A_h B_h over pool block indices (cin = -1: zero),
 // computed only on the output rows [r0, r1) x columns [c0, c1) (rounded out to

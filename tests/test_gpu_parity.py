@@ -344,12 +344,15 @@ def test_site_guard_reselects_on_upload(dwhmc, oracle):
     ctx.close()
 
 
+@pytest.mark.parametrize("inv0", ["1", "0"])
 @pytest.mark.parametrize("Lx,Ly", [(20, 4), (40, 3), (12, 5)])
-def test_site_guard_reselects_mid_sweep(dwhmc, oracle, Lx, Ly):
+def test_site_guard_reselects_mid_sweep(dwhmc, oracle, monkeypatch, Lx, Ly, inv0):
     """Site guard: a trajectory whose drift takes a site mean past the cap is
     rerun from its start with re-selected poles (the level-0 inversion launch
-    sets the flag); the result equals a context built with the final cap and
+    sets the flag: k_cr_inv0 / k_cr_inv0_32, or with DWHMC_CR_INV0=0 k_cr_inv
+    / k_cr_inv32); the result equals a context built with the final cap and
     matches the oracle."""
+    monkeypatch.setenv("DWHMC_CR_INV0", inv0)
     O = oracle
     p, dis, Delta0 = make_case(O, Lx, Ly, 4.0, seed=22 + Lx, amp=0.0)
     rng = np.random.default_rng(23)
@@ -563,6 +566,29 @@ def test_cr_ragged_chains(dwhmc, oracle, Lx, Ly):
     assert abs(Ef - Ef_ref) <= 1e-11 * abs(Ef_ref), (Ef, Ef_ref)
     hole_ref = O.measure_observables(cache, p, Delta)["hole_conc"]
     assert abs(2.0 * ctx.hole_trace()[0] / p.N - 1.0 - hole_ref) <= 1e-11
+    ctx.close()
+
+
+@pytest.mark.parametrize("inv0,inv32", [("1", "1"), ("0", "1"), ("1", "0"), ("0", "0")])
+@pytest.mark.parametrize("Lx,Ly", [(12, 5), (16, 6), (8, 8), (20, 3)])
+def test_cr_inversion_variants(dwhmc, oracle, monkeypatch, Lx, Ly, inv0, inv32):
+    """The CR inversion kernels against the eigen oracle: level 0 from the
+    static particle block (k_cr_inv0_32 / k_cr_inv0, DWHMC_CR_INV0) or whole;
+    BP = 32 blocks by the one-wave Schur complement (k_cr_inv32,
+    DWHMC_CR_INV32) or the two-wave panel inversion (k_cr_inv<2>).  8 x 8
+    runs two-row BP = 32 blocks, 20 x 3 BP = 64 (k_cr_inv32 unused)."""
+    O = oracle
+    monkeypatch.setenv("DWHMC_CR_INV0", inv0)
+    monkeypatch.setenv("DWHMC_CR_INV32", inv32)
+    p, dis, Delta = make_case(O, Lx, Ly, 8.0, seed=Lx * 13 + Ly)
+    cache, F_ref, Ef_ref = O.evaluate(p, dis, Delta)
+    P_ref, _ = O.pairing_P(cache.U, cache.E_n, p)
+    ctx = device_ctx(dwhmc, p, dis, "cr")
+    ctx.set_pairing(Delta)
+    ctx.factorize()
+    assert np.max(np.abs(ctx.pairing()[0] - P_ref)) <= 1e-11
+    assert np.max(np.abs(ctx.forces()[0] - F_ref)) <= 1e-10 * (1 + np.max(np.abs(F_ref)))
+    assert abs(ctx.fermion_energy()[0] - Ef_ref) <= 1e-11 * abs(Ef_ref)
     ctx.close()
 
 
