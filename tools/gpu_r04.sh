@@ -4,7 +4,7 @@
 #   tscan   the published T scan's low-temperature rows (investigation, 8 chains)
 #   bench   the driver's command + C3 x200 + C2 + C5
 #   prof    rocprofv3 kernel stats + PMC traffic passes (tools/profile_round.sh) + step trace
-#   profc2  rocprofv3 kernel stats of the C2 bench (L = 16, beta = 8)
+#   profc2  rocprofv3 kernel stats of the C2 bench (L = 16, beta = 8; PROF_CFG / PROF_STEPS: another config)
 #   sq      SQ / MFMA-busy counters of the bench (tools/pmc_sq.sh) + the f64 MFMA peak micro
 #   c2rows  C2 with one and two lattice rows per CR block (DWHMC_CR_ROWS), alternated
 #   micro   tools/micro/inv16_variants and launch_floor (prebuilt in-tree)
@@ -59,7 +59,7 @@ PY
       rm -f "$R/gpurun_out/prof_$TAG/stats/run_kernel_trace.csv" ;;
     profc2)
       (export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/profc2" -o run -- \
-        python3 bench.py --config C2 --steps 200 --warmup 20 --no-cpu-baseline --no-c1 > "$O/profc2.json" 2> "$O/profc2.err") \
+        python3 bench.py --config ${PROF_CFG:-C2} --steps ${PROF_STEPS:-200} --warmup 20 --no-cpu-baseline --no-c1 > "$O/profc2.json" 2> "$O/profc2.err") \
         || { tail -20 "$O/profc2.err"; exit 1; }
       python3 tools/trace_step.py "$O/profc2/run_kernel_trace.csv" > "$O/step_c2.txt" || exit 1
       rm -f "$O/profc2/run_kernel_trace.csv"; tail -25 "$O/step_c2.txt" ;;
