@@ -625,6 +625,113 @@ __global__ __launch_bounds__(256) void k_cr_inv0(double2* __restrict__ pool, int
   CR_STAMP(9);
 }
 
+// HP = 48 (BP = 96): 3 x 3 tiles, one wave per tile (9 waves).  Z = R B,
+// S = A + B conj(Z) as tile products; S^-1 by block Gauss-Jordan over the
+// three diagonal tiles (pivot p: its wave inverts S_pp in registers, row p
+// <- S_pp^-1 S_pj, the rest S_ij -= S_ip S_pj, column p <- -S_ip S_pp^-1;
+// tiles meet in two alternating LDS buffers); Y = Z conj(X).  Three 16 x 16
+// register inversions on the chain instead of k_cr_inv<6>'s six, and a
+// quarter of its flops.  The R and B tiles' LDS becomes the Gauss-Jordan
+// buffers once S is formed.
+__global__ __launch_bounds__(576) void k_cr_inv0_96(double2* __restrict__ pool, int64_t item,
+                                                    const int* __restrict__ blk, const int* __restrict__ rblk,
+                                                    const int* __restrict__ dst, int gcol,
+                                                    const int* __restrict__ slot, double* __restrict__ ldpart,
+                                                    const double* __restrict__ ldA, int nslots,
+                                                    const double2* __restrict__ Delta,
+                                                    const int* __restrict__ site4, int N, int P, double cap4,
+                                                    int* __restrict__ flag) {
+  constexpr int BP = 96, HP = 48, TSZ = 16 * 17;
+  __shared__ double2 sZ[9][TSZ], s1[9][TSZ], s2[9][TSZ], sP[TSZ];
+  __shared__ double ldw[3];
+  const int bi = blockIdx.y, li = blockIdx.x;
+  if (li == gcol) {
+    if (bi % P == 0) inv0_site_guard(Delta + (int64_t)(bi / P) * 2 * N, site4, N, cap4, flag);
+    return;
+  }
+  const double2* D = pool + (int64_t)bi * item + (int64_t)blk[li] * HP * BP;
+  const double2* Rm = pool + (int64_t)bi * item + (int64_t)rblk[li] * HP * BP;
+  double2* Mo = pool + (int64_t)bi * item + (int64_t)dst[li] * HP * BP;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  const int ti = w / 3, tj = w - 3 * (w / 3);
+  d4 sr, si;   // A, then S, then (S^-1) tile (ti, tj)
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int row = ti * 16 + lk + 4 * rr, col = tj * 16 + lr;
+    const double2 a = D[(int64_t)row * BP + col];
+    s2[w][(lk + 4 * rr) * 17 + lr] = D[(int64_t)row * BP + HP + col];   // B
+    s1[w][(lk + 4 * rr) * 17 + lr] = Rm[(int64_t)row * BP + col];       // R
+    sr[rr] = a.x;
+    si[rr] = a.y;
+  }
+  __syncthreads();
+  d4 br, bim, zr = {0.0, 0.0, 0.0, 0.0}, zi = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {   // Z = R B
+    tile_from_lds(s2[3 * k + tj], br, bim);
+    mma16_3m<false>(zr, zi, s1[3 * ti + k], br, bim);
+  }
+  tile_to_lds(sZ[w], zr, zi);
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {   // S = A + B conj(Z)
+    tile_from_lds<true>(sZ[3 * k + tj], br, bim);
+    mma16_3m<false>(sr, si, s2[3 * ti + k], br, bim);
+  }
+  tile_to_lds(s1[w], sr, si);   // R is dead (read only before the last barrier)
+  __syncthreads();
+  double ld = 0.0;
+#pragma unroll
+  for (int p = 0; p < 3; ++p) {
+    double2(*cur)[TSZ] = (p & 1) ? s2 : s1;
+    double2(*nxt)[TSZ] = (p & 1) ? s1 : s2;
+    if (ti == p && tj == p) {
+      ld = 0.5 * log(wave_inv16_c(sr, si));
+      tile_to_lds(sP, sr, si);
+    }
+    __syncthreads();
+    if (ti == p && tj != p) {   // row p <- S_pp^-1 S_pj
+      d4 nr = {0.0, 0.0, 0.0, 0.0}, ni = {0.0, 0.0, 0.0, 0.0};
+      mma16_3m<false>(nr, ni, sP, sr, si);
+      sr = nr;
+      si = ni;
+      tile_to_lds(cur[w], sr, si);
+    }
+    __syncthreads();
+    if (ti != p && tj != p) {   // S_ij -= S_ip S_pj (old column p, new row p)
+      tile_from_lds(cur[3 * p + tj], br, bim);
+      mma16_3m<true>(sr, si, cur[3 * ti + p], br, bim);
+    } else if (ti != p) {       // column p <- -S_ip S_pp^-1
+      d4 nr = {0.0, 0.0, 0.0, 0.0}, ni = {0.0, 0.0, 0.0, 0.0};
+      tile_from_lds(sP, br, bim);
+      mma16_3m<true>(nr, ni, cur[w], br, bim);
+      sr = nr;
+      si = ni;
+    }
+    tile_to_lds(nxt[w], sr, si);
+    __syncthreads();
+  }
+  // X = S^-1 in s2 (p = 2 wrote nxt = s2); Y = Z conj(X)
+  d4 yr = {0.0, 0.0, 0.0, 0.0}, yi = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    tile_from_lds<true>(s2[3 * k + tj], br, bim);
+    mma16_3m<false>(yr, yi, sZ[3 * ti + k], br, bim);
+  }
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int row = ti * 16 + lk + 4 * rr, col = tj * 16 + lr;
+    Mo[(int64_t)row * BP + col] = make_double2(sr[rr], si[rr]);
+    Mo[(int64_t)row * BP + HP + col] = make_double2(yr[rr], yi[rr]);
+  }
+  if (l == 0 && ti == tj) ldw[ti] = ld;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int64_t o = (int64_t)bi * nslots + slot[li];
+    ldpart[o] = 0.5 * ldA[o] + ldw[0] + ldw[1] + ldw[2];
+  }
+}
+
 // HP = 16 (BP = 32): every matrix is one tile and one wave does the whole
 // chain: Z = R B, S = A + B conj(Z), S^-1 (one register inversion), Y = Z
 // conj(X) -- one 16 x 16 inversion and three tile products where k_cr_inv<2>
@@ -1158,16 +1265,17 @@ __global__ __launch_bounds__(256) void k_cr_fermion_energy(const double2* __rest
 // ---------------------------------------------------------------------------
 bool cr_supported_bp(int BP) { return BP == 32 || BP == 64 || BP == 96 || BP == 128; }
 bool cr_supported_side(int BP) { return BP == 64; }
-bool cr_supported_inv0(int BP) { return BP == 64 || BP == 32; }
+bool cr_supported_inv0(int BP) { return BP == 64 || BP == 32 || BP == 96; }
 
 void launch_cr_inv0(const CrDims& c, double2* pool, const int* blk, const int* rblk, const int* dst,
                     const int* slot, int n, double* ldpart, const double* ldA, hipStream_t s,
                     const double2* Delta, const int* site4, double cap4, int* flag) {
   if (n <= 0) return;
   const bool guard = Delta != nullptr && site4 != nullptr && flag != nullptr;
-  hipLaunchKernelGGL(c.BP == 32 ? k_cr_inv0_32 : k_cr_inv0, dim3(n + (guard ? 1 : 0), c.nbatch),
-                     dim3(c.BP == 32 ? 64 : 256), 0, s, pool, c.item, blk, rblk,
-                     dst, guard ? n : -1, slot, ldpart, ldA, c.Ly, guard ? Delta : nullptr, site4, c.N, c.P, cap4, flag);
+  hipLaunchKernelGGL(c.BP == 32 ? k_cr_inv0_32 : c.BP == 96 ? k_cr_inv0_96 : k_cr_inv0,
+                     dim3(n + (guard ? 1 : 0), c.nbatch), dim3(c.BP == 32 ? 64 : c.BP == 96 ? 576 : 256), 0, s, pool,
+                     c.item, blk, rblk, dst, guard ? n : -1, slot, ldpart, ldA, c.Ly, guard ? Delta : nullptr, site4,
+                     c.N, c.P, cap4, flag);
 }
 
 void launch_cr_fill(const CrDims& c, double2* pool, const int* list, int nlist, const int* hcol,

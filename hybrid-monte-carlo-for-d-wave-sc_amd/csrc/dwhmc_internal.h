@@ -93,7 +93,7 @@ struct SiteGuard {
 };
 void launch_cr_inv(const CrDims& c, double2* pool, const int* blk, const int* dst, const int* slot,
                    int n, double* ldpart, hipStream_t s, const SiteGuard& sg = SiteGuard{});
-// level-0 inversions of blocks blk[i] (BP = 64) from the static R = A^-1
+// level-0 inversions of blocks blk[i] (BP = 32, 64, 96) from the static R = A^-1
 // blocks rblk[i] (k_cr_inv0); ln|det| = ldA/2 + ln|det S| into ldpart slots
 bool cr_supported_inv0(int BP);
 // Delta != nullptr: one extra workgroup per chain checks the site guard
