@@ -552,7 +552,8 @@ def test_cr_ragged_chains(dwhmc, oracle, Lx, Ly):
     static-particle-block level-0 inversions: k_cr_inv0_32 on the BP = 32
     chains (Lx <= 16, one-wave Schur complement), k_cr_inv0 on the BP = 64
     ones (17 <= Lx <= 32, which also run the side-work schedule,
-    k_cr_inv_side) on odd and short chains."""
+    k_cr_inv_side), k_cr_inv0_96 on the BP = 96 ones (33 <= Lx <= 48) on odd
+    and short chains."""
     O = oracle
     p, dis, Delta = make_case(O, Lx, Ly, 8.0, seed=Lx * 31 + Ly)
     cache, F_ref, Ef_ref = O.evaluate(p, dis, Delta)
