@@ -51,6 +51,19 @@ TRAFFIC_FILES = [os.path.join(ROOT, "profiles", f) for f in ("r04_pmc_traffic.js
 # SQ counter passes (tools/pmc_sq.sh -> tools/pmc_mfma.py): executed MFMA work per launch
 MFMA_FILES = [os.path.join(ROOT, "profiles", f) for f in ("r04_sq_mfma_L32.json",)]
 CLOCK_GHZ = 2.4                # the clock PEAK_F64_TFLOPS is quoted at (1024 SIMDs x 32 flop/cycle)
+ASSEMBLY_REPS = 200            # warm assembly launches timed for `assembly`
+
+
+def inv_kernels(bp: int, coarse: bool) -> str:
+    """The plan's block-inversion kernels: level 0 from the
+    static particle block (k_cr_inv0 at BP = 64, k_cr_inv0_96 at 96,
+    k_cr_inv0_32 at 32); coarser levels k_cr_inv<BP/16>, at BP = 32 the
+    one-wave Schur complement k_cr_inv32 (the level-0 / coarse stages carrying
+    side work are reported under cr_inv_side)."""
+    l0 = {32: "k_cr_inv0_32", 64: "k_cr_inv0", 96: "k_cr_inv0_96"}.get(bp, f"k_cr_inv<{bp // 16}>")
+    if not coarse:
+        return l0
+    return l0 + " + " + ("k_cr_inv32" if bp == 32 else f"k_cr_inv<{bp // 16}>")
 
 
 def measured_traffic(kernel, L, beta, chains):
@@ -294,7 +307,11 @@ def main(argv=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    preset = PRESETS[a.config or ("C4" if world > 1 else "C3")]
+    # launched by torch.distributed.run (the driver's multi-GPU command; also at
+    # --nproc-per-node 1): the replica branch with its RCCL collectives runs
+    # for any world size, so the N = 1 run exercises the same code as N = 8
+    distributed = world > 1 or ("MASTER_ADDR" in os.environ and "WORLD_SIZE" in os.environ)
+    preset = PRESETS[a.config or ("C4" if distributed else "C3")]
     custom = any(getattr(a, k) not in (None, preset[k]) for k in ("L", "beta", "chains"))
     for k in ("L", "beta", "chains"):
         if getattr(a, k) is None:
@@ -306,7 +323,7 @@ def main(argv=None):
     # the default, RCCL over xGMI with one GPU per rank
     backend = os.environ.get("DWHMC_BENCH_BACKEND", "nccl")
     tdev = "cpu"
-    if world > 1:
+    if distributed:
         import torch
         import torch.distributed as dist
         if backend == "gloo":
@@ -395,7 +412,15 @@ def main(argv=None):
             ctx.run_sweeps(f, n, nt, dt, p.mass)
         ctx.synchronize()
         for k in names:
-            kern[k] = ctx.timing_read(k)
+            if k != "assemble":
+                kern[k] = ctx.timing_read(k)
+        # the assembly launch runs once per trajectory (inside one the force
+        # kernel scatters the drifted Δ itself): time it over many warm
+        # launches so the figure is the kernel's, not one cold launch's
+        ctx.timing_enable(["assemble"])
+        ctx.timing_reset()
+        ctx.bench_assembly(ASSEMBLY_REPS)
+        kern["assemble"] = ctx.timing_read("assemble")
         ctx.timing_enable(False)
     # observables gather over RCCL (the only collective): acceptance and <dH>
     obs = np.array([acc.mean(), dH.mean(), float(np.mean(np.exp(-dH)))], dtype=np.float64)
@@ -428,7 +453,7 @@ def main(argv=None):
             "config": {"workload": workload,
                        "L": a.L, "N": N, "bdg_dim": 2 * N, "beta": a.beta, "chains_per_gpu": a.chains,
                        "Nt": Nt, "dt": dt, "therm_sweeps": a.therm, "poles": P, "kappa": info["kappa"],
-                       "parallelism": f"replicas x{world}" if world > 1 else "single GPU"},
+                       "parallelism": f"replicas x{world}" if distributed else "single GPU"},
             "timed_trajectories": [{"sweeps": n, "Nt": nt} for _, n, nt in timed],
             "host_enqueue_ms": 1000.0 * t_enq,
             "warmup_sweeps": w_sw,
@@ -439,7 +464,10 @@ def main(argv=None):
             "ref_equiv_tflops": leap * (40.0 / 3.0) * (2 * N) ** 3 / el / 1e12,
             "dense_equiv_tflops": leap * P * 8.0 * N ** 3 / el / 1e12,
         }
-        if world > 1 and backend == "gloo":
+        if distributed:
+            rec["collectives"] = {"backend": dist.get_backend(), "device": tdev,
+                                  "ops": ["barrier", "all_reduce(max time)", "gather(observables)"]}
+        if distributed and backend == "gloo":
             rec["rehearsal"] = f"gloo collectives, {world} ranks on {torch.cuda.device_count()} GPU(s): not a scaling measurement"
         if not cr:
             rec["alg_tflops"] = rec["dense_equiv_tflops"]
@@ -462,11 +490,7 @@ def main(argv=None):
                 # the whole leapfrog step against the fp64 MFMA peak (north_star: >= 0.30 at L=32)
                 rec["alg_frac_of_peak"] = rec["alg_tflops"] / world / PEAK_F64_TFLOPS
                 nt = info["block"] // 16
-                # level-0 inversions: k_cr_inv0 (static particle block, BP = 64)
-                # when the plan has no plain k_cr_inv stage besides it
-                rec["cr_inv"] = {"bound": "latency",
-                                 "kernel": ("k_cr_inv0" if info["block"] == 64 else f"k_cr_inv<{nt}>")
-                                 + (f" + k_cr_inv<{nt}>" if info["block"] == 64 and ni > replay_steps else ""),
+                rec["cr_inv"] = {"bound": "latency", "kernel": inv_kernels(info["block"], ni > replay_steps),
                                  "launches_per_step": ni / replay_steps,
                                  "achieved_tflops": wi / (msi * 1e-3) / 1e12 if msi > 0 else None,
                                  "avg_launch_us": 1000.0 * msi / ni if ni else None,
@@ -513,7 +537,10 @@ def main(argv=None):
                 rec["assembly"] = {"bound": "hbm", "kernel": "k_cr_fill" if cr else "k_assemble",
                                    "achieved": gbs,
                                    "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS,
-                                   "bytes_per_launch": w / n, "avg_launch_us": 1000.0 * ms / n}
+                                   "bytes_per_launch": w / n, "avg_launch_us": 1000.0 * ms / n,
+                                   "launches_timed": n,
+                                   "what": f"{ASSEMBLY_REPS} back-to-back warm launches (dwh_bench_assembly) "
+                                           "after the timed region, HIP events per launch"}
         if world == 1 and not a.no_c1 and a.L != PRESETS["C1"]["L"]:
             rec["c1"] = c1_line(m, local)
         if not a.no_cpu_baseline and world == 1:

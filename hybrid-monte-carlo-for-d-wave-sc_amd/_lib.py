@@ -42,7 +42,7 @@ class dwh_info_t(C.Structure):
     _fields_ = [("N", C.c_int64), ("Np", C.c_int64), ("nchains", C.c_int64), ("npoles", C.c_int64),
                 ("kappa", C.c_double), ("e_bound", C.c_double), ("err_tanh", C.c_double),
                 ("delta_cap", C.c_double), ("device_bytes", C.c_int64), ("algo", C.c_int64),
-                ("block", C.c_int64)]
+                ("block", C.c_int64), ("eig_half", C.c_int64)]
 
 
 _P = C.c_void_p
@@ -81,6 +81,7 @@ SIGNATURES = {
     "dwh_timing_enable": (C.c_int, [_P, _I32]),
     "dwh_timing_read": (C.c_int, [_P, C.c_char_p, _DP, C.POINTER(_I64), _DP]),
     "dwh_timing_reset": (C.c_int, [_P]),
+    "dwh_bench_assembly": (C.c_int, [_P, _I64]),
     "dwh_eigensystem": (C.c_int, [_P, _I64, _P, _P]),
     "dwh_transport_grid": (C.c_int, [_D, _D, _D, C.POINTER(_I64), C.POINTER(_I64)]),
     "dwh_measure_transport": (C.c_int, [_P, _I64, _D, _D, _D, _DP, _DP, _P, _I64, _P, _P, _I64, _P]),

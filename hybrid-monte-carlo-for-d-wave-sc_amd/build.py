@@ -17,14 +17,21 @@ LIB = os.path.join(PKG, "libdwhmc.so")
 SOURCES = [os.path.join(CSRC, "dwhmc_kernels.hip"), os.path.join(CSRC, "dwhmc_cr.hip"),
            os.path.join(CSRC, "dwhmc_eig.hip"), os.path.join(CSRC, "dwhmc_gemm.hip"),
            os.path.join(CSRC, "dwhmc_transport.hip"), os.path.join(CSRC, "dwhmc_api.cpp")]
-# rocBLAS (zgemm / dgemm products of the eigensolver and J_mn) and rocSOLVER
-# (zheevd / zheev: opt-in via DWHMC_EIG_SOLVER, and the fallback) serve the
-# transport measurement and the eig path only
+# rocSOLVER (zheevd / zheev: opt-in via DWHMC_EIG_SOLVER for A/B runs) is the
+# only vendor library the measurement path can call; every product runs on the
+# library's own MFMA kernel (dwhmc_gemm.hip).  rocBLAS is linked for the
+# rocsolver handle only.
 LIBS = ["-L/opt/rocm/lib", "-lrocsolver", "-lrocblas", "-Wl,-rpath,/opt/rocm/lib"]
 DEPS = SOURCES + [os.path.join(CSRC, "dwhmc_internal.h"), os.path.join(CSRC, "dwhmc_device.h"),
                   os.path.join(CSRC, "pole_table.inc"), os.path.join(CSRC, "pole_table_eps5e-12.inc"),
                   os.path.join(ROOT, "include", "dwhmc.h")]
-ARCH = os.environ.get("DWHMC_OFFLOAD_ARCH", "gfx950")
+# gfx950 only: several kernels use more than the 64 KiB of LDS per workgroup
+# earlier CDNA parts allow (k_gemm<complex> 66.5 KiB, k_cr_inv0_96 ~119 KiB),
+# and the tiling is sized for CDNA4's 160 KiB per CU
+ARCH = "gfx950"
+if os.environ.get("DWHMC_OFFLOAD_ARCH", ARCH) != ARCH:
+    raise SystemExit(f"libdwhmc targets gfx950 (MI355X) only; DWHMC_OFFLOAD_ARCH="
+                     f"{os.environ['DWHMC_OFFLOAD_ARCH']} is not supported")
 
 
 def hipcc() -> str:

@@ -298,6 +298,10 @@ class FermionContext:
     def timing_reset(self):
         self._c(self._lib.dwh_timing_reset(self._h))
 
+    def bench_assembly(self, reps: int):
+        """dwh_bench_assembly: reps back-to-back assembly launches (timer "assemble")."""
+        self._c(self._lib.dwh_bench_assembly(self._h, int(reps)))
+
     def timing_read(self, name: str):
         ms = C.c_double()
         n = C.c_int64()

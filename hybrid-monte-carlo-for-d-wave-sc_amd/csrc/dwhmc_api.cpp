@@ -6,8 +6,9 @@
 //   * pairing pattern D[r, c] <- Δ[src]/2 with the reference's overwrite order
 //                                            (src/Hamiltonian.jl:55-86)
 //   * pole selection from the compiled table for κ = β E'/2; beyond the
-//     table the eigendecomposition path (algo eig: rocSOLVER zheevd per step,
-//     the reference's own diagonalize + compute_forces!)
+//     table the eigendecomposition path (algo eig: the library's own
+//     eigensolver per step, dwhmc_eig.hip — the reference's own diagonalize
+//     + compute_forces!)
 //   * the per-sweep launch sequence of hmc_sweep! (src/HMC.jl:71-144)
 // All arithmetic runs in the HIP kernels (dwhmc_kernels.hip); there is no CPU
 // fallback: a missing device is an error.
@@ -126,15 +127,9 @@ struct CrPlan {
 // (8 x 8: 4 blocks of two rows instead of 8 half-empty ones, one CR level
 // less).  Wider lattices keep one row per block: more rows would widen the
 // blocks, and at L = 16 two rows per block (BP 64) measured slower than one
-// (profiles/r04_exp_cr_two_row_blocks_C2.txt).  DWHMC_CR_ROWS = r forces r
-// (tests, A/B), falling back to the default when Ly % r != 0 or the block
-// r Lx is not a supported size.
+// (profiles/r04_exp_cr_two_row_blocks_C2.txt).
 int cr_rows_per_block(int64_t Lx, int64_t Ly) {
   auto ok = [&](int64_t r) { return r >= 1 && Ly % r == 0 && dwh::cr_supported_bp((int)(2 * ((r * Lx + 15) / 16 * 16))); };
-  if (const char* e = std::getenv("DWHMC_CR_ROWS")) {
-    const int r = std::atoi(e);
-    if (ok(r)) return r;
-  }
   int64_t r = std::max<int64_t>(1, 16 / Lx);
   while (r > 1 && !ok(r)) --r;
   return (int)r;
@@ -162,9 +157,9 @@ int cr_rows_per_block(int64_t Lx, int64_t Ly) {
 // to m = 4 (below that the stages are pure latency) and only where the
 // receiving inversion stage leaves a quarter of the ncu CUs idle (nbatch =
 // chains x poles inversion workgroups per block).
-// DWHMC_CR_SIDE_W (default 2): inversion stages between a level and the one
-// that runs its W products; DWHMC_CR_SIDE_M (default 4): smallest level size
-// m whose products move (A/B knobs; profiles/r02_exp_cr_side_work.txt).
+// side_woff = 2: inversion stages between a level and the one that runs its
+// W products; side_m = 4: smallest level size m whose products move
+// (profiles/r02_exp_cr_side_work.txt, r04_exp_cr_side_knobs_C3.txt).
 //
 // inv0: the level-0 inversions use static R = A^-1 blocks (k_cr_inv0), one
 // per eliminated row, computed at context creation.
@@ -177,14 +172,9 @@ int cr_rows_per_block(int64_t Lx, int64_t Ly) {
 // force reads changes (computed from Dcol below, not assumed diagonal).
 CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol, bool side, int nbatch,
                      int ncu, bool inv0) {
-  const int side_woff = [] {
-    const char* e = std::getenv("DWHMC_CR_SIDE_W");
-    return e ? std::max(1, std::atoi(e)) : 2;
-  }();
-  const int side_m = [] {
-    const char* e = std::getenv("DWHMC_CR_SIDE_M");
-    return e ? std::max(2, std::atoi(e)) : 4;
-  }();
+  // W products two inversion stages after their level, side work from m = 4
+  // (profiles/r02_exp_cr_side_work.txt, r04_exp_cr_side_knobs_C3.txt)
+  constexpr int side_woff = 2, side_m = 4;
   CrPlan pl;
   const int HP = BP / 2;
   int nblk = 3 * Ly;
@@ -689,11 +679,11 @@ struct dwh_ctx {
   // map column by column (half solve, c0 = N everywhere, no fallback):
   // transport's pair sums then run over half the pairs
   bool eig_ph = false;
+  int eig_ph_last = -1;    // dwh_info_t::eig_half: eig_ph of the last eigensolve (-1: none yet)
   double *d_eig_d = nullptr, *d_eig_e = nullptr, *d_eig_tn = nullptr;
 
   // timing
   int timing = 0;   // bitmask over TimerName (bit i = kTimerNames[i])
-  bool gj_pair = true;   // DWHMC_GJ_PAIR=0: one rank-64 update per pivot step (A/B knob)
   std::vector<TimingRec> recs;
   std::vector<hipEvent_t> pool;
   double t_ms[T_COUNT] = {0};
@@ -828,14 +818,7 @@ void run_gj(dwh_ctx* ctx, double2* M) {
   int cur = 0;
   for (int k = 0; k < d.nb;) {
     double2* colcopy = (k == 0) ? CpA[cur] : nullptr;
-    if (!ctx->gj_pair) {
-      double2* nxt = k + 1 < d.nb ? CpA[cur ^ 1] : nullptr;
-      gj_pivot(ctx, M, k, ctx->Pb1, ctx->XR1, colcopy, nxt);
-      dwh::GJPanelPtrs sg{CpA[cur], nullptr, ctx->XR1, nullptr, ctx->Pb1, nullptr, nullptr, nxt};
-      gj_update(ctx, M, k, 0, sg);
-      cur ^= 1;
-      k += 1;
-    } else if (k + 1 < d.nb) {
+    if (k + 1 < d.nb) {
       gj_pivot(ctx, M, k, ctx->Pb1, ctx->XR1, colcopy, nullptr);
       dwh::GJPanelPtrs e{CpA[cur], nullptr, ctx->XR1, nullptr, ctx->Pb1, nullptr, ctx->CpB, nullptr};
       gj_update(ctx, M, k, 1, e);
@@ -854,6 +837,26 @@ void run_gj(dwh_ctx* ctx, double2* M) {
   }
 }
 
+// The per-factorisation assembly launch (timer "assemble"), with its
+// algorithmic bytes.  CR: the pairing entries Δ/2 scattered into the level-0
+// blocks of every batch item (16 B each; no level-0 block is rewritten, CR
+// inverts them out of place); dense: S^T = -(h + z) - D^H R D written from R
+// (read R once, write S^T).
+void assembly_enqueue(dwh_ctx* ctx) {
+  if (ctx->algo == ALGO_CR) {
+    const dwh::CrDims& c = ctx->cr;
+    const CrPlan& pl = ctx->plan;
+    Scope s(ctx, T_ASSEMBLE,
+            (double)pl.fill_step.size() * 8.0 * c.BP * (double)c.BP * c.nbatch + 16.0 * (double)pl.n_ph * c.nbatch);
+    dwh::launch_cr_fill(c, ctx->bpool, ctx->d_fill_step, (int)pl.fill_step.size(), ctx->hcol, ctx->hval, ctx->Dcol,
+                        ctx->Dsrc, ctx->Delta, ctx->d_y, ctx->d_off_ph, ctx->stream);
+  } else {
+    const Dims& d = ctx->d;
+    Scope s(ctx, T_ASSEMBLE, (double)d.nbatch * 32.0 * d.N * (double)d.N);
+    dwh::launch_assemble(d, ctx->R, ctx->S, ctx->Dcol, ctx->Dv, ctx->hcol, ctx->hval, ctx->d_y, ctx->stream);
+  }
+}
+
 // level-0 blocks -> CR stages -> gather of the selected G entries
 void cr_enqueue(dwh_ctx* ctx) {
   const dwh::CrDims& c = ctx->cr;
@@ -864,15 +867,7 @@ void cr_enqueue(dwh_ctx* ctx) {
     // into the level-0 blocks of every batch item (16 B each)
     // inside a trajectory the previous step's force kernel already scattered
     // the drifted Δ into the pool (pairing_in_pool)
-    const CrPlan& pl = ctx->plan;
-    if (!ctx->pairing_in_pool) {
-      Scope s(ctx, T_ASSEMBLE,
-              (double)pl.fill_step.size() * 8.0 * c.BP * (double)c.BP * c.nbatch +
-                  16.0 * (double)pl.n_ph * c.nbatch);
-      dwh::launch_cr_fill(c, ctx->bpool, ctx->d_fill_step, (int)pl.fill_step.size(), ctx->hcol,
-                          ctx->hval, ctx->Dcol, ctx->Dsrc, ctx->Delta, ctx->d_y, ctx->d_off_ph,
-                          ctx->stream);
-    }
+    if (!ctx->pairing_in_pool) assembly_enqueue(ctx);
     ctx->pairing_in_pool = false;
   }
   const CrPlan& plan = ctx->plan;
@@ -927,9 +922,10 @@ TrSrc chains_src(const dwh_ctx* ctx, int64_t c0);
 int eigen_solve(dwh_ctx* ctx, const TrSrc& src, int m);
 int eigen_info_check(dwh_ctx* ctx, int m);
 
-// algo eig: zheevd of every chain's H_BdG (src/Hamiltonian.jl:96-114), ρ =
-// U diag(f) U^H by one batched zgemm, then P, Tr ρ_hh and E_f
-// (src/Observables.jl:14-62, src/HMC.jl:21-27) in k_eig_gather
+// algo eig: the library's eigensolver on every chain's H_BdG
+// (src/Hamiltonian.jl:96-114), ρ = U diag(f) U^H by one batched product, then
+// P, Tr ρ_hh and E_f (src/Observables.jl:14-62, src/HMC.jl:21-27) in
+// k_eig_gather
 void eig_enqueue(dwh_ctx* ctx) {
   const int N = ctx->d.N, n2 = 2 * N, nc = ctx->d.nc;
   if (int rc = eigen_solve(ctx, chains_src(ctx, 0), nc)) {
@@ -942,6 +938,11 @@ void eig_enqueue(dwh_ctx* ctx) {
   // rho = (U f) U^H, the library's own product
   dwh::gemm_z('N', 'C', n2, n2, n2, make_double2(1.0, 0.0), b.JU, n2, sA, b.U, n2, sA, make_double2(0.0, 0.0),
               b.Jmn, n2, sA, nc, ctx->stream);
+  if (hipGetLastError() != hipSuccess) {   // a refused launch surfaces at the next eig_check
+    ctx->err = "eig path: rho product launch failed";
+    ctx->async_rc = DWH_ERR_HIP;
+    return;
+  }
   dwh::launch_eig_gather(b.Jmn, b.E, N, nc, ctx->Dcol, ctx->bond_ij, ctx->beta, ctx->Pair, ctx->Ef, ctx->Trhh,
                          ctx->stream);
 }
@@ -977,12 +978,7 @@ void factorize_enqueue(dwh_ctx* ctx, const dwh::KickDrift& kd) {
     return;
   }
   dwh::launch_dvals(d, ctx->Dsrc, ctx->Delta, ctx->Dv, ctx->stream);
-  {
-    // algorithmic bytes: read R once, write S^T
-    Scope s(ctx, T_ASSEMBLE, (double)d.nbatch * 32.0 * d.N * (double)d.N);
-    dwh::launch_assemble(d, ctx->R, ctx->S, ctx->Dcol, ctx->Dv, ctx->hcol, ctx->hval, ctx->d_y,
-                         ctx->stream);
-  }
+  assembly_enqueue(ctx);
   run_gj(ctx, ctx->S);
   {
     Scope s(ctx, T_CONTRACT, (double)d.nbatch * 32.0 * d.N * (double)d.N);
@@ -1440,7 +1436,6 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
       ctx->tr_rowptr[r + 1] = (int)ctx->tr_col.size();
     }
   }
-  if (const char* e = std::getenv("DWHMC_GJ_PAIR")) ctx->gj_pair = std::atoi(e) != 0;
   ctx->kappa = kappa;
   ctx->Ebound = Ep;
   ctx->hmax = hmax;
@@ -2035,6 +2030,7 @@ int eigen_solve(dwh_ctx* ctx, const TrSrc& src, int m) {
   HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
   if (!bad && own && ctx->eig_half && (int)ctx->eig_c0h.size() == m)
     ctx->eig_ph = std::all_of(ctx->eig_c0h.begin(), ctx->eig_c0h.end(), [&](int c) { return c == ctx->d.N; });
+  ctx->eig_ph_last = ctx->eig_ph ? 1 : 0;
   if (bad) {
     Scope sc(ctx, T_EIG_VENDOR, m);
     rc = eigen_enqueue(ctx, src, m, true);
@@ -2280,6 +2276,17 @@ int dwh_info(dwh_ctx* ctx, dwh_info_t* out) {
   out->device_bytes = ctx->device_bytes;
   out->algo = ctx->algo;
   out->block = ctx->algo == ALGO_CR ? ctx->cr.BP : ctx->algo == ALGO_EIG ? 0 : kGJ;
+  out->eig_half = ctx->eig_ph_last;
+  return DWH_OK;
+}
+
+int dwh_bench_assembly(dwh_ctx* ctx, int64_t reps) {
+  if (!ctx || reps < 0) return fail(ctx, DWH_ERR_ARG, "dwh_bench_assembly: bad argument");
+  if (ctx->algo == ALGO_EIG) return fail(ctx, DWH_ERR_STATE, "dwh_bench_assembly: the eig path has no per-step assembly");
+  if (int rc = settle(ctx)) return rc;
+  for (int64_t r = 0; r < reps; ++r) assembly_enqueue(ctx);
+  HIPCHECK(ctx, hipGetLastError());
+  HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
   return DWH_OK;
 }
 
@@ -2335,7 +2342,6 @@ int reselect_poles(dwh_ctx* ctx, double new_cap) {
   ctx->dH = nullptr;
   ctx->ndraws = 0;
   n->timing = ctx->timing;
-  n->gj_pair = ctx->gj_pair;
   std::copy(ctx->t_ms, ctx->t_ms + T_COUNT, n->t_ms);
   std::copy(ctx->t_n, ctx->t_n + T_COUNT, n->t_n);
   std::copy(ctx->t_work, ctx->t_work + T_COUNT, n->t_work);

@@ -8,6 +8,10 @@
 
 #include <utility>
 
+// CDNA4 only: LDS footprints above 64 KiB per workgroup, f64 MFMA layouts of gfx950
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "libdwhmc device code targets gfx950 (MI355X) only"
+#endif
 
 namespace dwh {
 

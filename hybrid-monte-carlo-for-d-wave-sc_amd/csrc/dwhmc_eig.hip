@@ -27,11 +27,14 @@
 //  3. k_eig_invit: inverse iteration, T - lambda I = LU with partial pivoting
 //     streamed per thread (two solves from a fixed pseudo-random start,
 //     one thread per eigenvalue); k_eig_orth: the vectors of eigenvalue
-//     clusters (consecutive gaps <= 2.5e-4 ||T||, so every other pair is
-//     orthogonal to ~1e-12 already) orthonormalised by Cholesky QR, twice
-//     (exact degeneracies of clean lattices included).
-//     Then one symmetric orthogonalisation step over all vectors (the
-//     library's real products, dwhmc_gemm.hip, driven by dwhmc_api.cpp).
+//     clusters (consecutive gaps <= kEigClusterTol = 1e-6 ||T||)
+//     orthonormalised by Cholesky QR, twice (exact degeneracies of clean
+//     lattices included).  Every other pair is orthogonal only to
+//     ~eps ||T|| / gap <= ~2e-10 after inverse iteration; one symmetric
+//     (Löwdin) orthogonalisation step over all vectors (the library's real
+//     products, dwhmc_gemm.hip, driven by dwhmc_api.cpp) takes those overlaps
+//     to rounding.  (kEigZeroTol = 2.5e-4 ||T|| is a different tolerance: the
+//     particle-hole split point c0 below.)
 //     For H_BdG (the only matrices the library decomposes) steps 3-4 run on
 //     the upper half of the spectrum only: from c0 (n/2, or lower when the
 //     levels around zero are closer than kEigZeroTol, found on the host from
@@ -362,9 +365,6 @@ __device__ __forceinline__ ColScal col_scalars(int n, int i, const double2* __re
 // v_i and w_{i-1} at an index x >= i+1 from (p, c0, v_{i-1}) there
 __device__ __forceinline__ double2 col_vnew(const ColScal& q, int x, int i, double2 px, double2 cx, double2 vx) {
   return x == i + 1 ? make_double2(1.0, 0.0) : cmul(csub(csub(cx, cmul(q.tp, px)), cmul(q.bu, vx)), q.sc);
-}
-__device__ __forceinline__ double2 col_wnew(const ColScal& q, double2 px, double2 vx) {
-  return cadd(cmul(q.tp, px), cmul(q.al, vx));
 }
 
 template <int KM>   // most pending pairs (kEigDeferMax; K = 1 runs k_eig_pass1 / 1f)
@@ -1211,18 +1211,10 @@ __global__ __launch_bounds__(256) void k_eig_tw(const double2* __restrict__ Tb, 
 
 }  // namespace
 
-// batch size from which passes defer their pairs (DWHMC_EIG_DEFER_MIN
-// overrides kEigDeferMin), and the deferral depth K (DWHMC_EIG_DEFER_K
-// overrides kEigDefer, 1 .. kEigDeferMax); read at each launch
-int eig_defer_min() {
-  const char* e = std::getenv("DWHMC_EIG_DEFER_MIN");
-  return e ? std::max(1, std::atoi(e)) : kEigDeferMin;
-}
-int eig_defer_k(int m) {
-  if (m < eig_defer_min()) return 1;
-  const char* e = std::getenv("DWHMC_EIG_DEFER_K");
-  return e ? std::min(kEigDeferMax, std::max(1, std::atoi(e))) : kEigDefer;
-}
+// the deferral depth K of a batch of m matrices: kEigDefer from kEigDeferMin
+// matrices on (HBM-bound passes), 1 below (latency-bound;
+// profiles/r04_exp_eig_defer_*.json)
+int eig_defer_k(int m) { return m < kEigDeferMin ? 1 : kEigDefer; }
 
 void launch_eig_step(double2* A, int n, int i, int64_t sA, const double2* part, int64_t sP, double2* pfin,
                      double2* colfin, double2* vv, double2* ww, double* d, double* e, double2* tau,
@@ -1257,18 +1249,16 @@ void launch_eig_pass(double2* A, int n, int i, int64_t sA, double2* part, int64_
 }
 
 // Column i of the reduction: one matrix (K = 1) folds step i into pass i for
-// 1 <= i <= n-2 (k_eig_reduce with the g partials, then k_eig_pass1f;
-// DWHMC_EIG_FUSED=0: step + pass, A/B); else step i, then pass i.
+// 1 <= i <= n-2 (k_eig_reduce with the g partials, then k_eig_pass1f); else
+// step i, then pass i.
 void launch_eig_column(double2* A, int n, int i, int64_t sA, double2* part, int64_t sP, double2* pfin,
                        double2* colfin, double2* vv, double2* ww, double* d, double* e, double2* tau,
                        double2* dpart, double2* gpart, int m, hipStream_t s) {
   const int K = eig_defer_k(m);
-  // DWHMC_EIG_FUSED=0: step + pass for one matrix too (A/B).  (Batches keep
-  // the step: folding it into the deferred pass measured slower, every pass
-  // workgroup re-reading the column's vectors: 14.1 vs 13.2 ms per
-  // measurement at 16 snapshots, profiles/r04_exp_eig_fused_step.txt.)
-  const char* ef = std::getenv("DWHMC_EIG_FUSED");
-  if (K == 1 && i >= 1 && i <= n - 2 && !(ef && *ef == '0')) {
+  // Batches keep the step: folding it into the deferred pass measured slower,
+  // every pass workgroup re-reading the column's vectors: 14.1 vs 13.2 ms per
+  // measurement at 16 snapshots (profiles/r04_exp_eig_fused_step.txt).
+  if (K == 1 && i >= 1 && i <= n - 2) {
     const int ngp = (n - i + 255) / 256;
     hipLaunchKernelGGL(k_eig_reduce, dim3(ngp, m), dim3(256), 0, s, part, sP, n, i, pfin, A, sA, colfin, vv, ww,
                        dpart, K, (const double2*)tau, gpart);

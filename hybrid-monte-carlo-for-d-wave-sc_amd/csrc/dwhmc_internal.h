@@ -297,7 +297,6 @@ void launch_eig_theta(double2* U, int n, int64_t sA, const int* c0, int m, hipSt
 void launch_eig_zt_to_u(const double* Zt, double2* U, int n, int64_t sZ, int64_t sA, int m, hipStream_t s,
                         int j0 = 0);
 constexpr int kEigDeferMin = 4;             // batches from this many matrices defer their rank-2 pairs
-int eig_defer_min();                        // kEigDeferMin or DWHMC_EIG_DEFER_MIN
 int eig_defer_k(int m);                     // deferral depth for m matrices (1: none)
 constexpr int kEigGS = 8;                   // row slices of each block's Gram sum
 // compact-WY T of every reflector block; Gp: m x nblk x kEigGS x kEigNB^2 scratch

@@ -3,9 +3,10 @@
 //
 // This is the measurement path the reference runs every measure_transport_freq
 // sweeps (src/Simulation.jl:170-186), not the leapfrog hot path: the
-// eigenpairs come from rocSOLVER zheevd (zheev where it fails) and J_mn = U^H (J ⊕ J) U from rocBLAS
-// zgemm (dwhmc_api.cpp drives both); the kernels here are everything around
-// them.  All matrices are column-major with leading dimension n2 = 2N (the
+// eigenpairs come from the library's own Hermitian eigensolver
+// (dwhmc_eig.hip) and J_mn = U^H (J ⊕ J) U from its own batched fp64 MFMA
+// product (dwhmc_gemm.hip), both driven by dwhmc_api.cpp; the kernels here
+// are everything around them.  All matrices are column-major with leading dimension n2 = 2N (the
 // eigenvector of E_n is column n of U, as Julia's eigen! returns it).
 //
 // The O(n2^2 · n_ω) optical-conductivity sum is the only heavy kernel: every

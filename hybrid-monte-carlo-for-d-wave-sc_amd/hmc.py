@@ -242,8 +242,9 @@ class SpectrumResult:
 
 def measure_transport_and_spectra(cache: ComputeCache, p: ModelParameters, chain: int = 0) -> SpectrumResult:
     """src/Observables.jl:314-526 on the device: eigenpairs of H_BdG at the Δ
-    the cache's context holds (the library's eigensolver), J_mn = U^H J U (rocBLAS
-    zgemm), stiffness / conductivities / DOS / A(k, 0) in HIP kernels."""
+    the cache's context holds (the library's eigensolver), J_mn = U^H J U (the
+    library's fp64 MFMA product), stiffness / conductivities / DOS / A(k, 0) in
+    HIP kernels."""
     r = cache.require().measure_transport(p.eta, p.domega, p.omega_max, chain=chain)
     return SpectrumResult(**r)
 

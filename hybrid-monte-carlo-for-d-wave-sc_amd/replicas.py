@@ -104,10 +104,11 @@ def run_local(p, cfg: ReplicaConfig, rank: int, device: int, make_context, initi
 def gather_observables(local: np.ndarray, dist=None, device=None):
     """Gather (n_sweeps, chains, N_OBS) records of every rank to rank 0 ->
     (world*chains, n_sweeps, N_OBS) on rank 0, None elsewhere.  Uses the
-    process group's backend (RCCL on GPUs, gloo on CPU)."""
+    process group's backend (RCCL on GPUs with device = the rank's GPU, gloo
+    on CPU); an initialised group of one rank still runs the collective."""
     import torch
     rec = np.ascontiguousarray(np.transpose(local, (1, 0, 2)))
-    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+    if dist is None or not dist.is_initialized():
         return rec
     t = torch.as_tensor(rec, dtype=torch.float64)
     if device is not None:

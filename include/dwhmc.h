@@ -55,6 +55,8 @@ typedef struct {
   int64_t algo;       /* 0 = dense Schur-complement Gauss-Jordan, 1 = block cyclic reduction,
                          2 = eigendecomposition */
   int64_t block;      /* dense: GJ block (64); cr: padded lattice-row block BP >= 2 Lx; eig: 0 */
+  int64_t eig_half;   /* last eigensolve (transport / eig path): 1 = particle-hole half solve,
+                         J_mn and the pair sums over the columns < N; 0 = every column; -1 = none yet */
 } dwh_info_t;
 
 /* ModelParameters + initialize_cache + init_static_H!
@@ -188,6 +190,14 @@ int dwh_timing_enable(dwh_ctx* ctx, int32_t enable);
 int dwh_timing_read(dwh_ctx* ctx, const char* name, double* total_ms, int64_t* launches,
                     double* work);
 int dwh_timing_reset(dwh_ctx* ctx);
+/* Enqueues the per-factorisation assembly launch (timer "assemble": CR, the
+ * pairing entries Δ/2 scattered into the level-0 blocks, replacing
+ * update_H_BdG! src/Hamiltonian.jl:55-86; dense, the Schur-complement
+ * assembly) reps times back to back on the context's stream and waits, so a
+ * bench reads a warm per-launch average with the timers instead of the one
+ * launch a factorisation makes.  Idempotent: the pool keeps the current Δ.
+ * eig path: DWH_ERR_STATE. */
+int dwh_bench_assembly(dwh_ctx* ctx, int64_t reps);
 
 /* ---- measurement path (not the leapfrog step) ----------------------------
  * Eigen-decomposition of one chain's H_BdG(Δ) at the device Δ: what the

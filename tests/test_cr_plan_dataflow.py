@@ -94,44 +94,6 @@ def test_cr_plan_flops_c3_side_work(dwhmc):
     assert side_f > 0.2 * (prod + side_f)
 
 
-ROWS2_LATTICES = [(4, 2), (8, 4), (5, 6), (16, 16), (16, 2), (16, 4), (12, 10), (32, 32), (20, 8), (64, 4)]
-
-
-@pytest.mark.parametrize("Lx,Ly", ROWS2_LATTICES)
-def test_cr_two_row_blocks_dataflow_and_flops(dwhmc, monkeypatch, Lx, Ly):
-    """Two lattice rows per CR block (DWHMC_CR_ROWS=2, C2's candidate
-    blocking): the same dataflow invariants, the gathers reading only tiles
-    the restricted level-0 backward stages write (the vertical bonds between
-    blocks sit on off-diagonal B tiles there), and the plan's flops equal the
-    independent count of the two-row recursion (tools/cr_model.py)."""
-    from tools.cr_model import cr_flop_count
-    monkeypatch.setenv("DWHMC_CR_ROWS", "2")
-    lib = dwhmc.load_library()
-    rows = 2 if 2 * 2 * ((2 * Lx + 15) // 16 * 16) <= 256 and Ly % 2 == 0 else default_rows(Lx, Ly)
-    inv_ref, prod_ref = cr_flop_count(Lx, Ly, rows)
-    for side in (0, 1):
-        for inv0 in (0, 1):
-            rc, stats, err = check(lib, Lx, Ly, 10, side, inv0)
-            assert rc == 0, (Lx, Ly, side, inv0, err)
-            inv, prod, side_f = plan_flops(lib, Lx, Ly, 10, side, inv0)
-            assert inv == pytest.approx(inv_ref, rel=1e-12), (side, inv0)
-            assert prod + side_f == pytest.approx(prod_ref, rel=1e-12), (side, inv0, prod, side_f)
-
-
-def test_cr_two_row_blocks_c2_shape(dwhmc, monkeypatch):
-    """C2 (L = 16) with two rows per block: BP = 64, 8 blocks, 3 levels —
-    4 inversion launches (the level-0 one from the static particle block,
-    three carrying side work) and 12 product launches instead of 5 and 16."""
-    lib = dwhmc.load_library()
-    rc, s1, err = check(lib, 16, 16, 10, 1, 1)
-    assert rc == 0, err
-    monkeypatch.setenv("DWHMC_CR_ROWS", "2")
-    rc, s2, err = check(lib, 16, 16, 10, 1, 1)
-    assert rc == 0, err
-    assert list(s1[:4]) == [21, 5, 0, 16]
-    assert list(s2[:4]) == [16, 4, 3, 12]
-
-
 @pytest.mark.parametrize("Lx,Ly,rows,blocks", [(8, 8, 2, 4), (4, 4, 4, 1), (4, 6, 3, 2), (6, 9, 1, 9), (5, 7, 1, 7),
                                                (3, 3, 3, 1), (16, 16, 1, 16), (8, 5, 1, 5), (2, 10, 5, 2)])
 def test_cr_default_rows_per_block(dwhmc, monkeypatch, Lx, Ly, rows, blocks):
@@ -139,7 +101,6 @@ def test_cr_default_rows_per_block(dwhmc, monkeypatch, Lx, Ly, rows, blocks):
     (cr_rows_per_block): 8 x 8 (C1) runs 4 two-row blocks, one CR level less
     than 8 half-empty one-row blocks; the inversion count of the plan shows the
     block count."""
-    monkeypatch.delenv("DWHMC_CR_ROWS", raising=False)
     assert default_rows(Lx, Ly) == rows
     lib = dwhmc.load_library()
     rc, st, err = check(lib, Lx, Ly, 10, 1, 1)

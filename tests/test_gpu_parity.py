@@ -823,38 +823,3 @@ def test_guard_falls_back_to_eig_beyond_table(dwhmc, oracle):
     assert np.max(np.abs(ctx.forces()[0] - F_ref)) <= 1e-10 * (1 + np.max(np.abs(F_ref)))
     assert abs(ctx.fermion_energy()[0] - Ef_ref) <= 1e-11 * abs(Ef_ref)
     ctx.close()
-
-
-@pytest.mark.parametrize("Lx,Ly", [(16, 16), (8, 4), (12, 10), (20, 8), (6, 2), (32, 8)])
-def test_cr_two_row_blocks(dwhmc, oracle, monkeypatch, Lx, Ly):
-    """Two lattice rows per CR block (DWHMC_CR_ROWS=2): the same oracle
-    results — P, F, E_f, hole density after one factorisation and the HMC
-    sweeps of a trajectory (the vertical bonds between blocks read
-    off-diagonal B tiles of the level-0 G blocks; padded blocks at 2 Lx = 40,
-    the 2-block chain at Ly = 2, BP = 128 at 2 Lx = 64)."""
-    O = oracle
-    monkeypatch.setenv("DWHMC_CR_ROWS", "2")
-    p, dis, Delta = make_case(O, Lx, Ly, 8.0, seed=Lx * 13 + Ly, amp=0.1)
-    cache, F_ref, Ef_ref = O.evaluate(p, dis, Delta)
-    P_ref, _ = O.pairing_P(cache.U, cache.E_n, p)
-    ctx = device_ctx(dwhmc, p, dis, "cr")
-    assert ctx.info["block"] == 2 * ((2 * Lx + 15) // 16 * 16)
-    ctx.set_pairing(Delta)
-    ctx.factorize()
-    assert np.max(np.abs(ctx.pairing()[0] - P_ref)) <= 1e-11
-    assert np.max(np.abs(ctx.forces()[0] - F_ref)) <= 1e-10 * (1 + np.max(np.abs(F_ref)))
-    assert abs(ctx.fermion_energy()[0] - Ef_ref) <= 1e-11 * abs(Ef_ref)
-    hole_ref = O.measure_observables(cache, p, Delta)["hole_conc"]
-    assert abs(2.0 * ctx.hole_trace()[0] / p.N - 1.0 - hole_ref) <= 1e-11
-    Nt = 3
-    dt = O.calc_optimal_dt(p.beta, p.J, p.mass, Nt)
-    rng = np.random.default_rng(8)
-    draws = [((rng.standard_normal((p.N, 2)) + 1j * rng.standard_normal((p.N, 2))) * math.sqrt(0.5),
-              float(rng.random())) for _ in range(2)]
-    ref = _oracle_after_sweeps(O, p, dis, Delta, draws, Nt, dt)
-    for (noise, u), (acc_r, dH_r, D_r, _) in zip(draws, ref):
-        acc, dH = ctx.hmc_sweep(noise, np.array([u]), Nt, dt, p.mass)
-        assert bool(acc[0]) == acc_r and abs(dH[0] - dH_r) <= 1e-8 * (1 + abs(dH_r))
-        assert np.max(np.abs(ctx.get_state()[0][0] - D_r)) <= 1e-10
-    ctx.close()
-

@@ -95,3 +95,74 @@ def test_bench_two_ranks_gloo(tmp_path):
     assert rec["n_gpus"] == 2 and rec["steps"] == 8 and rec["value"] > 0
     assert "rehearsal" in rec and 0.0 <= rec["acceptance"] <= 1.0
     assert rec["config"]["parallelism"] == "replicas x2"
+
+
+def _rccl_worker(rank, world, port, out):
+    """One rank, RCCL (backend nccl) bound to the GPU: the replicas' observable
+    gather on device tensors, as replicas.py / tools/run_replicas.py run it per GPU."""
+    import torch
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    tr = []
+    rep, local = _local(rank, tr)
+    rec = rep.gather_observables(local, dist, device=dev)
+    trec = rep.gather_observables(np.stack(tr), dist, device=dev)
+    t = torch.tensor([1.0 + rank], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    np.save(out, rec)
+    np.save(out + ".tr.npy", trec)
+    np.save(out + ".max.npy", t.cpu().numpy())
+    dist.barrier()
+    backend = dist.get_backend()
+    dist.destroy_process_group()
+    assert backend == "nccl"
+
+
+def test_rccl_gather_world1(tmp_path):
+    """The RCCL branch at world size 1 (the first execution of the collective
+    the 8-GPU replica run uses): init_process_group("nccl", device_id=GPU),
+    gather_observables on device tensors, the max all_reduce — the gathered
+    records equal the replica run alone, bit for bit."""
+    out = str(tmp_path / "rec.npy")
+    mp.spawn(_rccl_worker, args=(1, _free_port(), out), nprocs=1, join=True)
+    rec = np.load(out)
+    t0 = []
+    rep, l0 = _local(0, t0)
+    assert np.array_equal(rec, np.transpose(l0, (1, 0, 2)))
+    assert np.array_equal(np.load(out + ".tr.npy"), np.transpose(np.stack(t0), (1, 0, 2)))
+    assert float(np.load(out + ".max.npy")[0]) == 1.0
+
+
+def _bench(args, env_extra=None, torchrun=False):
+    env = dict(os.environ, **(env_extra or {}))
+    env.pop("DWHMC_BENCH_BACKEND", None)
+    cmd = [sys.executable]
+    if torchrun:
+        cmd += ["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr", "127.0.0.1",
+                "--master-port", str(_free_port())]
+    cmd += [os.path.join(ROOT, "bench.py")] + args
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def test_bench_rccl_world1_matches_plain():
+    """The driver's multi-GPU command shape at --nproc-per-node 1 with the
+    default backend (RCCL over the rank's GPU): the replica branch runs —
+    nccl init with device_id, the max-time all_reduce and the observable
+    gather on device tensors — and its C3 rate equals the plain run's within
+    the box spread (same workload, one replica)."""
+    args = ["--gpus", "1", "--steps", "40", "--warmup", "5", "--no-cpu-baseline", "--no-c1", "--no-timing"]
+    plain = _bench(args)
+    rec = _bench(args, torchrun=True)
+    assert rec["n_gpus"] == 1 and rec["config"]["parallelism"] == "replicas x1"
+    assert rec["collectives"]["backend"] == "nccl" and rec["collectives"]["device"] == "cuda:0"
+    assert "rehearsal" not in rec
+    assert plain["config"]["parallelism"] == "single GPU"
+    assert rec["config"]["L"] == plain["config"]["L"] == 32 and rec["config"]["poles"] == plain["config"]["poles"]
+    assert abs(rec["value"] / plain["value"] - 1.0) <= 0.10, (rec["value"], plain["value"])

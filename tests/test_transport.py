@@ -289,14 +289,17 @@ def test_transport_clean_degenerate_spectrum(dwhmc, oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("Lx,Ly,mu,half", [(8, 8, 0.0, "1"), (12, 8, 0.0, "1"), (8, 8, -1.0, "1"), (6, 6, -1.08, "0")])
-def test_transport_particle_hole_half(dwhmc, oracle, monkeypatch, Lx, Ly, mu, half):
+@pytest.mark.parametrize("Lx,Ly,mu,half,ran_half", [(8, 8, 0.0, "1", 0), (12, 8, 0.0, "1", 0), (8, 8, -1.0, "1", 1),
+                                                     (6, 6, -1.08, "0", 0)])
+def test_transport_particle_hole_half(dwhmc, oracle, monkeypatch, Lx, Ly, mu, half, ran_half):
     """The particle-hole half measurement: with the eigensolver's half solve
     (columns j < N the partners Θ of columns n2-1-j) J_mn is formed in its
     columns < N only and Λ, the DC sum and σ(ω) run over half the pairs.  A
     clean lattice at μ = 0 with L % 4 == 0 has exact zero modes (a cluster
     across E = 0, solved whole, so U is not partner-closed there): every pair
-    is summed.  half = "0" (DWHMC_EIG_HALF=0): the full solve and sums."""
+    is summed.  half = "0" (DWHMC_EIG_HALF=0): the full solve and sums.
+    ran_half: which path the library reports it took (dwh_info_t::eig_half),
+    so the half-sum code cannot pass silently on the full path."""
     O = oracle
     monkeypatch.setenv("DWHMC_EIG_HALF", half)
     p = O.ModelParameters(Lx, Ly, 1.0, -0.35, mu, 0.0, 0.0, 16.0, 0.8, 1.0)
@@ -309,7 +312,9 @@ def test_transport_particle_hole_half(dwhmc, oracle, monkeypatch, Lx, Ly, mu, ha
     ref = O.measure_transport_and_spectra(cache, p)
     ctx = _ctx(dwhmc, p, np.zeros(N))
     ctx.set_pairing(D)
+    assert ctx.info["eig_half"] == -1
     r = ctx.measure_transport(p.eta, p.domega, p.omega_max)
+    assert ctx.info["eig_half"] == ran_half
     ctx.close()
     _check_transport(r, ref)
 

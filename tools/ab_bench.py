@@ -1,8 +1,7 @@
 #!/usr/bin/env python3
 """Interleaved in-process A/B of context variants (env knobs read at create):
-python tools/ab_bench.py --L 32 --beta 16 --variants "PAIR=1" "PAIR=0"
-PAIR -> DWHMC_GJ_PAIR (paired rank-128 Gauss-Jordan updates or one rank-64
-update per pivot step); LIB=path loads another build of the library
+python tools/ab_bench.py --L 32 --beta 16 --variants "CR_INV0=1" "CR_INV0=0"
+KEY=VAL sets the context knob DWHMC_KEY; LIB=path loads another build of the library
 (hybrid-monte-carlo-for-d-wave-sc_amd/build.py --out build/var/x.so -D ...) so
 kernel variants are compared in one process.  Prints ms per leapfrog step
 (median / min over rounds) and the per-kernel event totals of the last round."""
@@ -26,7 +25,7 @@ def main():
     ap.add_argument("--Nt", type=int, default=10)
     ap.add_argument("--sweeps", type=int, default=3)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--variants", nargs="+", default=["PAIR=1", "PAIR=0"])
+    ap.add_argument("--variants", nargs="+", default=["CR_INV0=1", "CR_INV0=0"])
     a = ap.parse_args()
     import dwhmc_loader
     m = dwhmc_loader.load_package()
@@ -47,10 +46,9 @@ def main():
         kv = dict(x.split("=") for x in v.split(",") if x)
         for k in touched:                       # knobs of the previous variant do not leak
             os.environ.pop(k, None)
-        os.environ["DWHMC_GJ_PAIR"] = kv.get("PAIR", "1")
         # any other KEY=VAL of the variant sets the context knob DWHMC_KEY
         for k, val in kv.items():
-            if k not in ("PAIR", "LIB"):
+            if k != "LIB":
                 os.environ["DWHMC_" + k] = val
                 touched.add("DWHMC_" + k)
         ctx = m.FermionContext(p.Lx, p.Ly, p.t, p.tp, p.mu, p.beta, p.J, p.nn_table, p.nnn_table,

@@ -42,7 +42,10 @@ def main():
     m = dwhmc_loader.load_package()
     rep = import_module(m.__name__ + ".replicas")
     device = None
-    if world > 1:
+    # under torch.distributed.run (any world size, also --nproc-per-node 1) the
+    # RCCL group runs, so one GPU exercises the collective path of eight
+    distributed = world > 1 or "MASTER_ADDR" in os.environ
+    if distributed:
         if torch.cuda.is_available():
             torch.cuda.set_device(local)
             device = torch.device("cuda", local)
@@ -61,11 +64,11 @@ def main():
     tr_local = []
     local_rec = rep.run_local(p, cfg, rank, local, make_context, m.initialize_state, m.calc_optimal_dt,
                               transport_out=tr_local)
-    allrec = rep.gather_observables(local_rec, dist if world > 1 else None, device)
+    allrec = rep.gather_observables(local_rec, dist if distributed else None, device)
     alltr = None
     if tr_local:
         import numpy as np
-        alltr = rep.gather_observables(np.stack(tr_local), dist if world > 1 else None, device)
+        alltr = rep.gather_observables(np.stack(tr_local), dist if distributed else None, device)
     if rank == 0:
         os.makedirs(a.out, exist_ok=True)
         path = os.path.join(a.out, "observables.csv")
