@@ -405,7 +405,7 @@ def main(argv=None):
         # per-launch averages.
         replay = schedule(w_sw, min(a.steps, 2 * Nt), Nt)
         replay_steps = sum(n * nt for _, n, nt in replay)
-        names = [dom, "assemble"] + (["cr_inv", "cr_inv_side"] if cr else [])
+        names = [dom, "assemble"] + (["cr_inv", "cr_inv_side", "cr_sparse"] if cr else [])
         ctx.timing_enable(names)
         ctx.timing_reset()
         for f, n, nt in replay:
@@ -481,10 +481,12 @@ def main(argv=None):
                 kfam = [f"k_cr_gemm<{info['block']},1,4>", f"k_cr_gemm<{info['block']},1,1>"]
                 msi, ni, wi = kern["cr_inv"]
                 mss, ns, ws = kern["cr_inv_side"]
+                msp, nsp, wsp = kern["cr_sparse"]
                 # the CR path's own algorithmic flops per leapfrog step (block
-                # products, incl. the side work of the inversion stages, and
-                # block inversions at 8 BP^3 each) x the timed steps
-                wall = w + wi + ws
+                # products, incl. the side work of the inversion stages, the
+                # sparse level-0 products, and block inversions at 8 BP^3
+                # each) x the timed steps
+                wall = w + wi + ws + wsp
                 rec["alg_tflops"] = wall / replay_steps * a.steps * world / el / 1e12
                 rec["alg_flops_per_step"] = wall / replay_steps / a.chains
                 # the whole leapfrog step against the fp64 MFMA peak (north_star: >= 0.30 at L=32)
@@ -495,6 +497,13 @@ def main(argv=None):
                                  "achieved_tflops": wi / (msi * 1e-3) / 1e12 if msi > 0 else None,
                                  "avg_launch_us": 1000.0 * msi / ni if ni else None,
                                  "ms_per_step": msi / replay_steps}
+                if nsp:
+                    rec["cr_sparse"] = {"bound": "latency", "kernel": "k_cr_sp_fwd + k_cr_sp_bwd",
+                                        "what": "level-0 products with the sparse U / L blocks (VALU)",
+                                        "launches_per_step": nsp / replay_steps,
+                                        "avg_launch_us": 1000.0 * msp / nsp,
+                                        "flops_per_launch": wsp / nsp,
+                                        "ms_per_step": msp / replay_steps}
                 if ns:
                     rec["cr_inv_side"] = {"bound": "latency", "kernel": f"k_cr_inv_side<{nt}>",
                                           "what": "block inversions + off-critical-path block products "

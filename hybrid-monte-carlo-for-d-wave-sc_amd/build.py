@@ -14,7 +14,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libdwhmc.so")
-SOURCES = [os.path.join(CSRC, "dwhmc_kernels.hip"), os.path.join(CSRC, "dwhmc_cr.hip"),
+SOURCES = [os.path.join(CSRC, "dwhmc_kernels.hip"), os.path.join(CSRC, "dwhmc_cr.hip"), os.path.join(CSRC, "dwhmc_cr_sparse.hip"),
            os.path.join(CSRC, "dwhmc_eig.hip"), os.path.join(CSRC, "dwhmc_gemm.hip"),
            os.path.join(CSRC, "dwhmc_transport.hip"), os.path.join(CSRC, "dwhmc_api.cpp")]
 # rocSOLVER (zheevd / zheev: opt-in via DWHMC_EIG_SOLVER for A/B runs) is the

@@ -283,7 +283,7 @@ class FermionContext:
 
     # -- timing ----------------------------------------------------------
     TIMERS = ("gj_update", "gj_pivot", "assemble", "contract", "step", "gj_edge", "cr_gemm", "cr_inv",
-              "cr_inv_side", "eig_own", "eig_vendor")
+              "cr_inv_side", "eig_own", "eig_vendor", "cr_sparse")
 
     def timing_enable(self, on=True):
         """on: True (all timers), False, or an iterable of timer names."""

@@ -84,12 +84,13 @@ const PoleTable* pole_table(std::string* err) {
 
 enum TimerName {
   T_GJ_UPDATE = 0, T_GJ_PIVOT, T_ASSEMBLE, T_CONTRACT, T_STEP, T_GJ_EDGE, T_CR_GEMM, T_CR_INV, T_CR_INVSIDE,
-  T_EIG_OWN, T_EIG_VENDOR, T_COUNT
+  T_EIG_OWN, T_EIG_VENDOR, T_CR_SPARSE, T_COUNT
 };
 const char* kTimerNames[T_COUNT] = {"gj_update", "gj_pivot", "assemble", "contract",
                                     "step",      "gj_edge",  "cr_gemm",  "cr_inv",
                                     "cr_inv_side",
-                                    "eig_own",   "eig_vendor"};   // eigensolves (work: matrices)
+                                    "eig_own",   "eig_vendor",   // eigensolves (work: matrices)
+                                    "cr_sparse"};
 
 enum Algo { ALGO_DENSE = 0, ALGO_CR = 1, ALGO_EIG = 2 };
 
@@ -106,6 +107,7 @@ struct CrStage {
                         // maxt32 tiles each), flops in `flops`
   dwh::CrGemmCfg cfg;   // products: tile / K-split chosen once per context
   int l0 = 0;           // inversions: level 0 from the static R = A^-1 blocks (k_cr_inv0)
+  int sp = 0;           // kind 2 (sparse level-0 stage): 0 forward (CrPlan::sp_fwd), 1 backward (sp_bwd)
 };
 
 struct CrPlan {
@@ -119,7 +121,64 @@ struct CrPlan {
   std::vector<int> fill_all, fill_step;      // level-0 blocks written at create / every step
   std::vector<int64_t> off_ph;               // pairing entries outside fill_step (-1: none)
   int n_ph = 0;                              // entries of off_ph >= 0
+  // sparse level 0 (dwhmc_cr_sparse.hip): the stages' tasks and the level-0
+  // U / L patterns (CrPlan::rowpat / colpat: [3 Ly][kCrSpNZ][BP])
+  std::vector<dwh::CrSpFwd> sp_fwd;
+  std::vector<dwh::CrSpBwd> sp_bwd;
+  std::vector<int> rowpat, colpat;
 };
+
+// Nonzero patterns of the level-0 U[y] = A[y, y+1] (pool block Ly + y) and
+// L[y] = A[y+1, y] (2 Ly + y) blocks, from the hopping / pairing tables
+// exactly as k_cr_fill writes them (top half: hopping at (x, x_j), pairing at
+// (x, HP + x_j) for partners j in the other row), as entries of the FULL
+// block: row x of the top half, and row HP + x synthesised from it (M-form:
+// [conj B | -conj A]).  Entry = top-half offset | (column for rowpat, row for
+// colpat) << 14 | op << 22 (op 0 as stored, 1 conj, 2 -conj).  False when a
+// row or column holds more than kCrSpNZ entries (the dense level 0 then runs).
+bool cr_sparse_patterns(int Lx, int Ly, int BP, const std::vector<int>& hcol, const std::vector<int>& Dcol,
+                        std::vector<int>& rowpat, std::vector<int>& colpat) {
+  const int HP = BP / 2, NZ = dwh::kCrSpNZ;
+  rowpat.assign((size_t)3 * Ly * NZ * BP, -1);
+  colpat.assign((size_t)3 * Ly * NZ * BP, -1);
+  for (int t = 1; t <= 2; ++t)
+    for (int y = 0; y < Ly; ++y) {
+      if ((t == 1 && Ly < 2) || (t == 2 && Ly < 3)) continue;   // k_cr_fill's zero blocks
+      const int b = t * Ly + y;
+      const int yr = (t == 2) ? (y + 1) % Ly : y, yc = (t == 1) ? (y + 1) % Ly : y;
+      std::set<std::pair<int, int>> top;
+      for (int x = 0; x < Lx; ++x) {
+        const int i = yr * Lx + x;
+        for (int s = 0; s < kHSlots; ++s) {
+          const int j = hcol[(size_t)i * kHSlots + s];
+          if (j >= 0 && j / Lx == yc) top.insert({x, j % Lx});
+        }
+        for (int s = 0; s < kSlots; ++s) {
+          const int j = Dcol[(size_t)i * kSlots + s];
+          if (j >= 0 && j / Lx == yc) top.insert({x, HP + j % Lx});
+        }
+      }
+      std::vector<int> rn(BP, 0), cn(BP, 0);
+      auto put = [&](int r, int c, int off, int op) {
+        if (rn[r] >= NZ || cn[c] >= NZ) return false;
+        rowpat[((size_t)b * NZ + rn[r]++) * BP + r] = off | (c << 14) | (op << 22);
+        colpat[((size_t)b * NZ + cn[c]++) * BP + c] = off | (r << 14) | (op << 22);
+        return true;
+      };
+      for (const auto& xc : top) {
+        const int x = xc.first, c = xc.second, off = x * BP + c;
+        if (!put(x, c, off, 0)) return false;
+        if (!(c >= HP ? put(HP + x, c - HP, off, 1) : put(HP + x, c + HP, off, 2))) return false;
+      }
+    }
+  return true;
+}
+// nonzeros of row r / column c of level-0 block b in the patterns
+int sp_nrow(const std::vector<int>& pat, int b, int r, int BP) {
+  int n = 0;
+  for (int e = 0; e < dwh::kCrSpNZ; ++e) n += pat[((size_t)b * dwh::kCrSpNZ + e) * BP + r] >= 0;
+  return n;
+}
 
 // Lattice rows per CR block.  Default: as many rows as fill the narrowest
 // block half (16 sites) — R = 16 / Lx, lowered to a divisor of Ly — so a
@@ -171,12 +230,25 @@ int cr_rows_per_block(int64_t Lx, int64_t Ly) {
 // recursion is the same; only which entries of the level-0 G blocks the
 // force reads changes (computed from Dcol below, not assumed diagonal).
 CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol, bool side, int nbatch,
-                     int ncu, bool inv0) {
+                     int ncu, bool inv0, const std::vector<int>* hcol) {
   // W products two inversion stages after their level, side work from m = 4
   // (profiles/r02_exp_cr_side_work.txt, r04_exp_cr_side_knobs_C3.txt)
   constexpr int side_woff = 2, side_m = 4;
   CrPlan pl;
   const int HP = BP / 2;
+  // sparse level 0 (dwhmc_cr_sparse.hip): even Ly >= 4, a supported block,
+  // patterns within kCrSpNZ; DWHMC_CR_SPARSE0=0 keeps the dense level 0 (A/B)
+  const bool sparse0 = [&] {
+    const char* e = std::getenv("DWHMC_CR_SPARSE0");
+    if ((e && *e == '0') || !hcol || Ly % 2 != 0 || Ly < 4 || !dwh::cr_supported_sparse0(BP)) return false;
+    return cr_sparse_patterns(Lx, Ly, BP, *hcol, Dcol, pl.rowpat, pl.colpat);
+  }();
+  if (!sparse0) {
+    pl.rowpat.clear();
+    pl.colpat.clear();
+  }
+  auto nr = [&](int b, int r) { return sp_nrow(pl.rowpat, b, r, BP); };
+  auto nc = [&](int b, int c) { return sp_nrow(pl.colpat, b, c, BP); };
   int nblk = 3 * Ly;
   std::vector<char> qform(3 * Ly, 0);   // per pool block: Q-form (products V, W)
   auto nb = [&]() {
@@ -193,6 +265,7 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol, bool 
     std::vector<int> Dinv;             // block holding D_e^-1 (then G_ee), by position e
     std::vector<int> V1, V2, W1, W2;   // indexed by position e
     std::vector<char> elim;
+    bool sparse = false;               // level 0 by the sparse stages (no V / W blocks)
   };
   // Level-0 blocks are inverted out of place (they are never overwritten, so
   // per step only their pairing entries change), coarser blocks in place.
@@ -381,6 +454,34 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol, bool 
     const std::vector<int> dinv = add_inv(inv, slot);
     cur.Dinv.assign(m, -1);
     for (size_t i = 0; i < cur.E.size(); ++i) cur.Dinv[cur.E[i]] = dinv[i];
+    if (sparse0 && levels.empty() && m % 2 == 0 && m >= 4) {
+      // level 0: D', U', L' of every kept row in one sparse stage (no V / W)
+      CrStage st{};
+      st.kind = 2;
+      st.sp = 0;
+      st.first = (int)pl.sp_fwd.size();
+      Level nxt;
+      nxt.m = (int)cur.K.size();
+      for (int k : cur.K) {
+        const int er = k + 1, el = (k - 1 + m) % m;
+        const int Dn = nb(), Un = nb(), Ln = nb();
+        pl.sp_fwd.push_back(dwh::CrSpFwd{cur.D[k], cur.U[k], cur.L[k], cur.U[el], cur.L[el], cur.U[er], cur.L[er],
+                                         cur.Dinv[er], cur.Dinv[el], Dn, Un, Ln});
+        for (int r = 0; r < HP; ++r)   // V1r, V2r, V2l rows
+          st.flops += 8.0 * BP * (nr(cur.U[k], r) + nr(cur.L[er], r) + nr(cur.L[el], r));
+        for (int c = 0; c < BP; ++c)   // D' (2 terms), U', L'
+          st.flops += 8.0 * HP * (2 * nc(cur.L[k], c) + nc(cur.U[el], c) + nc(cur.U[er], c));
+        nxt.D.push_back(Dn);
+        nxt.U.push_back(Un);
+        nxt.L.push_back(Ln);
+      }
+      st.n = (int)pl.sp_fwd.size() - st.first;
+      pl.stages.push_back(st);
+      cur.sparse = true;
+      levels.push_back(cur);
+      cur = nxt;
+      continue;
+    }
     for (int e : cur.E) {
       const int a = e - 1;
       cur.V1[e] = nbq();
@@ -470,6 +571,65 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol, bool 
     // its need tiles.
     const bool sel = (li == 0);
     const int H0 = sel ? HP : 0, H1 = sel ? HP + Lx : BP;
+    if (lv.sparse) {
+      // sparse level 0: Z_a, Z_c, Y_a, Y_c, M in one sparse stage, then
+      // one-term products G_ae = -Z_a Dinv, G_ce = -Z_c Dinv, G_ea = -Dinv Y_a,
+      // G_ec = -Dinv Y_c (need tiles), T = -Dinv M; then G_ee = Dinv - T Dinv
+      CrStage st{};
+      st.kind = 2;
+      st.sp = 1;
+      st.first = (int)pl.sp_bwd.size();
+      struct Bw { int e, a, za, zc, ya, yc, mx; };
+      std::vector<Bw> bw;
+      for (int e : lv.E) {
+        const int a = e - 1, c = (e + 1) % m;
+        const int ia = a / 2, ic = (c / 2) % mn;
+        const int Gaa = GD[ia], Gcc = GD[ic], Gac = GU[ia], Gca = GL[ia];
+        const Bw x{e, a, nbq(), nbq(), nbq(), nbq(), nb()};
+        bw.push_back(x);
+        pl.sp_bwd.push_back(dwh::CrSpBwd{Gaa, Gac, Gca, Gcc, lv.U[a], lv.L[e], lv.L[a], lv.U[e], x.za, x.zc, x.ya,
+                                         x.yc, x.mx, 0, 0, 0});
+        for (int cc = 0; cc < BP; ++cc) st.flops += 8.0 * HP * 2 * (nc(lv.U[a], cc) + nc(lv.L[e], cc));   // Z_a, Z_c
+        for (int r = 0; r < HP; ++r) st.flops += 8.0 * BP * 3 * (nr(lv.L[a], r) + nr(lv.U[e], r));       // Y_a, Y_c, M
+      }
+      st.n = (int)pl.sp_bwd.size() - st.first;
+      pl.stages.push_back(st);
+      std::vector<int> tn(m, -1);
+      for (const Bw& x : bw) {
+        const int e = x.e, a = x.a, D = lv.Dinv[e];
+        const int gea = nb(), gec = nb(), gae = nb(), gce = nb();
+        tn[e] = nbq();
+        w_c0 = H0;
+        w_c1 = H1;
+        keep_next = &need[2][a];   // G_ea = G_L[a]
+        task(gea, -1, {{D, x.ya}});
+        keep_next = &need[1][e];   // G_ec = G_U[e]
+        task(gec, -1, {{D, x.yc}});
+        keep_next = nullptr;
+        w_c0 = 0;
+        w_c1 = BP;
+        task(gae, -1, {{x.za, D}});
+        task(gce, -1, {{x.zc, D}});
+        task(tn[e], -1, {{D, x.mx}});
+        gu[a] = gae;
+        gl[a] = gea;
+        gu[e] = gec;
+        gl[e] = gce;
+      }
+      flush(-1.0);
+      for (int e : lv.E) {
+        const int gee = nb();
+        keep_next = &need[0][e];
+        task(gee, lv.Dinv[e], {{tn[e], lv.Dinv[e]}});
+        gd[e] = gee;
+      }
+      keep_next = nullptr;
+      flush(-1.0);
+      GD = gd;
+      GU = gu;
+      GL = gl;
+      continue;
+    }
     std::vector<int> Gae(m, -1), Gce(m, -1);
     for (int e : lv.E) {
       const int a = e - 1, c = (e + 1) % m;
@@ -632,6 +792,9 @@ struct dwh_ctx {
   double2* bpool = nullptr;   // CR block pool (nbatch x nblk blocks)
   dwh::CrTask* d_tasks = nullptr;
   dwh::CrTile* d_tiles16 = nullptr;
+  dwh::CrSpFwd* d_sp_fwd = nullptr;
+  dwh::CrSpBwd* d_sp_bwd = nullptr;
+  int *d_rowpat = nullptr, *d_colpat = nullptr;
   double* efpart = nullptr;     // per (chain, pole) E_f / Tr G22 partials
   unsigned* efdone = nullptr;   // per chain: pole blocks done (k_cr_fermion_energy)
   int *d_inv_blk = nullptr, *d_inv_dst = nullptr, *d_inv_slot = nullptr, *d_inv0_r = nullptr;
@@ -894,6 +1057,14 @@ void cr_enqueue(dwh_ctx* ctx) {
       dwh::launch_cr_inv(c, ctx->bpool, ctx->d_inv_blk + st.first, ctx->d_inv_dst + st.first,
                          ctx->d_inv_slot + st.first, st.n, ctx->ldpart, ctx->stream, guard);
       guard = dwh::SiteGuard{};
+    } else if (st.kind == 2) {
+      Scope s(ctx, T_CR_SPARSE, st.flops * c.nbatch);
+      if (st.sp == 0)
+        dwh::launch_cr_sp_fwd(c, ctx->bpool, ctx->d_sp_fwd + st.first, st.n, ctx->d_rowpat, ctx->d_colpat,
+                              ctx->stream);
+      else
+        dwh::launch_cr_sp_bwd(c, ctx->bpool, ctx->d_sp_bwd + st.first, st.n, ctx->d_rowpat, ctx->d_colpat,
+                              ctx->stream);
     } else {
       Scope s(ctx, T_CR_GEMM, st.flops * c.nbatch);
       dwh::launch_cr_gemm(c, ctx->bpool, ctx->d_tasks + st.first, st.n, st.maxt32, st.maxt16,
@@ -1475,7 +1646,7 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
       // DWHMC_CR_INV0=0: level-0 blocks inverted whole (k_cr_inv) like the rest
       const char* e0 = std::getenv("DWHMC_CR_INV0");
       const bool inv0 = dwh::cr_supported_inv0(BP) && !(e0 && *e0 == '0');
-      ctx->plan = build_cr_plan(Lxc, Lyc, BP, Dcol, side, d.nbatch, ncu, inv0);
+      ctx->plan = build_cr_plan(Lxc, Lyc, BP, Dcol, side, d.nbatch, ncu, inv0, &hcol);
       dwh::CrDims& c = ctx->cr;
       c.Lx = Lxc;
       c.Ly = Lyc;
@@ -1497,6 +1668,9 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
           if (st.kind == 0)
             std::fprintf(stderr, "cr stage %2d: inv%s blocks=%d side_tasks=%d side_flops/item=%.3g\n", i,
                          st.l0 ? "0 " : "  ", st.n, st.ntiles, st.flops);
+          else if (st.kind == 2)
+            std::fprintf(stderr, "cr stage %2d: sparse %s tasks=%d flops/item=%.3g\n", i, st.sp ? "bwd" : "fwd", st.n,
+                         st.flops);
           else
             std::fprintf(stderr, "cr stage %2d: gemm  tasks=%d maxt32=%d maxt16=%d ntmax=%d flops/item=%.3g cfg=%d:%d ntiles=%d\n",
                          i, st.n, st.maxt32, st.maxt16, st.ntmax, st.flops, st.cfg.ts, st.cfg.ksplit, st.ntiles);
@@ -1540,6 +1714,10 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     ALLOC(bpool, (size_t)d.nbatch * ctx->cr.item);
     ALLOC(d_tasks, pl.tasks.size());
     ALLOC(d_tiles16, pl.tiles16.size());
+    ALLOC(d_sp_fwd, pl.sp_fwd.size());
+    ALLOC(d_sp_bwd, pl.sp_bwd.size());
+    ALLOC(d_rowpat, pl.rowpat.size());
+    ALLOC(d_colpat, pl.colpat.size());
     ALLOC(efpart, 2 * (size_t)d.nbatch);
     ALLOC(efdone, (size_t)d.nc);
     ALLOC(d_inv_blk, pl.inv_blk.size());
@@ -1634,6 +1812,10 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     const CrPlan& pl = ctx->plan;
     UP(d_tasks, pl.tasks.data(), pl.tasks.size());
     UP(d_tiles16, pl.tiles16.data(), pl.tiles16.size());
+    UP(d_sp_fwd, pl.sp_fwd.data(), pl.sp_fwd.size());
+    UP(d_sp_bwd, pl.sp_bwd.data(), pl.sp_bwd.size());
+    UP(d_rowpat, pl.rowpat.data(), pl.rowpat.size());
+    UP(d_colpat, pl.colpat.data(), pl.colpat.size());
     UP(d_inv_blk, pl.inv_blk.data(), pl.inv_blk.size());
     UP(d_inv_dst, pl.inv_dst.data(), pl.inv_dst.size());
     UP(d_inv_slot, pl.inv_slot.data(), pl.inv_slot.size());
@@ -2832,6 +3014,34 @@ int dwh_debug_gemm(int32_t device, int32_t cplx, char opa, char opb, int64_t M, 
 }  // extern "C"
 
 namespace {
+// hopping columns (kHSlots per site: the site, then its NN / NNN partners in
+// build_hrow's order) of a periodic Lx x Ly lattice with the reference's
+// tables (src/Types.jl:60-80): what dwh_create derives from ModelParameters
+std::vector<int> standard_hcol(int Lx, int Ly) {
+  const int N = Lx * Ly;
+  std::vector<int64_t> nn((size_t)4 * N), nnn((size_t)4 * N);
+  auto idx = [&](int x, int y) { return (int64_t)(((y % Ly + Ly) % Ly) * Lx + ((x % Lx + Lx) % Lx)) + 1; };
+  for (int y = 0; y < Ly; ++y)
+    for (int x = 0; x < Lx; ++x) {
+      const int i = y * Lx + x;
+      nn[0 * N + i] = idx(x + 1, y);
+      nn[1 * N + i] = idx(x, y + 1);
+      nn[2 * N + i] = idx(x - 1, y);
+      nn[3 * N + i] = idx(x, y - 1);
+      nnn[0 * N + i] = idx(x + 1, y + 1);
+      nnn[1 * N + i] = idx(x - 1, y + 1);
+      nnn[2 * N + i] = idx(x - 1, y - 1);
+      nnn[3 * N + i] = idx(x + 1, y - 1);
+    }
+  const auto hrow = build_hrow(N, 1.0, -0.35, nn.data(), nnn.data());
+  std::vector<int> hcol((size_t)N * kHSlots, -1);
+  for (int i = 0; i < N; ++i) {
+    hcol[(size_t)i * kHSlots] = i;
+    for (size_t k = 0; k < hrow[i].size() && k + 1 < (size_t)kHSlots; ++k) hcol[(size_t)i * kHSlots + 1 + k] = hrow[i][k].first;
+  }
+  return hcol;
+}
+
 // pairing columns (+x, +y, -x, -y) of every site of a periodic Lx x Ly lattice
 std::vector<int> nn_pairing_cols(int Lx, int Ly) {
   const int N = Lx * Ly;
@@ -2864,14 +3074,18 @@ int dwh_debug_cr_plan_check(int64_t Lx, int64_t Ly, int64_t nbatch, int32_t side
     return fail(nullptr, DWH_ERR_ARG, "lattice row too wide for the CR path");
   const int rows = cr_rows_per_block(Lx, Ly), Lxc = (int)Lx * rows, Lyc = (int)Ly / rows;
   const int BP = 2 * ((Lxc + 15) / 16 * 16);
+  const std::vector<int> hcol = standard_hcol((int)Lx, (int)Ly);
   const CrPlan pl = build_cr_plan(Lxc, Lyc, BP, Dcol, side && dwh::cr_supported_side(BP), (int)nbatch,
-                                  256, inv0 && dwh::cr_supported_inv0(BP));
+                                  256, inv0 && dwh::cr_supported_inv0(BP), &hcol);
   if (const char* e = std::getenv("DWHMC_CR_PLAN_DUMP"); e && *e == '1') {
     int i = 0;
     for (const CrStage& st : pl.stages) {
       if (st.kind == 0)
         std::fprintf(stderr, "cr stage %2d: inv%s blocks=%d (x%lld wg) side_tasks=%d maxt32=%d side_flops/item=%.3g\n", i,
                      st.l0 ? "0 " : "  ", st.n, (long long)nbatch, st.ntiles, st.maxt32, st.flops);
+      else if (st.kind == 2)
+        std::fprintf(stderr, "cr stage %2d: sparse %s tasks=%d flops/item=%.3g\n", i, st.sp ? "bwd" : "fwd", st.n,
+                     st.flops);
       else
         std::fprintf(stderr, "cr stage %2d: gemm  tasks=%d maxt32=%d maxt16=%d ntmax=%d flops/item=%.3g ntiles=%d\n", i,
                      st.n, st.maxt32, st.maxt16, st.ntmax, st.flops, st.ntiles);
@@ -2895,6 +3109,16 @@ int dwh_debug_cr_plan_check(int64_t Lx, int64_t Ly, int64_t nbatch, int32_t side
     if (st.kind == 0) {
       for (int k = 0; k < st.n; ++k) whole[pl.inv_dst[st.first + k]] = 1;
       for (int k = 0; k < st.ntiles; ++k) whole[pl.tasks[st.tfirst + k].out] = 1;
+    } else if (st.kind == 2) {
+      for (int k = 0; k < st.n; ++k) {
+        if (st.sp == 0) {
+          const dwh::CrSpFwd& t = pl.sp_fwd[st.first + k];
+          whole[t.od] = whole[t.ou] = whole[t.ol] = 1;
+        } else {
+          const dwh::CrSpBwd& t = pl.sp_bwd[st.first + k];
+          whole[t.oza] = whole[t.ozc] = whole[t.oya] = whole[t.oyc] = whole[t.omx] = 1;
+        }
+      }
     } else {
       for (int k = 0; k < st.ntiles; ++k) {
         const dwh::CrTile& t = pl.tiles16[st.tfirst + k];
@@ -2922,6 +3146,20 @@ int dwh_debug_cr_plan_check(int64_t Lx, int64_t Ly, int64_t nbatch, int32_t side
       }
       if (st.ntiles > 0) ++nside;
       for (int k = 0; k < st.ntiles; ++k) add_task(pl.tasks[st.tfirst + k], k);
+    } else if (st.kind == 2) {
+      ++ngemm;
+      for (int k = 0; k < st.n; ++k) {
+        const int id = k + (1 << 21);
+        if (st.sp == 0) {
+          const dwh::CrSpFwd& t = pl.sp_fwd[st.first + k];
+          for (int b : {t.dk, t.uk, t.lk, t.uel, t.lel, t.uer, t.ler, t.dir, t.dil}) rd.push_back({b, id});
+          for (int b : {t.od, t.ou, t.ol}) wr.push_back({b, id});
+        } else {
+          const dwh::CrSpBwd& t = pl.sp_bwd[st.first + k];
+          for (int b : {t.gaa, t.gac, t.gca, t.gcc, t.ua, t.le, t.la, t.ue}) rd.push_back({b, id});
+          for (int b : {t.oza, t.ozc, t.oya, t.oyc, t.omx}) wr.push_back({b, id});
+        }
+      }
     } else {
       ++ngemm;
       for (int k = 0; k < st.n; ++k) add_task(pl.tasks[st.first + k], k);
@@ -2985,8 +3223,9 @@ int dwh_debug_cr_plan_flops(int64_t Lx, int64_t Ly, int64_t nbatch, int32_t side
   const int rows = cr_rows_per_block(Lx, Ly), Lxc = (int)Lx * rows, Lyc = (int)Ly / rows;
   const int BP = 2 * ((Lxc + 15) / 16 * 16);
   std::vector<int> Dcol = nn_pairing_cols((int)Lx, (int)Ly);
+  const std::vector<int> hcol = standard_hcol((int)Lx, (int)Ly);
   const CrPlan pl = build_cr_plan(Lxc, Lyc, BP, Dcol, side && dwh::cr_supported_side(BP), (int)nbatch,
-                                  256, inv0 && dwh::cr_supported_inv0(BP));
+                                  256, inv0 && dwh::cr_supported_inv0(BP), &hcol);
   const double bp3 = 8.0 * BP * (double)BP * BP;
   flops[0] = flops[1] = flops[2] = 0.0;
   for (const CrStage& st : pl.stages) {

@@ -109,6 +109,28 @@ bool cr_supported_side(int BP);
 void launch_cr_inv_side(const CrDims& c, double2* pool, const int* blk, const int* dst, const int* slot,
                         int n, double* ldpart, const CrTask* stasks, int nst, int maxt32, hipStream_t s,
                         const SiteGuard& sg = SiteGuard{});
+// Sparse level-0 stages (dwhmc_cr_sparse.hip): the level-0 U / L blocks have
+// at most kCrSpNZ nonzeros per row and column (vertical hopping + one pairing
+// entry); rowpat / colpat hold them per pool block ([block][entry][BP], entry
+// = top-half offset | index << 14 | op << 22, -1 empty; dwhmc_cr_sparse.hip)
+constexpr int kCrSpNZ = 4;
+bool cr_supported_sparse0(int BP);
+// forward, per kept row k (er = k+1, el = k-1): D'_k = D_k + V1r L_k + V2l U_el,
+// U'_k = V1r U_er, L'_k = V2r L_k with V1r = -U_k Dinv_er, V2r = -L_er Dinv_er,
+// V2l = -L_el Dinv_el (pool block indices)
+struct CrSpFwd {
+  int dk, uk, lk, uel, lel, uer, ler, dir, dil, od, ou, ol;
+};
+// backward, per eliminated row e (a = e-1, c = e+1): Z_a = G_aa U_a + G_ac L_e,
+// Z_c = G_ca U_a + G_cc L_e, Y_a = L_a G_aa + U_e G_ca, Y_c = L_a G_ac + U_e G_cc,
+// M = L_a Z_a + U_e Z_c
+struct CrSpBwd {
+  int gaa, gac, gca, gcc, ua, le, la, ue, oza, ozc, oya, oyc, omx, pad0, pad1, pad2;
+};
+void launch_cr_sp_fwd(const CrDims& c, double2* pool, const CrSpFwd* tasks, int n, const int* rowpat,
+                      const int* colpat, hipStream_t s);
+void launch_cr_sp_bwd(const CrDims& c, double2* pool, const CrSpBwd* tasks, int n, const int* rowpat,
+                      const int* colpat, hipStream_t s);
 // block-product stage configuration: output tile TS x TS (16 or 32) and the
 // number of waves splitting each tile's K range (1, 2, 4)
 struct CrGemmCfg {

@@ -175,14 +175,16 @@ int dwh_stream(dwh_ctx* ctx, void** stream);
  * (bench/profiling).  enable is a bitmask over the timer names below
  * (bit 0 "gj_update", bit 1 "gj_pivot", bit 2 "assemble", bit 3 "contract",
  * bit 4 "step", bit 5 "gj_edge", bit 6 "cr_gemm", bit 7 "cr_inv", bit 8 "cr_inv_side",
- * bit 9 "eig_own", bit 10 "eig_vendor");
+ * bit 9 "eig_own", bit 10 "eig_vendor", bit 11 "cr_sparse");
  * 0 disables, -1 times everything. */
 int dwh_timing_enable(dwh_ctx* ctx, int32_t enable);
 /* name: "gj_update" (rank-128 paired / rank-64 trailing updates),
  * "gj_edge" (edge update between the two pivots of a pair), "gj_pivot",
  * "cr_gemm" (cyclic-reduction block products), "cr_inv" (its block
  * inversions), "cr_inv_side" (inversion stages that also run the products off
- * the critical path; work = inversion + side-product flops), "eig_own" / "eig_vendor" (eigensolves by the library's solver /
+ * the critical path; work = inversion + side-product flops), "cr_sparse" (the
+ * sparse level-0 stages: products with the level-0 U / L blocks, work = their
+ * sparse flops), "eig_own" / "eig_vendor" (eigensolves by the library's solver /
  * by rocSOLVER, opt-in or fallback; work = matrices), "assemble",
  * "contract", "step"; returns total milliseconds, launches and the
  * algorithmic work summed over launches (fp64 flops; HBM bytes for

@@ -24,7 +24,9 @@ def check(lib, Lx, Ly, nbatch, side, inv0):
 
 @pytest.mark.parametrize("Lx,Ly", LATTICES)
 @pytest.mark.parametrize("nbatch", [14, 56])
-def test_cr_schedule_dataflow(dwhmc, Lx, Ly, nbatch):
+@pytest.mark.parametrize("sparse0", ["1", "0"])
+def test_cr_schedule_dataflow(dwhmc, monkeypatch, Lx, Ly, nbatch, sparse0):
+    monkeypatch.setenv("DWHMC_CR_SPARSE0", sparse0)
     lib = dwhmc.load_library()
     for side in (0, 1):
         for inv0 in (0, 1):
@@ -33,16 +35,23 @@ def test_cr_schedule_dataflow(dwhmc, Lx, Ly, nbatch):
             assert stats[0] == stats[1] + stats[3] and stats[1] >= 1
 
 
-def test_cr_schedule_c3_shape(dwhmc):
-    """The C3 plan (L = 32, 14 poles): 6 inversion launches, 5 of them with
-    side work, 20 product launches."""
+def test_cr_schedule_c3_shape(dwhmc, monkeypatch):
+    """The C3 plan (L = 32, 14 poles): 6 inversion launches, 4 of them with
+    side work, 20 product launches, two of them the sparse level-0 stages
+    (level 0 makes no U'/L' side work for the level-1
+    inversion); the dense level 0 (DWHMC_CR_SPARSE0=0) puts side work on 5."""
     lib = dwhmc.load_library()
+    monkeypatch.delenv("DWHMC_CR_SPARSE0", raising=False)
     rc, stats, err = check(lib, 32, 32, 14, 1, 1)
     assert rc == 0, err
-    assert list(stats[:4]) == [26, 6, 5, 20]
+    assert list(stats[:4]) == [26, 6, 4, 20]
     rc, stats, err = check(lib, 32, 32, 14, 0, 1)
     assert rc == 0, err
     assert list(stats[:4]) == [26, 6, 0, 20]
+    monkeypatch.setenv("DWHMC_CR_SPARSE0", "0")
+    rc, stats, err = check(lib, 32, 32, 14, 1, 1)
+    assert rc == 0, err
+    assert list(stats[:4]) == [26, 6, 5, 20]
 
 
 def test_cr_schedule_rejects_wide_rows(dwhmc):
@@ -70,14 +79,19 @@ def plan_flops(lib, Lx, Ly, nbatch, side, inv0):
 @pytest.mark.parametrize("Lx,Ly", [(4, 1), (4, 2), (3, 3), (8, 8), (17, 4), (20, 6), (24, 24), (32, 5),
                                    (32, 32), (32, 33), (48, 48), (64, 9)])
 @pytest.mark.parametrize("nbatch", [13, 52])
-def test_cr_plan_flops_independent_count(dwhmc, Lx, Ly, nbatch):
+@pytest.mark.parametrize("sparse0", ["1", "0"])
+def test_cr_plan_flops_independent_count(dwhmc, monkeypatch, Lx, Ly, nbatch, sparse0):
     """The plan's per-stage algorithmic flops (what the cr_* timers, bench.py's
     alg_flops_per_step and the roofline use) against tools/cr_model.py's count
     of the recursion: moving products into inversion launches (side work)
-    must move their flops with them, never drop them (VERDICT r02 weak #3)."""
+    must move their flops with them, never drop them.
+    With the sparse level 0 (default for even block rows >= 4) the count of
+    its sparse products comes from the nonzeros of an oracle-assembled BdG
+    matrix, not from the library's tables."""
     from tools.cr_model import cr_flop_count
+    monkeypatch.setenv("DWHMC_CR_SPARSE0", sparse0)
     lib = dwhmc.load_library()
-    inv_ref, prod_ref = cr_flop_count(Lx, Ly, default_rows(Lx, Ly))
+    inv_ref, prod_ref = cr_flop_count(Lx, Ly, default_rows(Lx, Ly), sparse0=sparse0 == "1")
     for side in (0, 1):
         for inv0 in (0, 1):
             inv, prod, side_f = plan_flops(lib, Lx, Ly, nbatch, side, inv0)
@@ -88,10 +102,12 @@ def test_cr_plan_flops_independent_count(dwhmc, Lx, Ly, nbatch):
 
 
 def test_cr_plan_flops_c3_side_work(dwhmc):
-    """At C3 (L = 32, 13 poles) the side work carries real products."""
+    """At C3 (L = 32, 13 poles) the side work carries real products (the W
+    products of levels 1 and 2 and U'/L' of levels 1-3: 16 % of the product
+    flops with the sparse level 0, which leaves no level-0 side work)."""
     lib = dwhmc.load_library()
     inv, prod, side_f = plan_flops(lib, 32, 32, 13, 1, 1)
-    assert side_f > 0.2 * (prod + side_f)
+    assert side_f > 0.12 * (prod + side_f)
 
 
 @pytest.mark.parametrize("Lx,Ly,rows,blocks", [(8, 8, 2, 4), (4, 4, 4, 1), (4, 6, 3, 2), (6, 9, 1, 9), (5, 7, 1, 7),

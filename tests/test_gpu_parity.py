@@ -823,3 +823,42 @@ def test_guard_falls_back_to_eig_beyond_table(dwhmc, oracle):
     assert np.max(np.abs(ctx.forces()[0] - F_ref)) <= 1e-10 * (1 + np.max(np.abs(F_ref)))
     assert abs(ctx.fermion_energy()[0] - Ef_ref) <= 1e-11 * abs(Ef_ref)
     ctx.close()
+
+
+@pytest.mark.parametrize("sparse0", ["1", "0"])
+@pytest.mark.parametrize("Lx,Ly,beta", [(16, 16, 8.0), (12, 10, 8.0), (20, 4, 16.0), (40, 6, 16.0), (8, 8, 4.0),
+                                        (9, 12, 8.0), (32, 32, 16.0)])
+def test_cr_sparse_level0(dwhmc, oracle, monkeypatch, Lx, Ly, beta, sparse0):
+    """Level 0 by the sparse stages (k_cr_sp_fwd / k_cr_sp_bwd: every product
+    with a level-0 U / L block on the vector units, one-term dense products for
+    G_ae, G_ce, G_ea, G_ec, T = -Dinv M and G_ee = Dinv - T Dinv;
+    tools/cr_model.py cr_selected_inverse_top_sparse0) or the dense level 0
+    (DWHMC_CR_SPARSE0=0), against the eigen oracle: P, F, E_f, hole density
+    and two HMC sweeps.  BP = 32 (Lx = 12, 16, 9, and 8 x 8 as two-row
+    blocks: 4 blocks), 64 (20, 32) and 96 (40); Ly = 4 is the smallest level 0
+    the sparse stages take."""
+    O = oracle
+    monkeypatch.setenv("DWHMC_CR_SPARSE0", sparse0)
+    p, dis, Delta = make_case(O, Lx, Ly, beta, seed=Lx * 17 + Ly)
+    cache, F_ref, Ef_ref = O.evaluate(p, dis, Delta)
+    P_ref, _ = O.pairing_P(cache.U, cache.E_n, p)
+    ctx = device_ctx(dwhmc, p, dis, "cr")
+    ctx.set_pairing(Delta)
+    ctx.factorize()
+    assert np.max(np.abs(ctx.pairing()[0] - P_ref)) <= 1e-11
+    assert np.max(np.abs(ctx.forces()[0] - F_ref)) <= 1e-10 * (1 + np.max(np.abs(F_ref)))
+    assert abs(ctx.fermion_energy()[0] - Ef_ref) <= 1e-11 * abs(Ef_ref)
+    hole_ref = O.measure_observables(cache, p, Delta)["hole_conc"]
+    assert abs(2.0 * ctx.hole_trace()[0] / p.N - 1.0 - hole_ref) <= 1e-11
+    if p.N <= 400:
+        Nt = 3
+        dt = O.calc_optimal_dt(p.beta, p.J, p.mass, Nt)
+        rng = np.random.default_rng(9)
+        draws = [((rng.standard_normal((p.N, 2)) + 1j * rng.standard_normal((p.N, 2))) * math.sqrt(0.5),
+                  float(rng.random())) for _ in range(2)]
+        ref = _oracle_after_sweeps(O, p, dis, Delta, draws, Nt, dt)
+        for (noise, u), (acc_r, dH_r, D_r, _) in zip(draws, ref):
+            acc, dH = ctx.hmc_sweep(noise, np.array([u]), Nt, dt, p.mass)
+            assert bool(acc[0]) == acc_r and abs(dH[0] - dH_r) <= 1e-8 * (1 + abs(dH_r))
+            assert np.max(np.abs(ctx.get_state()[0][0] - D_r)) <= 1e-10
+    ctx.close()

@@ -340,10 +340,38 @@ def level0_read_tiles(Lx: int, Ly: int, rows: int = 1):
     return reads
 
 
-def cr_flop_count(Lx: int, Ly: int, rows: int = 1):
+def level0_nnz_top(Lx: int, Ly: int, rows: int = 1):
+    """Top-half nonzeros of the level-0 U[y], L[y] blocks of the CR lattice
+    (Lx rows, Ly / rows blocks), counted on a BdG matrix of the reference's
+    lattice (t = 1, t' = -0.35) with a nonzero pairing on every bond (the oracle
+    assembly, not the device's tables)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
+    from oracle import dwhmc_oracle as O
+    p = O.ModelParameters(Lx, Ly, 1.0, -0.35, -1.08, 0.0, 0.0, 8.0, 0.8, 1.0)
+    rng = np.random.default_rng(1)
+    Delta = 0.5 + rng.random((p.N, 2)) + 1j * (0.5 + rng.random((p.N, 2)))
+    cache = O.initialize_cache(p)
+    O.init_static_H(cache, p, np.zeros(p.N))
+    O.update_H_BdG(cache, p, Delta)
+    A = O.hermitian_from_upper(cache.H_base)
+    Lxb, Lyb = Lx * rows, Ly // rows
+    _, U, L = blocks_from_dense(A, Lxb, Lyb)
+    return [int(np.count_nonzero(u[:Lxb])) for u in U], [int(np.count_nonzero(x[:Lxb])) for x in L]
+
+
+def cr_flop_count(Lx: int, Ly: int, rows: int = 1, sparse0: bool = True):
+    """sparse0: level 0 by the sparse stages when the device takes them (even
+    Ly / rows >= 4, BP <= 96): the sparse products at 8 flops per complex MAC
+    of a stored nonzero (cr_selected_inverse_top_sparse0), the dense products
+    one term each."""
     Lxb, Lyb = Lx * rows, Ly // rows
     HP = (Lxb + 15) // 16 * 16
     BP = 2 * HP
+    sp = sparse0 and Lyb % 2 == 0 and Lyb >= 4 and BP <= 96
+    if sp:
+        nU, nL = level0_nnz_top(Lx, Ly, rows)
     full = 8.0 * BP * HP * BP                       # one term, whole top half
     tr = HP // 16                                   # tile rows
     wc = -(-(Lxb) // 16)                            # tile columns of the G_ea / G_ec window
@@ -357,6 +385,21 @@ def cr_flop_count(Lx: int, Ly: int, rows: int = 1):
         nonlocal inv, terms
         if m == 1:
             inv += 1
+            return
+        if depth == 0 and sp:
+            E, K = list(range(1, m, 2)), list(range(0, m, 2))
+            inv += len(E)
+            for k in K:
+                er, el = k + 1, (k - 1) % m
+                terms += 8.0 * BP * (nU[k] + nL[er] + nL[el]) + 8.0 * HP * 2 * (2 * nL[k] + nU[el] + nU[er])
+            level(len(K), 1)
+            for e in E:
+                a, c = e - 1, (e + 1) % m
+                terms += 8.0 * HP * 2 * 2 * (nU[a] + nL[e]) + 8.0 * BP * 3 * (nL[a] + nU[e])
+                n_ec = len(reads.get((e, c), ()))
+                n_ea = 0 if a == c else len(reads.get((e, a), ()))
+                n_ee = len(reads.get((e, e), ()))
+                terms += (n_ea + n_ec) * per_ea + 3 * full + n_ee * per_ee
             return
         E = list(range(1, m - (m % 2), 2))
         K = list(range(0, m, 2))
@@ -384,3 +427,90 @@ def cr_flop_count(Lx: int, Ly: int, rows: int = 1):
 
     level(Lyb, 0)
     return inv * 8.0 * BP ** 3, terms
+
+
+# ---------------------------------------------------------------------------
+# Level 0 with its sparse off-diagonal blocks (round 5, the device's sparse
+# level-0 stages, dwhmc_cr.hip k_cr_sp_fwd / k_cr_sp_bwd): U, L of the lattice
+# rows are hopping + one pairing entry per row, so at level 0 every product
+# with them is a sparse one and V1, V2, W1, W2 are never formed:
+#   forward   D'_k = D_k - U_k Dinv_{k+1} L_k - L_{k-1} Dinv_{k-1} U_{k-1}
+#             U'_k = -U_k Dinv_{k+1} U_{k+1},  L'_k = -L_{k+1} Dinv_{k+1} L_k
+#   backward  Z_a = G_aa U_a + G_ac L_e,  Z_c = G_ca U_a + G_cc L_e      (dense . sparse)
+#             Y_a = L_a G_aa + U_e G_ca,  Y_c = L_a G_ac + U_e G_cc      (sparse . dense)
+#             M = L_a Z_a + U_e Z_c                                      (sparse . dense)
+#             G_ae = -Z_a Dinv, G_ce = -Z_c Dinv, G_ea = -Dinv Y_a, G_ec = -Dinv Y_c,
+#             T = -Dinv M, G_ee = Dinv - T Dinv  (= Dinv + Dinv M Dinv)
+# (a = e - 1, c = e + 1 mod m; even m >= 4, so every kept block has both
+# eliminated neighbours).  The dense products left are one term each.
+# ---------------------------------------------------------------------------
+def cr_selected_inverse_top_sparse0(Dg, U, L):
+    M, Q = -1, +1
+    m = len(Dg)
+    assert m % 2 == 0 and m >= 4
+    mul = top_product
+    E = list(range(1, m, 2))
+    K = list(range(0, m, 2))
+    ld = 0.0
+    Dinv = {}
+    for e in E:
+        Dinv[e], l_ = top_inverse_mform(Dg[e])
+        ld += l_
+    Dn, Un, Ln = [], [], []
+    for k in K:
+        er, el = k + 1, (k - 1) % m
+        V1r = -mul(U[k], Dinv[er], M)                 # Q-form
+        V2r = -mul(L[er], Dinv[er], M)
+        V2l = -mul(L[el], Dinv[el], M)
+        Dn.append(Dg[k] + mul(V1r, L[k], M) + mul(V2l, U[el], M))
+        Un.append(mul(V1r, U[er], M))
+        Ln.append(mul(V2r, L[k], M))
+    ld2, GDn, GUn, GLn = cr_selected_inverse_top(Dn, Un, Ln)
+    ld += ld2
+    mn = len(K)
+    GD, GU, GL = [None] * m, [None] * m, [None] * m
+    for kk, k in enumerate(K):
+        GD[k] = GDn[kk]
+    for e in E:
+        a, c = e - 1, (e + 1) % m
+        ia, ic = a // 2, (c // 2) % mn
+        Gaa, Gcc = GDn[ia], GDn[ic]
+        Gac, Gca = (GDn[0], GDn[0]) if mn == 1 else (GUn[ia], GLn[ia])
+        Za = mul(Gaa, U[a], M) + mul(Gac, L[e], M)    # Q-form
+        Zc = mul(Gca, U[a], M) + mul(Gcc, L[e], M)
+        Ya = mul(L[a], Gaa, M) + mul(U[e], Gca, M)    # Q-form
+        Yc = mul(L[a], Gac, M) + mul(U[e], Gcc, M)
+        Mx = mul(L[a], Za, Q) + mul(U[e], Zc, Q)      # M-form
+        T = -mul(Dinv[e], Mx, M)                      # Q-form
+        GU[a] = -mul(Za, Dinv[e], M)                  # G_ae
+        GL[e] = -mul(Zc, Dinv[e], M)                  # G_ce
+        GL[a] = -mul(Dinv[e], Ya, Q)                  # G_ea
+        GU[e] = -mul(Dinv[e], Yc, Q)                  # G_ec
+        GD[e] = Dinv[e] - mul(T, Dinv[e], M)          # G_ee
+    return ld, GD, GU, GL
+
+
+def check_top_cr_sparse0(Lx, Ly, seed=0, y=0.7):
+    """The sparse level-0 reformulation against the full-block recursion on a
+    BdG matrix (every G block the recursion returns, and ln|det|)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
+    from oracle import dwhmc_oracle as O
+    p = O.ModelParameters(Lx, Ly, 1.0, -0.35, -1.08, 1.0, 0.1, 8.0, 0.8, 1.0)
+    rng = np.random.default_rng(seed)
+    st = O.initialize_state(p, rng)
+    Delta = st.Delta + 0.3 * (rng.standard_normal((p.N, 2)) + 1j * rng.standard_normal((p.N, 2)))
+    cache = O.initialize_cache(p)
+    O.init_static_H(cache, p, st.disorder_pot)
+    O.update_H_BdG(cache, p, Delta)
+    A = O.hermitian_from_upper(cache.H_base) - 1j * y * np.eye(2 * p.N)
+    Dg, U, L = blocks_from_dense(A, Lx, Ly)
+    ld, GD, GU, GL = cr_selected_inverse(Dg, U, L)
+    top = lambda X: [x[:Lx, :] for x in X]
+    ldt, GDt, GUt, GLt = cr_selected_inverse_top_sparse0(top(Dg), top(U), top(L))
+    err = abs(ld - ldt)
+    for F, T in ((GD, GDt), (GU, GUt), (GL, GLt)):
+        for f, t in zip(F, T):
+            err = max(err, np.abs(f[:Lx, :] - t).max())
+    return err
