@@ -134,13 +134,14 @@ struct CrPlan {
 // (x, HP + x_j) for partners j in the other row), as entries of the FULL
 // block: row x of the top half, and row HP + x synthesised from it (M-form:
 // [conj B | -conj A]).  Entry = top-half offset | (column for rowpat, row for
-// colpat) << 14 | op << 22 (op 0 as stored, 1 conj, 2 -conj).  False when a
+// colpat) << 14 | op << 22 (op 0 as stored, 1 conj, 2 -conj, 3 empty).  False when a
 // row or column holds more than kCrSpNZ entries (the dense level 0 then runs).
 bool cr_sparse_patterns(int Lx, int Ly, int BP, const std::vector<int>& hcol, const std::vector<int>& Dcol,
                         std::vector<int>& rowpat, std::vector<int>& colpat) {
   const int HP = BP / 2, NZ = dwh::kCrSpNZ;
-  rowpat.assign((size_t)3 * Ly * NZ * BP, -1);
-  colpat.assign((size_t)3 * Ly * NZ * BP, -1);
+  const int empty = 3 << 22;   // op 3: weight zero (dwhmc_cr_sparse.hip sp_val)
+  rowpat.assign((size_t)3 * Ly * NZ * BP, empty);
+  colpat.assign((size_t)3 * Ly * NZ * BP, empty);
   for (int t = 1; t <= 2; ++t)
     for (int y = 0; y < Ly; ++y) {
       if ((t == 1 && Ly < 2) || (t == 2 && Ly < 3)) continue;   // k_cr_fill's zero blocks
@@ -176,7 +177,7 @@ bool cr_sparse_patterns(int Lx, int Ly, int BP, const std::vector<int>& hcol, co
 // nonzeros of row r / column c of level-0 block b in the patterns
 int sp_nrow(const std::vector<int>& pat, int b, int r, int BP) {
   int n = 0;
-  for (int e = 0; e < dwh::kCrSpNZ; ++e) n += pat[((size_t)b * dwh::kCrSpNZ + e) * BP + r] >= 0;
+  for (int e = 0; e < dwh::kCrSpNZ; ++e) n += ((pat[((size_t)b * dwh::kCrSpNZ + e) * BP + r] >> 22) & 3) != 3;
   return n;
 }
 

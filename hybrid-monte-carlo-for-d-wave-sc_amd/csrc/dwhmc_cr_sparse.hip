@@ -17,7 +17,7 @@
 //   backward (k_cr_sp_bwd, per eliminated row e, a = e-1, c = e+1):
 //     Z_a = G_aa U_a + G_ac L_e,  Z_c = G_ca U_a + G_cc L_e     (dense . sparse)
 //     Y_a = L_a G_aa + U_e G_ca,  Y_c = L_a G_ac + U_e G_cc     (sparse . dense)
-//     M   = L_a Z_a + U_e Z_c                                   (sparse . dense, Z from LDS)
+//     M   = L_a Z_a + U_e Z_c = Y_a U_a + Y_c L_e               (dense . sparse, Y rows in LDS)
 //   after which one-term dense products (k_cr_gemm) finish the level:
 //     G_ae = -Z_a Dinv, G_ce = -Z_c Dinv, G_ea = -Dinv Y_a, G_ec = -Dinv Y_c,
 //     T = -Dinv M, then G_ee = Dinv - T Dinv.
@@ -29,18 +29,25 @@
 // and pairing tables exactly as k_cr_fill writes the blocks): entry = offset
 // of the stored top-half element | (column or row index) << 14 | op << 22,
 // op 0: the element, 1: its conjugate, 2: minus its conjugate (the
-// synthesised bottom half); -1: empty.  Pattern layout [block][entry][BP]
-// (lanes over the last index read contiguous words).
+// synthesised bottom half), 3: empty (reads element 0, weight zero, so every
+// load is unconditional and issued up front).  Pattern layout
+// [block][entry][BP] (lanes over the last index read contiguous words).
+// One wave per output row: every row of every output depends only on rows of
+// the inputs, and the backward M = L_a Z_a + U_e Z_c is formed as
+// Y_a U_a + Y_c L_e (the same sum regrouped), from the wave's own Y rows.
 #include "dwhmc_device.h"
 #include "dwhmc_internal.h"
 
 namespace dwh {
 namespace {
 
+// stored value of pattern entry e (op 3: zero)
 __device__ __forceinline__ double2 sp_val(const double2* __restrict__ S, int e) {
   const int off = e & 0x3fff, op = (e >> 22) & 3;
   const double2 v = S[off];
-  return op == 0 ? v : (op == 1 ? make_double2(v.x, -v.y) : make_double2(-v.x, v.y));
+  const double sr = op == 2 ? -1.0 : (op == 3 ? 0.0 : 1.0);
+  const double si = op == 1 ? -1.0 : (op == 3 ? 0.0 : 1.0);
+  return make_double2(sr * v.x, si * v.y);
 }
 __device__ __forceinline__ int sp_idx(int e) { return (e >> 14) & 0xff; }
 
@@ -55,14 +62,21 @@ __device__ __forceinline__ void cmac(double2& a, double2 b, double2 c) {
 template <int BP>
 __device__ __forceinline__ double2 full_at(const double2* __restrict__ X, double s, int kk, int c) {
   constexpr int HP = BP / 2;
-  if (kk < HP) return X[kk * BP + c];
-  const int cc = c < HP ? c + HP : c - HP;
-  const double2 u = X[(kk - HP) * BP + cc];
-  const double sg = c < HP ? -s : s;
-  return make_double2(sg * u.x, -sg * u.y);
+  const bool top = kk < HP;
+  const int cc = top ? c : (c < HP ? c + HP : c - HP);
+  const double2 u = X[(top ? kk : kk - HP) * BP + cc];
+  const double sg = top ? 1.0 : (c < HP ? -s : s);
+  return top ? u : make_double2(sg * u.x, -sg * u.y);
 }
 
-constexpr int kSpRowsWG = 4;   // one row per wave, four waves per workgroup
+constexpr int kSpRowsWG = 4;   // one output row per wave, four waves per workgroup
+constexpr int NZ = kCrSpNZ;
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 // forward: one wave per output row r of the kept row k's D', U', L'
 template <int BP>
@@ -79,41 +93,47 @@ __global__ __launch_bounds__(256) void k_cr_sp_fwd(double2* __restrict__ pool, i
   double2* base = pool + (int64_t)blockIdx.y * item;
   const double2 *Dir = base + t->dir * BB, *Dil = base + t->dil * BB;
   const double2 *Uk = base + t->uk * BB, *Ler = base + t->ler * BB, *Lel = base + t->lel * BB;
-  // V rows: V1r[r, :] = -U_k[r, :] Dinv_er, V2r = -L_er[r, :] Dinv_er, V2l = -L_el[r, :] Dinv_el
+  const double2 *Lk = base + t->lk * BB, *Uel = base + t->uel * BB, *Uer = base + t->uer * BB;
+  const double2* Dk = base + t->dk * BB;
+  // row r of U_k, L_er, L_el (uniform) and the column patterns of this lane's
+  // columns of L_k, U_el, U_er: every pattern load first, then every value
+  int pu[NZ], pr[NZ], pl[NZ], ql[NCL][NZ], qu[NCL][NZ], qr[NCL][NZ];
+#pragma unroll
+  for (int e = 0; e < NZ; ++e) {
+    pu[e] = rowpat[(t->uk * NZ + e) * BP + r];
+    pr[e] = rowpat[(t->ler * NZ + e) * BP + r];
+    pl[e] = rowpat[(t->lel * NZ + e) * BP + r];
+#pragma unroll
+    for (int j = 0; j < NCL; ++j) {
+      const int c = min(l + 64 * j, BP - 1);
+      ql[j][e] = colpat[(t->lk * NZ + e) * BP + c];
+      qu[j][e] = colpat[(t->uel * NZ + e) * BP + c];
+      qr[j][e] = colpat[(t->uer * NZ + e) * BP + c];
+    }
+  }
   double2 v1[NCL], v2r[NCL], v2l[NCL];
 #pragma unroll
   for (int j = 0; j < NCL; ++j) v1[j] = v2r[j] = v2l[j] = make_double2(0.0, 0.0);
 #pragma unroll
-  for (int e = 0; e < kCrSpNZ; ++e) {
-    const int pu = rowpat[(t->uk * kCrSpNZ + e) * BP + r];
-    const int pr = rowpat[(t->ler * kCrSpNZ + e) * BP + r];
-    const int pl = rowpat[(t->lel * kCrSpNZ + e) * BP + r];
-    const double2 vu = pu >= 0 ? sp_val(Uk, pu) : make_double2(0.0, 0.0);
-    const double2 vr = pr >= 0 ? sp_val(Ler, pr) : make_double2(0.0, 0.0);
-    const double2 vl = pl >= 0 ? sp_val(Lel, pl) : make_double2(0.0, 0.0);
+  for (int e = 0; e < NZ; ++e) {
+    const double2 vu = sp_val(Uk, pu[e]), vr = sp_val(Ler, pr[e]), vl = sp_val(Lel, pl[e]);
 #pragma unroll
     for (int j = 0; j < NCL; ++j) {
-      const int c = l + 64 * j;
-      if (c >= BP) continue;
-      if (pu >= 0) cmac(v1[j], vu, full_at<BP>(Dir, -1.0, sp_idx(pu), c));
-      if (pr >= 0) cmac(v2r[j], vr, full_at<BP>(Dir, -1.0, sp_idx(pr), c));
-      if (pl >= 0) cmac(v2l[j], vl, full_at<BP>(Dil, -1.0, sp_idx(pl), c));
+      const int c = min(l + 64 * j, BP - 1);
+      cmac(v1[j], vu, full_at<BP>(Dir, -1.0, sp_idx(pu[e]), c));
+      cmac(v2r[j], vr, full_at<BP>(Dir, -1.0, sp_idx(pr[e]), c));
+      cmac(v2l[j], vl, full_at<BP>(Dil, -1.0, sp_idx(pl[e]), c));
     }
   }
 #pragma unroll
   for (int j = 0; j < NCL; ++j) {
     const int c = l + 64 * j;
     if (c >= BP) continue;
-    sc[w][0][c] = make_double2(-v1[j].x, -v1[j].y);
-    sc[w][1][c] = make_double2(-v2r[j].x, -v2r[j].y);
-    sc[w][2][c] = make_double2(-v2l[j].x, -v2l[j].y);
+    sc[w][0][c] = make_double2(-v1[j].x, -v1[j].y);   // V1r = -U_k Dinv_er
+    sc[w][1][c] = make_double2(-v2r[j].x, -v2r[j].y);  // V2r = -L_er Dinv_er
+    sc[w][2][c] = make_double2(-v2l[j].x, -v2l[j].y);  // V2l = -L_el Dinv_el
   }
-  // the wave reads what its other lanes wrote
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const double2 *Lk = base + t->lk * BB, *Uel = base + t->uel * BB, *Uer = base + t->uer * BB;
-  const double2* Dk = base + t->dk * BB;
+  wave_sync();
   double2 *On = base + t->od * BB, *Ou = base + t->ou * BB, *Ol = base + t->ol * BB;
 #pragma unroll
   for (int j = 0; j < NCL; ++j) {
@@ -121,17 +141,12 @@ __global__ __launch_bounds__(256) void k_cr_sp_fwd(double2* __restrict__ pool, i
     if (c >= BP) continue;
     double2 d = Dk[r * BP + c], u = make_double2(0.0, 0.0), lo = make_double2(0.0, 0.0);
 #pragma unroll
-    for (int e = 0; e < kCrSpNZ; ++e) {
-      const int ql = colpat[(t->lk * kCrSpNZ + e) * BP + c];
-      const int qu = colpat[(t->uel * kCrSpNZ + e) * BP + c];
-      const int qr = colpat[(t->uer * kCrSpNZ + e) * BP + c];
-      if (ql >= 0) {
-        const double2 v = sp_val(Lk, ql);
-        cmac(d, sc[w][0][sp_idx(ql)], v);    // V1r L_k
-        cmac(lo, sc[w][1][sp_idx(ql)], v);   // V2r L_k
-      }
-      if (qu >= 0) cmac(d, sc[w][2][sp_idx(qu)], sp_val(Uel, qu));   // V2l U_el
-      if (qr >= 0) cmac(u, sc[w][0][sp_idx(qr)], sp_val(Uer, qr));   // V1r U_er
+    for (int e = 0; e < NZ; ++e) {
+      const double2 vl = sp_val(Lk, ql[j][e]), vu = sp_val(Uel, qu[j][e]), vr = sp_val(Uer, qr[j][e]);
+      cmac(d, sc[w][0][sp_idx(ql[j][e])], vl);    // V1r L_k
+      cmac(lo, sc[w][1][sp_idx(ql[j][e])], vl);   // V2r L_k
+      cmac(d, sc[w][2][sp_idx(qu[j][e])], vu);    // V2l U_el
+      cmac(u, sc[w][0][sp_idx(qr[j][e])], vr);    // V1r U_er
     }
     On[r * BP + c] = d;
     Ou[r * BP + c] = u;
@@ -139,112 +154,89 @@ __global__ __launch_bounds__(256) void k_cr_sp_fwd(double2* __restrict__ pool, i
   }
 }
 
-// backward: z = 0 workgroups form Z_a, Z_c (to the pool and LDS) and then M;
-// z = 1 workgroups form Y_a, Y_c.  Waves over rows.
+// backward: one wave per output row r of the eliminated row e's Z_a, Z_c,
+// Y_a, Y_c and M = Y_a U_a + Y_c L_e
 template <int BP>
 __global__ __launch_bounds__(256) void k_cr_sp_bwd(double2* __restrict__ pool, int64_t item,
                                                    const CrSpBwd* __restrict__ tasks, const int* __restrict__ rowpat,
-                                                   const int* __restrict__ colpat) {
+                                                   const int* __restrict__ colpat, int nrb) {
   constexpr int HP = BP / 2, NCL = (BP + 63) / 64;
   constexpr int64_t BB = (int64_t)HP * BP;
+  __shared__ double2 sc[kSpRowsWG][2][BP];
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-  const CrSpBwd* t = tasks + blockIdx.x;
+  const int ti = __builtin_amdgcn_readfirstlane(blockIdx.x / nrb);
+  const int r = __builtin_amdgcn_readfirstlane((blockIdx.x - ti * nrb) * kSpRowsWG + w);
+  const CrSpBwd* t = tasks + ti;
   double2* base = pool + (int64_t)blockIdx.y * item;
   const double2 *Gaa = base + t->gaa * BB, *Gac = base + t->gac * BB, *Gca = base + t->gca * BB,
                 *Gcc = base + t->gcc * BB;
   const double2 *Ua = base + t->ua * BB, *Le = base + t->le * BB, *La = base + t->la * BB, *Ue = base + t->ue * BB;
-  if (blockIdx.z == 1) {
-    // Y_a[r, :] = L_a[r, :] G_aa + U_e[r, :] G_ca, Y_c[r, :] = L_a[r, :] G_ac + U_e[r, :] G_cc
-    double2 *Oya = base + t->oya * BB, *Oyc = base + t->oyc * BB;
-    for (int r = w; r < HP; r += 4) {
-      double2 ya[NCL], yc[NCL];
+  int pa[NZ], pe[NZ], qa[NCL][NZ], qe[NCL][NZ];
 #pragma unroll
-      for (int j = 0; j < NCL; ++j) ya[j] = yc[j] = make_double2(0.0, 0.0);
+  for (int e = 0; e < NZ; ++e) {
+    pa[e] = rowpat[(t->la * NZ + e) * BP + r];
+    pe[e] = rowpat[(t->ue * NZ + e) * BP + r];
 #pragma unroll
-      for (int e = 0; e < kCrSpNZ; ++e) {
-        const int pa = rowpat[(t->la * kCrSpNZ + e) * BP + r];
-        const int pe = rowpat[(t->ue * kCrSpNZ + e) * BP + r];
-        const double2 va = pa >= 0 ? sp_val(La, pa) : make_double2(0.0, 0.0);
-        const double2 ve = pe >= 0 ? sp_val(Ue, pe) : make_double2(0.0, 0.0);
-#pragma unroll
-        for (int j = 0; j < NCL; ++j) {
-          const int c = l + 64 * j;
-          if (c >= BP) continue;
-          if (pa >= 0) {
-            cmac(ya[j], va, full_at<BP>(Gaa, -1.0, sp_idx(pa), c));
-            cmac(yc[j], va, full_at<BP>(Gac, -1.0, sp_idx(pa), c));
-          }
-          if (pe >= 0) {
-            cmac(ya[j], ve, full_at<BP>(Gca, -1.0, sp_idx(pe), c));
-            cmac(yc[j], ve, full_at<BP>(Gcc, -1.0, sp_idx(pe), c));
-          }
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < NCL; ++j) {
-        const int c = l + 64 * j;
-        if (c >= BP) continue;
-        Oya[r * BP + c] = ya[j];
-        Oyc[r * BP + c] = yc[j];
-      }
+    for (int j = 0; j < NCL; ++j) {
+      const int c = min(l + 64 * j, BP - 1);
+      qa[j][e] = colpat[(t->ua * NZ + e) * BP + c];
+      qe[j][e] = colpat[(t->le * NZ + e) * BP + c];
     }
-    return;
   }
-  __shared__ double2 Z[2][HP * BP];
-  double2 *Oza = base + t->oza * BB, *Ozc = base + t->ozc * BB, *Omx = base + t->omx * BB;
+  // Y_a[r, :] = L_a[r, :] G_aa + U_e[r, :] G_ca, Y_c[r, :] = L_a[r, :] G_ac + U_e[r, :] G_cc
+  double2 ya[NCL], yc[NCL], za[NCL], zc[NCL];
+#pragma unroll
+  for (int j = 0; j < NCL; ++j) ya[j] = yc[j] = za[j] = zc[j] = make_double2(0.0, 0.0);
+#pragma unroll
+  for (int e = 0; e < NZ; ++e) {
+    const double2 va = sp_val(La, pa[e]), ve = sp_val(Ue, pe[e]);
+#pragma unroll
+    for (int j = 0; j < NCL; ++j) {
+      const int c = min(l + 64 * j, BP - 1);
+      cmac(ya[j], va, full_at<BP>(Gaa, -1.0, sp_idx(pa[e]), c));
+      cmac(yc[j], va, full_at<BP>(Gac, -1.0, sp_idx(pa[e]), c));
+      cmac(ya[j], ve, full_at<BP>(Gca, -1.0, sp_idx(pe[e]), c));
+      cmac(yc[j], ve, full_at<BP>(Gcc, -1.0, sp_idx(pe[e]), c));
+    }
+  }
   // Z_a[r, :] = G_aa[r, :] U_a + G_ac[r, :] L_e, Z_c[r, :] = G_ca[r, :] U_a + G_cc[r, :] L_e
-  for (int r = w; r < HP; r += 4) {
 #pragma unroll
-    for (int j = 0; j < NCL; ++j) {
-      const int c = l + 64 * j;
-      if (c >= BP) continue;
-      double2 za = make_double2(0.0, 0.0), zc = make_double2(0.0, 0.0);
+  for (int j = 0; j < NCL; ++j)
 #pragma unroll
-      for (int e = 0; e < kCrSpNZ; ++e) {
-        const int qa = colpat[(t->ua * kCrSpNZ + e) * BP + c];
-        const int qe = colpat[(t->le * kCrSpNZ + e) * BP + c];
-        if (qa >= 0) {
-          const double2 v = sp_val(Ua, qa);
-          cmac(za, Gaa[r * BP + sp_idx(qa)], v);
-          cmac(zc, Gca[r * BP + sp_idx(qa)], v);
-        }
-        if (qe >= 0) {
-          const double2 v = sp_val(Le, qe);
-          cmac(za, Gac[r * BP + sp_idx(qe)], v);
-          cmac(zc, Gcc[r * BP + sp_idx(qe)], v);
-        }
-      }
-      Z[0][r * BP + c] = za;
-      Z[1][r * BP + c] = zc;
-      Oza[r * BP + c] = za;
-      Ozc[r * BP + c] = zc;
+    for (int e = 0; e < NZ; ++e) {
+      const double2 vua = sp_val(Ua, qa[j][e]), vle = sp_val(Le, qe[j][e]);
+      const int ka = sp_idx(qa[j][e]), ke = sp_idx(qe[j][e]);
+      cmac(za[j], Gaa[r * BP + ka], vua);
+      cmac(zc[j], Gca[r * BP + ka], vua);
+      cmac(za[j], Gac[r * BP + ke], vle);
+      cmac(zc[j], Gcc[r * BP + ke], vle);
     }
+  double2 *Oza = base + t->oza * BB, *Ozc = base + t->ozc * BB, *Oya = base + t->oya * BB,
+          *Oyc = base + t->oyc * BB, *Omx = base + t->omx * BB;
+#pragma unroll
+  for (int j = 0; j < NCL; ++j) {
+    const int c = l + 64 * j;
+    if (c >= BP) continue;
+    sc[w][0][c] = ya[j];
+    sc[w][1][c] = yc[j];
+    Oya[r * BP + c] = ya[j];
+    Oyc[r * BP + c] = yc[j];
+    Oza[r * BP + c] = za[j];
+    Ozc[r * BP + c] = zc[j];
   }
-  __syncthreads();
-  // M[r, :] = L_a[r, :] Z_a + U_e[r, :] Z_c (Z Q-form)
-  for (int r = w; r < HP; r += 4) {
-    double2 mx[NCL];
+  wave_sync();
+  // M[r, :] = Y_a[r, :] U_a + Y_c[r, :] L_e
 #pragma unroll
-    for (int j = 0; j < NCL; ++j) mx[j] = make_double2(0.0, 0.0);
+  for (int j = 0; j < NCL; ++j) {
+    const int c = l + 64 * j;
+    if (c >= BP) continue;
+    double2 mx = make_double2(0.0, 0.0);
 #pragma unroll
-    for (int e = 0; e < kCrSpNZ; ++e) {
-      const int pa = rowpat[(t->la * kCrSpNZ + e) * BP + r];
-      const int pe = rowpat[(t->ue * kCrSpNZ + e) * BP + r];
-      const double2 va = pa >= 0 ? sp_val(La, pa) : make_double2(0.0, 0.0);
-      const double2 ve = pe >= 0 ? sp_val(Ue, pe) : make_double2(0.0, 0.0);
-#pragma unroll
-      for (int j = 0; j < NCL; ++j) {
-        const int c = l + 64 * j;
-        if (c >= BP) continue;
-        if (pa >= 0) cmac(mx[j], va, full_at<BP>(Z[0], 1.0, sp_idx(pa), c));
-        if (pe >= 0) cmac(mx[j], ve, full_at<BP>(Z[1], 1.0, sp_idx(pe), c));
-      }
+    for (int e = 0; e < NZ; ++e) {
+      cmac(mx, sc[w][0][sp_idx(qa[j][e])], sp_val(Ua, qa[j][e]));
+      cmac(mx, sc[w][1][sp_idx(qe[j][e])], sp_val(Le, qe[j][e]));
     }
-#pragma unroll
-    for (int j = 0; j < NCL; ++j) {
-      const int c = l + 64 * j;
-      if (c < BP) Omx[r * BP + c] = mx[j];
-    }
+    Omx[r * BP + c] = mx;
   }
 }
 
@@ -267,11 +259,12 @@ void launch_cr_sp_fwd(const CrDims& c, double2* pool, const CrSpFwd* tasks, int 
 void launch_cr_sp_bwd(const CrDims& c, double2* pool, const CrSpBwd* tasks, int n, const int* rowpat,
                       const int* colpat, hipStream_t s) {
   if (n <= 0) return;
-  const dim3 g(n, c.nbatch, 2), b(256);
+  const int nrb = c.BP / 2 / kSpRowsWG;
+  const dim3 g(n * nrb, c.nbatch), b(64 * kSpRowsWG);
   switch (c.BP) {
-    case 32: hipLaunchKernelGGL(k_cr_sp_bwd<32>, g, b, 0, s, pool, c.item, tasks, rowpat, colpat); break;
-    case 64: hipLaunchKernelGGL(k_cr_sp_bwd<64>, g, b, 0, s, pool, c.item, tasks, rowpat, colpat); break;
-    default: hipLaunchKernelGGL(k_cr_sp_bwd<96>, g, b, 0, s, pool, c.item, tasks, rowpat, colpat); break;
+    case 32: hipLaunchKernelGGL(k_cr_sp_bwd<32>, g, b, 0, s, pool, c.item, tasks, rowpat, colpat, nrb); break;
+    case 64: hipLaunchKernelGGL(k_cr_sp_bwd<64>, g, b, 0, s, pool, c.item, tasks, rowpat, colpat, nrb); break;
+    default: hipLaunchKernelGGL(k_cr_sp_bwd<96>, g, b, 0, s, pool, c.item, tasks, rowpat, colpat, nrb); break;
   }
 }
 

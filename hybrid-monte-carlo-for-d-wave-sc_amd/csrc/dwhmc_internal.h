@@ -112,7 +112,7 @@ void launch_cr_inv_side(const CrDims& c, double2* pool, const int* blk, const in
 // Sparse level-0 stages (dwhmc_cr_sparse.hip): the level-0 U / L blocks have
 // at most kCrSpNZ nonzeros per row and column (vertical hopping + one pairing
 // entry); rowpat / colpat hold them per pool block ([block][entry][BP], entry
-// = top-half offset | index << 14 | op << 22, -1 empty; dwhmc_cr_sparse.hip)
+// = top-half offset | index << 14 | op << 22, op 3 empty; dwhmc_cr_sparse.hip)
 constexpr int kCrSpNZ = 4;
 bool cr_supported_sparse0(int BP);
 // forward, per kept row k (er = k+1, el = k-1): D'_k = D_k + V1r L_k + V2l U_el,
@@ -123,7 +123,7 @@ struct CrSpFwd {
 };
 // backward, per eliminated row e (a = e-1, c = e+1): Z_a = G_aa U_a + G_ac L_e,
 // Z_c = G_ca U_a + G_cc L_e, Y_a = L_a G_aa + U_e G_ca, Y_c = L_a G_ac + U_e G_cc,
-// M = L_a Z_a + U_e Z_c
+// M = L_a Z_a + U_e Z_c (= Y_a U_a + Y_c L_e, the form the kernel uses)
 struct CrSpBwd {
   int gaa, gac, gca, gcc, ua, le, la, ue, oza, ozc, oya, oyc, omx, pad0, pad1, pad2;
 };

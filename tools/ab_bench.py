@@ -75,7 +75,7 @@ def main():
         ctx.timing_reset()
         ctx.run_sweeps(0, 1, a.Nt, dt, p.mass)
         ctx.synchronize()
-        keys = ("cr_gemm", "cr_inv", "cr_inv_side", "step") if ctx.info.get("algorithm", "cr") != "dense" else \
+        keys = ("cr_gemm", "cr_inv", "cr_inv_side", "cr_sparse", "step") if ctx.info.get("algorithm", "cr") != "dense" else \
             ("gj_update", "gj_pivot", "assemble", "contract", "step")
         kt = {k: ctx.timing_read(k) for k in keys}
         ctx.timing_enable(False)
