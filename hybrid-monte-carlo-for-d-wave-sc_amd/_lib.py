@@ -82,6 +82,7 @@ SIGNATURES = {
     "dwh_timing_read": (C.c_int, [_P, C.c_char_p, _DP, C.POINTER(_I64), _DP]),
     "dwh_timing_reset": (C.c_int, [_P]),
     "dwh_bench_assembly": (C.c_int, [_P, _I64]),
+    "dwh_debug_cr_stamps": (C.c_int, [_P, _I32, _P, _I64]),
     "dwh_eigensystem": (C.c_int, [_P, _I64, _P, _P]),
     "dwh_transport_grid": (C.c_int, [_D, _D, _D, C.POINTER(_I64), C.POINTER(_I64)]),
     "dwh_measure_transport": (C.c_int, [_P, _I64, _D, _D, _D, _DP, _DP, _P, _I64, _P, _P, _I64, _P]),

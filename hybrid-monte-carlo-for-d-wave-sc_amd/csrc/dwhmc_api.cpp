@@ -2463,6 +2463,30 @@ int dwh_info(dwh_ctx* ctx, dwh_info_t* out) {
   return DWH_OK;
 }
 
+int dwh_debug_cr_stamps(dwh_ctx* ctx, int32_t inv_stage, uint64_t* out, int64_t nwg) {
+  if (!ctx || !out || nwg < 1) return fail(ctx, DWH_ERR_ARG, "dwh_debug_cr_stamps: bad argument");
+  if (ctx->algo != ALGO_CR) return fail(ctx, DWH_ERR_STATE, "dwh_debug_cr_stamps: CR path only");
+#ifdef CR_STAMPS
+  int key = -1, k = 0;
+  for (const CrStage& st : ctx->plan.stages)
+    if (st.kind == 0 && k++ == inv_stage) key = ctx->plan.inv_blk[st.first];
+  if (key < 0) return fail(ctx, DWH_ERR_ARG, "dwh_debug_cr_stamps: no such inversion stage");
+  if (int rc = settle(ctx)) return rc;
+  HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+  if (dwh::cr_stamps_arm(key) != 0) return fail(ctx, DWH_ERR_HIP, "dwh_debug_cr_stamps: arm");
+  cr_enqueue(ctx);
+  HIPCHECK(ctx, hipGetLastError());
+  HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+  if (dwh::cr_stamps_arm(-1) != 0 ||
+      dwh::cr_stamps_read(reinterpret_cast<unsigned long long*>(out), (int)std::min<int64_t>(nwg, dwh::kCrStampWG)) != 0)
+    return fail(ctx, DWH_ERR_HIP, "dwh_debug_cr_stamps: read");
+  return DWH_OK;
+#else
+  (void)inv_stage;
+  return fail(ctx, DWH_ERR_STATE, "dwh_debug_cr_stamps: not a -DCR_STAMPS build");
+#endif
+}
+
 int dwh_bench_assembly(dwh_ctx* ctx, int64_t reps) {
   if (!ctx || reps < 0) return fail(ctx, DWH_ERR_ARG, "dwh_bench_assembly: bad argument");
   if (ctx->algo == ALGO_EIG) return fail(ctx, DWH_ERR_STATE, "dwh_bench_assembly: the eig path has no per-step assembly");

@@ -35,20 +35,39 @@
 
 namespace dwh {
 
-// Diagnostic build only (-DCR_STAMPS, tools/micro/cr_inv_stamps.hip): per-block
-// s_memtime stamps of k_cr_inv's phases; never compiled into the library.
+// Diagnostic build only (-DCR_STAMPS: tools/cr_inv_sched_stamps.py through
+// dwh_debug_cr_stamps, tools/micro/cr_inv_stamps.hip): per-workgroup stamps of
+// the inversion launch whose first inverted block is g_cr_stamp_key, in the
+// library's own schedule (side work and guard workgroups included).  Row of a
+// workgroup (blockIdx.y * gridDim.x + blockIdx.x < kCrStampWG): [0] / [30]
+// s_memrealtime (100 MHz, chip-wide) at entry / exit, [1..29] s_memtime
+// (shader clock) at the phase boundaries of the kernel, [31] kind (1
+// inversion, 2 side work, 3 guard).  Wave 0's view.  Never in the library.
 #ifdef CR_STAMPS
-__device__ unsigned long long g_cr_stamps[1024][16];
-#define CR_STAMP(i)                                                                  \
-  do {                                                                               \
-    __builtin_amdgcn_sched_barrier(0);                                               \
-    if (threadIdx.x == 0)                                                            \
-      g_cr_stamps[blockIdx.y * gridDim.x + blockIdx.x][i] = __builtin_amdgcn_s_memtime(); \
-    __builtin_amdgcn_sched_barrier(0);                                               \
+__device__ unsigned long long g_cr_stamps[kCrStampWG][32];
+__device__ int g_cr_stamp_key = -1;
+#define CR_STAMP_INIT(blkp) const bool stamp_on = (blkp)[0] == g_cr_stamp_key
+#define CR_STAMP_AT(i, v)                                                               \
+  do {                                                                                  \
+    __builtin_amdgcn_sched_barrier(0);                                                  \
+    const int wg_ = blockIdx.y * gridDim.x + blockIdx.x;                                \
+    if (stamp_on && threadIdx.x == 0 && wg_ < kCrStampWG) g_cr_stamps[wg_][i] = (v);     \
+    __builtin_amdgcn_sched_barrier(0);                                                  \
   } while (0)
+#define CR_STAMP(i) CR_STAMP_AT(i, __builtin_amdgcn_s_memtime())
+#define CR_RSTAMP(i) CR_STAMP_AT(i, __builtin_amdgcn_s_memrealtime())
 #else
+#define CR_STAMP_INIT(blkp) \
+  do {                      \
+  } while (0)
+#define CR_STAMP_AT(i, v) \
+  do {                    \
+  } while (0)
 #define CR_STAMP(i) \
   do {              \
+  } while (0)
+#define CR_RSTAMP(i) \
+  do {               \
   } while (0)
 #endif
 
@@ -236,7 +255,9 @@ __device__ __forceinline__ void cr_inv_wg(double2* __restrict__ pool, int64_t it
   double2* Mo = pool + (int64_t)bi * item + (int64_t)dst[li] * HP * BP;   // may equal M
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
   d4 ar[NT], ai[NT];
-  CR_STAMP(0);
+  CR_STAMP_INIT(blk);
+  CR_RSTAMP(0);
+  CR_STAMP(1);
   // Tiles in the MFMA C layout (lane: rows lk + 4 rr, column lr), except the
   // diagonal tile (w, w), which is kept TRANSPOSED until it becomes this
   // wave's pivot: its C layout is then the strided inversion layout (lane:
@@ -262,7 +283,10 @@ __device__ __forceinline__ void cr_inv_wg(double2* __restrict__ pool, int64_t it
       ar[I][rr] = v.x;
       ai[I][rr] = v.y;
     }
-  CR_STAMP(1);
+#ifdef CR_STAMPS
+  if (stamp_on) __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+  CR_STAMP(2);
   double ld = 0.0;
   // in-place inverse of the (transposed-stored) diagonal tile
   auto invert = [&](d4& tr, d4& ti) -> double {
@@ -278,7 +302,7 @@ __device__ __forceinline__ void cr_inv_wg(double2* __restrict__ pool, int64_t it
     return r;
   };
   if (w == 0) ld += invert(ar[0], ai[0]);
-  CR_STAMP(2);
+  CR_STAMP(3);
 #pragma unroll
   for (int kb = 0; kb < NT; ++kb) {
     double2(*P)[TSZ] = pan[kb & 1];
@@ -294,6 +318,7 @@ __device__ __forceinline__ void cr_inv_wg(double2* __restrict__ pool, int64_t it
         }
     }
     __syncthreads();
+    CR_STAMP(4 + 3 * kb);
     // phase 1: the publisher reads P^-1; every other wave forms X = P^-1 A_kJ
     // from its tile kb; the lookahead wave hands X and its not-yet-updated
     // column tiles to the next panel (the other waves update them there, off
@@ -333,6 +358,7 @@ __device__ __forceinline__ void cr_inv_wg(double2* __restrict__ pool, int64_t it
       }
     }
     if (has_next) __syncthreads();
+    CR_STAMP(5 + 3 * kb);
     // phase 2
     if (w == kb) {
       // this wave's column: A_Ik <- -A_Ik P^-1, tile kb <- P^-1
@@ -382,9 +408,8 @@ __device__ __forceinline__ void cr_inv_wg(double2* __restrict__ pool, int64_t it
           else mma16_3m<true>(ar[I], ai[I], P[I], xr, xi);
         }
     }
-    if (kb == 0) CR_STAMP(3);
+    CR_STAMP(6 + 3 * kb);
   }
-  CR_STAMP(4);
   // top half of the inverse: tile rows I < NT / 2
 #pragma unroll
   for (int I = 0; I < NT / 2; ++I)
@@ -399,7 +424,12 @@ __device__ __forceinline__ void cr_inv_wg(double2* __restrict__ pool, int64_t it
     for (int k = 0; k < NT; ++k) t += ldw[k];
     ldpart[(int64_t)bi * nslots + slot[li]] = t;
   }
-  CR_STAMP(5);
+#ifdef CR_STAMPS
+  if (stamp_on) __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+  CR_STAMP(28);
+  CR_RSTAMP(30);
+  CR_STAMP_AT(31, 1ull);
 }
 
 // the site guard of chain c (SiteGuard, dwhmc_internal.h): one workgroup
@@ -501,10 +531,14 @@ __global__ __launch_bounds__(256) void k_cr_inv0(double2* __restrict__ pool, int
   __shared__ double2 sR[4][TSZ], sB[4][TSZ], sZ[4][TSZ], sS[4][TSZ], sX[4][TSZ], sA[4][TSZ];
   __shared__ double ldw[2];
   const int bi = blockIdx.y, li = blockIdx.x;
+  CR_STAMP_INIT(blk);
+  CR_RSTAMP(0);
   // site guard (launch_cr_inv0 with Delta): the extra last workgroup column,
   // pole 0 of each chain, on a CU the inversions leave idle
   if (li == gcol) {
     if (bi % P == 0) inv0_site_guard(Delta + (int64_t)(bi / P) * 2 * N, site4, N, cap4, flag);
+    CR_RSTAMP(30);
+    CR_STAMP_AT(31, 3ull);
     return;
   }
   const double2* D = pool + (int64_t)bi * item + (int64_t)blk[li] * HP * BP;
@@ -512,7 +546,7 @@ __global__ __launch_bounds__(256) void k_cr_inv0(double2* __restrict__ pool, int
   double2* Mo = pool + (int64_t)bi * item + (int64_t)dst[li] * HP * BP;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
   const int ti = w >> 1, tj = w & 1;
-  CR_STAMP(0);
+  CR_STAMP(1);
   // this wave's tiles: A (C layout, registers), R and B (LDS)
   d4 acr, aci;
 #pragma unroll
@@ -527,7 +561,7 @@ __global__ __launch_bounds__(256) void k_cr_inv0(double2* __restrict__ pool, int
     sR[w][(lk + 4 * rr) * 17 + lr] = r;
   }
   __syncthreads();
-  CR_STAMP(1);
+  CR_STAMP(2);
   // Z = R B
   d4 zr = {0.0, 0.0, 0.0, 0.0}, zi = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -538,7 +572,7 @@ __global__ __launch_bounds__(256) void k_cr_inv0(double2* __restrict__ pool, int
   }
   tile_to_lds(sZ[w], zr, zi);
   __syncthreads();
-  CR_STAMP(2);
+  CR_STAMP(3);
   // S = A + B conj(Z)
   d4 sr = acr, si = aci;
 #pragma unroll
@@ -551,7 +585,7 @@ __global__ __launch_bounds__(256) void k_cr_inv0(double2* __restrict__ pool, int
   if (w == 0) ld += 0.5 * log(wave_inv16_c(sr, si));   // S00^-1 (C layout in, C layout out)
   tile_to_lds(sS[w], sr, si);                           // S00^-1, S01, S10, S11
   __syncthreads();
-  CR_STAMP(3);
+  CR_STAMP(4);
   // P = S00^-1 S01 (wave 1, sA[1]); Q = S10 S00^-1 (wave 2, registers + sA[2]);
   // wave 3 forms P itself (no barrier in its chain), T = S11 - S10 P and T^-1
   d4 qr = {0.0, 0.0, 0.0, 0.0}, qi = {0.0, 0.0, 0.0, 0.0};
@@ -573,7 +607,6 @@ __global__ __launch_bounds__(256) void k_cr_inv0(double2* __restrict__ pool, int
     tile_to_lds(sX[3], sr, si);
   }
   __syncthreads();
-  CR_STAMP(4);
   CR_STAMP(5);
   // X01 = -P T^-1 (wave 1), X10 = -T^-1 Q (wave 2), X00 = S00^-1 + P (T^-1 Q)
   // (wave 0; = S00^-1 - X01 Q), X11 = T^-1 (wave 3)
@@ -599,7 +632,6 @@ __global__ __launch_bounds__(256) void k_cr_inv0(double2* __restrict__ pool, int
   }
   __syncthreads();
   CR_STAMP(6);
-  CR_STAMP(7);
   // Y = Z conj(X)
   d4 yr = {0.0, 0.0, 0.0, 0.0}, yi = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -608,7 +640,7 @@ __global__ __launch_bounds__(256) void k_cr_inv0(double2* __restrict__ pool, int
     tile_from_lds<true>(sX[2 * k + tj], br, bim);
     mma16_3m<false>(yr, yi, sZ[2 * ti + k], br, bim);
   }
-  CR_STAMP(8);
+  CR_STAMP(7);
   // top half of D^-1 = [X | Y]
 #pragma unroll
   for (int rr = 0; rr < 4; ++rr) {
@@ -622,7 +654,12 @@ __global__ __launch_bounds__(256) void k_cr_inv0(double2* __restrict__ pool, int
     const int64_t o = (int64_t)bi * nslots + slot[li];
     ldpart[o] = 0.5 * ldA[o] + ldw[0] + ldw[1];
   }
-  CR_STAMP(9);
+#ifdef CR_STAMPS
+  if (stamp_on) __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+  CR_STAMP(28);
+  CR_RSTAMP(30);
+  CR_STAMP_AT(31, 1ull);
 }
 
 // HP = 48 (BP = 96): 3 x 3 tiles, one wave per tile (9 waves).  Z = R B,
@@ -1133,13 +1170,22 @@ __global__ __launch_bounds__(64 * NT) void k_cr_inv_side(double2* __restrict__ p
     cr_inv_wg<NT>(pool, item, b / ninv, b - (b / ninv) * ninv, blk, dst, slot, ldpart, nslots, pan, ldw);
     return;
   }
+  CR_STAMP_INIT(blk);
+  CR_RSTAMP(0);
   // the workgroups after the side work check the site guard (level-0 launches)
   if (b >= nall + nside) {
     site_guard_wg(sg, N, b - nall - nside);
+    CR_RSTAMP(30);
+    CR_STAMP_AT(31, 3ull);
     return;
   }
   cr_gemm_wg<16 * NT, 2, 1, 0, true>(pool, item, stasks, nst, maxt, nullptr, 0, total, 1.0,
                                     xcd_remap(b - nall, nside));
+#ifdef CR_STAMPS
+  if (stamp_on) __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+  CR_RSTAMP(30);
+  CR_STAMP_AT(31, 2ull);
 }
 
 // ---------------------------------------------------------------------------
@@ -1418,6 +1464,21 @@ void launch_cr_fermion_energy(const CrDims& c, const double2* pool, const int64_
 }
 
 }  // namespace dwh
+
+#ifdef CR_STAMPS
+namespace dwh {
+int cr_stamps_arm(int key) {
+  static unsigned long long zero[kCrStampWG][32];
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_cr_stamps), zero, sizeof(zero)) != hipSuccess) return -2;
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_cr_stamp_key), &key, sizeof(int)) == hipSuccess ? 0 : -2;
+}
+int cr_stamps_read(unsigned long long* out, int nwg) {
+  if (nwg > kCrStampWG) nwg = kCrStampWG;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_cr_stamps), (size_t)nwg * 32 * sizeof(unsigned long long)) ==
+                 hipSuccess ? 0 : -2;
+}
+}  // namespace dwh
+#endif
 
 #ifdef CR_GEMM_STAMPS
 extern "C" int dwh_debug_gemm_stamps_select(int total) {

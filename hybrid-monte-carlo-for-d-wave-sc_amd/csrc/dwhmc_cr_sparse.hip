@@ -69,6 +69,11 @@ __device__ __forceinline__ double2 full_at(const double2* __restrict__ X, double
   return top ? u : make_double2(sg * u.x, -sg * u.y);
 }
 
+// a lane's complex value in every lane
+__device__ __forceinline__ double2 readlane_c(double2 v, int lane) {
+  return make_double2(readlane_f64(v.x, lane), readlane_f64(v.y, lane));
+}
+
 constexpr int kSpRowsWG = 4;   // one output row per wave, four waves per workgroup
 constexpr int NZ = kCrSpNZ;
 
@@ -78,7 +83,10 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// forward: one wave per output row r of the kept row k's D', U', L'
+// forward: one wave per output row r of the kept row k's D', U', L'.  Every
+// operand of the row is loaded into registers first (pattern words, then all
+// values and dense elements at once: one memory round trip each), then the
+// arithmetic; the V rows meet in LDS.
 template <int BP>
 __global__ __launch_bounds__(256) void k_cr_sp_fwd(double2* __restrict__ pool, int64_t item,
                                                    const CrSpFwd* __restrict__ tasks, const int* __restrict__ rowpat,
@@ -89,73 +97,99 @@ __global__ __launch_bounds__(256) void k_cr_sp_fwd(double2* __restrict__ pool, i
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int ti = __builtin_amdgcn_readfirstlane(blockIdx.x / nrb);
   const int r = __builtin_amdgcn_readfirstlane((blockIdx.x - ti * nrb) * kSpRowsWG + w);
-  const CrSpFwd* t = tasks + ti;
+  const CrSpFwd t = tasks[ti];
   double2* base = pool + (int64_t)blockIdx.y * item;
-  const double2 *Dir = base + t->dir * BB, *Dil = base + t->dil * BB;
-  const double2 *Uk = base + t->uk * BB, *Ler = base + t->ler * BB, *Lel = base + t->lel * BB;
-  const double2 *Lk = base + t->lk * BB, *Uel = base + t->uel * BB, *Uer = base + t->uer * BB;
-  const double2* Dk = base + t->dk * BB;
-  // row r of U_k, L_er, L_el (uniform) and the column patterns of this lane's
-  // columns of L_k, U_el, U_er: every pattern load first, then every value
-  int pu[NZ], pr[NZ], pl[NZ], ql[NCL][NZ], qu[NCL][NZ], qr[NCL][NZ];
+  const double2 *Dir = base + t.dir * BB, *Dil = base + t.dil * BB;
+  const double2 *Uk = base + t.uk * BB, *Ler = base + t.ler * BB, *Lel = base + t.lel * BB;
+  const double2 *Lk = base + t.lk * BB, *Uel = base + t.uel * BB, *Uer = base + t.uer * BB;
+  const double2* Dk = base + t.dk * BB;
+  int cl[NCL];
+#pragma unroll
+  for (int j = 0; j < NCL; ++j) cl[j] = min(l + 64 * j, BP - 1);
+  // 1. pattern words: row r of U_k, L_er, L_el (lanes 0 .. 3 NZ - 1 load one
+  // word and its value each: vector loads, no scalar-load chain), this lane's
+  // columns of L_k, U_el, U_er
+  const int lb = l / NZ < 3 ? l / NZ : 0, le = l % NZ;
+  const int myb = lb == 0 ? t.uk : (lb == 1 ? t.ler : t.lel);
+  const int myp = rowpat[(myb * NZ + le) * BP + r];
+  int ql[NCL][NZ], qu[NCL][NZ], qr[NCL][NZ];
 #pragma unroll
   for (int e = 0; e < NZ; ++e) {
-    pu[e] = rowpat[(t->uk * NZ + e) * BP + r];
-    pr[e] = rowpat[(t->ler * NZ + e) * BP + r];
-    pl[e] = rowpat[(t->lel * NZ + e) * BP + r];
 #pragma unroll
     for (int j = 0; j < NCL; ++j) {
-      const int c = min(l + 64 * j, BP - 1);
-      ql[j][e] = colpat[(t->lk * NZ + e) * BP + c];
-      qu[j][e] = colpat[(t->uel * NZ + e) * BP + c];
-      qr[j][e] = colpat[(t->uer * NZ + e) * BP + c];
+      ql[j][e] = colpat[(t.lk * NZ + e) * BP + cl[j]];
+      qu[j][e] = colpat[(t.uel * NZ + e) * BP + cl[j]];
+      qr[j][e] = colpat[(t.uer * NZ + e) * BP + cl[j]];
     }
   }
-  double2 v1[NCL], v2r[NCL], v2l[NCL];
-#pragma unroll
-  for (int j = 0; j < NCL; ++j) v1[j] = v2r[j] = v2l[j] = make_double2(0.0, 0.0);
+  const double2 myv = sp_val(base + myb * BB, myp);
+  int pu[NZ], pr[NZ], pl[NZ];
+  double2 vu[NZ], vr[NZ], vl[NZ];
 #pragma unroll
   for (int e = 0; e < NZ; ++e) {
-    const double2 vu = sp_val(Uk, pu[e]), vr = sp_val(Ler, pr[e]), vl = sp_val(Lel, pl[e]);
+    pu[e] = __builtin_amdgcn_readlane(myp, e);
+    pr[e] = __builtin_amdgcn_readlane(myp, NZ + e);
+    pl[e] = __builtin_amdgcn_readlane(myp, 2 * NZ + e);
+    vu[e] = readlane_c(myv, e);
+    vr[e] = readlane_c(myv, NZ + e);
+    vl[e] = readlane_c(myv, 2 * NZ + e);
+  }
+  // 2. every dense element and column value the row needs
+  double2 xu[NZ][NCL], xr[NZ][NCL], xl[NZ][NCL];
+  double2 wl[NCL][NZ], wu[NCL][NZ], wr[NCL][NZ], dk[NCL];
+#pragma unroll
+  for (int e = 0; e < NZ; ++e) {
 #pragma unroll
     for (int j = 0; j < NCL; ++j) {
-      const int c = min(l + 64 * j, BP - 1);
-      cmac(v1[j], vu, full_at<BP>(Dir, -1.0, sp_idx(pu[e]), c));
-      cmac(v2r[j], vr, full_at<BP>(Dir, -1.0, sp_idx(pr[e]), c));
-      cmac(v2l[j], vl, full_at<BP>(Dil, -1.0, sp_idx(pl[e]), c));
+      xu[e][j] = full_at<BP>(Dir, -1.0, sp_idx(pu[e]), cl[j]);
+      xr[e][j] = full_at<BP>(Dir, -1.0, sp_idx(pr[e]), cl[j]);
+      xl[e][j] = full_at<BP>(Dil, -1.0, sp_idx(pl[e]), cl[j]);
+      wl[j][e] = sp_val(Lk, ql[j][e]);
+      wu[j][e] = sp_val(Uel, qu[j][e]);
+      wr[j][e] = sp_val(Uer, qr[j][e]);
     }
   }
 #pragma unroll
-  for (int j = 0; j < NCL; ++j) {
-    const int c = l + 64 * j;
-    if (c >= BP) continue;
-    sc[w][0][c] = make_double2(-v1[j].x, -v1[j].y);   // V1r = -U_k Dinv_er
-    sc[w][1][c] = make_double2(-v2r[j].x, -v2r[j].y);  // V2r = -L_er Dinv_er
-    sc[w][2][c] = make_double2(-v2l[j].x, -v2l[j].y);  // V2l = -L_el Dinv_el
-  }
-  wave_sync();
-  double2 *On = base + t->od * BB, *Ou = base + t->ou * BB, *Ol = base + t->ol * BB;
+  for (int j = 0; j < NCL; ++j) dk[j] = Dk[r * BP + cl[j]];
+  // 3. V rows: V1r = -U_k Dinv_er, V2r = -L_er Dinv_er, V2l = -L_el Dinv_el
 #pragma unroll
   for (int j = 0; j < NCL; ++j) {
-    const int c = l + 64 * j;
-    if (c >= BP) continue;
-    double2 d = Dk[r * BP + c], u = make_double2(0.0, 0.0), lo = make_double2(0.0, 0.0);
+    double2 v1 = make_double2(0.0, 0.0), v2r = v1, v2l = v1;
 #pragma unroll
     for (int e = 0; e < NZ; ++e) {
-      const double2 vl = sp_val(Lk, ql[j][e]), vu = sp_val(Uel, qu[j][e]), vr = sp_val(Uer, qr[j][e]);
-      cmac(d, sc[w][0][sp_idx(ql[j][e])], vl);    // V1r L_k
-      cmac(lo, sc[w][1][sp_idx(ql[j][e])], vl);   // V2r L_k
-      cmac(d, sc[w][2][sp_idx(qu[j][e])], vu);    // V2l U_el
-      cmac(u, sc[w][0][sp_idx(qr[j][e])], vr);    // V1r U_er
+      cmac(v1, vu[e], xu[e][j]);
+      cmac(v2r, vr[e], xr[e][j]);
+      cmac(v2l, vl[e], xl[e][j]);
     }
-    On[r * BP + c] = d;
-    Ou[r * BP + c] = u;
-    Ol[r * BP + c] = lo;
+    if (l + 64 * j < BP) {
+      sc[w][0][cl[j]] = make_double2(-v1.x, -v1.y);
+      sc[w][1][cl[j]] = make_double2(-v2r.x, -v2r.y);
+      sc[w][2][cl[j]] = make_double2(-v2l.x, -v2l.y);
+    }
+  }
+  wave_sync();
+  // 4. D'_k = D_k + V1r L_k + V2l U_el, U'_k = V1r U_er, L'_k = V2r L_k
+  double2 *On = base + t.od * BB, *Ou = base + t.ou * BB, *Ol = base + t.ol * BB;
+#pragma unroll
+  for (int j = 0; j < NCL; ++j) {
+    double2 d = dk[j], u = make_double2(0.0, 0.0), lo = make_double2(0.0, 0.0);
+#pragma unroll
+    for (int e = 0; e < NZ; ++e) {
+      cmac(d, sc[w][0][sp_idx(ql[j][e])], wl[j][e]);
+      cmac(lo, sc[w][1][sp_idx(ql[j][e])], wl[j][e]);
+      cmac(d, sc[w][2][sp_idx(qu[j][e])], wu[j][e]);
+      cmac(u, sc[w][0][sp_idx(qr[j][e])], wr[j][e]);
+    }
+    if (l + 64 * j < BP) {
+      On[r * BP + cl[j]] = d;
+      Ou[r * BP + cl[j]] = u;
+      Ol[r * BP + cl[j]] = lo;
+    }
   }
 }
 
 // backward: one wave per output row r of the eliminated row e's Z_a, Z_c,
-// Y_a, Y_c and M = Y_a U_a + Y_c L_e
+// Y_a, Y_c and M = Y_a U_a + Y_c L_e; loads first, as in the forward kernel
 template <int BP>
 __global__ __launch_bounds__(256) void k_cr_sp_bwd(double2* __restrict__ pool, int64_t item,
                                                    const CrSpBwd* __restrict__ tasks, const int* __restrict__ rowpat,
@@ -166,77 +200,93 @@ __global__ __launch_bounds__(256) void k_cr_sp_bwd(double2* __restrict__ pool, i
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int ti = __builtin_amdgcn_readfirstlane(blockIdx.x / nrb);
   const int r = __builtin_amdgcn_readfirstlane((blockIdx.x - ti * nrb) * kSpRowsWG + w);
-  const CrSpBwd* t = tasks + ti;
+  const CrSpBwd t = tasks[ti];
   double2* base = pool + (int64_t)blockIdx.y * item;
-  const double2 *Gaa = base + t->gaa * BB, *Gac = base + t->gac * BB, *Gca = base + t->gca * BB,
-                *Gcc = base + t->gcc * BB;
-  const double2 *Ua = base + t->ua * BB, *Le = base + t->le * BB, *La = base + t->la * BB, *Ue = base + t->ue * BB;
-  int pa[NZ], pe[NZ], qa[NCL][NZ], qe[NCL][NZ];
+  const double2 *Gaa = base + t.gaa * BB, *Gac = base + t.gac * BB, *Gca = base + t.gca * BB,
+                *Gcc = base + t.gcc * BB;
+  const double2 *Ua = base + t.ua * BB, *Le = base + t.le * BB, *La = base + t.la * BB, *Ue = base + t.ue * BB;
+  int cl[NCL];
+#pragma unroll
+  for (int j = 0; j < NCL; ++j) cl[j] = min(l + 64 * j, BP - 1);
+  // row r of L_a, U_e through lanes 0 .. 2 NZ - 1 (as in the forward kernel)
+  const int myb = l / NZ == 1 ? t.ue : t.la, le = l % NZ;
+  const int myp = rowpat[(myb * NZ + le) * BP + r];
+  int qa[NCL][NZ], qe[NCL][NZ];
 #pragma unroll
   for (int e = 0; e < NZ; ++e) {
-    pa[e] = rowpat[(t->la * NZ + e) * BP + r];
-    pe[e] = rowpat[(t->ue * NZ + e) * BP + r];
 #pragma unroll
     for (int j = 0; j < NCL; ++j) {
-      const int c = min(l + 64 * j, BP - 1);
-      qa[j][e] = colpat[(t->ua * NZ + e) * BP + c];
-      qe[j][e] = colpat[(t->le * NZ + e) * BP + c];
+      qa[j][e] = colpat[(t.ua * NZ + e) * BP + cl[j]];
+      qe[j][e] = colpat[(t.le * NZ + e) * BP + cl[j]];
     }
   }
-  // Y_a[r, :] = L_a[r, :] G_aa + U_e[r, :] G_ca, Y_c[r, :] = L_a[r, :] G_ac + U_e[r, :] G_cc
-  double2 ya[NCL], yc[NCL], za[NCL], zc[NCL];
-#pragma unroll
-  for (int j = 0; j < NCL; ++j) ya[j] = yc[j] = za[j] = zc[j] = make_double2(0.0, 0.0);
+  const double2 myv = sp_val(base + myb * BB, myp);
+  int pa[NZ], pe[NZ];
+  double2 va[NZ], ve[NZ];
 #pragma unroll
   for (int e = 0; e < NZ; ++e) {
-    const double2 va = sp_val(La, pa[e]), ve = sp_val(Ue, pe[e]);
+    pa[e] = __builtin_amdgcn_readlane(myp, e);
+    pe[e] = __builtin_amdgcn_readlane(myp, NZ + e);
+    va[e] = readlane_c(myv, e);
+    ve[e] = readlane_c(myv, NZ + e);
+  }
+  double2 gaa[NZ][NCL], gac[NZ][NCL], gca[NZ][NCL], gcc[NZ][NCL];
+  double2 wa[NCL][NZ], we[NCL][NZ], raa[NCL][NZ], rca[NCL][NZ], rac[NCL][NZ], rcc[NCL][NZ];
+#pragma unroll
+  for (int e = 0; e < NZ; ++e) {
 #pragma unroll
     for (int j = 0; j < NCL; ++j) {
-      const int c = min(l + 64 * j, BP - 1);
-      cmac(ya[j], va, full_at<BP>(Gaa, -1.0, sp_idx(pa[e]), c));
-      cmac(yc[j], va, full_at<BP>(Gac, -1.0, sp_idx(pa[e]), c));
-      cmac(ya[j], ve, full_at<BP>(Gca, -1.0, sp_idx(pe[e]), c));
-      cmac(yc[j], ve, full_at<BP>(Gcc, -1.0, sp_idx(pe[e]), c));
-    }
-  }
-  // Z_a[r, :] = G_aa[r, :] U_a + G_ac[r, :] L_e, Z_c[r, :] = G_ca[r, :] U_a + G_cc[r, :] L_e
-#pragma unroll
-  for (int j = 0; j < NCL; ++j)
-#pragma unroll
-    for (int e = 0; e < NZ; ++e) {
-      const double2 vua = sp_val(Ua, qa[j][e]), vle = sp_val(Le, qe[j][e]);
+      gaa[e][j] = full_at<BP>(Gaa, -1.0, sp_idx(pa[e]), cl[j]);
+      gac[e][j] = full_at<BP>(Gac, -1.0, sp_idx(pa[e]), cl[j]);
+      gca[e][j] = full_at<BP>(Gca, -1.0, sp_idx(pe[e]), cl[j]);
+      gcc[e][j] = full_at<BP>(Gcc, -1.0, sp_idx(pe[e]), cl[j]);
+      wa[j][e] = sp_val(Ua, qa[j][e]);
+      we[j][e] = sp_val(Le, qe[j][e]);
       const int ka = sp_idx(qa[j][e]), ke = sp_idx(qe[j][e]);
-      cmac(za[j], Gaa[r * BP + ka], vua);
-      cmac(zc[j], Gca[r * BP + ka], vua);
-      cmac(za[j], Gac[r * BP + ke], vle);
-      cmac(zc[j], Gcc[r * BP + ke], vle);
+      raa[j][e] = Gaa[r * BP + ka];
+      rca[j][e] = Gca[r * BP + ka];
+      rac[j][e] = Gac[r * BP + ke];
+      rcc[j][e] = Gcc[r * BP + ke];
     }
-  double2 *Oza = base + t->oza * BB, *Ozc = base + t->ozc * BB, *Oya = base + t->oya * BB,
-          *Oyc = base + t->oyc * BB, *Omx = base + t->omx * BB;
+  }
+  double2 *Oza = base + t.oza * BB, *Ozc = base + t.ozc * BB, *Oya = base + t.oya * BB,
+          *Oyc = base + t.oyc * BB, *Omx = base + t.omx * BB;
 #pragma unroll
   for (int j = 0; j < NCL; ++j) {
-    const int c = l + 64 * j;
-    if (c >= BP) continue;
-    sc[w][0][c] = ya[j];
-    sc[w][1][c] = yc[j];
-    Oya[r * BP + c] = ya[j];
-    Oyc[r * BP + c] = yc[j];
-    Oza[r * BP + c] = za[j];
-    Ozc[r * BP + c] = zc[j];
+    // Y_a[r, :] = L_a[r, :] G_aa + U_e[r, :] G_ca, Y_c[r, :] = L_a[r, :] G_ac + U_e[r, :] G_cc
+    // Z_a[r, :] = G_aa[r, :] U_a + G_ac[r, :] L_e, Z_c[r, :] = G_ca[r, :] U_a + G_cc[r, :] L_e
+    double2 ya = make_double2(0.0, 0.0), yc = ya, za = ya, zc = ya;
+#pragma unroll
+    for (int e = 0; e < NZ; ++e) {
+      cmac(ya, va[e], gaa[e][j]);
+      cmac(yc, va[e], gac[e][j]);
+      cmac(ya, ve[e], gca[e][j]);
+      cmac(yc, ve[e], gcc[e][j]);
+      cmac(za, raa[j][e], wa[j][e]);
+      cmac(zc, rca[j][e], wa[j][e]);
+      cmac(za, rac[j][e], we[j][e]);
+      cmac(zc, rcc[j][e], we[j][e]);
+    }
+    if (l + 64 * j < BP) {
+      sc[w][0][cl[j]] = ya;
+      sc[w][1][cl[j]] = yc;
+      Oya[r * BP + cl[j]] = ya;
+      Oyc[r * BP + cl[j]] = yc;
+      Oza[r * BP + cl[j]] = za;
+      Ozc[r * BP + cl[j]] = zc;
+    }
   }
   wave_sync();
   // M[r, :] = Y_a[r, :] U_a + Y_c[r, :] L_e
 #pragma unroll
   for (int j = 0; j < NCL; ++j) {
-    const int c = l + 64 * j;
-    if (c >= BP) continue;
     double2 mx = make_double2(0.0, 0.0);
 #pragma unroll
     for (int e = 0; e < NZ; ++e) {
-      cmac(mx, sc[w][0][sp_idx(qa[j][e])], sp_val(Ua, qa[j][e]));
-      cmac(mx, sc[w][1][sp_idx(qe[j][e])], sp_val(Le, qe[j][e]));
+      cmac(mx, sc[w][0][sp_idx(qa[j][e])], wa[j][e]);
+      cmac(mx, sc[w][1][sp_idx(qe[j][e])], we[j][e]);
     }
-    Omx[r * BP + c] = mx;
+    if (l + 64 * j < BP) Omx[r * BP + cl[j]] = mx;
   }
 }
 

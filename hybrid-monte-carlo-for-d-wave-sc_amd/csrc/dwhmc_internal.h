@@ -62,6 +62,12 @@ inline int cr_task_tiles(const CrTask& t, int ts) {
   return ((t.r1 + ts - 1) / ts - t.r0 / ts) * ((t.c1 + ts - 1) / ts - t.c0 / ts);
 }
 bool cr_supported_bp(int BP);
+// diagnostic stamp builds (-DCR_STAMPS, dwh_debug_cr_stamps): workgroups recorded per launch
+constexpr int kCrStampWG = 2048;
+#ifdef CR_STAMPS
+int cr_stamps_arm(int key);   // clears the stamps, records the launch whose first block is `key`
+int cr_stamps_read(unsigned long long* out, int nwg);
+#endif
 // level-0 blocks of `list` (ids t*Ly + y, t = 0 D / 1 U / 2 L) fully
 // rewritten, plus (off_ph != nullptr) the pairing entries Δ[Dsrc]/2 of the
 // level-0 blocks outside the list, in one launch

@@ -200,6 +200,13 @@ int dwh_timing_reset(dwh_ctx* ctx);
  * launch a factorisation makes.  Idempotent: the pool keeps the current Δ.
  * eig path: DWH_ERR_STATE. */
 int dwh_bench_assembly(dwh_ctx* ctx, int64_t reps);
+/* Diagnostic: one CR factorisation at the context's Δ with per-workgroup phase
+ * stamps of its inv_stage-th inversion launch (in the plan's own schedule,
+ * side work included) into out (nwg rows of 32 uint64: [0]/[30]
+ * s_memrealtime at entry/exit, [1..29] s_memtime phase stamps, [31] kind 1
+ * inversion / 2 side work / 3 guard).  Only a library built with -DCR_STAMPS
+ * records them (tools/cr_inv_sched_stamps.py); others return DWH_ERR_STATE. */
+int dwh_debug_cr_stamps(dwh_ctx* ctx, int32_t inv_stage, uint64_t* out, int64_t nwg);
 
 /* ---- measurement path (not the leapfrog step) ----------------------------
  * Eigen-decomposition of one chain's H_BdG(Δ) at the device Δ: what the
