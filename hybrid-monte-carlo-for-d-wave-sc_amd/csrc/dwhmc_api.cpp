@@ -174,6 +174,47 @@ bool cr_sparse_patterns(int Lx, int Ly, int BP, const std::vector<int>& hcol, co
     }
   return true;
 }
+// Column-pattern values of the level-0 U / L blocks in the kernels' own
+// [block][entry][BP] order, so the dense . sparse products read them
+// coalesced instead of gathering one pool row per lane: the static hopping
+// entries as stored (op applied; chain-independent: U / L hold no diagonal),
+// and for the pairing entries the Δ index whose Δ/2 k_cr_fill / the force
+// scatter writes there (src, the kernel applies op), exactly as k_cr_fill
+// resolves both (the last matching table slot).
+void cr_sparse_colvals(const std::vector<int>& colpat, int Lx, int Ly, int BP, const std::vector<int>& hcol,
+                       const std::vector<double>& hval, const std::vector<int>& Dcol, const std::vector<int>& Dsrc,
+                       std::vector<double2>& colval, std::vector<int>& colsrc) {
+  const int HP = BP / 2, NZ = dwh::kCrSpNZ;
+  colval.assign(colpat.size(), make_double2(0.0, 0.0));
+  colsrc.assign(colpat.size(), -1);
+  for (int t = 1; t <= 2; ++t)
+    for (int y = 0; y < Ly; ++y) {
+      const int b = t * Ly + y;
+      const int yr = (t == 2) ? (y + 1) % Ly : y, yc = (t == 1) ? (y + 1) % Ly : y;
+      for (int e = 0; e < NZ; ++e)
+        for (int c = 0; c < BP; ++c) {
+          const size_t k = ((size_t)b * NZ + e) * BP + c;
+          const int w = colpat[k], op = (w >> 22) & 3;
+          if (op == 3) continue;
+          const int off = w & 0x3fff, x = off / BP, ct = off % BP;
+          const int i = yr * Lx + x;
+          if (ct < HP) {
+            const int j = yc * Lx + ct;
+            double h = 0.0;
+            for (int sl = 0; sl < kHSlots; ++sl)
+              if (hcol[(size_t)i * kHSlots + sl] == j) h = hval[(size_t)i * kHSlots + sl];
+            colval[k] = make_double2(op == 2 ? -h : h, 0.0);
+          } else {
+            const int j = yc * Lx + (ct - HP);
+            int src = -1;
+            for (int sl = 0; sl < kSlots; ++sl)
+              if (Dcol[(size_t)i * kSlots + sl] == j) src = Dsrc[(size_t)i * kSlots + sl];
+            colsrc[k] = src;
+          }
+        }
+    }
+}
+
 // nonzeros of row r / column c of level-0 block b in the patterns
 int sp_nrow(const std::vector<int>& pat, int b, int r, int BP) {
   int n = 0;
@@ -795,7 +836,10 @@ struct dwh_ctx {
   dwh::CrTile* d_tiles16 = nullptr;
   dwh::CrSpFwd* d_sp_fwd = nullptr;
   dwh::CrSpBwd* d_sp_bwd = nullptr;
-  int *d_rowpat = nullptr, *d_colpat = nullptr;
+  int *d_rowpat = nullptr, *d_colpat = nullptr, *d_colsrc = nullptr;
+  double2* d_colval = nullptr;
+  std::vector<double2> colval_host;   // cr_sparse_colvals
+  std::vector<int> colsrc_host;
   double* efpart = nullptr;     // per (chain, pole) E_f / Tr G22 partials
   unsigned* efdone = nullptr;   // per chain: pole blocks done (k_cr_fermion_energy)
   int *d_inv_blk = nullptr, *d_inv_dst = nullptr, *d_inv_slot = nullptr, *d_inv0_r = nullptr;
@@ -1062,10 +1106,10 @@ void cr_enqueue(dwh_ctx* ctx) {
       Scope s(ctx, T_CR_SPARSE, st.flops * c.nbatch);
       if (st.sp == 0)
         dwh::launch_cr_sp_fwd(c, ctx->bpool, ctx->d_sp_fwd + st.first, st.n, ctx->d_rowpat, ctx->d_colpat,
-                              ctx->stream);
+                              ctx->d_colval, ctx->d_colsrc, ctx->Delta, ctx->stream);
       else
         dwh::launch_cr_sp_bwd(c, ctx->bpool, ctx->d_sp_bwd + st.first, st.n, ctx->d_rowpat, ctx->d_colpat,
-                              ctx->stream);
+                              ctx->d_colval, ctx->d_colsrc, ctx->Delta, ctx->stream);
     } else {
       Scope s(ctx, T_CR_GEMM, st.flops * c.nbatch);
       dwh::launch_cr_gemm(c, ctx->bpool, ctx->d_tasks + st.first, st.n, st.maxt32, st.maxt16,
@@ -1718,6 +1762,11 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     ALLOC(d_sp_fwd, pl.sp_fwd.size());
     ALLOC(d_sp_bwd, pl.sp_bwd.size());
     ALLOC(d_rowpat, pl.rowpat.size());
+    if (!pl.colpat.empty())
+      cr_sparse_colvals(pl.colpat, ctx->cr.Lx, ctx->cr.Ly, ctx->cr.BP, hcol, hval, Dcol, Dsrc, ctx->colval_host,
+                        ctx->colsrc_host);
+    ALLOC(d_colval, ctx->colval_host.size());
+    ALLOC(d_colsrc, ctx->colsrc_host.size());
     ALLOC(d_colpat, pl.colpat.size());
     ALLOC(efpart, 2 * (size_t)d.nbatch);
     ALLOC(efdone, (size_t)d.nc);
@@ -1816,6 +1865,8 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     UP(d_sp_fwd, pl.sp_fwd.data(), pl.sp_fwd.size());
     UP(d_sp_bwd, pl.sp_bwd.data(), pl.sp_bwd.size());
     UP(d_rowpat, pl.rowpat.data(), pl.rowpat.size());
+    UP(d_colval, ctx->colval_host.data(), ctx->colval_host.size());
+    UP(d_colsrc, ctx->colsrc_host.data(), ctx->colsrc_host.size());
     UP(d_colpat, pl.colpat.data(), pl.colpat.size());
     UP(d_inv_blk, pl.inv_blk.data(), pl.inv_blk.size());
     UP(d_inv_dst, pl.inv_dst.data(), pl.inv_dst.size());

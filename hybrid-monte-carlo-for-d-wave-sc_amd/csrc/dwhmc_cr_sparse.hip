@@ -69,6 +69,19 @@ __device__ __forceinline__ double2 full_at(const double2* __restrict__ X, double
   return top ? u : make_double2(sg * u.x, -sg * u.y);
 }
 
+// value of column-pattern entry k (meta word m): the static hopping value, or
+// op(Δ[src] / 2) of a pairing entry (the value k_cr_fill keeps in the pool)
+__device__ __forceinline__ double2 sp_cval(const double2* __restrict__ cval, const int* __restrict__ csrc,
+                                           const double2* __restrict__ Dc, int k, int m) {
+  const double2 v = cval[k];
+  const int src = csrc[k];
+  const double2 d = Dc[src < 0 ? 0 : src];
+  const int op = (m >> 22) & 3;
+  const double h = src < 0 ? 0.0 : 0.5;
+  const double sr = op == 2 ? -h : h, si = op == 0 ? h : -h;   // op 1: conj, op 2: -conj
+  return make_double2(v.x + sr * d.x, v.y + si * d.y);
+}
+
 // a lane's complex value in every lane
 __device__ __forceinline__ double2 readlane_c(double2 v, int lane) {
   return make_double2(readlane_f64(v.x, lane), readlane_f64(v.y, lane));
@@ -90,10 +103,13 @@ __device__ __forceinline__ void wave_sync() {
 template <int BP>
 __global__ __launch_bounds__(256) void k_cr_sp_fwd(double2* __restrict__ pool, int64_t item,
                                                    const CrSpFwd* __restrict__ tasks, const int* __restrict__ rowpat,
-                                                   const int* __restrict__ colpat, int nrb) {
+                                                   const int* __restrict__ colpat, const double2* __restrict__ cval,
+                                                   const int* __restrict__ csrc, const double2* __restrict__ Delta,
+                                                   int twoN, int P, int nrb) {
   constexpr int HP = BP / 2, NCL = (BP + 63) / 64;
   constexpr int64_t BB = (int64_t)HP * BP;
   __shared__ double2 sc[kSpRowsWG][3][BP];
+  const double2* Dc = Delta + (int64_t)(blockIdx.y / P) * twoN;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int ti = __builtin_amdgcn_readfirstlane(blockIdx.x / nrb);
   const int r = __builtin_amdgcn_readfirstlane((blockIdx.x - ti * nrb) * kSpRowsWG + w);
@@ -144,9 +160,9 @@ __global__ __launch_bounds__(256) void k_cr_sp_fwd(double2* __restrict__ pool, i
       xu[e][j] = full_at<BP>(Dir, -1.0, sp_idx(pu[e]), cl[j]);
       xr[e][j] = full_at<BP>(Dir, -1.0, sp_idx(pr[e]), cl[j]);
       xl[e][j] = full_at<BP>(Dil, -1.0, sp_idx(pl[e]), cl[j]);
-      wl[j][e] = sp_val(Lk, ql[j][e]);
-      wu[j][e] = sp_val(Uel, qu[j][e]);
-      wr[j][e] = sp_val(Uer, qr[j][e]);
+      wl[j][e] = sp_cval(cval, csrc, Dc, (t.lk * NZ + e) * BP + cl[j], ql[j][e]);
+      wu[j][e] = sp_cval(cval, csrc, Dc, (t.uel * NZ + e) * BP + cl[j], qu[j][e]);
+      wr[j][e] = sp_cval(cval, csrc, Dc, (t.uer * NZ + e) * BP + cl[j], qr[j][e]);
     }
   }
 #pragma unroll
@@ -193,10 +209,13 @@ __global__ __launch_bounds__(256) void k_cr_sp_fwd(double2* __restrict__ pool, i
 template <int BP>
 __global__ __launch_bounds__(256) void k_cr_sp_bwd(double2* __restrict__ pool, int64_t item,
                                                    const CrSpBwd* __restrict__ tasks, const int* __restrict__ rowpat,
-                                                   const int* __restrict__ colpat, int nrb) {
+                                                   const int* __restrict__ colpat, const double2* __restrict__ cval,
+                                                   const int* __restrict__ csrc, const double2* __restrict__ Delta,
+                                                   int twoN, int P, int nrb) {
   constexpr int HP = BP / 2, NCL = (BP + 63) / 64;
   constexpr int64_t BB = (int64_t)HP * BP;
   __shared__ double2 sc[kSpRowsWG][2][BP];
+  const double2* Dc = Delta + (int64_t)(blockIdx.y / P) * twoN;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int ti = __builtin_amdgcn_readfirstlane(blockIdx.x / nrb);
   const int r = __builtin_amdgcn_readfirstlane((blockIdx.x - ti * nrb) * kSpRowsWG + w);
@@ -240,8 +259,8 @@ __global__ __launch_bounds__(256) void k_cr_sp_bwd(double2* __restrict__ pool, i
       gac[e][j] = full_at<BP>(Gac, -1.0, sp_idx(pa[e]), cl[j]);
       gca[e][j] = full_at<BP>(Gca, -1.0, sp_idx(pe[e]), cl[j]);
       gcc[e][j] = full_at<BP>(Gcc, -1.0, sp_idx(pe[e]), cl[j]);
-      wa[j][e] = sp_val(Ua, qa[j][e]);
-      we[j][e] = sp_val(Le, qe[j][e]);
+      wa[j][e] = sp_cval(cval, csrc, Dc, (t.ua * NZ + e) * BP + cl[j], qa[j][e]);
+      we[j][e] = sp_cval(cval, csrc, Dc, (t.le * NZ + e) * BP + cl[j], qe[j][e]);
       const int ka = sp_idx(qa[j][e]), ke = sp_idx(qe[j][e]);
       raa[j][e] = Gaa[r * BP + ka];
       rca[j][e] = Gca[r * BP + ka];
@@ -295,26 +314,28 @@ __global__ __launch_bounds__(256) void k_cr_sp_bwd(double2* __restrict__ pool, i
 bool cr_supported_sparse0(int BP) { return BP == 32 || BP == 64 || BP == 96; }
 
 void launch_cr_sp_fwd(const CrDims& c, double2* pool, const CrSpFwd* tasks, int n, const int* rowpat,
-                      const int* colpat, hipStream_t s) {
+                      const int* colpat, const double2* colval, const int* colsrc, const double2* Delta,
+                      hipStream_t s) {
   if (n <= 0) return;
   const int nrb = c.BP / 2 / kSpRowsWG;
   const dim3 g(n * nrb, c.nbatch), b(64 * kSpRowsWG);
   switch (c.BP) {
-    case 32: hipLaunchKernelGGL(k_cr_sp_fwd<32>, g, b, 0, s, pool, c.item, tasks, rowpat, colpat, nrb); break;
-    case 64: hipLaunchKernelGGL(k_cr_sp_fwd<64>, g, b, 0, s, pool, c.item, tasks, rowpat, colpat, nrb); break;
-    default: hipLaunchKernelGGL(k_cr_sp_fwd<96>, g, b, 0, s, pool, c.item, tasks, rowpat, colpat, nrb); break;
+    case 32: hipLaunchKernelGGL(k_cr_sp_fwd<32>, g, b, 0, s, pool, c.item, tasks, rowpat, colpat, colval, colsrc, Delta, 2 * c.N, c.P, nrb); break;
+    case 64: hipLaunchKernelGGL(k_cr_sp_fwd<64>, g, b, 0, s, pool, c.item, tasks, rowpat, colpat, colval, colsrc, Delta, 2 * c.N, c.P, nrb); break;
+    default: hipLaunchKernelGGL(k_cr_sp_fwd<96>, g, b, 0, s, pool, c.item, tasks, rowpat, colpat, colval, colsrc, Delta, 2 * c.N, c.P, nrb); break;
   }
 }
 
 void launch_cr_sp_bwd(const CrDims& c, double2* pool, const CrSpBwd* tasks, int n, const int* rowpat,
-                      const int* colpat, hipStream_t s) {
+                      const int* colpat, const double2* colval, const int* colsrc, const double2* Delta,
+                      hipStream_t s) {
   if (n <= 0) return;
   const int nrb = c.BP / 2 / kSpRowsWG;
   const dim3 g(n * nrb, c.nbatch), b(64 * kSpRowsWG);
   switch (c.BP) {
-    case 32: hipLaunchKernelGGL(k_cr_sp_bwd<32>, g, b, 0, s, pool, c.item, tasks, rowpat, colpat, nrb); break;
-    case 64: hipLaunchKernelGGL(k_cr_sp_bwd<64>, g, b, 0, s, pool, c.item, tasks, rowpat, colpat, nrb); break;
-    default: hipLaunchKernelGGL(k_cr_sp_bwd<96>, g, b, 0, s, pool, c.item, tasks, rowpat, colpat, nrb); break;
+    case 32: hipLaunchKernelGGL(k_cr_sp_bwd<32>, g, b, 0, s, pool, c.item, tasks, rowpat, colpat, colval, colsrc, Delta, 2 * c.N, c.P, nrb); break;
+    case 64: hipLaunchKernelGGL(k_cr_sp_bwd<64>, g, b, 0, s, pool, c.item, tasks, rowpat, colpat, colval, colsrc, Delta, 2 * c.N, c.P, nrb); break;
+    default: hipLaunchKernelGGL(k_cr_sp_bwd<96>, g, b, 0, s, pool, c.item, tasks, rowpat, colpat, colval, colsrc, Delta, 2 * c.N, c.P, nrb); break;
   }
 }
 

@@ -133,10 +133,15 @@ struct CrSpFwd {
 struct CrSpBwd {
   int gaa, gac, gca, gcc, ua, le, la, ue, oza, ozc, oya, oyc, omx, pad0, pad1, pad2;
 };
+// colval / colsrc: the column-pattern values in colpat's order (static
+// hopping value with op applied; or the Δ index of a pairing entry, -1 none),
+// Delta: the chains' N x 2 Δ (batch item bi reads chain bi / P)
 void launch_cr_sp_fwd(const CrDims& c, double2* pool, const CrSpFwd* tasks, int n, const int* rowpat,
-                      const int* colpat, hipStream_t s);
+                      const int* colpat, const double2* colval, const int* colsrc, const double2* Delta,
+                      hipStream_t s);
 void launch_cr_sp_bwd(const CrDims& c, double2* pool, const CrSpBwd* tasks, int n, const int* rowpat,
-                      const int* colpat, hipStream_t s);
+                      const int* colpat, const double2* colval, const int* colsrc, const double2* Delta,
+                      hipStream_t s);
 // block-product stage configuration: output tile TS x TS (16 or 32) and the
 // number of waves splitting each tile's K range (1, 2, 4)
 struct CrGemmCfg {
