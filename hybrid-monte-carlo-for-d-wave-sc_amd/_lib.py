@@ -42,7 +42,8 @@ class dwh_info_t(C.Structure):
     _fields_ = [("N", C.c_int64), ("Np", C.c_int64), ("nchains", C.c_int64), ("npoles", C.c_int64),
                 ("kappa", C.c_double), ("e_bound", C.c_double), ("err_tanh", C.c_double),
                 ("delta_cap", C.c_double), ("device_bytes", C.c_int64), ("algo", C.c_int64),
-                ("block", C.c_int64), ("eig_half", C.c_int64)]
+                ("block", C.c_int64), ("eig_half", C.c_int64),
+                ("eig_long_clusters", C.c_int64)]
 
 
 _P = C.c_void_p

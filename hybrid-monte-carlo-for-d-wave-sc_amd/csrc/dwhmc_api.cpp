@@ -887,6 +887,7 @@ struct dwh_ctx {
   // map column by column (half solve, c0 = N everywhere, no fallback):
   // transport's pair sums then run over half the pairs
   bool eig_ph = false;
+  int64_t eig_long_clusters = 0;   // clusters longer than k_eig_orth's limit, orthonormalised by long_clusters
   int eig_ph_last = -1;    // dwh_info_t::eig_half: eig_ph of the last eigensolve (-1: none yet)
   double *d_eig_d = nullptr, *d_eig_e = nullptr, *d_eig_tn = nullptr;
 
@@ -2073,6 +2074,81 @@ struct EigPhase {
   }
 };
 
+// Clusters longer than maxc (runs of eigenvalues with gaps <= kEigClusterTol
+// ||T||, e.g. the degenerate shells of clean lattices, which k_eig_orth's one
+// workgroup does not take): Cholesky QR, twice, on the library's own real
+// products — G = Y Y^T of the cluster's rows Y of Zt (the vectors), G = R^T R
+// on the host, Y <- R^-T Y — before the Löwdin step.  Replaces round 4's
+// rocSOLVER zheev fallback (minutes at n = 4608).  Ud: scratch (the slots' U
+// buffers, free between inverse iteration and the Löwdin step).  A
+// non-positive pivot sets d_tr_bad (eigen_solve's vendor fallback, as for a
+// non-finite result).  Synchronises the stream when a long cluster exists.
+int long_clusters(dwh_ctx* ctx, const std::vector<double>& Eh, const std::vector<double>& tn, double* Zt, double* Ud,
+                  int n, int64_t sZ, int m, int maxc, bool half) {
+  hipStream_t s = ctx->stream;
+  std::vector<double> G, W;
+  for (int k = 0; k < m; ++k) {
+    const double* E = Eh.data() + (size_t)k * n;
+    const double tol = dwh::kEigClusterTol * tn[k];
+    const int jstart = half ? ctx->eig_c0h[k] : 0;
+    for (int j = jstart; j < n;) {
+      int end = j + 1;
+      while (end < n && E[end] - E[end - 1] <= tol) ++end;
+      const int L = end - j;
+      if (L > maxc) {
+        double* Y = Zt + (int64_t)k * sZ + j;   // L x n, leading dimension n (column-major Zt)
+        double* Gd = Ud + (int64_t)k * sZ;      // L x L
+        double* Tmp = Gd + (int64_t)L * L;      // L x n
+        G.resize((size_t)L * L);
+        W.assign((size_t)L * L, 0.0);
+        for (int round = 0; round < 2; ++round) {
+          dwh::gemm_d('N', 'T', L, L, n, 1.0, Y, n, 0, Y, n, 0, 0.0, Gd, L, 0, 1, s);
+          HIPCHECK(ctx, hipGetLastError());
+          HIPCHECK(ctx, hipMemcpyAsync(G.data(), Gd, G.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+          HIPCHECK(ctx, hipStreamSynchronize(s));
+          // G = R^T R (R upper, stored in G's upper triangle, column-major)
+          bool ok = true;
+          for (int c = 0; c < L && ok; ++c) {
+            for (int r = 0; r <= c; ++r) {
+              double x = G[(size_t)c * L + r];
+              for (int q = 0; q < r; ++q) x -= G[(size_t)r * L + q] * G[(size_t)c * L + q];
+              if (r < c) {
+                G[(size_t)c * L + r] = x / G[(size_t)r * L + r];
+              } else {
+                if (!(x > 0.0)) ok = false;
+                G[(size_t)c * L + c] = ok ? std::sqrt(x) : 0.0;
+              }
+            }
+          }
+          if (!ok) {
+            const int one = 1;
+            HIPCHECK(ctx, hipMemcpyAsync(ctx->d_tr_bad, &one, sizeof(int), hipMemcpyHostToDevice, s));
+            HIPCHECK(ctx, hipStreamSynchronize(s));
+            return DWH_OK;
+          }
+          // W = R^-T (lower triangular): R^T W = I, forward substitution per column
+          // (R^T[i][q] = R[q][i] = G[i * L + q] for q <= i)
+          std::fill(W.begin(), W.end(), 0.0);
+          for (int c = 0; c < L; ++c)
+            for (int i = c; i < L; ++i) {
+              double x = i == c ? 1.0 : 0.0;
+              for (int q = c; q < i; ++q) x -= G[(size_t)i * L + q] * W[(size_t)c * L + q];
+              W[(size_t)c * L + i] = x / G[(size_t)i * L + i];
+            }
+          HIPCHECK(ctx, hipMemcpyAsync(Gd, W.data(), W.size() * sizeof(double), hipMemcpyHostToDevice, s));
+          dwh::gemm_d('N', 'N', L, n, L, 1.0, Gd, L, 0, Y, n, 0, 0.0, Tmp, L, 0, 1, s);
+          HIPCHECK(ctx, hipMemcpy2DAsync(Y, (size_t)n * sizeof(double), Tmp, (size_t)L * sizeof(double),
+                                         (size_t)L * sizeof(double), n, hipMemcpyDeviceToDevice, s));
+          HIPCHECK(ctx, hipGetLastError());
+        }
+        ctx->eig_long_clusters++;
+      }
+      j = end;
+    }
+  }
+  return DWH_OK;
+}
+
 int own_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m) {
   const int N = ctx->d.N, n = 2 * N;
   const dwh::TrBufs& b = ctx->tr;
@@ -2121,8 +2197,8 @@ int own_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m) {
   ph.mark("bisect");
   double* Zt = reinterpret_cast<double*>(b.Jmn);
   double* Ud = reinterpret_cast<double*>(b.U);
-  // DWHMC_EIG_MAX_CLUSTER (tests): a shorter cluster limit, to exercise the
-  // rocSOLVER fallback of eigen_solve
+  // DWHMC_EIG_MAX_CLUSTER (tests): a shorter limit for the single-workgroup
+  // cluster orthonormalisation, to exercise the long-cluster path below
   int maxc = dwh::kEigMaxCluster;
   if (const char* e = std::getenv("DWHMC_EIG_MAX_CLUSTER")) maxc = std::max(1, std::min(maxc, std::atoi(e)));
   // Particle-hole half solve (H_BdG: E <-> -E with eigenvectors (u; v) <->
@@ -2142,11 +2218,13 @@ int own_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m) {
   ctx->eig_half = half;
   ctx->eig_c0h.assign(half ? m : 0, N);
   int j0 = 0;
+  // the eigenvalues on the host (one synchronisation): the half solve's c0
+  // and the clusters longer than maxc
+  std::vector<double> Eh((size_t)m * n), tn(m);
+  HIPCHECK(ctx, hipMemcpyAsync(Eh.data(), b.E, Eh.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+  HIPCHECK(ctx, hipMemcpyAsync(tn.data(), ctx->d_eig_tn, m * sizeof(double), hipMemcpyDeviceToHost, s));
+  HIPCHECK(ctx, hipStreamSynchronize(s));
   if (half) {
-    std::vector<double> Eh((size_t)m * n), tn(m);
-    HIPCHECK(ctx, hipMemcpyAsync(Eh.data(), b.E, Eh.size() * sizeof(double), hipMemcpyDeviceToHost, s));
-    HIPCHECK(ctx, hipMemcpyAsync(tn.data(), ctx->d_eig_tn, m * sizeof(double), hipMemcpyDeviceToHost, s));
-    HIPCHECK(ctx, hipStreamSynchronize(s));
     j0 = N;
     for (int k = 0; k < m; ++k) {
       const double* E = Eh.data() + (size_t)k * n;
@@ -2169,6 +2247,8 @@ int own_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m) {
   dwh::launch_eig_invit(ctx->d_eig_d, ctx->d_eig_e, n, b.E, ctx->d_eig_tn, Zt, Zt + sA, Ud, Ud + sA, sZ,
                         ctx->d_tr_bad, m, s, maxc, j0, half ? ctx->d_eig_c0 : nullptr);
   ph.mark("invit+orth");
+  if ((rc = long_clusters(ctx, Eh, tn, Zt, Ud, n, sZ, m, maxc, half))) return rc;
+  ph.mark("long clusters");
   // One symmetric (Löwdin) orthogonalisation step over the computed vectors:
   // with Y = Z^T (column-major Zt, its rows j0.. the vectors) and G = Y Y^T =
   // I + F, Y <- (3/2 I - 1/2 G) Y leaves ||F|| -> O(||F||^2).  Outside clusters
@@ -2511,6 +2591,7 @@ int dwh_info(dwh_ctx* ctx, dwh_info_t* out) {
   out->algo = ctx->algo;
   out->block = ctx->algo == ALGO_CR ? ctx->cr.BP : ctx->algo == ALGO_EIG ? 0 : kGJ;
   out->eig_half = ctx->eig_ph_last;
+  out->eig_long_clusters = ctx->eig_long_clusters;
   return DWH_OK;
 }
 

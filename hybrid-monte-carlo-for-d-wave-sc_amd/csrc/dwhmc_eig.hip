@@ -27,9 +27,10 @@
 //  3. k_eig_invit: inverse iteration, T - lambda I = LU with partial pivoting
 //     streamed per thread (two solves from a fixed pseudo-random start,
 //     one thread per eigenvalue); k_eig_orth: the vectors of eigenvalue
-//     clusters (consecutive gaps <= kEigClusterTol = 1e-6 ||T||)
-//     orthonormalised by Cholesky QR, twice (exact degeneracies of clean
-//     lattices included).  Every other pair is orthogonal only to
+//     clusters (consecutive gaps <= kEigClusterTol = 1e-6 ||T||, up to
+//     kEigMaxCluster long; longer ones by the same Cholesky QR on the
+//     library's products, driven from the host) orthonormalised by Cholesky
+//     QR, twice (exact degeneracies of clean lattices included).  Every other pair is orthogonal only to
 //     ~eps ||T|| / gap <= ~2e-10 after inverse iteration; one symmetric
 //     (Löwdin) orthogonalisation step over all vectors (the library's real
 //     products, dwhmc_gemm.hip, driven by dwhmc_api.cpp) takes those overlaps
@@ -970,11 +971,9 @@ __global__ __launch_bounds__(256) void k_eig_orth(const double* __restrict__ E, 
   int end = j + 1;
   while (end < n && end - j <= MC && E[end] - E[end - 1] <= tol) ++end;
   const int kc = end - j;
-  if (kc == 1) return;
-  if (kc > maxc) {
-    if (tid == 0) *bad = 1;
-    return;
-  }
+  // a cluster longer than maxc is orthonormalised by the host-driven Cholesky
+  // QR over several workgroups (own_heev_enqueue, dwhmc_api.cpp)
+  if (kc == 1 || kc > maxc) return;
   constexpr int RC = 64;   // rows per LDS chunk (Gram sums, substitution)
   __shared__ double G[MC][MC + 1];
   __shared__ double Zs[RC][MC + 1];

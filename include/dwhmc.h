@@ -57,6 +57,8 @@ typedef struct {
   int64_t block;      /* dense: GJ block (64); cr: padded lattice-row block BP >= 2 Lx; eig: 0 */
   int64_t eig_half;   /* last eigensolve (transport / eig path): 1 = particle-hole half solve,
                          J_mn and the pair sums over the columns < N; 0 = every column; -1 = none yet */
+  int64_t eig_long_clusters; /* eigenvalue clusters so far too long for the one-workgroup
+                                orthonormalisation, taken by the multi-workgroup Cholesky QR */
 } dwh_info_t;
 
 /* ModelParameters + initialize_cache + init_static_H!

@@ -214,15 +214,17 @@ def test_own_eigensolver_L48(dwhmc, oracle):
 
 
 @pytest.mark.gpu
-def test_eigensolver_vendor_fallback(dwhmc, oracle, monkeypatch):
-    """The rocSOLVER fallback of eigen_solve (k_eig_orth flags a cluster
-    longer than its limit): DWHMC_EIG_MAX_CLUSTER=1 makes every degenerate
-    pair of a clean lattice a flagged cluster, so the own solve is followed by
-    rocSOLVER's zheev (eig_vendor counts it), whose eigenpairs meet the same
-    tolerances (the bad-flag hand-off was never exercised)."""
+@pytest.mark.parametrize("Lx,Ly,maxc", [(12, 10, "1"), (24, 24, "4")])
+def test_eigensolver_long_clusters(dwhmc, oracle, monkeypatch, Lx, Ly, maxc):
+    """Clusters longer than k_eig_orth's one-workgroup limit are
+    orthonormalised in the library (Cholesky QR twice on its own products,
+    R from the host) instead of the round-4 rocSOLVER zheev fallback:
+    DWHMC_EIG_MAX_CLUSTER lowers the limit so the degenerate shells of a clean
+    lattice take that path (eig_long_clusters > 0, eig_vendor == 0), and the
+    eigenpairs meet test_own_eigensolver_full_size's tolerances."""
     O = oracle
-    monkeypatch.setenv("DWHMC_EIG_MAX_CLUSTER", "1")
-    p = O.ModelParameters(12, 10, T, TP, -1.0, 0.0, 0.0, 4.0, 0.8, 1.0)
+    monkeypatch.setenv("DWHMC_EIG_MAX_CLUSTER", maxc)
+    p = O.ModelParameters(Lx, Ly, T, TP, -1.0, 0.0, 0.0, 4.0, 0.8, 1.0)
     dis = np.zeros(p.N)
     D = np.stack([np.full(p.N, 0.2), np.full(p.N, -0.2)], 1).astype(np.complex128)
     cache, _, _ = O.evaluate(p, dis, D)
@@ -231,11 +233,43 @@ def test_eigensolver_vendor_fallback(dwhmc, oracle, monkeypatch):
     ctx.timing_enable(["eig_own", "eig_vendor"])
     E, U = ctx.eigensystem(0)
     own, vendor = ctx.timing_read("eig_own")[1], ctx.timing_read("eig_vendor")[1]
+    nlong = ctx.info["eig_long_clusters"]
     ctx.close()
-    assert (own, vendor) == (1, 1)
+    assert (own, vendor) == (1, 0) and nlong > 0, (own, vendor, nlong)
     H = O.hermitian_from_upper(cache.H_base)
     scale = 1 + np.max(np.abs(cache.E_n))
     assert np.max(np.abs(E - cache.E_n)) <= 1e-12 * scale
+    assert np.max(np.abs(H @ U - U * E[None, :])) <= 1e-11 * scale
+    assert np.max(np.abs(U.conj().T @ U - np.eye(2 * p.N))) <= 1e-12
+
+
+@pytest.mark.gpu
+def test_own_eigensolver_L48_low_cluster_limit(dwhmc, oracle, monkeypatch):
+    """C5's lattice with the one-workgroup cluster limit at 2: every cluster of
+    3+ levels takes the multi-workgroup path; no rocSOLVER solve (which took
+    more than 400 s here in round 4), within 60 s, at the tolerances of
+    test_own_eigensolver_L48."""
+    import time
+    import scipy.linalg as sla
+    O = oracle
+    monkeypatch.setenv("DWHMC_EIG_MAX_CLUSTER", "2")
+    p, dis, D = _case(O, 48, 48, 32.0, seed=4848)
+    cache = O.initialize_cache(p)
+    O.init_static_H(cache, p, dis)
+    O.update_H_BdG(cache, p, D)
+    Eref = sla.eigh(cache.H_base, lower=False, eigvals_only=True, driver="evr", check_finite=False)
+    ctx = _ctx(dwhmc, p, dis)
+    ctx.set_pairing(D)
+    ctx.timing_enable(["eig_own", "eig_vendor"])
+    t0 = time.perf_counter()
+    E, U = ctx.eigensystem(0)
+    el = time.perf_counter() - t0
+    own, vendor = ctx.timing_read("eig_own")[1], ctx.timing_read("eig_vendor")[1]
+    ctx.close()
+    assert (own, vendor) == (1, 0) and el < 60.0, (own, vendor, el)
+    scale = 1 + np.max(np.abs(Eref))
+    assert np.max(np.abs(E - Eref)) <= 1e-12 * scale
+    H = O.hermitian_from_upper(cache.H_base)
     assert np.max(np.abs(H @ U - U * E[None, :])) <= 1e-11 * scale
     assert np.max(np.abs(U.conj().T @ U - np.eye(2 * p.N))) <= 1e-12
 
