@@ -1469,7 +1469,7 @@ void launch_cr_fermion_energy(const CrDims& c, const double2* pool, const int64_
 namespace dwh {
 int cr_stamps_arm(int key) {
   static unsigned long long zero[kCrStampWG][32];
-  if (hipMemcpyToSymbol(HIP_SYMBOL(g_cr_stamps), zero, sizeof(zero)) != hipSuccess) return -2;
+  if (key >= 0 && hipMemcpyToSymbol(HIP_SYMBOL(g_cr_stamps), zero, sizeof(zero)) != hipSuccess) return -2;
   return hipMemcpyToSymbol(HIP_SYMBOL(g_cr_stamp_key), &key, sizeof(int)) == hipSuccess ? 0 : -2;
 }
 int cr_stamps_read(unsigned long long* out, int nwg) {

@@ -96,10 +96,30 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// forward: one wave per output row r of the kept row k's D', U', L'.  Every
-// operand of the row is loaded into registers first (pattern words, then all
-// values and dense elements at once: one memory round trip each), then the
-// arithmetic; the V rows meet in LDS.
+// Column data of the sparse right operands (dense . sparse products): every
+// output row of a workgroup uses the same column patterns, so the workgroup
+// stages them once in LDS — the value (static hopping or op(Δ/2)) and the
+// row index of each entry — instead of every row re-reading them.
+template <int BP, int NB>
+__device__ __forceinline__ void stage_columns(double2 (*cv)[kCrSpNZ][BP], unsigned char (*ci)[kCrSpNZ][BP],
+                                              const int (&blk)[NB], const int* __restrict__ colpat,
+                                              const double2* __restrict__ cval, const int* __restrict__ csrc,
+                                              const double2* __restrict__ Dc) {
+  for (int q = threadIdx.x; q < NB * NZ * BP; q += blockDim.x) {
+    const int b = q / (NZ * BP), e = (q / BP) % NZ, c = q % BP;
+    int bk = blk[0];
+#pragma unroll
+    for (int x = 1; x < NB; ++x)
+      if (b == x) bk = blk[x];
+    const int k = (bk * NZ + e) * BP + c, m = colpat[k];
+    cv[b][e][c] = sp_cval(cval, csrc, Dc, k, m);
+    ci[b][e][c] = (unsigned char)sp_idx(m);
+  }
+}
+
+// forward: one wave per output row r of the kept row k's D', U', L'; the
+// row's operands are loaded into registers up front (pattern words through
+// lanes, then every value and dense element at once), the V rows meet in LDS.
 template <int BP>
 __global__ __launch_bounds__(256) void k_cr_sp_fwd(double2* __restrict__ pool, int64_t item,
                                                    const CrSpFwd* __restrict__ tasks, const int* __restrict__ rowpat,
@@ -108,6 +128,8 @@ __global__ __launch_bounds__(256) void k_cr_sp_fwd(double2* __restrict__ pool, i
                                                    int twoN, int P, int nrb) {
   constexpr int HP = BP / 2, NCL = (BP + 63) / 64;
   constexpr int64_t BB = (int64_t)HP * BP;
+  __shared__ double2 cv[3][NZ][BP];
+  __shared__ unsigned char ci[3][NZ][BP];
   __shared__ double2 sc[kSpRowsWG][3][BP];
   const double2* Dc = Delta + (int64_t)(blockIdx.y / P) * twoN;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
@@ -115,67 +137,45 @@ __global__ __launch_bounds__(256) void k_cr_sp_fwd(double2* __restrict__ pool, i
   const int r = __builtin_amdgcn_readfirstlane((blockIdx.x - ti * nrb) * kSpRowsWG + w);
   const CrSpFwd t = tasks[ti];
   double2* base = pool + (int64_t)blockIdx.y * item;
-  const double2 *Dir = base + t.dir * BB, *Dil = base + t.dil * BB;
-  const double2 *Uk = base + t.uk * BB, *Ler = base + t.ler * BB, *Lel = base + t.lel * BB;
-  const double2 *Lk = base + t.lk * BB, *Uel = base + t.uel * BB, *Uer = base + t.uer * BB;
-  const double2* Dk = base + t.dk * BB;
+  const double2 *Dir = base + t.dir * BB, *Dil = base + t.dil * BB, *Dk = base + t.dk * BB;
   int cl[NCL];
 #pragma unroll
   for (int j = 0; j < NCL; ++j) cl[j] = min(l + 64 * j, BP - 1);
-  // 1. pattern words: row r of U_k, L_er, L_el (lanes 0 .. 3 NZ - 1 load one
-  // word and its value each: vector loads, no scalar-load chain), this lane's
-  // columns of L_k, U_el, U_er
+  // row r of U_k, L_er, L_el: lanes 0 .. 3 NZ - 1 load one pattern word and its value each
   const int lb = l / NZ < 3 ? l / NZ : 0, le = l % NZ;
   const int myb = lb == 0 ? t.uk : (lb == 1 ? t.ler : t.lel);
   const int myp = rowpat[(myb * NZ + le) * BP + r];
-  int ql[NCL][NZ], qu[NCL][NZ], qr[NCL][NZ];
-#pragma unroll
-  for (int e = 0; e < NZ; ++e) {
-#pragma unroll
-    for (int j = 0; j < NCL; ++j) {
-      ql[j][e] = colpat[(t.lk * NZ + e) * BP + cl[j]];
-      qu[j][e] = colpat[(t.uel * NZ + e) * BP + cl[j]];
-      qr[j][e] = colpat[(t.uer * NZ + e) * BP + cl[j]];
-    }
-  }
   const double2 myv = sp_val(base + myb * BB, myp);
+  double2 dk[NCL];
+#pragma unroll
+  for (int j = 0; j < NCL; ++j) dk[j] = Dk[r * BP + cl[j]];
   int pu[NZ], pr[NZ], pl[NZ];
-  double2 vu[NZ], vr[NZ], vl[NZ];
 #pragma unroll
   for (int e = 0; e < NZ; ++e) {
     pu[e] = __builtin_amdgcn_readlane(myp, e);
     pr[e] = __builtin_amdgcn_readlane(myp, NZ + e);
     pl[e] = __builtin_amdgcn_readlane(myp, 2 * NZ + e);
-    vu[e] = readlane_c(myv, e);
-    vr[e] = readlane_c(myv, NZ + e);
-    vl[e] = readlane_c(myv, 2 * NZ + e);
   }
-  // 2. every dense element and column value the row needs
   double2 xu[NZ][NCL], xr[NZ][NCL], xl[NZ][NCL];
-  double2 wl[NCL][NZ], wu[NCL][NZ], wr[NCL][NZ], dk[NCL];
 #pragma unroll
-  for (int e = 0; e < NZ; ++e) {
+  for (int e = 0; e < NZ; ++e)
 #pragma unroll
     for (int j = 0; j < NCL; ++j) {
       xu[e][j] = full_at<BP>(Dir, -1.0, sp_idx(pu[e]), cl[j]);
       xr[e][j] = full_at<BP>(Dir, -1.0, sp_idx(pr[e]), cl[j]);
       xl[e][j] = full_at<BP>(Dil, -1.0, sp_idx(pl[e]), cl[j]);
-      wl[j][e] = sp_cval(cval, csrc, Dc, (t.lk * NZ + e) * BP + cl[j], ql[j][e]);
-      wu[j][e] = sp_cval(cval, csrc, Dc, (t.uel * NZ + e) * BP + cl[j], qu[j][e]);
-      wr[j][e] = sp_cval(cval, csrc, Dc, (t.uer * NZ + e) * BP + cl[j], qr[j][e]);
     }
-  }
-#pragma unroll
-  for (int j = 0; j < NCL; ++j) dk[j] = Dk[r * BP + cl[j]];
-  // 3. V rows: V1r = -U_k Dinv_er, V2r = -L_er Dinv_er, V2l = -L_el Dinv_el
+  const int cb[3] = {t.lk, t.uel, t.uer};
+  stage_columns<BP, 3>(cv, ci, cb, colpat, cval, csrc, Dc);
+  // V1r = -U_k Dinv_er, V2r = -L_er Dinv_er, V2l = -L_el Dinv_el
 #pragma unroll
   for (int j = 0; j < NCL; ++j) {
     double2 v1 = make_double2(0.0, 0.0), v2r = v1, v2l = v1;
 #pragma unroll
     for (int e = 0; e < NZ; ++e) {
-      cmac(v1, vu[e], xu[e][j]);
-      cmac(v2r, vr[e], xr[e][j]);
-      cmac(v2l, vl[e], xl[e][j]);
+      cmac(v1, readlane_c(myv, e), xu[e][j]);
+      cmac(v2r, readlane_c(myv, NZ + e), xr[e][j]);
+      cmac(v2l, readlane_c(myv, 2 * NZ + e), xl[e][j]);
     }
     if (l + 64 * j < BP) {
       sc[w][0][cl[j]] = make_double2(-v1.x, -v1.y);
@@ -183,29 +183,33 @@ __global__ __launch_bounds__(256) void k_cr_sp_fwd(double2* __restrict__ pool, i
       sc[w][2][cl[j]] = make_double2(-v2l.x, -v2l.y);
     }
   }
-  wave_sync();
-  // 4. D'_k = D_k + V1r L_k + V2l U_el, U'_k = V1r U_er, L'_k = V2r L_k
+  __syncthreads();
+  // D'_k = D_k + V1r L_k + V2l U_el, U'_k = V1r U_er, L'_k = V2r L_k
   double2 *On = base + t.od * BB, *Ou = base + t.ou * BB, *Ol = base + t.ol * BB;
 #pragma unroll
   for (int j = 0; j < NCL; ++j) {
+    const int c = cl[j];
     double2 d = dk[j], u = make_double2(0.0, 0.0), lo = make_double2(0.0, 0.0);
 #pragma unroll
     for (int e = 0; e < NZ; ++e) {
-      cmac(d, sc[w][0][sp_idx(ql[j][e])], wl[j][e]);
-      cmac(lo, sc[w][1][sp_idx(ql[j][e])], wl[j][e]);
-      cmac(d, sc[w][2][sp_idx(qu[j][e])], wu[j][e]);
-      cmac(u, sc[w][0][sp_idx(qr[j][e])], wr[j][e]);
+      const double2 vl = cv[0][e][c], vu = cv[1][e][c], vr = cv[2][e][c];
+      const int kl = ci[0][e][c], ku = ci[1][e][c], kr = ci[2][e][c];
+      cmac(d, sc[w][0][kl], vl);
+      cmac(lo, sc[w][1][kl], vl);
+      cmac(d, sc[w][2][ku], vu);
+      cmac(u, sc[w][0][kr], vr);
     }
     if (l + 64 * j < BP) {
-      On[r * BP + cl[j]] = d;
-      Ou[r * BP + cl[j]] = u;
-      Ol[r * BP + cl[j]] = lo;
+      On[r * BP + c] = d;
+      Ou[r * BP + c] = u;
+      Ol[r * BP + c] = lo;
     }
   }
 }
 
 // backward: one wave per output row r of the eliminated row e's Z_a, Z_c,
-// Y_a, Y_c and M = Y_a U_a + Y_c L_e; loads first, as in the forward kernel
+// Y_a, Y_c and M = Y_a U_a + Y_c L_e.  Row r of each G block is staged in the
+// wave's LDS (Z gathers from it), full rows of the G blocks feed Y.
 template <int BP>
 __global__ __launch_bounds__(256) void k_cr_sp_bwd(double2* __restrict__ pool, int64_t item,
                                                    const CrSpBwd* __restrict__ tasks, const int* __restrict__ rowpat,
@@ -214,6 +218,9 @@ __global__ __launch_bounds__(256) void k_cr_sp_bwd(double2* __restrict__ pool, i
                                                    int twoN, int P, int nrb) {
   constexpr int HP = BP / 2, NCL = (BP + 63) / 64;
   constexpr int64_t BB = (int64_t)HP * BP;
+  __shared__ double2 cv[2][NZ][BP];
+  __shared__ unsigned char ci[2][NZ][BP];
+  __shared__ double2 gr[kSpRowsWG][4][BP];
   __shared__ double2 sc[kSpRowsWG][2][BP];
   const double2* Dc = Delta + (int64_t)(blockIdx.y / P) * twoN;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
@@ -223,89 +230,84 @@ __global__ __launch_bounds__(256) void k_cr_sp_bwd(double2* __restrict__ pool, i
   double2* base = pool + (int64_t)blockIdx.y * item;
   const double2 *Gaa = base + t.gaa * BB, *Gac = base + t.gac * BB, *Gca = base + t.gca * BB,
                 *Gcc = base + t.gcc * BB;
-  const double2 *Ua = base + t.ua * BB, *Le = base + t.le * BB, *La = base + t.la * BB, *Ue = base + t.ue * BB;
   int cl[NCL];
 #pragma unroll
   for (int j = 0; j < NCL; ++j) cl[j] = min(l + 64 * j, BP - 1);
-  // row r of L_a, U_e through lanes 0 .. 2 NZ - 1 (as in the forward kernel)
+  // row r of L_a, U_e through lanes 0 .. 2 NZ - 1
   const int myb = l / NZ == 1 ? t.ue : t.la, le = l % NZ;
   const int myp = rowpat[(myb * NZ + le) * BP + r];
-  int qa[NCL][NZ], qe[NCL][NZ];
-#pragma unroll
-  for (int e = 0; e < NZ; ++e) {
-#pragma unroll
-    for (int j = 0; j < NCL; ++j) {
-      qa[j][e] = colpat[(t.ua * NZ + e) * BP + cl[j]];
-      qe[j][e] = colpat[(t.le * NZ + e) * BP + cl[j]];
-    }
-  }
   const double2 myv = sp_val(base + myb * BB, myp);
+  // rows r of the G blocks (for Z) into this wave's LDS
+#pragma unroll
+  for (int j = 0; j < NCL; ++j)
+    if (l + 64 * j < BP) {
+      gr[w][0][cl[j]] = Gaa[r * BP + cl[j]];
+      gr[w][1][cl[j]] = Gca[r * BP + cl[j]];
+      gr[w][2][cl[j]] = Gac[r * BP + cl[j]];
+      gr[w][3][cl[j]] = Gcc[r * BP + cl[j]];
+    }
   int pa[NZ], pe[NZ];
-  double2 va[NZ], ve[NZ];
 #pragma unroll
   for (int e = 0; e < NZ; ++e) {
     pa[e] = __builtin_amdgcn_readlane(myp, e);
     pe[e] = __builtin_amdgcn_readlane(myp, NZ + e);
-    va[e] = readlane_c(myv, e);
-    ve[e] = readlane_c(myv, NZ + e);
   }
   double2 gaa[NZ][NCL], gac[NZ][NCL], gca[NZ][NCL], gcc[NZ][NCL];
-  double2 wa[NCL][NZ], we[NCL][NZ], raa[NCL][NZ], rca[NCL][NZ], rac[NCL][NZ], rcc[NCL][NZ];
 #pragma unroll
-  for (int e = 0; e < NZ; ++e) {
+  for (int e = 0; e < NZ; ++e)
 #pragma unroll
     for (int j = 0; j < NCL; ++j) {
       gaa[e][j] = full_at<BP>(Gaa, -1.0, sp_idx(pa[e]), cl[j]);
       gac[e][j] = full_at<BP>(Gac, -1.0, sp_idx(pa[e]), cl[j]);
       gca[e][j] = full_at<BP>(Gca, -1.0, sp_idx(pe[e]), cl[j]);
       gcc[e][j] = full_at<BP>(Gcc, -1.0, sp_idx(pe[e]), cl[j]);
-      wa[j][e] = sp_cval(cval, csrc, Dc, (t.ua * NZ + e) * BP + cl[j], qa[j][e]);
-      we[j][e] = sp_cval(cval, csrc, Dc, (t.le * NZ + e) * BP + cl[j], qe[j][e]);
-      const int ka = sp_idx(qa[j][e]), ke = sp_idx(qe[j][e]);
-      raa[j][e] = Gaa[r * BP + ka];
-      rca[j][e] = Gca[r * BP + ka];
-      rac[j][e] = Gac[r * BP + ke];
-      rcc[j][e] = Gcc[r * BP + ke];
     }
-  }
+  const int cb[2] = {t.ua, t.le};
+  stage_columns<BP, 2>(cv, ci, cb, colpat, cval, csrc, Dc);
+  __syncthreads();
   double2 *Oza = base + t.oza * BB, *Ozc = base + t.ozc * BB, *Oya = base + t.oya * BB,
           *Oyc = base + t.oyc * BB, *Omx = base + t.omx * BB;
 #pragma unroll
   for (int j = 0; j < NCL; ++j) {
+    const int c = cl[j];
     // Y_a[r, :] = L_a[r, :] G_aa + U_e[r, :] G_ca, Y_c[r, :] = L_a[r, :] G_ac + U_e[r, :] G_cc
     // Z_a[r, :] = G_aa[r, :] U_a + G_ac[r, :] L_e, Z_c[r, :] = G_ca[r, :] U_a + G_cc[r, :] L_e
     double2 ya = make_double2(0.0, 0.0), yc = ya, za = ya, zc = ya;
 #pragma unroll
     for (int e = 0; e < NZ; ++e) {
-      cmac(ya, va[e], gaa[e][j]);
-      cmac(yc, va[e], gac[e][j]);
-      cmac(ya, ve[e], gca[e][j]);
-      cmac(yc, ve[e], gcc[e][j]);
-      cmac(za, raa[j][e], wa[j][e]);
-      cmac(zc, rca[j][e], wa[j][e]);
-      cmac(za, rac[j][e], we[j][e]);
-      cmac(zc, rcc[j][e], we[j][e]);
+      const double2 va = readlane_c(myv, e), ve = readlane_c(myv, NZ + e);
+      cmac(ya, va, gaa[e][j]);
+      cmac(yc, va, gac[e][j]);
+      cmac(ya, ve, gca[e][j]);
+      cmac(yc, ve, gcc[e][j]);
+      const double2 wa = cv[0][e][c], we = cv[1][e][c];
+      const int ka = ci[0][e][c], ke = ci[1][e][c];
+      cmac(za, gr[w][0][ka], wa);
+      cmac(zc, gr[w][1][ka], wa);
+      cmac(za, gr[w][2][ke], we);
+      cmac(zc, gr[w][3][ke], we);
     }
     if (l + 64 * j < BP) {
-      sc[w][0][cl[j]] = ya;
-      sc[w][1][cl[j]] = yc;
-      Oya[r * BP + cl[j]] = ya;
-      Oyc[r * BP + cl[j]] = yc;
-      Oza[r * BP + cl[j]] = za;
-      Ozc[r * BP + cl[j]] = zc;
+      sc[w][0][c] = ya;
+      sc[w][1][c] = yc;
+      Oya[r * BP + c] = ya;
+      Oyc[r * BP + c] = yc;
+      Oza[r * BP + c] = za;
+      Ozc[r * BP + c] = zc;
     }
   }
   wave_sync();
   // M[r, :] = Y_a[r, :] U_a + Y_c[r, :] L_e
 #pragma unroll
   for (int j = 0; j < NCL; ++j) {
+    const int c = cl[j];
     double2 mx = make_double2(0.0, 0.0);
 #pragma unroll
     for (int e = 0; e < NZ; ++e) {
-      cmac(mx, sc[w][0][sp_idx(qa[j][e])], wa[j][e]);
-      cmac(mx, sc[w][1][sp_idx(qe[j][e])], we[j][e]);
+      cmac(mx, sc[w][0][ci[0][e][c]], cv[0][e][c]);
+      cmac(mx, sc[w][1][ci[1][e][c]], cv[1][e][c]);
     }
-    if (l + 64 * j < BP) Omx[r * BP + cl[j]] = mx;
+    if (l + 64 * j < BP) Omx[r * BP + c] = mx;
   }
 }
 

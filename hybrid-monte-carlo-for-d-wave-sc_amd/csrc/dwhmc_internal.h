@@ -65,7 +65,7 @@ bool cr_supported_bp(int BP);
 // diagnostic stamp builds (-DCR_STAMPS, dwh_debug_cr_stamps): workgroups recorded per launch
 constexpr int kCrStampWG = 2048;
 #ifdef CR_STAMPS
-int cr_stamps_arm(int key);   // clears the stamps, records the launch whose first block is `key`
+int cr_stamps_arm(int key);   // key >= 0: clears the stamps, records the launch whose first block is `key`; -1: off
 int cr_stamps_read(unsigned long long* out, int nwg);
 #endif
 // level-0 blocks of `list` (ids t*Ly + y, t = 0 D / 1 U / 2 L) fully
