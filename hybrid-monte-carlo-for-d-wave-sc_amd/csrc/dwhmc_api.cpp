@@ -102,6 +102,7 @@ struct CrStage {
   double sg;       // products: sign of the sum
   double flops;    // products: algorithmic fp64 flops per batch item (restricted ranges)
   int maxt32, maxt16, ntmax;
+  int pfirst = 0, npairs = 0;   // products with cfg.pair: range in dwh_ctx::tiles16p
   int tfirst, ntiles;   // products: range in CrPlan::tiles16 (the stage's (task, tile) pairs);
                         // inversions: their side-work tasks in CrPlan::tasks (launch_cr_inv_side,
                         // maxt32 tiles each), flops in `flops`
@@ -834,6 +835,8 @@ struct dwh_ctx {
   double2* bpool = nullptr;   // CR block pool (nbatch x nblk blocks)
   dwh::CrTask* d_tasks = nullptr;
   dwh::CrTile* d_tiles16 = nullptr;
+  std::vector<dwh::CrTile> tiles16p;   // tile pairs of the stages with cfg.pair
+  dwh::CrTile* d_tiles16p = nullptr;
   dwh::CrSpFwd* d_sp_fwd = nullptr;
   dwh::CrSpBwd* d_sp_bwd = nullptr;
   int *d_rowpat = nullptr, *d_colpat = nullptr, *d_colsrc = nullptr;
@@ -1113,7 +1116,10 @@ void cr_enqueue(dwh_ctx* ctx) {
                               ctx->d_colval, ctx->d_colsrc, ctx->Delta, ctx->stream);
     } else {
       Scope s(ctx, T_CR_GEMM, st.flops * c.nbatch);
-      dwh::launch_cr_gemm(c, ctx->bpool, ctx->d_tasks + st.first, st.n, st.maxt32, st.maxt16,
+      if (st.cfg.pair)
+        dwh::launch_cr_gemm_pair(c, ctx->bpool, ctx->d_tiles16p + st.pfirst, st.npairs, st.sg, ctx->stream);
+      else
+        dwh::launch_cr_gemm(c, ctx->bpool, ctx->d_tasks + st.first, st.n, st.maxt32, st.maxt16,
                           ctx->d_tiles16 + st.tfirst, st.ntiles, st.cfg, st.sg, ctx->stream);
     }
   }
@@ -1708,6 +1714,28 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
       d.nld = Lyc;
       for (CrStage& st : ctx->plan.stages)
         if (st.kind == 1) st.cfg = dwh::cr_gemm_config(c, st.n, st.maxt32, st.maxt16, st.ntmax, st.ntiles);
+      // DWHMC_CR_PAIR=1: the K-split-1 stages with two adjacent 16 x 16 tiles
+      // per wave (k_cr_gemm_pair; A/B of VERDICT r04 next #1 (ii))
+      const char* ep = std::getenv("DWHMC_CR_PAIR");
+      const bool pair = ep && *ep == '1';
+      for (CrStage& st : ctx->plan.stages) {
+        if (st.kind != 1 || !pair || st.cfg.ts != 16 || st.cfg.ksplit != 1) continue;
+        st.cfg.pair = 1;
+        st.pfirst = (int)ctx->tiles16p.size();
+        for (int k = 0; k < st.ntiles; ++k) {
+          dwh::CrTile t = ctx->plan.tiles16[st.tfirst + k];
+          t.pad1 = -1;
+          if (k + 1 < st.ntiles) {
+            const dwh::CrTile& u = ctx->plan.tiles16[st.tfirst + k + 1];
+            if (u.out == t.out && u.tr == t.tr && u.tc != t.tc) {
+              t.pad1 = u.tc;
+              ++k;
+            }
+          }
+          ctx->tiles16p.push_back(t);
+        }
+        st.npairs = (int)ctx->tiles16p.size() - st.pfirst;
+      }
       if (const char* e = std::getenv("DWHMC_CR_PLAN_DUMP"); e && *e == '1') {
         int i = 0;
         for (const CrStage& st : ctx->plan.stages) {
@@ -1760,6 +1788,7 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     ALLOC(bpool, (size_t)d.nbatch * ctx->cr.item);
     ALLOC(d_tasks, pl.tasks.size());
     ALLOC(d_tiles16, pl.tiles16.size());
+    ALLOC(d_tiles16p, ctx->tiles16p.size());
     ALLOC(d_sp_fwd, pl.sp_fwd.size());
     ALLOC(d_sp_bwd, pl.sp_bwd.size());
     ALLOC(d_rowpat, pl.rowpat.size());
@@ -1863,6 +1892,7 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     const CrPlan& pl = ctx->plan;
     UP(d_tasks, pl.tasks.data(), pl.tasks.size());
     UP(d_tiles16, pl.tiles16.data(), pl.tiles16.size());
+    UP(d_tiles16p, ctx->tiles16p.data(), ctx->tiles16p.size());
     UP(d_sp_fwd, pl.sp_fwd.data(), pl.sp_fwd.size());
     UP(d_sp_bwd, pl.sp_bwd.data(), pl.sp_bwd.size());
     UP(d_rowpat, pl.rowpat.data(), pl.rowpat.size());

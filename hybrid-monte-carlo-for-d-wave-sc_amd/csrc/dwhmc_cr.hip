@@ -1137,6 +1137,111 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MI == 1 ? k
   cr_gemm_wg<BP, MI, KSPLIT>(pool, item, tasks, ntasks, maxt, tlist, ntl, total, sg, xcd_remap(blockIdx.x, nwg));
 }
 
+// Two horizontally adjacent 16 x 16 output tiles per wave (the stages with
+// K split 1): one A fragment and its (re + im) sum per k-step feed both tiles'
+// three accumulator chains (6 independent MFMA chains per wave, one fewer
+// A load and fp64 add per 6 MFMAs than two single-tile waves).
+template <int BP>
+__device__ __forceinline__ void cr_term_pair(const double2* A, const double2* Bt, int c0a, int crota, unsigned smaska,
+                                             int c0b, int crotb, unsigned smaskb, d4 (&t)[2][3]) {
+  constexpr int HP = BP / 2, KS = BP / 4, KH = HP / 4, PF = kGemmPf;
+  auto load = [&](int s, double2& a, double2& ba, double2& bb) {
+    a = A[s * 4];
+    const int64_t ro = s < KH ? (int64_t)s * 4 * BP : (int64_t)(s - KH) * 4 * BP;
+    ba = Bt[ro + (s < KH ? c0a : crota)];
+    bb = Bt[ro + (s < KH ? c0b : crotb)];
+  };
+  double2 fa[PF], fb0[PF], fb1[PF];
+#pragma unroll
+  for (int p = 0; p < PF; ++p) load(p, fa[p], fb0[p], fb1[p]);
+#pragma unroll
+  for (int j = 0; j < KS; ++j) {
+    const int cs = j % PF;
+    const bool syn = j >= KH;
+    const double ar = fa[cs].x, ai = fa[cs].y, as = ar + ai;
+    double br[2], bi[2], bs[2];
+    const double2 ub[2] = {fb0[cs], fb1[cs]};
+    const unsigned sm[2] = {smaska, smaskb};
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      if (syn) {
+        br[q] = flip_sign(ub[q].x, sm[q]);
+        bi[q] = flip_sign(ub[q].y, sm[q] ^ 0x80000000u);
+        bs[q] = flip_sign(ub[q].x - ub[q].y, sm[q]);
+      } else {
+        br[q] = ub[q].x;
+        bi[q] = ub[q].y;
+        bs[q] = br[q] + bi[q];
+      }
+    }
+    if (j + PF < KS) load(j + PF, fa[cs], fb0[cs], fb1[cs]);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      t[q][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar, br[q], t[q][0], 0, 0, 0);
+      t[q][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai, bi[q], t[q][1], 0, 0, 0);
+      t[q][2] = __builtin_amdgcn_mfma_f64_16x16x4f64(as, bs[q], t[q][2], 0, 0, 0);
+    }
+  }
+}
+
+// tlist: the stage's tile pairs (CrTile::pad1 = the second tile's column, -1:
+// a single tile); total = pairs x batch items; one pair per wave
+template <int BP>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kGemmWaves))) void k_cr_gemm_pair(
+    double2* __restrict__ pool, int64_t item, const CrTile* __restrict__ tlist, int ntl, int total, double sg, int nwg) {
+  constexpr int HP = BP / 2;
+  constexpr int64_t BB = (int64_t)HP * BP;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  const int gt = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, nwg) * 4 + w);
+  const int bi = gt / ntl, rmd = gt - bi * ntl;
+  if (gt >= total) return;
+  const CrTile* tp = tlist + rmd;
+  const int tr = tp->tr, tca = tp->tc, tcb = tp->pad1, cin = tp->cin, out = tp->out;
+  const int tcx = tcb >= 0 ? tcb : tca;
+  double2* base = pool + (int64_t)bi * item;
+  d4 t[2][3];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) t[q][k] = d4{0.0, 0.0, 0.0, 0.0};
+  double2 cpf[2][4];
+  const int64_t ra = (int64_t)(tr * 16 + lk) * BP;
+  if (cin >= 0) {
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      cpf[0][rr] = base[cin * BB + ra + (int64_t)4 * rr * BP + tca * 16 + lr];
+      cpf[1][rr] = base[cin * BB + ra + (int64_t)4 * rr * BP + tcx * 16 + lr];
+    }
+  }
+  const int nt = tp->nt, bq = tp->bq;
+  const int c0a = tca * 16, c0b = tcx * 16;
+  const int crota = c0a < HP ? c0a + HP : c0a - HP, crotb = c0b < HP ? c0b + HP : c0b - HP;
+#pragma unroll 1
+  for (int h = 0; h < nt; ++h) {
+    const double2* A = base + tp->a[h] * BB + (int64_t)(tr * 16 + lr) * BP + lk;
+    const double2* Bt = base + tp->b[h] * BB + (int64_t)lk * BP + lr;
+    const bool q = (bq >> h) & 1;
+    const unsigned sma = ((c0a < HP) == q) ? 0x80000000u : 0u, smb = ((c0b < HP) == q) ? 0x80000000u : 0u;
+    cr_term_pair<BP>(A, Bt, c0a, crota, sma, c0b, crotb, smb, t);
+  }
+  double2* O = base + out * BB + ra;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    if (q == 1 && tcb < 0) break;
+    const int tc = q ? tcb : tca;
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const double a = t[q][0][rr], b = t[q][1][rr], c = t[q][2][rr];
+      double2 x = make_double2(sg * (a - b), sg * (c - a - b));
+      if (cin >= 0) {
+        x.x += cpf[q][rr].x;
+        x.y += cpf[q][rr].y;
+      }
+      O[(int64_t)4 * rr * BP + tc * 16 + lr] = x;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // An inversion stage with side work: the first ninv x nbatch workgroups
 // invert (k_cr_inv), the rest run product tiles that are off the critical
@@ -1413,6 +1518,18 @@ CrGemmCfg cr_gemm_config(const CrDims& c, int ntasks, int maxt32, int maxt16, in
   if (forced.ts == 16 || (forced.ts == 32 && ts32_ok)) return forced;
   const int64_t T = (int64_t)ntiles16 * c.nbatch;
   return CrGemmCfg{16, T >= 2048 ? 1 : 4};
+}
+
+void launch_cr_gemm_pair(const CrDims& c, double2* pool, const CrTile* tlp, int ntlp, double sg, hipStream_t s) {
+  if (ntlp <= 0) return;
+  const int total = c.nbatch * ntlp;
+  const dim3 g((total + 3) / 4), b(256);
+  switch (c.BP) {
+    case 32: hipLaunchKernelGGL(k_cr_gemm_pair<32>, g, b, 0, s, pool, c.item, tlp, ntlp, total, sg, (int)g.x); break;
+    case 64: hipLaunchKernelGGL(k_cr_gemm_pair<64>, g, b, 0, s, pool, c.item, tlp, ntlp, total, sg, (int)g.x); break;
+    case 96: hipLaunchKernelGGL(k_cr_gemm_pair<96>, g, b, 0, s, pool, c.item, tlp, ntlp, total, sg, (int)g.x); break;
+    default: hipLaunchKernelGGL(k_cr_gemm_pair<128>, g, b, 0, s, pool, c.item, tlp, ntlp, total, sg, (int)g.x); break;
+  }
 }
 
 void launch_cr_gemm(const CrDims& c, double2* pool, const CrTask* tasks, int ntasks, int maxt32,

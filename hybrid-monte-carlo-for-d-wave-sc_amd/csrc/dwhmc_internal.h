@@ -146,7 +146,10 @@ void launch_cr_sp_bwd(const CrDims& c, double2* pool, const CrSpBwd* tasks, int 
 // number of waves splitting each tile's K range (1, 2, 4)
 struct CrGemmCfg {
   int ts, ksplit;
+  int pair = 0;   // K split 1, 16 x 16 tiles: two horizontally adjacent tiles per wave (k_cr_gemm_pair)
 };
+// tile pairs of a stage (CrTile::pad1 = the second tile's column, -1 single), one per wave
+void launch_cr_gemm_pair(const CrDims& c, double2* pool, const CrTile* tlp, int ntlp, double sg, hipStream_t s);
 // maxt32 / maxt16: the largest cr_task_tiles over the stage's tasks at ts = 32 / 16;
 // ntmax: the largest term count
 CrGemmCfg cr_gemm_config(const CrDims& c, int ntasks, int maxt32, int maxt16, int ntmax, int ntiles16);
