@@ -102,7 +102,6 @@ struct CrStage {
   double sg;       // products: sign of the sum
   double flops;    // products: algorithmic fp64 flops per batch item (restricted ranges)
   int maxt32, maxt16, ntmax;
-  int pfirst = 0, npairs = 0;   // products with cfg.pair: range in dwh_ctx::tiles16p
   int tfirst, ntiles;   // products: range in CrPlan::tiles16 (the stage's (task, tile) pairs);
                         // inversions: their side-work tasks in CrPlan::tasks (launch_cr_inv_side,
                         // maxt32 tiles each), flops in `flops`
@@ -128,6 +127,42 @@ struct CrPlan {
   std::vector<dwh::CrSpBwd> sp_bwd;
   std::vector<int> rowpat, colpat;
 };
+
+// The sparse stages' per-task operand arrays (launch_cr_sp_fwd / _bwd,
+// dwhmc_internal.h): per task, kCrSpNZ x BP row-pattern words of each left
+// sparse operand (row), and the column entries of each right one — value
+// (cv) and meta word (cm: Δ index + 1 | op << 22 | row << 24).  Forward tasks
+// first, the backward ones from element bwd0.
+struct SpTaskArrays {
+  std::vector<int> row, cm;
+  std::vector<double2> cv;
+  size_t bwd0 = 0;
+};
+SpTaskArrays cr_sparse_task_arrays(const CrPlan& pl, int BP, const std::vector<double2>& colval,
+                                   const std::vector<int>& colsrc) {
+  const int NZ = dwh::kCrSpNZ, E = NZ * BP;
+  SpTaskArrays a;
+  auto put = [&](int rb, int cb) {   // left block rb (rows), right block cb (columns); -1: none
+    if (rb >= 0) a.row.insert(a.row.end(), pl.rowpat.begin() + (size_t)rb * E, pl.rowpat.begin() + (size_t)(rb + 1) * E);
+    if (cb < 0) return;
+    for (int k = cb * E; k < (cb + 1) * E; ++k) {
+      const int w = pl.colpat[k], op = (w >> 22) & 3, idx = (w >> 14) & 0xff, src = colsrc[k];
+      a.cv.push_back(colval[k]);
+      a.cm.push_back((src < 0 ? 0 : src + 1) | op << 22 | idx << 24);
+    }
+  };
+  for (const dwh::CrSpFwd& t : pl.sp_fwd) {
+    put(t.uk, t.lk);
+    put(t.ler, t.uel);
+    put(t.lel, t.uer);
+  }
+  a.bwd0 = a.row.size();
+  for (const dwh::CrSpBwd& t : pl.sp_bwd) {
+    put(t.la, t.ua);
+    put(t.ue, t.le);
+  }
+  return a;
+}
 
 // Nonzero patterns of the level-0 U[y] = A[y, y+1] (pool block Ly + y) and
 // L[y] = A[y+1, y] (2 Ly + y) blocks, from the hopping / pairing tables
@@ -280,10 +315,16 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol, bool 
   CrPlan pl;
   const int HP = BP / 2;
   // sparse level 0 (dwhmc_cr_sparse.hip): even Ly >= 4, a supported block,
-  // patterns within kCrSpNZ; DWHMC_CR_SPARSE0=0 keeps the dense level 0 (A/B)
+  // patterns within kCrSpNZ, and BP >= 64 — at BP = 32 the dense level-0
+  // products are cheaper than the two sparse launches (C2 L = 16: 10.3k vs
+  // 9.5k steps/s; C3 L = 32: 3.82k vs 3.74k; C5 L = 48: 1.27k vs 1.08k,
+  // profiles/r05_exp_sparse_level0.txt).  DWHMC_CR_SPARSE0=1 / 0 forces it
+  // on (any supported BP) / off.
   const bool sparse0 = [&] {
     const char* e = std::getenv("DWHMC_CR_SPARSE0");
+    const bool force = e && *e == '1';
     if ((e && *e == '0') || !hcol || Ly % 2 != 0 || Ly < 4 || !dwh::cr_supported_sparse0(BP)) return false;
+    if (!force && BP < 64) return false;
     return cr_sparse_patterns(Lx, Ly, BP, *hcol, Dcol, pl.rowpat, pl.colpat);
   }();
   if (!sparse0) {
@@ -835,14 +876,11 @@ struct dwh_ctx {
   double2* bpool = nullptr;   // CR block pool (nbatch x nblk blocks)
   dwh::CrTask* d_tasks = nullptr;
   dwh::CrTile* d_tiles16 = nullptr;
-  std::vector<dwh::CrTile> tiles16p;   // tile pairs of the stages with cfg.pair
-  dwh::CrTile* d_tiles16p = nullptr;
   dwh::CrSpFwd* d_sp_fwd = nullptr;
   dwh::CrSpBwd* d_sp_bwd = nullptr;
-  int *d_rowpat = nullptr, *d_colpat = nullptr, *d_colsrc = nullptr;
-  double2* d_colval = nullptr;
-  std::vector<double2> colval_host;   // cr_sparse_colvals
-  std::vector<int> colsrc_host;
+  SpTaskArrays sp_arr;   // the sparse stages' per-task operand arrays
+  int *d_sp_row = nullptr, *d_sp_cm = nullptr;
+  double2* d_sp_cv = nullptr;
   double* efpart = nullptr;     // per (chain, pole) E_f / Tr G22 partials
   unsigned* efdone = nullptr;   // per chain: pole blocks done (k_cr_fermion_energy)
   int *d_inv_blk = nullptr, *d_inv_dst = nullptr, *d_inv_slot = nullptr, *d_inv0_r = nullptr;
@@ -1108,18 +1146,19 @@ void cr_enqueue(dwh_ctx* ctx) {
       guard = dwh::SiteGuard{};
     } else if (st.kind == 2) {
       Scope s(ctx, T_CR_SPARSE, st.flops * c.nbatch);
+      const size_t spE = (size_t)dwh::kCrSpNZ * c.BP;
       if (st.sp == 0)
-        dwh::launch_cr_sp_fwd(c, ctx->bpool, ctx->d_sp_fwd + st.first, st.n, ctx->d_rowpat, ctx->d_colpat,
-                              ctx->d_colval, ctx->d_colsrc, ctx->Delta, ctx->stream);
+        dwh::launch_cr_sp_fwd(c, ctx->bpool, ctx->d_sp_fwd + st.first, st.n, ctx->d_sp_row + st.first * 3 * spE,
+                              ctx->d_sp_cv + st.first * 3 * spE, ctx->d_sp_cm + st.first * 3 * spE, ctx->Delta,
+                              ctx->stream);
       else
-        dwh::launch_cr_sp_bwd(c, ctx->bpool, ctx->d_sp_bwd + st.first, st.n, ctx->d_rowpat, ctx->d_colpat,
-                              ctx->d_colval, ctx->d_colsrc, ctx->Delta, ctx->stream);
+        dwh::launch_cr_sp_bwd(c, ctx->bpool, ctx->d_sp_bwd + st.first, st.n,
+                              ctx->d_sp_row + ctx->sp_arr.bwd0 + st.first * 2 * spE,
+                              ctx->d_sp_cv + ctx->sp_arr.bwd0 + st.first * 2 * spE,
+                              ctx->d_sp_cm + ctx->sp_arr.bwd0 + st.first * 2 * spE, ctx->Delta, ctx->stream);
     } else {
       Scope s(ctx, T_CR_GEMM, st.flops * c.nbatch);
-      if (st.cfg.pair)
-        dwh::launch_cr_gemm_pair(c, ctx->bpool, ctx->d_tiles16p + st.pfirst, st.npairs, st.sg, ctx->stream);
-      else
-        dwh::launch_cr_gemm(c, ctx->bpool, ctx->d_tasks + st.first, st.n, st.maxt32, st.maxt16,
+      dwh::launch_cr_gemm(c, ctx->bpool, ctx->d_tasks + st.first, st.n, st.maxt32, st.maxt16,
                           ctx->d_tiles16 + st.tfirst, st.ntiles, st.cfg, st.sg, ctx->stream);
     }
   }
@@ -1714,28 +1753,6 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
       d.nld = Lyc;
       for (CrStage& st : ctx->plan.stages)
         if (st.kind == 1) st.cfg = dwh::cr_gemm_config(c, st.n, st.maxt32, st.maxt16, st.ntmax, st.ntiles);
-      // DWHMC_CR_PAIR=1: the K-split-1 stages with two adjacent 16 x 16 tiles
-      // per wave (k_cr_gemm_pair; A/B of VERDICT r04 next #1 (ii))
-      const char* ep = std::getenv("DWHMC_CR_PAIR");
-      const bool pair = ep && *ep == '1';
-      for (CrStage& st : ctx->plan.stages) {
-        if (st.kind != 1 || !pair || st.cfg.ts != 16 || st.cfg.ksplit != 1) continue;
-        st.cfg.pair = 1;
-        st.pfirst = (int)ctx->tiles16p.size();
-        for (int k = 0; k < st.ntiles; ++k) {
-          dwh::CrTile t = ctx->plan.tiles16[st.tfirst + k];
-          t.pad1 = -1;
-          if (k + 1 < st.ntiles) {
-            const dwh::CrTile& u = ctx->plan.tiles16[st.tfirst + k + 1];
-            if (u.out == t.out && u.tr == t.tr && u.tc != t.tc) {
-              t.pad1 = u.tc;
-              ++k;
-            }
-          }
-          ctx->tiles16p.push_back(t);
-        }
-        st.npairs = (int)ctx->tiles16p.size() - st.pfirst;
-      }
       if (const char* e = std::getenv("DWHMC_CR_PLAN_DUMP"); e && *e == '1') {
         int i = 0;
         for (const CrStage& st : ctx->plan.stages) {
@@ -1788,16 +1805,17 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     ALLOC(bpool, (size_t)d.nbatch * ctx->cr.item);
     ALLOC(d_tasks, pl.tasks.size());
     ALLOC(d_tiles16, pl.tiles16.size());
-    ALLOC(d_tiles16p, ctx->tiles16p.size());
     ALLOC(d_sp_fwd, pl.sp_fwd.size());
     ALLOC(d_sp_bwd, pl.sp_bwd.size());
-    ALLOC(d_rowpat, pl.rowpat.size());
-    if (!pl.colpat.empty())
-      cr_sparse_colvals(pl.colpat, ctx->cr.Lx, ctx->cr.Ly, ctx->cr.BP, hcol, hval, Dcol, Dsrc, ctx->colval_host,
-                        ctx->colsrc_host);
-    ALLOC(d_colval, ctx->colval_host.size());
-    ALLOC(d_colsrc, ctx->colsrc_host.size());
-    ALLOC(d_colpat, pl.colpat.size());
+    if (!pl.colpat.empty()) {
+      std::vector<double2> colval;
+      std::vector<int> colsrc;
+      cr_sparse_colvals(pl.colpat, ctx->cr.Lx, ctx->cr.Ly, ctx->cr.BP, hcol, hval, Dcol, Dsrc, colval, colsrc);
+      ctx->sp_arr = cr_sparse_task_arrays(pl, ctx->cr.BP, colval, colsrc);
+    }
+    ALLOC(d_sp_row, ctx->sp_arr.row.size());
+    ALLOC(d_sp_cv, ctx->sp_arr.cv.size());
+    ALLOC(d_sp_cm, ctx->sp_arr.cm.size());
     ALLOC(efpart, 2 * (size_t)d.nbatch);
     ALLOC(efdone, (size_t)d.nc);
     ALLOC(d_inv_blk, pl.inv_blk.size());
@@ -1892,13 +1910,11 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     const CrPlan& pl = ctx->plan;
     UP(d_tasks, pl.tasks.data(), pl.tasks.size());
     UP(d_tiles16, pl.tiles16.data(), pl.tiles16.size());
-    UP(d_tiles16p, ctx->tiles16p.data(), ctx->tiles16p.size());
     UP(d_sp_fwd, pl.sp_fwd.data(), pl.sp_fwd.size());
     UP(d_sp_bwd, pl.sp_bwd.data(), pl.sp_bwd.size());
-    UP(d_rowpat, pl.rowpat.data(), pl.rowpat.size());
-    UP(d_colval, ctx->colval_host.data(), ctx->colval_host.size());
-    UP(d_colsrc, ctx->colsrc_host.data(), ctx->colsrc_host.size());
-    UP(d_colpat, pl.colpat.data(), pl.colpat.size());
+    UP(d_sp_row, ctx->sp_arr.row.data(), ctx->sp_arr.row.size());
+    UP(d_sp_cv, ctx->sp_arr.cv.data(), ctx->sp_arr.cv.size());
+    UP(d_sp_cm, ctx->sp_arr.cm.data(), ctx->sp_arr.cm.size());
     UP(d_inv_blk, pl.inv_blk.data(), pl.inv_blk.size());
     UP(d_inv_dst, pl.inv_dst.data(), pl.inv_dst.size());
     UP(d_inv_slot, pl.inv_slot.data(), pl.inv_slot.size());

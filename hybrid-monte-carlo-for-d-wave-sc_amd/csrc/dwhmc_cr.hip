@@ -287,13 +287,15 @@ __device__ __forceinline__ void cr_inv_wg(double2* __restrict__ pool, int64_t it
   if (stamp_on) __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
   CR_STAMP(2);
-  double ld = 0.0;
+  // Π |pivot|^2 of this wave's pivot tile (each wave inverts exactly one);
+  // its log is taken after the loop, off the pivot chain
+  double pp = 1.0;
   // in-place inverse of the (transposed-stored) diagonal tile
   auto invert = [&](d4& tr, d4& ti) -> double {
     double2 dv[4];
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) dv[jj] = make_double2(tr[jj], ti[jj]);
-    const double r = 0.5 * log(wave_inv16_dpp<true>(dv));
+    const double r = wave_inv16_dpp<true>(dv);
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
       tr[jj] = dv[jj].x;
@@ -301,7 +303,7 @@ __device__ __forceinline__ void cr_inv_wg(double2* __restrict__ pool, int64_t it
     }
     return r;
   };
-  if (w == 0) ld += invert(ar[0], ai[0]);
+  if (w == 0) pp = invert(ar[0], ai[0]);
   CR_STAMP(3);
 #pragma unroll
   for (int kb = 0; kb < NT; ++kb) {
@@ -381,7 +383,7 @@ __device__ __forceinline__ void cr_inv_wg(double2* __restrict__ pool, int64_t it
       for (int I = 0; I < NT; ++I)
         if (I == kb + 1) {
           mma16_3m_T<true>(ar[I], ai[I], P[I], xr, xi);
-          ld += invert(ar[I], ai[I]);
+          pp = invert(ar[I], ai[I]);
 #pragma unroll
           for (int rr = 0; rr < 4; ++rr) Q[I][lr * 17 + lk + 4 * rr] = make_double2(ar[I][rr], ai[I][rr]);
         }
@@ -416,7 +418,7 @@ __device__ __forceinline__ void cr_inv_wg(double2* __restrict__ pool, int64_t it
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr)
       Mo[(int64_t)(I * 16 + lk + 4 * rr) * BP + w * 16 + lr] = make_double2(ar[I][rr], ai[I][rr]);
-  if (l == 0) ldw[w] = ld;
+  if (l == 0) ldw[w] = 0.5 * log(pp);
   __syncthreads();
   if (threadIdx.x == 0) {
     double t = 0.0;
@@ -581,8 +583,8 @@ __global__ __launch_bounds__(256) void k_cr_inv0(double2* __restrict__ pool, int
     tile_from_lds<true>(sZ[2 * k + tj], br, bim);
     mma16_3m<false>(sr, si, sB[2 * ti + k], br, bim);
   }
-  double ld = 0.0;
-  if (w == 0) ld += 0.5 * log(wave_inv16_c(sr, si));   // S00^-1 (C layout in, C layout out)
+  double pp = 1.0;   // Π |pivot|^2 (waves 0, 3); the log after the chain
+  if (w == 0) pp = wave_inv16_c(sr, si);   // S00^-1 (C layout in, C layout out)
   tile_to_lds(sS[w], sr, si);                           // S00^-1, S01, S10, S11
   __syncthreads();
   CR_STAMP(4);
@@ -603,7 +605,7 @@ __global__ __launch_bounds__(256) void k_cr_inv0(double2* __restrict__ pool, int
     tile_from_lds(sS[1], br, bim);
     mma16_3m<false>(pr, pi, sS[0], br, bim);   // P
     mma16_3m<true>(sr, si, sS[2], pr, pi);     // T = S11 - S10 P
-    ld += 0.5 * log(wave_inv16_c(sr, si));
+    pp = wave_inv16_c(sr, si);
     tile_to_lds(sX[3], sr, si);
   }
   __syncthreads();
@@ -648,7 +650,7 @@ __global__ __launch_bounds__(256) void k_cr_inv0(double2* __restrict__ pool, int
     Mo[(int64_t)row * BP + col] = make_double2(xr[rr], xi[rr]);
     Mo[(int64_t)row * BP + HP + col] = make_double2(yr[rr], yi[rr]);
   }
-  if (l == 0 && (w == 0 || w == 3)) ldw[w == 3] = ld;
+  if (l == 0 && (w == 0 || w == 3)) ldw[w == 3] = 0.5 * log(pp);
   __syncthreads();
   if (threadIdx.x == 0) {
     const int64_t o = (int64_t)bi * nslots + slot[li];
@@ -717,13 +719,13 @@ __global__ __launch_bounds__(576) void k_cr_inv0_96(double2* __restrict__ pool, 
   }
   tile_to_lds(s1[w], sr, si);   // R is dead (read only before the last barrier)
   __syncthreads();
-  double ld = 0.0;
+  double pp = 1.0;   // Π |pivot|^2 of the diagonal waves; the log after the chain
 #pragma unroll
   for (int p = 0; p < 3; ++p) {
     double2(*cur)[TSZ] = (p & 1) ? s2 : s1;
     double2(*nxt)[TSZ] = (p & 1) ? s1 : s2;
     if (ti == p && tj == p) {
-      ld = 0.5 * log(wave_inv16_c(sr, si));
+      pp = wave_inv16_c(sr, si);
       tile_to_lds(sP, sr, si);
     }
     __syncthreads();
@@ -761,7 +763,7 @@ __global__ __launch_bounds__(576) void k_cr_inv0_96(double2* __restrict__ pool, 
     Mo[(int64_t)row * BP + col] = make_double2(sr[rr], si[rr]);
     Mo[(int64_t)row * BP + HP + col] = make_double2(yr[rr], yi[rr]);
   }
-  if (l == 0 && ti == tj) ldw[ti] = ld;
+  if (l == 0 && ti == tj) ldw[ti] = 0.5 * log(pp);
   __syncthreads();
   if (threadIdx.x == 0) {
     const int64_t o = (int64_t)bi * nslots + slot[li];
@@ -791,7 +793,7 @@ __device__ __forceinline__ void cr_inv32_wave(double2* __restrict__ pool, int64_
   double2* Mo = pool + (int64_t)bi * item + (int64_t)dst[li] * HP * BP;
   const int l = threadIdx.x, lr = l & 15, lk = l >> 4;
   d4 sr, si;   // A, then S, then X = S^-1
-  double ld = 0.0;
+  double ld = 0.0, pa = 1.0;   // pa, ps: Π |pivot|^2 of A and S (their logs after the chain)
   if constexpr (STATIC) {
     const double2* Rm = pool + (int64_t)bi * item + (int64_t)rblk[li] * HP * BP;
 #pragma unroll
@@ -814,7 +816,7 @@ __device__ __forceinline__ void cr_inv32_wave(double2* __restrict__ pool, int64_
       sr[rr] = rr_[rr] = a.x;
       si[rr] = ri_[rr] = a.y;
     }
-    ld = 0.5 * log(wave_inv16_c(rr_, ri_));   // R = A^-1
+    pa = wave_inv16_c(rr_, ri_);   // R = A^-1
     tile_to_lds(sR, rr_, ri_);
   }
   __syncthreads();
@@ -825,7 +827,7 @@ __device__ __forceinline__ void cr_inv32_wave(double2* __restrict__ pool, int64_
   __syncthreads();
   tile_from_lds<true>(sZ, br, bim);
   mma16_3m<false>(sr, si, sB, br, bim);   // S = A + B conj(Z)
-  ld += 0.5 * log(wave_inv16_c(sr, si));
+  const double ps = wave_inv16_c(sr, si);
   tile_to_lds(sX, sr, si);
   __syncthreads();
   d4 yr = {0.0, 0.0, 0.0, 0.0}, yi = {0.0, 0.0, 0.0, 0.0};
@@ -837,7 +839,7 @@ __device__ __forceinline__ void cr_inv32_wave(double2* __restrict__ pool, int64_
     Mo[(int64_t)row * BP + lr] = make_double2(sr[rr], si[rr]);
     Mo[(int64_t)row * BP + HP + lr] = make_double2(yr[rr], yi[rr]);
   }
-  if (l == 0) ldpart[(int64_t)bi * nslots + slot[li]] = ld;
+  if (l == 0) ldpart[(int64_t)bi * nslots + slot[li]] = ld + 0.5 * (log(pa) + log(ps));
 }
 
 __global__ __launch_bounds__(64) void k_cr_inv0_32(double2* __restrict__ pool, int64_t item,
@@ -1137,111 +1139,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MI == 1 ? k
   cr_gemm_wg<BP, MI, KSPLIT>(pool, item, tasks, ntasks, maxt, tlist, ntl, total, sg, xcd_remap(blockIdx.x, nwg));
 }
 
-// Two horizontally adjacent 16 x 16 output tiles per wave (the stages with
-// K split 1): one A fragment and its (re + im) sum per k-step feed both tiles'
-// three accumulator chains (6 independent MFMA chains per wave, one fewer
-// A load and fp64 add per 6 MFMAs than two single-tile waves).
-template <int BP>
-__device__ __forceinline__ void cr_term_pair(const double2* A, const double2* Bt, int c0a, int crota, unsigned smaska,
-                                             int c0b, int crotb, unsigned smaskb, d4 (&t)[2][3]) {
-  constexpr int HP = BP / 2, KS = BP / 4, KH = HP / 4, PF = kGemmPf;
-  auto load = [&](int s, double2& a, double2& ba, double2& bb) {
-    a = A[s * 4];
-    const int64_t ro = s < KH ? (int64_t)s * 4 * BP : (int64_t)(s - KH) * 4 * BP;
-    ba = Bt[ro + (s < KH ? c0a : crota)];
-    bb = Bt[ro + (s < KH ? c0b : crotb)];
-  };
-  double2 fa[PF], fb0[PF], fb1[PF];
-#pragma unroll
-  for (int p = 0; p < PF; ++p) load(p, fa[p], fb0[p], fb1[p]);
-#pragma unroll
-  for (int j = 0; j < KS; ++j) {
-    const int cs = j % PF;
-    const bool syn = j >= KH;
-    const double ar = fa[cs].x, ai = fa[cs].y, as = ar + ai;
-    double br[2], bi[2], bs[2];
-    const double2 ub[2] = {fb0[cs], fb1[cs]};
-    const unsigned sm[2] = {smaska, smaskb};
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      if (syn) {
-        br[q] = flip_sign(ub[q].x, sm[q]);
-        bi[q] = flip_sign(ub[q].y, sm[q] ^ 0x80000000u);
-        bs[q] = flip_sign(ub[q].x - ub[q].y, sm[q]);
-      } else {
-        br[q] = ub[q].x;
-        bi[q] = ub[q].y;
-        bs[q] = br[q] + bi[q];
-      }
-    }
-    if (j + PF < KS) load(j + PF, fa[cs], fb0[cs], fb1[cs]);
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      t[q][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar, br[q], t[q][0], 0, 0, 0);
-      t[q][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai, bi[q], t[q][1], 0, 0, 0);
-      t[q][2] = __builtin_amdgcn_mfma_f64_16x16x4f64(as, bs[q], t[q][2], 0, 0, 0);
-    }
-  }
-}
-
-// tlist: the stage's tile pairs (CrTile::pad1 = the second tile's column, -1:
-// a single tile); total = pairs x batch items; one pair per wave
-template <int BP>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kGemmWaves))) void k_cr_gemm_pair(
-    double2* __restrict__ pool, int64_t item, const CrTile* __restrict__ tlist, int ntl, int total, double sg, int nwg) {
-  constexpr int HP = BP / 2;
-  constexpr int64_t BB = (int64_t)HP * BP;
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
-  const int gt = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, nwg) * 4 + w);
-  const int bi = gt / ntl, rmd = gt - bi * ntl;
-  if (gt >= total) return;
-  const CrTile* tp = tlist + rmd;
-  const int tr = tp->tr, tca = tp->tc, tcb = tp->pad1, cin = tp->cin, out = tp->out;
-  const int tcx = tcb >= 0 ? tcb : tca;
-  double2* base = pool + (int64_t)bi * item;
-  d4 t[2][3];
-#pragma unroll
-  for (int q = 0; q < 2; ++q)
-#pragma unroll
-    for (int k = 0; k < 3; ++k) t[q][k] = d4{0.0, 0.0, 0.0, 0.0};
-  double2 cpf[2][4];
-  const int64_t ra = (int64_t)(tr * 16 + lk) * BP;
-  if (cin >= 0) {
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      cpf[0][rr] = base[cin * BB + ra + (int64_t)4 * rr * BP + tca * 16 + lr];
-      cpf[1][rr] = base[cin * BB + ra + (int64_t)4 * rr * BP + tcx * 16 + lr];
-    }
-  }
-  const int nt = tp->nt, bq = tp->bq;
-  const int c0a = tca * 16, c0b = tcx * 16;
-  const int crota = c0a < HP ? c0a + HP : c0a - HP, crotb = c0b < HP ? c0b + HP : c0b - HP;
-#pragma unroll 1
-  for (int h = 0; h < nt; ++h) {
-    const double2* A = base + tp->a[h] * BB + (int64_t)(tr * 16 + lr) * BP + lk;
-    const double2* Bt = base + tp->b[h] * BB + (int64_t)lk * BP + lr;
-    const bool q = (bq >> h) & 1;
-    const unsigned sma = ((c0a < HP) == q) ? 0x80000000u : 0u, smb = ((c0b < HP) == q) ? 0x80000000u : 0u;
-    cr_term_pair<BP>(A, Bt, c0a, crota, sma, c0b, crotb, smb, t);
-  }
-  double2* O = base + out * BB + ra;
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    if (q == 1 && tcb < 0) break;
-    const int tc = q ? tcb : tca;
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      const double a = t[q][0][rr], b = t[q][1][rr], c = t[q][2][rr];
-      double2 x = make_double2(sg * (a - b), sg * (c - a - b));
-      if (cin >= 0) {
-        x.x += cpf[q][rr].x;
-        x.y += cpf[q][rr].y;
-      }
-      O[(int64_t)4 * rr * BP + tc * 16 + lr] = x;
-    }
-  }
-}
-
 // ---------------------------------------------------------------------------
 // An inversion stage with side work: the first ninv x nbatch workgroups
 // invert (k_cr_inv), the rest run product tiles that are off the critical
@@ -1518,18 +1415,6 @@ CrGemmCfg cr_gemm_config(const CrDims& c, int ntasks, int maxt32, int maxt16, in
   if (forced.ts == 16 || (forced.ts == 32 && ts32_ok)) return forced;
   const int64_t T = (int64_t)ntiles16 * c.nbatch;
   return CrGemmCfg{16, T >= 2048 ? 1 : 4};
-}
-
-void launch_cr_gemm_pair(const CrDims& c, double2* pool, const CrTile* tlp, int ntlp, double sg, hipStream_t s) {
-  if (ntlp <= 0) return;
-  const int total = c.nbatch * ntlp;
-  const dim3 g((total + 3) / 4), b(256);
-  switch (c.BP) {
-    case 32: hipLaunchKernelGGL(k_cr_gemm_pair<32>, g, b, 0, s, pool, c.item, tlp, ntlp, total, sg, (int)g.x); break;
-    case 64: hipLaunchKernelGGL(k_cr_gemm_pair<64>, g, b, 0, s, pool, c.item, tlp, ntlp, total, sg, (int)g.x); break;
-    case 96: hipLaunchKernelGGL(k_cr_gemm_pair<96>, g, b, 0, s, pool, c.item, tlp, ntlp, total, sg, (int)g.x); break;
-    default: hipLaunchKernelGGL(k_cr_gemm_pair<128>, g, b, 0, s, pool, c.item, tlp, ntlp, total, sg, (int)g.x); break;
-  }
 }
 
 void launch_cr_gemm(const CrDims& c, double2* pool, const CrTask* tasks, int ntasks, int maxt32,

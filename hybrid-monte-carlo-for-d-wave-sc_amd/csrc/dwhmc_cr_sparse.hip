@@ -69,17 +69,14 @@ __device__ __forceinline__ double2 full_at(const double2* __restrict__ X, double
   return top ? u : make_double2(sg * u.x, -sg * u.y);
 }
 
-// value of column-pattern entry k (meta word m): the static hopping value, or
-// op(Δ[src] / 2) of a pairing entry (the value k_cr_fill keeps in the pool)
-__device__ __forceinline__ double2 sp_cval(const double2* __restrict__ cval, const int* __restrict__ csrc,
-                                           const double2* __restrict__ Dc, int k, int m) {
-  const double2 v = cval[k];
-  const int src = csrc[k];
-  const double2 d = Dc[src < 0 ? 0 : src];
+// column entry: a static hopping value (v, op applied) or, for a pairing
+// entry, op(Δ[src] / 2) (the value k_cr_fill keeps in the pool) — never both;
+// meta word m: src + 1 (0: none) in bits 0-21, op in 22-23 (1 conj,
+// 2 -conj), row in 24-31.  x: the entry's one load (tcv or Δ).
+__device__ __forceinline__ double2 sp_cval(double2 x, int m) {
+  if ((m & 0x3fffff) == 0) return x;
   const int op = (m >> 22) & 3;
-  const double h = src < 0 ? 0.0 : 0.5;
-  const double sr = op == 2 ? -h : h, si = op == 0 ? h : -h;   // op 1: conj, op 2: -conj
-  return make_double2(v.x + sr * d.x, v.y + si * d.y);
+  return make_double2(op == 2 ? -0.5 * x.x : 0.5 * x.x, op == 0 ? 0.5 * x.y : -0.5 * x.y);   // op 1: conj, 2: -conj
 }
 
 // a lane's complex value in every lane
@@ -89,6 +86,19 @@ __device__ __forceinline__ double2 readlane_c(double2 v, int lane) {
 
 constexpr int kSpRowsWG = 4;   // one output row per wave, four waves per workgroup
 constexpr int NZ = kCrSpNZ;
+// waves per SIMD the register budget is sized for at BP <= 64 (forward,
+// backward): five (<= 96 VGPRs) and four (<= 128), the most without scratch
+// spills (-DSP_WAVES_F / -DSP_WAVES_B for A/B builds)
+#ifndef SP_WAVES_F
+#define SP_WAVES_F 5
+#endif
+#ifndef SP_WAVES_B
+#define SP_WAVES_B 4
+#endif
+template <int BP>
+constexpr int kSpWavesF = BP <= 64 ? SP_WAVES_F : 2;
+template <int BP>
+constexpr int kSpWavesB = BP <= 64 ? SP_WAVES_B : 2;
 
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -98,22 +108,30 @@ __device__ __forceinline__ void wave_sync() {
 
 // Column data of the sparse right operands (dense . sparse products): every
 // output row of a workgroup uses the same column patterns, so the workgroup
-// stages them once in LDS — the value (static hopping or op(Δ/2)) and the
-// row index of each entry — instead of every row re-reading them.
+// stages them once in LDS — the value and the row index of each entry — from
+// the task's own column arrays (tcm / tcv: [NB][kCrSpNZ][BP], coalesced, no
+// dependence on the task descriptor), one load per entry behind the meta word.
 template <int BP, int NB>
 __device__ __forceinline__ void stage_columns(double2 (*cv)[kCrSpNZ][BP], unsigned char (*ci)[kCrSpNZ][BP],
-                                              const int (&blk)[NB], const int* __restrict__ colpat,
-                                              const double2* __restrict__ cval, const int* __restrict__ csrc,
+                                              const double2* __restrict__ tcv, const int* __restrict__ tcm,
                                               const double2* __restrict__ Dc) {
-  for (int q = threadIdx.x; q < NB * NZ * BP; q += blockDim.x) {
-    const int b = q / (NZ * BP), e = (q / BP) % NZ, c = q % BP;
-    int bk = blk[0];
+  constexpr int TOT = NB * NZ * BP, IT = (TOT + 64 * kSpRowsWG - 1) / (64 * kSpRowsWG);
+  int m[IT];
 #pragma unroll
-    for (int x = 1; x < NB; ++x)
-      if (b == x) bk = blk[x];
-    const int k = (bk * NZ + e) * BP + c, m = colpat[k];
-    cv[b][e][c] = sp_cval(cval, csrc, Dc, k, m);
-    ci[b][e][c] = (unsigned char)sp_idx(m);
+  for (int i = 0; i < IT; ++i) m[i] = tcm[min((int)threadIdx.x + 64 * kSpRowsWG * i, TOT - 1)];
+  double2 x[IT];
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {   // one load per entry: the static value or Δ
+    const int q = min((int)threadIdx.x + 64 * kSpRowsWG * i, TOT - 1), s = m[i] & 0x3fffff;
+    x[i] = *(s ? Dc + (s - 1) : tcv + q);
+  }
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int q = threadIdx.x + 64 * kSpRowsWG * i;
+    if (q < TOT) {
+      (&cv[0][0][0])[q] = sp_cval(x[i], m[i]);
+      (&ci[0][0][0])[q] = (unsigned char)((unsigned)m[i] >> 24);
+    }
   }
 }
 
@@ -121,13 +139,13 @@ __device__ __forceinline__ void stage_columns(double2 (*cv)[kCrSpNZ][BP], unsign
 // row's operands are loaded into registers up front (pattern words through
 // lanes, then every value and dense element at once), the V rows meet in LDS.
 template <int BP>
-__global__ __launch_bounds__(256) void k_cr_sp_fwd(double2* __restrict__ pool, int64_t item,
-                                                   const CrSpFwd* __restrict__ tasks, const int* __restrict__ rowpat,
-                                                   const int* __restrict__ colpat, const double2* __restrict__ cval,
-                                                   const int* __restrict__ csrc, const double2* __restrict__ Delta,
-                                                   int twoN, int P, int nrb) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kSpWavesF<BP>))) void k_cr_sp_fwd(double2* __restrict__ pool, int64_t item,
+                                                   const CrSpFwd* __restrict__ tasks, const int* __restrict__ trow,
+                                                   const double2* __restrict__ tcv, const int* __restrict__ tcm,
+                                                   const double2* __restrict__ Delta, int twoN, int P, int nrb) {
   constexpr int HP = BP / 2, NCL = (BP + 63) / 64;
   constexpr int64_t BB = (int64_t)HP * BP;
+  constexpr int TA = 3 * NZ * BP;   // per-task row / column array size
   __shared__ double2 cv[3][NZ][BP];
   __shared__ unsigned char ci[3][NZ][BP];
   __shared__ double2 sc[kSpRowsWG][3][BP];
@@ -144,7 +162,7 @@ __global__ __launch_bounds__(256) void k_cr_sp_fwd(double2* __restrict__ pool, i
   // row r of U_k, L_er, L_el: lanes 0 .. 3 NZ - 1 load one pattern word and its value each
   const int lb = l / NZ < 3 ? l / NZ : 0, le = l % NZ;
   const int myb = lb == 0 ? t.uk : (lb == 1 ? t.ler : t.lel);
-  const int myp = rowpat[(myb * NZ + le) * BP + r];
+  const int myp = trow[(int64_t)ti * TA + (lb * NZ + le) * BP + r];
   const double2 myv = sp_val(base + myb * BB, myp);
   double2 dk[NCL];
 #pragma unroll
@@ -165,8 +183,7 @@ __global__ __launch_bounds__(256) void k_cr_sp_fwd(double2* __restrict__ pool, i
       xr[e][j] = full_at<BP>(Dir, -1.0, sp_idx(pr[e]), cl[j]);
       xl[e][j] = full_at<BP>(Dil, -1.0, sp_idx(pl[e]), cl[j]);
     }
-  const int cb[3] = {t.lk, t.uel, t.uer};
-  stage_columns<BP, 3>(cv, ci, cb, colpat, cval, csrc, Dc);
+  stage_columns<BP, 3>(cv, ci, tcv + (int64_t)ti * TA, tcm + (int64_t)ti * TA, Dc);
   // V1r = -U_k Dinv_er, V2r = -L_er Dinv_er, V2l = -L_el Dinv_el
 #pragma unroll
   for (int j = 0; j < NCL; ++j) {
@@ -211,17 +228,17 @@ __global__ __launch_bounds__(256) void k_cr_sp_fwd(double2* __restrict__ pool, i
 // Y_a, Y_c and M = Y_a U_a + Y_c L_e.  Row r of each G block is staged in the
 // wave's LDS (Z gathers from it), full rows of the G blocks feed Y.
 template <int BP>
-__global__ __launch_bounds__(256) void k_cr_sp_bwd(double2* __restrict__ pool, int64_t item,
-                                                   const CrSpBwd* __restrict__ tasks, const int* __restrict__ rowpat,
-                                                   const int* __restrict__ colpat, const double2* __restrict__ cval,
-                                                   const int* __restrict__ csrc, const double2* __restrict__ Delta,
-                                                   int twoN, int P, int nrb) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kSpWavesB<BP>))) void k_cr_sp_bwd(double2* __restrict__ pool, int64_t item,
+                                                   const CrSpBwd* __restrict__ tasks, const int* __restrict__ trow,
+                                                   const double2* __restrict__ tcv, const int* __restrict__ tcm,
+                                                   const double2* __restrict__ Delta, int twoN, int P, int nrb) {
   constexpr int HP = BP / 2, NCL = (BP + 63) / 64;
   constexpr int64_t BB = (int64_t)HP * BP;
+  constexpr int TA = 2 * NZ * BP;   // per-task row / column array size
   __shared__ double2 cv[2][NZ][BP];
   __shared__ unsigned char ci[2][NZ][BP];
   __shared__ double2 gr[kSpRowsWG][4][BP];
-  __shared__ double2 sc[kSpRowsWG][2][BP];
+  double2(*sc)[4][BP] = gr;   // the Y rows (sc[w][0 / 1]) reuse the wave's G rows once Z is formed
   const double2* Dc = Delta + (int64_t)(blockIdx.y / P) * twoN;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int ti = __builtin_amdgcn_readfirstlane(blockIdx.x / nrb);
@@ -234,8 +251,9 @@ __global__ __launch_bounds__(256) void k_cr_sp_bwd(double2* __restrict__ pool, i
 #pragma unroll
   for (int j = 0; j < NCL; ++j) cl[j] = min(l + 64 * j, BP - 1);
   // row r of L_a, U_e through lanes 0 .. 2 NZ - 1
-  const int myb = l / NZ == 1 ? t.ue : t.la, le = l % NZ;
-  const int myp = rowpat[(myb * NZ + le) * BP + r];
+  const int lb = l / NZ == 1 ? 1 : 0, le = l % NZ;
+  const int myb = lb ? t.ue : t.la;
+  const int myp = trow[(int64_t)ti * TA + (lb * NZ + le) * BP + r];
   const double2 myv = sp_val(base + myb * BB, myp);
   // rows r of the G blocks (for Z) into this wave's LDS
 #pragma unroll
@@ -262,11 +280,11 @@ __global__ __launch_bounds__(256) void k_cr_sp_bwd(double2* __restrict__ pool, i
       gca[e][j] = full_at<BP>(Gca, -1.0, sp_idx(pe[e]), cl[j]);
       gcc[e][j] = full_at<BP>(Gcc, -1.0, sp_idx(pe[e]), cl[j]);
     }
-  const int cb[2] = {t.ua, t.le};
-  stage_columns<BP, 2>(cv, ci, cb, colpat, cval, csrc, Dc);
+  stage_columns<BP, 2>(cv, ci, tcv + (int64_t)ti * TA, tcm + (int64_t)ti * TA, Dc);
   __syncthreads();
   double2 *Oza = base + t.oza * BB, *Ozc = base + t.ozc * BB, *Oya = base + t.oya * BB,
           *Oyc = base + t.oyc * BB, *Omx = base + t.omx * BB;
+  double2 yk[NCL][2];
 #pragma unroll
   for (int j = 0; j < NCL; ++j) {
     const int c = cl[j];
@@ -288,14 +306,21 @@ __global__ __launch_bounds__(256) void k_cr_sp_bwd(double2* __restrict__ pool, i
       cmac(zc, gr[w][3][ke], we);
     }
     if (l + 64 * j < BP) {
-      sc[w][0][c] = ya;
-      sc[w][1][c] = yc;
       Oya[r * BP + c] = ya;
       Oyc[r * BP + c] = yc;
       Oza[r * BP + c] = za;
       Ozc[r * BP + c] = zc;
     }
+    yk[j][0] = ya;
+    yk[j][1] = yc;
   }
+  wave_sync();   // every lane's Z gathers from gr[w] are done
+#pragma unroll
+  for (int j = 0; j < NCL; ++j)
+    if (l + 64 * j < BP) {
+      sc[w][0][cl[j]] = yk[j][0];
+      sc[w][1][cl[j]] = yk[j][1];
+    }
   wave_sync();
   // M[r, :] = Y_a[r, :] U_a + Y_c[r, :] L_e
 #pragma unroll
@@ -315,29 +340,27 @@ __global__ __launch_bounds__(256) void k_cr_sp_bwd(double2* __restrict__ pool, i
 
 bool cr_supported_sparse0(int BP) { return BP == 32 || BP == 64 || BP == 96; }
 
-void launch_cr_sp_fwd(const CrDims& c, double2* pool, const CrSpFwd* tasks, int n, const int* rowpat,
-                      const int* colpat, const double2* colval, const int* colsrc, const double2* Delta,
-                      hipStream_t s) {
+void launch_cr_sp_fwd(const CrDims& c, double2* pool, const CrSpFwd* tasks, int n, const int* trow,
+                      const double2* tcv, const int* tcm, const double2* Delta, hipStream_t s) {
   if (n <= 0) return;
   const int nrb = c.BP / 2 / kSpRowsWG;
   const dim3 g(n * nrb, c.nbatch), b(64 * kSpRowsWG);
   switch (c.BP) {
-    case 32: hipLaunchKernelGGL(k_cr_sp_fwd<32>, g, b, 0, s, pool, c.item, tasks, rowpat, colpat, colval, colsrc, Delta, 2 * c.N, c.P, nrb); break;
-    case 64: hipLaunchKernelGGL(k_cr_sp_fwd<64>, g, b, 0, s, pool, c.item, tasks, rowpat, colpat, colval, colsrc, Delta, 2 * c.N, c.P, nrb); break;
-    default: hipLaunchKernelGGL(k_cr_sp_fwd<96>, g, b, 0, s, pool, c.item, tasks, rowpat, colpat, colval, colsrc, Delta, 2 * c.N, c.P, nrb); break;
+    case 32: hipLaunchKernelGGL(k_cr_sp_fwd<32>, g, b, 0, s, pool, c.item, tasks, trow, tcv, tcm, Delta, 2 * c.N, c.P, nrb); break;
+    case 64: hipLaunchKernelGGL(k_cr_sp_fwd<64>, g, b, 0, s, pool, c.item, tasks, trow, tcv, tcm, Delta, 2 * c.N, c.P, nrb); break;
+    default: hipLaunchKernelGGL(k_cr_sp_fwd<96>, g, b, 0, s, pool, c.item, tasks, trow, tcv, tcm, Delta, 2 * c.N, c.P, nrb); break;
   }
 }
 
-void launch_cr_sp_bwd(const CrDims& c, double2* pool, const CrSpBwd* tasks, int n, const int* rowpat,
-                      const int* colpat, const double2* colval, const int* colsrc, const double2* Delta,
-                      hipStream_t s) {
+void launch_cr_sp_bwd(const CrDims& c, double2* pool, const CrSpBwd* tasks, int n, const int* trow,
+                      const double2* tcv, const int* tcm, const double2* Delta, hipStream_t s) {
   if (n <= 0) return;
   const int nrb = c.BP / 2 / kSpRowsWG;
   const dim3 g(n * nrb, c.nbatch), b(64 * kSpRowsWG);
   switch (c.BP) {
-    case 32: hipLaunchKernelGGL(k_cr_sp_bwd<32>, g, b, 0, s, pool, c.item, tasks, rowpat, colpat, colval, colsrc, Delta, 2 * c.N, c.P, nrb); break;
-    case 64: hipLaunchKernelGGL(k_cr_sp_bwd<64>, g, b, 0, s, pool, c.item, tasks, rowpat, colpat, colval, colsrc, Delta, 2 * c.N, c.P, nrb); break;
-    default: hipLaunchKernelGGL(k_cr_sp_bwd<96>, g, b, 0, s, pool, c.item, tasks, rowpat, colpat, colval, colsrc, Delta, 2 * c.N, c.P, nrb); break;
+    case 32: hipLaunchKernelGGL(k_cr_sp_bwd<32>, g, b, 0, s, pool, c.item, tasks, trow, tcv, tcm, Delta, 2 * c.N, c.P, nrb); break;
+    case 64: hipLaunchKernelGGL(k_cr_sp_bwd<64>, g, b, 0, s, pool, c.item, tasks, trow, tcv, tcm, Delta, 2 * c.N, c.P, nrb); break;
+    default: hipLaunchKernelGGL(k_cr_sp_bwd<96>, g, b, 0, s, pool, c.item, tasks, trow, tcv, tcm, Delta, 2 * c.N, c.P, nrb); break;
   }
 }
 

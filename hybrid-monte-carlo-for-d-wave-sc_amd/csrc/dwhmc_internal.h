@@ -133,23 +133,23 @@ struct CrSpFwd {
 struct CrSpBwd {
   int gaa, gac, gca, gcc, ua, le, la, ue, oza, ozc, oya, oyc, omx, pad0, pad1, pad2;
 };
-// colval / colsrc: the column-pattern values in colpat's order (static
-// hopping value with op applied; or the Δ index of a pairing entry, -1 none),
-// Delta: the chains' N x 2 Δ (batch item bi reads chain bi / P)
-void launch_cr_sp_fwd(const CrDims& c, double2* pool, const CrSpFwd* tasks, int n, const int* rowpat,
-                      const int* colpat, const double2* colval, const int* colsrc, const double2* Delta,
-                      hipStream_t s);
-void launch_cr_sp_bwd(const CrDims& c, double2* pool, const CrSpBwd* tasks, int n, const int* rowpat,
-                      const int* colpat, const double2* colval, const int* colsrc, const double2* Delta,
-                      hipStream_t s);
+// Per task (tasks[ti]), arrays of kCrSpNZ x BP entries for each of its sparse
+// operands, so a workgroup reads its patterns without first reading the
+// task: trow — the row-pattern words of the left sparse operands (forward:
+// U_k, L_er, L_el; backward: L_a, U_e); tcv / tcm — the column entries of the
+// right ones (forward: L_k, U_el, U_er; backward: U_a, L_e): static hopping
+// value with op applied, and meta = (Δ index + 1, 0 none) | op << 22 |
+// row << 24.  Delta: the chains' N x 2 Δ (batch item bi reads chain bi / P).
+void launch_cr_sp_fwd(const CrDims& c, double2* pool, const CrSpFwd* tasks, int n, const int* trow,
+                      const double2* tcv, const int* tcm, const double2* Delta, hipStream_t s);
+void launch_cr_sp_bwd(const CrDims& c, double2* pool, const CrSpBwd* tasks, int n, const int* trow,
+                      const double2* tcv, const int* tcm, const double2* Delta, hipStream_t s);
 // block-product stage configuration: output tile TS x TS (16 or 32) and the
 // number of waves splitting each tile's K range (1, 2, 4)
 struct CrGemmCfg {
   int ts, ksplit;
-  int pair = 0;   // K split 1, 16 x 16 tiles: two horizontally adjacent tiles per wave (k_cr_gemm_pair)
 };
 // tile pairs of a stage (CrTile::pad1 = the second tile's column, -1 single), one per wave
-void launch_cr_gemm_pair(const CrDims& c, double2* pool, const CrTile* tlp, int ntlp, double sg, hipStream_t s);
 // maxt32 / maxt16: the largest cr_task_tiles over the stage's tasks at ts = 32 / 16;
 // ntmax: the largest term count
 CrGemmCfg cr_gemm_config(const CrDims& c, int ntasks, int maxt32, int maxt16, int ntmax, int ntiles16);

@@ -593,18 +593,18 @@ def test_cr_inversion_variants(dwhmc, oracle, monkeypatch, Lx, Ly, inv0, inv32):
     ctx.close()
 
 
-@pytest.mark.parametrize("cfg", ["16:1", "16:2", "16:4", "32:1", "32:2", "16:1p"])
+@pytest.mark.parametrize("cfg", ["16:1", "16:2", "16:4", "32:1", "32:2"])
 @pytest.mark.parametrize("Lx,Ly", [(20, 6), (40, 3), (12, 5), (16, 8)])
 def test_cr_block_product_variants(dwhmc, oracle, monkeypatch, cfg, Lx, Ly):
     """Every compiled block-product kernel variant (16x16 / 32x32 wave tiles,
-    K split 1/2/4; DWHMC_CR_GEMM, read at context creation; "p": two adjacent
-    16x16 tiles per wave, k_cr_gemm_pair, DWHMC_CR_PAIR) against the eigen
+    K split 1/2/4; DWHMC_CR_GEMM, read at context creation) against the eigen
     oracle, on BP = 64 (Lx = 20), 96 (Lx = 40) and 32 (Lx = 12, 16) blocks
-    (16 x 8: the sparse level 0 and its one-term restricted stages).
-    32-wide tiles need BP/2 % 32 == 0 and fall back to 16x16 otherwise."""
+    (16 x 8: the sparse level 0 forced on, and its one-term restricted
+    stages).  32-wide tiles need BP/2 % 32 == 0 and fall back to 16x16
+    otherwise."""
     O = oracle
-    monkeypatch.setenv("DWHMC_CR_GEMM", cfg.rstrip("p"))
-    monkeypatch.setenv("DWHMC_CR_PAIR", "1" if cfg.endswith("p") else "0")
+    monkeypatch.setenv("DWHMC_CR_GEMM", cfg)
+    monkeypatch.setenv("DWHMC_CR_SPARSE0", "1")
     p, dis, Delta = make_case(O, Lx, Ly, 8.0, seed=Lx * 7 + Ly)
     cache, F_ref, Ef_ref = O.evaluate(p, dis, Delta)
     P_ref, _ = O.pairing_P(cache.U, cache.E_n, p)
