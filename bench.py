@@ -46,10 +46,12 @@ METRIC = "fp64 leapfrog steps/sec at L=32, 1→8 MI355X; % fp64 MFMA roofline"
 PEAK_F64_TFLOPS = 78.6        # MI355X dense fp64 matrix peak (= fp64 vector peak on CDNA4)
 PEAK_HBM_GBS = 8000.0         # MI355X HBM3E peak (MI355X_MICROARCH.md)
 # newest committed PMC summary first (profiles/README.md)
-TRAFFIC_FILES = [os.path.join(ROOT, "profiles", f) for f in ("r04_pmc_traffic.json", "r03_pmc_traffic.json", "r02_pmc_traffic.json",
+TRAFFIC_FILES = [os.path.join(ROOT, "profiles", f) for f in ("r05_pmc_traffic.json", "r04_pmc_traffic.json", "r03_pmc_traffic.json", "r02_pmc_traffic.json",
                                                                      "r01_pmc_traffic.json")]
 # SQ counter passes (tools/pmc_sq.sh -> tools/pmc_mfma.py): executed MFMA work per launch
-MFMA_FILES = [os.path.join(ROOT, "profiles", f) for f in ("r04_sq_mfma_L32.json",)]
+MFMA_FILES = [os.path.join(ROOT, "profiles", f) for f in ("r05_sq_mfma_L32.json", "r04_sq_mfma_L32.json")]
+# rocprofv3 --kernel-trace --stats summaries of the driver's command (tools/profile_round.sh)
+KSTATS_FILES = {(32, 16.0, 1): [os.path.join(ROOT, "profiles", f) for f in ("r05_L32_beta16_kernel_stats.csv",)]}
 CLOCK_GHZ = 2.4                # the clock PEAK_F64_TFLOPS is quoted at (1024 SIMDs x 32 flop/cycle)
 ASSEMBLY_REPS = 200            # warm assembly launches timed for `assembly`
 
@@ -64,6 +66,23 @@ def inv_kernels(bp: int, coarse: bool) -> str:
     if not coarse:
         return l0
     return l0 + " + " + ("k_cr_inv32" if bp == 32 else f"k_cr_inv<{bp // 16}>")
+
+
+def profiled_kernel_us(kernel, L, beta, chains):
+    """Mean duration (µs) and call count of `kernel` in the committed rocprofv3
+    --stats summary of this exact workload's bench command, else (None, 0, None)."""
+    import csv
+    for path in KSTATS_FILES.get((L, float(beta), chains), []):
+        try:
+            with open(path) as f:
+                rows = [r for r in csv.DictReader(f) if kernel + "(" in r["Name"] or r["Name"].endswith(kernel)]
+        except (OSError, KeyError):
+            continue
+        if rows:
+            calls = sum(int(r["Calls"]) for r in rows)
+            tot = sum(float(r["TotalDurationNs"]) for r in rows)
+            return tot / calls / 1000.0, calls, os.path.relpath(path, ROOT)
+    return None, 0, None
 
 
 def measured_traffic(kernel, L, beta, chains):
@@ -542,14 +561,26 @@ def main(argv=None):
             rec[f"{dom}_ms_per_step"] = ms / replay_steps
             ms, n, w = kern["assemble"]
             if n and ms > 0:
-                gbs = w / n / (ms / n * 1e-3) / 1e9
-                rec["assembly"] = {"bound": "hbm", "kernel": "k_cr_fill" if cr else "k_assemble",
+                akern = "k_cr_fill" if cr else "k_assemble"
+                ev_us = 1000.0 * ms / n
+                # the kernel's duration: rocprofv3's mean over the same command's
+                # launches (the profile's fills are these warm back-to-back
+                # launches plus one per trajectory); a HIP event pair around a
+                # 2-3 µs launch adds its own packet processing, so the event
+                # figure is kept beside it, not used for the rate
+                pr_us, pr_calls, pr_src = profiled_kernel_us(akern, a.L, a.beta, a.chains)
+                us = pr_us if pr_us else ev_us
+                gbs = w / n / (us * 1e-6) / 1e9
+                rec["assembly"] = {"bound": "hbm", "kernel": akern,
                                    "achieved": gbs,
                                    "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS,
-                                   "bytes_per_launch": w / n, "avg_launch_us": 1000.0 * ms / n,
+                                   "bytes_per_launch": w / n, "avg_launch_us": us,
+                                   "avg_source": (f"{pr_src} (rocprofv3 --stats mean over {pr_calls} launches)"
+                                                  if pr_us else "HIP events per launch"),
+                                   "event_avg_launch_us": ev_us,
                                    "launches_timed": n,
                                    "what": f"{ASSEMBLY_REPS} back-to-back warm launches (dwh_bench_assembly) "
-                                           "after the timed region, HIP events per launch"}
+                                           "after the timed region"}
         if world == 1 and not a.no_c1 and a.L != PRESETS["C1"]["L"]:
             rec["c1"] = c1_line(m, local)
         if not a.no_cpu_baseline and world == 1:
