@@ -129,22 +129,28 @@ struct CrPlan {
 };
 
 // The sparse stages' per-task operand arrays (launch_cr_sp_fwd / _bwd,
-// dwhmc_internal.h): per task, kCrSpNZ x BP row-pattern words of each left
-// sparse operand (row), and the column entries of each right one — value
-// (cv) and meta word (cm: Δ index + 1 | op << 22 | row << 24).  Forward tasks
-// first, the backward ones from element bwd0.
+// dwhmc_internal.h).  Per task: the row-pattern words of its left sparse
+// operands, laid out [row r < HP][operand][entry] so a wave reads its row's
+// words (and then their values) with scalar loads (row); and the column
+// entries of its right operands, [operand][entry][column], value (cv) and
+// meta word (cm: Δ index + 1 | op << 22 | row << 24), read coalesced.
+// Forward tasks first; the backward ones from row_bwd0 / col_bwd0.
 struct SpTaskArrays {
   std::vector<int> row, cm;
   std::vector<double2> cv;
-  size_t bwd0 = 0;
+  size_t row_bwd0 = 0, col_bwd0 = 0;
 };
+
 SpTaskArrays cr_sparse_task_arrays(const CrPlan& pl, int BP, const std::vector<double2>& colval,
                                    const std::vector<int>& colsrc) {
-  const int NZ = dwh::kCrSpNZ, E = NZ * BP;
+  const int NZ = dwh::kCrSpNZ, E = NZ * BP, HP = BP / 2;
   SpTaskArrays a;
-  auto put = [&](int rb, int cb) {   // left block rb (rows), right block cb (columns); -1: none
-    if (rb >= 0) a.row.insert(a.row.end(), pl.rowpat.begin() + (size_t)rb * E, pl.rowpat.begin() + (size_t)(rb + 1) * E);
-    if (cb < 0) return;
+  auto rows = [&](std::initializer_list<int> rbs) {   // [r][operand][entry]
+    for (int r = 0; r < HP; ++r)
+      for (int rb : rbs)
+        for (int e = 0; e < NZ; ++e) a.row.push_back(pl.rowpat[(size_t)rb * E + (size_t)e * BP + r]);
+  };
+  auto cols = [&](int cb) {
     for (int k = cb * E; k < (cb + 1) * E; ++k) {
       const int w = pl.colpat[k], op = (w >> 22) & 3, idx = (w >> 14) & 0xff, src = colsrc[k];
       a.cv.push_back(colval[k]);
@@ -152,14 +158,17 @@ SpTaskArrays cr_sparse_task_arrays(const CrPlan& pl, int BP, const std::vector<d
     }
   };
   for (const dwh::CrSpFwd& t : pl.sp_fwd) {
-    put(t.uk, t.lk);
-    put(t.ler, t.uel);
-    put(t.lel, t.uer);
+    rows({t.uk, t.ler, t.lel});
+    cols(t.lk);
+    cols(t.uel);
+    cols(t.uer);
   }
-  a.bwd0 = a.row.size();
+  a.row_bwd0 = a.row.size();
+  a.col_bwd0 = a.cv.size();
   for (const dwh::CrSpBwd& t : pl.sp_bwd) {
-    put(t.la, t.ua);
-    put(t.ue, t.le);
+    rows({t.la, t.ue});
+    cols(t.ua);
+    cols(t.le);
   }
   return a;
 }
@@ -1146,16 +1155,17 @@ void cr_enqueue(dwh_ctx* ctx) {
       guard = dwh::SiteGuard{};
     } else if (st.kind == 2) {
       Scope s(ctx, T_CR_SPARSE, st.flops * c.nbatch);
-      const size_t spE = (size_t)dwh::kCrSpNZ * c.BP;
+      const size_t spE = (size_t)dwh::kCrSpNZ * c.BP, spR = (size_t)dwh::kCrSpNZ * (c.BP / 2);
+      const SpTaskArrays& sa = ctx->sp_arr;
       if (st.sp == 0)
-        dwh::launch_cr_sp_fwd(c, ctx->bpool, ctx->d_sp_fwd + st.first, st.n, ctx->d_sp_row + st.first * 3 * spE,
+        dwh::launch_cr_sp_fwd(c, ctx->bpool, ctx->d_sp_fwd + st.first, st.n, ctx->d_sp_row + st.first * 3 * spR,
                               ctx->d_sp_cv + st.first * 3 * spE, ctx->d_sp_cm + st.first * 3 * spE, ctx->Delta,
                               ctx->stream);
       else
         dwh::launch_cr_sp_bwd(c, ctx->bpool, ctx->d_sp_bwd + st.first, st.n,
-                              ctx->d_sp_row + ctx->sp_arr.bwd0 + st.first * 2 * spE,
-                              ctx->d_sp_cv + ctx->sp_arr.bwd0 + st.first * 2 * spE,
-                              ctx->d_sp_cm + ctx->sp_arr.bwd0 + st.first * 2 * spE, ctx->Delta, ctx->stream);
+                              ctx->d_sp_row + sa.row_bwd0 + st.first * 2 * spR,
+                              ctx->d_sp_cv + sa.col_bwd0 + st.first * 2 * spE,
+                              ctx->d_sp_cm + sa.col_bwd0 + st.first * 2 * spE, ctx->Delta, ctx->stream);
     } else {
       Scope s(ctx, T_CR_GEMM, st.flops * c.nbatch);
       dwh::launch_cr_gemm(c, ctx->bpool, ctx->d_tasks + st.first, st.n, st.maxt32, st.maxt16,

@@ -460,11 +460,12 @@ __global__ __launch_bounds__(64 * NT) void k_cr_inv(double2* __restrict__ pool, 
                                                     SiteGuard sg, int N, int P) {
   __shared__ double2 pan[2][NT][16 * 17];
   __shared__ double ldw[NT];
-  if ((int)blockIdx.x == gcol) {   // the guard column, pole 0 of each chain
-    if (blockIdx.y % P == 0) site_guard_wg(sg, N, blockIdx.y / P);
+  const int2 xy = xcd_grid2d();
+  if (xy.x == gcol) {   // the guard column, pole 0 of each chain
+    if (xy.y % P == 0) site_guard_wg(sg, N, xy.y / P);
     return;
   }
-  cr_inv_wg<NT>(pool, item, blockIdx.y, blockIdx.x, blk, dst, slot, ldpart, nslots, pan, ldw);
+  cr_inv_wg<NT>(pool, item, xy.y, xy.x, blk, dst, slot, ldpart, nslots, pan, ldw);
 }
 
 // ---------------------------------------------------------------------------
@@ -532,7 +533,8 @@ __global__ __launch_bounds__(256) void k_cr_inv0(double2* __restrict__ pool, int
   constexpr int BP = 64, HP = 32, TSZ = 16 * 17;
   __shared__ double2 sR[4][TSZ], sB[4][TSZ], sZ[4][TSZ], sS[4][TSZ], sX[4][TSZ], sA[4][TSZ];
   __shared__ double ldw[2];
-  const int bi = blockIdx.y, li = blockIdx.x;
+  const int2 xy = xcd_grid2d();
+  const int bi = xy.y, li = xy.x;
   CR_STAMP_INIT(blk);
   CR_RSTAMP(0);
   // site guard (launch_cr_inv0 with Delta): the extra last workgroup column,
@@ -683,7 +685,8 @@ __global__ __launch_bounds__(576) void k_cr_inv0_96(double2* __restrict__ pool, 
   constexpr int BP = 96, HP = 48, TSZ = 16 * 17;
   __shared__ double2 sZ[9][TSZ], s1[9][TSZ], s2[9][TSZ], sP[TSZ];
   __shared__ double ldw[3];
-  const int bi = blockIdx.y, li = blockIdx.x;
+  const int2 xy = xcd_grid2d();
+  const int bi = xy.y, li = xy.x;
   if (li == gcol) {
     if (bi % P == 0) inv0_site_guard(Delta + (int64_t)(bi / P) * 2 * N, site4, N, cap4, flag);
     return;
@@ -850,7 +853,8 @@ __global__ __launch_bounds__(64) void k_cr_inv0_32(double2* __restrict__ pool, i
                                                    const double2* __restrict__ Delta,
                                                    const int* __restrict__ site4, int N, int P, double cap4,
                                                    int* __restrict__ flag) {
-  const int bi = blockIdx.y, li = blockIdx.x;
+  const int2 xy = xcd_grid2d();
+  const int bi = xy.y, li = xy.x;
   if (li == gcol) {
     if (bi % P == 0) inv0_site_guard(Delta + (int64_t)(bi / P) * 2 * N, site4, N, cap4, flag);
     return;
@@ -864,7 +868,8 @@ __global__ __launch_bounds__(64) void k_cr_inv32(double2* __restrict__ pool, int
                                                  int gcol, const int* __restrict__ slot,
                                                  double* __restrict__ ldpart, int nslots, SiteGuard sg, int N,
                                                  int P) {
-  const int bi = blockIdx.y, li = blockIdx.x;
+  const int2 xy = xcd_grid2d();
+  const int bi = xy.y, li = xy.x;
   if (li == gcol) {
     if (bi % P == 0) site_guard_wg(sg, N, bi / P);
     return;
@@ -892,6 +897,11 @@ __global__ __launch_bounds__(64) void k_cr_inv32(double2* __restrict__ pool, int
 // minimum waves per SIMD the 16 x 16 tile kernels are compiled for, and their
 // operand prefetch depth in k-steps
 constexpr int kGemmWaves = 2, kGemmPf = 4;
+// -DCR_GEMM_4M=1 (A/B builds): complex MACs as four real MFMAs with no fp64
+// VALU in the K loop, instead of 3M's three plus two fp64 adds per k-step
+#ifndef CR_GEMM_4M
+#define CR_GEMM_4M 0
+#endif
 
 __device__ __forceinline__ double flip_sign(double x, unsigned m) {
   const unsigned long long b = __builtin_bit_cast(unsigned long long, x);
@@ -926,31 +936,43 @@ __device__ __forceinline__ void cr_term(const double2* A, const double2* Bt, int
   for (int j = 0; j < KSS; ++j) {
     const int cs = j % PF;
     const bool syn = S0 + j >= KH;   // compile time
-    double ar[MI], ai[MI], as[MI], br[MI], bi[MI], bs[MI];
+    double ar[MI], ai[MI], br[MI], bi[MI];
+#if !CR_GEMM_4M
+    double as[MI], bs[MI];
+#endif
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi) {
       ar[mi] = fa[cs][mi].x;
       ai[mi] = fa[cs][mi].y;
-      as[mi] = ar[mi] + ai[mi];
       if (syn) {
         const double ux = fb[cs][mi].x, uy = fb[cs][mi].y;
         br[mi] = flip_sign(ux, smask);
         bi[mi] = flip_sign(uy, smask ^ 0x80000000u);
-        bs[mi] = flip_sign(ux - uy, smask);
       } else {
         br[mi] = fb[cs][mi].x;
         bi[mi] = fb[cs][mi].y;
-        bs[mi] = br[mi] + bi[mi];
       }
+#if !CR_GEMM_4M
+      as[mi] = ar[mi] + ai[mi];
+      bs[mi] = syn ? flip_sign(fb[cs][mi].x - fb[cs][mi].y, smask) : br[mi] + bi[mi];
+#endif
     }
     if (j + PF < KSS) load(S0 + j + PF, fa[cs], fb[cs]);
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
       for (int ni = 0; ni < MI; ++ni) {
+#if CR_GEMM_4M
+        // four real products, no fp64 VALU: t3 collects both cross terms
+        t1[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[mi], br[ni], t1[mi][ni], 0, 0, 0);
+        t3[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[mi], bi[ni], t3[mi][ni], 0, 0, 0);
+        t2[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[mi], bi[ni], t2[mi][ni], 0, 0, 0);
+        t3[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[mi], br[ni], t3[mi][ni], 0, 0, 0);
+#else
         t1[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[mi], br[ni], t1[mi][ni], 0, 0, 0);
         t2[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[mi], bi[ni], t2[mi][ni], 0, 0, 0);
         t3[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(as[mi], bs[ni], t3[mi][ni], 0, 0, 0);
+#endif
       }
   }
 }
@@ -1088,7 +1110,11 @@ __device__ __forceinline__ void cr_gemm_wg(double2* __restrict__ pool, int64_t i
   auto partial = [&](int v) {
     const int mi = v / (MI * 4), ni = (v / 4) % MI, rr = v % 4;
     const double a = t1[mi][ni][rr], b = t2[mi][ni][rr], c = t3[mi][ni][rr];
+#if CR_GEMM_4M
+    return make_double2(sg * (a - b), sg * c);
+#else
     return make_double2(sg * (a - b), sg * (c - a - b));
+#endif
   };
   if constexpr (KSPLIT == 1) {
     if (!valid) return;
@@ -1169,7 +1195,9 @@ __global__ __launch_bounds__(64 * NT) void k_cr_inv_side(double2* __restrict__ p
   const int b = blockIdx.x, nall = ninv * nbatch;
   // inversions first: their branch needs only the leading (preloaded) arguments
   if (b < nall) {
-    cr_inv_wg<NT>(pool, item, b / ninv, b - (b / ninv) * ninv, blk, dst, slot, ldpart, nslots, pan, ldw);
+    // the batch items grouped per XCD (xcd_remap over the inversion range)
+    const int bl = CR_XCD_ITEMS ? xcd_remap(b, nall) : b;
+    cr_inv_wg<NT>(pool, item, bl / ninv, bl - (bl / ninv) * ninv, blk, dst, slot, ldpart, nslots, pan, ldw);
     return;
   }
   CR_STAMP_INIT(blk);

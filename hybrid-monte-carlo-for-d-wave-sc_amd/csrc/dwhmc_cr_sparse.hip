@@ -41,13 +41,18 @@
 namespace dwh {
 namespace {
 
-// stored value of pattern entry e (op 3: zero)
-__device__ __forceinline__ double2 sp_val(const double2* __restrict__ S, int e) {
+// stored value of pattern entry e (op 3: zero), times -1 when NEG, for a
+// wave-uniform entry: the op's signs and the zeroing act on the bit patterns
+// (scalar ALU; the value comes through a scalar load)
+template <bool NEG = false>
+__device__ __forceinline__ double2 sp_sval(const double2* __restrict__ S, int e) {
+  constexpr unsigned long long SB = 1ull << 63, N = NEG ? SB : 0ull;
   const int off = e & 0x3fff, op = (e >> 22) & 3;
   const double2 v = S[off];
-  const double sr = op == 2 ? -1.0 : (op == 3 ? 0.0 : 1.0);
-  const double si = op == 1 ? -1.0 : (op == 3 ? 0.0 : 1.0);
-  return make_double2(sr * v.x, si * v.y);
+  const unsigned long long keep = op == 3 ? 0ull : ~0ull;
+  const unsigned long long bx = (__builtin_bit_cast(unsigned long long, v.x) ^ (op == 2 ? SB : 0ull) ^ N) & keep;
+  const unsigned long long by = (__builtin_bit_cast(unsigned long long, v.y) ^ (op == 1 ? SB : 0ull) ^ N) & keep;
+  return make_double2(__builtin_bit_cast(double, bx), __builtin_bit_cast(double, by));
 }
 __device__ __forceinline__ int sp_idx(int e) { return (e >> 14) & 0xff; }
 
@@ -57,17 +62,32 @@ __device__ __forceinline__ void cmac(double2& a, double2 b, double2 c) {
   a.y = fma(b.x, c.y, fma(b.y, c.x, a.y));
 }
 
-// element (kk, c) of the full block whose top half is X (row-major HP x BP),
-// form s = -1 (M) / +1 (Q): bottom rows synthesised from the top half
-template <int BP>
-__device__ __forceinline__ double2 full_at(const double2* __restrict__ X, double s, int kk, int c) {
-  constexpr int HP = BP / 2;
-  const bool top = kk < HP;
-  const int cc = top ? c : (c < HP ? c + HP : c - HP);
-  const double2 u = X[(top ? kk : kk - HP) * BP + cc];
-  const double sg = top ? 1.0 : (c < HP ? -s : s);
-  return top ? u : make_double2(sg * u.x, -sg * u.y);
+__device__ __forceinline__ double sp_flip(double x, unsigned m) {
+  return __builtin_bit_cast(double, __builtin_bit_cast(unsigned long long, x) ^ ((unsigned long long)m << 32));
 }
+
+// Column c of the full BP x BP M-form block whose top half X (row-major
+// HP x BP) is stored, with its lane-constant parts precomputed: a row access
+// is one select for the column and two sign-bit XORs.  Bottom row HP + k,
+// column c: conj(X[k, c + HP]) (c < HP) or -conj(X[k, c - HP]) (c >= HP).
+template <int BP>
+struct FullCol {
+  int c, crot;
+  unsigned mx, my;   // sign-bit masks of a synthesised entry's real / imaginary part
+  __device__ __forceinline__ explicit FullCol(int col) : c(col) {
+    constexpr int HP = BP / 2;
+    crot = c < HP ? c + HP : c - HP;
+    mx = c >= HP ? 0x80000000u : 0u;
+    my = c < HP ? 0x80000000u : 0u;
+  }
+  // element (kk, c), kk wave-uniform
+  __device__ __forceinline__ double2 at(const double2* __restrict__ X, int kk) const {
+    constexpr int HP = BP / 2;
+    const bool top = kk < HP;
+    const double2 u = X[(top ? kk : kk - HP) * BP + (top ? c : crot)];
+    return make_double2(sp_flip(u.x, top ? 0u : mx), sp_flip(u.y, top ? 0u : my));
+  }
+};
 
 // column entry: a static hopping value (v, op applied) or, for a pairing
 // entry, op(Δ[src] / 2) (the value k_cr_fill keeps in the pool) — never both;
@@ -79,21 +99,17 @@ __device__ __forceinline__ double2 sp_cval(double2 x, int m) {
   return make_double2(op == 2 ? -0.5 * x.x : 0.5 * x.x, op == 0 ? 0.5 * x.y : -0.5 * x.y);   // op 1: conj, 2: -conj
 }
 
-// a lane's complex value in every lane
-__device__ __forceinline__ double2 readlane_c(double2 v, int lane) {
-  return make_double2(readlane_f64(v.x, lane), readlane_f64(v.y, lane));
-}
-
 constexpr int kSpRowsWG = 4;   // one output row per wave, four waves per workgroup
 constexpr int NZ = kCrSpNZ;
 // waves per SIMD the register budget is sized for at BP <= 64 (forward,
-// backward): five (<= 96 VGPRs) and four (<= 128), the most without scratch
-// spills (-DSP_WAVES_F / -DSP_WAVES_B for A/B builds)
+// backward): six (<= 80 VGPRs, 79 used) and five (<= 96), the most without
+// scratch spills, so the C3 forward stage (1536 workgroups of 25 KB LDS) is
+// resident in one round (-DSP_WAVES_F / -DSP_WAVES_B for A/B builds)
 #ifndef SP_WAVES_F
-#define SP_WAVES_F 5
+#define SP_WAVES_F 6
 #endif
 #ifndef SP_WAVES_B
-#define SP_WAVES_B 4
+#define SP_WAVES_B 5
 #endif
 template <int BP>
 constexpr int kSpWavesF = BP <= 64 ? SP_WAVES_F : 2;
@@ -145,44 +161,52 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kSpWavesF<B
                                                    const double2* __restrict__ Delta, int twoN, int P, int nrb) {
   constexpr int HP = BP / 2, NCL = (BP + 63) / 64;
   constexpr int64_t BB = (int64_t)HP * BP;
-  constexpr int TA = 3 * NZ * BP;   // per-task row / column array size
+  constexpr int TA = 3 * NZ * BP, TR = 3 * NZ * HP;   // per-task column / row array sizes
   __shared__ double2 cv[3][NZ][BP];
   __shared__ unsigned char ci[3][NZ][BP];
   __shared__ double2 sc[kSpRowsWG][3][BP];
-  const double2* Dc = Delta + (int64_t)(blockIdx.y / P) * twoN;
+  const double2* Dc = Delta + (int64_t)(__builtin_amdgcn_readfirstlane(xcd_grid2d().y) / P) * twoN;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-  const int ti = __builtin_amdgcn_readfirstlane(blockIdx.x / nrb);
-  const int r = __builtin_amdgcn_readfirstlane((blockIdx.x - ti * nrb) * kSpRowsWG + w);
+  const int2 xy = xcd_grid2d();   // batch items grouped per XCD
+  const int ti = __builtin_amdgcn_readfirstlane(xy.x / nrb);
+  const int r = __builtin_amdgcn_readfirstlane((xy.x - ti * nrb) * kSpRowsWG + w);
   const CrSpFwd t = tasks[ti];
-  double2* base = pool + (int64_t)blockIdx.y * item;
+  double2* base = pool + (int64_t)xy.y * item;
   const double2 *Dir = base + t.dir * BB, *Dil = base + t.dil * BB, *Dk = base + t.dk * BB;
   int cl[NCL];
 #pragma unroll
   for (int j = 0; j < NCL; ++j) cl[j] = min(l + 64 * j, BP - 1);
-  // row r of U_k, L_er, L_el: lanes 0 .. 3 NZ - 1 load one pattern word and its value each
-  const int lb = l / NZ < 3 ? l / NZ : 0, le = l % NZ;
-  const int myb = lb == 0 ? t.uk : (lb == 1 ? t.ler : t.lel);
-  const int myp = trow[(int64_t)ti * TA + (lb * NZ + le) * BP + r];
-  const double2 myv = sp_val(base + myb * BB, myp);
-  double2 dk[NCL];
-#pragma unroll
-  for (int j = 0; j < NCL; ++j) dk[j] = Dk[r * BP + cl[j]];
+  // row r of U_k, L_er, L_el: pattern words and values are wave-uniform
+  // (scalar loads), negated here so the V rows come out with their sign
+  const int* rw = trow + (int64_t)ti * TR + r * 3 * NZ;
   int pu[NZ], pr[NZ], pl[NZ];
 #pragma unroll
   for (int e = 0; e < NZ; ++e) {
-    pu[e] = __builtin_amdgcn_readlane(myp, e);
-    pr[e] = __builtin_amdgcn_readlane(myp, NZ + e);
-    pl[e] = __builtin_amdgcn_readlane(myp, 2 * NZ + e);
+    pu[e] = rw[e];
+    pr[e] = rw[NZ + e];
+    pl[e] = rw[2 * NZ + e];
   }
+  double2 wu[NZ], wr[NZ], wl[NZ];
+#pragma unroll
+  for (int e = 0; e < NZ; ++e) {
+    wu[e] = sp_sval<true>(base + t.uk * BB, pu[e]);
+    wr[e] = sp_sval<true>(base + t.ler * BB, pr[e]);
+    wl[e] = sp_sval<true>(base + t.lel * BB, pl[e]);
+  }
+  double2 dk[NCL];
+#pragma unroll
+  for (int j = 0; j < NCL; ++j) dk[j] = Dk[r * BP + cl[j]];
   double2 xu[NZ][NCL], xr[NZ][NCL], xl[NZ][NCL];
 #pragma unroll
-  for (int e = 0; e < NZ; ++e)
+  for (int j = 0; j < NCL; ++j) {
+    const FullCol<BP> fc(cl[j]);
 #pragma unroll
-    for (int j = 0; j < NCL; ++j) {
-      xu[e][j] = full_at<BP>(Dir, -1.0, sp_idx(pu[e]), cl[j]);
-      xr[e][j] = full_at<BP>(Dir, -1.0, sp_idx(pr[e]), cl[j]);
-      xl[e][j] = full_at<BP>(Dil, -1.0, sp_idx(pl[e]), cl[j]);
+    for (int e = 0; e < NZ; ++e) {
+      xu[e][j] = fc.at(Dir, sp_idx(pu[e]));
+      xr[e][j] = fc.at(Dir, sp_idx(pr[e]));
+      xl[e][j] = fc.at(Dil, sp_idx(pl[e]));
     }
+  }
   stage_columns<BP, 3>(cv, ci, tcv + (int64_t)ti * TA, tcm + (int64_t)ti * TA, Dc);
   // V1r = -U_k Dinv_er, V2r = -L_er Dinv_er, V2l = -L_el Dinv_el
 #pragma unroll
@@ -190,14 +214,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kSpWavesF<B
     double2 v1 = make_double2(0.0, 0.0), v2r = v1, v2l = v1;
 #pragma unroll
     for (int e = 0; e < NZ; ++e) {
-      cmac(v1, readlane_c(myv, e), xu[e][j]);
-      cmac(v2r, readlane_c(myv, NZ + e), xr[e][j]);
-      cmac(v2l, readlane_c(myv, 2 * NZ + e), xl[e][j]);
+      cmac(v1, wu[e], xu[e][j]);
+      cmac(v2r, wr[e], xr[e][j]);
+      cmac(v2l, wl[e], xl[e][j]);
     }
     if (l + 64 * j < BP) {
-      sc[w][0][cl[j]] = make_double2(-v1.x, -v1.y);
-      sc[w][1][cl[j]] = make_double2(-v2r.x, -v2r.y);
-      sc[w][2][cl[j]] = make_double2(-v2l.x, -v2l.y);
+      sc[w][0][cl[j]] = v1;
+      sc[w][1][cl[j]] = v2r;
+      sc[w][2][cl[j]] = v2l;
     }
   }
   __syncthreads();
@@ -234,27 +258,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kSpWavesB<B
                                                    const double2* __restrict__ Delta, int twoN, int P, int nrb) {
   constexpr int HP = BP / 2, NCL = (BP + 63) / 64;
   constexpr int64_t BB = (int64_t)HP * BP;
-  constexpr int TA = 2 * NZ * BP;   // per-task row / column array size
+  constexpr int TA = 2 * NZ * BP, TR = 2 * NZ * HP;   // per-task column / row array sizes
   __shared__ double2 cv[2][NZ][BP];
   __shared__ unsigned char ci[2][NZ][BP];
   __shared__ double2 gr[kSpRowsWG][4][BP];
   double2(*sc)[4][BP] = gr;   // the Y rows (sc[w][0 / 1]) reuse the wave's G rows once Z is formed
-  const double2* Dc = Delta + (int64_t)(blockIdx.y / P) * twoN;
+  const double2* Dc = Delta + (int64_t)(__builtin_amdgcn_readfirstlane(xcd_grid2d().y) / P) * twoN;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-  const int ti = __builtin_amdgcn_readfirstlane(blockIdx.x / nrb);
-  const int r = __builtin_amdgcn_readfirstlane((blockIdx.x - ti * nrb) * kSpRowsWG + w);
+  const int2 xy = xcd_grid2d();   // batch items grouped per XCD
+  const int ti = __builtin_amdgcn_readfirstlane(xy.x / nrb);
+  const int r = __builtin_amdgcn_readfirstlane((xy.x - ti * nrb) * kSpRowsWG + w);
   const CrSpBwd t = tasks[ti];
-  double2* base = pool + (int64_t)blockIdx.y * item;
+  double2* base = pool + (int64_t)xy.y * item;
   const double2 *Gaa = base + t.gaa * BB, *Gac = base + t.gac * BB, *Gca = base + t.gca * BB,
                 *Gcc = base + t.gcc * BB;
   int cl[NCL];
 #pragma unroll
   for (int j = 0; j < NCL; ++j) cl[j] = min(l + 64 * j, BP - 1);
-  // row r of L_a, U_e through lanes 0 .. 2 NZ - 1
-  const int lb = l / NZ == 1 ? 1 : 0, le = l % NZ;
-  const int myb = lb ? t.ue : t.la;
-  const int myp = trow[(int64_t)ti * TA + (lb * NZ + le) * BP + r];
-  const double2 myv = sp_val(base + myb * BB, myp);
+  // row r of L_a, U_e: wave-uniform pattern words and values (scalar loads)
+  const int* rw = trow + (int64_t)ti * TR + r * 2 * NZ;
+  int pa[NZ], pe[NZ];
+#pragma unroll
+  for (int e = 0; e < NZ; ++e) {
+    pa[e] = rw[e];
+    pe[e] = rw[NZ + e];
+  }
+  double2 va[NZ], ve[NZ];
+#pragma unroll
+  for (int e = 0; e < NZ; ++e) {
+    va[e] = sp_sval(base + t.la * BB, pa[e]);
+    ve[e] = sp_sval(base + t.ue * BB, pe[e]);
+  }
   // rows r of the G blocks (for Z) into this wave's LDS
 #pragma unroll
   for (int j = 0; j < NCL; ++j)
@@ -264,22 +298,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kSpWavesB<B
       gr[w][2][cl[j]] = Gac[r * BP + cl[j]];
       gr[w][3][cl[j]] = Gcc[r * BP + cl[j]];
     }
-  int pa[NZ], pe[NZ];
-#pragma unroll
-  for (int e = 0; e < NZ; ++e) {
-    pa[e] = __builtin_amdgcn_readlane(myp, e);
-    pe[e] = __builtin_amdgcn_readlane(myp, NZ + e);
-  }
   double2 gaa[NZ][NCL], gac[NZ][NCL], gca[NZ][NCL], gcc[NZ][NCL];
 #pragma unroll
-  for (int e = 0; e < NZ; ++e)
+  for (int j = 0; j < NCL; ++j) {
+    const FullCol<BP> fc(cl[j]);
 #pragma unroll
-    for (int j = 0; j < NCL; ++j) {
-      gaa[e][j] = full_at<BP>(Gaa, -1.0, sp_idx(pa[e]), cl[j]);
-      gac[e][j] = full_at<BP>(Gac, -1.0, sp_idx(pa[e]), cl[j]);
-      gca[e][j] = full_at<BP>(Gca, -1.0, sp_idx(pe[e]), cl[j]);
-      gcc[e][j] = full_at<BP>(Gcc, -1.0, sp_idx(pe[e]), cl[j]);
+    for (int e = 0; e < NZ; ++e) {
+      gaa[e][j] = fc.at(Gaa, sp_idx(pa[e]));
+      gac[e][j] = fc.at(Gac, sp_idx(pa[e]));
+      gca[e][j] = fc.at(Gca, sp_idx(pe[e]));
+      gcc[e][j] = fc.at(Gcc, sp_idx(pe[e]));
     }
+  }
   stage_columns<BP, 2>(cv, ci, tcv + (int64_t)ti * TA, tcm + (int64_t)ti * TA, Dc);
   __syncthreads();
   double2 *Oza = base + t.oza * BB, *Ozc = base + t.ozc * BB, *Oya = base + t.oya * BB,
@@ -293,11 +323,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kSpWavesB<B
     double2 ya = make_double2(0.0, 0.0), yc = ya, za = ya, zc = ya;
 #pragma unroll
     for (int e = 0; e < NZ; ++e) {
-      const double2 va = readlane_c(myv, e), ve = readlane_c(myv, NZ + e);
-      cmac(ya, va, gaa[e][j]);
-      cmac(yc, va, gac[e][j]);
-      cmac(ya, ve, gca[e][j]);
-      cmac(yc, ve, gcc[e][j]);
+      cmac(ya, va[e], gaa[e][j]);
+      cmac(yc, va[e], gac[e][j]);
+      cmac(ya, ve[e], gca[e][j]);
+      cmac(yc, ve[e], gcc[e][j]);
       const double2 wa = cv[0][e][c], we = cv[1][e][c];
       const int ka = ci[0][e][c], ke = ci[1][e][c];
       cmac(za, gr[w][0][ka], wa);

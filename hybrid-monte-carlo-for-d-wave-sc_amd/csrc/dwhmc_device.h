@@ -51,6 +51,23 @@ __device__ __forceinline__ int xcd_remap(int orig, int total) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
 }
 
+// The same grouping for a 2D grid (x: work within a batch item, y: batch
+// item): this workgroup's (x, y) after remapping its linear index, so a
+// batch item's workgroups share an XCD (and the XCD the block-product stages
+// give it, up to rounding), and the blocks one stage writes are read by the
+// next through that XCD's L2.  -DCR_XCD_ITEMS=0: hardware order (A/B).
+#ifndef CR_XCD_ITEMS
+#define CR_XCD_ITEMS 1
+#endif
+__device__ __forceinline__ int2 xcd_grid2d() {
+#if CR_XCD_ITEMS
+  const int nx = gridDim.x, g = xcd_remap(blockIdx.x + nx * blockIdx.y, nx * gridDim.y);
+  return make_int2(g % nx, g / nx);
+#else
+  return make_int2(blockIdx.x, blockIdx.y);
+#endif
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
