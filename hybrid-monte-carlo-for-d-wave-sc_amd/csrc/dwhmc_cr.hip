@@ -896,7 +896,13 @@ __global__ __launch_bounds__(64) void k_cr_inv32(double2* __restrict__ pool, int
 // ---------------------------------------------------------------------------
 // minimum waves per SIMD the 16 x 16 tile kernels are compiled for, and their
 // operand prefetch depth in k-steps
-constexpr int kGemmWaves = 2, kGemmPf = 4;
+#ifndef CR_GEMM_WAVES
+#define CR_GEMM_WAVES 2
+#endif
+#ifndef CR_GEMM_PF
+#define CR_GEMM_PF 4
+#endif
+constexpr int kGemmWaves = CR_GEMM_WAVES, kGemmPf = CR_GEMM_PF;
 // -DCR_GEMM_4M=1 (A/B builds): complex MACs as four real MFMAs with no fp64
 // VALU in the K loop, instead of 3M's three plus two fp64 adds per k-step
 #ifndef CR_GEMM_4M
