@@ -955,7 +955,8 @@ __global__ __launch_bounds__(64) void k_eig_invit(const double* __restrict__ d, 
 // separated eigenvalues are orthogonal to ~2 eps ||T|| / gap already; inside a
 // cluster the rotation is O(that) for distinct eigenvalues, and an orthonormal
 // basis of the eigenspace for exactly degenerate ones.  One workgroup per
-// candidate first index; *bad = 1 when a cluster is too long or G is not
+// candidate first index; clusters longer than maxc are left to the host-driven
+// Cholesky QR (long_clusters in dwhmc_api.cpp); *bad = 1 when G is not
 // positive definite (the caller then re-solves with rocSOLVER's zheev).
 __global__ __launch_bounds__(256) void k_eig_orth(const double* __restrict__ E, const double* __restrict__ tnorm,
                                                   int n, double* __restrict__ Zt, int64_t sZ, double ctol,

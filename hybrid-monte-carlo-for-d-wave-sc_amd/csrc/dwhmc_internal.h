@@ -286,8 +286,8 @@ constexpr int kEigMaxN = 5120;              // rows k_eig_step holds in register
 // eigenvalue gap / ||T|| below which inverse-iteration vectors are
 // orthonormalised together (Cholesky QR); wider gaps leave overlaps <= ~eps /
 // 1e-6 that the symmetric orthogonalisation step squares away.  (2.5e-4 in
-// round 3 made runs of >64 "clustered" levels from n ~ 3000 on, and with them
-// the rocSOLVER fallback.)
+// round 3 made runs of >64 "clustered" levels from n ~ 3000 on; runs that
+// long are now orthonormalised by the host-driven Cholesky QR.)
 constexpr double kEigClusterTol = 1e-6;
 // the particle-hole half solve computes the partners' vectors itself unless
 // the gap below c0 exceeds this (the partner images are not orthogonalised

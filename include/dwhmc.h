@@ -217,10 +217,11 @@ int dwh_debug_cr_stamps(dwh_ctx* ctx, int32_t inv_stage, uint64_t* out, int64_t 
  * transport and spectra need.  The library's own Hermitian eigensolver on
  * the context's stream (dwhmc_eig.hip: Householder tridiagonalisation,
  * multisection on Sturm counts, inverse iteration with cluster
- * orthonormalisation, blocked back-transform; rocBLAS zgemm / dgemm for the
- * plain products); DWHMC_EIG_SOLVER=evd / ev selects rocSOLVER zheevd / zheev
- * instead, and rocSOLVER zheev is the fallback when the own solver flags a
- * result (eigenvalue cluster longer than 64, non-finite values).
+ * orthonormalisation (clusters of any length), blocked back-transform; the
+ * plain products on the library's own MFMA kernel, dwhmc_gemm.hip);
+ * DWHMC_EIG_SOLVER=evd / ev selects rocSOLVER zheevd / zheev instead (A/B),
+ * and rocSOLVER zheev re-solves only a result with non-finite values or an
+ * order above the own solver's 5120.
  * E: 2N, ascending; U (nullable): 2N x 2N column-major, the eigenvector of
  * E[n] in column n (phases are the solver's). */
 int dwh_eigensystem(dwh_ctx* ctx, int64_t chain, double* E, dwh_c128* U);
@@ -237,15 +238,16 @@ int dwh_transport_grid(double eta, double domega, double omega_max, int64_t* n_o
  * antinodal DOS on the DOS grid (n_dos values each) and A(k, ω=0) as the
  * column-major Lx x Ly map (element (kx, ky) at kx + Lx·ky, FFTW's forward
  * sign).  n_omega / n_dos must equal dwh_transport_grid's.  The current
- * operator J_x [:237-283] is built once per context; J_mn = U^H (J ⊕ J) U is a
- * rocBLAS zgemm; the rest runs in dwhmc_transport.hip. */
+ * operator J_x [:237-283] is built once per context; J_mn = U^H (J ⊕ J) U is
+ * the library's own MFMA product (dwhmc_gemm.hip); the rest runs in
+ * dwhmc_transport.hip. */
 int dwh_measure_transport(dwh_ctx* ctx, int64_t chain, double eta, double domega, double omega_max,
                           double* stiffness, double* dc_cond, double* sigma, int64_t n_omega,
                           double* dos, double* dos_an, int64_t n_dos, double* ak0);
 
 /* dwh_measure_transport for every chain of the context at once: the
  * eigensolves and J_mn products are batched over the chains (every kernel
- * of the eigensolver and the rocBLAS products take all chains per launch).
+ * of the eigensolver and the products take all chains per launch).
  * Outputs per chain c at stiffness[c], dc_cond[c], sigma[c*n_omega],
  * dos[c*n_dos], dos_an[c*n_dos], ak0[c*Lx*Ly]. */
 int dwh_measure_transport_batched(dwh_ctx* ctx, double eta, double domega, double omega_max,
