@@ -1430,7 +1430,9 @@ void launch_cr_inv_side(const CrDims& c, double2* pool, const int* blk, const in
 // configuration for every stage (A/B runs; tests/test_gpu_parity.py runs
 // every compiled variant).
 CrGemmCfg cr_gemm_config(const CrDims& c, int ntasks, int maxt32, int maxt16, int ntmax, int ntiles16) {
+  (void)ntasks;
   (void)maxt32;
+  (void)maxt16;
   (void)ntmax;
   // read at every context creation (tests switch it between contexts)
   const CrGemmCfg forced = [] {
@@ -1446,13 +1448,6 @@ CrGemmCfg cr_gemm_config(const CrDims& c, int ntasks, int maxt32, int maxt16, in
   const bool ts32_ok = (c.BP / 2) % 32 == 0;   // 32-wide tiles must not straddle A | B
   if (forced.ts == 16 || (forced.ts == 32 && ts32_ok)) return forced;
   const int64_t T = (int64_t)ntiles16 * c.nbatch;
-  // A/B (temporary): DWHMC_CR_BIG=TS:KSPLIT:T0 for the unrestricted stages of >= T0 tiles
-  if (const char* e = std::getenv("DWHMC_CR_BIG")) {
-    int ts = 0, ks = 1, t0 = 1 << 30;
-    if (std::sscanf(e, "%d:%d:%d", &ts, &ks, &t0) == 3 && T >= t0 && ntiles16 == ntasks * maxt16 &&
-        (ts == 16 || (ts == 32 && ts32_ok)))
-      return CrGemmCfg{ts, ks};
-  }
   return CrGemmCfg{16, T >= 2048 ? 1 : 4};
 }
 
