@@ -660,8 +660,9 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol, bool 
     // Level 0 is the last backward level: G_ea, G_ec (cross-block bonds, not
     // operands of anything after them) are formed only on the B-part tiles
     // the vertical pairing bonds read (need); G_ae, G_ce (right operands of
-    // G_ee) need their whole top half, G_ee (in-block bonds, hole diagonal)
-    // its need tiles.
+    // G_ee in the dense level 0) need their whole top half there, and only
+    // their need tiles in the sparse level 0 (G_ee from T = -Dinv M); G_ee
+    // (in-block bonds, hole diagonal) its need tiles.
     const bool sel = (li == 0);
     const int H0 = sel ? HP : 0, H1 = sel ? HP + Lx : BP;
     if (lv.sparse) {
@@ -698,11 +699,15 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol, bool 
         task(gea, -1, {{D, x.ya}});
         keep_next = &need[1][e];   // G_ec = G_U[e]
         task(gec, -1, {{D, x.yc}});
+        // G_ae = G_U[a] and G_ce = G_L[e] are read only by the gathers here
+        // (G_ee comes from T, not from them): their need tiles only
+        keep_next = &need[1][a];
+        task(gae, -1, {{x.za, D}});
+        keep_next = &need[2][e];
+        task(gce, -1, {{x.zc, D}});
         keep_next = nullptr;
         w_c0 = 0;
         w_c1 = BP;
-        task(gae, -1, {{x.za, D}});
-        task(gce, -1, {{x.zc, D}});
         task(tn[e], -1, {{D, x.mx}});
         gu[a] = gae;
         gl[a] = gea;

@@ -399,7 +399,10 @@ def cr_flop_count(Lx: int, Ly: int, rows: int = 1, sparse0: bool = True):
                 n_ec = len(reads.get((e, c), ()))
                 n_ea = 0 if a == c else len(reads.get((e, a), ()))
                 n_ee = len(reads.get((e, e), ()))
-                terms += (n_ea + n_ec) * per_ea + 3 * full + n_ee * per_ee
+                # G_ae = G[a, e], G_ce = G[c, e]: only the gathers read them here
+                n_ae = len(reads.get((a, e), ()))
+                n_ce = 0 if a == c else len(reads.get((c, e), ()))
+                terms += (n_ea + n_ec + n_ae + n_ce) * per_ea + full + n_ee * per_ee
             return
         E = list(range(1, m - (m % 2), 2))
         K = list(range(0, m, 2))
