@@ -945,6 +945,8 @@ struct dwh_ctx {
   int64_t eig_long_clusters = 0;   // clusters longer than k_eig_orth's limit, orthonormalised by long_clusters
   int eig_ph_last = -1;    // dwh_info_t::eig_half: eig_ph of the last eigensolve (-1: none yet)
   double *d_eig_d = nullptr, *d_eig_e = nullptr, *d_eig_tn = nullptr;
+  hipStream_t eig_sx[3] = {};       // extra streams of the sub-batched tridiagonalisation
+  hipEvent_t eig_ev[4] = {};
 
   // timing
   int timing = 0;   // bitmask over TimerName (bit i = kTimerNames[i])
@@ -2047,12 +2049,14 @@ int transport_prepare(dwh_ctx* ctx, int64_t nw, int64_t nd, int slots) {
     ctx->tr_slots = slots;
     ctx->tr_nw = ctx->tr_nd = -1;   // per-slot outputs below are re-sized too
   }
-  if (nw != ctx->tr_nw) {
+  if (nw != ctx->tr_nw || nd != ctx->tr_nd) {
+    // partials of the σ chunks and of the DOS slices (one after the other)
     HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
     drop_alloc(ctx, b.part);
     drop_alloc(ctx, b.sigma);
     b.part = b.sigma = nullptr;
-    if ((rc = dalloc(ctx, &b.part, (size_t)dwh::tr_sigma_chunks(N) * nw)) ||
+    const size_t np = std::max<size_t>((size_t)dwh::tr_sigma_chunks(N) * nw, (size_t)2 * dwh::tr_dos_slices(N) * nd);
+    if ((rc = dalloc(ctx, &b.part, std::max<size_t>(np, 1))) ||
         (rc = dalloc(ctx, &b.sigma, (size_t)ctx->tr_slots * nw)))
       return rc;
     ctx->tr_nw = nw;
@@ -2210,6 +2214,9 @@ int long_clusters(dwh_ctx* ctx, const std::vector<double>& Eh, const std::vector
   return DWH_OK;
 }
 
+// sub-batch streams of own_heev_enqueue's tridiagonalisation (default / most)
+constexpr int kEigStreams = 2, kEigStreamsMax = 4;
+
 int own_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m) {
   const int N = ctx->d.N, n = 2 * N;
   const dwh::TrBufs& b = ctx->tr;
@@ -2219,8 +2226,7 @@ int own_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m) {
   // back-transform: W = V^H U is only NB x n, so with fewer than 4 matrices
   // its K range is split into up to KS chunks (one batched zgemm per matrix)
   constexpr int KS = 8;
-  const int ks = m >= 4 ? 1 : KS;
-  const int64_t sP = (int64_t)T * n, sT = (int64_t)nblk * NB * NB, sW = (int64_t)NB * n, sWs = ks * sW;
+  const int64_t sP = (int64_t)T * n, sT = (int64_t)nblk * NB * NB, sW = (int64_t)NB * n;
   int rc;
   if (m > ctx->eig_slots) {
     HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
@@ -2247,11 +2253,40 @@ int own_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m) {
   EigPhase ph(s);
   if ((rc = assemble_slots(ctx, src, m, A))) return rc;
   ph.mark("assemble");
+  // Batches of 8+ matrices run as sub-batches of 4+ on their own streams,
+  // column by column: one sub-batch's HBM-bound pass overlaps another's
+  // latency-bound reduce and step (DWHMC_EIG_STREAMS: the number of streams,
+  // 1 = one stream, A/B)
+  int ng = m >= 8 ? kEigStreams : 1;
+  if (const char* es = std::getenv("DWHMC_EIG_STREAMS")) ng = std::max(1, std::min(std::atoi(es), kEigStreamsMax));
+  ng = std::max(1, std::min(ng, m / dwh::kEigDeferMin));
+  for (int g = 1; g < ng; ++g)
+    if (!ctx->eig_sx[g - 1] &&
+        hipStreamCreateWithFlags(&ctx->eig_sx[g - 1], hipStreamNonBlocking) != hipSuccess)
+      return fail(ctx, DWH_ERR_HIP, "eigensolver stream creation failed");
+  for (int g = 0; g < ng && ng > 1; ++g)
+    if (!ctx->eig_ev[g] && hipEventCreateWithFlags(&ctx->eig_ev[g], hipEventDisableTiming) != hipSuccess)
+      return fail(ctx, DWH_ERR_HIP, "eigensolver event creation failed");
+  if (ng > 1) {
+    HIPCHECK(ctx, hipEventRecord(ctx->eig_ev[0], s));
+    for (int g = 1; g < ng; ++g) HIPCHECK(ctx, hipStreamWaitEvent(ctx->eig_sx[g - 1], ctx->eig_ev[0], 0));
+  }
+  const int64_t sDp = (int64_t)2 * dwh::kEigDeferMax * T, sGp = (int64_t)3 * dwh::kEigGP, sR = (int64_t)dwh::kEigRing * n;
   for (int i = 0; i < n; ++i) {
     if (ph.on && i % 512 == 0 && i > 0) ph.mark("tridiag/512");
-    dwh::launch_eig_column(A, n, i, sA, ctx->d_eig_part, sP, ctx->d_eig_pfin, ctx->d_eig_colfin, ctx->d_eig_vv,
-                           ctx->d_eig_ww, ctx->d_eig_d, ctx->d_eig_e, ctx->d_eig_tau, ctx->d_eig_dpart,
-                           ctx->d_eig_gpart, m, s);
+    for (int g = 0; g < ng; ++g) {
+      const int64_t k0 = (int64_t)m * g / ng;
+      const int mg = (int)((int64_t)m * (g + 1) / ng - k0);
+      dwh::launch_eig_column(A + k0 * sA, n, i, sA, ctx->d_eig_part + k0 * sP, sP, ctx->d_eig_pfin + k0 * n,
+                             ctx->d_eig_colfin + k0 * n, ctx->d_eig_vv + k0 * sR, ctx->d_eig_ww + k0 * sR,
+                             ctx->d_eig_d + k0 * n, ctx->d_eig_e + k0 * n, ctx->d_eig_tau + k0 * n,
+                             ctx->d_eig_dpart + k0 * sDp, ctx->d_eig_gpart + k0 * sGp, mg,
+                             g ? ctx->eig_sx[g - 1] : s);
+    }
+  }
+  for (int g = 1; g < ng; ++g) {
+    HIPCHECK(ctx, hipEventRecord(ctx->eig_ev[g], ctx->eig_sx[g - 1]));
+    HIPCHECK(ctx, hipStreamWaitEvent(s, ctx->eig_ev[g], 0));
   }
   ph.mark("tridiag");
   dwh::launch_eig_bisect(ctx->d_eig_d, ctx->d_eig_e, n, b.E, ctx->d_eig_tn, m, s);
@@ -2331,6 +2366,12 @@ int own_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m) {
   // U = (I - V_0 T_0 V_0^H) ... (I - V_last T_last V_last^H) Z, last block first,
   // on the library's own products (dwhmc_gemm.hip), columns j0.. only
   const double2 one = make_double2(1.0, 0.0), zero = make_double2(0.0, 0.0), mone = make_double2(-1.0, 0.0);
+  const int ks = m >= 4 ? 1 : KS;
+  const int64_t sWs = ks * sW;
+  // V^H block by block into the slots' Jmn buffers (free after the Löwdin step)
+  double2* Vt = b.Jmn;
+  const int ldv = std::min(NB, n - 1);   // as k_eig_vt lays the blocks out
+  dwh::launch_eig_vt(A, n, sA, Vt, m, s);
   for (int blk = nblk - 1; blk >= 0; --blk) {
     const int r0 = blk * NB, kb = std::min(NB, n - 1 - r0), ms = n - r0 - 1;
     const double2* Vb = A + (r0 + 1) + (int64_t)r0 * n;
@@ -2340,8 +2381,8 @@ int own_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m) {
     // chunk s at rows s kb of W: one launch for every (matrix, chunk)
     const int c = ks == 1 ? ms : std::max(16, ((ms + ks - 1) / ks + 15) / 16 * 16);
     const int nfull = ms / c, rem = ms - nfull * c, S = nfull + (rem > 0);
-    dwh::gemm_z_chunked('C', 'N', kb, M, c, rem > 0 ? rem : c, S, one, Vb, n, c, sA, Us, n, c, sA, zero,
-                        ctx->d_eig_W, ldw, kb, sWs, m, s);
+    dwh::gemm_z_chunked('N', 'N', kb, M, c, rem > 0 ? rem : c, S, one, Vt + (int64_t)r0 * n, ldv, (int64_t)c * ldv, sA,
+                        Us, n, c, sA, zero, ctx->d_eig_W, ldw, kb, sWs, m, s);
     dwh::launch_eig_tw(ctx->d_eig_T + (int64_t)blk * NB * NB, sT, ctx->d_eig_W, ldw, sWs, S, kb, M,
                        ctx->d_eig_W2, sW, m, s);
     dwh::gemm_z('N', 'N', ms, M, kb, mone, Vb, n, sA, ctx->d_eig_W2, NB, sW, one, Us, n, sA, m, s);
@@ -2630,6 +2671,10 @@ void dwh_destroy(dwh_ctx* ctx) {
   for (auto e : ctx->pool) (void)hipEventDestroy(e);
   if (ctx->blas) (void)rocblas_destroy_handle(ctx->blas);
   for (void* p : ctx->allocations) (void)hipFree(p);
+  for (hipEvent_t ev : ctx->eig_ev)
+    if (ev) (void)hipEventDestroy(ev);
+  for (hipStream_t st : ctx->eig_sx)
+    if (st) (void)hipStreamDestroy(st);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }

@@ -22,8 +22,9 @@
 //                   accumulates the tile's share of A v_i, partials written
 //                   once per slot and summed in a fixed order
 //                   (bit-reproducible).
-//  2. k_eig_bisect: every eigenvalue of T on Sturm counts, one wave per
-//     eigenvalue index, 64-section per round down to the last bit.
+//  2. k_eig_bisect: every eigenvalue of T on Sturm counts, 64 (one matrix)
+//     down to 4 (batches) lanes per eigenvalue index, a multisection per
+//     round down to the last bit.
 //  3. k_eig_invit: inverse iteration, T - lambda I = LU with partial pivoting
 //     streamed per thread (two solves from a fixed pseudo-random start,
 //     one thread per eigenvalue); k_eig_orth: the vectors of eigenvalue
@@ -754,14 +755,18 @@ __device__ void gersh(const double* __restrict__ d, const double* __restrict__ e
   }
 }
 
-// One wave per eigenvalue index j: 64-section of [lo, hi] per round (lane l
-// counts at lo + (l+1)(hi-lo)/65; the counts are monotone in l, so a ballot
-// finds the sub-interval holding eigenvalue j), ~9 rounds to the last bit
-// instead of ~53 bisection steps.  Sturm count: the dstebz recurrence with
-// d and e^2 broadcast from LDS and 1/q by v_rcp_f64 + one Newton step.
-constexpr int kBisW = 8;   // waves (eigenvalues) per workgroup
+// G lanes per eigenvalue index j (G | 64, 64 / G eigenvalues per wave): a
+// G-section of [lo, hi] per round (lane l of the group counts at
+// lo + (l+1)(hi-lo)/(G+1); the counts are monotone in l, so the group's bits
+// of a ballot find the sub-interval holding eigenvalue j), rounds to the last
+// bit.  G = 64 (~9 rounds) when few eigenvalues are asked for (the rounds are
+// the latency); batches use smaller groups, the same bits from fewer Sturm
+// counts (G x rounds per eigenvalue: 64 x 9 = 576, 4 x 23 = 92).  Sturm count:
+// the dstebz recurrence with d and e^2 broadcast from LDS and 1/q by
+// v_rcp_f64 + one Newton step.
+constexpr int kBisW = 8;   // waves per workgroup
 __global__ __launch_bounds__(64 * kBisW) void k_eig_bisect(const double* __restrict__ d,
-                                                           const double* __restrict__ e, int n,
+                                                           const double* __restrict__ e, int n, int lgG,
                                                            double* __restrict__ E, double* __restrict__ tnorm) {
   extern __shared__ double lds[];   // d[0, n), e^2[n, 2n)
   const int k = blockIdx.y, lane = threadIdx.x & 63;
@@ -781,15 +786,20 @@ __global__ __launch_bounds__(64 * kBisW) void k_eig_bisect(const double* __restr
   gl -= 2.0 * DBL_EPSILON * tn * n + 1e-300;
   gu += 2.0 * DBL_EPSILON * tn * n + 1e-300;
   const double pivmin = DBL_MIN * fmax(1.0, emax);
-  const int j = blockIdx.x * kBisW + (threadIdx.x >> 6);
-  if (j >= n) return;
+  const int G = 1 << lgG, g0 = lane & ~(G - 1), gi = lane & (G - 1);
+  const int j = ((blockIdx.x * kBisW + (threadIdx.x >> 6)) << (6 - lgG)) + (lane >> lgG);
+  if (((blockIdx.x * kBisW + (threadIdx.x >> 6)) << (6 - lgG)) >= n) return;   // whole wave idle
+  const unsigned long long gmask = G == 64 ? ~0ull : ((1ull << G) - 1);
   const double* ld = lds;
   const double* le2 = lds + n;
+  const double step = 1.0 / (G + 1);
   double lo = gl, hi = gu;
-  for (int it = 0; it < 64; ++it) {
+  bool done = j >= n;
+  for (int it = 0; it < 256; ++it) {
     const double mid = 0.5 * (lo + hi);
-    if (mid <= lo || mid >= hi) break;
-    const double x = fmin(lo + (lane + 1) * ((hi - lo) * (1.0 / 65.0)), hi);
+    if (mid <= lo || mid >= hi) done = true;
+    if (__ballot(!done) == 0) break;
+    const double x = fmin(lo + (gi + 1) * ((hi - lo) * step), hi);
     double q = ld[0] - x;
     if (fabs(q) < pivmin) q = -pivmin;
     int c = q < 0.0;
@@ -803,16 +813,18 @@ __global__ __launch_bounds__(64 * kBisW) void k_eig_bisect(const double* __restr
       if (fabs(q) < pivmin) q = -pivmin;
       c += q < 0.0;
     }
-    // first lane whose count exceeds j: eigenvalue j lies in (x_{f-1}, x_f]
-    const unsigned long long above = __ballot(c > j);
-    const int f = above ? __builtin_ctzll(above) : 64;
-    const double xf = __shfl(x, f < 64 ? f : 63, 64), xp = __shfl(x, f > 0 ? f - 1 : 0, 64);
-    const double nlo = f > 0 ? xp : lo, nhi = f < 64 ? xf : hi;
-    if (nlo == lo && nhi == hi) break;
-    lo = nlo;
-    hi = nhi;
+    // first lane of the group whose count exceeds j: eigenvalue j lies in (x_{f-1}, x_f]
+    const unsigned long long above = (__ballot(c > j) >> g0) & gmask;
+    const int f = above ? __builtin_ctzll(above) : G;
+    const double xf = __shfl(x, g0 + (f < G ? f : G - 1), 64), xp = __shfl(x, g0 + (f > 0 ? f - 1 : 0), 64);
+    const double nlo = f > 0 ? xp : lo, nhi = f < G ? xf : hi;
+    if (nlo == lo && nhi == hi) done = true;
+    if (!done) {
+      lo = nlo;
+      hi = nhi;
+    }
   }
-  if (lane == 0) E[j] = 0.5 * (lo + hi);
+  if (gi == 0 && j < n) E[j] = 0.5 * (lo + hi);
 }
 
 // start vector entry r of eigenvalue m: splitmix64 of (m, r) in [-1/2, 1/2)
@@ -1178,6 +1190,36 @@ __global__ __launch_bounds__(256) void k_eig_tfac(const double2* __restrict__ Gp
   }
 }
 
+// Vt: the reflector blocks conjugate-transposed, block b (columns b NB ..
+// b NB + kb - 1 of V, rows from b NB + 1) at Vt + b NB n as kb x (n - b NB - 1),
+// leading dimension ldv = min(NB, n - 1) (fits the n x n slot), so the
+// back-transform's W = V^H U is an 'N','N' product (1.7x faster than 'C','N'
+// on V in place: profiles/r05_exp_backtransform_vt.txt).  Block (x, b, k):
+// 32 rows of block b.
+__global__ __launch_bounds__(256) void k_eig_vt(const double2* __restrict__ A, int n, int64_t sA,
+                                                double2* __restrict__ Vt) {
+  __shared__ double2 tile[kEigNB][33];
+  const int b = blockIdx.y, k = blockIdx.z, r0 = b * kEigNB, rr0 = blockIdx.x * 32;
+  const int ms = n - r0 - 1, kb = min(kEigNB, n - 1 - r0), ldv = min(kEigNB, n - 1);
+  if (rr0 >= ms) return;
+  A += k * sA;
+  Vt += k * sA + (int64_t)r0 * n;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int idx = threadIdx.x + 256 * q, j = idx >> 5, r = idx & 31;
+    tile[j][r] = (j < kb && rr0 + r < ms) ? A[(r0 + 1 + rr0 + r) + (int64_t)(r0 + j) * n] : cz();
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int idx = threadIdx.x + 256 * q, r = idx >> 6, j = idx & 63;
+    if (rr0 + r < ms) {
+      const double2 v = tile[j][r];
+      if (j < ldv) Vt[j + (int64_t)(rr0 + r) * ldv] = make_double2(v.x, -v.y);
+    }
+  }
+}
+
 // W2 = T (sum over the S K-chunks of W): T kb x kb (ld kEigNB), chunk s of W
 // at rows s kb (ld ldw).  One workgroup per 16 columns: the chunk sums of its
 // columns (coalesced over the rows) and T staged in LDS, then 64 MACs per output.
@@ -1272,8 +1314,13 @@ void launch_eig_column(double2* A, int n, int i, int64_t sA, double2* part, int6
 }
 
 void launch_eig_bisect(const double* d, const double* e, int n, double* E, double* tnorm, int m, hipStream_t s) {
-  hipLaunchKernelGGL(k_eig_bisect, dim3((n + kBisW - 1) / kBisW, m), dim3(64 * kBisW), 2 * n * sizeof(double), s, d, e,
-                     n, E, tnorm);
+  // lanes per eigenvalue: 64 down to 4 as the batch grows, keeping >= ~2048
+  // waves (two per SIMD) in flight
+  int lgG = 6;
+  while (lgG > 2 && ((int64_t)m * n << (lgG - 1)) >= (int64_t)2048 * 64) --lgG;
+  const int per_wg = kBisW << (6 - lgG);
+  hipLaunchKernelGGL(k_eig_bisect, dim3((n + per_wg - 1) / per_wg, m), dim3(64 * kBisW), 2 * n * sizeof(double), s, d,
+                     e, n, lgG, E, tnorm);
 }
 
 void launch_eig_invit(const double* d, const double* e, int n, const double* E, const double* tnorm, double* Zt,
@@ -1304,6 +1351,12 @@ void launch_eig_tfac(const double2* V, int n, int64_t sA, const double2* tau, do
   if (nblk <= 0) return;
   hipLaunchKernelGGL(k_eig_tgram, dim3(nblk, kEigGS, m), dim3(256), 0, s, V, n, sA, Gp);
   hipLaunchKernelGGL(k_eig_tfac, dim3(nblk, m), dim3(256), 0, s, Gp, n, tau, Tb, sT);
+}
+
+void launch_eig_vt(const double2* A, int n, int64_t sA, double2* Vt, int m, hipStream_t s) {
+  const int nblk = (n - 1 + kEigNB - 1) / kEigNB;
+  if (nblk < 1) return;
+  hipLaunchKernelGGL(k_eig_vt, dim3((n - 1 + 31) / 32, nblk, m), dim3(256), 0, s, A, n, sA, Vt);
 }
 
 void launch_eig_tw(const double2* Tb, int64_t sT, const double2* W, int ldw, int64_t sW, int S, int kb, int n,

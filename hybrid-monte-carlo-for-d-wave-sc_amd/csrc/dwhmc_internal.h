@@ -246,6 +246,9 @@ struct TrGrid {
   double w0, d0, dw;
   int nw, nd;
 };
+// DOS eigenvalue slices (k_tr_dos partials: 2 x slices x nd doubles in the
+// σ partial buffer)
+int tr_dos_slices(int N);
 int tr_sigma_chunks(int N);   // rows of TrBufs::part (each nw long)
 // dense H_BdG of one chain into A (zeroed beforehand)
 void launch_tr_assemble(double2* A, int N, const int* hcol, const double* hval, const int* Dcol,
@@ -339,6 +342,9 @@ constexpr int kEigGS = 8;                   // row slices of each block's Gram s
 void launch_eig_tfac(const double2* V, int n, int64_t sA, const double2* tau, double2* Gp, double2* Tb, int64_t sT,
                      int m, hipStream_t s);
 // W2 (kb x n, ld kEigNB) = T (sum of the S row chunks of W, chunk s at rows s kb, ld ldw)
+// the reflector blocks of V conjugate-transposed (block b at Vt + b kEigNB n,
+// leading dimension kEigNB), for the back-transform's W = V^H U
+void launch_eig_vt(const double2* A, int n, int64_t sA, double2* Vt, int m, hipStream_t s);
 void launch_eig_tw(const double2* Tb, int64_t sT, const double2* W, int ldw, int64_t sW, int S, int kb, int n,
                    double2* W2, int64_t sW2, int m, hipStream_t s);
 

@@ -21,6 +21,7 @@ namespace {
 
 constexpr int kTB = 256;   // threads per block of every kernel here
 constexpr double kInvPi = 0.31830988618379067154;
+constexpr int kMaxDft = 1024;   // longest lattice side of the A(k, 0) DFT passes (twiddle table in LDS)
 
 // LogExpFunctions.logistic, overflow-safe (the fermi factor f_n = logistic(-βE_n))
 __device__ inline double logistic_d(double x) {
@@ -177,16 +178,18 @@ __device__ inline double grid_point(double start, double step, int k) {
 // -ΔE_nm, so the two add up to
 //     c_nm [1/a - 1/b] = c_nm · 4ω ΔE_nm / (a b),  a, b = (ω ∓ ΔE_nm)^2 + η^2,
 // and σ(ω) = π/N · (1/π) η/ω · Σ_{ordered} = 4η/N · Σ_{n<m} c_nm ΔE_nm / (a b):
-// half the pairs, one reciprocal per pair, and no 1/ω at small ω.  With E
+// half the pairs, one reciprocal per pair (v_rcp_f64 + one Newton step),
+// and no 1/ω at small ω.  With E
 // ascending, f_n - f_m vanishes (< 1e-12) for whole runs of m on either side
 // of the Fermi level; a 256-pair tile whose c are all zero is skipped.
 // Block (x, y): ω_k for k in the x tile, rows n in [y·rows, (y+1)·rows),
 // m > n read down column n of J_mn (|J_nm| = |J_mn|, J_mn Hermitian).
-__device__ inline double rcp_nr(double p) {
-  double r = __builtin_amdgcn_rcp(p);          // v_rcp_f64, then two Newton steps
-  r = fma(r, fma(-p, r, 1.0), r);
-  r = fma(r, fma(-p, r, 1.0), r);
-  return r;
+// one Newton step (<= ~11 ulp, the bisection's Sturm count uses the same): the
+// σ terms are positive-weighted sums, so a few-ulp relative error per term
+// is a few-ulp relative error of σ
+__device__ inline double rcp_nr1(double p) {
+  const double r = __builtin_amdgcn_rcp(p);
+  return fma(r, fma(-p, r, 1.0), r);
 }
 
 // ph (launch_tr_reduce): rows n < N only, m in (n, n2-1-n], the pairs
@@ -229,8 +232,8 @@ k_tr_sigma(const double2* __restrict__ Jmn, int n2, const double* __restrict__ E
         const double a1 = w - sdE[q + 1], b1 = w + sdE[q + 1];
         const double p0 = fma(a0, a0, eta2) * fma(b0, b0, eta2);
         const double p1 = fma(a1, a1, eta2) * fma(b1, b1, eta2);
-        acc0 = fma(scd[q], rcp_nr(p0), acc0);
-        acc1 = fma(scd[q + 1], rcp_nr(p1), acc1);
+        acc0 = fma(scd[q], rcp_nr1(p0), acc0);
+        acc1 = fma(scd[q + 1], rcp_nr1(p1), acc1);
       }
       __syncthreads();
     }
@@ -238,14 +241,21 @@ k_tr_sigma(const double2* __restrict__ Jmn, int n2, const double* __restrict__ E
   if (k < nw) part[(size_t)blockIdx.y * nw + k] = acc0 + acc1;
 }
 
-// σ(ω_k) = 4η/N Σ_chunks part
+// σ(ω_k) = 4η/N Σ_chunks part: 64 ω per block, wave q sums the chunks
+// [q nchunk/4, (q+1) nchunk/4), the four in wave order
 __global__ void k_tr_sigma_sum(const double* __restrict__ part, int nchunk, int nw, double eta, int N,
                                double* __restrict__ sigma) {
-  const int k = blockIdx.x * kTB + threadIdx.x;
-  if (k >= nw) return;
+  __shared__ double sh[4][64];
+  const int l = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int k = blockIdx.x * 64 + l;
   double s = 0;
-  for (int c = 0; c < nchunk; ++c) s += part[(size_t)c * nw + k];
-  sigma[k] = s * (4.0 * eta / N);
+  if (k < nw) {
+    const int c0 = nchunk * q / 4, c1 = nchunk * (q + 1) / 4;
+    for (int c = c0; c < c1; ++c) s += part[(size_t)c * nw + k];
+  }
+  sh[q][l] = s;
+  __syncthreads();
+  if (q == 0 && k < nw) sigma[k] = (((sh[0][l] + sh[1][l]) + sh[2][l]) + sh[3][l]) * (4.0 * eta / N);
 }
 
 // out[0] = stiffness = Σ dia / N - Σ lam / N; out[1] = dc = Σ dc / N
@@ -270,19 +280,35 @@ __global__ void k_tr_scalars(const double* __restrict__ dia, const double* __res
   }
 }
 
-// DOS and antinodal DOS on the grid -ω_max:Δω:ω_max (:446-490)
+// DOS and antinodal DOS on the grid -ω_max:Δω:ω_max (:446-490): slice y of
+// the eigenvalue range into part[y][k] (dos, dos_an interleaved), then the
+// slices in a fixed order (k_tr_dos_sum)
 __global__ void k_tr_dos(const double* __restrict__ E, const double* __restrict__ Wn,
-                         const double* __restrict__ wan, int n2, int N, double eta, double w_start,
-                         double w_step, int nd, double* __restrict__ dos, double* __restrict__ dos_an) {
+                         const double* __restrict__ wan, int n2, double eta, double w_start,
+                         double w_step, int nd, int per, double2* __restrict__ part) {
   const int k = blockIdx.x * kTB + threadIdx.x;
   if (k >= nd) return;
   const double w = grid_point(w_start, w_step, k), eta2 = eta * eta;
+  const int n0 = blockIdx.y * per, n1 = min(n0 + per, n2);
   double a = 0, b = 0;
-  for (int n = 0; n < n2; ++n) {
+  for (int n = n0; n < n1; ++n) {
     const double d = w - E[n];
     const double l = kInvPi * (eta / (d * d + eta2));
     a += Wn[n] * l;
     b += wan[n] * l;
+  }
+  part[(size_t)blockIdx.y * nd + k] = make_double2(a, b);
+}
+
+__global__ void k_tr_dos_sum(const double2* __restrict__ part, int nsl, int nd, int N, double* __restrict__ dos,
+                             double* __restrict__ dos_an) {
+  const int k = blockIdx.x * kTB + threadIdx.x;
+  if (k >= nd) return;
+  double a = 0, b = 0;
+  for (int c = 0; c < nsl; ++c) {
+    const double2 p = part[(size_t)c * nd + k];
+    a += p.x;
+    b += p.y;
   }
   dos[k] = a / N;
   dos_an[k] = b;
@@ -293,6 +319,9 @@ __global__ void k_tr_dos(const double* __restrict__ E, const double* __restrict_
 // T[kx + Lx y, n] = Σ_x u[x + Lx y, n] e^{-2πi kx x / Lx}
 __global__ void k_tr_dft_x(const double2* __restrict__ U, int n2, int Lx, int Ly,
                            double2* __restrict__ T) {
+  __shared__ double2 tw[kMaxDft];   // (cos, sin) of -2π q / Lx, computed once per block
+  for (int q = threadIdx.x; q < Lx; q += kTB) sincospi(-2.0 * (double)q / Lx, &tw[q].y, &tw[q].x);
+  __syncthreads();
   const int N = Lx * Ly;
   const int idx = blockIdx.x * kTB + threadIdx.x;
   if (idx >= N) return;
@@ -300,8 +329,8 @@ __global__ void k_tr_dft_x(const double2* __restrict__ U, int n2, int Lx, int Ly
   const double2* u = U + (size_t)n * n2 + (size_t)y * Lx;
   double2 acc = make_double2(0.0, 0.0);
   for (int x = 0; x < Lx; ++x) {
-    double s, c;
-    sincospi(-2.0 * (double)((kx * x) % Lx) / Lx, &s, &c);
+    const double2 t = tw[(kx * x) % Lx];
+    const double s = t.y, c = t.x;
     const double2 a = u[x];
     acc.x += a.x * c - a.y * s;
     acc.y += a.x * s + a.y * c;
@@ -312,6 +341,9 @@ __global__ void k_tr_dft_x(const double2* __restrict__ U, int n2, int Lx, int Ly
 // Pass y and weight: Pw[kx + Lx ky, n] = w0_n |Σ_y T[kx + Lx y, n] e^{-2πi ky y / Ly}|^2
 __global__ void k_tr_dft_y(const double2* __restrict__ T, const double* __restrict__ w0, int Lx,
                            int Ly, double* __restrict__ Pw) {
+  __shared__ double2 tw[kMaxDft];
+  for (int q = threadIdx.x; q < Ly; q += kTB) sincospi(-2.0 * (double)q / Ly, &tw[q].y, &tw[q].x);
+  __syncthreads();
   const int N = Lx * Ly;
   const int idx = blockIdx.x * kTB + threadIdx.x;
   if (idx >= N) return;
@@ -319,8 +351,8 @@ __global__ void k_tr_dft_y(const double2* __restrict__ T, const double* __restri
   const double2* tcol = T + (size_t)n * N + kx;
   double2 acc = make_double2(0.0, 0.0);
   for (int y = 0; y < Ly; ++y) {
-    double s, c;
-    sincospi(-2.0 * (double)((ky * y) % Ly) / Ly, &s, &c);
+    const double2 t = tw[(ky * y) % Ly];
+    const double s = t.y, c = t.x;
     const double2 a = tcol[(size_t)y * Lx];
     acc.x += a.x * c - a.y * s;
     acc.y += a.x * s + a.y * c;
@@ -448,6 +480,8 @@ void launch_tr_current(const double2* U, double2* JU, int N, const int* rowptr, 
 }
 
 int tr_sigma_chunks(int N) { return std::min(2 * N, 512); }
+constexpr int kDosPer = 128;   // eigenvalues per DOS slice
+int tr_dos_slices(int N) { return cdiv(2 * N, kDosPer); }
 
 void launch_tr_reduce(const TrBufs& b, int N, int Lx, int Ly, double beta, double eta,
                       const TrGrid& g, bool ph, hipStream_t s) {
@@ -460,14 +494,20 @@ void launch_tr_reduce(const TrBufs& b, int N, int Lx, int Ly, double beta, doubl
     const int used = cdiv(npair, rows);
     hipLaunchKernelGGL(k_tr_sigma, dim3(cdiv(g.nw, kTB), used), dim3(kTB), 0, s, b.Jmn, n2, b.E,
                        b.f, eta, g.w0, g.dw, g.nw, rows, npair, (int)ph, b.part);
-    hipLaunchKernelGGL(k_tr_sigma_sum, dim3(cdiv(g.nw, kTB)), dim3(kTB), 0, s, b.part, used, g.nw,
+    hipLaunchKernelGGL(k_tr_sigma_sum, dim3(cdiv(g.nw, 64)), dim3(256), 0, s, b.part, used, g.nw,
                        eta, N, b.sigma);
   }
   hipLaunchKernelGGL(k_tr_scalars, dim3(1), dim3(kTB), 0, s, b.dia, b.lam, b.dc, n2, N, npair, ph ? 2.0 : 1.0,
                      b.scalars);
-  if (g.nd > 0)
-    hipLaunchKernelGGL(k_tr_dos, dim3(cdiv(g.nd, kTB)), dim3(kTB), 0, s, b.E, b.Wn, b.wan, n2, N,
-                       eta, g.d0, g.dw, g.nd, b.dos, b.dos_an);
+  if (g.nd > 0) {
+    // eigenvalue slices of kDosPer (partials in the σ partial buffer, free
+    // again after k_tr_sigma_sum; sized for both)
+    const int pr = kDosPer, ns = tr_dos_slices(N);
+    double2* dp = reinterpret_cast<double2*>(b.part);
+    hipLaunchKernelGGL(k_tr_dos, dim3(cdiv(g.nd, kTB), ns), dim3(kTB), 0, s, b.E, b.Wn, b.wan, n2, eta, g.d0, g.dw,
+                       g.nd, pr, dp);
+    hipLaunchKernelGGL(k_tr_dos_sum, dim3(cdiv(g.nd, kTB)), dim3(kTB), 0, s, dp, ns, g.nd, N, b.dos, b.dos_an);
+  }
   // A(k, 0): T reuses JU, the weighted |FFT|^2 reuses J_mn (both no longer needed)
   hipLaunchKernelGGL(k_tr_dft_x, dim3(cdiv(N, kTB), n2), dim3(kTB), 0, s, b.U, n2, Lx, Ly, b.JU);
   double* Pw = reinterpret_cast<double*>(b.Jmn);

@@ -81,6 +81,16 @@ for step in "$@"; do
       timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -k "${PARITY_K:-factorize_matches or full_size or hmc_sweep_matches}" \
         --timeout 300 --timeout-method thread > "$O/parity.log" 2>&1 || { tail -40 "$O/parity.log"; exit 1; }
       tail -3 "$O/parity.log" ;;
+    tpar)
+      timeout -k 10 600 python -u -m pytest tests/test_transport.py tests/test_gpu_parity.py tests/test_simulation.py -m gpu -x -q \
+        -k "${TPAR_K:-eig or transport or eigensystem or measure}" --timeout 300 --timeout-method thread > "$O/tpar.log" 2>&1 \
+        || { tail -40 "$O/tpar.log"; exit 1; }
+      tail -3 "$O/tpar.log" ;;
+    tprof)
+      (export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/tprof" -o run -- \
+        python3 tools/transport_single.py 32 ${TP_K:-3} ${TP_S:-16} > "$O/tprof.txt" 2> "$O/tprof.err") \
+        || { tail -20 "$O/tprof.err"; exit 1; }
+      rm -f "$O/tprof/run_kernel_trace.csv"; cat "$O/tprof.txt" ;;
     trans)
       timeout -k 10 200 python -u tests/bench_transport.py --steps 3 --snapshots 4,8,16 > "$O/transport.json" \
         2> "$O/transport.err" || exit 1 ;;

@@ -1,5 +1,6 @@
 """K single-chain transport measurements at L x L (the bench_transport
-workload, m = 1) for profiling: python tools/transport_single.py [L] [K]."""
+workload, m = 1) for profiling: python tools/transport_single.py [L] [K] [S].
+S > 0: K calls of measure_transport_deltas over S Δ snapshots instead."""
 import os
 import sys
 import time
@@ -22,6 +23,18 @@ def main():
     ctx = m.FermionContext(p.Lx, p.Ly, p.t, p.tp, p.mu, p.beta, p.J, p.nn_table, p.nnn_table, st.disorder_pot,
                            lib_path=os.environ.get("DWHMC_LIB"))
     ctx.set_pairing(D)
+    S = int(sys.argv[3]) if len(sys.argv) > 3 else 0
+    if S > 0:
+        rng = np.random.default_rng(11)
+        Ds = np.stack([D + 0.01 * k * rng.standard_normal((p.N, 2)) for k in range(S)])
+        ctx.measure_transport_deltas(Ds, p.eta, p.domega, p.omega_max)
+        t0 = time.perf_counter()
+        for _ in range(K):
+            ctx.measure_transport_deltas(Ds, p.eta, p.domega, p.omega_max)
+        dt = (time.perf_counter() - t0) / K
+        print(f"L={L} {S} snapshots: {1e3 * dt:.2f} ms per call, {1e3 * dt / S:.2f} ms per measurement", flush=True)
+        ctx.close()
+        return
     ctx.measure_transport(p.eta, p.domega, p.omega_max)
     t0 = time.perf_counter()
     for _ in range(K):
