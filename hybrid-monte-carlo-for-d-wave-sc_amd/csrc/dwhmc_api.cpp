@@ -2383,8 +2383,12 @@ int own_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m) {
     const int nfull = ms / c, rem = ms - nfull * c, S = nfull + (rem > 0);
     dwh::gemm_z_chunked('N', 'N', kb, M, c, rem > 0 ? rem : c, S, one, Vt + (int64_t)r0 * n, ldv, (int64_t)c * ldv, sA,
                         Us, n, c, sA, zero, ctx->d_eig_W, ldw, kb, sWs, m, s);
-    dwh::launch_eig_tw(ctx->d_eig_T + (int64_t)blk * NB * NB, sT, ctx->d_eig_W, ldw, sWs, S, kb, M,
-                       ctx->d_eig_W2, sW, m, s);
+    if (S == 1)   // W2 = T W on the MFMA (4x faster than k_eig_tw's LDS MACs at 16 matrices)
+      dwh::gemm_z('N', 'N', kb, M, kb, one, ctx->d_eig_T + (int64_t)blk * NB * NB, NB, sT, ctx->d_eig_W, ldw, sWs,
+                  zero, ctx->d_eig_W2, NB, sW, m, s);
+    else
+      dwh::launch_eig_tw(ctx->d_eig_T + (int64_t)blk * NB * NB, sT, ctx->d_eig_W, ldw, sWs, S, kb, M,
+                         ctx->d_eig_W2, sW, m, s);
     dwh::gemm_z('N', 'N', ms, M, kb, mone, Vb, n, sA, ctx->d_eig_W2, NB, sW, one, Us, n, sA, m, s);
   }
   if (half) dwh::launch_eig_theta(b.U, n, sA, ctx->d_eig_c0, m, s);
@@ -2500,8 +2504,19 @@ int transport_run(dwh_ctx* ctx, const TrSrc& src, int m, double eta, double dome
   HIPCHECK(ctx, hipGetLastError());
   // J_mn = U^H (J ⊕ J) U  (src/Observables.jl:334-335), the library's own product
   const dwh::TrBufs& b0 = ctx->tr;
-  dwh::gemm_z('C', 'N', n2, ncol, n2, make_double2(1.0, 0.0), b0.U, n2, sA, b0.JU, n2, sA, make_double2(0.0, 0.0),
-              b0.Jmn, n2, sA, m, s);
+  const double2 one = make_double2(1.0, 0.0), zero = make_double2(0.0, 0.0);
+  if (ph) {
+    // only columns < N of J_mn: its columns [N, n2) hold U^H half by half
+    // (N x n2, ld N), so both products are 'N','N' (1.6x faster than the
+    // conjugate-transposed operand: profiles/r05_exp_backtransform_vt.txt)
+    double2* Ut = b0.Jmn + (int64_t)N * n2;
+    for (int h = 0; h < 2; ++h) {
+      dwh::launch_tr_conj_transpose(b0.U + (int64_t)h * N * n2, n2, N, n2, sA, Ut, N, sA, m, s);
+      dwh::gemm_z('N', 'N', N, ncol, n2, one, Ut, N, sA, b0.JU, n2, sA, zero, b0.Jmn + (int64_t)h * N, n2, sA, m, s);
+    }
+  } else {
+    dwh::gemm_z('C', 'N', n2, ncol, n2, one, b0.U, n2, sA, b0.JU, n2, sA, zero, b0.Jmn, n2, sA, m, s);
+  }
   HIPCHECK(ctx, hipGetLastError());
   const dwh::TrGrid g{eta, -omega_max, domega, (int)nw, (int)nd};
   for (int k = 0; k < m; ++k)

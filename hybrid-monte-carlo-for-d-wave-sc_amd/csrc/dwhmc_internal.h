@@ -248,6 +248,9 @@ struct TrGrid {
 };
 // DOS eigenvalue slices (k_tr_dos partials: 2 x slices x nd doubles in the
 // σ partial buffer)
+// out_k = in_k^H (in: R x C, ld lin; out: C x R, ld lout), k < m
+void launch_tr_conj_transpose(const double2* in, int R, int C, int lin, int64_t sin, double2* out, int lout,
+                              int64_t sout, int m, hipStream_t s);
 int tr_dos_slices(int N);
 int tr_sigma_chunks(int N);   // rows of TrBufs::part (each nw long)
 // dense H_BdG of one chain into A (zeroed beforehand)

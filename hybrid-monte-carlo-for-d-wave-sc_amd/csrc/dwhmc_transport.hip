@@ -203,7 +203,7 @@ k_tr_sigma(const double2* __restrict__ Jmn, int n2, const double* __restrict__ E
   const int tid = threadIdx.x;
   const int k = blockIdx.x * kTB + tid;
   const double w = grid_point(w_start, w_step, k < nw ? k : nw - 1);
-  const double eta2 = eta * eta;
+  const double eta2 = eta * eta, w4 = 4.0 * w;
   const int n0 = blockIdx.y * rows, n1 = min(n0 + rows, nrow);
   double acc0 = 0, acc1 = 0;
   for (int n = n0; n < n1; ++n) {
@@ -228,10 +228,12 @@ k_tr_sigma(const double2* __restrict__ Jmn, int n2, const double* __restrict__ E
       __syncthreads();
 #pragma unroll 4
       for (int q = 0; q < kTB; q += 2) {
-        const double a0 = w - sdE[q], b0 = w + sdE[q];
-        const double a1 = w - sdE[q + 1], b1 = w + sdE[q + 1];
-        const double p0 = fma(a0, a0, eta2) * fma(b0, b0, eta2);
-        const double p1 = fma(a1, a1, eta2) * fma(b1, b1, eta2);
+        // b = (ω+ΔE)^2 + η^2 = a + 4ωΔE (ΔE >= 0, ω > 0: no cancellation)
+        const double d0 = sdE[q], d1 = sdE[q + 1];
+        const double a0 = w - d0, a1 = w - d1;
+        const double e0 = fma(a0, a0, eta2), e1 = fma(a1, a1, eta2);
+        const double p0 = e0 * fma(w4, d0, e0);
+        const double p1 = e1 * fma(w4, d1, e1);
         acc0 = fma(scd[q], rcp_nr1(p0), acc0);
         acc1 = fma(scd[q + 1], rcp_nr1(p1), acc1);
       }
@@ -239,6 +241,31 @@ k_tr_sigma(const double2* __restrict__ Jmn, int n2, const double* __restrict__ E
     }
   }
   if (k < nw) part[(size_t)blockIdx.y * nw + k] = acc0 + acc1;
+}
+
+// out = in^H per matrix k (in: R x C, ld lin; out: C x R, ld lout), 32 x 32
+// tiles through LDS (both sides coalesced)
+__global__ void __launch_bounds__(kTB)
+k_tr_conj_transpose(const double2* __restrict__ in, int R, int C, int lin, int64_t sin,
+                    double2* __restrict__ out, int lout, int64_t sout) {
+  __shared__ double2 tile[32][33];
+  const int r0 = blockIdx.x * 32, c0 = blockIdx.y * 32, k = blockIdx.z;
+  in += k * sin;
+  out += k * sout;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int idx = threadIdx.x + kTB * q, c = idx >> 5, r = idx & 31;
+    if (r0 + r < R && c0 + c < C) tile[c][r] = in[(r0 + r) + (int64_t)(c0 + c) * lin];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int idx = threadIdx.x + kTB * q, r = idx >> 5, c = idx & 31;
+    if (r0 + r < R && c0 + c < C) {
+      const double2 v = tile[c][r];
+      out[(c0 + c) + (int64_t)(r0 + r) * lout] = make_double2(v.x, -v.y);
+    }
+  }
 }
 
 // σ(ω_k) = 4η/N Σ_chunks part: 64 ω per block, wave q sums the chunks
@@ -477,6 +504,13 @@ void launch_tr_current(const double2* U, double2* JU, int N, const int* rowptr, 
                        const double* val, int ncol, hipStream_t s) {
   hipLaunchKernelGGL(k_tr_current, dim3(cdiv(2 * N, kTB), ncol), dim3(kTB), 0, s, U, JU, 2 * N,
                      N, rowptr, col, val);
+}
+
+void launch_tr_conj_transpose(const double2* in, int R, int C, int lin, int64_t sin, double2* out, int lout,
+                              int64_t sout, int m, hipStream_t s) {
+  if (R <= 0 || C <= 0 || m <= 0) return;
+  hipLaunchKernelGGL(k_tr_conj_transpose, dim3(cdiv(R, 32), cdiv(C, 32), m), dim3(kTB), 0, s, in, R, C, lin, sin,
+                     out, lout, sout);
 }
 
 int tr_sigma_chunks(int N) { return std::min(2 * N, 512); }

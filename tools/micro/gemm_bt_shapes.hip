@@ -64,5 +64,27 @@ int main(int argc, char** argv) {
     }
     printf("U -= V W2  ms %4d     : N,N %8.1f us (%5.1f TF)\n", ms, 1e3 * tu, 6.0 * NB * M * (double)ms * batch / (tu * 1e-3) * 1e-12);
   }
+  // J_mn = U^H (J U): M = n, N = n / 2, K = n, 'C','N' vs 'N','N' on U^H (A as scratch)
+  for (int b2 : {batch}) {
+    float tcn = 0, tnn = 0;
+    for (int rep = 0; rep < 4; ++rep) {
+      float t;
+      CK(hipEventRecord(e0, 0));
+      dwh::gemm_z('C', 'N', n, M, n, one, U, n, sA, A, n, sA, zero, W, n, (int64_t)n * M, b2 > 8 ? 8 : b2, 0);
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      CK(hipEventElapsedTime(&t, e0, e1));
+      if (rep) tcn += t / 3;
+      CK(hipEventRecord(e0, 0));
+      dwh::gemm_z('N', 'N', n, M, n, one, U, n, sA, A, n, sA, zero, W, n, (int64_t)n * M, b2 > 8 ? 8 : b2, 0);
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      CK(hipEventElapsedTime(&t, e0, e1));
+      if (rep) tnn += t / 3;
+    }
+    const double fl = 6.0 * n * M * (double)n * (b2 > 8 ? 8 : b2);
+    printf("J_mn shape %d x %d x %d, batch %d: C,N %8.1f us (%5.1f TF)   N,N %8.1f us (%5.1f TF)\n", n, M, n,
+           b2 > 8 ? 8 : b2, 1e3 * tcn, fl / (tcn * 1e-3) * 1e-12, 1e3 * tnn, fl / (tnn * 1e-3) * 1e-12);
+  }
   return 0;
 }
