@@ -123,9 +123,16 @@ __global__ __launch_bounds__(256) void k_eig_reduce(const double2* __restrict__ 
   const bool rd = !eig_write_pass(i - 1, K);
   const int f = eig_pend_first(i - 1, K), np = rd ? i - 1 - f : 0;
   __shared__ double2 dots[2 * KD];
-  if (tid < 2 * np) {   // ascending tile order
+  if (tid < 2 * np) {   // ascending tile order, 16 loads in flight
     double2 s = cz();
-    for (int Y = t0; Y < T; ++Y) s = cadd(s, dpart[((int64_t)k * T + Y) * 2 * KD + tid]);
+    for (int Y0 = t0; Y0 < T; Y0 += 16) {
+      double2 q[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) q[u] = Y0 + u < T ? dpart[((int64_t)k * T + Y0 + u) * 2 * KD + tid] : cz();
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+        if (Y0 + u < T) s = cadd(s, q[u]);
+    }
     dots[tid] = s;
   }
   __syncthreads();
@@ -145,12 +152,24 @@ __global__ __launch_bounds__(256) void k_eig_reduce(const double2* __restrict__ 
         if (Y0 + u < T) s = cadd(s, q[u]);
     }
     double2 c = A[k * sA + r + (int64_t)i * n];
-    for (int q = 0; q < np; ++q) {
-      const int sl = (f + q) % kEigRing;
-      const double2 vj = vv[(int64_t)sl * n + r], wj = ww[(int64_t)sl * n + r];
-      s = csub(csub(s, cmul(vj, dots[2 * q])), cmul(wj, dots[2 * q + 1]));
-      const double2 vji = vv[(int64_t)sl * n + i], wji = ww[(int64_t)sl * n + i];
-      c = csub(csub(c, cmulc(vj, wji)), cmulc(wj, vji));
+    // the pending pairs' entries all loaded before the corrections (np < KD)
+    double2 vj[KD], wj[KD], vji[KD], wji[KD];
+#pragma unroll
+    for (int q = 0; q < KD; ++q) {
+      if (q < np) {
+        const int sl = (f + q) % kEigRing;
+        vj[q] = vv[(int64_t)sl * n + r];
+        wj[q] = ww[(int64_t)sl * n + r];
+        vji[q] = vv[(int64_t)sl * n + i];
+        wji[q] = ww[(int64_t)sl * n + i];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < KD; ++q) {
+      if (q < np) {
+        s = csub(csub(s, cmul(vj[q], dots[2 * q])), cmul(wj[q], dots[2 * q + 1]));
+        c = csub(csub(c, cmulc(vj[q], wji[q])), cmulc(wj[q], vji[q]));
+      }
     }
     pfin[(int64_t)k * n + r] = s;
     colfin[(int64_t)k * n + r] = c;
