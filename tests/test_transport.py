@@ -416,6 +416,33 @@ def test_transport_deltas_matches_per_state(dwhmc, oracle, Lx, Ly, ns):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("Lx,Ly,ns,streams", [(6, 4, 9, "1"), (8, 8, 12, "3")])
+def test_transport_deltas_sub_batch_streams(dwhmc, oracle, monkeypatch, Lx, Ly, ns, streams):
+    """Batches of 8+ matrices tridiagonalise as sub-batches on their own
+    streams (two by default; DWHMC_EIG_STREAMS sets the count): every
+    snapshot's result is bit-identical to the one-stream / three-stream run
+    (each matrix sees the same kernels and deferral depth) and equals the
+    oracle."""
+    O = oracle
+    p, dis, D0 = _case(O, Lx, Ly, 8.0, seed=900)
+    snaps = [_case(O, Lx, Ly, 8.0, seed=910 + k)[2] for k in range(ns)]
+    ctx = _ctx(dwhmc, p, dis)
+    ctx.set_pairing(D0)
+    monkeypatch.delenv("DWHMC_EIG_STREAMS", raising=False)
+    rs = ctx.measure_transport_deltas(np.stack(snaps), p.eta, p.domega, p.omega_max)
+    monkeypatch.setenv("DWHMC_EIG_STREAMS", streams)
+    ro = ctx.measure_transport_deltas(np.stack(snaps), p.eta, p.domega, p.omega_max)
+    ctx.close()
+    assert len(rs) == len(ro) == ns
+    for a, b in zip(rs, ro):
+        for k in a:
+            assert np.array_equal(np.asarray(a[k]), np.asarray(b[k])), k
+    for k in (0, ns // 2, ns - 1):
+        cache, _, _ = O.evaluate(p, dis, snaps[k])
+        _check_transport(rs[k], O.measure_transport_and_spectra(cache, p))
+
+
+@pytest.mark.gpu
 def test_transport_L32_properties(dwhmc, oracle):
     """BASELINE C3 size (N = 1024): device vs oracle at full size, plus the
     size-independent checks ∫DOS dω ≈ 1 on the grid and A(k,0) ≥ 0."""
