@@ -1276,13 +1276,25 @@ __global__ __launch_bounds__(256) void k_eig_tw(const double2* __restrict__ Tb, 
 // matrices on (HBM-bound passes), 1 below (latency-bound;
 // profiles/r04_exp_eig_defer_*.json)
 int eig_defer_k(int m) { return m < kEigDeferMin ? 1 : kEigDefer; }
+// first column of a batch's one-matrix-scheme tail: n - M rounded up to a
+// multiple of kEigDefer (column s-1 a write pass), M = DWHMC_EIG_SWITCH_M
+// (A/B; 0: no tail)
+int eig_switch_col(int n) {
+  static const int M = [] {
+    const char* v = std::getenv("DWHMC_EIG_SWITCH_M");
+    return v ? std::atoi(v) : kEigSwitchM;
+  }();
+  if (M <= 0) return n + 1;
+  const int s0 = std::max(kEigDefer, n - M);
+  return (s0 + kEigDefer - 1) / kEigDefer * kEigDefer;
+}
 
 void launch_eig_step(double2* A, int n, int i, int64_t sA, const double2* part, int64_t sP, double2* pfin,
                      double2* colfin, double2* vv, double2* ww, double* d, double* e, double2* tau,
-                     const double2* dpart, int m, hipStream_t s) {
+                     const double2* dpart, int m, int K, hipStream_t s) {
   if (i > 0)
     hipLaunchKernelGGL(k_eig_reduce, dim3((n - i + 255) / 256, m), dim3(256), 0, s, part, sP, n, i, pfin, A, sA,
-                       colfin, vv, ww, dpart, eig_defer_k(m), (const double2*)tau, (double2*)nullptr);
+                       colfin, vv, ww, dpart, K, (const double2*)tau, (double2*)nullptr);
   const int rs = (n - i + kStepT - 1) / kStepT;   // row slots the rows i..n-1 need
   static_assert(kEigMaxN <= 5 * kStepT, "k_eig_step instantiations");
 #define DWH_EIG_STEP(R) \
@@ -1298,10 +1310,9 @@ void launch_eig_step(double2* A, int n, int i, int64_t sA, const double2* part, 
 }
 
 void launch_eig_pass(double2* A, int n, int i, int64_t sA, double2* part, int64_t sP, const double2* vv,
-                     const double2* ww, double2* dpart, int m, hipStream_t s) {
+                     const double2* ww, double2* dpart, int m, int K, hipStream_t s) {
   const int T = (n + kEigTB - 1) / kEigTB, t0 = (i + 1) / kEigTB, nT = T - t0;
   if (nT <= 0) return;
-  const int K = eig_defer_k(m);
   if (K == 1)
     hipLaunchKernelGGL(k_eig_pass1, dim3(nT * (nT + 1) / 2, m), dim3(256), 0, s, A, n, i, sA, part, sP, vv, ww, t0);
   else
@@ -1315,10 +1326,15 @@ void launch_eig_pass(double2* A, int n, int i, int64_t sA, double2* part, int64_
 void launch_eig_column(double2* A, int n, int i, int64_t sA, double2* part, int64_t sP, double2* pfin,
                        double2* colfin, double2* vv, double2* ww, double* d, double* e, double2* tau,
                        double2* dpart, double2* gpart, int m, hipStream_t s) {
-  const int K = eig_defer_k(m);
   // Batches keep the step: folding it into the deferred pass measured slower,
   // every pass workgroup re-reading the column's vectors: 14.1 vs 13.2 ms per
-  // measurement at 16 snapshots (profiles/r04_exp_eig_fused_step.txt).
+  // measurement at 16 snapshots (profiles/r04_exp_eig_fused_step.txt) -- over
+  // the HBM-bound columns.  The last kEigSwitchM columns (small trailing
+  // triangles: the launches are the cost) run the one-matrix scheme instead
+  // (K = 1: reduce + the pass with the step folded in, two launches per column
+  // instead of three), switching after a write pass so no pair is pending.
+  int K = eig_defer_k(m);
+  if (K > 1 && i >= eig_switch_col(n)) K = 1;
   if (K == 1 && i >= 1 && i <= n - 2) {
     const int ngp = (n - i + 255) / 256;
     hipLaunchKernelGGL(k_eig_reduce, dim3(ngp, m), dim3(256), 0, s, part, sP, n, i, pfin, A, sA, colfin, vv, ww,
@@ -1328,8 +1344,8 @@ void launch_eig_column(double2* A, int n, int i, int64_t sA, double2* part, int6
                        colfin, gpart, ngp, d, e, tau, t0);
     return;
   }
-  launch_eig_step(A, n, i, sA, part, sP, pfin, colfin, vv, ww, d, e, tau, dpart, m, s);
-  if (i < n - 1) launch_eig_pass(A, n, i, sA, part, sP, vv, ww, dpart, m, s);
+  launch_eig_step(A, n, i, sA, part, sP, pfin, colfin, vv, ww, d, e, tau, dpart, m, K, s);
+  if (i < n - 1) launch_eig_pass(A, n, i, sA, part, sP, vv, ww, dpart, m, K, s);
 }
 
 void launch_eig_bisect(const double* d, const double* e, int n, double* E, double* tnorm, int m, hipStream_t s) {

@@ -304,6 +304,7 @@ constexpr int kEigMaxCluster = 64;          // longest such run (else *bad: vend
 // of kEigDeferMin+ matrices apply them every kEigDefer-th pass (at most
 // kEigDeferMax pending); v_j / w_j live in a ring of kEigRing slots per matrix
 constexpr int kEigDefer = 8;
+constexpr int kEigSwitchM = 512;   // trailing columns a batch runs in the one-matrix scheme (eig_switch_col)
 constexpr int kEigDeferMax = 8;
 constexpr int kEigRing = kEigDeferMax + 2;
 constexpr int kEigGP = (kEigMaxN + 255) / 256;   // k_eig_reduce workgroups per matrix (g partials)
@@ -315,14 +316,14 @@ constexpr int kEigGP = (kEigMaxN + 255) / 256;   // k_eig_reduce workgroups per 
 // pfin, colfin: n per matrix
 void launch_eig_step(double2* A, int n, int i, int64_t sA, const double2* part, int64_t sP, double2* pfin,
                      double2* colfin, double2* vv, double2* ww, double* d, double* e, double2* tau,
-                     const double2* dpart, int m, hipStream_t s);
+                     const double2* dpart, int m, int K, hipStream_t s);
 // step i + pass i (one matrix: folded into one pass launch); gpart: 3 kEigGP per matrix
 void launch_eig_column(double2* A, int n, int i, int64_t sA, double2* part, int64_t sP, double2* pfin,
                        double2* colfin, double2* vv, double2* ww, double* d, double* e, double2* tau,
                        double2* dpart, double2* gpart, int m, hipStream_t s);
 // the pending pairs on the trailing triangle (write passes) + hemv partials of v_i
 void launch_eig_pass(double2* A, int n, int i, int64_t sA, double2* part, int64_t sP, const double2* vv,
-                     const double2* ww, double2* dpart, int m, hipStream_t s);
+                     const double2* ww, double2* dpart, int m, int K, hipStream_t s);
 // eigenvalues ascending into E, ||T|| bound per matrix into tnorm
 void launch_eig_bisect(const double* d, const double* e, int n, double* E, double* tnorm, int m, hipStream_t s);
 // eigenvectors of T into Zt (Zt[r n + j]: component r of vector j), clusters orthonormalised;
