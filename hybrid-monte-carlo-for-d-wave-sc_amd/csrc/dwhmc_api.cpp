@@ -2272,6 +2272,7 @@ int own_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m) {
     for (int g = 1; g < ng; ++g) HIPCHECK(ctx, hipStreamWaitEvent(ctx->eig_sx[g - 1], ctx->eig_ev[0], 0));
   }
   const int64_t sDp = (int64_t)2 * dwh::kEigDeferMax * T, sGp = (int64_t)3 * dwh::kEigGP, sR = (int64_t)dwh::kEigRing * n;
+  const int sw = dwh::eig_switch_col(n);
   for (int i = 0; i < n; ++i) {
     if (ph.on && i % 512 == 0 && i > 0) ph.mark("tridiag/512");
     for (int g = 0; g < ng; ++g) {
@@ -2281,7 +2282,7 @@ int own_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m) {
                              ctx->d_eig_colfin + k0 * n, ctx->d_eig_vv + k0 * sR, ctx->d_eig_ww + k0 * sR,
                              ctx->d_eig_d + k0 * n, ctx->d_eig_e + k0 * n, ctx->d_eig_tau + k0 * n,
                              ctx->d_eig_dpart + k0 * sDp, ctx->d_eig_gpart + k0 * sGp, mg,
-                             g ? ctx->eig_sx[g - 1] : s);
+                             g ? ctx->eig_sx[g - 1] : s, sw);
     }
   }
   for (int g = 1; g < ng; ++g) {

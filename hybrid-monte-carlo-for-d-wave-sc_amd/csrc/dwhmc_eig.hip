@@ -1280,10 +1280,8 @@ int eig_defer_k(int m) { return m < kEigDeferMin ? 1 : kEigDefer; }
 // multiple of kEigDefer (column s-1 a write pass), M = DWHMC_EIG_SWITCH_M
 // (A/B; 0: no tail)
 int eig_switch_col(int n) {
-  static const int M = [] {
-    const char* v = std::getenv("DWHMC_EIG_SWITCH_M");
-    return v ? std::atoi(v) : kEigSwitchM;
-  }();
+  const char* v = std::getenv("DWHMC_EIG_SWITCH_M");   // read per solve (tests switch it)
+  const int M = v ? std::atoi(v) : kEigSwitchM;
   if (M <= 0) return n + 1;
   const int s0 = std::max(kEigDefer, n - M);
   return (s0 + kEigDefer - 1) / kEigDefer * kEigDefer;
@@ -1325,7 +1323,7 @@ void launch_eig_pass(double2* A, int n, int i, int64_t sA, double2* part, int64_
 // step i, then pass i.
 void launch_eig_column(double2* A, int n, int i, int64_t sA, double2* part, int64_t sP, double2* pfin,
                        double2* colfin, double2* vv, double2* ww, double* d, double* e, double2* tau,
-                       double2* dpart, double2* gpart, int m, hipStream_t s) {
+                       double2* dpart, double2* gpart, int m, hipStream_t s, int sw) {
   // Batches keep the step: folding it into the deferred pass measured slower,
   // every pass workgroup re-reading the column's vectors: 14.1 vs 13.2 ms per
   // measurement at 16 snapshots (profiles/r04_exp_eig_fused_step.txt) -- over
@@ -1334,7 +1332,7 @@ void launch_eig_column(double2* A, int n, int i, int64_t sA, double2* part, int6
   // (K = 1: reduce + the pass with the step folded in, two launches per column
   // instead of three), switching after a write pass so no pair is pending.
   int K = eig_defer_k(m);
-  if (K > 1 && i >= eig_switch_col(n)) K = 1;
+  if (K > 1 && i >= sw) K = 1;
   if (K == 1 && i >= 1 && i <= n - 2) {
     const int ngp = (n - i + 255) / 256;
     hipLaunchKernelGGL(k_eig_reduce, dim3(ngp, m), dim3(256), 0, s, part, sP, n, i, pfin, A, sA, colfin, vv, ww,

@@ -320,7 +320,11 @@ void launch_eig_step(double2* A, int n, int i, int64_t sA, const double2* part, 
 // step i + pass i (one matrix: folded into one pass launch); gpart: 3 kEigGP per matrix
 void launch_eig_column(double2* A, int n, int i, int64_t sA, double2* part, int64_t sP, double2* pfin,
                        double2* colfin, double2* vv, double2* ww, double* d, double* e, double2* tau,
-                       double2* dpart, double2* gpart, int m, hipStream_t s);
+                       double2* dpart, double2* gpart, int m, hipStream_t s, int sw);
+// first column a batch runs in the one-matrix scheme (eig_switch_col: the last
+// kEigSwitchM columns, DWHMC_EIG_SWITCH_M overrides, 0 = none), passed to
+// launch_eig_column as sw
+int eig_switch_col(int n);
 // the pending pairs on the trailing triangle (write passes) + hemv partials of v_i
 void launch_eig_pass(double2* A, int n, int i, int64_t sA, double2* part, int64_t sP, const double2* vv,
                      const double2* ww, double2* dpart, int m, int K, hipStream_t s);

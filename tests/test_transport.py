@@ -443,6 +443,27 @@ def test_transport_deltas_sub_batch_streams(dwhmc, oracle, monkeypatch, Lx, Ly, 
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("switch_m", ["0", "64", "512"])
+def test_transport_deferred_batch_switch(dwhmc, oracle, monkeypatch, switch_m):
+    """Batches of 4+ matrices tridiagonalise with the 8-deep deferral and run
+    their last DWHMC_EIG_SWITCH_M columns in the one-matrix scheme (0: the
+    deferral to the end, 64: a long deferred run then the switch, 512: at
+    n = 512 the switch after the first write pass) -- every setting equals the
+    oracle per snapshot."""
+    O = oracle
+    p, dis, D0 = _case(O, 16, 16, 8.0, seed=950)
+    snaps = [_case(O, 16, 16, 8.0, seed=960 + k)[2] for k in range(4)]
+    monkeypatch.setenv("DWHMC_EIG_SWITCH_M", switch_m)
+    ctx = _ctx(dwhmc, p, dis)
+    ctx.set_pairing(D0)
+    rs = ctx.measure_transport_deltas(np.stack(snaps), p.eta, p.domega, p.omega_max)
+    ctx.close()
+    for k in (0, 3):
+        cache, _, _ = O.evaluate(p, dis, snaps[k])
+        _check_transport(rs[k], O.measure_transport_and_spectra(cache, p))
+
+
+@pytest.mark.gpu
 def test_transport_L32_properties(dwhmc, oracle):
     """BASELINE C3 size (N = 1024): device vs oracle at full size, plus the
     size-independent checks ∫DOS dω ≈ 1 on the grid and A(k,0) ≥ 0."""
