@@ -68,6 +68,13 @@ def inv_kernels(bp: int, coarse: bool) -> str:
     return l0 + " + " + ("k_cr_inv32" if bp == 32 else f"k_cr_inv<{bp // 16}>")
 
 
+def survey_poles(P: int, beta: float) -> int:
+    """SURVEY.md §8(d)'s P(β): the distinct pole LUs, capped at 8/10/12/15
+    for β = 4/8/16/32 (min(actual, cap); no cap for other β)."""
+    cap = {4.0: 8, 8.0: 10, 16.0: 12, 32.0: 15}.get(float(beta))
+    return min(P, cap) if cap else P
+
+
 def profiled_kernel_us(kernel, L, beta, chains):
     """Mean duration (µs) and call count of `kernel` in the committed rocprofv3
     --stats summary of this exact workload's bench command, else (None, 0, None)."""
@@ -131,6 +138,28 @@ def measured_mfma(kernels, L, beta, chains):
             flops = sum(k["mfma_exec_flops_per_launch"] * k["launches_per_step"] for k in ks) / n
             return busy, flops, rec.get("attainable_tflops"), "profiles/" + os.path.basename(path)
     return None, None, None, None
+
+
+def measured_step_mfma(L, beta, chains):
+    """Executed MFMA flops per leapfrog step summed over EVERY kernel of the
+    committed SQ counter pass of this workload (block products, inversions,
+    side work; the sparse and bond kernels contribute zero), and the file."""
+    for path in MFMA_FILES:
+        try:
+            with open(path) as f:
+                rec = json.load(f)
+        except (OSError, ValueError):
+            continue
+        w = rec.get("workload", {})
+        if (w.get("L"), w.get("beta"), w.get("chains")) != (L, beta, chains):
+            continue
+        ks = rec.get("kernels", {})
+        if ks:
+            # (the sparse level-0 kernels' names come out empty in the counter pass)
+            per = {(k or "k_cr_sp_fwd+k_cr_sp_bwd"): v["mfma_exec_flops_per_launch"] * v["launches_per_step"]
+                   for k, v in ks.items()}
+            return sum(per.values()), per, "profiles/" + os.path.basename(path)
+    return None, None, None
 
 
 # BASELINE.json configs (SURVEY.md §8d); the headline line is C3.
@@ -403,12 +432,24 @@ def main(argv=None):
     ctx.synchronize()
     el = time.perf_counter() - t0
     gc.enable()
+    el_local = el
+    per_rank = None
     if dist is not None:
         import torch
         t = torch.tensor([el], dtype=torch.float64, device=tdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
         dist.barrier()
+        # each rank's own rate and thermalised Nt next to the max-time
+        # aggregate, so a straggler (or a rank whose chain settled at a longer
+        # trajectory) shows in the record
+        t = torch.tensor([float(rank), a.steps * a.chains / el_local, 1000.0 * el_local / a.steps, float(Nt)],
+                         dtype=torch.float64, device=tdev)
+        gl = [torch.zeros_like(t) for _ in range(world)] if rank == 0 else None
+        dist.gather(t, gl, dst=0)
+        if rank == 0:
+            per_rank = [{"rank": int(x[0]), "value": float(x[1]), "ms_per_step": float(x[2]), "Nt_final": int(x[3])}
+                        for x in torch.stack(gl).cpu().numpy()]
 
     acc, dH = ctx.sweep_results(w_sw, n_draws(timed))
     info = ctx.info
@@ -481,15 +522,23 @@ def main(argv=None):
             "acceptance": float(obs[0]), "mean_dH": float(obs[1]), "mean_exp_minus_dH": float(obs[2]),
             "algorithm": "block cyclic reduction" if cr else "dense Schur complement + Gauss-Jordan",
             "ref_equiv_tflops": leap * (40.0 / 3.0) * (2 * N) ** 3 / el / 1e12,
-            "dense_equiv_tflops": leap * P * 8.0 * N ** 3 / el / 1e12,
+            # W = P(β) · 8 n³ per step (zgetrf + zgetri of the
+            # n = 2N BdG matrix per distinct pole, P capped at 8/10/12/15 for
+            # β = 4/8/16/32) — a dense-LU count the CR path does not execute
+            "survey_W_tflops": leap * survey_poles(P, a.beta) * 8.0 * (2 * N) ** 3 / el / 1e12,
+            "survey_W_poles": survey_poles(P, a.beta),
+            # the N x N Schur complement of the dense path (DWH_ALGO_DENSE), P poles
+            "dense_schur_equiv_tflops": leap * P * 8.0 * N ** 3 / el / 1e12,
         }
         if distributed:
             rec["collectives"] = {"backend": dist.get_backend(), "device": tdev,
-                                  "ops": ["barrier", "all_reduce(max time)", "gather(observables)"]}
+                                  "ops": ["barrier", "all_reduce(max time)", "gather(per-rank rates)",
+                                          "gather(observables)"]}
+            rec["per_rank"] = per_rank
         if distributed and backend == "gloo":
             rec["rehearsal"] = f"gloo collectives, {world} ranks on {torch.cuda.device_count()} GPU(s): not a scaling measurement"
         if not cr:
-            rec["alg_tflops"] = rec["dense_equiv_tflops"]
+            rec["alg_tflops"] = rec["dense_schur_equiv_tflops"]
         if kern:
             ms, n, w = kern[dom]
             ach = w / n / (ms / n * 1e-3) / 1e12 if n and ms > 0 else None
@@ -558,27 +607,34 @@ def main(argv=None):
                 rf["attainable_peak"] = att
                 rf["hw_frac_of_attainable"] = xfl / dur / 1e12 / att if att else None
                 rf["mfma_source"] = msrc
+            if cr:
+                # the whole step in executed-MFMA terms: every MFMA kernel's SQ
+                # summary (not only the product family) over this run's time per step
+                sfl, sper, ssrc = measured_step_mfma(a.L, a.beta, a.chains)
+                if sfl is not None:
+                    rec["step_hw_frac"] = sfl / (ms_per_step * 1e-3) / 1e12 / PEAK_F64_TFLOPS
+                    rec["step_hw"] = {"mfma_exec_flops_per_step": sfl, "per_kernel": sper, "source": ssrc,
+                                      "what": "executed MFMA flops per step (SQ_VALU_MFMA_BUSY_CYCLES of every "
+                                              "kernel) / ms_per_step / peak"}
             rec[f"{dom}_ms_per_step"] = ms / replay_steps
             ms, n, w = kern["assemble"]
             if n and ms > 0:
                 akern = "k_cr_fill" if cr else "k_assemble"
-                ev_us = 1000.0 * ms / n
-                # the kernel's duration: rocprofv3's mean over the same command's
-                # launches (the profile's fills are these warm back-to-back
-                # launches plus one per trajectory); a HIP event pair around a
-                # 2-3 µs launch adds its own packet processing, so the event
-                # figure is kept beside it, not used for the rate
-                pr_us, pr_calls, pr_src = profiled_kernel_us(akern, a.L, a.beta, a.chains)
-                us = pr_us if pr_us else ev_us
+                us = 1000.0 * ms / n
                 gbs = w / n / (us * 1e-6) / 1e9
+                # this run's HIP-event figure is the rate; the committed rocprofv3
+                # mean of the same command (a HIP event pair around a 2-3 µs
+                # launch adds its own packet time) is reported beside it, named
+                pr_us, pr_calls, pr_src = profiled_kernel_us(akern, a.L, a.beta, a.chains)
                 rec["assembly"] = {"bound": "hbm", "kernel": akern,
                                    "achieved": gbs,
                                    "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS,
                                    "bytes_per_launch": w / n, "avg_launch_us": us,
-                                   "avg_source": (f"{pr_src} (rocprofv3 --stats mean over {pr_calls} launches)"
-                                                  if pr_us else "HIP events per launch"),
-                                   "event_avg_launch_us": ev_us,
+                                   "avg_source": "this run's HIP events per launch",
                                    "launches_timed": n,
+                                   "profiled_avg_launch_us": pr_us,
+                                   "profiled_source": (f"{pr_src} (rocprofv3 --stats mean over {pr_calls} launches, "
+                                                       "committed profile, not this run)" if pr_us else None),
                                    "what": f"{ASSEMBLY_REPS} back-to-back warm launches (dwh_bench_assembly) "
                                            "after the timed region"}
         if world == 1 and not a.no_c1 and a.L != PRESETS["C1"]["L"]:

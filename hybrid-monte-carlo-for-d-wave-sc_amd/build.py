@@ -17,8 +17,8 @@ LIB = os.path.join(PKG, "libdwhmc.so")
 SOURCES = [os.path.join(CSRC, "dwhmc_kernels.hip"), os.path.join(CSRC, "dwhmc_cr.hip"), os.path.join(CSRC, "dwhmc_cr_sparse.hip"),
            os.path.join(CSRC, "dwhmc_eig.hip"), os.path.join(CSRC, "dwhmc_gemm.hip"),
            os.path.join(CSRC, "dwhmc_transport.hip"), os.path.join(CSRC, "dwhmc_api.cpp")]
-# rocSOLVER (zheevd / zheev: opt-in via DWHMC_EIG_SOLVER for A/B runs, and the
-# re-solve of a non-finite result or an order above kEigMaxN) is the
+# rocSOLVER (zheevd for an order above kEigMaxN, zheev as the re-solve of a
+# non-finite result) is the
 # only vendor library the measurement path can call; every product runs on the
 # library's own MFMA kernel (dwhmc_gemm.hip).  rocBLAS is linked for the
 # rocsolver handle only.

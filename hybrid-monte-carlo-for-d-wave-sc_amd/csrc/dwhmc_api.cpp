@@ -2420,31 +2420,29 @@ int eigen_enqueue(dwh_ctx* ctx, const TrSrc& src, int m, bool qr) {
   return DWH_OK;
 }
 
-// eigen_enqueue with the divide-and-conquer zheevd, then a scan of E and U for
-// non-finite values: rocSOLVER's zheevd returns NaN eigenvectors for spectra
-// with exactly degenerate eigenvalues (the clean lattice, W = 0), so those
-// chains are decomposed again with the QR-iteration zheev (slower, robust).
-// Synchronises the stream.  DWHMC_EIG_SOLVER=ev: zheev from the start.
+// The library's own eigensolver for every order up to kEigMaxN; rocSOLVER only
+// beyond it (zheevd) and as the re-solve (QR-iteration zheev) of a solve that
+// left a non-finite value: rocSOLVER's zheevd returns NaN eigenvectors for
+// spectra with exactly degenerate eigenvalues (the clean lattice, W = 0).
+// Synchronises the stream.
 int eigen_solve(dwh_ctx* ctx, const TrSrc& src, int m) {
-  const char* es = std::getenv("DWHMC_EIG_SOLVER");
-  const bool qr = es && std::strcmp(es, "ev") == 0;
-  const bool evd = es && std::strcmp(es, "evd") == 0;
   int rc;
+  const int64_t n2 = 2 * (int64_t)ctx->d.N;
+  const bool own = n2 <= dwh::kEigMaxN;
+  ctx->eig_ph = false;
+  ctx->eig_ph_last = 0;   // dwh_info_t::eig_half describes this solve on every exit path
   HIPCHECK(ctx, hipMemsetAsync(ctx->d_tr_bad, 0, sizeof(int), ctx->stream));
-  if (!qr && !evd && 2 * ctx->d.N <= dwh::kEigMaxN) {
-    // default: the own solver (k_eig_orth flags an over-long cluster in
-    // d_tr_bad); rocSOLVER zheev only if it flagged or produced non-finite values
+  if (own) {
+    // the own solver (k_eig_orth flags an over-long cluster in d_tr_bad);
+    // rocSOLVER zheev only if it flagged or produced non-finite values
     HIPCHECK(ctx, hipMemsetAsync(ctx->d_tr_info, 0, m * sizeof(int), ctx->stream));
     Scope sc(ctx, T_EIG_OWN, m);
     rc = own_heev_enqueue(ctx, src, m);
   } else {
     Scope sc(ctx, T_EIG_VENDOR, m);
-    rc = eigen_enqueue(ctx, src, m, qr);
+    rc = eigen_enqueue(ctx, src, m, false);
   }
-  ctx->eig_ph = false;
-  if (rc || qr) return rc;
-  const int64_t n2 = 2 * (int64_t)ctx->d.N;
-  const bool own = !evd && n2 <= dwh::kEigMaxN;   // the own solver ran (see above)
+  if (rc) return rc;
   dwh::launch_nonfinite(ctx->tr.U, m * n2 * n2, ctx->tr.E, m * n2, ctx->d_tr_bad, ctx->stream);
   int bad = 0;
   HIPCHECK(ctx, hipMemcpyAsync(&bad, ctx->d_tr_bad, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));

@@ -341,13 +341,22 @@ __global__ void k_tr_dos_sum(const double2* __restrict__ part, int nsl, int nd, 
   dos_an[k] = b;
 }
 
+// (cos, sin) of -2π q / L: the twiddle the LDS tables hold, for sides above kMaxDft
+__device__ __forceinline__ double2 dft_twiddle(int q, int L) {
+  double2 t;
+  sincospi(-2.0 * (double)q / L, &t.y, &t.x);
+  return t;
+}
+
 // A(k, ω=0) (:492-516): FFT2 of every particle column u_n as an Lx x Ly image
 // (site i = x + Lx y), done as two direct DFT passes.  Pass x:
 // T[kx + Lx y, n] = Σ_x u[x + Lx y, n] e^{-2πi kx x / Lx}
 __global__ void k_tr_dft_x(const double2* __restrict__ U, int n2, int Lx, int Ly,
                            double2* __restrict__ T) {
   __shared__ double2 tw[kMaxDft];   // (cos, sin) of -2π q / Lx, computed once per block
-  for (int q = threadIdx.x; q < Lx; q += kTB) sincospi(-2.0 * (double)q / Lx, &tw[q].y, &tw[q].x);
+  const bool tab = Lx <= kMaxDft;    // longer sides: each twiddle by sincospi (no table)
+  if (tab)
+    for (int q = threadIdx.x; q < Lx; q += kTB) sincospi(-2.0 * (double)q / Lx, &tw[q].y, &tw[q].x);
   __syncthreads();
   const int N = Lx * Ly;
   const int idx = blockIdx.x * kTB + threadIdx.x;
@@ -356,7 +365,7 @@ __global__ void k_tr_dft_x(const double2* __restrict__ U, int n2, int Lx, int Ly
   const double2* u = U + (size_t)n * n2 + (size_t)y * Lx;
   double2 acc = make_double2(0.0, 0.0);
   for (int x = 0; x < Lx; ++x) {
-    const double2 t = tw[(kx * x) % Lx];
+    const double2 t = tab ? tw[(kx * x) % Lx] : dft_twiddle((kx * x) % Lx, Lx);
     const double s = t.y, c = t.x;
     const double2 a = u[x];
     acc.x += a.x * c - a.y * s;
@@ -369,7 +378,9 @@ __global__ void k_tr_dft_x(const double2* __restrict__ U, int n2, int Lx, int Ly
 __global__ void k_tr_dft_y(const double2* __restrict__ T, const double* __restrict__ w0, int Lx,
                            int Ly, double* __restrict__ Pw) {
   __shared__ double2 tw[kMaxDft];
-  for (int q = threadIdx.x; q < Ly; q += kTB) sincospi(-2.0 * (double)q / Ly, &tw[q].y, &tw[q].x);
+  const bool tab = Ly <= kMaxDft;
+  if (tab)
+    for (int q = threadIdx.x; q < Ly; q += kTB) sincospi(-2.0 * (double)q / Ly, &tw[q].y, &tw[q].x);
   __syncthreads();
   const int N = Lx * Ly;
   const int idx = blockIdx.x * kTB + threadIdx.x;
@@ -378,7 +389,7 @@ __global__ void k_tr_dft_y(const double2* __restrict__ T, const double* __restri
   const double2* tcol = T + (size_t)n * N + kx;
   double2 acc = make_double2(0.0, 0.0);
   for (int y = 0; y < Ly; ++y) {
-    const double2 t = tw[(ky * y) % Ly];
+    const double2 t = tab ? tw[(ky * y) % Ly] : dft_twiddle((ky * y) % Ly, Ly);
     const double s = t.y, c = t.x;
     const double2 a = tcol[(size_t)y * Lx];
     acc.x += a.x * c - a.y * s;

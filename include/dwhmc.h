@@ -219,9 +219,8 @@ int dwh_debug_cr_stamps(dwh_ctx* ctx, int32_t inv_stage, uint64_t* out, int64_t 
  * multisection on Sturm counts, inverse iteration with cluster
  * orthonormalisation (clusters of any length), blocked back-transform; the
  * plain products on the library's own MFMA kernel, dwhmc_gemm.hip);
- * DWHMC_EIG_SOLVER=evd / ev selects rocSOLVER zheevd / zheev instead (A/B),
- * and rocSOLVER zheev re-solves only a result with non-finite values or an
- * order above the own solver's 5120.
+ * rocSOLVER runs only for an order above the own solver's 5120 (zheevd) and
+ * as the re-solve (zheev) of a result with non-finite values.
  * E: 2N, ascending; U (nullable): 2N x 2N column-major, the eigenvector of
  * E[n] in column n (phases are the solver's). */
 int dwh_eigensystem(dwh_ctx* ctx, int64_t chain, double* E, dwh_c128* U);

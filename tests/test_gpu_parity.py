@@ -55,9 +55,12 @@ def test_mfma_f64_layout(dwhmc):
     assert dwhmc.selftest_mfma(0) == 0
 
 
+# (20, 6) and (36, 4): BP = 64 and 96 with even Ly >= 4, i.e. the default
+# sparse level 0 (on from BP = 64) in the fast sweep, ahead of the full-size
+# tests
 @pytest.mark.parametrize("Lx,Ly,beta", [(4, 4, 4.0), (6, 6, 8.0), (5, 7, 16.0), (8, 8, 16.0),
                                         (16, 16, 8.0), (16, 8, 16.0), (3, 3, 4.0), (2, 2, 4.0),
-                                        (2, 5, 8.0)])
+                                        (2, 5, 8.0), (20, 6, 8.0), (36, 4, 16.0)])
 def test_factorize_matches_oracle(dwhmc, oracle, Lx, Ly, beta, algo3):
     algo = algo3
     O = oracle
@@ -65,6 +68,8 @@ def test_factorize_matches_oracle(dwhmc, oracle, Lx, Ly, beta, algo3):
     cache, F_ref, Ef_ref = O.evaluate(p, dis, Delta)
     P_ref, _ = O.pairing_P(cache.U, cache.E_n, p)
     ctx = device_ctx(dwhmc, p, dis, algo)
+    if algo == "cr" and Lx in (20, 36):
+        assert ctx.info["block"] == {20: 64, 36: 96}[Lx]
     ctx.set_pairing(Delta)
     ctx.factorize()
     P = ctx.pairing()[0]

@@ -214,6 +214,41 @@ def test_own_eigensolver_L48(dwhmc, oracle):
 
 
 @pytest.mark.gpu
+def test_eigensystem_above_own_limit_vendor_route(dwhmc, oracle):
+    """The one size where rocSOLVER is the only route:
+    n = 2N = 5200 > kEigMaxN = 5120 (52 x 50) runs zheevd, counted by the
+    eig_vendor timer, and dwh_info_t::eig_half reports 0 for it (ADVICE r05).
+    Size-independent checks, no LAPACK solve of n = 5200 on the host: the
+    eigenvalues ascend, Σ E = tr H = 0 and Σ E² = ‖H‖_F² (1e-10 relative),
+    and for 96 eigenpairs spread over the spectrum ‖H u − E u‖ ≤ 1e-10
+    (1 + max|E|) and their Gram matrix is I within 1e-12."""
+    O, m = oracle, dwhmc
+    p, dis, D = _case(O, 52, 50, 16.0, seed=5250)
+    cache = O.initialize_cache(p)
+    O.init_static_H(cache, p, dis)
+    O.update_H_BdG(cache, p, D)
+    H = O.hermitian_from_upper(cache.H_base)
+    del cache
+    ctx = _ctx(m, p, dis)
+    ctx.set_pairing(D)
+    ctx.timing_enable(["eig_own", "eig_vendor"])
+    E, U = ctx.eigensystem(0)
+    own, vendor = ctx.timing_read("eig_own")[1], ctx.timing_read("eig_vendor")[1]
+    half = ctx.info["eig_half"]
+    ctx.close()
+    assert (own, vendor) == (0, 1) and half == 0
+    assert np.all(np.isfinite(E)) and np.all(np.isfinite(U))
+    assert np.all(np.diff(E) >= 0)
+    fro2 = float(np.sum(np.abs(H) ** 2))
+    assert abs(E.sum()) <= 1e-10 * np.sqrt(fro2) * len(E)
+    assert abs(np.sum(E ** 2) - fro2) <= 1e-10 * fro2
+    S = np.linspace(0, len(E) - 1, 96).astype(int)
+    res = np.max(np.abs(H @ U[:, S] - U[:, S] * E[S][None, :]))
+    assert res <= 1e-10 * (1 + np.max(np.abs(E))), res
+    assert np.max(np.abs(U[:, S].conj().T @ U[:, S] - np.eye(len(S)))) <= 1e-12
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("Lx,Ly,maxc", [(12, 10, "1"), (24, 24, "4")])
 def test_eigensolver_long_clusters(dwhmc, oracle, monkeypatch, Lx, Ly, maxc):
     """Clusters longer than k_eig_orth's one-workgroup limit are

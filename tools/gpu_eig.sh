@@ -1,8 +1,8 @@
 #!/bin/bash
 # Own-eigensolver pass (via gpurun): bash tools/gpu_eig.sh TAG [quick]
 # eigensolver tests, the transport + eig-path parity tests, transport timing
-# with the own solver and with rocSOLVER zheevd (DWHMC_EIG_SOLVER=evd), and a
-# kernel-trace profile of the L=32 measurement.
+# with the own solver, and a kernel-trace profile of the L=32 measurement.
+# (Round 6: the rocSOLVER A/B knob is gone; rocSOLVER runs only above n = 5120.)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:?tag}
@@ -19,9 +19,7 @@ timeout -k 10 600 python -u -m pytest tests/test_transport.py tests/test_gpu_par
 tail -3 "$O/tests.log"
 timeout -k 10 300 python -u tests/bench_transport.py --steps 3 --snapshots 4,8,16 > "$O/transport_own.json" \
   2> "$O/transport_own.err" || { tail -20 "$O/transport_own.err"; exit 1; }
-DWHMC_EIG_SOLVER=evd timeout -k 10 300 python -u tests/bench_transport.py --steps 3 --snapshots 4,8,16 \
-  > "$O/transport_evd.json" 2> "$O/transport_evd.err" || { tail -20 "$O/transport_evd.err"; exit 1; }
-cat "$O/transport_own.json" "$O/transport_evd.json"
+cat "$O/transport_own.json"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof" -o run -- \
   python3 "$R/tests/bench_transport.py" --steps 2 --snapshots "" --chains 1 > "$O/prof_bench.json" 2> "$O/prof.err" \
