@@ -106,6 +106,7 @@ struct CrStage {
                         // inversions: their side-work tasks in CrPlan::tasks (launch_cr_inv_side,
                         // maxt32 tiles each), flops in `flops`
   dwh::CrGemmCfg cfg;   // products: tile / K-split chosen once per context
+  int sfirst = 0, nswg = 0;   // 16 x 16 products: their dispatch-ordered slots (CrPlan::slots, nswg workgroups)
   int l0 = 0;           // inversions: level 0 from the static R = A^-1 blocks (k_cr_inv0)
   int sp = 0;           // kind 2 (sparse level-0 stage): 0 forward (CrPlan::sp_fwd), 1 backward (sp_bwd)
 };
@@ -115,6 +116,8 @@ struct CrPlan {
   std::vector<CrStage> stages;
   std::vector<dwh::CrTask> tasks;
   std::vector<dwh::CrTile> tiles16;          // per product stage: its 16 x 16 tiles with their operands
+  std::vector<dwh::CrSlot> slots;            // per 16 x 16 product stage: its tiles of every batch item,
+                                             // dispatch order (dwh::cr_gemm_slots; built with the stage configs)
   std::vector<int> inv_blk, inv_dst, inv_slot;   // inversion source / destination block, ln|det| slot
   std::vector<int> inv0_r;                       // level-0 inversions (l0 stage): R = A^-1 block per entry
   std::vector<int64_t> goff, doff;
@@ -889,7 +892,7 @@ struct dwh_ctx {
   CrPlan plan;
   double2* bpool = nullptr;   // CR block pool (nbatch x nblk blocks)
   dwh::CrTask* d_tasks = nullptr;
-  dwh::CrTile* d_tiles16 = nullptr;
+  dwh::CrSlot* d_slots = nullptr;
   dwh::CrSpFwd* d_sp_fwd = nullptr;
   dwh::CrSpBwd* d_sp_bwd = nullptr;
   SpTaskArrays sp_arr;   // the sparse stages' per-task operand arrays
@@ -1176,7 +1179,7 @@ void cr_enqueue(dwh_ctx* ctx) {
     } else {
       Scope s(ctx, T_CR_GEMM, st.flops * c.nbatch);
       dwh::launch_cr_gemm(c, ctx->bpool, ctx->d_tasks + st.first, st.n, st.maxt32, st.maxt16,
-                          ctx->d_tiles16 + st.tfirst, st.ntiles, st.cfg, st.sg, ctx->stream);
+                          ctx->d_slots + st.sfirst, st.nswg, st.cfg, st.sg, ctx->stream);
     }
   }
 }
@@ -1768,8 +1771,23 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
       const char* e32 = std::getenv("DWHMC_CR_INV32");
       c.inv32 = !(e32 && *e32 == '0');
       d.nld = Lyc;
-      for (CrStage& st : ctx->plan.stages)
-        if (st.kind == 1) st.cfg = dwh::cr_gemm_config(c, st.n, st.maxt32, st.maxt16, st.ntmax, st.ntiles);
+      if ((uint64_t)c.item >= (uint64_t)dwh::kCrNone) {
+        ctx->err = "CR pool: a batch item exceeds 2^32 elements (32-bit block-product offsets)";
+        g_create_error = ctx->err;
+        delete ctx;
+        return DWH_ERR_ARG;
+      }
+      CrPlan& pl = ctx->plan;
+      pl.slots.clear();
+      for (CrStage& st : pl.stages) {
+        if (st.kind != 1) continue;
+        st.cfg = dwh::cr_gemm_config(c, st.n, st.maxt32, st.maxt16, st.ntmax, st.ntiles);
+        if (st.cfg.ts != 16) continue;
+        st.nswg = dwh::cr_gemm_slot_wgs(c, st.ntiles, st.cfg);
+        st.sfirst = (int)pl.slots.size();
+        pl.slots.resize(pl.slots.size() + (size_t)st.nswg * (4 / st.cfg.ksplit));
+        dwh::cr_gemm_slots(c, pl.tiles16.data() + st.tfirst, st.ntiles, st.cfg, pl.slots.data() + st.sfirst);
+      }
       if (const char* e = std::getenv("DWHMC_CR_PLAN_DUMP"); e && *e == '1') {
         int i = 0;
         for (const CrStage& st : ctx->plan.stages) {
@@ -1821,7 +1839,7 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
     const CrPlan& pl = ctx->plan;
     ALLOC(bpool, (size_t)d.nbatch * ctx->cr.item);
     ALLOC(d_tasks, pl.tasks.size());
-    ALLOC(d_tiles16, pl.tiles16.size());
+    ALLOC(d_slots, pl.slots.size());
     ALLOC(d_sp_fwd, pl.sp_fwd.size());
     ALLOC(d_sp_bwd, pl.sp_bwd.size());
     if (!pl.colpat.empty()) {
@@ -1926,7 +1944,7 @@ int create_impl(dwh_ctx** out, int64_t Lx, int64_t Ly, double t, double tp, doub
   if (ctx->algo == ALGO_CR) {
     const CrPlan& pl = ctx->plan;
     UP(d_tasks, pl.tasks.data(), pl.tasks.size());
-    UP(d_tiles16, pl.tiles16.data(), pl.tiles16.size());
+    UP(d_slots, pl.slots.data(), pl.slots.size());
     UP(d_sp_fwd, pl.sp_fwd.data(), pl.sp_fwd.size());
     UP(d_sp_bwd, pl.sp_bwd.data(), pl.sp_bwd.size());
     UP(d_sp_row, ctx->sp_arr.row.data(), ctx->sp_arr.row.size());

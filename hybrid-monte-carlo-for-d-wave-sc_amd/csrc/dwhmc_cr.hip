@@ -983,11 +983,11 @@ __device__ __forceinline__ void cr_term(const double2* A, const double2* Bt, int
   }
 }
 
-// This wave's share of an output tile over all terms (the stage sign sg is
-// applied in the epilogue: negating every A fragment negates the sums exactly).
-// D: CrTile or CrTask (operand fields read through the uniform pointer: scalar loads)
-template <int BP, int MI, int KSPLIT, int KQ, int PFX = 0, typename D>
-__device__ __forceinline__ void cr_tile_part(const double2* base, const D* __restrict__ tk, int tr, int tc,
+// This wave's share of a 32 x 32 output tile of task tk over all its terms
+// (the stage sign sg is applied in the epilogue: negating every A fragment
+// negates the sums exactly); operand fields read through the uniform pointer
+template <int BP, int MI, int KSPLIT, int KQ, int PFX = 0>
+__device__ __forceinline__ void cr_tile_part(const double2* base, const CrTask* __restrict__ tk, int tr, int tc,
                                              d4 (&t1)[MI][MI], d4 (&t2)[MI][MI], d4 (&t3)[MI][MI]) {
   constexpr int TS = 16 * MI, HP = BP / 2;
   constexpr int64_t BB = (int64_t)HP * BP;
@@ -1005,114 +1005,33 @@ __device__ __forceinline__ void cr_tile_part(const double2* base, const D* __res
   }
 }
 
-// One workgroup's share of a product stage: workgroup slot g of the 1D
-// grid (already XCD-remapped by the caller) covers tiles g * TPW .. + TPW - 1.
-// TILESIGN: the sign of each tile comes from its descriptor (CrTile::neg;
-// side-work tile lists mix stages of both signs) instead of sg.  PFX: operand
-// prefetch depth in k-steps (0: the kGemmPf default).
-template <int BP, int MI, int KSPLIT, int PFX = 0, bool TILESIGN = false>
-__device__ __forceinline__ void cr_gemm_wg(double2* __restrict__ pool, int64_t item,
-                                           const CrTask* __restrict__ tasks, int ntasks, int maxt,
-                                           const CrTile* __restrict__ tlist, int ntl, int total,
-                                           double sg, int g) {
-  constexpr int TS = 16 * MI, TPW = 4 / KSPLIT, HP = BP / 2, NV = MI * MI * 4;
-  constexpr int64_t BB = (int64_t)HP * BP;
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
-  const int kq = w % KSPLIT;
-#ifdef CR_GEMM_STAMPS
-  const bool stamp = (total == g_gemm_sel);
-  GEMM_STAMP(0, stamp);
-  GEMM_STAMP(1, stamp);
-  if (stamp && threadIdx.x == 0 && blockIdx.x < 65536)
-    g_gemm_stamps[blockIdx.x][7] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
-#endif
-  const int gt = __builtin_amdgcn_readfirstlane(g * TPW + w / KSPLIT);
-  // 16 x 16 tiles: the stage's compact tile list, one 64-byte descriptor per
-  // tile (one scalar load, no idle waves for restricted tasks); 32 x 32
-  // tiles: ntasks x maxt slots of the task list
-  // launch_cr_gemm passes the tile list exactly for the 16 x 16 kernels
-  const int per_item = MI == 1 ? ntl : ntasks * maxt;
-  const int bi = gt / per_item;
-  const int rmd = gt - bi * per_item;
-  bool valid = gt < total;
-  const CrTile* tp = nullptr;
-  const CrTask* tk = nullptr;
-  int tr, tc, cin, out;
-  if constexpr (MI == 1) {
-    tp = tlist + (valid ? rmd : 0);
-    tr = tp->tr;
-    tc = tp->tc;
-    cin = tp->cin;
-    out = tp->out;
-    if constexpr (TILESIGN) sg = tp->neg ? -1.0 : 1.0;
-  } else {
-    const int tsk = rmd / maxt, tile = rmd - tsk * maxt;
-    tk = tasks + (valid ? tsk : 0);
-    if constexpr (TILESIGN) sg = (tk->bq & kCrNegBit) ? -1.0 : 1.0;
-    const int tr0 = tk->r0 / TS, tc0 = tk->c0 / TS;
-    const int ct = (tk->c1 + TS - 1) / TS - tc0;
-    const int rt = (tk->r1 + TS - 1) / TS - tr0;
-    valid = valid && tile < rt * ct;   // restricted task: fewer tiles than the stage maximum
-    tr = tr0 + (valid ? tile / ct : 0);
-    tc = tc0 + (valid ? tile % ct : 0);
-    cin = tk->cin;
-    out = tk->out;
-  }
-  double2* base = pool + (int64_t)(valid ? bi : 0) * item;
-  d4 t1[MI][MI], t2[MI][MI], t3[MI][MI];
-#pragma unroll
-  for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < MI; ++ni) {
-      t1[mi][ni] = d4{0.0, 0.0, 0.0, 0.0};
-      t2[mi][ni] = d4{0.0, 0.0, 0.0, 0.0};
-      t3[mi][ni] = d4{0.0, 0.0, 0.0, 0.0};
-    }
-#ifdef CR_GEMM_STAMPS
-  if (stamp) __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  GEMM_STAMP(2, stamp);
-#endif
-  double2* O = base + out * BB + (int64_t)(tr * TS + lk) * BP + tc * TS + lr;
-  const double2* C = cin >= 0 ? base + cin * BB + (int64_t)(tr * TS + lk) * BP + tc * TS + lr : nullptr;
-  // register slot v of this wave's output share <-> offset in the block
-  auto slot_off = [&](int v) -> int64_t {
-    const int mi = v / (MI * 4), ni = (v / 4) % MI, rr = v % 4;
-    return (int64_t)(mi * 16 + 4 * rr) * BP + ni * 16;
-  };
-  constexpr int NPF = NV / KSPLIT;   // slots this wave writes (v % KSPLIT == kq)
-  double2 cpf[NPF];
-#pragma unroll
-  for (int i = 0; i < NPF; ++i) cpf[i] = make_double2(0.0, 0.0);
-  // the accumulate input is loaded at tile start (its latency overlaps the operand loads)
-  if (C && valid) {
-#pragma unroll
-    for (int i = 0; i < NPF; ++i) cpf[i] = C[slot_off(i * KSPLIT + kq)];
-  }
-  auto run = [&](auto kqc) {
-    constexpr int KQ = decltype(kqc)::value;
-    if constexpr (MI == 1) cr_tile_part<BP, MI, KSPLIT, KQ, PFX>(base, tp, tr, tc, t1, t2, t3);
-    else cr_tile_part<BP, MI, KSPLIT, KQ, PFX>(base, tk, tr, tc, t1, t2, t3);
-  };
-  if (valid) {
-    if (KSPLIT == 1 || kq == 0) run(std::integral_constant<int, 0>{});
-    if constexpr (KSPLIT >= 2) {
-      if (kq == 1) run(std::integral_constant<int, 1>{});
-    }
-    if constexpr (KSPLIT == 4) {
-      if (kq == 2) run(std::integral_constant<int, 2>{});
-      if (kq == 3) run(std::integral_constant<int, 3>{});
-    }
-  }
+// register slot v = (mi MI + ni) 4 + rr of a wave's TS x TS output share <->
+// element offset from the lane's own output element
+template <int BP, int MI>
+__device__ __forceinline__ int64_t cr_slot_off(int v) {
+  const int mi = v / (MI * 4), ni = (v / 4) % MI, rr = v % 4;
+  return (int64_t)(mi * 16 + 4 * rr) * BP + ni * 16;
+}
+
+// Epilogue of both descriptor forms: out = [C] + sg (t1 - t2, t3 - t1 - t2)
+// at O (the lane's first output element; C likewise, cpf its values loaded at
+// tile start).  KSPLIT > 1: the waves of a tile sum their partials through LDS
+// (every wave of the workgroup reaches the barrier, valid or not).
+template <int BP, int MI, int KSPLIT>
+__device__ __forceinline__ void cr_tile_store(d4 (&t1)[MI][MI], d4 (&t2)[MI][MI], d4 (&t3)[MI][MI], double sg,
+                                              double2* O, bool hasc, const double2 (&cpf)[MI * MI * 4 / KSPLIT],
+                                              bool valid, [[maybe_unused]] bool stamp = false) {
+  constexpr int NV = MI * MI * 4;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, kq = w % KSPLIT;
   auto put = [&](int v, double2 x) {
-    const int64_t o = slot_off(v);
-    if (C) {
+    if (hasc) {
       const double2 c = cpf[v / KSPLIT];
       x.x += c.x;
       x.y += c.y;
     }
-    O[o] = x;
+    O[cr_slot_off<BP, MI>(v)] = x;
   };
-  // complex partial of register slot v = (mi * MI + ni) * 4 + rr
+  // complex partial of register slot v
   auto partial = [&](int v) {
     const int mi = v / (MI * 4), ni = (v / 4) % MI, rr = v % 4;
     const double a = t1[mi][ni][rr], b = t2[mi][ni][rr], c = t3[mi][ni][rr];
@@ -1152,23 +1071,167 @@ __device__ __forceinline__ void cr_gemm_wg(double2* __restrict__ pool, int64_t i
       }
       put(v, x);
     }
-#ifdef CR_GEMM_STAMPS
-    if (stamp) __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    GEMM_STAMP(5, stamp);
-    GEMM_STAMP(6, stamp);
-#endif
   }
+}
+
+// The accumulate input of the lane's slots (v % KSPLIT == kq), loaded at
+// tile start so its latency overlaps the operand loads
+template <int BP, int MI, int KSPLIT>
+__device__ __forceinline__ void cr_tile_cin(const double2* C, double2 (&cpf)[MI * MI * 4 / KSPLIT]) {
+  const int kq = (threadIdx.x >> 6) % KSPLIT;
+#pragma unroll
+  for (int i = 0; i < MI * MI * 4 / KSPLIT; ++i) cpf[i] = C[cr_slot_off<BP, MI>(i * KSPLIT + kq)];
+}
+
+// One workgroup's share of a 32 x 32 product stage (task list; side work of
+// the inversion launches and the DWHMC_CR_GEMM=32 A/B configurations):
+// workgroup slot g of the 1D grid (already XCD-remapped by the caller) covers
+// tiles g * TPW .. + TPW - 1 of ntasks x maxt task slots per batch item.
+// TILESIGN: each task's sign from its descriptor (kCrNegBit; side-work task
+// lists mix stages of both signs) instead of sg.  PFX: operand prefetch depth
+// in k-steps (0: the default).
+template <int BP, int MI, int KSPLIT, int PFX = 0, bool TILESIGN = false>
+__device__ __forceinline__ void cr_gemm_wg(double2* __restrict__ pool, int64_t item,
+                                           const CrTask* __restrict__ tasks, int ntasks, int maxt, int total,
+                                           double sg, int g) {
+  static_assert(MI == 2, "16 x 16 stages run k_cr_gemm16 (dispatch-ordered slots)");
+  constexpr int TS = 16 * MI, TPW = 4 / KSPLIT, HP = BP / 2, NV = MI * MI * 4;
+  constexpr int64_t BB = (int64_t)HP * BP;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  const int kq = w % KSPLIT;
+  const int gt = __builtin_amdgcn_readfirstlane(g * TPW + w / KSPLIT);
+  const int per_item = ntasks * maxt;
+  const int bi = gt / per_item;
+  const int rmd = gt - bi * per_item;
+  bool valid = gt < total;
+  const int tsk = rmd / maxt, tile = rmd - tsk * maxt;
+  const CrTask* tk = tasks + (valid ? tsk : 0);
+  if constexpr (TILESIGN) sg = (tk->bq & kCrNegBit) ? -1.0 : 1.0;
+  const int tr0 = tk->r0 / TS, tc0 = tk->c0 / TS;
+  const int ct = (tk->c1 + TS - 1) / TS - tc0;
+  const int rt = (tk->r1 + TS - 1) / TS - tr0;
+  valid = valid && tile < rt * ct;   // restricted task: fewer tiles than the stage maximum
+  const int tr = tr0 + (valid ? tile / ct : 0);
+  const int tc = tc0 + (valid ? tile % ct : 0);
+  const int cin = tk->cin, out = tk->out;
+  double2* base = pool + (int64_t)(valid ? bi : 0) * item;
+  d4 t1[MI][MI], t2[MI][MI], t3[MI][MI];
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < MI; ++ni) {
+      t1[mi][ni] = d4{0.0, 0.0, 0.0, 0.0};
+      t2[mi][ni] = d4{0.0, 0.0, 0.0, 0.0};
+      t3[mi][ni] = d4{0.0, 0.0, 0.0, 0.0};
+    }
+  double2* O = base + out * BB + (int64_t)(tr * TS + lk) * BP + tc * TS + lr;
+  const bool hasc = cin >= 0;
+  double2 cpf[NV / KSPLIT];
+#pragma unroll
+  for (int i = 0; i < NV / KSPLIT; ++i) cpf[i] = make_double2(0.0, 0.0);
+  if (hasc && valid) cr_tile_cin<BP, MI, KSPLIT>(base + cin * BB + (int64_t)(tr * TS + lk) * BP + tc * TS + lr, cpf);
+  auto run = [&](auto kqc) {
+    constexpr int KQ = decltype(kqc)::value;
+    cr_tile_part<BP, MI, KSPLIT, KQ, PFX>(base, tk, tr, tc, t1, t2, t3);
+  };
+  if (valid) {
+    if (KSPLIT == 1 || kq == 0) run(std::integral_constant<int, 0>{});
+    if constexpr (KSPLIT >= 2) {
+      if (kq == 1) run(std::integral_constant<int, 1>{});
+    }
+  }
+  cr_tile_store<BP, MI, KSPLIT>(t1, t2, t3, sg, O, hasc, cpf, valid);
 }
 
 // Argument order: what the first loads need leads (the build preloads the
 // leading kernel-argument dwords into SGPRs, build.py), and the grid size is
 // an argument (gridDim is a hidden argument, read by an s_load)
 template <int BP, int MI, int KSPLIT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MI == 1 ? kGemmWaves : 2))) void k_cr_gemm(double2* __restrict__ pool, int64_t item,
-                                                 const CrTile* __restrict__ tlist, int ntl, int total,
-                                                 double sg, int nwg, int ntasks, int maxt,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_cr_gemm(double2* __restrict__ pool, int64_t item,
+                                                 int total, double sg, int nwg, int ntasks, int maxt,
                                                  const CrTask* __restrict__ tasks) {
-  cr_gemm_wg<BP, MI, KSPLIT>(pool, item, tasks, ntasks, maxt, tlist, ntl, total, sg, xcd_remap(blockIdx.x, nwg));
+  cr_gemm_wg<BP, MI, KSPLIT>(pool, item, tasks, ntasks, maxt, total, sg, xcd_remap(blockIdx.x, nwg));
+}
+
+// 16 x 16 output tiles from dispatch-ordered slots (CrSlot: the host did the
+// XCD remap, the batch-item split and every block / tile address): wave w
+// of workgroup b takes slot b * TPW + w / KSPLIT with one 64-byte scalar load
+// and issues its operand loads right after it.  Empty slots (out == kCrNone)
+// pad the last workgroup.
+template <int BP, int KSPLIT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kGemmWaves))) void k_cr_gemm16(
+    double2* __restrict__ pool, const CrSlot* __restrict__ slots, double sg) {
+  constexpr int TPW = 4 / KSPLIT, NV = 4;
+  // the wave index as a scalar: the K-quarter dispatch below branches on SCC
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+  const int kq = w % KSPLIT;
+#ifdef CR_GEMM_STAMPS
+  const bool g_gemm_on = (int)(gridDim.x * TPW) == g_gemm_sel;
+  GEMM_STAMP(0, g_gemm_on);
+  GEMM_STAMP(1, g_gemm_on);
+  if (g_gemm_on && threadIdx.x == 0 && blockIdx.x < 65536)
+    g_gemm_stamps[blockIdx.x][7] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
+#endif
+  // the whole slot in one s_load_dwordx16 (CrSlot field order: base lo / hi,
+  // out, cin, nt, smask, a[4], b[4], rot)
+  typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+  const u32x16 d = *reinterpret_cast<const u32x16*>(slots + (blockIdx.x * TPW + w / KSPLIT));
+  const uint32_t out = d[2], cin = d[3];
+  const bool valid = out != kCrNone;
+  double2* base = pool + (((uint64_t)d[1] << 32) | d[0]);
+  d4 t1[1][1], t2[1][1], t3[1][1];
+  t1[0][0] = d4{0.0, 0.0, 0.0, 0.0};
+  t2[0][0] = d4{0.0, 0.0, 0.0, 0.0};
+  t3[0][0] = d4{0.0, 0.0, 0.0, 0.0};
+#ifdef CR_GEMM_STAMPS
+  if (g_gemm_on) __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  GEMM_STAMP(2, g_gemm_on);
+#endif
+  const int lo = lk * BP + lr;   // the lane's first output element in a tile
+  const bool hasc = cin != kCrNone;
+  double2 cpf[NV / KSPLIT];
+#pragma unroll
+  for (int i = 0; i < NV / KSPLIT; ++i) cpf[i] = make_double2(0.0, 0.0);
+  if (hasc && valid) cr_tile_cin<BP, 1, KSPLIT>(base + cin + lo, cpf);
+  auto run = [&](auto kqc) {
+    constexpr int KQ = decltype(kqc)::value;
+    const int nt = (int)d[4], rot = (int)d[14];
+    // the terms' operands rotate through scalar registers (a dynamic index
+    // into the slot would be lowered to VGPR-indexed moves)
+    uint32_t a0 = d[6], a1 = d[7], a2 = d[8], a3 = d[9], b0 = d[10], b1 = d[11], b2 = d[12], b3 = d[13];
+    unsigned sm = d[5];
+#pragma unroll 1
+    for (int h = 0; h < nt; ++h) {
+      cr_term<BP, 1, KSPLIT, KQ>(base + a0 + (lr * BP + lk), base + b0 + lo, 0, rot, (sm & 1u) << 31, t1, t2, t3);
+      a0 = a1;
+      a1 = a2;
+      a2 = a3;
+      b0 = b1;
+      b1 = b2;
+      b2 = b3;
+      sm >>= 1;
+    }
+  };
+  if (valid) {
+    if (KSPLIT == 1 || kq == 0) run(std::integral_constant<int, 0>{});
+    if constexpr (KSPLIT >= 2) {
+      if (kq == 1) run(std::integral_constant<int, 1>{});
+    }
+    if constexpr (KSPLIT == 4) {
+      if (kq == 2) run(std::integral_constant<int, 2>{});
+      if (kq == 3) run(std::integral_constant<int, 3>{});
+    }
+  }
+#ifdef CR_GEMM_STAMPS
+  cr_tile_store<BP, 1, KSPLIT>(t1, t2, t3, sg, base + out + lo, hasc, cpf, valid, g_gemm_on);
+#else
+  cr_tile_store<BP, 1, KSPLIT>(t1, t2, t3, sg, base + out + lo, hasc, cpf, valid);
+#endif
+#ifdef CR_GEMM_STAMPS
+  if (g_gemm_on) __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  GEMM_STAMP(5, g_gemm_on);
+  GEMM_STAMP(6, g_gemm_on);
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -1215,8 +1278,7 @@ __global__ __launch_bounds__(64 * NT) void k_cr_inv_side(double2* __restrict__ p
     CR_STAMP_AT(31, 3ull);
     return;
   }
-  cr_gemm_wg<16 * NT, 2, 1, 0, true>(pool, item, stasks, nst, maxt, nullptr, 0, total, 1.0,
-                                    xcd_remap(b - nall, nside));
+  cr_gemm_wg<16 * NT, 2, 1, 0, true>(pool, item, stasks, nst, maxt, total, 1.0, xcd_remap(b - nall, nside));
 #ifdef CR_STAMPS
   if (stamp_on) __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
@@ -1451,27 +1513,81 @@ CrGemmCfg cr_gemm_config(const CrDims& c, int ntasks, int maxt32, int maxt16, in
   return CrGemmCfg{16, T >= 2048 ? 1 : 4};
 }
 
-void launch_cr_gemm(const CrDims& c, double2* pool, const CrTask* tasks, int ntasks, int maxt32,
-                    int maxt16, const CrTile* tl16, int ntl16, const CrGemmCfg& cfg, double sg,
-                    hipStream_t s) {
-  if (ntasks <= 0) return;
-  const int maxt = cfg.ts == 32 ? maxt32 : maxt16;
-  const CrTile* tl = cfg.ts == 32 ? nullptr : tl16;
-  const int total = c.nbatch * (tl ? ntl16 : ntasks * maxt);
+// host twin of xcd_remap (dwhmc_device.h)
+static int xcd_remap_host(int orig, int total) {
+  const int q = total / 8, r = total % 8, xcd = orig % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+
+int cr_gemm_slot_wgs(const CrDims& c, int ntl16, const CrGemmCfg& cfg) {
   const int tpw = 4 / cfg.ksplit;
-  const dim3 g((total + tpw - 1) / tpw), b(256);
-#define CR_GEMM(BPV, MIV, KSV) \
-  hipLaunchKernelGGL((k_cr_gemm<BPV, MIV, KSV>), g, b, 0, s, pool, c.item, tl, ntl16, total, sg, (int)g.x, \
-                     ntasks, maxt, tasks)
-#define CR_GEMM_BP(BPV)                        \
-  if (cfg.ts == 16) {                          \
-    if (cfg.ksplit == 4) CR_GEMM(BPV, 1, 4);   \
-    else if (cfg.ksplit == 2) CR_GEMM(BPV, 1, 2); \
-    else CR_GEMM(BPV, 1, 1);                   \
-  } else {                                     \
-    if (cfg.ksplit == 2) CR_GEMM(BPV, 2, 2);   \
-    else CR_GEMM(BPV, 2, 1);                   \
+  return (c.nbatch * ntl16 + tpw - 1) / tpw;
+}
+
+// Slot b * TPW + j of the launch = tile (xcd_remap(b, nwg) * TPW + j) of the
+// stage's nbatch x ntl16 tiles (batch item major): the order the round-5
+// kernel derived on the device, so the work distribution over XCDs is kept.
+void cr_gemm_slots(const CrDims& c, const CrTile* tl16, int ntl16, const CrGemmCfg& cfg, CrSlot* out) {
+  const int tpw = 4 / cfg.ksplit, nwg = cr_gemm_slot_wgs(c, ntl16, cfg), HP = c.BP / 2;
+  const int64_t total = (int64_t)c.nbatch * ntl16, BB = (int64_t)HP * c.BP;
+  for (int b = 0; b < nwg; ++b)
+    for (int j = 0; j < tpw; ++j) {
+      CrSlot& sl = out[(size_t)b * tpw + j];
+      sl = CrSlot{};
+      const int64_t gt = (int64_t)xcd_remap_host(b, nwg) * tpw + j;
+      if (gt >= total) {   // padding of the last workgroup
+        sl.out = kCrNone;
+        sl.cin = kCrNone;
+        continue;
+      }
+      const int bi = (int)(gt / ntl16);
+      const CrTile& t = tl16[gt - (int64_t)bi * ntl16];
+      const int r0 = 16 * t.tr, c0 = 16 * t.tc;
+      sl.base = (uint64_t)bi * (uint64_t)c.item;
+      sl.out = (uint32_t)(t.out * BB + (int64_t)r0 * c.BP + c0);
+      sl.cin = t.cin >= 0 ? (uint32_t)(t.cin * BB + (int64_t)r0 * c.BP + c0) : kCrNone;
+      sl.nt = t.nt;
+      for (int h = 0; h < t.nt; ++h) {
+        sl.a[h] = (uint32_t)(t.a[h] * BB + (int64_t)r0 * c.BP);
+        sl.b[h] = (uint32_t)(t.b[h] * BB + c0);
+        const bool q = (t.bq >> h) & 1;
+        if ((c0 < HP) == q) sl.smask |= 1u << h;   // synthesised rows: sgn < 0
+      }
+      sl.rot = (c0 < HP ? c0 + HP : c0 - HP) - c0;
+    }
+}
+
+void launch_cr_gemm(const CrDims& c, double2* pool, const CrTask* tasks, int ntasks, int maxt32,
+                    int maxt16, const CrSlot* slots, int nslot_wgs, const CrGemmCfg& cfg, double sg,
+                    hipStream_t s) {
+  (void)maxt16;
+  if (ntasks <= 0) return;
+  const dim3 b(256);
+  if (cfg.ts == 16) {
+    const dim3 g(nslot_wgs);
+#define CR_GEMM16(BPV, KSV) hipLaunchKernelGGL((k_cr_gemm16<BPV, KSV>), g, b, 0, s, pool, slots, sg)
+#define CR_GEMM16_BP(BPV)                        \
+  if (cfg.ksplit == 4) CR_GEMM16(BPV, 4);        \
+  else if (cfg.ksplit == 2) CR_GEMM16(BPV, 2);   \
+  else CR_GEMM16(BPV, 1);
+    switch (c.BP) {
+      case 32: CR_GEMM16_BP(32) break;
+      case 64: CR_GEMM16_BP(64) break;
+      case 96: CR_GEMM16_BP(96) break;
+      default: CR_GEMM16_BP(128) break;
+    }
+#undef CR_GEMM16_BP
+#undef CR_GEMM16
+    return;
   }
+  const int total = c.nbatch * ntasks * maxt32;
+  const int tpw = 4 / cfg.ksplit;
+  const dim3 g((total + tpw - 1) / tpw);
+#define CR_GEMM(BPV, KSV) \
+  hipLaunchKernelGGL((k_cr_gemm<BPV, 2, KSV>), g, b, 0, s, pool, c.item, total, sg, (int)g.x, ntasks, maxt32, tasks)
+#define CR_GEMM_BP(BPV)                      \
+  if (cfg.ksplit == 2) CR_GEMM(BPV, 2);      \
+  else CR_GEMM(BPV, 1);
   switch (c.BP) {
     case 32: CR_GEMM_BP(32) break;
     case 64: CR_GEMM_BP(64) break;

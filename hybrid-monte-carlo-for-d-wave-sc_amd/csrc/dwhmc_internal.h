@@ -2,6 +2,7 @@
 // gfx950 kernels (dwhmc_kernels.hip).  Not part of the public ABI.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 
 namespace dwh {
@@ -57,6 +58,29 @@ struct alignas(64) CrTile {
   int a[4], b[4];
   int tr, tc, neg, pad1;   // neg: 1 = negative sign
 };
+// One 16 x 16 output tile of ONE batch item of a product stage, stored in
+// dispatch order (slot blockIdx.x * tiles-per-workgroup + tile: the host applies
+// the XCD-aware remap and the batch-item split), with every operand resolved
+// to an element offset: a wave reads its whole descriptor with one 64-byte
+// scalar load and forms no block, batch-item or tile address itself.
+// base: the batch item's first pool element; out / cin: the tile origin (row
+// 16 tr, column 16 tc) of the output / accumulate input within the item
+// (cin kCrNone: none; out kCrNone: an empty slot); a[h]: A_h at row 16 tr;
+// b[h]: B_h at column 16 tc; rot: the column shift of the synthesised B rows'
+// source ((c + HP) mod BP - c); bit h of smask: term h's synthesised rows carry
+// a negative sign.
+constexpr uint32_t kCrNone = 0xffffffffu;
+struct alignas(64) CrSlot {
+  uint64_t base;
+  uint32_t out, cin;
+  int nt;
+  unsigned smask;
+  uint32_t a[4], b[4];
+  int rot, pad;
+};
+static_assert(sizeof(CrSlot) == 64 && offsetof(CrSlot, out) == 8 && offsetof(CrSlot, nt) == 16 &&
+                  offsetof(CrSlot, a) == 24 && offsetof(CrSlot, b) == 40 && offsetof(CrSlot, rot) == 56,
+              "k_cr_gemm16 reads a slot as 16 dwords in this order");
 // wave tiles of a task at tile size ts
 inline int cr_task_tiles(const CrTask& t, int ts) {
   return ((t.r1 + ts - 1) / ts - t.r0 / ts) * ((t.c1 + ts - 1) / ts - t.c0 / ts);
@@ -153,9 +177,14 @@ struct CrGemmCfg {
 // maxt32 / maxt16: the largest cr_task_tiles over the stage's tasks at ts = 32 / 16;
 // ntmax: the largest term count
 CrGemmCfg cr_gemm_config(const CrDims& c, int ntasks, int maxt32, int maxt16, int ntmax, int ntiles16);
-// tl16: the stage's (task, tile) list at 16 x 16 tiles (ntl16 entries per batch item)
+// 16 x 16 stages (cfg.ts == 16): the dispatch-ordered slots of the stage's
+// (task, tile) list tl16 (ntl16 entries per batch item) over every batch item,
+// a whole number of workgroups (cr_gemm_slot_wgs of them)
+int cr_gemm_slot_wgs(const CrDims& c, int ntl16, const CrGemmCfg& cfg);
+void cr_gemm_slots(const CrDims& c, const CrTile* tl16, int ntl16, const CrGemmCfg& cfg, CrSlot* out);
+// slots: the stage's cr_gemm_slots (16 x 16 stages); tasks: 32 x 32 stages
 void launch_cr_gemm(const CrDims& c, double2* pool, const CrTask* tasks, int ntasks, int maxt32,
-                    int maxt16, const CrTile* tl16, int ntl16, const CrGemmCfg& cfg, double sg,
+                    int maxt16, const CrSlot* slots, int nslot_wgs, const CrGemmCfg& cfg, double sg,
                     hipStream_t s);
 
 // dense h - i y_q (padded with identity) for every (chain, pole): R init input
