@@ -17,6 +17,7 @@
 #include <rocsolver/rocsolver.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <chrono>
 #include <cstdio>
@@ -343,6 +344,27 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol, bool 
     pl.rowpat.clear();
     pl.colpat.clear();
   }
+  // Backward merge (round 6): the G_ee stage of a coarse level u runs inside
+  // the first backward stage of the next finer level f (m_f <= merge_max_m,
+  // not level 0), one launch less per merged pair.  f's products that would
+  // read G_ee(u) = Dinv + W1 G_ae + W2 G_ce = Dinv + G_ea V1 + G_ec V2 (u's
+  // quantities at that position) read its expansion instead:
+  //   W G_ee = (W Dinv) + (W W1) G_ae + (W W2) G_ce,
+  //   G_ee V = (Dinv V) + G_ea (V1 V) + G_ec (V2 V),
+  // the three forward products of each (W Dinv as the accumulate input)
+  // formed off the critical path: side work of the final inversion (BP = 64)
+  // or inside the top level's D' stage (other BP), while their cost fits
+  // (tools/cr_model.py cr_flop_count restates the policy).
+  // Default: levels up to m_f = 4 with side work (BP = 64; C3 +0.4 %, m_f = 8
+  // -0.3 %: its products lengthen the final inversion and the merged m = 8
+  // stage runs several workgroup rounds), up to 8 without (C2 +3.2 %;
+  // profiles/r06_exp_cr_merge.txt).  DWHMC_CR_MERGE=m: levels up to m_f = m
+  // (0: every G_ee stage on its own; A/B, tests).
+  const int merge_max_m = [&] {
+    const char* e = std::getenv("DWHMC_CR_MERGE");
+    return e ? std::max(0, std::atoi(e)) : side ? 4 : 8;
+  }();
+  const bool merge = merge_max_m >= 2;
   auto nr = [&](int b, int r) { return sp_nrow(pl.rowpat, b, r, BP); };
   auto nc = [&](int b, int c) { return sp_nrow(pl.colpat, b, c, BP); };
   int nblk = 3 * Ly;
@@ -362,6 +384,13 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol, bool 
     std::vector<int> V1, V2, W1, W2;   // indexed by position e
     std::vector<char> elim;
     bool sparse = false;               // level 0 by the sparse stages (no V / W blocks)
+    // backward merge: this level's first backward stage also runs the G_ee
+    // stage of the level above; xa / xc[e]: the blocks of the expansion of
+    // G_aa / G_cc (when G_ee of the level above): {Dinv V, V1 V, V2 V,
+    // W Dinv, W W1, W W2} (-1: none)
+    bool merged = false;
+    std::vector<std::array<int, 6>> xa, xc;
+    std::vector<int> Gea, Gec, Gae, Gce;   // backward outputs by eliminated position
   };
   // Level-0 blocks are inverted out of place (they are never overwritten, so
   // per step only their pairing entries change), coarser blocks in place.
@@ -531,8 +560,10 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol, bool 
     const int m = cur.m;
     // inv_ord: this level's inversion stage (added below)
     const bool side_ul = side && m >= side_m && idle_ok(inv_ord + 1);
-    const int w_ord = std::min(n_inv - 1, inv_ord + side_woff);
-    const bool side_w = side && m >= side_m && idle_ok(w_ord);
+    // with the backward merge the final inversion hosts the merge products,
+    // which read W: the W products go at most to the stage before it
+    const int w_ord = std::min(n_inv - (merge ? 2 : 1), inv_ord + side_woff);
+    const bool side_w = side && m >= side_m && w_ord > inv_ord && idle_ok(w_ord);
     cur.elim.assign(m, 0);
     cur.E.clear();
     cur.K.clear();
@@ -637,19 +668,107 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol, bool 
         nxt.L.push_back(cur.L[k]);
       }
     }
+    // the top level (its only kept block is the final one): plan the
+    // backward merges now that every forward block exists; their products go
+    // into this D' stage (no side work) or the final inversion (side work)
+    std::vector<dwh::CrTask> merge_tasks;
+    if (merge && nxt.m == 1) {
+      std::vector<Level*> all;
+      for (Level& lv : levels) all.push_back(&lv);
+      all.push_back(&cur);
+      // budget: side work of two workgroup rounds (4 wave tiles each) on the
+      // CUs the final inversion leaves idle (a side workgroup takes ~6 us of
+      // the inversion's ~16), or 16 x 16 tiles added to this (latency-bound)
+      // D' stage
+      const int64_t t32 = (int64_t)((HP + 31) / 32) * ((BP + 31) / 32), t16 = (int64_t)(HP / 16) * (BP / 16);
+      int64_t side_t = 0;
+      for (const dwh::CrTask& t : side_tasks[n_inv - 1]) side_t += dwh::cr_task_tiles(t, 32);
+      const int64_t budget = side ? 8 * ((int64_t)ncu - nbatch) - side_t * nbatch : 1024;
+      int64_t used = 0;
+      for (int li = (int)all.size() - 2; li >= 1; --li) {
+        Level& f = *all[li];
+        const Level& u = *all[li + 1];
+        if (f.sparse || f.m > merge_max_m) break;
+        int nx = 0;
+        for (int e : f.E) {
+          const int a = e - 1, c = (e + 1) % f.m;
+          nx += u.elim[a / 2] + u.elim[(c / 2) % u.m];
+        }
+        const int64_t cost = 6 * (int64_t)nx * nbatch * (side ? t32 : t16);
+        if (used + cost > budget) break;
+        used += cost;
+        f.merged = true;
+        f.xa.assign(f.m, {-1, -1, -1, -1, -1, -1});
+        f.xc.assign(f.m, {-1, -1, -1, -1, -1, -1});
+        for (int e : f.E) {
+          const int a = e - 1, c = (e + 1) % f.m;
+          // p: u's eliminated position next to e; V, W: the f products that meet G_ee(u)[p]
+          auto expand = [&](int pu, int V, int W) {
+            std::array<int, 6> x;
+            x[0] = nb();    // Dinv V  (M Q -> M)
+            x[1] = nbq();   // V1 V    (Q Q -> Q)
+            x[2] = nbq();   // V2 V
+            x[3] = nb();    // W Dinv  (Q M -> M)
+            x[4] = nbq();   // W W1
+            x[5] = nbq();   // W W2
+            const int src[6][2] = {{u.Dinv[pu], V}, {u.V1[pu], V}, {u.V2[pu], V},
+                                   {W, u.Dinv[pu]}, {W, u.W1[pu]}, {W, u.W2[pu]}};
+            for (int k = 0; k < 6; ++k) {
+              dwh::CrTask t{};
+              t.out = x[k];
+              t.cin = -1;
+              t.r0 = 0;
+              t.r1 = HP;
+              t.c0 = 0;
+              t.c1 = BP;
+              t.nt = 1;
+              t.a[0] = src[k][0];
+              t.b[0] = src[k][1];
+              t.bq = qform[src[k][1]] ? 1 : 0;
+              merge_tasks.push_back(t);
+            }
+            return x;
+          };
+          if (u.elim[a / 2]) f.xa[e] = expand(a / 2, f.V1[e], f.W1[e]);
+          if (u.elim[(c / 2) % u.m]) f.xc[e] = expand((c / 2) % u.m, f.V2[e], f.W2[e]);
+        }
+      }
+      if (!side)
+        for (const dwh::CrTask& t : merge_tasks) {
+          cur_tasks.push_back(t);
+          cur_keep.push_back(nullptr);
+        }
+    }
     flush(1.0);
     if (!ul_tasks.empty()) {
       cur_tasks = ul_tasks;
       cur_keep.assign(ul_tasks.size(), nullptr);
       flush(1.0, true, inv_ord);
     }
+    if (side && !merge_tasks.empty()) {
+      cur_tasks = merge_tasks;
+      cur_keep.assign(merge_tasks.size(), nullptr);
+      flush(1.0, true, n_inv - 1);
+    }
     levels.push_back(cur);
     cur = nxt;
   }
   const int Dfin = add_inv({cur.D[0]}, slot)[0];
   std::vector<int> GD{Dfin}, GU{Dfin}, GL{Dfin};
+  // the G_ee tasks of the level above when they run in this level's first stage
+  struct GeeTask { int out, cin, a0, b0, a1, b1; };
+  std::vector<GeeTask> pend;
+  auto emit_pend = [&] {
+    for (const GeeTask& t : pend) task(t.out, t.cin, {{t.a0, t.b0}, {t.a1, t.b1}});
+    pend.clear();
+  };
   for (int li = (int)levels.size() - 1; li >= 0; --li) {
-    const Level& lv = levels[li];
+    Level& lv = levels[li];
+    // a pending G_ee stage whose finer level does not merge runs on its own
+    if (!pend.empty() && !lv.merged) {
+      emit_pend();
+      flush(1.0);
+    }
     const int m = lv.m, mn = (int)lv.K.size();
     std::vector<int> gd(m, -1), gu(m, -1), gl(m, -1);
     for (int kk = 0; kk < mn; ++kk) {
@@ -731,7 +850,16 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol, bool 
       GL = gl;
       continue;
     }
-    std::vector<int> Gae(m, -1), Gce(m, -1);
+    // merged: this stage also runs the level above's G_ee (pend), and reads
+    // G_ee(u) = Dinv + W1 G_ae + W2 G_ce = Dinv + G_ea V1 + G_ec V2 (u's
+    // blocks at that position) through its expansion (xa / xc, formed in the
+    // forward pass)
+    const Level* up = lv.merged ? &levels[li + 1] : nullptr;
+    emit_pend();
+    lv.Gea.assign(m, -1);
+    lv.Gec.assign(m, -1);
+    lv.Gae.assign(m, -1);
+    lv.Gce.assign(m, -1);
     for (int e : lv.E) {
       const int a = e - 1, c = (e + 1) % m;
       const int ia = a / 2, ic = (c / 2) % mn;
@@ -739,32 +867,62 @@ CrPlan build_cr_plan(int Lx, int Ly, int BP, const std::vector<int>& Dcol, bool 
       const int Gac = mn == 1 ? GD[0] : GU[ia];
       const int Gca = mn == 1 ? GD[0] : GL[ia];
       const int gea = nb(), gec = nb(), gae = nb(), gce = nb();
+      const bool xa = up && lv.xa[e][0] >= 0, xc = up && lv.xc[e][0] >= 0;
       w_c0 = H0;
       w_c1 = H1;
       keep_next = sel ? &need[2][a] : nullptr;   // G_ea = G[a + 1, a] = G_L[a]
-      task(gea, -1, {{lv.W1[e], Gaa}, {lv.W2[e], Gca}});
+      if (xa) {   // W1 G_aa = (W1 Dinv) + (W1 W1u) G_ae,u + (W1 W2u) G_ce,u
+        const std::array<int, 6>& x = lv.xa[e];
+        task(gea, x[3], {{x[4], up->Gae[ia]}, {x[5], up->Gce[ia]}, {lv.W2[e], Gca}});
+      } else {
+        task(gea, -1, {{lv.W1[e], Gaa}, {lv.W2[e], Gca}});
+      }
       keep_next = sel ? &need[1][e] : nullptr;   // G_ec = G[e, e + 1] = G_U[e]
-      task(gec, -1, {{lv.W1[e], Gac}, {lv.W2[e], Gcc}});
+      if (xc) {   // W2 G_cc
+        const std::array<int, 6>& x = lv.xc[e];
+        task(gec, x[3], {{lv.W1[e], Gac}, {x[4], up->Gae[ic]}, {x[5], up->Gce[ic]}});
+      } else {
+        task(gec, -1, {{lv.W1[e], Gac}, {lv.W2[e], Gcc}});
+      }
       keep_next = nullptr;
       w_c0 = 0;
       w_c1 = BP;
-      task(gae, -1, {{Gaa, lv.V1[e]}, {Gac, lv.V2[e]}});
-      task(gce, -1, {{Gca, lv.V1[e]}, {Gcc, lv.V2[e]}});
+      if (xa) {   // G_aa V1 = (Dinv V1) + G_ea,u (V1u V1) + G_ec,u (V2u V1)
+        const std::array<int, 6>& x = lv.xa[e];
+        task(gae, x[0], {{up->Gea[ia], x[1]}, {up->Gec[ia], x[2]}, {Gac, lv.V2[e]}});
+      } else {
+        task(gae, -1, {{Gaa, lv.V1[e]}, {Gac, lv.V2[e]}});
+      }
+      if (xc) {   // G_cc V2
+        const std::array<int, 6>& x = lv.xc[e];
+        task(gce, x[0], {{Gca, lv.V1[e]}, {up->Gea[ic], x[1]}, {up->Gec[ic], x[2]}});
+      } else {
+        task(gce, -1, {{Gca, lv.V1[e]}, {Gcc, lv.V2[e]}});
+      }
       gu[a] = gae;
       gl[a] = gea;
       gu[e] = gec;
       gl[e] = gce;
-      Gae[e] = gae;
-      Gce[e] = gce;
+      lv.Gea[e] = gea;
+      lv.Gec[e] = gec;
+      lv.Gae[e] = gae;
+      lv.Gce[e] = gce;
     }
     flush(1.0);
+    // G_ee = Dinv + W1 G_ae + W2 G_ce, in place; deferred into the next finer
+    // level's first stage when that one merges
+    const bool defer = li >= 1 && levels[li - 1].merged;
     for (int e : lv.E) {
-      keep_next = sel ? &need[0][e] : nullptr;
-      task(lv.Dinv[e], lv.Dinv[e], {{lv.W1[e], Gae[e]}, {lv.W2[e], Gce[e]}});
+      if (defer) {
+        pend.push_back(GeeTask{lv.Dinv[e], lv.Dinv[e], lv.W1[e], lv.Gae[e], lv.W2[e], lv.Gce[e]});
+      } else {
+        keep_next = sel ? &need[0][e] : nullptr;
+        task(lv.Dinv[e], lv.Dinv[e], {{lv.W1[e], lv.Gae[e]}, {lv.W2[e], lv.Gce[e]}});
+      }
       gd[e] = lv.Dinv[e];
     }
     keep_next = nullptr;
-    flush(1.0);
+    if (!defer) flush(1.0);
     GD = gd;
     GU = gu;
     GL = gl;

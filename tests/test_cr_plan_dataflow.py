@@ -25,8 +25,10 @@ def check(lib, Lx, Ly, nbatch, side, inv0):
 @pytest.mark.parametrize("Lx,Ly", LATTICES)
 @pytest.mark.parametrize("nbatch", [14, 56])
 @pytest.mark.parametrize("sparse0", ["1", "0"])
-def test_cr_schedule_dataflow(dwhmc, monkeypatch, Lx, Ly, nbatch, sparse0):
+@pytest.mark.parametrize("merge", ["8", "0"])
+def test_cr_schedule_dataflow(dwhmc, monkeypatch, Lx, Ly, nbatch, sparse0, merge):
     monkeypatch.setenv("DWHMC_CR_SPARSE0", sparse0)
+    monkeypatch.setenv("DWHMC_CR_MERGE", merge)
     lib = dwhmc.load_library()
     for side in (0, 1):
         for inv0 in (0, 1):
@@ -37,21 +39,44 @@ def test_cr_schedule_dataflow(dwhmc, monkeypatch, Lx, Ly, nbatch, sparse0):
 
 def test_cr_schedule_c3_shape(dwhmc, monkeypatch):
     """The C3 plan (L = 32, 14 poles): 6 inversion launches, 4 of them with
-    side work, 20 product launches, two of them the sparse level-0 stages
+    side work, 19 product launches, two of them the sparse level-0 stages
     (level 0 makes no U'/L' side work for the level-1
-    inversion); the dense level 0 (DWHMC_CR_SPARSE0=0) puts side work on 5."""
+    inversion): the backward merge (round 6) runs the G_ee stage of the m = 2
+    level inside the m = 4 level's first stage, 25 launches instead of 26
+    (DWHMC_CR_MERGE=0), 24 with DWHMC_CR_MERGE=8 (the m = 4 one too); without
+    side work the merge products sit in the top level's D' stage only while
+    they stay small (BP = 64: none); the dense level 0 (DWHMC_CR_SPARSE0=0)
+    puts side work on 5."""
     lib = dwhmc.load_library()
     monkeypatch.delenv("DWHMC_CR_SPARSE0", raising=False)
+    monkeypatch.delenv("DWHMC_CR_MERGE", raising=False)
     rc, stats, err = check(lib, 32, 32, 14, 1, 1)
     assert rc == 0, err
-    assert list(stats[:4]) == [26, 6, 4, 20]
+    assert list(stats[:4]) == [25, 6, 4, 19]
+    monkeypatch.setenv("DWHMC_CR_MERGE", "8")
+    rc, stats, err = check(lib, 32, 32, 14, 1, 1)
+    assert rc == 0, err
+    assert list(stats[:4]) == [24, 6, 4, 18]
+    monkeypatch.delenv("DWHMC_CR_MERGE", raising=False)
     rc, stats, err = check(lib, 32, 32, 14, 0, 1)
     assert rc == 0, err
     assert list(stats[:4]) == [26, 6, 0, 20]
+    # four chains (56 batch items): one merge fits the idle CUs
+    rc, stats, err = check(lib, 32, 32, 56, 1, 1)
+    assert rc == 0, err
+    assert list(stats[:4]) == [25, 6, 3, 19]
+    monkeypatch.setenv("DWHMC_CR_MERGE", "0")
+    rc, stats, err = check(lib, 32, 32, 14, 1, 1)
+    assert rc == 0, err
+    assert list(stats[:4]) == [26, 6, 4, 20]
     monkeypatch.setenv("DWHMC_CR_SPARSE0", "0")
     rc, stats, err = check(lib, 32, 32, 14, 1, 1)
     assert rc == 0, err
     assert list(stats[:4]) == [26, 6, 5, 20]
+    monkeypatch.setenv("DWHMC_CR_MERGE", "8")
+    rc, stats, err = check(lib, 32, 32, 14, 1, 1)
+    assert rc == 0, err
+    assert list(stats[:4]) == [24, 6, 5, 18]
 
 
 def test_cr_schedule_rejects_wide_rows(dwhmc):
@@ -91,8 +116,10 @@ def test_cr_plan_flops_independent_count(dwhmc, monkeypatch, Lx, Ly, nbatch, spa
     from tools.cr_model import cr_flop_count
     monkeypatch.setenv("DWHMC_CR_SPARSE0", sparse0)
     lib = dwhmc.load_library()
-    inv_ref, prod_ref = cr_flop_count(Lx, Ly, default_rows(Lx, Ly), sparse0=sparse0 == "1")
     for side in (0, 1):
+        # the backward merge's products depend on where they can run (side work or not)
+        inv_ref, prod_ref = cr_flop_count(Lx, Ly, default_rows(Lx, Ly), sparse0=sparse0 == "1", nbatch=nbatch,
+                                          side=bool(side))
         for inv0 in (0, 1):
             inv, prod, side_f = plan_flops(lib, Lx, Ly, nbatch, side, inv0)
             assert inv == pytest.approx(inv_ref, rel=1e-12), (side, inv0)

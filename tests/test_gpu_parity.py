@@ -870,3 +870,30 @@ def test_cr_sparse_level0(dwhmc, oracle, monkeypatch, Lx, Ly, beta, sparse0):
             assert bool(acc[0]) == acc_r and abs(dH[0] - dH_r) <= 1e-8 * (1 + abs(dH_r))
             assert np.max(np.abs(ctx.get_state()[0][0] - D_r)) <= 1e-10
     ctx.close()
+
+
+@pytest.mark.parametrize("merge", ["0", "4", "8"])
+@pytest.mark.parametrize("Lx,Ly,beta", [(20, 16, 8.0), (12, 16, 8.0), (20, 12, 16.0), (9, 24, 4.0)])
+def test_cr_backward_merge(dwhmc, oracle, monkeypatch, merge, Lx, Ly, beta):
+    """The backward merge (round 6, build_cr_plan): a coarse level's G_ee stage
+    inside the next finer level's first stage, whose products read G_ee
+    through its expansion (forward products as side work of the final
+    inversion at BP = 64, inside the top level's D' stage at BP = 32).
+    DWHMC_CR_MERGE = 0 / 4 / 8 (levels up to that size) against the eigen
+    oracle at the factorisation tolerances, on BP = 64 (Lx = 20) and BP = 32
+    (Lx = 12, 9) lattices with even and odd coarse levels (Ly = 16, 12, 24)."""
+    O = oracle
+    monkeypatch.setenv("DWHMC_CR_MERGE", merge)
+    p, dis, Delta = make_case(O, Lx, Ly, beta, seed=Lx * 11 + Ly)
+    cache, F_ref, Ef_ref = O.evaluate(p, dis, Delta)
+    P_ref, _ = O.pairing_P(cache.U, cache.E_n, p)
+    ctx = device_ctx(dwhmc, p, dis, "cr")
+    ctx.set_pairing(Delta)
+    ctx.factorize()
+    assert np.max(np.abs(ctx.pairing()[0] - P_ref)) <= 1e-11
+    assert np.max(np.abs(ctx.forces()[0] - F_ref)) <= 1e-10 * (1 + np.max(np.abs(F_ref)))
+    Ef = ctx.fermion_energy()[0]
+    assert abs(Ef - Ef_ref) <= 1e-11 * abs(Ef_ref), (Ef, Ef_ref)
+    hole_ref = O.measure_observables(cache, p, Delta)["hole_conc"]
+    assert abs(2.0 * ctx.hole_trace()[0] / p.N - 1.0 - hole_ref) <= 1e-11
+    ctx.close()

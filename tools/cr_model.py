@@ -214,17 +214,23 @@ def check_top_half(n=5, seed=0, y=0.6):
     return err
 
 
-def cr_selected_inverse_top(Dg, U, L):
+def cr_selected_inverse_top(Dg, U, L, merge=frozenset(), depth=0, _aux=False):
     """cr_selected_inverse on top halves (n x 2n) with the form bookkeeping of
     the device planner: D, U, L, inverses and G blocks are M-form; V, W are
-    Q-form.  Inputs/outputs are top halves of M-form blocks."""
+    Q-form.  Inputs/outputs are top halves of M-form blocks.
+    merge: the depths f whose first backward stage runs the G_ee stage of the
+    level above (u = f + 1) in the device plan (build_cr_plan, round 6): f's
+    products then read G_ee(u) at its eliminated positions p through
+        W G_ee = (W Dinv) + (W W1) G_ae + (W W2) G_ce,
+        G_ee V = (Dinv V) + G_ea (V1 V) + G_ec (V2 V)
+    (u's blocks at p), as the device does; the result is the same inverse."""
     M, Q = -1, +1
     m = len(Dg)
     mul = top_product
     if m == 1:
         Dfin = Dg[0] + U[0] + L[0]
         G, ld = top_inverse_mform(Dfin)
-        return ld, [G], [G], [G]
+        return (ld, [G], [G], [G], {}) if _aux else (ld, [G], [G], [G])
     E = list(range(1, m - (m % 2), 2))
     K = [k for k in range(m) if k % 2 == 0]
     ld = 0.0
@@ -258,30 +264,48 @@ def cr_selected_inverse_top(Dg, U, L):
         else:
             Un.append(U[k])
             Ln.append(L[k])
-    ld2, GDn, GUn, GLn = cr_selected_inverse_top(Dn, Un, Ln)
+    ld2, GDn, GUn, GLn, up = cr_selected_inverse_top(Dn, Un, Ln, merge, depth + 1, True)
     ld += ld2
     mn = len(K)
+    mrg = depth in merge and depth >= 1
     GD, GU, GL = [None] * m, [None] * m, [None] * m
     for kk, k in enumerate(K):
         GD[k] = GDn[kk]
         if k + 1 not in Dinv:
             GU[k], GL[k] = GUn[kk], GLn[kk]
+    aux = {}
     for e in E:
         a, c = e - 1, (e + 1) % m
         ia, ic = a // 2, (c // 2) % mn
         Gaa, Gcc = GDn[ia], GDn[ic]
         Gac, Gca = (GDn[0], GDn[0]) if mn == 1 else (GUn[ia], GLn[ia])
-        Gea = mul(W1[e], Gaa, M) + mul(W2[e], Gca, M)
-        Gec = mul(W1[e], Gac, M) + mul(W2[e], Gcc, M)
-        Gae = mul(Gaa, V1[e], Q) + mul(Gac, V2[e], Q)
-        Gce = mul(Gca, V1[e], Q) + mul(Gcc, V2[e], Q)
+        if mrg and ia in up:      # G_aa = G_ee(u)[ia]: its expansion (forward products x)
+            x = up[ia]
+            Gea = (mul(W1[e], x["Dinv"], M) + mul(mul(W1[e], x["W1"], Q), x["Gae"], M)
+                   + mul(mul(W1[e], x["W2"], Q), x["Gce"], M) + mul(W2[e], Gca, M))
+            Gae = (mul(x["Dinv"], V1[e], Q) + mul(x["Gea"], mul(x["V1"], V1[e], Q), Q)
+                   + mul(x["Gec"], mul(x["V2"], V1[e], Q), Q) + mul(Gac, V2[e], Q))
+        else:
+            Gea = mul(W1[e], Gaa, M) + mul(W2[e], Gca, M)
+            Gae = mul(Gaa, V1[e], Q) + mul(Gac, V2[e], Q)
+        if mrg and ic in up:      # G_cc = G_ee(u)[ic]
+            x = up[ic]
+            Gec = (mul(W2[e], x["Dinv"], M) + mul(mul(W2[e], x["W1"], Q), x["Gae"], M)
+                   + mul(mul(W2[e], x["W2"], Q), x["Gce"], M) + mul(W1[e], Gac, M))
+            Gce = (mul(x["Dinv"], V2[e], Q) + mul(x["Gea"], mul(x["V1"], V2[e], Q), Q)
+                   + mul(x["Gec"], mul(x["V2"], V2[e], Q), Q) + mul(Gca, V1[e], Q))
+        else:
+            Gec = mul(W1[e], Gac, M) + mul(W2[e], Gcc, M)
+            Gce = mul(Gca, V1[e], Q) + mul(Gcc, V2[e], Q)
         GD[e] = Dinv[e] + mul(W1[e], Gae, M) + mul(W2[e], Gce, M)
         GU[a], GL[a], GU[e], GL[e] = Gae, Gea, Gec, Gce
-    return ld, GD, GU, GL
+        aux[e] = dict(Dinv=Dinv[e], V1=V1[e], V2=V2[e], W1=W1[e], W2=W2[e], Gea=Gea, Gec=Gec, Gae=Gae, Gce=Gce)
+    return (ld, GD, GU, GL, aux) if _aux else (ld, GD, GU, GL)
 
 
-def check_top_cr(Lx, Ly, seed=0, y=0.7):
-    """cr_selected_inverse_top against the full-block version on a BdG matrix."""
+def check_top_cr(Lx, Ly, seed=0, y=0.7, merge=frozenset()):
+    """cr_selected_inverse_top (with the backward merge at the depths in
+    `merge`) against the full-block version on a BdG matrix."""
     import os
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
@@ -297,7 +321,7 @@ def check_top_cr(Lx, Ly, seed=0, y=0.7):
     Dg, U, L = blocks_from_dense(A, Lx, Ly)
     ld, GD, GU, GL = cr_selected_inverse(Dg, U, L)
     top = lambda X: [x[:Lx, :] for x in X]
-    ldt, GDt, GUt, GLt = cr_selected_inverse_top(top(Dg), top(U), top(L))
+    ldt, GDt, GUt, GLt = cr_selected_inverse_top(top(Dg), top(U), top(L), merge)
     err = abs(ld - ldt)
     for F, T in ((GD, GDt), (GU, GUt), (GL, GLt)):
         for f, t in zip(F, T):
@@ -361,15 +385,59 @@ def level0_nnz_top(Lx: int, Ly: int, rows: int = 1):
     return [int(np.count_nonzero(u[:Lxb])) for u in U], [int(np.count_nonzero(x[:Lxb])) for x in L]
 
 
-def cr_flop_count(Lx: int, Ly: int, rows: int = 1, sparse0: bool = True):
+def merge_depths(Lyb: int, BP: int, nbatch: int, side: bool, sp0: bool, ncu: int = 256, merge=True):
+    """The depths f whose first backward stage runs the G_ee stage of the
+    level above (build_cr_plan's backward merge, round 6): from the level
+    below the top downwards, m_f <= 8, not level 0 (sparse or dense), while
+    the six forward products per expanded position fit the budget (side work:
+    two rounds of 4 wave tiles on the CUs the final inversion leaves idle;
+    else 1024 16 x 16 tiles in the top level's D' stage)."""
+    HP = BP // 2
+    ms = []
+    m = Lyb
+    while m > 1:
+        ms.append(m)
+        m = (m + 1) // 2
+    out = set()
+    # merge: True = the default depth (m_f <= 4 with side work, 8 without), an
+    # int = DWHMC_CR_MERGE's m, False / 0 = off
+    max_m = (4 if side else 8) if merge is True else int(merge)
+    if max_m < 2 or len(ms) < 2:
+        return out
+    t32 = -(-HP // 32) * -(-BP // 32)
+    t16 = (HP // 16) * (BP // 16)
+    budget = 8 * (ncu - nbatch) if side else 1024
+    used = 0
+    for d in range(len(ms) - 2, 0, -1):
+        mf, mu = ms[d], ms[d + 1]
+        if mf > max_m:
+            break
+        elim_u = set(range(1, mu - mu % 2, 2))
+        nx = 0
+        for e in range(1, mf - mf % 2, 2):
+            a, c = e - 1, (e + 1) % mf
+            nx += (a // 2 in elim_u) + ((c // 2) % mu in elim_u)
+        cost = 6 * nx * nbatch * (t32 if side else t16)
+        if used + cost > budget:
+            break
+        used += cost
+        out.add(d)
+    return out
+
+
+def cr_flop_count(Lx: int, Ly: int, rows: int = 1, sparse0: bool = True, nbatch: int = 1, side: bool = False,
+                  merge=True):
     """sparse0: level 0 by the sparse stages when the device takes them (even
     Ly / rows >= 4, BP <= 96): the sparse products at 8 flops per complex MAC
     of a stored nonzero (cr_selected_inverse_top_sparse0), the dense products
-    one term each."""
+    one term each.  nbatch / side (BP = 64 side work on) / merge: the backward
+    merge's extra products (merge_depths): per expanded position six forward
+    products and one more term in each of two backward products."""
     Lxb, Lyb = Lx * rows, Ly // rows
     HP = (Lxb + 15) // 16 * 16
     BP = 2 * HP
     sp = sparse0 and Lyb % 2 == 0 and Lyb >= 4 and BP <= 96
+    mdepths = merge_depths(Lyb, BP, nbatch, side and BP == 64, sp, merge=merge)
     if sp:
         nU, nL = level0_nnz_top(Lx, Ly, rows)
     full = 8.0 * BP * HP * BP                       # one term, whole top half
@@ -427,6 +495,12 @@ def cr_flop_count(Lx: int, Ly: int, rows: int = 1, sparse0: bool = True):
                 terms += 2 * (n_ea + n_ec) * per_ea + 2 * 2 * full + 2 * n_ee * per_ee
             else:
                 terms += 5 * 2 * full               # G_ea, G_ec, G_ae, G_ce, G_ee: 2 terms each
+                if depth in mdepths:                # expansions of G_ee of the level above
+                    mu = len(K)
+                    a, c = e - 1, (e + 1) % m
+                    for p in (a // 2, (c // 2) % mu):
+                        if p % 2 == 1 and p < mu - mu % 2:
+                            terms += 8 * full
 
     level(Lyb, 0)
     return inv * 8.0 * BP ** 3, terms
