@@ -160,3 +160,58 @@ def test_fused_step_scalars():
     S1, S2, S3 = np.sum(np.abs(a[q]) ** 2), np.vdot(v[q], a[q]), np.sum(np.abs(v[q]) ** 2)
     xn = S1 - 2.0 * np.real(np.conj(b) * S2) + abs(b) ** 2 * S3
     assert abs(xn - np.sum(np.abs(c_step[q]) ** 2)) <= 1e-12 * (S1 + abs(b) ** 2 * S3)
+
+
+# --------------------------------------------------------------------------
+# Structure-preserving (quaternion) reduction, tools/qeig_proto.py: the
+# costed next step for the one-matrix measurement -- half
+# the Householder steps of the one-stage reduction, one matrix-vector product
+# per site (H Theta v = -Theta H v), the particle rows only.  CPU prototype.
+import qeig_proto as QP  # noqa: E402
+
+
+@pytest.mark.parametrize("M,seed,clean", [(3, 0, False), (7, 1, False), (12, 2, False), (10, 3, True)])
+def test_quaternion_reduction_random_bdg(M, seed, clean):
+    """Random BdG-form H (h Hermitian, D symmetric): the reduced 2 x 2-block
+    tridiagonal T = [[A, C], [conj C, -A]] (A real tridiagonal, C diagonal)
+    has H's spectrum, and the whole pipeline (block Sturm bisection, pivoted
+    band inverse iteration, site rotations, 2 (M - 1) rank-1 reflectors in
+    compact WY) gives eigenpairs at the one-stage solver's tolerances."""
+    H = QP.bdg_matrix(M, seed, clean)
+    a, d, Y, V, tau = QP.qtridiagonalize_top(H[:M])
+    g, a2, d2, b = QP.site_rotations(a, d, Y)
+    T = QP.block_tridiag_dense(a2, d2, b)
+    ev = np.linalg.eigvalsh(H)
+    scale = 1 + np.max(np.abs(ev))
+    assert np.max(np.abs(np.linalg.eigvalsh(T) - ev)) <= 1e-12 * scale
+    E, U = QP.eigh_quat(H)
+    assert np.max(np.abs(E - ev)) <= 1e-12 * scale
+    assert np.max(np.abs(H @ U - U * E[None, :])) <= 1e-11 * scale
+    assert np.max(np.abs(U.conj().T @ U - np.eye(2 * M))) <= 1e-12
+
+
+@pytest.mark.parametrize("Lx,Ly,clean,mu", [(6, 6, False, -1.08), (8, 8, True, 0.0), (6, 4, True, -1.0)])
+def test_quaternion_reduction_bdg_lattices(oracle, Lx, Ly, clean, mu):
+    """The reference's H_BdG (oracle assembly of src/Hamiltonian.jl), disordered
+    and clean (exactly degenerate shells, the zero modes of mu = 0)."""
+    O = oracle
+    p = O.ModelParameters(Lx, Ly, 1.0, -0.35, mu, 0.0 if clean else 1.0, 0.1, 8.0, 0.8, 1.0)
+    N = p.N
+    rng = np.random.default_rng(Lx + Ly)
+    st = O.initialize_state(p, rng)
+    if clean:
+        D = np.stack([np.full(N, 0.2), np.full(N, -0.2)], 1).astype(complex)
+        dis = np.zeros(N)
+    else:
+        D = st.Delta + 0.25 * np.exp(0.3j * rng.standard_normal((N, 2)))
+        dis = st.disorder_pot
+    cache = O.initialize_cache(p)
+    O.init_static_H(cache, p, dis)
+    O.update_H_BdG(cache, p, D)
+    H = O.hermitian_from_upper(cache.H_base)
+    E, U = QP.eigh_quat(H)
+    ev = np.linalg.eigvalsh(H)
+    scale = 1 + np.max(np.abs(ev))
+    assert np.max(np.abs(E - ev)) <= 1e-12 * scale
+    assert np.max(np.abs(H @ U - U * E[None, :])) <= 1e-11 * scale
+    assert np.max(np.abs(U.conj().T @ U - np.eye(2 * N))) <= 1e-12
