@@ -91,6 +91,7 @@ SIGNATURES = {
     "dwh_measure_transport_deltas": (C.c_int, [_P, _I64, _I64, _P, _D, _D, _D, _P, _P, _P, _I64, _P, _P, _I64,
                                                _P]),
     "dwh_debug_dense_H": (C.c_int, [_P, _I64, _P]),
+    "dwh_debug_qeig": (C.c_int, [_P, _I64, _P, _P]),
     "dwh_debug_level0": (C.c_int, [_P, _I64, _I64, _I32, _P, _P]),
     "dwh_debug_cr_plan_check": (C.c_int, [_I64, _I64, _I64, _I32, _I32, _P]),
     "dwh_debug_cr_plan_flops": (C.c_int, [_I64, _I64, _I64, _I32, _I32, _P]),

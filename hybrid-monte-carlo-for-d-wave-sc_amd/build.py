@@ -16,7 +16,8 @@ CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libdwhmc.so")
 SOURCES = [os.path.join(CSRC, "dwhmc_kernels.hip"), os.path.join(CSRC, "dwhmc_cr.hip"), os.path.join(CSRC, "dwhmc_cr_sparse.hip"),
            os.path.join(CSRC, "dwhmc_eig.hip"), os.path.join(CSRC, "dwhmc_gemm.hip"),
-           os.path.join(CSRC, "dwhmc_transport.hip"), os.path.join(CSRC, "dwhmc_api.cpp")]
+           os.path.join(CSRC, "dwhmc_transport.hip"), os.path.join(CSRC, "dwhmc_qeig.hip"),
+           os.path.join(CSRC, "dwhmc_api.cpp")]
 # rocSOLVER (zheevd for an order above kEigMaxN, zheev as the re-solve of a
 # non-finite result) is the
 # only vendor library the measurement path can call; every product runs on the

@@ -1106,6 +1106,7 @@ struct dwh_ctx {
   int64_t eig_long_clusters = 0;   // clusters longer than k_eig_orth's limit, orthonormalised by long_clusters
   int eig_ph_last = -1;    // dwh_info_t::eig_half: eig_ph of the last eigensolve (-1: none yet)
   double *d_eig_d = nullptr, *d_eig_e = nullptr, *d_eig_tn = nullptr;
+  double* d_q = nullptr;   // structure-preserving eigenvalue solver (dwhmc_qeig.hip) workspace, one matrix
   hipStream_t eig_sx[3] = {};       // extra streams of the sub-batched tridiagonalisation
   hipEvent_t eig_ev[4] = {};
 
@@ -2729,6 +2730,74 @@ int dwh_transport_grid(double eta, double domega, double omega_max, int64_t* n_o
   return DWH_OK;
 }
 
+// Eigenvalues only, by the structure-preserving reduction (dwhmc_qeig.hip):
+// H_BdG of src assembled into the slot's JU, reduced site by site on its
+// particle rows, site rotations, block Sturm bisection; the 2N ascending
+// eigenvalues into the slot's E (device).  ms (optional): the reduction's
+// device time (HIP events; synchronises).
+int qeig_values(dwh_ctx* ctx, const TrSrc& src, float* ms) {
+  const int M = ctx->d.N, n = 2 * M;
+  if (!dwh::q_supported(M)) return fail(ctx, DWH_ERR_ARG, "structure-preserving solver: lattice too large");
+  const int64_t sA = (int64_t)n * n, sP = dwh::q_part_elems(M);
+  // workspace (doubles): scratch 2 sP | W 2n | Y 2n | qd 2M | rd 2M | G 2n | tau M | qa M | ra M | rb M | tn 2
+  const int64_t oW = 2 * sP, oY = oW + 2 * n, oqd = oY + 2 * n, ord = oqd + 2 * M, oG = ord + 2 * M,
+                otau = oG + 2 * n, oqa = otau + M, ora = oqa + M, orb = ora + M, otn = orb + M, tot = otn + 2;
+  int rc;
+  if (!ctx->d_q && (rc = dalloc(ctx, &ctx->d_q, (size_t)tot))) return rc;
+  double* w = ctx->d_q;
+  auto z2 = [&](int64_t o) { return reinterpret_cast<double2*>(w + o); };
+  hipStream_t s = ctx->stream;
+  double2* A = ctx->tr.JU;
+  if ((rc = assemble_slots(ctx, src, 1, A))) return rc;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (ms) {
+    HIPCHECK(ctx, hipEventCreate(&e0));
+    HIPCHECK(ctx, hipEventCreate(&e1));
+    HIPCHECK(ctx, hipEventRecord(e0, s));
+  }
+  dwh::launch_q_reduce(A, M, sA, z2(0), sP, z2(oW), w + otau, z2(oY), w + oqa, z2(oqd), 1, s);
+  if (ms) HIPCHECK(ctx, hipEventRecord(e1, s));
+  dwh::launch_q_rot(w + oqa, z2(oqd), z2(oY), M, w + ora, z2(ord), w + orb, z2(oG), 1, s);
+  dwh::launch_q_bisect(w + ora, z2(ord), w + orb, M, ctx->tr.E, w + otn, 1, s);
+  HIPCHECK(ctx, hipGetLastError());
+  if (ms) {
+    HIPCHECK(ctx, hipStreamSynchronize(s));
+    HIPCHECK(ctx, hipEventElapsedTime(ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+  }
+  return DWH_OK;
+}
+
+// Development entry (tools/qeig_check.py): qeig_values of `chain`, the
+// eigenvalues into E and the reduction's device time into *ms.
+int dwh_debug_qeig(dwh_ctx* ctx, int64_t chain, double* E, double* ms) {
+  if (!ctx || !E) return fail(ctx, DWH_ERR_ARG, "NULL argument");
+  if (chain < 0 || chain >= ctx->d.nc) return fail(ctx, DWH_ERR_ARG, "chain index out of range");
+  HIPCHECK(ctx, hipSetDevice(ctx->device));
+  SETTLE(ctx);
+  int rc;
+  if ((rc = transport_prepare(ctx, std::max<int64_t>(ctx->tr_nw, 0), std::max<int64_t>(ctx->tr_nd, 0), 1)))
+    return rc;
+  float t = 0.0f;
+  if ((rc = qeig_values(ctx, chains_src(ctx, chain), &t))) return rc;
+  const int M = ctx->d.N;
+  HIPCHECK(ctx, hipMemcpyAsync(E, ctx->tr.E, 2 * (size_t)M * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+  if (ms) *ms = t;
+#ifdef QSTAMPS
+  if (const char* f = std::getenv("QSTAMPS_FILE")) {   // diagnostic builds: the phase stamps
+    std::vector<unsigned long long> st((size_t)std::min(M, 4096) * 16);
+    if (dwh::q_stamps_read(st.data(), std::min(M, 4096)) == 0)
+      if (FILE* fp = std::fopen(f, "wb")) {
+        std::fwrite(st.data(), sizeof(unsigned long long), st.size(), fp);
+        std::fclose(fp);
+      }
+  }
+#endif
+  return DWH_OK;
+}
+
 int dwh_eigensystem(dwh_ctx* ctx, int64_t chain, double* E, dwh_c128* U) {
   if (!ctx || !E) return fail(ctx, DWH_ERR_ARG, "NULL argument");
   if (chain < 0 || chain >= ctx->d.nc) return fail(ctx, DWH_ERR_ARG, "chain index out of range");
@@ -2737,8 +2806,23 @@ int dwh_eigensystem(dwh_ctx* ctx, int64_t chain, double* E, dwh_c128* U) {
   int rc;
   if ((rc = transport_prepare(ctx, std::max<int64_t>(ctx->tr_nw, 0), std::max<int64_t>(ctx->tr_nd, 0), 1)))
     return rc;
-  if ((rc = eigen_solve(ctx, chains_src(ctx, chain), 1))) return rc;
   const size_t n2 = 2 * (size_t)ctx->d.N;
+  if (!U && dwh::q_supported(ctx->d.N) && (int64_t)n2 <= dwh::kEigMaxN) {
+    // eigenvalues only: the structure-preserving reduction (half the
+    // launches and a quarter of the pass traffic of the one-stage path)
+    Scope sc(ctx, T_EIG_OWN, 1);
+    ctx->eig_ph = false;
+    ctx->eig_ph_last = 0;
+    if ((rc = qeig_values(ctx, chains_src(ctx, chain), nullptr))) return rc;
+    HIPCHECK(ctx, hipMemsetAsync(ctx->d_tr_bad, 0, sizeof(int), ctx->stream));
+    dwh::launch_nonfinite(ctx->tr.U, 0, ctx->tr.E, (int64_t)n2, ctx->d_tr_bad, ctx->stream);
+    int bad = 0;
+    HIPCHECK(ctx, hipMemcpyAsync(E, ctx->tr.E, n2 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHECK(ctx, hipMemcpyAsync(&bad, ctx->d_tr_bad, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+    if (!bad) return DWH_OK;   // (non-finite eigenvalues: the full solve below)
+  }
+  if ((rc = eigen_solve(ctx, chains_src(ctx, chain), 1))) return rc;
   HIPCHECK(ctx, hipMemcpyAsync(E, ctx->tr.E, n2 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
   if (U)
     HIPCHECK(ctx, hipMemcpyAsync(U, ctx->tr.U, n2 * n2 * sizeof(double2), hipMemcpyDeviceToHost,

@@ -385,6 +385,24 @@ void launch_eig_vt(const double2* A, int n, int64_t sA, double2* Vt, int m, hipS
 void launch_eig_tw(const double2* Tb, int64_t sT, const double2* W, int ldw, int64_t sW, int S, int kb, int n,
                    double2* W2, int64_t sW2, int m, hipStream_t s);
 
+// Structure-preserving (quaternion) eigensolver (dwhmc_qeig.hip): m matrices
+// of order n = 2M, column-major at stride sA, reduced site by site on their
+// particle rows (A's bottom rows then hold the reflectors); part: q_part_elems
+// per matrix (stride sP); W: 2M per matrix; tau, qa: M; Y: 2M; qd: M
+int q_part_elems(int M);
+bool q_supported(int M);   // sites per matrix the reduction takes (1 .. 3072)
+#ifdef QSTAMPS
+int q_stamps_read(unsigned long long* out, int nsteps);   // diagnostic builds (-DQSTAMPS)
+#endif
+void launch_q_reduce(double2* A, int M, int64_t sA, double2* part, int64_t sP, double2* W, double* tau, double2* Y,
+                     double* qa, double2* qd, int m, hipStream_t s);
+// site rotations: (ra, rd, rb) = T's blocks (a', d', b), G: per site (al, be)
+void launch_q_rot(const double* qa, const double2* qd, const double2* Y, int M, double* ra, double2* rd, double* rb,
+                  double2* G, int m, hipStream_t s);
+// the 2M eigenvalues of T ascending into E (stride 2M), ||T|| bound into tnorm
+void launch_q_bisect(const double* ra, const double2* rd, const double* rb, int M, double* E, double* tnorm, int m,
+                     hipStream_t s);
+
 // The library's own batched fp64 products (dwhmc_gemm.hip):
 // C = alpha op(A) op(B) + beta C, column-major, op 'N' or 'C' (conjugate
 // transpose; 'T' for real), per-matrix strides sA / sB / sC (elements)

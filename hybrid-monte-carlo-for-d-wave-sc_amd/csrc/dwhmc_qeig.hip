@@ -1,0 +1,772 @@
+// Structure-preserving (quaternion) Hermitian eigensolver for the BdG matrix
+// of the transport / spectra measurement (src/Observables.jl:314-526, the
+// eigen!(Hermitian(H)) of src/Hamiltonian.jl:96-114); numpy prototype with the
+// same algebra: tools/qeig_proto.py.
+//
+// H_BdG = [[h, D], [conj D, -conj h]] (h Hermitian, D symmetric) anticommutes
+// with Theta (u; v) = (-conj v; conj u), Theta^2 = -1.
+// Unitaries that commute with Theta keep that form, so the matrix is reduced
+// site by site (M = N sites, n = 2M) on its particle rows only:
+//
+//   step j        x = column j below site j+1 (particle and hole entries of
+//                 the sites j+1 ..), v = x + s x1 (x1: site j+1's two entries,
+//                 s = |x| / |x1|), U = I - tau (v v^H + Theta v (Theta v)^H),
+//                 tau = 2 / |v|^2, U x = y = -s x1.  Since H Theta = -Theta H,
+//                 one matrix-vector product p = H v per site; w1 = tau p -
+//                 tau^2 / 2 (r v - conj(c) Theta v), r = v^H p, c = v^H Theta p,
+//                 and H <- H - v w1^H - w1 v^H + Theta v (Theta w1)^H +
+//                 Theta w1 (Theta v)^H on the particle rows of the sites > j+1.
+//   launches      k_q_rs (one workgroup per matrix): p = H v_j read from P,
+//                 w1_j, site j+1's two columns updated, its diagonal block and
+//                 the reflector v_{j+1}; k_q_pass (one workgroup per 64 x 64
+//                 lower-triangle tile of h and of D on the remaining sites):
+//                 update j applied and written back, p = H v_{j+1} from the
+//                 same tiles (both triangles by symmetry) into P by 64-bit
+//                 fixed-point integer atomics (exact: bit-reproducible in any
+//                 order).  Two launches per SITE (the one-stage reduction
+//                 needs two per column, i.e. twice as many), each pass over
+//                 m^2 stored elements (m active sites; the one-stage pass
+//                 reads (2m)^2 / 2).  L = 32: 16.1 ms against 29.5 ms for the
+//                 one-stage tridiagonalisation (profiles/r06_qeig_reduction_L32.txt:
+//                 latency-bound, ~14-20 us per site for two dependent launches).
+//   rotations     k_q_rot: unit quaternions g_j per site make the
+//                 off-diagonal site blocks b_j sigma_z: T = [[A, C], [conj C,
+//                 -A]] with A = tridiag(a'; b) real and C = diag(d') complex.
+//   eigenvalues   k_q_bisect: G-lane multisection on block Sturm counts
+//                 (S_{j+1} = D_{j+1} - x - b_j^2 sigma_z S_j^-1 sigma_z, the
+//                 negative eigenvalues of each 2 x 2 S_j).
+//
+// Storage (one matrix; A column-major n x n, ld n): the particle rows of A
+// (rows < M) hold the reducing matrix; the reflector v_j is kept in the
+// bottom rows of columns 2j (particle entries, row M + site) and 2j + 1 (hole
+// entries), which the reduction never reads.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <cfloat>
+
+#include "dwhmc_device.h"
+#include "dwhmc_internal.h"
+
+namespace dwh {
+namespace {
+
+constexpr int kQTB = 64;     // pass tile: rows x columns
+constexpr int kQRS = 1024;   // k_q_rs threads
+constexpr int kQMaxR = 3;    // rows per k_q_rs thread: M <= kQMaxM
+}  // namespace
+constexpr int kQMaxM = kQRS * kQMaxR;
+namespace {
+
+__device__ __forceinline__ double2 cconj(double2 a) { return make_double2(a.x, -a.y); }
+__device__ __forceinline__ double2 cneg(double2 a) { return make_double2(-a.x, -a.y); }
+__device__ __forceinline__ double2 cscale(double s, double2 a) { return make_double2(s * a.x, s * a.y); }
+// a * conj(b) accumulated: acc + a conj(b)
+__device__ __forceinline__ double2 cmac_c(double2 acc, double2 a, double2 b) {
+  return make_double2(fma(a.x, b.x, fma(a.y, b.y, acc.x)), fma(a.y, b.x, fma(-a.x, b.y, acc.y)));
+}
+// acc + a b
+__device__ __forceinline__ double2 cmac(double2 acc, double2 a, double2 b) {
+  return make_double2(fma(a.x, b.x, fma(-a.y, b.y, acc.x)), fma(a.x, b.y, fma(a.y, b.x, acc.y)));
+}
+
+// Sum over a 16-lane DPP row, in every lane of the row (quad swaps, then the
+// half-row and row mirrors: no LDS traffic; a + b = b + a, so all 16 lanes
+// hold the same bits)
+__device__ __forceinline__ double dpp_sum16(double x) {
+  x += __builtin_amdgcn_update_dpp(x, x, 0xB1, 0xf, 0xf, true);    // quad_perm [1,0,3,2]
+  x += __builtin_amdgcn_update_dpp(x, x, 0x4E, 0xf, 0xf, true);    // quad_perm [2,3,0,1]
+  x += __builtin_amdgcn_update_dpp(x, x, 0x141, 0xf, 0xf, true);   // row_half_mirror
+  x += __builtin_amdgcn_update_dpp(x, x, 0x140, 0xf, 0xf, true);   // row_mirror
+  return x;
+}
+// wave total (uniform): the four row sums in a fixed order
+__device__ __forceinline__ double dpp_wave_sum(double x) {
+  x = dpp_sum16(x);
+  return (readlane_f64(x, 0) + readlane_f64(x, 16)) + (readlane_f64(x, 32) + readlane_f64(x, 48));
+}
+// v_permlane32_swap (W = 32: lanes 32-63 of a <-> lanes 0-31 of b) or
+// v_permlane16_swap (W = 16: the odd 16-lane rows of a <-> the even rows of
+// b) on both dwords of a pair of doubles: afterwards a + b holds, in the
+// lanes whose bit log2(W) is clear, a summed with its partner lane and, in
+// the others, b summed with its partner
+template <int W>
+__device__ __forceinline__ void perm_swap(double& a, double& b) {
+  uint2 ua = __builtin_bit_cast(uint2, a), ub = __builtin_bit_cast(uint2, b);
+  if constexpr (W == 32) {
+    const auto r0 = __builtin_amdgcn_permlane32_swap(ua.x, ub.x, false, false);
+    const auto r1 = __builtin_amdgcn_permlane32_swap(ua.y, ub.y, false, false);
+    ua = make_uint2(r0[0], r1[0]);
+    ub = make_uint2(r0[1], r1[1]);
+  } else {
+    const auto r0 = __builtin_amdgcn_permlane16_swap(ua.x, ub.x, false, false);
+    const auto r1 = __builtin_amdgcn_permlane16_swap(ua.y, ub.y, false, false);
+    ua = make_uint2(r0[0], r1[0]);
+    ub = make_uint2(r0[1], r1[1]);
+  }
+  a = __builtin_bit_cast(double, ua);
+  b = __builtin_bit_cast(double, ub);
+}
+
+// workgroup totals of three values (fixed order; every thread returns them).
+// One barrier: sh must not be reused by the previous reduction of the kernel.
+__device__ __forceinline__ void block_sum3(double& a, double& b, double& c, double (*sh)[3]) {
+  a = dpp_wave_sum(a);
+  b = dpp_wave_sum(b);
+  c = dpp_wave_sum(c);
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sh[w][0] = a;
+    sh[w][1] = b;
+    sh[w][2] = c;
+  }
+  __syncthreads();
+  a = b = c = 0.0;
+  for (int k = 0; k < nw; ++k) {
+    a += sh[k][0];
+    b += sh[k][1];
+    c += sh[k][2];
+  }
+}
+
+// Per-matrix scratch q of the reduction (doubles): P [M][4] as 64-bit fixed
+// point (p_p re, im, p_h re, im of p = H v, accumulated by k_q_pass with
+// integer atomics: exact, so the sum is the same bits in any order), the
+// fixed-point scale of each reflector [M], the Frobenius partials [256] and
+// ||H||_F.
+__host__ __device__ __forceinline__ int64_t q_scale_off(int M) { return 4 * (int64_t)M; }
+__host__ __device__ __forceinline__ int64_t q_fro_off(int M) { return 5 * (int64_t)M; }
+constexpr int kQFro = 256;   // k_q_fro workgroups
+
+// Diagnostic build only (-DQSTAMPS, tools/q_ab.sh): s_memrealtime (100 MHz)
+// of wave 0 at the phases of k_q_rs ([j][0..7]) and of k_q_pass's
+// workgroup 0 ([j][8..14]), the shader clock at k_q_rs's end ([j][15]);
+// read back by dwh_debug_qeig into $QSTAMPS_FILE.
+#ifdef QSTAMPS
+__device__ unsigned long long g_qst[4096][16];
+#define QSTAMP(cond, i)                                                    \
+  do {                                                                     \
+    unsigned long long t_ = __builtin_amdgcn_s_memrealtime();              \
+    asm volatile("" ::"s"(t_));                                            \
+    if ((cond) && threadIdx.x == 0 && j >= 0 && j < 4096) g_qst[j][i] = t_; \
+  } while (0)
+#else
+#define QSTAMP(cond, i) \
+  do {                  \
+  } while (0)
+#endif
+#define QST(i) QSTAMP(true, i)
+#define QSTP(i) QSTAMP(blockIdx.x == 0, 8 + (i))
+
+// Partial sums of |H_ij|^2 over the particle rows (all 2M columns): ||H||_F
+// bounds |(H v)_i| / |v| for every trailing block the reduction meets (the
+// similarity transforms keep the Frobenius norm), hence the fixed-point
+// scale of p.
+__global__ __launch_bounds__(256) void k_q_fro(const double2* __restrict__ A, int M, int64_t sA,
+                                               double* __restrict__ q, int64_t sQ) {
+  const int k = blockIdx.y, n = 2 * M;
+  A += k * sA;
+  double s = 0.0;
+  for (int c = blockIdx.x; c < n; c += kQFro)
+    for (int r = threadIdx.x; r < M; r += 256) {
+      const double2 a = A[r + (int64_t)c * n];
+      s += a.x * a.x + a.y * a.y;
+    }
+  __shared__ double sh[4][3];
+  double d1 = 0.0, d2 = 0.0;
+  block_sum3(s, d1, d2, sh);
+  if (threadIdx.x == 0) q[k * sQ + q_fro_off(M) + blockIdx.x] = s;
+}
+
+// Step j of the reduction for one matrix (blockIdx.x), j = -1 .. M-2:
+// (j >= 0) p = H v_j (P, from k_q_pass), r, c, w1_j (to W by site: W[s]
+// particle, W[M + s] hole); site j+1's columns updated with pair j; its
+// diagonal block (qa, qd); (j + 1 <= M - 2) the reflector v_{j+1}, tau, y and
+// its fixed-point scale.  j = -1 also forms ||H||_F from k_q_fro's partials.
+// Every load is issued first and every global store comes after the last
+// barrier (a barrier waits for the stores in flight).
+__global__ __launch_bounds__(kQRS) void k_q_rs(double2* __restrict__ A, int M, int j, int64_t sA,
+                                               double* __restrict__ q, int64_t sQ,
+                                               double2* __restrict__ W, double* __restrict__ tau,
+                                               double2* __restrict__ Y, double* __restrict__ qa,
+                                               double2* __restrict__ qd) {
+  const int k = blockIdx.x, n = 2 * M, t = threadIdx.x;
+  A += k * sA;
+  q += k * sQ;
+  long long* P = reinterpret_cast<long long*>(q);
+  W += (int64_t)k * n;
+  tau += (int64_t)k * M;
+  Y += (int64_t)k * 2 * M;
+  qa += (int64_t)k * M;
+  qd += (int64_t)k * M;
+  __shared__ double sh1[kQRS / 64][3], sh2[kQRS / 64][3];
+  __shared__ double2 bc[6];
+  const int s0 = j + 1;            // site j+1: the column pair reduced next
+  const int m = M - s0;            // active sites of step j (j >= 0), rows i <-> site s0 + i
+  const bool upd = j >= 0;
+  QST(0);
+  const double2 z = make_double2(0.0, 0.0);
+  double2 cp[kQMaxR], ch[kQMaxR];  // site s0's particle / hole column at row s0 + i (updated)
+  double2 pp[kQMaxR], ph[kQMaxR], vp[kQMaxR], vh[kQMaxR], wp[kQMaxR], wh[kQMaxR];
+  const double2* vpj = A + M + (int64_t)(2 * j) * n;       // v_j by site: particle
+  const double2* vhj = A + M + (int64_t)(2 * j + 1) * n;   // hole
+  // uniform values as vector loads (a scalar load is sunk to its use, after
+  // the first reduction: a second memory round trip)
+  int zv;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(zv));
+  const double tj = upd ? tau[j + zv] : 0.0;
+  const double isc = upd ? 1.0 / q[q_scale_off(M) + j + zv] : 0.0;
+  const double fro = upd ? q[q_fro_off(M) + kQFro + zv] : (t < kQFro ? q[q_fro_off(M) + t] : 0.0);
+#pragma unroll
+  for (int u = 0; u < kQMaxR; ++u) {
+    const int i = t + u * kQRS;
+    cp[u] = ch[u] = pp[u] = ph[u] = vp[u] = vh[u] = wp[u] = wh[u] = z;
+    if (i < m) {
+      cp[u] = A[(int64_t)(s0 + i) + (int64_t)s0 * n];
+      ch[u] = A[(int64_t)(s0 + i) + (int64_t)(M + s0) * n];
+      if (upd) {
+        const long long* ps = P + 4 * (int64_t)(s0 + i);
+        pp[u] = make_double2((double)ps[0] * isc, (double)ps[1] * isc);
+        ph[u] = make_double2((double)ps[2] * isc, (double)ps[3] * isc);
+        vp[u] = vpj[s0 + i];
+        vh[u] = vhj[s0 + i];
+      }
+    }
+  }
+  double hf = fro;
+  if (upd) {
+    double r = 0.0, cr = 0.0, ci = 0.0;
+#pragma unroll
+    for (int u = 0; u < kQMaxR; ++u) {
+      // r = v^H p; c = v^H Theta p, (Theta p)_p = -conj p_h, (Theta p)_h = conj p_p
+      r += vp[u].x * pp[u].x + vp[u].y * pp[u].y + vh[u].x * ph[u].x + vh[u].y * ph[u].y;
+      const double2 c1 = cmac_c(z, cneg(cconj(ph[u])), vp[u]);   // conj(vp) (-conj ph)
+      const double2 c2 = cmac_c(z, cconj(pp[u]), vh[u]);
+      cr += c1.x + c2.x;
+      ci += c1.y + c2.y;
+    }
+    QST(1);
+    // the row-0 entries (thread 0) published with this reduction's barrier
+    if (t == 0) {
+      bc[0] = vp[0];
+      bc[1] = vh[0];
+      bc[2] = pp[0];
+      bc[3] = ph[0];
+    }
+    block_sum3(r, cr, ci, sh1);
+    QST(2);
+    // w1 = tau p - tau^2 / 2 (r v - conj(c) Theta v), (Theta v)_p = -conj v_h, (Theta v)_h = conj v_p
+    const double h2 = 0.5 * tj * tj;
+    const double2 cc = make_double2(cr, -ci);
+    auto w1 = [&](double2 a_p, double2 a_h, double2 b_p, double2 b_h, double2& o_p, double2& o_h) {
+      // (a: v, b: p) -> (o_p, o_h) = w1
+      const double2 tvp = cneg(cconj(a_h)), tvh = cconj(a_p);
+      const double2 ap = cmac(cscale(r, a_p), cneg(cc), tvp), ah = cmac(cscale(r, a_h), cneg(cc), tvh);
+      o_p = make_double2(tj * b_p.x - h2 * ap.x, tj * b_p.y - h2 * ap.y);
+      o_h = make_double2(tj * b_h.x - h2 * ah.x, tj * b_h.y - h2 * ah.y);
+    };
+#pragma unroll
+    for (int u = 0; u < kQMaxR; ++u) w1(vp[u], vh[u], pp[u], ph[u], wp[u], wh[u]);
+    const double2 v0p = bc[0], v0h = bc[1];
+    double2 w0p, w0h;
+    w1(bc[0], bc[1], bc[2], bc[3], w0p, w0h);
+    QST(3);
+    // column s0 (particle, l = 0): v_l = v0p, w_l = w0p, tv_l = -conj v0h, tw_l = -conj w0h;
+    // column M + s0 (hole, l = m): v_l = v0h, w_l = w0h, tv_l = conj v0p, tw_l = conj w0p
+    const double2 Lv[2] = {v0p, v0h}, Lw[2] = {w0p, w0h};
+    const double2 Ltv[2] = {cneg(cconj(v0h)), cconj(v0p)}, Ltw[2] = {cneg(cconj(w0h)), cconj(w0p)};
+#pragma unroll
+    for (int u = 0; u < kQMaxR; ++u) {
+      const double2 tvr = cneg(cconj(vh[u])), twr = cneg(cconj(wh[u]));
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        double2 d = z;
+        d = cmac_c(d, vp[u], Lw[hh]);
+        d = cmac_c(d, wp[u], Lv[hh]);
+        d = cmac_c(d, cneg(tvr), Ltw[hh]);
+        d = cmac_c(d, cneg(twr), Ltv[hh]);
+        if (hh == 0) {
+          cp[u].x -= d.x;
+          cp[u].y -= d.y;
+        } else {
+          ch[u].x -= d.x;
+          ch[u].y -= d.y;
+        }
+      }
+    }
+  }
+  const bool refl = s0 <= M - 2;
+  // the reflector of site s0: x = rows i >= 1 (sites s0 + 1 ..): x_p = cp, x_h = conj ch
+  double nx = 0.0, sc = 0.0, tq = 0.0;
+  double2 yp = z, yh = z;
+  bool e1only = false;   // x1 = 0: v = x + |x| e_p (site s0 + 1)
+  if (refl || !upd) {
+    double nx2 = 0.0, d1 = 0.0;
+#pragma unroll
+    for (int u = 0; u < kQMaxR; ++u) {
+      const int i = t + u * kQRS;
+      if (i >= 1 && i < m) nx2 += cp[u].x * cp[u].x + cp[u].y * cp[u].y + ch[u].x * ch[u].x + ch[u].y * ch[u].y;
+    }
+    // x1: row i = 1 (thread 1), published with the norm's barrier
+    if (t == 1) {
+      bc[4] = cp[0];
+      bc[5] = cconj(ch[0]);
+    }
+    QST(4);
+    // j = -1: the Frobenius partials (k_q_fro) in the same reduction
+    double fsum = !upd && t < kQFro ? fro : 0.0;
+    block_sum3(nx2, fsum, d1, sh2);
+    if (!upd) hf = sqrt(fsum);
+    QST(5);
+    const double2 x1p = bc[4], x1h = bc[5];
+    nx = sqrt(nx2);
+    const double n1 = sqrt(x1p.x * x1p.x + x1p.y * x1p.y + x1h.x * x1h.x + x1h.y * x1h.y);
+    if (refl && nx > 0.0) {
+      if (n1 > 0.0) {
+        sc = nx / n1;
+        tq = 1.0 / (nx * (nx + n1));   // 2 / |v|^2, |v|^2 = 2 |x| (|x| + |x1|)
+        yp = cscale(-sc, x1p);
+        yh = cscale(-sc, x1h);
+      } else {
+        e1only = true;
+        tq = 1.0 / (nx * nx);
+        yp = make_double2(-nx, 0.0);
+      }
+    }
+  }
+  QST(6);
+  // the stores
+  if (t == 0) {   // site s0's diagonal block (row i = 0 of its columns)
+    qa[s0] = cp[0].x;
+    qd[s0] = ch[0];
+  }
+  double2* vpn = A + M + (int64_t)(2 * s0) * n;       // v_{s0} by site
+  double2* vhn = A + M + (int64_t)(2 * s0 + 1) * n;
+#pragma unroll
+  for (int u = 0; u < kQMaxR; ++u) {
+    const int i = t + u * kQRS;
+    if (i >= m) continue;
+    if (upd) {
+      W[s0 + i] = wp[u];
+      W[M + s0 + i] = wh[u];
+      long long* ps = P + 4 * (int64_t)(s0 + i);   // zeroed for the next pass's atomics
+      ps[0] = ps[1] = ps[2] = ps[3] = 0;
+    }
+    if (refl && i >= 1) {
+      double2 xp = cp[u], xh = cconj(ch[u]);
+      if (i == 1) {
+        if (e1only) {
+          xp.x += nx;
+        } else {
+          xp = cscale(1.0 + sc, xp);
+          xh = cscale(1.0 + sc, xh);
+        }
+      }
+      vpn[s0 + i] = nx > 0.0 ? xp : z;
+      vhn[s0 + i] = nx > 0.0 ? xh : z;
+    }
+  }
+  if (t == 0) {
+    if (!upd) q[q_fro_off(M) + kQFro] = hf;
+    if (refl) {
+      tau[s0] = tq;
+      Y[2 * s0] = yp;
+      Y[2 * s0 + 1] = yh;
+      // fixed-point scale of p = H v_{s0}: |p_i| <= ||H||_F |v| = ||H||_F sqrt(2 / tau) < 2^60 / scale
+      const double bnd = tq > 0.0 ? hf * sqrt(2.0 / tq) : 0.0;
+      q[q_scale_off(M) + s0] = bnd > 0.0 ? ldexp(1.0, 59 - ilogb(bnd)) : 1.0;
+    }
+  }
+  QST(7);
+#ifdef QSTAMPS
+  {
+    unsigned long long c_ = __builtin_amdgcn_s_memtime();   // shader clock: the clock rate from [7] / [15]
+    asm volatile("" ::"s"(c_));
+    if (threadIdx.x == 0 && j >= 0 && j < 4096) g_qst[j][15] = c_;
+  }
+#endif
+}
+
+__device__ __forceinline__ void q_tri_decode(int b, int& R, int& C) {
+  int r = (int)((sqrt(8.0 * b + 1.0) - 1.0) * 0.5);
+  while ((r + 1) * (r + 2) / 2 <= b) ++r;
+  while (r * (r + 1) / 2 > b) --r;
+  R = r;
+  C = b - r * (r + 1) / 2;
+}
+
+// Pass of step j (j = -1 .. M-3) over the sites s >= s1 = j+2: pair j applied
+// (j >= 0) to the lower triangles of h (particle rows x particle columns) and
+// of D (particle rows x hole columns, D = D^T) and written back, and p = H
+// v_{j+1} from the same tiles (the upper triangles by symmetry: h^H = h, D^T
+// = D):
+//   p_p = h v'_p + D v'_h,  p_h = conj(D) v'_p - conj(h) v'_h.
+// One workgroup of 16 waves per lower 64 x 64 tile (R, C) of h or of D (tiles
+// at fixed 64-site boundaries); lane = row, wave w the columns 4 w .. 4 w + 3
+// (four elements per thread: the waves hide each other's FP64 and LDS
+// latency).  Row sums through LDS; column sums by a lane transpose-reduce
+// (17 shuffles for 4 columns x 4 doubles).  Both go to P as 64-bit fixed
+// point (scale from k_q_rs) by integer atomics: exact in any order, so
+// bit-reproducible, and no separate partial-sum launch.
+constexpr int kQPW = 16;   // waves per pass workgroup
+__global__ __launch_bounds__(64 * kQPW) void k_q_pass(double2* __restrict__ A, int M, int j, int64_t sA,
+                                                      const double2* __restrict__ W, double* __restrict__ q,
+                                                      int64_t sQ) {
+  const int k = blockIdx.y, n = 2 * M, s1 = j + 2;
+  const int nT = (M + kQTB - 1) / kQTB, t0 = s1 / kQTB, nt = nT - t0, ntri = nt * (nt + 1) / 2;
+  const int type = (int)blockIdx.x >= ntri ? 1 : 0;   // 0: h, 1: D
+  int R, C;
+  q_tri_decode(blockIdx.x - type * ntri, R, C);
+  R += t0;
+  C += t0;
+  A += k * sA;
+  W += (int64_t)k * n;
+  q += k * sQ;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  QSTP(0);
+  const int sr = R * kQTB + lane;
+  const bool rok = sr >= s1 && sr < M;
+  const int64_t cb = type ? (int64_t)M * n : 0;   // D: columns M + s
+  // the tile (lower triangle), in flight while the vectors are staged
+  double2 a[4];
+  unsigned act = 0;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int sc = C * kQTB + 4 * w + u;
+    const bool ok = rok && sc >= s1 && sc <= sr;
+    act |= (unsigned)ok << u;
+    a[u] = ok ? A[cb + sr + (int64_t)sc * n] : make_double2(0.0, 0.0);
+  }
+  int zv;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(zv));
+  const double scale = q[q_scale_off(M) + j + 1 + zv];
+  // per column: v_l, w_l, tv_l, tw_l (pair j, by block type), v'_p, v'_h (v_{j+1})
+  __shared__ double2 cv[kQTB][6];
+  __shared__ double rowp[kQPW][kQTB][4];
+  __shared__ double colsum[kQTB][4];
+  const double2* vpj = A + M + (int64_t)(2 * j) * n;
+  const double2* vhj = A + M + (int64_t)(2 * j + 1) * n;
+  const double2* vpn = A + M + (int64_t)(2 * (j + 1)) * n;
+  const double2* vhn = A + M + (int64_t)(2 * (j + 1) + 1) * n;
+  const double2 z = make_double2(0.0, 0.0);
+  if (tid < kQTB) {
+    const int sc = C * kQTB + tid;
+    double2 v = z, wv = z, tv = z, tw = z, np = z, nh = z;
+    if (sc >= s1 && sc < M) {
+      if (j >= 0) {
+        const double2 vp = vpj[sc], vh = vhj[sc], wp = W[sc], wh = W[M + sc];
+        v = type ? vh : vp;
+        wv = type ? wh : wp;
+        tv = type ? cconj(vp) : cneg(cconj(vh));
+        tw = type ? cconj(wp) : cneg(cconj(wh));
+      }
+      np = vpn[sc];
+      nh = vhn[sc];
+    }
+    cv[tid][0] = v;
+    cv[tid][1] = wv;
+    cv[tid][2] = tv;
+    cv[tid][3] = tw;
+    cv[tid][4] = np;
+    cv[tid][5] = nh;
+  }
+  double2 vr = z, wr = z, tvr = z, twr = z, npr = z, nhr = z;
+  if (rok) {
+    if (j >= 0) {
+      vr = vpj[sr];
+      wr = W[sr];
+      tvr = cneg(cconj(vhj[sr]));
+      twr = cneg(cconj(W[M + sr]));
+    }
+    npr = vpn[sr];
+    nhr = vhn[sr];
+  }
+  __syncthreads();
+  QSTP(1);
+  double2 rp = z, rh = z;
+  double cs[16];   // column sums: [u][p_p re, im, p_h re, im]
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int cl = 4 * w + u;
+    double2 x = a[u];
+    const bool on = (act >> u) & 1;
+    if (on && j >= 0) {
+      double2 d = z;
+      d = cmac_c(d, vr, cv[cl][1]);
+      d = cmac_c(d, wr, cv[cl][0]);
+      d = cmac_c(d, cneg(tvr), cv[cl][3]);
+      d = cmac_c(d, cneg(twr), cv[cl][2]);
+      x.x -= d.x;
+      x.y -= d.y;
+      a[u] = x;   // stored after the barrier below (a barrier waits for stores in flight)
+    }
+    const double2 cnp = cv[cl][4], cnh = cv[cl][5];
+    const bool off = on && C * kQTB + cl < sr;   // strictly below the diagonal: also the transpose
+    double2 cpp, cph;
+    if (type == 0) {   // h: p_p += h v'_p, p_h -= conj(h) v'_h; transposed: conj(h) v'_p, -h v'_h
+      rp = cmac(rp, x, cnp);
+      rh = cmac(rh, cneg(cconj(x)), cnh);
+      cpp = cmac(z, cconj(x), npr);
+      cph = cmac(z, cneg(x), nhr);
+    } else {           // D: p_p += D v'_h, p_h += conj(D) v'_p; transposed: the same
+      rp = cmac(rp, x, cnh);
+      rh = cmac(rh, cconj(x), cnp);
+      cpp = cmac(z, x, nhr);
+      cph = cmac(z, cconj(x), npr);
+    }
+    cs[4 * u] = off ? cpp.x : 0.0;
+    cs[4 * u + 1] = off ? cpp.y : 0.0;
+    cs[4 * u + 2] = off ? cph.x : 0.0;
+    cs[4 * u + 3] = off ? cph.y : 0.0;
+  }
+  QSTP(2);
+  // column sums over the 64 lanes, transpose-reduce without LDS: each stage
+  // pairs lanes that differ in one index bit (v_permlane32 / 16_swap for
+  // bits 5 / 4, DPP row_mirror / row_half_mirror for bits 3 / 2) and halves
+  // the values a lane holds; lane l ends with value (l >> 2) & 15, summed
+  // over a quarter of the lanes, then the quad sums
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    perm_swap<32>(cs[i], cs[i + 8]);
+    cs[i] += cs[i + 8];
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    perm_swap<16>(cs[i], cs[i + 4]);
+    cs[i] += cs[i + 4];
+  }
+  {
+    const bool up3 = lane & 8, up2 = lane & 4;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const double send = up3 ? cs[i] : cs[i + 2], keep = up3 ? cs[i + 2] : cs[i];
+      cs[i] = keep + __builtin_amdgcn_update_dpp(send, send, 0x140, 0xf, 0xf, true);   // row_mirror
+    }
+    const double send = up2 ? cs[0] : cs[1], keep = up2 ? cs[1] : cs[0];
+    cs[0] = keep + __builtin_amdgcn_update_dpp(send, send, 0x141, 0xf, 0xf, true);     // row_half_mirror
+  }
+  cs[0] += __builtin_amdgcn_update_dpp(cs[0], cs[0], 0xB1, 0xf, 0xf, true);   // quad_perm [1,0,3,2]
+  cs[0] += __builtin_amdgcn_update_dpp(cs[0], cs[0], 0x4E, 0xf, 0xf, true);   // quad_perm [2,3,0,1]
+  QSTP(3);
+  if ((lane & 3) == 0) {
+    const int vi = (lane >> 2) & 15;
+    colsum[4 * w + (vi >> 2)][vi & 3] = cs[0];
+  }
+  rowp[w][lane][0] = rp.x;
+  rowp[w][lane][1] = rp.y;
+  rowp[w][lane][2] = rh.x;
+  rowp[w][lane][3] = rh.y;
+  __syncthreads();
+  QSTP(4);
+  if (j >= 0) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if ((act >> u) & 1) A[cb + sr + (int64_t)(C * kQTB + 4 * w + u) * n] = a[u];
+  }
+  QSTP(5);
+  if (tid < 4 * kQTB) {
+    const int so = tid >> 2, e = tid & 3;
+    double rv = 0.0;
+#pragma unroll
+    for (int ww = 0; ww < kQPW; ++ww) rv += rowp[ww][so][e];
+    const double cvs = colsum[so][e];
+    unsigned long long* P = reinterpret_cast<unsigned long long*>(q);
+    const int srs = R * kQTB + so, scs = C * kQTB + so;
+    auto fx = [&](double x) { return (unsigned long long)__double2ll_rn(x * scale); };
+    if (R == C) {
+      if (srs < M && srs >= s1) atomicAdd(&P[(int64_t)srs * 4 + e], fx(rv + cvs));
+    } else {
+      if (srs < M && srs >= s1) atomicAdd(&P[(int64_t)srs * 4 + e], fx(rv));
+      if (scs < M && scs >= s1) atomicAdd(&P[(int64_t)scs * 4 + e], fx(cvs));
+    }
+  }
+  QSTP(6);
+}
+
+// quaternion product of unit quaternions (al, be) <-> [[al, -conj be], [be, conj al]]
+__device__ __forceinline__ void qmul(double2 a1, double2 b1, double2 a2, double2 b2, double2& a, double2& b) {
+  // al = a1 a2 - conj(b1) b2, be = b1 a2 + conj(a1) b2
+  a = make_double2(a1.x * a2.x - a1.y * a2.y - (b1.x * b2.x + b1.y * b2.y),
+                   a1.x * a2.y + a1.y * a2.x - (b1.x * b2.y - b1.y * b2.x));
+  b = make_double2(b1.x * a2.x - b1.y * a2.y + (a1.x * b2.x + a1.y * b2.y),
+                   b1.x * a2.y + b1.y * a2.x + (a1.x * b2.y - a1.y * b2.x));
+}
+
+// Site rotations (one thread per matrix): g_0 = 1, g_{j+1} = q_j g~_j / |q_j|
+// (q_j = quat(y_p, y_h), g~ = sigma_z g sigma_z = quat(al, -be)); the rotated
+// diagonal blocks g^H [[a, d], [conj d, -a]] g -> (qa', qd'), b_j = |q_j|.
+// g stored as (al, be) per site in G[2 s], G[2 s + 1].
+__global__ void k_q_rot(const double* __restrict__ qa, const double2* __restrict__ qd,
+                        const double2* __restrict__ Y, int M, double* __restrict__ ra, double2* __restrict__ rd,
+                        double* __restrict__ rb, double2* __restrict__ G, int m) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= m) return;
+  qa += (int64_t)k * M;
+  qd += (int64_t)k * M;
+  Y += (int64_t)k * 2 * M;
+  ra += (int64_t)k * M;
+  rd += (int64_t)k * M;
+  rb += (int64_t)k * M;
+  G += (int64_t)k * 2 * M;
+  double2 al = make_double2(1.0, 0.0), be = make_double2(0.0, 0.0);
+  for (int s = 0; s < M; ++s) {
+    G[2 * s] = al;
+    G[2 * s + 1] = be;
+    // D' = g^H D g, g = [[al, -conj be], [be, conj al]], D = [[a, d], [conj d, -a]]
+    const double a = qa[s];
+    const double2 d = qd[s];
+    // D g columns: c0 = D (al; be), c1 = D (-conj be; conj al)
+    const double2 c00 = make_double2(a * al.x + (d.x * be.x - d.y * be.y), a * al.y + (d.x * be.y + d.y * be.x));
+    const double2 c10 = make_double2((d.x * al.x + d.y * al.y) - a * be.x, (d.x * al.y - d.y * al.x) - a * be.y);
+    const double2 nbe = make_double2(-be.x, be.y), cal = make_double2(al.x, -al.y);   // -conj be, conj al
+    const double2 c01 = make_double2(a * nbe.x + (d.x * cal.x - d.y * cal.y), a * nbe.y + (d.x * cal.y + d.y * cal.x));
+    const double2 c11 = make_double2((d.x * nbe.x + d.y * nbe.y) - a * cal.x, (d.x * nbe.y - d.y * nbe.x) - a * cal.y);
+    // row 0 of g^H = (conj al, conj be): D'00 = conj(al) c00 + conj(be) c10, D'01 = conj(al) c01 + conj(be) c11
+    ra[s] = (al.x * c00.x + al.y * c00.y) + (be.x * c10.x + be.y * c10.y);
+    rd[s] = make_double2((al.x * c01.x + al.y * c01.y) + (be.x * c11.x + be.y * c11.y),
+                         (al.x * c01.y - al.y * c01.x) + (be.x * c11.y - be.y * c11.x));
+    if (s + 1 < M) {
+      const double2 yp = Y[2 * s], yh = Y[2 * s + 1];
+      const double nq = sqrt(yp.x * yp.x + yp.y * yp.y + yh.x * yh.x + yh.y * yh.y);
+      rb[s] = nq;
+      const double2 ta = al, tb = make_double2(-be.x, -be.y);   // g~ = quat(al, -be)
+      if (nq > 0.0) {
+        double2 na, nb;
+        qmul(yp, yh, ta, tb, na, nb);
+        al = make_double2(na.x / nq, na.y / nq);
+        be = make_double2(nb.x / nq, nb.y / nq);
+      } else {
+        al = ta;
+        be = tb;
+      }
+    } else {
+      rb[s] = 0.0;
+    }
+  }
+}
+
+// Eigenvalues of T by G-lane multisection on block Sturm counts (as
+// k_eig_bisect): S_0 = D_0 - x, S_{s+1} = D_{s+1} - x - b_s^2 sigma_z S_s^-1
+// sigma_z; S = [[p, q], [conj q, r]] contributes 1 negative eigenvalue when
+// det < 0, 2 when det > 0 and p < 0.  A determinant below pivmin = (eps
+// ||T||)^2 is replaced by -pivmin (keeps b^2 / det and the next determinant
+// finite).  LDS: a' [0, M), d' [M, 3M) (re, im), b^2 [3M, 4M).
+constexpr int kQBisW = 8;
+__global__ __launch_bounds__(64 * kQBisW) void k_q_bisect(const double* __restrict__ ra, const double2* __restrict__ rd,
+                                                          const double* __restrict__ rb, int M, int lgG,
+                                                          double* __restrict__ E, double* __restrict__ tnorm) {
+  extern __shared__ double lds[];
+  const int k = blockIdx.y, lane = threadIdx.x & 63, n = 2 * M;
+  ra += (int64_t)k * M;
+  rd += (int64_t)k * M;
+  rb += (int64_t)k * M;
+  E += (int64_t)k * n;
+  __shared__ double shn[kQBisW];
+  double tl = 0.0;
+  for (int s = threadIdx.x; s < M; s += blockDim.x) {
+    const double a = ra[s];
+    const double2 d = rd[s];
+    const double bl = s > 0 ? rb[s - 1] : 0.0, br = s + 1 < M ? rb[s] : 0.0;
+    lds[s] = a;
+    lds[M + 2 * s] = d.x;
+    lds[M + 2 * s + 1] = d.y;
+    lds[3 * M + s] = br * br;
+    tl = fmax(tl, fabs(a) + sqrt(d.x * d.x + d.y * d.y) + fabs(bl) + fabs(br));
+  }
+  for (int off = 32; off > 0; off >>= 1) tl = fmax(tl, __shfl_xor(tl, off, 64));
+  if (lane == 0) shn[threadIdx.x >> 6] = tl;
+  __syncthreads();
+  double tn = 0.0;
+  for (int w = 0; w < kQBisW; ++w) tn = fmax(tn, shn[w]);
+  if (blockIdx.x == 0 && threadIdx.x == 0) tnorm[k] = tn;
+  const double gl = -tn * (1.0 + 4.0 * DBL_EPSILON) - 1e-300, gu = tn * (1.0 + 4.0 * DBL_EPSILON) + 1e-300;
+  const double pivmin = (DBL_EPSILON * tn) * (DBL_EPSILON * tn) + DBL_MIN;
+  const int G = 1 << lgG, g0 = lane & ~(G - 1), gi = lane & (G - 1);
+  const int j = ((blockIdx.x * kQBisW + (threadIdx.x >> 6)) << (6 - lgG)) + (lane >> lgG);
+  if (((blockIdx.x * kQBisW + (threadIdx.x >> 6)) << (6 - lgG)) >= n) return;
+  const unsigned long long gmask = G == 64 ? ~0ull : ((1ull << G) - 1);
+  const double step = 1.0 / (G + 1);
+  double lo = gl, hi = gu;
+  bool done = j >= n;
+  for (int it = 0; it < 256; ++it) {
+    const double mid = 0.5 * (lo + hi);
+    if (mid <= lo || mid >= hi) done = true;
+    if (__ballot(!done) == 0) break;
+    const double x = fmin(lo + (gi + 1) * ((hi - lo) * step), hi);
+    double p = lds[0] - x, qr = lds[M], qi = lds[M + 1], r = -lds[0] - x;
+    int c = 0;
+    for (int s = 0; s < M; ++s) {
+      double det = p * r - (qr * qr + qi * qi);
+      if (fabs(det) < pivmin) det = -pivmin;
+      c += det < 0.0 ? 1 : (p < 0.0 ? 2 : 0);
+      if (s + 1 < M) {
+        const double r0 = __builtin_amdgcn_rcp(det);
+        const double rq = fma(r0, fma(-det, r0, 1.0), r0);
+        const double f = lds[3 * M + s] * rq;
+        const double a1 = lds[s + 1];
+        const double np = (a1 - x) - f * r, nr = (-a1 - x) - f * p;
+        qr = lds[M + 2 * (s + 1)] - f * qr;
+        qi = lds[M + 2 * (s + 1) + 1] - f * qi;
+        p = np;
+        r = nr;
+      }
+    }
+    const unsigned long long above = (__ballot(c > j) >> g0) & gmask;
+    const int f = above ? __builtin_ctzll(above) : G;
+    const double xf = __shfl(x, g0 + (f < G ? f : G - 1), 64), xp = __shfl(x, g0 + (f > 0 ? f - 1 : 0), 64);
+    const double nlo = f > 0 ? xp : lo, nhi = f < G ? xf : hi;
+    if (nlo == lo && nhi == hi) done = true;
+    if (!done) {
+      lo = nlo;
+      hi = nhi;
+    }
+  }
+  if (gi == 0 && j < n) E[j] = 0.5 * (lo + hi);
+}
+
+}  // namespace
+
+#ifdef QSTAMPS
+int q_stamps_read(unsigned long long* out, int nsteps) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_qst), (size_t)nsteps * 16 * sizeof(unsigned long long)) == hipSuccess ? 0 : 1;
+}
+#endif
+
+bool q_supported(int M) { return M >= 1 && M <= kQMaxM; }
+
+// the per-matrix scratch in double2 units
+int q_part_elems(int M) { return (int)((q_fro_off(M) + kQFro + 2) / 2); }
+
+void launch_q_reduce(double2* A, int M, int64_t sA, double2* part, int64_t sP, double2* W, double* tau, double2* Y,
+                     double* qa, double2* qd, int m, hipStream_t s) {
+  if (M < 1 || M > kQMaxM) return;   // callers check q_supported(M)
+  double* q = reinterpret_cast<double*>(part);
+  const int64_t sQ = 2 * sP;
+  const int nT = (M + kQTB - 1) / kQTB;
+  (void)hipMemset2DAsync(q, (size_t)sQ * sizeof(double), 0, (size_t)4 * M * sizeof(double), m, s);   // P
+  hipLaunchKernelGGL(k_q_fro, dim3(kQFro, m), dim3(256), 0, s, A, M, sA, q, sQ);
+  for (int j = -1; j <= M - 2; ++j) {
+    hipLaunchKernelGGL(k_q_rs, dim3(m), dim3(kQRS), 0, s, A, M, j, sA, q, sQ, W, tau, Y, qa, qd);
+    if (j <= M - 3) {
+      const int nt = nT - (j + 2) / kQTB;
+      hipLaunchKernelGGL(k_q_pass, dim3(nt * (nt + 1), m), dim3(64 * kQPW), 0, s, A, M, j, sA, W, q, sQ);
+    }
+  }
+}
+
+void launch_q_rot(const double* qa, const double2* qd, const double2* Y, int M, double* ra, double2* rd, double* rb,
+                  double2* G, int m, hipStream_t s) {
+  hipLaunchKernelGGL(k_q_rot, dim3((m + 63) / 64), dim3(64), 0, s, qa, qd, Y, M, ra, rd, rb, G, m);
+}
+
+void launch_q_bisect(const double* ra, const double2* rd, const double* rb, int M, double* E, double* tnorm, int m,
+                     hipStream_t s) {
+  const int n = 2 * M;
+  int lgG = 6;
+  while (lgG > 2 && ((int64_t)m * n << (lgG - 1)) >= (int64_t)2048 * 64) --lgG;
+  const int per_wg = kQBisW << (6 - lgG);
+  hipLaunchKernelGGL(k_q_bisect, dim3((n + per_wg - 1) / per_wg, m), dim3(64 * kQBisW), 4 * M * sizeof(double), s,
+                     ra, rd, rb, M, lgG, E, tnorm);
+}
+
+}  // namespace dwh

@@ -283,6 +283,12 @@ int dwh_measure_transport_deltas(dwh_ctx* ctx, int64_t chain, int64_t nstates, c
  * assembly launch on the device Δ; refill == 0 reads the pool as the last
  * trajectory step left it (Δ/2 scattered by the force kernel). */
 int dwh_debug_dense_H(dwh_ctx* ctx, int64_t chain, dwh_c128* H);
+
+/* Development entry of the structure-preserving (quaternion) eigensolver
+ * (dwhmc_qeig.hip, tools/qeig_proto.py): the 2N eigenvalues of H_BdG(Δ of
+ * `chain`) ascending into E, the site-by-site reduction's device time into
+ * *ms (nullable). */
+int dwh_debug_qeig(dwh_ctx* ctx, int64_t chain, double* E, double* ms);
 int dwh_debug_level0(dwh_ctx* ctx, int64_t chain, int64_t pole, int32_t refill, dwh_c128* M, double* y);
 
 /* Host-only check of the cyclic-reduction schedule dwh_create builds for an
