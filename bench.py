@@ -46,12 +46,12 @@ METRIC = "fp64 leapfrog steps/sec at L=32, 1→8 MI355X; % fp64 MFMA roofline"
 PEAK_F64_TFLOPS = 78.6        # MI355X dense fp64 matrix peak (= fp64 vector peak on CDNA4)
 PEAK_HBM_GBS = 8000.0         # MI355X HBM3E peak (MI355X_MICROARCH.md)
 # newest committed PMC summary first (profiles/README.md)
-TRAFFIC_FILES = [os.path.join(ROOT, "profiles", f) for f in ("r05_pmc_traffic.json", "r04_pmc_traffic.json", "r03_pmc_traffic.json", "r02_pmc_traffic.json",
+TRAFFIC_FILES = [os.path.join(ROOT, "profiles", f) for f in ("r06_pmc_traffic.json", "r05_pmc_traffic.json", "r04_pmc_traffic.json", "r03_pmc_traffic.json", "r02_pmc_traffic.json",
                                                                      "r01_pmc_traffic.json")]
 # SQ counter passes (tools/pmc_sq.sh -> tools/pmc_mfma.py): executed MFMA work per launch
-MFMA_FILES = [os.path.join(ROOT, "profiles", f) for f in ("r05_sq_mfma_L32.json", "r04_sq_mfma_L32.json")]
+MFMA_FILES = [os.path.join(ROOT, "profiles", f) for f in ("r06_sq_mfma_L32.json", "r05_sq_mfma_L32.json", "r04_sq_mfma_L32.json")]
 # rocprofv3 --kernel-trace --stats summaries of the driver's command (tools/profile_round.sh)
-KSTATS_FILES = {(32, 16.0, 1): [os.path.join(ROOT, "profiles", f) for f in ("r05_L32_beta16_kernel_stats.csv",)]}
+KSTATS_FILES = {(32, 16.0, 1): [os.path.join(ROOT, "profiles", f) for f in ("r06_L32_beta16_kernel_stats.csv", "r05_L32_beta16_kernel_stats.csv")]}
 CLOCK_GHZ = 2.4                # the clock PEAK_F64_TFLOPS is quoted at (1024 SIMDs x 32 flop/cycle)
 ASSEMBLY_REPS = 200            # warm assembly launches timed for `assembly`
 
