@@ -43,7 +43,7 @@ class dwh_info_t(C.Structure):
                 ("kappa", C.c_double), ("e_bound", C.c_double), ("err_tanh", C.c_double),
                 ("delta_cap", C.c_double), ("device_bytes", C.c_int64), ("algo", C.c_int64),
                 ("block", C.c_int64), ("eig_half", C.c_int64),
-                ("eig_long_clusters", C.c_int64)]
+                ("eig_long_clusters", C.c_int64), ("eig_quat", C.c_int64)]
 
 
 _P = C.c_void_p

@@ -1105,8 +1105,13 @@ struct dwh_ctx {
   bool eig_ph = false;
   int64_t eig_long_clusters = 0;   // clusters longer than k_eig_orth's limit, orthonormalised by long_clusters
   int eig_ph_last = -1;    // dwh_info_t::eig_half: eig_ph of the last eigensolve (-1: none yet)
+  int eig_quat_last = 0;   // the last eigensolve took the structure-preserving solver
   double *d_eig_d = nullptr, *d_eig_e = nullptr, *d_eig_tn = nullptr;
-  double* d_q = nullptr;   // structure-preserving eigenvalue solver (dwhmc_qeig.hip) workspace, one matrix
+  // structure-preserving solver (dwhmc_qeig.hip) workspace: q_slots matrices
+  // (q_bufs), the eigenvector stage's for q_vec_slots (q_heev_enqueue)
+  double* d_q = nullptr;
+  int q_slots = 0, q_vec_slots = 0;
+  double2 *d_qz = nullptr, *d_qs = nullptr, *d_qg = nullptr;
   hipStream_t eig_sx[3] = {};       // extra streams of the sub-batched tridiagonalisation
   hipEvent_t eig_ev[4] = {};
 
@@ -2394,15 +2399,16 @@ int long_clusters(dwh_ctx* ctx, const std::vector<double>& Eh, const std::vector
 // sub-batch streams of own_heev_enqueue's tridiagonalisation (default / most)
 constexpr int kEigStreams = 2, kEigStreamsMax = 4;
 
-int own_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m) {
+// back-transform: W = V^H U is only NB x n, so with fewer than 4 matrices its
+// K range is split into up to kEigKS chunks (one batched zgemm per matrix)
+constexpr int kEigKS = 8;
+
+// the own eigensolver's per-matrix workspace for m matrices (both solvers)
+int eig_scratch(dwh_ctx* ctx, int m) {
   const int N = ctx->d.N, n = 2 * N;
-  const dwh::TrBufs& b = ctx->tr;
-  const int64_t sA = (int64_t)n * n, sZ = 2 * sA;   // sZ in doubles
   const int T = (n + dwh::kEigTB - 1) / dwh::kEigTB, NB = dwh::kEigNB;
   const int nblk = std::max(1, (n - 1 + NB - 1) / NB);
-  // back-transform: W = V^H U is only NB x n, so with fewer than 4 matrices
-  // its K range is split into up to KS chunks (one batched zgemm per matrix)
-  constexpr int KS = 8;
+  constexpr int KS = kEigKS;
   const int64_t sP = (int64_t)T * n, sT = (int64_t)nblk * NB * NB, sW = (int64_t)NB * n;
   int rc;
   if (m > ctx->eig_slots) {
@@ -2425,6 +2431,60 @@ int own_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m) {
       return rc;
     ctx->eig_slots = m;
   }
+  return DWH_OK;
+}
+
+// U = (I - V_0 T_0 V_0^H) ... (I - V_last T_last V_last^H) U on the columns
+// j0.. of the slots' U: the reflectors' V (n x n per matrix, column c = v_c
+// on the rows > c, zeros above) and complex tau (ctx->d_eig_tau), V^H block
+// by block into Vt (an n x n slot buffer); the library's own products
+// (dwhmc_gemm.hip)
+int eig_back_transform(dwh_ctx* ctx, const double2* V, double2* Vt, int j0, int m) {
+  const int N = ctx->d.N, n = 2 * N, NB = dwh::kEigNB;
+  const dwh::TrBufs& b = ctx->tr;
+  const int64_t sA = (int64_t)n * n;
+  const int nblk = std::max(1, (n - 1 + NB - 1) / NB);
+  const int64_t sT = (int64_t)nblk * NB * NB, sW = (int64_t)NB * n;
+  const int M = n - j0;
+  hipStream_t s = ctx->stream;
+  dwh::launch_eig_tfac(V, n, sA, ctx->d_eig_tau, ctx->d_eig_W, ctx->d_eig_T, sT, m, s);   // W as Gram scratch
+  HIPCHECK(ctx, hipGetLastError());
+  const double2 one = make_double2(1.0, 0.0), zero = make_double2(0.0, 0.0), mone = make_double2(-1.0, 0.0);
+  const int ks = m >= 4 ? 1 : kEigKS;
+  const int64_t sWs = ks * sW;
+  const int ldv = std::min(NB, n - 1);   // as k_eig_vt lays the blocks out
+  dwh::launch_eig_vt(V, n, sA, Vt, m, s);
+  for (int blk = nblk - 1; blk >= 0; --blk) {
+    const int r0 = blk * NB, kb = std::min(NB, n - 1 - r0), ms = n - r0 - 1;
+    const double2* Vb = V + (r0 + 1) + (int64_t)r0 * n;
+    double2* Us = b.U + (r0 + 1) + (int64_t)j0 * n;
+    const int ldw = ks * NB;
+    // W = V^H U in K chunks of c rows (a multiple of 16, the last one shorter),
+    // chunk s at rows s kb of W: one launch for every (matrix, chunk)
+    const int c = ks == 1 ? ms : std::max(16, ((ms + ks - 1) / ks + 15) / 16 * 16);
+    const int nfull = ms / c, rem = ms - nfull * c, S = nfull + (rem > 0);
+    dwh::gemm_z_chunked('N', 'N', kb, M, c, rem > 0 ? rem : c, S, one, Vt + (int64_t)r0 * n, ldv, (int64_t)c * ldv, sA,
+                        Us, n, c, sA, zero, ctx->d_eig_W, ldw, kb, sWs, m, s);
+    if (S == 1)   // W2 = T W on the MFMA (4x faster than k_eig_tw's LDS MACs at 16 matrices)
+      dwh::gemm_z('N', 'N', kb, M, kb, one, ctx->d_eig_T + (int64_t)blk * NB * NB, NB, sT, ctx->d_eig_W, ldw, sWs,
+                  zero, ctx->d_eig_W2, NB, sW, m, s);
+    else
+      dwh::launch_eig_tw(ctx->d_eig_T + (int64_t)blk * NB * NB, sT, ctx->d_eig_W, ldw, sWs, S, kb, M,
+                         ctx->d_eig_W2, sW, m, s);
+    dwh::gemm_z('N', 'N', ms, M, kb, mone, Vb, n, sA, ctx->d_eig_W2, NB, sW, one, Us, n, sA, m, s);
+  }
+  HIPCHECK(ctx, hipGetLastError());
+  return DWH_OK;
+}
+
+int own_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m) {
+  const int N = ctx->d.N, n = 2 * N;
+  const dwh::TrBufs& b = ctx->tr;
+  const int64_t sA = (int64_t)n * n, sZ = 2 * sA;   // sZ in doubles
+  const int T = (n + dwh::kEigTB - 1) / dwh::kEigTB;
+  const int64_t sP = (int64_t)T * n;
+  int rc;
+  if ((rc = eig_scratch(ctx, m))) return rc;
   hipStream_t s = ctx->stream;
   double2* A = b.JU;
   EigPhase ph(s);
@@ -2539,36 +2599,8 @@ int own_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m) {
   HIPCHECK(ctx, hipGetLastError());
   ph.mark("lowdin");
   if (n < 2) return DWH_OK;
-  dwh::launch_eig_tfac(A, n, sA, ctx->d_eig_tau, ctx->d_eig_W, ctx->d_eig_T, sT, m, s);   // W as Gram scratch
-  HIPCHECK(ctx, hipGetLastError());
-  // U = (I - V_0 T_0 V_0^H) ... (I - V_last T_last V_last^H) Z, last block first,
-  // on the library's own products (dwhmc_gemm.hip), columns j0.. only
-  const double2 one = make_double2(1.0, 0.0), zero = make_double2(0.0, 0.0), mone = make_double2(-1.0, 0.0);
-  const int ks = m >= 4 ? 1 : KS;
-  const int64_t sWs = ks * sW;
   // V^H block by block into the slots' Jmn buffers (free after the Löwdin step)
-  double2* Vt = b.Jmn;
-  const int ldv = std::min(NB, n - 1);   // as k_eig_vt lays the blocks out
-  dwh::launch_eig_vt(A, n, sA, Vt, m, s);
-  for (int blk = nblk - 1; blk >= 0; --blk) {
-    const int r0 = blk * NB, kb = std::min(NB, n - 1 - r0), ms = n - r0 - 1;
-    const double2* Vb = A + (r0 + 1) + (int64_t)r0 * n;
-    double2* Us = b.U + (r0 + 1) + (int64_t)j0 * n;
-    const int ldw = ks * NB;
-    // W = V^H U in K chunks of c rows (a multiple of 16, the last one shorter),
-    // chunk s at rows s kb of W: one launch for every (matrix, chunk)
-    const int c = ks == 1 ? ms : std::max(16, ((ms + ks - 1) / ks + 15) / 16 * 16);
-    const int nfull = ms / c, rem = ms - nfull * c, S = nfull + (rem > 0);
-    dwh::gemm_z_chunked('N', 'N', kb, M, c, rem > 0 ? rem : c, S, one, Vt + (int64_t)r0 * n, ldv, (int64_t)c * ldv, sA,
-                        Us, n, c, sA, zero, ctx->d_eig_W, ldw, kb, sWs, m, s);
-    if (S == 1)   // W2 = T W on the MFMA (4x faster than k_eig_tw's LDS MACs at 16 matrices)
-      dwh::gemm_z('N', 'N', kb, M, kb, one, ctx->d_eig_T + (int64_t)blk * NB * NB, NB, sT, ctx->d_eig_W, ldw, sWs,
-                  zero, ctx->d_eig_W2, NB, sW, m, s);
-    else
-      dwh::launch_eig_tw(ctx->d_eig_T + (int64_t)blk * NB * NB, sT, ctx->d_eig_W, ldw, sWs, S, kb, M,
-                         ctx->d_eig_W2, sW, m, s);
-    dwh::gemm_z('N', 'N', ms, M, kb, mone, Vb, n, sA, ctx->d_eig_W2, NB, sW, one, Us, n, sA, m, s);
-  }
+  if ((rc = eig_back_transform(ctx, A, b.Jmn, j0, m))) return rc;
   if (half) dwh::launch_eig_theta(b.U, n, sA, ctx->d_eig_c0, m, s);
   ph.mark("backtransform");
   HIPCHECK(ctx, hipGetLastError());
@@ -2597,6 +2629,8 @@ int eigen_enqueue(dwh_ctx* ctx, const TrSrc& src, int m, bool qr) {
   return DWH_OK;
 }
 
+int q_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m, bool* done);
+
 // The library's own eigensolver for every order up to kEigMaxN; rocSOLVER only
 // beyond it (zheevd) and as the re-solve (QR-iteration zheev) of a solve that
 // left a non-finite value: rocSOLVER's zheevd returns NaN eigenvectors for
@@ -2614,7 +2648,14 @@ int eigen_solve(dwh_ctx* ctx, const TrSrc& src, int m) {
     // rocSOLVER zheev only if it flagged or produced non-finite values
     HIPCHECK(ctx, hipMemsetAsync(ctx->d_tr_info, 0, m * sizeof(int), ctx->stream));
     Scope sc(ctx, T_EIG_OWN, m);
-    rc = own_heev_enqueue(ctx, src, m);
+    // the structure-preserving solver first (DWHMC_EIG_QUAT=0: the one-stage
+    // solver only, A/B); it declines spectra with clusters or crowding at zero
+    bool done = false;
+    const char* qe = std::getenv("DWHMC_EIG_QUAT");
+    if (dwh::q_supported(ctx->d.N) && !(qe && *qe == '0')) rc = q_heev_enqueue(ctx, src, m, &done);
+    else rc = DWH_OK;
+    if (!rc && !done) rc = own_heev_enqueue(ctx, src, m);
+    ctx->eig_quat_last = done ? 1 : 0;
   } else {
     Scope sc(ctx, T_EIG_VENDOR, m);
     rc = eigen_enqueue(ctx, src, m, false);
@@ -2715,6 +2756,161 @@ int transport_run(dwh_ctx* ctx, const TrSrc& src, int m, double eta, double dome
   return DWH_OK;
 }
 
+// Workspace of the structure-preserving solver (dwhmc_qeig.hip) for q_slots
+// matrices, one array per quantity (the kernels' per-matrix strides):
+// reduction scratch, w, y, the diagonal blocks before / after the site
+// rotations, the rotations, tau, ||T||; for the eigenvectors (q_vec_slots
+// matrices, nv = N columns): Zt (n x nv), the inverse iteration's LU
+// scratch, the Löwdin Gram matrix (nv x nv).
+struct QBufs {
+  double2 *part, *W, *Y, *qd, *rd, *G;
+  double *tau, *qa, *ra, *rb, *tn;
+  int64_t sP;
+};
+QBufs q_bufs(dwh_ctx* ctx) {
+  const int M = ctx->d.N, n = 2 * M, m = ctx->q_slots;
+  const int64_t sP = dwh::q_part_elems(M);
+  double* w = ctx->d_q;
+  QBufs q;
+  q.sP = sP;
+  int64_t o = 0;   // doubles
+  auto take2 = [&](int64_t per) { double2* p = reinterpret_cast<double2*>(w + o); o += 2 * per * m; return p; };
+  auto take1 = [&](int64_t per) { double* p = w + o; o += per * m; return p; };
+  q.part = take2(sP);
+  q.W = take2(n);
+  q.Y = take2(n);
+  q.qd = take2(M);
+  q.rd = take2(M);
+  q.G = take2(n);
+  q.tau = take1(M);
+  q.qa = take1(M);
+  q.ra = take1(M);
+  q.rb = take1(M);
+  q.tn = take1(2);
+  return q;
+}
+int64_t q_bufs_doubles(int M, int m) {
+  const int n = 2 * M;
+  return m * (2 * (int64_t)dwh::q_part_elems(M) + 2 * (3 * (int64_t)n + 2 * M) + 4 * (int64_t)M + 2);
+}
+
+// Eigenvalues by the structure-preserving reduction: H_BdG of the m sources
+// assembled into the slots' JU, reduced site by site on their particle rows
+// (the reflectors left in JU's bottom rows), site rotations, block Sturm
+// bisection; the 2N ascending eigenvalues of each into the slots' E (device).
+// ms (optional, m = 1): the reduction's device time (HIP events; synchronises).
+int qeig_values(dwh_ctx* ctx, const TrSrc& src, int m, float* ms) {
+  const int M = ctx->d.N, n = 2 * M;
+  if (!dwh::q_supported(M)) return fail(ctx, DWH_ERR_ARG, "structure-preserving solver: lattice too large");
+  const int64_t sA = (int64_t)n * n;
+  int rc;
+  if (m > ctx->q_slots) {
+    HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+    drop_alloc(ctx, ctx->d_q);
+    ctx->d_q = nullptr;
+    ctx->q_slots = 0;
+    if ((rc = dalloc(ctx, &ctx->d_q, (size_t)q_bufs_doubles(M, m)))) return rc;
+    ctx->q_slots = m;
+  }
+  const QBufs q = q_bufs(ctx);
+  hipStream_t s = ctx->stream;
+  double2* A = ctx->tr.JU;
+  if ((rc = assemble_slots(ctx, src, m, A))) return rc;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (ms) {
+    HIPCHECK(ctx, hipEventCreate(&e0));
+    HIPCHECK(ctx, hipEventCreate(&e1));
+    HIPCHECK(ctx, hipEventRecord(e0, s));
+  }
+  dwh::launch_q_reduce(A, M, sA, q.part, q.sP, q.W, q.tau, q.Y, q.qa, q.qd, m, s);
+  if (ms) HIPCHECK(ctx, hipEventRecord(e1, s));
+  dwh::launch_q_rot(q.qa, q.qd, q.Y, M, q.ra, q.rd, q.rb, q.G, m, s);
+  dwh::launch_q_bisect(q.ra, q.rd, q.rb, M, ctx->tr.E, q.tn, m, s);
+  HIPCHECK(ctx, hipGetLastError());
+  if (ms) {
+    HIPCHECK(ctx, hipStreamSynchronize(s));
+    HIPCHECK(ctx, hipEventElapsedTime(ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+  }
+  return DWH_OK;
+}
+
+// Every eigenpair by the structure-preserving solver (m matrices): qeig_values,
+// then — when every matrix's spectrum is clear of crowding at zero (gap at
+// the middle > kEigZeroTol ||T||) and of clusters (consecutive gaps >
+// kEigClusterTol ||T||), checked on the host from the eigenvalues (one
+// synchronisation) — the particle-hole half: inverse iteration on T for the
+// N upper eigenvalues (k_q_invit), one Löwdin step (the library's complex
+// products), the site rotations into U' (interleaved rows), the reflector
+// pairs as a one-stage V and its back-transform, then the BdG row order and
+// the Theta partners for the lower half (k_q_final).  *done = false: not
+// taken (the caller runs the one-stage solver; the slots' JU / E are
+// overwritten either way).
+int q_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m, bool* done) {
+  *done = false;
+  const int N = ctx->d.N, n = 2 * N, j0 = N, nv = n - j0;
+  const dwh::TrBufs& b = ctx->tr;
+  const int64_t sA = (int64_t)n * n;
+  int rc;
+  if ((rc = qeig_values(ctx, src, m, nullptr))) return rc;
+  const QBufs q = q_bufs(ctx);
+  hipStream_t s = ctx->stream;
+  const char* eh = std::getenv("DWHMC_EIG_HALF");   // =0: every column solved (the one-stage solver)
+  if (n % 2 || (eh && *eh == '0')) return DWH_OK;
+  std::vector<double> Eh((size_t)m * n), tn((size_t)2 * m);
+  HIPCHECK(ctx, hipMemcpyAsync(Eh.data(), b.E, Eh.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+  HIPCHECK(ctx, hipMemcpyAsync(tn.data(), q.tn, m * sizeof(double), hipMemcpyDeviceToHost, s));
+  HIPCHECK(ctx, hipStreamSynchronize(s));
+  for (int k = 0; k < m; ++k) {
+    const double* E = Eh.data() + (size_t)k * n;
+    if (!(E[N] - E[N - 1] > dwh::kEigZeroTol * tn[k])) return DWH_OK;
+    for (int j = N + 1; j < n; ++j)
+      if (!(E[j] - E[j - 1] > dwh::kEigClusterTol * tn[k])) return DWH_OK;
+  }
+  // vector workspace
+  const int64_t sZ = (int64_t)n * nv, sS = dwh::q_invit_scratch(N, j0), sG = (int64_t)nv * nv;
+  if (m > ctx->q_vec_slots) {
+    HIPCHECK(ctx, hipStreamSynchronize(s));
+    for (void* p : {(void*)ctx->d_qz, (void*)ctx->d_qs, (void*)ctx->d_qg}) drop_alloc(ctx, p);
+    ctx->d_qz = ctx->d_qs = ctx->d_qg = nullptr;
+    ctx->q_vec_slots = 0;
+    if ((rc = dalloc(ctx, &ctx->d_qz, (size_t)m * sZ)) || (rc = dalloc(ctx, &ctx->d_qs, (size_t)m * sS)) ||
+        (rc = dalloc(ctx, &ctx->d_qg, (size_t)m * sG)))
+      return rc;
+    ctx->q_vec_slots = m;
+  }
+  if ((rc = eig_scratch(ctx, m))) return rc;
+  EigPhase ph(s);
+  ph.mark("q values");
+  dwh::launch_q_invit(q.ra, q.rd, q.rb, N, b.E, q.tn, j0, ctx->d_qz, sZ, ctx->d_qs, sS, m, s);
+  ph.mark("q invit");
+  // Löwdin on X = Zt (nv x n, ld nv): G' = X X^H (= conj(Z^H Z)), Y^T = 1.5 X - 0.5 G' X into the slots' Jmn
+  const double2 one = make_double2(1.0, 0.0), zero = make_double2(0.0, 0.0);
+  dwh::gemm_z('N', 'C', nv, nv, n, one, ctx->d_qz, nv, sZ, ctx->d_qz, nv, sZ, zero, ctx->d_qg, nv, sG, m, s);
+  HIPCHECK(ctx, hipMemcpy2DAsync(b.Jmn, sA * sizeof(double2), ctx->d_qz, sZ * sizeof(double2), sZ * sizeof(double2), m,
+                                 hipMemcpyDeviceToDevice, s));
+  dwh::gemm_z('N', 'N', nv, n, nv, make_double2(-0.5, 0.0), ctx->d_qg, nv, sG, ctx->d_qz, nv, sZ,
+              make_double2(1.5, 0.0), b.Jmn, nv, sA, m, s);
+  // the site rotations, transposed into the slots' U columns j0.. (interleaved rows)
+  dwh::launch_q_ztu(b.Jmn, sA, q.G, N, j0, b.U, sA, m, s);
+  ph.mark("q lowdin");
+  // the reflector pairs as V (slots' Jmn) and complex tau; V^H blocks into the slots' JU
+  dwh::launch_q_vexpand(b.JU, sA, q.tau, N, b.Jmn, ctx->d_eig_tau, m, s);
+  HIPCHECK(ctx, hipGetLastError());
+  if ((rc = eig_back_transform(ctx, b.Jmn, b.JU, j0, m))) return rc;
+  ph.mark("q backtransform");
+  // BdG row order and the Theta partners, through the slots' JU
+  dwh::launch_q_final(b.U, sA, N, j0, b.JU, m, s);
+  HIPCHECK(ctx, hipMemcpyAsync(b.U, b.JU, (size_t)m * sA * sizeof(double2), hipMemcpyDeviceToDevice, s));
+  HIPCHECK(ctx, hipGetLastError());
+  ph.mark("q final");
+  ctx->eig_half = true;
+  ctx->eig_c0h.assign(m, N);
+  *done = true;
+  return DWH_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -2730,45 +2926,6 @@ int dwh_transport_grid(double eta, double domega, double omega_max, int64_t* n_o
   return DWH_OK;
 }
 
-// Eigenvalues only, by the structure-preserving reduction (dwhmc_qeig.hip):
-// H_BdG of src assembled into the slot's JU, reduced site by site on its
-// particle rows, site rotations, block Sturm bisection; the 2N ascending
-// eigenvalues into the slot's E (device).  ms (optional): the reduction's
-// device time (HIP events; synchronises).
-int qeig_values(dwh_ctx* ctx, const TrSrc& src, float* ms) {
-  const int M = ctx->d.N, n = 2 * M;
-  if (!dwh::q_supported(M)) return fail(ctx, DWH_ERR_ARG, "structure-preserving solver: lattice too large");
-  const int64_t sA = (int64_t)n * n, sP = dwh::q_part_elems(M);
-  // workspace (doubles): scratch 2 sP | W 2n | Y 2n | qd 2M | rd 2M | G 2n | tau M | qa M | ra M | rb M | tn 2
-  const int64_t oW = 2 * sP, oY = oW + 2 * n, oqd = oY + 2 * n, ord = oqd + 2 * M, oG = ord + 2 * M,
-                otau = oG + 2 * n, oqa = otau + M, ora = oqa + M, orb = ora + M, otn = orb + M, tot = otn + 2;
-  int rc;
-  if (!ctx->d_q && (rc = dalloc(ctx, &ctx->d_q, (size_t)tot))) return rc;
-  double* w = ctx->d_q;
-  auto z2 = [&](int64_t o) { return reinterpret_cast<double2*>(w + o); };
-  hipStream_t s = ctx->stream;
-  double2* A = ctx->tr.JU;
-  if ((rc = assemble_slots(ctx, src, 1, A))) return rc;
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  if (ms) {
-    HIPCHECK(ctx, hipEventCreate(&e0));
-    HIPCHECK(ctx, hipEventCreate(&e1));
-    HIPCHECK(ctx, hipEventRecord(e0, s));
-  }
-  dwh::launch_q_reduce(A, M, sA, z2(0), sP, z2(oW), w + otau, z2(oY), w + oqa, z2(oqd), 1, s);
-  if (ms) HIPCHECK(ctx, hipEventRecord(e1, s));
-  dwh::launch_q_rot(w + oqa, z2(oqd), z2(oY), M, w + ora, z2(ord), w + orb, z2(oG), 1, s);
-  dwh::launch_q_bisect(w + ora, z2(ord), w + orb, M, ctx->tr.E, w + otn, 1, s);
-  HIPCHECK(ctx, hipGetLastError());
-  if (ms) {
-    HIPCHECK(ctx, hipStreamSynchronize(s));
-    HIPCHECK(ctx, hipEventElapsedTime(ms, e0, e1));
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-  }
-  return DWH_OK;
-}
-
 // Development entry (tools/qeig_check.py): qeig_values of `chain`, the
 // eigenvalues into E and the reduction's device time into *ms.
 int dwh_debug_qeig(dwh_ctx* ctx, int64_t chain, double* E, double* ms) {
@@ -2780,7 +2937,7 @@ int dwh_debug_qeig(dwh_ctx* ctx, int64_t chain, double* E, double* ms) {
   if ((rc = transport_prepare(ctx, std::max<int64_t>(ctx->tr_nw, 0), std::max<int64_t>(ctx->tr_nd, 0), 1)))
     return rc;
   float t = 0.0f;
-  if ((rc = qeig_values(ctx, chains_src(ctx, chain), &t))) return rc;
+  if ((rc = qeig_values(ctx, chains_src(ctx, chain), 1, &t))) return rc;
   const int M = ctx->d.N;
   HIPCHECK(ctx, hipMemcpyAsync(E, ctx->tr.E, 2 * (size_t)M * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
   HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
@@ -2813,7 +2970,7 @@ int dwh_eigensystem(dwh_ctx* ctx, int64_t chain, double* E, dwh_c128* U) {
     Scope sc(ctx, T_EIG_OWN, 1);
     ctx->eig_ph = false;
     ctx->eig_ph_last = 0;
-    if ((rc = qeig_values(ctx, chains_src(ctx, chain), nullptr))) return rc;
+    if ((rc = qeig_values(ctx, chains_src(ctx, chain), 1, nullptr))) return rc;
     HIPCHECK(ctx, hipMemsetAsync(ctx->d_tr_bad, 0, sizeof(int), ctx->stream));
     dwh::launch_nonfinite(ctx->tr.U, 0, ctx->tr.E, (int64_t)n2, ctx->d_tr_bad, ctx->stream);
     int bad = 0;
@@ -2972,6 +3129,7 @@ int dwh_info(dwh_ctx* ctx, dwh_info_t* out) {
   out->block = ctx->algo == ALGO_CR ? ctx->cr.BP : ctx->algo == ALGO_EIG ? 0 : kGJ;
   out->eig_half = ctx->eig_ph_last;
   out->eig_long_clusters = ctx->eig_long_clusters;
+  out->eig_quat = ctx->eig_quat_last;
   return DWH_OK;
 }
 

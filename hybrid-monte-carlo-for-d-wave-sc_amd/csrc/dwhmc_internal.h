@@ -402,6 +402,22 @@ void launch_q_rot(const double* qa, const double2* qd, const double2* Y, int M, 
 // the 2M eigenvalues of T ascending into E (stride 2M), ||T|| bound into tnorm
 void launch_q_bisect(const double* ra, const double2* rd, const double* rb, int M, double* E, double* tnorm, int m,
                      hipStream_t s);
+// eigenvectors of the particle-hole half (E indices j0 .. 2M-1, nv = 2M - j0):
+// inverse iteration into Zt (row r of vector jj at Zt[r nv + jj], interleaved
+// rows 2s / 2s+1 = particle / hole of site s; LU scratch S: q_invit_scratch
+// double2 per matrix)
+int64_t q_invit_scratch(int M, int j0);
+void launch_q_invit(const double* ra, const double2* rd, const double* rb, int M, const double* E, const double* tnorm,
+                    int j0, double2* Zt, int64_t sZ, double2* S, int64_t sS, int m, hipStream_t s);
+// U' columns j0.. (n x n, interleaved rows) = site rotations G of Yt (nv x n, ld nv)
+void launch_q_ztu(const double2* Yt, int64_t sY, const double2* G, int M, int j0, double2* U, int64_t sU, int m,
+                  hipStream_t s);
+// the reflector pairs as the one-stage back-transform's V (n x n, interleaved
+// rows; columns 2j, 2j+1 = v_j, Theta v_j) and complex tau (n per matrix)
+void launch_q_vexpand(const double2* A, int64_t sA, const double* tau, int M, double2* V, double2* tauc, int m,
+                      hipStream_t s);
+// U (BdG order) from U' (interleaved): columns >= j0 copied, below j0 the Theta partners
+void launch_q_final(const double2* Ui, int64_t sU, int M, int j0, double2* U, int m, hipStream_t s);
 
 // The library's own batched fp64 products (dwhmc_gemm.hip):
 // C = alpha op(A) op(B) + beta C, column-major, op 'N' or 'C' (conjugate

@@ -592,15 +592,20 @@ __device__ __forceinline__ void qmul(double2 a1, double2 b1, double2 a2, double2
                    b1.x * a2.y + b1.y * a2.x + (a1.x * b2.y - a1.y * b2.x));
 }
 
-// Site rotations (one thread per matrix): g_0 = 1, g_{j+1} = q_j g~_j / |q_j|
-// (q_j = quat(y_p, y_h), g~ = sigma_z g sigma_z = quat(al, -be)); the rotated
-// diagonal blocks g^H [[a, d], [conj d, -a]] g -> (qa', qd'), b_j = |q_j|.
-// g stored as (al, be) per site in G[2 s], G[2 s + 1].
-__global__ void k_q_rot(const double* __restrict__ qa, const double2* __restrict__ qd,
-                        const double2* __restrict__ Y, int M, double* __restrict__ ra, double2* __restrict__ rd,
-                        double* __restrict__ rb, double2* __restrict__ G, int m) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= m) return;
+// Site rotations (one workgroup per matrix): g_0 = 1, g_{j+1} = q^_j
+// tau(g_j), q^_j = quat(y_p, y_h) / |q_j| (1 when q_j = 0), tau(quat(al, be))
+// = quat(al, -be) = k g k^-1 with k = i sigma_z = quat(i, 0).  Hence g_j =
+// x_{j-1} .. x_1 x_0 k^-j with x_i = q^_i k: a prefix product of unit
+// quaternions (per-thread chunks, then a Hillis-Steele scan of the chunk
+// totals in LDS, later factors on the left), k^-j = quat((-i)^j, 0).  The
+// rotated diagonal blocks g^H [[a, d], [conj d, -a]] g -> (ra, rd), b_j =
+// |q_j|; g as (al, be) per site in G[2 s], G[2 s + 1].
+constexpr int kQRotT = 1024;
+__global__ __launch_bounds__(kQRotT) void k_q_rot(const double* __restrict__ qa, const double2* __restrict__ qd,
+                                                  const double2* __restrict__ Y, int M, double* __restrict__ ra,
+                                                  double2* __restrict__ rd, double* __restrict__ rb,
+                                                  double2* __restrict__ G) {
+  const int k = blockIdx.x, t = threadIdx.x;
   qa += (int64_t)k * M;
   qd += (int64_t)k * M;
   Y += (int64_t)k * 2 * M;
@@ -608,40 +613,97 @@ __global__ void k_q_rot(const double* __restrict__ qa, const double2* __restrict
   rd += (int64_t)k * M;
   rb += (int64_t)k * M;
   G += (int64_t)k * 2 * M;
-  double2 al = make_double2(1.0, 0.0), be = make_double2(0.0, 0.0);
-  for (int s = 0; s < M; ++s) {
+  __shared__ double2 sa[2][kQRotT], sb[2][kQRotT];
+  const int ne = M - 1, per = (ne + kQRotT - 1) / kQRotT, i0 = t * per;
+  double2 la[kQMaxR], lb[kQMaxR];
+  double nq[kQMaxR];
+  double2 ta = make_double2(1.0, 0.0), tb = make_double2(0.0, 0.0);   // the chunk's product
+#pragma unroll
+  for (int u = 0; u < kQMaxR; ++u) {
+    const int i = i0 + u;
+    nq[u] = 0.0;
+    if (u < per && i < ne) {
+      const double2 yp = Y[2 * i], yh = Y[2 * i + 1];
+      const double q2 = yp.x * yp.x + yp.y * yp.y + yh.x * yh.x + yh.y * yh.y;
+      nq[u] = sqrt(q2);
+      double2 xa = make_double2(1.0, 0.0), xb = make_double2(0.0, 0.0);
+      if (nq[u] > 0.0) {
+        const double iv = 1.0 / nq[u];
+        xa = make_double2(yp.x * iv, yp.y * iv);
+        xb = make_double2(yh.x * iv, yh.y * iv);
+      }
+      // x = q^ k = quat(i al, i be)
+      xa = make_double2(-xa.y, xa.x);
+      xb = make_double2(-xb.y, xb.x);
+      double2 na, nb;
+      qmul(xa, xb, ta, tb, na, nb);   // later factor on the left
+      ta = na;
+      tb = nb;
+    }
+    la[u] = ta;
+    lb[u] = tb;
+  }
+  // inclusive scan of the chunk totals over the threads (ping-pong buffers)
+  int cur = 0;
+  sa[0][t] = ta;
+  sb[0][t] = tb;
+  __syncthreads();
+  for (int d = 1; d < kQRotT; d <<= 1) {
+    double2 va = sa[cur][t], vb = sb[cur][t];
+    if (t >= d) {
+      double2 na, nb;
+      qmul(va, vb, sa[cur][t - d], sb[cur][t - d], na, nb);
+      va = na;
+      vb = nb;
+    }
+    sa[cur ^ 1][t] = va;
+    sb[cur ^ 1][t] = vb;
+    cur ^= 1;
+    __syncthreads();
+  }
+  const double2 ea = t > 0 ? sa[cur][t - 1] : make_double2(1.0, 0.0);   // product of the earlier chunks
+  const double2 eb = t > 0 ? sb[cur][t - 1] : make_double2(0.0, 0.0);
+  auto site = [&](int s, double2 al, double2 be, double b) {
+    // renormalise, then D' = g^H D g, g = [[al, -conj be], [be, conj al]], D = [[a, d], [conj d, -a]]
+    const double nn = 1.0 / sqrt(al.x * al.x + al.y * al.y + be.x * be.x + be.y * be.y);
+    al = make_double2(al.x * nn, al.y * nn);
+    be = make_double2(be.x * nn, be.y * nn);
     G[2 * s] = al;
     G[2 * s + 1] = be;
-    // D' = g^H D g, g = [[al, -conj be], [be, conj al]], D = [[a, d], [conj d, -a]]
     const double a = qa[s];
     const double2 d = qd[s];
-    // D g columns: c0 = D (al; be), c1 = D (-conj be; conj al)
     const double2 c00 = make_double2(a * al.x + (d.x * be.x - d.y * be.y), a * al.y + (d.x * be.y + d.y * be.x));
     const double2 c10 = make_double2((d.x * al.x + d.y * al.y) - a * be.x, (d.x * al.y - d.y * al.x) - a * be.y);
     const double2 nbe = make_double2(-be.x, be.y), cal = make_double2(al.x, -al.y);   // -conj be, conj al
     const double2 c01 = make_double2(a * nbe.x + (d.x * cal.x - d.y * cal.y), a * nbe.y + (d.x * cal.y + d.y * cal.x));
     const double2 c11 = make_double2((d.x * nbe.x + d.y * nbe.y) - a * cal.x, (d.x * nbe.y - d.y * nbe.x) - a * cal.y);
-    // row 0 of g^H = (conj al, conj be): D'00 = conj(al) c00 + conj(be) c10, D'01 = conj(al) c01 + conj(be) c11
     ra[s] = (al.x * c00.x + al.y * c00.y) + (be.x * c10.x + be.y * c10.y);
     rd[s] = make_double2((al.x * c01.x + al.y * c01.y) + (be.x * c11.x + be.y * c11.y),
                          (al.x * c01.y - al.y * c01.x) + (be.x * c11.y - be.y * c11.x));
-    if (s + 1 < M) {
-      const double2 yp = Y[2 * s], yh = Y[2 * s + 1];
-      const double nq = sqrt(yp.x * yp.x + yp.y * yp.y + yh.x * yh.x + yh.y * yh.y);
-      rb[s] = nq;
-      const double2 ta = al, tb = make_double2(-be.x, -be.y);   // g~ = quat(al, -be)
-      if (nq > 0.0) {
-        double2 na, nb;
-        qmul(yp, yh, ta, tb, na, nb);
-        al = make_double2(na.x / nq, na.y / nq);
-        be = make_double2(nb.x / nq, nb.y / nq);
-      } else {
-        al = ta;
-        be = tb;
-      }
-    } else {
-      rb[s] = 0.0;
+    rb[s] = b;
+  };
+  if (t == 0) site(0, make_double2(1.0, 0.0), make_double2(0.0, 0.0), ne > 0 ? nq[0] : 0.0);
+#pragma unroll
+  for (int u = 0; u < kQMaxR; ++u) {
+    const int i = i0 + u;
+    if (u < per && i < ne) {
+      double2 pa, pb;
+      qmul(la[u], lb[u], ea, eb, pa, pb);   // P_{i+1} = x_i .. x_0
+      // g_{i+1} = P_{i+1} k^-(i+1) = quat(pa c, pb c), c = (-i)^(i+1)
+      const int j = (i + 1) & 3;
+      const double2 c = j == 0 ? make_double2(1.0, 0.0)
+                        : j == 1 ? make_double2(0.0, -1.0)
+                        : j == 2 ? make_double2(-1.0, 0.0) : make_double2(0.0, 1.0);
+      const double2 al = make_double2(pa.x * c.x - pa.y * c.y, pa.x * c.y + pa.y * c.x);
+      const double2 be = make_double2(pb.x * c.x - pb.y * c.y, pb.x * c.y + pb.y * c.x);
+      const double bn = i + 1 < ne ? (u + 1 < per ? nq[u + 1] : 0.0) : 0.0;
+      site(i + 1, al, be, bn);
     }
+  }
+  // b of the sites whose q lives in the next thread's chunk
+  if (per > 0 && i0 + per - 1 < ne && i0 + per < ne) {
+    const double2 yp = Y[2 * (i0 + per)], yh = Y[2 * (i0 + per) + 1];
+    rb[i0 + per] = sqrt(yp.x * yp.x + yp.y * yp.y + yh.x * yh.x + yh.y * yh.y);
   }
 }
 
@@ -653,7 +715,7 @@ __global__ void k_q_rot(const double* __restrict__ qa, const double2* __restrict
 // finite).  LDS: a' [0, M), d' [M, 3M) (re, im), b^2 [3M, 4M).
 constexpr int kQBisW = 8;
 __global__ __launch_bounds__(64 * kQBisW) void k_q_bisect(const double* __restrict__ ra, const double2* __restrict__ rd,
-                                                          const double* __restrict__ rb, int M, int lgG,
+                                                          const double* __restrict__ rb, int M, int lgG, int jofs,
                                                           double* __restrict__ E, double* __restrict__ tnorm) {
   extern __shared__ double lds[];
   const int k = blockIdx.y, lane = threadIdx.x & 63, n = 2 * M;
@@ -682,8 +744,10 @@ __global__ __launch_bounds__(64 * kQBisW) void k_q_bisect(const double* __restri
   const double gl = -tn * (1.0 + 4.0 * DBL_EPSILON) - 1e-300, gu = tn * (1.0 + 4.0 * DBL_EPSILON) + 1e-300;
   const double pivmin = (DBL_EPSILON * tn) * (DBL_EPSILON * tn) + DBL_MIN;
   const int G = 1 << lgG, g0 = lane & ~(G - 1), gi = lane & (G - 1);
-  const int j = ((blockIdx.x * kQBisW + (threadIdx.x >> 6)) << (6 - lgG)) + (lane >> lgG);
-  if (((blockIdx.x * kQBisW + (threadIdx.x >> 6)) << (6 - lgG)) >= n) return;
+  // indices jofs .. n-1; (jofs > 0) the lower half mirrored: the spectrum of
+  // T is symmetric (particle-hole), E_{n-1-j} = -E_j
+  const int j = jofs + ((blockIdx.x * kQBisW + (threadIdx.x >> 6)) << (6 - lgG)) + (lane >> lgG);
+  if (jofs + ((blockIdx.x * kQBisW + (threadIdx.x >> 6)) << (6 - lgG)) >= n) return;
   const unsigned long long gmask = G == 64 ? ~0ull : ((1ull << G) - 1);
   const double step = 1.0 / (G + 1);
   double lo = gl, hi = gu;
@@ -721,7 +785,294 @@ __global__ __launch_bounds__(64 * kQBisW) void k_q_bisect(const double* __restri
       hi = nhi;
     }
   }
-  if (gi == 0 && j < n) E[j] = 0.5 * (lo + hi);
+  if (gi == 0 && j < n) {
+    const double e = 0.5 * (lo + hi);
+    E[j] = e;
+    if (jofs > 0) E[n - 1 - j] = -e;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Eigenvectors of the particle-hole half (indices j0 .. n-1 of E, nv = n - j0)
+// ---------------------------------------------------------------------------
+
+// entry (r, c) of T - lam in the interleaved site order (row 2s: particle of
+// site s, 2s+1: hole): row 2s = b_{s-1} @ 2s-2, a_s - lam @ 2s, d_s @ 2s+1,
+// b_s @ 2s+2; row 2s+1 = -b_{s-1} @ 2s-1, conj d_s @ 2s, -a_s - lam @ 2s+1,
+// -b_s @ 2s+3.  T's arrays in LDS: a [0, M), b [M, 2M), d [2M, 4M) (re, im).
+__device__ __forceinline__ double2 q_tent(const double* L, int M, double lam, int r, int c) {
+  const int n = 2 * M;
+  if (r >= n || c < 0 || c >= n) return make_double2(0.0, 0.0);
+  const int s = r >> 1, dc = c - r;
+  const bool hole = r & 1;
+  if (dc == 0) return make_double2(hole ? -L[s] - lam : L[s] - lam, 0.0);
+  if (dc == 2 && s + 1 < M) return make_double2(hole ? -L[M + s] : L[M + s], 0.0);
+  if (dc == -2 && s > 0) return make_double2(hole ? -L[M + s - 1] : L[M + s - 1], 0.0);
+  if (!hole && dc == 1) return make_double2(L[2 * M + 2 * s], L[2 * M + 2 * s + 1]);
+  if (hole && dc == -1) return make_double2(L[2 * M + 2 * s], -L[2 * M + 2 * s + 1]);
+  return make_double2(0.0, 0.0);
+}
+
+__device__ __forceinline__ double q_start(int j, int r) {
+  unsigned long long x = ((unsigned long long)(unsigned)j << 32 | (unsigned)r) + 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  return (double)(x >> 11) * 0x1.0p-53 - 0.5;
+}
+
+__device__ __forceinline__ double2 cmul2(double2 a, double2 b) {
+  return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ double2 csub2(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
+
+// Inverse iteration, one eigenvalue per thread (tools/qeig_proto.py
+// band_solve_pivoted): T - lam = P L U with partial pivoting over the three
+// rows that reach column k (lower bandwidth 2, so U's rows carry columns
+// k .. k+4; a pivot below eps ||T|| is clamped), the eliminated right-hand
+// side in the same sweep; per step six complex (1/u_kk, u_k,k+1..k+4, y_k)
+// into the scratch S[(k 6 + e) nv + jj] (coalesced over the threads), then the
+// back substitution.  Two solves from a fixed pseudo-random start (lam is
+// bisected to the last bit), normalised: vector jj in Zt[r nv + jj] (row r
+// in the interleaved order).
+__global__ __launch_bounds__(64) void k_q_invit(const double* __restrict__ ra, const double2* __restrict__ rd,
+                                                const double* __restrict__ rb, int M, const double* __restrict__ E,
+                                                const double* __restrict__ tnorm, int j0, double2* __restrict__ Zt,
+                                                int64_t sZ, double2* __restrict__ S, int64_t sS) {
+  extern __shared__ double lds[];
+  const int k = blockIdx.y, n = 2 * M, nv = n - j0;
+  for (int i = threadIdx.x; i < M; i += blockDim.x) {
+    lds[i] = ra[(int64_t)k * M + i];
+    lds[M + i] = rb[(int64_t)k * M + i];
+    const double2 dv = rd[(int64_t)k * M + i];
+    lds[2 * M + 2 * i] = dv.x;
+    lds[2 * M + 2 * i + 1] = dv.y;
+  }
+  __syncthreads();
+  const int jj = blockIdx.x * blockDim.x + threadIdx.x;
+  if (jj >= nv) return;
+  const double lam = E[(int64_t)k * n + j0 + jj];
+  const double tn = tnorm[k];
+  const double small = tn > 0.0 ? DBL_EPSILON * tn : DBL_EPSILON;
+  double2* z = Zt + k * sZ + jj;
+  double2* sc = S + k * sS + jj;
+  const double2 zero = make_double2(0.0, 0.0);
+  double scale = 1.0;
+  for (int it = 0; it < 2; ++it) {
+    auto rhs = [&](int r) -> double2 {
+      if (r >= n) return zero;
+      if (it == 0) return make_double2(q_start(j0 + jj, 2 * r), q_start(j0 + jj, 2 * r + 1));
+      const double2 v = z[(int64_t)r * nv];
+      return make_double2(v.x * scale, v.y * scale);
+    };
+    double2 w0[5], w1[5], w2[5];
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
+      w0[c] = q_tent(lds, M, lam, 0, c);
+      w1[c] = q_tent(lds, M, lam, 1, c);
+      w2[c] = q_tent(lds, M, lam, 2, c);
+    }
+    double2 y0 = rhs(0), y1 = rhs(1), y2 = rhs(2);
+    // one elimination step (row kk leaves the window into the scratch)
+    auto step = [&](int kk, double2 ny) {
+      double2 nr[5];   // the next window row (row kk+3 at columns kk+1 .. kk+5)
+#pragma unroll
+      for (int c = 0; c < 5; ++c) nr[c] = q_tent(lds, M, lam, kk + 3, kk + 1 + c);
+      const double m0 = w0[0].x * w0[0].x + w0[0].y * w0[0].y;
+      const double m1 = w1[0].x * w1[0].x + w1[0].y * w1[0].y;
+      const double m2 = w2[0].x * w2[0].x + w2[0].y * w2[0].y;
+      const int sel = m1 > m0 ? (m2 > m1 ? 2 : 1) : (m2 > m0 ? 2 : 0);
+#pragma unroll
+      for (int c = 0; c < 5; ++c) {
+        const double2 p0 = w0[c], p1 = w1[c], p2 = w2[c];
+        w0[c] = sel == 0 ? p0 : (sel == 1 ? p1 : p2);
+        w1[c] = sel == 1 ? p0 : p1;
+        w2[c] = sel == 2 ? p0 : p2;
+      }
+      {
+        const double2 q0 = y0, q1 = y1, q2 = y2;
+        y0 = sel == 0 ? q0 : (sel == 1 ? q1 : q2);
+        y1 = sel == 1 ? q0 : q1;
+        y2 = sel == 2 ? q0 : q2;
+      }
+      double pm = w0[0].x * w0[0].x + w0[0].y * w0[0].y;
+      if (pm < small * small) {
+        w0[0] = make_double2(small, 0.0);
+        pm = small * small;
+      }
+      const double ip = rcp_nr(pm);
+      const double2 r = make_double2(w0[0].x * ip, -w0[0].y * ip);   // 1 / u_kk
+      const double2 f1 = cmul2(w1[0], r), f2 = cmul2(w2[0], r);
+#pragma unroll
+      for (int c = 1; c < 5; ++c) {
+        w1[c] = csub2(w1[c], cmul2(f1, w0[c]));
+        w2[c] = csub2(w2[c], cmul2(f2, w0[c]));
+      }
+      y1 = csub2(y1, cmul2(f1, y0));
+      y2 = csub2(y2, cmul2(f2, y0));
+      double2* st = sc + (int64_t)kk * 6 * nv;
+      st[0] = r;
+#pragma unroll
+      for (int c = 1; c < 5; ++c) st[(int64_t)c * nv] = w0[c];
+      st[(int64_t)5 * nv] = y0;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        w0[c] = w1[c + 1];
+        w1[c] = w2[c + 1];
+      }
+      w0[4] = w1[4] = zero;
+#pragma unroll
+      for (int c = 0; c < 5; ++c) w2[c] = nr[c];
+      y0 = y1;
+      y1 = y2;
+      y2 = ny;
+    };
+    // forward sweep in blocks of FB steps, the next block's right-hand side
+    // rows loaded one block ahead (a load's wait then only covers loads and
+    // stores issued before it, not this block's scratch stores)
+    constexpr int FB = 8;
+    double2 ra_[FB], rb_[FB];
+#pragma unroll
+    for (int u = 0; u < FB; ++u) ra_[u] = rhs(3 + u);
+    for (int k0 = 0; k0 < n; k0 += 2 * FB) {
+#pragma unroll
+      for (int u = 0; u < FB; ++u) rb_[u] = rhs(k0 + FB + 3 + u);
+#pragma unroll
+      for (int u = 0; u < FB; ++u)
+        if (k0 + u < n) step(k0 + u, ra_[u]);
+#pragma unroll
+      for (int u = 0; u < FB; ++u) ra_[u] = rhs(k0 + 2 * FB + 3 + u);
+#pragma unroll
+      for (int u = 0; u < FB; ++u)
+        if (k0 + FB + u < n) step(k0 + FB + u, rb_[u]);
+    }
+    // back substitution: x_k = (y_k - sum_t u_k,k+t x_{k+t}) / u_kk, the next
+    // block's factors loaded one block ahead
+    double2 x1 = zero, x2 = zero, x3 = zero, x4 = zero;
+    double nrm = 0.0;
+    constexpr int PB = 4;
+    double2 fa[PB][6], fb[PB][6];
+    auto load_blk = [&](int k0, double2 (&f)[PB][6]) {
+#pragma unroll
+      for (int u = 0; u < PB; ++u) {
+        const int kk = k0 - u;
+#pragma unroll
+        for (int e = 0; e < 6; ++e) f[u][e] = kk >= 0 ? sc[((int64_t)kk * 6 + e) * nv] : zero;
+      }
+    };
+    auto solve_blk = [&](int k0, const double2 (&f)[PB][6]) {
+#pragma unroll
+      for (int u = 0; u < PB; ++u) {
+        const int kk = k0 - u;
+        if (kk >= 0) {
+          double2 t = f[u][5];
+          t = csub2(t, cmul2(f[u][1], x1));
+          t = csub2(t, cmul2(f[u][2], x2));
+          t = csub2(t, cmul2(f[u][3], x3));
+          t = csub2(t, cmul2(f[u][4], x4));
+          const double2 x = cmul2(t, f[u][0]);
+          z[(int64_t)kk * nv] = x;
+          nrm += x.x * x.x + x.y * x.y;
+          x4 = x3;
+          x3 = x2;
+          x2 = x1;
+          x1 = x;
+        }
+      }
+    };
+    load_blk(n - 1, fa);
+    for (int k0 = n - 1; k0 >= 0; k0 -= 2 * PB) {
+      load_blk(k0 - PB, fb);
+      solve_blk(k0, fa);
+      load_blk(k0 - 2 * PB, fa);
+      solve_blk(k0 - PB, fb);
+    }
+    scale = 1.0 / sqrt(nrm);
+  }
+  for (int r = 0; r < n; ++r) {
+    const double2 v = z[(int64_t)r * nv];
+    z[(int64_t)r * nv] = make_double2(v.x * scale, v.y * scale);
+  }
+}
+
+// U' (column-major n x n, interleaved rows) columns j0 + jj from Yt (nv x n,
+// ld nv: vector jj's entry r at Yt[jj + r nv]) with the site rotations g_s
+// (G[2 s] = al, G[2 s + 1] = be; g = [[al, -conj be], [be, conj al]]) applied
+// to each row pair (2 s, 2 s + 1): through a 32-row x 64-column LDS tile.
+__global__ __launch_bounds__(256) void k_q_ztu(const double2* __restrict__ Yt, int64_t sY, const double2* __restrict__ G,
+                                               int M, int j0, double2* __restrict__ U, int64_t sU) {
+  const int k = blockIdx.z, n = 2 * M, nv = n - j0;
+  const int r0 = blockIdx.y * 32, c0 = blockIdx.x * 64;
+  Yt += k * sY;
+  G += (int64_t)k * n;
+  U += k * sU;
+  __shared__ double2 t[32][65];
+  for (int q = threadIdx.x; q < 32 * 64; q += 256) {
+    const int rr = q >> 6, cc = q & 63, r = r0 + rr, c = c0 + cc;   // read: columns contiguous
+    t[rr][cc] = (r < n && c < nv) ? Yt[c + (int64_t)r * nv] : make_double2(0.0, 0.0);
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < 32 * 64; q += 256) {
+    const int cc = q >> 5, rr = q & 31, r = r0 + rr, c = c0 + cc;   // write: rows contiguous
+    if (r >= n || c >= nv) continue;
+    const int s = r >> 1, rp = rr & ~1;
+    const double2 zp = t[rp][cc], zh = t[rp + 1][cc];
+    const double2 al = G[2 * s], be = G[2 * s + 1];
+    double2 o;
+    if (!(r & 1))   // al zp - conj(be) zh
+      o = make_double2(al.x * zp.x - al.y * zp.y - (be.x * zh.x + be.y * zh.y),
+                       al.x * zp.y + al.y * zp.x - (be.x * zh.y - be.y * zh.x));
+    else            // be zp + conj(al) zh
+      o = make_double2(be.x * zp.x - be.y * zp.y + (al.x * zh.x + al.y * zh.y),
+                       be.x * zp.y + be.y * zp.x + (al.x * zh.y - al.y * zh.x));
+    U[r + (int64_t)(j0 + c) * n] = o;
+  }
+}
+
+// V' (column-major n x n, interleaved rows) for the one-stage back-transform
+// (dwhmc_eig.hip): column 2j = v_j, 2j+1 = Theta v_j (Theta (u; v) = (-conj
+// v; conj u)) on the rows of the sites > j, zero elsewhere; columns 2M-2,
+// 2M-1 zero; tau'[2j] = tau'[2j+1] = tau_j (real).  v_j from A's bottom rows
+// (the reduction's storage: particle at row M + s of column 2j, hole of 2j+1).
+__global__ __launch_bounds__(256) void k_q_vexpand(const double2* __restrict__ A, int64_t sA,
+                                                   const double* __restrict__ tau, int M, double2* __restrict__ V,
+                                                   double2* __restrict__ tauc) {
+  const int k = blockIdx.z, n = 2 * M, c = blockIdx.y, r = blockIdx.x * 256 + threadIdx.x;
+  A += k * sA;
+  V += k * sA;
+  const int j = c >> 1, s = r >> 1;
+  if (r == 0) tauc[(int64_t)k * n + c] = make_double2(j <= M - 2 ? tau[(int64_t)k * M + j] : 0.0, 0.0);
+  if (r >= n) return;
+  double2 o = make_double2(0.0, 0.0);
+  if (j <= M - 2 && s >= j + 1) {
+    const double2 vp = A[M + s + (int64_t)(2 * j) * n], vh = A[M + s + (int64_t)(2 * j + 1) * n];
+    if (!(c & 1))
+      o = (r & 1) ? vh : vp;
+    else
+      o = (r & 1) ? make_double2(vp.x, -vp.y) : make_double2(-vh.x, vh.y);
+  }
+  V[r + (int64_t)c * n] = o;
+}
+
+// The eigenvectors in the BdG order: column j >= j0 from U' (interleaved rows),
+// column j < j0 the particle-hole partner Theta of column n - 1 - j.
+__global__ __launch_bounds__(256) void k_q_final(const double2* __restrict__ Ui, int64_t sU, int M, int j0,
+                                                 double2* __restrict__ U) {
+  const int k = blockIdx.z, n = 2 * M, j = blockIdx.y, r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= n) return;
+  Ui += k * sU;
+  U += k * sU;
+  const bool hole = r >= M;
+  const int s = hole ? r - M : r;
+  double2 o;
+  if (j >= j0) {
+    o = Ui[2 * s + (hole ? 1 : 0) + (int64_t)j * n];
+  } else {
+    const int jp = n - 1 - j;
+    const double2 v = Ui[2 * s + (hole ? 0 : 1) + (int64_t)jp * n];
+    o = hole ? make_double2(v.x, -v.y) : make_double2(-v.x, v.y);
+  }
+  U[r + (int64_t)j * n] = o;
 }
 
 }  // namespace
@@ -756,17 +1107,44 @@ void launch_q_reduce(double2* A, int M, int64_t sA, double2* part, int64_t sP, d
 
 void launch_q_rot(const double* qa, const double2* qd, const double2* Y, int M, double* ra, double2* rd, double* rb,
                   double2* G, int m, hipStream_t s) {
-  hipLaunchKernelGGL(k_q_rot, dim3((m + 63) / 64), dim3(64), 0, s, qa, qd, Y, M, ra, rd, rb, G, m);
+  hipLaunchKernelGGL(k_q_rot, dim3(m), dim3(kQRotT), 0, s, qa, qd, Y, M, ra, rd, rb, G);
 }
 
 void launch_q_bisect(const double* ra, const double2* rd, const double* rb, int M, double* E, double* tnorm, int m,
                      hipStream_t s) {
-  const int n = 2 * M;
+  // the upper half only, the lower mirrored (E_{n-1-j} = -E_j)
+  const int n = 2 * M, jofs = M, ni = n - jofs;
   int lgG = 6;
-  while (lgG > 2 && ((int64_t)m * n << (lgG - 1)) >= (int64_t)2048 * 64) --lgG;
+  while (lgG > 2 && ((int64_t)m * ni << (lgG - 1)) >= (int64_t)2048 * 64) --lgG;
   const int per_wg = kQBisW << (6 - lgG);
-  hipLaunchKernelGGL(k_q_bisect, dim3((n + per_wg - 1) / per_wg, m), dim3(64 * kQBisW), 4 * M * sizeof(double), s,
-                     ra, rd, rb, M, lgG, E, tnorm);
+  hipLaunchKernelGGL(k_q_bisect, dim3((ni + per_wg - 1) / per_wg, m), dim3(64 * kQBisW), 4 * M * sizeof(double), s,
+                     ra, rd, rb, M, lgG, jofs, E, tnorm);
+}
+
+int64_t q_invit_scratch(int M, int j0) { return (int64_t)2 * M * 6 * (2 * M - j0); }
+
+void launch_q_invit(const double* ra, const double2* rd, const double* rb, int M, const double* E, const double* tnorm,
+                    int j0, double2* Zt, int64_t sZ, double2* S, int64_t sS, int m, hipStream_t s) {
+  const int nv = 2 * M - j0;
+  hipLaunchKernelGGL(k_q_invit, dim3((nv + 63) / 64, m), dim3(64), (size_t)4 * M * sizeof(double), s, ra, rd, rb, M,
+                     E, tnorm, j0, Zt, sZ, S, sS);
+}
+
+void launch_q_ztu(const double2* Yt, int64_t sY, const double2* G, int M, int j0, double2* U, int64_t sU, int m,
+                  hipStream_t s) {
+  const int n = 2 * M, nv = n - j0;
+  hipLaunchKernelGGL(k_q_ztu, dim3((nv + 63) / 64, (n + 31) / 32, m), dim3(256), 0, s, Yt, sY, G, M, j0, U, sU);
+}
+
+void launch_q_vexpand(const double2* A, int64_t sA, const double* tau, int M, double2* V, double2* tauc, int m,
+                      hipStream_t s) {
+  const int n = 2 * M;
+  hipLaunchKernelGGL(k_q_vexpand, dim3((n + 255) / 256, n, m), dim3(256), 0, s, A, sA, tau, M, V, tauc);
+}
+
+void launch_q_final(const double2* Ui, int64_t sU, int M, int j0, double2* U, int m, hipStream_t s) {
+  const int n = 2 * M;
+  hipLaunchKernelGGL(k_q_final, dim3((n + 255) / 256, n, m), dim3(256), 0, s, Ui, sU, M, j0, U);
 }
 
 }  // namespace dwh

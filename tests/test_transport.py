@@ -550,3 +550,31 @@ def test_host_mirror_measure_transport_and_spectra(dwhmc, oracle):
     oc, _, _ = O.evaluate(po, st.disorder_pot, st.Delta)
     ref = O.measure_transport_and_spectra(oc, po)
     _check_transport({k: getattr(res, k) for k in ref}, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("Lx,Ly,quat", [(6, 4, "1"), (8, 8, "1"), (12, 8, "1"), (12, 8, "0"), (16, 16, "1")])
+def test_transport_structure_preserving_solver(dwhmc, oracle, monkeypatch, Lx, Ly, quat):
+    """The measurement on the structure-preserving eigensolver (reduction site
+    by site, inverse iteration on the 2 x 2-block tridiagonal T, site
+    rotations, reflector-pair back-transform, Θ partners: csrc/dwhmc_qeig.hip)
+    against the oracle at the same tolerances, and DWHMC_EIG_QUAT=0 (the
+    one-stage solver); dwh_info_t::eig_quat reports which one ran."""
+    O = oracle
+    monkeypatch.setenv("DWHMC_EIG_QUAT", quat)
+    p, dis, D = _case(O, Lx, Ly, 16.0, seed=700 + Lx + Ly)
+    cache, _, _ = O.evaluate(p, dis, D)
+    ref = O.measure_transport_and_spectra(cache, p)
+    ctx = _ctx(dwhmc, p, dis)
+    ctx.set_pairing(D)
+    r = ctx.measure_transport(p.eta, p.domega, p.omega_max)
+    assert ctx.info["eig_quat"] == (1 if quat == "1" else 0)
+    assert ctx.info["eig_half"] == 1
+    E, U = ctx.eigensystem(0)
+    ctx.close()
+    _check_transport(r, ref)
+    n = 2 * p.N
+    H = O.hermitian_from_upper(cache.H_base)
+    scale = 1.0 + np.max(np.abs(E))
+    assert np.max(np.abs(H @ U - U * E[None, :])) / scale < 1e-12
+    assert np.max(np.abs(U.conj().T @ U - np.eye(n))) < 1e-12
