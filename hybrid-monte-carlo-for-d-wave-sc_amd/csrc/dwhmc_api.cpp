@@ -2401,7 +2401,10 @@ constexpr int kEigStreams = 2, kEigStreamsMax = 4;
 
 // back-transform: W = V^H U is only NB x n, so with fewer than 4 matrices its
 // K range is split into up to kEigKS chunks (one batched zgemm per matrix)
-constexpr int kEigKS = 8;
+#ifndef EIG_KS
+#define EIG_KS 8   // (A/B builds)
+#endif
+constexpr int kEigKS = EIG_KS;
 
 // the own eigensolver's per-matrix workspace for m matrices (both solvers)
 int eig_scratch(dwh_ctx* ctx, int m) {

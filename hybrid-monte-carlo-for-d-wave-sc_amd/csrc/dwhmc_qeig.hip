@@ -52,6 +52,13 @@ namespace dwh {
 namespace {
 
 constexpr int kQTB = 64;     // pass tile: rows x columns
+#ifndef QINVIT_ITERS
+#define QINVIT_ITERS 2   // inverse-iteration solves per eigenvector (at most)
+#endif
+#ifndef QINVIT_SHARE
+#define QINVIT_SHARE 1e-6
+#endif
+constexpr double kQInvitShare = QINVIT_SHARE;   // bound on the other eigenvectors' share after one solve
 constexpr int kQRS = 1024;   // k_q_rs threads
 constexpr int kQMaxR = 3;    // rows per k_q_rs thread: M <= kQMaxM
 }  // namespace
@@ -132,10 +139,13 @@ __device__ __forceinline__ void block_sum3(double& a, double& b, double& c, doub
 // Per-matrix scratch q of the reduction (doubles): P [M][4] as 64-bit fixed
 // point (p_p re, im, p_h re, im of p = H v, accumulated by k_q_pass with
 // integer atomics: exact, so the sum is the same bits in any order), the
-// fixed-point scale of each reflector [M], the Frobenius partials [256] and
-// ||H||_F.
-__host__ __device__ __forceinline__ int64_t q_scale_off(int M) { return 4 * (int64_t)M; }
-__host__ __device__ __forceinline__ int64_t q_fro_off(int M) { return 5 * (int64_t)M; }
+// dots r = v^H p and c' = sum (v_h p_p - v_p p_h) (c = v^H Theta p = conj c')
+// accumulated the same way [4], the fixed-point scales of p and of the dots
+// per reflector [M] each, the Frobenius partials [256] and ||H||_F.
+__host__ __device__ __forceinline__ int64_t q_racc_off(int M) { return 4 * (int64_t)M; }
+__host__ __device__ __forceinline__ int64_t q_scale_off(int M) { return 4 * (int64_t)M + 4; }
+__host__ __device__ __forceinline__ int64_t q_scale2_off(int M) { return 5 * (int64_t)M + 4; }
+__host__ __device__ __forceinline__ int64_t q_fro_off(int M) { return 6 * (int64_t)M + 4; }
 constexpr int kQFro = 256;   // k_q_fro workgroups
 
 // Diagnostic build only (-DQSTAMPS, tools/q_ab.sh): s_memrealtime (100 MHz)
@@ -199,7 +209,7 @@ __global__ __launch_bounds__(kQRS) void k_q_rs(double2* __restrict__ A, int M, i
   Y += (int64_t)k * 2 * M;
   qa += (int64_t)k * M;
   qd += (int64_t)k * M;
-  __shared__ double sh1[kQRS / 64][3], sh2[kQRS / 64][3];
+  __shared__ double sh2[kQRS / 64][3];
   __shared__ double2 bc[6];
   const int s0 = j + 1;            // site j+1: the column pair reduced next
   const int m = M - s0;            // active sites of step j (j >= 0), rows i <-> site s0 + i
@@ -207,7 +217,7 @@ __global__ __launch_bounds__(kQRS) void k_q_rs(double2* __restrict__ A, int M, i
   QST(0);
   const double2 z = make_double2(0.0, 0.0);
   double2 cp[kQMaxR], ch[kQMaxR];  // site s0's particle / hole column at row s0 + i (updated)
-  double2 pp[kQMaxR], ph[kQMaxR], vp[kQMaxR], vh[kQMaxR], wp[kQMaxR], wh[kQMaxR];
+  double2 vp[kQMaxR], vh[kQMaxR], wp[kQMaxR], wh[kQMaxR];
   const double2* vpj = A + M + (int64_t)(2 * j) * n;       // v_j by site: particle
   const double2* vhj = A + M + (int64_t)(2 * j + 1) * n;   // hole
   // uniform values as vector loads (a scalar load is sunk to its use, after
@@ -216,60 +226,54 @@ __global__ __launch_bounds__(kQRS) void k_q_rs(double2* __restrict__ A, int M, i
   asm volatile("v_mov_b32 %0, 0" : "=v"(zv));
   const double tj = upd ? tau[j + zv] : 0.0;
   const double isc = upd ? 1.0 / q[q_scale_off(M) + j + zv] : 0.0;
+  const double isc2 = upd ? 1.0 / q[q_scale2_off(M) + j + zv] : 0.0;
+  long long* Racc = reinterpret_cast<long long*>(q + q_racc_off(M));
+  const long long ra0 = upd ? Racc[zv] : 0, ra1 = upd ? Racc[1 + zv] : 0, ra2 = upd ? Racc[2 + zv] : 0;
   const double fro = upd ? q[q_fro_off(M) + kQFro + zv] : (t < kQFro ? q[q_fro_off(M) + t] : 0.0);
+  // r = v^H p and c = v^H Theta p = conj(sum v_h p_p - v_p p_h), accumulated
+  // by k_q_pass tile by tile (fixed point, exact); w1 = tau p - tau^2 / 2 (r v
+  // - conj(c) Theta v), (Theta v)_p = -conj v_h, (Theta v)_h = conj v_p, formed
+  // as p arrives
+  const double r = (double)ra0 * isc2, cr = (double)ra1 * isc2, ci = -(double)ra2 * isc2;
+  const double h2 = 0.5 * tj * tj;
+  const double2 cc = make_double2(cr, -ci);
+  auto w1 = [&](double2 a_p, double2 a_h, double2 b_p, double2 b_h, double2& o_p, double2& o_h) {
+    // (a: v, b: p) -> (o_p, o_h) = w1
+    const double2 tvp = cneg(cconj(a_h)), tvh = cconj(a_p);
+    const double2 ap = cmac(cscale(r, a_p), cneg(cc), tvp), ah = cmac(cscale(r, a_h), cneg(cc), tvh);
+    o_p = make_double2(tj * b_p.x - h2 * ap.x, tj * b_p.y - h2 * ap.y);
+    o_h = make_double2(tj * b_h.x - h2 * ah.x, tj * b_h.y - h2 * ah.y);
+  };
 #pragma unroll
   for (int u = 0; u < kQMaxR; ++u) {
     const int i = t + u * kQRS;
-    cp[u] = ch[u] = pp[u] = ph[u] = vp[u] = vh[u] = wp[u] = wh[u] = z;
+    cp[u] = ch[u] = vp[u] = vh[u] = wp[u] = wh[u] = z;
     if (i < m) {
       cp[u] = A[(int64_t)(s0 + i) + (int64_t)s0 * n];
       ch[u] = A[(int64_t)(s0 + i) + (int64_t)(M + s0) * n];
       if (upd) {
         const long long* ps = P + 4 * (int64_t)(s0 + i);
-        pp[u] = make_double2((double)ps[0] * isc, (double)ps[1] * isc);
-        ph[u] = make_double2((double)ps[2] * isc, (double)ps[3] * isc);
+        const double2 pp = make_double2((double)ps[0] * isc, (double)ps[1] * isc);
+        const double2 ph = make_double2((double)ps[2] * isc, (double)ps[3] * isc);
         vp[u] = vpj[s0 + i];
         vh[u] = vhj[s0 + i];
+        w1(vp[u], vh[u], pp, ph, wp[u], wh[u]);
       }
     }
   }
   double hf = fro;
   if (upd) {
-    double r = 0.0, cr = 0.0, ci = 0.0;
-#pragma unroll
-    for (int u = 0; u < kQMaxR; ++u) {
-      // r = v^H p; c = v^H Theta p, (Theta p)_p = -conj p_h, (Theta p)_h = conj p_p
-      r += vp[u].x * pp[u].x + vp[u].y * pp[u].y + vh[u].x * ph[u].x + vh[u].y * ph[u].y;
-      const double2 c1 = cmac_c(z, cneg(cconj(ph[u])), vp[u]);   // conj(vp) (-conj ph)
-      const double2 c2 = cmac_c(z, cconj(pp[u]), vh[u]);
-      cr += c1.x + c2.x;
-      ci += c1.y + c2.y;
-    }
     QST(1);
-    // the row-0 entries (thread 0) published with this reduction's barrier
+    // the row-0 entries (thread 0)
     if (t == 0) {
       bc[0] = vp[0];
       bc[1] = vh[0];
-      bc[2] = pp[0];
-      bc[3] = ph[0];
+      bc[2] = wp[0];
+      bc[3] = wh[0];
     }
-    block_sum3(r, cr, ci, sh1);
+    __syncthreads();
     QST(2);
-    // w1 = tau p - tau^2 / 2 (r v - conj(c) Theta v), (Theta v)_p = -conj v_h, (Theta v)_h = conj v_p
-    const double h2 = 0.5 * tj * tj;
-    const double2 cc = make_double2(cr, -ci);
-    auto w1 = [&](double2 a_p, double2 a_h, double2 b_p, double2 b_h, double2& o_p, double2& o_h) {
-      // (a: v, b: p) -> (o_p, o_h) = w1
-      const double2 tvp = cneg(cconj(a_h)), tvh = cconj(a_p);
-      const double2 ap = cmac(cscale(r, a_p), cneg(cc), tvp), ah = cmac(cscale(r, a_h), cneg(cc), tvh);
-      o_p = make_double2(tj * b_p.x - h2 * ap.x, tj * b_p.y - h2 * ap.y);
-      o_h = make_double2(tj * b_h.x - h2 * ah.x, tj * b_h.y - h2 * ah.y);
-    };
-#pragma unroll
-    for (int u = 0; u < kQMaxR; ++u) w1(vp[u], vh[u], pp[u], ph[u], wp[u], wh[u]);
-    const double2 v0p = bc[0], v0h = bc[1];
-    double2 w0p, w0h;
-    w1(bc[0], bc[1], bc[2], bc[3], w0p, w0h);
+    const double2 v0p = bc[0], v0h = bc[1], w0p = bc[2], w0h = bc[3];
     QST(3);
     // column s0 (particle, l = 0): v_l = v0p, w_l = w0p, tv_l = -conj v0h, tw_l = -conj w0h;
     // column M + s0 (hole, l = m): v_l = v0h, w_l = w0h, tv_l = conj v0p, tw_l = conj w0p
@@ -353,21 +357,19 @@ __global__ __launch_bounds__(kQRS) void k_q_rs(double2* __restrict__ A, int M, i
       ps[0] = ps[1] = ps[2] = ps[3] = 0;
     }
     if (refl && i >= 1) {
-      double2 xp = cp[u], xh = cconj(ch[u]);
-      if (i == 1) {
-        if (e1only) {
-          xp.x += nx;
-        } else {
-          xp = cscale(1.0 + sc, xp);
-          xh = cscale(1.0 + sc, xh);
-        }
-      }
-      vpn[s0 + i] = nx > 0.0 ? xp : z;
-      vhn[s0 + i] = nx > 0.0 ? xh : z;
+      // row 1 (site s0 + 1): x1 (1 + s), or x1 + |x| e_p when x1 = 0 (branch-free)
+      const bool first = i == 1;
+      const double fac = first && !e1only ? 1.0 + sc : 1.0, add = first && e1only ? nx : 0.0;
+      const double keep = nx > 0.0 ? 1.0 : 0.0;
+      const double2 xp = make_double2(keep * (fac * cp[u].x + add), keep * fac * cp[u].y);
+      const double2 xh = make_double2(keep * fac * ch[u].x, -keep * fac * ch[u].y);
+      vpn[s0 + i] = xp;
+      vhn[s0 + i] = xh;
     }
   }
   if (t == 0) {
     if (!upd) q[q_fro_off(M) + kQFro] = hf;
+    if (upd) Racc[0] = Racc[1] = Racc[2] = 0;   // for the next pass's atomics
     if (refl) {
       tau[s0] = tq;
       Y[2 * s0] = yp;
@@ -375,6 +377,9 @@ __global__ __launch_bounds__(kQRS) void k_q_rs(double2* __restrict__ A, int M, i
       // fixed-point scale of p = H v_{s0}: |p_i| <= ||H||_F |v| = ||H||_F sqrt(2 / tau) < 2^60 / scale
       const double bnd = tq > 0.0 ? hf * sqrt(2.0 / tq) : 0.0;
       q[q_scale_off(M) + s0] = bnd > 0.0 ? ldexp(1.0, 59 - ilogb(bnd)) : 1.0;
+      // and of the dots: |r|, |c| <= ||H||_F |v|^2
+      const double bnd2 = tq > 0.0 ? hf * (2.0 / tq) : 0.0;
+      q[q_scale2_off(M) + s0] = bnd2 > 0.0 ? ldexp(1.0, 59 - ilogb(bnd2)) : 1.0;
     }
   }
   QST(7);
@@ -442,6 +447,7 @@ __global__ __launch_bounds__(64 * kQPW) void k_q_pass(double2* __restrict__ A, i
   const double scale = q[q_scale_off(M) + j + 1 + zv];
   // per column: v_l, w_l, tv_l, tw_l (pair j, by block type), v'_p, v'_h (v_{j+1})
   __shared__ double2 cv[kQTB][6];
+  __shared__ double2 rowv[kQTB][2];   // v_{j+1} at the tile's rows (particle, hole)
   __shared__ double rowp[kQPW][kQTB][4];
   __shared__ double colsum[kQTB][4];
   const double2* vpj = A + M + (int64_t)(2 * j) * n;
@@ -480,6 +486,10 @@ __global__ __launch_bounds__(64 * kQPW) void k_q_pass(double2* __restrict__ A, i
     }
     npr = vpn[sr];
     nhr = vhn[sr];
+  }
+  if (tid < kQTB) {
+    rowv[tid][0] = npr;
+    rowv[tid][1] = nhr;
   }
   __syncthreads();
   QSTP(1);
@@ -573,11 +583,52 @@ __global__ __launch_bounds__(64 * kQPW) void k_q_pass(double2* __restrict__ A, i
     unsigned long long* P = reinterpret_cast<unsigned long long*>(q);
     const int srs = R * kQTB + so, scs = C * kQTB + so;
     auto fx = [&](double x) { return (unsigned long long)__double2ll_rn(x * scale); };
+    // this entry's share of r = v^H p and c' = sum (v_h p_p - v_p p_h)
+    double dr = 0.0, dcr = 0.0, dci = 0.0;
+    auto dots = [&](double val, double2 vp, double2 vh) {
+      if (e == 0) {        // Re p_p
+        dr += vp.x * val;
+        dcr += vh.x * val;
+        dci += vh.y * val;
+      } else if (e == 1) { // Im p_p
+        dr += vp.y * val;
+        dcr -= vh.y * val;
+        dci += vh.x * val;
+      } else if (e == 2) { // Re p_h
+        dr += vh.x * val;
+        dcr -= vp.x * val;
+        dci -= vp.y * val;
+      } else {             // Im p_h
+        dr += vh.y * val;
+        dcr += vp.y * val;
+        dci -= vp.x * val;
+      }
+    };
     if (R == C) {
-      if (srs < M && srs >= s1) atomicAdd(&P[(int64_t)srs * 4 + e], fx(rv + cvs));
+      if (srs < M && srs >= s1) {
+        atomicAdd(&P[(int64_t)srs * 4 + e], fx(rv + cvs));
+        dots(rv + cvs, rowv[so][0], rowv[so][1]);
+      }
     } else {
-      if (srs < M && srs >= s1) atomicAdd(&P[(int64_t)srs * 4 + e], fx(rv));
-      if (scs < M && scs >= s1) atomicAdd(&P[(int64_t)scs * 4 + e], fx(cvs));
+      if (srs < M && srs >= s1) {
+        atomicAdd(&P[(int64_t)srs * 4 + e], fx(rv));
+        dots(rv, rowv[so][0], rowv[so][1]);
+      }
+      if (scs < M && scs >= s1) {
+        atomicAdd(&P[(int64_t)scs * 4 + e], fx(cvs));
+        dots(cvs, cv[so][4], cv[so][5]);
+      }
+    }
+    // per wave (no barrier: the tile's stores are in flight), three fixed-point atomics
+    dr = dpp_wave_sum(dr);
+    dcr = dpp_wave_sum(dcr);
+    dci = dpp_wave_sum(dci);
+    if (lane == 0) {
+      const double sc2 = q[q_scale2_off(M) + j + 1];
+      unsigned long long* Ra = reinterpret_cast<unsigned long long*>(q + q_racc_off(M));
+      atomicAdd(&Ra[0], (unsigned long long)__double2ll_rn(dr * sc2));
+      atomicAdd(&Ra[1], (unsigned long long)__double2ll_rn(dcr * sc2));
+      atomicAdd(&Ra[2], (unsigned long long)__double2ll_rn(dci * sc2));
     }
   }
   QSTP(6);
@@ -712,8 +763,12 @@ __global__ __launch_bounds__(kQRotT) void k_q_rot(const double* __restrict__ qa,
 // sigma_z; S = [[p, q], [conj q, r]] contributes 1 negative eigenvalue when
 // det < 0, 2 when det > 0 and p < 0.  A determinant below pivmin = (eps
 // ||T||)^2 is replaced by -pivmin (keeps b^2 / det and the next determinant
-// finite).  LDS: a' [0, M), d' [M, 3M) (re, im), b^2 [3M, 4M).
-constexpr int kQBisW = 8;
+// finite).  LDS: one record (a', d' re, d' im, b^2) per site.
+#ifndef QBIS_W
+#define QBIS_W 4
+#endif
+constexpr int kQBisW = QBIS_W;   // waves per bisection workgroup
+constexpr int kQBisPad = 8;   // Sturm sweep block (sites); zero records past M
 __global__ __launch_bounds__(64 * kQBisW) void k_q_bisect(const double* __restrict__ ra, const double2* __restrict__ rd,
                                                           const double* __restrict__ rb, int M, int lgG, int jofs,
                                                           double* __restrict__ E, double* __restrict__ tnorm) {
@@ -725,14 +780,18 @@ __global__ __launch_bounds__(64 * kQBisW) void k_q_bisect(const double* __restri
   E += (int64_t)k * n;
   __shared__ double shn[kQBisW];
   double tl = 0.0;
-  for (int s = threadIdx.x; s < M; s += blockDim.x) {
+  // one 32-byte record per site: a, d (re, im), b^2 (b_{M-1} = 0); zero
+  // records past M (kQBisPad) so the blocked sweep reads without bounds checks
+  double4* rec = reinterpret_cast<double4*>(lds);
+  for (int s = threadIdx.x; s < M + kQBisPad; s += blockDim.x) {
+    if (s >= M) {
+      rec[s] = make_double4(0.0, 0.0, 0.0, 0.0);
+      continue;
+    }
     const double a = ra[s];
     const double2 d = rd[s];
     const double bl = s > 0 ? rb[s - 1] : 0.0, br = s + 1 < M ? rb[s] : 0.0;
-    lds[s] = a;
-    lds[M + 2 * s] = d.x;
-    lds[M + 2 * s + 1] = d.y;
-    lds[3 * M + s] = br * br;
+    rec[s] = make_double4(a, d.x, d.y, br * br);
     tl = fmax(tl, fabs(a) + sqrt(d.x * d.x + d.y * d.y) + fabs(bl) + fabs(br));
   }
   for (int off = 32; off > 0; off >>= 1) tl = fmax(tl, __shfl_xor(tl, off, 64));
@@ -741,7 +800,9 @@ __global__ __launch_bounds__(64 * kQBisW) void k_q_bisect(const double* __restri
   double tn = 0.0;
   for (int w = 0; w < kQBisW; ++w) tn = fmax(tn, shn[w]);
   if (blockIdx.x == 0 && threadIdx.x == 0) tnorm[k] = tn;
-  const double gl = -tn * (1.0 + 4.0 * DBL_EPSILON) - 1e-300, gu = tn * (1.0 + 4.0 * DBL_EPSILON) + 1e-300;
+  // (jofs > 0: the upper half of a spectrum symmetric about 0 lies in [0, ||T||])
+  const double gl = jofs > 0 ? -1e-300 : -tn * (1.0 + 4.0 * DBL_EPSILON) - 1e-300,
+               gu = tn * (1.0 + 4.0 * DBL_EPSILON) + 1e-300;
   const double pivmin = (DBL_EPSILON * tn) * (DBL_EPSILON * tn) + DBL_MIN;
   const int G = 1 << lgG, g0 = lane & ~(G - 1), gi = lane & (G - 1);
   // indices jofs .. n-1; (jofs > 0) the lower half mirrored: the spectrum of
@@ -757,20 +818,28 @@ __global__ __launch_bounds__(64 * kQBisW) void k_q_bisect(const double* __restri
     if (mid <= lo || mid >= hi) done = true;
     if (__ballot(!done) == 0) break;
     const double x = fmin(lo + (gi + 1) * ((hi - lo) * step), hi);
-    double p = lds[0] - x, qr = lds[M], qi = lds[M + 1], r = -lds[0] - x;
+    const double4 r0s = rec[0];
+    double p = r0s.x - x, qr = r0s.y, qi = r0s.z, r = -r0s.x - x;
     int c = 0;
-    for (int s = 0; s < M; ++s) {
-      double det = p * r - (qr * qr + qi * qi);
-      if (fabs(det) < pivmin) det = -pivmin;
-      c += det < 0.0 ? 1 : (p < 0.0 ? 2 : 0);
-      if (s + 1 < M) {
-        const double r0 = __builtin_amdgcn_rcp(det);
-        const double rq = fma(r0, fma(-det, r0, 1.0), r0);
-        const double f = lds[3 * M + s] * rq;
-        const double a1 = lds[s + 1];
+    // blocks of kQBisPad sites, the block's records read up front (one LDS
+    // wait per block, not one per site on the chain); past M the records are
+    // zero (b^2 = 0: no coupling) and the counts are masked
+    for (int s0 = 0; s0 < M; s0 += kQBisPad) {
+      double4 rr[kQBisPad + 1];
+#pragma unroll
+      for (int u = 0; u <= kQBisPad; ++u) rr[u] = rec[s0 + u];
+#pragma unroll
+      for (int u = 0; u < kQBisPad; ++u) {
+        double det = p * r - (qr * qr + qi * qi);
+        if (fabs(det) < pivmin) det = -pivmin;
+        c += s0 + u < M ? (det < 0.0 ? 1 : (p < 0.0 ? 2 : 0)) : 0;
+        const double q0 = __builtin_amdgcn_rcp(det);
+        const double rq = fma(q0, fma(-det, q0, 1.0), q0);
+        const double f = rr[u].w * rq;
+        const double a1 = rr[u + 1].x;
         const double np = (a1 - x) - f * r, nr = (-a1 - x) - f * p;
-        qr = lds[M + 2 * (s + 1)] - f * qr;
-        qi = lds[M + 2 * (s + 1) + 1] - f * qi;
+        qr = rr[u + 1].y - f * qr;
+        qi = rr[u + 1].z - f * qi;
         p = np;
         r = nr;
       }
@@ -813,12 +882,16 @@ __device__ __forceinline__ double2 q_tent(const double* L, int M, double lam, in
   return make_double2(0.0, 0.0);
 }
 
+// start vector entry (a fixed pseudo-random value in [-1/2, 1/2) per
+// (eigenvalue index, component): a 32-bit integer hash, cheap inside the sweep)
 __device__ __forceinline__ double q_start(int j, int r) {
-  unsigned long long x = ((unsigned long long)(unsigned)j << 32 | (unsigned)r) + 0x9E3779B97F4A7C15ull;
-  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-  x ^= x >> 31;
-  return (double)(x >> 11) * 0x1.0p-53 - 0.5;
+  unsigned h = (unsigned)r * 0x9E3779B1u ^ (unsigned)j * 0x85EBCA6Bu;
+  h ^= h >> 15;
+  h *= 0x2C1B3C6Du;
+  h ^= h >> 12;
+  h *= 0x297A2D39u;
+  h ^= h >> 15;
+  return (double)h * 0x1.0p-32 - 0.5;
 }
 
 __device__ __forceinline__ double2 cmul2(double2 a, double2 b) {
@@ -858,7 +931,7 @@ __global__ __launch_bounds__(64) void k_q_invit(const double* __restrict__ ra, c
   double2* sc = S + k * sS + jj;
   const double2 zero = make_double2(0.0, 0.0);
   double scale = 1.0;
-  for (int it = 0; it < 2; ++it) {
+  for (int it = 0; it < QINVIT_ITERS; ++it) {
     auto rhs = [&](int r) -> double2 {
       if (r >= n) return zero;
       if (it == 0) return make_double2(q_start(j0 + jj, 2 * r), q_start(j0 + jj, 2 * r + 1));
@@ -873,11 +946,26 @@ __global__ __launch_bounds__(64) void k_q_invit(const double* __restrict__ ra, c
       w2[c] = q_tent(lds, M, lam, 2, c);
     }
     double2 y0 = rhs(0), y1 = rhs(1), y2 = rhs(2);
+    double nb2 = (y0.x * y0.x + y0.y * y0.y) + (y1.x * y1.x + y1.y * y1.y) + (y2.x * y2.x + y2.y * y2.y);
     // one elimination step (row kk leaves the window into the scratch)
-    auto step = [&](int kk, double2 ny) {
-      double2 nr[5];   // the next window row (row kk+3 at columns kk+1 .. kk+5)
-#pragma unroll
-      for (int c = 0; c < 5; ++c) nr[c] = q_tent(lds, M, lam, kk + 3, kk + 1 + c);
+    // hole: the parity of row kk+3 (a compile-time constant in the unrolled sweep)
+    auto step = [&](int kk, bool hole, double2 ny) {
+      // the next window row: row r = kk+3 at columns r-2 .. r+2, branch-free
+      //   particle (s = r/2): [ b_{s-1}, 0, a_s - lam, d_s, b_s ]
+      //   hole:               [ -b_{s-1}, conj d_s, -a_s - lam, 0, -b_s ]
+      // (b_{M-1} = 0 from k_q_rot; rows past n are zero)
+      double2 nr[5];
+      {
+        const int r = kk + 3, sr = min(r >> 1, M - 1);
+        const double on = r < n ? 1.0 : 0.0, sg = hole ? -on : on;
+        const double as = lds[sr], bs = lds[M + sr], bm = lds[M + sr - 1];
+        const double dr = lds[2 * M + 2 * sr], di = lds[2 * M + 2 * sr + 1];
+        nr[0] = make_double2(sg * bm, 0.0);
+        nr[1] = hole ? make_double2(on * dr, -on * di) : zero;
+        nr[2] = make_double2(sg * as - on * lam, 0.0);
+        nr[3] = hole ? zero : make_double2(on * dr, on * di);
+        nr[4] = make_double2(sg * bs, 0.0);
+      }
       const double m0 = w0[0].x * w0[0].x + w0[0].y * w0[0].y;
       const double m1 = w1[0].x * w1[0].x + w1[0].y * w1[0].y;
       const double m2 = w2[0].x * w2[0].x + w2[0].y * w2[0].y;
@@ -926,11 +1014,12 @@ __global__ __launch_bounds__(64) void k_q_invit(const double* __restrict__ ra, c
       y0 = y1;
       y1 = y2;
       y2 = ny;
+      nb2 += ny.x * ny.x + ny.y * ny.y;
     };
     // forward sweep in blocks of FB steps, the next block's right-hand side
     // rows loaded one block ahead (a load's wait then only covers loads and
     // stores issued before it, not this block's scratch stores)
-    constexpr int FB = 8;
+    constexpr int FB = 4;
     double2 ra_[FB], rb_[FB];
 #pragma unroll
     for (int u = 0; u < FB; ++u) ra_[u] = rhs(3 + u);
@@ -939,12 +1028,12 @@ __global__ __launch_bounds__(64) void k_q_invit(const double* __restrict__ ra, c
       for (int u = 0; u < FB; ++u) rb_[u] = rhs(k0 + FB + 3 + u);
 #pragma unroll
       for (int u = 0; u < FB; ++u)
-        if (k0 + u < n) step(k0 + u, ra_[u]);
+        if (k0 + u < n) step(k0 + u, (u + 1) & 1, ra_[u]);
 #pragma unroll
       for (int u = 0; u < FB; ++u) ra_[u] = rhs(k0 + 2 * FB + 3 + u);
 #pragma unroll
       for (int u = 0; u < FB; ++u)
-        if (k0 + FB + u < n) step(k0 + FB + u, rb_[u]);
+        if (k0 + FB + u < n) step(k0 + FB + u, (FB + u + 1) & 1, rb_[u]);
     }
     // back substitution: x_k = (y_k - sum_t u_k,k+t x_{k+t}) / u_kk, the next
     // block's factors loaded one block ahead
@@ -988,6 +1077,23 @@ __global__ __launch_bounds__(64) void k_q_invit(const double* __restrict__ ra, c
       solve_blk(k0 - PB, fb);
     }
     scale = 1.0 / sqrt(nrm);
+    // a second solve only where the first may not have converged: the growth
+    // g = |x| / |b| bounds the other eigenvectors' share of x by 1 / (g gap)
+    // (gap: to the nearest other eigenvalue); above kQInvitShare (a start
+    // vector nearly orthogonal to the eigenvector, or a small gap) the wave
+    // solves again from x.  Below it the Löwdin step leaves O(share^2): L = 32
+    // disordered, one solve everywhere, residual 5e-15 ||H||, orthogonality
+    // 4e-14 (two solves: 7e-16, 3e-15; profiles/r06_qeig_eigensystem.txt)
+    if (it == 0 && QINVIT_ITERS > 1) {
+      const int jg = j0 + jj;
+      const double* Ek = E + (int64_t)k * n;
+      double gap = DBL_MAX;
+      if (jg > 0) gap = fmin(gap, lam - Ek[jg - 1]);
+      if (jg + 1 < n) gap = fmin(gap, Ek[jg + 1] - lam);
+      const double g = sqrt(nrm / nb2);
+      const bool need = !(g * gap * kQInvitShare > 1.0);
+      if (__ballot(need) == 0) break;
+    }
   }
   for (int r = 0; r < n; ++r) {
     const double2 v = z[(int64_t)r * nv];
@@ -1094,7 +1200,7 @@ void launch_q_reduce(double2* A, int M, int64_t sA, double2* part, int64_t sP, d
   double* q = reinterpret_cast<double*>(part);
   const int64_t sQ = 2 * sP;
   const int nT = (M + kQTB - 1) / kQTB;
-  (void)hipMemset2DAsync(q, (size_t)sQ * sizeof(double), 0, (size_t)4 * M * sizeof(double), m, s);   // P
+  (void)hipMemset2DAsync(q, (size_t)sQ * sizeof(double), 0, (size_t)(4 * M + 4) * sizeof(double), m, s);   // P, dots
   hipLaunchKernelGGL(k_q_fro, dim3(kQFro, m), dim3(256), 0, s, A, M, sA, q, sQ);
   for (int j = -1; j <= M - 2; ++j) {
     hipLaunchKernelGGL(k_q_rs, dim3(m), dim3(kQRS), 0, s, A, M, j, sA, q, sQ, W, tau, Y, qa, qd);
@@ -1117,8 +1223,8 @@ void launch_q_bisect(const double* ra, const double2* rd, const double* rb, int 
   int lgG = 6;
   while (lgG > 2 && ((int64_t)m * ni << (lgG - 1)) >= (int64_t)2048 * 64) --lgG;
   const int per_wg = kQBisW << (6 - lgG);
-  hipLaunchKernelGGL(k_q_bisect, dim3((ni + per_wg - 1) / per_wg, m), dim3(64 * kQBisW), 4 * M * sizeof(double), s,
-                     ra, rd, rb, M, lgG, jofs, E, tnorm);
+  hipLaunchKernelGGL(k_q_bisect, dim3((ni + per_wg - 1) / per_wg, m), dim3(64 * kQBisW),
+                     (size_t)4 * (M + kQBisPad) * sizeof(double), s, ra, rd, rb, M, lgG, jofs, E, tnorm);
 }
 
 int64_t q_invit_scratch(int M, int j0) { return (int64_t)2 * M * 6 * (2 * M - j0); }

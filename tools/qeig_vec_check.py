@@ -37,7 +37,8 @@ def main():
             H = O.hermitian_from_upper(cache.H_base)
             ev = np.linalg.eigvalsh(H)
             hn = np.max(np.abs(ev))
-            ctx = m.FermionContext(p.Lx, p.Ly, p.t, p.tp, p.mu, p.beta, p.J, p.nn_table, p.nnn_table, dis)
+            ctx = m.FermionContext(p.Lx, p.Ly, p.t, p.tp, p.mu, p.beta, p.J, p.nn_table, p.nnn_table, dis,
+                                   lib_path=os.environ.get("DWHMC_LIB"))
             ctx.set_pairing(D)
             out = []
             for q in ("1", "0"):
