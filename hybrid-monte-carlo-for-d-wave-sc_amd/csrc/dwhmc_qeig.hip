@@ -140,12 +140,15 @@ __device__ __forceinline__ void block_sum3(double& a, double& b, double& c, doub
 // point (p_p re, im, p_h re, im of p = H v, accumulated by k_q_pass with
 // integer atomics: exact, so the sum is the same bits in any order), the
 // dots r = v^H p and c' = sum (v_h p_p - v_p p_h) (c = v^H Theta p = conj c')
-// accumulated the same way [4], the fixed-point scales of p and of the dots
+// accumulated the same way in kQDotSlots slots [slot][4] (a pass workgroup
+// adds into slot blockIdx % kQDotSlots: one hot address would serialise the
+// atomics, +12 ms at L = 32), the fixed-point scales of p and of the dots
 // per reflector [M] each, the Frobenius partials [256] and ||H||_F.
+constexpr int kQDotSlots = 64;   // dot accumulators (spread over the pass workgroups: no hot address)
 __host__ __device__ __forceinline__ int64_t q_racc_off(int M) { return 4 * (int64_t)M; }
-__host__ __device__ __forceinline__ int64_t q_scale_off(int M) { return 4 * (int64_t)M + 4; }
-__host__ __device__ __forceinline__ int64_t q_scale2_off(int M) { return 5 * (int64_t)M + 4; }
-__host__ __device__ __forceinline__ int64_t q_fro_off(int M) { return 6 * (int64_t)M + 4; }
+__host__ __device__ __forceinline__ int64_t q_scale_off(int M) { return 4 * (int64_t)M + 4 * kQDotSlots; }
+__host__ __device__ __forceinline__ int64_t q_scale2_off(int M) { return 5 * (int64_t)M + 4 * kQDotSlots; }
+__host__ __device__ __forceinline__ int64_t q_fro_off(int M) { return 6 * (int64_t)M + 4 * kQDotSlots; }
 constexpr int kQFro = 256;   // k_q_fro workgroups
 
 // Diagnostic build only (-DQSTAMPS, tools/q_ab.sh): s_memrealtime (100 MHz)
@@ -210,7 +213,7 @@ __global__ __launch_bounds__(kQRS) void k_q_rs(double2* __restrict__ A, int M, i
   qa += (int64_t)k * M;
   qd += (int64_t)k * M;
   __shared__ double sh2[kQRS / 64][3];
-  __shared__ double2 bc[6];
+  __shared__ double2 bc[8];
   const int s0 = j + 1;            // site j+1: the column pair reduced next
   const int m = M - s0;            // active sites of step j (j >= 0), rows i <-> site s0 + i
   const bool upd = j >= 0;
@@ -228,52 +231,67 @@ __global__ __launch_bounds__(kQRS) void k_q_rs(double2* __restrict__ A, int M, i
   const double isc = upd ? 1.0 / q[q_scale_off(M) + j + zv] : 0.0;
   const double isc2 = upd ? 1.0 / q[q_scale2_off(M) + j + zv] : 0.0;
   long long* Racc = reinterpret_cast<long long*>(q + q_racc_off(M));
-  const long long ra0 = upd ? Racc[zv] : 0, ra1 = upd ? Racc[1 + zv] : 0, ra2 = upd ? Racc[2 + zv] : 0;
+  // wave 0: one dot slot per lane
+  long long ra0 = 0, ra1 = 0, ra2 = 0;
+  if (upd && t < kQDotSlots) {
+    ra0 = Racc[4 * t];
+    ra1 = Racc[4 * t + 1];
+    ra2 = Racc[4 * t + 2];
+  }
   const double fro = upd ? q[q_fro_off(M) + kQFro + zv] : (t < kQFro ? q[q_fro_off(M) + t] : 0.0);
-  // r = v^H p and c = v^H Theta p = conj(sum v_h p_p - v_p p_h), accumulated
-  // by k_q_pass tile by tile (fixed point, exact); w1 = tau p - tau^2 / 2 (r v
-  // - conj(c) Theta v), (Theta v)_p = -conj v_h, (Theta v)_h = conj v_p, formed
-  // as p arrives
-  const double r = (double)ra0 * isc2, cr = (double)ra1 * isc2, ci = -(double)ra2 * isc2;
-  const double h2 = 0.5 * tj * tj;
-  const double2 cc = make_double2(cr, -ci);
-  auto w1 = [&](double2 a_p, double2 a_h, double2 b_p, double2 b_h, double2& o_p, double2& o_h) {
-    // (a: v, b: p) -> (o_p, o_h) = w1
-    const double2 tvp = cneg(cconj(a_h)), tvh = cconj(a_p);
-    const double2 ap = cmac(cscale(r, a_p), cneg(cc), tvp), ah = cmac(cscale(r, a_h), cneg(cc), tvh);
-    o_p = make_double2(tj * b_p.x - h2 * ap.x, tj * b_p.y - h2 * ap.y);
-    o_h = make_double2(tj * b_h.x - h2 * ah.x, tj * b_h.y - h2 * ah.y);
-  };
+  double2 pp[kQMaxR], ph[kQMaxR];
 #pragma unroll
   for (int u = 0; u < kQMaxR; ++u) {
     const int i = t + u * kQRS;
-    cp[u] = ch[u] = vp[u] = vh[u] = wp[u] = wh[u] = z;
+    cp[u] = ch[u] = vp[u] = vh[u] = wp[u] = wh[u] = pp[u] = ph[u] = z;
     if (i < m) {
       cp[u] = A[(int64_t)(s0 + i) + (int64_t)s0 * n];
       ch[u] = A[(int64_t)(s0 + i) + (int64_t)(M + s0) * n];
       if (upd) {
         const long long* ps = P + 4 * (int64_t)(s0 + i);
-        const double2 pp = make_double2((double)ps[0] * isc, (double)ps[1] * isc);
-        const double2 ph = make_double2((double)ps[2] * isc, (double)ps[3] * isc);
+        pp[u] = make_double2((double)ps[0] * isc, (double)ps[1] * isc);
+        ph[u] = make_double2((double)ps[2] * isc, (double)ps[3] * isc);
         vp[u] = vpj[s0 + i];
         vh[u] = vhj[s0 + i];
-        w1(vp[u], vh[u], pp, ph, wp[u], wh[u]);
       }
     }
   }
   double hf = fro;
   if (upd) {
     QST(1);
-    // the row-0 entries (thread 0)
-    if (t == 0) {
-      bc[0] = vp[0];
-      bc[1] = vh[0];
-      bc[2] = wp[0];
-      bc[3] = wh[0];
+    // r = v^H p and c = v^H Theta p = conj(sum v_h p_p - v_p p_h), accumulated
+    // by k_q_pass tile by tile (fixed point, exact): wave 0 sums the slots;
+    // published with the row-0 entries (thread 0) through one barrier
+    if (t < 64) {
+      const double s0r = dpp_wave_sum((double)ra0 * isc2), s1r = dpp_wave_sum((double)ra1 * isc2),
+                   s2r = dpp_wave_sum((double)ra2 * isc2);
+      if (t == 0) {
+        bc[6] = make_double2(s0r, s1r);
+        bc[7] = make_double2(-s2r, 0.0);
+        bc[0] = vp[0];
+        bc[1] = vh[0];
+        bc[2] = pp[0];
+        bc[3] = ph[0];
+      }
     }
     __syncthreads();
     QST(2);
-    const double2 v0p = bc[0], v0h = bc[1], w0p = bc[2], w0h = bc[3];
+    const double r = bc[6].x, cr = bc[6].y, ci = bc[7].x;
+    // w1 = tau p - tau^2 / 2 (r v - conj(c) Theta v), (Theta v)_p = -conj v_h, (Theta v)_h = conj v_p
+    const double h2 = 0.5 * tj * tj;
+    const double2 cc = make_double2(cr, -ci);
+    auto w1 = [&](double2 a_p, double2 a_h, double2 b_p, double2 b_h, double2& o_p, double2& o_h) {
+      // (a: v, b: p) -> (o_p, o_h) = w1
+      const double2 tvp = cneg(cconj(a_h)), tvh = cconj(a_p);
+      const double2 ap = cmac(cscale(r, a_p), cneg(cc), tvp), ah = cmac(cscale(r, a_h), cneg(cc), tvh);
+      o_p = make_double2(tj * b_p.x - h2 * ap.x, tj * b_p.y - h2 * ap.y);
+      o_h = make_double2(tj * b_h.x - h2 * ah.x, tj * b_h.y - h2 * ah.y);
+    };
+#pragma unroll
+    for (int u = 0; u < kQMaxR; ++u) w1(vp[u], vh[u], pp[u], ph[u], wp[u], wh[u]);
+    const double2 v0p = bc[0], v0h = bc[1];
+    double2 w0p, w0h;
+    w1(bc[0], bc[1], bc[2], bc[3], w0p, w0h);
     QST(3);
     // column s0 (particle, l = 0): v_l = v0p, w_l = w0p, tv_l = -conj v0h, tw_l = -conj w0h;
     // column M + s0 (hole, l = m): v_l = v0h, w_l = w0h, tv_l = conj v0p, tw_l = conj w0p
@@ -340,6 +358,7 @@ __global__ __launch_bounds__(kQRS) void k_q_rs(double2* __restrict__ A, int M, i
   }
   QST(6);
   // the stores
+  if (upd && t < kQDotSlots) Racc[4 * t] = Racc[4 * t + 1] = Racc[4 * t + 2] = 0;   // for the next pass
   if (t == 0) {   // site s0's diagonal block (row i = 0 of its columns)
     qa[s0] = cp[0].x;
     qd[s0] = ch[0];
@@ -369,7 +388,7 @@ __global__ __launch_bounds__(kQRS) void k_q_rs(double2* __restrict__ A, int M, i
   }
   if (t == 0) {
     if (!upd) q[q_fro_off(M) + kQFro] = hf;
-    if (upd) Racc[0] = Racc[1] = Racc[2] = 0;   // for the next pass's atomics
+
     if (refl) {
       tau[s0] = tq;
       Y[2 * s0] = yp;
@@ -625,7 +644,7 @@ __global__ __launch_bounds__(64 * kQPW) void k_q_pass(double2* __restrict__ A, i
     dci = dpp_wave_sum(dci);
     if (lane == 0) {
       const double sc2 = q[q_scale2_off(M) + j + 1];
-      unsigned long long* Ra = reinterpret_cast<unsigned long long*>(q + q_racc_off(M));
+      unsigned long long* Ra = reinterpret_cast<unsigned long long*>(q + q_racc_off(M)) + 4 * (blockIdx.x % kQDotSlots);
       atomicAdd(&Ra[0], (unsigned long long)__double2ll_rn(dr * sc2));
       atomicAdd(&Ra[1], (unsigned long long)__double2ll_rn(dcr * sc2));
       atomicAdd(&Ra[2], (unsigned long long)__double2ll_rn(dci * sc2));
@@ -1200,7 +1219,8 @@ void launch_q_reduce(double2* A, int M, int64_t sA, double2* part, int64_t sP, d
   double* q = reinterpret_cast<double*>(part);
   const int64_t sQ = 2 * sP;
   const int nT = (M + kQTB - 1) / kQTB;
-  (void)hipMemset2DAsync(q, (size_t)sQ * sizeof(double), 0, (size_t)(4 * M + 4) * sizeof(double), m, s);   // P, dots
+  (void)hipMemset2DAsync(q, (size_t)sQ * sizeof(double), 0, (size_t)(4 * M + 4 * kQDotSlots) * sizeof(double), m,
+                         s);   // P, dots
   hipLaunchKernelGGL(k_q_fro, dim3(kQFro, m), dim3(256), 0, s, A, M, sA, q, sQ);
   for (int j = -1; j <= M - 2; ++j) {
     hipLaunchKernelGGL(k_q_rs, dim3(m), dim3(kQRS), 0, s, A, M, j, sA, q, sQ, W, tau, Y, qa, qd);
