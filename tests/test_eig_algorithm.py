@@ -215,3 +215,57 @@ def test_quaternion_reduction_bdg_lattices(oracle, Lx, Ly, clean, mu):
     assert np.max(np.abs(E - ev)) <= 1e-12 * scale
     assert np.max(np.abs(H @ U - U * E[None, :])) <= 1e-11 * scale
     assert np.max(np.abs(U.conj().T @ U - np.eye(2 * N))) <= 1e-12
+
+
+def _qmul(a1, b1, a2, b2):
+    """quat(a1, b1) quat(a2, b2), quat(al, be) = [[al, -conj be], [be, conj al]] (k_q_rot's qmul)."""
+    return a1 * a2 - np.conj(b1) * b2, b1 * a2 + np.conj(a1) * b2
+
+
+@pytest.mark.parametrize("M,seed", [(2, 0), (9, 1), (40, 2)])
+def test_site_rotations_prefix_scan(M, seed):
+    """k_q_rot (csrc/dwhmc_qeig.hip) forms the site rotations as a prefix
+    product instead of the recurrence g_{j+1} = q^_j tau(g_j), tau(quat(al,
+    be)) = quat(al, -be) = k g k^-1 (k = i sigma_z): g_j = x_{j-1} .. x_0
+    k^-j with x_i = q^_i k and k^-j = quat((-i)^j, 0).  Both equal
+    tools/qeig_proto.py site_rotations' g (including q_j = 0, q^ = 1)."""
+    rng = np.random.default_rng(seed)
+    Y = rng.standard_normal((M - 1, 2)) + 1j * rng.standard_normal((M - 1, 2))
+    if M > 3:
+        Y[1] = 0.0
+    a = rng.standard_normal(M)
+    d = rng.standard_normal(M) + 1j * rng.standard_normal(M)
+    g_ref, _, _, _ = QP.site_rotations(a, d, Y)
+    pa, pb = 1.0 + 0j, 0.0 + 0j   # the prefix product, later factors on the left
+    for j in range(M):
+        if j > 0:
+            nq = np.hypot(abs(Y[j - 1, 0]), abs(Y[j - 1, 1]))
+            qa, qb = (Y[j - 1, 0] / nq, Y[j - 1, 1] / nq) if nq > 0 else (1.0 + 0j, 0.0 + 0j)
+            pa, pb = _qmul(1j * qa, 1j * qb, pa, pb)   # x = q^ k = quat(i q^a, i q^b)
+        c = (-1j) ** j
+        np.testing.assert_allclose(QP.quat(pa * c, pb * c), g_ref[j], atol=1e-13)
+
+
+def test_pass_dot_shares():
+    """k_q_pass adds each p entry's share of r = v^H p and c' = sum (v_h p_p -
+    v_p p_h) (c = v^H Theta p = conj c') component by component (Re / Im of
+    p_p, p_h): the per-component formulas sum to the dots."""
+    rng = np.random.default_rng(5)
+    m = 7
+    vp, vh, pp, ph = (rng.standard_normal(m) + 1j * rng.standard_normal(m) for _ in range(4))
+    r = c_re = c_im = 0.0
+    for i in range(m):
+        for e, val in enumerate((pp[i].real, pp[i].imag, ph[i].real, ph[i].imag)):
+            if e == 0:
+                r += vp[i].real * val; c_re += vh[i].real * val; c_im += vh[i].imag * val
+            elif e == 1:
+                r += vp[i].imag * val; c_re -= vh[i].imag * val; c_im += vh[i].real * val
+            elif e == 2:
+                r += vh[i].real * val; c_re -= vp[i].real * val; c_im -= vp[i].imag * val
+            else:
+                r += vh[i].imag * val; c_re += vp[i].imag * val; c_im -= vp[i].real * val
+    v = np.concatenate([vp, vh])
+    p = np.concatenate([pp, ph])
+    assert abs(r - np.vdot(v, p).real) < 1e-12
+    c = np.vdot(v, QP.theta(p))
+    assert abs(complex(c_re, -c_im) - c) < 1e-12
