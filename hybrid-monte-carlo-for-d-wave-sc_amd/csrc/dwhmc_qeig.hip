@@ -1107,7 +1107,11 @@ __global__ __launch_bounds__(64) void k_q_invit(const double* __restrict__ ra, c
       const int jg = j0 + jj;
       const double* Ek = E + (int64_t)k * n;
       double gap = DBL_MAX;
-      if (jg > 0) gap = fmin(gap, lam - Ek[jg - 1]);
+      // (the lowest computed vector's lower neighbour -lam is its own
+      // partner's eigenvalue: a share of Theta u in x only rotates the pair
+      // x, Theta x inside their exactly orthogonal plane, by ~1 / (g 2 lam),
+      // which moves the residual by ~1 / g)
+      if (jg > j0) gap = fmin(gap, lam - Ek[jg - 1]);
       if (jg + 1 < n) gap = fmin(gap, Ek[jg + 1] - lam);
       const double g = sqrt(nrm / nb2);
       const bool need = !(g * gap * kQInvitShare > 1.0);
