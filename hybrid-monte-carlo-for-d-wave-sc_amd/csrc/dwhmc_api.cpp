@@ -2870,11 +2870,22 @@ int q_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m, bool* done) {
   // sees): E_N + E_{N+1} > kEigZeroTol ||T||, the one-stage half solve's
   // bound on it.  A single level near zero is harmless: x_N and Theta x_N
   // are orthogonal exactly (<u, Theta u> = 0 for Theta^2 = -1).
+  // Clusters (consecutive gaps <= kEigClusterTol ||T||) up to q_max_cluster()
+  // long are orthonormalised in the structure-preserving path (k_q_orth);
+  // longer ones are declined.
+  bool clusters = false;
   for (int k = 0; k < m; ++k) {
     const double* E = Eh.data() + (size_t)k * n;
     if (N + 1 < n && !(E[N] + E[N + 1] > dwh::kEigZeroTol * tn[k])) return DWH_OK;
-    for (int j = N + 1; j < n; ++j)
-      if (!(E[j] - E[j - 1] > dwh::kEigClusterTol * tn[k])) return DWH_OK;
+    int run = 1;
+    for (int j = N + 1; j < n; ++j) {
+      if (!(E[j] - E[j - 1] > dwh::kEigClusterTol * tn[k])) {
+        clusters = true;
+        if (++run > dwh::q_max_cluster()) return DWH_OK;
+      } else {
+        run = 1;
+      }
+    }
   }
   // vector workspace
   const int64_t sZ = (int64_t)n * nv, sS = dwh::q_invit_scratch(N, j0), sG = (int64_t)nv * nv;
@@ -2892,6 +2903,7 @@ int q_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m, bool* done) {
   EigPhase ph(s);
   ph.mark("q values");
   dwh::launch_q_invit(q.ra, q.rd, q.rb, N, b.E, q.tn, j0, ctx->d_qz, sZ, ctx->d_qs, sS, m, s);
+  if (clusters) dwh::launch_q_orth(b.E, q.tn, N, j0, ctx->d_qz, sZ, dwh::kEigClusterTol, ctx->d_tr_bad, m, s);
   ph.mark("q invit");
   // Löwdin on X = Zt (nv x n, ld nv): G' = X X^H (= conj(Z^H Z)), Y^T = 1.5 X - 0.5 G' X into the slots' Jmn
   const double2 one = make_double2(1.0, 0.0), zero = make_double2(0.0, 0.0);

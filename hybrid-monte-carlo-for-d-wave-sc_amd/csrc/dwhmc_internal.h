@@ -409,6 +409,11 @@ void launch_q_bisect(const double* ra, const double2* rd, const double* rb, int 
 int64_t q_invit_scratch(int M, int j0);
 void launch_q_invit(const double* ra, const double2* rd, const double* rb, int M, const double* E, const double* tnorm,
                     int j0, double2* Zt, int64_t sZ, double2* S, int64_t sS, int m, hipStream_t s);
+// the vectors of eigenvalue clusters (gaps <= ctol ||T||, at most q_max_cluster()
+// long) orthonormalised in Zt (two rounds of Cholesky QR); *bad = 1 on failure
+int q_max_cluster();
+void launch_q_orth(const double* E, const double* tnorm, int M, int j0, double2* Zt, int64_t sZ, double ctol, int* bad,
+                   int m, hipStream_t s);
 // U' columns j0.. (n x n, interleaved rows) = site rotations G of Yt (nv x n, ld nv)
 void launch_q_ztu(const double2* Yt, int64_t sY, const double2* G, int M, int j0, double2* U, int64_t sU, int m,
                   hipStream_t s);

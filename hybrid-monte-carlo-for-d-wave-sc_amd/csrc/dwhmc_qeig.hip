@@ -59,6 +59,8 @@ constexpr int kQTB = 64;     // pass tile: rows x columns
 #define QINVIT_SHARE 1e-6
 #endif
 constexpr double kQInvitShare = QINVIT_SHARE;   // bound on the other eigenvectors' share after one solve
+constexpr int kQMaxCluster = 32;   // longest eigenvalue cluster the structure-preserving solver orthonormalises
+constexpr double kQClusterShift = 1e-12;   // a cluster member's inverse-iteration shift below its level, x ||T||
 constexpr int kQRS = 1024;   // k_q_rs threads
 constexpr int kQMaxR = 3;    // rows per k_q_rs thread: M <= kQMaxM
 }  // namespace
@@ -943,8 +945,20 @@ __global__ __launch_bounds__(64) void k_q_invit(const double* __restrict__ ra, c
   __syncthreads();
   const int jj = blockIdx.x * blockDim.x + threadIdx.x;
   if (jj >= nv) return;
-  const double lam = E[(int64_t)k * n + j0 + jj];
   const double tn = tnorm[k];
+  // A member of a cluster (a neighbour within kEigClusterTol ||T||) is solved
+  // at e - kQClusterShift ||T||: for an exactly degenerate level the members'
+  // bisected values differ by ulps, and solving at them weights the
+  // eigenspace's directions by 1 / (E_i - e) — ratios of 10..1000, so the
+  // vectors turn nearly parallel and k_q_orth's Cholesky QR amplifies their
+  // out-of-cluster rounding by as much (clean 10 x 10: residual 3e-13,
+  // 1.5e-12 against the Theta partners).  A shift far above the ulp spread
+  // and far below the gap to the next level weights the eigenspace evenly.
+  const double* Ek = E + (int64_t)k * n;
+  const double e = Ek[j0 + jj];
+  const double ctol = kEigClusterTol * tn;
+  const bool member = (jj > 0 && e - Ek[j0 + jj - 1] <= ctol) || (j0 + jj + 1 < n && Ek[j0 + jj + 1] - e <= ctol);
+  const double lam = member ? e - kQClusterShift * tn : e;
   const double small = tn > 0.0 ? DBL_EPSILON * tn : DBL_EPSILON;
   double2* z = Zt + k * sZ + jj;
   double2* sc = S + k * sS + jj;
@@ -1105,14 +1119,13 @@ __global__ __launch_bounds__(64) void k_q_invit(const double* __restrict__ ra, c
     // 4e-14 (two solves: 7e-16, 3e-15; profiles/r06_qeig_eigensystem.txt)
     if (it == 0 && QINVIT_ITERS > 1) {
       const int jg = j0 + jj;
-      const double* Ek = E + (int64_t)k * n;
       double gap = DBL_MAX;
       // (the lowest computed vector's lower neighbour -lam is its own
       // partner's eigenvalue: a share of Theta u in x only rotates the pair
       // x, Theta x inside their exactly orthogonal plane, by ~1 / (g 2 lam),
       // which moves the residual by ~1 / g)
-      if (jg > j0) gap = fmin(gap, lam - Ek[jg - 1]);
-      if (jg + 1 < n) gap = fmin(gap, Ek[jg + 1] - lam);
+      if (jg > j0) gap = fmin(gap, e - Ek[jg - 1]);
+      if (jg + 1 < n) gap = fmin(gap, Ek[jg + 1] - e);
       const double g = sqrt(nrm / nb2);
       const bool need = !(g * gap * kQInvitShare > 1.0);
       if (__ballot(need) == 0) break;
@@ -1121,6 +1134,134 @@ __global__ __launch_bounds__(64) void k_q_invit(const double* __restrict__ ra, c
   for (int r = 0; r < n; ++r) {
     const double2 v = z[(int64_t)r * nv];
     z[(int64_t)r * nv] = make_double2(v.x * scale, v.y * scale);
+  }
+}
+
+// Clusters of the computed eigenvalues (consecutive gaps <= ctol ||T||, at
+// most kQMaxCluster long: longer ones are declined on the host) get their
+// inverse-iteration vectors orthonormalised, as k_eig_orth does for the
+// one-stage solver's real vectors: two rounds of Cholesky QR on the
+// cluster's columns of Zt (G = Z^H Z = L L^H, Z <- Z L^-H; a cluster's
+// columns are contiguous in each row of Zt).  One workgroup per candidate
+// first index; *bad = 1 when G is not positive definite (the caller's
+// re-solve).
+__global__ __launch_bounds__(256) void k_q_orth(const double* __restrict__ E, const double* __restrict__ tnorm, int M,
+                                                int j0, double2* __restrict__ Zt, int64_t sZ, double ctol,
+                                                int* __restrict__ bad) {
+  constexpr int MC = kQMaxCluster, RC = 32;
+  const int k = blockIdx.y, n = 2 * M, nv = n - j0, jj = blockIdx.x, tid = threadIdx.x;
+  E += (int64_t)k * n;
+  Zt += k * sZ;
+  const double tol = ctol * tnorm[k];
+  if (jj > 0 && E[j0 + jj] - E[j0 + jj - 1] <= tol) return;   // inside a cluster
+  int end = jj + 1;
+  while (end < nv && end - jj < MC && E[j0 + end] - E[j0 + end - 1] <= tol) ++end;
+  const int kc = end - jj;
+  if (kc == 1) return;
+  __shared__ double2 G[MC][MC + 1];
+  __shared__ double2 Zs[RC][MC + 1];
+  __shared__ int fail;
+  constexpr int NPT = (MC * (MC + 1) / 2 + 255) / 256;
+  const int npair = kc * (kc + 1) / 2;
+  auto pair_of = [&](int pq, int& pr, int& qc) {
+    int r = (int)((sqrt(8.0 * pq + 1.0) - 1.0) * 0.5);
+    while ((r + 1) * (r + 2) / 2 <= pq) ++r;
+    while (r * (r + 1) / 2 > pq) --r;
+    pr = r;
+    qc = pq - r * (r + 1) / 2;
+  };
+  for (int round = 0; round < 2; ++round) {
+    // G = Z_c^H Z_c (lower triangle), rows staged RC at a time
+    double2 acc[NPT];
+#pragma unroll
+    for (int u = 0; u < NPT; ++u) acc[u] = make_double2(0.0, 0.0);
+    for (int r0 = 0; r0 < n; r0 += RC) {
+      for (int q = tid; q < RC * kc; q += 256) {
+        const int rr = q / kc, c = q % kc, r = r0 + rr;
+        Zs[rr][c] = r < n ? Zt[(int64_t)r * nv + jj + c] : make_double2(0.0, 0.0);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < NPT; ++u) {
+        const int pq = tid + 256 * u;
+        if (pq < npair) {
+          int pr, qc;
+          pair_of(pq, pr, qc);
+          double2 a = acc[u];
+          for (int rr = 0; rr < RC; ++rr) {   // conj(z_p) z_q
+            const double2 zp = Zs[rr][pr], zq = Zs[rr][qc];
+            a.x += zp.x * zq.x + zp.y * zq.y;
+            a.y += zp.x * zq.y - zp.y * zq.x;
+          }
+          acc[u] = a;
+        }
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int u = 0; u < NPT; ++u) {
+      const int pq = tid + 256 * u;
+      if (pq < npair) {
+        int pr, qc;
+        pair_of(pq, pr, qc);
+        G[pr][qc] = acc[u];
+      }
+    }
+    if (tid == 0) fail = 0;
+    __syncthreads();
+    // Cholesky G = L L^H, right-looking, in place (lower)
+    for (int c = 0; c < kc; ++c) {
+      if (tid == 0) {
+        const double g = G[c][c].x;   // the columns are normalised: a pivot this small means cond(Z) > ~1e7
+        if (!(g > 1e-14)) fail = 1;
+        G[c][c] = make_double2(sqrt(fmax(g, DBL_MIN)), 0.0);
+      }
+      __syncthreads();
+      for (int r = c + 1 + tid; r < kc; r += 256) {
+        const double d = G[c][c].x;
+        G[r][c] = make_double2(G[r][c].x / d, G[r][c].y / d);
+      }
+      __syncthreads();
+      for (int pq = tid; pq < kc * kc; pq += 256) {   // G[p][q] -= L[p][c] conj(L[q][c])
+        const int pp = pq / kc, qq = pq % kc;
+        if (qq > c && pp >= qq) {
+          const double2 a = G[pp][c], b = G[qq][c];
+          G[pp][qq].x -= a.x * b.x + a.y * b.y;
+          G[pp][qq].y -= a.y * b.x - a.x * b.y;
+        }
+      }
+      __syncthreads();
+    }
+    if (fail) {
+      if (tid == 0) *bad = 1;
+      return;
+    }
+    // each row z <- z L^-H: y = conj(z)^T, L y' = y, z <- conj(y')^T
+    for (int r0 = 0; r0 < n; r0 += RC) {
+      for (int q = tid; q < RC * kc; q += 256) {
+        const int rr = q / kc, c = q % kc, r = r0 + rr;
+        Zs[rr][c] = r < n ? Zt[(int64_t)r * nv + jj + c] : make_double2(0.0, 0.0);
+      }
+      __syncthreads();
+      if (tid < RC) {
+        for (int pp = 0; pp < kc; ++pp) {
+          double2 v = make_double2(Zs[tid][pp].x, -Zs[tid][pp].y);   // conj z_p
+          for (int qq = 0; qq < pp; ++qq) {   // - L[p][q] y'_q, y'_q = conj(new z_q)
+            const double2 l = G[pp][qq], y = make_double2(Zs[tid][qq].x, -Zs[tid][qq].y);
+            v.x -= l.x * y.x - l.y * y.y;
+            v.y -= l.x * y.y + l.y * y.x;
+          }
+          const double d = G[pp][pp].x;
+          Zs[tid][pp] = make_double2(v.x / d, -v.y / d);   // conj back
+        }
+      }
+      __syncthreads();
+      for (int q = tid; q < RC * kc; q += 256) {
+        const int rr = q / kc, c = q % kc, r = r0 + rr;
+        if (r < n) Zt[(int64_t)r * nv + jj + c] = Zs[rr][c];
+      }
+      __syncthreads();
+    }
   }
 }
 
@@ -1275,6 +1416,14 @@ void launch_q_vexpand(const double2* A, int64_t sA, const double* tau, int M, do
 void launch_q_final(const double2* Ui, int64_t sU, int M, int j0, double2* U, int m, hipStream_t s) {
   const int n = 2 * M;
   hipLaunchKernelGGL(k_q_final, dim3((n + 255) / 256, n, m), dim3(256), 0, s, Ui, sU, M, j0, U);
+}
+
+int q_max_cluster() { return kQMaxCluster; }
+
+void launch_q_orth(const double* E, const double* tnorm, int M, int j0, double2* Zt, int64_t sZ, double ctol, int* bad,
+                   int m, hipStream_t s) {
+  const int nv = 2 * M - j0;
+  hipLaunchKernelGGL(k_q_orth, dim3(nv, m), dim3(256), 0, s, E, tnorm, M, j0, Zt, sZ, ctol, bad);
 }
 
 }  // namespace dwh

@@ -259,6 +259,7 @@ def test_eigensolver_long_clusters(dwhmc, oracle, monkeypatch, Lx, Ly, maxc):
     eigenpairs meet test_own_eigensolver_full_size's tolerances."""
     O = oracle
     monkeypatch.setenv("DWHMC_EIG_MAX_CLUSTER", maxc)
+    monkeypatch.setenv("DWHMC_EIG_QUAT", "0")   # the one-stage solver's cluster paths
     p = O.ModelParameters(Lx, Ly, T, TP, -1.0, 0.0, 0.0, 4.0, 0.8, 1.0)
     dis = np.zeros(p.N)
     D = np.stack([np.full(p.N, 0.2), np.full(p.N, -0.2)], 1).astype(np.complex128)
@@ -288,6 +289,7 @@ def test_own_eigensolver_L48_low_cluster_limit(dwhmc, oracle, monkeypatch):
     import scipy.linalg as sla
     O = oracle
     monkeypatch.setenv("DWHMC_EIG_MAX_CLUSTER", "2")
+    monkeypatch.setenv("DWHMC_EIG_QUAT", "0")
     p, dis, D = _case(O, 48, 48, 32.0, seed=4848)
     cache = O.initialize_cache(p)
     O.init_static_H(cache, p, dis)
@@ -307,6 +309,39 @@ def test_own_eigensolver_L48_low_cluster_limit(dwhmc, oracle, monkeypatch):
     H = O.hermitian_from_upper(cache.H_base)
     assert np.max(np.abs(H @ U - U * E[None, :])) <= 1e-11 * scale
     assert np.max(np.abs(U.conj().T @ U - np.eye(2 * p.N))) <= 1e-12
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("Lx,Ly,beta", [(12, 10, 4.0), (16, 16, 8.0), (32, 32, 16.0)])
+def test_structure_preserving_solver_clusters(dwhmc, oracle, Lx, Ly, beta):
+    """Clean lattices (W = 0, uniform d-wave Δ, μ = -1: degenerate shells of up
+    to 8+ levels, no zero modes) through the structure-preserving eigensolver:
+    its inverse-iteration vectors of each cluster are orthonormalised by
+    Cholesky QR (k_q_orth) instead of the solver declining to the one-stage
+    path.  eig_quat == 1, no rocSOLVER fallback, and the tolerances of
+    test_own_eigensolver_full_size; the measurement against the oracle."""
+    O = oracle
+    p = O.ModelParameters(Lx, Ly, T, TP, -1.0, 0.0, 0.0, beta, 0.8, 1.0)
+    dis = np.zeros(p.N)
+    D = np.stack([np.full(p.N, 0.2), np.full(p.N, -0.2)], 1).astype(np.complex128)
+    cache, _, _ = O.evaluate(p, dis, D)
+    ctx = _ctx(dwhmc, p, dis)
+    ctx.set_pairing(D)
+    ctx.timing_enable(["eig_own", "eig_vendor"])
+    E, U = ctx.eigensystem(0)
+    own, vendor = ctx.timing_read("eig_own")[1], ctx.timing_read("eig_vendor")[1]
+    quat, half = ctx.info["eig_quat"], ctx.info["eig_half"]
+    r = ctx.measure_transport(p.eta, p.domega, p.omega_max) if Lx < 32 else None
+    ctx.close()
+    assert (own, vendor, quat, half) == (1, 0, 1, 1), (own, vendor, quat, half)
+    H = O.hermitian_from_upper(cache.H_base)
+    scale = 1 + np.max(np.abs(cache.E_n))
+    assert np.all(np.isfinite(U))
+    assert np.max(np.abs(E - cache.E_n)) <= 1e-12 * scale
+    assert np.max(np.abs(H @ U - U * E[None, :])) <= 1e-11 * scale
+    assert np.max(np.abs(U.conj().T @ U - np.eye(2 * p.N))) <= 1e-12
+    if r is not None:
+        _check_transport(r, O.measure_transport_and_spectra(cache, p))
 
 
 def _check_transport(r, ref):
