@@ -2866,19 +2866,23 @@ int q_heev_enqueue(dwh_ctx* ctx, const TrSrc& src, int m, bool* done) {
   HIPCHECK(ctx, hipMemcpyAsync(tn.data(), q.tn, m * sizeof(double), hipMemcpyDeviceToHost, s));
   HIPCHECK(ctx, hipStreamSynchronize(s));
   // Crowding at zero matters through E_j + E_k of two computed vectors j != k
-  // (x_j against the partner Theta x_k, which no orthogonalisation step
-  // sees): E_N + E_{N+1} > kEigZeroTol ||T||, the one-stage half solve's
+  // (x_j against the partner Theta x_k, which the Löwdin step does not
+  // see): E_N + E_{N+1} <= kEigZeroTol ||T||, the one-stage half solve's
   // bound on it.  A single level near zero is harmless: x_N and Theta x_N
   // are orthogonal exactly (<u, Theta u> = 0 for Theta^2 = -1).
   // Clusters (consecutive gaps <= kEigClusterTol ||T||) up to q_max_cluster()
   // long are orthonormalised in the structure-preserving path (k_q_orth);
   // longer ones are declined.
+  // A crowd at zero (q_zero_crowd) of up to q_max_cluster() / 2 levels is
+  // orthonormalised together with its Theta partners (k_q_orth).
   bool clusters = false;
   for (int k = 0; k < m; ++k) {
     const double* E = Eh.data() + (size_t)k * n;
-    if (N + 1 < n && !(E[N] + E[N + 1] > dwh::kEigZeroTol * tn[k])) return DWH_OK;
+    const int crowd = dwh::q_zero_crowd(E, n, j0, tn[k]);
+    if (2 * crowd > dwh::q_max_cluster()) return DWH_OK;
+    clusters = clusters || crowd > 0;
     int run = 1;
-    for (int j = N + 1; j < n; ++j) {
+    for (int j = j0 + std::max(crowd, 1); j < n; ++j) {
       if (!(E[j] - E[j - 1] > dwh::kEigClusterTol * tn[k])) {
         clusters = true;
         if (++run > dwh::q_max_cluster()) return DWH_OK;

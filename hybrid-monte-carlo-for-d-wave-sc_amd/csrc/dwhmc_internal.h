@@ -412,6 +412,9 @@ void launch_q_invit(const double* ra, const double2* rd, const double* rb, int M
 // the vectors of eigenvalue clusters (gaps <= ctol ||T||, at most q_max_cluster()
 // long) orthonormalised in Zt (two rounds of Cholesky QR); *bad = 1 on failure
 int q_max_cluster();
+// the crowd at zero of one matrix's eigenvalues E (n, computed from j0): the
+// number of levels k_q_orth orthonormalises with their Theta partners, 0: none
+int q_zero_crowd(const double* E, int n, int j0, double tn);
 void launch_q_orth(const double* E, const double* tnorm, int M, int j0, double2* Zt, int64_t sZ, double ctol, int* bad,
                    int m, hipStream_t s);
 // U' columns j0.. (n x n, interleaved rows) = site rotations G of Yt (nv x n, ld nv)

@@ -1137,6 +1137,21 @@ __global__ __launch_bounds__(64) void k_q_invit(const double* __restrict__ ra, c
   }
 }
 
+// The crowd at zero: when E_N + E_{N+1} <= kEigZeroTol ||T|| (j0 = N), the
+// levels j0 .. j0 + c - 1 with E_j + E_N within it (extended over cluster
+// gaps): their vectors x_j overlap the partners Theta x_k of one another (by
+// ~eps ||T|| / (E_j + E_k)), which the Löwdin step over the x's cannot see.
+// 0 when there is none.  The same function on the host (q_zero_crowd) and in
+// k_q_orth, so both see the same c.
+__host__ __device__ inline int q_crowd(const double* E, int n, int j0, double tn) {
+  const int nv = n - j0;
+  const double zt = kEigZeroTol * tn, ct = kEigClusterTol * tn;
+  if (nv < 2 || E[j0] + E[j0 + 1] > zt) return 0;
+  int c = 2;
+  while (c < nv && (E[j0 + c] + E[j0] <= zt || E[j0 + c] - E[j0 + c - 1] <= ct)) ++c;
+  return c;
+}
+
 // Clusters of the computed eigenvalues (consecutive gaps <= ctol ||T||, at
 // most kQMaxCluster long: longer ones are declined on the host) get their
 // inverse-iteration vectors orthonormalised, as k_eig_orth does for the
@@ -1144,7 +1159,12 @@ __global__ __launch_bounds__(64) void k_q_invit(const double* __restrict__ ra, c
 // cluster's columns of Zt (G = Z^H Z = L L^H, Z <- Z L^-H; a cluster's
 // columns are contiguous in each row of Zt).  One workgroup per candidate
 // first index; *bad = 1 when G is not positive definite (the caller's
-// re-solve).
+// re-solve).  The crowd at zero (q_crowd, c <= kQMaxCluster / 2 levels) is
+// orthonormalised as the 2c columns x_0, Theta x_0, x_1, Theta x_1, ...
+// (Theta in T's interleaved basis: (Theta z)_2s = -conj z_2s+1, (Theta
+// z)_2s+1 = conj z_2s): Cholesky QR in that order keeps the pairs (the
+// new Theta x_i is Theta of the new x_i, as Theta preserves the span of the
+// earlier pairs), and only the x columns are written back.
 __global__ __launch_bounds__(256) void k_q_orth(const double* __restrict__ E, const double* __restrict__ tnorm, int M,
                                                 int j0, double2* __restrict__ Zt, int64_t sZ, double ctol,
                                                 int* __restrict__ bad) {
@@ -1153,16 +1173,31 @@ __global__ __launch_bounds__(256) void k_q_orth(const double* __restrict__ E, co
   E += (int64_t)k * n;
   Zt += k * sZ;
   const double tol = ctol * tnorm[k];
-  if (jj > 0 && E[j0 + jj] - E[j0 + jj - 1] <= tol) return;   // inside a cluster
-  int end = jj + 1;
-  while (end < nv && end - jj < MC && E[j0 + end] - E[j0 + end - 1] <= tol) ++end;
-  const int kc = end - jj;
-  if (kc == 1) return;
+  const int ce = q_crowd(E, n, j0, tnorm[k]);
+  const bool theta = jj == 0 && ce >= 2;
+  if (jj > 0 && jj < ce) return;   // inside the crowd
+  int kc = ce;
+  if (!theta) {
+    if (jj > 0 && E[j0 + jj] - E[j0 + jj - 1] <= tol) return;   // inside a cluster
+    int end = jj + 1;
+    while (end < nv && end - jj < MC && E[j0 + end] - E[j0 + end - 1] <= tol) ++end;
+    kc = end - jj;
+    if (kc == 1) return;
+  }
+  const int kw = theta ? 2 * kc : kc;   // working columns
+  // working column c of row r (theta: x_{c/2}, and Theta x_{c/2} for odd c)
+  auto zin = [&](int r, int c) -> double2 {
+    if (r >= n) return make_double2(0.0, 0.0);
+    if (!theta) return Zt[(int64_t)r * nv + jj + c];
+    if (!(c & 1)) return Zt[(int64_t)r * nv + jj + (c >> 1)];
+    const double2 p = Zt[(int64_t)(r ^ 1) * nv + jj + (c >> 1)];
+    return (r & 1) ? make_double2(p.x, -p.y) : make_double2(-p.x, p.y);
+  };
   __shared__ double2 G[MC][MC + 1];
   __shared__ double2 Zs[RC][MC + 1];
   __shared__ int fail;
   constexpr int NPT = (MC * (MC + 1) / 2 + 255) / 256;
-  const int npair = kc * (kc + 1) / 2;
+  const int npair = kw * (kw + 1) / 2;
   auto pair_of = [&](int pq, int& pr, int& qc) {
     int r = (int)((sqrt(8.0 * pq + 1.0) - 1.0) * 0.5);
     while ((r + 1) * (r + 2) / 2 <= pq) ++r;
@@ -1176,9 +1211,9 @@ __global__ __launch_bounds__(256) void k_q_orth(const double* __restrict__ E, co
 #pragma unroll
     for (int u = 0; u < NPT; ++u) acc[u] = make_double2(0.0, 0.0);
     for (int r0 = 0; r0 < n; r0 += RC) {
-      for (int q = tid; q < RC * kc; q += 256) {
-        const int rr = q / kc, c = q % kc, r = r0 + rr;
-        Zs[rr][c] = r < n ? Zt[(int64_t)r * nv + jj + c] : make_double2(0.0, 0.0);
+      for (int q = tid; q < RC * kw; q += 256) {
+        const int rr = q / kw, c = q % kw;
+        Zs[rr][c] = zin(r0 + rr, c);
       }
       __syncthreads();
 #pragma unroll
@@ -1210,20 +1245,20 @@ __global__ __launch_bounds__(256) void k_q_orth(const double* __restrict__ E, co
     if (tid == 0) fail = 0;
     __syncthreads();
     // Cholesky G = L L^H, right-looking, in place (lower)
-    for (int c = 0; c < kc; ++c) {
+    for (int c = 0; c < kw; ++c) {
       if (tid == 0) {
         const double g = G[c][c].x;   // the columns are normalised: a pivot this small means cond(Z) > ~1e7
         if (!(g > 1e-14)) fail = 1;
         G[c][c] = make_double2(sqrt(fmax(g, DBL_MIN)), 0.0);
       }
       __syncthreads();
-      for (int r = c + 1 + tid; r < kc; r += 256) {
+      for (int r = c + 1 + tid; r < kw; r += 256) {
         const double d = G[c][c].x;
         G[r][c] = make_double2(G[r][c].x / d, G[r][c].y / d);
       }
       __syncthreads();
-      for (int pq = tid; pq < kc * kc; pq += 256) {   // G[p][q] -= L[p][c] conj(L[q][c])
-        const int pp = pq / kc, qq = pq % kc;
+      for (int pq = tid; pq < kw * kw; pq += 256) {   // G[p][q] -= L[p][c] conj(L[q][c])
+        const int pp = pq / kw, qq = pq % kw;
         if (qq > c && pp >= qq) {
           const double2 a = G[pp][c], b = G[qq][c];
           G[pp][qq].x -= a.x * b.x + a.y * b.y;
@@ -1238,13 +1273,13 @@ __global__ __launch_bounds__(256) void k_q_orth(const double* __restrict__ E, co
     }
     // each row z <- z L^-H: y = conj(z)^T, L y' = y, z <- conj(y')^T
     for (int r0 = 0; r0 < n; r0 += RC) {
-      for (int q = tid; q < RC * kc; q += 256) {
-        const int rr = q / kc, c = q % kc, r = r0 + rr;
-        Zs[rr][c] = r < n ? Zt[(int64_t)r * nv + jj + c] : make_double2(0.0, 0.0);
+      for (int q = tid; q < RC * kw; q += 256) {
+        const int rr = q / kw, c = q % kw;
+        Zs[rr][c] = zin(r0 + rr, c);
       }
       __syncthreads();
       if (tid < RC) {
-        for (int pp = 0; pp < kc; ++pp) {
+        for (int pp = 0; pp < kw; ++pp) {
           double2 v = make_double2(Zs[tid][pp].x, -Zs[tid][pp].y);   // conj z_p
           for (int qq = 0; qq < pp; ++qq) {   // - L[p][q] y'_q, y'_q = conj(new z_q)
             const double2 l = G[pp][qq], y = make_double2(Zs[tid][qq].x, -Zs[tid][qq].y);
@@ -1256,9 +1291,9 @@ __global__ __launch_bounds__(256) void k_q_orth(const double* __restrict__ E, co
         }
       }
       __syncthreads();
-      for (int q = tid; q < RC * kc; q += 256) {
+      for (int q = tid; q < RC * kc; q += 256) {   // the x columns back
         const int rr = q / kc, c = q % kc, r = r0 + rr;
-        if (r < n) Zt[(int64_t)r * nv + jj + c] = Zs[rr][c];
+        if (r < n) Zt[(int64_t)r * nv + jj + c] = Zs[rr][theta ? 2 * c : c];
       }
       __syncthreads();
     }
@@ -1417,6 +1452,8 @@ void launch_q_final(const double2* Ui, int64_t sU, int M, int j0, double2* U, in
   const int n = 2 * M;
   hipLaunchKernelGGL(k_q_final, dim3((n + 255) / 256, n, m), dim3(256), 0, s, Ui, sU, M, j0, U);
 }
+
+int q_zero_crowd(const double* E, int n, int j0, double tn) { return q_crowd(E, n, j0, tn); }
 
 int q_max_cluster() { return kQMaxCluster; }
 

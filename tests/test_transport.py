@@ -393,19 +393,24 @@ def test_transport_clean_degenerate_spectrum(dwhmc, oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("Lx,Ly,mu,half,ran_half", [(8, 8, 0.0, "1", 0), (12, 8, 0.0, "1", 0), (8, 8, -1.0, "1", 1),
-                                                     (6, 6, -1.08, "0", 0)])
-def test_transport_particle_hole_half(dwhmc, oracle, monkeypatch, Lx, Ly, mu, half, ran_half):
+@pytest.mark.parametrize("Lx,Ly,mu,half,quat,ran_half", [(8, 8, 0.0, "1", "0", 0), (12, 8, 0.0, "1", "0", 0),
+                                                          (8, 8, 0.0, "1", "1", 1), (12, 8, 0.0, "1", "1", 1),
+                                                          (8, 8, -1.0, "1", "1", 1), (6, 6, -1.08, "0", "1", 0)])
+def test_transport_particle_hole_half(dwhmc, oracle, monkeypatch, Lx, Ly, mu, half, quat, ran_half):
     """The particle-hole half measurement: with the eigensolver's half solve
     (columns j < N the partners Θ of columns n2-1-j) J_mn is formed in its
     columns < N only and Λ, the DC sum and σ(ω) run over half the pairs.  A
-    clean lattice at μ = 0 with L % 4 == 0 has exact zero modes (a cluster
-    across E = 0, solved whole, so U is not partner-closed there): every pair
-    is summed.  half = "0" (DWHMC_EIG_HALF=0): the full solve and sums.
-    ran_half: which path the library reports it took (dwh_info_t::eig_half),
-    so the half-sum code cannot pass silently on the full path."""
+    clean lattice at μ = 0 with L % 4 == 0 has exact zero modes: the
+    one-stage solver (quat = "0") solves that cluster across E = 0 whole, so
+    U is not partner-closed there and every pair is summed; the
+    structure-preserving solver orthonormalises the crowd together with its
+    Θ partners (k_q_orth), so U stays partner-closed and the half sums run.
+    half = "0" (DWHMC_EIG_HALF=0): the full solve and sums.  ran_half: which
+    path the library reports it took (dwh_info_t::eig_half), so the half-sum
+    code cannot pass silently on the full path."""
     O = oracle
     monkeypatch.setenv("DWHMC_EIG_HALF", half)
+    monkeypatch.setenv("DWHMC_EIG_QUAT", quat)
     p = O.ModelParameters(Lx, Ly, 1.0, -0.35, mu, 0.0, 0.0, 16.0, 0.8, 1.0)
     N = p.N
     D = np.stack([np.full(N, 0.2), np.full(N, -0.2)], 1).astype(np.complex128)
@@ -419,8 +424,15 @@ def test_transport_particle_hole_half(dwhmc, oracle, monkeypatch, Lx, Ly, mu, ha
     assert ctx.info["eig_half"] == -1
     r = ctx.measure_transport(p.eta, p.domega, p.omega_max)
     assert ctx.info["eig_half"] == ran_half
+    assert ctx.info["eig_quat"] == (1 if quat == "1" and half == "1" else 0)
+    E, U = ctx.eigensystem(0)
     ctx.close()
     _check_transport(r, ref)
+    H = O.hermitian_from_upper(cache.H_base)
+    scale = 1 + np.max(np.abs(cache.E_n))
+    assert np.max(np.abs(E - cache.E_n)) <= 1e-12 * scale
+    assert np.max(np.abs(H @ U - U * E[None, :])) <= 1e-11 * scale
+    assert np.max(np.abs(U.conj().T @ U - np.eye(2 * N))) <= 1e-12
 
 
 @pytest.mark.gpu

@@ -18,9 +18,10 @@ def main():
     import dwhmc_loader
     from oracle import dwhmc_oracle as O
     m = dwhmc_loader.load_package()
+    mu = float(os.environ.get("QCL_MU", "-1"))   # 0: the nodal zero modes (L % 4 == 0)
     Ls = [int(x) for x in sys.argv[1:]] or [10, 12, 16]
     for L in Ls:
-        p = O.ModelParameters(L, L, 1.0, -0.35, -1.0, 0.0, 0.0, 16.0, 0.8, 1.0)
+        p = O.ModelParameters(L, L, 1.0, -0.35, mu, 0.0, 0.0, 16.0, 0.8, 1.0)
         N = p.N
         D = np.stack([np.full(N, 0.2), np.full(N, -0.2)], 1).astype(complex)
         dis = np.zeros(N)
@@ -51,7 +52,7 @@ def main():
         i, j = np.unravel_index(np.argmax(G), G.shape)
         rows = np.max(G, axis=1)
         worst = np.argsort(rows)[::-1][:8]
-        print(f"L={L} n={2 * N} own={own} vendor={vendor} quat={quat} res {res:.1e} orth {G.max():.1e} "
+        print(f"L={L} mu={mu} n={2 * N} own={own} vendor={vendor} quat={quat} res {res:.1e} orth {G.max():.1e} "
               f"at ({i},{j}) E {E[i]:.6f} {E[j]:.6f}; E err {np.max(np.abs(E - ev)) / (1 + hn):.1e}; "
               f"eigensystem {ts[0]:.2f} ms (one-stage {ts[1]:.2f} ms)", flush=True)
         print("  worst columns:", [(int(c), round(float(E[c]), 6), f"{rows[c]:.1e}") for c in worst], flush=True)
