@@ -2652,7 +2652,7 @@ int eigen_solve(dwh_ctx* ctx, const TrSrc& src, int m) {
     HIPCHECK(ctx, hipMemsetAsync(ctx->d_tr_info, 0, m * sizeof(int), ctx->stream));
     Scope sc(ctx, T_EIG_OWN, m);
     // the structure-preserving solver first (DWHMC_EIG_QUAT=0: the one-stage
-    // solver only, A/B); it declines spectra with clusters or crowding at zero
+    // solver only, A/B); it declines spectra with over-long clusters or crowds
     bool done = false;
     const char* qe = std::getenv("DWHMC_EIG_QUAT");
     if (dwh::q_supported(ctx->d.N) && !(qe && *qe == '0')) rc = q_heev_enqueue(ctx, src, m, &done);
@@ -2840,11 +2840,12 @@ int qeig_values(dwh_ctx* ctx, const TrSrc& src, int m, float* ms) {
 }
 
 // Every eigenpair by the structure-preserving solver (m matrices): qeig_values,
-// then — when every matrix's spectrum is clear of crowding at zero (gap at
-// the middle > kEigZeroTol ||T||) and of clusters (consecutive gaps >
-// kEigClusterTol ||T||), checked on the host from the eigenvalues (one
-// synchronisation) — the particle-hole half: inverse iteration on T for the
-// N upper eigenvalues (k_q_invit), one Löwdin step (the library's complex
+// then — when no matrix's spectrum has a cluster (consecutive gaps <=
+// kEigClusterTol ||T||) longer than q_max_cluster() or a crowd at zero
+// (q_zero_crowd) longer than half that, checked on the host from the
+// eigenvalues (one synchronisation) — the particle-hole half: inverse
+// iteration on T for the N upper eigenvalues (k_q_invit), the clusters and
+// the crowd orthonormalised (k_q_orth), one Löwdin step (the library's complex
 // products), the site rotations into U' (interleaved rows), the reflector
 // pairs as a one-stage V and its back-transform, then the BdG row order and
 // the Theta partners for the lower half (k_q_final).  *done = false: not
