@@ -525,6 +525,34 @@ def test_transport_deltas_sub_batch_streams(dwhmc, oracle, monkeypatch, Lx, Ly, 
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("Lx,Ly,mu", [(8, 8, 0.0), (12, 10, -1.0)])
+def test_transport_deltas_clean_structure_preserving(dwhmc, oracle, Lx, Ly, mu):
+    """A batch of clean-lattice snapshots through the structure-preserving
+    eigensolver: uniform d-wave Δ under global phases (degenerate shells; at
+    μ = 0 the nodal zero modes, a crowd at zero) mixed with non-uniform
+    phases (no exact degeneracy), so one k_q_orth launch sees matrices with
+    and without clusters.  eig_quat == 1 and every snapshot equals the
+    oracle."""
+    O = oracle
+    p = O.ModelParameters(Lx, Ly, T, TP, mu, 0.0, 0.0, 16.0, 0.8, 1.0)
+    N = p.N
+    dis = np.zeros(N)
+    base = np.stack([np.full(N, 0.2), np.full(N, -0.2)], 1).astype(np.complex128)
+    rng = np.random.default_rng(Lx * 7 + Ly)
+    snaps = [base * np.exp(1j * ph) for ph in (0.0, 0.7, -2.1)]
+    snaps += [base * np.exp(0.2j * rng.standard_normal((N, 1))) for _ in range(2)]
+    ctx = _ctx(dwhmc, p, dis)
+    ctx.set_pairing(snaps[0])
+    rs = ctx.measure_transport_deltas(np.stack(snaps), p.eta, p.domega, p.omega_max)
+    quat, half = ctx.info["eig_quat"], ctx.info["eig_half"]
+    ctx.close()
+    assert (quat, half) == (1, 1), (quat, half)
+    for k, D in enumerate(snaps):
+        cache, _, _ = O.evaluate(p, dis, D)
+        _check_transport(rs[k], O.measure_transport_and_spectra(cache, p))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("switch_m", ["0", "64", "512"])
 def test_transport_deferred_batch_switch(dwhmc, oracle, monkeypatch, switch_m):
     """Batches of 4+ matrices tridiagonalise with the 8-deep deferral and run
