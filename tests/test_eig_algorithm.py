@@ -269,3 +269,47 @@ def test_pass_dot_shares():
     assert abs(r - np.vdot(v, p).real) < 1e-12
     c = np.vdot(v, QP.theta(p))
     assert abs(complex(c_re, -c_im) - c) < 1e-12
+
+
+def _theta_interleaved(z):
+    """Theta in T's site-interleaved basis (k_q_orth's zin): (Theta z)_2s =
+    -conj z_2s+1, (Theta z)_2s+1 = conj z_2s."""
+    t = np.empty_like(z)
+    t[0::2] = -np.conj(z[1::2])
+    t[1::2] = np.conj(z[0::2])
+    return t
+
+
+@pytest.mark.parametrize("n,c,seed", [(16, 1, 0), (24, 3, 1), (64, 8, 2)])
+def test_crowd_pair_cholesky_qr(n, c, seed):
+    """k_q_orth's crowd at zero: two rounds of Cholesky QR on the columns x0,
+    Theta x0, x1, Theta x1, ... (in that order) give orthonormal columns in
+    which every odd column is Theta of the even one before it, so writing back
+    only the x columns leaves U partner-closed; and the interleaved Theta
+    anticommutes with T's block form [[a, d], [conj d, -a]], b diag(1, -1)."""
+    rng = np.random.default_rng(seed)
+    X = rng.standard_normal((n, c)) + 1j * rng.standard_normal((n, c))
+    X[:, -1] += 0.999 * X[:, 0]   # a nearly dependent member, as inverse iteration can give
+    for _ in range(2):
+        Z = np.empty((n, 2 * c), complex)
+        Z[:, 0::2] = X
+        Z[:, 1::2] = np.stack([_theta_interleaved(X[:, i]) for i in range(c)], 1)
+        L = np.linalg.cholesky(Z.conj().T @ Z)
+        Q = np.linalg.solve(L, Z.conj().T).conj().T   # Z L^-H
+        np.testing.assert_allclose(Q[:, 1::2], np.stack([_theta_interleaved(Q[:, 2 * i]) for i in range(c)], 1),
+                                   atol=1e-12)
+        X = Q[:, 0::2]
+    assert np.max(np.abs(Q.conj().T @ Q - np.eye(2 * c))) <= 1e-13
+    M = n // 2
+    a = rng.standard_normal(M)
+    b = rng.standard_normal(M - 1)
+    d = rng.standard_normal(M) + 1j * rng.standard_normal(M)
+    T = np.zeros((n, n), complex)
+    for s in range(M):
+        T[2 * s, 2 * s], T[2 * s + 1, 2 * s + 1] = a[s], -a[s]
+        T[2 * s, 2 * s + 1], T[2 * s + 1, 2 * s] = d[s], np.conj(d[s])
+        if s + 1 < M:
+            T[2 * s, 2 * s + 2] = T[2 * s + 2, 2 * s] = b[s]
+            T[2 * s + 1, 2 * s + 3] = T[2 * s + 3, 2 * s + 1] = -b[s]
+    z = rng.standard_normal(n) + 1j * rng.standard_normal(n)
+    np.testing.assert_allclose(T @ _theta_interleaved(z), -_theta_interleaved(T @ z), atol=1e-12)
