@@ -1112,6 +1112,10 @@ struct dwh_ctx {
   double* d_q = nullptr;
   int q_slots = 0, q_vec_slots = 0;
   double2 *d_qz = nullptr, *d_qs = nullptr, *d_qg = nullptr;
+  // the reduction's launch sequence as a graph (its arguments: the slots, d_q, m)
+  hipGraphExec_t q_graph = nullptr;
+  const void* q_graph_key[2] = {};
+  int q_graph_m = 0;
   hipStream_t eig_sx[3] = {};       // extra streams of the sub-batched tridiagonalisation
   hipEvent_t eig_ev[4] = {};
 
@@ -2825,7 +2829,35 @@ int qeig_values(dwh_ctx* ctx, const TrSrc& src, int m, float* ms) {
     HIPCHECK(ctx, hipEventCreate(&e1));
     HIPCHECK(ctx, hipEventRecord(e0, s));
   }
-  dwh::launch_q_reduce(A, M, sA, q.part, q.sP, q.W, q.tau, q.Y, q.qa, q.qd, m, s);
+  const char* qg = std::getenv("DWHMC_Q_GRAPH");
+  if (!(qg && *qg == '0')) {
+    // the 2 M launches captured once per (slots, workspace, m) and replayed:
+    // one L = 32 measurement 24.4-24.7 -> 24.2-24.3 ms
+    // (profiles/r06_exp_qreduce_graph.txt; DWHMC_Q_GRAPH=0: stream launches)
+    if (!ctx->q_graph || ctx->q_graph_key[0] != A || ctx->q_graph_key[1] != ctx->d_q || ctx->q_graph_m != m) {
+      if (ctx->q_graph) {
+        HIPCHECK(ctx, hipStreamSynchronize(s));
+        (void)hipGraphExecDestroy(ctx->q_graph);
+        ctx->q_graph = nullptr;
+      }
+      hipGraph_t g = nullptr;
+      HIPCHECK(ctx, hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+      dwh::launch_q_reduce(A, M, sA, q.part, q.sP, q.W, q.tau, q.Y, q.qa, q.qd, m, s);
+      HIPCHECK(ctx, hipStreamEndCapture(s, &g));
+      const hipError_t e = hipGraphInstantiate(&ctx->q_graph, g, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(g);
+      if (e != hipSuccess) {
+        ctx->q_graph = nullptr;
+        return fail(ctx, DWH_ERR_HIP, std::string("reduction graph: ") + hipGetErrorString(e));
+      }
+      ctx->q_graph_key[0] = A;
+      ctx->q_graph_key[1] = ctx->d_q;
+      ctx->q_graph_m = m;
+    }
+    HIPCHECK(ctx, hipGraphLaunch(ctx->q_graph, s));
+  } else {
+    dwh::launch_q_reduce(A, M, sA, q.part, q.sP, q.W, q.tau, q.Y, q.qa, q.qd, m, s);
+  }
   if (ms) HIPCHECK(ctx, hipEventRecord(e1, s));
   dwh::launch_q_rot(q.qa, q.qd, q.Y, M, q.ra, q.rd, q.rb, q.G, m, s);
   dwh::launch_q_bisect(q.ra, q.rd, q.rb, M, ctx->tr.E, q.tn, m, s);
@@ -3126,6 +3158,7 @@ void dwh_destroy(dwh_ctx* ctx) {
   }
   for (auto e : ctx->pool) (void)hipEventDestroy(e);
   if (ctx->blas) (void)rocblas_destroy_handle(ctx->blas);
+  if (ctx->q_graph) (void)hipGraphExecDestroy(ctx->q_graph);
   for (void* p : ctx->allocations) (void)hipFree(p);
   for (hipEvent_t ev : ctx->eig_ev)
     if (ev) (void)hipEventDestroy(ev);
