@@ -60,8 +60,9 @@ typedef struct {
   int64_t eig_long_clusters; /* eigenvalue clusters so far too long for the one-workgroup
                                 orthonormalisation, taken by the multi-workgroup Cholesky QR */
   int64_t eig_quat;   /* last eigensolve with vectors: 1 = the structure-preserving (quaternion)
-                         solver, 0 = the one-stage tridiagonalisation (spectra with clusters or
-                         crowding at zero, or DWHMC_EIG_QUAT=0) */
+                         solver, 0 = the one-stage tridiagonalisation (spectra with a cluster
+                         longer than 32 levels or a crowd at zero longer than 16, or
+                         DWHMC_EIG_QUAT=0) */
 } dwh_info_t;
 
 /* ModelParameters + initialize_cache + init_static_H!
