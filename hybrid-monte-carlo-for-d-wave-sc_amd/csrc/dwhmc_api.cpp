@@ -2830,10 +2830,12 @@ int qeig_values(dwh_ctx* ctx, const TrSrc& src, int m, float* ms) {
     HIPCHECK(ctx, hipEventRecord(e0, s));
   }
   const char* qg = std::getenv("DWHMC_Q_GRAPH");
-  if (!(qg && *qg == '0')) {
-    // the 2 M launches captured once per (slots, workspace, m) and replayed:
-    // one L = 32 measurement 24.4-24.7 -> 24.2-24.3 ms
-    // (profiles/r06_exp_qreduce_graph.txt; DWHMC_Q_GRAPH=0: stream launches)
+  if (qg && *qg == '1') {
+    // opt-in: the 2 M launches captured once per (slots, workspace, m) and
+    // replayed — one L = 32 measurement 24.4-24.7 -> 24.2-24.3 ms, but
+    // tests/bench_transport.py under rocprofv3 --kernel-trace segfaulted with
+    // it (recapture for a new batch size) and not without it
+    // (profiles/r06_exp_qreduce_graph.txt), so stream launches stay the default
     if (!ctx->q_graph || ctx->q_graph_key[0] != A || ctx->q_graph_key[1] != ctx->d_q || ctx->q_graph_m != m) {
       if (ctx->q_graph) {
         HIPCHECK(ctx, hipStreamSynchronize(s));
