@@ -44,6 +44,7 @@
 #include <stdint.h>
 
 #include <cfloat>
+#include <cstdlib>
 
 #include "dwhmc_device.h"
 #include "dwhmc_internal.h"
@@ -1137,6 +1138,215 @@ __global__ __launch_bounds__(64) void k_q_invit(const double* __restrict__ ra, c
   }
 }
 
+// The same inverse iteration with one 16-lane DPP row per eigenvalue (four
+// per one-wave workgroup, which leaves the back substitution's prefetch its
+// 512 registers): lanes 0..4 hold column c = lane of the three window
+// rows, lane 12 the right-hand side's three window entries, the others zeros
+// (lane 5: what column 4 shifts in; lane 8: what lane 7 shifts in, so no
+// right-hand side value walks down into the columns).  Per step lane 0 picks the pivot row (row_newbcast),
+// forms 1 / u_kk and the two multipliers (row_newbcast to the row), every
+// lane eliminates its own entries, one store per lane writes the step's six
+// complex (lane 0: 1 / u_kk, lanes 1..4: u_k,k+c, lane 12: y_k; the scratch
+// layout of k_q_invit), and the window moves one column by row_shl:1 with the
+// banks of lanes 8..15 masked (the right-hand side lane shifts its own
+// entries).  The thread-per-eigenvalue sweep issued ~385 instructions per
+// step on one wave per SIMD; this one ~100, on 16x the waves.  The back
+// substitution runs redundantly in all 16 lanes of a row (same addresses:
+// one transaction), lane 0 storing.  Same operation order as k_q_invit per
+// eigenvalue, so the same vectors up to the order of the pivot magnitudes'
+// sums (identical).
+__device__ __forceinline__ double2 dpp_bcast0(double2 v) {
+  return make_double2(__builtin_amdgcn_update_dpp(v.x, v.x, 0x150, 0xf, 0xf, true),
+                      __builtin_amdgcn_update_dpp(v.y, v.y, 0x150, 0xf, 0xf, true));
+}
+// lanes 0..7 of each row take lane + 1's value (lane 7: lane 8's, unused);
+// lanes 8..15 keep their own (bank mask 0b0011)
+__device__ __forceinline__ double2 dpp_shl1_lo(double2 v) {
+  return make_double2(__builtin_amdgcn_update_dpp(v.x, v.x, 0x101, 0xf, 0x3, true),
+                      __builtin_amdgcn_update_dpp(v.y, v.y, 0x101, 0xf, 0x3, true));
+}
+
+__global__ __launch_bounds__(64) void k_q_invit16(const double* __restrict__ ra, const double2* __restrict__ rd,
+                                                   const double* __restrict__ rb, int M, const double* __restrict__ E,
+                                                   const double* __restrict__ tnorm, int j0, double2* __restrict__ Zt,
+                                                   int64_t sZ, double2* __restrict__ S, int64_t sS) {
+  extern __shared__ double lds[];
+  const int k = blockIdx.y, n = 2 * M, nv = n - j0;
+  for (int i = threadIdx.x; i < M; i += blockDim.x) {
+    lds[i] = ra[(int64_t)k * M + i];
+    lds[M + i] = rb[(int64_t)k * M + i];
+    const double2 dv = rd[(int64_t)k * M + i];
+    lds[2 * M + 2 * i] = dv.x;
+    lds[2 * M + 2 * i + 1] = dv.y;
+  }
+  __syncthreads();
+  const int l = threadIdx.x & 15;
+  const int jj = blockIdx.x * (blockDim.x >> 4) + (threadIdx.x >> 4);
+  if (jj >= nv) return;   // whole 16-lane rows (DPP rows) leave together
+  const double tn = tnorm[k];
+  const double* Ek = E + (int64_t)k * n;
+  const double e = Ek[j0 + jj];
+  const double ctol = kEigClusterTol * tn;
+  const bool member = (jj > 0 && e - Ek[j0 + jj - 1] <= ctol) || (j0 + jj + 1 < n && Ek[j0 + jj + 1] - e <= ctol);
+  const double lam = member ? e - kQClusterShift * tn : e;   // (k_q_invit)
+  const double small = tn > 0.0 ? DBL_EPSILON * tn : DBL_EPSILON;
+  double2* z = Zt + k * sZ + jj;
+  double2* sc = S + k * sS + jj;
+  const double2 zero = make_double2(0.0, 0.0);
+  const bool ylane = l == 12;
+  // this lane's share of a new row [b_{s-1}, (hole) conj d, a - lam, (particle) d, b_s]
+  const double c0 = l == 0 ? 1.0 : 0.0, c1 = l == 1 ? 1.0 : 0.0, c2 = l == 2 ? 1.0 : 0.0, c3 = l == 3 ? 1.0 : 0.0,
+               c4 = l == 4 ? 1.0 : 0.0;
+  // scratch entry of this lane's store: 0 (1/u_kk), 1..4 (u), 5 (y); others none
+  const int est = l < 5 ? l : 5;
+  const bool stl = l < 5 || ylane;
+  double scale = 1.0;
+  for (int it = 0; it < QINVIT_ITERS; ++it) {
+    auto rhs = [&](int r) -> double2 {
+      if (r >= n) return zero;
+      if (it == 0) return make_double2(q_start(j0 + jj, 2 * r), q_start(j0 + jj, 2 * r + 1));
+      const double2 v = z[(int64_t)r * nv];
+      return make_double2(v.x * scale, v.y * scale);
+    };
+    double2 w0, w1, w2;
+    if (ylane) {
+      w0 = rhs(0);
+      w1 = rhs(1);
+      w2 = rhs(2);
+    } else {
+      w0 = l < 5 ? q_tent(lds, M, lam, 0, l) : zero;
+      w1 = l < 5 ? q_tent(lds, M, lam, 1, l) : zero;
+      w2 = l < 5 ? q_tent(lds, M, lam, 2, l) : zero;
+    }
+    double nb2 = (w0.x * w0.x + w0.y * w0.y) + (w1.x * w1.x + w1.y * w1.y) + (w2.x * w2.x + w2.y * w2.y);
+    auto step = [&](int kk, bool hole, double2 ny) {
+      // pivot row: lane 0's magnitudes (ties resolved as in k_q_invit)
+      const double m0 = w0.x * w0.x + w0.y * w0.y;
+      const double m1 = w1.x * w1.x + w1.y * w1.y;
+      const double m2 = w2.x * w2.x + w2.y * w2.y;
+      const int sel0 = m1 > m0 ? (m2 > m1 ? 2 : 1) : (m2 > m0 ? 2 : 0);
+      const int sel = __builtin_amdgcn_update_dpp(sel0, sel0, 0x150, 0xf, 0xf, true);
+      {
+        // the row swap by 0/1 weights (exact for finite entries): a select
+        // chain on the broadcast index became a dynamically indexed stack
+        // array (scratch round trips on the pivot chain)
+        const double s1 = sel == 1 ? 1.0 : 0.0, s2 = sel == 2 ? 1.0 : 0.0, s0 = 1.0 - s1 - s2;
+        const double2 p0 = w0, p1 = w1, p2 = w2;
+        w0 = make_double2(fma(s2, p2.x, fma(s1, p1.x, s0 * p0.x)), fma(s2, p2.y, fma(s1, p1.y, s0 * p0.y)));
+        w1 = make_double2(fma(s1, p0.x, (1.0 - s1) * p1.x), fma(s1, p0.y, (1.0 - s1) * p1.y));
+        w2 = make_double2(fma(s2, p0.x, (1.0 - s2) * p2.x), fma(s2, p0.y, (1.0 - s2) * p2.y));
+      }
+      // lane 0: 1 / u_kk and the multipliers
+      // (branch-free, component-wise: a branch or a select of whole double2
+      // values here also became a stack array)
+      double pm = w0.x * w0.x + w0.y * w0.y;
+      const bool tiny = l == 0 && pm < small * small;   // the pivot only (lane 0)
+      w0.x = tiny ? small : w0.x;
+      w0.y = tiny ? 0.0 : w0.y;
+      pm = tiny ? small * small : pm;
+      const double ip = rcp_nr(pm);
+      const double2 r = make_double2(w0.x * ip, -w0.y * ip);   // 1 / u_kk (lane 0)
+      const double2 f1 = dpp_bcast0(cmul2(w1, r)), f2 = dpp_bcast0(cmul2(w2, r));
+      // the step's row of U (and y_k) before the update (lane 0: 1 / u_kk)
+      const double2 sv = make_double2(l == 0 ? r.x : w0.x, l == 0 ? r.y : w0.y);
+      if (stl) sc[((int64_t)kk * 6 + est) * nv] = sv;
+      w1 = csub2(w1, cmul2(f1, w0));
+      w2 = csub2(w2, cmul2(f2, w0));
+      // the window moves one column (the right-hand side lane: one row)
+      w0 = dpp_shl1_lo(w1);
+      w1 = dpp_shl1_lo(w2);
+      // the next window row r = kk + 3 (k_q_invit's row formula, this lane's column)
+      const int rr = kk + 3, sr = min(rr >> 1, M - 1);
+      const double on = rr < n ? 1.0 : 0.0, sg = hole ? -on : on;
+      const double as = lds[sr], bs = lds[M + sr], bm = lds[M + sr - 1];
+      const double dr = lds[2 * M + 2 * sr], di = lds[2 * M + 2 * sr + 1];
+      const double cd = hole ? c1 : c3;
+      const double2 nr = make_double2(sg * (c0 * bm + c2 * as + c4 * bs) - c2 * on * lam + cd * on * dr,
+                                      (hole ? -cd : cd) * on * di);
+      w2 = make_double2(ylane ? ny.x : nr.x, ylane ? ny.y : nr.y);
+      nb2 += ny.x * ny.x + ny.y * ny.y;
+    };
+    constexpr int FB = 4;
+    double2 ra_[FB], rb_[FB];
+#pragma unroll
+    for (int u = 0; u < FB; ++u) ra_[u] = rhs(3 + u);
+    for (int k0 = 0; k0 < n; k0 += 2 * FB) {
+#pragma unroll
+      for (int u = 0; u < FB; ++u) rb_[u] = rhs(k0 + FB + 3 + u);
+#pragma unroll
+      for (int u = 0; u < FB; ++u)
+        if (k0 + u < n) step(k0 + u, (u + 1) & 1, ra_[u]);
+#pragma unroll
+      for (int u = 0; u < FB; ++u) ra_[u] = rhs(k0 + 2 * FB + 3 + u);
+#pragma unroll
+      for (int u = 0; u < FB; ++u)
+        if (k0 + FB + u < n) step(k0 + FB + u, (FB + u + 1) & 1, rb_[u]);
+    }
+    nb2 = __builtin_amdgcn_update_dpp(nb2, nb2, 0x15C, 0xf, 0xf, true);   // lane 12's (row_newbcast:12)
+    // the scratch stores of the row's other lanes before its reads
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // back substitution (every lane of the row the same; lane 0 stores x)
+    double2 x1 = zero, x2 = zero, x3 = zero, x4 = zero;
+    double nrm = 0.0;
+    constexpr int PB = 4;
+    double2 fa[PB][6], fb[PB][6];
+    auto load_blk = [&](int k0, double2 (&f)[PB][6]) {
+#pragma unroll
+      for (int u = 0; u < PB; ++u) {
+        const int kk = k0 - u;
+#pragma unroll
+        for (int q = 0; q < 6; ++q) f[u][q] = kk >= 0 ? sc[((int64_t)kk * 6 + q) * nv] : zero;
+      }
+    };
+    auto solve_blk = [&](int k0, const double2 (&f)[PB][6]) {
+#pragma unroll
+      for (int u = 0; u < PB; ++u) {
+        const int kk = k0 - u;
+        if (kk >= 0) {
+          double2 t = f[u][5];
+          t = csub2(t, cmul2(f[u][1], x1));
+          t = csub2(t, cmul2(f[u][2], x2));
+          t = csub2(t, cmul2(f[u][3], x3));
+          t = csub2(t, cmul2(f[u][4], x4));
+          const double2 x = cmul2(t, f[u][0]);
+          if (l == 0) z[(int64_t)kk * nv] = x;
+          nrm += x.x * x.x + x.y * x.y;
+          x4 = x3;
+          x3 = x2;
+          x2 = x1;
+          x1 = x;
+        }
+      }
+    };
+    load_blk(n - 1, fa);
+    for (int k0 = n - 1; k0 >= 0; k0 -= 2 * PB) {
+      load_blk(k0 - PB, fb);
+      solve_blk(k0, fa);
+      load_blk(k0 - 2 * PB, fa);
+      solve_blk(k0 - PB, fb);
+    }
+    scale = 1.0 / sqrt(nrm);
+    if (it == 0 && QINVIT_ITERS > 1) {   // (k_q_invit's test)
+      const int jg = j0 + jj;
+      double gap = DBL_MAX;
+      if (jg > j0) gap = fmin(gap, e - Ek[jg - 1]);
+      if (jg + 1 < n) gap = fmin(gap, Ek[jg + 1] - e);
+      const double g = sqrt(nrm / nb2);
+      const bool need = !(g * gap * kQInvitShare > 1.0);
+      if (__ballot(need) == 0) break;
+      // lane 0's z stores before the right-hand side lane reads them
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+  if (l == 0)
+    for (int r = 0; r < n; ++r) {
+      const double2 v = z[(int64_t)r * nv];
+      z[(int64_t)r * nv] = make_double2(v.x * scale, v.y * scale);
+    }
+}
+
 // The crowd at zero: when E_N + E_{N+1} <= kEigZeroTol ||T|| (j0 = N), the
 // levels j0 .. j0 + c - 1 with E_j + E_N within it (extended over cluster
 // gaps): their vectors x_j overlap the partners Theta x_k of one another (by
@@ -1432,8 +1642,19 @@ int64_t q_invit_scratch(int M, int j0) { return (int64_t)2 * M * 6 * (2 * M - j0
 void launch_q_invit(const double* ra, const double2* rd, const double* rb, int M, const double* E, const double* tnorm,
                     int j0, double2* Zt, int64_t sZ, double2* S, int64_t sS, int m, hipStream_t s) {
   const int nv = 2 * M - j0;
-  hipLaunchKernelGGL(k_q_invit, dim3((nv + 63) / 64, m), dim3(64), (size_t)4 * M * sizeof(double), s, ra, rd, rb, M,
-                     E, tnorm, j0, Zt, sZ, S, sS);
+  // 16-lane rows (k_q_invit16) while they fit one wave per SIMD (m nv <=
+  // 4096): one L = 32 measurement 24.4 -> 23.8 ms; for larger batches the
+  // thread per eigenvalue issues less in total (16 snapshots: 7.19 against
+  // 7.59 ms per measurement; profiles/r06_exp_qinvit_lanes.txt).
+  // DWHMC_QINVIT_THREAD=1 / 0 forces either (A/B).
+  const char* env = std::getenv("DWHMC_QINVIT_THREAD");
+  const bool thread = env && *env ? *env == '1' : (int64_t)m * nv > 4096;
+  if (thread)
+    hipLaunchKernelGGL(k_q_invit, dim3((nv + 63) / 64, m), dim3(64), (size_t)4 * M * sizeof(double), s, ra, rd, rb,
+                       M, E, tnorm, j0, Zt, sZ, S, sS);
+  else
+    hipLaunchKernelGGL(k_q_invit16, dim3((nv + 3) / 4, m), dim3(64), (size_t)4 * M * sizeof(double), s, ra, rd, rb,
+                       M, E, tnorm, j0, Zt, sZ, S, sS);
 }
 
 void launch_q_ztu(const double2* Yt, int64_t sY, const double2* G, int M, int j0, double2* U, int64_t sU, int m,
