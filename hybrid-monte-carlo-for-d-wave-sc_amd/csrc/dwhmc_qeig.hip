@@ -45,6 +45,7 @@
 
 #include <cfloat>
 #include <cstdlib>
+#include <type_traits>
 
 #include "dwhmc_device.h"
 #include "dwhmc_internal.h"
@@ -1155,6 +1156,14 @@ __global__ __launch_bounds__(64) void k_q_invit(const double* __restrict__ ra, c
 // one transaction), lane 0 storing.  Same operation order as k_q_invit per
 // eigenvalue, so the same vectors up to the order of the pivot magnitudes'
 // sums (identical).
+// f(integral_constant<int, U>) for U = 0 .. 15 (compile-time DPP controls)
+template <int U = 0, class F>
+__device__ __forceinline__ void q_unroll16(F&& f) {
+  if constexpr (U < 16) {
+    f(std::integral_constant<int, U>{});
+    q_unroll16<U + 1>(f);
+  }
+}
 __device__ __forceinline__ double2 dpp_bcast0(double2 v) {
   return make_double2(__builtin_amdgcn_update_dpp(v.x, v.x, 0x150, 0xf, 0xf, true),
                       __builtin_amdgcn_update_dpp(v.y, v.y, 0x150, 0xf, 0xf, true));
@@ -1266,21 +1275,20 @@ __global__ __launch_bounds__(64) void k_q_invit16(const double* __restrict__ ra,
       w2 = make_double2(ylane ? ny.x : nr.x, ylane ? ny.y : nr.y);
       nb2 += ny.x * ny.x + ny.y * ny.y;
     };
-    constexpr int FB = 4;
-    double2 ra_[FB], rb_[FB];
-#pragma unroll
-    for (int u = 0; u < FB; ++u) ra_[u] = rhs(3 + u);
-    for (int k0 = 0; k0 < n; k0 += 2 * FB) {
-#pragma unroll
-      for (int u = 0; u < FB; ++u) rb_[u] = rhs(k0 + FB + 3 + u);
-#pragma unroll
-      for (int u = 0; u < FB; ++u)
-        if (k0 + u < n) step(k0 + u, (u + 1) & 1, ra_[u]);
-#pragma unroll
-      for (int u = 0; u < FB; ++u) ra_[u] = rhs(k0 + 2 * FB + 3 + u);
-#pragma unroll
-      for (int u = 0; u < FB; ++u)
-        if (k0 + FB + u < n) step(k0 + FB + u, (FB + u + 1) & 1, rb_[u]);
+    // the right-hand side's rows 16 at a time, one per lane (lane l: row
+    // k0 + 3 + l, the next 16 loaded a block ahead), each step's row reaching
+    // the row's lanes by row_newbcast: one hash or load per 16 steps and lane
+    // instead of one per step in every lane
+    double2 rv = rhs(3 + l);
+    for (int k0 = 0; k0 < n; k0 += 16) {
+      const double2 rn = rhs(k0 + 16 + 3 + l);
+      q_unroll16([&](auto uc) {
+        constexpr int u = decltype(uc)::value;
+        const double2 ny = make_double2(__builtin_amdgcn_update_dpp(rv.x, rv.x, 0x150 + u, 0xf, 0xf, true),
+                                        __builtin_amdgcn_update_dpp(rv.y, rv.y, 0x150 + u, 0xf, 0xf, true));
+        if (k0 + u < n) step(k0 + u, (u + 1) & 1, ny);
+      });
+      rv = rn;
     }
     nb2 = __builtin_amdgcn_update_dpp(nb2, nb2, 0x15C, 0xf, 0xf, true);   // lane 12's (row_newbcast:12)
     // the scratch stores of the row's other lanes before its reads
