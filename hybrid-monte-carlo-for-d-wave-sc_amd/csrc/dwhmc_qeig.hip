@@ -1386,7 +1386,7 @@ __host__ __device__ inline int q_crowd(const double* E, int n, int j0, double tn
 __global__ __launch_bounds__(256) void k_q_orth(const double* __restrict__ E, const double* __restrict__ tnorm, int M,
                                                 int j0, double2* __restrict__ Zt, int64_t sZ, double ctol,
                                                 int* __restrict__ bad) {
-  constexpr int MC = kQMaxCluster, RC = 32;
+  constexpr int MC = kQMaxCluster, RC = 64;   // rows staged per chunk (64: half the barriers of 32)
   const int k = blockIdx.y, n = 2 * M, nv = n - j0, jj = blockIdx.x, tid = threadIdx.x;
   E += (int64_t)k * n;
   Zt += k * sZ;
